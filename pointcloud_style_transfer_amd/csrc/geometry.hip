@@ -1,0 +1,352 @@
+// PointNet++ geometry kernels for gfx950: square_distance, index_points, farthest-point
+// sampling, ball query and the fused SetAbstraction group gather.
+// Reference: models/pointnet2_encoder.py (citations per kernel).
+// All distance arithmetic uses explicit *_rn intrinsics so the reference's CPU rounding
+//  is reproduced bit for bit.
+#include "common.h"
+
+namespace pcst {
+
+// ------------------------------------------------------------------ square_distance
+// pointnet2_encoder.py:8-15.  One thread per (b, s, n) output element, n fastest.
+__global__ void square_distance_kernel(const float* __restrict__ src, const float* __restrict__ dst,
+                                       int64_t S, int64_t N, int64_t total, float* __restrict__ out) {
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t n = e % N;
+    const int64_t bs = e / N;
+    const int64_t b = bs / S;
+    const float* a = src + bs * 3;
+    const float* q = dst + (b * N + n) * 3;
+    float d = fmul(-2.0f, dot3(a[0], a[1], a[2], q[0], q[1], q[2]));
+    d = fadd(d, sqnorm3(a[0], a[1], a[2]));
+    d = fadd(d, sqnorm3(q[0], q[1], q[2]));
+    out[e] = d;
+  }
+}
+
+// ------------------------------------------------------------------ index_points
+// pointnet2_encoder.py:17-28: gather rows with the index clamped to [0, N-1].
+__global__ void index_points_kernel(const float* __restrict__ pts, int64_t N, int64_t C,
+                                    const int64_t* __restrict__ idx, int64_t K, int64_t total,
+                                    float* __restrict__ out) {
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t c = e % C;
+    const int64_t bk = e / C;
+    const int64_t b = bk / K;
+    int64_t g = idx[bk];
+    g = g < 0 ? 0 : (g > N - 1 ? N - 1 : g);
+    out[e] = pts[(b * N + g) * C + c];
+  }
+}
+
+// ------------------------------------------------------------------ farthest point sampling
+// pointnet2_encoder.py:30-45.  One 512-thread workgroup per cloud; each thread keeps PPT
+// points and their running min-distance in registers (point n = tid + k*512), so a whole
+// 30000-point cloud is register-resident (60 points x 4 floats per lane).  Per iteration:
+// per-thread scan in ascending n with strict '>' (lowest index wins ties, Q3), a 64-lane
+// butterfly arg-max, one LDS exchange of the 8 wave winners, one barrier.  The winner's
+// coordinates are re-read with a wave-uniform (scalar) load.
+constexpr int kFpsThreads = 512;
+constexpr int kFpsWaves = kFpsThreads / 64;
+
+__device__ __forceinline__ void argmax_merge(float& v, int& i, float ov, int oi) {
+  if (ov > v || (ov == v && oi < i)) { v = ov; i = oi; }
+}
+
+template <int PPT>
+__global__ __launch_bounds__(kFpsThreads) void fps_reg_kernel(const float* __restrict__ xyz,
+                                                              int N, int npoint,
+                                                              const int64_t* __restrict__ start,
+                                                              int64_t* __restrict__ out) {
+  const int b = blockIdx.x;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wid = tid >> 6;
+  const float* P = xyz + (int64_t)b * N * 3;
+  float px[PPT], py[PPT], pz[PPT], dist[PPT];
+#pragma unroll
+  for (int k = 0; k < PPT; ++k) {
+    const int n = tid + k * kFpsThreads;
+    if (n < N) {
+      px[k] = P[n * 3 + 0]; py[k] = P[n * 3 + 1]; pz[k] = P[n * 3 + 2];
+      dist[k] = 1e10f;
+    } else {
+      px[k] = py[k] = pz[k] = 0.0f;
+      dist[k] = -1.0f;  // never the arg-max: real distances are >= 0
+    }
+  }
+  __shared__ float s_val[2][kFpsWaves];
+  __shared__ int s_idx[2][kFpsWaves];
+  int far = (int)start[b];
+  int64_t* o = out + (int64_t)b * npoint;
+  for (int it = 0; it < npoint; ++it) {
+    far = __builtin_amdgcn_readfirstlane(far);
+    if (tid == 0) o[it] = far;
+    const float cx = P[far * 3 + 0], cy = P[far * 3 + 1], cz = P[far * 3 + 2];
+    float best = -2.0f;
+    int bestk = 0;
+#pragma unroll
+    for (int k = 0; k < PPT; ++k) {
+      const float dx = fsub(px[k], cx), dy = fsub(py[k], cy), dz = fsub(pz[k], cz);
+      const float d = fadd(fadd(fmul(dx, dx), fmul(dy, dy)), fmul(dz, dz));
+      dist[k] = d < dist[k] ? d : dist[k];
+      if (dist[k] > best) { best = dist[k]; bestk = k; }
+    }
+    int bi = tid + bestk * kFpsThreads;
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+      const float ov = __shfl_xor(best, off);
+      const int oi = __shfl_xor(bi, off);
+      argmax_merge(best, bi, ov, oi);
+    }
+    const int slot = it & 1;
+    if (lane == 0) { s_val[slot][wid] = best; s_idx[slot][wid] = bi; }
+    __syncthreads();
+    float v = s_val[slot][0];
+    int i = s_idx[slot][0];
+#pragma unroll
+    for (int w = 1; w < kFpsWaves; ++w) argmax_merge(v, i, s_val[slot][w], s_idx[slot][w]);
+    far = i;
+  }
+}
+
+// Fallback for N > 512*60: running distances in global memory (caller workspace), one
+// workgroup per cloud streaming the cloud every iteration.
+__global__ __launch_bounds__(1024) void fps_global_kernel(const float* __restrict__ xyz, int N,
+                                                          int npoint,
+                                                          const int64_t* __restrict__ start,
+                                                          float* __restrict__ distbuf,
+                                                          int64_t* __restrict__ out) {
+  const int b = blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const float* P = xyz + (int64_t)b * N * 3;
+  float* D = distbuf + (int64_t)b * N;
+  for (int n = tid; n < N; n += 1024) D[n] = 1e10f;
+  __shared__ float s_val[2][16];
+  __shared__ int s_idx[2][16];
+  int far = (int)start[b];
+  for (int it = 0; it < npoint; ++it) {
+    far = __builtin_amdgcn_readfirstlane(far);
+    if (tid == 0) out[(int64_t)b * npoint + it] = far;
+    const float cx = P[far * 3 + 0], cy = P[far * 3 + 1], cz = P[far * 3 + 2];
+    float best = -2.0f;
+    int bi = 0;
+    for (int n = tid; n < N; n += 1024) {
+      const float dx = fsub(P[n * 3 + 0], cx), dy = fsub(P[n * 3 + 1], cy),
+                  dz = fsub(P[n * 3 + 2], cz);
+      const float d = fadd(fadd(fmul(dx, dx), fmul(dy, dy)), fmul(dz, dz));
+      float cur = D[n];
+      if (d < cur) { cur = d; D[n] = d; }
+      if (cur > best) { best = cur; bi = n; }
+    }
+    for (int off = 32; off >= 1; off >>= 1) {
+      const float ov = __shfl_xor(best, off);
+      const int oi = __shfl_xor(bi, off);
+      argmax_merge(best, bi, ov, oi);
+    }
+    const int slot = it & 1;
+    if (lane == 0) { s_val[slot][wid] = best; s_idx[slot][wid] = bi; }
+    __syncthreads();
+    float v = s_val[slot][0];
+    int i = s_idx[slot][0];
+    for (int w = 1; w < 16; ++w) argmax_merge(v, i, s_val[slot][w], s_idx[slot][w]);
+    far = i;
+  }
+}
+
+// ------------------------------------------------------------------ ball query
+// pointnet2_encoder.py:47-59.  One wave per centroid scans the cloud in ascending index
+// order, 64 points per step (4 steps in flight), keeps the in-radius points with a ballot +
+// prefix popcount (exactly the first `nsample` in index order, as the reference's full sort
+// does) and exits as soon as nsample are found.
+__global__ __launch_bounds__(256) void ball_query_kernel(float r2, int nsample,
+                                                         const float* __restrict__ xyz,
+                                                         const float* __restrict__ new_xyz,
+                                                         int B, int N, int S,
+                                                         int64_t* __restrict__ out) {
+  const int lane = threadIdx.x & 63;
+  const int64_t q = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (q >= (int64_t)B * S) return;
+  const int b = (int)(q / S);
+  const float* a = new_xyz + q * 3;
+  const float a0 = a[0], a1 = a[1], a2 = a[2];
+  const float na = sqnorm3(a0, a1, a2);
+  const float* P = xyz + (int64_t)b * N * 3;
+  int64_t* o = out + q * nsample;
+  int cnt = 0;
+  int first = N;
+  for (int base = 0; base < N && cnt < nsample; base += 256) {
+    float d[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int n = base + u * 64 + lane;
+      d[u] = 3.4e38f;
+      if (n < N) {
+        const float q0 = P[n * 3 + 0], q1 = P[n * 3 + 1], q2 = P[n * 3 + 2];
+        float dd = fmul(-2.0f, dot3(a0, a1, a2, q0, q1, q2));
+        dd = fadd(dd, na);
+        d[u] = fadd(dd, sqnorm3(q0, q1, q2));
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int n = base + u * 64 + lane;
+      const bool in = (n < N) && !(d[u] > r2);
+      const unsigned long long m = __ballot(in);
+      if (m == 0ull) continue;
+      if (cnt == 0) first = base + u * 64 + (__ffsll((long long)m) - 1);
+      const int slot = cnt + __popcll(m & lanemask_lt());
+      if (in && slot < nsample) o[slot] = n;
+      cnt += __popcll(m);
+      if (cnt >= nsample) break;
+    }
+  }
+  for (int k = (cnt < nsample ? cnt : nsample) + lane; k < nsample; k += 64) o[k] = first;
+}
+
+// ------------------------------------------------------------------ group gather
+// pointnet2_encoder.py:92-99: new_xyz = index_points(xyz, fps_idx); grouped =
+// cat(index_points(xyz, gidx) - new_xyz, index_points(feats, gidx)).
+__global__ void new_xyz_kernel(const float* __restrict__ xyz, int64_t N,
+                               const int64_t* __restrict__ fps_idx, int64_t S, int64_t total,
+                               float* __restrict__ new_xyz) {
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t c = e % 3, bs = e / 3, b = bs / S;
+    int64_t g = fps_idx[bs];
+    g = g < 0 ? 0 : (g > N - 1 ? N - 1 : g);
+    new_xyz[e] = xyz[(b * N + g) * 3 + c];
+  }
+}
+
+__global__ void group_gather_kernel(const float* __restrict__ xyz, const float* __restrict__ feats,
+                                    int64_t N, int64_t C, const float* __restrict__ new_xyz,
+                                    const int64_t* __restrict__ gidx, int64_t S, int64_t ns,
+                                    int64_t total, float* __restrict__ grouped) {
+  const int64_t W = 3 + C;
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t c = e % W, r = e / W;  // r = (b*S + s)*ns + k
+    const int64_t bs = r / ns, b = bs / S;
+    int64_t g = gidx[r];
+    g = g < 0 ? 0 : (g > N - 1 ? N - 1 : g);
+    float v;
+    if (c < 3) v = fsub(xyz[(b * N + g) * 3 + c], new_xyz[bs * 3 + c]);
+    else v = feats[(b * N + g) * C + (c - 3)];
+    grouped[e] = v;
+  }
+}
+
+static int grid_for(int64_t total, int threads = 256) {
+  int64_t g = cdiv(total, threads);
+  return (int)(g > 8192 ? 8192 : (g < 1 ? 1 : g));
+}
+
+}  // namespace pcst
+
+using namespace pcst;
+
+extern "C" int pcst_square_distance(const float* src, const float* dst, int64_t B, int64_t S,
+                                    int64_t N, float* out, void* stream) {
+  PCST_CHECK_ARG(B >= 0 && S >= 0 && N >= 0, "square_distance: bad shape");
+  const int64_t total = B * S * N;
+  if (total == 0) return PCST_OK;
+  PCST_CHECK_ARG(src && dst && out, "square_distance: null pointer");
+  hipLaunchKernelGGL(square_distance_kernel, dim3(grid_for(total)), dim3(256), 0, as_stream(stream),
+                     src, dst, S, N, total, out);
+  PCST_LAUNCH_CHECK("square_distance");
+  return PCST_OK;
+}
+
+extern "C" int pcst_index_points(const float* points, int64_t B, int64_t N, int64_t C,
+                                 const int64_t* idx, int64_t K, float* out, void* stream) {
+  PCST_CHECK_ARG(B >= 0 && N > 0 && C > 0 && K >= 0, "index_points: bad shape");
+  const int64_t total = B * K * C;
+  if (total == 0) return PCST_OK;
+  PCST_CHECK_ARG(points && idx && out, "index_points: null pointer");
+  hipLaunchKernelGGL(index_points_kernel, dim3(grid_for(total)), dim3(256), 0, as_stream(stream),
+                     points, N, C, idx, K, total, out);
+  PCST_LAUNCH_CHECK("index_points");
+  return PCST_OK;
+}
+
+template <int PPT>
+static void launch_fps(const float* xyz, int B, int N, int npoint, const int64_t* start,
+                       int64_t* out, hipStream_t s) {
+  hipLaunchKernelGGL(fps_reg_kernel<PPT>, dim3(B), dim3(kFpsThreads), 0, s, xyz, N, npoint, start,
+                     out);
+}
+
+extern "C" int pcst_fps_workspace_size(int64_t B, int64_t N, size_t* bytes) {
+  *bytes = (N > (int64_t)kFpsThreads * 60) ? (size_t)(B * N) * sizeof(float) : 0;
+  return PCST_OK;
+}
+
+extern "C" int pcst_fps_ws(const float* xyz, int64_t B, int64_t N, int64_t npoint,
+                           const int64_t* start_idx, int64_t* out_idx, void* workspace,
+                           void* stream) {
+  PCST_CHECK_ARG(B >= 0 && N > 0 && npoint >= 0 && N < (1ll << 31), "fps: bad shape");
+  if (B == 0 || npoint == 0) return PCST_OK;
+  PCST_CHECK_ARG(xyz && start_idx && out_idx, "fps: null pointer");
+  hipStream_t s = as_stream(stream);
+  const int64_t ppt = cdiv(N, kFpsThreads);
+  const int b = (int)B, n = (int)N, np = (int)npoint;
+  if (ppt <= 1) launch_fps<1>(xyz, b, n, np, start_idx, out_idx, s);
+  else if (ppt <= 2) launch_fps<2>(xyz, b, n, np, start_idx, out_idx, s);
+  else if (ppt <= 4) launch_fps<4>(xyz, b, n, np, start_idx, out_idx, s);
+  else if (ppt <= 8) launch_fps<8>(xyz, b, n, np, start_idx, out_idx, s);
+  else if (ppt <= 16) launch_fps<16>(xyz, b, n, np, start_idx, out_idx, s);
+  else if (ppt <= 24) launch_fps<24>(xyz, b, n, np, start_idx, out_idx, s);
+  else if (ppt <= 32) launch_fps<32>(xyz, b, n, np, start_idx, out_idx, s);
+  else if (ppt <= 40) launch_fps<40>(xyz, b, n, np, start_idx, out_idx, s);
+  else if (ppt <= 48) launch_fps<48>(xyz, b, n, np, start_idx, out_idx, s);
+  else if (ppt <= 60) launch_fps<60>(xyz, b, n, np, start_idx, out_idx, s);
+  else {
+    PCST_CHECK_ARG(workspace != nullptr, "fps: N > 30720 needs a workspace of B*N floats");
+    hipLaunchKernelGGL(fps_global_kernel, dim3(b), dim3(1024), 0, s, xyz, n, np, start_idx,
+                       static_cast<float*>(workspace), out_idx);
+  }
+  PCST_LAUNCH_CHECK("fps");
+  return PCST_OK;
+}
+
+extern "C" int pcst_fps(const float* xyz, int64_t B, int64_t N, int64_t npoint,
+                        const int64_t* start_idx, int64_t* out_idx, void* stream) {
+  PCST_CHECK_ARG(N <= (int64_t)kFpsThreads * 60, "fps: N > 30720 needs pcst_fps_ws");
+  return pcst_fps_ws(xyz, B, N, npoint, start_idx, out_idx, nullptr, stream);
+}
+
+extern "C" int pcst_ball_query(double radius, int64_t nsample, const float* xyz,
+                               const float* new_xyz, int64_t B, int64_t N, int64_t S,
+                               int64_t* out_idx, void* stream) {
+  PCST_CHECK_ARG(B >= 0 && N > 0 && S >= 0 && nsample > 0 && N < (1ll << 31),
+                 "ball_query: bad shape");
+  if (B * S == 0) return PCST_OK;
+  PCST_CHECK_ARG(xyz && new_xyz && out_idx, "ball_query: null pointer");
+  const float r2 = (float)(radius * radius);  // python float r**2, then cast to fp32 (Q4)
+  const int64_t waves = B * S;
+  hipLaunchKernelGGL(ball_query_kernel, dim3((unsigned)cdiv(waves, 4)), dim3(256), 0,
+                     as_stream(stream), r2, (int)nsample, xyz, new_xyz, (int)B, (int)N, (int)S,
+                     out_idx);
+  PCST_LAUNCH_CHECK("ball_query");
+  return PCST_OK;
+}
+
+extern "C" int pcst_group_gather(const float* xyz, const float* feats, int64_t B, int64_t N,
+                                 int64_t C, const int64_t* fps_idx, const int64_t* group_idx,
+                                 int64_t S, int64_t ns, float* new_xyz, float* grouped,
+                                 void* stream) {
+  PCST_CHECK_ARG(B >= 0 && N > 0 && C >= 0 && S >= 0 && ns > 0, "group_gather: bad shape");
+  PCST_CHECK_ARG(C == 0 || feats != nullptr, "group_gather: feats required when C > 0");
+  if (B * S == 0) return PCST_OK;
+  hipStream_t s = as_stream(stream);
+  const int64_t t1 = B * S * 3;
+  hipLaunchKernelGGL(new_xyz_kernel, dim3(grid_for(t1)), dim3(256), 0, s, xyz, N, fps_idx, S, t1,
+                     new_xyz);
+  const int64_t t2 = B * S * ns * (3 + C);
+  hipLaunchKernelGGL(group_gather_kernel, dim3(grid_for(t2)), dim3(256), 0, s, xyz, feats, N, C,
+                     new_xyz, group_idx, S, ns, t2, grouped);
+  PCST_LAUNCH_CHECK("group_gather");
+  return PCST_OK;
+}

@@ -1,0 +1,110 @@
+"""Random draws of the hot path, routed through one switchable source.
+
+The reference draws with torch's generators at fixed call sites
+(FPS start `pointnet2_encoder.py:36` on the CPU generator; `randperm` in the voxel
+downsample `diffusion_model.py:101,111`; x_T `randn` `:234`; the cond-drop
+`rand` `:177`; trainer `randint`/`randn_like` `trainer.py:75-76`,
+`diffusion_model.py:214`).  Our code makes the same draws, in the same order,
+through `source()`.  Parity tests install a `replay(...)` source that feeds back
+the draws recorded from the reference, so a device run can be compared
+bit-for-bit with the reference's outputs.
+
+On the performance path the voxel downsample does not call `randperm` at all: it
+draws its random subset on the device (Philox keys + sort, `csrc/voxel.hip`),
+seeded from `device_seed()`.
+"""
+from __future__ import annotations
+
+import contextlib
+
+import numpy as np
+import torch
+
+
+class TorchRNG:
+    replaying = False
+
+    def randint(self, low, high, size, device=None):
+        return torch.randint(low, high, size, dtype=torch.long, device=device)
+
+    def randperm(self, n, device=None):
+        return torch.randperm(n, device=device)
+
+    def randn(self, shape, device=None):
+        return torch.randn(shape, device=device)
+
+    def rand(self, shape, device=None):
+        return torch.rand(shape, device=device)
+
+    def randn_like(self, x):
+        return torch.randn_like(x)
+
+    def device_seed(self):
+        return int(torch.randint(0, 2**62, (1,), dtype=torch.long).item())
+
+
+class ReplayRNG:
+    """Returns recorded draws in call order; the kind of every draw is checked."""
+
+    replaying = True
+
+    def __init__(self, draws):
+        self.draws = [(str(n), np.asarray(v)) for n, v in draws]
+        self.pos = 0
+
+    @classmethod
+    def from_npz(cls, z, prefix):
+        names = list(z[f"{prefix}_names"])
+        return cls([(str(n), z[f"{prefix}_{i}"]) for i, n in enumerate(names)])
+
+    def _next(self, kind):
+        if self.pos >= len(self.draws):
+            raise RuntimeError(f"replay exhausted at draw {self.pos} ({kind})")
+        name, val = self.draws[self.pos]
+        if name != kind:
+            raise RuntimeError(f"replay: expected {kind}, recorded {name} at draw {self.pos}")
+        self.pos += 1
+        return val
+
+    def randint(self, low, high, size, device=None):
+        return torch.from_numpy(self._next("randint").astype(np.int64)).to(device)
+
+    def randperm(self, n, device=None):
+        v = self._next("randperm")
+        if len(v) != n:
+            raise RuntimeError(f"replay: randperm length {len(v)} recorded, {n} requested")
+        return torch.from_numpy(v.astype(np.int64)).to(device)
+
+    def randn(self, shape, device=None):
+        return torch.from_numpy(self._next("randn").astype(np.float32)).to(device)
+
+    def rand(self, shape, device=None):
+        return torch.from_numpy(self._next("rand").astype(np.float32)).to(device)
+
+    def randn_like(self, x):
+        return torch.from_numpy(self._next("randn_like").astype(np.float32)).to(x.device)
+
+    def device_seed(self):
+        return 0
+
+    @property
+    def exhausted(self):
+        return self.pos == len(self.draws)
+
+
+_source = TorchRNG()
+
+
+def source():
+    return _source
+
+
+@contextlib.contextmanager
+def replay(draws_or_rng):
+    global _source
+    prev = _source
+    _source = draws_or_rng if isinstance(draws_or_rng, ReplayRNG) else ReplayRNG(draws_or_rng)
+    try:
+        yield _source
+    finally:
+        _source = prev

@@ -1,0 +1,83 @@
+"""HIP geometry kernels vs the reference's golden vectors and the oracle (bit-exact)."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def H():
+    from pointcloud_style_transfer_amd import _hip
+
+    assert torch.cuda.is_available(), "GPU tests need the HIP device"
+    _hip.lib()
+    return _hip
+
+
+def dev(a, dtype=None):
+    t = torch.from_numpy(np.ascontiguousarray(a))
+    if dtype is not None:
+        t = t.to(dtype)
+    return t.cuda()
+
+
+def test_square_distance(H, golden):
+    g = golden("geometry.npz")
+    out = H.square_distance(dev(g["sqd_src"]), dev(g["sqd_dst"])).cpu().numpy()
+    np.testing.assert_array_equal(out, g["sqd_out"])
+
+
+def test_index_points(H, golden):
+    g = golden("geometry.npz")
+    out = H.index_points(dev(g["ip_points"]), dev(g["ip_idx"])).cpu().numpy()
+    np.testing.assert_array_equal(out, g["ip_out"])
+
+
+@pytest.mark.parametrize("key", ["fps_a", "fps_b", "fps_c", "fps_tie"])
+def test_fps_golden(H, golden, key):
+    g = golden("geometry.npz")
+    out = H.fps(dev(g[f"{key}_xyz"]), int(g[f"{key}_npoint"]), dev(g[f"{key}_start"]))
+    np.testing.assert_array_equal(out.cpu().numpy(), g[f"{key}_idx"])
+
+
+@pytest.mark.parametrize("N,npoint,B", [(1, 1, 1), (7, 5, 3), (513, 100, 2), (9000, 300, 2),
+                                        (30720, 64, 1), (40000, 32, 2)])
+def test_fps_vs_oracle_sizes(H, N, npoint, B):
+    rng = np.random.default_rng(N)
+    xyz = rng.standard_normal((B, N, 3)).astype(np.float32)
+    start = rng.integers(0, N, B)
+    out = H.fps(dev(xyz), npoint, dev(start)).cpu().numpy()
+    np.testing.assert_array_equal(out, O.farthest_point_sample(xyz, npoint, start))
+
+
+@pytest.mark.parametrize("key", ["bq_sa1", "bq_sa2", "bq_edge"])
+def test_ball_query_golden(H, golden, key):
+    g = golden("geometry.npz")
+    out = H.ball_query(float(g[f"{key}_radius"]), int(g[f"{key}_nsample"]),
+                       dev(g[f"{key}_xyz"]), dev(g[f"{key}_new"]))
+    np.testing.assert_array_equal(out.cpu().numpy(), g[f"{key}_idx"])
+
+
+@pytest.mark.parametrize("N,S,ns,r", [(100, 10, 8, 0.3), (5000, 77, 64, 0.1), (3000, 40, 512, 0.5)])
+def test_ball_query_vs_oracle(H, N, S, ns, r):
+    rng = np.random.default_rng(S)
+    xyz = rng.uniform(-1, 1, (2, N, 3)).astype(np.float32)
+    new = xyz[:, rng.integers(0, N, S)]
+    out = H.ball_query(r, ns, dev(xyz), dev(new)).cpu().numpy()
+    np.testing.assert_array_equal(out, O.query_ball_point(r, ns, xyz, new))
+
+
+def test_group_gather(H, golden):
+    g = golden("geometry.npz")
+    xyz = g["fps_c_xyz"]
+    fidx = g["fps_c_idx"]
+    gidx = g["bq_sa2_idx"]
+    feats = np.random.default_rng(0).standard_normal((2, xyz.shape[1], 5)).astype(np.float32)
+    new, grouped = H.group_gather(dev(xyz), dev(feats), dev(fidx), dev(gidx))
+    ref_new = O.index_points(xyz, fidx)
+    np.testing.assert_array_equal(new.cpu().numpy(), ref_new)
+    ref = np.concatenate([O.index_points(xyz, gidx) - ref_new[:, :, None], O.index_points(feats, gidx)], -1)
+    np.testing.assert_array_equal(grouped.cpu().numpy(), ref)
