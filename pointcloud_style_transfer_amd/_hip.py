@@ -33,8 +33,21 @@ SIGNATURES = {
     "pcst_fps_workspace_size": [_I, _I, _SZ],
     "pcst_ball_query": [_D, _I, _P, _P, _I, _I, _I, _P, _P],
     "pcst_group_gather": [_P, _P, _I, _I, _I, _P, _P, _I, _I, _P, _P, _P],
+    "pcst_voxel_workspace_size": [_I, _I, _SZ],
+    "pcst_voxel_stats": [_P, _I, _I, _I, _P, _P, _P],
+    "pcst_voxel_select": [_P, _I, _I, _I, _P, _P, _P, _P, ctypes.c_uint64, _P, _P, _P],
+    "pcst_voxel_downsample": [_P, _I, _I, _I, _P, ctypes.c_uint64, _P, _P, _P],
+    "pcst_voxel_error": [_P, _I, _I, _P, _P],
+    "pcst_knn_workspace_size": [_I, _I, _I, _SZ],
+    "pcst_knn3_interp": [_P, _P, _P, _I, _I, _I, _P, _P, _P],
+    "pcst_knn_error": [_P, _I, _I, _I, _P, _P],
+    "pcst_noise_mlp_blob_bytes": [ctypes.c_int],
+    "pcst_noise_cond": [_P, _P, _I, _P, _P, _P, _P, _P, _P, _P, _P],
+    "pcst_noise_mlp": [_P, _I, _I, _P, _I, _P, _I, _P, ctypes.c_int, _P, _P],
+    "pcst_cfg_ddim_step": [_P, _P, _P, _P, _I, _F, _F, _F, _F, _F, _P, _P, _P],
 }
-_RESTYPES = {"pcst_version": ctypes.c_char_p, "pcst_last_error": ctypes.c_char_p}
+_RESTYPES = {"pcst_version": ctypes.c_char_p, "pcst_last_error": ctypes.c_char_p,
+             "pcst_noise_mlp_blob_bytes": ctypes.c_int64}
 
 _lib = None
 
@@ -154,3 +167,125 @@ def group_gather(xyz, feats, fps_idx, group_idx):
     _call("pcst_group_gather", _ptr(xyz), _ptr(feats), B, N, C, _ptr(fps_idx), _ptr(group_idx),
           S, ns, _ptr(new_xyz), _ptr(grouped), _stream())
     return new_xyz, grouped
+
+
+def _workspace(fn, *dims, device):
+    sz = ctypes.c_size_t(0)
+    _call(fn, *dims, ctypes.byref(sz))
+    return torch.empty(max(sz.value, 1), dtype=torch.uint8, device=device)
+
+
+# ----------------------------------------------------------------------------- voxel downsample
+def voxel_downsample(points, target, seed=0, perm_provider=None):
+    """HierarchicalProcessor._voxel_grid_downsample_torch for N > target, all clouds at once.
+
+    perm_provider=None: the random subset is drawn on the device from `seed`.
+    perm_provider(b, n) -> int64 tensor: replay the reference's torch.randperm(n) for cloud b
+    (needs the unique-voxel count, so this path synchronises; used for parity runs).
+    Returns (points [B,T,3], idx [B,T] int64)."""
+    require_device(points)
+    points = _f32(points)
+    B, N, _ = points.shape
+    dev = points.device
+    ws = _workspace("pcst_voxel_workspace_size", B, N, device=dev)
+    out_idx = torch.empty(B, target, dtype=torch.int64, device=dev)
+    out_pts = torch.empty(B, target, 3, dtype=torch.float32, device=dev)
+    if perm_provider is None:
+        _call("pcst_voxel_downsample", _ptr(points), B, N, target, _ptr(ws), seed & (2**64 - 1),
+              _ptr(out_idx), _ptr(out_pts), _stream())
+        return out_pts, out_idx
+    counts = torch.empty(2 * B, dtype=torch.int32, device=dev)
+    _call("pcst_voxel_stats", _ptr(points), B, N, target, _ptr(ws), _ptr(counts), _stream())
+    c = counts.cpu().tolist()
+    perms, offs, lens = [], [], []
+    off = 0
+    for b in range(B):
+        U, P = c[b], c[B + b]
+        n = U if U > target else (P if U < target else 0)
+        offs.append(off)
+        lens.append(n)
+        if n:
+            p = perm_provider(b, n).to(device=dev, dtype=torch.int64)
+            perms.append(p)
+            off += n
+    perm = torch.cat(perms) if perms else torch.zeros(1, dtype=torch.int64, device=dev)
+    offs_t = torch.tensor(offs, dtype=torch.int64, device=dev)
+    lens_t = torch.tensor(lens, dtype=torch.int64, device=dev)
+    _call("pcst_voxel_select", _ptr(points), B, N, target, _ptr(ws), _ptr(perm), _ptr(offs_t),
+          _ptr(lens_t), 0, _ptr(out_idx), _ptr(out_pts), _stream())
+    err = torch.zeros(1, dtype=torch.int32, device=dev)
+    _call("pcst_voxel_error", _ptr(ws), B, N, _ptr(err), _stream())
+    if int(err.item()):
+        raise RuntimeError(f"voxel_select: replayed permutation mismatch (code {int(err.item())})")
+    return out_pts, out_idx
+
+
+def voxel_stats(points, target):
+    """(U [B], P [B]) on the host -- unique voxels and pool size (diagnostics / tests)."""
+    require_device(points)
+    points = _f32(points)
+    B, N, _ = points.shape
+    ws = _workspace("pcst_voxel_workspace_size", B, N, device=points.device)
+    counts = torch.empty(2 * B, dtype=torch.int32, device=points.device)
+    _call("pcst_voxel_stats", _ptr(points), B, N, target, _ptr(ws), _ptr(counts), _stream())
+    c = counts.cpu()
+    return c[:B], c[B:]
+
+
+# ----------------------------------------------------------------------------- kNN upsample
+def knn3_interp(coarse, orig, idx, check=False):
+    """HierarchicalProcessor.upsample_knn: coarse [B,M,3], orig [B,N,3], idx [B,M] -> [B,N,3]."""
+    require_device(coarse, orig, idx)
+    coarse, orig, idx = _f32(coarse), _f32(orig), _i64(idx)
+    B, N, _ = orig.shape
+    M = idx.shape[1]
+    ws = _workspace("pcst_knn_workspace_size", B, N, M, device=orig.device)
+    out = torch.empty(B, N, 3, dtype=torch.float32, device=orig.device)
+    _call("pcst_knn3_interp", _ptr(coarse), _ptr(orig), _ptr(idx), B, N, M, _ptr(out), _ptr(ws),
+          _stream())
+    if check:
+        err = torch.zeros(1, dtype=torch.int32, device=orig.device)
+        _call("pcst_knn_error", _ptr(ws), B, N, M, _ptr(err), _stream())
+        if int(err.item()):
+            raise RuntimeError("knn3_interp: coarse index outside [0, N)")
+    return out
+
+
+# ----------------------------------------------------------------------------- noise MLP
+def noise_mlp_blob_bytes(precision):
+    return int(lib().pcst_noise_mlp_blob_bytes(precision))
+
+
+def noise_cond(t, style, freqs, wt, bt, ws_, bs, b4):
+    require_device(t, style)
+    t, style = _i64(t), _f32(style)
+    C = t.shape[0]
+    cond = torch.empty(C, 256, dtype=torch.float32, device=style.device)
+    _call("pcst_noise_cond", _ptr(t), _ptr(style), C, _ptr(freqs), _ptr(wt), _ptr(bt), _ptr(ws_),
+          _ptr(bs), _ptr(b4), _ptr(cond), _stream())
+    return cond
+
+
+def noise_mlp(pts, points_per_cloud, cond, blob, bias, precision, out=None):
+    """pts [P,3] (P = clouds*points_per_cloud, cloud-major) -> eps [P,3]."""
+    require_device(pts, cond, blob, bias)
+    pts = _f32(pts)
+    P = pts.shape[0]
+    if out is None:
+        out = torch.empty(P, 3, dtype=torch.float32, device=pts.device)
+    _call("pcst_noise_mlp", _ptr(pts), P, points_per_cloud, _ptr(cond), cond.shape[0], _ptr(blob),
+          blob.numel(), _ptr(bias), precision, _ptr(out), _stream())
+    return out
+
+
+# ----------------------------------------------------------------------------- CFG / DDIM update
+def cfg_ddim_step(x, eps_c, eps_u, source, guidance_scale, coeffs, x_cat=None, out=None):
+    """coeffs = (sqrt(1-a_t), sqrt(a_t)+1e-8, sqrt(a_prev), sqrt(1-a_prev)) as fp32 values."""
+    require_device(x, eps_c, eps_u, source, x_cat)
+    x = _f32(x)
+    if out is None:
+        out = torch.empty_like(x)
+    c1, c2, c3, c4 = (float(c) for c in coeffs)
+    _call("pcst_cfg_ddim_step", _ptr(x), _ptr(eps_c), _ptr(eps_u), _ptr(source), x.numel(),
+          float(guidance_scale), c1, c2, c3, c4, _ptr(out), _ptr(x_cat), _stream())
+    return out

@@ -1,0 +1,55 @@
+// Fused classifier-free-guidance + DDIM update of DiffusionProcess.guided_sample_loop
+// (models/diffusion_model.py:248-260) and of ddim_sample_loop (:283-290).
+//   eps = eps_u + s*(eps_c - eps_u)                          (CFG only)
+//   x0  = (x - sqrt(1-a_t)*eps) / (sqrt(a_t) + 1e-8)
+//   x0  = x0 + 0.1*(source - x0)                             (guided only)
+//   x0  = tanh(x0/1.8)*1.8
+//   x'  = sqrt(a_prev)*x0 + sqrt(1-a_prev)*eps
+// The four per-step scalars are computed on the host in fp32 exactly as the reference's 0-d
+// tensor ops do.  The new x is also written into both halves of the next step's CFG batch
+// (torch.cat([x]*2), :240), so no separate concatenation pass exists.
+#include "common.h"
+
+namespace pcst {
+
+__global__ void cfg_ddim_kernel(const float* __restrict__ x, const float* __restrict__ eps_c,
+                                const float* __restrict__ eps_u, const float* __restrict__ src,
+                                int64_t n, float scale, float c1, float c2, float c3, float c4,
+                                float* __restrict__ x_out, float* __restrict__ x_cat) {
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < n;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    float eps = eps_c[e];
+    if (eps_u) {
+      const float u = eps_u[e];
+      eps = fadd(u, fmul(scale, fsub(eps, u)));
+    }
+    float x0 = __fdiv_rn(fsub(x[e], fmul(c1, eps)), c2);
+    if (src) x0 = fadd(x0, fmul(0.1f, fsub(src[e], x0)));
+    x0 = fmul(tanhf(__fdiv_rn(x0, 1.8f)), 1.8f);
+    const float xn = fadd(fmul(c3, x0), fmul(c4, eps));
+    x_out[e] = xn;
+    if (x_cat) {
+      x_cat[e] = xn;
+      x_cat[n + e] = xn;
+    }
+  }
+}
+
+}  // namespace pcst
+
+using namespace pcst;
+
+extern "C" int pcst_cfg_ddim_step(const float* x, const float* eps_c, const float* eps_u,
+                                  const float* source, int64_t n, float guidance_scale,
+                                  float sqrt_1m_at, float sqrt_at_eps, float sqrt_aprev,
+                                  float sqrt_1m_aprev, float* x_out, float* x_cat, void* stream) {
+  PCST_CHECK_ARG(n >= 0, "cfg_ddim_step: bad size");
+  if (n == 0) return PCST_OK;
+  PCST_CHECK_ARG(x && eps_c && x_out, "cfg_ddim_step: null pointer");
+  const int64_t g = std::min<int64_t>(cdiv(n, 256), 4096);
+  hipLaunchKernelGGL(cfg_ddim_kernel, dim3((unsigned)g), dim3(256), 0, as_stream(stream), x, eps_c,
+                     eps_u, source, n, guidance_scale, sqrt_1m_at, sqrt_at_eps, sqrt_aprev,
+                     sqrt_1m_aprev, x_out, x_cat);
+  PCST_LAUNCH_CHECK("cfg_ddim_step");
+  return PCST_OK;
+}

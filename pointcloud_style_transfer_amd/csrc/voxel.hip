@@ -1,0 +1,412 @@
+// Voxel-hash downsample of HierarchicalProcessor._voxel_grid_downsample_torch
+// (models/diffusion_model.py:69-122), all clouds of a batch at once, entirely on the device
+// (no host round trip for the data-dependent unique-voxel count U or pool size P).
+//
+// Pipeline (one segment per cloud, grid.y = cloud):
+//   minmax -> voxel size + int32 wrap-around hash -> stable LSD radix sort (hash, index)
+//   -> unique voxels (head flags, tile scan) -> per-voxel index sum/count (wave segmented
+//   reduction + int64 atomics, exact and order independent) -> representative
+//   trunc(f32(sum)/f32(count)) in ascending signed-hash order (Q5/Q6) -> pool of
+//   non-representative indices in ascending order (tile compaction) -> selection:
+//     U > T : reps[perm[:T]]          U < T : reps ++ pool[perm[:T-U]]      U == T : reps
+//   with perm either replayed (parity) or drawn on the device: Philox-style 32-bit keys
+//   per candidate + the same radix sort = torch.randperm's random-key-sort construction.
+#include "common.h"
+#include "sort.h"
+#include "cloud.h"
+
+namespace pcst {
+
+struct VoxelWS {
+  int32_t* mm;           // [B][6] ordered-int min xyz, max xyz
+  uint32_t *kA, *vA, *kB, *vB;  // [B][N]
+  uint32_t* hist;        // radix hist
+  uint32_t* tileh;       // [B][tiles]
+  int32_t* U;            // [B]
+  int32_t* P;            // [B]
+  int32_t* cand;         // [B]
+  unsigned long long* sum;  // [B][N]
+  uint32_t* cnt;         // [B][N]
+  int64_t* reps;         // [B][N]
+  uint32_t* isrep;       // [B][N]
+  int32_t* pool;         // [B][N]
+  int32_t* err;          // [1]
+  size_t bytes;
+};
+
+static VoxelWS carve_voxel(void* base, int64_t B, int64_t N) {
+  Carver c(base);
+  VoxelWS w;
+  const size_t BN = (size_t)(B * N);
+  const int64_t tiles = cdiv(N, kSortTile);
+  w.mm = c.take<int32_t>(B * 6);
+  w.kA = c.take<uint32_t>(BN);
+  w.vA = c.take<uint32_t>(BN);
+  w.kB = c.take<uint32_t>(BN);
+  w.vB = c.take<uint32_t>(BN);
+  w.hist = c.take<uint32_t>(radix_hist_words((int)B, N));
+  w.tileh = c.take<uint32_t>(B * tiles);
+  w.U = c.take<int32_t>(B);
+  w.P = c.take<int32_t>(B);
+  w.cand = c.take<int32_t>(B);
+  w.err = c.take<int32_t>(4);
+  // zeroed every call: sum, cnt, isrep are contiguous so one memset covers them
+  w.sum = c.take<unsigned long long>(BN);
+  w.cnt = c.take<uint32_t>(BN);
+  w.isrep = c.take<uint32_t>(BN);
+  w.reps = c.take<int64_t>(BN);
+  w.pool = c.take<int32_t>(BN);
+  w.bytes = c.bytes();
+  return w;
+}
+
+// voxel_size = (prod(range)/target)^(1/3) * 1.2 with the reference's fp32/fp64 steps
+// (diffusion_model.py:82-87): range < 1e-6 -> 1; prod = (r0*r1)*r2 in fp32; pow of the 0-d
+// fp32 tensor is evaluated in double (verified bit-exact), then * 1.2f; < 1e-6 -> 1e-3.
+__device__ __forceinline__ float voxel_size(const int32_t* M, int64_t target) {
+  float r[3];
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    r[c] = fsub(ord2f(M[3 + c]), ord2f(M[c]));
+    if (r[c] < 1e-6f) r[c] = 1.0f;
+  }
+  const float prod = fmul(fmul(r[0], r[1]), r[2]);
+  const float q = __fdiv_rn(prod, (float)target);
+  float vs = (float)pow((double)q, 1.0 / 3.0);
+  vs = fmul(vs, 1.2f);
+  if (vs < 1e-6f) vs = 1e-3f;
+  return vs;
+}
+
+__device__ __forceinline__ int32_t wrap_mul(int32_t a, uint32_t m) {
+  return (int32_t)((uint32_t)a * m);
+}
+
+// v = int32(floor((p - min) / vs)); h = (vx*73856093)^(vy*19349663)^(vz*83492791) (int32 wrap,
+// Q5).  Sort key = h ^ 0x80000000 so unsigned order == torch.unique's signed order.
+__global__ __launch_bounds__(256) void vox_hash_kernel(const float* __restrict__ pts, int N,
+                                                       int64_t target, const int32_t* __restrict__ mm,
+                                                       uint32_t* __restrict__ keys,
+                                                       uint32_t* __restrict__ vals) {
+  const int b = blockIdx.y;
+  const int32_t* M = mm + b * 6;
+  const float vs = voxel_size(M, target);
+  const float m0 = ord2f(M[0]), m1 = ord2f(M[1]), m2 = ord2f(M[2]);
+  const float* P = pts + (int64_t)b * N * 3;
+  for (int n = blockIdx.x * 256 + threadIdx.x; n < N; n += gridDim.x * 256) {
+    const int32_t vx = (int32_t)floorf(__fdiv_rn(fsub(P[n * 3 + 0], m0), vs));
+    const int32_t vy = (int32_t)floorf(__fdiv_rn(fsub(P[n * 3 + 1], m1), vs));
+    const int32_t vz = (int32_t)floorf(__fdiv_rn(fsub(P[n * 3 + 2], m2), vs));
+    const int32_t h = wrap_mul(vx, 73856093u) ^ wrap_mul(vy, 19349663u) ^ wrap_mul(vz, 83492791u);
+    keys[(int64_t)b * N + n] = (uint32_t)h ^ 0x80000000u;
+    vals[(int64_t)b * N + n] = (uint32_t)n;
+  }
+}
+
+// Tile element i for (wave w, round r, lane l): base + w*1024 + r*64 + l (input order).
+__device__ __forceinline__ int tile_elem(int base, int w, int r, int lane) {
+  return base + w * (kSortRounds * 64) + r * 64 + lane;
+}
+
+// Count voxel heads (first element of each run of equal sorted keys) per tile.
+__global__ __launch_bounds__(256) void vox_head_count_kernel(const uint32_t* __restrict__ keys,
+                                                             int N, int tiles,
+                                                             uint32_t* __restrict__ tileh) {
+  const int b = blockIdx.y, tile = blockIdx.x;
+  const int base = tile * kSortTile;
+  const uint32_t* K = keys + (int64_t)b * N;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  uint32_t c = 0;
+  for (int r = 0; r < kSortRounds; ++r) {
+    const int i = tile_elem(base, w, r, lane);
+    const bool head = i < N && (i == 0 || K[i] != K[i - 1]);
+    c += __popcll(__ballot(head));
+  }
+  __shared__ uint32_t s[4];
+  if (lane == 0) s[w] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) tileh[(int64_t)b * tiles + tile] = s[0] + s[1] + s[2] + s[3];
+}
+
+// Per-voxel sum of point indices and count: segment id = (#heads in [0, i]) - 1; a wave
+// segmented scan leaves one int64 atomic per voxel run per 64 elements.
+__global__ __launch_bounds__(256) void vox_segsum_kernel(const uint32_t* __restrict__ keys,
+                                                         const uint32_t* __restrict__ vals, int N,
+                                                         int tiles,
+                                                         const uint32_t* __restrict__ tileoff,
+                                                         unsigned long long* __restrict__ sum,
+                                                         uint32_t* __restrict__ cnt) {
+  const int b = blockIdx.y, tile = blockIdx.x;
+  const int base = tile * kSortTile;
+  if (base >= N) return;
+  const uint32_t* K = keys + (int64_t)b * N;
+  const uint32_t* V = vals + (int64_t)b * N;
+  unsigned long long* S = sum + (int64_t)b * N;
+  uint32_t* C = cnt + (int64_t)b * N;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const unsigned long long lt = lanemask_lt();
+  unsigned long long heads[kSortRounds];
+  uint32_t wc = 0;
+#pragma unroll
+  for (int r = 0; r < kSortRounds; ++r) {
+    const int i = tile_elem(base, w, r, lane);
+    heads[r] = __ballot(i < N && (i == 0 || K[i] != K[i - 1]));
+    wc += __popcll(heads[r]);
+  }
+  __shared__ uint32_t s[4];
+  if (lane == 0) s[w] = wc;
+  __syncthreads();
+  int run = (int)tileoff[(int64_t)b * tiles + tile];
+  for (int q = 0; q < w; ++q) run += (int)s[q];
+#pragma unroll
+  for (int r = 0; r < kSortRounds; ++r) {
+    const int i = tile_elem(base, w, r, lane);
+    const bool valid = i < N;
+    const int seg = run + (int)__popcll(heads[r] & (lt | (1ull << lane))) - 1;
+    run += (int)__popcll(heads[r]);
+    unsigned long long v = valid ? (unsigned long long)V[i] : 0ull;
+    uint32_t c = valid ? 1u : 0u;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const unsigned long long ov = __shfl_up(v, off);
+      const uint32_t oc = __shfl_up(c, off);
+      const int os = __shfl_up(seg, off);
+      if (lane >= off && os == seg) { v += ov; c += oc; }
+    }
+    const int nseg = __shfl_down(seg, 1);
+    const bool last = valid && (lane == 63 || nseg != seg || i + 1 >= N);
+    if (last) {
+      atomicAdd(&S[seg], v);
+      atomicAdd(&C[seg], c);
+    }
+  }
+}
+
+// rep_k = trunc(f32(sum_k) / f32(count_k))  (int64 / int64 true division -> float32, Q6).
+__global__ void vox_reps_kernel(const unsigned long long* __restrict__ sum,
+                                const uint32_t* __restrict__ cnt, const int32_t* __restrict__ U,
+                                int N, int64_t* __restrict__ reps, uint32_t* __restrict__ isrep) {
+  const int b = blockIdx.y;
+  const int u = U[b];
+  for (int k = blockIdx.x * 256 + threadIdx.x; k < u; k += gridDim.x * 256) {
+    const float fs = (float)(long long)sum[(int64_t)b * N + k];
+    const float fc = (float)cnt[(int64_t)b * N + k];
+    const int64_t r = (int64_t)__fdiv_rn(fs, fc);
+    reps[(int64_t)b * N + k] = r;
+    isrep[(int64_t)b * N + r] = 1u;
+  }
+}
+
+// Pool = ascending indices n with !isrep[n] (diffusion_model.py:105-108).
+__global__ __launch_bounds__(256) void vox_pool_count_kernel(const uint32_t* __restrict__ isrep,
+                                                             int N, int tiles,
+                                                             uint32_t* __restrict__ tileh) {
+  const int b = blockIdx.y, tile = blockIdx.x;
+  const int base = tile * kSortTile;
+  const uint32_t* F = isrep + (int64_t)b * N;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  uint32_t c = 0;
+  for (int r = 0; r < kSortRounds; ++r) {
+    const int i = tile_elem(base, w, r, lane);
+    c += __popcll(__ballot(i < N && F[i] == 0u));
+  }
+  __shared__ uint32_t s[4];
+  if (lane == 0) s[w] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) tileh[(int64_t)b * tiles + tile] = s[0] + s[1] + s[2] + s[3];
+}
+
+__global__ __launch_bounds__(256) void vox_pool_write_kernel(const uint32_t* __restrict__ isrep,
+                                                             int N, int tiles,
+                                                             const uint32_t* __restrict__ tileoff,
+                                                             int32_t* __restrict__ pool) {
+  const int b = blockIdx.y, tile = blockIdx.x;
+  const int base = tile * kSortTile;
+  if (base >= N) return;
+  const uint32_t* F = isrep + (int64_t)b * N;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const unsigned long long lt = lanemask_lt();
+  unsigned long long m[kSortRounds];
+  uint32_t wc = 0;
+#pragma unroll
+  for (int r = 0; r < kSortRounds; ++r) {
+    const int i = tile_elem(base, w, r, lane);
+    m[r] = __ballot(i < N && F[i] == 0u);
+    wc += __popcll(m[r]);
+  }
+  __shared__ uint32_t s[4];
+  if (lane == 0) s[w] = wc;
+  __syncthreads();
+  uint32_t run = tileoff[(int64_t)b * tiles + tile];
+  for (int q = 0; q < w; ++q) run += s[q];
+#pragma unroll
+  for (int r = 0; r < kSortRounds; ++r) {
+    const int i = tile_elem(base, w, r, lane);
+    if ((m[r] >> lane) & 1ull) pool[(int64_t)b * N + run + __popcll(m[r] & lt)] = i;
+    run += __popcll(m[r]);
+  }
+}
+
+__global__ void vox_cand_kernel(const int32_t* U, const int32_t* P, int B, int64_t target,
+                                int32_t* cand) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  const int u = U[b];
+  cand[b] = u > target ? u : (u < target ? P[b] : 0);
+}
+
+// splitmix64 finaliser: counter-based random keys (seed, cloud, candidate).
+__device__ __forceinline__ uint32_t rand_key(uint64_t seed, int b, int i) {
+  uint64_t z = seed + 0x9E3779B97F4A7C15ull * ((uint64_t)b * 0x100000001ull + (uint64_t)i + 1);
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return (uint32_t)((z ^ (z >> 31)) >> 32);
+}
+
+__global__ void vox_randkey_kernel(const int32_t* __restrict__ cand, int N, uint64_t seed,
+                                   uint32_t* __restrict__ keys, uint32_t* __restrict__ vals) {
+  const int b = blockIdx.y;
+  const int n = cand[b];
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
+    keys[(int64_t)b * N + i] = rand_key(seed, b, i);
+    vals[(int64_t)b * N + i] = (uint32_t)i;
+  }
+}
+
+// Final selection + gather of the kept points (diffusion_model.py:99-119).
+// perm source: replayed int64 perms (perm + perm_off[b], perm_len[b]) or device-drawn (dperm).
+__global__ void vox_select_kernel(const float* __restrict__ pts, int N, int64_t T,
+                                  const int32_t* __restrict__ U, const int32_t* __restrict__ P,
+                                  const int64_t* __restrict__ reps, const int32_t* __restrict__ pool,
+                                  const int64_t* __restrict__ perm, const int64_t* __restrict__ perm_off,
+                                  const int64_t* __restrict__ perm_len,
+                                  const uint32_t* __restrict__ dperm, int32_t* __restrict__ err,
+                                  int64_t* __restrict__ out_idx, float* __restrict__ out_pts) {
+  const int b = blockIdx.y;
+  const int u = U[b], p = P[b];
+  const int64_t* R = reps + (int64_t)b * N;
+  for (int64_t j = blockIdx.x * 256 + threadIdx.x; j < T; j += gridDim.x * 256) {
+    int64_t r;
+    int64_t pj = -1;  // position drawn from the permutation
+    if (u == T) {
+      r = R[j];
+    } else if (u > T) {
+      pj = j;
+    } else {
+      if (j < u) r = R[j];
+      else pj = j - u;
+    }
+    if (pj >= 0) {
+      int64_t k;
+      if (perm) {
+        const int64_t need = u > T ? u : p;
+        if (perm_len[b] != need && threadIdx.x == 0) atomicOr(err, 1);
+        k = perm[perm_off[b] + pj];
+        if (k < 0 || k >= need) { atomicOr(err, 2); k = 0; }
+      } else {
+        k = dperm[(int64_t)b * N + pj];
+      }
+      r = u > T ? R[k] : (int64_t)pool[(int64_t)b * N + k];
+    }
+    out_idx[(int64_t)b * T + j] = r;
+    const float* src = pts + ((int64_t)b * N + r) * 3;
+    float* dst = out_pts + ((int64_t)b * T + j) * 3;
+    dst[0] = src[0]; dst[1] = src[1]; dst[2] = src[2];
+  }
+}
+
+}  // namespace pcst
+
+using namespace pcst;
+
+extern "C" int pcst_voxel_workspace_size(int64_t B, int64_t N, size_t* bytes) {
+  PCST_CHECK_ARG(B >= 0 && N >= 0 && bytes, "voxel_workspace_size: bad args");
+  *bytes = carve_voxel(nullptr, B, N).bytes;
+  return PCST_OK;
+}
+
+static int voxel_grid(int64_t N) { return (int)std::min<int64_t>(cdiv(N, 256), 1024); }
+
+extern "C" int pcst_voxel_stats(const float* pts, int64_t B, int64_t N, int64_t target,
+                                void* workspace, int32_t* counts_out, void* stream) {
+  PCST_CHECK_ARG(B > 0 && N > target && target > 0 && N < (1ll << 30), "voxel_stats: bad shape");
+  PCST_CHECK_ARG(pts && workspace, "voxel_stats: null pointer");
+  hipStream_t s = as_stream(stream);
+  VoxelWS w = carve_voxel(workspace, B, N);
+  const int tiles = (int)cdiv(N, kSortTile);
+  const int b = (int)B, n = (int)N;
+  const size_t zero_bytes = (size_t)((char*)w.reps - (char*)w.sum);
+  PCST_HIP(hipMemsetAsync(w.sum, 0, zero_bytes, s), "voxel_stats: memset");
+  PCST_HIP(hipMemsetAsync(w.err, 0, 16, s), "voxel_stats: memset");
+  launch_cloud_minmax(pts, b, n, w.mm, s);
+  hipLaunchKernelGGL(vox_hash_kernel, dim3(voxel_grid(N), b), dim3(256), 0, s, pts, n, target, w.mm,
+                     w.kA, w.vA);
+  SegCounts all{nullptr, n};
+  int rc = radix_sort_pairs(w.kA, w.vA, w.kB, w.vB, w.hist, b, N, all, 0, 32, s);
+  if (rc) return rc;
+  hipLaunchKernelGGL(vox_head_count_kernel, dim3(tiles, b), dim3(256), 0, s, w.kA, n, tiles,
+                     w.tileh);
+  hipLaunchKernelGGL(seg_scan_kernel, dim3(b), dim3(1024), 0, s, w.tileh, 1, tiles, all,
+                     kSortTile, w.U);
+  hipLaunchKernelGGL(vox_segsum_kernel, dim3(tiles, b), dim3(256), 0, s, w.kA, w.vA, n, tiles,
+                     w.tileh, w.sum, w.cnt);
+  hipLaunchKernelGGL(vox_reps_kernel, dim3(voxel_grid(N), b), dim3(256), 0, s, w.sum, w.cnt, w.U,
+                     n, w.reps, w.isrep);
+  hipLaunchKernelGGL(vox_pool_count_kernel, dim3(tiles, b), dim3(256), 0, s, w.isrep, n, tiles,
+                     w.tileh);
+  hipLaunchKernelGGL(seg_scan_kernel, dim3(b), dim3(1024), 0, s, w.tileh, 1, tiles, all,
+                     kSortTile, w.P);
+  hipLaunchKernelGGL(vox_pool_write_kernel, dim3(tiles, b), dim3(256), 0, s, w.isrep, n, tiles,
+                     w.tileh, w.pool);
+  hipLaunchKernelGGL(vox_cand_kernel, dim3(cdiv(B, 256)), dim3(256), 0, s, w.U, w.P, b, target,
+                     w.cand);
+  if (counts_out) {
+    PCST_HIP(hipMemcpyAsync(counts_out, w.U, sizeof(int32_t) * B, hipMemcpyDeviceToDevice, s),
+             "voxel_stats: copy U");
+    PCST_HIP(hipMemcpyAsync(counts_out + B, w.P, sizeof(int32_t) * B, hipMemcpyDeviceToDevice, s),
+             "voxel_stats: copy P");
+  }
+  PCST_LAUNCH_CHECK("voxel_stats");
+  return PCST_OK;
+}
+
+extern "C" int pcst_voxel_select(const float* pts, int64_t B, int64_t N, int64_t target,
+                                 void* workspace, const int64_t* perm, const int64_t* perm_off,
+                                 const int64_t* perm_len, uint64_t seed, int64_t* out_idx,
+                                 float* out_pts, void* stream) {
+  PCST_CHECK_ARG(B > 0 && N > target && target > 0, "voxel_select: bad shape");
+  PCST_CHECK_ARG(pts && workspace && out_idx && out_pts, "voxel_select: null pointer");
+  PCST_CHECK_ARG(!perm || (perm_off && perm_len), "voxel_select: perm needs perm_off/perm_len");
+  hipStream_t s = as_stream(stream);
+  VoxelWS w = carve_voxel(workspace, B, N);
+  const int b = (int)B, n = (int)N;
+  if (!perm) {
+    hipLaunchKernelGGL(vox_randkey_kernel, dim3(voxel_grid(N), b), dim3(256), 0, s, w.cand, n,
+                       seed, w.kA, w.vA);
+    SegCounts cc{w.cand, 0};
+    int rc = radix_sort_pairs(w.kA, w.vA, w.kB, w.vB, w.hist, b, N, cc, 0, 32, s);
+    if (rc) return rc;
+  }
+  hipLaunchKernelGGL(vox_select_kernel, dim3((unsigned)std::min<int64_t>(cdiv(target, 256), 1024), b),
+                     dim3(256), 0, s, pts, n, target, w.U, w.P, w.reps, w.pool, perm, perm_off,
+                     perm_len, w.vA, w.err, out_idx, out_pts);
+  PCST_LAUNCH_CHECK("voxel_select");
+  return PCST_OK;
+}
+
+extern "C" int pcst_voxel_error(void* workspace, int64_t B, int64_t N, int32_t* err_out,
+                                void* stream) {
+  VoxelWS w = carve_voxel(workspace, B, N);
+  PCST_HIP(hipMemcpyAsync(err_out, w.err, sizeof(int32_t), hipMemcpyDeviceToDevice,
+                          as_stream(stream)), "voxel_error");
+  return PCST_OK;
+}
+
+extern "C" int pcst_voxel_downsample(const float* pts, int64_t B, int64_t N, int64_t target,
+                                     void* workspace, uint64_t seed, int64_t* out_idx,
+                                     float* out_pts, void* stream) {
+  int rc = pcst_voxel_stats(pts, B, N, target, workspace, nullptr, stream);
+  if (rc) return rc;
+  return pcst_voxel_select(pts, B, N, target, workspace, nullptr, nullptr, nullptr, seed, out_idx,
+                           out_pts, stream);
+}

@@ -1,0 +1,132 @@
+"""Host-side packing of NoisePredictor weights into the streaming layout of
+csrc/noise_mlp.hip (done once per weight version, cached on the module).
+
+Blob = sequence of 32 KiB parts; every layer starts on a fresh part.  A part holds
+MFMA A-operand fragments, each the exact bytes one wave reads with one 16-B (bf16)
+or 4-B (f32) per-lane LDS load:
+
+  bf16 (v_mfma_f32_32x32x16_bf16), fragment (ob, s) = 1 KiB:
+     lane l = (r = l & 31, h = l >> 5), element j  ->  W[32 ob + r, k]
+     k = 32 (s // 2) + 16 (s % 2) + 8 (j >> 2) + 4 h + (j & 3)
+  f32 (v_mfma_f32_32x32x2_f32), fragment (ob, s) = 256 B:
+     lane l = (r, h)  ->  W[32 ob + r, k],  k = 32 (s // 16) + (rr & 3) + 8 (rr >> 2) + 4 h,
+     rr = s % 16
+
+The k permutation is the row order in which the previous layer's accumulator
+registers arrive as this layer's B operand (the C/D map row = (reg & 3) + 8 (reg >> 2)
++ 4 (lane >> 5)), so activations never leave registers between layers.
+
+Order: point_encoder.2, point_encoder.4, 6 x 16 residual chunks (W1 rows of the chunk,
+then W2 columns of the chunk for the 8 output blocks), output_mlp.0 / .2 / .4.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+PART = 32768
+BF16, F32 = 1, 0
+
+# bias table offsets (floats) -- must match csrc/noise_mlp.hip
+OFF_W0, OFF_B0, OFF_B2, OFF_B1, OFF_BB2, OFF_O0, OFF_O2, OFF_O4, BIAS_FLOATS = (
+    0, 384, 512, 768, 3840, 5376, 5632, 5760, 5792)
+
+
+def _kmap(precision, nsteps):
+    """k index [s, lane, j] (bf16) or [s, lane] (f32) for a K = 32*nblocks input."""
+    lanes = np.arange(64)
+    h = lanes >> 5
+    if precision == BF16:
+        s = np.arange(nsteps)[:, None, None]
+        j = np.arange(8)[None, None, :]
+        return (32 * (s // 2) + 16 * (s % 2) + 8 * (j >> 2) + 4 * h[None, :, None] + (j & 3))
+    s = np.arange(nsteps)[:, None]
+    rr = s % 16
+    return 32 * (s // 16) + (rr & 3) + 8 * (rr >> 2) + 4 * h[None, :]
+
+
+def _frags(W, precision):
+    """W [O, K] float32 (O padded to a multiple of 32) -> [O/32, S, fragment elements]."""
+    O, K = W.shape
+    ks = 16 if precision == BF16 else 2
+    nsteps = K // ks
+    km = _kmap(precision, nsteps)
+    r = np.arange(64) & 31
+    nob = (O + 31) // 32
+    Wp = np.zeros((nob * 32, K), np.float32)
+    Wp[:O] = W
+    out = []
+    for ob in range(nob):
+        rows = ob * 32 + r  # [64]
+        if precision == BF16:
+            f = Wp[rows[None, :, None], km]  # [S, 64, 8]
+        else:
+            f = Wp[rows[None, :], km]  # [S, 64]
+        out.append(f.reshape(nsteps, -1))
+    return np.stack(out)  # [nob, S, 512 or 64]
+
+
+def _to_bytes(a, precision):
+    t = torch.from_numpy(np.ascontiguousarray(a, np.float32))
+    if precision == BF16:
+        t = t.to(torch.bfloat16)
+    return t.contiguous().view(torch.uint8).numpy().reshape(-1)
+
+
+def _pad_part(b):
+    n = (-len(b)) % PART
+    return np.concatenate([b, np.zeros(n, np.uint8)]) if n else b
+
+
+def pack_blob(sd, precision, pre="noise_predictor"):
+    """sd: mapping name -> float32 numpy array (NoisePredictor params).  Returns uint8 array."""
+    g = lambda n: np.asarray(sd[f"{pre}.{n}"], np.float32)  # noqa: E731
+    parts = []
+
+    def layer(W):
+        F = _frags(W, precision)
+        parts.append(_pad_part(_to_bytes(F.reshape(-1), precision)))
+
+    layer(g("point_encoder.2.weight"))
+    layer(g("point_encoder.4.weight"))
+    ks = 16 if precision == BF16 else 2
+    opb = 32 // ks
+    for i in range(6):
+        F1 = _frags(g(f"layers.{i}.0.weight"), precision)  # [16, 256/ks, e]
+        F2 = _frags(g(f"layers.{i}.2.weight"), precision)  # [8, 512/ks, e]
+        for c in range(16):
+            w1 = _to_bytes(F1[c].reshape(-1), precision)
+            w2 = _to_bytes(F2[:, c * opb:(c + 1) * opb].reshape(-1), precision)
+            if precision == BF16:
+                parts.append(_pad_part(np.concatenate([w1, w2])))
+            else:
+                parts.append(_pad_part(w1))
+                parts.append(_pad_part(w2))
+    layer(g("output_mlp.0.weight"))
+    layer(g("output_mlp.2.weight"))
+    layer(g("output_mlp.4.weight"))
+    return np.concatenate(parts)
+
+
+def pack_bias(sd, pre="noise_predictor"):
+    g = lambda n: np.asarray(sd[f"{pre}.{n}"], np.float32)  # noqa: E731
+    t = np.zeros(BIAS_FLOATS, np.float32)
+    t[OFF_W0:OFF_W0 + 384] = g("point_encoder.0.weight").reshape(-1)
+    t[OFF_B0:OFF_B0 + 128] = g("point_encoder.0.bias")
+    t[OFF_B2:OFF_B2 + 256] = g("point_encoder.2.bias")
+    for i in range(6):
+        t[OFF_B1 + 512 * i:OFF_B1 + 512 * (i + 1)] = g(f"layers.{i}.0.bias")
+        t[OFF_BB2 + 256 * i:OFF_BB2 + 256 * (i + 1)] = g(f"layers.{i}.2.bias")
+    t[OFF_O0:OFF_O0 + 256] = g("output_mlp.0.bias")
+    t[OFF_O2:OFF_O2 + 128] = g("output_mlp.2.bias")
+    t[OFF_O4:OFF_O4 + 3] = g("output_mlp.4.bias")
+    return t
+
+
+def time_freqs(dim=128):
+    """TimeEmbedding frequency table exactly as the reference builds it on the CPU
+    (diffusion_model.py:18-22): exp(arange(half) * -(ln 1e4 / (half-1))) in fp32."""
+    import math
+
+    half = dim // 2
+    return torch.exp(torch.arange(half) * -(math.log(10000) / (half - 1))).float()

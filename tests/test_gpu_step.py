@@ -1,0 +1,186 @@
+"""HIP kernels of the guided denoising step vs reference golden vectors and the oracle:
+voxel downsample (bit-exact with replayed permutations), kNN-3 IDW upsample (bit-exact),
+fused noise MLP (fp32 mode within 1e-4 rel; bf16 mode within the bf16 tolerance below),
+CFG/DDIM update."""
+import numpy as np
+import pytest
+import torch
+
+from conftest import assert_close
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+# bf16 operands with fp32 accumulation through 17 chained layers: normwise relative error
+# of the predicted noise vs the fp32 reference (stated tolerance of the perf path).
+BF16_NORM_RTOL = 3e-2
+
+
+@pytest.fixture(scope="module")
+def H():
+    from pointcloud_style_transfer_amd import _hip
+
+    assert torch.cuda.is_available()
+    _hip.lib()
+    return _hip
+
+
+def dev(a):
+    return torch.from_numpy(np.ascontiguousarray(a)).cuda()
+
+
+def provider_from(draws):
+    it = iter(draws)
+
+    def p(b, n):
+        v = next(it)
+        assert len(v) == n, (len(v), n)
+        return torch.from_numpy(np.asarray(v, np.int64))
+    return p
+
+
+@pytest.mark.parametrize("key", ["pad", "sub"])
+def test_voxel_golden(H, golden, key):
+    g = golden("hierarchical.npz")
+    names = list(g[f"{key}_rng_names"])
+    draws = [g[f"{key}_rng_{i}"] for i in range(len(names))]
+    pts, idx = H.voxel_downsample(dev(g[f"{key}_pts"]), int(g[f"{key}_target"]),
+                                  perm_provider=provider_from(draws))
+    np.testing.assert_array_equal(idx.cpu().numpy(), g[f"{key}_idx"])
+    np.testing.assert_array_equal(pts.cpu().numpy(), g[f"{key}_down"])
+
+
+def test_voxel_golden_120k(H, golden):
+    from pointcloud_style_transfer_amd.synthetic import lidar_like_cloud
+
+    g = golden("hierarchical.npz")
+    pts = lidar_like_cloud(int(g["full_seed"]), 120000)[None]
+    _, idx = H.voxel_downsample(dev(pts), 30000, perm_provider=provider_from([g["full_perm"]]))
+    np.testing.assert_array_equal(idx.cpu().numpy(), g["full_idx"].astype(np.int64))
+
+
+@pytest.mark.parametrize("N,T,B,sig", [(5000, 1000, 3, (1, 1, 0.15)), (20000, 3000, 2, (1, 1, 1e-3)),
+                                        (70000, 30000, 2, (1, 1, 0.15)), (9000, 8000, 1, (1, 1, 1))])
+def test_voxel_vs_oracle_random_perm(H, N, T, B, sig):
+    """Reps/pool bit-exact vs the oracle; the device-drawn subset is a valid draw."""
+    rng = np.random.default_rng(N)
+    pts = (rng.standard_normal((B, N, 3)) * np.array(sig)).astype(np.float32)
+    U, P = H.voxel_stats(dev(pts), T)
+    for b in range(B):
+        reps, _, _ = O.voxel_reps(pts[b], T)
+        assert int(U[b]) == len(reps)
+        assert int(P[b]) == N - len(np.unique(reps))
+    # replay random permutations drawn here -> bit-exact vs the oracle
+    perms = []
+    for b in range(B):
+        n = int(U[b]) if int(U[b]) > T else (int(P[b]) if int(U[b]) < T else 0)
+        if n:
+            perms.append(rng.permutation(n))
+    _, idx = H.voxel_downsample(dev(pts), T, perm_provider=provider_from(perms))
+    _, ref = O.voxel_downsample(pts, T, O.Replay([("randperm", p) for p in perms]))
+    np.testing.assert_array_equal(idx.cpu().numpy(), ref)
+    # device-drawn subset: reps are always kept (pad branch) and the rest comes from the pool
+    _, idx2 = H.voxel_downsample(dev(pts), T, seed=1234)
+    idx2 = idx2.cpu().numpy()
+    for b in range(B):
+        reps, _, _ = O.voxel_reps(pts[b], T)
+        if len(reps) < T:
+            np.testing.assert_array_equal(idx2[b][:len(reps)], reps)
+            extra = idx2[b][len(reps):]
+            assert len(np.unique(extra)) == len(extra)
+            assert not np.isin(extra, reps).any()
+        else:
+            assert np.isin(idx2[b], reps).all()
+
+
+def test_knn_golden(H, golden):
+    g = golden("hierarchical.npz")
+    out = H.knn3_interp(dev(g["knn_coarse"]), dev(g["knn_orig"]), dev(g["knn_idx"]), check=True)
+    np.testing.assert_array_equal(out.cpu().numpy(), g["knn_out"])
+
+
+def test_knn_golden_120k(H, golden):
+    from pointcloud_style_transfer_amd.synthetic import lidar_like_cloud, standard_normal
+
+    g = golden("hierarchical.npz")
+    pts = lidar_like_cloud(int(g["full_seed"]), 120000)[None]
+    idx = g["full_idx"].astype(np.int64)
+    coarse = standard_normal(int(g["knn_full_coarse_seed"]), (1, 120000, 3))[:, idx[0]]
+    out = H.knn3_interp(dev(coarse), dev(pts), dev(idx), check=True)
+    np.testing.assert_array_equal(out.cpu().numpy(), g["knn_full_out"])
+
+
+@pytest.mark.parametrize("N,M,B,sig", [(3000, 700, 2, (1, 1, 1)), (40000, 10000, 2, (3, 1, 0.01)),
+                                        (500, 2, 1, (1, 1, 1)), (1000, 1, 1, (1, 1, 1))])
+def test_knn_vs_oracle(H, N, M, B, sig):
+    rng = np.random.default_rng(M)
+    orig = (rng.standard_normal((B, N, 3)) * np.array(sig)).astype(np.float32)
+    idx = np.stack([rng.choice(N, M, replace=False) for _ in range(B)])
+    field = rng.standard_normal((B, N, 3)).astype(np.float32)
+    coarse = np.stack([field[b][idx[b]] for b in range(B)])
+    out = H.knn3_interp(dev(coarse), dev(orig), dev(idx), check=True).cpu().numpy()
+    np.testing.assert_array_equal(out, O.upsample_knn(coarse, orig, idx))
+
+
+def _noise_params(det_state, H, precision):
+    from pointcloud_style_transfer_amd import packing
+
+    blob = torch.from_numpy(packing.pack_blob(det_state, precision)).cuda()
+    assert blob.numel() == H.noise_mlp_blob_bytes(precision)
+    bias = dev(packing.pack_bias(det_state))
+    g = lambda n: dev(det_state[f"noise_predictor.{n}"])  # noqa: E731
+    freqs = packing.time_freqs(128).cuda()
+    return blob, bias, (freqs, g("time_proj.weight"), g("time_proj.bias"), g("style_proj.weight"),
+                        g("style_proj.bias"), g("point_encoder.4.bias"))
+
+
+@pytest.mark.parametrize("precision", [0, 1])
+def test_noise_mlp_golden(H, golden, det_state, precision):
+    g = golden("noise_predictor.npz")
+    blob, bias, cp = _noise_params(det_state, H, precision)
+    pts = g["points"]  # [2, 4096, 3]
+    for t in g["ts"]:
+        cond = H.noise_cond(dev(g[f"t{t}_tvec"]), dev(g["style"]), *cp)
+        out = H.noise_mlp(dev(pts.reshape(-1, 3)), 4096, cond, blob, bias, precision)
+        out = out.cpu().numpy().reshape(2, 4096, 3)
+        ref = g[f"t{t}_out"]
+        if precision == 0:
+            assert_close(out, ref)
+        else:
+            err = np.linalg.norm(out - ref) / np.linalg.norm(ref)
+            assert err < BF16_NORM_RTOL, err
+
+
+@pytest.mark.parametrize("P,T", [(1, 1), (33, 33), (1000, 300), (60000, 30000)])
+def test_noise_mlp_shapes_vs_oracle(H, det_state, P, T):
+    blob, bias, cp = _noise_params(det_state, H, 0)
+    rng = np.random.default_rng(P)
+    C = (P + T - 1) // T
+    pts = rng.standard_normal((P, 3)).astype(np.float32)
+    t = rng.integers(0, 1000, C)
+    style = rng.standard_normal((C, 256)).astype(np.float32) * 0.3
+    cond = H.noise_cond(dev(t), dev(style), *cp)
+    out = H.noise_mlp(dev(pts), T, cond, blob, bias, 0).cpu().numpy()
+    pad = np.zeros((C * T, 3), np.float32)
+    pad[:P] = pts
+    ref = O.noise_predictor(det_state, pad.reshape(C, T, 3), t, style).reshape(-1, 3)[:P]
+    assert_close(out, ref)
+
+
+def test_cfg_ddim_step(H, golden):
+    g = golden("schedule_losses.npz")
+    ac = g["alphas_cumprod"]
+    rng = np.random.default_rng(5)
+    x, ec, eu, src = (rng.standard_normal((2, 5000, 3)).astype(np.float32) for _ in range(4))
+    for t, tp in [(999, 888), (10, 0), (0, -1)]:
+        a = np.float32(ac[t])
+        ap = np.float32(ac[tp]) if tp >= 0 else np.float32(1.0)
+        coeffs = (np.sqrt(np.float32(1) - a), np.sqrt(a) + np.float32(1e-8), np.sqrt(ap),
+                  np.sqrt(np.float32(1) - ap))
+        xc = torch.empty(4, 5000, 3, device="cuda")
+        out = H.cfg_ddim_step(dev(x), dev(ec), dev(eu), dev(src), 7.5, coeffs, x_cat=xc)
+        sched = O.Schedule()
+        sched.alphas_cumprod = ac
+        ref = O.guided_update(sched, x, ec, eu, src, t, tp, 7.5)
+        assert_close(out.cpu().numpy(), ref, rtol=1e-5)
+        np.testing.assert_array_equal(xc.cpu().numpy(), np.concatenate([out.cpu().numpy()] * 2))
