@@ -1,0 +1,246 @@
+"""Benchmark: denoising steps/s of the guided (CFG) sampling loop on 120000-point clouds
+(BASELINE.json metric, config 2: 120k sim->real cloud, full 1000-step schedule, bf16 noise
+MLP, fp32 geometry), one process per GPU.
+
+A "step" = one iteration of DiffusionProcess.guided_sample_loop (diffusion_model.py:238-260):
+voxel downsample of the CFG batch (2 x 120000 -> 2 x 30000), fused noise MLP on 60000 points,
+kNN-3 upsample back to 2 x 120000, CFG + DDIM update.  Each rank denoises its own cloud(s)
+(independent objects: no data-path collective; scaling "weak").  The one-time style encode is
+timed separately and excluded.
+
+Prints ONE JSON line on rank 0 (driver contract), including `roofline` for the dominant
+kernel (pcst noise MLP, MFMA-bound) measured with HIP events around its launches inside the
+timed region, and `cpu_baseline` (the oracle, a port of the reference path, on host cores).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+FLOP_PER_POINT = 3_540_480          # NoisePredictor MACs x 2
+MFMA_BF16_PEAK_TFLOPS = 2500.0      # MI355X dense bf16 (MI355X_MICROARCH.md)
+MFMA_F32_PEAK_TFLOPS = 157.3
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--clouds-per-gpu", type=int, default=1)
+    ap.add_argument("--points", type=int, default=120000)
+    ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--cpu-steps", type=int, default=3)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "noise_mlp_traffic.json"))
+    return ap.parse_args()
+
+
+def setup_dist(args):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch.distributed as dist
+
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+    else:
+        torch.cuda.set_device(0)
+    return world, rank, local
+
+
+def build_model(precision, device):
+    from pointcloud_style_transfer_amd.config.config import Config
+    from pointcloud_style_transfer_amd.models.diffusion_model import (DiffusionProcess,
+                                                                        PointCloudDiffusionModel)
+
+    cfg = Config(precision=precision, make_dirs=False)
+    torch.manual_seed(0)  # random-init weights of the reference architecture
+    model = PointCloudDiffusionModel(cfg).to(device).eval()
+    return cfg, model, DiffusionProcess(cfg, device=str(device))
+
+
+def cpu_baseline(args, cfg, model, src, cond, xT):
+    """The oracle (numpy + C port of the reference path) on host cores: per-step cost of the
+    same guided step on the same 120k clouds, (t(1+k) - t(1)) / k."""
+    from oracle import oracle as O
+
+    threads = int(os.environ.get("OMP_NUM_THREADS", str(min(os.cpu_count() or 1, 16))))
+    sd = {k: v.detach().float().cpu().numpy() for k, v in model.state_dict().items()}
+    sched = O.Schedule()
+    ts = O.timesteps_for(1000, 1000)
+    rng = np.random.default_rng(6000)
+
+    class RandReplay:  # fresh permutations for every downsample (the oracle never draws itself)
+        def next(self, kind):
+            raise RuntimeError
+
+    B = 1
+    x = xT[:1].copy()
+    style = np.zeros((1, 256), np.float32) + 0.1
+    style_in = np.concatenate([style, np.zeros_like(style)])
+
+    def step(i):
+        nonlocal x
+        t = ts[i]
+        x_in = np.concatenate([x, x])
+        outs, idxs = [], []
+        for b in range(2):
+            reps, _, _ = O.voxel_reps(x_in[b], cfg.global_points)
+            perm = rng.permutation(len(x_in[b]) - len(np.unique(reps))) if len(reps) < cfg.global_points \
+                else rng.permutation(len(reps))
+            p, ix = O.voxel_downsample(x_in[b:b + 1], cfg.global_points, O.Replay([("randperm", perm)]))
+            outs.append(p[0])
+            idxs.append(ix[0])
+        xc, xi = np.stack(outs), np.stack(idxs)
+        nc = O.noise_predictor(sd, xc, np.full(2, t), style_in)
+        eps = O.upsample_knn(nc, x_in, xi)
+        x = O.guided_update(sched, x, eps[:B], eps[B:], src[:1], t, ts[i + 1], 7.5)
+
+    t0 = time.perf_counter()
+    step(0)
+    t1 = time.perf_counter()
+    for i in range(1, 1 + args.cpu_steps):
+        step(i)
+    t2 = time.perf_counter()
+    per = (t2 - t1) / args.cpu_steps
+    return {"value": round(1.0 / per, 4), "unit": "denoising-steps/s", "cores": threads,
+            "kind": "port",
+            "sample": f"oracle guided step on 1 x {args.points}-pt cloud (CFG x2, 30k coarse), "
+                      f"{args.cpu_steps} steps after 1 untimed (first {t1 - t0:.1f}s), "
+                      f"{per:.2f} s/step; numpy/OpenBLAS fp32 MLP + C voxel/kNN"}
+
+
+def main():
+    args = parse()
+    world, rank, local = setup_dist(args)
+    device = torch.device("cuda", torch.cuda.current_device())
+    from pointcloud_style_transfer_amd import _hip
+    from pointcloud_style_transfer_amd.synthetic import lidar_like_cloud, standard_normal
+
+    cfg, model, dp = build_model(args.precision, device)
+    C = args.clouds_per_gpu
+    src_np = np.stack([lidar_like_cloud(1000 + rank * C + i, args.points) for i in range(C)])
+    cond_np = np.stack([lidar_like_cloud(2000 + rank * C + i, args.points) for i in range(C)])
+    xT_np = np.stack([standard_normal(3000 + rank * C + i, (args.points, 3)) for i in range(C)])
+    src = torch.from_numpy(src_np).to(device)
+    cond = torch.from_numpy(cond_np).to(device)
+    x = torch.from_numpy(xT_np).to(device)
+
+    hp = model.hierarchical_processor
+    npred = model.noise_predictor
+    with torch.no_grad():
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        style = model.style_encoder(hp.downsample(cond)[0])
+        torch.cuda.synchronize()
+        style_s = time.perf_counter() - t0
+        style_in = torch.cat([style, torch.zeros_like(style)])
+        npred.packed()
+        timesteps = torch.linspace(dp.num_timesteps - 1, 0, dp.num_timesteps).long().tolist()
+        x_cat = torch.cat([x, x]).contiguous()
+        ev = []
+
+        def step(i, timed):
+            nonlocal x
+            t = timesteps[i % len(timesteps)]
+            t_prev = timesteps[i % len(timesteps) + 1] if t > 0 else -1
+            t_in = torch.full((2 * C,), t, device=device, dtype=torch.long)
+            xc, xi = hp.downsample(x_cat)
+            if timed:
+                e0 = torch.cuda.Event(enable_timing=True)
+                e1 = torch.cuda.Event(enable_timing=True)
+                blob, bias, _ = npred.packed()
+                cnd = npred.cond(t_in, style_in)
+                e0.record()
+                nc = _hip.noise_mlp(xc.reshape(-1, 3), cfg.global_points, cnd, blob, bias,
+                                    npred.precision_code).view(2 * C, -1, 3)
+                e1.record()
+                ev.append((e0, e1))
+            else:
+                nc = npred(xc, t_in, style_in)
+            eps = hp.upsample_knn(nc, x_cat, xi)
+            x = _hip.cfg_ddim_step(x, eps[:C], eps[C:], src, 7.5, dp._coeffs(t, t_prev),
+                                   x_cat=x_cat)
+
+        for i in range(args.warmup):
+            step(i, False)
+        if world > 1:
+            import torch.distributed as dist
+
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i in range(args.steps):
+            step(args.warmup + i, True)
+        torch.cuda.synchronize()
+        elapsed = time.perf_counter() - t0
+        if world > 1:
+            dist.barrier()
+            tt = torch.tensor([elapsed], device=device, dtype=torch.float64)
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            elapsed = float(tt.item())
+
+    mlp_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    flop = FLOP_PER_POINT * 2 * C * cfg.global_points
+    peak = MFMA_BF16_PEAK_TFLOPS if args.precision == "bf16" else MFMA_F32_PEAK_TFLOPS
+    achieved = flop / (mlp_ms * 1e-3) / 1e12
+    traffic = None
+    if os.path.exists(args.traffic_json):
+        try:
+            with open(args.traffic_json) as f:
+                traffic = json.load(f).get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+    total_steps = world * C * args.steps
+    value = total_steps / elapsed
+    if rank == 0:
+        base = None
+        if not args.no_cpu_baseline:
+            torch.cuda.synchronize()
+            base = cpu_baseline(args, cfg, model, src_np, cond_np, xT_np)
+        line = {
+            "metric": "denoising-steps/sec on 120k-pt cloud",
+            "value": round(value, 3),
+            "unit": "denoising-steps/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": args.precision,
+            "data": "synthetic (numpy PCG64 anisotropic Gaussian clouds, random-init weights)",
+            "config": {"workload": "guided_sample_loop step, 120000-pt sim->real cloud, CFG x2, "
+                                   "30000 coarse, full 1000-step schedule (BASELINE configs[1])",
+                       "points": args.points, "coarse_points": cfg.global_points,
+                       "clouds_per_gpu": C, "guidance_scale": 7.5,
+                       "parallelism": f"independent clouds x{world}",
+                       "style_encode_s": round(style_s, 4)},
+            "roofline": {"kernel": "pcst noise_mlp", "bound": "mfma",
+                         "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
+                         "frac": round(achieved / peak, 4), "traffic": traffic,
+                         "algorithmic": f"{FLOP_PER_POINT} FLOP/pt x {2 * C * cfg.global_points} pts",
+                         "avg_launch_ms": round(mlp_ms, 4)},
+            "cpu_baseline": base,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -66,6 +66,102 @@ int pcst_group_gather(const float* xyz, const float* feats, int64_t B, int64_t N
                       const int64_t* fps_idx, const int64_t* group_idx, int64_t S, int64_t ns,
                       float* new_xyz, float* grouped, void* stream);
 
+/* FPS for clouds larger than 30720 points: running distances in a caller workspace of
+ * pcst_fps_workspace_size() bytes (0 when the register-resident kernel applies). */
+int pcst_fps_workspace_size(int64_t B, int64_t N, size_t* bytes);
+int pcst_fps_ws(const float* xyz, int64_t B, int64_t N, int64_t npoint, const int64_t* start_idx,
+                int64_t* out_idx, void* workspace, void* stream);
+
+/* SetAbstraction.apply_mlp layer (pointnet2_encoder.py:106-112) and other per-point linear
+ * layers: Y[m,o] = act(scale[o]*(X[m,:].W[o,:]) + shift[o]) on exact-f32 MFMA, X [M,K],
+ * W [O,K] (Conv2d 1x1 weight), scale/shift may be NULL (1/0).  pool_ns > 0: Y[g,o] = max over
+ * rows g*ns..g*ns+ns-1 (torch.max(points, 3)); requires relu. */
+int pcst_pointwise_linear(const float* X, int64_t M, int64_t K, const float* W, int64_t O,
+                          const float* scale, const float* shift, int relu, int64_t pool_ns,
+                          float* Y, void* stream);
+/* Train-mode BatchNorm statistics of Z [M,O]: mean and biased variance per channel (float64),
+ * deterministic.  workspace: pcst_channel_stats_workspace_size() bytes. */
+int pcst_channel_stats_workspace_size(int64_t O, size_t* bytes);
+int pcst_channel_stats(const float* Z, int64_t M, int64_t O, double* mean, double* var,
+                       void* workspace, void* stream);
+/* Y = act(scale*Z + shift) per channel, optional max-pool over groups of pool_ns rows. */
+int pcst_affine_act(const float* Z, int64_t M, int64_t O, const float* scale, const float* shift,
+                    int relu, int64_t pool_ns, float* Y, void* stream);
+
+/* ---- models/diffusion_model.py --------------------------------------------------------- */
+
+/* HierarchicalProcessor._voxel_grid_downsample_torch (diffusion_model.py:69-122) for all B
+ * clouds (N > target) on the device.  Split into stats (unique voxels U, pool size P; written
+ * to counts_out[0..B) and [B..2B) if non-NULL) and select.  select with perm == NULL draws the
+ * random subset on the device from `seed` (random keys + sort, torch.randperm's construction);
+ * with perm != NULL it replays per-cloud permutations (perm + perm_off[b], length perm_len[b]
+ * must be U when U > target, P when U < target, 0 when U == target).
+ * Outputs: out_idx [B,target] int64, out_pts [B,target,3]. */
+int pcst_voxel_workspace_size(int64_t B, int64_t N, size_t* bytes);
+int pcst_voxel_stats(const float* pts, int64_t B, int64_t N, int64_t target, void* workspace,
+                     int32_t* counts_out, void* stream);
+int pcst_voxel_select(const float* pts, int64_t B, int64_t N, int64_t target, void* workspace,
+                      const int64_t* perm, const int64_t* perm_off, const int64_t* perm_len,
+                      uint64_t seed, int64_t* out_idx, float* out_pts, void* stream);
+int pcst_voxel_downsample(const float* pts, int64_t B, int64_t N, int64_t target, void* workspace,
+                          uint64_t seed, int64_t* out_idx, float* out_pts, void* stream);
+/* Copies the replay-validation error word (0 = ok) to err_out (device int32). */
+int pcst_voxel_error(void* workspace, int64_t B, int64_t N, int32_t* err_out, void* stream);
+
+/* HierarchicalProcessor.upsample_knn (diffusion_model.py:127-153): coarse [B,M,3] values at
+ * orig[idx] ([B,M] int64), orig [B,N,3] -> out [B,N,3]; exact float64 3-NN IDW (bit-exact vs
+ * the reference's sklearn KD-tree path). */
+int pcst_knn_workspace_size(int64_t B, int64_t N, int64_t M, size_t* bytes);
+int pcst_knn3_interp(const float* coarse, const float* orig, const int64_t* idx, int64_t B,
+                     int64_t N, int64_t M, float* out, void* workspace, void* stream);
+int pcst_knn_error(void* workspace, int64_t B, int64_t N, int64_t M, int32_t* err_out,
+                   void* stream);
+
+/* NoisePredictor.forward (diffusion_model.py:38-61), fused.  precision: 0 = exact f32 MFMA
+ * (parity), 1 = bf16 MFMA with fp32 accumulation and fp32 residual stream.  blob/bias are the
+ * packed weights of packing.py (blob 16-byte aligned, pcst_noise_mlp_blob_bytes() bytes).
+ * pcst_noise_cond computes cond[c] = b4 + time_proj(TimeEmbedding(t_c)) + style_proj(style_c)
+ * (freqs = the reference's 64-entry exp table).  pts [P,3] cloud-major with
+ * points_per_cloud points per cloud; out [P,3]. */
+int64_t pcst_noise_mlp_blob_bytes(int precision);
+int pcst_noise_cond(const int64_t* t, const float* style, int64_t nclouds, const float* freqs,
+                    const float* wt, const float* bt, const float* ws, const float* bs,
+                    const float* b4, float* cond, void* stream);
+int pcst_noise_mlp(const float* pts, int64_t P, int64_t points_per_cloud, const float* cond,
+                   int64_t nclouds, const void* blob, int64_t blob_bytes, const float* bias,
+                   int precision, float* out, void* stream);
+
+/* CFG + DDIM update of guided_sample_loop (diffusion_model.py:248-260); eps_u == NULL gives
+ * ddim_sample_loop's update (:283-290), source == NULL skips the source pull.  x_cat (optional,
+ * [2,n]) receives the new x twice: the next step's CFG batch. */
+int pcst_cfg_ddim_step(const float* x, const float* eps_c, const float* eps_u, const float* source,
+                       int64_t n, float guidance_scale, float sqrt_1m_at, float sqrt_at_eps,
+                       float sqrt_aprev, float sqrt_1m_aprev, float* x_out, float* x_cat,
+                       void* stream);
+
+/* ---- models/losses.py ------------------------------------------------------------------ */
+
+/* chamfer_distance_chunked_optimized (losses.py:8-63), never materialising N x M:
+ * min1/arg1 [B,N] = row minima pred->target of clamp((|p|^2+|q|^2) + (-2 p.q), 0) (first index
+ * on ties), min2/arg2 [B,M] target->pred, out [B] = mean(min1) + mean(min2) (may be NULL). */
+int pcst_chamfer_fwd(const float* pred, const float* target, int64_t B, int64_t N, int64_t M,
+                     float* min1, int32_t* arg1, float* min2, int32_t* arg2, float* out,
+                     void* stream);
+/* Gradient of sum_b grad_out[b]*chamfer[b]; ACCUMULATES into grad_pred [B,N,3] and/or
+ * grad_target [B,M,3] (either may be NULL).  Deterministic (sorted scatter, no float atomics). */
+int pcst_chamfer_bwd_workspace_size(int64_t B, int64_t N, int64_t M, size_t* bytes);
+int pcst_chamfer_bwd(const float* pred, const float* target, int64_t B, int64_t N, int64_t M,
+                     const int32_t* arg1, const int32_t* arg2, const float* grad_out,
+                     float* grad_pred, float* grad_target, void* workspace, void* stream);
+
+/* F.l1_loss mean reduction (losses.py:90): out[0] = mean|a-b| (fixed-order float64 sum);
+ * backward grad_a = sign(a-b) * grad_out[0] / n. */
+int pcst_l1_workspace_size(size_t* bytes);
+int pcst_l1_fwd(const float* a, const float* b, int64_t n, float* out, void* workspace,
+                void* stream);
+int pcst_l1_bwd(const float* a, const float* b, int64_t n, const float* grad_out, float* grad_a,
+                void* stream);
+
 #ifdef __cplusplus
 }
 #endif

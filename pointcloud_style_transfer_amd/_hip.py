@@ -45,6 +45,16 @@ SIGNATURES = {
     "pcst_noise_cond": [_P, _P, _I, _P, _P, _P, _P, _P, _P, _P, _P],
     "pcst_noise_mlp": [_P, _I, _I, _P, _I, _P, _I, _P, ctypes.c_int, _P, _P],
     "pcst_cfg_ddim_step": [_P, _P, _P, _P, _I, _F, _F, _F, _F, _F, _P, _P, _P],
+    "pcst_pointwise_linear": [_P, _I, _I, _P, _I, _P, _P, ctypes.c_int, _I, _P, _P],
+    "pcst_channel_stats_workspace_size": [_I, _SZ],
+    "pcst_channel_stats": [_P, _I, _I, _P, _P, _P, _P],
+    "pcst_affine_act": [_P, _I, _I, _P, _P, ctypes.c_int, _I, _P, _P],
+    "pcst_chamfer_fwd": [_P, _P, _I, _I, _I, _P, _P, _P, _P, _P, _P],
+    "pcst_chamfer_bwd_workspace_size": [_I, _I, _I, _SZ],
+    "pcst_chamfer_bwd": [_P, _P, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P],
+    "pcst_l1_workspace_size": [_SZ],
+    "pcst_l1_fwd": [_P, _P, _I, _P, _P, _P],
+    "pcst_l1_bwd": [_P, _P, _I, _P, _P, _P],
 }
 _RESTYPES = {"pcst_version": ctypes.c_char_p, "pcst_last_error": ctypes.c_char_p,
              "pcst_noise_mlp_blob_bytes": ctypes.c_int64}
@@ -289,3 +299,90 @@ def cfg_ddim_step(x, eps_c, eps_u, source, guidance_scale, coeffs, x_cat=None, o
     _call("pcst_cfg_ddim_step", _ptr(x), _ptr(eps_c), _ptr(eps_u), _ptr(source), x.numel(),
           float(guidance_scale), c1, c2, c3, c4, _ptr(out), _ptr(x_cat), _stream())
     return out
+
+
+# ----------------------------------------------------------------------------- per-point linear
+def pointwise_linear(X, W, scale=None, shift=None, relu=False, pool_ns=0):
+    """X [M,K], W [O,K] -> act(scale*(X W^T)+shift) [M,O], or max-pooled [M/ns, O]."""
+    require_device(X, W, scale, shift)
+    X, W = _f32(X), _f32(W)
+    M, K = X.shape
+    O = W.shape[0]
+    rows = M // pool_ns if pool_ns else M
+    Y = torch.empty(rows, O, dtype=torch.float32, device=X.device)
+    _call("pcst_pointwise_linear", _ptr(X), M, K, _ptr(W), O,
+          _ptr(None if scale is None else _f32(scale)), _ptr(None if shift is None else _f32(shift)),
+          int(relu), pool_ns, _ptr(Y), _stream())
+    return Y
+
+
+def channel_stats(Z):
+    """Per-channel (mean, biased var) of Z [M,O] as float64 device tensors (deterministic)."""
+    require_device(Z)
+    Z = _f32(Z)
+    M, O = Z.shape
+    ws = _workspace("pcst_channel_stats_workspace_size", O, device=Z.device)
+    mean = torch.empty(O, dtype=torch.float64, device=Z.device)
+    var = torch.empty(O, dtype=torch.float64, device=Z.device)
+    _call("pcst_channel_stats", _ptr(Z), M, O, _ptr(mean), _ptr(var), _ptr(ws), _stream())
+    return mean, var
+
+
+def affine_act(Z, scale, shift, relu=True, pool_ns=0):
+    require_device(Z, scale, shift)
+    Z = _f32(Z)
+    M, O = Z.shape
+    rows = M // pool_ns if pool_ns else M
+    Y = torch.empty(rows, O, dtype=torch.float32, device=Z.device)
+    _call("pcst_affine_act", _ptr(Z), M, O, _ptr(_f32(scale)), _ptr(_f32(shift)), int(relu),
+          pool_ns, _ptr(Y), _stream())
+    return Y
+
+
+# ----------------------------------------------------------------------------- losses
+def chamfer_fwd(pred, target):
+    """-> (chamfer [B], arg1 [B,N] int32, arg2 [B,M] int32)."""
+    require_device(pred, target)
+    pred, target = _f32(pred), _f32(target)
+    B, N, _ = pred.shape
+    M = target.shape[1]
+    dev = pred.device
+    min1 = torch.empty(B, N, dtype=torch.float32, device=dev)
+    min2 = torch.empty(B, M, dtype=torch.float32, device=dev)
+    arg1 = torch.empty(B, N, dtype=torch.int32, device=dev)
+    arg2 = torch.empty(B, M, dtype=torch.int32, device=dev)
+    out = torch.empty(B, dtype=torch.float32, device=dev)
+    _call("pcst_chamfer_fwd", _ptr(pred), _ptr(target), B, N, M, _ptr(min1), _ptr(arg1),
+          _ptr(min2), _ptr(arg2), _ptr(out), _stream())
+    return out, arg1, arg2
+
+
+def chamfer_bwd(pred, target, arg1, arg2, grad_out, need_pred=True, need_target=False):
+    require_device(pred, target, arg1, arg2, grad_out)
+    pred, target, grad_out = _f32(pred), _f32(target), _f32(grad_out)
+    B, N, _ = pred.shape
+    M = target.shape[1]
+    ws = _workspace("pcst_chamfer_bwd_workspace_size", B, N, M, device=pred.device)
+    gp = torch.zeros_like(pred) if need_pred else None
+    gt = torch.zeros_like(target) if need_target else None
+    _call("pcst_chamfer_bwd", _ptr(pred), _ptr(target), B, N, M, _ptr(arg1.contiguous()),
+          _ptr(arg2.contiguous()), _ptr(grad_out), _ptr(gp), _ptr(gt), _ptr(ws), _stream())
+    return gp, gt
+
+
+def l1_fwd(a, b):
+    require_device(a, b)
+    a, b = _f32(a), _f32(b)
+    ws = _workspace("pcst_l1_workspace_size", device=a.device)
+    out = torch.empty((), dtype=torch.float32, device=a.device)
+    _call("pcst_l1_fwd", _ptr(a), _ptr(b), a.numel(), _ptr(out), _ptr(ws), _stream())
+    return out
+
+
+def l1_bwd(a, b, grad_out):
+    require_device(a, b, grad_out)
+    a, b = _f32(a), _f32(b)
+    ga = torch.empty_like(a)
+    _call("pcst_l1_bwd", _ptr(a), _ptr(b), a.numel(), _ptr(_f32(grad_out.reshape(1))), _ptr(ga),
+          _stream())
+    return ga

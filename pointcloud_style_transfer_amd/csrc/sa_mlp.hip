@@ -1,0 +1,195 @@
+// SetAbstraction grouped MLP + max-pool (models/pointnet2_encoder.py:106-112) and the other
+// small per-point linear layers of the style encoder, on exact-f32 MFMA
+// (v_mfma_f32_32x32x2_f32: a k-ordered fmaf chain, so results match an fp32 reference to
+// summation order only).
+//
+//   Y[m, o] = act(scale[o] * (X[m, :] . W[o, :]) + shift[o])      (Conv2d 1x1 + BN + ReLU)
+//   pooled: Y[g, o] = max over rows m in group g (g = m / ns)      (torch.max(points, 3))
+//
+// Eval-mode BN is folded into (scale, shift) by the host.  Train-mode BN needs batch
+// statistics of the pre-BN activations: linear pass with (1, bias), channel_stats (deterministic
+// two-level float64 reduction), then affine_act (+pool).
+//
+// Tile: 64 rows x 64 channels per 256-thread workgroup (2x2 waves of 32x32), K staged through
+// LDS in 32-deep slices (rows padded to 33 floats: conflict-free column reads).
+// Max-pool after ReLU: every candidate is >= 0, so the max is an order-independent
+// atomicMax on the float bits into a zero-initialised output.
+#include "common.h"
+
+namespace pcst {
+
+typedef __attribute__((ext_vector_type(16))) float f32x16;
+constexpr int kBM = 64, kBN = 64, kBK = 32, kLd = kBK + 1;
+
+__device__ __forceinline__ int crow(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
+
+template <bool POOL>
+__global__ __launch_bounds__(256) void pw_linear_kernel(const float* __restrict__ X, int64_t M,
+                                                        int K, const float* __restrict__ W, int O,
+                                                        const float* __restrict__ scale,
+                                                        const float* __restrict__ shift, int relu,
+                                                        int64_t ns, float* __restrict__ Y) {
+  __shared__ float As[kBM][kLd];
+  __shared__ float Bs[kBN][kLd];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wr = wid >> 1, wc = wid & 1, h = lane >> 5, l32 = lane & 31;
+  const int64_t m0 = (int64_t)blockIdx.x * kBM;
+  const int o0 = blockIdx.y * kBN;
+  f32x16 acc = f32x16{};
+  for (int k0 = 0; k0 < K; k0 += kBK) {
+    for (int e = tid; e < kBM * kBK; e += 256) {
+      const int r = e / kBK, k = e % kBK;
+      const int64_t m = m0 + r;
+      As[r][k] = (m < M && k0 + k < K) ? X[m * K + k0 + k] : 0.0f;
+      const int o = o0 + r;
+      Bs[r][k] = (o < O && k0 + k < K) ? W[(int64_t)o * K + k0 + k] : 0.0f;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int kk = 0; kk < kBK; kk += 2) {
+      const float a = As[wr * 32 + l32][kk + h];
+      const float b = Bs[wc * 32 + l32][kk + h];
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc, 0, 0, 0);
+    }
+    __syncthreads();
+  }
+  // C layout: column (channel) = lane & 31, row (point) = crow(r, h)
+  const int o = o0 + wc * 32 + l32;
+  const float sc = (o < O && scale) ? scale[o] : 1.0f;
+  const float sh = (o < O && shift) ? shift[o] : 0.0f;
+  const int64_t mb = m0 + wr * 32;
+  if (!POOL) {
+    if (o < O) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int64_t m = mb + crow(r, h);
+        float v = fmaf(acc[r], sc, sh);
+        if (relu) v = fmaxf(v, 0.0f);
+        if (m < M) Y[m * O + o] = v;
+      }
+    }
+    return;
+  }
+  // pooled (relu required): groups of ns consecutive rows
+  if (ns % 32 == 0) {
+    float mx = 0.0f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int64_t m = mb + crow(r, h);
+      const float v = fmaxf(fmaf(acc[r], sc, sh), 0.0f);
+      if (m < M) mx = fmaxf(mx, v);
+    }
+    mx = fmaxf(mx, __shfl_xor(mx, 32));
+    if (h == 0 && o < O && mb < M)
+      atomicMax(reinterpret_cast<unsigned int*>(&Y[(mb / ns) * O + o]), __float_as_uint(mx));
+  } else if (o < O) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int64_t m = mb + crow(r, h);
+      const float v = fmaxf(fmaf(acc[r], sc, sh), 0.0f);
+      if (m < M) atomicMax(reinterpret_cast<unsigned int*>(&Y[(m / ns) * O + o]), __float_as_uint(v));
+    }
+  }
+}
+
+// Deterministic per-channel statistics of Z [M, O]: partial float64 sums over row chunks,
+// then an in-order combine.  mean[o], var[o] (biased, as BatchNorm normalises with).
+constexpr int kStatChunks = 64;
+
+__global__ void channel_partial_kernel(const float* __restrict__ Z, int64_t M, int O,
+                                       const double* __restrict__ mean, double* __restrict__ part) {
+  const int o = blockIdx.x * 256 + threadIdx.x;
+  const int chunk = blockIdx.y;
+  if (o >= O) return;
+  const int64_t per = (M + kStatChunks - 1) / kStatChunks;
+  const int64_t a = chunk * per, e = a + per < M ? a + per : M;
+  double s = 0.0;
+  const double mu = mean ? mean[o] : 0.0;
+  for (int64_t m = a; m < e; ++m) {
+    const double v = (double)Z[m * O + o] - mu;
+    s += mean ? v * v : v;
+  }
+  part[(int64_t)chunk * O + o] = s;
+}
+
+__global__ void channel_combine_kernel(const double* __restrict__ part, int64_t M, int O,
+                                       double* __restrict__ out) {
+  const int o = blockIdx.x * 256 + threadIdx.x;
+  if (o >= O) return;
+  double s = 0.0;
+  for (int c = 0; c < kStatChunks; ++c) s += part[(int64_t)c * O + o];
+  out[o] = s / (double)M;
+}
+
+__global__ void affine_act_kernel(const float* __restrict__ Z, int64_t M, int O,
+                                  const float* __restrict__ scale, const float* __restrict__ shift,
+                                  int relu, int64_t ns, float* __restrict__ Y) {
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < M * O;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int o = (int)(e % O);
+    const int64_t m = e / O;
+    float v = fmaf(Z[e], scale[o], shift[o]);
+    if (relu) v = fmaxf(v, 0.0f);
+    if (ns > 0) atomicMax(reinterpret_cast<unsigned int*>(&Y[(m / ns) * O + o]), __float_as_uint(v));
+    else Y[e] = v;
+  }
+}
+
+}  // namespace pcst
+
+using namespace pcst;
+
+extern "C" int pcst_pointwise_linear(const float* X, int64_t M, int64_t K, const float* W,
+                                     int64_t O, const float* scale, const float* shift, int relu,
+                                     int64_t pool_ns, float* Y, void* stream) {
+  PCST_CHECK_ARG(M >= 0 && K > 0 && O > 0 && K < (1 << 20) && O < (1 << 20), "pointwise_linear: bad shape");
+  PCST_CHECK_ARG(pool_ns == 0 || (relu && M % pool_ns == 0),
+                 "pointwise_linear: pooling needs relu and M %% ns == 0");
+  if (M == 0) return PCST_OK;
+  PCST_CHECK_ARG(X && W && Y, "pointwise_linear: null pointer");
+  hipStream_t s = as_stream(stream);
+  if (pool_ns > 0) PCST_HIP(hipMemsetAsync(Y, 0, sizeof(float) * (M / pool_ns) * O, s), "memset");
+  dim3 grid((unsigned)cdiv(M, kBM), (unsigned)cdiv(O, kBN));
+  if (pool_ns > 0)
+    hipLaunchKernelGGL(pw_linear_kernel<true>, grid, dim3(256), 0, s, X, M, (int)K, W, (int)O,
+                       scale, shift, relu, pool_ns, Y);
+  else
+    hipLaunchKernelGGL(pw_linear_kernel<false>, grid, dim3(256), 0, s, X, M, (int)K, W, (int)O,
+                       scale, shift, relu, (int64_t)0, Y);
+  PCST_LAUNCH_CHECK("pointwise_linear");
+  return PCST_OK;
+}
+
+extern "C" int pcst_channel_stats_workspace_size(int64_t O, size_t* bytes) {
+  *bytes = sizeof(double) * (size_t)(kStatChunks * O);
+  return PCST_OK;
+}
+
+extern "C" int pcst_channel_stats(const float* Z, int64_t M, int64_t O, double* mean, double* var,
+                                  void* workspace, void* stream) {
+  PCST_CHECK_ARG(M > 0 && O > 0, "channel_stats: bad shape");
+  hipStream_t s = as_stream(stream);
+  double* part = static_cast<double*>(workspace);
+  dim3 g((unsigned)cdiv(O, 256), kStatChunks);
+  hipLaunchKernelGGL(channel_partial_kernel, g, dim3(256), 0, s, Z, M, (int)O, (const double*)nullptr, part);
+  hipLaunchKernelGGL(channel_combine_kernel, dim3((unsigned)cdiv(O, 256)), dim3(256), 0, s, part, M, (int)O, mean);
+  hipLaunchKernelGGL(channel_partial_kernel, g, dim3(256), 0, s, Z, M, (int)O, (const double*)mean, part);
+  hipLaunchKernelGGL(channel_combine_kernel, dim3((unsigned)cdiv(O, 256)), dim3(256), 0, s, part, M, (int)O, var);
+  PCST_LAUNCH_CHECK("channel_stats");
+  return PCST_OK;
+}
+
+extern "C" int pcst_affine_act(const float* Z, int64_t M, int64_t O, const float* scale,
+                               const float* shift, int relu, int64_t pool_ns, float* Y,
+                               void* stream) {
+  PCST_CHECK_ARG(M >= 0 && O > 0, "affine_act: bad shape");
+  PCST_CHECK_ARG(pool_ns == 0 || (relu && M % pool_ns == 0), "affine_act: pooling needs relu");
+  if (M == 0) return PCST_OK;
+  hipStream_t s = as_stream(stream);
+  if (pool_ns > 0) PCST_HIP(hipMemsetAsync(Y, 0, sizeof(float) * (M / pool_ns) * O, s), "memset");
+  const int64_t g = std::min<int64_t>(cdiv(M * O, 256), 8192);
+  hipLaunchKernelGGL(affine_act_kernel, dim3((unsigned)g), dim3(256), 0, s, Z, M, (int)O, scale,
+                     shift, relu, pool_ns, Y);
+  PCST_LAUNCH_CHECK("affine_act");
+  return PCST_OK;
+}

@@ -1,0 +1,181 @@
+"""The drop-in modules (models.pointnet2_encoder / diffusion_model / losses) on the GPU vs the
+reference's golden vectors, with the reference's random draws replayed."""
+import numpy as np
+import pytest
+import torch
+
+from conftest import assert_close, assert_mostly_close
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def mods():
+    from pointcloud_style_transfer_amd import rng
+    from pointcloud_style_transfer_amd.config.config import Config
+    from pointcloud_style_transfer_amd.models import diffusion_model as dm
+    from pointcloud_style_transfer_amd.models import losses
+    from pointcloud_style_transfer_amd.models import pointnet2_encoder as pn
+
+    assert torch.cuda.is_available()
+    return dict(rng=rng, Config=Config, dm=dm, pn=pn, losses=losses)
+
+
+def make_model(mods, **cfg):
+    from detweights import load_into
+
+    c = mods["Config"](make_dirs=False, precision="fp32", **cfg)
+    m = mods["dm"].PointCloudDiffusionModel(c)
+    load_into(m)
+    return c, m.cuda()
+
+
+def dev(a):
+    return torch.from_numpy(np.ascontiguousarray(a)).cuda()
+
+
+@pytest.mark.parametrize("mode", ["eval", "train"])
+def test_set_abstraction_modules(mods, golden, mode):
+    g = golden("encoder.npz")
+    _, m = make_model(mods)
+    m.train(mode == "train")
+    enc = m.style_encoder.encoder
+    rp = mods["rng"].ReplayRNG.from_npz(g, f"{mode}_rng")
+    with torch.no_grad(), mods["rng"].replay(rp):
+        l1x, l1p = enc.sa1(dev(g["xyz"]), None)
+        np.testing.assert_array_equal(l1x.cpu().numpy(), g[f"{mode}_l1_xyz"])
+        assert_close(l1p.cpu().numpy(), g[f"{mode}_l1_points"])
+        l2x, l2p = enc.sa2(dev(g[f"{mode}_l1_xyz"]), dev(g[f"{mode}_l1_points"]).permute(0, 2, 1))
+        np.testing.assert_array_equal(l2x.cpu().numpy(), g[f"{mode}_l2_xyz"])
+        assert_close(l2p.cpu().numpy(), g[f"{mode}_l2_points"])
+        _, l3 = enc.sa3(dev(g[f"{mode}_l2_xyz"]), dev(g[f"{mode}_l2_points"]).permute(0, 2, 1))
+        assert_close(l3.cpu().numpy(), g[f"{mode}_l3"])
+    assert rp.exhausted
+
+
+def test_style_encoder_module(mods, golden):
+    from pointcloud_style_transfer_amd.synthetic import lidar_like_cloud
+
+    g = golden("encoder.npz")
+    _, m = make_model(mods)
+    m.eval()
+    with torch.no_grad(), mods["rng"].replay(mods["rng"].ReplayRNG.from_npz(g, "style_rng")):
+        assert_close(m.style_encoder(dev(g["xyz"])).cpu().numpy(), g["style"])
+    with torch.no_grad(), mods["rng"].replay(mods["rng"].ReplayRNG.from_npz(g, "style30_rng")):
+        out = m.style_encoder(dev(lidar_like_cloud(43, 30000)[None])).cpu().numpy()
+    assert_close(out, g["style30"])
+
+
+def test_noise_predictor_module(mods, golden):
+    g = golden("noise_predictor.npz")
+    _, m = make_model(mods)
+    m.eval()
+    with torch.no_grad():
+        for t in g["ts"]:
+            out = m.noise_predictor(dev(g["points"]), dev(g[f"t{t}_tvec"]), dev(g["style"]))
+            assert_close(out.cpu().numpy(), g[f"t{t}_out"])
+
+
+def test_guided_loop_direct_cfg1(mods, golden):
+    g = golden("sampling.npz")
+    c, m = make_model(mods)
+    m.eval()
+    dp = mods["dm"].DiffusionProcess(c, device="cuda")
+    rp = mods["rng"].ReplayRNG.from_npz(g, "a_rng")
+    with mods["rng"].replay(rp):
+        out = dp.guided_sample_loop(m, dev(g["a_src"]), dev(g["a_cond"]), 10, 7.5)
+    assert rp.exhausted
+    assert_mostly_close(out.cpu().numpy(), g["a_out"])
+
+
+def test_guided_loop_hierarchical(mods, golden):
+    g = golden("sampling.npz")
+    c, m = make_model(mods, total_points=4096, global_points=1024)
+    m.eval()
+    dp = mods["dm"].DiffusionProcess(c, device="cuda")
+    rp = mods["rng"].ReplayRNG.from_npz(g, "b_rng")
+    with mods["rng"].replay(rp):
+        out = dp.guided_sample_loop(m, dev(g["b_src"]), dev(g["b_cond"]), 3, 7.5)
+    assert rp.exhausted
+    assert_mostly_close(out.cpu().numpy(), g["b_out"], max_abs=5e-2)
+
+
+def test_guided_step_teacher_forced(mods, golden):
+    """Per-step parity: feed the reference's own x_in of every step; the downsample indices
+    must match bit-exactly and the step's noise/upsample within 1e-4."""
+    g = golden("sampling.npz")
+    c, m = make_model(mods, total_points=4096, global_points=1024)
+    m.eval()
+    names = list(g["b_rng_names"])
+    perms = [g[f"b_rng_{i}"] for i, n in enumerate(names) if n == "randperm"]
+    n = int(g["b_cap_down_idx_n"])
+    hp = m.hierarchical_processor
+    for i in range(1, n):  # 0 is the cond downsample
+        x_in = g[f"b_cap_down_in_{i}"]
+        ps = perms[1 + 2 * (i - 1): 1 + 2 * i]
+        with torch.no_grad(), mods["rng"].replay([("randperm", p) for p in ps]):
+            xc, xi = hp.downsample(dev(x_in))
+        np.testing.assert_array_equal(xi.cpu().numpy(), g[f"b_cap_down_idx_{i}"])
+        with torch.no_grad():
+            nc = m.noise_predictor(xc, dev(g[f"b_cap_np_t_{i - 1}"]), dev(g[f"b_cap_np_style_{i - 1}"]))
+            assert_close(nc.cpu().numpy(), g[f"b_cap_np_out_{i - 1}"])
+            up = hp.upsample_knn(dev(g[f"b_cap_np_out_{i - 1}"]), dev(x_in), xi)
+        np.testing.assert_array_equal(up.cpu().numpy(), g[f"b_cap_up_out_{i - 1}"])
+
+
+def test_ddim_loop(mods, golden):
+    g = golden("sampling.npz")
+    c, m = make_model(mods)
+    m.eval()
+    dp = mods["dm"].DiffusionProcess(c, device="cuda")
+    rp = mods["rng"].ReplayRNG.from_npz(g, "c_rng")
+    with mods["rng"].replay(rp):
+        out = dp.ddim_sample_loop(m, (1, 2048, 3), dev(g["a_cond"]), 4)
+    assert rp.exhausted
+    assert_mostly_close(out.cpu().numpy(), g["c_out"])
+
+
+def test_model_forward_train_mode(mods, golden):
+    g = golden("sampling.npz")
+    c, m = make_model(mods, total_points=4096, global_points=1024)
+    m.train()
+    for mod in m.modules():
+        if isinstance(mod, torch.nn.Dropout):
+            mod.p = 0.0
+    rp = mods["rng"].ReplayRNG.from_npz(g, "d_rng")
+    with torch.no_grad(), mods["rng"].replay(rp):
+        pred, idx = m(dev(g["d_noisy"]), dev(g["d_t"]), dev(g["d_cond"]), cond_drop_prob=0.5)
+    np.testing.assert_array_equal(idx.cpu().numpy(), g["d_idx"])
+    assert_close(pred.cpu().numpy(), g["d_pred"])
+
+
+def test_chamfer_and_loss(mods, golden):
+    g = golden("schedule_losses.npz")
+    L = mods["losses"]
+    p = dev(g["cd_pred"]).requires_grad_(True)
+    q = dev(g["cd_target"]).requires_grad_(True)
+    cd = L.chamfer_distance_chunked_optimized(p, q)
+    assert_close(cd.detach().cpu().numpy(), g["cd_out"], rtol=1e-5)
+    cd.sum().backward()
+    assert_close(p.grad.cpu().numpy(), g["cd_grad_pred"])
+    assert_close(q.grad.cpu().numpy(), g["cd_grad_target"])
+    cd2 = L.chamfer_distance_chunked_optimized(dev(g["cd_pred"][:, :1500]), dev(g["cd_target"][:, :700]), 256)
+    assert_close(cd2.cpu().numpy(), g["cd2_out"], rtol=1e-5)
+    pn, an, pp, tp = (dev(a) for a in g["dl_inputs"])
+    total, d = L.DiffusionLoss(1.0, 0.1)(pn, an, pp, tp)
+    assert abs(d["noise_loss"] - float(g["dl_noise"])) < 1e-6
+    assert abs(d["chamfer_loss"] - float(g["dl_chamfer"])) < 1e-5 * float(g["dl_chamfer"])
+    assert abs(float(total) - float(g["dl_total"])) < 1e-5 * float(g["dl_total"])
+
+
+def test_chamfer_determinism(mods):
+    L = mods["losses"]
+    rng = np.random.default_rng(0)
+    a = rng.standard_normal((2, 5000, 3)).astype(np.float32)
+    b = rng.standard_normal((2, 4000, 3)).astype(np.float32)
+    grads = []
+    for _ in range(2):
+        p = dev(a).requires_grad_(True)
+        L.chamfer_distance_chunked_optimized(p, dev(b)).sum().backward()
+        grads.append(p.grad.cpu().numpy())
+    np.testing.assert_array_equal(grads[0], grads[1])
