@@ -1,42 +1,241 @@
-// Small per-cloud reductions shared by several kernels.
+// Per-cloud reductions and scans shared by several kernels (internal linkage).
+//  - cloud statistics (min, max, sum, sum of squares per axis) as a two-level reduction:
+//    per-block partial records, no contended atomics; consumers fold the partials;
+//  - exclusive scan of a long u32 array per segment (tile reduce -> tile-sum scan -> tile
+//    scan), all loads coalesced.
 #pragma once
 #include "common.h"
 
 namespace pcst {
 namespace {  // internal linkage: included by several translation units
 
-// mm[b][0..2] = ordered-int min xyz, mm[b][3..5] = max xyz.
-__global__ void cloud_mm_init_kernel(int32_t* mm, int B) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < B * 6) mm[i] = (i % 6) < 3 ? INT32_MAX : INT32_MIN;
-}
+constexpr int kStatBlocks = 64;  // partial records per cloud
 
-__global__ __launch_bounds__(256) void cloud_minmax_kernel(const float* __restrict__ pts, int N,
-                                                           int32_t* __restrict__ mm) {
-  const int b = blockIdx.y;
+struct StatRec {
+  float mn[3], mx[3];
+  double s[3], ss[3];
+};
+
+__global__ __launch_bounds__(256) void cloud_stats_partial_kernel(const float* __restrict__ pts,
+                                                                  int N, StatRec* __restrict__ part) {
+  const int b = blockIdx.y, blk = blockIdx.x;
   const float* P = pts + (int64_t)b * N * 3;
-  float mn0 = 3.4e38f, mn1 = 3.4e38f, mn2 = 3.4e38f, mx0 = -3.4e38f, mx1 = -3.4e38f, mx2 = -3.4e38f;
-  for (int n = blockIdx.x * 256 + threadIdx.x; n < N; n += gridDim.x * 256) {
-    const float x = P[n * 3], y = P[n * 3 + 1], z = P[n * 3 + 2];
-    mn0 = fminf(mn0, x); mn1 = fminf(mn1, y); mn2 = fminf(mn2, z);
-    mx0 = fmaxf(mx0, x); mx1 = fmaxf(mx1, y); mx2 = fmaxf(mx2, z);
+  float mn[3] = {3.4e38f, 3.4e38f, 3.4e38f}, mx[3] = {-3.4e38f, -3.4e38f, -3.4e38f};
+  double s[3] = {0, 0, 0}, ss[3] = {0, 0, 0};
+  for (int n = blk * 256 + threadIdx.x; n < N; n += kStatBlocks * 256) {
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      const float v = P[n * 3 + c];
+      mn[c] = fminf(mn[c], v);
+      mx[c] = fmaxf(mx[c], v);
+      s[c] += v;
+      ss[c] += (double)v * v;
+    }
   }
+#pragma unroll
   for (int off = 32; off >= 1; off >>= 1) {
-    mn0 = fminf(mn0, __shfl_xor(mn0, off)); mn1 = fminf(mn1, __shfl_xor(mn1, off));
-    mn2 = fminf(mn2, __shfl_xor(mn2, off)); mx0 = fmaxf(mx0, __shfl_xor(mx0, off));
-    mx1 = fmaxf(mx1, __shfl_xor(mx1, off)); mx2 = fmaxf(mx2, __shfl_xor(mx2, off));
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      mn[c] = fminf(mn[c], __shfl_xor(mn[c], off));
+      mx[c] = fmaxf(mx[c], __shfl_xor(mx[c], off));
+      s[c] += __shfl_xor(s[c], off);
+      ss[c] += __shfl_xor(ss[c], off);
+    }
   }
+  __shared__ StatRec w[4];
+  const int wid = threadIdx.x >> 6;
   if ((threadIdx.x & 63) == 0) {
-    int32_t* M = mm + b * 6;
-    atomicMin(&M[0], f2ord(mn0)); atomicMin(&M[1], f2ord(mn1)); atomicMin(&M[2], f2ord(mn2));
-    atomicMax(&M[3], f2ord(mx0)); atomicMax(&M[4], f2ord(mx1)); atomicMax(&M[5], f2ord(mx2));
+    for (int c = 0; c < 3; ++c) {
+      w[wid].mn[c] = mn[c]; w[wid].mx[c] = mx[c]; w[wid].s[c] = s[c]; w[wid].ss[c] = ss[c];
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    StatRec r = w[0];
+    for (int q = 1; q < 4; ++q)
+      for (int c = 0; c < 3; ++c) {
+        r.mn[c] = fminf(r.mn[c], w[q].mn[c]);
+        r.mx[c] = fmaxf(r.mx[c], w[q].mx[c]);
+        r.s[c] += w[q].s[c];
+        r.ss[c] += w[q].ss[c];
+      }
+    part[b * kStatBlocks + blk] = r;
   }
 }
 
-inline void launch_cloud_minmax(const float* pts, int B, int N, int32_t* mm, hipStream_t s) {
-  hipLaunchKernelGGL(cloud_mm_init_kernel, dim3((unsigned)cdiv(B * 6, 256)), dim3(256), 0, s, mm, B);
-  const int gx = (int)std::min<int64_t>(cdiv(N, 256), 64);
-  hipLaunchKernelGGL(cloud_minmax_kernel, dim3(gx, B), dim3(256), 0, s, pts, N, mm);
+// Fold the partial records of cloud b (fixed order: deterministic).
+__device__ __forceinline__ StatRec fold_stats(const StatRec* __restrict__ part, int b) {
+  StatRec r = part[b * kStatBlocks];
+  for (int q = 1; q < kStatBlocks; ++q) {
+    const StatRec& o = part[b * kStatBlocks + q];
+    for (int c = 0; c < 3; ++c) {
+      r.mn[c] = fminf(r.mn[c], o.mn[c]);
+      r.mx[c] = fmaxf(r.mx[c], o.mx[c]);
+      r.s[c] += o.s[c];
+      r.ss[c] += o.ss[c];
+    }
+  }
+  return r;
+}
+
+inline void launch_cloud_stats(const float* pts, int B, int N, StatRec* part, hipStream_t s) {
+  hipLaunchKernelGGL(cloud_stats_partial_kernel, dim3(kStatBlocks, B), dim3(256), 0, s, pts, N,
+                     part);
+}
+
+// ---- exclusive scan of `len` u32 per segment (stride `stride`), in place, optional totals.
+constexpr int kScanItems = 16;
+constexpr int kScanTile = 256 * kScanItems;  // 4096
+
+__device__ __forceinline__ uint32_t block_excl_scan_256(uint32_t v, uint32_t* sh, uint32_t& total) {
+  // sh: 256 + 4 words
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  uint32_t x = v;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const uint32_t y = __shfl_up(x, off);
+    if (lane >= off) x += y;
+  }
+  if (lane == 63) sh[256 + w] = x;
+  __syncthreads();
+  uint32_t wofs = 0;
+  for (int q = 0; q < w; ++q) wofs += sh[256 + q];
+  total = sh[256] + sh[257] + sh[258] + sh[259];
+  __syncthreads();
+  return wofs + x - v;
+}
+
+__global__ __launch_bounds__(256) void scan_tile_sum_kernel(const uint32_t* __restrict__ data,
+                                                            int64_t len, int64_t stride,
+                                                            uint32_t* __restrict__ tsum, int tiles) {
+  const int seg = blockIdx.y, tile = blockIdx.x;
+  const uint32_t* D = data + seg * stride;
+  const int64_t base = (int64_t)tile * kScanTile;
+  uint32_t acc = 0;
+#pragma unroll
+  for (int k = 0; k < kScanItems; ++k) {
+    const int64_t i = base + k * 256 + threadIdx.x;
+    if (i < len) acc += D[i];
+  }
+  for (int off = 32; off >= 1; off >>= 1) acc += __shfl_xor(acc, off);
+  __shared__ uint32_t w[4];
+  if ((threadIdx.x & 63) == 0) w[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) tsum[(int64_t)seg * tiles + tile] = w[0] + w[1] + w[2] + w[3];
+}
+
+// single workgroup per segment: exclusive scan of up to 256*kScanItems tile sums
+__global__ __launch_bounds__(256) void scan_tsum_kernel(uint32_t* __restrict__ tsum, int tiles,
+                                                        int32_t* __restrict__ total) {
+  const int seg = blockIdx.x;
+  uint32_t* T = tsum + (int64_t)seg * tiles;
+  __shared__ uint32_t sh[260];
+  uint32_t carry = 0;
+  for (int base = 0; base < tiles; base += 256) {
+    const int i = base + threadIdx.x;
+    const uint32_t v = i < tiles ? T[i] : 0u;
+    uint32_t tot;
+    const uint32_t ex = block_excl_scan_256(v, sh, tot);
+    if (i < tiles) T[i] = carry + ex;
+    carry += tot;
+  }
+  if (total && threadIdx.x == 0) total[seg] = (int32_t)carry;
+}
+
+// tile-local scan (items blocked per thread via LDS transpose) + tile offset
+__global__ __launch_bounds__(256) void scan_tile_kernel(uint32_t* __restrict__ data, int64_t len,
+                                                        int64_t stride,
+                                                        const uint32_t* __restrict__ toff, int tiles) {
+  const int seg = blockIdx.y, tile = blockIdx.x;
+  uint32_t* D = data + seg * stride;
+  const int64_t base = (int64_t)tile * kScanTile;
+  __shared__ uint32_t buf[kScanTile + kScanTile / 32];
+  __shared__ uint32_t sh[260];
+  auto pad = [](int i) { return i + (i >> 5); };
+#pragma unroll
+  for (int k = 0; k < kScanItems; ++k) {
+    const int j = k * 256 + threadIdx.x;
+    const int64_t i = base + j;
+    buf[pad(j)] = i < len ? D[i] : 0u;
+  }
+  __syncthreads();
+  uint32_t v[kScanItems], s = 0;
+#pragma unroll
+  for (int k = 0; k < kScanItems; ++k) {
+    v[k] = buf[pad(threadIdx.x * kScanItems + k)];
+    s += v[k];
+  }
+  uint32_t tot;
+  uint32_t run = block_excl_scan_256(s, sh, tot) + toff[(int64_t)seg * tiles + tile];
+#pragma unroll
+  for (int k = 0; k < kScanItems; ++k) {
+    buf[pad(threadIdx.x * kScanItems + k)] = run;
+    run += v[k];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < kScanItems; ++k) {
+    const int j = k * 256 + threadIdx.x;
+    const int64_t i = base + j;
+    if (i < len) D[i] = buf[pad(j)];
+  }
+}
+
+inline size_t scan_tsum_words(int nseg, int64_t len) { return (size_t)nseg * cdiv(len, kScanTile); }
+
+// One workgroup per segment, whole array staged in LDS (len <= kSmallScanMax): coalesced
+// load, 16 contiguous entries per thread, block scan, coalesced store.  total[seg] optional.
+constexpr int kSmallScanMax = 16384;
+__global__ __launch_bounds__(1024) void seg_scan_small_kernel(uint32_t* __restrict__ data, int len,
+                                                              int64_t stride,
+                                                              int32_t* __restrict__ total) {
+  __shared__ uint32_t buf[kSmallScanMax + kSmallScanMax / 32];
+  __shared__ uint32_t wsum[16];
+  uint32_t* D = data + blockIdx.x * stride;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  auto pad = [](int i) { return i + (i >> 5); };
+  for (int i = t; i < kSmallScanMax; i += 1024) buf[pad(i)] = i < len ? D[i] : 0u;
+  __syncthreads();
+  uint32_t v[16], s = 0;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    v[k] = buf[pad(t * 16 + k)];
+    s += v[k];
+  }
+  uint32_t x = s;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const uint32_t y = __shfl_up(x, off);
+    if (lane >= off) x += y;
+  }
+  if (lane == 63) wsum[w] = x;
+  __syncthreads();
+  uint32_t run = x - s;
+  for (int q = 0; q < w; ++q) run += wsum[q];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    buf[pad(t * 16 + k)] = run;
+    run += v[k];
+  }
+  if (total && t == 1023) total[blockIdx.x] = (int32_t)run;
+  __syncthreads();
+  for (int i = t; i < len; i += 1024) D[i] = buf[pad(i)];
+}
+
+inline void seg_scan_small(uint32_t* data, int nseg, int len, int64_t stride, int32_t* totals,
+                           hipStream_t s) {
+  hipLaunchKernelGGL(seg_scan_small_kernel, dim3(nseg), dim3(1024), 0, s, data, len, stride, totals);
+}
+
+// exclusive scan of data[seg*stride + 0..len) for every segment; totals[seg] if non-null.
+inline void seg_scan_long(uint32_t* data, int nseg, int64_t len, int64_t stride, uint32_t* tsum,
+                          int32_t* totals, hipStream_t s) {
+  const int tiles = (int)cdiv(len, kScanTile);
+  hipLaunchKernelGGL(scan_tile_sum_kernel, dim3(tiles, nseg), dim3(256), 0, s, data, len, stride,
+                     tsum, tiles);
+  hipLaunchKernelGGL(scan_tsum_kernel, dim3(nseg), dim3(256), 0, s, tsum, tiles, totals);
+  hipLaunchKernelGGL(scan_tile_kernel, dim3(tiles, nseg), dim3(256), 0, s, data, len, stride, tsum,
+                     tiles);
 }
 
 }  // namespace

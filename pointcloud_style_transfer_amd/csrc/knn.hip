@@ -8,80 +8,87 @@
 //                  exact ties -> lower j; w = 1/(sqrt(rdist)+1e-8), w /= ((w0+w1)+w2),
 //                  value = ((v0*w0 + v1*w1) + v2*w2) in float64, rounded to float32.
 //
-// Exact search on a uniform grid over the cloud's bounding box (refs counting-sorted by cell,
-// ~2 refs per cell), shell-by-shell around the query's cell until the 3rd-best distance is
-// below the distance to the unvisited region.  All distance/weight arithmetic is float64 with
-// *_rn intrinsics (no contraction), so neighbour sets and weights match the reference.
+// Exact search on a uniform grid whose cell size follows the cloud's PEAK density (estimated
+// from the per-axis spread, ~3 refs per cell where the cloud is densest), so a dense core is
+// not searched through overfull cells.  Refs and queries are both counting-sorted by cell:
+// neighbouring lanes search neighbouring cells (coherent loads, similar trip counts).  Each
+// candidate is screened with an fp32 distance (relative error < 3e-7, screened against the
+// current 3rd-best x (1 + 2e-6)) and only survivors are ranked in exact float64.
 #include "common.h"
-#include "sort.h"
 #include "cloud.h"
 
 namespace pcst {
 
 struct KnnWS {
-  int32_t* mm;       // [B][6]
-  float* gp;         // [B][8]: origin xyz, cell size, inv size, dims xyz (as float bits)
-  uint32_t* known;   // [B][N]  (j+1 of the last coarse row writing n, 0 = query)
-  uint32_t* ccount;  // [B][C]  counts, then (after the scan) cell starts
-  uint32_t* cursor;  // [B][C]  fill cursors
-  float4* refs;      // [B][M]  (x, y, z, j as bits), cell-sorted
+  StatRec* stats;    // [B][kStatBlocks]
+  float* gp;         // [B][8]: origin xyz, cell size, inv size, dims xyz (int bits)
   int32_t* err;
+  uint32_t* known;   // [B][N]  (j+1 of the last coarse row writing n, 0 = query)
+  uint32_t* rstart;  // [B][C+1] ref counts -> starts
+  uint32_t* rcur;    // [B][C]   fill cursors
+  uint32_t* qstart;  // [B][C+1] query counts -> starts
+  uint32_t* qcur;    // [B][C]
+  uint32_t* tsum;    // scan scratch
+  float4* refs;      // [B][M]   (x, y, z, j) cell-sorted
+  int32_t* qorder;   // [B][N]   point index in cell order
   int64_t C;
   size_t bytes;
 };
 
+static int64_t knn_cells(int64_t M) { return std::max<int64_t>(4096, 24 * M); }
+
 static KnnWS carve_knn(void* base, int64_t B, int64_t N, int64_t M) {
   Carver c(base);
   KnnWS w;
-  w.C = std::max<int64_t>(64, 2 * M);
-  w.mm = c.take<int32_t>(B * 6);
+  w.C = knn_cells(M);
+  w.stats = c.take<StatRec>(B * kStatBlocks);
   w.gp = c.take<float>(B * 8);
   w.err = c.take<int32_t>(4);
   w.known = c.take<uint32_t>(B * N);
-  w.ccount = c.take<uint32_t>(B * w.C);
-  w.cursor = c.take<uint32_t>(B * w.C);
+  w.rstart = c.take<uint32_t>(B * (w.C + 1));
+  w.qstart = c.take<uint32_t>(B * (w.C + 1));
+  w.rcur = c.take<uint32_t>(B * w.C);
+  w.qcur = c.take<uint32_t>(B * w.C);
+  w.tsum = c.take<uint32_t>(scan_tsum_words((int)B, w.C + 1));
   w.refs = c.take<float4>(B * M);
+  w.qorder = c.take<int32_t>(B * N);
   w.bytes = c.bytes();
   return w;
 }
 
-// Grid: ~2 refs per cell over the bounding box, at most C cells, each dim in [1, 1024].
-__global__ void knn_grid_params_kernel(const int32_t* __restrict__ mm, int B, int64_t M, int64_t C,
-                                       float* __restrict__ gp) {
+// Cell size from the peak density of a Gaussian with the cloud's per-axis spread:
+// rho_max = M / ((2 pi)^1.5 sx sy sz); s^3 = 3 / rho_max.  Capped so the bounding box holds
+// at most C cells (and at most 2048 per axis).
+__global__ void knn_grid_params_kernel(const StatRec* __restrict__ stats, int B, int64_t N,
+                                       int64_t M, int64_t C, float* __restrict__ gp) {
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= B) return;
-  const int32_t* Mm = mm + b * 6;
-  double lo[3], ext[3];
+  const StatRec r = fold_stats(stats, b);
+  double ext[3], sig[3];
   for (int c = 0; c < 3; ++c) {
-    lo[c] = ord2f(Mm[c]);
-    ext[c] = (double)ord2f(Mm[3 + c]) - lo[c];
-    if (!(ext[c] > 1e-12)) ext[c] = 1e-12;
+    ext[c] = (double)r.mx[c] - (double)r.mn[c];
+    if (!(ext[c] > 1e-9)) ext[c] = 1e-9;
+    const double mean = r.s[c] / (double)N;
+    double var = r.ss[c] / (double)N - mean * mean;
+    sig[c] = sqrt(fmax(var, 0.0));
+    sig[c] = fmax(sig[c], 1e-3 * ext[c]);
   }
-  const double cells = fmax(1.0, (double)M / 2.0);
-  double s = cbrt(ext[0] * ext[1] * ext[2] / cells);
-  // thin dimensions: shrink s so the other dims carry the cells
-  for (int it = 0; it < 3; ++it) {
-    int flat = 0;
-    double vol = 1.0;
-    for (int c = 0; c < 3; ++c) {
-      if (ext[c] < s) ++flat;
-      else vol *= ext[c];
-    }
-    if (flat == 0 || flat == 3) break;
-    s = pow(vol / cells, 1.0 / (3 - flat));
-  }
+  const double rho = (double)M / (15.7496099457 * sig[0] * sig[1] * sig[2]);
+  double s = cbrt(3.0 / rho);
+  // a cell must not be smaller than a thin dimension forces: keep at least ~1 ref per
+  // cell on average over the occupied extent
   int d[3];
-  for (;;) {
+  for (int it = 0; it < 200; ++it) {
     int64_t tot = 1;
     for (int c = 0; c < 3; ++c) {
-      d[c] = (int)fmin(1024.0, fmax(1.0, ceil(ext[c] / s)));
+      d[c] = (int)fmin(2048.0, fmax(1.0, ceil(ext[c] / s)));
       tot *= d[c];
     }
     if (tot <= C) break;
     s *= 1.1;
   }
   float* G = gp + b * 8;
-  G[0] = (float)lo[0]; G[1] = (float)lo[1]; G[2] = (float)lo[2];
+  G[0] = r.mn[0]; G[1] = r.mn[1]; G[2] = r.mn[2];
   G[3] = (float)s;
   G[4] = (float)(1.0 / s);
   G[5] = __int_as_float(d[0]); G[6] = __int_as_float(d[1]); G[7] = __int_as_float(d[2]);
@@ -90,6 +97,13 @@ __global__ void knn_grid_params_kernel(const int32_t* __restrict__ mm, int B, in
 __device__ __forceinline__ int cell_coord(float p, float o, float inv, int d) {
   int c = (int)floorf((p - o) * inv);
   return c < 0 ? 0 : (c >= d ? d - 1 : c);
+}
+
+__device__ __forceinline__ int64_t cell_of(const float* p, const float* G) {
+  const int dx = __float_as_int(G[5]), dy = __float_as_int(G[6]), dz = __float_as_int(G[7]);
+  const int cx = cell_coord(p[0], G[0], G[4], dx), cy = cell_coord(p[1], G[1], G[4], dy),
+            cz = cell_coord(p[2], G[2], G[4], dz);
+  return ((int64_t)cz * dy + cy) * dx + cx;
 }
 
 __global__ void knn_known_kernel(const int64_t* __restrict__ idx, int64_t N, int64_t M,
@@ -102,38 +116,42 @@ __global__ void knn_known_kernel(const int64_t* __restrict__ idx, int64_t N, int
   }
 }
 
+// count refs (j < M, point orig[idx[j]]) and queries (all N points) per cell
 __global__ void knn_count_kernel(const float* __restrict__ orig, const int64_t* __restrict__ idx,
                                  int64_t N, int64_t M, int64_t C, const float* __restrict__ gp,
-                                 uint32_t* __restrict__ ccount) {
+                                 uint32_t* __restrict__ rcount, uint32_t* __restrict__ qcount) {
   const int b = blockIdx.y;
   const float* G = gp + b * 8;
-  const int dx = __float_as_int(G[5]), dy = __float_as_int(G[6]), dz = __float_as_int(G[7]);
-  for (int64_t j = blockIdx.x * 256 + threadIdx.x; j < M; j += gridDim.x * 256) {
-    int64_t n = idx[b * M + j];
-    n = n < 0 ? 0 : (n >= N ? N - 1 : n);
-    const float* p = orig + (b * N + n) * 3;
-    const int cx = cell_coord(p[0], G[0], G[4], dx), cy = cell_coord(p[1], G[1], G[4], dy),
-              cz = cell_coord(p[2], G[2], G[4], dz);
-    atomicAdd(&ccount[b * C + ((int64_t)cz * dy + cy) * dx + cx], 1u);
+  for (int64_t e = blockIdx.x * 256 + threadIdx.x; e < M + N; e += gridDim.x * 256) {
+    if (e < M) {
+      int64_t n = idx[b * M + e];
+      n = n < 0 ? 0 : (n >= N ? N - 1 : n);
+      atomicAdd(&rcount[b * (C + 1) + cell_of(orig + (b * N + n) * 3, G)], 1u);
+    } else {
+      const int64_t n = e - M;
+      atomicAdd(&qcount[b * (C + 1) + cell_of(orig + (b * N + n) * 3, G)], 1u);
+    }
   }
 }
 
-// After the exclusive scan ccount[c] = start of cell c; refs are placed through a copy of
-// the starts used as atomic cursors (in-cell order is irrelevant: ties break on j).
 __global__ void knn_fill_kernel(const float* __restrict__ orig, const int64_t* __restrict__ idx,
                                 int64_t N, int64_t M, int64_t C, const float* __restrict__ gp,
-                                uint32_t* __restrict__ cursor, float4* __restrict__ refs) {
+                                uint32_t* __restrict__ rcur, uint32_t* __restrict__ qcur,
+                                float4* __restrict__ refs, int32_t* __restrict__ qorder) {
   const int b = blockIdx.y;
   const float* G = gp + b * 8;
-  const int dx = __float_as_int(G[5]), dy = __float_as_int(G[6]), dz = __float_as_int(G[7]);
-  for (int64_t j = blockIdx.x * 256 + threadIdx.x; j < M; j += gridDim.x * 256) {
-    int64_t n = idx[b * M + j];
-    n = n < 0 ? 0 : (n >= N ? N - 1 : n);
-    const float* p = orig + (b * N + n) * 3;
-    const int cx = cell_coord(p[0], G[0], G[4], dx), cy = cell_coord(p[1], G[1], G[4], dy),
-              cz = cell_coord(p[2], G[2], G[4], dz);
-    const uint32_t pos = atomicAdd(&cursor[b * C + ((int64_t)cz * dy + cy) * dx + cx], 1u);
-    refs[b * M + pos] = make_float4(p[0], p[1], p[2], __int_as_float((int)j));
+  for (int64_t e = blockIdx.x * 256 + threadIdx.x; e < M + N; e += gridDim.x * 256) {
+    if (e < M) {
+      int64_t n = idx[b * M + e];
+      n = n < 0 ? 0 : (n >= N ? N - 1 : n);
+      const float* p = orig + (b * N + n) * 3;
+      const uint32_t pos = atomicAdd(&rcur[b * C + cell_of(p, G)], 1u);
+      refs[b * M + pos] = make_float4(p[0], p[1], p[2], __int_as_float((int)e));
+    } else {
+      const int64_t n = e - M;
+      const uint32_t pos = atomicAdd(&qcur[b * C + cell_of(orig + (b * N + n) * 3, G)], 1u);
+      qorder[b * N + pos] = (int32_t)n;
+    }
   }
 }
 
@@ -163,10 +181,12 @@ struct Top3 {
 __global__ __launch_bounds__(256) void knn_query_kernel(
     const float* __restrict__ orig, const float* __restrict__ vals, int64_t N, int64_t M,
     int64_t C, const float* __restrict__ gp, const uint32_t* __restrict__ known,
-    const uint32_t* __restrict__ cstart, const float4* __restrict__ refs, float* __restrict__ out) {
+    const uint32_t* __restrict__ rstart, const float4* __restrict__ refs,
+    const int32_t* __restrict__ qorder, float* __restrict__ out) {
   const int b = blockIdx.y;
-  const int64_t n = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (n >= N) return;
+  const int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (k >= N) return;
+  const int64_t n = qorder[b * N + k];
   const float* V = vals + b * M * 3;
   float* O = out + (b * N + n) * 3;
   const uint32_t kn = known[b * N + n];
@@ -178,40 +198,45 @@ __global__ __launch_bounds__(256) void knn_query_kernel(
   const float* G = gp + b * 8;
   const int dx = __float_as_int(G[5]), dy = __float_as_int(G[6]), dz = __float_as_int(G[7]);
   const float* q = orig + (b * N + n) * 3;
-  const double qx = q[0], qy = q[1], qz = q[2];
-  const int cx = cell_coord(q[0], G[0], G[4], dx), cy = cell_coord(q[1], G[1], G[4], dy),
-            cz = cell_coord(q[2], G[2], G[4], dz);
+  const float fx = q[0], fy = q[1], fz = q[2];
+  const double qx = fx, qy = fy, qz = fz;
+  const int cx = cell_coord(fx, G[0], G[4], dx), cy = cell_coord(fy, G[1], G[4], dy),
+            cz = cell_coord(fz, G[2], G[4], dz);
   const double ox = G[0], oy = G[1], oz = G[2], s = G[3];
   const double slack = 1e-5 * s;  // covers fp32 cell-assignment rounding
-  const uint32_t* CS = cstart + b * C;
+  const uint32_t* RS = rstart + b * (C + 1);
   const float4* R = refs + b * M;
-  const int k = M < 3 ? (int)M : 3;
+  const int kk = M < 3 ? (int)M : 3;
   Top3 t;
   t.init();
+  float thr = INFINITY;  // fp32 screen: candidates above it cannot enter the top k
   const int rmax = max(dx, max(dy, dz));
   for (int r = 0; r <= rmax; ++r) {
-    for (int z = cz - r; z <= cz + r; ++z) {
-      if (z < 0 || z >= dz) continue;
-      for (int y = cy - r; y <= cy + r; ++y) {
-        if (y < 0 || y >= dy) continue;
+    const int z0 = max(cz - r, 0), z1 = min(cz + r, dz - 1);
+    const int y0 = max(cy - r, 0), y1 = min(cy + r, dy - 1);
+    for (int z = z0; z <= z1; ++z) {
+      for (int y = y0; y <= y1; ++y) {
         const bool face = (z == cz - r || z == cz + r || y == cy - r || y == cy + r);
         const int step = (face || r == 0) ? 1 : 2 * r;
         for (int x = cx - r; x <= cx + r; x += step) {
           if (x < 0 || x >= dx) continue;
           const int64_t cell = ((int64_t)z * dy + y) * dx + x;
-          const uint32_t a = CS[cell];
-          const uint32_t e = cell + 1 < C ? CS[cell + 1] : (uint32_t)M;
+          const uint32_t a = RS[cell], e = RS[cell + 1];
           for (uint32_t i = a; i < e; ++i) {
             const float4 ref = R[i];
-            const double ex = dsub(qx, (double)ref.x), ey = dsub(qy, (double)ref.y),
-                         ez = dsub(qz, (double)ref.z);
-            const double d = dadd(dadd(dmul(ex, ex), dmul(ey, ey)), dmul(ez, ez));
+            const float ex = fx - ref.x, ey = fy - ref.y, ez = fz - ref.z;
+            const float d32 = fmaf(ez, ez, fmaf(ey, ey, ex * ex));
+            if (d32 > thr) continue;
+            const double ux = dsub(qx, (double)ref.x), uy = dsub(qy, (double)ref.y),
+                         uz = dsub(qz, (double)ref.z);
+            const double d = dadd(dadd(dmul(ux, ux), dmul(uy, uy)), dmul(uz, uz));
             t.push(d, __float_as_int(ref.w));
+            if (t.d[kk - 1] != INFINITY) thr = (float)(t.d[kk - 1] * (1.0 + 2e-6)) + 1e-30f;
           }
         }
       }
     }
-    if (t.d[k - 1] == INFINITY) continue;
+    if (t.d[kk - 1] == INFINITY) continue;
     // distance from q to the unvisited region outside the (2r+1)^3 block
     double bound = INFINITY;
     if (cx - r > 0) bound = fmin(bound, qx - (ox + (cx - r) * s));
@@ -221,17 +246,17 @@ __global__ __launch_bounds__(256) void knn_query_kernel(
     if (cz - r > 0) bound = fmin(bound, qz - (oz + (cz - r) * s));
     if (cz + r + 1 < dz) bound = fmin(bound, (oz + (cz + r + 1) * s) - qz);
     bound -= slack;
-    if (bound == INFINITY || (bound > 0 && t.d[k - 1] < bound * bound)) break;
+    if (bound == INFINITY || (bound > 0 && t.d[kk - 1] < bound * bound)) break;
   }
   double w[3], wsum = 0.0;
-  for (int i = 0; i < k; ++i) {
+  for (int i = 0; i < kk; ++i) {
     w[i] = __ddiv_rn(1.0, dadd(__dsqrt_rn(t.d[i]), 1e-8));
     wsum = i == 0 ? w[0] : dadd(wsum, w[i]);
   }
-  for (int i = 0; i < k; ++i) w[i] = __ddiv_rn(w[i], wsum);
+  for (int i = 0; i < kk; ++i) w[i] = __ddiv_rn(w[i], wsum);
   for (int c = 0; c < 3; ++c) {
     double acc = 0.0;
-    for (int i = 0; i < k; ++i) {
+    for (int i = 0; i < kk; ++i) {
       const double term = dmul((double)V[(int64_t)t.j[i] * 3 + c], w[i]);
       acc = i == 0 ? term : dadd(acc, term);
     }
@@ -252,32 +277,34 @@ extern "C" int pcst_knn_workspace_size(int64_t B, int64_t N, int64_t M, size_t* 
 extern "C" int pcst_knn3_interp(const float* coarse, const float* orig, const int64_t* idx,
                                 int64_t B, int64_t N, int64_t M, float* out, void* workspace,
                                 void* stream) {
-  PCST_CHECK_ARG(B >= 0 && N > 0 && M > 0 && N < (1ll << 31) && M < (1ll << 31),
+  PCST_CHECK_ARG(B >= 0 && N > 0 && M > 0 && N < (1ll << 31) && M < (1ll << 27),
                  "knn3_interp: bad shape");
   if (B == 0) return PCST_OK;
   PCST_CHECK_ARG(coarse && orig && idx && out && workspace, "knn3_interp: null pointer");
   hipStream_t s = as_stream(stream);
   KnnWS w = carve_knn(workspace, B, N, M);
   const int b = (int)B;
-  PCST_HIP(hipMemsetAsync(w.err, 0, 16, s), "knn: memset");
-  PCST_HIP(hipMemsetAsync(w.known, 0, sizeof(uint32_t) * B * N, s), "knn: memset");
-  PCST_HIP(hipMemsetAsync(w.ccount, 0, sizeof(uint32_t) * B * w.C, s), "knn: memset");
-  launch_cloud_minmax(orig, b, (int)N, w.mm, s);
-  hipLaunchKernelGGL(knn_grid_params_kernel, dim3((unsigned)cdiv(B, 64)), dim3(64), 0, s, w.mm, b,
-                     M, w.C, w.gp);
+  const int64_t C = w.C;
+  // known + both count arrays are contiguous in the carve: one memset
+  PCST_HIP(hipMemsetAsync(w.err, 0, (size_t)((char*)w.rcur - (char*)w.err), s), "knn: memset");
+  launch_cloud_stats(orig, b, (int)N, w.stats, s);
+  hipLaunchKernelGGL(knn_grid_params_kernel, dim3((unsigned)cdiv(B, 64)), dim3(64), 0, s, w.stats,
+                     b, N, M, C, w.gp);
   const unsigned gm = (unsigned)std::min<int64_t>(cdiv(M, 256), 1024);
   hipLaunchKernelGGL(knn_known_kernel, dim3(gm, b), dim3(256), 0, s, idx, N, M, w.known, w.err);
-  hipLaunchKernelGGL(knn_count_kernel, dim3(gm, b), dim3(256), 0, s, orig, idx, N, M, w.C, w.gp,
-                     w.ccount);
-  SegCounts cc{nullptr, (int32_t)w.C};
-  hipLaunchKernelGGL(seg_scan_kernel, dim3(b), dim3(1024), 0, s, w.ccount, 1, (int)w.C, cc, 1,
-                     (int32_t*)nullptr);
-  PCST_HIP(hipMemcpyAsync(w.cursor, w.ccount, sizeof(uint32_t) * B * w.C,
-                          hipMemcpyDeviceToDevice, s), "knn: copy starts");
-  hipLaunchKernelGGL(knn_fill_kernel, dim3(gm, b), dim3(256), 0, s, orig, idx, N, M, w.C, w.gp,
-                     w.cursor, w.refs);
+  const unsigned ga = (unsigned)std::min<int64_t>(cdiv(M + N, 256), 2048);
+  hipLaunchKernelGGL(knn_count_kernel, dim3(ga, b), dim3(256), 0, s, orig, idx, N, M, C, w.gp,
+                     w.rstart, w.qstart);
+  seg_scan_long(w.rstart, b, C + 1, C + 1, w.tsum, nullptr, s);
+  seg_scan_long(w.qstart, b, C + 1, C + 1, w.tsum, nullptr, s);
+  PCST_HIP(hipMemcpy2DAsync(w.rcur, sizeof(uint32_t) * C, w.rstart, sizeof(uint32_t) * (C + 1),
+                            sizeof(uint32_t) * C, B, hipMemcpyDeviceToDevice, s), "knn: cursors");
+  PCST_HIP(hipMemcpy2DAsync(w.qcur, sizeof(uint32_t) * C, w.qstart, sizeof(uint32_t) * (C + 1),
+                            sizeof(uint32_t) * C, B, hipMemcpyDeviceToDevice, s), "knn: cursors");
+  hipLaunchKernelGGL(knn_fill_kernel, dim3(ga, b), dim3(256), 0, s, orig, idx, N, M, C, w.gp,
+                     w.rcur, w.qcur, w.refs, w.qorder);
   hipLaunchKernelGGL(knn_query_kernel, dim3((unsigned)cdiv(N, 256), b), dim3(256), 0, s, orig,
-                     coarse, N, M, w.C, w.gp, w.known, w.ccount, w.refs, out);
+                     coarse, N, M, C, w.gp, w.known, w.rstart, w.refs, w.qorder, out);
   PCST_LAUNCH_CHECK("knn3_interp");
   return PCST_OK;
 }

@@ -7,6 +7,7 @@
 // (wave, round, lane), i.e. the input order, which is what makes the scatter stable.
 #pragma once
 #include "common.h"
+#include "cloud.h"
 
 namespace pcst {
 namespace {  // internal linkage: included by several translation units
@@ -39,40 +40,6 @@ __global__ __launch_bounds__(kSortThreads) void radix_hist_kernel(
   }
   __syncthreads();
   hist[((int64_t)seg * 256 + threadIdx.x) * tiles + tile] = cnt[threadIdx.x];
-}
-
-// Exclusive scan, in place, of `len` u32 entries per segment (digit-major tile tables).
-// `valid_tiles` limits the tiles that hold data: entries for tiles >= valid are skipped
-// (left untouched) so the scan only counts real data.  Optionally stores the total.
-__global__ __launch_bounds__(1024) void seg_scan_kernel(uint32_t* __restrict__ data, int rows,
-                                                        int tiles, SegCounts counts, int tile_elems,
-                                                        int32_t* __restrict__ total) {
-  const int seg = blockIdx.x;
-  const int n = counts.get(seg);
-  const int vt = (n + tile_elems - 1) / tile_elems;
-  uint32_t* D = data + (int64_t)seg * rows * tiles;
-  const int len = rows * vt;  // logical entries (row-major over valid tiles)
-  const int per = (len + 1023) / 1024;
-  const int t = threadIdx.x;
-  uint32_t local = 0;
-  for (int j = t * per; j < min(len, (t + 1) * per); ++j) local += D[(j / vt) * tiles + (j % vt)];
-  __shared__ uint32_t s[1024];
-  s[t] = local;
-  __syncthreads();
-  for (int off = 1; off < 1024; off <<= 1) {
-    uint32_t v = t >= off ? s[t - off] : 0u;
-    __syncthreads();
-    s[t] += v;
-    __syncthreads();
-  }
-  uint32_t run = s[t] - local;  // exclusive prefix of this thread's chunk
-  for (int j = t * per; j < min(len, (t + 1) * per); ++j) {
-    uint32_t& e = D[(j / vt) * tiles + (j % vt)];
-    const uint32_t v = e;
-    e = run;
-    run += v;
-  }
-  if (total && t == 1023) total[seg] = (int32_t)s[1023];
 }
 
 // Stable scatter of one 8-bit digit pass.
@@ -159,12 +126,17 @@ inline int radix_sort_pairs(uint32_t* keys, uint32_t* vals, uint32_t* ktmp, uint
                             int end_bit, hipStream_t s) {
   const int tiles = (int)cdiv(cap, kSortTile);
   if (nseg == 0 || tiles == 0) return PCST_OK;
+  if (256 * tiles > kSmallScanMax) {
+    set_error("radix_sort_pairs: segment capacity %lld exceeds %d", (long long)cap,
+              kSmallScanMax / 256 * kSortTile);
+    return PCST_EUNSUPPORTED;
+  }
   uint32_t *ki = keys, *vi = vals, *ko = ktmp, *vo = vtmp;
   for (int sh = begin_bit; sh < end_bit; sh += 8) {
     hipLaunchKernelGGL(radix_hist_kernel, dim3(tiles, nseg), dim3(kSortThreads), 0, s, ki, cap,
                        counts, sh, tiles, hist);
-    hipLaunchKernelGGL(seg_scan_kernel, dim3(nseg), dim3(1024), 0, s, hist, 256, tiles, counts,
-                       kSortTile, (int32_t*)nullptr);
+    // tiles past a segment's count hold zero histograms, so the whole table scans as one
+    seg_scan_small(hist, nseg, 256 * tiles, (int64_t)256 * tiles, nullptr, s);
     hipLaunchKernelGGL(radix_scatter_kernel, dim3(tiles, nseg), dim3(kSortThreads), 0, s, ki, vi,
                        ko, vo, cap, counts, sh, tiles, hist);
     uint32_t* t = ki; ki = ko; ko = t;

@@ -18,7 +18,7 @@
 namespace pcst {
 
 struct VoxelWS {
-  int32_t* mm;           // [B][6] ordered-int min xyz, max xyz
+  StatRec* mm;           // [B][kStatBlocks] partial min/max records
   uint32_t *kA, *vA, *kB, *vB;  // [B][N]
   uint32_t* hist;        // radix hist
   uint32_t* tileh;       // [B][tiles]
@@ -31,6 +31,7 @@ struct VoxelWS {
   uint32_t* isrep;       // [B][N]
   int32_t* pool;         // [B][N]
   int32_t* err;          // [1]
+  float4* vp;            // [B] min xyz + voxel size
   size_t bytes;
 };
 
@@ -39,7 +40,7 @@ static VoxelWS carve_voxel(void* base, int64_t B, int64_t N) {
   VoxelWS w;
   const size_t BN = (size_t)(B * N);
   const int64_t tiles = cdiv(N, kSortTile);
-  w.mm = c.take<int32_t>(B * 6);
+  w.mm = c.take<StatRec>(B * kStatBlocks);
   w.kA = c.take<uint32_t>(BN);
   w.vA = c.take<uint32_t>(BN);
   w.kB = c.take<uint32_t>(BN);
@@ -50,6 +51,7 @@ static VoxelWS carve_voxel(void* base, int64_t B, int64_t N) {
   w.P = c.take<int32_t>(B);
   w.cand = c.take<int32_t>(B);
   w.err = c.take<int32_t>(4);
+  w.vp = c.take<float4>(B);
   // zeroed every call: sum, cnt, isrep are contiguous so one memset covers them
   w.sum = c.take<unsigned long long>(BN);
   w.cnt = c.take<uint32_t>(BN);
@@ -63,11 +65,11 @@ static VoxelWS carve_voxel(void* base, int64_t B, int64_t N) {
 // voxel_size = (prod(range)/target)^(1/3) * 1.2 with the reference's fp32/fp64 steps
 // (diffusion_model.py:82-87): range < 1e-6 -> 1; prod = (r0*r1)*r2 in fp32; pow of the 0-d
 // fp32 tensor is evaluated in double (verified bit-exact), then * 1.2f; < 1e-6 -> 1e-3.
-__device__ __forceinline__ float voxel_size(const int32_t* M, int64_t target) {
+__device__ __forceinline__ float voxel_size(const StatRec& M, int64_t target) {
   float r[3];
 #pragma unroll
   for (int c = 0; c < 3; ++c) {
-    r[c] = fsub(ord2f(M[3 + c]), ord2f(M[c]));
+    r[c] = fsub(M.mx[c], M.mn[c]);
     if (r[c] < 1e-6f) r[c] = 1.0f;
   }
   const float prod = fmul(fmul(r[0], r[1]), r[2]);
@@ -78,6 +80,15 @@ __device__ __forceinline__ float voxel_size(const int32_t* M, int64_t target) {
   return vs;
 }
 
+// per cloud: fold the stat partials once -> (min x, min y, min z, voxel size)
+__global__ void vox_params_kernel(const StatRec* __restrict__ mm, int B, int64_t target,
+                                  float4* __restrict__ vp) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  const StatRec M = fold_stats(mm, b);
+  vp[b] = make_float4(M.mn[0], M.mn[1], M.mn[2], voxel_size(M, target));
+}
+
 __device__ __forceinline__ int32_t wrap_mul(int32_t a, uint32_t m) {
   return (int32_t)((uint32_t)a * m);
 }
@@ -85,13 +96,13 @@ __device__ __forceinline__ int32_t wrap_mul(int32_t a, uint32_t m) {
 // v = int32(floor((p - min) / vs)); h = (vx*73856093)^(vy*19349663)^(vz*83492791) (int32 wrap,
 // Q5).  Sort key = h ^ 0x80000000 so unsigned order == torch.unique's signed order.
 __global__ __launch_bounds__(256) void vox_hash_kernel(const float* __restrict__ pts, int N,
-                                                       int64_t target, const int32_t* __restrict__ mm,
+                                                       const float4* __restrict__ vp,
                                                        uint32_t* __restrict__ keys,
                                                        uint32_t* __restrict__ vals) {
   const int b = blockIdx.y;
-  const int32_t* M = mm + b * 6;
-  const float vs = voxel_size(M, target);
-  const float m0 = ord2f(M[0]), m1 = ord2f(M[1]), m2 = ord2f(M[2]);
+  const float4 v4 = vp[b];
+  const float vs = v4.w;
+  const float m0 = v4.x, m1 = v4.y, m2 = v4.z;
   const float* P = pts + (int64_t)b * N * 3;
   for (int n = blockIdx.x * 256 + threadIdx.x; n < N; n += gridDim.x * 256) {
     const int32_t vx = (int32_t)floorf(__fdiv_rn(fsub(P[n * 3 + 0], m0), vs));
@@ -338,24 +349,24 @@ extern "C" int pcst_voxel_stats(const float* pts, int64_t B, int64_t N, int64_t 
   const size_t zero_bytes = (size_t)((char*)w.reps - (char*)w.sum);
   PCST_HIP(hipMemsetAsync(w.sum, 0, zero_bytes, s), "voxel_stats: memset");
   PCST_HIP(hipMemsetAsync(w.err, 0, 16, s), "voxel_stats: memset");
-  launch_cloud_minmax(pts, b, n, w.mm, s);
-  hipLaunchKernelGGL(vox_hash_kernel, dim3(voxel_grid(N), b), dim3(256), 0, s, pts, n, target, w.mm,
+  launch_cloud_stats(pts, b, n, w.mm, s);
+  hipLaunchKernelGGL(vox_params_kernel, dim3((unsigned)cdiv(B, 64)), dim3(64), 0, s, w.mm, b,
+                     target, w.vp);
+  hipLaunchKernelGGL(vox_hash_kernel, dim3(voxel_grid(N), b), dim3(256), 0, s, pts, n, w.vp,
                      w.kA, w.vA);
   SegCounts all{nullptr, n};
   int rc = radix_sort_pairs(w.kA, w.vA, w.kB, w.vB, w.hist, b, N, all, 0, 32, s);
   if (rc) return rc;
   hipLaunchKernelGGL(vox_head_count_kernel, dim3(tiles, b), dim3(256), 0, s, w.kA, n, tiles,
                      w.tileh);
-  hipLaunchKernelGGL(seg_scan_kernel, dim3(b), dim3(1024), 0, s, w.tileh, 1, tiles, all,
-                     kSortTile, w.U);
+  seg_scan_small(w.tileh, b, tiles, tiles, w.U, s);
   hipLaunchKernelGGL(vox_segsum_kernel, dim3(tiles, b), dim3(256), 0, s, w.kA, w.vA, n, tiles,
                      w.tileh, w.sum, w.cnt);
   hipLaunchKernelGGL(vox_reps_kernel, dim3(voxel_grid(N), b), dim3(256), 0, s, w.sum, w.cnt, w.U,
                      n, w.reps, w.isrep);
   hipLaunchKernelGGL(vox_pool_count_kernel, dim3(tiles, b), dim3(256), 0, s, w.isrep, n, tiles,
                      w.tileh);
-  hipLaunchKernelGGL(seg_scan_kernel, dim3(b), dim3(1024), 0, s, w.tileh, 1, tiles, all,
-                     kSortTile, w.P);
+  seg_scan_small(w.tileh, b, tiles, tiles, w.P, s);
   hipLaunchKernelGGL(vox_pool_write_kernel, dim3(tiles, b), dim3(256), 0, s, w.isrep, n, tiles,
                      w.tileh, w.pool);
   hipLaunchKernelGGL(vox_cand_kernel, dim3(cdiv(B, 256)), dim3(256), 0, s, w.U, w.P, b, target,
