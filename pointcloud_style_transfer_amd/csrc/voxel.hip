@@ -326,13 +326,289 @@ __global__ void vox_select_kernel(const float* __restrict__ pts, int N, int64_t 
   }
 }
 
+// ============================================================================================
+// Performance path (device-drawn subset).  The step's result does not depend on the ORDER of
+// the kept indices (the noise MLP is per point and the upsample addresses rows by index), so
+// the sorts of the replay path are replaced by:
+//   open-addressing voxel table (int64 index sums / counts by integer atomics: exact)
+//   -> representatives (same values as the sorted path, arbitrary list order)
+//   -> random subset of the candidates (reps if U > T, pool if U < T) = the `need` smallest
+//      counter-based random keys (key of a rep = f(seed, voxel hash), of a pool point =
+//      f(seed, index): independent of list order, hence deterministic), found by a 12-bit
+//      radix select plus an exact sort of the boundary bin.
+constexpr int kSelBins = 4096;
+constexpr int kTieCap = 8192;
+
+struct VoxelFastWS {
+  StatRec* mm;
+  float4* vp;
+  int32_t* cnt4;          // [B][4]: U, selected, ties, err
+  int32_t* sel;           // [B][4]: bin*, rem, need, U>T flag
+  uint32_t* hist;         // [B][kSelBins]
+  unsigned long long* tkey;  // [B][H]  0 = empty, else (1<<32)|hash
+  unsigned long long* tsum;  // [B][H]
+  uint32_t* tcnt;         // [B][H]
+  uint32_t* isrep;        // [B][N]
+  int64_t* reps;          // [B][N]
+  uint32_t* rhash;        // [B][N]
+  unsigned long long* ties;  // [B][kTieCap] (key<<32 | id)
+  int64_t H;
+  size_t bytes;
+};
+
+static int64_t vox_table_size(int64_t N) {
+  int64_t h = 1024;
+  while (h < 2 * N) h <<= 1;
+  return h;
+}
+
+static VoxelFastWS carve_voxel_fast(void* base, int64_t B, int64_t N) {
+  Carver c(base);
+  VoxelFastWS w;
+  w.H = vox_table_size(N);
+  w.mm = c.take<StatRec>(B * kStatBlocks);
+  w.vp = c.take<float4>(B);
+  w.sel = c.take<int32_t>(B * 4);
+  w.reps = c.take<int64_t>(B * N);
+  w.rhash = c.take<uint32_t>(B * N);
+  w.ties = c.take<unsigned long long>(B * kTieCap);
+  // zeroed every call (one memset): counters, histogram, table, rep flags
+  w.cnt4 = c.take<int32_t>(B * 4);
+  w.hist = c.take<uint32_t>(B * kSelBins);
+  w.tkey = c.take<unsigned long long>(B * w.H);
+  w.tsum = c.take<unsigned long long>(B * w.H);
+  w.tcnt = c.take<uint32_t>(B * w.H);
+  w.isrep = c.take<uint32_t>(B * N);
+  w.bytes = c.bytes();
+  return w;
+}
+
+__device__ __forceinline__ uint32_t mix32(uint32_t x) {
+  x ^= x >> 16; x *= 0x7feb352dU; x ^= x >> 15; x *= 0x846ca68bU; x ^= x >> 16;
+  return x;
+}
+
+__global__ __launch_bounds__(256) void voxf_insert_kernel(const float* __restrict__ pts, int N,
+                                                          const float4* __restrict__ vp, int64_t H,
+                                                          unsigned long long* __restrict__ tkey,
+                                                          unsigned long long* __restrict__ tsum,
+                                                          uint32_t* __restrict__ tcnt) {
+  const int b = blockIdx.y;
+  const float4 v4 = vp[b];
+  const float* P = pts + (int64_t)b * N * 3;
+  unsigned long long* K = tkey + b * H;
+  for (int n = blockIdx.x * 256 + threadIdx.x; n < N; n += gridDim.x * 256) {
+    const int32_t vx = (int32_t)floorf(__fdiv_rn(fsub(P[n * 3 + 0], v4.x), v4.w));
+    const int32_t vy = (int32_t)floorf(__fdiv_rn(fsub(P[n * 3 + 1], v4.y), v4.w));
+    const int32_t vz = (int32_t)floorf(__fdiv_rn(fsub(P[n * 3 + 2], v4.z), v4.w));
+    const uint32_t h = (uint32_t)(wrap_mul(vx, 73856093u) ^ wrap_mul(vy, 19349663u) ^
+                                  wrap_mul(vz, 83492791u));
+    const unsigned long long kw = (1ull << 32) | h;
+    int64_t slot = mix32(h) & (H - 1);
+    for (;;) {
+      const unsigned long long old = atomicCAS(&K[slot], 0ull, kw);
+      if (old == 0ull || old == kw) break;
+      slot = (slot + 1) & (H - 1);
+    }
+    atomicAdd(&tsum[b * H + slot], (unsigned long long)n);
+    atomicAdd(&tcnt[b * H + slot], 1u);
+  }
+}
+
+// occupied slot -> representative trunc(f32(sum)/f32(count)) (Q6); list order = arrival order
+__global__ __launch_bounds__(256) void voxf_reps_kernel(const unsigned long long* __restrict__ tkey,
+                                                        const unsigned long long* __restrict__ tsum,
+                                                        const uint32_t* __restrict__ tcnt, int64_t H,
+                                                        int N, int64_t T, int32_t* __restrict__ cnt4,
+                                                        int64_t* __restrict__ reps,
+                                                        uint32_t* __restrict__ rhash,
+                                                        uint32_t* __restrict__ isrep,
+                                                        int64_t* __restrict__ out_idx) {
+  const int b = blockIdx.y;
+  for (int64_t s = blockIdx.x * 256 + threadIdx.x; s < H; s += (int64_t)gridDim.x * 256) {
+    const unsigned long long kw = tkey[b * H + s];
+    if (!kw) continue;
+    const float fs = (float)(long long)tsum[b * H + s];
+    const float fc = (float)tcnt[b * H + s];
+    const int64_t r = (int64_t)__fdiv_rn(fs, fc);
+    const int k = atomicAdd(&cnt4[b * 4 + 0], 1);
+    reps[(int64_t)b * N + k] = r;
+    rhash[(int64_t)b * N + k] = (uint32_t)kw;
+    isrep[(int64_t)b * N + r] = 1u;
+    if (k < T) out_idx[b * T + k] = r;  // the U <= T case keeps every rep
+  }
+}
+
+// candidate e of cloud b: (key, id); returns false if e is not a candidate
+__device__ __forceinline__ bool voxf_cand(int b, int e, int N, int U, int64_t T, uint64_t seed,
+                                          const uint32_t* __restrict__ rhash,
+                                          const uint32_t* __restrict__ isrep, uint32_t& key,
+                                          uint32_t& id) {
+  if (U > T) {
+    if (e >= U) return false;
+    id = (uint32_t)e;
+    key = rand_key(seed, b, (int)(rhash[(int64_t)b * N + e] & 0x7fffffff));
+    return true;
+  }
+  if (U == T || e >= N || isrep[(int64_t)b * N + e]) return false;
+  id = (uint32_t)e;
+  key = rand_key(seed, b + 0x10000, e);
+  return true;
+}
+
+__global__ __launch_bounds__(256) void voxf_hist_kernel(int N, int64_t T, uint64_t seed,
+                                                        const int32_t* __restrict__ cnt4,
+                                                        const uint32_t* __restrict__ rhash,
+                                                        const uint32_t* __restrict__ isrep,
+                                                        uint32_t* __restrict__ hist) {
+  const int b = blockIdx.y;
+  const int U = cnt4[b * 4];
+  __shared__ uint32_t h[kSelBins];
+  for (int i = threadIdx.x; i < kSelBins; i += 256) h[i] = 0;
+  __syncthreads();
+  for (int e = blockIdx.x * 256 + threadIdx.x; e < N; e += gridDim.x * 256) {
+    uint32_t key, id;
+    if (voxf_cand(b, e, N, U, T, seed, rhash, isrep, key, id)) atomicAdd(&h[key >> 20], 1u);
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < kSelBins; i += 256)
+    if (h[i]) atomicAdd(&hist[b * kSelBins + i], h[i]);
+}
+
+// per cloud: the boundary bin b* and how many of it are still needed
+__global__ __launch_bounds__(256) void voxf_find_kernel(const uint32_t* __restrict__ hist,
+                                                        const int32_t* __restrict__ cnt4, int N,
+                                                        int64_t T, int32_t* __restrict__ sel) {
+  const int b = blockIdx.x;
+  const int U = cnt4[b * 4];
+  const int need = U > T ? (int)T : (U < T ? (int)(T - U) : 0);
+  __shared__ uint32_t sh[260];
+  const int per = kSelBins / 256;
+  uint32_t v[kSelBins / 256], s = 0;
+  for (int k = 0; k < per; ++k) {
+    v[k] = hist[b * kSelBins + threadIdx.x * per + k];
+    s += v[k];
+  }
+  uint32_t tot;
+  uint32_t run = block_excl_scan_256(s, sh, tot);
+  for (int k = 0; k < per; ++k) {
+    if (need > 0 && run < (uint32_t)need && run + v[k] >= (uint32_t)need) {
+      sel[b * 4 + 0] = threadIdx.x * per + k;
+      sel[b * 4 + 1] = need - (int)run;
+    }
+    run += v[k];
+  }
+  if (threadIdx.x == 0) {
+    sel[b * 4 + 2] = need;
+    sel[b * 4 + 3] = U > T ? 1 : 0;
+    if (need == 0) { sel[b * 4 + 0] = -1; sel[b * 4 + 1] = 0; }
+  }
+}
+
+__device__ __forceinline__ void voxf_emit(int b, int N, int64_t T, int U, int pos, uint32_t id,
+                                          const int64_t* __restrict__ reps,
+                                          int64_t* __restrict__ out_idx) {
+  const int64_t r = U > T ? reps[(int64_t)b * N + id] : (int64_t)id;
+  const int64_t j = U > T ? pos : U + pos;
+  out_idx[b * T + j] = r;
+}
+
+__global__ __launch_bounds__(256) void voxf_select_kernel(int N, int64_t T, uint64_t seed,
+                                                          const int32_t* __restrict__ sel,
+                                                          int32_t* __restrict__ cnt4,
+                                                          const uint32_t* __restrict__ rhash,
+                                                          const uint32_t* __restrict__ isrep,
+                                                          const int64_t* __restrict__ reps,
+                                                          unsigned long long* __restrict__ ties,
+                                                          int64_t* __restrict__ out_idx) {
+  const int b = blockIdx.y;
+  const int bstar = sel[b * 4 + 0];
+  if (bstar < 0) return;
+  const int U = cnt4[b * 4];
+  for (int e = blockIdx.x * 256 + threadIdx.x; e < N; e += gridDim.x * 256) {
+    uint32_t key, id;
+    if (!voxf_cand(b, e, N, U, T, seed, rhash, isrep, key, id)) continue;
+    const int bin = (int)(key >> 20);
+    if (bin < bstar) {
+      const int pos = atomicAdd(&cnt4[b * 4 + 1], 1);
+      voxf_emit(b, N, T, U, pos, id, reps, out_idx);
+    } else if (bin == bstar) {
+      const int t = atomicAdd(&cnt4[b * 4 + 2], 1);
+      if (t < kTieCap) ties[(int64_t)b * kTieCap + t] = ((unsigned long long)key << 32) | id;
+      else atomicOr(&cnt4[b * 4 + 3], 1);
+    }
+  }
+}
+
+// boundary bin: exact order by (key, id), keep the first `rem` (one workgroup per cloud)
+__global__ __launch_bounds__(1024) void voxf_ties_kernel(int N, int64_t T,
+                                                         const int32_t* __restrict__ sel,
+                                                         const int32_t* __restrict__ cnt4,
+                                                         const unsigned long long* __restrict__ ties,
+                                                         const int64_t* __restrict__ reps,
+                                                         int64_t* __restrict__ out_idx) {
+  const int b = blockIdx.x;
+  if (sel[b * 4 + 0] < 0) return;
+  const int rem = sel[b * 4 + 1];
+  const int U = cnt4[b * 4];
+  const int nt = min(cnt4[b * 4 + 2], kTieCap);
+  const int base = cnt4[b * 4 + 1];  // entries below the boundary bin
+  const unsigned long long* Tb = ties + (int64_t)b * kTieCap;
+  for (int i = threadIdx.x; i < nt; i += 1024) {
+    const unsigned long long v = Tb[i];
+    int rank = 0;
+    for (int k = 0; k < nt; ++k) rank += Tb[k] < v;
+    if (rank < rem) voxf_emit(b, N, T, U, base + rank, (uint32_t)v, reps, out_idx);
+  }
+}
+
+__global__ void voxf_gather_kernel(const float* __restrict__ pts, int N, int64_t T,
+                                   const int64_t* __restrict__ out_idx, float* __restrict__ out_pts) {
+  const int b = blockIdx.y;
+  for (int64_t j = blockIdx.x * 256 + threadIdx.x; j < T; j += gridDim.x * 256) {
+    const int64_t r = out_idx[b * T + j];
+    const float* src = pts + ((int64_t)b * N + r) * 3;
+    float* dst = out_pts + (b * T + j) * 3;
+    dst[0] = src[0]; dst[1] = src[1]; dst[2] = src[2];
+  }
+}
+
+static int voxel_fast(const float* pts, int64_t B, int64_t N, int64_t T, void* workspace,
+                      uint64_t seed, int64_t* out_idx, float* out_pts, hipStream_t s) {
+  VoxelFastWS w = carve_voxel_fast(workspace, B, N);
+  const int b = (int)B, n = (int)N;
+  const size_t zero = (size_t)((char*)w.isrep - (char*)w.cnt4) + sizeof(uint32_t) * B * N;
+  PCST_HIP(hipMemsetAsync(w.cnt4, 0, zero, s), "voxel: memset");
+  launch_cloud_stats(pts, b, n, w.mm, s);
+  hipLaunchKernelGGL(vox_params_kernel, dim3((unsigned)cdiv(B, 64)), dim3(64), 0, s, w.mm, b, T,
+                     w.vp);
+  const unsigned gp = (unsigned)std::min<int64_t>(cdiv(N, 256), 1024);
+  hipLaunchKernelGGL(voxf_insert_kernel, dim3(gp, b), dim3(256), 0, s, pts, n, w.vp, w.H, w.tkey,
+                     w.tsum, w.tcnt);
+  hipLaunchKernelGGL(voxf_reps_kernel, dim3((unsigned)std::min<int64_t>(cdiv(w.H, 256), 2048), b),
+                     dim3(256), 0, s, w.tkey, w.tsum, w.tcnt, w.H, n, T, w.cnt4, w.reps, w.rhash,
+                     w.isrep, out_idx);
+  const unsigned gs = (unsigned)std::min<int64_t>(cdiv(N, 256), 256);
+  hipLaunchKernelGGL(voxf_hist_kernel, dim3(gs, b), dim3(256), 0, s, n, T, seed, w.cnt4, w.rhash,
+                     w.isrep, w.hist);
+  hipLaunchKernelGGL(voxf_find_kernel, dim3(b), dim3(256), 0, s, w.hist, w.cnt4, n, T, w.sel);
+  hipLaunchKernelGGL(voxf_select_kernel, dim3(gs, b), dim3(256), 0, s, n, T, seed, w.sel, w.cnt4,
+                     w.rhash, w.isrep, w.reps, w.ties, out_idx);
+  hipLaunchKernelGGL(voxf_ties_kernel, dim3(b), dim3(1024), 0, s, n, T, w.sel, w.cnt4, w.ties,
+                     w.reps, out_idx);
+  hipLaunchKernelGGL(voxf_gather_kernel, dim3((unsigned)std::min<int64_t>(cdiv(T, 256), 1024), b),
+                     dim3(256), 0, s, pts, n, T, out_idx, out_pts);
+  PCST_LAUNCH_CHECK("voxel_downsample");
+  return PCST_OK;
+}
+
 }  // namespace pcst
 
 using namespace pcst;
 
 extern "C" int pcst_voxel_workspace_size(int64_t B, int64_t N, size_t* bytes) {
   PCST_CHECK_ARG(B >= 0 && N >= 0 && bytes, "voxel_workspace_size: bad args");
-  *bytes = carve_voxel(nullptr, B, N).bytes;
+  *bytes = std::max(carve_voxel(nullptr, B, N).bytes, carve_voxel_fast(nullptr, B, N).bytes);
   return PCST_OK;
 }
 
@@ -416,8 +692,7 @@ extern "C" int pcst_voxel_error(void* workspace, int64_t B, int64_t N, int32_t* 
 extern "C" int pcst_voxel_downsample(const float* pts, int64_t B, int64_t N, int64_t target,
                                      void* workspace, uint64_t seed, int64_t* out_idx,
                                      float* out_pts, void* stream) {
-  int rc = pcst_voxel_stats(pts, B, N, target, workspace, nullptr, stream);
-  if (rc) return rc;
-  return pcst_voxel_select(pts, B, N, target, workspace, nullptr, nullptr, nullptr, seed, out_idx,
-                           out_pts, stream);
+  PCST_CHECK_ARG(B > 0 && N > target && target > 0 && N < (1ll << 30), "voxel_downsample: bad shape");
+  PCST_CHECK_ARG(pts && workspace && out_idx && out_pts, "voxel_downsample: null pointer");
+  return voxel_fast(pts, B, N, target, workspace, seed, out_idx, out_pts, as_stream(stream));
 }

@@ -79,18 +79,27 @@ def test_voxel_vs_oracle_random_perm(H, N, T, B, sig):
     _, idx = H.voxel_downsample(dev(pts), T, perm_provider=provider_from(perms))
     _, ref = O.voxel_downsample(pts, T, O.Replay([("randperm", p) for p in perms]))
     np.testing.assert_array_equal(idx.cpu().numpy(), ref)
-    # device-drawn subset: reps are always kept (pad branch) and the rest comes from the pool
-    _, idx2 = H.voxel_downsample(dev(pts), T, seed=1234)
+    # device-drawn subset (perf path: order-free): the reps multiset is exact, every rep is
+    # kept in the pad branch and the rest is a duplicate-free draw from the pool
+    pts_d, idx2 = H.voxel_downsample(dev(pts), T, seed=1234)
     idx2 = idx2.cpu().numpy()
+    np.testing.assert_array_equal(pts_d.cpu().numpy(), np.stack([pts[b][idx2[b]] for b in range(B)]))
+    _, idx3 = H.voxel_downsample(dev(pts), T, seed=1234)
+    np.testing.assert_array_equal(np.sort(idx2, 1), np.sort(idx3.cpu().numpy(), 1))  # deterministic set
     for b in range(B):
         reps, _, _ = O.voxel_reps(pts[b], T)
-        if len(reps) < T:
-            np.testing.assert_array_equal(idx2[b][:len(reps)], reps)
-            extra = idx2[b][len(reps):]
+        U = len(reps)
+        if U < T:
+            np.testing.assert_array_equal(np.sort(idx2[b][:U]), np.sort(reps))
+            extra = idx2[b][U:]
             assert len(np.unique(extra)) == len(extra)
             assert not np.isin(extra, reps).any()
         else:
             assert np.isin(idx2[b], reps).all()
+            # T distinct list positions: the kept multiset is a sub-multiset of reps
+            vals, cnt = np.unique(idx2[b], return_counts=True)
+            rv, rc = np.unique(reps, return_counts=True)
+            assert (cnt <= rc[np.searchsorted(rv, vals)]).all()
 
 
 def test_knn_golden(H, golden):
