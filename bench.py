@@ -161,7 +161,7 @@ def main():
             if timed:
                 e0 = torch.cuda.Event(enable_timing=True)
                 e1 = torch.cuda.Event(enable_timing=True)
-                blob, bias, _ = npred.packed()
+                blob, bias = npred.packed()[:2]
                 cnd = npred.cond(t_in, style_in)
                 e0.record()
                 nc = _hip.noise_mlp(xc.reshape(-1, 3), cfg.global_points, cnd, blob, bias,

@@ -121,7 +121,8 @@ int pcst_knn_error(void* workspace, int64_t B, int64_t N, int64_t M, int32_t* er
  * (parity), 1 = bf16 MFMA with fp32 accumulation and fp32 residual stream.  blob/bias are the
  * packed weights of packing.py (blob 16-byte aligned, pcst_noise_mlp_blob_bytes() bytes).
  * pcst_noise_cond computes cond[c] = b4 + time_proj(TimeEmbedding(t_c)) + style_proj(style_c)
- * (freqs = the reference's 64-entry exp table).  pts [P,3] cloud-major with
+ * (freqs = the reference's 64-entry exp table; wt = time_proj.weight^T [128,256] and
+ * ws = style_proj.weight^T [256,256], transposed for coalesced reads).  pts [P,3] cloud-major with
  * points_per_cloud points per cloud; out [P,3]. */
 int64_t pcst_noise_mlp_blob_bytes(int precision);
 int pcst_noise_cond(const int64_t* t, const float* style, int64_t nclouds, const float* freqs,

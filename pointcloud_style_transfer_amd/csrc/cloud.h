@@ -78,6 +78,26 @@ __device__ __forceinline__ StatRec fold_stats(const StatRec* __restrict__ part, 
   return r;
 }
 
+// Same fold by one 64-lane wave (lane q reads partial q, butterfly combine): call from all
+// lanes of a wave; every lane returns the result.  (Float min/max are order-free; the float64
+// sums are combined in a fixed butterfly order, so the result is deterministic.)
+__device__ __forceinline__ StatRec fold_stats_wave(const StatRec* __restrict__ part, int b) {
+  static_assert(kStatBlocks == 64, "one partial per lane");
+  const int lane = threadIdx.x & 63;
+  StatRec r = part[b * kStatBlocks + lane];
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) {
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      r.mn[c] = fminf(r.mn[c], __shfl_xor(r.mn[c], off));
+      r.mx[c] = fmaxf(r.mx[c], __shfl_xor(r.mx[c], off));
+      r.s[c] += __shfl_xor(r.s[c], off);
+      r.ss[c] += __shfl_xor(r.ss[c], off);
+    }
+  }
+  return r;
+}
+
 inline void launch_cloud_stats(const float* pts, int B, int N, StatRec* part, hipStream_t s) {
   hipLaunchKernelGGL(cloud_stats_partial_kernel, dim3(kStatBlocks, B), dim3(256), 0, s, pts, N,
                      part);

@@ -19,23 +19,28 @@
 
 namespace pcst {
 
+constexpr int kRingMax = 3;  // shells searched per query before the exhaustive outlier pass
+
 struct KnnWS {
   StatRec* stats;    // [B][kStatBlocks]
   float* gp;         // [B][8]: origin xyz, cell size, inv size, dims xyz (int bits)
-  int32_t* err;
-  uint32_t* known;   // [B][N]  (j+1 of the last coarse row writing n, 0 = query)
-  uint32_t* rstart;  // [B][C+1] ref counts -> starts
-  uint32_t* rcur;    // [B][C]   fill cursors
-  uint32_t* qstart;  // [B][C+1] query counts -> starts
-  uint32_t* qcur;    // [B][C]
   uint32_t* tsum;    // scan scratch
   float4* refs;      // [B][M]   (x, y, z, j) cell-sorted
   int32_t* qorder;   // [B][N]   point index in cell order
+  int32_t* olist;    // [B][N]   queries left to the exhaustive pass
+  // zeroed every call (contiguous):
+  int32_t* err;
+  int32_t* ocount;   // [B]
+  uint32_t* known;   // [B][N]  (j+1 of the last coarse row writing n, 0 = query)
+  uint32_t* rstart;  // [B][C+1] ref counts -> starts
+  uint32_t* qstart;  // [B][C+1] query counts -> starts
+  uint32_t* rcur;    // [B][C]   fill cursors (offsets from the starts)
+  uint32_t* qcur;    // [B][C]
   int64_t C;
   size_t bytes;
 };
 
-static int64_t knn_cells(int64_t M) { return std::max<int64_t>(4096, 24 * M); }
+static int64_t knn_cells(int64_t M) { return std::max<int64_t>(4096, 16 * M); }
 
 static KnnWS carve_knn(void* base, int64_t B, int64_t N, int64_t M) {
   Carver c(base);
@@ -43,15 +48,17 @@ static KnnWS carve_knn(void* base, int64_t B, int64_t N, int64_t M) {
   w.C = knn_cells(M);
   w.stats = c.take<StatRec>(B * kStatBlocks);
   w.gp = c.take<float>(B * 8);
+  w.tsum = c.take<uint32_t>(scan_tsum_words((int)B, w.C + 1));
+  w.refs = c.take<float4>(B * M);
+  w.qorder = c.take<int32_t>(B * N);
+  w.olist = c.take<int32_t>(B * N);
   w.err = c.take<int32_t>(4);
+  w.ocount = c.take<int32_t>(B);
   w.known = c.take<uint32_t>(B * N);
   w.rstart = c.take<uint32_t>(B * (w.C + 1));
   w.qstart = c.take<uint32_t>(B * (w.C + 1));
   w.rcur = c.take<uint32_t>(B * w.C);
   w.qcur = c.take<uint32_t>(B * w.C);
-  w.tsum = c.take<uint32_t>(scan_tsum_words((int)B, w.C + 1));
-  w.refs = c.take<float4>(B * M);
-  w.qorder = c.take<int32_t>(B * N);
   w.bytes = c.bytes();
   return w;
 }
@@ -59,11 +66,12 @@ static KnnWS carve_knn(void* base, int64_t B, int64_t N, int64_t M) {
 // Cell size from the peak density of a Gaussian with the cloud's per-axis spread:
 // rho_max = M / ((2 pi)^1.5 sx sy sz); s^3 = 3 / rho_max.  Capped so the bounding box holds
 // at most C cells (and at most 2048 per axis).
-__global__ void knn_grid_params_kernel(const StatRec* __restrict__ stats, int B, int64_t N,
-                                       int64_t M, int64_t C, float* __restrict__ gp) {
-  const int b = blockIdx.x * blockDim.x + threadIdx.x;
-  if (b >= B) return;
-  const StatRec r = fold_stats(stats, b);
+__global__ __launch_bounds__(64) void knn_grid_params_kernel(const StatRec* __restrict__ stats,
+                                                             int B, int64_t N, int64_t M, int64_t C,
+                                                             float* __restrict__ gp) {
+  const int b = blockIdx.x;  // one wave per cloud
+  const StatRec r = fold_stats_wave(stats, b);
+  if (threadIdx.x != 0) return;
   double ext[3], sig[3];
   for (int c = 0; c < 3; ++c) {
     ext[c] = (double)r.mx[c] - (double)r.mn[c];
@@ -74,7 +82,7 @@ __global__ void knn_grid_params_kernel(const StatRec* __restrict__ stats, int B,
     sig[c] = fmax(sig[c], 1e-3 * ext[c]);
   }
   const double rho = (double)M / (15.7496099457 * sig[0] * sig[1] * sig[2]);
-  double s = cbrt(3.0 / rho);
+  double s = cbrt(4.0 / rho);
   // a cell must not be smaller than a thin dimension forces: keep at least ~1 ref per
   // cell on average over the occupied extent
   int d[3];
@@ -136,8 +144,10 @@ __global__ void knn_count_kernel(const float* __restrict__ orig, const int64_t* 
 
 __global__ void knn_fill_kernel(const float* __restrict__ orig, const int64_t* __restrict__ idx,
                                 int64_t N, int64_t M, int64_t C, const float* __restrict__ gp,
-                                uint32_t* __restrict__ rcur, uint32_t* __restrict__ qcur,
-                                float4* __restrict__ refs, int32_t* __restrict__ qorder) {
+                                const uint32_t* __restrict__ rstart,
+                                const uint32_t* __restrict__ qstart, uint32_t* __restrict__ rcur,
+                                uint32_t* __restrict__ qcur, float4* __restrict__ refs,
+                                int32_t* __restrict__ qorder) {
   const int b = blockIdx.y;
   const float* G = gp + b * 8;
   for (int64_t e = blockIdx.x * 256 + threadIdx.x; e < M + N; e += gridDim.x * 256) {
@@ -145,11 +155,13 @@ __global__ void knn_fill_kernel(const float* __restrict__ orig, const int64_t* _
       int64_t n = idx[b * M + e];
       n = n < 0 ? 0 : (n >= N ? N - 1 : n);
       const float* p = orig + (b * N + n) * 3;
-      const uint32_t pos = atomicAdd(&rcur[b * C + cell_of(p, G)], 1u);
+      const int64_t c = cell_of(p, G);
+      const uint32_t pos = rstart[b * (C + 1) + c] + atomicAdd(&rcur[b * C + c], 1u);
       refs[b * M + pos] = make_float4(p[0], p[1], p[2], __int_as_float((int)e));
     } else {
       const int64_t n = e - M;
-      const uint32_t pos = atomicAdd(&qcur[b * C + cell_of(orig + (b * N + n) * 3, G)], 1u);
+      const int64_t c = cell_of(orig + (b * N + n) * 3, G);
+      const uint32_t pos = qstart[b * (C + 1) + c] + atomicAdd(&qcur[b * C + c], 1u);
       qorder[b * N + pos] = (int32_t)n;
     }
   }
@@ -178,11 +190,31 @@ struct Top3 {
   }
 };
 
+// IDW of the reference (float64, sequential sums), rounded to float32
+__device__ __forceinline__ void idw_write(const Top3& t, int kk, const float* __restrict__ V,
+                                          float* __restrict__ O) {
+  double w[3], wsum = 0.0;
+  for (int i = 0; i < kk; ++i) {
+    w[i] = __ddiv_rn(1.0, dadd(__dsqrt_rn(t.d[i]), 1e-8));
+    wsum = i == 0 ? w[0] : dadd(wsum, w[i]);
+  }
+  for (int i = 0; i < kk; ++i) w[i] = __ddiv_rn(w[i], wsum);
+  for (int c = 0; c < 3; ++c) {
+    double acc = 0.0;
+    for (int i = 0; i < kk; ++i) {
+      const double term = dmul((double)V[(int64_t)t.j[i] * 3 + c], w[i]);
+      acc = i == 0 ? term : dadd(acc, term);
+    }
+    O[c] = (float)acc;
+  }
+}
+
 __global__ __launch_bounds__(256) void knn_query_kernel(
     const float* __restrict__ orig, const float* __restrict__ vals, int64_t N, int64_t M,
     int64_t C, const float* __restrict__ gp, const uint32_t* __restrict__ known,
     const uint32_t* __restrict__ rstart, const float4* __restrict__ refs,
-    const int32_t* __restrict__ qorder, float* __restrict__ out) {
+    const int32_t* __restrict__ qorder, int32_t* __restrict__ olist, int32_t* __restrict__ ocount,
+    float* __restrict__ out) {
   const int b = blockIdx.y;
   const int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (k >= N) return;
@@ -210,7 +242,9 @@ __global__ __launch_bounds__(256) void knn_query_kernel(
   Top3 t;
   t.init();
   float thr = INFINITY;  // fp32 screen: candidates above it cannot enter the top k
-  const int rmax = max(dx, max(dy, dz));
+  const int rall = max(dx, max(dy, dz));
+  const int rmax = min(rall, kRingMax);
+  bool done = false;
   for (int r = 0; r <= rmax; ++r) {
     const int z0 = max(cz - r, 0), z1 = min(cz + r, dz - 1);
     const int y0 = max(cy - r, 0), y1 = min(cy + r, dy - 1);
@@ -246,21 +280,57 @@ __global__ __launch_bounds__(256) void knn_query_kernel(
     if (cz - r > 0) bound = fmin(bound, qz - (oz + (cz - r) * s));
     if (cz + r + 1 < dz) bound = fmin(bound, (oz + (cz + r + 1) * s) - qz);
     bound -= slack;
-    if (bound == INFINITY || (bound > 0 && t.d[kk - 1] < bound * bound)) break;
-  }
-  double w[3], wsum = 0.0;
-  for (int i = 0; i < kk; ++i) {
-    w[i] = __ddiv_rn(1.0, dadd(__dsqrt_rn(t.d[i]), 1e-8));
-    wsum = i == 0 ? w[0] : dadd(wsum, w[i]);
-  }
-  for (int i = 0; i < kk; ++i) w[i] = __ddiv_rn(w[i], wsum);
-  for (int c = 0; c < 3; ++c) {
-    double acc = 0.0;
-    for (int i = 0; i < kk; ++i) {
-      const double term = dmul((double)V[(int64_t)t.j[i] * 3 + c], w[i]);
-      acc = i == 0 ? term : dadd(acc, term);
+    if (bound == INFINITY || (bound > 0 && t.d[kk - 1] < bound * bound)) {
+      done = true;
+      break;
     }
-    O[c] = (float)acc;
+  }
+  if (!done) {  // sparse neighbourhood: leave it to the exhaustive wave-per-query pass
+    olist[b * N + atomicAdd(&ocount[b], 1)] = (int32_t)n;
+    return;
+  }
+  idw_write(t, kk, V, O);
+}
+
+// Exhaustive 3-NN for the queries the shell search left: one wave per query, each lane scans
+// M/64 refs with its own top-3, then a butterfly merge (lexicographic (d, j): deterministic).
+__global__ __launch_bounds__(256) void knn_outlier_kernel(
+    const float* __restrict__ orig, const float* __restrict__ vals, int64_t N, int64_t M,
+    const float4* __restrict__ refs, const int32_t* __restrict__ olist,
+    const int32_t* __restrict__ ocount, float* __restrict__ out) {
+  const int b = blockIdx.y;
+  const int lane = threadIdx.x & 63;
+  const int wg = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int cnt = ocount[b];
+  const float4* R = refs + b * M;
+  const float* V = vals + b * M * 3;
+  const int kk = M < 3 ? (int)M : 3;
+  for (int q = wg; q < cnt; q += gridDim.x * 4) {
+    const int64_t n = olist[b * N + q];
+    const float* p = orig + (b * N + n) * 3;
+    const float fx = p[0], fy = p[1], fz = p[2];
+    const double qx = fx, qy = fy, qz = fz;
+    Top3 t;
+    t.init();
+    float thr = INFINITY;
+    for (int64_t i = lane; i < M; i += 64) {
+      const float4 ref = R[i];
+      const float ex = fx - ref.x, ey = fy - ref.y, ez = fz - ref.z;
+      const float d32 = fmaf(ez, ez, fmaf(ey, ey, ex * ex));
+      if (d32 > thr) continue;
+      const double ux = dsub(qx, (double)ref.x), uy = dsub(qy, (double)ref.y),
+                   uz = dsub(qz, (double)ref.z);
+      t.push(dadd(dadd(dmul(ux, ux), dmul(uy, uy)), dmul(uz, uz)), __float_as_int(ref.w));
+      if (t.d[kk - 1] != INFINITY) thr = (float)(t.d[kk - 1] * (1.0 + 2e-6)) + 1e-30f;
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+      double od[3];
+      int oj[3];
+      for (int k = 0; k < 3; ++k) { od[k] = __shfl_xor(t.d[k], off); oj[k] = __shfl_xor(t.j[k], off); }
+      for (int k = 0; k < 3; ++k) t.push(od[k], oj[k]);
+    }
+    if (lane == 0) idw_write(t, kk, V, out + (b * N + n) * 3);
   }
 }
 
@@ -285,11 +355,12 @@ extern "C" int pcst_knn3_interp(const float* coarse, const float* orig, const in
   KnnWS w = carve_knn(workspace, B, N, M);
   const int b = (int)B;
   const int64_t C = w.C;
-  // known + both count arrays are contiguous in the carve: one memset
-  PCST_HIP(hipMemsetAsync(w.err, 0, (size_t)((char*)w.rcur - (char*)w.err), s), "knn: memset");
+  // counters, known flags, count and cursor arrays are contiguous in the carve: one memset
+  PCST_HIP(hipMemsetAsync(w.err, 0, (size_t)(w.bytes - ((char*)w.err - (char*)workspace)), s),
+           "knn: memset");
   launch_cloud_stats(orig, b, (int)N, w.stats, s);
-  hipLaunchKernelGGL(knn_grid_params_kernel, dim3((unsigned)cdiv(B, 64)), dim3(64), 0, s, w.stats,
-                     b, N, M, C, w.gp);
+  hipLaunchKernelGGL(knn_grid_params_kernel, dim3((unsigned)B), dim3(64), 0, s, w.stats, b, N, M,
+                     C, w.gp);
   const unsigned gm = (unsigned)std::min<int64_t>(cdiv(M, 256), 1024);
   hipLaunchKernelGGL(knn_known_kernel, dim3(gm, b), dim3(256), 0, s, idx, N, M, w.known, w.err);
   const unsigned ga = (unsigned)std::min<int64_t>(cdiv(M + N, 256), 2048);
@@ -297,14 +368,13 @@ extern "C" int pcst_knn3_interp(const float* coarse, const float* orig, const in
                      w.rstart, w.qstart);
   seg_scan_long(w.rstart, b, C + 1, C + 1, w.tsum, nullptr, s);
   seg_scan_long(w.qstart, b, C + 1, C + 1, w.tsum, nullptr, s);
-  PCST_HIP(hipMemcpy2DAsync(w.rcur, sizeof(uint32_t) * C, w.rstart, sizeof(uint32_t) * (C + 1),
-                            sizeof(uint32_t) * C, B, hipMemcpyDeviceToDevice, s), "knn: cursors");
-  PCST_HIP(hipMemcpy2DAsync(w.qcur, sizeof(uint32_t) * C, w.qstart, sizeof(uint32_t) * (C + 1),
-                            sizeof(uint32_t) * C, B, hipMemcpyDeviceToDevice, s), "knn: cursors");
   hipLaunchKernelGGL(knn_fill_kernel, dim3(ga, b), dim3(256), 0, s, orig, idx, N, M, C, w.gp,
-                     w.rcur, w.qcur, w.refs, w.qorder);
+                     w.rstart, w.qstart, w.rcur, w.qcur, w.refs, w.qorder);
   hipLaunchKernelGGL(knn_query_kernel, dim3((unsigned)cdiv(N, 256), b), dim3(256), 0, s, orig,
-                     coarse, N, M, C, w.gp, w.known, w.rstart, w.refs, w.qorder, out);
+                     coarse, N, M, C, w.gp, w.known, w.rstart, w.refs, w.qorder, w.olist, w.ocount,
+                     out);
+  hipLaunchKernelGGL(knn_outlier_kernel, dim3(256, b), dim3(256), 0, s, orig, coarse, N, M, w.refs,
+                     w.olist, w.ocount, out);
   PCST_LAUNCH_CHECK("knn3_interp");
   return PCST_OK;
 }

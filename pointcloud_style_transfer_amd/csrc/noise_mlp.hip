@@ -305,10 +305,11 @@ __global__ __launch_bounds__(256) void cond_bias_kernel(
   else if (o < 128) emb[o] = cosf(tf * freqs[o - 64]);
   sty[o] = style[c * 256 + o];
   __syncthreads();
+  // wt / ws are the TRANSPOSED weights ([in][out]): lane o reads consecutive addresses
   float a = bt[o];
-  for (int i = 0; i < 128; ++i) a = fmaf(wt[o * 128 + i], emb[i], a);
+  for (int i = 0; i < 128; ++i) a = fmaf(wt[i * 256 + o], emb[i], a);
   float b = bs[o];
-  for (int i = 0; i < 256; ++i) b = fmaf(ws[o * 256 + i], sty[i], b);
+  for (int i = 0; i < 256; ++i) b = fmaf(ws[i * 256 + o], sty[i], b);
   cond[c * 256 + o] = (b4[o] + a) + b;
 }
 

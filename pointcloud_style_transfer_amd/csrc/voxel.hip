@@ -81,12 +81,11 @@ __device__ __forceinline__ float voxel_size(const StatRec& M, int64_t target) {
 }
 
 // per cloud: fold the stat partials once -> (min x, min y, min z, voxel size)
-__global__ void vox_params_kernel(const StatRec* __restrict__ mm, int B, int64_t target,
-                                  float4* __restrict__ vp) {
-  const int b = blockIdx.x * blockDim.x + threadIdx.x;
-  if (b >= B) return;
-  const StatRec M = fold_stats(mm, b);
-  vp[b] = make_float4(M.mn[0], M.mn[1], M.mn[2], voxel_size(M, target));
+__global__ __launch_bounds__(64) void vox_params_kernel(const StatRec* __restrict__ mm, int B,
+                                                        int64_t target, float4* __restrict__ vp) {
+  const int b = blockIdx.x;  // one wave per cloud
+  const StatRec M = fold_stats_wave(mm, b);
+  if (threadIdx.x == 0) vp[b] = make_float4(M.mn[0], M.mn[1], M.mn[2], voxel_size(M, target));
 }
 
 __device__ __forceinline__ int32_t wrap_mul(int32_t a, uint32_t m) {
@@ -338,6 +337,8 @@ __global__ void vox_select_kernel(const float* __restrict__ pts, int N, int64_t 
 //      radix select plus an exact sort of the boundary bin.
 constexpr int kSelBins = 4096;
 constexpr int kTieCap = 8192;
+constexpr int kVoxChunk = 2048;  // points aggregated per workgroup in LDS
+constexpr int kVoxLds = 4096;    // LDS table slots (load factor <= 1/2)
 
 struct VoxelFastWS {
   StatRec* mm;
@@ -393,25 +394,47 @@ __global__ __launch_bounds__(256) void voxf_insert_kernel(const float* __restric
                                                           unsigned long long* __restrict__ tkey,
                                                           unsigned long long* __restrict__ tsum,
                                                           uint32_t* __restrict__ tcnt) {
+  // Each workgroup first aggregates its kVoxChunk points in an LDS table (LDS atomics), then
+  // publishes one global (sum, count) per distinct voxel: dense voxels see at most one global
+  // atomic per workgroup instead of one per point.
   const int b = blockIdx.y;
   const float4 v4 = vp[b];
   const float* P = pts + (int64_t)b * N * 3;
   unsigned long long* K = tkey + b * H;
-  for (int n = blockIdx.x * 256 + threadIdx.x; n < N; n += gridDim.x * 256) {
+  __shared__ unsigned long long lkey[kVoxLds];
+  __shared__ unsigned long long lsum[kVoxLds];
+  __shared__ uint32_t lcnt[kVoxLds];
+  for (int i = threadIdx.x; i < kVoxLds; i += 256) { lkey[i] = 0ull; lsum[i] = 0ull; lcnt[i] = 0u; }
+  __syncthreads();
+  const int n0 = blockIdx.x * kVoxChunk, n1 = min(n0 + kVoxChunk, N);
+  for (int n = n0 + threadIdx.x; n < n1; n += 256) {
     const int32_t vx = (int32_t)floorf(__fdiv_rn(fsub(P[n * 3 + 0], v4.x), v4.w));
     const int32_t vy = (int32_t)floorf(__fdiv_rn(fsub(P[n * 3 + 1], v4.y), v4.w));
     const int32_t vz = (int32_t)floorf(__fdiv_rn(fsub(P[n * 3 + 2], v4.z), v4.w));
     const uint32_t h = (uint32_t)(wrap_mul(vx, 73856093u) ^ wrap_mul(vy, 19349663u) ^
                                   wrap_mul(vz, 83492791u));
     const unsigned long long kw = (1ull << 32) | h;
-    int64_t slot = mix32(h) & (H - 1);
+    int slot = (int)(mix32(h) & (kVoxLds - 1));
+    for (;;) {  // <= kVoxChunk keys in kVoxLds = 2 kVoxChunk slots: always terminates
+      const unsigned long long old = atomicCAS(&lkey[slot], 0ull, kw);
+      if (old == 0ull || old == kw) break;
+      slot = (slot + 1) & (kVoxLds - 1);
+    }
+    atomicAdd(&lsum[slot], (unsigned long long)n);
+    atomicAdd(&lcnt[slot], 1u);
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < kVoxLds; i += 256) {
+    const unsigned long long kw = lkey[i];
+    if (!kw) continue;
+    int64_t slot = mix32((uint32_t)kw) & (H - 1);
     for (;;) {
       const unsigned long long old = atomicCAS(&K[slot], 0ull, kw);
       if (old == 0ull || old == kw) break;
       slot = (slot + 1) & (H - 1);
     }
-    atomicAdd(&tsum[b * H + slot], (unsigned long long)n);
-    atomicAdd(&tcnt[b * H + slot], 1u);
+    atomicAdd(&tsum[b * H + slot], lsum[i]);
+    atomicAdd(&tcnt[b * H + slot], lcnt[i]);
   }
 }
 
@@ -424,18 +447,31 @@ __global__ __launch_bounds__(256) void voxf_reps_kernel(const unsigned long long
                                                         uint32_t* __restrict__ rhash,
                                                         uint32_t* __restrict__ isrep,
                                                         int64_t* __restrict__ out_idx) {
+  // one contiguous slot range per workgroup, one counter atomic per workgroup
   const int b = blockIdx.y;
-  for (int64_t s = blockIdx.x * 256 + threadIdx.x; s < H; s += (int64_t)gridDim.x * 256) {
-    const unsigned long long kw = tkey[b * H + s];
+  const int64_t chunk = (H + gridDim.x - 1) / gridDim.x;
+  const int64_t s0 = blockIdx.x * chunk, s1 = s0 + chunk < H ? s0 + chunk : H;
+  const unsigned long long* K = tkey + b * H;
+  uint32_t mine = 0;
+  for (int64_t s = s0 + threadIdx.x; s < s1; s += 256) mine += K[s] != 0ull;
+  __shared__ uint32_t sh[260];
+  __shared__ int base;
+  uint32_t tot;
+  uint32_t off = block_excl_scan_256(mine, sh, tot);
+  if (threadIdx.x == 0) base = tot ? atomicAdd(&cnt4[b * 4 + 0], (int)tot) : 0;
+  __syncthreads();
+  int k = base + (int)off;
+  for (int64_t s = s0 + threadIdx.x; s < s1; s += 256) {
+    const unsigned long long kw = K[s];
     if (!kw) continue;
     const float fs = (float)(long long)tsum[b * H + s];
     const float fc = (float)tcnt[b * H + s];
     const int64_t r = (int64_t)__fdiv_rn(fs, fc);
-    const int k = atomicAdd(&cnt4[b * 4 + 0], 1);
     reps[(int64_t)b * N + k] = r;
     rhash[(int64_t)b * N + k] = (uint32_t)kw;
     isrep[(int64_t)b * N + r] = 1u;
     if (k < T) out_idx[b * T + k] = r;  // the U <= T case keeps every rep
+    ++k;
   }
 }
 
@@ -521,21 +557,42 @@ __global__ __launch_bounds__(256) void voxf_select_kernel(int N, int64_t T, uint
                                                           const int64_t* __restrict__ reps,
                                                           unsigned long long* __restrict__ ties,
                                                           int64_t* __restrict__ out_idx) {
+  // one contiguous candidate range per workgroup, two counter atomics per workgroup
   const int b = blockIdx.y;
   const int bstar = sel[b * 4 + 0];
   if (bstar < 0) return;
   const int U = cnt4[b * 4];
-  for (int e = blockIdx.x * 256 + threadIdx.x; e < N; e += gridDim.x * 256) {
+  const int chunk = (N + gridDim.x - 1) / gridDim.x;
+  const int e0 = blockIdx.x * chunk, e1 = min(e0 + chunk, N);
+  uint32_t nlo = 0, nti = 0;
+  for (int e = e0 + threadIdx.x; e < e1; e += 256) {
+    uint32_t key, id;
+    if (!voxf_cand(b, e, N, U, T, seed, rhash, isrep, key, id)) continue;
+    const int bin = (int)(key >> 20);
+    nlo += bin < bstar;
+    nti += bin == bstar;
+  }
+  __shared__ uint32_t sh[260];
+  __shared__ int base_lo, base_ti;
+  uint32_t tlo, tti;
+  const uint32_t olo = block_excl_scan_256(nlo, sh, tlo);
+  const uint32_t oti = block_excl_scan_256(nti, sh, tti);
+  if (threadIdx.x == 0) {
+    base_lo = tlo ? atomicAdd(&cnt4[b * 4 + 1], (int)tlo) : 0;
+    base_ti = tti ? atomicAdd(&cnt4[b * 4 + 2], (int)tti) : 0;
+  }
+  __syncthreads();
+  int plo = base_lo + (int)olo, pti = base_ti + (int)oti;
+  for (int e = e0 + threadIdx.x; e < e1; e += 256) {
     uint32_t key, id;
     if (!voxf_cand(b, e, N, U, T, seed, rhash, isrep, key, id)) continue;
     const int bin = (int)(key >> 20);
     if (bin < bstar) {
-      const int pos = atomicAdd(&cnt4[b * 4 + 1], 1);
-      voxf_emit(b, N, T, U, pos, id, reps, out_idx);
+      voxf_emit(b, N, T, U, plo++, id, reps, out_idx);
     } else if (bin == bstar) {
-      const int t = atomicAdd(&cnt4[b * 4 + 2], 1);
-      if (t < kTieCap) ties[(int64_t)b * kTieCap + t] = ((unsigned long long)key << 32) | id;
+      if (pti < kTieCap) ties[(int64_t)b * kTieCap + pti] = ((unsigned long long)key << 32) | id;
       else atomicOr(&cnt4[b * 4 + 3], 1);
+      ++pti;
     }
   }
 }
@@ -580,19 +637,19 @@ static int voxel_fast(const float* pts, int64_t B, int64_t N, int64_t T, void* w
   const size_t zero = (size_t)((char*)w.isrep - (char*)w.cnt4) + sizeof(uint32_t) * B * N;
   PCST_HIP(hipMemsetAsync(w.cnt4, 0, zero, s), "voxel: memset");
   launch_cloud_stats(pts, b, n, w.mm, s);
-  hipLaunchKernelGGL(vox_params_kernel, dim3((unsigned)cdiv(B, 64)), dim3(64), 0, s, w.mm, b, T,
+  hipLaunchKernelGGL(vox_params_kernel, dim3((unsigned)B), dim3(64), 0, s, w.mm, b, T,
                      w.vp);
-  const unsigned gp = (unsigned)std::min<int64_t>(cdiv(N, 256), 1024);
-  hipLaunchKernelGGL(voxf_insert_kernel, dim3(gp, b), dim3(256), 0, s, pts, n, w.vp, w.H, w.tkey,
+  hipLaunchKernelGGL(voxf_insert_kernel, dim3((unsigned)cdiv(N, kVoxChunk), b), dim3(256), 0, s,
+                     pts, n, w.vp, w.H, w.tkey,
                      w.tsum, w.tcnt);
-  hipLaunchKernelGGL(voxf_reps_kernel, dim3((unsigned)std::min<int64_t>(cdiv(w.H, 256), 2048), b),
+  hipLaunchKernelGGL(voxf_reps_kernel, dim3(128, b),
                      dim3(256), 0, s, w.tkey, w.tsum, w.tcnt, w.H, n, T, w.cnt4, w.reps, w.rhash,
                      w.isrep, out_idx);
   const unsigned gs = (unsigned)std::min<int64_t>(cdiv(N, 256), 256);
   hipLaunchKernelGGL(voxf_hist_kernel, dim3(gs, b), dim3(256), 0, s, n, T, seed, w.cnt4, w.rhash,
                      w.isrep, w.hist);
   hipLaunchKernelGGL(voxf_find_kernel, dim3(b), dim3(256), 0, s, w.hist, w.cnt4, n, T, w.sel);
-  hipLaunchKernelGGL(voxf_select_kernel, dim3(gs, b), dim3(256), 0, s, n, T, seed, w.sel, w.cnt4,
+  hipLaunchKernelGGL(voxf_select_kernel, dim3(128, b), dim3(256), 0, s, n, T, seed, w.sel, w.cnt4,
                      w.rhash, w.isrep, w.reps, w.ties, out_idx);
   hipLaunchKernelGGL(voxf_ties_kernel, dim3(b), dim3(1024), 0, s, n, T, w.sel, w.cnt4, w.ties,
                      w.reps, out_idx);
@@ -626,7 +683,7 @@ extern "C" int pcst_voxel_stats(const float* pts, int64_t B, int64_t N, int64_t 
   PCST_HIP(hipMemsetAsync(w.sum, 0, zero_bytes, s), "voxel_stats: memset");
   PCST_HIP(hipMemsetAsync(w.err, 0, 16, s), "voxel_stats: memset");
   launch_cloud_stats(pts, b, n, w.mm, s);
-  hipLaunchKernelGGL(vox_params_kernel, dim3((unsigned)cdiv(B, 64)), dim3(64), 0, s, w.mm, b,
+  hipLaunchKernelGGL(vox_params_kernel, dim3((unsigned)B), dim3(64), 0, s, w.mm, b,
                      target, w.vp);
   hipLaunchKernelGGL(vox_hash_kernel, dim3(voxel_grid(N), b), dim3(256), 0, s, pts, n, w.vp,
                      w.kA, w.vA);

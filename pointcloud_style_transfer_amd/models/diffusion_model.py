@@ -107,20 +107,22 @@ class NoisePredictor(nn.Module):
             blob = torch.from_numpy(packing.pack_blob(sd, self.precision_code)).to(dev)
             bias = torch.from_numpy(packing.pack_bias(sd)).to(dev)
             freqs = self.time_embedding.freqs(dev)
-            self._packed = (blob, bias, freqs)
+            wt_t = self.time_proj.weight.detach().float().t().contiguous()
+            ws_t = self.style_proj.weight.detach().float().t().contiguous()
+            self._packed = (blob, bias, freqs, wt_t, ws_t)
             self._pack_key = key
         return self._packed
 
     def cond(self, timestep: torch.Tensor, style_feat: torch.Tensor) -> torch.Tensor:
-        _, _, freqs = self.packed()
-        return _hip.noise_cond(timestep, style_feat, freqs, self.time_proj.weight.detach(),
-                               self.time_proj.bias.detach(), self.style_proj.weight.detach(),
-                               self.style_proj.bias.detach(), self.point_encoder[4].bias.detach())
+        _, _, freqs, wt_t, ws_t = self.packed()
+        return _hip.noise_cond(timestep, style_feat, freqs, wt_t, self.time_proj.bias.detach(),
+                               ws_t, self.style_proj.bias.detach(),
+                               self.point_encoder[4].bias.detach())
 
     def forward(self, noisy_points: torch.Tensor, timestep: torch.Tensor,
                 style_feat: torch.Tensor) -> torch.Tensor:
         B, N, _ = noisy_points.shape
-        blob, bias, _ = self.packed()
+        blob, bias = self.packed()[:2]
         cond = self.cond(timestep.to(noisy_points.device), style_feat)
         out = _hip.noise_mlp(noisy_points.reshape(B * N, 3), N, cond, blob, bias,
                              self.precision_code)

@@ -139,7 +139,8 @@ def _noise_params(det_state, H, precision):
     bias = dev(packing.pack_bias(det_state))
     g = lambda n: dev(det_state[f"noise_predictor.{n}"])  # noqa: E731
     freqs = packing.time_freqs(128).cuda()
-    return blob, bias, (freqs, g("time_proj.weight"), g("time_proj.bias"), g("style_proj.weight"),
+    return blob, bias, (freqs, g("time_proj.weight").t().contiguous(), g("time_proj.bias"),
+                        g("style_proj.weight").t().contiguous(),
                         g("style_proj.bias"), g("point_encoder.4.bias"))
 
 
