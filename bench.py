@@ -47,15 +47,10 @@ def parse():
 
 
 def setup_dist(args):
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        import torch.distributed as dist
+    from pointcloud_style_transfer_amd.distributed import init_from_env
 
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
-    else:
+    world, rank, local = init_from_env("nccl")
+    if world == 1:
         torch.cuda.set_device(0)
     return world, rank, local
 
@@ -130,10 +125,13 @@ def main():
     from pointcloud_style_transfer_amd.synthetic import lidar_like_cloud, standard_normal
 
     cfg, model, dp = build_model(args.precision, device)
+    from pointcloud_style_transfer_amd.distributed import max_over_ranks, shard
+
     C = args.clouds_per_gpu
-    src_np = np.stack([lidar_like_cloud(1000 + rank * C + i, args.points) for i in range(C)])
-    cond_np = np.stack([lidar_like_cloud(2000 + rank * C + i, args.points) for i in range(C)])
-    xT_np = np.stack([standard_normal(3000 + rank * C + i, (args.points, 3)) for i in range(C)])
+    mine = shard(world * C, rank, world)  # this rank's clouds (SURVEY §8d seeds 1000+i ...)
+    src_np = np.stack([lidar_like_cloud(1000 + i, args.points) for i in mine])
+    cond_np = np.stack([lidar_like_cloud(2000 + i, args.points) for i in mine])
+    xT_np = np.stack([standard_normal(3000 + i, (args.points, 3)) for i in mine])
     src = torch.from_numpy(src_np).to(device)
     cond = torch.from_numpy(cond_np).to(device)
     x = torch.from_numpy(xT_np).to(device)
@@ -191,9 +189,7 @@ def main():
         elapsed = time.perf_counter() - t0
         if world > 1:
             dist.barrier()
-            tt = torch.tensor([elapsed], device=device, dtype=torch.float64)
-            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-            elapsed = float(tt.item())
+            elapsed = max_over_ranks(elapsed, device=device)
 
     mlp_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
     flop = FLOP_PER_POINT * 2 * C * cfg.global_points

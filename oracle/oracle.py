@@ -79,6 +79,21 @@ class Replay:
 
 
 # ------------------------------------------------------------------ pointnet2_encoder.py
+def normalize_point_cloud(points, target_range=1.8):
+    """`PointCloudPreprocessor.normalize_point_cloud` (data/preprocessing.py:21-38): float64
+    centre/scale; the callers cast to float32."""
+    c = points.mean(axis=0)
+    pc = points - c
+    m = np.max(np.abs(pc))
+    s = 1.0 if m < 1e-6 else target_range / m
+    return pc * s, {"center": c, "scale": s, "method": "isotropic", "target_range": target_range}
+
+
+def denormalize_point_cloud(points, params):
+    """data/preprocessing.py:40-42."""
+    return (points / params["scale"]) + params["center"]
+
+
 def square_distance(src, dst):
     """`square_distance` (pointnet2_encoder.py:8-15)."""
     src, dst = _f32(src), _f32(dst)

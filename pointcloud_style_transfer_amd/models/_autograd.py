@@ -1,0 +1,57 @@
+"""Autograd for the training path: per-point linear layers on the pointwise MFMA kernel
+(csrc/sa_mlp.hip), forward and backward.
+
+  forward   Y  = act(X W^T + b)                      pcst_pointwise_linear
+  backward  dZ = dY * [Y > 0]  (ReLU)
+            dX = dZ W          = linear(dZ, W^T)     pcst_pointwise_linear
+            dW = dZ^T X        = linear(dZ^T, X^T)   pcst_pointwise_linear (K = rows)
+            db = dZ^T 1        = linear(dZ^T, 1)     pcst_pointwise_linear
+All products are exact-f32 MFMA; the reduction over rows is inside one kernel (no atomics),
+so gradients are deterministic.
+"""
+from __future__ import annotations
+
+import torch
+
+from .. import _hip
+
+
+class LinearFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, relu):
+        x2 = x.reshape(-1, x.shape[-1]).float().contiguous()
+        W = weight.reshape(weight.shape[0], -1).float().contiguous()
+        y = _hip.pointwise_linear(x2, W, None, None if bias is None else bias.float(), relu, 0)
+        ctx.relu = relu
+        ctx.has_bias = bias is not None
+        ctx.wshape = weight.shape
+        ctx.xshape = x.shape
+        ctx.save_for_backward(x2, W, y if relu else None)
+        return y.view(*x.shape[:-1], W.shape[0])
+
+    @staticmethod
+    def backward(ctx, gy):
+        x2, W, y = ctx.saved_tensors
+        dz = gy.reshape(-1, W.shape[0]).float().contiguous()
+        if ctx.relu:
+            dz = dz * (y > 0)
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            dx = _hip.pointwise_linear(dz, W.t().contiguous()).view(ctx.xshape)
+        if ctx.needs_input_grad[1] or (ctx.has_bias and ctx.needs_input_grad[2]):
+            dzt = dz.t().contiguous()
+            if ctx.needs_input_grad[1]:
+                dw = _hip.pointwise_linear(dzt, x2.t().contiguous()).view(ctx.wshape)
+            if ctx.has_bias and ctx.needs_input_grad[2]:
+                ones = torch.ones(1, dz.shape[0], device=dz.device)
+                db = _hip.pointwise_linear(dzt, ones).view(-1)
+        return dx, dw, db, None
+
+
+def linear(x, lin, relu=False):
+    """nn.Linear / Conv2d-1x1 module applied through LinearFn."""
+    return LinearFn.apply(x, lin.weight, lin.bias, relu)
+
+
+def needs_grad(module) -> bool:
+    return torch.is_grad_enabled() and any(p.requires_grad for p in module.parameters())

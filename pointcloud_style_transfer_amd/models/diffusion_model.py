@@ -26,6 +26,7 @@ from .. import _hip
 from .. import packing
 from .. import rng as _rng
 from ..config.config import Config
+from . import _autograd as _ag
 from .pointnet2_encoder import PointNet2Encoder
 
 
@@ -62,6 +63,10 @@ class StyleEncoder(nn.Module):
 
     def forward(self, points: torch.Tensor) -> torch.Tensor:
         f = self.encoder(points)
+        if _ag.needs_grad(self):
+            h = _ag.linear(f, self.style_mlp[0], True)
+            h = self.style_mlp[2](h)
+            return _ag.linear(h, self.style_mlp[3], True)
         h = _linear(f, self.style_mlp[0], True)
         if self.training and self.style_mlp[2].p > 0:
             h = F.dropout(h, self.style_mlp[2].p, True)
@@ -119,9 +124,32 @@ class NoisePredictor(nn.Module):
                                ws_t, self.style_proj.bias.detach(),
                                self.point_encoder[4].bias.detach())
 
+    def _dropout_active(self) -> bool:
+        return self.training and any(l[3].p > 0 for l in self.layers)
+
+    def _forward_autograd(self, noisy_points, timestep, style_feat):
+        """Differentiable path (training): every linear on the MFMA GEMM kernel with its
+        backward (models/_autograd.py); residual adds / dropout as device tensor ops."""
+        pe = self.point_encoder
+        h = _ag.linear(noisy_points, pe[0], True)
+        h = _ag.linear(h, pe[2], True)
+        pf = _ag.linear(h, pe[4])
+        tf = _ag.linear(self.time_embedding(timestep.to(noisy_points.device)), self.time_proj)
+        sf = _ag.linear(style_feat, self.style_proj)
+        x = pf + tf.unsqueeze(1) + sf.unsqueeze(1)
+        for layer in self.layers:
+            d = _ag.linear(_ag.linear(x, layer[0], True), layer[2])
+            x = layer[3](d) + x
+        h = _ag.linear(x, self.output_mlp[0], True)
+        h = _ag.linear(h, self.output_mlp[2], True)
+        return _ag.linear(h, self.output_mlp[4])
+
     def forward(self, noisy_points: torch.Tensor, timestep: torch.Tensor,
                 style_feat: torch.Tensor) -> torch.Tensor:
         B, N, _ = noisy_points.shape
+        if (_ag.needs_grad(self) or self._dropout_active()
+                or (style_feat.requires_grad and torch.is_grad_enabled())):
+            return self._forward_autograd(noisy_points, timestep, style_feat)
         blob, bias = self.packed()[:2]
         cond = self.cond(timestep.to(noisy_points.device), style_feat)
         out = _hip.noise_mlp(noisy_points.reshape(B * N, 3), N, cond, blob, bias,

@@ -13,9 +13,11 @@ from typing import List, Optional, Tuple
 
 import torch
 import torch.nn as nn
+import torch.nn.functional as F
 
 from .. import _hip
 from .. import rng as _rng
+from . import _autograd as _ag
 
 
 def square_distance(src: torch.Tensor, dst: torch.Tensor) -> torch.Tensor:
@@ -73,7 +75,14 @@ class SetAbstraction(nn.Module):
         fidx = farthest_point_sample(xyz, self.npoint)
         new_xyz = index_points(xyz, fidx)
         gidx = query_ball_point(self.radius, self.nsample, xyz, new_xyz)
-        new_xyz, grouped = _hip.group_gather(xyz, points, fidx, gidx)
+        if points is not None and points.requires_grad and torch.is_grad_enabled():
+            # training: centred xyz from the kernel, features gathered with autograd
+            new_xyz, gxyz = _hip.group_gather(xyz, None, fidx, gidx)
+            bidx = torch.arange(B, device=xyz.device).view(B, 1, 1)
+            g = torch.cat([gxyz, points[bidx, gidx.clamp(0, N - 1)]], dim=-1)
+            grouped = g
+        else:
+            new_xyz, grouped = _hip.group_gather(xyz, points, fidx, gidx)
         feats = self.apply_mlp(grouped.reshape(B * self.npoint * self.nsample, -1),
                                pool_ns=self.nsample)
         return new_xyz, feats.view(B, self.npoint, -1).permute(0, 2, 1)
@@ -81,6 +90,8 @@ class SetAbstraction(nn.Module):
     def apply_mlp(self, x: torch.Tensor, pool_ns: int) -> torch.Tensor:
         """(Conv2d 1x1 -> BatchNorm2d -> ReLU) x L, then max over each group of `pool_ns`
         rows.  x: [rows, C] channel-last."""
+        if _ag.needs_grad(self) or (x.requires_grad and torch.is_grad_enabled()):
+            return self._apply_mlp_train(x, pool_ns)
         n = len(self.mlp_convs)
         for i, (conv, bn) in enumerate(zip(self.mlp_convs, self.mlp_bns)):
             W = conv.weight.view(conv.out_channels, -1)
@@ -102,6 +113,19 @@ class SetAbstraction(nn.Module):
                 shift = bn.bias.detach() - mean.float() * scale
                 x = _hip.affine_act(z, scale, shift, True, pool)
         return x
+
+    def _apply_mlp_train(self, x: torch.Tensor, pool_ns: int) -> torch.Tensor:
+        """Differentiable variant: conv GEMMs on the MFMA kernel (models/_autograd.py),
+        BatchNorm/ReLU/max as device tensor ops."""
+        for conv, bn in zip(self.mlp_convs, self.mlp_bns):
+            z = _ag.LinearFn.apply(x, conv.weight, conv.bias, False)
+            z = F.batch_norm(z, bn.running_mean, bn.running_var, bn.weight, bn.bias,
+                             bn.training, bn.momentum, bn.eps)
+            if bn.training and bn.track_running_stats:
+                bn.num_batches_tracked.add_(1)
+            x = F.relu(z)
+        C = x.shape[-1]
+        return x.view(-1, pool_ns, C).max(dim=1)[0]
 
 
 class PointNet2Encoder(nn.Module):

@@ -1,0 +1,250 @@
+"""Training entry point -- drop-in for the reference's `training/trainer.py` (DiffusionTrainer,
+CosineWithWarmupLR: same constructor, epoch/step semantics, loss, clipping, AdamW, EMA and
+checkpoint cadence).
+
+Compute runs on the MI355X kernels: voxel downsample, FPS / ball query, the per-point linear
+layers (forward AND backward, models/_autograd.py), Chamfer / L1 losses (csrc/chamfer.hip).
+Data parallelism: when torch.distributed is initialised with world_size > 1
+the model is wrapped in DistributedDataParallel (RCCL all-reduce of the fp32 gradients over
+xGMI, overlapped with backward); BN statistics stay rank-local as in the reference (no
+SyncBN); clip/AdamW/EMA run replicated after the all-reduce, so ranks stay identical.
+
+Differences kept deliberately: the custom kernels compute in fp32 under `use_amp` (autocast
+does not lower them), so the step is at least as precise as the reference's fp16 autocast;
+the GradScaler logic is kept as is.  TensorBoard is optional (not installed here).
+"""
+from __future__ import annotations
+
+import math
+import os
+
+import numpy as np
+import torch
+import torch.distributed as dist
+import torch.optim as optim
+from torch.amp import GradScaler, autocast
+
+from .. import rng as _rng
+from ..config.config import Config
+from ..models.diffusion_model import DiffusionProcess, PointCloudDiffusionModel
+from ..models.losses import DiffusionLoss
+from ..utils.checkpoint import CheckpointManager
+from ..utils.ema import ExponentialMovingAverage
+from ..utils.logger import Logger
+
+try:  # trainer.py:5 -- optional here
+    from torch.utils.tensorboard import SummaryWriter
+except Exception:  # noqa: BLE001
+    class SummaryWriter:  # type: ignore
+        def __init__(self, *a, **k):
+            pass
+
+        def add_scalar(self, *a, **k):
+            pass
+
+        def close(self):
+            pass
+
+
+class CosineWithWarmupLR:
+    """`CosineWithWarmupLR` (trainer.py:20-34)."""
+
+    def __init__(self, optimizer, warmup_epochs, total_epochs, min_lr_ratio=0.01):
+        self.optimizer = optimizer
+        self.warmup_epochs = warmup_epochs
+        self.total_epochs = total_epochs
+        self.min_lr_ratio = min_lr_ratio
+        self.base_lrs = [g["lr"] for g in optimizer.param_groups]
+        self.current_epoch = 0
+
+    def step(self):
+        self.current_epoch += 1
+        if self.current_epoch <= self.warmup_epochs:
+            scale = self.current_epoch / self.warmup_epochs
+        else:
+            progress = (self.current_epoch - self.warmup_epochs) / (self.total_epochs - self.warmup_epochs)
+            scale = self.min_lr_ratio + 0.5 * (1 - self.min_lr_ratio) * (1 + math.cos(math.pi * progress))
+        for g, base in zip(self.optimizer.param_groups, self.base_lrs):
+            g["lr"] = base * scale
+
+
+def _progress(it, desc):
+    try:
+        from tqdm import tqdm
+
+        return tqdm(it, desc=desc)
+    except Exception:  # noqa: BLE001
+        return it
+
+
+class DiffusionTrainer:
+    """`DiffusionTrainer` (trainer.py:36-232)."""
+
+    def __init__(self, config: Config, device: str = "cuda"):
+        self.config = config
+        self.device = torch.device(device)
+        self.device_type = "cuda" if "cuda" in str(self.device) else "cpu"
+        self.distributed = dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
+        self.rank = dist.get_rank() if self.distributed else 0
+        self.logger = Logger(name="DiffusionTrainer", log_dir=config.log_dir,
+                             experiment_name=config.experiment_name, file_output=self.rank == 0)
+        self.model = PointCloudDiffusionModel(config).to(self.device)
+        self.diffusion_process = DiffusionProcess(config, device=str(self.device))
+        self.loss_fn = DiffusionLoss(noise_weight=1.0, chamfer_weight=config.lambda_chamfer)
+        self.optimizer = optim.AdamW(self.model.parameters(), lr=config.learning_rate,
+                                     weight_decay=config.weight_decay, betas=(0.9, 0.95))
+        if config.lr_scheduler == "cosine_with_warmup":
+            self.scheduler = CosineWithWarmupLR(self.optimizer, config.warmup_epochs,
+                                                config.num_epochs, config.min_lr_ratio)
+        else:
+            self.scheduler = optim.lr_scheduler.CosineAnnealingLR(
+                self.optimizer, T_max=config.num_epochs, eta_min=config.learning_rate * 0.01)
+        self.scaler = GradScaler(enabled=(config.use_amp and self.device_type == "cuda"))
+        self.ema = ExponentialMovingAverage(self.model.parameters(), decay=config.ema_decay)
+        self.writer = SummaryWriter(log_dir=os.path.join(config.log_dir, config.experiment_name))
+        self.checkpoint_manager = CheckpointManager(config.checkpoint_dir, config.experiment_name)
+        self.best_val_loss = float("inf")
+        self.current_epoch = 0
+        self.patience_counter = 0
+        self.max_patience = 20
+        self.gradient_accumulation_steps = config.gradient_accumulation_steps
+        self.gradient_clip_norm = 1.0
+        self.ddp_model = self.model
+        if self.distributed:
+            from torch.nn.parallel import DistributedDataParallel as DDP
+
+            self.ddp_model = DDP(self.model, device_ids=[self.device.index] if self.device.index is not None else None,
+                                 broadcast_buffers=False, bucket_cap_mb=16)
+
+    # ------------------------------------------------------------------ one step
+    def train_step(self, batch, batch_idx: int, num_batches: int):
+        """Body of the per-batch loop of train_one_epoch (trainer.py:70-127)."""
+        sim = batch["sim_full"].to(self.device)
+        real = batch["real_full"].to(self.device)
+        B, N, C = sim.shape
+        src = _rng.source()
+        t = src.randint(0, self.config.num_timesteps, (B,), device=self.device).long()
+        noisy, actual_noise = self.diffusion_process.q_sample(sim, t)
+        with autocast(device_type=self.device_type, enabled=self.config.use_amp):
+            pred, indices = self.ddp_model(noisy_points=noisy, timestep=t, condition_points=real,
+                                           cond_drop_prob=self.config.cond_drop_prob,
+                                           use_hierarchical=self.config.use_hierarchical)
+            if indices is not None:
+                ie = indices.unsqueeze(-1).expand(-1, -1, C)
+                actual_coarse = torch.gather(actual_noise, 1, ie)
+                pred_x0_coarse = sim_coarse = None
+                if self.config.lambda_chamfer > 0:
+                    noisy_coarse = torch.gather(noisy, 1, ie)
+                    sim_coarse = torch.gather(sim, 1, ie)
+                    a = self.diffusion_process.sqrt_alphas_cumprod[t].view(B, 1, 1)
+                    b = self.diffusion_process.sqrt_one_minus_alphas_cumprod[t].view(B, 1, 1)
+                    pred_x0_coarse = (noisy_coarse - b * pred) / (a + 1e-8)
+                loss, loss_dict = self.loss_fn(predicted_noise=pred, actual_noise=actual_coarse,
+                                               predicted_points_coarse=pred_x0_coarse,
+                                               target_points_coarse=sim_coarse)
+            else:
+                loss, loss_dict = self.loss_fn(predicted_noise=pred, actual_noise=actual_noise)
+            loss = loss / self.gradient_accumulation_steps
+        self.scaler.scale(loss).backward()
+        if (batch_idx + 1) % self.gradient_accumulation_steps == 0 or batch_idx == num_batches - 1:
+            self.scaler.unscale_(self.optimizer)
+            torch.nn.utils.clip_grad_norm_(self.model.parameters(), self.gradient_clip_norm)
+            self.scaler.step(self.optimizer)
+            self.scaler.update()
+            self.optimizer.zero_grad()
+            self.ema.update()
+        return loss, loss_dict
+
+    def train_one_epoch(self, data_loader):
+        self.model.train()
+        total = 0.0
+        pbar = _progress(data_loader, f"Epoch {self.current_epoch}/{self.config.num_epochs} [Train]")
+        self.optimizer.zero_grad()
+        n = len(data_loader)
+        for batch_idx, batch in enumerate(pbar):
+            loss, loss_dict = self.train_step(batch, batch_idx, n)
+            total += loss.item() * self.gradient_accumulation_steps
+            if hasattr(pbar, "set_postfix"):
+                pbar.set_postfix({"Loss": f"{loss_dict.get('total_loss', 0):.4f}",
+                                  "L1": f"{loss_dict.get('noise_loss', 0):.4f}",
+                                  "CD": f"{loss_dict.get('chamfer_loss', 0):.4f}",
+                                  "LR": f"{self.optimizer.param_groups[0]['lr']:.2e}"})
+        avg = total / n
+        self.writer.add_scalar("Loss/Train", avg, self.current_epoch)
+        return avg
+
+    @torch.no_grad()
+    def validate_one_epoch(self, data_loader):
+        """trainer.py:140-174 (EMA weights, eval mode, noise loss only)."""
+        self.ema.apply_shadow()
+        try:
+            self.model.eval()
+            total = 0.0
+            for batch in _progress(data_loader, f"Epoch {self.current_epoch} [Val]"):
+                sim = batch["sim_full"].to(self.device)
+                real = batch["real_full"].to(self.device)
+                B, N, C = sim.shape
+                t = _rng.source().randint(0, self.config.num_timesteps, (B,), device=self.device).long()
+                noisy, actual = self.diffusion_process.q_sample(sim, t)
+                pred, idx = self.model(noisy_points=noisy, timestep=t, condition_points=real,
+                                       cond_drop_prob=0, use_hierarchical=self.config.use_hierarchical)
+                if idx is not None:
+                    actual = torch.gather(actual, 1, idx.unsqueeze(-1).expand(-1, -1, C))
+                loss, _ = self.loss_fn(pred, actual)
+                if torch.isfinite(loss):
+                    total += loss.item()
+            avg = total / len(data_loader)
+            self.writer.add_scalar("Loss/Validation", avg, self.current_epoch)
+            return avg
+        finally:
+            self.ema.restore()
+
+    def save_sample_results(self, data_loader, num_samples: int = 2):
+        """trainer.py:176-196."""
+        self.ema.apply_shadow()
+        try:
+            self.model.eval()
+            batch = next(iter(data_loader))
+            sim = batch["sim_full"][:num_samples].to(self.device)
+            real = batch["real_full"][:num_samples].to(self.device)
+            with torch.no_grad():
+                out = self.diffusion_process.guided_sample_loop(
+                    model=self.model, source_points=sim, condition_points=real,
+                    num_inference_steps=50, guidance_scale=self.config.guidance_scale)
+            d = os.path.join(self.config.result_dir, self.config.experiment_name,
+                             f"epoch_{self.current_epoch:04d}")
+            os.makedirs(d, exist_ok=True)
+            for i in range(num_samples):
+                np.save(os.path.join(d, f"original_sim_{i}.npy"), sim[i].cpu().numpy())
+                np.save(os.path.join(d, f"reference_real_{i}.npy"), real[i].cpu().numpy())
+                np.save(os.path.join(d, f"transferred_{i}.npy"), out[i].cpu().numpy())
+        finally:
+            self.ema.restore()
+
+    def train(self, train_loader, val_loader):
+        """trainer.py:198-232."""
+        self.current_epoch = self.checkpoint_manager.load(self.model, self.optimizer, self.ema)
+        for _ in range(self.current_epoch):
+            if hasattr(self.scheduler, "step"):
+                self.scheduler.step()
+        for epoch in range(self.current_epoch, self.config.num_epochs):
+            self.current_epoch = epoch
+            avg = self.train_one_epoch(train_loader)
+            self.logger.info(f"Epoch {epoch}: train loss {avg:.6f}")
+            if hasattr(self.scheduler, "step"):
+                self.scheduler.step()
+            if epoch % self.config.val_interval == 0:
+                v = self.validate_one_epoch(val_loader)
+                is_best = v < self.best_val_loss
+                if is_best:
+                    self.best_val_loss = v
+                    self.patience_counter = 0
+                else:
+                    self.patience_counter += 1
+                if self.rank == 0:
+                    self.checkpoint_manager.save(self.model, self.optimizer, self.ema, epoch, is_best)
+                if self.patience_counter >= self.max_patience:
+                    break
+                if epoch > 0 and epoch % (self.config.save_interval * 2) == 0 and self.rank == 0:
+                    self.save_sample_results(val_loader)
+        self.writer.close()

@@ -1,0 +1,174 @@
+"""Host-side logic around the hot path (CPU only): checkpoint format and safe loading, EMA,
+the LR schedule, the inference normaliser.  Pinned by the reference's checkpoint manifest
+(tests/golden/checkpoint_manifest.json, written from a checkpoint the reference saved) and by
+the formulas cited from the reference sources."""
+import io
+import json
+import math
+import os
+import pickletools
+import zipfile
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN
+
+
+@pytest.fixture()
+def tiny_model(tmp_path, monkeypatch):
+    from detweights import load_into
+    from pointcloud_style_transfer_amd.config.config import Config
+    from pointcloud_style_transfer_amd.models.diffusion_model import PointCloudDiffusionModel
+
+    monkeypatch.chdir(tmp_path)
+    cfg = Config(total_points=4096, global_points=1024, use_amp=False,
+                 gradient_accumulation_steps=1, experiment_name="golden")
+    m = PointCloudDiffusionModel(cfg)
+    load_into(m)
+    return cfg, m
+
+
+def _pickle_globals(path):
+    seen = set()
+    with zipfile.ZipFile(path) as zf:
+        pkl = [n for n in zf.namelist() if n.endswith("data.pkl")][0]
+        for op, arg, _ in pickletools.genops(io.BytesIO(zf.read(pkl))):
+            if op.name in ("GLOBAL", "STACK_GLOBAL") and arg:
+                seen.add(str(arg).replace(" ", "."))
+    return sorted(g for g in seen if "(" not in g)
+
+
+def test_checkpoint_matches_reference_format(tiny_model):
+    from pointcloud_style_transfer_amd.utils.checkpoint import CheckpointManager, safe_load
+    from pointcloud_style_transfer_amd.utils.ema import ExponentialMovingAverage
+    from pointcloud_style_transfer_amd.config.config import Config
+
+    with open(os.path.join(GOLDEN, "checkpoint_manifest.json")) as f:
+        man = json.load(f)
+    cfg, m = tiny_model
+    opt = torch.optim.AdamW(m.parameters(), lr=cfg.learning_rate, weight_decay=cfg.weight_decay,
+                            betas=(0.9, 0.95))
+    # one optimizer step so the AdamW state exists, as in the reference's checkpoint
+    for p in m.parameters():
+        p.grad = torch.ones_like(p) * 1e-3
+    opt.step()
+    ema = ExponentialMovingAverage(m.parameters(), decay=cfg.ema_decay)
+    cm = CheckpointManager(cfg.checkpoint_dir, cfg.experiment_name)
+    cm.save(m, opt, ema, epoch=3, is_best=True)
+    d = os.path.join(cfg.checkpoint_dir, cfg.experiment_name)
+    assert sorted(os.listdir(d)) == man["files"]
+    path = os.path.join(d, "ckpt_epoch_0003.pth")
+    # the same pickle globals as the reference's file -- Config under config.config
+    assert _pickle_globals(path) == man["pickle_globals"]
+    ck = safe_load(path)
+    assert sorted(ck.keys()) == man["top_keys"]
+    assert ck["epoch"] == man["epoch"]
+    assert isinstance(ck["config"], Config)
+    for k, v in man["config_fields"].items():
+        assert getattr(ck["config"], k) == v, k
+    assert [[k, list(v.shape), str(v.dtype)] for k, v in ck["model_state_dict"].items()] \
+        == man["model_state_dict"]
+    assert sorted(ck["optimizer_state_dict"].keys()) == man["optimizer_keys"]
+    assert len(ck["optimizer_state_dict"]["state"]) == man["optimizer_n_state"]
+    assert sorted(ck["optimizer_state_dict"]["state"][0].keys()) == man["optimizer_state_keys"]
+    assert sorted(ck["ema_state_dict"].keys()) == man["ema_keys"]
+    assert ck["ema_state_dict"]["decay"] == man["ema_decay"]
+    assert [list(p.shape) for p in ck["ema_state_dict"]["shadow_params"]] == man["ema_shapes"]
+    # resume: CheckpointManager.load returns epoch + 1 and restores the weights
+    from pointcloud_style_transfer_amd.models.diffusion_model import PointCloudDiffusionModel
+
+    m2 = PointCloudDiffusionModel(cfg)
+    opt2 = torch.optim.AdamW(m2.parameters(), lr=cfg.learning_rate)
+    ema2 = ExponentialMovingAverage(m2.parameters(), decay=0.5)
+    assert cm.load(m2, opt2, ema2) == 4
+    for (k, a), b in zip(m.state_dict().items(), m2.state_dict().values()):
+        assert torch.equal(a, b), k
+    assert ema2.decay == cfg.ema_decay
+
+
+def test_safe_load_refuses_arbitrary_globals(tmp_path):
+    from pointcloud_style_transfer_amd.utils.checkpoint import safe_load
+
+    class Evil:
+        def __reduce__(self):
+            return (os.system, ("true",))
+
+    p = tmp_path / "evil.pth"
+    torch.save({"x": Evil()}, p)
+    with pytest.raises(Exception):
+        safe_load(str(p))
+
+
+def test_ema_matches_reference_formula():
+    from pointcloud_style_transfer_amd.utils.ema import ExponentialMovingAverage
+
+    torch.manual_seed(0)
+    ps = [torch.nn.Parameter(torch.randn(5, 3)), torch.nn.Parameter(torch.randn(7)),
+          torch.nn.Parameter(torch.randn(2), requires_grad=False)]
+    ema = ExponentialMovingAverage(ps, decay=0.9)
+    assert len(ema.shadow_params) == 2
+    want = [p.detach().clone() for p in ps[:2]]
+    for _ in range(3):
+        with torch.no_grad():
+            for p in ps:
+                p.add_(0.5)
+        ema.update()
+        want = [0.9 * w + 0.1 * p.detach() for w, p in zip(want, ps[:2])]  # ema.py:39-53
+    for w, s in zip(want, ema.shadow_params):
+        torch.testing.assert_close(s, w, rtol=1e-6, atol=1e-6)
+    before = [p.detach().clone() for p in ps]
+    ema.apply_shadow()
+    for p, s in zip(ps[:2], ema.shadow_params):
+        assert torch.equal(p.data, s)
+    ema.restore()
+    for p, b in zip(ps, before):
+        assert torch.equal(p.data, b)
+    st = ema.state_dict()
+    assert set(st) == {"decay", "shadow_params"} and st["decay"] == 0.9
+
+
+def test_cosine_with_warmup_schedule():
+    from pointcloud_style_transfer_amd.training.trainer import CosineWithWarmupLR
+
+    p = torch.nn.Parameter(torch.zeros(1))
+    opt = torch.optim.AdamW([p], lr=1e-4)
+    s = CosineWithWarmupLR(opt, warmup_epochs=20, total_epochs=200, min_lr_ratio=0.01)
+    lrs = []
+    for _ in range(200):
+        s.step()
+        lrs.append(opt.param_groups[0]["lr"])
+    # trainer.py:20-34
+    assert lrs[0] == pytest.approx(1e-4 / 20)
+    assert lrs[19] == pytest.approx(1e-4)
+    e = 100
+    prog = (e - 20) / 180
+    assert lrs[e - 1] == pytest.approx(1e-4 * (0.01 + 0.5 * 0.99 * (1 + math.cos(math.pi * prog))))
+    assert lrs[-1] == pytest.approx(1e-6)
+
+
+def test_normalizer_matches_oracle():
+    from oracle import oracle as O
+    from pointcloud_style_transfer_amd.data.preprocessing import PointCloudPreprocessor
+
+    rng = np.random.default_rng(7)
+    pts = (rng.standard_normal((5000, 3)) * [30, 20, 2] + [100, -50, 3]).astype(np.float64)
+    pp = PointCloudPreprocessor()
+    n, prm = pp.normalize_point_cloud(pts)
+    n2, prm2 = O.normalize_point_cloud(pts)
+    np.testing.assert_array_equal(n, n2)
+    assert n.dtype == np.float64 and np.abs(n).max() <= 1.8 + 1e-9  # callers cast to f32
+    back = pp.denormalize_point_cloud(n, prm)
+    np.testing.assert_array_equal(back, O.denormalize_point_cloud(n2, prm2))
+    np.testing.assert_allclose(back, pts, rtol=1e-5, atol=1e-4)
+
+
+def test_inference_requires_gpu():
+    """No CPU fallback: the entry point refuses to run without the HIP device."""
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    from pointcloud_style_transfer_amd.scripts.inference import DiffusionInference
+
+    with pytest.raises(RuntimeError, match="HIP"):
+        DiffusionInference("nonexistent.pth", "cuda")
