@@ -29,6 +29,7 @@ sys.path.insert(0, REPO)
 FLOP_PER_POINT = 3_540_480          # NoisePredictor MACs x 2
 MFMA_BF16_PEAK_TFLOPS = 2500.0      # MI355X dense bf16 (MI355X_MICROARCH.md)
 MFMA_F32_PEAK_TFLOPS = 157.3
+HBM_PEAK_GBS = 8000.0
 
 
 def parse():
@@ -117,6 +118,39 @@ def cpu_baseline(args, cfg, model, src, cond, xT):
                       f"{per:.2f} s/step; numpy/OpenBLAS fp32 MLP + C voxel/kNN"}
 
 
+def encoder_rooflines(xc, device, reps=5):
+    """SA1 farthest-point sampling (512 of 30000) and ball query (r 0.2, 32) on the coarse
+    condition cloud, timed with HIP events on the launch stream; achieved bandwidth in the
+    SURVEY §8d scan model (FPS npoint*N*16 B, ball query S*N*12 B + S*ns*8 B)."""
+    from pointcloud_style_transfer_amd import _hip
+
+    B, N, _ = xc.shape
+    start = torch.zeros(B, dtype=torch.long, device=device)
+    ev = lambda: torch.cuda.Event(enable_timing=True)  # noqa: E731
+    t_fps, t_bq = [], []
+    for _ in range(reps):
+        e0, e1, e2 = ev(), ev(), ev()
+        e0.record()
+        idx = _hip.fps(xc, 512, start)
+        e1.record()
+        new_xyz = _hip.index_points(xc, idx)
+        e2.record()
+        _hip.ball_query(0.2, 32, xc, new_xyz)
+        e3 = ev()
+        e3.record()
+        torch.cuda.synchronize()
+        t_fps.append(e0.elapsed_time(e1))
+        t_bq.append(e2.elapsed_time(e3))
+    out = {}
+    for name, ms, byts in (("fps", min(t_fps), 512 * N * 16 * B),
+                           ("ball_query", min(t_bq), (512 * N * 12 + 512 * 32 * 8) * B)):
+        gbs = byts / (ms * 1e-3) / 1e9
+        out[name] = {"bound": "hbm (scan model)", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4), "ms": round(ms, 4),
+                     "shape": f"B={B} N={N} S=512"}
+    return out
+
+
 def main():
     args = parse()
     world, rank, local = setup_dist(args)
@@ -145,6 +179,7 @@ def main():
         torch.cuda.synchronize()
         style_s = time.perf_counter() - t0
         style_in = torch.cat([style, torch.zeros_like(style)])
+        enc = encoder_rooflines(hp.downsample(cond)[0], device)
         npred.packed()
         timesteps = torch.linspace(dp.num_timesteps - 1, 0, dp.num_timesteps).long().tolist()
         x_cat = torch.cat([x, x]).contiguous()
@@ -234,6 +269,7 @@ def main():
                          "algorithmic": f"{FLOP_PER_POINT} FLOP/pt x {2 * C * cfg.global_points} pts",
                          "avg_launch_ms": round(mlp_ms, 4)},
             "cpu_baseline": base,
+            "encoder_rooflines": enc,
         }
         print(json.dumps(line), flush=True)
     if world > 1:

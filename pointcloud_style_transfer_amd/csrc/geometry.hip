@@ -111,6 +111,94 @@ __global__ __launch_bounds__(kFpsThreads) void fps_reg_kernel(const float* __res
   }
 }
 
+// 1024-thread variant (the default for N <= 30720): 16 waves (4 per SIMD) keep up to 30
+// points per lane.  The arg-max is carried as one 64-bit key, (distance bits << 32) | ~n:
+// non-negative floats order like their bit patterns, and ~n makes the lowest index win ties
+// (Q3).  In-row DPP steps + readlane replace the LDS-crossbar shuffles, and one LDS exchange
+// of the 16 wave keys per iteration finishes the reduction.
+constexpr int kFps2Threads = 1024;
+constexpr int kFps2Waves = kFps2Threads / 64;
+
+__device__ __forceinline__ uint64_t u64max(uint64_t a, uint64_t b) { return a > b ? a : b; }
+
+template <int CTRL>
+__device__ __forceinline__ uint64_t dpp_u64(uint64_t v) {
+  const uint32_t lo = __builtin_amdgcn_update_dpp(0u, (uint32_t)v, CTRL, 0xf, 0xf, false);
+  const uint32_t hi = __builtin_amdgcn_update_dpp(0u, (uint32_t)(v >> 32), CTRL, 0xf, 0xf, false);
+  return ((uint64_t)hi << 32) | lo;
+}
+
+// max over the 16 lanes of each DPP row; every lane of the row ends with the row maximum
+__device__ __forceinline__ uint64_t row_max_u64(uint64_t k) {
+  k = u64max(k, dpp_u64<0xB1>(k));   // quad_perm [1,0,3,2]
+  k = u64max(k, dpp_u64<0x4E>(k));   // quad_perm [2,3,0,1]
+  k = u64max(k, dpp_u64<0x141>(k));  // row_half_mirror
+  k = u64max(k, dpp_u64<0x140>(k));  // row_mirror
+  return k;
+}
+
+__device__ __forceinline__ uint64_t wave_max_u64(uint64_t k) {
+  k = row_max_u64(k);
+  uint64_t m = 0;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)k, r * 16);
+    const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(k >> 32), r * 16);
+    m = u64max(m, ((uint64_t)hi << 32) | lo);
+  }
+  return m;
+}
+
+template <int PPT>
+__global__ __launch_bounds__(kFps2Threads) void fps_key_kernel(const float* __restrict__ xyz,
+                                                               int N, int npoint,
+                                                               const int64_t* __restrict__ start,
+                                                               int64_t* __restrict__ out) {
+  const int b = blockIdx.x;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wid = tid >> 6;
+  const float* P = xyz + (int64_t)b * N * 3;
+  float px[PPT], py[PPT], pz[PPT], dist[PPT];
+#pragma unroll
+  for (int k = 0; k < PPT; ++k) {
+    const int n = tid + k * kFps2Threads;
+    if (n < N) {
+      px[k] = P[n * 3 + 0]; py[k] = P[n * 3 + 1]; pz[k] = P[n * 3 + 2];
+      dist[k] = 1e10f;
+    } else {
+      px[k] = py[k] = pz[k] = 0.0f;
+      dist[k] = -1.0f;  // never updated, never the arg-max
+    }
+  }
+  __shared__ uint64_t s_key[2][kFps2Waves];
+  int far = (int)start[b];
+  int64_t* o = out + (int64_t)b * npoint;
+  for (int it = 0; it < npoint; ++it) {
+    far = __builtin_amdgcn_readfirstlane(far);
+    if (tid == 0) o[it] = far;
+    const float cx = P[far * 3 + 0], cy = P[far * 3 + 1], cz = P[far * 3 + 2];
+    float best = -2.0f;
+    int bestk = 0;
+#pragma unroll
+    for (int k = 0; k < PPT; ++k) {
+      const float dx = fsub(px[k], cx), dy = fsub(py[k], cy), dz = fsub(pz[k], cz);
+      const float d = fadd(fadd(fmul(dx, dx), fmul(dy, dy)), fmul(dz, dz));
+      dist[k] = d < dist[k] ? d : dist[k];
+      if (dist[k] > best) { best = dist[k]; bestk = k; }
+    }
+    const uint32_t n = (uint32_t)(tid + bestk * kFps2Threads);
+    const uint32_t bits = best > 0.0f ? __float_as_uint(best) : 0u;
+    const uint64_t key = wave_max_u64(((uint64_t)bits << 32) | (0xFFFFFFFFu - n));
+    const int slot = it & 1;
+    if (lane == 0) s_key[slot][wid] = key;
+    __syncthreads();
+    uint64_t g = lane < kFps2Waves ? s_key[slot][lane] : 0ull;
+    g = row_max_u64(g);
+    const uint32_t glo = __builtin_amdgcn_readlane((uint32_t)g, 0);
+    far = (int)(0xFFFFFFFFu - glo);
+  }
+}
+
 // Fallback for N > 512*60: running distances in global memory (caller workspace), one
 // workgroup per cloud streaming the cloud every iteration.
 __global__ __launch_bounds__(1024) void fps_global_kernel(const float* __restrict__ xyz, int N,
@@ -205,6 +293,73 @@ __global__ __launch_bounds__(256) void ball_query_kernel(float r2, int nsample,
   for (int k = (cnt < nsample ? cnt : nsample) + lane; k < nsample; k += 64) o[k] = first;
 }
 
+// Split-range variant (the default): one workgroup of kBqWaves waves per centroid; wave w
+// scans its contiguous slice of [0, N) in ascending order and keeps the first nsample hits of
+// the slice (early exit).  The result -- the first nsample hits of [0, N) -- is the
+// concatenation of the slices' lists in slice order, so it is identical to the sequential
+// scan.  The cloud is re-read per centroid from L2 (360 KB at N = 30000).
+constexpr int kBqWaves = 8;
+
+__global__ __launch_bounds__(kBqWaves * 64) void ball_query_split_kernel(
+    float r2, int nsample, const float* __restrict__ xyz, const float* __restrict__ new_xyz,
+    int N, int S, int64_t* __restrict__ out) {
+  extern __shared__ int bq_smem[];
+  int* s_cnt = bq_smem;              // [kBqWaves]
+  int* s_list = bq_smem + kBqWaves;  // [kBqWaves][nsample]
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t q = blockIdx.x;
+  const int b = (int)(q / S);
+  const float a0 = new_xyz[q * 3 + 0], a1 = new_xyz[q * 3 + 1], a2 = new_xyz[q * 3 + 2];
+  const float na = sqnorm3(a0, a1, a2);
+  const float* P = xyz + (int64_t)b * N * 3;
+  const int per = (int)((((int64_t)N + kBqWaves - 1) / kBqWaves + 63) / 64 * 64);
+  const int lo = w * per, hi = min(N, lo + per);
+  int* my = s_list + w * nsample;
+  int cnt = 0;
+  for (int base = lo; base < hi && cnt < nsample; base += 256) {
+    float d[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int n = base + u * 64 + lane;
+      d[u] = 3.4e38f;
+      if (n < hi) {
+        const float q0 = P[n * 3 + 0], q1 = P[n * 3 + 1], q2 = P[n * 3 + 2];
+        float dd = fmul(-2.0f, dot3(a0, a1, a2, q0, q1, q2));
+        dd = fadd(dd, na);
+        d[u] = fadd(dd, sqnorm3(q0, q1, q2));
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int n = base + u * 64 + lane;
+      const bool in = (n < hi) && !(d[u] > r2);
+      const unsigned long long m = __ballot(in);
+      if (m == 0ull) continue;
+      const int slot = cnt + __popcll(m & lanemask_lt());
+      if (in && slot < nsample) my[slot] = n;
+      cnt += __popcll(m);
+      if (cnt >= nsample) break;
+    }
+  }
+  if (lane == 0) s_cnt[w] = min(cnt, nsample);
+  __syncthreads();
+  int64_t* o = out + q * nsample;
+  int total = 0, first = N;
+  for (int v = 0; v < kBqWaves; ++v) {
+    if (first == N && s_cnt[v] > 0) first = s_list[v * nsample];
+    total += s_cnt[v];
+  }
+  for (int k = threadIdx.x; k < nsample; k += kBqWaves * 64) {
+    int val = first;
+    if (k < total) {
+      int v = 0, pre = 0;
+      while (k >= pre + s_cnt[v]) pre += s_cnt[v++];
+      val = s_list[v * nsample + (k - pre)];
+    }
+    o[k] = val;
+  }
+}
+
 // ------------------------------------------------------------------ group gather
 // pointnet2_encoder.py:92-99: new_xyz = index_points(xyz, fps_idx); grouped =
 // cat(index_points(xyz, gidx) - new_xyz, index_points(feats, gidx)).
@@ -278,6 +433,13 @@ static void launch_fps(const float* xyz, int B, int N, int npoint, const int64_t
                      out);
 }
 
+template <int PPT>
+static void launch_fps2(const float* xyz, int B, int N, int npoint, const int64_t* start,
+                        int64_t* out, hipStream_t s) {
+  hipLaunchKernelGGL(fps_key_kernel<PPT>, dim3(B), dim3(kFps2Threads), 0, s, xyz, N, npoint, start,
+                     out);
+}
+
 extern "C" int pcst_fps_workspace_size(int64_t B, int64_t N, size_t* bytes) {
   *bytes = (N > (int64_t)kFpsThreads * 60) ? (size_t)(B * N) * sizeof(float) : 0;
   return PCST_OK;
@@ -290,8 +452,20 @@ extern "C" int pcst_fps_ws(const float* xyz, int64_t B, int64_t N, int64_t npoin
   if (B == 0 || npoint == 0) return PCST_OK;
   PCST_CHECK_ARG(xyz && start_idx && out_idx, "fps: null pointer");
   hipStream_t s = as_stream(stream);
-  const int64_t ppt = cdiv(N, kFpsThreads);
   const int b = (int)B, n = (int)N, np = (int)npoint;
+  const int64_t ppt2 = cdiv(N, kFps2Threads);
+  if (ppt2 <= 30) {
+    if (ppt2 <= 1) launch_fps2<1>(xyz, b, n, np, start_idx, out_idx, s);
+    else if (ppt2 <= 2) launch_fps2<2>(xyz, b, n, np, start_idx, out_idx, s);
+    else if (ppt2 <= 4) launch_fps2<4>(xyz, b, n, np, start_idx, out_idx, s);
+    else if (ppt2 <= 8) launch_fps2<8>(xyz, b, n, np, start_idx, out_idx, s);
+    else if (ppt2 <= 16) launch_fps2<16>(xyz, b, n, np, start_idx, out_idx, s);
+    else if (ppt2 <= 24) launch_fps2<24>(xyz, b, n, np, start_idx, out_idx, s);
+    else launch_fps2<30>(xyz, b, n, np, start_idx, out_idx, s);
+    PCST_LAUNCH_CHECK("fps");
+    return PCST_OK;
+  }
+  const int64_t ppt = cdiv(N, kFpsThreads);
   if (ppt <= 1) launch_fps<1>(xyz, b, n, np, start_idx, out_idx, s);
   else if (ppt <= 2) launch_fps<2>(xyz, b, n, np, start_idx, out_idx, s);
   else if (ppt <= 4) launch_fps<4>(xyz, b, n, np, start_idx, out_idx, s);
@@ -326,9 +500,15 @@ extern "C" int pcst_ball_query(double radius, int64_t nsample, const float* xyz,
   PCST_CHECK_ARG(xyz && new_xyz && out_idx, "ball_query: null pointer");
   const float r2 = (float)(radius * radius);  // python float r**2, then cast to fp32 (Q4)
   const int64_t waves = B * S;
-  hipLaunchKernelGGL(ball_query_kernel, dim3((unsigned)cdiv(waves, 4)), dim3(256), 0,
-                     as_stream(stream), r2, (int)nsample, xyz, new_xyz, (int)B, (int)N, (int)S,
-                     out_idx);
+  const size_t lds = (size_t)kBqWaves * (1 + nsample) * sizeof(int);
+  if (lds <= 64 * 1024) {
+    hipLaunchKernelGGL(ball_query_split_kernel, dim3((unsigned)(B * S)), dim3(kBqWaves * 64), lds,
+                       as_stream(stream), r2, (int)nsample, xyz, new_xyz, (int)N, (int)S, out_idx);
+  } else {
+    hipLaunchKernelGGL(ball_query_kernel, dim3((unsigned)cdiv(waves, 4)), dim3(256), 0,
+                       as_stream(stream), r2, (int)nsample, xyz, new_xyz, (int)B, (int)N, (int)S,
+                       out_idx);
+  }
   PCST_LAUNCH_CHECK("ball_query");
   return PCST_OK;
 }

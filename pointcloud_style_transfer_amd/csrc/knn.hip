@@ -19,7 +19,7 @@
 
 namespace pcst {
 
-constexpr int kRingMax = 3;  // shells searched per query before the exhaustive outlier pass
+constexpr int kRingMax = 4;  // shells searched per query before the exhaustive outlier pass
 
 struct KnnWS {
   StatRec* stats;    // [B][kStatBlocks]
@@ -82,7 +82,7 @@ __global__ __launch_bounds__(64) void knn_grid_params_kernel(const StatRec* __re
     sig[c] = fmax(sig[c], 1e-3 * ext[c]);
   }
   const double rho = (double)M / (15.7496099457 * sig[0] * sig[1] * sig[2]);
-  double s = cbrt(4.0 / rho);
+  double s = cbrt(6.0 / rho);
   // a cell must not be smaller than a thin dimension forces: keep at least ~1 ref per
   // cell on average over the occupied extent
   int d[3];
@@ -245,28 +245,37 @@ __global__ __launch_bounds__(256) void knn_query_kernel(
   const int rall = max(dx, max(dy, dz));
   const int rmax = min(rall, kRingMax);
   bool done = false;
+  // refs of consecutive cells of one (z, y) row are contiguous (row-major counting sort), so
+  // a shell is visited as row RANGES: whole rows on its faces, the two end cells inside
+  auto scan = [&](uint32_t a, uint32_t e) {
+    for (uint32_t i = a; i < e; ++i) {
+      const float4 ref = R[i];
+      const float ex = fx - ref.x, ey = fy - ref.y, ez = fz - ref.z;
+      const float d32 = fmaf(ez, ez, fmaf(ey, ey, ex * ex));
+      if (d32 > thr) continue;
+      const double ux = dsub(qx, (double)ref.x), uy = dsub(qy, (double)ref.y),
+                   uz = dsub(qz, (double)ref.z);
+      const double d = dadd(dadd(dmul(ux, ux), dmul(uy, uy)), dmul(uz, uz));
+      t.push(d, __float_as_int(ref.w));
+      if (t.d[kk - 1] != INFINITY) thr = (float)(t.d[kk - 1] * (1.0 + 2e-6)) + 1e-30f;
+    }
+  };
   for (int r = 0; r <= rmax; ++r) {
     const int z0 = max(cz - r, 0), z1 = min(cz + r, dz - 1);
     const int y0 = max(cy - r, 0), y1 = min(cy + r, dy - 1);
+    const int xl = max(cx - r, 0), xh = min(cx + r, dx - 1);
     for (int z = z0; z <= z1; ++z) {
       for (int y = y0; y <= y1; ++y) {
-        const bool face = (z == cz - r || z == cz + r || y == cy - r || y == cy + r);
-        const int step = (face || r == 0) ? 1 : 2 * r;
-        for (int x = cx - r; x <= cx + r; x += step) {
-          if (x < 0 || x >= dx) continue;
-          const int64_t cell = ((int64_t)z * dy + y) * dx + x;
-          const uint32_t a = RS[cell], e = RS[cell + 1];
-          for (uint32_t i = a; i < e; ++i) {
-            const float4 ref = R[i];
-            const float ex = fx - ref.x, ey = fy - ref.y, ez = fz - ref.z;
-            const float d32 = fmaf(ez, ez, fmaf(ey, ey, ex * ex));
-            if (d32 > thr) continue;
-            const double ux = dsub(qx, (double)ref.x), uy = dsub(qy, (double)ref.y),
-                         uz = dsub(qz, (double)ref.z);
-            const double d = dadd(dadd(dmul(ux, ux), dmul(uy, uy)), dmul(uz, uz));
-            t.push(d, __float_as_int(ref.w));
-            if (t.d[kk - 1] != INFINITY) thr = (float)(t.d[kk - 1] * (1.0 + 2e-6)) + 1e-30f;
-          }
+        const int64_t row = ((int64_t)z * dy + y) * dx;
+        const bool face = (r == 0 || z == cz - r || z == cz + r || y == cy - r || y == cy + r);
+        if (face) {
+          scan(RS[row + xl], RS[row + xh + 1]);
+        } else {
+          const bool lo = cx - r >= 0, hi = cx + r < dx;
+          const uint32_t a0 = lo ? RS[row + cx - r] : 0u, e0 = lo ? RS[row + cx - r + 1] : 0u;
+          const uint32_t a1 = hi ? RS[row + cx + r] : 0u, e1 = hi ? RS[row + cx + r + 1] : 0u;
+          scan(a0, e0);
+          scan(a1, e1);
         }
       }
     }

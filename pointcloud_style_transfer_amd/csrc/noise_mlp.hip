@@ -30,11 +30,25 @@ constexpr int kOffW0 = 0, kOffB0 = 384, kOffB2 = 512, kOffB1 = 768, kOffBB2 = 38
               kOffO0 = 5376, kOffO2 = 5632, kOffO4 = 5760, kBiasFloats = 5792;
 constexpr int kCondSlots = 4;
 
+// Perf-experiment knobs, compiled only by tools/nm_variants.sh; the product build uses the
+// defaults.  PCST_NM_EXPERIMENT bits: 1 = no weight DMA after the first two parts,
+// 2 = no barrier between parts (both give wrong results; they time the overheads),
+// 8 = compiler-scheduled LDS fragment reads instead of the asm reads.
+#ifndef PCST_NM_EXPERIMENT
+#define PCST_NM_EXPERIMENT 0
+#endif
+#ifndef PCST_NM_NCB
+#define PCST_NM_NCB 1
+#endif
+
 struct TrBF16 {
   static constexpr int KS = 16;          // K per MFMA
   static constexpr int FRAG = 1024;      // bytes per A fragment
   static constexpr int OPB = 2;          // operands per 32-row block
   static constexpr int THREADS = 256;
+  static constexpr int NCB = PCST_NM_NCB;  // 32-point column blocks per wave (A-fragment reuse)
+  static constexpr int G = 4;              // fragments per pipelined LDS read group
+  static constexpr bool kAsmReads = !(PCST_NM_EXPERIMENT & 8);
   using A = bf16x8;
   using Op = bf16x8;
   __device__ static f32x16 mfma(A a, Op b, f32x16 c) {
@@ -51,6 +65,11 @@ struct TrBF16 {
       o[s] = t;
     }
   }
+  // registers 4gi..4gi+3 of a C block -> elements 4(gi&1).. of operand gi>>1
+  __device__ static void to_op4(const float (&v)[4], Op* o, int gi) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) o[gi >> 1][4 * (gi & 1) + j] = (__bf16)v[j];
+  }
 };
 
 struct TrF32 {
@@ -58,6 +77,9 @@ struct TrF32 {
   static constexpr int FRAG = 256;
   static constexpr int OPB = 16;
   static constexpr int THREADS = 256;
+  static constexpr int NCB = 1;
+  static constexpr int G = 8;
+  static constexpr bool kAsmReads = false;
   using A = float;
   using Op = float;
   __device__ static f32x16 mfma(A a, Op b, f32x16 c) {
@@ -73,85 +95,176 @@ struct TrF32 {
 // row of accumulator register r for lane half h inside a 32-row block
 __device__ __forceinline__ int crow(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
 
+// Weight parts stream HBM/L2 -> LDS (global_load_lds, 16 B per lane, no registers) through a
+// ring of kSlots 32 KiB slots, one part ahead of use: next() = barrier (part+1 has landed;
+// every wave is done with part-1), advance, then DMA part+2 into the slot part-1 held.  Three
+// slots let the residual loop read two consecutive parts at once (W2 of chunk c from part-1
+// while W1 of chunk c+1 runs on part).
 template <class TR>
 struct Streamer {
+  static constexpr int kSlots = 3;
+  static constexpr int kWaves = TR::THREADS / 64;
+  static constexpr int kPerWave = kPart / 1024 / kWaves;  // 1 KiB pieces per wave per part
   const char* blob;
-  char* lds;  // two kPart buffers
-  int part;   // part being computed
+  char* lds;   // kSlots x kPart
+  int part;    // part being computed
   int nparts;
+  int wave;    // wave index, wave-uniform (SGPR)
+
   __device__ void issue(int q) {
     if (q >= nparts) return;
-    constexpr int waves = TR::THREADS / 64;
-    constexpr int per_wave = kPart / 1024 / waves;  // 1 KiB wave-instructions per wave
-    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    char* dst = lds + (q & 1) * kPart;
-    const char* src = blob + (int64_t)q * kPart;
+    if ((PCST_NM_EXPERIMENT & 1) && q >= 2) return;
+    const int lane = threadIdx.x & 63;
+    // uniform LDS destination (M0) and global base; only lane*16 varies per lane
+    char* dst = lds + (q % kSlots) * kPart + wave * kPerWave * 1024;
+    const char* src = blob + (int64_t)q * kPart + wave * kPerWave * 1024;
 #pragma unroll
-    for (int i = 0; i < per_wave; ++i) {
-      const int chunk = w * per_wave + i;
-      __builtin_amdgcn_global_load_lds((const void*)(src + chunk * 1024 + lane * 16),
-                                       (__attribute__((address_space(3))) void*)(dst + chunk * 1024),
+    for (int i = 0; i < kPerWave; ++i)
+      __builtin_amdgcn_global_load_lds((const void*)(src + i * 1024 + lane * 16),
+                                       (__attribute__((address_space(3))) void*)(dst + i * 1024),
                                        16, 0, 0);
-    }
   }
   __device__ void begin() {  // part 0 resident, part 1 in flight
     issue(0);
     __syncthreads();
     issue(1);
   }
-  __device__ void next() {  // finish `part`, make part+1 resident, prefetch part+2
-    __syncthreads();
+  __device__ void next() {
+    if (!(PCST_NM_EXPERIMENT & 2)) __syncthreads();
     ++part;
     issue(part + 1);
   }
-  __device__ typename TR::A frag(int f) const {  // fragment f of the current part
-    const char* p = lds + (part & 1) * kPart + f * TR::FRAG +
-                    (threadIdx.x & 63) * (int)sizeof(typename TR::A);
-    return *reinterpret_cast<const typename TR::A*>(p);
+  // LDS byte address of fragment f of part q for this lane
+  __device__ uint32_t frag_addr(int q, int f) const {
+    return (uint32_t)(uintptr_t)(lds + (q % kSlots) * kPart + f * TR::FRAG +
+                                 (threadIdx.x & 63) * (int)sizeof(typename TR::A));
   }
+  __device__ typename TR::A frag_at(int q, int f) const {
+    return *reinterpret_cast<const typename TR::A*>(
+        lds + (q % kSlots) * kPart + f * TR::FRAG + (threadIdx.x & 63) * (int)sizeof(typename TR::A));
+  }
+  __device__ typename TR::A frag(int f) const { return frag_at(part, f); }
 };
 
-// acc = sum_s A(frag base+s) * in[s] for s in [S, NS): compile-time recursion so every
-// operand register index is static (a runtime index would send the operands to scratch).
-template <class TR, int S, int NS>
-struct KSteps {
-  __device__ static __forceinline__ void run(const Streamer<TR>& st, int base,
-                                             const typename TR::Op* in, f32x16& acc) {
-    acc = TR::mfma(st.frag(base + S), in[S], acc);
-    KSteps<TR, S + 1, NS>::run(st, base, in, acc);
-  }
-};
-template <class TR, int NS>
-struct KSteps<TR, NS, NS> {
-  __device__ static __forceinline__ void run(const Streamer<TR>&, int, const typename TR::Op*,
-                                             f32x16&) {}
+// bf16 fragment reads in inline asm.  With LDS DMA in flight the compiler stops counting LDS
+// waits and drains lgkmcnt(0) before every use, which exposes the LDS latency once per read
+// group; here the reads are issued a group ahead and waited for with a counted
+// s_waitcnt lgkmcnt(G) that is tied (in/out operands) to the registers it guards, so no MFMA
+// can be scheduled above it.  LDS operations complete in order, so a counted wait also
+// covers any compiler-issued LDS access older than these reads.
+template <int OFF>
+__device__ __forceinline__ bf16x8 lds_read_b128(uint32_t addr) {
+  bf16x8 v;
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(v) : "v"(addr), "i"(OFF));
+  return v;
+}
+template <int N>
+__device__ __forceinline__ void lgkm_wait4(bf16x8& a, bf16x8& b, bf16x8& c, bf16x8& d) {
+  asm volatile("s_waitcnt lgkmcnt(%4)" : "+v"(a), "+v"(b), "+v"(c), "+v"(d) : "n"(N));
+}
+
+struct NoHook {
+  __device__ void operator()(int) const {}
 };
 
-// Dense layer over NOB output blocks with K = KB 32-row input blocks.  Every layer starts on a
-// fresh part (the packing pads each layer to whole parts); inside a layer a part holds
-// FPP/NS whole output blocks.
-template <class TR, int NOB, int KB>
+template <class TR, int N, int KPER, int ICB, int AST, int ACB, class Hook = NoHook>
+__device__ __forceinline__ void run_seq(const Streamer<TR>& st, int q, int base,
+                                        const typename TR::Op* in, f32x16* acc,
+                                        const Hook& hook = Hook()) {
+  constexpr int G = TR::G;
+  static_assert(N % G == 0, "group size must divide the sequence");
+  using A = typename TR::A;
+  if constexpr (TR::kAsmReads) {
+    static_assert(G == 4, "asm read path is written for groups of 4 fragments");
+    const uint32_t a0 = st.frag_addr(q, base);
+    A cur[4], nxt[4];
+    cur[0] = lds_read_b128<0 * TR::FRAG>(a0);
+    cur[1] = lds_read_b128<1 * TR::FRAG>(a0);
+    cur[2] = lds_read_b128<2 * TR::FRAG>(a0);
+    cur[3] = lds_read_b128<3 * TR::FRAG>(a0);
+#pragma unroll
+    for (int g = 0; g < N; g += 4) {
+      if (g + 4 < N) {
+        nxt[0] = lds_read_b128<0>(a0 + (g + 4) * TR::FRAG);
+        nxt[1] = lds_read_b128<TR::FRAG>(a0 + (g + 4) * TR::FRAG);
+        nxt[2] = lds_read_b128<2 * TR::FRAG>(a0 + (g + 4) * TR::FRAG);
+        nxt[3] = lds_read_b128<3 * TR::FRAG>(a0 + (g + 4) * TR::FRAG);
+        lgkm_wait4<4>(cur[0], cur[1], cur[2], cur[3]);
+      } else {
+        lgkm_wait4<0>(cur[0], cur[1], cur[2], cur[3]);
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int i = g + j;
+#pragma unroll
+        for (int cb = 0; cb < TR::NCB; ++cb)
+          acc[(i / KPER) * AST + cb * ACB] =
+              TR::mfma(cur[j], in[cb * ICB + i % KPER], acc[(i / KPER) * AST + cb * ACB]);
+      }
+      hook(g / 4);  // VALU work that fills this group's MFMA shadow
+      if (g + 4 < N) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) cur[j] = nxt[j];
+      }
+    }
+  } else {
+    A cur[G];
+#pragma unroll
+    for (int j = 0; j < G; ++j) cur[j] = st.frag_at(q, base + j);
+#pragma unroll
+    for (int g = 0; g < N; g += G) {
+      A nxt[G];
+      if (g + G < N) {
+#pragma unroll
+        for (int j = 0; j < G; ++j) nxt[j] = st.frag_at(q, base + g + G + j);
+      }
+#pragma unroll
+      for (int j = 0; j < G; ++j) {
+        const int i = g + j;
+#pragma unroll
+        for (int cb = 0; cb < TR::NCB; ++cb)
+          acc[(i / KPER) * AST + cb * ACB] =
+              TR::mfma(cur[j], in[cb * ICB + i % KPER], acc[(i / KPER) * AST + cb * ACB]);
+      }
+      hook(g / G);
+      if (g + G < N) {
+#pragma unroll
+        for (int j = 0; j < G; ++j) cur[j] = nxt[j];
+      }
+    }
+  }
+}
+
+// Dense layer over NOB output blocks with K = KB 32-row input blocks; in[cb*KB*OPB + s],
+// acc[cb*8 + ob].  Every layer starts on a fresh part (the packing pads each layer to whole
+// parts); inside a layer a part holds OBPP whole output blocks.
+template <class TR, int NOB, int KB, int OB0 = 0>
 __device__ __forceinline__ void dense(Streamer<TR>& st, const typename TR::Op* in, f32x16* acc) {
   constexpr int NS = KB * TR::OPB;
   constexpr int FPP = kPart / TR::FRAG;
   constexpr int OBPP = FPP / NS;
   static_assert(OBPP >= 1 && FPP % NS == 0, "part must hold whole output blocks");
-#pragma unroll
-  for (int ob = 0; ob < NOB; ++ob) {
-    if (ob > 0 && ob % OBPP == 0) st.next();
-    KSteps<TR, 0, NS>::run(st, (ob % OBPP) * NS, in, acc[ob]);
+  constexpr int NOW = (NOB - OB0) < OBPP ? (NOB - OB0) : OBPP;
+  run_seq<TR, NOW * NS, NS, NS, 1, 8>(st, st.part, 0, in, acc + OB0);
+  if constexpr (OB0 + NOW < NOB) {
+    st.next();
+    dense<TR, NOB, KB, OB0 + NOW>(st, in, acc);
   }
 }
 
+// 16 bias values of a 32-row block in accumulator order (the accumulator's initial value)
+__device__ __forceinline__ f32x16 bias_block(const float* b, int h) {
+  f32x16 v;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) v[r] = b[crow(r, h)];
+  return v;
+}
+
 template <class TR>
-__device__ __forceinline__ void epilogue_op(const f32x16& acc, const float* bias, int h, bool relu,
-                                            typename TR::Op* out) {
+__device__ __forceinline__ void act_op(const f32x16& acc, bool relu, typename TR::Op* out) {
   float v[16];
 #pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    float x = acc[r] + bias[crow(r, h)];
-    v[r] = relu ? fmaxf(x, 0.0f) : x;
-  }
+  for (int r = 0; r < 16; ++r) v[r] = relu ? fmaxf(acc[r], 0.0f) : acc[r];
   TR::to_op(v, out);
 }
 
@@ -161,10 +274,11 @@ __global__ __launch_bounds__(TR::THREADS) void noise_mlp_kernel(
     int64_t nclouds, const char* __restrict__ blob, int nparts, const float* __restrict__ bias,
     float* __restrict__ out) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  float* sb = reinterpret_cast<float*>(smem + 2 * kPart);
+  float* sb = reinterpret_cast<float*>(smem + Streamer<TR>::kSlots * kPart);
   float* sc = sb + kBiasFloats;  // kCondSlots x 256
   using Op = typename TR::Op;
-  constexpr int PTS = TR::THREADS / 64 * 32;
+  constexpr int NCB = TR::NCB, OPB = TR::OPB;
+  constexpr int PTS = TR::THREADS / 64 * 32 * NCB;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, h = lane >> 5;
   const int64_t p0 = (int64_t)blockIdx.x * PTS;
   const int64_t c0 = p0 / T;
@@ -173,121 +287,186 @@ __global__ __launch_bounds__(TR::THREADS) void noise_mlp_kernel(
     const int64_t c = c0 + i / 256;
     sc[i] = c < nclouds ? cond[c * 256 + (i % 256)] : 0.0f;
   }
-  const int64_t p = p0 + wid * 32 + (lane & 31);
-  const bool valid = p < P;
-  const int64_t pc = valid ? p : (P - 1);
-  const float px = pts[pc * 3 + 0], py = pts[pc * 3 + 1], pz = pts[pc * 3 + 2];
-  const int64_t myc = pc / T;
-  const int slot = (int)(myc - c0);
+  int64_t p[NCB];
+  int slot[NCB];
+  float px[NCB], py[NCB], pz[NCB];
+#pragma unroll
+  for (int cb = 0; cb < NCB; ++cb) {
+    p[cb] = p0 + (wid * NCB + cb) * 32 + (lane & 31);
+    const int64_t pc = p[cb] < P ? p[cb] : (P - 1);
+    px[cb] = pts[pc * 3 + 0];
+    py[cb] = pts[pc * 3 + 1];
+    pz[cb] = pts[pc * 3 + 2];
+    slot[cb] = (int)(pc / T - c0);
+  }
   __syncthreads();
 
+  Streamer<TR> st{blob, smem, 0, nparts, __builtin_amdgcn_readfirstlane(wid)};
+  st.begin();
+
   // ---- h1 = relu(W0 p + b0), 128 rows, VALU, straight into operand form
-  Op h1[4 * TR::OPB];
+  Op h1[NCB * 4 * OPB];
 #pragma unroll
   for (int ob = 0; ob < 4; ++ob) {
-    float v[16];
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int row = ob * 32 + crow(r, h);
-      float x = sb[kOffB0 + row];
-      x = fmaf(sb[kOffW0 + row * 3 + 0], px, x);
-      x = fmaf(sb[kOffW0 + row * 3 + 1], py, x);
-      x = fmaf(sb[kOffW0 + row * 3 + 2], pz, x);
-      v[r] = fmaxf(x, 0.0f);
+    for (int cb = 0; cb < NCB; ++cb) {
+      float v[16];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = ob * 32 + crow(r, h);
+        float x = sb[kOffB0 + row];
+        x = fmaf(sb[kOffW0 + row * 3 + 0], px[cb], x);
+        x = fmaf(sb[kOffW0 + row * 3 + 1], py[cb], x);
+        x = fmaf(sb[kOffW0 + row * 3 + 2], pz[cb], x);
+        v[r] = fmaxf(x, 0.0f);
+      }
+      TR::to_op(v, &h1[cb * 4 * OPB + ob * OPB]);
     }
-    TR::to_op(v, &h1[ob * TR::OPB]);
   }
 
-  Streamer<TR> st{blob, smem, 0, nparts};
-  st.begin();
-  f32x16 acc[8];
-  Op xb[8 * TR::OPB];
+  f32x16 acc[NCB * 8];
+  Op xb[NCB * 8 * OPB];
 
   // ---- h2 = relu(W2 h1 + b2)
 #pragma unroll
-  for (int ob = 0; ob < 8; ++ob) acc[ob] = f32x16{};
+  for (int ob = 0; ob < 8; ++ob) {
+    const f32x16 b = bias_block(sb + kOffB2 + ob * 32, h);
+#pragma unroll
+    for (int cb = 0; cb < NCB; ++cb) acc[cb * 8 + ob] = b;
+  }
   dense<TR, 8, 4>(st, h1, acc);
 #pragma unroll
-  for (int ob = 0; ob < 8; ++ob) epilogue_op<TR>(acc[ob], sb + kOffB2 + ob * 32, h, true, &xb[ob * TR::OPB]);
+  for (int i = 0; i < NCB * 8; ++i) act_op<TR>(acc[i], true, &xb[i * OPB]);
 
   // ---- x = W4 h2 + cond[cloud]   (cond already contains b4)
-  f32x16 x[8];
+  f32x16 x[NCB * 8];
 #pragma unroll
-  for (int ob = 0; ob < 8; ++ob) {
+  for (int cb = 0; cb < NCB; ++cb) {
+    const bool in_lds = slot[cb] >= 0 && slot[cb] < kCondSlots;
+    const float* crow_src = in_lds ? sc + slot[cb] * 256 : cond + (c0 + slot[cb]) * 256;
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int row = ob * 32 + crow(r, h);
-      x[ob][r] = (slot >= 0 && slot < kCondSlots) ? sc[slot * 256 + row] : cond[myc * 256 + row];
-    }
+    for (int ob = 0; ob < 8; ++ob) x[cb * 8 + ob] = bias_block(crow_src + ob * 32, h);
   }
   {
-    Op h2[8 * TR::OPB];
+    Op h2[NCB * 8 * OPB];
 #pragma unroll
-    for (int i = 0; i < 8 * TR::OPB; ++i) h2[i] = xb[i];
+    for (int i = 0; i < NCB * 8 * OPB; ++i) h2[i] = xb[i];
     st.next();
     dense<TR, 8, 8>(st, h2, x);
   }
 #pragma unroll
-  for (int ob = 0; ob < 8; ++ob) {
-    float v[16];
-#pragma unroll
-    for (int r = 0; r < 16; ++r) v[r] = x[ob][r];
-    TR::to_op(v, &xb[ob * TR::OPB]);
-  }
+  for (int i = 0; i < NCB * 8; ++i) act_op<TR>(x[i], false, &xb[i * OPB]);
 
   // ---- 6 residual blocks, hidden 512 streamed in 16 chunks of 32 rows.  Per chunk the
   // packing holds W1 rows [32c, 32c+32) (all K) then W2 columns [32c, 32c+32) (all 8 output
   // blocks): one part in bf16, two parts (W1 | W2) in f32.
   constexpr int FPP = kPart / TR::FRAG;
-  constexpr int NSX = 8 * TR::OPB;                  // k-steps over x (K = 256)
-  constexpr bool W2_OWN_PART = (NSX + 8 * TR::OPB) > FPP;
+  constexpr int NSX = 8 * OPB;                  // k-steps over x (K = 256)
+  constexpr bool W2_OWN_PART = (NSX + 8 * OPB) > FPP;
   for (int layer = 0; layer < 6; ++layer) {
     const float* b1 = sb + kOffB1 + layer * 512;
     const float* b2 = sb + kOffBB2 + layer * 256;
-    for (int c = 0; c < 16; ++c) {
-      st.next();
-      f32x16 hc = f32x16{};
-      KSteps<TR, 0, NSX>::run(st, 0, xb, hc);
-      Op hb[TR::OPB];
-      epilogue_op<TR>(hc, b1 + c * 32, h, true, hb);
-      if (W2_OWN_PART) st.next();
-      const int base = W2_OWN_PART ? 0 : NSX;
+    if constexpr (W2_OWN_PART) {
+      // f32 parity path: W1 chunk and W2 chunk each fill a part; no cross-chunk overlap
+      for (int c = 0; c < 16; ++c) {
+        st.next();
+        f32x16 hc[NCB];
+        const f32x16 bc = bias_block(b1 + c * 32, h);
 #pragma unroll
-      for (int ob = 0; ob < 8; ++ob) KSteps<TR, 0, TR::OPB>::run(st, base + ob * TR::OPB, hb, x[ob]);
+        for (int cb = 0; cb < NCB; ++cb) hc[cb] = bc;
+        run_seq<TR, NSX, NSX, NSX, 1, 1>(st, st.part, 0, xb, hc);
+        Op hb[NCB * OPB];
+#pragma unroll
+        for (int cb = 0; cb < NCB; ++cb) act_op<TR>(hc[cb], true, &hb[cb * OPB]);
+        st.next();
+        run_seq<TR, 8 * OPB, OPB, OPB, 1, 8>(st, st.part, 0, hb, x);
+      }
+    } else {
+      // bf16: part c = [W1 rows of chunk c | W2 columns of chunk c].  Iteration c runs W1 of
+      // chunk c+1 (part c+1) then W2 of chunk c (part c) with chunk c+1's ReLU/convert
+      // epilogue in the W2 MFMA shadow.
+      Op hb[NCB * OPB];
+      st.next();
+      {
+        f32x16 hc[NCB];
+        const f32x16 bc = bias_block(b1, h);
+#pragma unroll
+        for (int cb = 0; cb < NCB; ++cb) hc[cb] = bc;
+        run_seq<TR, NSX, NSX, NSX, 1, 1>(st, st.part, 0, xb, hc);
+#pragma unroll
+        for (int cb = 0; cb < NCB; ++cb) act_op<TR>(hc[cb], true, &hb[cb * OPB]);
+      }
+      for (int c = 0; c < 15; ++c) {
+        st.next();
+        f32x16 hc[NCB];
+        const f32x16 bc = bias_block(b1 + (c + 1) * 32, h);
+#pragma unroll
+        for (int cb = 0; cb < NCB; ++cb) hc[cb] = bc;
+        run_seq<TR, NSX, NSX, NSX, 1, 1>(st, st.part, 0, xb, hc);
+        Op hn[NCB * OPB];
+        // W2 has 16 fragments = 4 groups of 4; group gi converts registers 4gi..4gi+3 of
+        // each hc[cb] (half of operand gi/2)
+        auto epi = [&](int gi) {
+#pragma unroll
+          for (int cb = 0; cb < NCB; ++cb) {
+            float v[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) v[k] = fmaxf(hc[cb][4 * gi + k], 0.0f);
+            TR::to_op4(v, &hn[cb * OPB], gi);
+          }
+        };
+        run_seq<TR, 8 * OPB, OPB, OPB, 1, 8>(st, st.part - 1, NSX, hb, x, epi);
+#pragma unroll
+        for (int i = 0; i < NCB * OPB; ++i) hb[i] = hn[i];
+      }
+      run_seq<TR, 8 * OPB, OPB, OPB, 1, 8>(st, st.part, NSX, hb, x);
     }
 #pragma unroll
     for (int ob = 0; ob < 8; ++ob) {
-      float v[16];
+      const f32x16 b = bias_block(b2 + ob * 32, h);
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        x[ob][r] += b2[ob * 32 + crow(r, h)];
-        v[r] = x[ob][r];
+      for (int cb = 0; cb < NCB; ++cb) {
+        x[cb * 8 + ob] += b;
+        act_op<TR>(x[cb * 8 + ob], false, &xb[(cb * 8 + ob) * OPB]);
       }
-      TR::to_op(v, &xb[ob * TR::OPB]);
     }
   }
 
   // ---- output MLP 256 -> 256 -> 128 -> 3
 #pragma unroll
-  for (int ob = 0; ob < 8; ++ob) acc[ob] = f32x16{};
+  for (int ob = 0; ob < 8; ++ob) {
+    const f32x16 b = bias_block(sb + kOffO0 + ob * 32, h);
+#pragma unroll
+    for (int cb = 0; cb < NCB; ++cb) acc[cb * 8 + ob] = b;
+  }
   st.next();
   dense<TR, 8, 8>(st, xb, acc);
 #pragma unroll
-  for (int ob = 0; ob < 8; ++ob) epilogue_op<TR>(acc[ob], sb + kOffO0 + ob * 32, h, true, &xb[ob * TR::OPB]);
+  for (int i = 0; i < NCB * 8; ++i) act_op<TR>(acc[i], true, &xb[i * OPB]);
 #pragma unroll
-  for (int ob = 0; ob < 4; ++ob) acc[ob] = f32x16{};
+  for (int ob = 0; ob < 4; ++ob) {
+    const f32x16 b = bias_block(sb + kOffO2 + ob * 32, h);
+#pragma unroll
+    for (int cb = 0; cb < NCB; ++cb) acc[cb * 8 + ob] = b;
+  }
   st.next();
   dense<TR, 4, 8>(st, xb, acc);
-  Op o2[4 * TR::OPB];
+  Op o2[NCB * 4 * OPB];
 #pragma unroll
-  for (int ob = 0; ob < 4; ++ob) epilogue_op<TR>(acc[ob], sb + kOffO2 + ob * 32, h, true, &o2[ob * TR::OPB]);
-  acc[0] = f32x16{};
+  for (int cb = 0; cb < NCB; ++cb)
+#pragma unroll
+    for (int ob = 0; ob < 4; ++ob) act_op<TR>(acc[cb * 8 + ob], true, &o2[(cb * 4 + ob) * OPB]);
+#pragma unroll
+  for (int cb = 0; cb < NCB; ++cb) acc[cb * 8] = f32x16{};
   st.next();
   dense<TR, 1, 4>(st, o2, acc);
-  if (valid && h == 0) {
-    out[p * 3 + 0] = acc[0][0] + sb[kOffO4 + 0];
-    out[p * 3 + 1] = acc[0][1] + sb[kOffO4 + 1];
-    out[p * 3 + 2] = acc[0][2] + sb[kOffO4 + 2];
+#pragma unroll
+  for (int cb = 0; cb < NCB; ++cb) {
+    if (p[cb] < P && h == 0) {
+      out[p[cb] * 3 + 0] = acc[cb * 8][0] + sb[kOffO4 + 0];
+      out[p[cb] * 3 + 1] = acc[cb * 8][1] + sb[kOffO4 + 1];
+      out[p[cb] * 3 + 2] = acc[cb * 8][2] + sb[kOffO4 + 2];
+    }
   }
 }
 
@@ -317,9 +496,9 @@ template <class TR>
 static int launch_noise_mlp(const float* pts, int64_t P, int64_t T, const float* cond,
                             int64_t nclouds, const void* blob, int64_t blob_bytes,
                             const float* bias, float* out, hipStream_t s) {
-  constexpr int PTS = TR::THREADS / 64 * 32;
+  constexpr int PTS = TR::THREADS / 64 * 32 * TR::NCB;
   const int nparts = (int)(blob_bytes / kPart);
-  const size_t lds = 2 * kPart + (kBiasFloats + kCondSlots * 256) * sizeof(float);
+  const size_t lds = Streamer<TR>::kSlots * kPart + (kBiasFloats + kCondSlots * 256) * sizeof(float);
   hipLaunchKernelGGL(noise_mlp_kernel<TR>, dim3((unsigned)cdiv(P, PTS)), dim3(TR::THREADS), lds, s,
                      pts, P, T, cond, nclouds, (const char*)blob, nparts, bias, out);
   return PCST_OK;

@@ -485,6 +485,90 @@ def gen_trainer_and_checkpoint():
     print("wrote checkpoint_manifest.json")
 
 
+from gen_sketch import gradient_sketch  # noqa: E402
+
+
+def gen_trainer_sketch():
+    """The trainer step of trainer_step.npz in fp32 and in fp64 (weights, data and every
+    random draw identical: both replay that fixture's recorded draws), stored as
+    32-projection sketches of each parameter gradient plus the exact normwise distance of
+    the fp32 gradient from the fp64 one -- the reference's own fp32 error, which is the
+    yardstick for ours."""
+    from training.trainer import DiffusionTrainer
+    from utils.ema import ExponentialMovingAverage
+
+    def run(dtype):
+        torch.set_default_dtype(dtype)
+        try:
+            cfg = Config(total_points=4096, global_points=1024, use_amp=False,
+                         gradient_accumulation_steps=1, experiment_name="golden_sketch")
+            tr = DiffusionTrainer(cfg, device="cpu")
+            load_into(tr.model)
+            tr.model.to(dtype)
+            tr.optimizer = torch.optim.AdamW(tr.model.parameters(), lr=cfg.learning_rate,
+                                             weight_decay=cfg.weight_decay, betas=(0.9, 0.95))
+            tr.ema = ExponentialMovingAverage(tr.model.parameters(), decay=cfg.ema_decay)
+            for mod in tr.model.modules():
+                if isinstance(mod, torch.nn.Dropout):
+                    mod.p = 0.0
+            grads = {}
+            o_step = tr.optimizer.step
+
+            def step(*a, **k):
+                for n, p in tr.model.named_parameters():
+                    grads[n] = p.grad.detach().double().clone()
+                return o_step(*a, **k)
+
+            tr.optimizer.step = step
+            sim = np.stack([lidar_like_cloud(91, 4096), lidar_like_cloud(92, 4096)])
+            real = np.stack([lidar_like_cloud(93, 4096), lidar_like_cloud(94, 4096)])
+            tr.train_one_epoch([{"sim_full": torch.from_numpy(sim).to(dtype),
+                                 "real_full": torch.from_numpy(real).to(dtype)}])
+            return grads
+        finally:
+            torch.set_default_dtype(torch.float32)
+
+    # both runs replay the draws recorded for trainer_step.npz, so the fp32 run IS that step
+    z = np.load(os.path.join(HERE, "trainer_step.npz"))
+    draws = [(str(n), torch.from_numpy(z[f"rng_{i}"])) for i, n in enumerate(z["rng_names"])]
+    orig = {n: getattr(torch, n) for n in RNGRecorder.NAMES}
+    pos = [0]
+
+    def replay(name, dtype):
+        def f(*a, **k):
+            n, v = draws[pos[0]]
+            pos[0] += 1
+            assert n == name, (n, name)
+            return v.to(dtype) if v.is_floating_point() else v.clone()
+        return f
+
+    grads = {}
+    for dtype in (torch.float32, torch.float64):
+        pos[0] = 0
+        for n in RNGRecorder.NAMES:
+            setattr(torch, n, replay(n, dtype))
+        try:
+            grads[dtype] = run(dtype)
+        finally:
+            for n, f in orig.items():
+                setattr(torch, n, f)
+        assert pos[0] == len(draws)
+    g32, g64 = grads[torch.float32], grads[torch.float64]
+    ref = z["grad_abs"]
+    for i, n in enumerate(g32):  # the fp32 run reproduces trainer_step.npz
+        if n.endswith(".bias") and "mlp_convs" in n:
+            continue  # pre-BN conv biases: rounding noise only
+        assert abs(g32[n].abs().sum().item() - ref[i]) <= 1e-5 * ref[i], n
+    names = list(g32)
+    out = {"param_names": np.array(names),
+           "sk32": np.stack([gradient_sketch(g32[n].numpy(), i) for i, n in enumerate(names)]),
+           "sk64": np.stack([gradient_sketch(g64[n].numpy(), i) for i, n in enumerate(names)]),
+           "rel32": np.array([(g32[n] - g64[n]).norm().item() / max(g64[n].norm().item(), 1e-300)
+                              for n in names]),
+           "norm64": np.array([g64[n].norm().item() for n in names])}
+    save("trainer_sketch.npz", **out)
+
+
 def gen_inference_cfg1():
     """BASELINE config 1: scripts/inference.py on CPU, 2048x3 .npy, 10 steps."""
     from utils.checkpoint import CheckpointManager
@@ -514,10 +598,11 @@ def gen_inference_cfg1():
 
 if __name__ == "__main__":
     which = sys.argv[1:] or ["geometry", "encoder", "noise", "hier", "sched", "sampling",
-                             "trainer", "cfg1"]
+                             "trainer", "cfg1", "trainer_sketch"]
     fns = {"geometry": gen_geometry, "encoder": gen_encoder, "noise": gen_noise_predictor,
            "hier": gen_hierarchical, "sched": gen_schedule_and_losses, "sampling": gen_sampling,
-           "trainer": gen_trainer_and_checkpoint, "cfg1": gen_inference_cfg1}
+           "trainer": gen_trainer_and_checkpoint, "cfg1": gen_inference_cfg1,
+           "trainer_sketch": gen_trainer_sketch}
     for w in which:
         torch.manual_seed(0)
         fns[w]()

@@ -13,7 +13,7 @@ import numpy as np
 import pytest
 import torch
 
-from conftest import assert_close, assert_mostly_close
+from conftest import assert_mostly_close
 
 pytestmark = pytest.mark.gpu
 
@@ -54,21 +54,46 @@ def test_trainer_step(golden, tmp_path, monkeypatch):
     np.testing.assert_allclose(avg, float(g["avg_loss"]), rtol=1e-4)
     names = [str(n) for n in g["param_names"]]
     assert names == list(grads)
-    # gradients: normwise per tensor (sums of |g| and the first 8 entries), 1e-3 rel -- the
-    # loss sums ~10^5 Chamfer terms whose fp32 order differs from the reference's bmm.
-    gabs = np.array([grads[n].abs().sum().item() for n in names])
-    np.testing.assert_allclose(gabs, g["grad_abs"], rtol=1e-3)
-    head = np.stack([np.pad(grads[n].flatten()[:8].numpy(), (0, 8 - min(8, grads[n].numel())))
-                     for n in names])
+    # Gradients against the reference's own fp32 accuracy.  tests/golden/trainer_sketch.npz
+    # holds, for this exact step, 32 random projections of each gradient as the reference
+    # computes it in fp32 and in fp64 (same draws), and the exact normwise error of its fp32
+    # gradient vs fp64 (~1-2e-3: the Chamfer term's |p|^2+|q|^2-2pq cancels).  Ours must be
+    # within 4x that error of the fp64 gradient (the 32-projection estimate is good to
+    # ~+-15%).  Conv biases in front of a train-mode BatchNorm have an analytically zero
+    # gradient (fp64: ~1e-15); both fp32 sides hold rounding noise there, so those must only
+    # be negligible next to their conv weight's.
+    import re
+
+    from gen_sketch import gradient_sketch
+
+    sk = golden("trainer_sketch.npz")
+    assert [str(n) for n in sk["param_names"]] == names
+    pre_bn = re.compile(r"style_encoder\.encoder\.sa\d\.mlp_convs\.\d+\.bias$")
+    bad = []
     for i, n in enumerate(names):
-        scale = max(np.abs(g["grad_head"][i]).max(), g["grad_abs"][i] / max(grads[n].numel(), 1))
-        np.testing.assert_allclose(head[i], g["grad_head"][i], rtol=1e-3, atol=1e-3 * scale,
-                                   err_msg=n)
+        gabs = grads[n].abs().sum().item()
+        if pre_bn.search(n):
+            wabs = grads[n[:-4] + "weight"].abs().sum().item()
+            if gabs > 1e-3 * wabs:
+                bad.append(f"{n}: pre-BN bias sum|g| {gabs:.3e} vs weight {wabs:.3e}")
+            continue
+        s_ours = gradient_sketch(grads[n].numpy(), i)
+        err = np.linalg.norm(s_ours - sk["sk64"][i]) / np.linalg.norm(sk["sk64"][i])
+        if err > 4 * sk["rel32"][i] + 1e-6:
+            bad.append(f"{n}: |ours - fp64| ~ {err:.2e} vs reference fp32 {sk['rel32'][i]:.2e}")
+    assert not bad, "\n".join(bad)
+    # AdamW + EMA: parameter sums after the step.  Adam's first step moves every element by
+    # ~lr * sign(g), so an element whose gradient is at rounding level can flip by 2 lr:
+    # allow that for 1% of the elements (all of them for the pre-BN biases).
     sd = tr.model.state_dict()
-    after = np.array([sd[n].double().sum().item() for n in names])
-    np.testing.assert_allclose(after, g["param_after_sum"], rtol=1e-5, atol=1e-4)
-    ema = np.array([p.double().sum().item() for p in tr.ema.shadow_params])
-    np.testing.assert_allclose(ema, g["ema_after_sum"], rtol=1e-5, atol=1e-4)
+    ema = {n: p.double().sum().item() for n, p in zip(names, tr.ema.shadow_params)}
+    for i, n in enumerate(names):
+        flips = sd[n].numel() if pre_bn.search(n) else 1 + 0.01 * sd[n].numel()
+        tol = 2 * cfg.learning_rate * flips
+        got = sd[n].double().sum().item()
+        assert abs(got - g["param_after_sum"][i]) <= tol + 1e-5 * abs(g["param_after_sum"][i]), n
+        e_tol = (1 - cfg.ema_decay) * tol + 1e-5 * abs(g["ema_after_sum"][i]) + 1e-6
+        assert abs(ema[n] - g["ema_after_sum"][i]) <= e_tol, n
 
 
 def test_inference_cfg1(golden, tmp_path, monkeypatch):
