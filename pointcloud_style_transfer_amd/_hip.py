@@ -14,7 +14,8 @@ import os
 import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libpcst_hip.so")
+# PCST_LIB overrides the library path (instrumented experiment builds only)
+LIB_PATH = os.environ.get("PCST_LIB") or os.path.join(_HERE, "libpcst_hip.so")
 
 _P = ctypes.c_void_p
 _I = ctypes.c_int64

@@ -16,10 +16,9 @@ struct StatRec {
   double s[3], ss[3];
 };
 
-__global__ __launch_bounds__(256) void cloud_stats_partial_kernel(const float* __restrict__ pts,
-                                                                  int N, StatRec* __restrict__ part) {
-  const int b = blockIdx.y, blk = blockIdx.x;
-  const float* P = pts + (int64_t)b * N * 3;
+// One 256-thread block's partial record (block blk of kStatBlocks) of cloud P: part[blk].
+__device__ __forceinline__ void cloud_stats_block(const float* __restrict__ P, int N, int blk,
+                                                  StatRec* __restrict__ part) {
   float mn[3] = {3.4e38f, 3.4e38f, 3.4e38f}, mx[3] = {-3.4e38f, -3.4e38f, -3.4e38f};
   double s[3] = {0, 0, 0}, ss[3] = {0, 0, 0};
   for (int n = blk * 256 + threadIdx.x; n < N; n += kStatBlocks * 256) {
@@ -59,8 +58,14 @@ __global__ __launch_bounds__(256) void cloud_stats_partial_kernel(const float* _
         r.s[c] += w[q].s[c];
         r.ss[c] += w[q].ss[c];
       }
-    part[b * kStatBlocks + blk] = r;
+    part[blk] = r;
   }
+}
+
+__global__ __launch_bounds__(256) void cloud_stats_partial_kernel(const float* __restrict__ pts,
+                                                                  int N, StatRec* __restrict__ part) {
+  const int b = blockIdx.y;
+  cloud_stats_block(pts + (int64_t)b * N * 3, N, blockIdx.x, part + b * kStatBlocks);
 }
 
 // Fold the partial records of cloud b (fixed order: deterministic).

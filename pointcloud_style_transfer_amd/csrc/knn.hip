@@ -8,184 +8,379 @@
 //                  exact ties -> lower j; w = 1/(sqrt(rdist)+1e-8), w /= ((w0+w1)+w2),
 //                  value = ((v0*w0 + v1*w1) + v2*w2) in float64, rounded to float32.
 //
-// Exact search on a uniform grid whose cell size follows the cloud's PEAK density (estimated
-// from the per-axis spread, ~3 refs per cell where the cloud is densest), so a dense core is
-// not searched through overfull cells.  Refs and queries are both counting-sorted by cell:
-// neighbouring lanes search neighbouring cells (coherent loads, similar trip counts).  Each
-// candidate is screened with an fp32 distance (relative error < 3e-7, screened against the
-// current 3rd-best x (1 + 2e-6)) and only survivors are ranked in exact float64.
+// Grid.  A uniform grid whose cell size follows the cloud's PEAK density (about kRefsPerCell
+// refs per cell where the cloud is densest).  Cells are numbered brick-major: 4x4x4-cell
+// bricks in row-major order, Morton order inside a brick, so consecutive cell ids form a
+// compact box and a brick's refs are one contiguous range.  Refs and the unknown rows
+// (queries) are counting-sorted by cell.
+//
+// Query pass (wave-cooperative).  One wave per chunk of <= 64 queries of one brick (the scan
+// kernel cuts the chunks).  Two passes, the second over refs the first did not visit:
+//   1. the cells of the chunk's cell bounding box grown by one cell;
+//   2. for lanes not yet settled that hold 3 refs: the cells of the union of their balls (the
+//      current 3rd distance bounds the true one, so a lane's ball holds its answer).
+// A lane is settled once its 3rd-best distance is below the distance to the unscanned region.
+// The refs of a pass are gathered into the wave's LDS window by LDS-DMA (global_load_lds, a
+// per-lane source address: a balanced copy, each lane finds the cell of its slot by a binary
+// search over the lanes' offsets) and every lane screens every staged ref: the fp32 three
+// smallest distances are kept branch-free, then only refs within (1 + 2e-6) of the fp32 3rd
+// best are ranked in exact float64.  Pass 2 runs under a staging budget (a wave's time is
+// bounded); lanes still open after it (sparse neighbourhoods: in the bench trajectory ~0.05 %
+// of the queries, which a wave-wide staging pass would serve at the cost of the kernel's tail)
+// go to the outlier list: one workgroup per outlier query scans every ref (knn_outlier_kernel).
+//
+// Launches: memset, pre (cloud stats + known rows), count (grid params, per-cell counts with
+// each element's rank in its cell, per-tile sums, known-row copies), scan (single pass: tile
+// offsets from the per-tile sums; the chunk list), fill (no atomics: start + rank), query,
+// outlier.
 #include "common.h"
 #include "cloud.h"
 
 namespace pcst {
 
-constexpr int kRingMax = 4;  // shells searched per query before the exhaustive outlier pass
+constexpr double kRefsPerCell = 8.0;     // refs per cell at the cloud's peak density
+constexpr int kCandCap = 512;            // LDS candidates per wave
+constexpr int kBallCells = 512;          // largest cell box one lane's ball may ask for
+constexpr int kBallUnion = 1024;         // largest union box of a ball pass
+constexpr uint32_t kBallBudget = 2048;   // refs the ball pass may stage
+constexpr int kKnnTile = 4096;           // scan tile (256 threads x 16)
+constexpr int kKnnMaxTiles = 1024;       // per-block LDS tile histogram in the count kernel
+constexpr int kPreKnownBlocks = 64;      // known-row scatter blocks per cloud in the pre kernel
+constexpr int kCountPerBlock = 1024;     // elements per count-kernel block (4 per thread)
+constexpr int kQueryBlocks = 1024;       // query workgroups per cloud (grid-stride over chunks)
+constexpr int kOutlierThreads = 1024;    // one outlier query per workgroup
+constexpr int kOutlierBlocks = 128;      // outlier workgroups per cloud
+
+#ifdef KNN_TRACE  // experiment builds only: per-chunk pass timings (tools/knn_trace.py)
+__device__ unsigned long long g_knn_trace[2 * 32768 * 8];
+#endif
 
 struct KnnWS {
   StatRec* stats;    // [B][kStatBlocks]
   float* gp;         // [B][8]: origin xyz, cell size, inv size, dims xyz (int bits)
-  uint32_t* tsum;    // scan scratch
   float4* refs;      // [B][M]   (x, y, z, j) cell-sorted
-  int32_t* qorder;   // [B][N]   point index in cell order
-  int32_t* olist;    // [B][N]   queries left to the exhaustive pass
+  int32_t* qorder;   // [B][N]   query row index in cell order
+  int2* crank;       // [B][M+N] (cell, rank in cell); cell -1 for known rows
+  uint2* chunks;     // [B][maxch] query ranges [q0, q1) of <= 64 queries inside one brick
+  int32_t* olist;    // [B][N]   outlier query rows
   // zeroed every call (contiguous):
   int32_t* err;
+  int32_t* nchunk;   // [B]
   int32_t* ocount;   // [B]
   uint32_t* known;   // [B][N]  (j+1 of the last coarse row writing n, 0 = query)
-  uint32_t* rstart;  // [B][C+1] ref counts -> starts
-  uint32_t* qstart;  // [B][C+1] query counts -> starts
-  uint32_t* rcur;    // [B][C]   fill cursors (offsets from the starts)
-  uint32_t* qcur;    // [B][C]
-  int64_t C;
+  uint64_t* tsum;    // [B][T]  per-tile sums of the packed counts
+  uint64_t* cnt;     // [B][T*kKnnTile] packed counts (refs | queries << 32) -> starts
+  int64_t Cmax, T, Cpad, maxch;
   size_t bytes;
 };
 
-static int64_t knn_cells(int64_t M) { return std::max<int64_t>(4096, 16 * M); }
+static int64_t knn_cells(int64_t M) {
+  return std::min<int64_t>(std::max<int64_t>(4096, 16 * M), (int64_t)kKnnMaxTiles * kKnnTile - 1);
+}
 
 static KnnWS carve_knn(void* base, int64_t B, int64_t N, int64_t M) {
   Carver c(base);
   KnnWS w;
-  w.C = knn_cells(M);
+  w.Cmax = knn_cells(M);
+  w.T = cdiv(w.Cmax + 1, kKnnTile);
+  w.Cpad = w.T * kKnnTile;
+  w.maxch = cdiv(N, 64) + w.Cmax / 64 + 1;
   w.stats = c.take<StatRec>(B * kStatBlocks);
   w.gp = c.take<float>(B * 8);
-  w.tsum = c.take<uint32_t>(scan_tsum_words((int)B, w.C + 1));
   w.refs = c.take<float4>(B * M);
   w.qorder = c.take<int32_t>(B * N);
+  w.crank = c.take<int2>(B * (M + N));
+  w.chunks = c.take<uint2>(B * w.maxch);
   w.olist = c.take<int32_t>(B * N);
   w.err = c.take<int32_t>(4);
+  w.nchunk = c.take<int32_t>(B);
   w.ocount = c.take<int32_t>(B);
   w.known = c.take<uint32_t>(B * N);
-  w.rstart = c.take<uint32_t>(B * (w.C + 1));
-  w.qstart = c.take<uint32_t>(B * (w.C + 1));
-  w.rcur = c.take<uint32_t>(B * w.C);
-  w.qcur = c.take<uint32_t>(B * w.C);
+  w.tsum = c.take<uint64_t>(B * w.T);
+  w.cnt = c.take<uint64_t>(B * w.Cpad);
   w.bytes = c.bytes();
   return w;
 }
 
-// Cell size from the peak density of a Gaussian with the cloud's per-axis spread:
-// rho_max = M / ((2 pi)^1.5 sx sy sz); s^3 = 3 / rho_max.  Capped so the bounding box holds
-// at most C cells (and at most 2048 per axis).
-__global__ __launch_bounds__(64) void knn_grid_params_kernel(const StatRec* __restrict__ stats,
-                                                             int B, int64_t N, int64_t M, int64_t C,
-                                                             float* __restrict__ gp) {
-  const int b = blockIdx.x;  // one wave per cloud
-  const StatRec r = fold_stats_wave(stats, b);
-  if (threadIdx.x != 0) return;
-  double ext[3], sig[3];
-  for (int c = 0; c < 3; ++c) {
-    ext[c] = (double)r.mx[c] - (double)r.mn[c];
-    if (!(ext[c] > 1e-9)) ext[c] = 1e-9;
-    const double mean = r.s[c] / (double)N;
-    double var = r.ss[c] / (double)N - mean * mean;
-    sig[c] = sqrt(fmax(var, 0.0));
-    sig[c] = fmax(sig[c], 1e-3 * ext[c]);
+struct Grid {
+  float o[3], s, inv;
+  int d[3], bx, by;
+  __device__ void load(const float* G) {
+    o[0] = G[0]; o[1] = G[1]; o[2] = G[2];
+    s = G[3]; inv = G[4];
+    d[0] = __float_as_int(G[5]); d[1] = __float_as_int(G[6]); d[2] = __float_as_int(G[7]);
+    bx = (d[0] + 3) >> 2;
+    by = (d[1] + 3) >> 2;
   }
-  const double rho = (double)M / (15.7496099457 * sig[0] * sig[1] * sig[2]);
-  double s = cbrt(6.0 / rho);
-  // a cell must not be smaller than a thin dimension forces: keep at least ~1 ref per
-  // cell on average over the occupied extent
-  int d[3];
-  for (int it = 0; it < 200; ++it) {
-    int64_t tot = 1;
-    for (int c = 0; c < 3; ++c) {
-      d[c] = (int)fmin(2048.0, fmax(1.0, ceil(ext[c] / s)));
-      tot *= d[c];
-    }
-    if (tot <= C) break;
-    s *= 1.1;
-  }
-  float* G = gp + b * 8;
-  G[0] = r.mn[0]; G[1] = r.mn[1]; G[2] = r.mn[2];
-  G[3] = (float)s;
-  G[4] = (float)(1.0 / s);
-  G[5] = __int_as_float(d[0]); G[6] = __int_as_float(d[1]); G[7] = __int_as_float(d[2]);
-}
+};
 
 __device__ __forceinline__ int cell_coord(float p, float o, float inv, int d) {
   int c = (int)floorf((p - o) * inv);
   return c < 0 ? 0 : (c >= d ? d - 1 : c);
 }
 
-__device__ __forceinline__ int64_t cell_of(const float* p, const float* G) {
-  const int dx = __float_as_int(G[5]), dy = __float_as_int(G[6]), dz = __float_as_int(G[7]);
-  const int cx = cell_coord(p[0], G[0], G[4], dx), cy = cell_coord(p[1], G[1], G[4], dy),
-            cz = cell_coord(p[2], G[2], G[4], dz);
-  return ((int64_t)cz * dy + cy) * dx + cx;
+// brick-major cell id: bricks row-major, Morton (x0 y0 z0 x1 y1 z1) inside the brick
+__device__ __forceinline__ int cell_id(int x, int y, int z, const Grid& g) {
+  const int m = (x & 1) | ((y & 1) << 1) | ((z & 1) << 2) | ((x & 2) << 2) | ((y & 2) << 3) |
+                ((z & 2) << 4);
+  return ((((z >> 2) * g.by + (y >> 2)) * g.bx + (x >> 2)) << 6) + m;
 }
 
-__global__ void knn_known_kernel(const int64_t* __restrict__ idx, int64_t N, int64_t M,
-                                 uint32_t* __restrict__ known, int32_t* __restrict__ err) {
+__device__ __forceinline__ int cell_of(const float* p, const Grid& g) {
+  return cell_id(cell_coord(p[0], g.o[0], g.inv, g.d[0]), cell_coord(p[1], g.o[1], g.inv, g.d[1]),
+                 cell_coord(p[2], g.o[2], g.inv, g.d[2]), g);
+}
+
+// Cell size from the peak density of a Gaussian with the cloud's per-axis spread:
+// rho_max = M / ((2 pi)^1.5 sx sy sz); s^3 = kRefsPerCell / rho_max.  Grown until the bricked
+// bounding box holds at most Cmax cells (and at most 2048 per axis).  Called by one whole
+// wave; lane 0 writes G.
+__device__ void knn_grid_params(const StatRec* __restrict__ stats, int b, int64_t N, int64_t M,
+                                int64_t Cmax, float* G) {
+  const StatRec r = fold_stats_wave(stats, b);
+  if ((threadIdx.x & 63) != 0) return;
+  double ext[3], sig[3];
+  for (int c = 0; c < 3; ++c) {
+    ext[c] = (double)r.mx[c] - (double)r.mn[c];
+    if (!(ext[c] > 1e-9)) ext[c] = 1e-9;
+    const double mean = r.s[c] / (double)N;
+    const double var = r.ss[c] / (double)N - mean * mean;
+    sig[c] = sqrt(fmax(var, 0.0));
+    sig[c] = fmax(sig[c], 1e-3 * ext[c]);
+  }
+  const double rho = (double)M / (15.7496099457 * sig[0] * sig[1] * sig[2]);
+  double s = cbrt(kRefsPerCell / rho);
+  int d[3];
+  for (int it = 0; it < 400; ++it) {
+    int64_t tot = 64;
+    for (int c = 0; c < 3; ++c) {
+      d[c] = (int)fmin(2048.0, fmax(1.0, ceil(ext[c] / s)));
+      tot *= (d[c] + 3) >> 2;
+    }
+    if (tot <= Cmax) break;
+    s *= 1.1;
+  }
+  G[0] = r.mn[0]; G[1] = r.mn[1]; G[2] = r.mn[2];
+  G[3] = (float)s;
+  G[4] = (float)(1.0 / s);
+  G[5] = __int_as_float(d[0]); G[6] = __int_as_float(d[1]); G[7] = __int_as_float(d[2]);
+}
+
+// blocks [0, kStatBlocks): cloud statistics; the rest: known[n] = max j+1 with idx[j] == n
+__global__ __launch_bounds__(256) void knn_pre_kernel(const float* __restrict__ orig,
+                                                      const int64_t* __restrict__ idx, int N,
+                                                      int64_t M, StatRec* __restrict__ stats,
+                                                      uint32_t* __restrict__ known,
+                                                      int32_t* __restrict__ err) {
   const int b = blockIdx.y;
-  for (int64_t j = blockIdx.x * 256 + threadIdx.x; j < M; j += gridDim.x * 256) {
+  if (blockIdx.x < kStatBlocks) {
+    cloud_stats_block(orig + (int64_t)b * N * 3, N, blockIdx.x, stats + b * kStatBlocks);
+    return;
+  }
+  const int blk = blockIdx.x - kStatBlocks;
+  for (int64_t j = (int64_t)blk * 256 + threadIdx.x; j < M; j += kPreKnownBlocks * 256) {
     const int64_t n = idx[b * M + j];
     if (n < 0 || n >= N) { atomicOr(err, 1); continue; }
-    atomicMax(&known[b * N + n], (uint32_t)(j + 1));
+    atomicMax(&known[b * (int64_t)N + n], (uint32_t)(j + 1));
   }
 }
 
-// count refs (j < M, point orig[idx[j]]) and queries (all N points) per cell
-__global__ void knn_count_kernel(const float* __restrict__ orig, const int64_t* __restrict__ idx,
-                                 int64_t N, int64_t M, int64_t C, const float* __restrict__ gp,
-                                 uint32_t* __restrict__ rcount, uint32_t* __restrict__ qcount) {
+// Per element e of [refs j < M | rows n = e - M]: its cell and its rank in the cell (the old
+// value of the cell's packed counter), per-tile sums via an LDS histogram; known rows copy
+// their coarse value to the output here.  Each thread handles 4 elements with their atomics
+// in flight together.
+__global__ __launch_bounds__(256) void knn_count_kernel(
+    const float* __restrict__ orig, const float* __restrict__ coarse,
+    const int64_t* __restrict__ idx, const StatRec* __restrict__ stats,
+    const uint32_t* __restrict__ known, int64_t N, int64_t M, int64_t Cmax, int64_t T,
+    int64_t Cpad, float* __restrict__ gp, uint64_t* __restrict__ cnt, uint64_t* __restrict__ tsum,
+    int2* __restrict__ crank, float* __restrict__ out) {
+  constexpr int U = kCountPerBlock / 256;
   const int b = blockIdx.y;
-  const float* G = gp + b * 8;
-  for (int64_t e = blockIdx.x * 256 + threadIdx.x; e < M + N; e += gridDim.x * 256) {
+  __shared__ float Gs[8];
+  __shared__ unsigned long long th[kKnnMaxTiles];
+  if (threadIdx.x < 64) knn_grid_params(stats, b, N, M, Cmax, Gs);
+  for (int t = threadIdx.x; t < T; t += 256) th[t] = 0ull;
+  __syncthreads();
+  if (blockIdx.x == 0 && threadIdx.x < 8) gp[b * 8 + threadIdx.x] = Gs[threadIdx.x];
+  Grid g;
+  g.load(Gs);
+  uint64_t* Cn = cnt + b * Cpad;
+  const int64_t e0 = (int64_t)blockIdx.x * kCountPerBlock + threadIdx.x;
+  int cell[U];
+  unsigned long long inc[U], old[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int64_t e = e0 + u * 256;
+    cell[u] = -1;
+    inc[u] = 0ull;
     if (e < M) {
       int64_t n = idx[b * M + e];
       n = n < 0 ? 0 : (n >= N ? N - 1 : n);
-      atomicAdd(&rcount[b * (C + 1) + cell_of(orig + (b * N + n) * 3, G)], 1u);
-    } else {
+      cell[u] = cell_of(orig + (b * N + n) * 3, g);
+      inc[u] = 1ull;
+    } else if (e < M + N) {
       const int64_t n = e - M;
-      atomicAdd(&qcount[b * (C + 1) + cell_of(orig + (b * N + n) * 3, G)], 1u);
+      const uint32_t kn = known[b * N + n];
+      if (kn) {
+        const float* v = coarse + (b * M + (int64_t)(kn - 1)) * 3;
+        float* o = out + (b * N + n) * 3;
+        o[0] = v[0]; o[1] = v[1]; o[2] = v[2];
+      } else {
+        cell[u] = cell_of(orig + (b * N + n) * 3, g);
+        inc[u] = 1ull << 32;
+      }
     }
+  }
+#pragma unroll
+  for (int u = 0; u < U; ++u)
+    old[u] = cell[u] >= 0 ? atomicAdd((unsigned long long*)&Cn[cell[u]], inc[u]) : 0ull;
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int64_t e = e0 + u * 256;
+    if (e >= M + N) continue;
+    int2 cr = make_int2(-1, 0);
+    if (cell[u] >= 0) {
+      atomicAdd(&th[cell[u] / kKnnTile], inc[u]);
+      cr = make_int2(cell[u], (int)(uint32_t)(e < M ? old[u] : old[u] >> 32));
+    }
+    crank[b * (M + N) + e] = cr;
+  }
+  __syncthreads();
+  for (int t = threadIdx.x; t < T; t += 256)
+    if (th[t]) atomicAdd((unsigned long long*)&tsum[b * T + t], th[t]);
+}
+
+__device__ __forceinline__ uint64_t block_excl_scan_256_u64(uint64_t v, unsigned long long* sh,
+                                                            uint64_t& total) {
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  uint64_t x = v;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const uint64_t y = __shfl_up(x, off);
+    if (lane >= off) x += y;
+  }
+  if (lane == 63) sh[w] = x;
+  __syncthreads();
+  uint64_t wofs = 0;
+  for (int q = 0; q < w; ++q) wofs += sh[q];
+  total = sh[0] + sh[1] + sh[2] + sh[3];
+  return wofs + x - v;
+}
+
+// Exclusive scan of the packed counts in place (the tile offset is the sum of the earlier
+// tiles' sums: at most kKnnMaxTiles words, read by the whole block), then the tile's 64
+// bricks are cut into chunks of <= 64 queries appended to the cloud's chunk list (order free:
+// chunks are independent).
+__global__ __launch_bounds__(256) void knn_scan_kernel(uint64_t* __restrict__ cnt,
+                                                       const uint64_t* __restrict__ tsum,
+                                                       int64_t T, int64_t Cpad,
+                                                       uint2* __restrict__ chunks, int64_t maxch,
+                                                       int32_t* __restrict__ nchunk) {
+  const int b = blockIdx.y, tile = blockIdx.x;
+  __shared__ unsigned long long buf[kKnnTile + kKnnTile / 32];
+  __shared__ unsigned long long sh[8];
+  auto pad = [](int i) { return i + (i >> 5); };
+  uint64_t* D = cnt + b * Cpad + (int64_t)tile * kKnnTile;
+  uint64_t pre = 0;
+  for (int t = threadIdx.x; t < tile; t += 256) pre += tsum[b * T + t];
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) pre += __shfl_xor(pre, off);
+  if ((threadIdx.x & 63) == 0) sh[4 + (threadIdx.x >> 6)] = pre;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) buf[pad(k * 256 + threadIdx.x)] = D[k * 256 + threadIdx.x];
+  __syncthreads();
+  const uint64_t base = sh[4] + sh[5] + sh[6] + sh[7];
+  uint64_t v[16], s = 0;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    v[k] = buf[pad(threadIdx.x * 16 + k)];
+    s += v[k];
+  }
+  uint64_t tot;
+  uint64_t run = block_excl_scan_256_u64(s, sh, tot) + base;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    buf[pad(threadIdx.x * 16 + k)] = run;
+    run += v[k];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < 16; ++k) D[k * 256 + threadIdx.x] = buf[pad(k * 256 + threadIdx.x)];
+  if (threadIdx.x < 64) {
+    const int t = threadIdx.x;
+    const uint32_t q0 = (uint32_t)(buf[pad(t * 64)] >> 32);
+    const uint32_t q1 = (uint32_t)((t < 63 ? buf[pad(t * 64 + 64)] : base + tot) >> 32);
+    const uint32_t nch = (q1 - q0 + 63) / 64;
+    uint32_t off = nch;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = __shfl_up(off, o);
+      if (t >= o) off += y;
+    }
+    const uint32_t all = __shfl(off, 63);
+    off -= nch;
+    uint32_t at = 0;
+    if (t == 0 && all) at = (uint32_t)atomicAdd(&nchunk[b], (int32_t)all);
+    at = __shfl(at, 0);
+    uint2* Ch = chunks + b * maxch + at + off;
+    for (uint32_t i = 0; i < nch; ++i)
+      Ch[i] = make_uint2(q0 + 64 * i, min(q0 + 64 * (i + 1), q1));
   }
 }
 
-__global__ void knn_fill_kernel(const float* __restrict__ orig, const int64_t* __restrict__ idx,
-                                int64_t N, int64_t M, int64_t C, const float* __restrict__ gp,
-                                const uint32_t* __restrict__ rstart,
-                                const uint32_t* __restrict__ qstart, uint32_t* __restrict__ rcur,
-                                uint32_t* __restrict__ qcur, float4* __restrict__ refs,
-                                int32_t* __restrict__ qorder) {
+__global__ __launch_bounds__(256) void knn_fill_kernel(const float* __restrict__ orig,
+                                                       const int64_t* __restrict__ idx, int64_t N,
+                                                       int64_t M, int64_t Cpad,
+                                                       const uint64_t* __restrict__ start,
+                                                       const int2* __restrict__ crank,
+                                                       float4* __restrict__ refs,
+                                                       int32_t* __restrict__ qorder) {
   const int b = blockIdx.y;
-  const float* G = gp + b * 8;
-  for (int64_t e = blockIdx.x * 256 + threadIdx.x; e < M + N; e += gridDim.x * 256) {
+  const uint64_t* S = start + b * Cpad;
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < M + N; e += gridDim.x * 256) {
+    const int2 cr = crank[b * (M + N) + e];
+    if (cr.x < 0) continue;
     if (e < M) {
       int64_t n = idx[b * M + e];
       n = n < 0 ? 0 : (n >= N ? N - 1 : n);
       const float* p = orig + (b * N + n) * 3;
-      const int64_t c = cell_of(p, G);
-      const uint32_t pos = rstart[b * (C + 1) + c] + atomicAdd(&rcur[b * C + c], 1u);
+      const uint32_t pos = (uint32_t)S[cr.x] + (uint32_t)cr.y;
       refs[b * M + pos] = make_float4(p[0], p[1], p[2], __int_as_float((int)e));
     } else {
-      const int64_t n = e - M;
-      const int64_t c = cell_of(orig + (b * N + n) * 3, G);
-      const uint32_t pos = qstart[b * (C + 1) + c] + atomicAdd(&qcur[b * C + c], 1u);
-      qorder[b * N + pos] = (int32_t)n;
+      const uint32_t pos = (uint32_t)(S[cr.x] >> 32) + (uint32_t)cr.y;
+      qorder[b * N + pos] = (int32_t)(e - M);
     }
   }
 }
 
 struct Top3 {
-  double d[3];
-  int j[3];
+  // named fields, not arrays: a runtime index would put an array in scratch
+  double d0, d1, d2;
+  int j0, j1, j2;
   __device__ void init() {
-    for (int k = 0; k < 3; ++k) { d[k] = INFINITY; j[k] = 0x7fffffff; }
+    d0 = d1 = d2 = INFINITY;
+    j0 = j1 = j2 = 0x7fffffff;
+  }
+  // kk-th best (kk in 1..3; a compile-time constant at every call site)
+  __device__ __forceinline__ double last(int kk) const {
+    return kk >= 3 ? d2 : (kk == 2 ? d1 : d0);
   }
   __device__ __forceinline__ void push(double dd, int jj) {
-    // lexicographic (distance, j): deterministic whatever the in-cell order
-    if (dd > d[2] || (dd == d[2] && jj >= j[2])) return;
-    if (dd < d[1] || (dd == d[1] && jj < j[1])) {
-      d[2] = d[1]; j[2] = j[1];
-      if (dd < d[0] || (dd == d[0] && jj < j[0])) {
-        d[1] = d[0]; j[1] = j[0];
-        d[0] = dd; j[0] = jj;
+    // lexicographic (distance, j): deterministic whatever the visiting order (a ref is never
+    // offered twice; the j guard would keep a repeat harmless)
+    if (dd > d2 || (dd == d2 && jj >= j2)) return;
+    if (jj == j0 || jj == j1) return;
+    if (dd < d1 || (dd == d1 && jj < j1)) {
+      d2 = d1; j2 = j1;
+      if (dd < d0 || (dd == d0 && jj < j0)) {
+        d1 = d0; j1 = j0;
+        d0 = dd; j0 = jj;
       } else {
-        d[1] = dd; j[1] = jj;
+        d1 = dd; j1 = jj;
       }
     } else {
-      d[2] = dd; j[2] = jj;
+      d2 = dd; j2 = jj;
     }
   }
 };
@@ -193,153 +388,404 @@ struct Top3 {
 // IDW of the reference (float64, sequential sums), rounded to float32
 __device__ __forceinline__ void idw_write(const Top3& t, int kk, const float* __restrict__ V,
                                           float* __restrict__ O) {
-  double w[3], wsum = 0.0;
-  for (int i = 0; i < kk; ++i) {
-    w[i] = __ddiv_rn(1.0, dadd(__dsqrt_rn(t.d[i]), 1e-8));
-    wsum = i == 0 ? w[0] : dadd(wsum, w[i]);
-  }
-  for (int i = 0; i < kk; ++i) w[i] = __ddiv_rn(w[i], wsum);
+  const double w0 = __ddiv_rn(1.0, dadd(__dsqrt_rn(t.d0), 1e-8));
+  const double w1 = kk > 1 ? __ddiv_rn(1.0, dadd(__dsqrt_rn(t.d1), 1e-8)) : 0.0;
+  const double w2 = kk > 2 ? __ddiv_rn(1.0, dadd(__dsqrt_rn(t.d2), 1e-8)) : 0.0;
+  double wsum = w0;
+  if (kk > 1) wsum = dadd(wsum, w1);
+  if (kk > 2) wsum = dadd(wsum, w2);
+  const double u0 = __ddiv_rn(w0, wsum), u1 = __ddiv_rn(w1, wsum), u2 = __ddiv_rn(w2, wsum);
+  const float* v0 = V + (int64_t)t.j0 * 3;
+  const float* v1 = V + (int64_t)(kk > 1 ? t.j1 : t.j0) * 3;
+  const float* v2 = V + (int64_t)(kk > 2 ? t.j2 : t.j0) * 3;
+#pragma unroll
   for (int c = 0; c < 3; ++c) {
-    double acc = 0.0;
-    for (int i = 0; i < kk; ++i) {
-      const double term = dmul((double)V[(int64_t)t.j[i] * 3 + c], w[i]);
-      acc = i == 0 ? term : dadd(acc, term);
-    }
+    double acc = dmul((double)v0[c], u0);
+    if (kk > 1) acc = dadd(acc, dmul((double)v1[c], u1));
+    if (kk > 2) acc = dadd(acc, dmul((double)v2[c], u2));
     O[c] = (float)acc;
   }
 }
 
-__global__ __launch_bounds__(256) void knn_query_kernel(
-    const float* __restrict__ orig, const float* __restrict__ vals, int64_t N, int64_t M,
-    int64_t C, const float* __restrict__ gp, const uint32_t* __restrict__ known,
-    const uint32_t* __restrict__ rstart, const float4* __restrict__ refs,
-    const int32_t* __restrict__ qorder, int32_t* __restrict__ olist, int32_t* __restrict__ ocount,
-    float* __restrict__ out) {
-  const int b = blockIdx.y;
-  const int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (k >= N) return;
-  const int64_t n = qorder[b * N + k];
-  const float* V = vals + b * M * 3;
-  float* O = out + (b * N + n) * 3;
-  const uint32_t kn = known[b * N + n];
-  if (kn) {
-    const float* v = V + (int64_t)(kn - 1) * 3;
-    O[0] = v[0]; O[1] = v[1]; O[2] = v[2];
-    return;
-  }
-  const float* G = gp + b * 8;
-  const int dx = __float_as_int(G[5]), dy = __float_as_int(G[6]), dz = __float_as_int(G[7]);
-  const float* q = orig + (b * N + n) * 3;
-  const float fx = q[0], fy = q[1], fz = q[2];
-  const double qx = fx, qy = fy, qz = fz;
-  const int cx = cell_coord(fx, G[0], G[4], dx), cy = cell_coord(fy, G[1], G[4], dy),
-            cz = cell_coord(fz, G[2], G[4], dz);
-  const double ox = G[0], oy = G[1], oz = G[2], s = G[3];
-  const double slack = 1e-5 * s;  // covers fp32 cell-assignment rounding
-  const uint32_t* RS = rstart + b * (C + 1);
-  const float4* R = refs + b * M;
-  const int kk = M < 3 ? (int)M : 3;
+__device__ __forceinline__ float dist32(float fx, float fy, float fz, float4 r) {
+  const float ex = fx - r.x, ey = fy - r.y, ez = fz - r.z;
+  return fmaf(ez, ez, fmaf(ey, ey, ex * ex));
+}
+
+// One query: an fp32 screen and the exact (float64) top-3.
+//   consider(): one candidate at a time (outlier pass): screen against the exact 3rd best.
+//   window():   a staged window of candidates in two phases.  Phase 1 keeps the fp32 three
+//               smallest distances branch-free (min / med3 / med3); phase 2 screens the window
+//               against that fp32 3rd best into a register mask per 64 refs; the survivors
+//               (~3 per lane) are then ranked in float64 by each lane alone.  Every member of the exact top-3 survives
+//               its window's screen: its fp32 distance is within (1 + 3e-7)^2 of its float64
+//               one, and the fp32 3rd best bounds the float64 3rd best the same way (a ref must
+//               never reach phase 1 twice: a repeat would shrink the fp32 3rd best).
+struct Query {
+  float fx, fy, fz;
+  double qx, qy, qz;
   Top3 t;
-  t.init();
-  float thr = INFINITY;  // fp32 screen: candidates above it cannot enter the top k
-  const int rall = max(dx, max(dy, dz));
-  const int rmax = min(rall, kRingMax);
-  bool done = false;
-  // refs of consecutive cells of one (z, y) row are contiguous (row-major counting sort), so
-  // a shell is visited as row RANGES: whole rows on its faces, the two end cells inside
-  auto scan = [&](uint32_t a, uint32_t e) {
-    for (uint32_t i = a; i < e; ++i) {
-      const float4 ref = R[i];
-      const float ex = fx - ref.x, ey = fy - ref.y, ez = fz - ref.z;
-      const float d32 = fmaf(ez, ez, fmaf(ey, ey, ex * ex));
-      if (d32 > thr) continue;
-      const double ux = dsub(qx, (double)ref.x), uy = dsub(qy, (double)ref.y),
-                   uz = dsub(qz, (double)ref.z);
-      const double d = dadd(dadd(dmul(ux, ux), dmul(uy, uy)), dmul(uz, uz));
-      t.push(d, __float_as_int(ref.w));
-      if (t.d[kk - 1] != INFINITY) thr = (float)(t.d[kk - 1] * (1.0 + 2e-6)) + 1e-30f;
+  float thr;            // exact-path screen (from the float64 3rd best)
+  float c0, c1, c2;     // fp32 three smallest distances seen (window path)
+  __device__ void init(float x, float y, float z) {
+    fx = x; fy = y; fz = z;
+    qx = x; qy = y; qz = z;
+    t.init();
+    thr = INFINITY;
+    c0 = c1 = c2 = INFINITY;
+  }
+  __device__ __forceinline__ void exact(float4 ref) {
+    const double ux = dsub(qx, (double)ref.x), uy = dsub(qy, (double)ref.y),
+                 uz = dsub(qz, (double)ref.z);
+    t.push(dadd(dadd(dmul(ux, ux), dmul(uy, uy)), dmul(uz, uz)), __float_as_int(ref.w));
+  }
+  __device__ __forceinline__ void consider(float4 ref, int kk) {
+    if (dist32(fx, fy, fz, ref) > thr) return;
+    exact(ref);
+    if (t.last(kk) != INFINITY) thr = (float)(t.last(kk) * (1.0 + 2e-6)) + 1e-30f;
+  }
+  __device__ __forceinline__ void window(const float4* L, int fill, int kk) {
+    int i = 0;
+    for (; i + 4 <= fill; i += 4) {
+      float d[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) d[u] = dist32(fx, fy, fz, L[i + u]);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const float n0 = fminf(c0, d[u]);
+        const float n1 = __builtin_amdgcn_fmed3f(c0, c1, d[u]);
+        const float n2 = __builtin_amdgcn_fmed3f(c1, c2, d[u]);
+        c0 = n0; c1 = n1; c2 = n2;
+      }
+    }
+    for (; i < fill; ++i) {
+      const float d = dist32(fx, fy, fz, L[i]);
+      const float n0 = fminf(c0, d);
+      const float n1 = __builtin_amdgcn_fmed3f(c0, c1, d);
+      const float n2 = __builtin_amdgcn_fmed3f(c1, c2, d);
+      c0 = n0; c1 = n1; c2 = n2;
+    }
+    const float ck = kk >= 3 ? c2 : (kk == 2 ? c1 : c0);
+    const float sc = fminf(ck * 1.000002f + 1e-30f, thr);
+    // phase 2 per block of 64 staged refs: a register mask of the screened-in refs (no LDS
+    // writes, so the reads pipeline), then each lane ranks its own survivors exactly
+    for (int b0 = 0; b0 < fill; b0 += 64) {
+      const int nb = min(64, fill - b0);
+      uint64_t m = 0;
+      int u = 0;
+      for (; u + 4 <= nb; u += 4) {
+        float d[4];
+#pragma unroll
+        for (int v = 0; v < 4; ++v) d[v] = dist32(fx, fy, fz, L[b0 + u + v]);
+#pragma unroll
+        for (int v = 0; v < 4; ++v) m |= (uint64_t)(d[v] <= sc) << (u + v);
+      }
+      for (; u < nb; ++u) m |= (uint64_t)(dist32(fx, fy, fz, L[b0 + u]) <= sc) << u;
+      while (m) {
+        const int k = __builtin_ctzll(m);
+        m &= m - 1;
+        exact(L[b0 + k]);
+      }
+    }
+    if (t.last(kk) != INFINITY) thr = fminf(thr, (float)(t.last(kk) * (1.0 + 2e-6)) + 1e-30f);
+  }
+};
+
+// LDS reads/writes of this wave done (before the window is overwritten or read)
+__device__ __forceinline__ void lds_order() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+// the window's LDS-DMA gathers landed (global_load_lds retires through vmcnt)
+__device__ __forceinline__ void dma_landed() {
+  asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
+}
+
+__device__ __forceinline__ int wave_min(int v) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) v = min(v, __shfl_xor(v, off));
+  return v;
+}
+__device__ __forceinline__ int wave_max(int v) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) v = max(v, __shfl_xor(v, off));
+  return v;
+}
+
+struct Box {
+  int x0, x1, y0, y1, z0, z1;
+  __device__ bool has(int x, int y, int z) const {
+    return x >= x0 && x <= x1 && y >= y0 && y <= y1 && z >= z0 && z <= z1;
+  }
+  __device__ int volume() const { return (x1 - x0 + 1) * (y1 - y0 + 1) * (z1 - z0 + 1); }
+};
+
+// Wave-cooperative scan of the refs of every cell of box `bx` that is not in `prev`: each lane
+// takes one cell per round (its ref range is contiguous; the next round's ranges are loaded
+// while this round's refs are staged), the round's refs are gathered into the wave's LDS
+// window by LDS-DMA (each lane finds the cell of its slot by a binary search over the lanes'
+// offsets) and every lane screens every staged ref.
+// Returns false (abandoned: the open lanes then go to the outlier pass, never to another
+// pass) once more than `budget` refs would be staged; otherwise charges them to `budget`.
+__device__ __forceinline__ bool scan_box(const Box& bx, const Box& prev, const Grid& g,
+                                         const uint64_t* __restrict__ S,
+                                         const float4* __restrict__ R, float4* L, Query& me,
+                                         int kk, uint32_t& budget) {
+  const int lane = threadIdx.x & 63;
+  const int nx = bx.x1 - bx.x0 + 1, ny = bx.y1 - bx.y0 + 1;
+  const int vol = bx.volume();
+  const float rnx = 1.0f / nx, rnxy = 1.0f / (nx * ny);  // exact quotients for li < 2^20
+  // packed start words of cell li and of its successor (empty if outside bx or inside prev)
+  auto unit = [&](int li, uint64_t& lo, uint64_t& hi) {
+    lo = hi = 0;
+    if (li < vol) {
+      const int qz = (int)(((float)li + 0.5f) * rnxy), rz = li - qz * nx * ny;
+      const int qy = (int)(((float)rz + 0.5f) * rnx), qx = rz - qy * nx;
+      const int x = bx.x0 + qx, y = bx.y0 + qy, z = bx.z0 + qz;
+      if (!prev.has(x, y, z)) {
+        const int u0 = cell_id(x, y, z, g);
+        lo = S[u0];
+        hi = S[u0 + 1];
+      }
     }
   };
-  for (int r = 0; r <= rmax; ++r) {
-    const int z0 = max(cz - r, 0), z1 = min(cz + r, dz - 1);
-    const int y0 = max(cy - r, 0), y1 = min(cy + r, dy - 1);
-    const int xl = max(cx - r, 0), xh = min(cx + r, dx - 1);
-    for (int z = z0; z <= z1; ++z) {
-      for (int y = y0; y <= y1; ++y) {
-        const int64_t row = ((int64_t)z * dy + y) * dx;
-        const bool face = (r == 0 || z == cz - r || z == cz + r || y == cy - r || y == cy + r);
-        if (face) {
-          scan(RS[row + xl], RS[row + xh + 1]);
+  uint64_t nlo, nhi;
+  unit(lane, nlo, nhi);
+  int fill = 0;
+  uint32_t staged = 0;
+  for (int c0 = 0; c0 < vol; c0 += 64) {
+    const uint32_t a = (uint32_t)nlo, cnt = (uint32_t)nhi - a;
+    if (c0 + 64 < vol) unit(c0 + 64 + lane, nlo, nhi);
+    uint32_t off = cnt;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = __shfl_up(off, o);
+      if (lane >= o) off += y;
+    }
+    const uint32_t tot = __shfl(off, 63);
+    off -= cnt;
+    staged += tot;
+    if (staged > budget) return false;
+    for (uint32_t w0 = 0; w0 < tot;) {
+      const uint32_t len = min(tot - w0, (uint32_t)(kCandCap - fill));
+      for (uint32_t t0 = 0; t0 < len; t0 += 64) {  // wave-uniform: every lane shuffles
+        const uint32_t t = t0 + lane, v = w0 + t;
+        int l = 0;  // last lane whose offset <= v (it owns slot v: zero-count lanes never do)
+#pragma unroll
+        for (int st = 32; st >= 1; st >>= 1)
+          if (__shfl(off, l + st) <= v) l += st;
+        const uint32_t src = __shfl(a, l) + (v - __shfl(off, l));
+        // LDS destination = wave-uniform base + 16 * lane: slot fill + t0 + lane
+        if (t < len)
+          __builtin_amdgcn_global_load_lds((const void*)(R + src),
+                                           (__attribute__((address_space(3))) void*)(L + fill + t0),
+                                           16, 0, 0);
+      }
+      fill += (int)len;
+      w0 += len;
+      if (fill == kCandCap) {
+        dma_landed();
+        me.window(L, fill, kk);
+        lds_order();
+        fill = 0;
+      }
+    }
+  }
+  dma_landed();
+  me.window(L, fill, kk);
+  lds_order();
+  budget -= staged;
+  return true;
+}
+
+// Distance from q to the region outside the box of cells [x0,x1]x[y0,y1]x[z0,z1] (faces on
+// the grid boundary excluded: nothing lies beyond them), less the cell-rounding slack.
+__device__ __forceinline__ double outside_bound(const Query& me, const Box& c, const Grid& g) {
+  const double ox = g.o[0], oy = g.o[1], oz = g.o[2], s = g.s;
+  double bound = INFINITY;
+  if (c.x0 > 0) bound = fmin(bound, me.qx - (ox + c.x0 * s));
+  if (c.x1 + 1 < g.d[0]) bound = fmin(bound, (ox + (c.x1 + 1) * s) - me.qx);
+  if (c.y0 > 0) bound = fmin(bound, me.qy - (oy + c.y0 * s));
+  if (c.y1 + 1 < g.d[1]) bound = fmin(bound, (oy + (c.y1 + 1) * s) - me.qy);
+  if (c.z0 > 0) bound = fmin(bound, me.qz - (oz + c.z0 * s));
+  if (c.z1 + 1 < g.d[2]) bound = fmin(bound, (oz + (c.z1 + 1) * s) - me.qz);
+  return bound - 1e-5 * s;  // covers fp32 cell-assignment rounding
+}
+
+__device__ __forceinline__ bool settled(const Query& me, const Box& cells, const Grid& g, int kk) {
+  if (me.t.last(kk) == INFINITY) return false;
+  const double bound = outside_bound(me, cells, g);
+  return bound == INFINITY || (bound > 0 && me.t.last(kk) < bound * bound);
+}
+
+// One wave per chunk of <= 64 queries of one brick; the passes of the header comment.
+template <int kk>  // min(M, 3), a compile-time constant so the top-3 stays in registers
+__global__ __launch_bounds__(256) void knn_query_kernel(
+    const float* __restrict__ orig, const float* __restrict__ vals, int64_t N, int64_t M,
+    int64_t Cpad, const float* __restrict__ gp, const uint64_t* __restrict__ start,
+    const float4* __restrict__ refs, const int32_t* __restrict__ qorder,
+    const uint2* __restrict__ chunks, int64_t maxch, const int32_t* __restrict__ nchunk,
+    int32_t* __restrict__ olist, int32_t* __restrict__ ocount, float* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) float4 cand[4][kCandCap];
+  const int b = blockIdx.y;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  Grid g;
+  g.load(gp + b * 8);
+  const uint64_t* S = start + b * Cpad;
+  const float4* R = refs + b * M;
+  const float* V = vals + b * M * 3;
+  float4* L = cand[wv];
+  const Box none = {1, 0, 1, 0, 1, 0};
+  const int nch = nchunk[b];
+  for (int item = blockIdx.x * 4 + wv; item < nch; item += gridDim.x * 4) {
+    const uint2 ch = chunks[b * maxch + item];
+    const bool valid = ch.x + lane < ch.y;
+#ifdef KNN_TRACE
+    const unsigned long long kt0 = clock64();
+    unsigned long long kt1 = 0, kt2 = 0;
+    uint32_t ks1 = 0, ks2 = 0, ks3 = 0, ko1 = 0, ko2 = 0, kvol = 0;
+#endif
+    const int64_t n = qorder[b * N + (valid ? ch.x + lane : ch.x)];
+    const float* qp = orig + (b * N + n) * 3;
+    Query me;
+    me.init(qp[0], qp[1], qp[2]);
+    const int cx = cell_coord(me.fx, g.o[0], g.inv, g.d[0]);
+    const int cy = cell_coord(me.fy, g.o[1], g.inv, g.d[1]);
+    const int cz = cell_coord(me.fz, g.o[2], g.inv, g.d[2]);
+    const int lx = wave_min(cx), hx = wave_max(cx), ly = wave_min(cy), hy = wave_max(cy),
+              lz = wave_min(cz), hz = wave_max(cz);
+    // 1. the chunk's cell box grown by one cell
+    Box pb = {max(lx - 1, 0), min(hx + 1, g.d[0] - 1), max(ly - 1, 0), min(hy + 1, g.d[1] - 1),
+              max(lz - 1, 0), min(hz + 1, g.d[2] - 1)};
+    uint32_t unlimited = 0xffffffffu;
+    scan_box(pb, none, g, S, R, L, me, kk, unlimited);
+    bool open = valid && !settled(me, pb, g, kk);
+    bool ok = true;
+#ifdef KNN_TRACE
+    kt1 = clock64();
+    ks1 = 0xffffffffu - unlimited;
+    ko1 = (uint32_t)__popcll(__ballot(open));
+#endif
+    // 2. the balls of the open lanes that hold kk refs
+    if (__any(open)) {
+      const double dk = me.t.last(kk);
+      bool ball = open && dk != INFINITY;
+      int bx0 = 0x7fffffff, bx1 = -1, by0 = 0x7fffffff, by1 = -1, bz0 = 0x7fffffff, bz1 = -1;
+      if (ball) {
+        const float r = (float)(sqrt(dk) * (1.0 + 1e-5)) + 1e-4f * g.s;
+        const Box lb = {cell_coord(me.fx - r, g.o[0], g.inv, g.d[0]),
+                        cell_coord(me.fx + r, g.o[0], g.inv, g.d[0]),
+                        cell_coord(me.fy - r, g.o[1], g.inv, g.d[1]),
+                        cell_coord(me.fy + r, g.o[1], g.inv, g.d[1]),
+                        cell_coord(me.fz - r, g.o[2], g.inv, g.d[2]),
+                        cell_coord(me.fz + r, g.o[2], g.inv, g.d[2])};
+        if (lb.volume() <= kBallCells) {
+          bx0 = lb.x0; bx1 = lb.x1; by0 = lb.y0; by1 = lb.y1; bz0 = lb.z0; bz1 = lb.z1;
         } else {
-          const bool lo = cx - r >= 0, hi = cx + r < dx;
-          const uint32_t a0 = lo ? RS[row + cx - r] : 0u, e0 = lo ? RS[row + cx - r + 1] : 0u;
-          const uint32_t a1 = hi ? RS[row + cx + r] : 0u, e1 = hi ? RS[row + cx + r + 1] : 0u;
-          scan(a0, e0);
-          scan(a1, e1);
+          ball = false;
+        }
+      }
+      if (__any(ball)) {
+        const Box bb = {min(pb.x0, wave_min(bx0)), max(pb.x1, wave_max(bx1)),
+                        min(pb.y0, wave_min(by0)), max(pb.y1, wave_max(by1)),
+                        min(pb.z0, wave_min(bz0)), max(pb.z1, wave_max(bz1))};
+#ifdef KNN_TRACE
+        kvol = bb.volume();
+#endif
+        if (bb.volume() <= kBallUnion) {
+          uint32_t budget = kBallBudget;
+          ok = scan_box(bb, pb, g, S, R, L, me, kk, budget);
+#ifdef KNN_TRACE
+          ks2 = ok ? kBallBudget - budget : 0xffffffffu;
+#endif
+          if (ok) {
+            pb = bb;
+            open = open && !settled(me, pb, g, kk);
+          }
         }
       }
     }
-    if (t.d[kk - 1] == INFINITY) continue;
-    // distance from q to the unvisited region outside the (2r+1)^3 block
-    double bound = INFINITY;
-    if (cx - r > 0) bound = fmin(bound, qx - (ox + (cx - r) * s));
-    if (cx + r + 1 < dx) bound = fmin(bound, (ox + (cx + r + 1) * s) - qx);
-    if (cy - r > 0) bound = fmin(bound, qy - (oy + (cy - r) * s));
-    if (cy + r + 1 < dy) bound = fmin(bound, (oy + (cy + r + 1) * s) - qy);
-    if (cz - r > 0) bound = fmin(bound, qz - (oz + (cz - r) * s));
-    if (cz + r + 1 < dz) bound = fmin(bound, (oz + (cz + r + 1) * s) - qz);
-    bound -= slack;
-    if (bound == INFINITY || (bound > 0 && t.d[kk - 1] < bound * bound)) {
-      done = true;
-      break;
+#ifdef KNN_TRACE
+    kt2 = clock64();
+    ko2 = (uint32_t)__popcll(__ballot(open));
+    ks3 = 0;
+#endif
+    // the rest (sparse neighbourhoods, ball too large, budget exceeded): the outlier pass
+    const uint64_t rest = __ballot(open);
+    if (rest) {
+      int at = 0;
+      if (lane == 0) at = atomicAdd(&ocount[b], (int)__popcll(rest));
+      at = __shfl(at, 0);
+      if (open) olist[b * N + at + (int)__popcll(rest & lanemask_lt())] = (int32_t)n;
     }
+    if (valid && !open) idw_write(me.t, kk, V, out + (b * N + n) * 3);
+#ifdef KNN_TRACE
+    const unsigned long long kt3 = clock64();
+    if (lane == 0 && item < 32768) {
+      unsigned long long* r = g_knn_trace + ((int64_t)b * 32768 + item) * 8;
+      r[0] = ((unsigned long long)(ch.y - ch.x) << 32) | 1u;
+      r[1] = ((unsigned long long)ko1 << 32) | ko2;
+      r[2] = kt0; r[3] = kt1; r[4] = kt2; r[5] = kt3;
+      r[6] = ((unsigned long long)ks1 << 32) | ks2;
+      r[7] = ((unsigned long long)ks3 << 32) | ((unsigned long long)__popcll(rest) << 16) | (kvol & 0xffff);
+    }
+#endif
   }
-  if (!done) {  // sparse neighbourhood: leave it to the exhaustive wave-per-query pass
-    olist[b * N + atomicAdd(&ocount[b], 1)] = (int32_t)n;
-    return;
-  }
-  idw_write(t, kk, V, O);
 }
 
-// Exhaustive 3-NN for the queries the shell search left: one wave per query, each lane scans
-// M/64 refs with its own top-3, then a butterfly merge (lexicographic (d, j): deterministic).
-__global__ __launch_bounds__(256) void knn_outlier_kernel(
-    const float* __restrict__ orig, const float* __restrict__ vals, int64_t N, int64_t M,
+// Exhaustive 3-NN of the outlier queries: one workgroup per query, thread i scans refs i,
+// i+1024, ... (4 loads in flight), then a wave butterfly and a merge of the waves
+// (lexicographic (d, j): deterministic).
+template <int kk>
+__global__ __launch_bounds__(kOutlierThreads) void knn_outlier_kernel(
+    const float* __restrict__ vals, int64_t N, int64_t M, const float* __restrict__ orig,
     const float4* __restrict__ refs, const int32_t* __restrict__ olist,
     const int32_t* __restrict__ ocount, float* __restrict__ out) {
+  constexpr int W = kOutlierThreads / 64;
+  constexpr int Q = kOutlierThreads;
+  __shared__ double sd[W][3];
+  __shared__ int sj[W][3];
   const int b = blockIdx.y;
-  const int lane = threadIdx.x & 63;
-  const int wg = blockIdx.x * 4 + (threadIdx.x >> 6);
-  const int cnt = ocount[b];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const float4* R = refs + b * M;
   const float* V = vals + b * M * 3;
-  const int kk = M < 3 ? (int)M : 3;
-  for (int q = wg; q < cnt; q += gridDim.x * 4) {
+  const int cnt = ocount[b];
+  for (int q = blockIdx.x; q < cnt; q += gridDim.x) {
     const int64_t n = olist[b * N + q];
     const float* p = orig + (b * N + n) * 3;
-    const float fx = p[0], fy = p[1], fz = p[2];
-    const double qx = fx, qy = fy, qz = fz;
-    Top3 t;
-    t.init();
-    float thr = INFINITY;
-    for (int64_t i = lane; i < M; i += 64) {
-      const float4 ref = R[i];
-      const float ex = fx - ref.x, ey = fy - ref.y, ez = fz - ref.z;
-      const float d32 = fmaf(ez, ez, fmaf(ey, ey, ex * ex));
-      if (d32 > thr) continue;
-      const double ux = dsub(qx, (double)ref.x), uy = dsub(qy, (double)ref.y),
-                   uz = dsub(qz, (double)ref.z);
-      t.push(dadd(dadd(dmul(ux, ux), dmul(uy, uy)), dmul(uz, uz)), __float_as_int(ref.w));
-      if (t.d[kk - 1] != INFINITY) thr = (float)(t.d[kk - 1] * (1.0 + 2e-6)) + 1e-30f;
+    Query me;
+    me.init(p[0], p[1], p[2]);
+    int64_t i = threadIdx.x;
+    for (; i + 3 * Q < M; i += 4 * Q) {
+      const float4 r0 = R[i], r1 = R[i + Q], r2 = R[i + 2 * Q], r3 = R[i + 3 * Q];
+      me.consider(r0, kk);
+      me.consider(r1, kk);
+      me.consider(r2, kk);
+      me.consider(r3, kk);
     }
+    for (; i < M; i += Q) me.consider(R[i], kk);
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) {
-      double od[3];
-      int oj[3];
-      for (int k = 0; k < 3; ++k) { od[k] = __shfl_xor(t.d[k], off); oj[k] = __shfl_xor(t.j[k], off); }
-      for (int k = 0; k < 3; ++k) t.push(od[k], oj[k]);
+      const double e0 = __shfl_xor(me.t.d0, off), e1 = __shfl_xor(me.t.d1, off),
+                   e2 = __shfl_xor(me.t.d2, off);
+      const int i0 = __shfl_xor(me.t.j0, off), i1 = __shfl_xor(me.t.j1, off),
+                i2 = __shfl_xor(me.t.j2, off);
+      me.t.push(e0, i0);
+      me.t.push(e1, i1);
+      me.t.push(e2, i2);
     }
-    if (lane == 0) idw_write(t, kk, V, out + (b * N + n) * 3);
+    if (lane == 0) {
+      sd[wv][0] = me.t.d0; sd[wv][1] = me.t.d1; sd[wv][2] = me.t.d2;
+      sj[wv][0] = me.t.j0; sj[wv][1] = me.t.j1; sj[wv][2] = me.t.j2;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      Top3 t = me.t;
+      for (int w = 1; w < W; ++w) {
+        t.push(sd[w][0], sj[w][0]);
+        t.push(sd[w][1], sj[w][1]);
+        t.push(sd[w][2], sj[w][2]);
+      }
+      idw_write(t, kk, V, out + (b * N + n) * 3);
+    }
+    __syncthreads();
   }
 }
 
@@ -356,37 +802,51 @@ extern "C" int pcst_knn_workspace_size(int64_t B, int64_t N, int64_t M, size_t* 
 extern "C" int pcst_knn3_interp(const float* coarse, const float* orig, const int64_t* idx,
                                 int64_t B, int64_t N, int64_t M, float* out, void* workspace,
                                 void* stream) {
-  PCST_CHECK_ARG(B >= 0 && N > 0 && M > 0 && N < (1ll << 31) && M < (1ll << 27),
+  PCST_CHECK_ARG(B >= 0 && N > 0 && M > 0 && N < (1ll << 31) && M < (1ll << 27) &&
+                     M + N < (1ll << 31),
                  "knn3_interp: bad shape");
   if (B == 0) return PCST_OK;
   PCST_CHECK_ARG(coarse && orig && idx && out && workspace, "knn3_interp: null pointer");
   hipStream_t s = as_stream(stream);
   KnnWS w = carve_knn(workspace, B, N, M);
   const int b = (int)B;
-  const int64_t C = w.C;
-  // counters, known flags, count and cursor arrays are contiguous in the carve: one memset
+  // error word, counters, known rows, tile sums and packed counts are contiguous in the carve
   PCST_HIP(hipMemsetAsync(w.err, 0, (size_t)(w.bytes - ((char*)w.err - (char*)workspace)), s),
            "knn: memset");
-  launch_cloud_stats(orig, b, (int)N, w.stats, s);
-  hipLaunchKernelGGL(knn_grid_params_kernel, dim3((unsigned)B), dim3(64), 0, s, w.stats, b, N, M,
-                     C, w.gp);
-  const unsigned gm = (unsigned)std::min<int64_t>(cdiv(M, 256), 1024);
-  hipLaunchKernelGGL(knn_known_kernel, dim3(gm, b), dim3(256), 0, s, idx, N, M, w.known, w.err);
-  const unsigned ga = (unsigned)std::min<int64_t>(cdiv(M + N, 256), 2048);
-  hipLaunchKernelGGL(knn_count_kernel, dim3(ga, b), dim3(256), 0, s, orig, idx, N, M, C, w.gp,
-                     w.rstart, w.qstart);
-  seg_scan_long(w.rstart, b, C + 1, C + 1, w.tsum, nullptr, s);
-  seg_scan_long(w.qstart, b, C + 1, C + 1, w.tsum, nullptr, s);
-  hipLaunchKernelGGL(knn_fill_kernel, dim3(ga, b), dim3(256), 0, s, orig, idx, N, M, C, w.gp,
-                     w.rstart, w.qstart, w.rcur, w.qcur, w.refs, w.qorder);
-  hipLaunchKernelGGL(knn_query_kernel, dim3((unsigned)cdiv(N, 256), b), dim3(256), 0, s, orig,
-                     coarse, N, M, C, w.gp, w.known, w.rstart, w.refs, w.qorder, w.olist, w.ocount,
-                     out);
-  hipLaunchKernelGGL(knn_outlier_kernel, dim3(256, b), dim3(256), 0, s, orig, coarse, N, M, w.refs,
-                     w.olist, w.ocount, out);
+  hipLaunchKernelGGL(knn_pre_kernel, dim3(kStatBlocks + kPreKnownBlocks, b), dim3(256), 0, s,
+                     orig, idx, (int)N, M, w.stats, w.known, w.err);
+  const unsigned gc = (unsigned)cdiv(M + N, kCountPerBlock);
+  hipLaunchKernelGGL(knn_count_kernel, dim3(gc, b), dim3(256), 0, s, orig, coarse, idx, w.stats,
+                     w.known, N, M, w.Cmax, w.T, w.Cpad, w.gp, w.cnt, w.tsum, w.crank, out);
+  hipLaunchKernelGGL(knn_scan_kernel, dim3((unsigned)w.T, b), dim3(256), 0, s, w.cnt, w.tsum, w.T,
+                     w.Cpad, w.chunks, w.maxch, w.nchunk);
+  const unsigned gf = (unsigned)std::min<int64_t>(cdiv(M + N, 256), 2048);
+  hipLaunchKernelGGL(knn_fill_kernel, dim3(gf, b), dim3(256), 0, s, orig, idx, N, M, w.Cpad, w.cnt,
+                     w.crank, w.refs, w.qorder);
+  // fixed grids stride over the chunk and outlier lists (their lengths live on the device)
+  const unsigned gq = (unsigned)std::min<int64_t>(cdiv(w.maxch, 4), kQueryBlocks);
+  auto qk = M >= 3 ? knn_query_kernel<3> : (M == 2 ? knn_query_kernel<2> : knn_query_kernel<1>);
+  hipLaunchKernelGGL(qk, dim3(gq, b), dim3(256), 0, s, orig, coarse, N, M, w.Cpad, w.gp, w.cnt,
+                     w.refs, w.qorder, w.chunks, w.maxch, w.nchunk, w.olist, w.ocount, out);
+  auto ok = M >= 3 ? knn_outlier_kernel<3>
+                   : (M == 2 ? knn_outlier_kernel<2> : knn_outlier_kernel<1>);
+  hipLaunchKernelGGL(ok, dim3(kOutlierBlocks, b), dim3(kOutlierThreads), 0, s, coarse, N, M, orig,
+                     w.refs, w.olist, w.ocount, out);
   PCST_LAUNCH_CHECK("knn3_interp");
   return PCST_OK;
 }
+
+#ifdef KNN_TRACE
+extern "C" int pcst_knn_trace_dump(void* host, size_t bytes) {
+  void* d = nullptr;
+  PCST_HIP(hipGetSymbolAddress(&d, HIP_SYMBOL(g_knn_trace)), "knn_trace: symbol");
+  PCST_HIP(hipDeviceSynchronize(), "knn_trace: sync");
+  if (host) PCST_HIP(hipMemcpy(host, d, std::min(bytes, sizeof(g_knn_trace)), hipMemcpyDeviceToHost), "knn_trace: copy");
+  PCST_HIP(hipMemset(d, 0, sizeof(g_knn_trace)), "knn_trace: reset");
+  PCST_HIP(hipDeviceSynchronize(), "knn_trace: sync");
+  return PCST_OK;
+}
+#endif
 
 extern "C" int pcst_knn_error(void* workspace, int64_t B, int64_t N, int64_t M, int32_t* err_out,
                               void* stream) {

@@ -15,7 +15,8 @@
 //
 // Weights stream through LDS in 32 KiB parts (double-buffered, global_load_lds 16 B/lane),
 // shared by all waves of the workgroup; bias tables and the per-cloud cond rows sit in LDS.
-// bf16 mode: 8 waves x 32 points per workgroup (2 waves/SIMD), fp32 accumulate, fp32 residual.
+// bf16 mode: 4 waves x 32 points per workgroup (1 wave/SIMD: 420 VGPR+AGPR per lane; a
+// 512-thread variant would have 256 and spills), fp32 accumulate, fp32 residual.
 // f32 mode (parity): exact-f32 MFMA, 4 waves x 32 points (1 wave/SIMD).
 #include "common.h"
 

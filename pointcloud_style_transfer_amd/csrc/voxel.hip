@@ -340,19 +340,25 @@ constexpr int kTieCap = 8192;
 constexpr int kVoxChunk = 2048;  // points aggregated per workgroup in LDS
 constexpr int kVoxLds = 4096;    // LDS table slots (load factor <= 1/2)
 
+// Copies.  guided_sample_loop downsamples the CFG batch cat([x] * 2) (diffusion_model.py:244-247):
+// identical clouds.  With copies = k the input is the B distinct clouds and the output has the
+// k*B rows of cat([x] * k) (row = c*B + b of cloud b = row % B): the voxel table and the
+// representatives are built once per cloud, only the random subset is drawn per row, with
+// the row's own keys -- the kept SET of every row equals the one the concatenated call draws
+// from the same seed.
 struct VoxelFastWS {
-  StatRec* mm;
-  float4* vp;
-  int32_t* cnt4;          // [B][4]: U, selected, ties, err
-  int32_t* sel;           // [B][4]: bin*, rem, need, U>T flag
-  uint32_t* hist;         // [B][kSelBins]
+  StatRec* mm;            // [B][kStatBlocks]
+  int32_t* sel;           // [R][4]: bin*, rem, need, U>T flag  (R = copies * B rows)
+  int64_t* reps;          // [B][N]
+  uint32_t* rhash;        // [B][N]
+  unsigned long long* ties;  // [R][kTieCap] (key<<32 | id)
+  // zeroed every call (one memset): counters, histograms, tables, rep flags
+  int32_t* cnt4;          // [R][4]: U (of cloud r, rows r < B), selected, ties, err
+  uint32_t* hist;         // [R][kSelBins]
   unsigned long long* tkey;  // [B][H]  0 = empty, else (1<<32)|hash
   unsigned long long* tsum;  // [B][H]
   uint32_t* tcnt;         // [B][H]
   uint32_t* isrep;        // [B][N]
-  int64_t* reps;          // [B][N]
-  uint32_t* rhash;        // [B][N]
-  unsigned long long* ties;  // [B][kTieCap] (key<<32 | id)
   int64_t H;
   size_t bytes;
 };
@@ -363,19 +369,18 @@ static int64_t vox_table_size(int64_t N) {
   return h;
 }
 
-static VoxelFastWS carve_voxel_fast(void* base, int64_t B, int64_t N) {
+static VoxelFastWS carve_voxel_fast(void* base, int64_t B, int64_t N, int64_t copies = 1) {
   Carver c(base);
   VoxelFastWS w;
+  const int64_t R = B * copies;
   w.H = vox_table_size(N);
   w.mm = c.take<StatRec>(B * kStatBlocks);
-  w.vp = c.take<float4>(B);
-  w.sel = c.take<int32_t>(B * 4);
+  w.sel = c.take<int32_t>(R * 4);
   w.reps = c.take<int64_t>(B * N);
   w.rhash = c.take<uint32_t>(B * N);
-  w.ties = c.take<unsigned long long>(B * kTieCap);
-  // zeroed every call (one memset): counters, histogram, table, rep flags
-  w.cnt4 = c.take<int32_t>(B * 4);
-  w.hist = c.take<uint32_t>(B * kSelBins);
+  w.ties = c.take<unsigned long long>(R * kTieCap);
+  w.cnt4 = c.take<int32_t>(R * 4);
+  w.hist = c.take<uint32_t>(R * kSelBins);
   w.tkey = c.take<unsigned long long>(B * w.H);
   w.tsum = c.take<unsigned long long>(B * w.H);
   w.tcnt = c.take<uint32_t>(B * w.H);
@@ -389,8 +394,11 @@ __device__ __forceinline__ uint32_t mix32(uint32_t x) {
   return x;
 }
 
+// Voxel table insert; the first wave also folds the cloud's min/max partials into the voxel
+// parameters (min xyz, voxel size) for its workgroup.
 __global__ __launch_bounds__(256) void voxf_insert_kernel(const float* __restrict__ pts, int N,
-                                                          const float4* __restrict__ vp, int64_t H,
+                                                          const StatRec* __restrict__ mm,
+                                                          int64_t T, int64_t H,
                                                           unsigned long long* __restrict__ tkey,
                                                           unsigned long long* __restrict__ tsum,
                                                           uint32_t* __restrict__ tcnt) {
@@ -398,14 +406,19 @@ __global__ __launch_bounds__(256) void voxf_insert_kernel(const float* __restric
   // publishes one global (sum, count) per distinct voxel: dense voxels see at most one global
   // atomic per workgroup instead of one per point.
   const int b = blockIdx.y;
-  const float4 v4 = vp[b];
   const float* P = pts + (int64_t)b * N * 3;
   unsigned long long* K = tkey + b * H;
   __shared__ unsigned long long lkey[kVoxLds];
   __shared__ unsigned long long lsum[kVoxLds];
   __shared__ uint32_t lcnt[kVoxLds];
+  __shared__ float4 vps;
+  if (threadIdx.x < 64) {
+    const StatRec M = fold_stats_wave(mm, b);
+    if (threadIdx.x == 0) vps = make_float4(M.mn[0], M.mn[1], M.mn[2], voxel_size(M, T));
+  }
   for (int i = threadIdx.x; i < kVoxLds; i += 256) { lkey[i] = 0ull; lsum[i] = 0ull; lcnt[i] = 0u; }
   __syncthreads();
+  const float4 v4 = vps;
   const int n0 = blockIdx.x * kVoxChunk, n1 = min(n0 + kVoxChunk, N);
   for (int n = n0 + threadIdx.x; n < n1; n += 256) {
     const int32_t vx = (int32_t)floorf(__fdiv_rn(fsub(P[n * 3 + 0], v4.x), v4.w));
@@ -438,15 +451,15 @@ __global__ __launch_bounds__(256) void voxf_insert_kernel(const float* __restric
   }
 }
 
-// occupied slot -> representative trunc(f32(sum)/f32(count)) (Q6); list order = arrival order
-__global__ __launch_bounds__(256) void voxf_reps_kernel(const unsigned long long* __restrict__ tkey,
-                                                        const unsigned long long* __restrict__ tsum,
-                                                        const uint32_t* __restrict__ tcnt, int64_t H,
-                                                        int N, int64_t T, int32_t* __restrict__ cnt4,
-                                                        int64_t* __restrict__ reps,
-                                                        uint32_t* __restrict__ rhash,
-                                                        uint32_t* __restrict__ isrep,
-                                                        int64_t* __restrict__ out_idx) {
+// occupied slot -> representative trunc(f32(sum)/f32(count)) (Q6); list order = arrival order.
+// When U <= T every rep is kept: rep k is written (index and point) to position k of every
+// copy row here.
+__global__ __launch_bounds__(256) void voxf_reps_kernel(
+    const float* __restrict__ pts, const unsigned long long* __restrict__ tkey,
+    const unsigned long long* __restrict__ tsum, const uint32_t* __restrict__ tcnt, int64_t H,
+    int N, int64_t T, int B, int copies, int32_t* __restrict__ cnt4, int64_t* __restrict__ reps,
+    uint32_t* __restrict__ rhash, uint32_t* __restrict__ isrep, int64_t* __restrict__ out_idx,
+    float* __restrict__ out_pts) {
   // one contiguous slot range per workgroup, one counter atomic per workgroup
   const int b = blockIdx.y;
   const int64_t chunk = (H + gridDim.x - 1) / gridDim.x;
@@ -470,191 +483,194 @@ __global__ __launch_bounds__(256) void voxf_reps_kernel(const unsigned long long
     reps[(int64_t)b * N + k] = r;
     rhash[(int64_t)b * N + k] = (uint32_t)kw;
     isrep[(int64_t)b * N + r] = 1u;
-    if (k < T) out_idx[b * T + k] = r;  // the U <= T case keeps every rep
+    if (k < T) {
+      const float* src = pts + ((int64_t)b * N + r) * 3;
+      const float x = src[0], y = src[1], z = src[2];
+      for (int c = 0; c < copies; ++c) {
+        const int64_t row = (int64_t)c * B + b;
+        out_idx[row * T + k] = r;
+        float* d = out_pts + (row * T + k) * 3;
+        d[0] = x; d[1] = y; d[2] = z;
+      }
+    }
     ++k;
   }
 }
 
-// candidate e of cloud b: (key, id); returns false if e is not a candidate
-__device__ __forceinline__ bool voxf_cand(int b, int e, int N, int U, int64_t T, uint64_t seed,
-                                          const uint32_t* __restrict__ rhash,
+// candidate e of row `row` (cloud cl): (key, id); returns false if e is not a candidate.  Keys
+// follow the row, the candidate arrays the cloud.
+__device__ __forceinline__ bool voxf_cand(int row, int cl, int e, int N, int U, int64_t T,
+                                          uint64_t seed, const uint32_t* __restrict__ rhash,
                                           const uint32_t* __restrict__ isrep, uint32_t& key,
                                           uint32_t& id) {
   if (U > T) {
     if (e >= U) return false;
     id = (uint32_t)e;
-    key = rand_key(seed, b, (int)(rhash[(int64_t)b * N + e] & 0x7fffffff));
+    key = rand_key(seed, row, (int)(rhash[(int64_t)cl * N + e] & 0x7fffffff));
     return true;
   }
-  if (U == T || e >= N || isrep[(int64_t)b * N + e]) return false;
+  if (U == T || e >= N || isrep[(int64_t)cl * N + e]) return false;
   id = (uint32_t)e;
-  key = rand_key(seed, b + 0x10000, e);
+  key = rand_key(seed, row + 0x10000, e);
   return true;
 }
 
-__global__ __launch_bounds__(256) void voxf_hist_kernel(int N, int64_t T, uint64_t seed,
+__global__ __launch_bounds__(256) void voxf_hist_kernel(int N, int64_t T, int B, uint64_t seed,
                                                         const int32_t* __restrict__ cnt4,
                                                         const uint32_t* __restrict__ rhash,
                                                         const uint32_t* __restrict__ isrep,
                                                         uint32_t* __restrict__ hist) {
-  const int b = blockIdx.y;
-  const int U = cnt4[b * 4];
+  const int row = blockIdx.y, cl = row % B;
+  const int U = cnt4[cl * 4];
   __shared__ uint32_t h[kSelBins];
   for (int i = threadIdx.x; i < kSelBins; i += 256) h[i] = 0;
   __syncthreads();
   for (int e = blockIdx.x * 256 + threadIdx.x; e < N; e += gridDim.x * 256) {
     uint32_t key, id;
-    if (voxf_cand(b, e, N, U, T, seed, rhash, isrep, key, id)) atomicAdd(&h[key >> 20], 1u);
+    if (voxf_cand(row, cl, e, N, U, T, seed, rhash, isrep, key, id)) atomicAdd(&h[key >> 20], 1u);
   }
   __syncthreads();
   for (int i = threadIdx.x; i < kSelBins; i += 256)
-    if (h[i]) atomicAdd(&hist[b * kSelBins + i], h[i]);
+    if (h[i]) atomicAdd(&hist[row * kSelBins + i], h[i]);
 }
 
-// per cloud: the boundary bin b* and how many of it are still needed
-__global__ __launch_bounds__(256) void voxf_find_kernel(const uint32_t* __restrict__ hist,
-                                                        const int32_t* __restrict__ cnt4, int N,
-                                                        int64_t T, int32_t* __restrict__ sel) {
-  const int b = blockIdx.x;
-  const int U = cnt4[b * 4];
+// kept candidate -> its output position (index and point)
+__device__ __forceinline__ void voxf_emit(int row, int cl, int N, int64_t T, int U, int pos,
+                                          uint32_t id, const int64_t* __restrict__ reps,
+                                          const float* __restrict__ pts,
+                                          int64_t* __restrict__ out_idx,
+                                          float* __restrict__ out_pts) {
+  const int64_t r = U > T ? reps[(int64_t)cl * N + id] : (int64_t)id;
+  const int64_t j = U > T ? pos : U + pos;
+  out_idx[row * T + j] = r;
+  const float* src = pts + ((int64_t)cl * N + r) * 3;
+  float* d = out_pts + (row * T + j) * 3;
+  d[0] = src[0]; d[1] = src[1]; d[2] = src[2];
+}
+
+// Every workgroup first finds the row's boundary bin b* (the bin holding the need-th smallest
+// key) from the histogram; workgroup 0 records it for the ties kernel.  Then: keys below b*
+// are kept (one contiguous candidate range per workgroup, two counter atomics per workgroup),
+// keys in b* go to the tie list.
+__global__ __launch_bounds__(256) void voxf_select_kernel(
+    const float* __restrict__ pts, int N, int64_t T, int B, uint64_t seed,
+    const uint32_t* __restrict__ hist, int32_t* __restrict__ sel, int32_t* __restrict__ cnt4,
+    const uint32_t* __restrict__ rhash, const uint32_t* __restrict__ isrep,
+    const int64_t* __restrict__ reps, unsigned long long* __restrict__ ties,
+    int64_t* __restrict__ out_idx, float* __restrict__ out_pts) {
+  const int row = blockIdx.y, cl = row % B;
+  const int U = cnt4[cl * 4];
   const int need = U > T ? (int)T : (U < T ? (int)(T - U) : 0);
   __shared__ uint32_t sh[260];
-  const int per = kSelBins / 256;
-  uint32_t v[kSelBins / 256], s = 0;
-  for (int k = 0; k < per; ++k) {
-    v[k] = hist[b * kSelBins + threadIdx.x * per + k];
-    s += v[k];
-  }
-  uint32_t tot;
-  uint32_t run = block_excl_scan_256(s, sh, tot);
-  for (int k = 0; k < per; ++k) {
-    if (need > 0 && run < (uint32_t)need && run + v[k] >= (uint32_t)need) {
-      sel[b * 4 + 0] = threadIdx.x * per + k;
-      sel[b * 4 + 1] = need - (int)run;
+  __shared__ int s_bstar, s_rem;
+  {
+    constexpr int per = kSelBins / 256;
+    uint32_t v[per], s = 0;
+#pragma unroll
+    for (int k = 0; k < per; ++k) {
+      v[k] = hist[row * kSelBins + threadIdx.x * per + k];
+      s += v[k];
     }
-    run += v[k];
+    if (threadIdx.x == 0) { s_bstar = -1; s_rem = 0; }
+    uint32_t tot;
+    uint32_t run = block_excl_scan_256(s, sh, tot);
+#pragma unroll
+    for (int k = 0; k < per; ++k) {
+      if (need > 0 && run < (uint32_t)need && run + v[k] >= (uint32_t)need) {
+        s_bstar = threadIdx.x * per + k;
+        s_rem = need - (int)run;
+      }
+      run += v[k];
+    }
+    __syncthreads();
   }
-  if (threadIdx.x == 0) {
-    sel[b * 4 + 2] = need;
-    sel[b * 4 + 3] = U > T ? 1 : 0;
-    if (need == 0) { sel[b * 4 + 0] = -1; sel[b * 4 + 1] = 0; }
+  const int bstar = s_bstar;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    sel[row * 4 + 0] = bstar;
+    sel[row * 4 + 1] = s_rem;
+    sel[row * 4 + 2] = need;
+    sel[row * 4 + 3] = U > T ? 1 : 0;
   }
-}
-
-__device__ __forceinline__ void voxf_emit(int b, int N, int64_t T, int U, int pos, uint32_t id,
-                                          const int64_t* __restrict__ reps,
-                                          int64_t* __restrict__ out_idx) {
-  const int64_t r = U > T ? reps[(int64_t)b * N + id] : (int64_t)id;
-  const int64_t j = U > T ? pos : U + pos;
-  out_idx[b * T + j] = r;
-}
-
-__global__ __launch_bounds__(256) void voxf_select_kernel(int N, int64_t T, uint64_t seed,
-                                                          const int32_t* __restrict__ sel,
-                                                          int32_t* __restrict__ cnt4,
-                                                          const uint32_t* __restrict__ rhash,
-                                                          const uint32_t* __restrict__ isrep,
-                                                          const int64_t* __restrict__ reps,
-                                                          unsigned long long* __restrict__ ties,
-                                                          int64_t* __restrict__ out_idx) {
-  // one contiguous candidate range per workgroup, two counter atomics per workgroup
-  const int b = blockIdx.y;
-  const int bstar = sel[b * 4 + 0];
   if (bstar < 0) return;
-  const int U = cnt4[b * 4];
   const int chunk = (N + gridDim.x - 1) / gridDim.x;
   const int e0 = blockIdx.x * chunk, e1 = min(e0 + chunk, N);
   uint32_t nlo = 0, nti = 0;
   for (int e = e0 + threadIdx.x; e < e1; e += 256) {
     uint32_t key, id;
-    if (!voxf_cand(b, e, N, U, T, seed, rhash, isrep, key, id)) continue;
+    if (!voxf_cand(row, cl, e, N, U, T, seed, rhash, isrep, key, id)) continue;
     const int bin = (int)(key >> 20);
     nlo += bin < bstar;
     nti += bin == bstar;
   }
-  __shared__ uint32_t sh[260];
   __shared__ int base_lo, base_ti;
   uint32_t tlo, tti;
   const uint32_t olo = block_excl_scan_256(nlo, sh, tlo);
   const uint32_t oti = block_excl_scan_256(nti, sh, tti);
   if (threadIdx.x == 0) {
-    base_lo = tlo ? atomicAdd(&cnt4[b * 4 + 1], (int)tlo) : 0;
-    base_ti = tti ? atomicAdd(&cnt4[b * 4 + 2], (int)tti) : 0;
+    base_lo = tlo ? atomicAdd(&cnt4[row * 4 + 1], (int)tlo) : 0;
+    base_ti = tti ? atomicAdd(&cnt4[row * 4 + 2], (int)tti) : 0;
   }
   __syncthreads();
   int plo = base_lo + (int)olo, pti = base_ti + (int)oti;
   for (int e = e0 + threadIdx.x; e < e1; e += 256) {
     uint32_t key, id;
-    if (!voxf_cand(b, e, N, U, T, seed, rhash, isrep, key, id)) continue;
+    if (!voxf_cand(row, cl, e, N, U, T, seed, rhash, isrep, key, id)) continue;
     const int bin = (int)(key >> 20);
     if (bin < bstar) {
-      voxf_emit(b, N, T, U, plo++, id, reps, out_idx);
+      voxf_emit(row, cl, N, T, U, plo++, id, reps, pts, out_idx, out_pts);
     } else if (bin == bstar) {
-      if (pti < kTieCap) ties[(int64_t)b * kTieCap + pti] = ((unsigned long long)key << 32) | id;
-      else atomicOr(&cnt4[b * 4 + 3], 1);
+      if (pti < kTieCap) ties[(int64_t)row * kTieCap + pti] = ((unsigned long long)key << 32) | id;
+      else atomicOr(&cnt4[row * 4 + 3], 1);
       ++pti;
     }
   }
 }
 
-// boundary bin: exact order by (key, id), keep the first `rem` (one workgroup per cloud)
-__global__ __launch_bounds__(1024) void voxf_ties_kernel(int N, int64_t T,
+// boundary bin: exact order by (key, id), keep the first `rem` (one workgroup per row)
+__global__ __launch_bounds__(1024) void voxf_ties_kernel(const float* __restrict__ pts, int N,
+                                                         int64_t T, int B,
                                                          const int32_t* __restrict__ sel,
                                                          const int32_t* __restrict__ cnt4,
                                                          const unsigned long long* __restrict__ ties,
                                                          const int64_t* __restrict__ reps,
-                                                         int64_t* __restrict__ out_idx) {
-  const int b = blockIdx.x;
-  if (sel[b * 4 + 0] < 0) return;
-  const int rem = sel[b * 4 + 1];
-  const int U = cnt4[b * 4];
-  const int nt = min(cnt4[b * 4 + 2], kTieCap);
-  const int base = cnt4[b * 4 + 1];  // entries below the boundary bin
-  const unsigned long long* Tb = ties + (int64_t)b * kTieCap;
+                                                         int64_t* __restrict__ out_idx,
+                                                         float* __restrict__ out_pts) {
+  const int row = blockIdx.x, cl = row % B;
+  if (sel[row * 4 + 0] < 0) return;
+  const int rem = sel[row * 4 + 1];
+  const int U = cnt4[cl * 4];
+  const int nt = min(cnt4[row * 4 + 2], kTieCap);
+  const int base = cnt4[row * 4 + 1];  // entries below the boundary bin
+  const unsigned long long* Tb = ties + (int64_t)row * kTieCap;
   for (int i = threadIdx.x; i < nt; i += 1024) {
     const unsigned long long v = Tb[i];
     int rank = 0;
     for (int k = 0; k < nt; ++k) rank += Tb[k] < v;
-    if (rank < rem) voxf_emit(b, N, T, U, base + rank, (uint32_t)v, reps, out_idx);
+    if (rank < rem) voxf_emit(row, cl, N, T, U, base + rank, (uint32_t)v, reps, pts, out_idx, out_pts);
   }
 }
 
-__global__ void voxf_gather_kernel(const float* __restrict__ pts, int N, int64_t T,
-                                   const int64_t* __restrict__ out_idx, float* __restrict__ out_pts) {
-  const int b = blockIdx.y;
-  for (int64_t j = blockIdx.x * 256 + threadIdx.x; j < T; j += gridDim.x * 256) {
-    const int64_t r = out_idx[b * T + j];
-    const float* src = pts + ((int64_t)b * N + r) * 3;
-    float* dst = out_pts + (b * T + j) * 3;
-    dst[0] = src[0]; dst[1] = src[1]; dst[2] = src[2];
-  }
-}
-
-static int voxel_fast(const float* pts, int64_t B, int64_t N, int64_t T, void* workspace,
-                      uint64_t seed, int64_t* out_idx, float* out_pts, hipStream_t s) {
-  VoxelFastWS w = carve_voxel_fast(workspace, B, N);
-  const int b = (int)B, n = (int)N;
-  const size_t zero = (size_t)((char*)w.isrep - (char*)w.cnt4) + sizeof(uint32_t) * B * N;
+// memset, stats, insert (+ voxel parameters), reps (+ kept reps), hist, select (+ boundary
+// bin, kept points), ties (+ kept points): 7 launches.
+static int voxel_fast(const float* pts, int64_t B, int64_t N, int64_t copies, int64_t T,
+                      void* workspace, uint64_t seed, int64_t* out_idx, float* out_pts,
+                      hipStream_t s) {
+  VoxelFastWS w = carve_voxel_fast(workspace, B, N, copies);
+  const int b = (int)B, n = (int)N, rows = (int)(B * copies);
+  const size_t zero = (size_t)((char*)(w.isrep + B * N) - (char*)w.cnt4);
   PCST_HIP(hipMemsetAsync(w.cnt4, 0, zero, s), "voxel: memset");
   launch_cloud_stats(pts, b, n, w.mm, s);
-  hipLaunchKernelGGL(vox_params_kernel, dim3((unsigned)B), dim3(64), 0, s, w.mm, b, T,
-                     w.vp);
   hipLaunchKernelGGL(voxf_insert_kernel, dim3((unsigned)cdiv(N, kVoxChunk), b), dim3(256), 0, s,
-                     pts, n, w.vp, w.H, w.tkey,
-                     w.tsum, w.tcnt);
-  hipLaunchKernelGGL(voxf_reps_kernel, dim3(128, b),
-                     dim3(256), 0, s, w.tkey, w.tsum, w.tcnt, w.H, n, T, w.cnt4, w.reps, w.rhash,
-                     w.isrep, out_idx);
+                     pts, n, w.mm, T, w.H, w.tkey, w.tsum, w.tcnt);
+  hipLaunchKernelGGL(voxf_reps_kernel, dim3(128, b), dim3(256), 0, s, pts, w.tkey, w.tsum, w.tcnt,
+                     w.H, n, T, b, (int)copies, w.cnt4, w.reps, w.rhash, w.isrep, out_idx, out_pts);
   const unsigned gs = (unsigned)std::min<int64_t>(cdiv(N, 256), 256);
-  hipLaunchKernelGGL(voxf_hist_kernel, dim3(gs, b), dim3(256), 0, s, n, T, seed, w.cnt4, w.rhash,
-                     w.isrep, w.hist);
-  hipLaunchKernelGGL(voxf_find_kernel, dim3(b), dim3(256), 0, s, w.hist, w.cnt4, n, T, w.sel);
-  hipLaunchKernelGGL(voxf_select_kernel, dim3(128, b), dim3(256), 0, s, n, T, seed, w.sel, w.cnt4,
-                     w.rhash, w.isrep, w.reps, w.ties, out_idx);
-  hipLaunchKernelGGL(voxf_ties_kernel, dim3(b), dim3(1024), 0, s, n, T, w.sel, w.cnt4, w.ties,
-                     w.reps, out_idx);
-  hipLaunchKernelGGL(voxf_gather_kernel, dim3((unsigned)std::min<int64_t>(cdiv(T, 256), 1024), b),
-                     dim3(256), 0, s, pts, n, T, out_idx, out_pts);
+  hipLaunchKernelGGL(voxf_hist_kernel, dim3(gs, rows), dim3(256), 0, s, n, T, b, seed, w.cnt4,
+                     w.rhash, w.isrep, w.hist);
+  hipLaunchKernelGGL(voxf_select_kernel, dim3(128, rows), dim3(256), 0, s, pts, n, T, b, seed,
+                     w.hist, w.sel, w.cnt4, w.rhash, w.isrep, w.reps, w.ties, out_idx, out_pts);
+  hipLaunchKernelGGL(voxf_ties_kernel, dim3(rows), dim3(1024), 0, s, pts, n, T, b, w.sel, w.cnt4,
+                     w.ties, w.reps, out_idx, out_pts);
   PCST_LAUNCH_CHECK("voxel_downsample");
   return PCST_OK;
 }
@@ -666,6 +682,13 @@ using namespace pcst;
 extern "C" int pcst_voxel_workspace_size(int64_t B, int64_t N, size_t* bytes) {
   PCST_CHECK_ARG(B >= 0 && N >= 0 && bytes, "voxel_workspace_size: bad args");
   *bytes = std::max(carve_voxel(nullptr, B, N).bytes, carve_voxel_fast(nullptr, B, N).bytes);
+  return PCST_OK;
+}
+
+extern "C" int pcst_voxel_copies_workspace_size(int64_t B, int64_t N, int64_t copies,
+                                                size_t* bytes) {
+  PCST_CHECK_ARG(B >= 0 && N >= 0 && copies >= 1 && bytes, "voxel_copies_workspace_size: bad args");
+  *bytes = carve_voxel_fast(nullptr, B, N, copies).bytes;
   return PCST_OK;
 }
 
@@ -751,5 +774,17 @@ extern "C" int pcst_voxel_downsample(const float* pts, int64_t B, int64_t N, int
                                      float* out_pts, void* stream) {
   PCST_CHECK_ARG(B > 0 && N > target && target > 0 && N < (1ll << 30), "voxel_downsample: bad shape");
   PCST_CHECK_ARG(pts && workspace && out_idx && out_pts, "voxel_downsample: null pointer");
-  return voxel_fast(pts, B, N, target, workspace, seed, out_idx, out_pts, as_stream(stream));
+  return voxel_fast(pts, B, N, 1, target, workspace, seed, out_idx, out_pts, as_stream(stream));
 }
+
+extern "C" int pcst_voxel_downsample_copies(const float* pts, int64_t B, int64_t N, int64_t copies,
+                                            int64_t target, void* workspace, uint64_t seed,
+                                            int64_t* out_idx, float* out_pts, void* stream) {
+  PCST_CHECK_ARG(B > 0 && copies >= 1 && B * copies < (1 << 15) && N > target && target > 0 &&
+                     N < (1ll << 30),
+                 "voxel_downsample_copies: bad shape");
+  PCST_CHECK_ARG(pts && workspace && out_idx && out_pts, "voxel_downsample_copies: null pointer");
+  return voxel_fast(pts, B, N, copies, target, workspace, seed, out_idx, out_pts,
+                    as_stream(stream));
+}
+

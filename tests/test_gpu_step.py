@@ -131,6 +131,42 @@ def test_knn_vs_oracle(H, N, M, B, sig):
     np.testing.assert_array_equal(out, O.upsample_knn(coarse, orig, idx))
 
 
+def _clustered(rng, N):
+    """tight clusters, a uniform halo and far outliers (sparse shells, exhaustive fallback)"""
+    centers = rng.uniform(-2, 2, (12, 3))
+    pts = centers[rng.integers(0, 12, N)] + rng.standard_normal((N, 3)) * 0.02
+    halo = rng.random(N) < 0.1
+    pts[halo] = rng.uniform(-3, 3, (halo.sum(), 3))
+    far = rng.random(N) < 0.002
+    pts[far] *= 25.0
+    return pts.astype(np.float32)
+
+
+@pytest.mark.parametrize("case", ["clustered", "duplicates", "overfull", "planar"])
+def test_knn_edge_cases(H, case):
+    rng = np.random.default_rng(11)
+    N, M = 20000, 5000
+    if case == "clustered":
+        orig = _clustered(rng, N)
+        idx = rng.choice(N, M, replace=False)
+    elif case == "duplicates":
+        orig = rng.standard_normal((N, 3)).astype(np.float32)
+        idx = rng.choice(N, M, replace=True)  # repeated rows: last coarse value wins
+    elif case == "overfull":
+        # thousands of refs in one cell (more than a wave's LDS stage) + exact distance ties
+        orig = rng.standard_normal((N, 3)).astype(np.float32)
+        orig[:6000] = np.round(orig[:6000] * 1e-3, 6)
+        idx = rng.choice(N, M, replace=False)
+    else:
+        orig = rng.standard_normal((N, 3)).astype(np.float32)
+        orig[:, 2] = 0.0
+        idx = rng.choice(N, M, replace=False)
+    orig, idx = orig[None], idx[None].astype(np.int64)
+    coarse = rng.standard_normal((1, M, 3)).astype(np.float32)
+    out = H.knn3_interp(dev(coarse), dev(orig), dev(idx), check=True).cpu().numpy()
+    np.testing.assert_array_equal(out, O.upsample_knn(coarse, orig, idx))
+
+
 def _noise_params(det_state, H, precision):
     from pointcloud_style_transfer_amd import packing
 
