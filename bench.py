@@ -3,7 +3,8 @@
 MLP, fp32 geometry), one process per GPU.
 
 A "step" = one iteration of DiffusionProcess.guided_sample_loop (diffusion_model.py:238-260):
-voxel downsample of the CFG batch (2 x 120000 -> 2 x 30000), fused noise MLP on 60000 points,
+voxel downsample of the CFG batch (2 x 120000 -> 2 x 30000; the two rows are copies of x, so
+the voxel table is built once and the subset drawn per row), fused noise MLP on 60000 points,
 kNN-3 upsample back to 2 x 120000, CFG + DDIM update.  Each rank denoises its own cloud(s)
 (independent objects: no data-path collective; scaling "weak").  The one-time style encode is
 timed separately and excluded.
@@ -182,6 +183,8 @@ def main():
         enc = encoder_rooflines(hp.downsample(cond)[0], device)
         npred.packed()
         timesteps = torch.linspace(dp.num_timesteps - 1, 0, dp.num_timesteps).long().tolist()
+        t_rows = torch.tensor(timesteps, dtype=torch.long).repeat_interleave(2 * C)
+        t_rows = t_rows.view(len(timesteps), 2 * C).to(device)
         x_cat = torch.cat([x, x]).contiguous()
         ev = []
 
@@ -189,8 +192,8 @@ def main():
             nonlocal x
             t = timesteps[i % len(timesteps)]
             t_prev = timesteps[i % len(timesteps) + 1] if t > 0 else -1
-            t_in = torch.full((2 * C,), t, device=device, dtype=torch.long)
-            xc, xi = hp.downsample(x_cat)
+            t_in = t_rows[i % len(timesteps)]
+            xc, xi = hp.downsample_copies(x, 2)
             if timed:
                 e0 = torch.cuda.Event(enable_timing=True)
                 e1 = torch.cuda.Event(enable_timing=True)

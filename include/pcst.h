@@ -105,6 +105,15 @@ int pcst_voxel_select(const float* pts, int64_t B, int64_t N, int64_t target, vo
                       uint64_t seed, int64_t* out_idx, float* out_pts, void* stream);
 int pcst_voxel_downsample(const float* pts, int64_t B, int64_t N, int64_t target, void* workspace,
                           uint64_t seed, int64_t* out_idx, float* out_pts, void* stream);
+/* The device-drawn downsample of cat([pts] * copies) (the CFG batch of guided_sample_loop,
+ * diffusion_model.py:244-247) from the B distinct clouds: the voxel table and representatives
+ * are built once per cloud, the subset is drawn per row (row = c*B + b) with the row's own keys,
+ * so every row keeps the same set as pcst_voxel_downsample on the concatenated batch with the
+ * same seed.  out_idx [copies*B,target], out_pts [copies*B,target,3]. */
+int pcst_voxel_copies_workspace_size(int64_t B, int64_t N, int64_t copies, size_t* bytes);
+int pcst_voxel_downsample_copies(const float* pts, int64_t B, int64_t N, int64_t copies,
+                                 int64_t target, void* workspace, uint64_t seed, int64_t* out_idx,
+                                 float* out_pts, void* stream);
 /* Copies the replay-validation error word (0 = ok) to err_out (device int32). */
 int pcst_voxel_error(void* workspace, int64_t B, int64_t N, int32_t* err_out, void* stream);
 

@@ -14,7 +14,8 @@ import os
 import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-# PCST_LIB overrides the library path (instrumented experiment builds only)
+# PCST_LIB overrides the library path (experiment builds of tools/ only; the product path and
+# every test load the in-tree libpcst_hip.so)
 LIB_PATH = os.environ.get("PCST_LIB") or os.path.join(_HERE, "libpcst_hip.so")
 
 _P = ctypes.c_void_p
@@ -39,6 +40,8 @@ SIGNATURES = {
     "pcst_voxel_select": [_P, _I, _I, _I, _P, _P, _P, _P, ctypes.c_uint64, _P, _P, _P],
     "pcst_voxel_downsample": [_P, _I, _I, _I, _P, ctypes.c_uint64, _P, _P, _P],
     "pcst_voxel_error": [_P, _I, _I, _P, _P],
+    "pcst_voxel_copies_workspace_size": [_I, _I, _I, _SZ],
+    "pcst_voxel_downsample_copies": [_P, _I, _I, _I, _I, _P, ctypes.c_uint64, _P, _P, _P],
     "pcst_knn_workspace_size": [_I, _I, _I, _SZ],
     "pcst_knn3_interp": [_P, _P, _P, _I, _I, _I, _P, _P, _P],
     "pcst_knn_error": [_P, _I, _I, _I, _P, _P],
@@ -187,24 +190,33 @@ def _workspace(fn, *dims, device):
 
 
 # ----------------------------------------------------------------------------- voxel downsample
-def voxel_downsample(points, target, seed=0, perm_provider=None):
+def voxel_downsample(points, target, seed=0, perm_provider=None, copies=1):
     """HierarchicalProcessor._voxel_grid_downsample_torch for N > target, all clouds at once.
 
     perm_provider=None: the random subset is drawn on the device from `seed`.
     perm_provider(b, n) -> int64 tensor: replay the reference's torch.randperm(n) for cloud b
     (needs the unique-voxel count, so this path synchronises; used for parity runs).
-    Returns (points [B,T,3], idx [B,T] int64)."""
+    copies=k: the result for torch.cat([points] * k) (rows c*B + b) -- on the device-drawn path
+    without building or re-hashing the copies (each row keeps the set the concatenated call
+    keeps for the same seed); the replay path concatenates, as the reference's draws are per row.
+    Returns (points [k*B,T,3], idx [k*B,T] int64)."""
     require_device(points)
     points = _f32(points)
+    if copies > 1 and perm_provider is not None:
+        points = torch.cat([points] * copies)
+        copies = 1
     B, N, _ = points.shape
     dev = points.device
+    if perm_provider is None:
+        ws = _workspace("pcst_voxel_copies_workspace_size", B, N, copies, device=dev)
+        out_idx = torch.empty(copies * B, target, dtype=torch.int64, device=dev)
+        out_pts = torch.empty(copies * B, target, 3, dtype=torch.float32, device=dev)
+        _call("pcst_voxel_downsample_copies", _ptr(points), B, N, copies, target, _ptr(ws),
+              seed & (2**64 - 1), _ptr(out_idx), _ptr(out_pts), _stream())
+        return out_pts, out_idx
     ws = _workspace("pcst_voxel_workspace_size", B, N, device=dev)
     out_idx = torch.empty(B, target, dtype=torch.int64, device=dev)
     out_pts = torch.empty(B, target, 3, dtype=torch.float32, device=dev)
-    if perm_provider is None:
-        _call("pcst_voxel_downsample", _ptr(points), B, N, target, _ptr(ws), seed & (2**64 - 1),
-              _ptr(out_idx), _ptr(out_pts), _stream())
-        return out_pts, out_idx
     counts = torch.empty(2 * B, dtype=torch.int32, device=dev)
     _call("pcst_voxel_stats", _ptr(points), B, N, target, _ptr(ws), _ptr(counts), _stream())
     c = counts.cpu().tolist()

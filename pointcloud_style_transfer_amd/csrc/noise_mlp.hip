@@ -473,24 +473,43 @@ __global__ __launch_bounds__(TR::THREADS) void noise_mlp_kernel(
 
 // cond[c] = b4 + time_proj(emb(t_c)) + style_proj(style_c)   (diffusion_model.py:15-26, 56-58)
 // freqs[64] is the reference's exp table computed on the host with torch's own CPU exp.
+// Grid (clouds, 8): workgroup y computes outputs [32y, 32y + 32); its 8 row groups split the
+// K ranges (16 of the 128 time features, 32 of the 256 style features each) and the partial
+// sums meet in LDS.
+constexpr int kCondSplit = 8;
 __global__ __launch_bounds__(256) void cond_bias_kernel(
     const int64_t* __restrict__ t, const float* __restrict__ style, const float* __restrict__ freqs,
     const float* __restrict__ wt, const float* __restrict__ bt, const float* __restrict__ ws,
     const float* __restrict__ bs, const float* __restrict__ b4, float* __restrict__ cond) {
-  const int c = blockIdx.x, o = threadIdx.x;
+  const int c = blockIdx.x, i = threadIdx.x;
+  const int o = blockIdx.y * 32 + (i & 31), g = i >> 5;
   __shared__ float emb[128];
   __shared__ float sty[256];
+  __shared__ float pa[kCondSplit][32], pb[kCondSplit][32];
   const float tf = (float)t[c];
-  if (o < 64) emb[o] = sinf(tf * freqs[o]);
-  else if (o < 128) emb[o] = cosf(tf * freqs[o - 64]);
-  sty[o] = style[c * 256 + o];
+  if (i < 64) emb[i] = sinf(tf * freqs[i]);
+  else if (i < 128) emb[i] = cosf(tf * freqs[i - 64]);
+  sty[i] = style[c * 256 + i];
   __syncthreads();
-  // wt / ws are the TRANSPOSED weights ([in][out]): lane o reads consecutive addresses
-  float a = bt[o];
-  for (int i = 0; i < 128; ++i) a = fmaf(wt[i * 256 + o], emb[i], a);
-  float b = bs[o];
-  for (int i = 0; i < 256; ++i) b = fmaf(ws[i * 256 + o], sty[i], b);
-  cond[c * 256 + o] = (b4[o] + a) + b;
+  // wt / ws are the TRANSPOSED weights ([in][out]): 32 lanes read 128 contiguous bytes
+  float a = 0.0f;
+#pragma unroll
+  for (int k = g * 16; k < g * 16 + 16; ++k) a = fmaf(wt[k * 256 + o], emb[k], a);
+  float b = 0.0f;
+#pragma unroll
+  for (int k = g * 32; k < g * 32 + 32; ++k) b = fmaf(ws[k * 256 + o], sty[k], b);
+  pa[g][i & 31] = a;
+  pb[g][i & 31] = b;
+  __syncthreads();
+  if (i < 32) {
+    float sa = bt[o], sb = bs[o];
+#pragma unroll
+    for (int q = 0; q < kCondSplit; ++q) {
+      sa += pa[q][i];
+      sb += pb[q][i];
+    }
+    cond[c * 256 + o] = (b4[o] + sa) + sb;
+  }
 }
 
 template <class TR>
@@ -528,7 +547,8 @@ extern "C" int pcst_noise_cond(const int64_t* t, const float* style, int64_t ncl
                                void* stream) {
   PCST_CHECK_ARG(nclouds >= 0, "noise_cond: bad shape");
   if (nclouds == 0) return PCST_OK;
-  hipLaunchKernelGGL(cond_bias_kernel, dim3((unsigned)nclouds), dim3(256), 0, as_stream(stream), t,
+  hipLaunchKernelGGL(cond_bias_kernel, dim3((unsigned)nclouds, 256 / 32), dim3(256), 0,
+                     as_stream(stream), t,
                      style, freqs, wt, bt, ws, bs, b4, cond);
   PCST_LAUNCH_CHECK("noise_cond");
   return PCST_OK;

@@ -178,6 +178,17 @@ class HierarchicalProcessor:
     def downsample(self, points: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
         return self._voxel_grid_downsample_torch(points, self.global_points)
 
+    def downsample_copies(self, points: torch.Tensor,
+                          copies: int) -> Tuple[torch.Tensor, torch.Tensor]:
+        """downsample(torch.cat([points] * copies)) -- the CFG batch of guided_sample_loop
+        (diffusion_model.py:244-247) -- without building or re-hashing the copies.  Replay runs
+        take the concatenated path: the reference draws one permutation per row."""
+        src = _rng.source()
+        if points.shape[1] <= self.global_points or src.replaying:
+            return self.downsample(torch.cat([points] * copies))
+        return _hip.voxel_downsample(points, self.global_points, seed=src.device_seed(),
+                                     copies=copies)
+
     def upsample_knn(self, coarse_points: torch.Tensor, original_points: torch.Tensor,
                      coarse_indices: torch.Tensor) -> torch.Tensor:
         return _hip.knn3_interp(coarse_points, original_points, coarse_indices)
@@ -282,14 +293,20 @@ class DiffusionProcess:
         source = source_points.float().contiguous()
         x_cat = torch.cat([x, x]).contiguous()
         npred = model.noise_predictor
-        for t in timesteps:
-            t_in = torch.full((2 * B,), t, device=device, dtype=torch.long)
+        # the CFG batch's timestep rows for the whole schedule, built once (one copy, no
+        # per-step fill kernel)
+        t_rows = torch.tensor(timesteps, dtype=torch.long).repeat_interleave(2 * B)
+        t_rows = t_rows.view(len(timesteps), 2 * B).to(device)
+        # the reference's t_prev lookup (first occurrence of t, diffusion_model.py:252)
+        t_prevs = [timesteps[timesteps.index(t) + 1] if t > 0 else -1 for t in timesteps]
+        for i, t in enumerate(timesteps):
+            t_in = t_rows[i]
             if use_hierarchical:
-                xc, xi = hp.downsample(x_cat)
+                xc, xi = hp.downsample_copies(x, 2)
                 eps = hp.upsample_knn(npred(xc, t_in, style_in), x_cat, xi)
             else:
                 eps = npred(x_cat, t_in, style_in)
-            t_prev = timesteps[timesteps.index(t) + 1] if t > 0 else -1
+            t_prev = t_prevs[i]
             x = _hip.cfg_ddim_step(x, eps[:B], eps[B:], source, guidance_scale,
                                    self._coeffs(t, t_prev), x_cat=x_cat)
         return x

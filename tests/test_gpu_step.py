@@ -102,6 +102,25 @@ def test_voxel_vs_oracle_random_perm(H, N, T, B, sig):
             assert (cnt <= rc[np.searchsorted(rv, vals)]).all()
 
 
+@pytest.mark.parametrize("N,T,B,copies,sig", [(120000, 30000, 1, 2, (1, 1, 1)),
+                                               (9000, 8000, 2, 3, (1, 1, 1)),
+                                               (20000, 3000, 2, 2, (1, 1, 1e-3))])
+def test_voxel_copies_matches_concat(H, N, T, B, copies, sig):
+    """downsample of cat([x] * copies) from the distinct clouds: per row the same kept set (and
+    the same points) as the concatenated call with the same seed."""
+    rng = np.random.default_rng(N + copies)
+    pts = (rng.standard_normal((B, N, 3)) * np.array(sig)).astype(np.float32)
+    x = dev(pts)
+    p1, i1 = H.voxel_downsample(torch.cat([x] * copies), T, seed=77)
+    p2, i2 = H.voxel_downsample(x, T, seed=77, copies=copies)
+    i1, i2 = i1.cpu().numpy(), i2.cpu().numpy()
+    assert i2.shape == (copies * B, T)
+    np.testing.assert_array_equal(np.sort(i1, 1), np.sort(i2, 1))
+    allp = np.concatenate([pts] * copies)
+    np.testing.assert_array_equal(p2.cpu().numpy(), np.stack([allp[r][i2[r]] for r in range(copies * B)]))
+    np.testing.assert_array_equal(p1.cpu().numpy(), np.stack([allp[r][i1[r]] for r in range(copies * B)]))
+
+
 def test_knn_golden(H, golden):
     g = golden("hierarchical.npz")
     out = H.knn3_interp(dev(g["knn_coarse"]), dev(g["knn_orig"]), dev(g["knn_idx"]), check=True)
