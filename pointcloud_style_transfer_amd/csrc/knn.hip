@@ -20,9 +20,9 @@
 //   2. for lanes not yet settled that hold 3 refs: the cells of the union of their balls (the
 //      current 3rd distance bounds the true one, so a lane's ball holds its answer).
 // A lane is settled once its 3rd-best distance is below the distance to the unscanned region.
-// The refs of a pass are gathered into the wave's LDS window by LDS-DMA (global_load_lds, a
-// per-lane source address: a balanced copy, each lane finds the cell of its slot by a binary
-// search over the lanes' offsets) and every lane screens every staged ref: the fp32 three
+// The refs of a pass are gathered into the wave's LDS window (x, y, z, j arrays) by LDS-DMA
+// (global_load_lds, a per-lane source address: a balanced copy, each lane finds the cell of its
+// slot by a binary search over the lanes' offsets) and every lane screens every staged ref: the fp32 three
 // smallest distances are kept branch-free, then only refs within (1 + 2e-6) of the fp32 3rd
 // best are ranked in exact float64.  Pass 2 runs under a staging budget (a wave's time is
 // bounded); lanes still open after it (sparse neighbourhoods: in the bench trajectory ~0.05 %
@@ -38,7 +38,10 @@
 
 namespace pcst {
 
-constexpr double kRefsPerCell = 8.0;     // refs per cell at the cloud's peak density
+#ifndef KNN_REFS_PER_CELL  // experiment builds may override
+#define KNN_REFS_PER_CELL 6.0
+#endif
+constexpr double kRefsPerCell = KNN_REFS_PER_CELL;  // refs per cell at the cloud's peak density
 constexpr int kCandCap = 512;            // LDS candidates per wave
 constexpr int kBallCells = 512;          // largest cell box one lane's ball may ask for
 constexpr int kBallUnion = 1024;         // largest union box of a ball pass
@@ -412,12 +415,43 @@ __device__ __forceinline__ float dist32(float fx, float fy, float fz, float4 r) 
   return fmaf(ez, ez, fmaf(ey, ey, ex * ex));
 }
 
+typedef float f2 __attribute__((ext_vector_type(2)));
+
+// dist32 on two refs at once (the same IEEE operations per component: v_pk_add/mul/fma_f32)
+__device__ __forceinline__ f2 dist2(f2 qx, f2 qy, f2 qz, f2 X, f2 Y, f2 Z) {
+  const f2 ex = qx - X, ey = qy - Y, ez = qz - Z;
+  return __builtin_elementwise_fma(ez, ez, __builtin_elementwise_fma(ey, ey, ex * ex));
+}
+
+// A wave's LDS window of staged refs as four arrays (x, y, z, j), 16-byte aligned
+struct Win {
+  float* x;
+  float* y;
+  float* z;
+  int* j;
+};
+
+// fp32 distances of refs i..i+3 of the window (i a multiple of 4): 16-byte LDS reads of each
+// coordinate array, packed (v_pk_*) arithmetic, two refs per instruction
+__device__ __forceinline__ void dist4(const Win& W, int i, f2 qx, f2 qy, f2 qz, f2& d01, f2& d23) {
+  const float4 X = *reinterpret_cast<const float4*>(W.x + i);
+  const float4 Y = *reinterpret_cast<const float4*>(W.y + i);
+  const float4 Z = *reinterpret_cast<const float4*>(W.z + i);
+  d01 = dist2(qx, qy, qz, f2{X.x, X.y}, f2{Y.x, Y.y}, f2{Z.x, Z.y});
+  d23 = dist2(qx, qy, qz, f2{X.z, X.w}, f2{Y.z, Y.w}, f2{Z.z, Z.w});
+}
+__device__ __forceinline__ float dist1(const Win& W, int i, float ax, float ay, float az) {
+  return dist32(ax, ay, az, make_float4(W.x[i], W.y[i], W.z[i], 0.0f));
+}
+
 // One query: an fp32 screen and the exact (float64) top-3.
 //   consider(): one candidate at a time (outlier pass): screen against the exact 3rd best.
 //   window():   a staged window of candidates in two phases.  Phase 1 keeps the fp32 three
 //               smallest distances branch-free (min / med3 / med3); phase 2 screens the window
 //               against that fp32 3rd best into a register mask per 64 refs; the survivors
-//               (~3 per lane) are then ranked in float64 by each lane alone.  Every member of the exact top-3 survives
+//               (~3 per lane) are then ranked in float64 by each lane alone.  The window is
+//               four coordinate arrays so both phases use packed fp32 math.  Every member of
+//               the exact top-3 survives
 //               its window's screen: its fp32 distance is within (1 + 3e-7)^2 of its float64
 //               one, and the fp32 3rd best bounds the float64 3rd best the same way (a ref must
 //               never reach phase 1 twice: a repeat would shrink the fp32 3rd best).
@@ -444,27 +478,25 @@ struct Query {
     exact(ref);
     if (t.last(kk) != INFINITY) thr = (float)(t.last(kk) * (1.0 + 2e-6)) + 1e-30f;
   }
-  __device__ __forceinline__ void window(const float4* L, int fill, int kk) {
+  __device__ __forceinline__ void top3_fp32(float d) {
+    const float n0 = fminf(c0, d);
+    const float n1 = __builtin_amdgcn_fmed3f(c0, c1, d);
+    const float n2 = __builtin_amdgcn_fmed3f(c1, c2, d);
+    c0 = n0; c1 = n1; c2 = n2;
+  }
+  __device__ __forceinline__ void window(const Win& W, int fill, int kk) {
+    const float ax = fx, ay = fy, az = fz;  // by value: keeps the query out of private memory
+    const f2 qx = {ax, ax}, qy = {ay, ay}, qz = {az, az};
     int i = 0;
     for (; i + 4 <= fill; i += 4) {
-      float d[4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) d[u] = dist32(fx, fy, fz, L[i + u]);
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const float n0 = fminf(c0, d[u]);
-        const float n1 = __builtin_amdgcn_fmed3f(c0, c1, d[u]);
-        const float n2 = __builtin_amdgcn_fmed3f(c1, c2, d[u]);
-        c0 = n0; c1 = n1; c2 = n2;
-      }
+      f2 d01, d23;
+      dist4(W, i, qx, qy, qz, d01, d23);
+      top3_fp32(d01.x);
+      top3_fp32(d01.y);
+      top3_fp32(d23.x);
+      top3_fp32(d23.y);
     }
-    for (; i < fill; ++i) {
-      const float d = dist32(fx, fy, fz, L[i]);
-      const float n0 = fminf(c0, d);
-      const float n1 = __builtin_amdgcn_fmed3f(c0, c1, d);
-      const float n2 = __builtin_amdgcn_fmed3f(c1, c2, d);
-      c0 = n0; c1 = n1; c2 = n2;
-    }
+    for (; i < fill; ++i) top3_fp32(dist1(W, i, ax, ay, az));
     const float ck = kk >= 3 ? c2 : (kk == 2 ? c1 : c0);
     const float sc = fminf(ck * 1.000002f + 1e-30f, thr);
     // phase 2 per block of 64 staged refs: a register mask of the screened-in refs (no LDS
@@ -474,17 +506,16 @@ struct Query {
       uint64_t m = 0;
       int u = 0;
       for (; u + 4 <= nb; u += 4) {
-        float d[4];
-#pragma unroll
-        for (int v = 0; v < 4; ++v) d[v] = dist32(fx, fy, fz, L[b0 + u + v]);
-#pragma unroll
-        for (int v = 0; v < 4; ++v) m |= (uint64_t)(d[v] <= sc) << (u + v);
+        f2 d01, d23;
+        dist4(W, b0 + u, qx, qy, qz, d01, d23);
+        m |= ((uint64_t)(d01.x <= sc) | ((uint64_t)(d01.y <= sc) << 1) |
+              ((uint64_t)(d23.x <= sc) << 2) | ((uint64_t)(d23.y <= sc) << 3)) << u;
       }
-      for (; u < nb; ++u) m |= (uint64_t)(dist32(fx, fy, fz, L[b0 + u]) <= sc) << u;
+      for (; u < nb; ++u) m |= (uint64_t)(dist1(W, b0 + u, ax, ay, az) <= sc) << u;
       while (m) {
-        const int k = __builtin_ctzll(m);
+        const int k = b0 + __builtin_ctzll(m);
         m &= m - 1;
-        exact(L[b0 + k]);
+        exact(make_float4(W.x[k], W.y[k], W.z[k], __int_as_float(W.j[k])));
       }
     }
     if (t.last(kk) != INFINITY) thr = fminf(thr, (float)(t.last(kk) * (1.0 + 2e-6)) + 1e-30f);
@@ -526,7 +557,7 @@ struct Box {
 // pass) once more than `budget` refs would be staged; otherwise charges them to `budget`.
 __device__ __forceinline__ bool scan_box(const Box& bx, const Box& prev, const Grid& g,
                                          const uint64_t* __restrict__ S,
-                                         const float4* __restrict__ R, float4* L, Query& me,
+                                         const float4* __restrict__ R, const Win& W, Query& me,
                                          int kk, uint32_t& budget) {
   const int lane = threadIdx.x & 63;
   const int nx = bx.x1 - bx.x0 + 1, ny = bx.y1 - bx.y0 + 1;
@@ -572,24 +603,27 @@ __device__ __forceinline__ bool scan_box(const Box& bx, const Box& prev, const G
         for (int st = 32; st >= 1; st >>= 1)
           if (__shfl(off, l + st) <= v) l += st;
         const uint32_t src = __shfl(a, l) + (v - __shfl(off, l));
-        // LDS destination = wave-uniform base + 16 * lane: slot fill + t0 + lane
-        if (t < len)
-          __builtin_amdgcn_global_load_lds((const void*)(R + src),
-                                           (__attribute__((address_space(3))) void*)(L + fill + t0),
-                                           16, 0, 0);
+        // LDS destination = wave-uniform base + 4 * lane: slot fill + t0 + lane of each array
+        if (t < len) {
+          const float* g = reinterpret_cast<const float*>(R + src);
+          __builtin_amdgcn_global_load_lds(g + 0, (__attribute__((address_space(3))) void*)(W.x + fill + t0), 4, 0, 0);
+          __builtin_amdgcn_global_load_lds(g + 1, (__attribute__((address_space(3))) void*)(W.y + fill + t0), 4, 0, 0);
+          __builtin_amdgcn_global_load_lds(g + 2, (__attribute__((address_space(3))) void*)(W.z + fill + t0), 4, 0, 0);
+          __builtin_amdgcn_global_load_lds(g + 3, (__attribute__((address_space(3))) void*)(W.j + fill + t0), 4, 0, 0);
+        }
       }
       fill += (int)len;
       w0 += len;
       if (fill == kCandCap) {
         dma_landed();
-        me.window(L, fill, kk);
+        me.window(W, fill, kk);
         lds_order();
         fill = 0;
       }
     }
   }
   dma_landed();
-  me.window(L, fill, kk);
+  me.window(W, fill, kk);
   lds_order();
   budget -= staged;
   return true;
@@ -623,7 +657,7 @@ __global__ __launch_bounds__(256) void knn_query_kernel(
     const float4* __restrict__ refs, const int32_t* __restrict__ qorder,
     const uint2* __restrict__ chunks, int64_t maxch, const int32_t* __restrict__ nchunk,
     int32_t* __restrict__ olist, int32_t* __restrict__ ocount, float* __restrict__ out) {
-  __shared__ __attribute__((aligned(16))) float4 cand[4][kCandCap];
+  __shared__ __attribute__((aligned(16))) float cand[4][4][kCandCap];
   const int b = blockIdx.y;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   Grid g;
@@ -631,7 +665,7 @@ __global__ __launch_bounds__(256) void knn_query_kernel(
   const uint64_t* S = start + b * Cpad;
   const float4* R = refs + b * M;
   const float* V = vals + b * M * 3;
-  float4* L = cand[wv];
+  const Win W = {cand[wv][0], cand[wv][1], cand[wv][2], reinterpret_cast<int*>(cand[wv][3])};
   const Box none = {1, 0, 1, 0, 1, 0};
   const int nch = nchunk[b];
   for (int item = blockIdx.x * 4 + wv; item < nch; item += gridDim.x * 4) {
@@ -655,7 +689,7 @@ __global__ __launch_bounds__(256) void knn_query_kernel(
     Box pb = {max(lx - 1, 0), min(hx + 1, g.d[0] - 1), max(ly - 1, 0), min(hy + 1, g.d[1] - 1),
               max(lz - 1, 0), min(hz + 1, g.d[2] - 1)};
     uint32_t unlimited = 0xffffffffu;
-    scan_box(pb, none, g, S, R, L, me, kk, unlimited);
+    scan_box(pb, none, g, S, R, W, me, kk, unlimited);
     bool open = valid && !settled(me, pb, g, kk);
     bool ok = true;
 #ifdef KNN_TRACE
@@ -691,7 +725,7 @@ __global__ __launch_bounds__(256) void knn_query_kernel(
 #endif
         if (bb.volume() <= kBallUnion) {
           uint32_t budget = kBallBudget;
-          ok = scan_box(bb, pb, g, S, R, L, me, kk, budget);
+          ok = scan_box(bb, pb, g, S, R, W, me, kk, budget);
 #ifdef KNN_TRACE
           ks2 = ok ? kBallBudget - budget : 0xffffffffu;
 #endif
