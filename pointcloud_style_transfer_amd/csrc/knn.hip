@@ -202,25 +202,23 @@ __global__ __launch_bounds__(256) void knn_count_kernel(
   const int b = blockIdx.y;
   __shared__ float Gs[8];
   __shared__ unsigned long long th[kKnnMaxTiles];
-  if (threadIdx.x < 64) knn_grid_params(stats, b, N, M, Cmax, Gs);
-  for (int t = threadIdx.x; t < T; t += 256) th[t] = 0ull;
-  __syncthreads();
-  if (blockIdx.x == 0 && threadIdx.x < 8) gp[b * 8 + threadIdx.x] = Gs[threadIdx.x];
-  Grid g;
-  g.load(Gs);
-  uint64_t* Cn = cnt + b * Cpad;
+  // the elements' coordinates are loaded first: their latency overlaps the grid parameters
   const int64_t e0 = (int64_t)blockIdx.x * kCountPerBlock + threadIdx.x;
-  int cell[U];
+  float px[U], py[U], pz[U];
+  bool need[U];
   unsigned long long inc[U], old[U];
 #pragma unroll
   for (int u = 0; u < U; ++u) {
     const int64_t e = e0 + u * 256;
-    cell[u] = -1;
+    need[u] = false;
     inc[u] = 0ull;
+    px[u] = py[u] = pz[u] = 0.0f;
     if (e < M) {
       int64_t n = idx[b * M + e];
       n = n < 0 ? 0 : (n >= N ? N - 1 : n);
-      cell[u] = cell_of(orig + (b * N + n) * 3, g);
+      const float* p = orig + (b * N + n) * 3;
+      px[u] = p[0]; py[u] = p[1]; pz[u] = p[2];
+      need[u] = true;
       inc[u] = 1ull;
     } else if (e < M + N) {
       const int64_t n = e - M;
@@ -230,10 +228,25 @@ __global__ __launch_bounds__(256) void knn_count_kernel(
         float* o = out + (b * N + n) * 3;
         o[0] = v[0]; o[1] = v[1]; o[2] = v[2];
       } else {
-        cell[u] = cell_of(orig + (b * N + n) * 3, g);
+        const float* p = orig + (b * N + n) * 3;
+        px[u] = p[0]; py[u] = p[1]; pz[u] = p[2];
+        need[u] = true;
         inc[u] = 1ull << 32;
       }
     }
+  }
+  if (threadIdx.x < 64) knn_grid_params(stats, b, N, M, Cmax, Gs);
+  for (int t = threadIdx.x; t < T; t += 256) th[t] = 0ull;
+  __syncthreads();
+  if (blockIdx.x == 0 && threadIdx.x < 8) gp[b * 8 + threadIdx.x] = Gs[threadIdx.x];
+  Grid g;
+  g.load(Gs);
+  uint64_t* Cn = cnt + b * Cpad;
+  int cell[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const float p[3] = {px[u], py[u], pz[u]};
+    cell[u] = need[u] ? cell_of(p, g) : -1;
   }
 #pragma unroll
   for (int u = 0; u < U; ++u)
@@ -764,9 +777,21 @@ __global__ __launch_bounds__(256) void knn_query_kernel(
   }
 }
 
+// butterfly merge of the lanes' top-3 lists (lanes differing in bits below 2*top): every lane
+// ends with the merged list; lexicographic (d, j) keeps it deterministic
+__device__ __forceinline__ void wave_merge_top3(Top3& t, int top = 32) {
+  for (int off = top; off >= 1; off >>= 1) {
+    const double e0 = __shfl_xor(t.d0, off), e1 = __shfl_xor(t.d1, off), e2 = __shfl_xor(t.d2, off);
+    const int i0 = __shfl_xor(t.j0, off), i1 = __shfl_xor(t.j1, off), i2 = __shfl_xor(t.j2, off);
+    t.push(e0, i0);
+    t.push(e1, i1);
+    t.push(e2, i2);
+  }
+}
+
 // Exhaustive 3-NN of the outlier queries: one workgroup per query, thread i scans refs i,
-// i+1024, ... (4 loads in flight), then a wave butterfly and a merge of the waves
-// (lexicographic (d, j): deterministic).
+// i+1024, ... (8 loads in flight), then a wave butterfly and a 16-lane butterfly over the
+// waves' results.
 template <int kk>
 __global__ __launch_bounds__(kOutlierThreads) void knn_outlier_kernel(
     const float* __restrict__ vals, int64_t N, int64_t M, const float* __restrict__ orig,
@@ -787,37 +812,37 @@ __global__ __launch_bounds__(kOutlierThreads) void knn_outlier_kernel(
     Query me;
     me.init(p[0], p[1], p[2]);
     int64_t i = threadIdx.x;
-    for (; i + 3 * Q < M; i += 4 * Q) {
-      const float4 r0 = R[i], r1 = R[i + Q], r2 = R[i + 2 * Q], r3 = R[i + 3 * Q];
-      me.consider(r0, kk);
-      me.consider(r1, kk);
-      me.consider(r2, kk);
-      me.consider(r3, kk);
-    }
-    for (; i < M; i += Q) me.consider(R[i], kk);
+    for (; i + 7 * Q < M; i += 8 * Q) {  // 8 loads in flight per thread
+      float4 r[8];
 #pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) {
-      const double e0 = __shfl_xor(me.t.d0, off), e1 = __shfl_xor(me.t.d1, off),
-                   e2 = __shfl_xor(me.t.d2, off);
-      const int i0 = __shfl_xor(me.t.j0, off), i1 = __shfl_xor(me.t.j1, off),
-                i2 = __shfl_xor(me.t.j2, off);
-      me.t.push(e0, i0);
-      me.t.push(e1, i1);
-      me.t.push(e2, i2);
+      for (int u = 0; u < 8; ++u) r[u] = R[i + u * Q];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) me.consider(r[u], kk);
     }
+    {
+      float4 r[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (i + u * Q < M) r[u] = R[i + u * Q];
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (i + u * Q < M) me.consider(r[u], kk);
+    }
+    wave_merge_top3(me.t);
     if (lane == 0) {
       sd[wv][0] = me.t.d0; sd[wv][1] = me.t.d1; sd[wv][2] = me.t.d2;
       sj[wv][0] = me.t.j0; sj[wv][1] = me.t.j1; sj[wv][2] = me.t.j2;
     }
     __syncthreads();
-    if (threadIdx.x == 0) {
-      Top3 t = me.t;
-      for (int w = 1; w < W; ++w) {
-        t.push(sd[w][0], sj[w][0]);
-        t.push(sd[w][1], sj[w][1]);
-        t.push(sd[w][2], sj[w][2]);
+    if (wv == 0) {  // the 16 wave results, merged by a 16-lane butterfly of wave 0
+      Top3 t;
+      t.init();
+      if (lane < W) {
+        t.d0 = sd[lane][0]; t.d1 = sd[lane][1]; t.d2 = sd[lane][2];
+        t.j0 = sj[lane][0]; t.j1 = sj[lane][1]; t.j2 = sj[lane][2];
       }
-      idw_write(t, kk, V, out + (b * N + n) * 3);
+      wave_merge_top3(t, W / 2);
+      if (lane == 0) idw_write(t, kk, V, out + (b * N + n) * 3);
     }
     __syncthreads();
   }
