@@ -337,8 +337,15 @@ __global__ void vox_select_kernel(const float* __restrict__ pts, int N, int64_t 
 //      radix select plus an exact sort of the boundary bin.
 constexpr int kSelBins = 4096;
 constexpr int kTieCap = 8192;
-constexpr int kVoxChunk = 2048;  // points aggregated per workgroup in LDS
-constexpr int kVoxLds = 4096;    // LDS table slots (load factor <= 1/2)
+#ifndef VOX_CHUNK  // experiment builds may override
+#define VOX_CHUNK 512
+#endif
+#ifndef VOX_REPS_BLOCKS
+#define VOX_REPS_BLOCKS 512
+#endif
+constexpr int kVoxChunk = VOX_CHUNK;      // points aggregated per workgroup in LDS
+constexpr int kVoxLds = 2 * kVoxChunk;    // LDS table slots (load factor <= 1/2)
+constexpr int kVoxRepsBlocks = VOX_REPS_BLOCKS;  // slot-range workgroups per cloud
 
 // Copies.  guided_sample_loop downsamples the CFG batch cat([x] * 2) (diffusion_model.py:244-247):
 // identical clouds.  With copies = k the input is the B distinct clouds and the output has the
@@ -662,7 +669,7 @@ static int voxel_fast(const float* pts, int64_t B, int64_t N, int64_t copies, in
   launch_cloud_stats(pts, b, n, w.mm, s);
   hipLaunchKernelGGL(voxf_insert_kernel, dim3((unsigned)cdiv(N, kVoxChunk), b), dim3(256), 0, s,
                      pts, n, w.mm, T, w.H, w.tkey, w.tsum, w.tcnt);
-  hipLaunchKernelGGL(voxf_reps_kernel, dim3(128, b), dim3(256), 0, s, pts, w.tkey, w.tsum, w.tcnt,
+  hipLaunchKernelGGL(voxf_reps_kernel, dim3(kVoxRepsBlocks, b), dim3(256), 0, s, pts, w.tkey, w.tsum, w.tcnt,
                      w.H, n, T, b, (int)copies, w.cnt4, w.reps, w.rhash, w.isrep, out_idx, out_pts);
   const unsigned gs = (unsigned)std::min<int64_t>(cdiv(N, 256), 256);
   hipLaunchKernelGGL(voxf_hist_kernel, dim3(gs, rows), dim3(256), 0, s, n, T, b, seed, w.cnt4,
