@@ -401,6 +401,23 @@ __device__ __forceinline__ uint32_t mix32(uint32_t x) {
   return x;
 }
 
+// Cloud statistics (blocks [0, kStatBlocks) of row y) and, in the other blocks, the zeroing of
+// the counters / histograms / tables / rep flags of this call (instead of a separate memset).
+constexpr int kVoxZeroBlocks = 128;
+__global__ __launch_bounds__(256) void voxf_stats_zero_kernel(const float* __restrict__ pts, int N,
+                                                              StatRec* __restrict__ part,
+                                                              uint4* __restrict__ zero,
+                                                              int64_t zero_words) {
+  const int b = blockIdx.y;
+  if (blockIdx.x < kStatBlocks) {
+    cloud_stats_block(pts + (int64_t)b * N * 3, N, blockIdx.x, part + b * kStatBlocks);
+    return;
+  }
+  const int64_t stride = (int64_t)kVoxZeroBlocks * gridDim.y * 256;
+  const int64_t z0 = ((int64_t)b * kVoxZeroBlocks + (blockIdx.x - kStatBlocks)) * 256 + threadIdx.x;
+  for (int64_t i = z0; i < zero_words; i += stride) zero[i] = make_uint4(0u, 0u, 0u, 0u);
+}
+
 // Voxel table insert; the first wave also folds the cloud's min/max partials into the voxel
 // parameters (min xyz, voxel size) for its workgroup.
 __global__ __launch_bounds__(256) void voxf_insert_kernel(const float* __restrict__ pts, int N,
@@ -657,16 +674,16 @@ __global__ __launch_bounds__(1024) void voxf_ties_kernel(const float* __restrict
   }
 }
 
-// memset, stats, insert (+ voxel parameters), reps (+ kept reps), hist, select (+ boundary
-// bin, kept points), ties (+ kept points): 7 launches.
+// stats (+ zeroing), insert (+ voxel parameters), reps (+ kept reps), hist, select (+ boundary
+// bin, kept points), ties (+ kept points): 6 launches.
 static int voxel_fast(const float* pts, int64_t B, int64_t N, int64_t copies, int64_t T,
                       void* workspace, uint64_t seed, int64_t* out_idx, float* out_pts,
                       hipStream_t s) {
   VoxelFastWS w = carve_voxel_fast(workspace, B, N, copies);
   const int b = (int)B, n = (int)N, rows = (int)(B * copies);
   const size_t zero = (size_t)((char*)(w.isrep + B * N) - (char*)w.cnt4);
-  PCST_HIP(hipMemsetAsync(w.cnt4, 0, zero, s), "voxel: memset");
-  launch_cloud_stats(pts, b, n, w.mm, s);
+  hipLaunchKernelGGL(voxf_stats_zero_kernel, dim3(kStatBlocks + kVoxZeroBlocks, b), dim3(256), 0, s,
+                     pts, n, w.mm, reinterpret_cast<uint4*>(w.cnt4), (int64_t)cdiv(zero, 16));
   hipLaunchKernelGGL(voxf_insert_kernel, dim3((unsigned)cdiv(N, kVoxChunk), b), dim3(256), 0, s,
                      pts, n, w.mm, T, w.H, w.tkey, w.tsum, w.tcnt);
   hipLaunchKernelGGL(voxf_reps_kernel, dim3(kVoxRepsBlocks, b), dim3(256), 0, s, pts, w.tkey, w.tsum, w.tcnt,
