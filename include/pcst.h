@@ -88,6 +88,15 @@ int pcst_channel_stats(const float* Z, int64_t M, int64_t O, double* mean, doubl
 int pcst_affine_act(const float* Z, int64_t M, int64_t O, const float* scale, const float* shift,
                     int relu, int64_t pool_ns, float* Y, void* stream);
 
+/* Weight / bias gradient of a per-point linear layer for the training path (autograd of
+ * nn.Linear / Conv2d-1x1, trainer.py:106 backward): dW [O,I] = dZ^T X, db [O] = column sums of
+ * dZ (db may be NULL), with dZ [M,O] and X [M,I] row-major.  Split over row chunks on exact-f32
+ * MFMA, partials combined in chunk order in float64 (deterministic).
+ * workspace: pcst_linear_wgrad_workspace_size() bytes. */
+int pcst_linear_wgrad_workspace_size(int64_t M, int64_t I, int64_t O, size_t* bytes);
+int pcst_linear_wgrad(const float* dZ, const float* X, int64_t M, int64_t I, int64_t O, float* dW,
+                      float* db, void* workspace, void* stream);
+
 /* ---- models/diffusion_model.py --------------------------------------------------------- */
 
 /* HierarchicalProcessor._voxel_grid_downsample_torch (diffusion_model.py:69-122) for all B

@@ -50,6 +50,8 @@ SIGNATURES = {
     "pcst_noise_mlp": [_P, _I, _I, _P, _I, _P, _I, _P, ctypes.c_int, _P, _P],
     "pcst_cfg_ddim_step": [_P, _P, _P, _P, _I, _F, _F, _F, _F, _F, _P, _P, _P],
     "pcst_pointwise_linear": [_P, _I, _I, _P, _I, _P, _P, ctypes.c_int, _I, _P, _P],
+    "pcst_linear_wgrad_workspace_size": [_I, _I, _I, _SZ],
+    "pcst_linear_wgrad": [_P, _P, _I, _I, _I, _P, _P, _P, _P],
     "pcst_channel_stats_workspace_size": [_I, _SZ],
     "pcst_channel_stats": [_P, _I, _I, _P, _P, _P, _P],
     "pcst_affine_act": [_P, _I, _I, _P, _P, ctypes.c_int, _I, _P, _P],
@@ -327,6 +329,21 @@ def pointwise_linear(X, W, scale=None, shift=None, relu=False, pool_ns=0):
           _ptr(None if scale is None else _f32(scale)), _ptr(None if shift is None else _f32(shift)),
           int(relu), pool_ns, _ptr(Y), _stream())
     return Y
+
+
+def linear_wgrad(dZ, X, bias=True):
+    """dZ [M,O], X [M,I] -> (dW = dZ^T X [O,I], db = dZ^T 1 [O] or None); deterministic."""
+    require_device(dZ, X)
+    dZ, X = _f32(dZ), _f32(X)
+    M, O = dZ.shape
+    I = X.shape[1]
+    if X.shape[0] != M:
+        raise RuntimeError(f"linear_wgrad: row mismatch {tuple(dZ.shape)} vs {tuple(X.shape)}")
+    ws = _workspace("pcst_linear_wgrad_workspace_size", M, I, O, device=dZ.device)
+    dW = torch.empty(O, I, dtype=torch.float32, device=dZ.device)
+    db = torch.empty(O, dtype=torch.float32, device=dZ.device) if bias else None
+    _call("pcst_linear_wgrad", _ptr(dZ), _ptr(X), M, I, O, _ptr(dW), _ptr(db), _ptr(ws), _stream())
+    return dW, db
 
 
 def channel_stats(Z):

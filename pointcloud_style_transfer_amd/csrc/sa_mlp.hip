@@ -135,6 +135,97 @@ __global__ void affine_act_kernel(const float* __restrict__ Z, int64_t M, int O,
   }
 }
 
+// Weight gradient of a per-point linear layer (training path, models/_autograd.py):
+//   dW[o, i] = sum_m dZ[m, o] * X[m, i]      db[o] = sum_m dZ[m, o]
+// dZ [M, O] and X [M, I] are read in their natural row-major layout (no transposed copies).
+// The reduction over the M rows (240k for the noise predictor at B=8) is split into chunks:
+// grid = (O tiles x I tiles, chunks); each workgroup reduces its rows on exact-f32 MFMA into a
+// partial [O, I] tile, and wgrad_combine sums the partials in chunk order in float64, so the
+// gradient is deterministic.  The MFMA A operand is dZ^T (lane = o), B is X (lane = i); both
+// tiles are staged k-major in LDS (row stride 96 floats: the two half-waves read rows kk and
+// kk+1 from disjoint bank ranges).
+constexpr int kWgLd = 96;
+
+__global__ __launch_bounds__(256) void wgrad_partial_kernel(const float* __restrict__ dZ,
+                                                            const float* __restrict__ X, int64_t M,
+                                                            int I, int O, int64_t rows_per_chunk,
+                                                            int tiles_i, float* __restrict__ partW,
+                                                            float* __restrict__ partB) {
+  __shared__ float As[kBK][kWgLd];  // dZ[m][o]
+  __shared__ float Bs[kBK][kWgLd];  // X[m][i]
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wr = wid >> 1, wc = wid & 1, h = lane >> 5, l32 = lane & 31;
+  const int o0 = (blockIdx.x / tiles_i) * kBN, i0 = (blockIdx.x % tiles_i) * kBN;
+  const int chunk = blockIdx.y;
+  const int64_t mb = (int64_t)chunk * rows_per_chunk;
+  const int64_t me = mb + rows_per_chunk < M ? mb + rows_per_chunk : M;
+  const bool bias = partB != nullptr && i0 == 0;
+  f32x16 acc = f32x16{};
+  float bsum = 0.0f;
+  for (int64_t k0 = mb; k0 < me; k0 += kBK) {
+#pragma unroll
+    for (int e = tid; e < kBK * kBN; e += 256) {
+      const int r = e >> 6, c = e & 63;
+      const int64_t m = k0 + r;
+      const bool mv = m < me;
+      As[r][c] = (mv && o0 + c < O) ? dZ[m * O + o0 + c] : 0.0f;
+      Bs[r][c] = (mv && i0 + c < I) ? X[m * I + i0 + c] : 0.0f;
+    }
+    __syncthreads();
+    if (bias && tid < kBN) {
+#pragma unroll 8
+      for (int r = 0; r < kBK; ++r) bsum += As[r][tid];
+    }
+#pragma unroll
+    for (int kk = 0; kk < kBK; kk += 2) {
+      const float a = As[kk + h][wr * 32 + l32];
+      const float b = Bs[kk + h][wc * 32 + l32];
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc, 0, 0, 0);
+    }
+    __syncthreads();
+  }
+  // C layout: column (i) = lane & 31, row (o) = crow(r, h)
+  const int i = i0 + wc * 32 + l32;
+  float* pw = partW + (int64_t)chunk * O * I;
+  if (i < I) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int o = o0 + wr * 32 + crow(r, h);
+      if (o < O) pw[(int64_t)o * I + i] = acc[r];
+    }
+  }
+  if (bias && tid < kBN && o0 + tid < O) partB[(int64_t)chunk * O + o0 + tid] = bsum;
+}
+
+// out[e] = sum over chunks of part[c][e], in chunk order, float64
+__global__ void wgrad_combine_kernel(const float* __restrict__ part, int64_t n, int chunks,
+                                     float* __restrict__ out) {
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < n;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    double s = 0.0;
+    for (int c = 0; c < chunks; ++c) s += (double)part[(int64_t)c * n + e];
+    out[e] = (float)s;
+  }
+}
+
+struct WgradPlan {
+  int tiles_i, tiles_o, chunks;
+  int64_t rows_per_chunk;
+};
+
+// enough workgroups to fill 256 CUs several times over; chunks of >= 256 rows
+static WgradPlan wgrad_plan(int64_t M, int64_t I, int64_t O) {
+  WgradPlan p;
+  p.tiles_i = (int)cdiv(I, kBN);
+  p.tiles_o = (int)cdiv(O, kBN);
+  const int64_t tiles = (int64_t)p.tiles_i * p.tiles_o;
+  int64_t chunks = cdiv(2048, tiles);
+  chunks = std::max<int64_t>(1, std::min<int64_t>(chunks, cdiv(M, 256)));
+  p.rows_per_chunk = cdiv(cdiv(M, chunks), kBK) * kBK;
+  p.chunks = (int)cdiv(M, p.rows_per_chunk);
+  return p;
+}
+
 }  // namespace pcst
 
 using namespace pcst;
@@ -191,5 +282,39 @@ extern "C" int pcst_affine_act(const float* Z, int64_t M, int64_t O, const float
   hipLaunchKernelGGL(affine_act_kernel, dim3((unsigned)g), dim3(256), 0, s, Z, M, (int)O, scale,
                      shift, relu, pool_ns, Y);
   PCST_LAUNCH_CHECK("affine_act");
+  return PCST_OK;
+}
+
+extern "C" int pcst_linear_wgrad_workspace_size(int64_t M, int64_t I, int64_t O, size_t* bytes) {
+  PCST_CHECK_ARG(M >= 0 && I > 0 && O > 0 && bytes, "linear_wgrad_workspace_size: bad args");
+  const WgradPlan p = wgrad_plan(std::max<int64_t>(M, 1), I, O);
+  *bytes = sizeof(float) * (size_t)p.chunks * (size_t)(O * I + O);
+  return PCST_OK;
+}
+
+extern "C" int pcst_linear_wgrad(const float* dZ, const float* X, int64_t M, int64_t I,
+                                 int64_t O, float* dW, float* db, void* workspace, void* stream) {
+  PCST_CHECK_ARG(M >= 0 && I > 0 && O > 0 && I < (1 << 20) && O < (1 << 20),
+                 "linear_wgrad: bad shape");
+  PCST_CHECK_ARG(dW && workspace && (M == 0 || (dZ && X)), "linear_wgrad: null pointer");
+  hipStream_t s = as_stream(stream);
+  if (M == 0) {
+    PCST_HIP(hipMemsetAsync(dW, 0, sizeof(float) * O * I, s), "memset");
+    if (db) PCST_HIP(hipMemsetAsync(db, 0, sizeof(float) * O, s), "memset");
+    return PCST_OK;
+  }
+  const WgradPlan p = wgrad_plan(M, I, O);
+  float* partW = static_cast<float*>(workspace);
+  float* partB = db ? partW + (int64_t)p.chunks * O * I : nullptr;
+  hipLaunchKernelGGL(wgrad_partial_kernel, dim3((unsigned)(p.tiles_i * p.tiles_o), (unsigned)p.chunks),
+                     dim3(256), 0, s, dZ, X, M, (int)I, (int)O, p.rows_per_chunk, p.tiles_i, partW,
+                     partB);
+  const int64_t n = O * I;
+  hipLaunchKernelGGL(wgrad_combine_kernel, dim3((unsigned)std::min<int64_t>(cdiv(n, 256), 2048)),
+                     dim3(256), 0, s, partW, n, p.chunks, dW);
+  if (db)
+    hipLaunchKernelGGL(wgrad_combine_kernel, dim3((unsigned)cdiv(O, 256)), dim3(256), 0, s, partB,
+                       O, p.chunks, db);
+  PCST_LAUNCH_CHECK("linear_wgrad");
   return PCST_OK;
 }

@@ -4,10 +4,9 @@
   forward   Y  = act(X W^T + b)                      pcst_pointwise_linear
   backward  dZ = dY * [Y > 0]  (ReLU)
             dX = dZ W          = linear(dZ, W^T)     pcst_pointwise_linear
-            dW = dZ^T X        = linear(dZ^T, X^T)   pcst_pointwise_linear (K = rows)
-            db = dZ^T 1        = linear(dZ^T, 1)     pcst_pointwise_linear
-All products are exact-f32 MFMA; the reduction over rows is inside one kernel (no atomics),
-so gradients are deterministic.
+            dW = dZ^T X, db = dZ^T 1                  pcst_linear_wgrad (split over row chunks)
+All products are exact-f32 MFMA; the row reduction combines fixed chunks in order (no
+atomics), so gradients are deterministic.
 """
 from __future__ import annotations
 
@@ -38,13 +37,10 @@ class LinearFn(torch.autograd.Function):
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
             dx = _hip.pointwise_linear(dz, W.t().contiguous()).view(ctx.xshape)
-        if ctx.needs_input_grad[1] or (ctx.has_bias and ctx.needs_input_grad[2]):
-            dzt = dz.t().contiguous()
-            if ctx.needs_input_grad[1]:
-                dw = _hip.pointwise_linear(dzt, x2.t().contiguous()).view(ctx.wshape)
-            if ctx.has_bias and ctx.needs_input_grad[2]:
-                ones = torch.ones(1, dz.shape[0], device=dz.device)
-                db = _hip.pointwise_linear(dzt, ones).view(-1)
+        need_b = ctx.has_bias and ctx.needs_input_grad[2]
+        if ctx.needs_input_grad[1] or need_b:
+            dw, db = _hip.linear_wgrad(dz, x2, bias=need_b)
+            dw = dw.view(ctx.wshape) if ctx.needs_input_grad[1] else None
         return dx, dw, db, None
 
 

@@ -1,0 +1,130 @@
+"""Trainer-step benchmark: BASELINE configs[2] (one DiffusionTrainer step, batch 8 x 120k-pt
+clouds, L1 + Chamfer loss, 1 GPU) and configs[3] under torchrun (8 clouds per rank, DDP with
+the RCCL gradient all-reduce).
+
+A "step" is DiffusionTrainer.train_step (trainer.py:70-127) with gradient_accumulation_steps
+= 1, so every timed step runs the forward (style encode with FPS / ball query / SA MLPs, voxel
+downsample, noise MLP), the L1 + Chamfer loss, the backward over the HIP kernels, clip, AdamW
+and the EMA update.  Inputs are resident in HBM before the timed region.  Prints one JSON line
+on rank 0; the Chamfer forward kernel is timed with HIP events on the launch stream.
+
+    python tools/bench_train.py [--batch 8] [--steps 5] [--warmup 2]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 tools/bench_train.py
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import tempfile
+import time
+
+import numpy as np
+import torch
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+
+CHAMFER_FLOP_PER_PAIR = 8          # VALU fp32, 8 FLOP per pair
+VALU_F32_PEAK_TFLOPS = 157.3       # MI355X vector fp32 (MI355X_MICROARCH.md)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=8, help="clouds per rank")
+    ap.add_argument("--points", type=int, default=120000)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--amp", type=int, default=1, help="Config.use_amp (reference default 1)")
+    args = ap.parse_args()
+
+    from pointcloud_style_transfer_amd import _hip
+    from pointcloud_style_transfer_amd.config.config import Config
+    from pointcloud_style_transfer_amd.distributed import init_from_env, max_over_ranks, shard
+    from pointcloud_style_transfer_amd.synthetic import lidar_like_cloud
+    from pointcloud_style_transfer_amd.training.trainer import DiffusionTrainer
+
+    world, rank, local = init_from_env("nccl")
+    torch.cuda.set_device(local if world > 1 else 0)
+    device = torch.device("cuda", torch.cuda.current_device())
+    logdir = tempfile.mkdtemp(prefix="pcst_train_")
+    cfg = Config(make_dirs=False, log_dir=logdir, checkpoint_dir=logdir, use_amp=bool(args.amp),
+                 gradient_accumulation_steps=1, batch_size=args.batch)
+    torch.manual_seed(0)
+    trainer = DiffusionTrainer(cfg, device=str(device))
+    trainer.model.train()
+
+    B = args.batch
+    mine = shard(world * B, rank, world)
+    sim = torch.from_numpy(np.stack([lidar_like_cloud(1000 + i, args.points) for i in mine]))
+    real = torch.from_numpy(np.stack([lidar_like_cloud(2000 + i, args.points) for i in mine]))
+    batch = {"sim_full": sim.to(device), "real_full": real.to(device)}
+
+    # Chamfer forward kernel timing: wrap the ABI call with HIP events on its stream
+    ev = []
+    orig = _hip.chamfer_fwd
+
+    def timed_chamfer(pred, target):
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record()
+        out = orig(pred, target)
+        e1.record()
+        ev.append((e0, e1, pred.shape[0] * pred.shape[1] * target.shape[1]))
+        return out
+
+    _hip.chamfer_fwd = timed_chamfer
+    for i in range(args.warmup):
+        trainer.train_step(batch, i, 1 << 30)
+    ev.clear()
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        loss, _ = trainer.train_step(batch, i, 1 << 30)
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        dist.barrier()
+        elapsed = max_over_ranks(elapsed, device=device)
+    _hip.chamfer_fwd = orig
+
+    ch_ms = float(np.mean([a.elapsed_time(b) for a, b, _ in ev])) if ev else None
+    pairs = ev[0][2] if ev else 0
+    # one forward call evaluates both directions over the same pairs (2 x B x N x M)
+    ch_tflops = (2 * pairs * CHAMFER_FLOP_PER_PAIR / (ch_ms * 1e-3) / 1e12) if ch_ms else None
+    value = world * B * args.steps / elapsed
+    if rank == 0:
+        print(json.dumps({
+            "metric": "trainer clouds/sec (120k-pt clouds, L1 + Chamfer)",
+            "value": round(value, 4),
+            "unit": "clouds/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 2),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "dtype": "fp32 (autocast on)" if args.amp else "fp32",
+            "data": "synthetic (numpy PCG64 anisotropic Gaussian clouds, random-init weights)",
+            "config": {"workload": "DiffusionTrainer.train_step, accumulation 1 "
+                                   "(BASELINE configs[2]; configs[3] under torchrun)",
+                       "clouds_per_gpu": B, "global_batch": world * B, "points": args.points,
+                       "parallelism": f"ddp{world}" if world > 1 else "single"},
+            "chamfer_fwd": {"bound": "valu fp32", "avg_launch_ms": round(ch_ms, 3) if ch_ms else None,
+                            "pairs_per_direction": pairs,
+                            "achieved": round(ch_tflops, 2) if ch_tflops else None,
+                            "peak": VALU_F32_PEAK_TFLOPS, "unit": "TFLOP/s",
+                            "frac": round(ch_tflops / VALU_F32_PEAK_TFLOPS, 4) if ch_tflops else None},
+            "final_loss": float(loss),
+        }), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
