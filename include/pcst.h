@@ -181,6 +181,19 @@ int pcst_l1_fwd(const float* a, const float* b, int64_t n, float* out, void* wor
 int pcst_l1_bwd(const float* a, const float* b, int64_t n, const float* grad_out, float* grad_a,
                 void* stream);
 
+/* ---- evaluation/metrics.py, compare.py (measurement only) -------------------------------- */
+
+/* K nearest rows of Q [B,M,3] for every row of P [B,N,3] (1 <= k <= 16): dist [B,N,k] float64
+ * Euclidean distances, ascending (ties to the lower index), idx [B,N,k] int32 (may be NULL).
+ * Replaces torch.cdist + min (metrics.py:31-41,100-104), sklearn NearestNeighbors
+ * (metrics.py:124-127,146-148) and cKDTree.query (compare.py:22-34). */
+int pcst_knn_dist(const float* P, const float* Q, int64_t B, int64_t N, int64_t M, int64_t k,
+                  double* dist, int32_t* idx, void* stream);
+/* earth_mover_distance's greedy matching (metrics.py:46-90), bit-exact: out [B] float32 =
+ * (sum over i in order of the nearest unused target's float64 distance) / N.  M <= 262144. */
+int pcst_emd_greedy(const float* P, const float* Q, int64_t B, int64_t N, int64_t M, float* out,
+                    void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -422,3 +422,73 @@ def diffusion_loss(pred_noise, actual_noise, pred_pts=None, tgt_pts=None,
         d["chamfer_loss"] = cl
     d["total_loss"] = total
     return total, d
+
+
+# ----------------------------------------------------------------------------- metrics
+def knn_dist(P, Q, k=1):
+    """Brute-force float64 Euclidean distances of the k nearest rows of Q for every row of P
+    (ties to the lower index), as sklearn NearestNeighbors / cKDTree / scipy cdist compute them
+    from fp32 inputs (evaluation/metrics.py:124-127,146-148; compare.py:22-34).  [B,N,k]."""
+    P = np.asarray(P, np.float64)
+    Q = np.asarray(Q, np.float64)
+    out = np.empty(P.shape[:2] + (k,))
+    for b in range(P.shape[0]):
+        for s in range(0, P.shape[1], 512):
+            d = P[b, s:s + 512, None, :] - Q[b, None, :, :]
+            d = np.sqrt((d[..., 0] * d[..., 0] + d[..., 1] * d[..., 1]) + d[..., 2] * d[..., 2])
+            o = np.argsort(d, axis=1, kind="stable")[:, :k]
+            out[b, s:s + 512] = np.take_along_axis(d, o, axis=1)
+    return out
+
+
+def metric_chamfer(pred, target, bidirectional=True):
+    """evaluation/metrics.py:20-44 (exact distances; the reference's cdist is fp32)."""
+    a = knn_dist(pred, target)[..., 0].mean(1)
+    if not bidirectional:
+        return a
+    return (a + knn_dist(target, pred)[..., 0].mean(1)) / 2
+
+
+def metric_hausdorff(pred, target):
+    """evaluation/metrics.py:92-107."""
+    return np.maximum(knn_dist(pred, target)[..., 0].max(1), knn_dist(target, pred)[..., 0].max(1))
+
+
+def metric_coverage(pred, target, threshold=0.01):
+    """evaluation/metrics.py:109-135."""
+    return float(np.mean((knn_dist(target, pred)[..., 0] < threshold).mean(1)))
+
+
+def metric_uniformity(points, k=8):
+    """evaluation/metrics.py:137-173."""
+    md = knn_dist(points, points, k + 1)[..., 1:].mean(2)
+    sc = [1.0 / (1.0 + s / m) if m > 0 else 0.0 for s, m in zip(md.std(1), md.mean(1))]
+    return float(np.mean(sc))
+
+
+def emd_greedy(pred, target):
+    """evaluation/metrics.py:46-90: greedy matching in pred order, scipy cdist distances,
+    strict < over ascending j; total summed in order, / N, cast to float32."""
+    out = []
+    for b in range(pred.shape[0]):
+        p = np.asarray(pred[b], np.float64)
+        q = np.asarray(target[b], np.float64)
+        d = p[:, None, :] - q[None, :, :]
+        D = np.sqrt((d[..., 0] * d[..., 0] + d[..., 1] * d[..., 1]) + d[..., 2] * d[..., 2])
+        used = np.zeros(len(q), bool)
+        total = 0.0
+        for i in range(len(p)):
+            row = np.where(used, np.inf, D[i])
+            j = int(np.argmin(row))   # first index of the minimum
+            total += float(row[j])
+            used[j] = True
+        out.append(total / len(p))
+    return np.array(out, dtype=np.float32)
+
+
+def similarity(pcd1, pcd2, threshold):
+    """compare.py:6-43 -> (precision %, recall %, F1)."""
+    prec = np.mean(knn_dist(pcd2[None], pcd1[None])[0, :, 0] < threshold)
+    rec = np.mean(knn_dist(pcd1[None], pcd2[None])[0, :, 0] < threshold)
+    f = 0.0 if prec + rec == 0 else 2 * (prec * rec) / (prec + rec)
+    return prec * 100, rec * 100, f

@@ -50,6 +50,8 @@ SIGNATURES = {
     "pcst_noise_mlp": [_P, _I, _I, _P, _I, _P, _I, _P, ctypes.c_int, _P, _P],
     "pcst_cfg_ddim_step": [_P, _P, _P, _P, _I, _F, _F, _F, _F, _F, _P, _P, _P],
     "pcst_pointwise_linear": [_P, _I, _I, _P, _I, _P, _P, ctypes.c_int, _I, _P, _P],
+    "pcst_knn_dist": [_P, _P, _I, _I, _I, _I, _P, _P, _P],
+    "pcst_emd_greedy": [_P, _P, _I, _I, _I, _P, _P],
     "pcst_linear_wgrad_workspace_size": [_I, _I, _I, _SZ],
     "pcst_linear_wgrad": [_P, _P, _I, _I, _I, _P, _P, _P, _P],
     "pcst_channel_stats_workspace_size": [_I, _SZ],
@@ -416,3 +418,29 @@ def l1_bwd(a, b, grad_out):
     _call("pcst_l1_bwd", _ptr(a), _ptr(b), a.numel(), _ptr(_f32(grad_out.reshape(1))), _ptr(ga),
           _stream())
     return ga
+
+
+# ----------------------------------------------------------------------------- metrics
+def knn_dist(P, Q, k=1, with_index=False):
+    """P [B,N,3], Q [B,M,3] -> float64 distances [B,N,k] to the k nearest rows of Q (ascending,
+    ties to the lower index) and, with_index, their int64 indices [B,N,k]."""
+    require_device(P, Q)
+    P, Q = _f32(P), _f32(Q)
+    B, N, _ = P.shape
+    M = Q.shape[1]
+    if Q.shape[0] != B:
+        raise RuntimeError(f"knn_dist: batch mismatch {tuple(P.shape)} vs {tuple(Q.shape)}")
+    dist = torch.empty(B, N, k, dtype=torch.float64, device=P.device)
+    idx = torch.empty(B, N, k, dtype=torch.int32, device=P.device) if with_index else None
+    _call("pcst_knn_dist", _ptr(P), _ptr(Q), B, N, M, k, _ptr(dist), _ptr(idx), _stream())
+    return (dist, idx.long()) if with_index else dist
+
+
+def emd_greedy(P, Q):
+    """Greedy-matching EMD of metrics.py:46-90 -> float32 [B]."""
+    require_device(P, Q)
+    P, Q = _f32(P), _f32(Q)
+    B, N, _ = P.shape
+    out = torch.empty(B, dtype=torch.float32, device=P.device)
+    _call("pcst_emd_greedy", _ptr(P), _ptr(Q), B, N, Q.shape[1], _ptr(out), _stream())
+    return out
