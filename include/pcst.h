@@ -181,6 +181,16 @@ int pcst_l1_fwd(const float* a, const float* b, int64_t n, float* out, void* wor
 int pcst_l1_bwd(const float* a, const float* b, int64_t n, const float* grad_out, float* grad_a,
                 void* stream);
 
+/* ---- data/preprocessing.py (offline) ------------------------------------------------------ */
+
+/* Per-point part of PointCloudPreprocessor._voxel_grid_downsample_numpy (preprocessing.py:45-104):
+ * key [n] = voxel coordinates floor(f32(f32(p - min) / voxel_size)) packed 21 bits per axis,
+ * dist [n] = float64 distance to the voxel centre min + (coord + 0.5) * voxel_size.  xyz_min is a
+ * HOST pointer (3 floats); *overflow (device int, zeroed by the caller) is set when a coordinate
+ * leaves [0, 2^21). */
+int pcst_voxel_center_dist(const float* pts, int64_t n, const float* xyz_min, float voxel_size,
+                           int64_t* key, double* dist, int* overflow, void* stream);
+
 /* ---- evaluation/metrics.py, compare.py (measurement only) -------------------------------- */
 
 /* K nearest rows of Q [B,M,3] for every row of P [B,N,3] (1 <= k <= 16): dist [B,N,k] float64

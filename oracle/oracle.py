@@ -492,3 +492,28 @@ def similarity(pcd1, pcd2, threshold):
     rec = np.mean(knn_dist(pcd1[None], pcd2[None])[0, :, 0] < threshold)
     f = 0.0 if prec + rec == 0 else 2 * (prec * rec) / (prec + rec)
     return prec * 100, rec * 100, f
+
+
+# ----------------------------------------------------------------------------- offline preprocessing
+def voxel_center_reps(points, target_size):
+    """data/preprocessing.py:56-93: voxel representatives (point nearest the voxel centre,
+    first index on ties) in first-appearance voxel order; float32 grid math, float64 norms."""
+    points = np.asarray(points, np.float32)
+    mn = points.min(axis=0)
+    rng_ = points.max(axis=0) - mn
+    rng_[rng_ < 1e-6] = 1.0
+    vs = (rng_.prod() / target_size) ** (1 / 3) * 1.2
+    if vs < 1e-6:
+        vs = np.float32(1e-3)
+    vox = np.floor((points - mn) / vs).astype(np.int64)
+    ctr = mn.astype(np.float64) + (vox + 0.5) * np.float64(vs)
+    d = points.astype(np.float64) - ctr
+    dist = np.sqrt((d[:, 0] * d[:, 0] + d[:, 1] * d[:, 1]) + d[:, 2] * d[:, 2])
+    key = (vox[:, 0] << 42) | (vox[:, 1] << 21) | vox[:, 2]
+    o = np.lexsort((np.arange(len(points)), dist, key))
+    ks = key[o]
+    head = np.ones(len(o), bool)
+    head[1:] = ks[1:] != ks[:-1]
+    reps = o[head]
+    _, first = np.unique(key, return_index=True)   # first index per voxel, sorted by key
+    return reps[np.argsort(first, kind="stable")]

@@ -11,6 +11,7 @@ from __future__ import annotations
 import ctypes
 import os
 
+import numpy as np
 import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -50,6 +51,7 @@ SIGNATURES = {
     "pcst_noise_mlp": [_P, _I, _I, _P, _I, _P, _I, _P, ctypes.c_int, _P, _P],
     "pcst_cfg_ddim_step": [_P, _P, _P, _P, _I, _F, _F, _F, _F, _F, _P, _P, _P],
     "pcst_pointwise_linear": [_P, _I, _I, _P, _I, _P, _P, ctypes.c_int, _I, _P, _P],
+    "pcst_voxel_center_dist": [_P, _I, _P, ctypes.c_float, _P, _P, _P, _P],
     "pcst_knn_dist": [_P, _P, _I, _I, _I, _I, _P, _P, _P],
     "pcst_emd_greedy": [_P, _P, _I, _I, _I, _P, _P],
     "pcst_linear_wgrad_workspace_size": [_I, _I, _I, _SZ],
@@ -444,3 +446,21 @@ def emd_greedy(P, Q):
     out = torch.empty(B, dtype=torch.float32, device=P.device)
     _call("pcst_emd_greedy", _ptr(P), _ptr(Q), B, N, Q.shape[1], _ptr(out), _stream())
     return out
+
+
+# ----------------------------------------------------------------------------- offline preprocessing
+def voxel_center_dist(points, xyz_min, voxel_size):
+    """points [n,3] (device) -> (packed voxel key int64 [n], float64 distance to the voxel
+    centre [n]) of preprocessing.py:71-85, with xyz_min / voxel_size computed by the caller."""
+    require_device(points)
+    points = _f32(points)
+    n = points.shape[0]
+    mn = (ctypes.c_float * 3)(*[float(v) for v in np.asarray(xyz_min, dtype=np.float32)])
+    key = torch.empty(n, dtype=torch.int64, device=points.device)
+    dist = torch.empty(n, dtype=torch.float64, device=points.device)
+    ovf = torch.zeros(1, dtype=torch.int32, device=points.device)
+    _call("pcst_voxel_center_dist", _ptr(points), n, ctypes.cast(mn, ctypes.c_void_p),
+          ctypes.c_float(float(np.float32(voxel_size))), _ptr(key), _ptr(dist), _ptr(ovf), _stream())
+    if int(ovf.item()):
+        raise RuntimeError("pcst: voxel coordinates exceed 2^21 per axis")
+    return key, dist
