@@ -97,6 +97,17 @@ int pcst_linear_wgrad_workspace_size(int64_t M, int64_t I, int64_t O, size_t* by
 int pcst_linear_wgrad(const float* dZ, const float* X, int64_t M, int64_t I, int64_t O, float* dW,
                       float* db, void* workspace, void* stream);
 
+/* bf16-MFMA variants for the training path under torch.autocast (trainer.py:81-106; the
+ * reference's CUDA autocast runs Linear layers in half precision): operands are fp32 tensors
+ * rounded to bf16 in LDS, accumulation and outputs fp32.
+ * gemm_nt: C [M,O] = act(scale*(A [M,K] . B [O,K]^T) + shift) (scale/shift may be NULL).
+ * linear_wgrad_bf16: as pcst_linear_wgrad (db from the unrounded fp32 dZ). */
+int pcst_gemm_nt_bf16(const float* A, int64_t M, int64_t K, const float* B, int64_t O,
+                      const float* scale, const float* shift, int relu, float* C, void* stream);
+int pcst_linear_wgrad_bf16_workspace_size(int64_t M, int64_t I, int64_t O, size_t* bytes);
+int pcst_linear_wgrad_bf16(const float* dZ, const float* X, int64_t M, int64_t I, int64_t O,
+                           float* dW, float* db, void* workspace, void* stream);
+
 /* ---- models/diffusion_model.py --------------------------------------------------------- */
 
 /* HierarchicalProcessor._voxel_grid_downsample_torch (diffusion_model.py:69-122) for all B

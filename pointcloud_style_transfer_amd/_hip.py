@@ -54,6 +54,9 @@ SIGNATURES = {
     "pcst_voxel_center_dist": [_P, _I, _P, ctypes.c_float, _P, _P, _P, _P],
     "pcst_knn_dist": [_P, _P, _I, _I, _I, _I, _P, _P, _P],
     "pcst_emd_greedy": [_P, _P, _I, _I, _I, _P, _P],
+    "pcst_gemm_nt_bf16": [_P, _I, _I, _P, _I, _P, _P, ctypes.c_int, _P, _P],
+    "pcst_linear_wgrad_bf16_workspace_size": [_I, _I, _I, _SZ],
+    "pcst_linear_wgrad_bf16": [_P, _P, _I, _I, _I, _P, _P, _P, _P],
     "pcst_linear_wgrad_workspace_size": [_I, _I, _I, _SZ],
     "pcst_linear_wgrad": [_P, _P, _I, _I, _I, _P, _P, _P, _P],
     "pcst_channel_stats_workspace_size": [_I, _SZ],
@@ -335,19 +338,36 @@ def pointwise_linear(X, W, scale=None, shift=None, relu=False, pool_ns=0):
     return Y
 
 
-def linear_wgrad(dZ, X, bias=True):
-    """dZ [M,O], X [M,I] -> (dW = dZ^T X [O,I], db = dZ^T 1 [O] or None); deterministic."""
+def linear_wgrad(dZ, X, bias=True, bf16=False):
+    """dZ [M,O], X [M,I] -> (dW = dZ^T X [O,I], db = dZ^T 1 [O] or None); deterministic.
+    bf16: operands rounded to bf16 for the MFMA (autocast training), fp32 accumulation."""
     require_device(dZ, X)
     dZ, X = _f32(dZ), _f32(X)
     M, O = dZ.shape
     I = X.shape[1]
     if X.shape[0] != M:
         raise RuntimeError(f"linear_wgrad: row mismatch {tuple(dZ.shape)} vs {tuple(X.shape)}")
-    ws = _workspace("pcst_linear_wgrad_workspace_size", M, I, O, device=dZ.device)
+    fn = "pcst_linear_wgrad_bf16" if bf16 else "pcst_linear_wgrad"
+    ws = _workspace(fn + "_workspace_size", M, I, O, device=dZ.device)
     dW = torch.empty(O, I, dtype=torch.float32, device=dZ.device)
     db = torch.empty(O, dtype=torch.float32, device=dZ.device) if bias else None
-    _call("pcst_linear_wgrad", _ptr(dZ), _ptr(X), M, I, O, _ptr(dW), _ptr(db), _ptr(ws), _stream())
+    _call(fn, _ptr(dZ), _ptr(X), M, I, O, _ptr(dW), _ptr(db), _ptr(ws), _stream())
     return dW, db
+
+
+def gemm_nt_bf16(A, B, scale=None, shift=None, relu=False):
+    """A [M,K], B [O,K] -> act(scale*(A B^T)+shift) [M,O] on bf16 MFMA (fp32 accumulation)."""
+    require_device(A, B, scale, shift)
+    A, B = _f32(A), _f32(B)
+    M, K = A.shape
+    O = B.shape[0]
+    if B.shape[1] != K:
+        raise RuntimeError(f"gemm_nt_bf16: K mismatch {tuple(A.shape)} vs {tuple(B.shape)}")
+    C = torch.empty(M, O, dtype=torch.float32, device=A.device)
+    _call("pcst_gemm_nt_bf16", _ptr(A), M, K, _ptr(B), O,
+          _ptr(None if scale is None else _f32(scale)), _ptr(None if shift is None else _f32(shift)),
+          int(relu), _ptr(C), _stream())
+    return C
 
 
 def channel_stats(Z):

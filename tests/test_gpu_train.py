@@ -55,3 +55,88 @@ def test_linear_fn_backward_matches_autograd(H):
     for a, b in ((gx, x64.grad), (gw, w64.grad), (gb, b64.grad)):
         err = (a.double() - b).norm() / b.norm()
         assert err.item() < 1e-5
+
+
+def _bf(t):
+    return t.bfloat16().double()
+
+
+@pytest.mark.parametrize("M,K,O,relu", [(1, 3, 64, True), (1000, 3, 128, True), (4097, 131, 256, False),
+                                        (60000, 256, 512, True), (60000, 512, 256, False),
+                                        (300, 259, 3, False)])
+def test_gemm_nt_bf16_vs_float64(H, M, K, O, relu):
+    """bf16-rounded operands, fp32 accumulation: matches the float64 product of the same
+    rounded operands up to fp32 summation order."""
+    g = torch.Generator(device="cuda").manual_seed(M + K + O)
+    A = torch.randn(M, K, device="cuda", generator=g)
+    B = torch.randn(O, K, device="cuda", generator=g)
+    shift = torch.randn(O, device="cuda", generator=g)
+    C = H.gemm_nt_bf16(A, B, None, shift, relu)
+    ref = _bf(A) @ _bf(B).t() + shift.double()
+    if relu:
+        ref = ref.clamp_min(0)
+    err = (C.double() - ref).norm() / ref.norm()
+    assert err.item() < 1e-6, err.item()
+
+
+@pytest.mark.parametrize("M,I,O", [(37, 3, 64), (4097, 259, 256), (240000, 256, 512), (8, 256, 512)])
+def test_linear_wgrad_bf16_vs_float64(H, M, I, O):
+    g = torch.Generator(device="cuda").manual_seed(M * 3 + I + O)
+    dz = torch.randn(M, O, device="cuda", generator=g)
+    x = torch.randn(M, I, device="cuda", generator=g)
+    dw, db = H.linear_wgrad(dz, x, bias=True, bf16=True)
+    ref = _bf(dz).t() @ _bf(x)
+    assert ((dw.double() - ref).norm() / ref.norm()).item() < 1e-6
+    ref_b = dz.double().sum(0)
+    assert ((db.double() - ref_b).norm() / ref_b.norm()).item() < 1e-6
+    dw2, _ = H.linear_wgrad(dz, x, bias=False, bf16=True)
+    assert torch.equal(dw, dw2)
+
+
+def test_linear_fn_uses_bf16_under_autocast(H):
+    from pointcloud_style_transfer_amd.models import _autograd as ag
+
+    torch.manual_seed(1)
+    lin = torch.nn.Linear(256, 512).cuda()
+    x = torch.randn(3000, 256, device="cuda", requires_grad=True)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        y = ag.linear(x, lin, relu=True)
+    assert y.dtype == torch.float32
+    y.sum().backward()
+    x64 = x.detach().double().requires_grad_()
+    w64 = lin.weight.detach().double().requires_grad_()
+    y64 = torch.relu(x64 @ w64.t() + lin.bias.detach().double())
+    y64.sum().backward()
+    rel = lambda a, b: ((a.double() - b).norm() / b.norm()).item()  # noqa: E731
+    assert 1e-7 < rel(y, y64) < 1e-2          # bf16 operands: not the f32 path, within bf16 error
+    # backward products against float64 with the kernel's own ReLU mask (bf16 rounding flips
+    # the mask of near-zero pre-activations; that is not a GEMM error)
+    mask = (y.detach() > 0).double()
+    assert rel(x.grad, mask @ w64.detach()) < 1e-2
+    assert rel(lin.weight.grad, mask.t() @ x64.detach()) < 1e-2
+
+
+def test_trainer_step_amp_close_to_fp32(H, tmp_path):
+    """One DiffusionTrainer step with use_amp (bf16 GEMMs) against the same step in fp32:
+    same draws, losses within the bf16 tolerance."""
+    import numpy as np
+
+    from pointcloud_style_transfer_amd.config.config import Config
+    from pointcloud_style_transfer_amd.synthetic import lidar_like_cloud
+    from pointcloud_style_transfer_amd.training.trainer import DiffusionTrainer
+
+    losses = []
+    for amp in (False, True):
+        cfg = Config(make_dirs=False, log_dir=str(tmp_path), checkpoint_dir=str(tmp_path),
+                     use_amp=amp, gradient_accumulation_steps=1, cond_drop_prob=0.0,
+                     global_points=2048)
+        torch.manual_seed(0)
+        tr = DiffusionTrainer(cfg, device="cuda")
+        tr.model.train()
+        sim = torch.from_numpy(np.stack([lidar_like_cloud(1000 + i, 8192) for i in range(2)]))
+        real = torch.from_numpy(np.stack([lidar_like_cloud(2000 + i, 8192) for i in range(2)]))
+        torch.manual_seed(5)
+        loss, _ = tr.train_step({"sim_full": sim.cuda(), "real_full": real.cuda()}, 0, 1)
+        losses.append(float(loss))
+    assert np.isfinite(losses).all()
+    assert abs(losses[1] - losses[0]) <= 2e-2 * abs(losses[0]), losses
