@@ -181,6 +181,11 @@ def main():
         style_s = time.perf_counter() - t0
         style_in = torch.cat([style, torch.zeros_like(style)])
         enc = encoder_rooflines(hp.downsample(cond)[0], device)
+        # the same kernels at BASELINE configs[4]'s per-GPU batch (256 clouds / 8 GPUs = 32
+        # coarse condition clouds in one launch: one workgroup per cloud)
+        xb = torch.from_numpy(np.stack([lidar_like_cloud(2000 + i, cfg.global_points)
+                                        for i in range(32)])).to(device)
+        enc.update({k + "_b32": v for k, v in encoder_rooflines(xb, device).items()})
         npred.packed()
         timesteps = torch.linspace(dp.num_timesteps - 1, 0, dp.num_timesteps).long().tolist()
         t_rows = torch.tensor(timesteps, dtype=torch.long).repeat_interleave(2 * C)

@@ -7,6 +7,9 @@
 
 namespace pcst {
 
+typedef float fps_f2 __attribute__((ext_vector_type(2)));
+
+
 // ------------------------------------------------------------------ square_distance
 // pointnet2_encoder.py:8-15.  One thread per (b, s, n) output element, n fastest.
 __global__ void square_distance_kernel(const float* __restrict__ src, const float* __restrict__ dst,
@@ -84,15 +87,32 @@ __global__ __launch_bounds__(kFpsThreads) void fps_reg_kernel(const float* __res
     far = __builtin_amdgcn_readfirstlane(far);
     if (tid == 0) o[it] = far;
     const float cx = P[far * 3 + 0], cy = P[far * 3 + 1], cz = P[far * 3 + 2];
-    float best = -2.0f;
-    int bestk = 0;
+    // two points per instruction: v_pk_add/mul_f32 perform the same IEEE operations per
+    // component ((dx*dx + dy*dy) + dz*dz, nothing fused: this file builds with
+    // -ffp-contract=off), so the distances are bit-identical to the scalar form
+    const fps_f2 c2x = {cx, cx}, c2y = {cy, cy}, c2z = {cz, cz};
 #pragma unroll
-    for (int k = 0; k < PPT; ++k) {
+    for (int k = 0; k + 1 < PPT; k += 2) {
+      const fps_f2 dx = fps_f2{px[k], px[k + 1]} - c2x;
+      const fps_f2 dy = fps_f2{py[k], py[k + 1]} - c2y;
+      const fps_f2 dz = fps_f2{pz[k], pz[k + 1]} - c2z;
+      const fps_f2 d = (dx * dx + dy * dy) + dz * dz;
+      dist[k] = d.x < dist[k] ? d.x : dist[k];
+      dist[k + 1] = d.y < dist[k + 1] ? d.y : dist[k + 1];
+    }
+    if (PPT & 1) {
+      const int k = PPT - 1;
       const float dx = fsub(px[k], cx), dy = fsub(py[k], cy), dz = fsub(pz[k], cz);
       const float d = fadd(fadd(fmul(dx, dx), fmul(dy, dy)), fmul(dz, dz));
       dist[k] = d < dist[k] ? d : dist[k];
-      if (dist[k] > best) { best = dist[k]; bestk = k; }
     }
+    // arg-max: the value by a max chain, then the lowest k holding it (lowest point index)
+    float best = dist[0];
+#pragma unroll
+    for (int k = 1; k < PPT; ++k) best = fmaxf(best, dist[k]);
+    int bestk = PPT - 1;
+#pragma unroll
+    for (int k = PPT - 2; k >= 0; --k) bestk = dist[k] == best ? k : bestk;
     int bi = tid + bestk * kFpsThreads;
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) {
@@ -177,15 +197,32 @@ __global__ __launch_bounds__(kFps2Threads) void fps_key_kernel(const float* __re
     far = __builtin_amdgcn_readfirstlane(far);
     if (tid == 0) o[it] = far;
     const float cx = P[far * 3 + 0], cy = P[far * 3 + 1], cz = P[far * 3 + 2];
-    float best = -2.0f;
-    int bestk = 0;
+    // two points per instruction: v_pk_add/mul_f32 perform the same IEEE operations per
+    // component ((dx*dx + dy*dy) + dz*dz, nothing fused: this file builds with
+    // -ffp-contract=off), so the distances are bit-identical to the scalar form
+    const fps_f2 c2x = {cx, cx}, c2y = {cy, cy}, c2z = {cz, cz};
 #pragma unroll
-    for (int k = 0; k < PPT; ++k) {
+    for (int k = 0; k + 1 < PPT; k += 2) {
+      const fps_f2 dx = fps_f2{px[k], px[k + 1]} - c2x;
+      const fps_f2 dy = fps_f2{py[k], py[k + 1]} - c2y;
+      const fps_f2 dz = fps_f2{pz[k], pz[k + 1]} - c2z;
+      const fps_f2 d = (dx * dx + dy * dy) + dz * dz;
+      dist[k] = d.x < dist[k] ? d.x : dist[k];
+      dist[k + 1] = d.y < dist[k + 1] ? d.y : dist[k + 1];
+    }
+    if (PPT & 1) {
+      const int k = PPT - 1;
       const float dx = fsub(px[k], cx), dy = fsub(py[k], cy), dz = fsub(pz[k], cz);
       const float d = fadd(fadd(fmul(dx, dx), fmul(dy, dy)), fmul(dz, dz));
       dist[k] = d < dist[k] ? d : dist[k];
-      if (dist[k] > best) { best = dist[k]; bestk = k; }
     }
+    // arg-max: the value by a max chain, then the lowest k holding it (lowest point index)
+    float best = dist[0];
+#pragma unroll
+    for (int k = 1; k < PPT; ++k) best = fmaxf(best, dist[k]);
+    int bestk = PPT - 1;
+#pragma unroll
+    for (int k = PPT - 2; k >= 0; --k) bestk = dist[k] == best ? k : bestk;
     const uint32_t n = (uint32_t)(tid + bestk * kFps2Threads);
     const uint32_t bits = best > 0.0f ? __float_as_uint(best) : 0u;
     const uint64_t key = wave_max_u64(((uint64_t)bits << 32) | (0xFFFFFFFFu - n));
