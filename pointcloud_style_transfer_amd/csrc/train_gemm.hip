@@ -73,6 +73,38 @@ __device__ __forceinline__ void stage_rows(const float* __restrict__ S, int64_t 
   }
 }
 
+// software-pipelined staging (K % 4 == 0): the next slice's float4s are loaded into registers
+// while the MFMAs of the current slice run, then rounded and stored after the barrier
+struct RowRegs {
+  float4 v[4];
+};
+
+__device__ __forceinline__ void load_rows(const float* __restrict__ S, int64_t R, int K, int64_t r0,
+                                          int k0, int tid, RowRegs& g) {
+#pragma unroll
+  for (int it = 0; it < 4; ++it) {
+    const int f = tid + 256 * it;
+    const int r = f >> 3, kc = (f & 7) * 4;
+    const int64_t row = r0 + r;
+    g.v[it] = (row < R && k0 + kc < K) ? *reinterpret_cast<const float4*>(S + row * K + k0 + kc)
+                                       : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+}
+
+__device__ __forceinline__ void store_rows(const RowRegs& g, __bf16 (*D)[kGLd], int tid) {
+#pragma unroll
+  for (int it = 0; it < 4; ++it) {
+    const int f = tid + 256 * it;
+    const int r = f >> 3, kc = (f & 7) * 4;
+    bf16x4 o;
+    o[0] = (__bf16)g.v[it].x;
+    o[1] = (__bf16)g.v[it].y;
+    o[2] = (__bf16)g.v[it].z;
+    o[3] = (__bf16)g.v[it].w;
+    *reinterpret_cast<bf16x4*>(&D[r][kc]) = o;
+  }
+}
+
 template <bool VEC>
 __global__ __launch_bounds__(256) void gemm_nt_bf16_kernel(const float* __restrict__ A, int64_t M,
                                                            int K, const float* __restrict__ B,
@@ -90,12 +122,29 @@ __global__ __launch_bounds__(256) void gemm_nt_bf16_kernel(const float* __restri
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = f32x16{};
-  for (int k0 = 0; k0 < K; k0 += kGK) {
-    stage_rows<VEC>(A, M, K, m0, k0, As, tid);
-    stage_rows<VEC>(B, O, K, o0, k0, Bs, tid);
-    __syncthreads();
-    mma_slice(As, Bs, wr, wc, l32, h, acc);
-    __syncthreads();
+  if (VEC) {
+    RowRegs ga, gb;
+    load_rows(A, M, K, m0, 0, tid, ga);
+    load_rows(B, O, K, o0, 0, tid, gb);
+    for (int k0 = 0; k0 < K; k0 += kGK) {
+      store_rows(ga, As, tid);
+      store_rows(gb, Bs, tid);
+      __syncthreads();
+      if (k0 + kGK < K) {
+        load_rows(A, M, K, m0, k0 + kGK, tid, ga);
+        load_rows(B, O, K, o0, k0 + kGK, tid, gb);
+      }
+      mma_slice(As, Bs, wr, wc, l32, h, acc);
+      __syncthreads();
+    }
+  } else {
+    for (int k0 = 0; k0 < K; k0 += kGK) {
+      stage_rows<false>(A, M, K, m0, k0, As, tid);
+      stage_rows<false>(B, O, K, o0, k0, Bs, tid);
+      __syncthreads();
+      mma_slice(As, Bs, wr, wc, l32, h, acc);
+      __syncthreads();
+    }
   }
 #pragma unroll
   for (int bn = 0; bn < 2; ++bn) {
@@ -115,22 +164,30 @@ __global__ __launch_bounds__(256) void gemm_nt_bf16_kernel(const float* __restri
   }
 }
 
-// stage columns [c0, c0+128) x rows [m0, m0+32) of a row-major [M, Cn] fp32 matrix, transposed
-// into D[c][m] as bf16: thread (c = tid & 127, half = tid >> 7) loads 16 rows of its column
-// (each load coalesced across the wave) and writes two 16-byte fragments.
-__device__ __forceinline__ void stage_cols(const float* __restrict__ S, int64_t Mend, int Cn,
-                                           int64_t m0, int c0, __bf16 (*D)[kGLd], int tid,
-                                           float* colsum) {
+struct ColRegs {
+  float v[16];
+};
+
+__device__ __forceinline__ void load_cols(const float* __restrict__ S, int64_t Mend, int Cn,
+                                          int64_t m0, int c0, int tid, ColRegs& g) {
   const int c = tid & 127, half = tid >> 7;
   const bool cv = c0 + c < Cn;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    const int64_t m = m0 + half * 16 + j;
+    g.v[j] = (cv && m < Mend) ? S[m * Cn + c0 + c] : 0.0f;
+  }
+}
+
+__device__ __forceinline__ void store_cols(const ColRegs& g, __bf16 (*D)[kGLd], int tid,
+                                           float* colsum) {
+  const int c = tid & 127, half = tid >> 7;
   bf16x8 f[2];
   float s = 0.0f;
 #pragma unroll
   for (int j = 0; j < 16; ++j) {
-    const int64_t m = m0 + half * 16 + j;
-    const float v = (cv && m < Mend) ? S[m * Cn + c0 + c] : 0.0f;
-    s += v;
-    f[j >> 3][j & 7] = (__bf16)v;
+    s += g.v[j];
+    f[j >> 3][j & 7] = (__bf16)g.v[j];
   }
   *reinterpret_cast<bf16x8*>(&D[c][half * 16]) = f[0];
   *reinterpret_cast<bf16x8*>(&D[c][half * 16 + 8]) = f[1];
@@ -158,10 +215,17 @@ __global__ __launch_bounds__(256) void wgrad_bf16_kernel(const float* __restrict
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = f32x16{};
   float bsum = 0.0f;
+  ColRegs ga, gb;
+  load_cols(dZ, me, O, mb, o0, tid, ga);
+  load_cols(X, me, I, mb, i0, tid, gb);
   for (int64_t k0 = mb; k0 < me; k0 += kGK) {
-    stage_cols(dZ, me, O, k0, o0, As, tid, bias ? &bsum : nullptr);
-    stage_cols(X, me, I, k0, i0, Bs, tid, nullptr);
+    store_cols(ga, As, tid, bias ? &bsum : nullptr);
+    store_cols(gb, Bs, tid, nullptr);
     __syncthreads();
+    if (k0 + kGK < me) {  // next slice in flight during this slice's MFMAs
+      load_cols(dZ, me, O, k0 + kGK, o0, tid, ga);
+      load_cols(X, me, I, k0 + kGK, i0, tid, gb);
+    }
     mma_slice(As, Bs, wr, wc, l32, h, acc);
     __syncthreads();
   }
@@ -195,6 +259,36 @@ __global__ void wgrad_bf16_combine_kernel(const float* __restrict__ part, int64_
   }
 }
 
+// n % 4 == 0: four consecutive outputs per thread, 8 chunk loads in flight, same in-order sums
+__global__ void wgrad_bf16_combine4_kernel(const float4* __restrict__ part, int64_t n4, int chunks,
+                                           float4* __restrict__ out) {
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < n4;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
+    int c = 0;
+    for (; c + 8 <= chunks; c += 8) {
+      float4 v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = part[(int64_t)(c + u) * n4 + e];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        s0 += (double)v[u].x;
+        s1 += (double)v[u].y;
+        s2 += (double)v[u].z;
+        s3 += (double)v[u].w;
+      }
+    }
+    for (; c < chunks; ++c) {
+      const float4 v = part[(int64_t)c * n4 + e];
+      s0 += (double)v.x;
+      s1 += (double)v.y;
+      s2 += (double)v.z;
+      s3 += (double)v.w;
+    }
+    out[e] = make_float4((float)s0, (float)s1, (float)s2, (float)s3);
+  }
+}
+
 struct Bf16WgradPlan {
   int tiles_i, tiles_o, chunks;
   int64_t rows_per_chunk;
@@ -205,7 +299,7 @@ static Bf16WgradPlan bf16_wgrad_plan(int64_t M, int64_t I, int64_t O) {
   p.tiles_i = (int)cdiv(I, kGT);
   p.tiles_o = (int)cdiv(O, kGT);
   const int64_t tiles = (int64_t)p.tiles_i * p.tiles_o;
-  int64_t chunks = cdiv(1024, tiles);
+  int64_t chunks = cdiv(512, tiles);  // ~2 workgroups per CU; fewer partials to combine
   chunks = std::max<int64_t>(1, std::min<int64_t>(chunks, cdiv(M, 512)));
   p.rows_per_chunk = cdiv(cdiv(M, chunks), kGK) * kGK;
   p.chunks = (int)cdiv(M, p.rows_per_chunk);
@@ -262,8 +356,15 @@ extern "C" int pcst_linear_wgrad_bf16(const float* dZ, const float* X, int64_t M
                      dim3(256), 0, s, dZ, X, M, (int)I, (int)O, p.rows_per_chunk, p.tiles_i, partW,
                      partB);
   const int64_t n = O * I;
-  hipLaunchKernelGGL(wgrad_bf16_combine_kernel, dim3((unsigned)std::min<int64_t>(cdiv(n, 256), 2048)),
-                     dim3(256), 0, s, partW, n, p.chunks, dW);
+  if (n % 4 == 0 && (uintptr_t)dW % 16 == 0)
+    hipLaunchKernelGGL(wgrad_bf16_combine4_kernel,
+                       dim3((unsigned)std::min<int64_t>(cdiv(n / 4, 256), 2048)), dim3(256), 0, s,
+                       reinterpret_cast<const float4*>(partW), n / 4, p.chunks,
+                       reinterpret_cast<float4*>(dW));
+  else
+    hipLaunchKernelGGL(wgrad_bf16_combine_kernel,
+                       dim3((unsigned)std::min<int64_t>(cdiv(n, 256), 2048)), dim3(256), 0, s,
+                       partW, n, p.chunks, dW);
   if (db)
     hipLaunchKernelGGL(wgrad_bf16_combine_kernel, dim3((unsigned)cdiv(O, 256)), dim3(256), 0, s,
                        partB, O, p.chunks, db);
