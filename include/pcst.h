@@ -143,6 +143,14 @@ int pcst_voxel_error(void* workspace, int64_t B, int64_t N, int32_t* err_out, vo
 int pcst_knn_workspace_size(int64_t B, int64_t N, int64_t M, size_t* bytes);
 int pcst_knn3_interp(const float* coarse, const float* orig, const int64_t* idx, int64_t B,
                      int64_t N, int64_t M, float* out, void* workspace, void* stream);
+/* The same computation in two phases on one workspace (knn3_interp = build then query):
+ * build reads only positions (orig, idx) -- the grid statistics, cell counts, scan and fill --
+ * so it can run on a second stream while the noise MLP produces `coarse`; query reads `coarse`
+ * and writes out.  The caller orders query after build on the workspace. */
+int pcst_knn3_build(const float* orig, const int64_t* idx, int64_t B, int64_t N, int64_t M,
+                    void* workspace, void* stream);
+int pcst_knn3_query(const float* coarse, const float* orig, int64_t B, int64_t N, int64_t M,
+                    float* out, void* workspace, void* stream);
 int pcst_knn_error(void* workspace, int64_t B, int64_t N, int64_t M, int32_t* err_out,
                    void* stream);
 

@@ -45,6 +45,8 @@ SIGNATURES = {
     "pcst_voxel_downsample_copies": [_P, _I, _I, _I, _I, _P, ctypes.c_uint64, _P, _P, _P],
     "pcst_knn_workspace_size": [_I, _I, _I, _SZ],
     "pcst_knn3_interp": [_P, _P, _P, _I, _I, _I, _P, _P, _P],
+    "pcst_knn3_build": [_P, _P, _I, _I, _I, _P, _P],
+    "pcst_knn3_query": [_P, _P, _I, _I, _I, _P, _P, _P],
     "pcst_knn_error": [_P, _I, _I, _I, _P, _P],
     "pcst_noise_mlp_blob_bytes": [ctypes.c_int],
     "pcst_noise_cond": [_P, _P, _I, _P, _P, _P, _P, _P, _P, _P, _P],
@@ -265,6 +267,32 @@ def voxel_stats(points, target):
 
 
 # ----------------------------------------------------------------------------- kNN upsample
+def knn3_build(orig, idx):
+    """Phase 1 of knn3_interp (positions only) on the current stream -> workspace handle
+    (orig, idx, workspace) for knn3_query."""
+    require_device(orig, idx)
+    orig, idx = _f32(orig), _i64(idx)
+    B, N, _ = orig.shape
+    M = idx.shape[1]
+    ws = _workspace("pcst_knn_workspace_size", B, N, M, device=orig.device)
+    _call("pcst_knn3_build", _ptr(orig), _ptr(idx), B, N, M, _ptr(ws), _stream())
+    return (orig, idx, ws)
+
+
+def knn3_query(coarse, handle):
+    """Phase 2 of knn3_interp on the current stream: coarse [B,M,3] -> [B,N,3]."""
+    orig, idx, ws = handle
+    require_device(coarse)
+    coarse = _f32(coarse)
+    B, N, _ = orig.shape
+    M = idx.shape[1]
+    if coarse.shape != (B, M, 3):
+        raise RuntimeError(f"knn3_query: coarse {tuple(coarse.shape)} != {(B, M, 3)}")
+    out = torch.empty(B, N, 3, dtype=torch.float32, device=orig.device)
+    _call("pcst_knn3_query", _ptr(coarse), _ptr(orig), B, N, M, _ptr(out), _ptr(ws), _stream())
+    return out
+
+
 def knn3_interp(coarse, orig, idx, check=False):
     """HierarchicalProcessor.upsample_knn: coarse [B,M,3], orig [B,N,3], idx [B,M] -> [B,N,3]."""
     require_device(coarse, orig, idx)

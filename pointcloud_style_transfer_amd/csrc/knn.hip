@@ -193,11 +193,10 @@ __global__ __launch_bounds__(256) void knn_pre_kernel(const float* __restrict__ 
 // their coarse value to the output here.  Each thread handles 4 elements with their atomics
 // in flight together.
 __global__ __launch_bounds__(256) void knn_count_kernel(
-    const float* __restrict__ orig, const float* __restrict__ coarse,
-    const int64_t* __restrict__ idx, const StatRec* __restrict__ stats,
-    const uint32_t* __restrict__ known, int64_t N, int64_t M, int64_t Cmax, int64_t T,
-    int64_t Cpad, float* __restrict__ gp, uint64_t* __restrict__ cnt, uint64_t* __restrict__ tsum,
-    int2* __restrict__ crank, float* __restrict__ out) {
+    const float* __restrict__ orig, const int64_t* __restrict__ idx,
+    const StatRec* __restrict__ stats, const uint32_t* __restrict__ known, int64_t N, int64_t M,
+    int64_t Cmax, int64_t T, int64_t Cpad, float* __restrict__ gp, uint64_t* __restrict__ cnt,
+    uint64_t* __restrict__ tsum, int2* __restrict__ crank) {
   constexpr int U = kCountPerBlock / 256;
   const int b = blockIdx.y;
   __shared__ float Gs[8];
@@ -223,11 +222,7 @@ __global__ __launch_bounds__(256) void knn_count_kernel(
     } else if (e < M + N) {
       const int64_t n = e - M;
       const uint32_t kn = known[b * N + n];
-      if (kn) {
-        const float* v = coarse + (b * M + (int64_t)(kn - 1)) * 3;
-        float* o = out + (b * N + n) * 3;
-        o[0] = v[0]; o[1] = v[1]; o[2] = v[2];
-      } else {
+      if (!kn) {  // known rows take the coarse value in the outlier pass (after the MLP)
         const float* p = orig + (b * N + n) * 3;
         px[u] = p[0]; py[u] = p[1]; pz[u] = p[2];
         need[u] = true;
@@ -796,12 +791,23 @@ template <int kk>
 __global__ __launch_bounds__(kOutlierThreads) void knn_outlier_kernel(
     const float* __restrict__ vals, int64_t N, int64_t M, const float* __restrict__ orig,
     const float4* __restrict__ refs, const int32_t* __restrict__ olist,
-    const int32_t* __restrict__ ocount, float* __restrict__ out) {
+    const int32_t* __restrict__ ocount, const uint32_t* __restrict__ known,
+    float* __restrict__ out) {
   constexpr int W = kOutlierThreads / 64;
   constexpr int Q = kOutlierThreads;
   __shared__ double sd[W][3];
   __shared__ int sj[W][3];
   const int b = blockIdx.y;
+  // rows that are coarse points take the coarse value (result[idx] = coarse; the last coarse
+  // row writing a point wins, as in the reference's index assignment)
+  for (int64_t n = (int64_t)blockIdx.x * Q + threadIdx.x; n < N; n += (int64_t)gridDim.x * Q) {
+    const uint32_t kn = known[b * N + n];
+    if (kn) {
+      const float* v = vals + (b * M + (int64_t)(kn - 1)) * 3;
+      float* o = out + (b * N + n) * 3;
+      o[0] = v[0]; o[1] = v[1]; o[2] = v[2];
+    }
+  }
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const float4* R = refs + b * M;
   const float* V = vals + b * M * 3;
@@ -858,14 +864,17 @@ extern "C" int pcst_knn_workspace_size(int64_t B, int64_t N, int64_t M, size_t* 
   return PCST_OK;
 }
 
-extern "C" int pcst_knn3_interp(const float* coarse, const float* orig, const int64_t* idx,
-                                int64_t B, int64_t N, int64_t M, float* out, void* workspace,
-                                void* stream) {
+// Phase 1 (positions only: the coarse set's points and the full cloud): grid statistics, the
+// packed cell counts, scan, fill.  Phase 2 (needs the coarse values, i.e. the noise MLP's
+// output): known rows, the query passes and the outlier pass.  Splitting them lets a caller run
+// phase 1 on a second stream while the MLP runs (guided_sample_loop).
+extern "C" int pcst_knn3_build(const float* orig, const int64_t* idx, int64_t B, int64_t N,
+                               int64_t M, void* workspace, void* stream) {
   PCST_CHECK_ARG(B >= 0 && N > 0 && M > 0 && N < (1ll << 31) && M < (1ll << 27) &&
                      M + N < (1ll << 31),
-                 "knn3_interp: bad shape");
+                 "knn3_build: bad shape");
   if (B == 0) return PCST_OK;
-  PCST_CHECK_ARG(coarse && orig && idx && out && workspace, "knn3_interp: null pointer");
+  PCST_CHECK_ARG(orig && idx && workspace, "knn3_build: null pointer");
   hipStream_t s = as_stream(stream);
   KnnWS w = carve_knn(workspace, B, N, M);
   const int b = (int)B;
@@ -875,13 +884,27 @@ extern "C" int pcst_knn3_interp(const float* coarse, const float* orig, const in
   hipLaunchKernelGGL(knn_pre_kernel, dim3(kStatBlocks + kPreKnownBlocks, b), dim3(256), 0, s,
                      orig, idx, (int)N, M, w.stats, w.known, w.err);
   const unsigned gc = (unsigned)cdiv(M + N, kCountPerBlock);
-  hipLaunchKernelGGL(knn_count_kernel, dim3(gc, b), dim3(256), 0, s, orig, coarse, idx, w.stats,
-                     w.known, N, M, w.Cmax, w.T, w.Cpad, w.gp, w.cnt, w.tsum, w.crank, out);
+  hipLaunchKernelGGL(knn_count_kernel, dim3(gc, b), dim3(256), 0, s, orig, idx, w.stats, w.known,
+                     N, M, w.Cmax, w.T, w.Cpad, w.gp, w.cnt, w.tsum, w.crank);
   hipLaunchKernelGGL(knn_scan_kernel, dim3((unsigned)w.T, b), dim3(256), 0, s, w.cnt, w.tsum, w.T,
                      w.Cpad, w.chunks, w.maxch, w.nchunk);
   const unsigned gf = (unsigned)std::min<int64_t>(cdiv(M + N, 256), 2048);
   hipLaunchKernelGGL(knn_fill_kernel, dim3(gf, b), dim3(256), 0, s, orig, idx, N, M, w.Cpad, w.cnt,
                      w.crank, w.refs, w.qorder);
+  PCST_LAUNCH_CHECK("knn3_build");
+  return PCST_OK;
+}
+
+extern "C" int pcst_knn3_query(const float* coarse, const float* orig, int64_t B, int64_t N,
+                               int64_t M, float* out, void* workspace, void* stream) {
+  PCST_CHECK_ARG(B >= 0 && N > 0 && M > 0 && N < (1ll << 31) && M < (1ll << 27) &&
+                     M + N < (1ll << 31),
+                 "knn3_query: bad shape");
+  if (B == 0) return PCST_OK;
+  PCST_CHECK_ARG(coarse && orig && out && workspace, "knn3_query: null pointer");
+  hipStream_t s = as_stream(stream);
+  KnnWS w = carve_knn(workspace, B, N, M);
+  const int b = (int)B;
   // fixed grids stride over the chunk and outlier lists (their lengths live on the device)
   const unsigned gq = (unsigned)std::min<int64_t>(cdiv(w.maxch, 4), kQueryBlocks);
   auto qk = M >= 3 ? knn_query_kernel<3> : (M == 2 ? knn_query_kernel<2> : knn_query_kernel<1>);
@@ -890,9 +913,17 @@ extern "C" int pcst_knn3_interp(const float* coarse, const float* orig, const in
   auto ok = M >= 3 ? knn_outlier_kernel<3>
                    : (M == 2 ? knn_outlier_kernel<2> : knn_outlier_kernel<1>);
   hipLaunchKernelGGL(ok, dim3(kOutlierBlocks, b), dim3(kOutlierThreads), 0, s, coarse, N, M, orig,
-                     w.refs, w.olist, w.ocount, out);
-  PCST_LAUNCH_CHECK("knn3_interp");
+                     w.refs, w.olist, w.ocount, w.known, out);
+  PCST_LAUNCH_CHECK("knn3_query");
   return PCST_OK;
+}
+
+extern "C" int pcst_knn3_interp(const float* coarse, const float* orig, const int64_t* idx,
+                                int64_t B, int64_t N, int64_t M, float* out, void* workspace,
+                                void* stream) {
+  int rc = pcst_knn3_build(orig, idx, B, N, M, workspace, stream);
+  if (rc) return rc;
+  return pcst_knn3_query(coarse, orig, B, N, M, out, workspace, stream);
 }
 
 #ifdef KNN_TRACE

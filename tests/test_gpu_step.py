@@ -249,3 +249,21 @@ def test_cfg_ddim_step(H, golden):
         ref = O.guided_update(sched, x, ec, eu, src, t, tp, 7.5)
         assert_close(out.cpu().numpy(), ref, rtol=1e-5)
         np.testing.assert_array_equal(xc.cpu().numpy(), np.concatenate([out.cpu().numpy()] * 2))
+
+
+def test_knn_build_query_phases_match_interp(H):
+    """pcst_knn3_build on a side stream + pcst_knn3_query gives the bit-identical result of the
+    one-call pcst_knn3_interp."""
+    rng = np.random.default_rng(21)
+    orig = dev(rng.standard_normal((2, 20000, 3)).astype(np.float32))
+    idx = dev(np.stack([rng.choice(20000, 5000, replace=False) for _ in range(2)]).astype(np.int64))
+    coarse = dev(rng.standard_normal((2, 5000, 3)).astype(np.float32))
+    ref = H.knn3_interp(coarse, orig, idx)
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        handle = H.knn3_build(orig, idx)
+    torch.cuda.current_stream().wait_stream(side)
+    handle[2].record_stream(torch.cuda.current_stream())
+    assert torch.equal(H.knn3_query(coarse, handle), ref)
+    assert torch.equal(H.knn3_query(coarse, H.knn3_build(orig, idx)), ref)
