@@ -176,6 +176,16 @@ int pcst_cfg_ddim_step(const float* x, const float* eps_c, const float* eps_u, c
                        int64_t n, float guidance_scale, float sqrt_1m_at, float sqrt_at_eps,
                        float sqrt_aprev, float sqrt_1m_aprev, float* x_out, float* x_cat,
                        void* stream);
+/* hipGraph-replayable forms of the per-step calls (BASELINE configs[4]: a captured denoise
+ * step): the per-step scalars live in device memory the caller updates between replays --
+ * coef_dev[4] = (sqrt_1m_at, sqrt_at_eps, sqrt_aprev, sqrt_1m_aprev); seed_dev[1] the subset
+ * seed.  x_out may equal x (elementwise, in place). */
+int pcst_cfg_ddim_step_dcoef(const float* x, const float* eps_c, const float* eps_u,
+                             const float* source, int64_t n, float guidance_scale,
+                             const float* coef_dev, float* x_out, float* x_cat, void* stream);
+int pcst_voxel_downsample_copies_dseed(const float* pts, int64_t B, int64_t N, int64_t copies,
+                                       int64_t target, void* workspace, const uint64_t* seed_dev,
+                                       int64_t* out_idx, float* out_pts, void* stream);
 
 /* ---- models/losses.py ------------------------------------------------------------------ */
 

@@ -46,6 +46,8 @@ SIGNATURES = {
     "pcst_knn_workspace_size": [_I, _I, _I, _SZ],
     "pcst_knn3_interp": [_P, _P, _P, _I, _I, _I, _P, _P, _P],
     "pcst_knn3_build": [_P, _P, _I, _I, _I, _P, _P],
+    "pcst_cfg_ddim_step_dcoef": [_P, _P, _P, _P, _I, ctypes.c_float, _P, _P, _P, _P],
+    "pcst_voxel_downsample_copies_dseed": [_P, _I, _I, _I, _I, _P, _P, _P, _P, _P],
     "pcst_knn3_query": [_P, _P, _I, _I, _I, _P, _P, _P],
     "pcst_knn_error": [_P, _I, _I, _I, _P, _P],
     "pcst_noise_mlp_blob_bytes": [ctypes.c_int],
@@ -512,3 +514,29 @@ def voxel_center_dist(points, xyz_min, voxel_size):
     if int(ovf.item()):
         raise RuntimeError("pcst: voxel coordinates exceed 2^21 per axis")
     return key, dist
+
+
+# ----------------------------------------------------------------------------- graph-replayable steps
+def cfg_ddim_step_dcoef(x, eps_c, eps_u, source, guidance_scale, coef, x_cat=None, out=None):
+    """cfg_ddim_step with the four fp32 coefficients read from the device tensor `coef` [4]."""
+    require_device(x, eps_c, eps_u, source, x_cat, coef)
+    if out is None:
+        out = torch.empty_like(x)
+    _call("pcst_cfg_ddim_step_dcoef", _ptr(x), _ptr(eps_c), _ptr(eps_u), _ptr(source), x.numel(),
+          float(guidance_scale), _ptr(coef), _ptr(out), _ptr(x_cat), _stream())
+    return out
+
+
+def voxel_downsample_copies_dseed(points, target, seed_dev, copies):
+    """voxel_downsample(points, target, copies=copies) with the subset seed read from the
+    device tensor `seed_dev` (int64 [1], the same bits as the host seed)."""
+    require_device(points, seed_dev)
+    points = _f32(points)
+    B, N, _ = points.shape
+    dev = points.device
+    ws = _workspace("pcst_voxel_copies_workspace_size", B, N, copies, device=dev)
+    out_idx = torch.empty(copies * B, target, dtype=torch.int64, device=dev)
+    out_pts = torch.empty(copies * B, target, 3, dtype=torch.float32, device=dev)
+    _call("pcst_voxel_downsample_copies_dseed", _ptr(points), B, N, copies, target, _ptr(ws),
+          _ptr(seed_dev), _ptr(out_idx), _ptr(out_pts), _stream())
+    return out_pts, out_idx

@@ -15,7 +15,14 @@ namespace pcst {
 __global__ void cfg_ddim_kernel(const float* __restrict__ x, const float* __restrict__ eps_c,
                                 const float* __restrict__ eps_u, const float* __restrict__ src,
                                 int64_t n, float scale, float c1, float c2, float c3, float c4,
-                                float* __restrict__ x_out, float* __restrict__ x_cat) {
+                                const float* __restrict__ coef, float* __restrict__ x_out,
+                                float* __restrict__ x_cat) {
+  if (coef) {  // device coefficients: hipGraph-replayable
+    c1 = coef[0];
+    c2 = coef[1];
+    c3 = coef[2];
+    c4 = coef[3];
+  }
   for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < n;
        e += (int64_t)gridDim.x * blockDim.x) {
     float eps = eps_c[e];
@@ -49,7 +56,21 @@ extern "C" int pcst_cfg_ddim_step(const float* x, const float* eps_c, const floa
   const int64_t g = std::min<int64_t>(cdiv(n, 256), 4096);
   hipLaunchKernelGGL(cfg_ddim_kernel, dim3((unsigned)g), dim3(256), 0, as_stream(stream), x, eps_c,
                      eps_u, source, n, guidance_scale, sqrt_1m_at, sqrt_at_eps, sqrt_aprev,
-                     sqrt_1m_aprev, x_out, x_cat);
+                     sqrt_1m_aprev, (const float*)nullptr, x_out, x_cat);
   PCST_LAUNCH_CHECK("cfg_ddim_step");
+  return PCST_OK;
+}
+
+extern "C" int pcst_cfg_ddim_step_dcoef(const float* x, const float* eps_c, const float* eps_u,
+                                        const float* source, int64_t n, float guidance_scale,
+                                        const float* coef_dev, float* x_out, float* x_cat,
+                                        void* stream) {
+  PCST_CHECK_ARG(n >= 0, "cfg_ddim_step_dcoef: bad size");
+  if (n == 0) return PCST_OK;
+  PCST_CHECK_ARG(x && eps_c && x_out && coef_dev, "cfg_ddim_step_dcoef: null pointer");
+  const int64_t g = std::min<int64_t>(cdiv(n, 256), 4096);
+  hipLaunchKernelGGL(cfg_ddim_kernel, dim3((unsigned)g), dim3(256), 0, as_stream(stream), x, eps_c,
+                     eps_u, source, n, guidance_scale, 0.f, 1.f, 0.f, 0.f, coef_dev, x_out, x_cat);
+  PCST_LAUNCH_CHECK("cfg_ddim_step_dcoef");
   return PCST_OK;
 }

@@ -539,11 +539,13 @@ __device__ __forceinline__ bool voxf_cand(int row, int cl, int e, int N, int U, 
   return true;
 }
 
-__global__ __launch_bounds__(256) void voxf_hist_kernel(int N, int64_t T, int B, uint64_t seed,
+__global__ __launch_bounds__(256) void voxf_hist_kernel(int N, int64_t T, int B, uint64_t seed_v,
+                                                        const uint64_t* __restrict__ seed_p,
                                                         const int32_t* __restrict__ cnt4,
                                                         const uint32_t* __restrict__ rhash,
                                                         const uint32_t* __restrict__ isrep,
                                                         uint32_t* __restrict__ hist) {
+  const uint64_t seed = seed_p ? *seed_p : seed_v;  // device seed: hipGraph-replayable
   const int row = blockIdx.y, cl = row % B;
   const int U = cnt4[cl * 4];
   __shared__ uint32_t h[kSelBins];
@@ -577,11 +579,13 @@ __device__ __forceinline__ void voxf_emit(int row, int cl, int N, int64_t T, int
 // are kept (one contiguous candidate range per workgroup, two counter atomics per workgroup),
 // keys in b* go to the tie list.
 __global__ __launch_bounds__(256) void voxf_select_kernel(
-    const float* __restrict__ pts, int N, int64_t T, int B, uint64_t seed,
+    const float* __restrict__ pts, int N, int64_t T, int B, uint64_t seed_v,
+    const uint64_t* __restrict__ seed_p,
     const uint32_t* __restrict__ hist, int32_t* __restrict__ sel, int32_t* __restrict__ cnt4,
     const uint32_t* __restrict__ rhash, const uint32_t* __restrict__ isrep,
     const int64_t* __restrict__ reps, unsigned long long* __restrict__ ties,
     int64_t* __restrict__ out_idx, float* __restrict__ out_pts) {
+  const uint64_t seed = seed_p ? *seed_p : seed_v;
   const int row = blockIdx.y, cl = row % B;
   const int U = cnt4[cl * 4];
   const int need = U > T ? (int)T : (U < T ? (int)(T - U) : 0);
@@ -677,8 +681,8 @@ __global__ __launch_bounds__(1024) void voxf_ties_kernel(const float* __restrict
 // stats (+ zeroing), insert (+ voxel parameters), reps (+ kept reps), hist, select (+ boundary
 // bin, kept points), ties (+ kept points): 6 launches.
 static int voxel_fast(const float* pts, int64_t B, int64_t N, int64_t copies, int64_t T,
-                      void* workspace, uint64_t seed, int64_t* out_idx, float* out_pts,
-                      hipStream_t s) {
+                      void* workspace, uint64_t seed, const uint64_t* seed_p, int64_t* out_idx,
+                      float* out_pts, hipStream_t s) {
   VoxelFastWS w = carve_voxel_fast(workspace, B, N, copies);
   const int b = (int)B, n = (int)N, rows = (int)(B * copies);
   const size_t zero = (size_t)((char*)(w.isrep + B * N) - (char*)w.cnt4);
@@ -689,10 +693,10 @@ static int voxel_fast(const float* pts, int64_t B, int64_t N, int64_t copies, in
   hipLaunchKernelGGL(voxf_reps_kernel, dim3(kVoxRepsBlocks, b), dim3(256), 0, s, pts, w.tkey, w.tsum, w.tcnt,
                      w.H, n, T, b, (int)copies, w.cnt4, w.reps, w.rhash, w.isrep, out_idx, out_pts);
   const unsigned gs = (unsigned)std::min<int64_t>(cdiv(N, 256), 256);
-  hipLaunchKernelGGL(voxf_hist_kernel, dim3(gs, rows), dim3(256), 0, s, n, T, b, seed, w.cnt4,
-                     w.rhash, w.isrep, w.hist);
+  hipLaunchKernelGGL(voxf_hist_kernel, dim3(gs, rows), dim3(256), 0, s, n, T, b, seed, seed_p,
+                     w.cnt4, w.rhash, w.isrep, w.hist);
   hipLaunchKernelGGL(voxf_select_kernel, dim3(128, rows), dim3(256), 0, s, pts, n, T, b, seed,
-                     w.hist, w.sel, w.cnt4, w.rhash, w.isrep, w.reps, w.ties, out_idx, out_pts);
+                     seed_p, w.hist, w.sel, w.cnt4, w.rhash, w.isrep, w.reps, w.ties, out_idx, out_pts);
   hipLaunchKernelGGL(voxf_ties_kernel, dim3(rows), dim3(1024), 0, s, pts, n, T, b, w.sel, w.cnt4,
                      w.ties, w.reps, out_idx, out_pts);
   PCST_LAUNCH_CHECK("voxel_downsample");
@@ -798,7 +802,8 @@ extern "C" int pcst_voxel_downsample(const float* pts, int64_t B, int64_t N, int
                                      float* out_pts, void* stream) {
   PCST_CHECK_ARG(B > 0 && N > target && target > 0 && N < (1ll << 30), "voxel_downsample: bad shape");
   PCST_CHECK_ARG(pts && workspace && out_idx && out_pts, "voxel_downsample: null pointer");
-  return voxel_fast(pts, B, N, 1, target, workspace, seed, out_idx, out_pts, as_stream(stream));
+  return voxel_fast(pts, B, N, 1, target, workspace, seed, nullptr, out_idx, out_pts,
+                    as_stream(stream));
 }
 
 extern "C" int pcst_voxel_downsample_copies(const float* pts, int64_t B, int64_t N, int64_t copies,
@@ -808,7 +813,20 @@ extern "C" int pcst_voxel_downsample_copies(const float* pts, int64_t B, int64_t
                      N < (1ll << 30),
                  "voxel_downsample_copies: bad shape");
   PCST_CHECK_ARG(pts && workspace && out_idx && out_pts, "voxel_downsample_copies: null pointer");
-  return voxel_fast(pts, B, N, copies, target, workspace, seed, out_idx, out_pts,
+  return voxel_fast(pts, B, N, copies, target, workspace, seed, nullptr, out_idx, out_pts,
+                    as_stream(stream));
+}
+
+extern "C" int pcst_voxel_downsample_copies_dseed(const float* pts, int64_t B, int64_t N,
+                                                  int64_t copies, int64_t target, void* workspace,
+                                                  const uint64_t* seed_dev, int64_t* out_idx,
+                                                  float* out_pts, void* stream) {
+  PCST_CHECK_ARG(B > 0 && copies >= 1 && B * copies < (1 << 15) && N > target && target > 0 &&
+                     N < (1ll << 30),
+                 "voxel_downsample_copies_dseed: bad shape");
+  PCST_CHECK_ARG(pts && workspace && seed_dev && out_idx && out_pts,
+                 "voxel_downsample_copies_dseed: null pointer");
+  return voxel_fast(pts, B, N, copies, target, workspace, 0, seed_dev, out_idx, out_pts,
                     as_stream(stream));
 }
 

@@ -268,6 +268,10 @@ class DiffusionProcess:
                                      target_range: float = 1.8) -> torch.Tensor:
         return torch.tanh(points / target_range) * target_range
 
+    def _timesteps(self, num_inference_steps: int):
+        """The guided loop's schedule: CPU linspace(999, 0, n).long() (diffusion_model.py:236)."""
+        return torch.linspace(self.num_timesteps - 1, 0, num_inference_steps).long().tolist()
+
     def _coeffs(self, t: int, t_prev: int):
         """fp32 scalars of the update, as the reference's 0-d tensor ops produce them."""
         one = np.float32(1.0)
@@ -279,8 +283,17 @@ class DiffusionProcess:
     def guided_sample_loop(self, model: PointCloudDiffusionModel, source_points: torch.Tensor,
                            condition_points: torch.Tensor, num_inference_steps: int = 50,
                            guidance_scale: float = 7.5, *,
-                           x_T: Optional[torch.Tensor] = None) -> torch.Tensor:
-        """`guided_sample_loop` (diffusion_model.py:224-261)."""
+                           x_T: Optional[torch.Tensor] = None, graph: bool = False) -> torch.Tensor:
+        """`guided_sample_loop` (diffusion_model.py:224-261).
+
+        graph=True (keyword-only, BASELINE configs[4]): the hierarchical denoise step is captured
+        once into a hipGraph and replayed per timestep; the per-step scalars (timestep rows, DDIM
+        coefficients, subset seed) are copied into static device buffers between replays.  Same
+        draws and kernels as the eager loop, so the result is bit-identical."""
+        if graph and source_points.shape[1] > model.config.global_points \
+                and not _rng.source().replaying:
+            return self._guided_sample_graph(model, source_points, condition_points,
+                                             num_inference_steps, guidance_scale, x_T)
         device = source_points.device
         shape = source_points.shape
         B = shape[0]
@@ -288,7 +301,7 @@ class DiffusionProcess:
         style_feat = model.style_encoder(hp.downsample(condition_points)[0])
         style_in = torch.cat([style_feat, torch.zeros_like(style_feat)])
         x = x_T.to(device).float() if x_T is not None else _rng.source().randn(shape, device)
-        timesteps = torch.linspace(self.num_timesteps - 1, 0, num_inference_steps).long().tolist()
+        timesteps = self._timesteps(num_inference_steps)
         use_hierarchical = shape[1] > model.config.global_points
         source = source_points.float().contiguous()
         x_cat = torch.cat([x, x]).contiguous()
@@ -309,6 +322,53 @@ class DiffusionProcess:
             t_prev = t_prevs[i]
             x = _hip.cfg_ddim_step(x, eps[:B], eps[B:], source, guidance_scale,
                                    self._coeffs(t, t_prev), x_cat=x_cat)
+        return x
+
+    def _guided_sample_graph(self, model, source_points, condition_points, num_inference_steps,
+                             guidance_scale, x_T):
+        device = source_points.device
+        shape = source_points.shape
+        B = shape[0]
+        hp = model.hierarchical_processor
+        npred = model.noise_predictor
+        style_feat = model.style_encoder(hp.downsample(condition_points)[0])
+        style_in = torch.cat([style_feat, torch.zeros_like(style_feat)])
+        x = (x_T.to(device).float() if x_T is not None
+             else _rng.source().randn(shape, device)).contiguous().clone()
+        timesteps = self._timesteps(num_inference_steps)
+        t_prevs = [timesteps[timesteps.index(t) + 1] if t > 0 else -1 for t in timesteps]
+        source = source_points.float().contiguous()
+        x_cat = torch.cat([x, x]).contiguous()
+        S = len(timesteps)
+        # per-step scalars, drawn/computed in the eager loop's order, resident on the device
+        seeds = [_rng.source().device_seed() & (2**64 - 1) for _ in range(S)]
+        seed_tab = torch.tensor([v - 2**64 if v >= 2**63 else v for v in seeds],
+                                dtype=torch.int64).to(device)
+        coef_tab = torch.tensor(np.array([self._coeffs(t, tp) for t, tp in zip(timesteps, t_prevs)],
+                                         dtype=np.float32)).to(device)
+        t_tab = torch.tensor(timesteps, dtype=torch.long).repeat_interleave(2 * B)
+        t_tab = t_tab.view(S, 2 * B).to(device)
+        t_cur, coef_cur, seed_cur = t_tab[0].clone(), coef_tab[0].clone(), seed_tab[:1].clone()
+        npred.packed()  # weight packing happens outside the capture
+
+        def step():
+            xc, xi = _hip.voxel_downsample_copies_dseed(x, model.config.global_points, seed_cur, 2)
+            eps = hp.upsample_knn(npred(xc, t_cur, style_in), x_cat, xi)
+            _hip.cfg_ddim_step_dcoef(x, eps[:B], eps[B:], source, guidance_scale, coef_cur,
+                                     x_cat=x_cat, out=x)
+
+        g = torch.cuda.CUDAGraph()
+        capture = torch.cuda.Stream(device=device)
+        capture.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(capture):
+            with torch.cuda.graph(g, stream=capture):
+                step()
+        torch.cuda.current_stream().wait_stream(capture)
+        for i in range(S):
+            t_cur.copy_(t_tab[i])
+            coef_cur.copy_(coef_tab[i])
+            seed_cur.copy_(seed_tab[i:i + 1])
+            g.replay()
         return x
 
     @torch.no_grad()
