@@ -254,7 +254,15 @@ __global__ void wgrad_bf16_combine_kernel(const float* __restrict__ part, int64_
   for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < n;
        e += (int64_t)gridDim.x * blockDim.x) {
     double s = 0.0;
-    for (int c = 0; c < chunks; ++c) s += (double)part[(int64_t)c * n + e];
+    int c = 0;
+    for (; c + 8 <= chunks; c += 8) {  // 8 loads in flight, summed in chunk order
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = part[(int64_t)(c + u) * n + e];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) s += (double)v[u];
+    }
+    for (; c < chunks; ++c) s += (double)part[(int64_t)c * n + e];
     out[e] = (float)s;
   }
 }
