@@ -115,8 +115,13 @@ __global__ void chamfer_keys_kernel(const int32_t* __restrict__ argm, int R, uin
   }
 }
 
-// scattered term: destination d (a row of D-side cloud, D_pts [B,ND,3]) sums, in ascending
-// source-row order, sign * g/NR * 2(src_r - dst_d) over source rows r with argmin(r) == d.
+// scattered term: destination d (a row of D-side cloud, D_pts [B,ND,3]) sums
+// sign * g/NR * 2(src_r - dst_d) over source rows r with argmin(r) == d.  A group of 16 lanes
+// serves one destination: lane j sums the contributions lo+j, lo+j+16, ... of d's sorted segment
+// in order, then the 16 partials are combined by a fixed xor tree, so the result is
+// deterministic and a destination with many sources (a point many rows collapse onto) costs
+// len/16 rounds instead of len.
+constexpr int kGatherLanes = 16;
 __global__ void chamfer_gather_kernel(const float* __restrict__ Dp, int ND,
                                       const float* __restrict__ Sp, int NR,
                                       const uint32_t* __restrict__ skeys,
@@ -124,30 +129,41 @@ __global__ void chamfer_gather_kernel(const float* __restrict__ Dp, int ND,
                                       const float* __restrict__ gout, float sign,
                                       float* __restrict__ grad) {
   const int b = blockIdx.y;
-  const int d = blockIdx.x * 256 + threadIdx.x;
-  if (d >= ND) return;
+  const int t = blockIdx.x * 256 + threadIdx.x;
+  const int d = t / kGatherLanes, j = t % kGatherLanes;
+  const bool valid = d < ND;  // whole 16-lane groups share validity (256 % 16 == 0)
   const uint32_t* K = skeys + (int64_t)b * NR;
-  int lo = 0, hi = NR;  // lower bound of d
+  int lo = 0, hi = valid ? NR : 0;  // lower bound of d
   while (lo < hi) {
     const int mid = (lo + hi) >> 1;
     if (K[mid] < (uint32_t)d) lo = mid + 1; else hi = mid;
   }
-  const float* q = Dp + ((int64_t)b * ND + d) * 3;
+  const float* q = Dp + ((int64_t)b * ND + (valid ? d : 0)) * 3;
   const float g = gout[b] * 2.0f / (float)NR;
   float a0 = 0.0f, a1 = 0.0f, a2 = 0.0f;
-  for (int k = lo; k < NR && K[k] == (uint32_t)d; ++k) {
-    const int r = (int)svals[(int64_t)b * NR + k];
-    const float* p = Sp + ((int64_t)b * NR + r) * 3;
-    if (raw_pair(p, q) >= 0.0f) {
-      a0 += g * (p[0] - q[0]);
-      a1 += g * (p[1] - q[1]);
-      a2 += g * (p[2] - q[2]);
+  if (valid) {
+    for (int k = lo + j; k < NR && K[k] == (uint32_t)d; k += kGatherLanes) {
+      const int r = (int)svals[(int64_t)b * NR + k];
+      const float* p = Sp + ((int64_t)b * NR + r) * 3;
+      if (raw_pair(p, q) >= 0.0f) {
+        a0 += g * (p[0] - q[0]);
+        a1 += g * (p[1] - q[1]);
+        a2 += g * (p[2] - q[2]);
+      }
     }
   }
-  float* o = grad + ((int64_t)b * ND + d) * 3;
-  o[0] += -sign * a0;
-  o[1] += -sign * a1;
-  o[2] += -sign * a2;
+#pragma unroll
+  for (int off = kGatherLanes / 2; off > 0; off >>= 1) {
+    a0 += __shfl_xor(a0, off);
+    a1 += __shfl_xor(a1, off);
+    a2 += __shfl_xor(a2, off);
+  }
+  if (valid && j == 0) {
+    float* o = grad + ((int64_t)b * ND + d) * 3;
+    o[0] += -sign * a0;
+    o[1] += -sign * a1;
+    o[2] += -sign * a2;
+  }
 }
 
 // ---- L1 (F.l1_loss, mean reduction): deterministic two-level float64 sum
@@ -247,8 +263,9 @@ extern "C" int pcst_chamfer_bwd(const float* pred, const float* target, int64_t 
     int rc = radix_sort_pairs(w.kA, w.vA, w.kB, w.vB, w.hist, (int)B, N, SegCounts{nullptr, (int32_t)N},
                               0, 32, s);
     if (rc) return rc;
-    hipLaunchKernelGGL(chamfer_gather_kernel, dim3((unsigned)cdiv(M, 256), b), dim3(256), 0, s,
-                       target, (int)M, pred, (int)N, w.kA, w.vA, grad_out, 1.0f, grad_target);
+    hipLaunchKernelGGL(chamfer_gather_kernel, dim3((unsigned)cdiv(M * kGatherLanes, 256), b),
+                       dim3(256), 0, s, target, (int)M, pred, (int)N, w.kA, w.vA, grad_out, 1.0f,
+                       grad_target);
   }
   // direction 2 (target rows -> pred argmin): direct on target, scattered on pred
   if (grad_target)
@@ -260,8 +277,9 @@ extern "C" int pcst_chamfer_bwd(const float* pred, const float* target, int64_t 
     int rc = radix_sort_pairs(w.kA, w.vA, w.kB, w.vB, w.hist, (int)B, M, SegCounts{nullptr, (int32_t)M},
                               0, 32, s);
     if (rc) return rc;
-    hipLaunchKernelGGL(chamfer_gather_kernel, dim3((unsigned)cdiv(N, 256), b), dim3(256), 0, s,
-                       pred, (int)N, target, (int)M, w.kA, w.vA, grad_out, 1.0f, grad_pred);
+    hipLaunchKernelGGL(chamfer_gather_kernel, dim3((unsigned)cdiv(N * kGatherLanes, 256), b),
+                       dim3(256), 0, s, pred, (int)N, target, (int)M, w.kA, w.vA, grad_out, 1.0f,
+                       grad_pred);
   }
   PCST_LAUNCH_CHECK("chamfer_bwd");
   return PCST_OK;
