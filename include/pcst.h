@@ -93,6 +93,8 @@ int pcst_affine_act(const float* Z, int64_t M, int64_t O, const float* scale, co
  * dZ (db may be NULL), with dZ [M,O] and X [M,I] row-major.  Split over row chunks on exact-f32
  * MFMA, partials combined in chunk order in float64 (deterministic).
  * workspace: pcst_linear_wgrad_workspace_size() bytes. */
+/* ReLU backward of the same layers: dz[i] = dy[i] * (y[i] > 0 ? 1 : 0), one pass. */
+int pcst_relu_bwd(const float* dy, const float* y, int64_t n, float* dz, void* stream);
 int pcst_linear_wgrad_workspace_size(int64_t M, int64_t I, int64_t O, size_t* bytes);
 int pcst_linear_wgrad(const float* dZ, const float* X, int64_t M, int64_t I, int64_t O, float* dW,
                       float* db, void* workspace, void* stream);

@@ -61,6 +61,7 @@ SIGNATURES = {
     "pcst_gemm_nt_bf16": [_P, _I, _I, _P, _I, _P, _P, ctypes.c_int, _P, _P],
     "pcst_linear_wgrad_bf16_workspace_size": [_I, _I, _I, _SZ],
     "pcst_linear_wgrad_bf16": [_P, _P, _I, _I, _I, _P, _P, _P, _P],
+    "pcst_relu_bwd": [_P, _P, _I, _P, _P],
     "pcst_linear_wgrad_workspace_size": [_I, _I, _I, _SZ],
     "pcst_linear_wgrad": [_P, _P, _I, _I, _I, _P, _P, _P, _P],
     "pcst_channel_stats_workspace_size": [_I, _SZ],
@@ -366,6 +367,17 @@ def pointwise_linear(X, W, scale=None, shift=None, relu=False, pool_ns=0):
           _ptr(None if scale is None else _f32(scale)), _ptr(None if shift is None else _f32(shift)),
           int(relu), pool_ns, _ptr(Y), _stream())
     return Y
+
+
+def relu_bwd(dy, y):
+    """dy * [y > 0] in one pass (the ReLU backward of the per-point layers)."""
+    require_device(dy, y)
+    dy, y = _f32(dy), _f32(y)
+    if dy.shape != y.shape:
+        raise RuntimeError(f"relu_bwd: shape mismatch {tuple(dy.shape)} vs {tuple(y.shape)}")
+    dz = torch.empty_like(dy)
+    _call("pcst_relu_bwd", _ptr(dy), _ptr(y), dy.numel(), _ptr(dz), _stream())
+    return dz
 
 
 def linear_wgrad(dZ, X, bias=True, bf16=False):

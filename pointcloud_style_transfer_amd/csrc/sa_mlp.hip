@@ -208,6 +208,24 @@ __global__ void wgrad_combine_kernel(const float* __restrict__ part, int64_t n, 
   }
 }
 
+// ReLU backward of the training path: dz = dy * [y > 0] in one pass (the product form keeps
+// torch's semantics: -0 and NaN propagate as in dy * mask)
+__global__ void relu_bwd_kernel(const float4* __restrict__ dy, const float4* __restrict__ y,
+                                int64_t n4, float4* __restrict__ dz) {
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < n4;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const float4 g = dy[e], v = y[e];
+    dz[e] = make_float4(g.x * (v.x > 0.f ? 1.f : 0.f), g.y * (v.y > 0.f ? 1.f : 0.f),
+                        g.z * (v.z > 0.f ? 1.f : 0.f), g.w * (v.w > 0.f ? 1.f : 0.f));
+  }
+}
+
+__global__ void relu_bwd_tail_kernel(const float* __restrict__ dy, const float* __restrict__ y,
+                                     int64_t b0, int64_t n, float* __restrict__ dz) {
+  const int64_t e = b0 + blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (e < n) dz[e] = dy[e] * (y[e] > 0.f ? 1.f : 0.f);
+}
+
 struct WgradPlan {
   int tiles_i, tiles_o, chunks;
   int64_t rows_per_chunk;
@@ -316,5 +334,23 @@ extern "C" int pcst_linear_wgrad(const float* dZ, const float* X, int64_t M, int
     hipLaunchKernelGGL(wgrad_combine_kernel, dim3((unsigned)cdiv(O, 256)), dim3(256), 0, s, partB,
                        O, p.chunks, db);
   PCST_LAUNCH_CHECK("linear_wgrad");
+  return PCST_OK;
+}
+
+extern "C" int pcst_relu_bwd(const float* dy, const float* y, int64_t n, float* dz, void* stream) {
+  PCST_CHECK_ARG(n >= 0, "relu_bwd: bad size");
+  if (n == 0) return PCST_OK;
+  PCST_CHECK_ARG(dy && y && dz, "relu_bwd: null pointer");
+  hipStream_t s = as_stream(stream);
+  const bool vec = ((uintptr_t)dy % 16 == 0) && ((uintptr_t)y % 16 == 0) && ((uintptr_t)dz % 16 == 0);
+  const int64_t n4 = vec ? n / 4 : 0;
+  if (n4 > 0)
+    hipLaunchKernelGGL(relu_bwd_kernel, dim3((unsigned)std::min<int64_t>(cdiv(n4, 256), 8192)),
+                       dim3(256), 0, s, reinterpret_cast<const float4*>(dy),
+                       reinterpret_cast<const float4*>(y), n4, reinterpret_cast<float4*>(dz));
+  if (n4 * 4 < n)
+    hipLaunchKernelGGL(relu_bwd_tail_kernel, dim3((unsigned)cdiv(n - n4 * 4, 256)), dim3(256), 0, s,
+                       dy, y, n4 * 4, n, dz);
+  PCST_LAUNCH_CHECK("relu_bwd");
   return PCST_OK;
 }

@@ -2,7 +2,7 @@
 (csrc/sa_mlp.hip), forward and backward.
 
   forward   Y  = act(X W^T + b)                      pcst_pointwise_linear
-  backward  dZ = dY * [Y > 0]  (ReLU)
+  backward  dZ = dY * [Y > 0]  (ReLU)                 pcst_relu_bwd
             dX = dZ W          = linear(dZ, W^T)     pcst_pointwise_linear
             dW = dZ^T X, db = dZ^T 1                  pcst_linear_wgrad (split over row chunks)
 All products are exact-f32 MFMA; the row reduction combines fixed chunks in order (no
@@ -40,7 +40,7 @@ class LinearFn(torch.autograd.Function):
         x2, W, y = ctx.saved_tensors
         dz = gy.reshape(-1, W.shape[0]).float().contiguous()
         if ctx.relu:
-            dz = dz * (y > 0)
+            dz = _hip.relu_bwd(dz, y)
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
             gemm = _hip.gemm_nt_bf16 if ctx.bf16 else _hip.pointwise_linear

@@ -140,3 +140,11 @@ def test_trainer_step_amp_close_to_fp32(H, tmp_path):
         losses.append(float(loss))
     assert np.isfinite(losses).all()
     assert abs(losses[1] - losses[0]) <= 2e-2 * abs(losses[0]), losses
+
+
+def test_relu_bwd_matches_torch(H):
+    g = torch.Generator(device="cuda").manual_seed(3)
+    for n in (1, 7, 4096, 1000003):
+        dy = torch.randn(n, device="cuda", generator=g)
+        y = torch.randn(n, device="cuda", generator=g).clamp_min(0)
+        assert torch.equal(H.relu_bwd(dy, y), dy * (y > 0))
