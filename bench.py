@@ -7,17 +7,29 @@ voxel downsample of the CFG batch (2 x 120000 -> 2 x 30000; the two rows are cop
 the voxel table is built once and the subset drawn per row), fused noise MLP on 60000 points,
 kNN-3 upsample back to 2 x 120000, CFG + DDIM update.  Each rank denoises its own cloud(s)
 (independent objects: no data-path collective; scaling "weak").  The one-time style encode is
-timed separately and excluded.
+timed separately (after one warm-up call) and excluded.
 
-Prints ONE JSON line on rank 0 (driver contract), including `roofline` for the dominant
-kernel (pcst noise MLP, MFMA-bound) measured with HIP events around its launches inside the
-timed region, and `cpu_baseline` (the oracle, a port of the reference path, on host cores).
+`--gpus N` with N > 1 outside torchrun re-launches itself under
+`python -m torch.distributed.run --nproc-per-node N` before anything touches the GPU (the
+parent only waits for it); under torchrun the world size must equal N.
+
+Prints ONE JSON line on rank 0 (driver contract), including
+  * `roofline` for the dominant kernel (pcst noise MLP, MFMA-bound) from HIP events around its
+    launches inside the timed region, with `traffic` from the committed PMC summary;
+  * `cpu_baseline` (N=1 only): the oracle -- a numpy + C port of the reference path -- timed
+    on the host cores over the same 50-step guided loop that the quality leg compares with;
+  * `quality` (N=1 only, outside the timed region): "Chamfer vs ref", the second half of
+    BASELINE's metric -- the HIP loop (bf16 and fp32 noise MLP) against the oracle loop on
+    the same 120k cloud, x_T and counter-keyed draws (rng.CounterRNG);
+  * `encoder_rooflines`: FPS / ball query in the SURVEY §8d scan model AND from PMC counters.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -31,6 +43,7 @@ FLOP_PER_POINT = 3_540_480          # NoisePredictor MACs x 2
 MFMA_BF16_PEAK_TFLOPS = 2500.0      # MI355X dense bf16 (MI355X_MICROARCH.md)
 MFMA_F32_PEAK_TFLOPS = 157.3
 HBM_PEAK_GBS = 8000.0
+QUALITY_SEED = 6000                 # replayed permutations
 
 
 def parse():
@@ -42,16 +55,41 @@ def parse():
     ap.add_argument("--clouds-per-gpu", type=int, default=1)
     ap.add_argument("--points", type=int, default=120000)
     ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32"])
-    ap.add_argument("--cpu-steps", type=int, default=3)
-    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--quality-steps", type=int, default=50,
+                    help="schedule length of the Chamfer-vs-ref / cpu_baseline loop")
+    ap.add_argument("--no-cpu-baseline", action="store_true",
+                    help="skip the oracle leg (cpu_baseline and quality)")
+    ap.add_argument("--no-encoder", action="store_true")
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "noise_mlp_traffic.json"))
+    ap.add_argument("--encoder-traffic-json",
+                    default=os.path.join(REPO, "profiles", "encoder_traffic.json"))
     return ap.parse_args()
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def maybe_spawn(args):
+    """--gpus N > 1 without a torchrun environment: start the N ranks as a child torchrun job
+    (this process has not touched the GPU) and exit with its code."""
+    if args.gpus <= 1 or "WORLD_SIZE" in os.environ:
+        return
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", MASTER_ADDR="127.0.0.1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={args.gpus}", "--master-addr", "127.0.0.1",
+           "--master-port", str(_free_port()), os.path.abspath(__file__)] + sys.argv[1:]
+    sys.exit(subprocess.call(cmd, env=env))
 
 
 def setup_dist(args):
     from pointcloud_style_transfer_amd.distributed import init_from_env
 
     world, rank, local = init_from_env("nccl")
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but the launcher started {world} ranks")
     if world == 1:
         torch.cuda.set_device(0)
     return world, rank, local
@@ -68,61 +106,132 @@ def build_model(precision, device):
     return cfg, model, DiffusionProcess(cfg, device=str(device))
 
 
-def cpu_baseline(args, cfg, model, src, cond, xT):
-    """The oracle (numpy + C port of the reference path) on host cores: per-step cost of the
-    same guided step on the same 120k clouds, (t(1+k) - t(1)) / k."""
+def host_cpu():
+    """CPU model, physical cores, the CPUs this process may run on, and the BLAS threads the
+    oracle uses (= min of the affinity set, OMP_NUM_THREADS and the physical cores)."""
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        import psutil
+
+        physical = psutil.cpu_count(logical=False) or os.cpu_count()
+    except Exception:  # noqa: BLE001
+        physical = os.cpu_count()
+    visible = len(os.sched_getaffinity(0))
+    cap = int(os.environ.get("OMP_NUM_THREADS", str(visible)))
+    threads = max(1, min(visible, cap, physical or visible))
+    return {"cpu_model": model, "physical_cores_on_host": physical,
+            "cpus_visible_to_process": visible, "threads": threads}
+
+
+def oracle_leg(args, cfg, model, dp, src_np, cond_np, xT_np, device):
+    """The oracle (numpy + C port of the reference path) runs the reference's guided loop on
+    host cores: `quality_steps` steps of linspace(999, 0, n) on cloud 0, counter-keyed draws.
+    The same schedule, x_T and draws drive the HIP loop in bf16 and fp32.  Returns
+    (cpu_baseline, quality)."""
     from oracle import oracle as O
+    from pointcloud_style_transfer_amd import rng as R
+    from pointcloud_style_transfer_amd.evaluation.metrics import PointCloudMetrics
 
-    threads = int(os.environ.get("OMP_NUM_THREADS", str(min(os.cpu_count() or 1, 16))))
+    cpu = host_cpu()
+    try:
+        from threadpoolctl import threadpool_limits
+
+        limiter = threadpool_limits(limits=cpu["threads"])
+    except Exception:  # noqa: BLE001
+        limiter = None
+    S = args.quality_steps
+    T = cfg.global_points
     sd = {k: v.detach().float().cpu().numpy() for k, v in model.state_dict().items()}
-    sched = O.Schedule()
-    ts = O.timesteps_for(1000, 1000)
-    rng = np.random.default_rng(6000)
+    sched = O.Schedule(cfg.num_timesteps, cfg.beta_schedule, cfg.noise_schedule_offset)
+    ts = O.timesteps_for(cfg.num_timesteps, S)
+    ctr = R.CounterRNG(QUALITY_SEED)   # the draw order of guided_sample_loop (see rng.py)
 
-    class RandReplay:  # fresh permutations for every downsample (the oracle never draws itself)
-        def next(self, kind):
-            raise RuntimeError
-
-    B = 1
-    x = xT[:1].copy()
-    style = np.zeros((1, 256), np.float32) + 0.1
-    style_in = np.concatenate([style, np.zeros_like(style)])
-
-    def step(i):
-        nonlocal x
-        t = ts[i]
-        x_in = np.concatenate([x, x])
+    def down(rows):
+        """voxel downsample of every row with the next counter-keyed permutation each."""
         outs, idxs = [], []
-        for b in range(2):
-            reps, _, _ = O.voxel_reps(x_in[b], cfg.global_points)
-            perm = rng.permutation(len(x_in[b]) - len(np.unique(reps))) if len(reps) < cfg.global_points \
-                else rng.permutation(len(reps))
-            p, ix = O.voxel_downsample(x_in[b:b + 1], cfg.global_points, O.Replay([("randperm", perm)]))
+        for b in range(rows.shape[0]):
+            reps, _, _ = O.voxel_reps(rows[b], T)
+            U = len(reps)   # reps may repeat an index (two voxels with the same mean index)
+            n = U if U > T else (rows.shape[1] - len(np.unique(reps)) if U < T else 0)
+            draws = [("randperm", ctr.generator().permutation(n))] if n else []
+            p, ix = O.voxel_downsample(rows[b:b + 1], T, O.Replay(draws))
             outs.append(p[0])
             idxs.append(ix[0])
-        xc, xi = np.stack(outs), np.stack(idxs)
+        return np.stack(outs), np.stack(idxs)
+
+    src, cond, x = src_np[:1], cond_np[:1], xT_np[:1].copy()
+    t_enc = time.perf_counter()
+    cdown, _ = down(cond)
+    starts = [("randint", ctr.generator().integers(0, cdown.shape[1], (1,), dtype=np.int64)),
+              ("randint", ctr.generator().integers(0, 512, (1,), dtype=np.int64))]
+    style = O.style_encoder(sd, cdown, O.Replay(starts))
+    t_enc = time.perf_counter() - t_enc
+    style_in = np.concatenate([style, np.zeros_like(style)])
+    step_s = []
+    for i, t in enumerate(ts):
+        t0 = time.perf_counter()
+        x_in = np.concatenate([x, x])
+        xc, xi = down(x_in)
         nc = O.noise_predictor(sd, xc, np.full(2, t), style_in)
         eps = O.upsample_knn(nc, x_in, xi)
-        x = O.guided_update(sched, x, eps[:B], eps[B:], src[:1], t, ts[i + 1], 7.5)
-
-    t0 = time.perf_counter()
-    step(0)
-    t1 = time.perf_counter()
-    for i in range(1, 1 + args.cpu_steps):
-        step(i)
-    t2 = time.perf_counter()
-    per = (t2 - t1) / args.cpu_steps
-    return {"value": round(1.0 / per, 4), "unit": "denoising-steps/s", "cores": threads,
+        x = O.guided_update(sched, x, eps[:1], eps[1:], src, int(t),
+                            int(ts[i + 1]) if t > 0 else -1, 7.5)
+        step_s.append(time.perf_counter() - t0)
+    if limiter is not None:
+        limiter.restore_original_limits()
+    per = float(np.median(step_s[1:])) if len(step_s) > 1 else step_s[0]
+    base = {"value": round(1.0 / per, 4), "unit": "denoising-steps/s", "cores": cpu["threads"],
             "kind": "port",
-            "sample": f"oracle guided step on 1 x {args.points}-pt cloud (CFG x2, 30k coarse), "
-                      f"{args.cpu_steps} steps after 1 untimed (first {t1 - t0:.1f}s), "
-                      f"{per:.2f} s/step; numpy/OpenBLAS fp32 MLP + C voxel/kNN"}
+            "sample": f"oracle (numpy/OpenBLAS fp32 MLP + C voxel/kNN, port of the reference "
+                      f"path) guided loop on 1 x {args.points}-pt cloud, CFG x2, 30k coarse, "
+                      f"{S}-step schedule; median of steps 2..{S}: {per:.3f} s/step "
+                      f"({sum(step_s):.1f} s total, style encode {t_enc:.2f} s)",
+            "host": cpu}
+
+    # the HIP loop on the same inputs and draws, bf16 (measured mode) and fp32 (parity mode)
+    met = PointCloudMetrics(device=str(device))
+    ref = torch.from_numpy(x).to(device)
+    quality = {"definition": "evaluation/metrics.py:20-44 Chamfer (Euclidean, both directions, "
+                             "/2) between the HIP output and the oracle output",
+               "schedule_steps": S, "points": args.points, "guidance_scale": 7.5,
+               "draws": f"rng.CounterRNG({QUALITY_SEED}) on both sides; same x_T (seed 3000)"}
+    prec0 = cfg.precision
+    for prec in ("bf16", "fp32"):
+        cfg.precision = prec
+        with R.replay(R.CounterRNG(QUALITY_SEED)):
+            out = dp.guided_sample_loop(model, torch.from_numpy(src).to(device),
+                                        torch.from_numpy(cond).to(device), S, 7.5,
+                                        x_T=torch.from_numpy(xT_np[:1]).to(device))
+        d = (out.double() - ref.double()).abs()
+        scale = ref.abs().max().double()
+        within = (d <= 1e-4 * (ref.abs().double() + 0.1 * scale)).double().mean()
+        quality[prec] = {
+            "chamfer_vs_ref": float(met.chamfer_distance(out, ref)[0]),
+            "frac_within_1e-4": round(float(within), 6),
+            "max_abs": float(d.max()),
+            "mean_abs": float(d.mean()),
+        }
+    cfg.precision = prec0
+    quality["criterion"] = "|hip - oracle| <= 1e-4 * (|oracle| + 0.1 max|oracle|) per element"
+    return base, quality
 
 
-def encoder_rooflines(xc, device, reps=5):
-    """SA1 farthest-point sampling (512 of 30000) and ball query (r 0.2, 32) on the coarse
-    condition cloud, timed with HIP events on the launch stream; achieved bandwidth in the
-    SURVEY §8d scan model (FPS npoint*N*16 B, ball query S*N*12 B + S*ns*8 B)."""
+def encoder_rooflines(xc, device, traffic, tag, reps=5):
+    """SA1 farthest-point sampling (512 of 30000) and ball query (r 0.2, 32) on coarse
+    condition clouds, timed with HIP events on the launch stream.  Two bandwidth figures:
+      * `scan_model`: SURVEY §8d's effective bytes (FPS npoint*N*16 B, ball query
+        S*N*12 B + S*ns*8 B) over the time -- a comparison figure; > 1.0 of peak is flagged,
+        it means the kernel does not re-stream what the model counts;
+      * `counters`: HBM bytes per launch from the committed rocprofv3 PMC pass
+        (FETCH_SIZE x2 + WRITE_SIZE, profiles/encoder_traffic.json) over the same time."""
     from pointcloud_style_transfer_amd import _hip
 
     B, N, _ = xc.shape
@@ -130,38 +239,51 @@ def encoder_rooflines(xc, device, reps=5):
     ev = lambda: torch.cuda.Event(enable_timing=True)  # noqa: E731
     t_fps, t_bq = [], []
     for _ in range(reps):
-        e0, e1, e2 = ev(), ev(), ev()
+        e0, e1, e2, e3 = ev(), ev(), ev(), ev()
         e0.record()
         idx = _hip.fps(xc, 512, start)
         e1.record()
         new_xyz = _hip.index_points(xc, idx)
         e2.record()
         _hip.ball_query(0.2, 32, xc, new_xyz)
-        e3 = ev()
         e3.record()
         torch.cuda.synchronize()
         t_fps.append(e0.elapsed_time(e1))
         t_bq.append(e2.elapsed_time(e3))
     out = {}
-    for name, ms, byts in (("fps", min(t_fps), 512 * N * 16 * B),
-                           ("ball_query", min(t_bq), (512 * N * 12 + 512 * 32 * 8) * B)):
+    for name, ms, byts in (("fps", float(np.median(t_fps)), 512 * N * 16 * B),
+                           ("ball_query", float(np.median(t_bq)), (512 * N * 12 + 512 * 32 * 8) * B)):
         gbs = byts / (ms * 1e-3) / 1e9
-        out[name] = {"bound": "hbm (scan model)", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4), "ms": round(ms, 4),
-                     "shape": f"B={B} N={N} S=512"}
+        rec = {"ms": round(ms, 4), "shape": f"B={B} N={N} S=512",
+               "scan_model": {"bytes": byts, "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS,
+                              "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4),
+                              "exceeds_peak": gbs > HBM_PEAK_GBS}}
+        tb = (traffic or {}).get(f"{name}_{tag}")
+        if tb:
+            g2 = tb / (ms * 1e-3) / 1e9
+            rec["counters"] = {"traffic_bytes": tb, "achieved": round(g2, 2), "peak": HBM_PEAK_GBS,
+                               "unit": "GB/s", "frac": round(g2 / HBM_PEAK_GBS, 5)}
+        else:
+            rec["counters"] = None
+        if name == "fps":
+            rec["per_round_us"] = round(ms * 1e3 / 512, 3)
+            rec["bound"] = "latency (512 dependent arg-max rounds)"
+        else:
+            rec["bound"] = "latency / L2 (one wave per centroid, early exit at nsample)"
+        out[name] = rec
     return out
 
 
 def main():
     args = parse()
+    maybe_spawn(args)
     world, rank, local = setup_dist(args)
     device = torch.device("cuda", torch.cuda.current_device())
     from pointcloud_style_transfer_amd import _hip
+    from pointcloud_style_transfer_amd.distributed import max_over_ranks, shard
     from pointcloud_style_transfer_amd.synthetic import lidar_like_cloud, standard_normal
 
     cfg, model, dp = build_model(args.precision, device)
-    from pointcloud_style_transfer_amd.distributed import max_over_ranks, shard
-
     C = args.clouds_per_gpu
     mine = shard(world * C, rank, world)  # this rank's clouds (SURVEY §8d seeds 1000+i ...)
     src_np = np.stack([lidar_like_cloud(1000 + i, args.points) for i in mine])
@@ -174,18 +296,26 @@ def main():
     hp = model.hierarchical_processor
     npred = model.noise_predictor
     with torch.no_grad():
+        model.style_encoder(hp.downsample(cond)[0])   # warm-up (first-call costs)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         style = model.style_encoder(hp.downsample(cond)[0])
         torch.cuda.synchronize()
         style_s = time.perf_counter() - t0
         style_in = torch.cat([style, torch.zeros_like(style)])
-        enc = encoder_rooflines(hp.downsample(cond)[0], device)
-        # the same kernels at BASELINE configs[4]'s per-GPU batch (256 clouds / 8 GPUs = 32
-        # coarse condition clouds in one launch: one workgroup per cloud)
-        xb = torch.from_numpy(np.stack([lidar_like_cloud(2000 + i, cfg.global_points)
-                                        for i in range(32)])).to(device)
-        enc.update({k + "_b32": v for k, v in encoder_rooflines(xb, device).items()})
+        enc = None
+        if rank == 0 and not args.no_encoder:
+            traffic = None
+            if os.path.exists(args.encoder_traffic_json):
+                with open(args.encoder_traffic_json) as f:
+                    traffic = json.load(f).get("bytes_per_launch")
+            enc = encoder_rooflines(hp.downsample(cond)[0][:1], device, traffic, "b1")
+            # the same kernels at BASELINE configs[4]'s per-GPU batch (256 clouds / 8 GPUs =
+            # 32 coarse condition clouds in one launch: one workgroup per cloud)
+            xb = torch.from_numpy(np.stack([lidar_like_cloud(2000 + i, cfg.global_points)
+                                            for i in range(32)])).to(device)
+            enc.update({k + "_b32": v for k, v in
+                        encoder_rooflines(xb, device, traffic, "b32").items()})
         npred.packed()
         timesteps = torch.linspace(dp.num_timesteps - 1, 0, dp.num_timesteps).long().tolist()
         t_rows = torch.tensor(timesteps, dtype=torch.long).repeat_interleave(2 * C)
@@ -243,15 +373,16 @@ def main():
         try:
             with open(args.traffic_json) as f:
                 traffic = json.load(f).get("hbm_bytes_per_launch")
-        except Exception:
+        except Exception:  # noqa: BLE001
             traffic = None
     total_steps = world * C * args.steps
     value = total_steps / elapsed
     if rank == 0:
-        base = None
-        if not args.no_cpu_baseline:
+        base = quality = None
+        if world == 1 and not args.no_cpu_baseline:
             torch.cuda.synchronize()
-            base = cpu_baseline(args, cfg, model, src_np, cond_np, xT_np)
+            with torch.no_grad():
+                base, quality = oracle_leg(args, cfg, model, dp, src_np, cond_np, xT_np, device)
         line = {
             "metric": "denoising-steps/sec on 120k-pt cloud",
             "value": round(value, 3),
@@ -269,7 +400,7 @@ def main():
                                    "30000 coarse, full 1000-step schedule (BASELINE configs[1])",
                        "points": args.points, "coarse_points": cfg.global_points,
                        "clouds_per_gpu": C, "guidance_scale": 7.5,
-                       "parallelism": f"independent clouds x{world}",
+                       "parallelism": f"independent clouds x{world} (one process per GPU)",
                        "style_encode_s": round(style_s, 4)},
             "roofline": {"kernel": "pcst noise_mlp", "bound": "mfma",
                          "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
@@ -277,6 +408,7 @@ def main():
                          "algorithmic": f"{FLOP_PER_POINT} FLOP/pt x {2 * C * cfg.global_points} pts",
                          "avg_launch_ms": round(mlp_ms, 4)},
             "cpu_baseline": base,
+            "quality": quality,
             "encoder_rooflines": enc,
         }
         print(json.dumps(line), flush=True)

@@ -9,6 +9,7 @@ CPU tensor is an error.
 from __future__ import annotations
 
 import ctypes
+import functools
 import os
 
 import numpy as np
@@ -112,7 +113,37 @@ def _call(name, *args):
 
 
 def _stream():
+    """torch's current stream of the current device.  Every public wrapper runs under
+    `_on_tensor_device`, so the current device is the one its tensors live on."""
     return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def _tensor_device_index(args, kwargs):
+    """Device index of the first HIP tensor among the arguments (duck-typed), else None."""
+    for a in list(args) + list(kwargs.values()):
+        if isinstance(a, (tuple, list)):  # knn3_query's (orig, idx, ws) handle
+            for b in a:
+                if getattr(b, "is_cuda", False):
+                    return b.device.index
+        elif getattr(a, "is_cuda", False):
+            return a.device.index
+    return None
+
+
+def _on_tensor_device(fn):
+    """Run a wrapper with the tensors' device current, so the launch goes to that device and
+    onto ITS current stream -- also when the caller's current device is another GPU (a model
+    on cuda:1 without torch.cuda.set_device)."""
+    @functools.wraps(fn)
+    def wrapper(*args, **kwargs):
+        idx = _tensor_device_index(args, kwargs)
+        if idx is not None and idx != torch.cuda.current_device():
+            with torch.cuda.device(idx):
+                return fn(*args, **kwargs)
+        return fn(*args, **kwargs)
+
+    wrapper.device_guarded = True
+    return wrapper
 
 
 def require_device(*tensors):
@@ -363,8 +394,11 @@ def pointwise_linear(X, W, scale=None, shift=None, relu=False, pool_ns=0):
     O = W.shape[0]
     rows = M // pool_ns if pool_ns else M
     Y = torch.empty(rows, O, dtype=torch.float32, device=X.device)
-    _call("pcst_pointwise_linear", _ptr(X), M, K, _ptr(W), O,
-          _ptr(None if scale is None else _f32(scale)), _ptr(None if shift is None else _f32(shift)),
+    # converted operands stay bound to locals until the call returns (a temporary whose
+    # block is freed before the launch could be handed to the next allocation)
+    scale = None if scale is None else _f32(scale)
+    shift = None if shift is None else _f32(shift)
+    _call("pcst_pointwise_linear", _ptr(X), M, K, _ptr(W), O, _ptr(scale), _ptr(shift),
           int(relu), pool_ns, _ptr(Y), _stream())
     return Y
 
@@ -406,8 +440,9 @@ def gemm_nt_bf16(A, B, scale=None, shift=None, relu=False):
     if B.shape[1] != K:
         raise RuntimeError(f"gemm_nt_bf16: K mismatch {tuple(A.shape)} vs {tuple(B.shape)}")
     C = torch.empty(M, O, dtype=torch.float32, device=A.device)
-    _call("pcst_gemm_nt_bf16", _ptr(A), M, K, _ptr(B), O,
-          _ptr(None if scale is None else _f32(scale)), _ptr(None if shift is None else _f32(shift)),
+    scale = None if scale is None else _f32(scale)
+    shift = None if shift is None else _f32(shift)
+    _call("pcst_gemm_nt_bf16", _ptr(A), M, K, _ptr(B), O, _ptr(scale), _ptr(shift),
           int(relu), _ptr(C), _stream())
     return C
 
@@ -430,7 +465,8 @@ def affine_act(Z, scale, shift, relu=True, pool_ns=0):
     M, O = Z.shape
     rows = M // pool_ns if pool_ns else M
     Y = torch.empty(rows, O, dtype=torch.float32, device=Z.device)
-    _call("pcst_affine_act", _ptr(Z), M, O, _ptr(_f32(scale)), _ptr(_f32(shift)), int(relu),
+    scale, shift = _f32(scale), _f32(shift)
+    _call("pcst_affine_act", _ptr(Z), M, O, _ptr(scale), _ptr(shift), int(relu),
           pool_ns, _ptr(Y), _stream())
     return Y
 
@@ -461,8 +497,9 @@ def chamfer_bwd(pred, target, arg1, arg2, grad_out, need_pred=True, need_target=
     ws = _workspace("pcst_chamfer_bwd_workspace_size", B, N, M, device=pred.device)
     gp = torch.zeros_like(pred) if need_pred else None
     gt = torch.zeros_like(target) if need_target else None
-    _call("pcst_chamfer_bwd", _ptr(pred), _ptr(target), B, N, M, _ptr(arg1.contiguous()),
-          _ptr(arg2.contiguous()), _ptr(grad_out), _ptr(gp), _ptr(gt), _ptr(ws), _stream())
+    arg1, arg2 = arg1.contiguous(), arg2.contiguous()
+    _call("pcst_chamfer_bwd", _ptr(pred), _ptr(target), B, N, M, _ptr(arg1),
+          _ptr(arg2), _ptr(grad_out), _ptr(gp), _ptr(gt), _ptr(ws), _stream())
     return gp, gt
 
 
@@ -479,8 +516,8 @@ def l1_bwd(a, b, grad_out):
     require_device(a, b, grad_out)
     a, b = _f32(a), _f32(b)
     ga = torch.empty_like(a)
-    _call("pcst_l1_bwd", _ptr(a), _ptr(b), a.numel(), _ptr(_f32(grad_out.reshape(1))), _ptr(ga),
-          _stream())
+    g = _f32(grad_out.reshape(1))
+    _call("pcst_l1_bwd", _ptr(a), _ptr(b), a.numel(), _ptr(g), _ptr(ga), _stream())
     return ga
 
 
@@ -552,3 +589,15 @@ def voxel_downsample_copies_dseed(points, target, seed_dev, copies):
     _call("pcst_voxel_downsample_copies_dseed", _ptr(points), B, N, copies, target, _ptr(ws),
           _ptr(seed_dev), _ptr(out_idx), _ptr(out_pts), _stream())
     return out_pts, out_idx
+
+
+# every public wrapper launches on its tensors' device (see _on_tensor_device)
+_GUARDED = ("square_distance", "index_points", "fps", "ball_query", "group_gather",
+            "voxel_downsample", "voxel_stats", "knn3_build", "knn3_query", "knn3_interp",
+            "noise_cond", "noise_mlp", "cfg_ddim_step", "pointwise_linear", "relu_bwd",
+            "linear_wgrad", "gemm_nt_bf16", "channel_stats", "affine_act", "chamfer_fwd",
+            "chamfer_bwd", "l1_fwd", "l1_bwd", "knn_dist", "emd_greedy", "voxel_center_dist",
+            "cfg_ddim_step_dcoef", "voxel_downsample_copies_dseed")
+for _name in _GUARDED:
+    globals()[_name] = _on_tensor_device(globals()[_name])
+del _name

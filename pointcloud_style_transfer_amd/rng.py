@@ -92,6 +92,43 @@ class ReplayRNG:
         return self.pos == len(self.draws)
 
 
+class CounterRNG:
+    """Counter-keyed draws for side-by-side runs (bench.py's "Chamfer vs ref" leg): the k-th
+    draw, whatever its kind, comes from numpy PCG64 seeded with (seed, k).  Two runs that make
+    their draws in the same order get the same values, and a permutation drawn for a different
+    length n (a voxel count that moved by a point) still comes from the same key.  Installed
+    with `replay(...)`, so the sampler takes its replay paths (host-drawn permutations)."""
+
+    replaying = True
+
+    def __init__(self, seed: int):
+        self.seed = int(seed)
+        self.k = 0
+
+    def generator(self) -> np.random.Generator:
+        g = np.random.default_rng([self.seed, self.k])
+        self.k += 1
+        return g
+
+    def randint(self, low, high, size, device=None):
+        return torch.from_numpy(self.generator().integers(low, high, size, dtype=np.int64)).to(device)
+
+    def randperm(self, n, device=None):
+        return torch.from_numpy(self.generator().permutation(int(n)).astype(np.int64)).to(device)
+
+    def randn(self, shape, device=None):
+        return torch.from_numpy(self.generator().standard_normal(shape, dtype=np.float32)).to(device)
+
+    def rand(self, shape, device=None):
+        return torch.from_numpy(self.generator().random(shape, dtype=np.float32)).to(device)
+
+    def randn_like(self, x):
+        return self.randn(tuple(x.shape), x.device)
+
+    def device_seed(self):
+        return 0
+
+
 _source = TorchRNG()
 
 
@@ -103,7 +140,8 @@ def source():
 def replay(draws_or_rng):
     global _source
     prev = _source
-    _source = draws_or_rng if isinstance(draws_or_rng, ReplayRNG) else ReplayRNG(draws_or_rng)
+    _source = (draws_or_rng if isinstance(draws_or_rng, (ReplayRNG, CounterRNG))
+               else ReplayRNG(draws_or_rng))
     try:
         yield _source
     finally:

@@ -5,7 +5,9 @@ Differences from the reference, all deliberate:
   * the checkpoint is read with `utils.checkpoint.safe_load` (weights_only=True with the
     pickled `config.config.Config` allow-listed) -- never an unpickling load;
   * there is no CPU fallback: the compute path is the HIP library, so a machine without a
-    GPU raises instead of silently switching device (the reference falls back at `:65`).
+    GPU, or `--device cpu`, raises instead of silently switching device (the reference
+    falls back to the CPU at `:65`; BASELINE configs[0] is that CPU plumbing run, which this
+    build serves on the GPU instead).
 Kept quirks: EMA weights are copied into the trainable parameters only and the BN buffers
 stay at their init values (Q9, `:98-113`); `.txt` delimiters differ for source (',') and
 reference (' ') (`:151-152`).
@@ -64,9 +66,13 @@ class DiffusionInference:
     """`DiffusionInference` (inference.py:62-171)."""
 
     def __init__(self, checkpoint_path: str, device: str = "cuda"):
+        dev = torch.device(device)
+        if dev.type != "cuda":
+            raise RuntimeError(f"DiffusionInference runs on the MI355X HIP path only; device "
+                               f"{device!r} is not supported (use 'cuda' or 'cuda:N')")
         if not torch.cuda.is_available():
             raise RuntimeError("DiffusionInference runs on the MI355X HIP path; no GPU is visible")
-        self.device = torch.device(device if device.startswith("cuda") else "cuda")
+        self.device = dev
         parts = os.path.normpath(checkpoint_path).split(os.sep)
         experiment_name = parts[-2] if len(parts) >= 2 else "default_inference"
         self.logger = Logger(name="Inference", log_dir="logs/inference",

@@ -9,12 +9,24 @@ the model is wrapped in DistributedDataParallel (RCCL all-reduce of the fp32 gra
 xGMI, overlapped with backward); BN statistics stay rank-local as in the reference (no
 SyncBN); clip/AdamW/EMA run replicated after the all-reduce, so ranks stay identical.
 
-Differences kept deliberately: the custom kernels compute in fp32 under `use_amp` (autocast
-does not lower them), so the step is at least as precise as the reference's fp16 autocast;
-the GradScaler logic is kept as is.  TensorBoard is optional (not installed here).
+Under DDP: micro-steps that do not end an accumulation window run under `no_sync()`, so the
+gradient all-reduce happens once per optimizer step (the summed micro-batch gradients equal the
+reference's accumulation over the same samples, trainer.py:115-125); ranks > 0 re-seed the
+torch generators with `initial_seed() + rank`, so each rank draws its own t, noise, dropout
+and voxel subsets; the EMA is built after the DDP wrap, from rank 0's broadcast weights; the
+validation loss is averaged over ranks before the best/patience decision, so every rank stops
+at the same epoch; the train sampler's epoch is set every epoch.
+
+Precision under `use_amp` (the reference's default): the per-point linear layers run on bf16
+MFMA with fp32 accumulation (models/_autograd.py -> pcst_gemm_nt_bf16 /
+pcst_linear_wgrad_bf16).  That keeps 8 mantissa bits per operand against the 11 of the
+reference's fp16 autocast, with fp32's exponent range; geometry, BN statistics, Chamfer and L1
+stay fp32.  `use_amp=False` runs every product in exact f32 (the gradient parity tests).
+The GradScaler logic is kept as is.  TensorBoard is optional (not installed here).
 """
 from __future__ import annotations
 
+import contextlib
 import math
 import os
 
@@ -100,7 +112,6 @@ class DiffusionTrainer:
             self.scheduler = optim.lr_scheduler.CosineAnnealingLR(
                 self.optimizer, T_max=config.num_epochs, eta_min=config.learning_rate * 0.01)
         self.scaler = GradScaler(enabled=(config.use_amp and self.device_type == "cuda"))
-        self.ema = ExponentialMovingAverage(self.model.parameters(), decay=config.ema_decay)
         self.writer = SummaryWriter(log_dir=os.path.join(config.log_dir, config.experiment_name))
         self.checkpoint_manager = CheckpointManager(config.checkpoint_dir, config.experiment_name)
         self.best_val_loss = float("inf")
@@ -115,10 +126,35 @@ class DiffusionTrainer:
 
             self.ddp_model = DDP(self.model, device_ids=[self.device.index] if self.device.index is not None else None,
                                  broadcast_buffers=False, bucket_cap_mb=16)
+            # every rank draws its own t / noise / dropout / voxel subsets
+            if self.rank > 0:
+                torch.manual_seed(torch.initial_seed() + self.rank)
+        # after the wrap: DDP has broadcast rank 0's weights, so every rank's shadows agree
+        self.ema = ExponentialMovingAverage(self.model.parameters(), decay=config.ema_decay)
 
     # ------------------------------------------------------------------ one step
+    def _is_sync_step(self, batch_idx: int, num_batches: int) -> bool:
+        return ((batch_idx + 1) % self.gradient_accumulation_steps == 0
+                or batch_idx == num_batches - 1)
+
     def train_step(self, batch, batch_idx: int, num_batches: int):
         """Body of the per-batch loop of train_one_epoch (trainer.py:70-127)."""
+        sync = self._is_sync_step(batch_idx, num_batches)
+        # DDP: all-reduce only on the micro-step that ends the accumulation window
+        ctx = (self.ddp_model.no_sync() if self.distributed and not sync
+               else contextlib.nullcontext())
+        with ctx:
+            loss, loss_dict = self._forward_backward(batch)
+        if sync:
+            self.scaler.unscale_(self.optimizer)
+            torch.nn.utils.clip_grad_norm_(self.model.parameters(), self.gradient_clip_norm)
+            self.scaler.step(self.optimizer)
+            self.scaler.update()
+            self.optimizer.zero_grad()
+            self.ema.update()
+        return loss, loss_dict
+
+    def _forward_backward(self, batch):
         sim = batch["sim_full"].to(self.device)
         real = batch["real_full"].to(self.device)
         B, N, C = sim.shape
@@ -146,13 +182,6 @@ class DiffusionTrainer:
                 loss, loss_dict = self.loss_fn(predicted_noise=pred, actual_noise=actual_noise)
             loss = loss / self.gradient_accumulation_steps
         self.scaler.scale(loss).backward()
-        if (batch_idx + 1) % self.gradient_accumulation_steps == 0 or batch_idx == num_batches - 1:
-            self.scaler.unscale_(self.optimizer)
-            torch.nn.utils.clip_grad_norm_(self.model.parameters(), self.gradient_clip_norm)
-            self.scaler.step(self.optimizer)
-            self.scaler.update()
-            self.optimizer.zero_grad()
-            self.ema.update()
         return loss, loss_dict
 
     def train_one_epoch(self, data_loader):
@@ -181,23 +210,34 @@ class DiffusionTrainer:
             self.model.eval()
             total = 0.0
             for batch in _progress(data_loader, f"Epoch {self.current_epoch} [Val]"):
-                sim = batch["sim_full"].to(self.device)
-                real = batch["real_full"].to(self.device)
-                B, N, C = sim.shape
-                t = _rng.source().randint(0, self.config.num_timesteps, (B,), device=self.device).long()
-                noisy, actual = self.diffusion_process.q_sample(sim, t)
-                pred, idx = self.model(noisy_points=noisy, timestep=t, condition_points=real,
-                                       cond_drop_prob=0, use_hierarchical=self.config.use_hierarchical)
-                if idx is not None:
-                    actual = torch.gather(actual, 1, idx.unsqueeze(-1).expand(-1, -1, C))
-                loss, _ = self.loss_fn(pred, actual)
-                if torch.isfinite(loss):
-                    total += loss.item()
+                loss = self._val_loss(batch)
+                if math.isfinite(loss):
+                    total += loss
             avg = total / len(data_loader)
+            if self.distributed:
+                # one decision for every rank (best / patience / stop), else a rank that
+                # breaks early leaves the others hanging in the gradient all-reduce
+                t = torch.tensor([avg], dtype=torch.float64, device=self.device)
+                dist.all_reduce(t, op=dist.ReduceOp.SUM)
+                avg = float(t.item()) / dist.get_world_size()
             self.writer.add_scalar("Loss/Validation", avg, self.current_epoch)
             return avg
         finally:
             self.ema.restore()
+
+    def _val_loss(self, batch) -> float:
+        """Noise loss of one validation batch (trainer.py:150-166)."""
+        sim = batch["sim_full"].to(self.device)
+        real = batch["real_full"].to(self.device)
+        B, N, C = sim.shape
+        t = _rng.source().randint(0, self.config.num_timesteps, (B,), device=self.device).long()
+        noisy, actual = self.diffusion_process.q_sample(sim, t)
+        pred, idx = self.model(noisy_points=noisy, timestep=t, condition_points=real,
+                               cond_drop_prob=0, use_hierarchical=self.config.use_hierarchical)
+        if idx is not None:
+            actual = torch.gather(actual, 1, idx.unsqueeze(-1).expand(-1, -1, C))
+        loss, _ = self.loss_fn(pred, actual)
+        return float(loss.item())
 
     def save_sample_results(self, data_loader, num_samples: int = 2):
         """trainer.py:176-196."""
@@ -229,6 +269,9 @@ class DiffusionTrainer:
                 self.scheduler.step()
         for epoch in range(self.current_epoch, self.config.num_epochs):
             self.current_epoch = epoch
+            sampler = getattr(train_loader, "sampler", None)
+            if hasattr(sampler, "set_epoch"):  # DistributedSampler: a new shuffle every epoch
+                sampler.set_epoch(epoch)
             avg = self.train_one_epoch(train_loader)
             self.logger.info(f"Epoch {epoch}: train loss {avg:.6f}")
             if hasattr(self.scheduler, "step"):

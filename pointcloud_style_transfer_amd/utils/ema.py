@@ -36,16 +36,18 @@ class ExponentialMovingAverage:
         if not self.shadow_params:
             return
         with torch.no_grad():
-            self.collected_params = [p.data.clone() for p in self._trainable()]
+            self.collected_params = [p.detach().clone() for p in self._trainable()]
+            # p.copy_ (not p.data.copy_) bumps the parameter's version counter, so weight
+            # caches keyed on it (NoisePredictor.packed) see the swap
             for p, s in zip(self._trainable(), self.shadow_params):
-                p.data.copy_(s)
+                p.copy_(s)
 
     def restore(self):
         if not self.collected_params:
             return
         with torch.no_grad():
             for p, c in zip(self._trainable(), self.collected_params):
-                p.data.copy_(c)
+                p.copy_(c)
         self.collected_params = []
 
     def state_dict(self) -> dict:

@@ -1,0 +1,72 @@
+"""Worker of tests/test_gpu_ddp.py (not a test module): one DiffusionTrainer process.
+
+    python tests/ddp_worker.py OUT.npz ACCUM MICRO_BATCHES_PER_RANK CLOUDS_PER_MICRO POINTS
+
+Under torch.distributed (RANK / WORLD_SIZE in the environment, gloo backend, every rank on
+cuda:0) the trainer wraps the model in DDP; without it the same code is the single-process
+reference.  Global micro-batch g (rank r, local step b: g = r * MICRO + b) trains on clouds
+[g * CLOUDS, (g + 1) * CLOUDS) with the draws of rng.CounterRNG(100 + g), so both set-ups see
+the same samples and the same t / noise / cond-drop / voxel / FPS draws.  The gradient each
+optimizer step applies (after clipping) and the parameters after the step are saved.
+"""
+import os
+import sys
+
+import numpy as np
+import torch
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+
+
+def main():
+    out, accum, micro, clouds, points = sys.argv[1], *map(int, sys.argv[2:6])
+    from pointcloud_style_transfer_amd import distributed as D
+    from pointcloud_style_transfer_amd import rng
+    from pointcloud_style_transfer_amd.config.config import Config
+    from pointcloud_style_transfer_amd.synthetic import lidar_like_cloud
+    from pointcloud_style_transfer_amd.training.trainer import DiffusionTrainer
+
+    world, rank, _ = D.init_from_env("gloo")
+    torch.cuda.set_device(0)
+    tmp = os.path.dirname(os.path.abspath(out))
+    os.chdir(tmp)
+    cfg = Config(make_dirs=False, log_dir=tmp, checkpoint_dir=tmp, use_amp=False,
+                 gradient_accumulation_steps=accum, global_points=2048, precision="fp32")
+    torch.manual_seed(0)
+    tr = DiffusionTrainer(cfg, device="cuda:0")
+    assert tr.distributed == (world > 1)
+    for m in tr.model.modules():
+        if isinstance(m, torch.nn.Dropout):
+            m.p = 0.0
+    tr.model.train()
+    grads = {}
+    o_step = tr.optimizer.step
+
+    def step(*a, **k):
+        for n, p in tr.model.named_parameters():
+            grads[n] = p.grad.detach().cpu().numpy().copy()
+        return o_step(*a, **k)
+
+    tr.optimizer.step = step
+    losses = []
+    for b in range(micro):
+        g = rank * micro + b
+        ids = range(g * clouds, (g + 1) * clouds)
+        sim = torch.from_numpy(np.stack([lidar_like_cloud(1000 + i, points) for i in ids]))
+        real = torch.from_numpy(np.stack([lidar_like_cloud(2000 + i, points) for i in ids]))
+        with rng.replay(rng.CounterRNG(100 + g)):
+            loss, _ = tr.train_step({"sim_full": sim.cuda(), "real_full": real.cuda()}, b, micro)
+        losses.append(float(loss.detach()))
+    torch.cuda.synchronize()
+    if rank == 0:
+        params = {f"param:{n}": p.detach().cpu().numpy() for n, p in tr.model.named_parameters()}
+        np.savez(out, losses=np.array(losses), **{f"grad:{k}": v for k, v in grads.items()},
+                 **params)
+    if world > 1:
+        torch.distributed.barrier()
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -569,6 +569,20 @@ def gen_trainer_sketch():
     save("trainer_sketch.npz", **out)
 
 
+def gen_ddim_hierarchical():
+    """ddim_sample_loop's hierarchical branch (diffusion_model.py:278-280): N=4096 > global
+    1024, 3 steps, eval mode; model.forward re-encodes the style every step."""
+    cfg = Config(total_points=4096, global_points=1024)
+    m = make_model(cfg).eval()
+    dp = ref_dm.DiffusionProcess(cfg, device="cpu")
+    cond = lidar_like_cloud(2003, 4096)[None]
+    with RNGRecorder() as rec:
+        x = dp.ddim_sample_loop(m, (1, 4096, 3), t32(cond), num_inference_steps=3)
+    out = {"cond": cond, "out": x.numpy()}
+    out.update(rec.pack("rng"))
+    save("ddim_hier.npz", **out)
+
+
 def gen_inference_cfg1():
     """BASELINE config 1: scripts/inference.py on CPU, 2048x3 .npy, 10 steps."""
     from utils.checkpoint import CheckpointManager
@@ -602,7 +616,7 @@ if __name__ == "__main__":
     fns = {"geometry": gen_geometry, "encoder": gen_encoder, "noise": gen_noise_predictor,
            "hier": gen_hierarchical, "sched": gen_schedule_and_losses, "sampling": gen_sampling,
            "trainer": gen_trainer_and_checkpoint, "cfg1": gen_inference_cfg1,
-           "trainer_sketch": gen_trainer_sketch}
+           "trainer_sketch": gen_trainer_sketch, "ddim_hier": gen_ddim_hierarchical}
     for w in which:
         torch.manual_seed(0)
         fns[w]()

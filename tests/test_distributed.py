@@ -71,3 +71,74 @@ def test_shard_partition(n, world):
     flat = [i for p in parts for i in p]
     assert flat == list(range(n))
     assert max(map(len, parts)) - min(map(len, parts)) <= 1
+
+
+def _train_worker(rank, world, port, tmp, q):
+    """DiffusionTrainer.train() under a world-2 gloo group on the CPU with the per-batch work
+    stubbed out (the HIP kernels need the GPU): the validation losses differ per rank so a
+    rank-local best/patience decision would stop the ranks at different epochs."""
+    os.environ.update(RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(world),
+                      MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    from pointcloud_style_transfer_amd import distributed as D
+    from pointcloud_style_transfer_amd.config.config import Config
+    from pointcloud_style_transfer_amd.training import trainer as T
+
+    try:
+        os.chdir(tmp)  # CheckpointManager logs under ./logs, as the reference's does
+        D.init_from_env("gloo")
+        torch.manual_seed(0)
+        cfg = Config(make_dirs=False, log_dir=tmp, checkpoint_dir=os.path.join(tmp, f"ck{rank}"),
+                     num_epochs=12, val_interval=1, save_interval=1000)
+        tr = T.DiffusionTrainer(cfg, device="cpu")
+        tr.max_patience = 2
+        # alone, rank 0 would stop at epoch 10 (best at 8) and rank 1 at epoch 2 (best at 0);
+        # the rank average is best at epoch 5 (1.23) and stops at epoch 7
+        curves = {0: [5, 4, 3, 2, 1, 0.5, 0.6, 0.4, 0.3, 0.7, 0.8, 0.9],
+                  1: [1, 1.5, 1.8, 1.9, 1.95, 1.96, 4, 4, 4, 4, 4, 4]}
+        val_calls = []
+
+        def val_loss(self, batch):
+            e = self.current_epoch
+            val_calls.append(e)
+            return float(curves[rank][e])
+
+        epochs = []
+        T.DiffusionTrainer._val_loss = val_loss
+        T.DiffusionTrainer.train_one_epoch = lambda self, dl: epochs.append(self.current_epoch) or 0.0
+
+        class Sampler:
+            seen = []
+
+            def set_epoch(self, e):
+                self.seen.append(e)
+
+        class Loader(list):
+            sampler = Sampler()
+
+        tr.train(Loader([None]), [None])
+        # EMA shadows were built after the DDP wrap: identical on both ranks
+        shadow = [s.sum().item() for s in tr.ema.shadow_params[:4]]
+        q.put({"rank": rank, "epochs": epochs, "best": tr.best_val_loss,
+               "set_epoch": Loader.sampler.seen, "shadow": shadow,
+               "seed": torch.initial_seed()})
+    finally:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+def test_world2_trainer_shared_early_stop(tmp_path):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_train_worker, args=(r, 2, port, str(tmp_path), q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = sorted([q.get(timeout=180) for _ in ps], key=lambda d: d["rank"])
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert res[0]["epochs"] == res[1]["epochs"] == list(range(8))
+    assert res[0]["best"] == res[1]["best"] == (0.5 + 1.96) / 2
+    assert res[0]["set_epoch"] == res[1]["set_epoch"] == list(range(8))
+    assert res[0]["shadow"] == res[1]["shadow"]
+    assert res[0]["seed"] != res[1]["seed"]  # per-rank draws

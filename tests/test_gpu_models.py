@@ -179,3 +179,19 @@ def test_chamfer_determinism(mods):
         L.chamfer_distance_chunked_optimized(p, dev(b)).sum().backward()
         grads.append(p.grad.cpu().numpy())
     np.testing.assert_array_equal(grads[0], grads[1])
+
+
+def test_ddim_loop_hierarchical(mods, golden):
+    """ddim_sample_loop's hierarchical branch (diffusion_model.py:278-280): N=4096 > global
+    1024, 3 steps; model.forward re-encodes the style from a fresh downsample every step, and
+    the coarse noise is upsampled with kNN-3.  Reference draws replayed (tests/golden/
+    ddim_hier.npz, gen_golden.py ddim_hier)."""
+    g = golden("ddim_hier.npz")
+    c, m = make_model(mods, total_points=4096, global_points=1024)
+    m.eval()
+    dp = mods["dm"].DiffusionProcess(c, device="cuda")
+    rp = mods["rng"].ReplayRNG.from_npz(g, "rng")
+    with mods["rng"].replay(rp):
+        out = dp.ddim_sample_loop(m, (1, 4096, 3), dev(g["cond"]), 3)
+    assert rp.exhausted
+    assert_mostly_close(out.cpu().numpy(), g["out"])

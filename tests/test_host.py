@@ -172,3 +172,95 @@ def test_inference_requires_gpu():
 
     with pytest.raises(RuntimeError, match="HIP"):
         DiffusionInference("nonexistent.pth", "cuda")
+
+
+@pytest.mark.parametrize("device", ["cpu", "meta"])
+def test_inference_rejects_non_hip_device(device):
+    """`--device cpu` raises (the reference falls back to the CPU at inference.py:65; this build
+    has no CPU path) -- on any machine, with or without a GPU."""
+    from pointcloud_style_transfer_amd.scripts.inference import DiffusionInference
+
+    with pytest.raises(RuntimeError, match="HIP path only"):
+        DiffusionInference("nonexistent.pth", device)
+
+
+def test_ema_swap_bumps_parameter_versions():
+    """apply_shadow / restore must be visible to caches keyed on the parameter's version
+    (NoisePredictor.packed): a p.data.copy_ would not bump it."""
+    from pointcloud_style_transfer_amd.utils.ema import ExponentialMovingAverage
+
+    lin = torch.nn.Linear(4, 3)
+    ema = ExponentialMovingAverage(lin.parameters(), decay=0.5)
+    with torch.no_grad():
+        lin.weight.add_(1.0)
+    ema.update()
+    v0 = lin.weight._version
+    w_raw = lin.weight.detach().clone()
+    ema.apply_shadow()
+    assert lin.weight._version > v0
+    assert not torch.equal(lin.weight, w_raw)
+    v1 = lin.weight._version
+    ema.restore()
+    assert lin.weight._version > v1
+    assert torch.equal(lin.weight, w_raw)
+
+
+def test_noise_predictor_pack_follows_ema_swap():
+    """The packed weight stream is rebuilt after apply_shadow and after restore (the pack key
+    is (data_ptr, _version) of every parameter)."""
+    from pointcloud_style_transfer_amd.config.config import Config
+    from pointcloud_style_transfer_amd.models.diffusion_model import NoisePredictor
+    from pointcloud_style_transfer_amd.utils.ema import ExponentialMovingAverage
+
+    npred = NoisePredictor(Config(make_dirs=False))
+    ema = ExponentialMovingAverage(npred.parameters(), decay=0.5)
+    key = lambda: tuple((p.data_ptr(), p._version) for p in npred.parameters())  # noqa: E731
+    k0 = key()
+    with torch.no_grad():
+        for p in npred.parameters():
+            p.mul_(0.5)
+    ema.update()
+    k1 = key()
+    ema.apply_shadow()
+    k2 = key()
+    ema.restore()
+    k3 = key()
+    assert len({k0, k1, k2, k3}) == 4
+
+
+def test_hip_wrappers_run_on_the_tensors_device(monkeypatch):
+    """Every public ctypes wrapper is device-guarded, and the guard makes the tensors' device
+    current when the caller's current device differs (a model on cuda:1 without
+    torch.cuda.set_device must not launch on cuda:0)."""
+    import inspect
+    import types
+
+    from pointcloud_style_transfer_amd import _hip
+
+    calling = [n for n, f in vars(_hip).items() if inspect.isfunction(f) and not n.startswith("_")
+               and "_call(" in inspect.getsource(f)]
+    assert calling and all(getattr(getattr(_hip, n), "device_guarded", False) for n in calling), \
+        [n for n in calling if not getattr(getattr(_hip, n), "device_guarded", False)]
+
+    entered = []
+
+    class FakeDev:
+        def __init__(self, idx):
+            self.idx = idx
+
+        def __enter__(self):
+            entered.append(self.idx)
+
+        def __exit__(self, *a):
+            return False
+
+    monkeypatch.setattr(_hip.torch.cuda, "current_device", lambda: 0)
+    monkeypatch.setattr(_hip.torch.cuda, "device", FakeDev)
+    seen = []
+    f = _hip._on_tensor_device(lambda *a, **k: seen.append(a) or "ok")
+    t1 = types.SimpleNamespace(is_cuda=True, device=types.SimpleNamespace(index=1))
+    t0 = types.SimpleNamespace(is_cuda=True, device=types.SimpleNamespace(index=0))
+    assert f(3.0, t1) == "ok" and entered == [1]
+    assert f(t0) == "ok" and entered == [1]          # already current: no switch
+    assert f((t1, None)) == "ok" and entered == [1, 1]  # tuple handle (knn3_query)
+    assert f(torch.zeros(2)) == "ok" and entered == [1, 1]  # CPU tensor: no switch
