@@ -326,15 +326,19 @@ __global__ void vox_select_kernel(const float* __restrict__ pts, int N, int64_t 
 }
 
 // ============================================================================================
-// Performance path (device-drawn subset).  The step's result does not depend on the ORDER of
-// the kept indices (the noise MLP is per point and the upsample addresses rows by index), so
-// the sorts of the replay path are replaced by:
+// Performance path (device-drawn subset).  The sorts of the replay path are replaced by:
 //   open-addressing voxel table (int64 index sums / counts by integer atomics: exact)
 //   -> representatives (same values as the sorted path, arbitrary list order)
 //   -> random subset of the candidates (reps if U > T, pool if U < T) = the `need` smallest
 //      counter-based random keys (key of a rep = f(seed, voxel hash), of a pool point =
 //      f(seed, index): independent of list order, hence deterministic), found by a 12-bit
-//      radix select plus an exact sort of the boundary bin.
+//      radix select plus an exact sort of the boundary bin;
+//   -> every kept point is MARKED (a per-row count over the point index: a representative
+//      index two voxels share is kept twice, as the reference keeps it) and the emit kernel
+//      writes the row in ascending point-index order by a tile prefix over the counts.
+// The kept multiset is fixed by the seed, and so is the row order: the result does not
+// depend on the arrival order of any atomic (the style encoder's FPS start and ball query
+// read positions in this list, so the order matters there).
 constexpr int kSelBins = 4096;
 constexpr int kTieCap = 8192;
 #ifndef VOX_CHUNK  // experiment builds may override
@@ -366,9 +370,14 @@ struct VoxelFastWS {
   unsigned long long* tsum;  // [B][H]
   uint32_t* tcnt;         // [B][H]
   uint32_t* isrep;        // [B][N]
-  int64_t H;
+  uint32_t* kcnt;         // [R][N]    times point n is kept in row r
+  uint32_t* ktile;        // [R][tiles] per-tile sums of kcnt (kEmitTile indices per tile)
+  int64_t H, tiles;
   size_t bytes;
 };
+
+constexpr int kEmitTile = 4096;   // 256 threads x 16 indices
+constexpr int kMarkTiles = 1024;  // tiles counted in LDS by the marking kernels
 
 static int64_t vox_table_size(int64_t N) {
   int64_t h = 1024;
@@ -392,6 +401,9 @@ static VoxelFastWS carve_voxel_fast(void* base, int64_t B, int64_t N, int64_t co
   w.tsum = c.take<unsigned long long>(B * w.H);
   w.tcnt = c.take<uint32_t>(B * w.H);
   w.isrep = c.take<uint32_t>(B * N);
+  w.tiles = cdiv(N, kEmitTile);
+  w.kcnt = c.take<uint32_t>(R * N);
+  w.ktile = c.take<uint32_t>(R * w.tiles);
   w.bytes = c.bytes();
   return w;
 }
@@ -475,15 +487,12 @@ __global__ __launch_bounds__(256) void voxf_insert_kernel(const float* __restric
   }
 }
 
-// occupied slot -> representative trunc(f32(sum)/f32(count)) (Q6); list order = arrival order.
-// When U <= T every rep is kept: rep k is written (index and point) to position k of every
-// copy row here.
+// occupied slot -> representative trunc(f32(sum)/f32(count)) (Q6); list order = arrival order
+// (only the SET matters downstream: rows are emitted in point-index order).
 __global__ __launch_bounds__(256) void voxf_reps_kernel(
-    const float* __restrict__ pts, const unsigned long long* __restrict__ tkey,
-    const unsigned long long* __restrict__ tsum, const uint32_t* __restrict__ tcnt, int64_t H,
-    int N, int64_t T, int B, int copies, int32_t* __restrict__ cnt4, int64_t* __restrict__ reps,
-    uint32_t* __restrict__ rhash, uint32_t* __restrict__ isrep, int64_t* __restrict__ out_idx,
-    float* __restrict__ out_pts) {
+    const unsigned long long* __restrict__ tkey, const unsigned long long* __restrict__ tsum,
+    const uint32_t* __restrict__ tcnt, int64_t H, int N, int32_t* __restrict__ cnt4,
+    int64_t* __restrict__ reps, uint32_t* __restrict__ rhash, uint32_t* __restrict__ isrep) {
   // one contiguous slot range per workgroup, one counter atomic per workgroup
   const int b = blockIdx.y;
   const int64_t chunk = (H + gridDim.x - 1) / gridDim.x;
@@ -507,16 +516,6 @@ __global__ __launch_bounds__(256) void voxf_reps_kernel(
     reps[(int64_t)b * N + k] = r;
     rhash[(int64_t)b * N + k] = (uint32_t)kw;
     isrep[(int64_t)b * N + r] = 1u;
-    if (k < T) {
-      const float* src = pts + ((int64_t)b * N + r) * 3;
-      const float x = src[0], y = src[1], z = src[2];
-      for (int c = 0; c < copies; ++c) {
-        const int64_t row = (int64_t)c * B + b;
-        out_idx[row * T + k] = r;
-        float* d = out_pts + (row * T + k) * 3;
-        d[0] = x; d[1] = y; d[2] = z;
-      }
-    }
     ++k;
   }
 }
@@ -560,37 +559,43 @@ __global__ __launch_bounds__(256) void voxf_hist_kernel(int N, int64_t T, int B,
     if (h[i]) atomicAdd(&hist[row * kSelBins + i], h[i]);
 }
 
-// kept candidate -> its output position (index and point)
-__device__ __forceinline__ void voxf_emit(int row, int cl, int N, int64_t T, int U, int pos,
-                                          uint32_t id, const int64_t* __restrict__ reps,
-                                          const float* __restrict__ pts,
-                                          int64_t* __restrict__ out_idx,
-                                          float* __restrict__ out_pts) {
-  const int64_t r = U > T ? reps[(int64_t)cl * N + id] : (int64_t)id;
-  const int64_t j = U > T ? pos : U + pos;
-  out_idx[row * T + j] = r;
-  const float* src = pts + ((int64_t)cl * N + r) * 3;
-  float* d = out_pts + (row * T + j) * 3;
-  d[0] = src[0]; d[1] = src[1]; d[2] = src[2];
+// kept candidate -> one more keep of its point index in this row (index n = the rep's index if
+// U > T, else the pool index itself); tile sums in LDS (lt) when the tile is < kMarkTiles
+__device__ __forceinline__ void voxf_mark(int row, int N, int64_t n, uint32_t* __restrict__ kcnt,
+                                          uint32_t* __restrict__ ktile, int64_t tiles,
+                                          uint32_t* lt) {
+  atomicAdd(&kcnt[(int64_t)row * N + n], 1u);
+  const int64_t tl = n / kEmitTile;
+  if (tl < kMarkTiles) atomicAdd(&lt[tl], 1u);
+  else atomicAdd(&ktile[row * tiles + tl], 1u);
+}
+
+__device__ __forceinline__ void voxf_flush_tiles(int row, int64_t tiles, const uint32_t* lt,
+                                                 uint32_t* __restrict__ ktile) {
+  __syncthreads();
+  const int nt = (int)(tiles < kMarkTiles ? tiles : kMarkTiles);
+  for (int i = threadIdx.x; i < nt; i += blockDim.x)
+    if (lt[i]) atomicAdd(&ktile[row * tiles + i], lt[i]);
 }
 
 // Every workgroup first finds the row's boundary bin b* (the bin holding the need-th smallest
-// key) from the histogram; workgroup 0 records it for the ties kernel.  Then: keys below b*
-// are kept (one contiguous candidate range per workgroup, two counter atomics per workgroup),
-// keys in b* go to the tie list.
+// key) from the histogram; workgroup 0 records it for the ties kernel.  Then, over one
+// contiguous candidate range per workgroup: U <= T keeps every representative; keys below b*
+// are kept, keys in b* go to the tie list (its order is irrelevant: the ties kernel ranks).
 __global__ __launch_bounds__(256) void voxf_select_kernel(
-    const float* __restrict__ pts, int N, int64_t T, int B, uint64_t seed_v,
-    const uint64_t* __restrict__ seed_p,
+    int N, int64_t T, int B, uint64_t seed_v, const uint64_t* __restrict__ seed_p,
     const uint32_t* __restrict__ hist, int32_t* __restrict__ sel, int32_t* __restrict__ cnt4,
     const uint32_t* __restrict__ rhash, const uint32_t* __restrict__ isrep,
     const int64_t* __restrict__ reps, unsigned long long* __restrict__ ties,
-    int64_t* __restrict__ out_idx, float* __restrict__ out_pts) {
+    uint32_t* __restrict__ kcnt, uint32_t* __restrict__ ktile, int64_t tiles) {
   const uint64_t seed = seed_p ? *seed_p : seed_v;
   const int row = blockIdx.y, cl = row % B;
   const int U = cnt4[cl * 4];
   const int need = U > T ? (int)T : (U < T ? (int)(T - U) : 0);
   __shared__ uint32_t sh[260];
+  __shared__ uint32_t lt[kMarkTiles];
   __shared__ int s_bstar, s_rem;
+  for (int i = threadIdx.x; i < kMarkTiles; i += 256) lt[i] = 0u;
   {
     constexpr int per = kSelBins / 256;
     uint32_t v[per], s = 0;
@@ -619,86 +624,122 @@ __global__ __launch_bounds__(256) void voxf_select_kernel(
     sel[row * 4 + 2] = need;
     sel[row * 4 + 3] = U > T ? 1 : 0;
   }
-  if (bstar < 0) return;
   const int chunk = (N + gridDim.x - 1) / gridDim.x;
   const int e0 = blockIdx.x * chunk, e1 = min(e0 + chunk, N);
-  uint32_t nlo = 0, nti = 0;
-  for (int e = e0 + threadIdx.x; e < e1; e += 256) {
-    uint32_t key, id;
-    if (!voxf_cand(row, cl, e, N, U, T, seed, rhash, isrep, key, id)) continue;
-    const int bin = (int)(key >> 20);
-    nlo += bin < bstar;
-    nti += bin == bstar;
+  const int64_t* R = reps + (int64_t)cl * N;
+  if (U <= T) {  // every representative entry is kept (a shared index twice)
+    for (int e = e0 + threadIdx.x; e < min(e1, U); e += 256)
+      voxf_mark(row, N, R[e], kcnt, ktile, tiles, lt);
   }
-  __shared__ int base_lo, base_ti;
-  uint32_t tlo, tti;
-  const uint32_t olo = block_excl_scan_256(nlo, sh, tlo);
-  const uint32_t oti = block_excl_scan_256(nti, sh, tti);
-  if (threadIdx.x == 0) {
-    base_lo = tlo ? atomicAdd(&cnt4[row * 4 + 1], (int)tlo) : 0;
-    base_ti = tti ? atomicAdd(&cnt4[row * 4 + 2], (int)tti) : 0;
-  }
-  __syncthreads();
-  int plo = base_lo + (int)olo, pti = base_ti + (int)oti;
-  for (int e = e0 + threadIdx.x; e < e1; e += 256) {
-    uint32_t key, id;
-    if (!voxf_cand(row, cl, e, N, U, T, seed, rhash, isrep, key, id)) continue;
-    const int bin = (int)(key >> 20);
-    if (bin < bstar) {
-      voxf_emit(row, cl, N, T, U, plo++, id, reps, pts, out_idx, out_pts);
-    } else if (bin == bstar) {
-      if (pti < kTieCap) ties[(int64_t)row * kTieCap + pti] = ((unsigned long long)key << 32) | id;
-      else atomicOr(&cnt4[row * 4 + 3], 1);
-      ++pti;
+  if (bstar >= 0) {
+    for (int e = e0 + threadIdx.x; e < e1; e += 256) {
+      uint32_t key, id;
+      if (!voxf_cand(row, cl, e, N, U, T, seed, rhash, isrep, key, id)) continue;
+      const int bin = (int)(key >> 20);
+      if (bin < bstar) {
+        voxf_mark(row, N, U > T ? R[id] : (int64_t)id, kcnt, ktile, tiles, lt);
+      } else if (bin == bstar) {
+        const int pti = atomicAdd(&cnt4[row * 4 + 2], 1);
+        if (pti < kTieCap) ties[(int64_t)row * kTieCap + pti] = ((unsigned long long)key << 32) | id;
+        else atomicOr(&cnt4[row * 4 + 3], 1);
+      }
     }
   }
+  voxf_flush_tiles(row, tiles, lt, ktile);
 }
 
 // boundary bin: exact order by (key, id), keep the first `rem` (one workgroup per row)
-__global__ __launch_bounds__(1024) void voxf_ties_kernel(const float* __restrict__ pts, int N,
-                                                         int64_t T, int B,
+__global__ __launch_bounds__(1024) void voxf_ties_kernel(int N, int64_t T, int B,
                                                          const int32_t* __restrict__ sel,
                                                          const int32_t* __restrict__ cnt4,
                                                          const unsigned long long* __restrict__ ties,
                                                          const int64_t* __restrict__ reps,
-                                                         int64_t* __restrict__ out_idx,
-                                                         float* __restrict__ out_pts) {
+                                                         uint32_t* __restrict__ kcnt,
+                                                         uint32_t* __restrict__ ktile,
+                                                         int64_t tiles) {
   const int row = blockIdx.x, cl = row % B;
   if (sel[row * 4 + 0] < 0) return;
   const int rem = sel[row * 4 + 1];
   const int U = cnt4[cl * 4];
   const int nt = min(cnt4[row * 4 + 2], kTieCap);
-  const int base = cnt4[row * 4 + 1];  // entries below the boundary bin
   const unsigned long long* Tb = ties + (int64_t)row * kTieCap;
   for (int i = threadIdx.x; i < nt; i += 1024) {
     const unsigned long long v = Tb[i];
     int rank = 0;
     for (int k = 0; k < nt; ++k) rank += Tb[k] < v;
-    if (rank < rem) voxf_emit(row, cl, N, T, U, base + rank, (uint32_t)v, reps, pts, out_idx, out_pts);
+    if (rank < rem) {
+      const uint32_t id = (uint32_t)v;
+      const int64_t n = U > T ? reps[(int64_t)cl * N + id] : (int64_t)id;
+      atomicAdd(&kcnt[(int64_t)row * N + n], 1u);
+      atomicAdd(&ktile[row * tiles + n / kEmitTile], 1u);
+    }
   }
 }
 
-// stats (+ zeroing), insert (+ voxel parameters), reps (+ kept reps), hist, select (+ boundary
-// bin, kept points), ties (+ kept points): 6 launches.
+// Row emit in ascending point-index order: tile j's offset is the sum of the earlier tiles'
+// keep counts; inside the tile a block scan places each index kcnt[n] times (index + point).
+__global__ __launch_bounds__(256) void voxf_emit_kernel(const float* __restrict__ pts, int N,
+                                                        int64_t T, int B,
+                                                        const uint32_t* __restrict__ kcnt,
+                                                        const uint32_t* __restrict__ ktile,
+                                                        int64_t tiles, int32_t* __restrict__ cnt4,
+                                                        int64_t* __restrict__ out_idx,
+                                                        float* __restrict__ out_pts) {
+  constexpr int kPer = kEmitTile / 256;
+  const int row = blockIdx.y, cl = row % B;
+  const int64_t tile = blockIdx.x;
+  __shared__ uint32_t sh[260];
+  uint32_t before = 0;
+  for (int64_t i = threadIdx.x; i < tile; i += 256) before += ktile[row * tiles + i];
+  uint32_t tot0;
+  block_excl_scan_256(before, sh, tot0);  // tot0 = sum over the earlier tiles
+  const int64_t n0 = tile * kEmitTile + threadIdx.x * kPer;
+  const uint32_t* C = kcnt + (int64_t)row * N;
+  uint32_t c[kPer], s = 0;
+#pragma unroll
+  for (int k = 0; k < kPer; ++k) {
+    c[k] = n0 + k < N ? C[n0 + k] : 0u;
+    s += c[k];
+  }
+  uint32_t tot;
+  int64_t pos = (int64_t)tot0 + block_excl_scan_256(s, sh, tot);
+  const float* P = pts + (int64_t)cl * N * 3;
+#pragma unroll
+  for (int k = 0; k < kPer; ++k) {
+    for (uint32_t q = 0; q < c[k]; ++q, ++pos) {
+      if (pos >= T) { atomicOr(&cnt4[row * 4 + 3], 2); break; }
+      const int64_t n = n0 + k;
+      out_idx[row * T + pos] = n;
+      float* d = out_pts + (row * T + pos) * 3;
+      d[0] = P[n * 3 + 0]; d[1] = P[n * 3 + 1]; d[2] = P[n * 3 + 2];
+    }
+  }
+}
+
+// stats (+ zeroing), insert (+ voxel parameters), reps, hist, select (+ boundary bin, marks),
+// ties (+ marks), emit (rows in point-index order): 7 launches.
 static int voxel_fast(const float* pts, int64_t B, int64_t N, int64_t copies, int64_t T,
                       void* workspace, uint64_t seed, const uint64_t* seed_p, int64_t* out_idx,
                       float* out_pts, hipStream_t s) {
   VoxelFastWS w = carve_voxel_fast(workspace, B, N, copies);
   const int b = (int)B, n = (int)N, rows = (int)(B * copies);
-  const size_t zero = (size_t)((char*)(w.isrep + B * N) - (char*)w.cnt4);
+  const size_t zero = (size_t)((char*)(w.ktile + rows * w.tiles) - (char*)w.cnt4);
   hipLaunchKernelGGL(voxf_stats_zero_kernel, dim3(kStatBlocks + kVoxZeroBlocks, b), dim3(256), 0, s,
                      pts, n, w.mm, reinterpret_cast<uint4*>(w.cnt4), (int64_t)cdiv(zero, 16));
   hipLaunchKernelGGL(voxf_insert_kernel, dim3((unsigned)cdiv(N, kVoxChunk), b), dim3(256), 0, s,
                      pts, n, w.mm, T, w.H, w.tkey, w.tsum, w.tcnt);
-  hipLaunchKernelGGL(voxf_reps_kernel, dim3(kVoxRepsBlocks, b), dim3(256), 0, s, pts, w.tkey, w.tsum, w.tcnt,
-                     w.H, n, T, b, (int)copies, w.cnt4, w.reps, w.rhash, w.isrep, out_idx, out_pts);
+  hipLaunchKernelGGL(voxf_reps_kernel, dim3(kVoxRepsBlocks, b), dim3(256), 0, s, w.tkey, w.tsum,
+                     w.tcnt, w.H, n, w.cnt4, w.reps, w.rhash, w.isrep);
   const unsigned gs = (unsigned)std::min<int64_t>(cdiv(N, 256), 256);
   hipLaunchKernelGGL(voxf_hist_kernel, dim3(gs, rows), dim3(256), 0, s, n, T, b, seed, seed_p,
                      w.cnt4, w.rhash, w.isrep, w.hist);
-  hipLaunchKernelGGL(voxf_select_kernel, dim3(128, rows), dim3(256), 0, s, pts, n, T, b, seed,
-                     seed_p, w.hist, w.sel, w.cnt4, w.rhash, w.isrep, w.reps, w.ties, out_idx, out_pts);
-  hipLaunchKernelGGL(voxf_ties_kernel, dim3(rows), dim3(1024), 0, s, pts, n, T, b, w.sel, w.cnt4,
-                     w.ties, w.reps, out_idx, out_pts);
+  hipLaunchKernelGGL(voxf_select_kernel, dim3(128, rows), dim3(256), 0, s, n, T, b, seed, seed_p,
+                     w.hist, w.sel, w.cnt4, w.rhash, w.isrep, w.reps, w.ties, w.kcnt, w.ktile,
+                     w.tiles);
+  hipLaunchKernelGGL(voxf_ties_kernel, dim3(rows), dim3(1024), 0, s, n, T, b, w.sel, w.cnt4,
+                     w.ties, w.reps, w.kcnt, w.ktile, w.tiles);
+  hipLaunchKernelGGL(voxf_emit_kernel, dim3((unsigned)w.tiles, rows), dim3(256), 0, s, pts, n, T,
+                     b, w.kcnt, w.ktile, w.tiles, w.cnt4, out_idx, out_pts);
   PCST_LAUNCH_CHECK("voxel_downsample");
   return PCST_OK;
 }
