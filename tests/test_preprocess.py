@@ -104,3 +104,179 @@ def test_save_hierarchical_file_loads(tmp_path):
     assert np.abs(item["sim_full"].numpy()).max() == pytest.approx(1.8, rel=1e-6)
     assert np.array_equal(item["sim_global"].numpy(),
                           item["sim_full"].numpy()[item["sim_global_indices"].numpy()])
+
+
+# ---------------------------------------------------------------- the reference-written file
+REF_DIR = "ref_hierarchical"
+
+
+@pytest.fixture(scope="module")
+def ref_manifest():
+    import json
+    import os
+
+    from conftest import GOLDEN
+
+    with open(os.path.join(GOLDEN, "ref_hierarchical_manifest.json")) as f:
+        man = json.load(f)
+    return man, os.path.join(GOLDEN, REF_DIR, man["file"])
+
+
+def _check_against_manifest(data, man):
+    assert sorted(data) == man["keys"]
+    for k, e in man["entries"].items():
+        v = data[k]
+        if e["type"] == "ndarray":
+            assert isinstance(v, np.ndarray) and str(v.dtype) == e["dtype"], k
+            assert list(v.shape) == e["shape"], k
+            assert float(np.asarray(v, np.float64).sum()) == pytest.approx(e["sum"], rel=1e-12, abs=1e-9), k
+        elif e["type"] == "dict":
+            assert sorted(v) == e["keys"], k
+            assert {kk: type(vv).__name__ for kk, vv in v.items()} == e["types"], k
+        else:
+            assert type(v).__name__ == e["type"] and v == e["value"], k
+
+
+def test_reference_written_file_loads(ref_manifest):
+    """f2 pin: a `*_hierarchical.pt` written by the reference's own save_hierarchical_data
+    (data/preprocessing.py:138-173; tests/golden/gen_preprocess.py hier) loads through
+    load_hierarchical_file (torch.load weights_only=True + the numpy allowlist, never an
+    unpickler) with every key, dtype, shape and value the manifest recorded; the file's pickle
+    names nothing beyond numpy reconstruction globals."""
+    from pointcloud_style_transfer_amd.data.dataset import load_hierarchical_file
+
+    man, path = ref_manifest
+    assert set(man["pickle_globals"]) <= {"_codecs.encode", "numpy._core.multiarray._reconstruct",
+                                          "numpy._core.multiarray.scalar", "numpy.dtype",
+                                          "numpy.ndarray", "numpy.core.multiarray._reconstruct",
+                                          "numpy.core.multiarray.scalar"}
+    _check_against_manifest(load_hierarchical_file(path), man)
+
+
+def test_reference_file_through_dataset(ref_manifest, tmp_path):
+    """HierarchicalPointCloudDataset / the collate over the reference-written file
+    (data/dataset.py:30-99,136-157): tensors of the recorded values, float32 / int64, the
+    global rows are the full rows at the global indices (the reference's own invariant)."""
+    import shutil
+
+    import torch
+
+    from pointcloud_style_transfer_amd.data.dataset import (HierarchicalPointCloudDataset,
+                                                             create_dataloaders,
+                                                             load_hierarchical_file)
+
+    man, path = ref_manifest
+    raw = load_hierarchical_file(path)
+    for split in ("train", "val"):
+        (tmp_path / split).mkdir()
+        for i in range(2):
+            shutil.copy(path, tmp_path / split / f"r{i}_hierarchical.pt")
+    item = HierarchicalPointCloudDataset(str(tmp_path / "train"))[0]
+    for k in ("sim_full", "real_full", "sim_global", "real_global"):
+        assert item[k].dtype == torch.float32 and np.array_equal(item[k].numpy(), raw[k]), k
+    for k in ("sim_global_indices", "real_global_indices"):
+        assert item[k].dtype == torch.int64 and np.array_equal(item[k].numpy(), raw[k]), k
+    for side in ("sim", "real"):
+        full, glob, gi = (item[f"{side}_full"].numpy(), item[f"{side}_global"].numpy(),
+                          item[f"{side}_global_indices"].numpy())
+        assert np.array_equal(glob, full[gi])
+    assert item["total_points"] == 4096 and item["global_points"] == 1024
+    tr, _ = create_dataloaders(str(tmp_path), batch_size=2, num_workers=0)
+    b = next(iter(tr))
+    assert b["sim_full"].shape == (2, 4096, 3) and len(b["real_norm_params"]) == 2
+
+
+def _sampler_worker(rank, world, port, d, q):
+    import os
+
+    os.environ.update(RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(world),
+                      MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+
+    from pointcloud_style_transfer_amd import distributed as D
+    from pointcloud_style_transfer_amd.data.dataset import create_dataloaders
+
+    try:
+        D.init_from_env("gloo")
+        tr, _ = create_dataloaders(d, batch_size=1, num_workers=0)
+        epochs = []
+        for e in range(2):
+            tr.sampler.set_epoch(e)
+            epochs.append([int(i) for i in tr.sampler])
+        q.put({"rank": rank, "epochs": epochs, "type": type(tr.sampler).__name__})
+    finally:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+def test_distributed_sampler_partitions_world2(ref_manifest, tmp_path):
+    """Under a world-2 process group the train loader's DistributedSampler gives each rank a
+    disjoint half of the files, and set_epoch (called by DiffusionTrainer.train) reshuffles."""
+    import shutil
+    import socket
+
+    import torch.multiprocessing as mp
+
+    _, path = ref_manifest
+    for split in ("train", "val"):
+        (tmp_path / split).mkdir()
+        for i in range(8):
+            shutil.copy(path, tmp_path / split / f"r{i}_hierarchical.pt")
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_sampler_worker, args=(r, 2, port, str(tmp_path), q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = sorted([q.get(timeout=120) for _ in ps], key=lambda d: d["rank"])
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert res[0]["type"] == "DistributedSampler"
+    for e in range(2):
+        a, b = res[0]["epochs"][e], res[1]["epochs"][e]
+        assert len(a) == len(b) == 4 and sorted(a + b) == list(range(8))
+    assert res[0]["epochs"][0] != res[0]["epochs"][1]  # reshuffled across epochs
+
+
+@pytest.mark.gpu
+def test_own_writer_matches_reference_format(ref_manifest, tmp_path):
+    """Our save_hierarchical_data writes the reference's format: the same keys, dtypes,
+    shapes, norm-param entry types and pickle globals as the reference-written file."""
+    import io
+    import pickletools
+    import zipfile
+
+    from pointcloud_style_transfer_amd.data.dataset import load_hierarchical_file
+    from pointcloud_style_transfer_amd.data.preprocessing import PointCloudPreprocessor
+    from pointcloud_style_transfer_amd.synthetic import lidar_like_cloud
+
+    man, _ = ref_manifest
+    pre = PointCloudPreprocessor(4096, 1024, rng=np.random.default_rng(3))
+    sim = lidar_like_cloud(1100, 4096) * np.float32(20.0) + np.float32(5.0)
+    real = lidar_like_cloud(2100, 4096) * np.float32(30.0) - np.float32(2.0)
+    path = pre.save_hierarchical_data(sim, real, str(tmp_path), "own0")
+    data = load_hierarchical_file(path)
+    assert sorted(data) == man["keys"]
+    for k, e in man["entries"].items():
+        v = data[k]
+        if e["type"] == "ndarray":
+            assert str(v.dtype) == e["dtype"] and list(v.shape) == e["shape"], k
+        elif e["type"] == "dict":
+            assert sorted(v) == e["keys"], k
+            assert {kk: type(vv).__name__ for kk, vv in v.items()} == e["types"], k
+        else:
+            assert type(v).__name__ == e["type"] and v == e["value"], k
+    # the deterministic parts equal the reference's values (the pad draw is random)
+    ref = load_hierarchical_file(ref_manifest[1])
+    for k in ("sim_full", "real_full"):
+        np.testing.assert_array_equal(data[k], ref[k])
+    globals_ = set()
+    with zipfile.ZipFile(path) as z:
+        pk = [n for n in z.namelist() if n.endswith("data.pkl")][0]
+        for op, arg, _ in pickletools.genops(io.BytesIO(z.read(pk))):
+            if op.name in ("GLOBAL", "STACK_GLOBAL") and arg:
+                globals_.add(str(arg).replace(" ", "."))
+    assert globals_ <= set(man["pickle_globals"]), globals_ - set(man["pickle_globals"])
