@@ -88,6 +88,36 @@ int pcst_channel_stats(const float* Z, int64_t M, int64_t O, double* mean, doubl
 int pcst_affine_act(const float* Z, int64_t M, int64_t O, const float* scale, const float* shift,
                     int relu, int64_t pool_ns, float* Y, void* stream);
 
+/* Training half of SetAbstraction (pointnet2_encoder.py:106-112 under autograd; replaces
+ * F.batch_norm / F.relu / torch.max and the advanced-index backward on the trainer's path).
+ * bn_train_coeffs: from the batch mean / biased var (pcst_channel_stats) -> scale =
+ *   gamma/sqrt(var+eps), shift = beta - mean*scale (fp32, as F.batch_norm's affine), invstd
+ *   (float64); updates running_mean / running_var in place with `momentum` (unbiased var) when
+ *   they are non-NULL (BatchNorm2d train mode).
+ * bn_relu_maxpool: Y [M/ns, O] = max over each group of ns rows of relu(scale*Z + shift) and
+ *   arg [M/ns, O] = the group row of the maximum (the first on ties).
+ * bn_relu_bwd: backward of relu(BN_train(Z)) (+ the max-pool when dY is NULL and dP/arg/ns
+ *   are given): dZ [M,O], dgamma, dbeta [O] (may be NULL); deterministic (float64 chunk sums
+ *   combined in order).  workspace: pcst_bn_relu_bwd_workspace_size() bytes.
+ * group_gather_bwd: backward of pcst_group_gather's feature part: dpoints [B,N,C] =
+ *   sum over the entries (s, k) with clamp(group_idx[b,s,k]) == n of dgrouped[b,s,k,3:];
+ *   each destination sums in ascending entry order after a stable sort (deterministic). */
+int pcst_bn_train_coeffs(const double* mean, const double* var, int64_t M, int64_t O,
+                         const float* gamma, const float* beta, double eps, double momentum,
+                         float* running_mean, float* running_var, float* scale, float* shift,
+                         double* invstd, void* stream);
+int pcst_bn_relu_maxpool(const float* Z, int64_t M, int64_t O, const float* scale,
+                         const float* shift, int64_t ns, float* Y, int32_t* arg, void* stream);
+int pcst_bn_relu_bwd_workspace_size(int64_t O, size_t* bytes);
+int pcst_bn_relu_bwd(const float* Z, int64_t M, int64_t O, const float* scale, const float* shift,
+                     const double* mean, const double* invstd, const float* gamma, const float* dY,
+                     const float* dP, const int32_t* arg, int64_t ns, float* dZ, float* dgamma,
+                     float* dbeta, void* workspace, void* stream);
+int pcst_group_gather_bwd_workspace_size(int64_t B, int64_t E, size_t* bytes);
+int pcst_group_gather_bwd(const float* dgrouped, const int64_t* group_idx, int64_t B, int64_t S,
+                          int64_t ns, int64_t N, int64_t C, float* dpoints, void* workspace,
+                          void* stream);
+
 /* Weight / bias gradient of a per-point linear layer for the training path (autograd of
  * nn.Linear / Conv2d-1x1, trainer.py:106 backward): dW [O,I] = dZ^T X, db [O] = column sums of
  * dZ (db may be NULL), with dZ [M,O] and X [M,I] row-major.  Split over row chunks on exact-f32

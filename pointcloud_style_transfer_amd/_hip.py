@@ -71,6 +71,12 @@ SIGNATURES = {
     "pcst_chamfer_fwd": [_P, _P, _I, _I, _I, _P, _P, _P, _P, _P, _P],
     "pcst_chamfer_bwd_workspace_size": [_I, _I, _I, _SZ],
     "pcst_chamfer_bwd": [_P, _P, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P],
+    "pcst_bn_train_coeffs": [_P, _P, _I, _I, _P, _P, _D, _D, _P, _P, _P, _P, _P, _P],
+    "pcst_bn_relu_maxpool": [_P, _I, _I, _P, _P, _I, _P, _P, _P],
+    "pcst_bn_relu_bwd_workspace_size": [_I, _SZ],
+    "pcst_bn_relu_bwd": [_P, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _I, _P, _P, _P, _P, _P],
+    "pcst_group_gather_bwd_workspace_size": [_I, _I, _SZ],
+    "pcst_group_gather_bwd": [_P, _P, _I, _I, _I, _I, _I, _P, _P, _P],
     "pcst_l1_workspace_size": [_SZ],
     "pcst_l1_fwd": [_P, _P, _I, _P, _P, _P],
     "pcst_l1_bwd": [_P, _P, _I, _P, _P, _P],
@@ -471,6 +477,73 @@ def affine_act(Z, scale, shift, relu=True, pool_ns=0):
     return Y
 
 
+# ----------------------------------------------------------------------------- SA training half
+def bn_train_coeffs(mean, var, M, gamma, beta, eps, momentum, running_mean=None, running_var=None):
+    """-> (scale fp32 [O], shift fp32 [O], invstd float64 [O]); running stats updated in place."""
+    require_device(mean, var, gamma, beta)
+    O = mean.shape[0]
+    if mean.dtype != torch.float64 or var.dtype != torch.float64:
+        raise RuntimeError("bn_train_coeffs: mean / var must be float64 (pcst_channel_stats)")
+    gamma, beta = _f32(gamma), _f32(beta)
+    for t in (running_mean, running_var):
+        if t is not None and (t.dtype != torch.float32 or not t.is_contiguous()):
+            raise RuntimeError("bn_train_coeffs: running stats must be contiguous fp32")
+    scale = torch.empty(O, dtype=torch.float32, device=mean.device)
+    shift = torch.empty_like(scale)
+    invstd = torch.empty(O, dtype=torch.float64, device=mean.device)
+    _call("pcst_bn_train_coeffs", _ptr(mean), _ptr(var), int(M), O, _ptr(gamma), _ptr(beta),
+          float(eps), float(momentum), _ptr(running_mean), _ptr(running_var), _ptr(scale),
+          _ptr(shift), _ptr(invstd), _stream())
+    return scale, shift, invstd
+
+
+def bn_relu_maxpool(Z, scale, shift, ns):
+    """-> (pooled [M/ns, O], arg int32 [M/ns, O]) of relu(scale*Z + shift)."""
+    require_device(Z, scale, shift)
+    Z, scale, shift = _f32(Z), _f32(scale), _f32(shift)
+    M, O = Z.shape
+    if M % ns:
+        raise RuntimeError(f"bn_relu_maxpool: {M} rows not a multiple of {ns}")
+    Y = torch.empty(M // ns, O, dtype=torch.float32, device=Z.device)
+    arg = torch.empty(M // ns, O, dtype=torch.int32, device=Z.device)
+    _call("pcst_bn_relu_maxpool", _ptr(Z), M, O, _ptr(scale), _ptr(shift), ns, _ptr(Y), _ptr(arg),
+          _stream())
+    return Y, arg
+
+
+def bn_relu_bwd(Z, scale, shift, mean, invstd, gamma, dY=None, dP=None, arg=None, ns=0):
+    """Backward of relu(BN_train(Z)) (+ max-pool when dP/arg given) -> (dZ, dgamma, dbeta)."""
+    require_device(Z, scale, shift, mean, invstd, gamma, dY, dP, arg)
+    Z, scale, shift, gamma = _f32(Z), _f32(scale), _f32(shift), _f32(gamma)
+    M, O = Z.shape
+    dY = None if dY is None else _f32(dY)
+    dP = None if dP is None else _f32(dP)
+    arg = None if arg is None else arg.contiguous()
+    ws = _workspace("pcst_bn_relu_bwd_workspace_size", O, device=Z.device)
+    dZ = torch.empty_like(Z)
+    dgamma = torch.empty(O, dtype=torch.float32, device=Z.device)
+    dbeta = torch.empty_like(dgamma)
+    _call("pcst_bn_relu_bwd", _ptr(Z), M, O, _ptr(scale), _ptr(shift), _ptr(mean), _ptr(invstd),
+          _ptr(gamma), _ptr(dY), _ptr(dP), _ptr(arg), int(ns), _ptr(dZ), _ptr(dgamma), _ptr(dbeta),
+          _ptr(ws), _stream())
+    return dZ, dgamma, dbeta
+
+
+def group_gather_bwd(dgrouped, group_idx, N):
+    """dgrouped [B,S,ns,3+C], group_idx [B,S,ns] -> dpoints [B,N,C] (deterministic)."""
+    require_device(dgrouped, group_idx)
+    dgrouped, group_idx = _f32(dgrouped), _i64(group_idx)
+    B, S, ns, W = dgrouped.shape
+    C = W - 3
+    if tuple(group_idx.shape) != (B, S, ns):
+        raise RuntimeError(f"group_gather_bwd: idx {tuple(group_idx.shape)} != {(B, S, ns)}")
+    ws = _workspace("pcst_group_gather_bwd_workspace_size", B, S * ns, device=dgrouped.device)
+    dP = torch.empty(B, N, C, dtype=torch.float32, device=dgrouped.device)
+    _call("pcst_group_gather_bwd", _ptr(dgrouped), _ptr(group_idx), B, S, ns, N, C, _ptr(dP),
+          _ptr(ws), _stream())
+    return dP
+
+
 # ----------------------------------------------------------------------------- losses
 def chamfer_fwd(pred, target):
     """-> (chamfer [B], arg1 [B,N] int32, arg2 [B,M] int32)."""
@@ -597,7 +670,8 @@ _GUARDED = ("square_distance", "index_points", "fps", "ball_query", "group_gathe
             "noise_cond", "noise_mlp", "cfg_ddim_step", "pointwise_linear", "relu_bwd",
             "linear_wgrad", "gemm_nt_bf16", "channel_stats", "affine_act", "chamfer_fwd",
             "chamfer_bwd", "l1_fwd", "l1_bwd", "knn_dist", "emd_greedy", "voxel_center_dist",
-            "cfg_ddim_step_dcoef", "voxel_downsample_copies_dseed")
+            "cfg_ddim_step_dcoef", "voxel_downsample_copies_dseed", "bn_train_coeffs",
+            "bn_relu_maxpool", "bn_relu_bwd", "group_gather_bwd")
 for _name in _GUARDED:
     globals()[_name] = _on_tensor_device(globals()[_name])
 del _name

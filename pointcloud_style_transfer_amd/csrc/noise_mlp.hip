@@ -168,8 +168,8 @@ struct NoHook {
   __device__ void operator()(int) const {}
 };
 
-template <class TR, int N, int KPER, int ICB, int AST, int ACB, class Hook = NoHook>
-__device__ __forceinline__ void run_seq(const Streamer<TR>& st, int q, int base,
+template <class TR, int N, int KPER, int ICB, int AST, int ACB, class Hook = NoHook, class ST>
+__device__ __forceinline__ void run_seq(const ST& st, int q, int base,
                                         const typename TR::Op* in, f32x16* acc,
                                         const Hook& hook = Hook()) {
   constexpr int G = TR::G;
@@ -471,6 +471,245 @@ __global__ __launch_bounds__(TR::THREADS) void noise_mlp_kernel(
   }
 }
 
+// ============================================================================================
+// bf16 production kernel: wave PAIRS.  A 512-thread workgroup (8 waves, 2 per SIMD) owns 128
+// points; waves w and w^4 form a pair that shares 32 points and splits every layer's OUTPUT
+// features: role 0 (waves 0-3) computes output blocks [0, NOB/2), role 1 the rest.  Per wave
+// that halves the live activations (residual stream 4 x 32 rows fp32 = 64 VGPRs, the full bf16
+// B operand of the next layer 64 VGPRs), so two waves fit on a SIMD (<= 256 VGPRs) and each
+// hides the other's LDS waits, epilogues and barrier skew behind its MFMAs; the SIMD's MFMA
+// work per 128 points is unchanged.
+//   * dense layers: after a layer each wave converts its own output blocks to bf16 operands and
+//     puts them in its LDS exchange area (8 KiB per wave); after the next part barrier it reads
+//     the partner's half, so both hold the full K operand;
+//   * residual blocks, per pair of hidden chunks (it, 8 + it): W1 part -- role 0 computes hidden
+//     chunk it, role 1 chunk 8 + it (K = 256, 16 MFMAs each); each writes its ReLU'd bf16
+//     chunk into its PARTNER's area; W2 part -- each reads the partner's chunk and accumulates
+//     both chunks into its own 4 residual blocks (16 MFMAs).
+// Exchange areas: a wave writes its layer outputs into its own area and its hidden chunks into
+// the partner's, and reads the opposite; with the part barriers in between, no exchange needs
+// a barrier of its own (see DESIGN.md §3 for the ordering argument).
+// Weights stream through a 2-slot ring of 32 KiB parts; the packing (packing.py, pair layout)
+// puts each role's fragments for a part in one half of it.
+constexpr int kPairThreads = 512;
+constexpr int kXBytes = 8192;  // exchange area per wave (8 operands x 1 KiB)
+
+struct Streamer2 {
+  static constexpr int kSlots = 2;
+  static constexpr int kWaves = kPairThreads / 64;
+  static constexpr int kPerWave = kPart / 1024 / kWaves;  // 1 KiB pieces per wave per part
+  const char* blob;
+  char* lds;
+  int part;
+  int nparts;
+  int wave;
+  __device__ void issue(int q) {
+    if (q >= nparts) return;
+    const int lane = threadIdx.x & 63;
+    char* dst = lds + (q & 1) * kPart + wave * kPerWave * 1024;
+    const char* src = blob + (int64_t)q * kPart + wave * kPerWave * 1024;
+#pragma unroll
+    for (int i = 0; i < kPerWave; ++i)
+      __builtin_amdgcn_global_load_lds((const void*)(src + i * 1024 + lane * 16),
+                                       (__attribute__((address_space(3))) void*)(dst + i * 1024),
+                                       16, 0, 0);
+  }
+  // __syncthreads waits for this wave's DMA (vmcnt 0) before the barrier: after it, the part
+  // issued one part earlier has landed for every wave, and every wave is done with the slot
+  // the next DMA overwrites.
+  __device__ void begin() {
+    issue(0);
+    __syncthreads();
+    issue(1);
+  }
+  __device__ void next() {
+    __syncthreads();
+    ++part;
+    issue(part + 1);
+  }
+  __device__ uint32_t frag_addr(int q, int f) const {
+    return (uint32_t)(uintptr_t)(lds + (q & 1) * kPart + f * 1024 + (threadIdx.x & 63) * 16);
+  }
+  __device__ bf16x8 frag_at(int q, int f) const {
+    return *reinterpret_cast<const bf16x8*>(lds + (q & 1) * kPart + f * 1024 + (threadIdx.x & 63) * 16);
+  }
+};
+
+template <int N>
+__device__ __forceinline__ void xput(char* X, int area, const bf16x8* ops) {
+  bf16x8* d = reinterpret_cast<bf16x8*>(X + area * kXBytes) + (threadIdx.x & 63);
+#pragma unroll
+  for (int i = 0; i < N; ++i) d[i * 64] = ops[i];
+}
+template <int N>
+__device__ __forceinline__ void xget(const char* X, int area, bf16x8* ops) {
+  const bf16x8* d = reinterpret_cast<const bf16x8*>(X + area * kXBytes) + (threadIdx.x & 63);
+#pragma unroll
+  for (int i = 0; i < N; ++i) ops[i] = d[i * 64];
+}
+
+// NOWN own output blocks of K = 16*NS, streamed as parts that hold OWNPP own blocks per role.
+template <int NOWN, int NS, int DONE = 0>
+__device__ __forceinline__ void dense_pair(Streamer2& st, int role, const bf16x8* in, f32x16* acc) {
+  constexpr int FPP = kPart / TrBF16::FRAG;
+  constexpr int OWNPP = FPP / NS / 2;
+  static_assert(OWNPP >= 1 && FPP % (2 * NS) == 0, "part must hold whole blocks for both roles");
+  constexpr int NOW = (NOWN - DONE) < OWNPP ? (NOWN - DONE) : OWNPP;
+  run_seq<TrBF16, NOW * NS, NS, NS, 1, 8>(st, st.part, role * OWNPP * NS, in, acc + DONE);
+  if constexpr (DONE + NOW < NOWN) {
+    st.next();
+    dense_pair<NOWN, NS, DONE + NOW>(st, role, in, acc);
+  }
+}
+
+// One wave's program; ROLE is a template parameter so that every register-array index is a
+// compile-time constant (a role-dependent index into a register array would go to scratch).
+template <int ROLE>
+__device__ __forceinline__ void pair_wave(const float* __restrict__ cond, const float* sb,
+                                          const float* sc, char* X, Streamer2& st, int wid,
+                                          int64_t c0, int slot, float px, float py, float pz,
+                                          int64_t p, int64_t P, float* __restrict__ out) {
+  using TR = TrBF16;
+  using Op = bf16x8;
+  constexpr int R = ROLE;
+  const int h = (threadIdx.x & 63) >> 5;
+  const int mate = wid ^ 4;
+
+  // ---- h1 = relu(W0 p + b0), all 128 rows in both roles (VALU), operand form
+  Op h1[8];
+#pragma unroll
+  for (int ob = 0; ob < 4; ++ob) {
+    float v[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int row = ob * 32 + crow(r, h);
+      float x = sb[kOffB0 + row];
+      x = fmaf(sb[kOffW0 + row * 3 + 0], px, x);
+      x = fmaf(sb[kOffW0 + row * 3 + 1], py, x);
+      x = fmaf(sb[kOffW0 + row * 3 + 2], pz, x);
+      v[r] = fmaxf(x, 0.0f);
+    }
+    TR::to_op(v, &h1[ob * 2]);
+  }
+
+  Op xb[16];   // the full K = 256 operand: blocks 0-3 at [0, 8), blocks 4-7 at [8, 16)
+  // own operands (already in xb[8R..]) -> own area; after the next part barrier the
+  // partner's half is read into xb[8(1-R)..]
+  auto put_own = [&](const f32x16* acc, bool relu) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) act_op<TR>(acc[j], relu, &xb[8 * R + 2 * j]);
+    xput<8>(X, wid, &xb[8 * R]);
+  };
+  auto get_mate = [&]() { xget<8>(X, mate, &xb[8 * (1 - R)]); };
+
+  // ---- h2 = relu(W2 h1 + b2): own blocks 4R + j
+  {
+    f32x16 acc[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[j] = bias_block(sb + kOffB2 + (4 * R + j) * 32, h);
+    dense_pair<4, 8>(st, R, h1, acc);
+    put_own(acc, true);
+  }
+  // ---- x = W4 h2 + cond[cloud]  (cond holds b4)
+  f32x16 x[4];
+  {
+    const bool in_lds = slot >= 0 && slot < kCondSlots;
+    const float* cs = in_lds ? sc + slot * 256 : cond + (c0 + slot) * 256;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) x[j] = bias_block(cs + (4 * R + j) * 32, h);
+  }
+  st.next();
+  get_mate();
+  dense_pair<4, 16>(st, R, xb, x);
+  put_own(x, false);
+
+  // ---- 6 residual blocks
+  for (int layer = 0; layer < 6; ++layer) {
+    const float* b1 = sb + kOffB1 + layer * 512;
+    const float* b2 = sb + kOffBB2 + layer * 256;
+    st.next();
+    get_mate();
+    for (int it = 0; it < 8; ++it) {
+      if (it) st.next();
+      // W1: hidden chunk (it | 8 + it) of this role, K = 256
+      f32x16 hc = bias_block(b1 + (it + 8 * R) * 32, h);
+      run_seq<TR, 16, 16, 16, 1, 1>(st, st.part, R * 16, xb, &hc);
+      Op hb[4];   // [chunk it op 0, op 1, chunk 8+it op 0, op 1]
+      act_op<TR>(hc, true, &hb[2 * R]);
+      xput<2>(X, mate, &hb[2 * R]);          // into the partner's area
+      st.next();
+      xget<2>(X, wid, &hb[2 * (1 - R)]);     // the partner's chunk, from this wave's area
+      // W2: own residual blocks += W2[block, chunk it] h_it + W2[block, chunk 8+it] h_8+it
+      run_seq<TR, 16, 4, 4, 1, 1>(st, st.part, R * 16, hb, x);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) x[j] += bias_block(b2 + (4 * R + j) * 32, h);
+    put_own(x, false);
+  }
+
+  // ---- output MLP 256 -> 256 -> 128 -> 3
+  {
+    f32x16 acc[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[j] = bias_block(sb + kOffO0 + (4 * R + j) * 32, h);
+    st.next();
+    get_mate();
+    dense_pair<4, 16>(st, R, xb, acc);
+    put_own(acc, true);
+  }
+  Op o2[8];  // K = 128 operand: blocks 0-1 at [0, 4), blocks 2-3 at [4, 8)
+  {
+    f32x16 acc[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[j] = bias_block(sb + kOffO2 + (2 * R + j) * 32, h);
+    st.next();
+    get_mate();
+    dense_pair<2, 16>(st, R, xb, acc);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) act_op<TR>(acc[j], true, &o2[4 * R + 2 * j]);
+    xput<4>(X, wid, &o2[4 * R]);
+  }
+  st.next();
+  xget<4>(X, mate, &o2[4 * (1 - R)]);
+  f32x16 acc0 = f32x16{};
+  run_seq<TR, 8, 8, 8, 1, 1>(st, st.part, 0, o2, &acc0);   // both roles: the same 3 rows
+  if (R == 0 && p < P && h == 0) {
+    out[p * 3 + 0] = acc0[0] + sb[kOffO4 + 0];
+    out[p * 3 + 1] = acc0[1] + sb[kOffO4 + 1];
+    out[p * 3 + 2] = acc0[2] + sb[kOffO4 + 2];
+  }
+}
+
+__global__ __launch_bounds__(kPairThreads) void noise_mlp_pair_kernel(
+    const float* __restrict__ pts, int64_t P, int64_t T, const float* __restrict__ cond,
+    int64_t nclouds, const char* __restrict__ blob, int nparts, const float* __restrict__ bias,
+    float* __restrict__ out) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* X = smem + Streamer2::kSlots * kPart;
+  float* sb = reinterpret_cast<float*>(X + Streamer2::kWaves * kXBytes);
+  float* sc = sb + kBiasFloats;  // kCondSlots x 256
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int64_t p0 = (int64_t)blockIdx.x * 128;
+  const int64_t c0 = p0 / T;
+  for (int i = tid; i < kBiasFloats; i += kPairThreads) sb[i] = bias[i];
+  for (int i = tid; i < kCondSlots * 256; i += kPairThreads) {
+    const int64_t c = c0 + i / 256;
+    sc[i] = c < nclouds ? cond[c * 256 + (i % 256)] : 0.0f;
+  }
+  const int64_t p = p0 + (wid & 3) * 32 + (lane & 31);
+  const int64_t pc = p < P ? p : (P - 1);
+  const float px = pts[pc * 3 + 0], py = pts[pc * 3 + 1], pz = pts[pc * 3 + 2];
+  const int slot = (int)(pc / T - c0);
+  __syncthreads();
+  Streamer2 st{blob, smem, 0, nparts, wid};
+  st.begin();
+  if (wid < 4)
+    pair_wave<0>(cond, sb, sc, X, st, wid, c0, slot, px, py, pz, p, P, out);
+  else
+    pair_wave<1>(cond, sb, sc, X, st, wid, c0, slot, px, py, pz, p, P, out);
+}
+
 // cond[c] = b4 + time_proj(emb(t_c)) + style_proj(style_c)   (diffusion_model.py:15-26, 56-58)
 // freqs[64] is the reference's exp table computed on the host with torch's own CPU exp.
 // Grid (clouds, 8): workgroup y computes outputs [32y, 32y + 32); its 8 row groups split the
@@ -566,9 +805,13 @@ extern "C" int pcst_noise_mlp(const float* pts, int64_t P, int64_t points_per_cl
   PCST_CHECK_ARG(((uintptr_t)blob & 15) == 0, "noise_mlp: blob must be 16-byte aligned");
   if (P == 0) return PCST_OK;
   hipStream_t s = as_stream(stream);
-  if (precision == 1)
-    launch_noise_mlp<TrBF16>(pts, P, points_per_cloud, cond, nclouds, blob, blob_bytes, bias, out, s);
-  else
+  if (precision == 1) {
+    const size_t lds = Streamer2::kSlots * kPart + Streamer2::kWaves * kXBytes +
+                       (kBiasFloats + kCondSlots * 256) * sizeof(float);
+    hipLaunchKernelGGL(noise_mlp_pair_kernel, dim3((unsigned)cdiv(P, 128)), dim3(kPairThreads), lds,
+                       s, pts, P, points_per_cloud, cond, nclouds, (const char*)blob,
+                       (int)(blob_bytes / kPart), bias, out);
+  } else
     launch_noise_mlp<TrF32>(pts, P, points_per_cloud, cond, nclouds, blob, blob_bytes, bias, out, s);
   PCST_LAUNCH_CHECK("noise_mlp");
   return PCST_OK;

@@ -76,11 +76,8 @@ class SetAbstraction(nn.Module):
         new_xyz = index_points(xyz, fidx)
         gidx = query_ball_point(self.radius, self.nsample, xyz, new_xyz)
         if points is not None and points.requires_grad and torch.is_grad_enabled():
-            # training: centred xyz from the kernel, features gathered with autograd
-            new_xyz, gxyz = _hip.group_gather(xyz, None, fidx, gidx)
-            bidx = torch.arange(B, device=xyz.device).view(B, 1, 1)
-            g = torch.cat([gxyz, points[bidx, gidx.clamp(0, N - 1)]], dim=-1)
-            grouped = g
+            # training: the same fused gather, with its deterministic scatter backward
+            new_xyz, grouped = _ag.GroupGatherFn.apply(xyz, points, fidx, gidx)
         else:
             new_xyz, grouped = _hip.group_gather(xyz, points, fidx, gidx)
         feats = self.apply_mlp(grouped.reshape(B * self.npoint * self.nsample, -1),
@@ -115,17 +112,22 @@ class SetAbstraction(nn.Module):
         return x
 
     def _apply_mlp_train(self, x: torch.Tensor, pool_ns: int) -> torch.Tensor:
-        """Differentiable variant: conv GEMMs on the MFMA kernel (models/_autograd.py),
-        BatchNorm/ReLU/max as device tensor ops."""
-        for conv, bn in zip(self.mlp_convs, self.mlp_bns):
+        """Differentiable variant: conv GEMMs on the MFMA kernel, train-mode BatchNorm + ReLU
+        (+ the max over nsample on the last layer) on csrc/sa_train.hip, all with HIP
+        backward (models/_autograd.py).  Eval-mode BN under autograd (not a trainer path)
+        keeps the torch ops."""
+        n = len(self.mlp_convs)
+        for i, (conv, bn) in enumerate(zip(self.mlp_convs, self.mlp_bns)):
             z = _ag.LinearFn.apply(x, conv.weight, conv.bias, False)
-            z = F.batch_norm(z, bn.running_mean, bn.running_var, bn.weight, bn.bias,
-                             bn.training, bn.momentum, bn.eps)
-            if bn.training and bn.track_running_stats:
-                bn.num_batches_tracked.add_(1)
-            x = F.relu(z)
-        C = x.shape[-1]
-        return x.view(-1, pool_ns, C).max(dim=1)[0]
+            last = i == n - 1
+            if bn.training:
+                x = _ag.bn_relu(z, bn, pool_ns if last else 0)
+                continue
+            x = F.relu(F.batch_norm(z, bn.running_mean, bn.running_var, bn.weight, bn.bias,
+                                    False, bn.momentum, bn.eps))
+            if last:
+                x = x.view(-1, pool_ns, x.shape[-1]).max(dim=1)[0]
+        return x
 
 
 class PointNet2Encoder(nn.Module):

@@ -16,8 +16,19 @@ The k permutation is the row order in which the previous layer's accumulator
 registers arrive as this layer's B operand (the C/D map row = (reg & 3) + 8 (reg >> 2)
 + 4 (lane >> 5)), so activations never leave registers between layers.
 
-Order: point_encoder.2, point_encoder.4, 6 x 16 residual chunks (W1 rows of the chunk,
-then W2 columns of the chunk for the 8 output blocks), output_mlp.0 / .2 / .4.
+f32 order (noise_mlp_kernel<TrF32>): point_encoder.2, point_encoder.4, 6 x 16 residual
+chunks (W1 rows of the chunk, then W2 columns of the chunk for the 8 output blocks),
+output_mlp.0 / .2 / .4.
+
+bf16 order (noise_mlp_pair_kernel, "pair layout"): the same layers, but every part holds the
+fragments of BOTH wave roles, role 0 in its first half and role 1 in its second:
+  dense layer (NOB output blocks, NS k-steps): part q = [role 0: blocks q*k .. q*k+k-1 |
+      role 1: blocks NOB/2 + q*k ..], k = 16 / NS own blocks per role and part;
+  residual layer, pair of hidden chunks (it, 8 + it), it = 0..7:
+      W1 part = [W1 rows of chunk it | W1 rows of chunk 8 + it]
+      W2 part = [for blocks 0-3: k-steps (2it, 2it+1, 2(8+it), 2(8+it)+1) |
+                 the same for blocks 4-7];
+  output_mlp.4 (one block): one part, read by both roles.
 """
 from __future__ import annotations
 
@@ -81,6 +92,8 @@ def _pad_part(b):
 def pack_blob(sd, precision, pre="noise_predictor"):
     """sd: mapping name -> float32 numpy array (NoisePredictor params).  Returns uint8 array."""
     g = lambda n: np.asarray(sd[f"{pre}.{n}"], np.float32)  # noqa: E731
+    if precision == BF16:
+        return _pack_pair(g)
     parts = []
 
     def layer(W):
@@ -89,22 +102,48 @@ def pack_blob(sd, precision, pre="noise_predictor"):
 
     layer(g("point_encoder.2.weight"))
     layer(g("point_encoder.4.weight"))
-    ks = 16 if precision == BF16 else 2
-    opb = 32 // ks
     for i in range(6):
-        F1 = _frags(g(f"layers.{i}.0.weight"), precision)  # [16, 256/ks, e]
-        F2 = _frags(g(f"layers.{i}.2.weight"), precision)  # [8, 512/ks, e]
+        F1 = _frags(g(f"layers.{i}.0.weight"), precision)  # [16, 256/2, e]
+        F2 = _frags(g(f"layers.{i}.2.weight"), precision)  # [8, 512/2, e]
         for c in range(16):
-            w1 = _to_bytes(F1[c].reshape(-1), precision)
-            w2 = _to_bytes(F2[:, c * opb:(c + 1) * opb].reshape(-1), precision)
-            if precision == BF16:
-                parts.append(_pad_part(np.concatenate([w1, w2])))
-            else:
-                parts.append(_pad_part(w1))
-                parts.append(_pad_part(w2))
+            parts.append(_pad_part(_to_bytes(F1[c].reshape(-1), precision)))
+            parts.append(_pad_part(_to_bytes(F2[:, c * 16:(c + 1) * 16].reshape(-1), precision)))
     layer(g("output_mlp.0.weight"))
     layer(g("output_mlp.2.weight"))
     layer(g("output_mlp.4.weight"))
+    return np.concatenate(parts)
+
+
+def _pack_pair(g):
+    """bf16 pair layout of noise_mlp_pair_kernel (module docstring)."""
+    parts = []
+    fpp = PART // 1024
+
+    def emit(frags):  # list of [S, 512] fragment groups in part order
+        b = _to_bytes(np.concatenate([f.reshape(-1) for f in frags]), BF16)
+        assert len(b) <= PART
+        parts.append(_pad_part(b))
+
+    def dense(W):
+        F = _frags(W, BF16)                  # [NOB, NS, 512]
+        nob, ns = F.shape[:2]
+        k = fpp // ns // 2                   # own blocks per role and part
+        half = nob // 2
+        for q in range(half // k):
+            emit([F[q * k:(q + 1) * k], F[half + q * k:half + (q + 1) * k]])
+
+    dense(g("point_encoder.2.weight"))
+    dense(g("point_encoder.4.weight"))
+    for i in range(6):
+        F1 = _frags(g(f"layers.{i}.0.weight"), BF16)  # [16 chunks, 16, 512]
+        F2 = _frags(g(f"layers.{i}.2.weight"), BF16)  # [8 blocks, 32, 512]
+        for it in range(8):
+            emit([F1[it], F1[8 + it]])
+            steps = [2 * it, 2 * it + 1, 2 * (8 + it), 2 * (8 + it) + 1]
+            emit([F2[0:4][:, steps], F2[4:8][:, steps]])
+    dense(g("output_mlp.0.weight"))
+    dense(g("output_mlp.2.weight"))
+    emit([_frags(g("output_mlp.4.weight"), BF16)])
     return np.concatenate(parts)
 
 

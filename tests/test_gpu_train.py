@@ -148,3 +148,74 @@ def test_relu_bwd_matches_torch(H):
         dy = torch.randn(n, device="cuda", generator=g)
         y = torch.randn(n, device="cuda", generator=g).clamp_min(0)
         assert torch.equal(H.relu_bwd(dy, y), dy * (y > 0))
+
+
+@pytest.mark.parametrize("M,O,ns", [(1024, 64, 0), (131072, 64, 0), (131072, 128, 32),
+                                    (65536, 256, 64), (1024, 256, 128), (96, 3, 32)])
+def test_bn_relu_fn_vs_torch_float64(H, M, O, ns):
+    """BNReLUFn (train-mode BatchNorm + ReLU (+ max over ns rows), csrc/sa_train.hip) against
+    torch's F.batch_norm(training=True) / relu / max in float64 with autograd, same upstream
+    gradient: outputs and dZ / dgamma / dbeta within fp32 rounding of the float64 result, the
+    running statistics updated as BatchNorm2d does, and the backward deterministic."""
+    import torch.nn.functional as F
+
+    from pointcloud_style_transfer_amd.models import _autograd as ag
+
+    g = torch.Generator(device="cuda").manual_seed(M + O + ns)
+    z = (torch.randn(M, O, device="cuda", generator=g) * 2 + 0.3).requires_grad_()
+    bn = torch.nn.BatchNorm2d(O).cuda().train()
+    with torch.no_grad():
+        bn.weight.uniform_(0.5, 1.5, generator=g)
+        bn.bias.uniform_(-0.2, 0.2, generator=g)
+        bn.running_mean.uniform_(-0.1, 0.1, generator=g)
+    rm0, rv0 = bn.running_mean.clone(), bn.running_var.clone()
+    y = ag.bn_relu(z, bn, ns)
+    gy = torch.randn(y.shape, device="cuda", generator=g)
+    y.backward(gy)
+    z64 = z.detach().double().requires_grad_()
+    w64 = bn.weight.detach().double().requires_grad_()
+    b64 = bn.bias.detach().double().requires_grad_()
+    rm, rv = rm0.double().clone(), rv0.double().clone()
+    y64 = torch.relu(F.batch_norm(z64, rm, rv, w64, b64, True, 0.1, bn.eps))
+    if ns:
+        y64 = y64.view(-1, ns, O).max(dim=1)[0]
+    y64.backward(gy.double())
+    rel = lambda a, b: ((a.double() - b).norm() / b.norm().clamp_min(1e-300)).item()  # noqa: E731
+    assert rel(y.detach(), y64.detach()) < 1e-6
+    assert rel(z.grad, z64.grad) < 1e-5
+    assert rel(bn.weight.grad, w64.grad) < 1e-5
+    assert rel(bn.bias.grad, b64.grad) < 1e-5
+    assert rel(bn.running_mean, rm) < 1e-6 and rel(bn.running_var, rv) < 1e-6
+    assert int(bn.num_batches_tracked) == 1
+    gz = z.grad.clone()
+    z.grad = None
+    ag.bn_relu(z, bn, ns).backward(gy)
+    assert torch.equal(z.grad, gz), "bn_relu backward must be deterministic"
+
+
+@pytest.mark.parametrize("B,N,C,S,ns", [(8, 512, 128, 128, 64), (2, 30, 5, 7, 16), (1, 1, 64, 3, 4)])
+def test_group_gather_fn_backward(H, B, N, C, S, ns):
+    """GroupGatherFn's scatter backward (pcst_group_gather_bwd) equals torch's advanced-index
+    backward in float64 (the reference's points[batch, idx] gather, pointnet2_encoder.py:20-28,
+    99), including clamped out-of-range indices (the ball query's pad value N), and is
+    bit-deterministic."""
+    from pointcloud_style_transfer_amd.models import _autograd as ag
+
+    g = torch.Generator(device="cuda").manual_seed(B * N + C)
+    xyz = torch.randn(B, N, 3, device="cuda", generator=g)
+    pts = torch.randn(B, N, C, device="cuda", generator=g).requires_grad_()
+    fidx = torch.randint(0, N, (B, S), device="cuda", generator=g)
+    gidx = torch.randint(0, N + 1, (B, S, ns), device="cuda", generator=g)   # N -> clamped
+    gidx[:, :, 1] = gidx[:, :, 0]   # repeated indices inside a group (the pad)
+    new_xyz, grouped = ag.GroupGatherFn.apply(xyz, pts, fidx, gidx)
+    gg = torch.randn(grouped.shape, device="cuda", generator=g)
+    grouped.backward(gg)
+    p64 = pts.detach().double().requires_grad_()
+    bidx = torch.arange(B, device="cuda").view(B, 1, 1)
+    p64[bidx, gidx.clamp(0, N - 1)].backward(gg[..., 3:].double())
+    err = (pts.grad.double() - p64.grad).abs().max().item()
+    assert err <= 1e-5 * max(1.0, p64.grad.abs().max().item())
+    first = pts.grad.clone()
+    pts.grad = None
+    ag.GroupGatherFn.apply(xyz, pts, fidx, gidx)[1].backward(gg)
+    assert torch.equal(pts.grad, first)

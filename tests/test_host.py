@@ -264,3 +264,80 @@ def test_hip_wrappers_run_on_the_tensors_device(monkeypatch):
     assert f(t0) == "ok" and entered == [1]          # already current: no switch
     assert f((t1, None)) == "ok" and entered == [1, 1]  # tuple handle (knn3_query)
     assert f(torch.zeros(2)) == "ok" and entered == [1, 1]  # CPU tensor: no switch
+
+
+def test_bf16_pair_packing_follows_the_kernel_read_schedule():
+    """packing.pack_blob(BF16) in the pair layout of noise_mlp_pair_kernel: replaying the
+    kernel's read schedule (part order, role halves, block / k-step per fragment, csrc/
+    noise_mlp.hip pair_wave) over the blob recovers every weight of every layer exactly (as
+    bf16), so a layout slip fails here rather than on the GPU."""
+    import torch
+
+    from pointcloud_style_transfer_amd import packing
+    from pointcloud_style_transfer_amd.model_spec import state_dict_shapes
+    from detweights import deterministic_state
+
+    sd = deterministic_state(state_dict_shapes())
+    pre = "noise_predictor"
+    blob = packing.pack_blob(sd, packing.BF16)
+    vals = torch.from_numpy(blob.copy()).view(torch.bfloat16).float().numpy()
+    fpe = 512                                   # bf16 elements per 1 KiB fragment
+    parts = vals.reshape(-1, packing.PART // 2)
+    km = packing._kmap(packing.BF16, 32)        # [S, 64, 8] logical k per (step, lane, j)
+    r = np.arange(64) & 31
+    state = {"q": 0}
+    got = {}
+
+    def frag(q, f):
+        return parts[q, f * fpe:(f + 1) * fpe].reshape(64, 8)
+
+    def put(name, block, step, q, f):
+        W = got.setdefault(name, {})
+        fr = frag(q, f)
+        for lane in range(64):
+            for j in range(8):
+                W[(block * 32 + r[lane], int(km[step, lane, j]))] = fr[lane, j]
+
+    def dense(name, nown, ns):
+        ownpp = 32 // ns // 2
+        done = 0
+        while done < nown:
+            now = min(nown - done, ownpp)
+            for role in (0, 1):
+                for i in range(now * ns):
+                    put(name, role * nown + done + i // ns, i % ns, state["q"], role * ownpp * ns + i)
+            done += now
+            if done < nown:
+                state["q"] += 1
+
+    dense("point_encoder.2", 4, 8)
+    state["q"] += 1
+    dense("point_encoder.4", 4, 16)
+    for layer in range(6):
+        for it in range(8):
+            state["q"] += 1
+            for role in (0, 1):
+                for i in range(16):
+                    put(f"layers.{layer}.0", it + 8 * role, i, state["q"], role * 16 + i)
+            state["q"] += 1
+            steps = [2 * it, 2 * it + 1, 2 * (8 + it), 2 * (8 + it) + 1]
+            for role in (0, 1):
+                for i in range(16):
+                    put(f"layers.{layer}.2", 4 * role + i // 4, steps[i % 4], state["q"], role * 16 + i)
+    state["q"] += 1
+    dense("output_mlp.0", 4, 16)
+    state["q"] += 1
+    dense("output_mlp.2", 2, 16)
+    state["q"] += 1
+    for i in range(8):
+        put("output_mlp.4", 0, i, state["q"], i)
+    assert state["q"] + 1 == parts.shape[0]
+    for name, W in got.items():
+        ref = torch.from_numpy(sd[f"{pre}.{name}.weight"]).bfloat16().float().numpy()
+        O, K = ref.shape
+        seen = np.full((max(O, 32), K), np.nan, np.float32)
+        for (o, k), v in W.items():
+            seen[o, k] = v
+        np.testing.assert_array_equal(seen[:O], ref, err_msg=name)
+        if O < 32:
+            assert (seen[O:] == 0).all(), name
