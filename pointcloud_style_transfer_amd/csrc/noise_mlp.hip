@@ -41,6 +41,9 @@ constexpr int kCondSlots = 4;
 #ifndef PCST_NM_NCB
 #define PCST_NM_NCB 1
 #endif
+#ifndef PCST_NM_PAIRX  // pair kernel: partner = wave ^ PAIRX (4: the partner shares the SIMD)
+#define PCST_NM_PAIRX 4
+#endif
 
 struct TrBF16 {
   static constexpr int KS = 16;          // K per MFMA
@@ -505,6 +508,7 @@ struct Streamer2 {
   int wave;
   __device__ void issue(int q) {
     if (q >= nparts) return;
+    if ((PCST_NM_EXPERIMENT & 1) && q >= 2) return;
     const int lane = threadIdx.x & 63;
     char* dst = lds + (q & 1) * kPart + wave * kPerWave * 1024;
     const char* src = blob + (int64_t)q * kPart + wave * kPerWave * 1024;
@@ -523,7 +527,7 @@ struct Streamer2 {
     issue(1);
   }
   __device__ void next() {
-    __syncthreads();
+    if (!(PCST_NM_EXPERIMENT & 2)) __syncthreads();
     ++part;
     issue(part + 1);
   }
@@ -573,7 +577,7 @@ __device__ __forceinline__ void pair_wave(const float* __restrict__ cond, const 
   using Op = bf16x8;
   constexpr int R = ROLE;
   const int h = (threadIdx.x & 63) >> 5;
-  const int mate = wid ^ 4;
+  const int mate = wid ^ PCST_NM_PAIRX;
 
   // ---- h1 = relu(W0 p + b0), all 128 rows in both roles (VALU), operand form
   Op h1[8];
@@ -697,14 +701,16 @@ __global__ __launch_bounds__(kPairThreads) void noise_mlp_pair_kernel(
     const int64_t c = c0 + i / 256;
     sc[i] = c < nclouds ? cond[c * 256 + (i % 256)] : 0.0f;
   }
-  const int64_t p = p0 + (wid & 3) * 32 + (lane & 31);
+  constexpr int PX = PCST_NM_PAIRX;
+  const int pair = (wid & (PX - 1)) | ((wid / (2 * PX)) * PX);  // wave index without the role bit
+  const int64_t p = p0 + pair * 32 + (lane & 31);
   const int64_t pc = p < P ? p : (P - 1);
   const float px = pts[pc * 3 + 0], py = pts[pc * 3 + 1], pz = pts[pc * 3 + 2];
   const int slot = (int)(pc / T - c0);
   __syncthreads();
   Streamer2 st{blob, smem, 0, nparts, wid};
   st.begin();
-  if (wid < 4)
+  if ((wid & PX) == 0)
     pair_wave<0>(cond, sb, sc, X, st, wid, c0, slot, px, py, pz, p, P, out);
   else
     pair_wave<1>(cond, sb, sc, X, st, wid, c0, slot, px, py, pz, p, P, out);

@@ -5,13 +5,14 @@
 set -u
 MODE=$1
 SETS=${2:-"0:1"}
-OUT=gpurun_out/nm
+OUT=tools/nm_bin
 mkdir -p $OUT
 for s in $SETS; do
-  e=${s%%:*}; n=${s##*:}
-  bin=$OUT/nm_${e}_${n}
-  extra="-DPCST_NM_EXPERIMENT=$e -DPCST_NM_NCB=$n"
-  # "v0:0" = the kernel of the previous commit (tools/_scratch/noise_mlp_v0.hip)
+  # SET = EXP:NCB[:PAIRX]
+  e=$(echo $s | cut -d: -f1); n=$(echo $s | cut -d: -f2); x=$(echo $s | cut -s -d: -f3)
+  bin=$OUT/nm_${e}_${n}${x:+_x$x}
+  extra="-DPCST_NM_EXPERIMENT=$e -DPCST_NM_NCB=$n ${x:+-DPCST_NM_PAIRX=$x}"
+  # "v0:0" = a saved earlier kernel (tools/_scratch/noise_mlp_v0.hip)
   if [ "$e" = v0 ]; then extra='-DNM_SRC="_scratch/noise_mlp_v0.hip"'; fi
   if [ "$MODE" = build ]; then
     /opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -mno-amdgpu-ieee -fno-honor-nans \
