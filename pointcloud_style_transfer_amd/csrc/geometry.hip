@@ -8,6 +8,7 @@
 namespace pcst {
 
 typedef float fps_f2 __attribute__((ext_vector_type(2)));
+typedef int fps_i2 __attribute__((ext_vector_type(2)));
 
 
 // ------------------------------------------------------------------ square_distance
@@ -174,20 +175,25 @@ __global__ __launch_bounds__(kFps2Threads) void fps_key_kernel(const float* __re
                                                                int N, int npoint,
                                                                const int64_t* __restrict__ start,
                                                                int64_t* __restrict__ out) {
+  // points k and k+1 of a lane live in one register pair (fps_f2), so the packed
+  // v_pk_add/mul_f32 distance math needs no operand moves
+  constexpr int H = (PPT + 1) / 2;
   const int b = blockIdx.x;
   const int tid = threadIdx.x;
   const int lane = tid & 63, wid = tid >> 6;
   const float* P = xyz + (int64_t)b * N * 3;
-  float px[PPT], py[PPT], pz[PPT], dist[PPT];
+  fps_f2 X[H], Y[H], Z[H];
+  fps_i2 D[H];
 #pragma unroll
-  for (int k = 0; k < PPT; ++k) {
-    const int n = tid + k * kFps2Threads;
-    if (n < N) {
-      px[k] = P[n * 3 + 0]; py[k] = P[n * 3 + 1]; pz[k] = P[n * 3 + 2];
-      dist[k] = 1e10f;
-    } else {
-      px[k] = py[k] = pz[k] = 0.0f;
-      dist[k] = -1.0f;  // never updated, never the arg-max
+  for (int j = 0; j < H; ++j) {
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const int n = tid + (2 * j + e) * kFps2Threads;
+      const bool ok = 2 * j + e < PPT && n < N;
+      X[j][e] = ok ? P[n * 3 + 0] : 0.0f;
+      Y[j][e] = ok ? P[n * 3 + 1] : 0.0f;
+      Z[j][e] = ok ? P[n * 3 + 2] : 0.0f;
+      D[j][e] = __float_as_int(ok ? 1e10f : -1.0f);  // -1: never updated, never the arg-max
     }
   }
   __shared__ uint64_t s_key[2][kFps2Waves];
@@ -197,34 +203,29 @@ __global__ __launch_bounds__(kFps2Threads) void fps_key_kernel(const float* __re
     far = __builtin_amdgcn_readfirstlane(far);
     if (tid == 0) o[it] = far;
     const float cx = P[far * 3 + 0], cy = P[far * 3 + 1], cz = P[far * 3 + 2];
-    // two points per instruction: v_pk_add/mul_f32 perform the same IEEE operations per
-    // component ((dx*dx + dy*dy) + dz*dz, nothing fused: this file builds with
-    // -ffp-contract=off), so the distances are bit-identical to the scalar form
+    // v_pk_add/mul_f32 perform the same IEEE operations per component ((dx*dx + dy*dy) +
+    // dz*dz, nothing fused: this file builds with -ffp-contract=off), so the distances are
+    // bit-identical to the scalar form.  The running distances are kept as int bit patterns:
+    // every value is -1.0 (a padding slot) or >= 0, and on those signed-int order IS float
+    // order, so the strict-< update is one v_min_i32 and the arg-max a v_max_i32 chain (the
+    // float min/max would add a canonicalising v_max per operand in IEEE mode).
     const fps_f2 c2x = {cx, cx}, c2y = {cy, cy}, c2z = {cz, cz};
 #pragma unroll
-    for (int k = 0; k + 1 < PPT; k += 2) {
-      const fps_f2 dx = fps_f2{px[k], px[k + 1]} - c2x;
-      const fps_f2 dy = fps_f2{py[k], py[k + 1]} - c2y;
-      const fps_f2 dz = fps_f2{pz[k], pz[k + 1]} - c2z;
+    for (int j = 0; j < H; ++j) {
+      const fps_f2 dx = X[j] - c2x, dy = Y[j] - c2y, dz = Z[j] - c2z;
       const fps_f2 d = (dx * dx + dy * dy) + dz * dz;
-      dist[k] = d.x < dist[k] ? d.x : dist[k];
-      dist[k + 1] = d.y < dist[k + 1] ? d.y : dist[k + 1];
-    }
-    if (PPT & 1) {
-      const int k = PPT - 1;
-      const float dx = fsub(px[k], cx), dy = fsub(py[k], cy), dz = fsub(pz[k], cz);
-      const float d = fadd(fadd(fmul(dx, dx), fmul(dy, dy)), fmul(dz, dz));
-      dist[k] = d < dist[k] ? d : dist[k];
+      D[j][0] = min(__float_as_int(d[0]), D[j][0]);
+      D[j][1] = min(__float_as_int(d[1]), D[j][1]);
     }
     // arg-max: the value by a max chain, then the lowest k holding it (lowest point index)
-    float best = dist[0];
+    int best = D[0][0];
 #pragma unroll
-    for (int k = 1; k < PPT; ++k) best = fmaxf(best, dist[k]);
-    int bestk = PPT - 1;
+    for (int k = 1; k < 2 * H; ++k) best = max(best, D[k >> 1][k & 1]);
+    int bestk = 2 * H - 1;
 #pragma unroll
-    for (int k = PPT - 2; k >= 0; --k) bestk = dist[k] == best ? k : bestk;
+    for (int k = 2 * H - 2; k >= 0; --k) bestk = D[k >> 1][k & 1] == best ? k : bestk;
     const uint32_t n = (uint32_t)(tid + bestk * kFps2Threads);
-    const uint32_t bits = best > 0.0f ? __float_as_uint(best) : 0u;
+    const uint32_t bits = best > 0 ? (uint32_t)best : 0u;
     const uint64_t key = wave_max_u64(((uint64_t)bits << 32) | (0xFFFFFFFFu - n));
     const int slot = it & 1;
     if (lane == 0) s_key[slot][wid] = key;

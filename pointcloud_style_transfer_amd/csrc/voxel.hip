@@ -678,6 +678,7 @@ __global__ __launch_bounds__(1024) void voxf_ties_kernel(int N, int64_t T, int B
 
 // Row emit in ascending point-index order: tile j's offset is the sum of the earlier tiles'
 // keep counts; inside the tile a block scan places each index kcnt[n] times (index + point).
+// The 16 points of a thread are loaded before any store, so their latencies overlap.
 __global__ __launch_bounds__(256) void voxf_emit_kernel(const float* __restrict__ pts, int N,
                                                         int64_t T, int B,
                                                         const uint32_t* __restrict__ kcnt,
@@ -689,29 +690,33 @@ __global__ __launch_bounds__(256) void voxf_emit_kernel(const float* __restrict_
   const int row = blockIdx.y, cl = row % B;
   const int64_t tile = blockIdx.x;
   __shared__ uint32_t sh[260];
-  uint32_t before = 0;
-  for (int64_t i = threadIdx.x; i < tile; i += 256) before += ktile[row * tiles + i];
-  uint32_t tot0;
-  block_excl_scan_256(before, sh, tot0);  // tot0 = sum over the earlier tiles
   const int64_t n0 = tile * kEmitTile + threadIdx.x * kPer;
   const uint32_t* C = kcnt + (int64_t)row * N;
-  uint32_t c[kPer], s = 0;
-#pragma unroll
-  for (int k = 0; k < kPer; ++k) {
-    c[k] = n0 + k < N ? C[n0 + k] : 0u;
-    s += c[k];
-  }
-  uint32_t tot;
-  int64_t pos = (int64_t)tot0 + block_excl_scan_256(s, sh, tot);
   const float* P = pts + (int64_t)cl * N * 3;
+  uint32_t c[kPer];
+  float q[kPer * 3];
+#pragma unroll
+  for (int k = 0; k < kPer; ++k) c[k] = n0 + k < N ? C[n0 + k] : 0u;
 #pragma unroll
   for (int k = 0; k < kPer; ++k) {
-    for (uint32_t q = 0; q < c[k]; ++q, ++pos) {
+    const int64_t n = n0 + k < N ? n0 + k : N - 1;
+    q[3 * k] = P[n * 3]; q[3 * k + 1] = P[n * 3 + 1]; q[3 * k + 2] = P[n * 3 + 2];
+  }
+  uint32_t before = 0;
+  for (int64_t i = threadIdx.x; i < tile; i += 256) before += ktile[row * tiles + i];
+  uint32_t s = 0;
+#pragma unroll
+  for (int k = 0; k < kPer; ++k) s += c[k];
+  uint32_t tot0, tot;
+  block_excl_scan_256(before, sh, tot0);  // tot0 = sum over the earlier tiles
+  int64_t pos = (int64_t)tot0 + block_excl_scan_256(s, sh, tot);
+#pragma unroll
+  for (int k = 0; k < kPer; ++k) {
+    for (uint32_t r = 0; r < c[k]; ++r, ++pos) {
       if (pos >= T) { atomicOr(&cnt4[row * 4 + 3], 2); break; }
-      const int64_t n = n0 + k;
-      out_idx[row * T + pos] = n;
+      out_idx[row * T + pos] = n0 + k;
       float* d = out_pts + (row * T + pos) * 3;
-      d[0] = P[n * 3 + 0]; d[1] = P[n * 3 + 1]; d[2] = P[n * 3 + 2];
+      d[0] = q[3 * k]; d[1] = q[3 * k + 1]; d[2] = q[3 * k + 2];
     }
   }
 }
