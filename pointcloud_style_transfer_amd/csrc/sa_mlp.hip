@@ -94,22 +94,36 @@ __global__ __launch_bounds__(256) void pw_linear_kernel(const float* __restrict_
 
 // Deterministic per-channel statistics of Z [M, O]: partial float64 sums over row chunks,
 // then an in-order combine.  mean[o], var[o] (biased, as BatchNorm normalises with).
-constexpr int kStatChunks = 64;
+// A 256-thread block covers TO = min(O, 64) channels x (256 / TO) row lanes of one chunk
+// (coalesced rows, every lane busy for narrow layers); the lanes fold in a fixed order.
+constexpr int kStatChunks = 256;
 
-__global__ void channel_partial_kernel(const float* __restrict__ Z, int64_t M, int O,
-                                       const double* __restrict__ mean, double* __restrict__ part) {
-  const int o = blockIdx.x * 256 + threadIdx.x;
-  const int chunk = blockIdx.y;
-  if (o >= O) return;
+__global__ __launch_bounds__(256) void channel_partial_kernel(const float* __restrict__ Z, int64_t M,
+                                                              int O, const double* __restrict__ mean,
+                                                              double* __restrict__ part) {
+  const int TO = O < 64 ? O : 64;
+  const int RL = 256 / TO;
+  const int oc = threadIdx.x % TO, rl = threadIdx.x / TO;
+  const int o = blockIdx.y * TO + oc;
+  const int chunk = blockIdx.x;
   const int64_t per = (M + kStatChunks - 1) / kStatChunks;
   const int64_t a = chunk * per, e = a + per < M ? a + per : M;
+  __shared__ double sh[256];
   double s = 0.0;
-  const double mu = mean ? mean[o] : 0.0;
-  for (int64_t m = a; m < e; ++m) {
-    const double v = (double)Z[m * O + o] - mu;
-    s += mean ? v * v : v;
+  if (rl < RL && o < O) {
+    const double mu = mean ? mean[o] : 0.0;
+    for (int64_t m = a + rl; m < e; m += RL) {
+      const double v = (double)Z[m * O + o] - mu;
+      s += mean ? v * v : v;
+    }
   }
-  part[(int64_t)chunk * O + o] = s;
+  sh[threadIdx.x] = s;
+  __syncthreads();
+  if (rl == 0 && o < O) {
+    double t = 0.0;
+    for (int q = 0; q < RL; ++q) t += sh[q * TO + oc];
+    part[(int64_t)chunk * O + o] = t;
+  }
 }
 
 __global__ void channel_combine_kernel(const double* __restrict__ part, int64_t M, int O,
@@ -279,7 +293,7 @@ extern "C" int pcst_channel_stats(const float* Z, int64_t M, int64_t O, double* 
   PCST_CHECK_ARG(M > 0 && O > 0, "channel_stats: bad shape");
   hipStream_t s = as_stream(stream);
   double* part = static_cast<double*>(workspace);
-  dim3 g((unsigned)cdiv(O, 256), kStatChunks);
+  dim3 g(kStatChunks, (unsigned)cdiv(O, O < 64 ? O : 64));
   hipLaunchKernelGGL(channel_partial_kernel, g, dim3(256), 0, s, Z, M, (int)O, (const double*)nullptr, part);
   hipLaunchKernelGGL(channel_combine_kernel, dim3((unsigned)cdiv(O, 256)), dim3(256), 0, s, part, M, (int)O, mean);
   hipLaunchKernelGGL(channel_partial_kernel, g, dim3(256), 0, s, Z, M, (int)O, (const double*)mean, part);
