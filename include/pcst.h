@@ -223,10 +223,12 @@ int pcst_voxel_downsample_copies_dseed(const float* pts, int64_t B, int64_t N, i
 
 /* chamfer_distance_chunked_optimized (losses.py:8-63), never materialising N x M:
  * min1/arg1 [B,N] = row minima pred->target of clamp((|p|^2+|q|^2) + (-2 p.q), 0) (first index
- * on ties), min2/arg2 [B,M] target->pred, out [B] = mean(min1) + mean(min2) (may be NULL). */
+ * on ties), min2/arg2 [B,M] target->pred, out [B] = mean(min1) + mean(min2) (may be NULL).
+ * workspace: both clouds repacked as point pairs for the packed-fp32 row-min kernel. */
+int pcst_chamfer_fwd_workspace_size(int64_t B, int64_t N, int64_t M, size_t* bytes);
 int pcst_chamfer_fwd(const float* pred, const float* target, int64_t B, int64_t N, int64_t M,
                      float* min1, int32_t* arg1, float* min2, int32_t* arg2, float* out,
-                     void* stream);
+                     void* workspace, void* stream);
 /* Gradient of sum_b grad_out[b]*chamfer[b]; ACCUMULATES into grad_pred [B,N,3] and/or
  * grad_target [B,M,3] (either may be NULL).  Deterministic (sorted scatter, no float atomics). */
 int pcst_chamfer_bwd_workspace_size(int64_t B, int64_t N, int64_t M, size_t* bytes);

@@ -68,7 +68,8 @@ SIGNATURES = {
     "pcst_channel_stats_workspace_size": [_I, _SZ],
     "pcst_channel_stats": [_P, _I, _I, _P, _P, _P, _P],
     "pcst_affine_act": [_P, _I, _I, _P, _P, ctypes.c_int, _I, _P, _P],
-    "pcst_chamfer_fwd": [_P, _P, _I, _I, _I, _P, _P, _P, _P, _P, _P],
+    "pcst_chamfer_fwd_workspace_size": [_I, _I, _I, _SZ],
+    "pcst_chamfer_fwd": [_P, _P, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P],
     "pcst_chamfer_bwd_workspace_size": [_I, _I, _I, _SZ],
     "pcst_chamfer_bwd": [_P, _P, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P],
     "pcst_bn_train_coeffs": [_P, _P, _I, _I, _P, _P, _D, _D, _P, _P, _P, _P, _P, _P],
@@ -557,8 +558,9 @@ def chamfer_fwd(pred, target):
     arg1 = torch.empty(B, N, dtype=torch.int32, device=dev)
     arg2 = torch.empty(B, M, dtype=torch.int32, device=dev)
     out = torch.empty(B, dtype=torch.float32, device=dev)
+    ws = _workspace("pcst_chamfer_fwd_workspace_size", B, N, M, device=dev)
     _call("pcst_chamfer_fwd", _ptr(pred), _ptr(target), B, N, M, _ptr(min1), _ptr(arg1),
-          _ptr(min2), _ptr(arg2), _ptr(out), _stream())
+          _ptr(min2), _ptr(arg2), _ptr(out), _ptr(ws), _stream())
     return out, arg1, arg2
 
 

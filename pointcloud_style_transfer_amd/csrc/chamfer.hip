@@ -3,9 +3,9 @@
 //
 // Forward, per direction: D = (|p|^2 + |q|^2) + (-2 p.q) with the reference's rounding
 // (dot = K=3 sgemm fma chain, unfused norms; -2*dot is exact so the final add is one fma),
-// clamp >= 0, row min with the first index on ties.  Targets stream through LDS in tiles of
-// 2048 points; each thread owns one query.  Never materialises the N x M matrix (the reference
-// chunks 1024 rows to bound it).  Means are reduced deterministically (fixed-order float64).
+// clamp >= 0, row min with the first index on ties.  Each thread owns one query row; the other
+// cloud streams through scalar loads in packed point pairs (v_pk_* math, see below).  Never
+// materialises the N x M matrix (the reference chunks 1024 rows to bound it).  Means are reduced deterministically (fixed-order float64).
 //
 // Backward (autograd of the reference formula): for a row i with argmin j and raw D >= 0,
 // dL/dp_i += g/N * 2(p_i - q_j) and dL/dq_j -= the same.  The scatter onto the argmin side is
@@ -16,49 +16,196 @@
 
 namespace pcst {
 
-constexpr int kCdTile = 2048;
-
 __device__ __forceinline__ float cd_dist(float px, float py, float pz, float np_, float qx,
                                          float qy, float qz, float nq) {
   const float dot = dot3(px, py, pz, qx, qy, qz);
   return ffma(-2.0f, dot, fadd(np_, nq));
 }
 
-// one direction: for every query row of P [B,N,3], min over Q [B,M,3]
-__global__ __launch_bounds__(256) void chamfer_rowmin_kernel(const float* __restrict__ P,
-                                                             const float* __restrict__ Q, int N,
-                                                             int M, float* __restrict__ mind,
-                                                             int32_t* __restrict__ argm) {
-  __shared__ float4 sq[kCdTile];
+// Row minima on packed fp32 math.  The D-side cloud is first repacked per point pair as
+// {x0,x1,y0,y1} {z0,z1,n0,n1} (n = |q|^2; padding pairs carry n = +inf), so every v_pk_* op
+// evaluates two pairs.  With m = -2p (a power-of-two scaling: every rounding step of the sgemm
+// dot commutes with it), D = (|p|^2 + n) + fma(mz, z, fma(my, y, mx * x)) is bit-identical to
+// cd_dist.  Since clamp(., 0) is monotone, min_k clamp(D_k) = clamp(min_k D_k): the inner loop
+// keeps one raw minimum (v_min3 over two pairs) per chunk of kCdChunk points, the row keeps the
+// first chunk reaching its best clamped value, and that chunk is re-scanned for the first index
+// with clamp(D) == best -- the reference's first-index argmin of the clamped matrix.  The packed
+// pairs are wave-uniform, so they arrive by scalar loads and cost no LDS traffic.
+typedef float cd_f2 __attribute__((ext_vector_type(2)));
+constexpr int kCdChunk = 256;  // points per argmin chunk (128 pairs)
+
+__global__ void chamfer_pack_kernel(const float* __restrict__ Q, int M, int Mp,
+                                    float4* __restrict__ Qp) {
   const int b = blockIdx.y;
-  const int i = blockIdx.x * 256 + threadIdx.x;
-  const bool valid = i < N;
-  const float* p = P + ((int64_t)b * N + (valid ? i : 0)) * 3;
-  const float px = p[0], py = p[1], pz = p[2];
-  const float np_ = sqnorm3(px, py, pz);
-  float best = INFINITY;
-  int bj = 0;
-  const float* Qb = Q + (int64_t)b * M * 3;
-  for (int t0 = 0; t0 < M; t0 += kCdTile) {
-    const int tn = min(kCdTile, M - t0);
-    __syncthreads();
-    for (int k = threadIdx.x; k < tn; k += 256) {
-      const float* q = Qb + (int64_t)(t0 + k) * 3;
-      const float qx = q[0], qy = q[1], qz = q[2];
-      sq[k] = make_float4(qx, qy, qz, sqnorm3(qx, qy, qz));
-    }
-    __syncthreads();
-#pragma unroll 4
-    for (int k = 0; k < tn; ++k) {
-      const float4 q = sq[k];
-      float d = cd_dist(px, py, pz, np_, q.x, q.y, q.z, q.w);
-      d = d < 0.0f ? 0.0f : d;
-      if (d < best) { best = d; bj = t0 + k; }
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;  // pair index
+  if (2 * j >= Mp) return;
+  float v[2][4];
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int k = 2 * j + u;
+    if (k < M) {
+      const float* q = Q + ((int64_t)b * M + k) * 3;
+      v[u][0] = q[0];
+      v[u][1] = q[1];
+      v[u][2] = q[2];
+      v[u][3] = sqnorm3(v[u][0], v[u][1], v[u][2]);
+    } else {
+      v[u][0] = v[u][1] = v[u][2] = 0.0f;
+      v[u][3] = INFINITY;
     }
   }
-  if (valid) {
-    mind[(int64_t)b * N + i] = best;
-    argm[(int64_t)b * N + i] = bj;
+  float4* o = Qp + ((int64_t)b * (Mp / 2) + j) * 2;
+  o[0] = make_float4(v[0][0], v[1][0], v[0][1], v[1][1]);
+  o[1] = make_float4(v[0][2], v[1][2], v[0][3], v[1][3]);
+}
+
+// raw D of 4 packed pairs (8 points) against R rows, folded into cmin[R]
+template <int R>
+__device__ __forceinline__ void cd_minpairs(const float4 (&q)[8], const cd_f2 (&mx2)[R],
+                                            const cd_f2 (&my2)[R], const cd_f2 (&mz2)[R],
+                                            const cd_f2 (&np2)[R], float (&cmin)[R]) {
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const float4 a = q[2 * u], e = q[2 * u + 1];
+    const cd_f2 x = {a.x, a.y}, y = {a.z, a.w}, z = {e.x, e.y}, n = {e.z, e.w};
+#pragma unroll
+    for (int w = 0; w < R; ++w) {
+      cd_f2 t = mx2[w] * x;
+      t = __builtin_elementwise_fma(my2[w], y, t);
+      t = __builtin_elementwise_fma(mz2[w], z, t);
+      const cd_f2 d = (np2[w] + n) + t;
+      cmin[w] = fminf(cmin[w], fminf(d.x, d.y));
+    }
+  }
+}
+
+// Block = S segments x 256 threads; a thread owns R rows (r + 256 w) of the block's 256 R rows
+// against segment s's chunks [s*per, (s+1)*per).  R rows share every scalar load; S segments
+// put more waves in flight.  The block combines the segments' (best, first chunk) in segment
+// order, and the winning chunk's re-scan is split over the S segments the same way.
+template <int S, int R>
+__global__ __launch_bounds__(256 * S) void chamfer_rowmin_kernel(const float* __restrict__ P,
+                                                                 const float4* __restrict__ Qp,
+                                                                 int N, int M, int Mp,
+                                                                 float* __restrict__ mind,
+                                                                 int32_t* __restrict__ argm) {
+  __shared__ float sbest[S][256 * R];
+  __shared__ int sidx[S][256 * R];
+  const int b = blockIdx.y;
+  const int r = threadIdx.x & 255;
+  const int seg = __builtin_amdgcn_readfirstlane(threadIdx.x >> 8);  // wave-uniform
+  float mx[R], my[R], mz[R], np_[R];
+  cd_f2 mx2[R], my2[R], mz2[R], np2[R];
+#pragma unroll
+  for (int w = 0; w < R; ++w) {
+    const int i = blockIdx.x * 256 * R + w * 256 + r;
+    const float* p = P + ((int64_t)b * N + (i < N ? i : 0)) * 3;
+    const float px = p[0], py = p[1], pz = p[2];
+    np_[w] = sqnorm3(px, py, pz);
+    mx[w] = -2.0f * px;
+    my[w] = -2.0f * py;
+    mz[w] = -2.0f * pz;
+    mx2[w] = cd_f2{mx[w], mx[w]};
+    my2[w] = cd_f2{my[w], my[w]};
+    mz2[w] = cd_f2{mz[w], mz[w]};
+    np2[w] = cd_f2{np_[w], np_[w]};
+  }
+  const float4* __restrict__ Qb = Qp + (int64_t)b * Mp;  // Mp/2 pairs x 2 float4
+  const int chunks = Mp / kCdChunk;
+  const int per = (chunks + S - 1) / S;
+  const int c0 = seg * per, c1 = c0 + per < chunks ? c0 + per : chunks;
+  float best[R];
+  int bchunk[R];
+#pragma unroll
+  for (int w = 0; w < R; ++w) {
+    best[w] = INFINITY;
+    bchunk[w] = 0;
+  }
+  for (int c = c0; c < c1; ++c) {
+    const float4* __restrict__ Qc = Qb + c * kCdChunk;
+    float cmin[R];
+#pragma unroll
+    for (int w = 0; w < R; ++w) cmin[w] = INFINITY;
+    // two 4-pair stages ping-pong in scalar registers
+    float4 A[8], Bq[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) A[u] = Qc[u];
+    for (int k = 0; k < kCdChunk / 2; k += 8) {
+#pragma unroll
+      for (int u = 0; u < 8; ++u) Bq[u] = Qc[2 * (k + 4) + u];
+      cd_minpairs<R>(A, mx2, my2, mz2, np2, cmin);
+      const int kn = k + 8 < kCdChunk / 2 ? k + 8 : k;  // the last reload is a harmless repeat
+#pragma unroll
+      for (int u = 0; u < 8; ++u) A[u] = Qc[2 * kn + u];
+      cd_minpairs<R>(Bq, mx2, my2, mz2, np2, cmin);
+    }
+#pragma unroll
+    for (int w = 0; w < R; ++w) {
+      const float cm = fmaxf(cmin[w], 0.0f);
+      if (cm < best[w]) {
+        best[w] = cm;
+        bchunk[w] = c;
+      }
+    }
+  }
+  if (S > 1) {
+#pragma unroll
+    for (int w = 0; w < R; ++w) {
+      sbest[seg][w * 256 + r] = best[w];
+      sidx[seg][w * 256 + r] = bchunk[w];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int w = 0; w < R; ++w) {
+      best[w] = INFINITY;
+      bchunk[w] = 0;
+#pragma unroll
+      for (int t = 0; t < S; ++t)
+        if (sbest[t][w * 256 + r] < best[w]) {  // strict: the earliest segment wins ties
+          best[w] = sbest[t][w * 256 + r];
+          bchunk[w] = sidx[t][w * 256 + r];
+        }
+    }
+    __syncthreads();
+  }
+  // first index of the winning chunk whose clamped distance equals best; segment s scans its
+  // 256/S points of the chunk
+  constexpr int kPer = kCdChunk / S;
+  int found[R];
+#pragma unroll
+  for (int w = 0; w < R; ++w) {
+    found[w] = kCdChunk;
+    const float4* Qc = Qb + bchunk[w] * kCdChunk;
+    for (int k = seg * kPer; k < (seg + 1) * kPer; ++k) {
+      const float4 a = Qc[2 * (k >> 1)], e = Qc[2 * (k >> 1) + 1];
+      const int u = k & 1;
+      const float x = u ? a.y : a.x, y = u ? a.w : a.z, z = u ? e.y : e.x, n = u ? e.w : e.z;
+      const float t = ffma(mz[w], z, ffma(my[w], y, fmul(mx[w], x)));
+      const float d = fadd(fadd(np_[w], n), t);
+      if (fmaxf(d, 0.0f) == best[w]) {
+        found[w] = k;
+        break;
+      }
+    }
+  }
+  if (S > 1) {
+#pragma unroll
+    for (int w = 0; w < R; ++w) sidx[seg][w * 256 + r] = found[w];
+    __syncthreads();
+    if (seg != 0) return;
+#pragma unroll
+    for (int w = 0; w < R; ++w)
+#pragma unroll
+      for (int t = 1; t < S; ++t) found[w] = min(found[w], sidx[t][w * 256 + r]);
+  }
+#pragma unroll
+  for (int w = 0; w < R; ++w) {
+    const int i = blockIdx.x * 256 * R + w * 256 + r;
+    const int bj = bchunk[w] * kCdChunk + (found[w] < kCdChunk ? found[w] : 0);
+    if (i < N) {
+      mind[(int64_t)b * N + i] = best[w];
+      argm[(int64_t)b * N + i] = bj < M ? bj : 0;
+    }
   }
 }
 
@@ -221,19 +368,54 @@ static CdWS carve_cd(void* base, int64_t B, int64_t R) {
 
 using namespace pcst;
 
+static inline int64_t cd_padded(int64_t n) { return cdiv(n, kCdChunk) * kCdChunk; }
+
+extern "C" int pcst_chamfer_fwd_workspace_size(int64_t B, int64_t N, int64_t M, size_t* bytes) {
+  PCST_CHECK_ARG(B >= 0 && N > 0 && M > 0 && bytes, "chamfer_fwd_workspace_size: bad args");
+  *bytes = sizeof(float) * 4 * (size_t)B * (size_t)(cd_padded(N) + cd_padded(M));
+  return PCST_OK;
+}
+
 extern "C" int pcst_chamfer_fwd(const float* pred, const float* target, int64_t B, int64_t N,
                                 int64_t M, float* min1, int32_t* arg1, float* min2,
-                                int32_t* arg2, float* out, void* stream) {
-  PCST_CHECK_ARG(B >= 0 && N > 0 && M > 0 && N < (1ll << 31) && M < (1ll << 31), "chamfer_fwd: bad shape");
+                                int32_t* arg2, float* out, void* workspace, void* stream) {
+  PCST_CHECK_ARG(B >= 0 && N > 0 && M > 0 && N < (1ll << 30) && M < (1ll << 30), "chamfer_fwd: bad shape");
   if (B == 0) return PCST_OK;
+  PCST_CHECK_ARG(pred && target && min1 && arg1 && min2 && arg2 && workspace, "chamfer_fwd: null pointer");
   hipStream_t s = as_stream(stream);
-  hipLaunchKernelGGL(chamfer_rowmin_kernel, dim3((unsigned)cdiv(N, 256), (unsigned)B), dim3(256), 0,
-                     s, pred, target, (int)N, (int)M, min1, arg1);
-  hipLaunchKernelGGL(chamfer_rowmin_kernel, dim3((unsigned)cdiv(M, 256), (unsigned)B), dim3(256), 0,
-                     s, target, pred, (int)M, (int)N, min2, arg2);
+  const int64_t Np = cd_padded(N), Mp = cd_padded(M);
+  float4* Pp = static_cast<float4*>(workspace);  // pred packed, B x Np/2 pairs x 2
+  float4* Tp = Pp + B * Np;                       // target packed
+  const unsigned b = (unsigned)B;
+  hipLaunchKernelGGL(chamfer_pack_kernel, dim3((unsigned)cdiv(Np / 2, 256), b), dim3(256), 0, s,
+                     pred, (int)N, (int)Np, Pp);
+  hipLaunchKernelGGL(chamfer_pack_kernel, dim3((unsigned)cdiv(Mp / 2, 256), b), dim3(256), 0, s,
+                     target, (int)M, (int)Mp, Tp);
+  static const int variant = [] {  // S x R experiment knob: 11, 21, 41, 12, 22, 14
+    const char* e = getenv("PCST_CD_VARIANT");
+    return e ? atoi(e) : 21;
+  }();
+  auto rowmin = [&](const float* P, const float4* Qp, int64_t n, int64_t m, int64_t mp, float* md,
+                    int32_t* am) {
+#define PCST_CD_LAUNCH(S_, R_)                                                                  \
+  hipLaunchKernelGGL((chamfer_rowmin_kernel<S_, R_>), dim3((unsigned)cdiv(n, 256 * R_), b),    \
+                     dim3(256 * S_), 0, s, P, Qp, (int)n, (int)m, (int)mp, md, am)
+    switch (variant) {
+      case 11: PCST_CD_LAUNCH(1, 1); break;
+      case 41: PCST_CD_LAUNCH(4, 1); break;
+      case 12: PCST_CD_LAUNCH(1, 2); break;
+      case 22: PCST_CD_LAUNCH(2, 2); break;
+      case 14: PCST_CD_LAUNCH(1, 4); break;
+      case 42: PCST_CD_LAUNCH(4, 2); break;
+      default: PCST_CD_LAUNCH(2, 1); break;
+    }
+#undef PCST_CD_LAUNCH
+  };
+  rowmin(pred, Tp, N, M, Mp, min1, arg1);
+  rowmin(target, Pp, M, N, Np, min2, arg2);
   if (out)
-    hipLaunchKernelGGL(chamfer_mean_kernel, dim3((unsigned)B), dim3(256), 0, s, min1, (int)N, min2,
-                       (int)M, out);
+    hipLaunchKernelGGL(chamfer_mean_kernel, dim3(b), dim3(256), 0, s, min1, (int)N, min2, (int)M,
+                       out);
   PCST_LAUNCH_CHECK("chamfer_fwd");
   return PCST_OK;
 }
