@@ -140,6 +140,33 @@ int pcst_linear_wgrad_bf16_workspace_size(int64_t M, int64_t I, int64_t O, size_
 int pcst_linear_wgrad_bf16(const float* dZ, const float* X, int64_t M, int64_t I, int64_t O,
                            float* dW, float* db, void* workspace, void* stream);
 
+/* Training GEMMs with bf16 activation storage and fused epilogues (csrc/train_mlp.hip): the
+ * NoisePredictor residual block x + Dropout(Linear2(ReLU(Linear1(x)))) (diffusion_model.py:48-52,
+ * 57-58) and its backward.  bf16 buffers are uint16_t (raw bfloat16 bits).  A [M,K] and B [O,K]
+ * are fp32 (rounded to bf16 when staged) or bf16 per a_bf16/b_bf16; O % 4 == 0, K % 8 == 0 for a
+ * bf16 operand (% 4 for fp32); all pointers 16-byte aligned.  epilogue:
+ *   0 EP_F32         C fp32 = act(acc + bias)
+ *   1 EP_BF16        C bf16 = act(acc + bias)
+ *   2 EP_RESID_DROP  C fp32 = aux_fp32 + keep(e) * (acc + bias) / (1 - drop_p)
+ *   3 EP_RELU_MASK   C bf16 = acc * [aux_bf16 > 0]
+ *   4 EP_ADD         C fp32 = acc + aux_fp32
+ *   5 EP_COND        C fp32 = ((acc + bias) + aux[g,0,:]) + aux[g,1,:],  g = m / group_rows
+ * C2 (may be NULL): bf16 copy of an fp32 C.  O % 4 == 0 except for EP_F32/EP_BF16.
+ * keep(e) for element e = m*O + o is hash(seed, e) >= drop_p * 2^32: a pure function of
+ * (seed, e), regenerated by pcst_dropout_grad_bf16 (out bf16 = g * keep * 1/(1-p), n % 4 == 0).
+ * bf16 A with bf16 B runs the pipelined kernel (64-deep K slices, two in flight). */
+int pcst_gemm_ex(const void* A, int a_bf16, int64_t M, int64_t K, const void* B, int b_bf16,
+                 int64_t O, const float* bias, int relu, int epilogue, const void* aux,
+                 uint64_t seed, float drop_p, int64_t group_rows, void* C, uint16_t* C2,
+                 void* stream);
+int pcst_dropout_grad_bf16(const float* g, int64_t n, uint64_t seed, float drop_p, uint16_t* out,
+                           void* stream);
+/* dW [O,I] = dZ^T X, db [O] = column sums of dZ (may be NULL), dZ [M,O] / X [M,I] fp32 or bf16;
+ * I % 8 == 0, O % 8 == 0.  Deterministic (chunk partials combined in order). */
+int pcst_linear_wgrad_ex_workspace_size(int64_t M, int64_t I, int64_t O, size_t* bytes);
+int pcst_linear_wgrad_ex(const void* dZ, int dz_bf16, const void* X, int x_bf16, int64_t M,
+                         int64_t I, int64_t O, float* dW, float* db, void* workspace, void* stream);
+
 /* ---- models/diffusion_model.py --------------------------------------------------------- */
 
 /* HierarchicalProcessor._voxel_grid_downsample_torch (diffusion_model.py:69-122) for all B

@@ -62,6 +62,11 @@ SIGNATURES = {
     "pcst_gemm_nt_bf16": [_P, _I, _I, _P, _I, _P, _P, ctypes.c_int, _P, _P],
     "pcst_linear_wgrad_bf16_workspace_size": [_I, _I, _I, _SZ],
     "pcst_linear_wgrad_bf16": [_P, _P, _I, _I, _I, _P, _P, _P, _P],
+    "pcst_gemm_ex": [_P, ctypes.c_int, _I, _I, _P, ctypes.c_int, _I, _P, ctypes.c_int,
+                     ctypes.c_int, _P, ctypes.c_uint64, _F, _I, _P, _P, _P],
+    "pcst_dropout_grad_bf16": [_P, _I, ctypes.c_uint64, _F, _P, _P],
+    "pcst_linear_wgrad_ex_workspace_size": [_I, _I, _I, _SZ],
+    "pcst_linear_wgrad_ex": [_P, ctypes.c_int, _P, ctypes.c_int, _I, _I, _I, _P, _P, _P, _P],
     "pcst_relu_bwd": [_P, _P, _I, _P, _P],
     "pcst_linear_wgrad_workspace_size": [_I, _I, _I, _SZ],
     "pcst_linear_wgrad": [_P, _P, _I, _I, _I, _P, _P, _P, _P],
@@ -454,6 +459,79 @@ def gemm_nt_bf16(A, B, scale=None, shift=None, relu=False):
     return C
 
 
+EP_F32, EP_BF16, EP_RESID_DROP, EP_RELU_MASK, EP_ADD, EP_COND = range(6)
+_EP_BF16_OUT = (EP_BF16, EP_RELU_MASK)
+
+
+def _f32_or_bf16(t):
+    if t.dtype == torch.bfloat16:
+        return t.contiguous(), 1
+    return _f32(t), 0
+
+
+def gemm_ex(A, B, bias=None, relu=False, epilogue=EP_F32, aux=None, seed=0, p=0.0,
+            group_rows=0, copy_bf16=False):
+    """A [M,K], B [O,K] (fp32 or bf16) -> epilogue(A B^T) on bf16 MFMA (csrc/train_mlp.hip):
+    EP_F32/EP_BF16 act(acc+bias) as fp32/bf16, EP_RESID_DROP aux + dropout_p(acc+bias) (fp32),
+    EP_RELU_MASK acc*[aux>0] (bf16, aux bf16), EP_ADD acc + aux (fp32), EP_COND
+    ((acc+bias) + aux[g,0]) + aux[g,1] with g = row // group_rows (fp32).  copy_bf16 (fp32
+    outputs): also return a bf16 copy, (C, C_bf16)."""
+    require_device(A, B, bias, aux)
+    A, a16 = _f32_or_bf16(A)
+    B, b16 = _f32_or_bf16(B)
+    M, K = A.shape
+    O = B.shape[0]
+    if B.shape[1] != K:
+        raise RuntimeError(f"gemm_ex: K mismatch {tuple(A.shape)} vs {tuple(B.shape)}")
+    bias = None if bias is None else _f32(bias)
+    if aux is not None:
+        want = torch.bfloat16 if epilogue == EP_RELU_MASK else torch.float32
+        shape = (M // max(group_rows, 1), 2, O) if epilogue == EP_COND else (M, O)
+        if aux.dtype != want or tuple(aux.shape) != shape:
+            raise RuntimeError(f"gemm_ex: aux must be {want} {list(shape)}, got "
+                               f"{aux.dtype} {list(aux.shape)}")
+        aux = aux.contiguous()
+    out_dtype = torch.bfloat16 if epilogue in _EP_BF16_OUT else torch.float32
+    C = torch.empty(M, O, dtype=out_dtype, device=A.device)
+    C2 = None
+    if copy_bf16:
+        if out_dtype != torch.float32:
+            raise RuntimeError("gemm_ex: copy_bf16 needs an fp32 epilogue")
+        C2 = torch.empty(M, O, dtype=torch.bfloat16, device=A.device)
+    _call("pcst_gemm_ex", _ptr(A), a16, M, K, _ptr(B), b16, O, _ptr(bias), int(relu),
+          int(epilogue), _ptr(aux), int(seed) & (2**64 - 1), float(p), int(group_rows), _ptr(C),
+          _ptr(C2), _stream())
+    return (C, C2) if copy_bf16 else C
+
+
+def dropout_grad_bf16(g, seed, p):
+    """Dropout backward with the mask regenerated from (seed, element index): bf16(g*keep/(1-p))."""
+    require_device(g)
+    g = _f32(g)
+    out = torch.empty(g.shape, dtype=torch.bfloat16, device=g.device)
+    _call("pcst_dropout_grad_bf16", _ptr(g), g.numel(), int(seed) & (2**64 - 1), float(p),
+          _ptr(out), _stream())
+    return out
+
+
+def linear_wgrad_ex(dZ, X, bias=True):
+    """dZ [M,O], X [M,I] (fp32 or bf16) -> (dW = dZ^T X [O,I], db [O] or None) on bf16 MFMA,
+    deterministic."""
+    require_device(dZ, X)
+    dZ, z16 = _f32_or_bf16(dZ)
+    X, x16 = _f32_or_bf16(X)
+    M, O = dZ.shape
+    I = X.shape[1]
+    if X.shape[0] != M:
+        raise RuntimeError(f"linear_wgrad_ex: row mismatch {tuple(dZ.shape)} vs {tuple(X.shape)}")
+    ws = _workspace("pcst_linear_wgrad_ex_workspace_size", M, I, O, device=dZ.device)
+    dW = torch.empty(O, I, dtype=torch.float32, device=dZ.device)
+    db = torch.empty(O, dtype=torch.float32, device=dZ.device) if bias else None
+    _call("pcst_linear_wgrad_ex", _ptr(dZ), z16, _ptr(X), x16, M, I, O, _ptr(dW), _ptr(db),
+          _ptr(ws), _stream())
+    return dW, db
+
+
 def channel_stats(Z):
     """Per-channel (mean, biased var) of Z [M,O] as float64 device tensors (deterministic)."""
     require_device(Z)
@@ -673,7 +751,8 @@ _GUARDED = ("square_distance", "index_points", "fps", "ball_query", "group_gathe
             "linear_wgrad", "gemm_nt_bf16", "channel_stats", "affine_act", "chamfer_fwd",
             "chamfer_bwd", "l1_fwd", "l1_bwd", "knn_dist", "emd_greedy", "voxel_center_dist",
             "cfg_ddim_step_dcoef", "voxel_downsample_copies_dseed", "bn_train_coeffs",
-            "bn_relu_maxpool", "bn_relu_bwd", "group_gather_bwd")
+            "bn_relu_maxpool", "bn_relu_bwd", "group_gather_bwd", "gemm_ex", "dropout_grad_bf16",
+            "linear_wgrad_ex")
 for _name in _GUARDED:
     globals()[_name] = _on_tensor_device(globals()[_name])
 del _name

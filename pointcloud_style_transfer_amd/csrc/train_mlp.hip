@@ -1,0 +1,1103 @@
+// Training-path GEMMs with bf16 activation storage and fused epilogues (the NoisePredictor's
+// residual blocks, reference models/diffusion_model.py:48-52,57-58, trained under autocast by
+// training/trainer.py:81-106).  Every product runs on v_mfma_f32_32x32x16_bf16 with fp32
+// accumulation; operands are bf16 either in HBM (activations written by a previous epilogue)
+// or rounded from fp32 while staged, so storing an activation as bf16 changes no product.
+//
+//   gemm_ex:   C[m, o] = epilogue(sum_k A[m, k] B[o, k])          forward and dX
+//     EP_F32         act(acc + bias)                     -> fp32
+//     EP_BF16        act(acc + bias)                     -> bf16
+//     EP_RESID_DROP  resid + keep(m, o) * (acc + bias) * s -> fp32  (x + Dropout(Linear2(h)))
+//     EP_RELU_MASK   acc * [h > 0]                       -> bf16  (ReLU backward of Linear1)
+//     EP_ADD         acc + add                           -> fp32  (residual gradient sum)
+//   wgrad_ex:  dW[o, i] = sum_m dZ[m, o] X[m, i],  db[o] = sum_m dZ[m, o]
+//   dropout_grad: dD = bf16(g * keep * s)  (Dropout backward, the mask regenerated)
+//
+// Dropout keeps element e = m * O + o iff hash(seed, e) >= p * 2^32: the mask is a pure function
+// of (seed, e), so the backward regenerates it instead of storing it.
+//
+// gemm_ex tiles 128 x 128 per 256-thread workgroup (2 x 2 waves of 64 x 64, K staged 32 deep,
+// software-pipelined through registers), maps tiles to workgroups so that the O-tiles of one
+// M-tile run on one XCD back to back (the A rows are read from HBM once, then hit that XCD's
+// L2), and writes the tile through LDS so the epilogue reads/writes rows with 16-byte accesses.
+// wgrad_ex stages dZ and X row-major (coalesced) and feeds both MFMA operands with
+// ds_read_b64_tr_b16 transposed reads; the M reduction is split into chunks whose partials are
+// combined in chunk order (deterministic), as csrc/train_gemm.hip does.
+#include "common.h"
+
+namespace pcst {
+
+typedef __attribute__((ext_vector_type(16))) float f32x16;
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+typedef short v4i16 __attribute__((ext_vector_type(4)));
+
+enum { EP_F32 = 0, EP_BF16 = 1, EP_RESID_DROP = 2, EP_RELU_MASK = 3, EP_ADD = 4, EP_COND = 5 };
+
+constexpr int kXT = 128, kXK = 32, kXLd = 40;  // tile, k slice, LDS row (bf16 elements, 80 B)
+constexpr int kCLd = 132;                      // epilogue LDS row (floats)
+
+__device__ __forceinline__ int xrow(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
+
+__device__ __forceinline__ uint32_t mix32(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x7feb352du;
+  x ^= x >> 15;
+  x *= 0x846ca68bu;
+  x ^= x >> 16;
+  return x;
+}
+// dropout draw of element e under a 64-bit seed
+__device__ __forceinline__ uint32_t drop_hash(uint32_t slo, uint32_t shi, uint64_t e) {
+  return mix32((uint32_t)e ^ slo ^ mix32((uint32_t)(e >> 32) + shi));
+}
+
+// ---- operand staging: rows [r0, r0+128) x k [k0, k0+32) of a row-major [R, K] matrix -> bf16 LDS
+template <typename T>
+struct XStage;
+
+template <>
+struct XStage<float> {  // K % 4 == 0
+  float4 v[4];
+  __device__ __forceinline__ void load(const float* __restrict__ S, int64_t R, int K, int64_t r0,
+                                       int k0, int tid) {
+#pragma unroll
+    for (int it = 0; it < 4; ++it) {
+      const int f = tid + 256 * it;
+      const int r = f >> 3, kc = (f & 7) * 4;
+      const int64_t row = r0 + r;
+      v[it] = (row < R && k0 + kc < K) ? *reinterpret_cast<const float4*>(S + row * K + k0 + kc)
+                                       : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  }
+  __device__ __forceinline__ void store(__bf16 (*D)[kXLd], int tid) const {
+#pragma unroll
+    for (int it = 0; it < 4; ++it) {
+      const int f = tid + 256 * it;
+      const int r = f >> 3, kc = (f & 7) * 4;
+      bf16x4 o;
+      o[0] = (__bf16)v[it].x;
+      o[1] = (__bf16)v[it].y;
+      o[2] = (__bf16)v[it].z;
+      o[3] = (__bf16)v[it].w;
+      *reinterpret_cast<bf16x4*>(&D[r][kc]) = o;
+    }
+  }
+};
+
+template <>
+struct XStage<uint16_t> {  // bf16 storage, K % 8 == 0
+  uint4 v[2];
+  __device__ __forceinline__ void load(const uint16_t* __restrict__ S, int64_t R, int K,
+                                       int64_t r0, int k0, int tid) {
+#pragma unroll
+    for (int it = 0; it < 2; ++it) {
+      const int f = tid + 256 * it;
+      const int r = f >> 2, kc = (f & 3) * 8;
+      const int64_t row = r0 + r;
+      v[it] = (row < R && k0 + kc < K) ? *reinterpret_cast<const uint4*>(S + row * K + k0 + kc)
+                                       : make_uint4(0u, 0u, 0u, 0u);
+    }
+  }
+  __device__ __forceinline__ void store(__bf16 (*D)[kXLd], int tid) const {
+#pragma unroll
+    for (int it = 0; it < 2; ++it) {
+      const int f = tid + 256 * it;
+      const int r = f >> 2, kc = (f & 3) * 8;
+      *reinterpret_cast<uint4*>(&D[r][kc]) = v[it];
+    }
+  }
+};
+
+// one 32-deep k slice: 2 x 2 blocks x 2 k-steps of 32x32x16
+__device__ __forceinline__ void xmma_slice(const __bf16 (*As)[kXLd], const __bf16 (*Bs)[kXLd],
+                                           int wr, int wc, int l32, int h, f32x16 (&acc)[2][2]) {
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) {
+    bf16x8 a[2], b[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      a[t] = *reinterpret_cast<const bf16x8*>(&As[wr * 64 + t * 32 + l32][ks * 16 + h * 8]);
+      b[t] = *reinterpret_cast<const bf16x8*>(&Bs[wc * 64 + t * 32 + l32][ks * 16 + h * 8]);
+    }
+#pragma unroll
+    for (int bm = 0; bm < 2; ++bm)
+#pragma unroll
+      for (int bn = 0; bn < 2; ++bn)
+        acc[bm][bn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[bm], b[bn], acc[bm][bn], 0, 0, 0);
+  }
+}
+
+struct GemmExArgs {
+  const float* bias;
+  int relu;
+  const void* aux;  // EP_RESID_DROP: resid fp32 [M,O]; EP_RELU_MASK: h bf16 [M,O]; EP_ADD: fp32;
+                    // EP_COND: [G, 2, O] fp32 (two per-group row vectors added in turn)
+  uint32_t seed_lo, seed_hi, thr;
+  float scale;
+  void* C;
+  uint16_t* C2;     // optional bf16 copy of an fp32 output (EP_F32, EP_RESID_DROP, EP_COND)
+  int64_t group_rows;  // EP_COND: rows per group
+};
+
+__device__ __forceinline__ void store4_bf16(uint16_t* p, float a, float b, float c, float d) {
+  bf16x4 o;
+  o[0] = (__bf16)a;
+  o[1] = (__bf16)b;
+  o[2] = (__bf16)c;
+  o[3] = (__bf16)d;
+  *reinterpret_cast<bf16x4*>(p) = o;
+}
+
+// epilogue: two passes of 64 rows through LDS; thread -> (column quad tid % 32, rows
+// tid / 32 + 8j), 16-byte row accesses for the output and the aux operand
+template <int EP>
+__device__ __forceinline__ void gemm_epilogue(const f32x16 (&acc)[2][2], float (*Cs)[kCLd],
+                                              int64_t M, int O, int64_t m0, int o0,
+                                              const GemmExArgs& args) {
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wr = wid >> 1, wc = wid & 1, h = lane >> 5, l32 = lane & 31;
+  const int cq = (tid & 31) * 4, rl = tid >> 5;
+  const int o = o0 + cq;
+  const int nv = O - o < 4 ? (O - o > 0 ? O - o : 0) : 4;  // valid columns of the quad
+  const bool vec = nv == 4 && (O & 3) == 0;
+  float bias4[4] = {0.f, 0.f, 0.f, 0.f};
+  if (args.bias)
+    for (int u = 0; u < nv; ++u) bias4[u] = args.bias[o + u];
+#pragma unroll
+  for (int pass = 0; pass < 2; ++pass) {
+    if (pass) __syncthreads();
+    if (wr == pass) {
+#pragma unroll
+      for (int bm = 0; bm < 2; ++bm)
+#pragma unroll
+        for (int bn = 0; bn < 2; ++bn)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) Cs[bm * 32 + xrow(r, h)][wc * 64 + bn * 32 + l32] = acc[bm][bn][r];
+    }
+    __syncthreads();
+#pragma unroll 2
+    for (int j = 0; j < 8; ++j) {
+      const int rr = rl + 8 * j;
+      const int64_t m = m0 + pass * 64 + rr;
+      if (m >= M || nv == 0) continue;
+      const float4 c = *reinterpret_cast<const float4*>(&Cs[rr][cq]);
+      const int64_t e = m * O + o;
+      float v[4] = {c.x + bias4[0], c.y + bias4[1], c.z + bias4[2], c.w + bias4[3]};
+      if (EP == EP_RELU_MASK || EP == EP_ADD) {  // no bias on the gradient products
+        v[0] = c.x;
+        v[1] = c.y;
+        v[2] = c.z;
+        v[3] = c.w;
+      }
+      if ((EP == EP_F32 || EP == EP_BF16) && args.relu) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) v[u] = fmaxf(v[u], 0.0f);
+      }
+      float y[4];
+      if (EP == EP_RESID_DROP) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const bool keep = drop_hash(args.seed_lo, args.seed_hi, (uint64_t)(e + u)) >= args.thr;
+          y[u] = keep ? v[u] * args.scale : 0.0f;
+        }
+      } else if (EP == EP_COND) {  // ((acc + b) + cond0[g]) + cond1[g], the reference's order
+        const float* cg = static_cast<const float*>(args.aux) + (m / args.group_rows) * 2 * O + o;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) y[u] = u < nv ? (v[u] + cg[u]) + cg[O + u] : 0.0f;
+      } else {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) y[u] = v[u];
+      }
+      if (EP == EP_RESID_DROP || EP == EP_ADD || EP == EP_RELU_MASK) {
+        if (vec) {
+          if (EP == EP_RELU_MASK) {
+            const uint2 hb = *reinterpret_cast<const uint2*>(static_cast<const uint16_t*>(args.aux) + e);
+            const int16_t hs[4] = {(int16_t)(hb.x & 0xffff), (int16_t)(hb.x >> 16),
+                                   (int16_t)(hb.y & 0xffff), (int16_t)(hb.y >> 16)};
+#pragma unroll
+            for (int u = 0; u < 4; ++u) y[u] = hs[u] > 0 ? y[u] : 0.0f;
+          } else {
+            const float4 a = *reinterpret_cast<const float4*>(static_cast<const float*>(args.aux) + e);
+            y[0] += a.x;
+            y[1] += a.y;
+            y[2] += a.z;
+            y[3] += a.w;
+          }
+        } else {
+          for (int u = 0; u < nv; ++u) {
+            if (EP == EP_RELU_MASK)
+              y[u] = (int16_t)static_cast<const uint16_t*>(args.aux)[e + u] > 0 ? y[u] : 0.0f;
+            else
+              y[u] += static_cast<const float*>(args.aux)[e + u];
+          }
+        }
+      }
+      if (EP == EP_BF16 || EP == EP_RELU_MASK) {
+        uint16_t* out = static_cast<uint16_t*>(args.C) + e;
+        if (vec) {
+          store4_bf16(out, y[0], y[1], y[2], y[3]);
+        } else {
+          for (int u = 0; u < nv; ++u) {
+            const __bf16 b = (__bf16)y[u];
+            out[u] = __builtin_bit_cast(uint16_t, b);
+          }
+        }
+      } else {
+        float* out = static_cast<float*>(args.C) + e;
+        if (vec) {
+          *reinterpret_cast<float4*>(out) = make_float4(y[0], y[1], y[2], y[3]);
+          if (args.C2) store4_bf16(args.C2 + e, y[0], y[1], y[2], y[3]);
+        } else {
+          for (int u = 0; u < nv; ++u) {
+            out[u] = y[u];
+            if (args.C2) args.C2[e + u] = __builtin_bit_cast(uint16_t, (__bf16)y[u]);
+          }
+        }
+      }
+    }
+  }
+}
+
+template <typename TA, typename TB, int EP>
+__global__ __launch_bounds__(256) void gemm_ex_kernel(const TA* __restrict__ A, int64_t M, int K,
+                                                      const TB* __restrict__ B, int O,
+                                                      int tiles_o, int ntiles, int per_xcd,
+                                                      GemmExArgs args) {
+  constexpr int kStageBytes = 2 * kXT * kXLd * 2;  // As + Bs
+  constexpr int kEpiBytes = 64 * kCLd * 4;         // half the C tile, fp32
+  __shared__ __attribute__((aligned(16))) char smem[kStageBytes > kEpiBytes ? kStageBytes : kEpiBytes];
+  __bf16 (*As)[kXLd] = reinterpret_cast<__bf16 (*)[kXLd]>(smem);
+  __bf16 (*Bs)[kXLd] = reinterpret_cast<__bf16 (*)[kXLd]>(smem + kXT * kXLd * 2);
+  float (*Cs)[kCLd] = reinterpret_cast<float (*)[kCLd]>(smem);
+
+  // XCD-aware tile order: workgroup L runs on XCD L % 8; tile t = xcd * per_xcd + L / 8, so the
+  // consecutive tiles of one XCD are the O-tiles of one M-tile
+  const int L = blockIdx.x;
+  const int t = (L & 7) * per_xcd + (L >> 3);
+  if (t >= ntiles) return;
+  const int64_t m0 = (int64_t)(t / tiles_o) * kXT;
+  const int o0 = (t % tiles_o) * kXT;
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wr = wid >> 1, wc = wid & 1, h = lane >> 5, l32 = lane & 31;
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x16{};
+  XStage<TA> ga;
+  XStage<TB> gb;
+  ga.load(A, M, K, m0, 0, tid);
+  gb.load(B, O, K, o0, 0, tid);
+  for (int k0 = 0; k0 < K; k0 += kXK) {
+    ga.store(As, tid);
+    gb.store(Bs, tid);
+    __syncthreads();
+    if (k0 + kXK < K) {  // next slice in flight during this slice's MFMAs
+      ga.load(A, M, K, m0, k0 + kXK, tid);
+      gb.load(B, O, K, o0, k0 + kXK, tid);
+    }
+    xmma_slice(As, Bs, wr, wc, l32, h, acc);
+    __syncthreads();
+  }
+
+  gemm_epilogue<EP>(acc, Cs, M, O, m0, o0, args);
+}
+
+// ---- bf16 x bf16 GEMM, K staged kBK deep through registers (the next slice's buffer loads in
+// flight during this slice's MFMAs) into a double-buffered LDS image: one barrier per slice.
+#ifndef PCST_GEMM_BK
+#define PCST_GEMM_BK 32
+#endif
+constexpr int kBK = PCST_GEMM_BK;   // k slice (32 or 64)
+constexpr int kBLd = kBK + 8;       // LDS row, bf16 elements (+16 B pad: conflict-free row reads)
+constexpr int kCPR = kBK / 8;       // 16-byte chunks per row slice
+constexpr int kBIt = kCPR / 2;      // loads per thread per operand per slice
+
+struct BfRegs {
+  uint4 a[kBIt], b[kBIt];
+};
+
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+// raw buffer over [p, p + bytes): loads past the end return 0, stores past it are dropped
+__device__ __forceinline__ rsrc_t make_rsrc(const void* p, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
+}
+typedef int v4i32 __attribute__((ext_vector_type(4)));
+typedef int v2i32 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint4 bload16(rsrc_t r, uint32_t voff, uint32_t soff) {
+  const v4i32 v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)voff, (int)soff, 0);
+  return make_uint4((uint32_t)v.x, (uint32_t)v.y, (uint32_t)v.z, (uint32_t)v.w);
+}
+
+// slice k0 of the A rows / B rows: byte offsets per thread fixed for the tile, the slice offset
+// is scalar; rows past M (or O) read 0 from the buffer bound, so the loads are branch-free
+__device__ __forceinline__ void bf_load(rsrc_t ra, rsrc_t rb, const uint32_t (&va)[kBIt],
+                                        const uint32_t (&vb)[kBIt], uint32_t soff, BfRegs& g) {
+#pragma unroll
+  for (int it = 0; it < kBIt; ++it) {
+    g.a[it] = bload16(ra, va[it], soff);
+    g.b[it] = bload16(rb, vb[it], soff);
+  }
+}
+
+__device__ __forceinline__ void bf_store(const BfRegs& g, __bf16 (*As)[kBLd], __bf16 (*Bs)[kBLd],
+                                         int tid) {
+#pragma unroll
+  for (int it = 0; it < kBIt; ++it) {
+    const int r = tid / kCPR + (256 / kCPR) * it, kc = (tid % kCPR) * 8;
+    *reinterpret_cast<uint4*>(&As[r][kc]) = g.a[it];
+    *reinterpret_cast<uint4*>(&Bs[r][kc]) = g.b[it];
+  }
+}
+
+// this wave's LDS writes done, then the workgroup barrier; the global loads in flight stay
+// in flight (no vmcnt wait), and the memory clobber keeps LDS accesses on their side
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+__device__ __forceinline__ void bf_mma(const __bf16 (*As)[kBLd], const __bf16 (*Bs)[kBLd], int wr,
+                                       int wc, int l32, int h, f32x16 (&acc)[2][2]) {
+#pragma unroll
+  for (int ks = 0; ks < kBK / 16; ++ks) {
+    bf16x8 a[2], b[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      a[t] = *reinterpret_cast<const bf16x8*>(&As[wr * 64 + t * 32 + l32][ks * 16 + h * 8]);
+      b[t] = *reinterpret_cast<const bf16x8*>(&Bs[wc * 64 + t * 32 + l32][ks * 16 + h * 8]);
+    }
+#pragma unroll
+    for (int bm = 0; bm < 2; ++bm)
+#pragma unroll
+      for (int bn = 0; bn < 2; ++bn)
+        acc[bm][bn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[bm], b[bn], acc[bm][bn], 0, 0, 0);
+  }
+}
+
+__device__ __forceinline__ uint2 pack4_bf16(float a, float b, float c, float d) {
+  bf16x4 o;
+  o[0] = (__bf16)a;
+  o[1] = (__bf16)b;
+  o[2] = (__bf16)c;
+  o[3] = (__bf16)d;
+  return *reinterpret_cast<const uint2*>(&o);
+}
+
+// epilogue for O % 128 == 0 (every column quad valid) and buffers < 4 GiB: the LDS round trip
+// of gemm_epilogue with 32-bit buffer offsets (rows past M are dropped by the buffer bound)
+template <int EP, int PASSES = 2>
+__device__ __forceinline__ void gemm_epilogue_fast(const f32x16 (&acc)[2][2], float (*Cs)[kCLd],
+                                                   int64_t M, int O, int64_t m0, int o0,
+                                                   const GemmExArgs& args) {
+  constexpr int RP = kXT / PASSES;  // rows per pass (64 or 32)
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wr = wid >> 1, wc = wid & 1, h = lane >> 5, l32 = lane & 31;
+  const int cq = (tid & 31) * 4, rl = tid >> 5;
+  constexpr bool kOutBf16 = EP == EP_BF16 || EP == EP_RELU_MASK;
+  const uint32_t nel = (uint32_t)(M * O);
+  const rsrc_t rc = make_rsrc(args.C, nel * (kOutBf16 ? 2u : 4u));
+  const rsrc_t rc2 = make_rsrc(args.C2, args.C2 ? nel * 2u : 0u);
+  const rsrc_t rx = make_rsrc(args.aux, args.aux ? nel * (EP == EP_RELU_MASK ? 2u : 4u) : 0u);
+  float bias4[4] = {0.f, 0.f, 0.f, 0.f};
+  if (args.bias && EP != EP_RELU_MASK && EP != EP_ADD) {
+    const float4 b = *reinterpret_cast<const float4*>(args.bias + o0 + cq);
+    bias4[0] = b.x;
+    bias4[1] = b.y;
+    bias4[2] = b.z;
+    bias4[3] = b.w;
+  }
+#pragma unroll
+  for (int pass = 0; pass < PASSES; ++pass) {
+    if (pass) __syncthreads();
+#pragma unroll
+    for (int bm = 0; bm < 2; ++bm) {
+      const int rb = wr * 64 + bm * 32;  // this block's first row in the tile
+      if (rb / RP != pass) continue;
+#pragma unroll
+      for (int bn = 0; bn < 2; ++bn)
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          Cs[rb % RP + xrow(r, h)][wc * 64 + bn * 32 + l32] = acc[bm][bn][r];
+    }
+    __syncthreads();
+    const uint32_t e0 = (uint32_t)((m0 + pass * RP + rl) * O + o0 + cq);
+#pragma unroll 4
+    for (int j = 0; j < RP / 8; ++j) {
+      const uint32_t e = e0 + (uint32_t)(8 * j * O);
+      const float4 c = *reinterpret_cast<const float4*>(&Cs[rl + 8 * j][cq]);
+      float y[4] = {c.x + bias4[0], c.y + bias4[1], c.z + bias4[2], c.w + bias4[3]};
+      if ((EP == EP_F32 || EP == EP_BF16) && args.relu) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) y[u] = fmaxf(y[u], 0.0f);
+      }
+      if (EP == EP_RESID_DROP) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const bool keep = drop_hash(args.seed_lo, args.seed_hi, (uint64_t)(e + u)) >= args.thr;
+          y[u] = keep ? y[u] * args.scale : 0.0f;
+        }
+      }
+      if (EP == EP_RESID_DROP || EP == EP_ADD) {
+        const v4i32 a = __builtin_amdgcn_raw_buffer_load_b128(rx, (int)(e * 4u), 0, 0);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) y[u] += __int_as_float(a[u]);
+      }
+      if (EP == EP_RELU_MASK) {
+        const v2i32 hb = __builtin_amdgcn_raw_buffer_load_b64(rx, (int)(e * 2u), 0, 0);
+        const int16_t hs[4] = {(int16_t)(hb.x & 0xffff), (int16_t)((uint32_t)hb.x >> 16),
+                               (int16_t)(hb.y & 0xffff), (int16_t)((uint32_t)hb.y >> 16)};
+#pragma unroll
+        for (int u = 0; u < 4; ++u) y[u] = hs[u] > 0 ? y[u] : 0.0f;
+      }
+      if (kOutBf16) {
+        const uint2 pk = pack4_bf16(y[0], y[1], y[2], y[3]);
+        __builtin_amdgcn_raw_buffer_store_b64(v2i32{(int)pk.x, (int)pk.y}, rc, (int)(e * 2u), 0, 0);
+      } else {
+        __builtin_amdgcn_raw_buffer_store_b128(
+            v4i32{__float_as_int(y[0]), __float_as_int(y[1]), __float_as_int(y[2]), __float_as_int(y[3])},
+            rc, (int)(e * 4u), 0, 0);
+        if (args.C2) {
+          const uint2 pk = pack4_bf16(y[0], y[1], y[2], y[3]);
+          __builtin_amdgcn_raw_buffer_store_b64(v2i32{(int)pk.x, (int)pk.y}, rc2, (int)(e * 2u), 0, 0);
+        }
+      }
+    }
+  }
+}
+
+template <int EP, bool FAST>
+__global__ __launch_bounds__(256) void gemm_bf_kernel(const uint16_t* __restrict__ A, int64_t M,
+                                                      int K, const uint16_t* __restrict__ B, int O,
+                                                      int tiles_o, int ntiles, int per_xcd,
+                                                      GemmExArgs args) {
+  constexpr int kBuf = kXT * kBLd * 2;  // one operand image, bytes
+  constexpr int kStage = 4 * kBuf;      // A, B x two buffers
+  constexpr int kEpi = 64 * kCLd * 4;
+  __shared__ __attribute__((aligned(16))) char smem[kStage > kEpi ? kStage : kEpi];
+  typedef __bf16 Row[kBLd];
+  Row* As0 = reinterpret_cast<Row*>(smem);
+  Row* Bs0 = reinterpret_cast<Row*>(smem + kBuf);
+  Row* As1 = reinterpret_cast<Row*>(smem + 2 * kBuf);
+  Row* Bs1 = reinterpret_cast<Row*>(smem + 3 * kBuf);
+
+  const int L = blockIdx.x;
+  const int t = (L & 7) * per_xcd + (L >> 3);
+  if (t >= ntiles) return;
+  const int64_t m0 = (int64_t)(t / tiles_o) * kXT;
+  const int o0 = (t % tiles_o) * kXT;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wr = wid >> 1, wc = wid & 1, h = lane >> 5, l32 = lane & 31;
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x16{};
+  // K % 64 == 0 and M*K*2, O*K*2 < 2^31 (host-checked)
+  const rsrc_t ra = make_rsrc(A, (uint32_t)(M * K * 2));
+  const rsrc_t rb = make_rsrc(B, (uint32_t)((int64_t)O * K * 2));
+  uint32_t va[kBIt], vb[kBIt];
+#pragma unroll
+  for (int it = 0; it < kBIt; ++it) {
+    const int r = tid / kCPR + (256 / kCPR) * it, kc = (tid % kCPR) * 8;
+    va[it] = (uint32_t)(((m0 + r) * K + kc) * 2);
+    vb[it] = (uint32_t)((((int64_t)o0 + r) * K + kc) * 2);
+  }
+  const int nk = K / kBK;
+  BfRegs g;
+  bf_load(ra, rb, va, vb, 0, g);
+  for (int k = 0; k < nk; ++k) {
+    Row* As = (k & 1) ? As1 : As0;
+    Row* Bs = (k & 1) ? Bs1 : Bs0;
+    bf_store(g, As, Bs, tid);
+    lds_barrier();  // one barrier per slice: the other buffer's readers finished a slice ago
+    if (k + 1 < nk) bf_load(ra, rb, va, vb, (uint32_t)((k + 1) * kBK * 2), g);
+    bf_mma(As, Bs, wr, wc, l32, h, acc);
+  }
+  __syncthreads();  // every wave's MFMA reads done before the epilogue reuses the LDS
+  if (FAST)
+    gemm_epilogue_fast<EP>(acc, reinterpret_cast<float (*)[kCLd]>(smem), M, O, m0, o0, args);
+  else
+    gemm_epilogue<EP>(acc, reinterpret_cast<float (*)[kCLd]>(smem), M, O, m0, o0, args);
+}
+
+// ---- bf16 x bf16 GEMM fed by LDS DMA (buffer_load ... lds, 16 B per lane): K staged 32 deep
+// through a ring of S LDS stages, S-1 slices in flight while a slice's MFMAs run, no staging
+// registers.  A DMA instruction fills 1 KiB of LDS contiguously (16 rows x 64 B), so the rows
+// are unpadded and the 16-byte chunk c of row r sits at c ^ ((r >> 2) & 3): conflict-free for
+// the 32x32x16 fragment reads under the ds_read_b128 lane groups (MI355X_MICROARCH.md, LDS).
+// One __shared__ array per stage lets the compiler's LDS-DMA tracking wait for exactly the
+// stage a read needs; the explicit vmcnt before each barrier makes every wave's part of the
+// slice land before any wave reads it.
+constexpr int kDK = 32;                      // k slice
+constexpr int kDStage = 2 * kXT * kDK * 2;   // A + B image, bytes (16 KiB)
+constexpr int kDStageAlloc = 32 * kCLd * 4;  // 16.5 KiB: a stage doubles as a 32-row epilogue pass
+static_assert(kDStageAlloc >= kDStage, "stage too small");
+
+__device__ __forceinline__ void dma_slice(rsrc_t ra, rsrc_t rb, uint32_t va0, uint32_t va1,
+                                          uint32_t vb0, uint32_t vb1, uint32_t soff, char* stage,
+                                          int wid) {
+  typedef __attribute__((address_space(3))) void* lds_ptr;
+  char* a = stage + wid * 2048;
+  char* b = stage + kXT * kDK * 2 + wid * 2048;
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (lds_ptr)a, 16, (int)va0, (int)soff, 0, 0);
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (lds_ptr)(a + 1024), 16, (int)va1, (int)soff, 0, 0);
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (lds_ptr)b, 16, (int)vb0, (int)soff, 0, 0);
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (lds_ptr)(b + 1024), 16, (int)vb1, (int)soff, 0, 0);
+}
+
+// Fragment reads in inline asm: invisible to the compiler's LDS-DMA tracking, which would
+// otherwise drain vmcnt(0) (every slice in flight) at the loop head.  Each read's wait is a
+// counted lgkmcnt tied to the registers it guards (as csrc/noise_mlp.hip does), so no MFMA
+// is scheduled above it; the vm_barrier before the reads makes the slice's DMA complete.
+template <int OFF>
+__device__ __forceinline__ bf16x8 dma_read(uint32_t addr) {
+  bf16x8 v;
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(v) : "v"(addr), "i"(OFF));
+  return v;
+}
+template <int N>
+__device__ __forceinline__ void dma_wait4(bf16x8& a, bf16x8& b, bf16x8& c, bf16x8& d) {
+  asm volatile("s_waitcnt lgkmcnt(%4)" : "+v"(a), "+v"(b), "+v"(c), "+v"(d) : "n"(N));
+}
+
+// lane byte offsets of the four fragment rows/chunks within a stage (see dma_lane_offsets)
+struct DmaLane {
+  uint32_t a0, a1, b0, b1;  // A / B image, k-step 0 / 1 (t = 1 is +2048 immediate)
+};
+
+__device__ __forceinline__ DmaLane dma_lane_offsets(int wr, int wc, int l32, int h) {
+  const int sw = (l32 >> 2) & 3;
+  const uint32_t p0 = (uint32_t)(((h) ^ sw) * 16), p1 = (uint32_t)(((2 + h) ^ sw) * 16);
+  const uint32_t ra = (uint32_t)((wr * 64 + l32) * 64), rb = (uint32_t)(kXT * kDK * 2 + (wc * 64 + l32) * 64);
+  return DmaLane{ra + p0, ra + p1, rb + p0, rb + p1};
+}
+
+__device__ __forceinline__ void dma_mma(const char* stage, const DmaLane& ln, f32x16 (&acc)[2][2]) {
+  const uint32_t base = (uint32_t)(uintptr_t)stage;
+  bf16x8 a0 = dma_read<0>(base + ln.a0), a1 = dma_read<2048>(base + ln.a0);
+  bf16x8 b0 = dma_read<0>(base + ln.b0), b1 = dma_read<2048>(base + ln.b0);
+  bf16x8 c0 = dma_read<0>(base + ln.a1), c1 = dma_read<2048>(base + ln.a1);
+  bf16x8 d0 = dma_read<0>(base + ln.b1), d1 = dma_read<2048>(base + ln.b1);
+  dma_wait4<4>(a0, a1, b0, b1);
+  acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b0, acc[0][0], 0, 0, 0);
+  acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b1, acc[0][1], 0, 0, 0);
+  acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b0, acc[1][0], 0, 0, 0);
+  acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b1, acc[1][1], 0, 0, 0);
+  __builtin_amdgcn_sched_barrier(0);  // k-step 0's MFMAs stay above k-step 1's wait
+  dma_wait4<0>(c0, c1, d0, d1);
+  acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(c0, d0, acc[0][0], 0, 0, 0);
+  acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(c0, d1, acc[0][1], 0, 0, 0);
+  acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(c1, d0, acc[1][0], 0, 0, 0);
+  acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(c1, d1, acc[1][1], 0, 0, 0);
+}
+
+template <int S>
+__device__ __forceinline__ void vm_barrier() {  // this wave's slice k landed, then all waves
+  if (S == 4)
+    asm volatile("s_waitcnt vmcnt(8)\n\ts_barrier" ::: "memory");
+  else
+    asm volatile("s_waitcnt vmcnt(4)\n\ts_barrier" ::: "memory");
+}
+
+template <int EP, int S>
+__global__ __launch_bounds__(256) void gemm_dma_kernel(const uint16_t* __restrict__ A, int64_t M,
+                                                       int K, const uint16_t* __restrict__ B, int O,
+                                                       int tiles_o, int ntiles, int per_xcd,
+                                                       GemmExArgs args) {
+  static_assert(S == 3 || S == 4, "3 or 4 stages");
+  __shared__ __attribute__((aligned(16))) char st0[kDStageAlloc];
+  __shared__ __attribute__((aligned(16))) char st1[kDStageAlloc];
+  __shared__ __attribute__((aligned(16))) char st2[kDStageAlloc];
+  __shared__ __attribute__((aligned(16))) char st3[S == 4 ? kDStageAlloc : 16];
+  const int L = blockIdx.x;
+  const int t = (L & 7) * per_xcd + (L >> 3);
+  if (t >= ntiles) return;
+  const int64_t m0 = (int64_t)(t / tiles_o) * kXT;
+  const int o0 = (t % tiles_o) * kXT;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wid >> 1, wc = wid & 1, h = lane >> 5, l32 = lane & 31;
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x16{};
+  const rsrc_t ra = make_rsrc(A, (uint32_t)(M * K * 2));
+  const rsrc_t rb = make_rsrc(B, (uint32_t)((int64_t)O * K * 2));
+  // lane -> (row within its 16-row piece, logical chunk); the piece is rows 32 wid + 16 i
+  const int pr = lane >> 2, pc = (lane & 3) ^ ((lane >> 4) & 3);
+  const int r0 = 32 * wid + pr;
+  const uint32_t va0 = (uint32_t)(((m0 + r0) * K + 8 * pc) * 2);
+  const uint32_t va1 = (uint32_t)(((m0 + r0 + 16) * K + 8 * pc) * 2);
+  const uint32_t vb0 = (uint32_t)((((int64_t)o0 + r0) * K + 8 * pc) * 2);
+  const uint32_t vb1 = (uint32_t)((((int64_t)o0 + r0 + 16) * K + 8 * pc) * 2);
+  const int nk = K / kDK;
+  char* stages[4] = {st0, st1, st2, st3};
+  const DmaLane ln = dma_lane_offsets(wr, wc, l32, h);
+#pragma unroll
+  for (int q = 0; q < S - 1; ++q) dma_slice(ra, rb, va0, va1, vb0, vb1, q * kDK * 2, stages[q], wid);
+  for (int k = 0; k < nk; k += S) {
+#pragma unroll
+    for (int q = 0; q < S; ++q) {
+      if (k + q < nk) {
+        vm_barrier<S>();
+        // slice k+q+S-1 into the stage read one step ago (every wave is past that read);
+        // slices past K read unused rows or buffer-bound zeros
+        dma_slice(ra, rb, va0, va1, vb0, vb1, (uint32_t)((k + q + S - 1) * kDK * 2),
+                  stages[(q + S - 1) % S], wid);
+        dma_mma(stages[q], ln, acc);
+      }
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the look-ahead DMAs landed
+  __syncthreads();
+  gemm_epilogue_fast<EP, 4>(acc, reinterpret_cast<float (*)[kCLd]>(st0), M, O, m0, o0, args);
+}
+
+// ---- Dropout backward: dD = bf16(g * keep * s), 4 elements per thread (n % 4 == 0)
+__global__ void dropout_grad_kernel(const float4* __restrict__ g, int64_t n4, uint32_t slo,
+                                    uint32_t shi, uint32_t thr, float scale,
+                                    uint2* __restrict__ out) {
+  for (int64_t q = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; q < n4;
+       q += (int64_t)gridDim.x * blockDim.x) {
+    const float4 v = g[q];
+    const float vs[4] = {v.x, v.y, v.z, v.w};
+    float y[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const bool keep = drop_hash(slo, shi, (uint64_t)(4 * q + u)) >= thr;
+      y[u] = keep ? vs[u] * scale : 0.0f;
+    }
+    bf16x4 o;
+    o[0] = (__bf16)y[0];
+    o[1] = (__bf16)y[1];
+    o[2] = (__bf16)y[2];
+    o[3] = (__bf16)y[3];
+    out[q] = *reinterpret_cast<const uint2*>(&o);
+  }
+}
+
+// ---- weight gradient with transposed LDS reads
+constexpr int kWS = 32;                 // m rows per slice
+constexpr int kWLdB = 2 * kXT + 64;     // LDS row bytes: 256 + 64 (row stride = 64 mod 256 B)
+
+// slice rows [m, m+32) x columns [c0, c0+128) of a row-major [*, Cn] matrix -> bf16 LDS image
+template <typename T>
+struct WStage;
+
+template <>
+struct WStage<float> {  // Cn % 4 == 0: thread -> (column quad tid % 32, rows tid / 32 + 8 it)
+  float4 v[4];
+  __device__ __forceinline__ void load(const float* __restrict__ S, int64_t mend, int Cn,
+                                       int64_t m, int c0, int tid) {
+    const int cq = (tid & 31) * 4;
+#pragma unroll
+    for (int it = 0; it < 4; ++it) {
+      const int64_t row = m + (tid >> 5) + 8 * it;
+      v[it] = (row < mend && c0 + cq < Cn) ? *reinterpret_cast<const float4*>(S + row * Cn + c0 + cq)
+                                           : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  }
+  __device__ __forceinline__ void store(char* D, int tid, float* csum) const {
+    const int cq = (tid & 31) * 4;
+#pragma unroll
+    for (int it = 0; it < 4; ++it) {
+      const int r = (tid >> 5) + 8 * it;
+      bf16x4 o;
+      o[0] = (__bf16)v[it].x;
+      o[1] = (__bf16)v[it].y;
+      o[2] = (__bf16)v[it].z;
+      o[3] = (__bf16)v[it].w;
+      *reinterpret_cast<bf16x4*>(D + r * kWLdB + cq * 2) = o;
+      if (csum) {  // unrounded fp32 column sums
+        csum[0] += v[it].x;
+        csum[1] += v[it].y;
+        csum[2] += v[it].z;
+        csum[3] += v[it].w;
+      }
+    }
+  }
+  static constexpr int kSumCols = 4, kRowLanes = 8;
+};
+
+template <>
+struct WStage<uint16_t> {  // Cn % 8 == 0: thread -> (column octet tid % 16, rows tid / 16 + 16 it)
+  uint4 v[2];
+  __device__ __forceinline__ void load(const uint16_t* __restrict__ S, int64_t mend, int Cn,
+                                       int64_t m, int c0, int tid) {
+    const int co = (tid & 15) * 8;
+#pragma unroll
+    for (int it = 0; it < 2; ++it) {
+      const int64_t row = m + (tid >> 4) + 16 * it;
+      v[it] = (row < mend && c0 + co < Cn) ? *reinterpret_cast<const uint4*>(S + row * Cn + c0 + co)
+                                           : make_uint4(0u, 0u, 0u, 0u);
+    }
+  }
+  __device__ __forceinline__ void store(char* D, int tid, float* csum) const {
+    const int co = (tid & 15) * 8;
+#pragma unroll
+    for (int it = 0; it < 2; ++it) {
+      const int r = (tid >> 4) + 16 * it;
+      *reinterpret_cast<uint4*>(D + r * kWLdB + co * 2) = v[it];
+      if (csum) {
+        const uint32_t w[4] = {v[it].x, v[it].y, v[it].z, v[it].w};
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          csum[2 * u] += __uint_as_float(w[u] << 16);
+          csum[2 * u + 1] += __uint_as_float(w[u] & 0xffff0000u);
+        }
+      }
+    }
+  }
+  static constexpr int kSumCols = 8, kRowLanes = 16;
+};
+
+// 32x32x16 operand fragment of columns [c, c+32) x rows [k, k+16) of a [row][col] bf16 image:
+// lane l gets column c + l % 32, rows k + 8 (l / 32) + 0..7 (two ds_read_b64_tr_b16)
+__device__ __forceinline__ bf16x8 tr_frag(const char* img, int c, int k, int lane) {
+  const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+  const char* base = img + (k + 8 * (g >> 1) + q) * kWLdB + (c + 16 * (g & 1) + 4 * p) * 2;
+  typedef __attribute__((address_space(3))) v4i16 lds_v4i16;
+  const v4i16 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(base));
+  const v4i16 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(base + 4 * kWLdB));
+  bf16x8 f;
+  const short s[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+#pragma unroll
+  for (int u = 0; u < 8; ++u) f[u] = __builtin_bit_cast(__bf16, s[u]);
+  return f;
+}
+
+template <typename TZ, typename TX>
+__global__ __launch_bounds__(256) void wgrad_ex_kernel(const TZ* __restrict__ dZ,
+                                                       const TX* __restrict__ X, int64_t M, int I,
+                                                       int O, int64_t rows_per_chunk, int tiles_i,
+                                                       int ntile, int total, int per_xcd,
+                                                       float* __restrict__ partW,
+                                                       float* __restrict__ partB) {
+  __shared__ __attribute__((aligned(16))) char Zs[kWS * kWLdB];
+  __shared__ __attribute__((aligned(16))) char Xs[kWS * kWLdB];
+  __shared__ float bred[WStage<TZ>::kRowLanes][kXT + 1];
+  const int L = blockIdx.x;
+  const int t = (L & 7) * per_xcd + (L >> 3);  // XCD-aware: one chunk's tiles share an L2
+  if (t >= total) return;
+  const int chunk = t / ntile, tile = t % ntile;
+  const int o0 = (tile / tiles_i) * kXT, i0 = (tile % tiles_i) * kXT;
+  const int64_t mb = (int64_t)chunk * rows_per_chunk;
+  const int64_t me = mb + rows_per_chunk < M ? mb + rows_per_chunk : M;
+  const bool bias = partB != nullptr && i0 == 0;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wr = wid >> 1, wc = wid & 1, h = lane >> 5, l32 = lane & 31;
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x16{};
+  float csum[WStage<TZ>::kSumCols];
+#pragma unroll
+  for (int u = 0; u < WStage<TZ>::kSumCols; ++u) csum[u] = 0.0f;
+  WStage<TZ> gz;
+  WStage<TX> gx;
+  gz.load(dZ, me, O, mb, o0, tid);
+  gx.load(X, me, I, mb, i0, tid);
+  for (int64_t k0 = mb; k0 < me; k0 += kWS) {
+    gz.store(Zs, tid, bias ? csum : nullptr);
+    gx.store(Xs, tid, nullptr);
+    __syncthreads();
+    if (k0 + kWS < me) {
+      gz.load(dZ, me, O, k0 + kWS, o0, tid);
+      gx.load(X, me, I, k0 + kWS, i0, tid);
+    }
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8 a[2], b[2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        a[u] = tr_frag(Zs, wr * 64 + u * 32, ks * 16, lane);
+        b[u] = tr_frag(Xs, wc * 64 + u * 32, ks * 16, lane);
+      }
+#pragma unroll
+      for (int bm = 0; bm < 2; ++bm)
+#pragma unroll
+        for (int bn = 0; bn < 2; ++bn)
+          acc[bm][bn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[bm], b[bn], acc[bm][bn], 0, 0, 0);
+    }
+    __syncthreads();
+  }
+  float* pw = partW + (int64_t)chunk * O * I;
+#pragma unroll
+  for (int bn = 0; bn < 2; ++bn) {
+    const int i = i0 + wc * 64 + bn * 32 + l32;
+    if (i >= I) continue;
+#pragma unroll
+    for (int bm = 0; bm < 2; ++bm)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int o = o0 + wr * 64 + bm * 32 + xrow(r, h);
+        if (o < O) pw[(int64_t)o * I + i] = acc[bm][bn][r];
+      }
+  }
+  if (bias) {  // column sums of the chunk: row lanes summed in fixed order
+    constexpr int SC = WStage<TZ>::kSumCols, RL = WStage<TZ>::kRowLanes;
+    const int rlane = tid / (kXT / SC), cb = (tid % (kXT / SC)) * SC;
+#pragma unroll
+    for (int u = 0; u < SC; ++u) bred[rlane][cb + u] = csum[u];
+    __syncthreads();
+    if (tid < kXT && o0 + tid < O) {
+      float s = 0.0f;
+#pragma unroll
+      for (int r = 0; r < RL; ++r) s += bred[r][tid];
+      partB[(int64_t)chunk * O + o0 + tid] = s;
+    }
+  }
+}
+
+__global__ void wgrad_ex_combine_kernel(const float4* __restrict__ part, int64_t n4, int chunks,
+                                        float4* __restrict__ out) {
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < n4;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
+    int c = 0;
+    for (; c + 8 <= chunks; c += 8) {  // 8 loads in flight, summed in chunk order
+      float4 v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = part[(int64_t)(c + u) * n4 + e];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        s0 += (double)v[u].x;
+        s1 += (double)v[u].y;
+        s2 += (double)v[u].z;
+        s3 += (double)v[u].w;
+      }
+    }
+    for (; c < chunks; ++c) {
+      const float4 v = part[(int64_t)c * n4 + e];
+      s0 += (double)v.x;
+      s1 += (double)v.y;
+      s2 += (double)v.z;
+      s3 += (double)v.w;
+    }
+    out[e] = make_float4((float)s0, (float)s1, (float)s2, (float)s3);
+  }
+}
+
+struct WgradExPlan {
+  int tiles_i, tiles_o, ntile, chunks, total, per_xcd;
+  int64_t rows_per_chunk;
+};
+
+static WgradExPlan wgrad_ex_plan(int64_t M, int64_t I, int64_t O) {
+  WgradExPlan p;
+  p.tiles_i = (int)cdiv(I, kXT);
+  p.tiles_o = (int)cdiv(O, kXT);
+  p.ntile = p.tiles_i * p.tiles_o;
+  int64_t chunks = cdiv(512, p.ntile);  // ~2 workgroups per CU
+  chunks = std::max<int64_t>(1, std::min<int64_t>(chunks, cdiv(M, 512)));
+  p.rows_per_chunk = cdiv(cdiv(M, chunks), kWS) * kWS;
+  p.chunks = (int)cdiv(M, p.rows_per_chunk);
+  p.total = p.chunks * p.ntile;
+  p.per_xcd = (int)cdiv(p.total, 8);
+  return p;
+}
+
+static uint32_t drop_threshold(float p) {
+  const double t = (double)p * 4294967296.0;
+  return t <= 0.0 ? 0u : (t >= 4294967295.0 ? 0xffffffffu : (uint32_t)t);
+}
+
+}  // namespace pcst
+
+using namespace pcst;
+
+#define PCST_GEMM_EX(TA, TB, EPV)                                                                  \
+  hipLaunchKernelGGL((gemm_ex_kernel<TA, TB, EPV>), dim3((unsigned)(8 * per)), dim3(256), 0, s,     \
+                     static_cast<const TA*>(A), M, (int)K, static_cast<const TB*>(B), (int)O,        \
+                     tiles_o, ntiles, per, args)
+
+template <typename TA, typename TB>
+static void launch_gemm_ex(int ep, const void* A, int64_t M, int64_t K, const void* B, int64_t O,
+                           int tiles_o, int ntiles, int per, const GemmExArgs& args, hipStream_t s) {
+  switch (ep) {
+    case EP_F32: PCST_GEMM_EX(TA, TB, EP_F32); break;
+    case EP_BF16: PCST_GEMM_EX(TA, TB, EP_BF16); break;
+    case EP_RESID_DROP: PCST_GEMM_EX(TA, TB, EP_RESID_DROP); break;
+    case EP_RELU_MASK: PCST_GEMM_EX(TA, TB, EP_RELU_MASK); break;
+    case EP_ADD: PCST_GEMM_EX(TA, TB, EP_ADD); break;
+    default: PCST_GEMM_EX(TA, TB, EP_COND); break;
+  }
+}
+#undef PCST_GEMM_EX
+
+#define PCST_GEMM_BF(EPV)                                                                          \
+  if (fast)                                                                                        \
+    hipLaunchKernelGGL((gemm_bf_kernel<EPV, true>), dim3((unsigned)(8 * per)), dim3(256), 0, s,     \
+                       static_cast<const uint16_t*>(A), M, (int)K, static_cast<const uint16_t*>(B),  \
+                       (int)O, tiles_o, ntiles, per, args);                                          \
+  else                                                                                             \
+    hipLaunchKernelGGL((gemm_bf_kernel<EPV, false>), dim3((unsigned)(8 * per)), dim3(256), 0, s,    \
+                       static_cast<const uint16_t*>(A), M, (int)K, static_cast<const uint16_t*>(B),  \
+                       (int)O, tiles_o, ntiles, per, args)
+
+#define PCST_GEMM_DMA(EPV)                                                                         \
+  if (stages == 3)                                                                                 \
+    hipLaunchKernelGGL((gemm_dma_kernel<EPV, 3>), dim3((unsigned)(8 * per)), dim3(256), 0, s,       \
+                       static_cast<const uint16_t*>(A), M, (int)K, static_cast<const uint16_t*>(B),  \
+                       (int)O, tiles_o, ntiles, per, args);                                          \
+  else                                                                                             \
+    hipLaunchKernelGGL((gemm_dma_kernel<EPV, 4>), dim3((unsigned)(8 * per)), dim3(256), 0, s,       \
+                       static_cast<const uint16_t*>(A), M, (int)K, static_cast<const uint16_t*>(B),  \
+                       (int)O, tiles_o, ntiles, per, args)
+
+static void launch_gemm_dma(int ep, int stages, const void* A, int64_t M, int64_t K, const void* B,
+                            int64_t O, int tiles_o, int ntiles, int per, const GemmExArgs& args,
+                            hipStream_t s) {
+  switch (ep) {
+    case EP_F32: PCST_GEMM_DMA(EP_F32); break;
+    case EP_BF16: PCST_GEMM_DMA(EP_BF16); break;
+    case EP_RESID_DROP: PCST_GEMM_DMA(EP_RESID_DROP); break;
+    case EP_RELU_MASK: PCST_GEMM_DMA(EP_RELU_MASK); break;
+    default: PCST_GEMM_DMA(EP_ADD); break;
+  }
+}
+#undef PCST_GEMM_DMA
+
+// bf16 kernel choice (experiment knob PCST_GEMM_KERNEL: 0 register-staged, 3/4 LDS-DMA stages)
+static int gemm_kernel_choice() {
+  static const int v = [] {
+    const char* e = getenv("PCST_GEMM_KERNEL");
+    return e ? atoi(e) : 0;  // measured: register staging 140 us vs DMA 146 (3) / 173 (4), K=256
+  }();
+  return v;
+}
+
+static void launch_gemm_bf(int ep, bool fast, const void* A, int64_t M, int64_t K, const void* B,
+                           int64_t O, int tiles_o, int ntiles, int per, const GemmExArgs& args,
+                           hipStream_t s) {
+  switch (ep) {
+    case EP_F32: PCST_GEMM_BF(EP_F32); break;
+    case EP_BF16: PCST_GEMM_BF(EP_BF16); break;
+    case EP_RESID_DROP: PCST_GEMM_BF(EP_RESID_DROP); break;
+    case EP_RELU_MASK: PCST_GEMM_BF(EP_RELU_MASK); break;
+    case EP_ADD: PCST_GEMM_BF(EP_ADD); break;
+    default: PCST_GEMM_BF(EP_COND); break;
+  }
+}
+#undef PCST_GEMM_BF
+
+extern "C" int pcst_gemm_ex(const void* A, int a_bf16, int64_t M, int64_t K, const void* B,
+                            int b_bf16, int64_t O, const float* bias, int relu, int epilogue,
+                            const void* aux, uint64_t seed, float drop_p, int64_t group_rows,
+                            void* C, uint16_t* C2, void* stream) {
+  PCST_CHECK_ARG(M >= 0 && K > 0 && O > 0 && K < (1 << 20) && O < (1 << 20), "gemm_ex: bad shape");
+  PCST_CHECK_ARG(epilogue >= EP_F32 && epilogue <= EP_COND, "gemm_ex: bad epilogue");
+  PCST_CHECK_ARG(K % (a_bf16 ? 8 : 4) == 0 && K % (b_bf16 ? 8 : 4) == 0,
+                 "gemm_ex: K must be a multiple of 8 (bf16 operand) or 4 (fp32 operand)");
+  PCST_CHECK_ARG(O % 4 == 0 || epilogue == EP_F32 || epilogue == EP_BF16,
+                 "gemm_ex: O must be a multiple of 4 for this epilogue");
+  PCST_CHECK_ARG(drop_p >= 0.0f && drop_p < 1.0f, "gemm_ex: dropout p must be in [0, 1)");
+  PCST_CHECK_ARG(epilogue != EP_COND || group_rows > 0, "gemm_ex: EP_COND needs group_rows > 0");
+  if (M == 0) return PCST_OK;
+  PCST_CHECK_ARG(A && B && C, "gemm_ex: null pointer");
+  PCST_CHECK_ARG(epilogue == EP_F32 || epilogue == EP_BF16 || aux, "gemm_ex: epilogue needs aux");
+  PCST_CHECK_ARG(((uintptr_t)A | (uintptr_t)B | (uintptr_t)C | (uintptr_t)C2 | (uintptr_t)aux) % 16 == 0,
+                 "gemm_ex: pointers must be 16-byte aligned");
+  hipStream_t s = as_stream(stream);
+  const int tiles_o = (int)cdiv(O, kXT);
+  const int64_t nt = cdiv(M, kXT) * tiles_o;
+  PCST_CHECK_ARG(nt < (1ll << 30), "gemm_ex: too many tiles");
+  const int ntiles = (int)nt, per = (int)cdiv(nt, 8);
+  GemmExArgs args;
+  args.bias = bias;
+  args.relu = relu;
+  args.aux = aux;
+  args.seed_lo = (uint32_t)seed;
+  args.seed_hi = (uint32_t)(seed >> 32);
+  args.thr = drop_threshold(drop_p);
+  args.scale = 1.0f / (1.0f - drop_p);
+  args.C = C;
+  args.C2 = C2;
+  args.group_rows = group_rows;
+  const int64_t lim = 1ll << 31;
+  if (a_bf16 && b_bf16 && K % kBK == 0 && M * K * 2 < lim && O * K * 2 < lim) {
+    const bool fast = O % kXT == 0 && epilogue != EP_COND && M * O * 4 < lim;
+    const int choice = gemm_kernel_choice();
+    if (fast && K % kDK == 0 && (choice == 3 || choice == 4))
+      launch_gemm_dma(epilogue, choice, A, M, K, B, O, tiles_o, ntiles, per, args, s);
+    else
+      launch_gemm_bf(epilogue, fast, A, M, K, B, O, tiles_o, ntiles, per, args, s);
+  } else if (a_bf16 && b_bf16)
+    launch_gemm_ex<uint16_t, uint16_t>(epilogue, A, M, K, B, O, tiles_o, ntiles, per, args, s);
+  else if (a_bf16)
+    launch_gemm_ex<uint16_t, float>(epilogue, A, M, K, B, O, tiles_o, ntiles, per, args, s);
+  else if (b_bf16)
+    launch_gemm_ex<float, uint16_t>(epilogue, A, M, K, B, O, tiles_o, ntiles, per, args, s);
+  else
+    launch_gemm_ex<float, float>(epilogue, A, M, K, B, O, tiles_o, ntiles, per, args, s);
+  PCST_LAUNCH_CHECK("gemm_ex");
+  return PCST_OK;
+}
+
+extern "C" int pcst_dropout_grad_bf16(const float* g, int64_t n, uint64_t seed, float drop_p,
+                                      uint16_t* out, void* stream) {
+  PCST_CHECK_ARG(n >= 0 && n % 4 == 0, "dropout_grad_bf16: n must be a multiple of 4");
+  PCST_CHECK_ARG(drop_p >= 0.0f && drop_p < 1.0f, "dropout_grad_bf16: p must be in [0, 1)");
+  if (n == 0) return PCST_OK;
+  PCST_CHECK_ARG(g && out && ((uintptr_t)g | (uintptr_t)out) % 16 == 0, "dropout_grad_bf16: bad pointer");
+  const int64_t n4 = n / 4;
+  hipLaunchKernelGGL(dropout_grad_kernel, dim3((unsigned)std::min<int64_t>(cdiv(n4, 256), 4096)),
+                     dim3(256), 0, as_stream(stream), reinterpret_cast<const float4*>(g), n4,
+                     (uint32_t)seed, (uint32_t)(seed >> 32), drop_threshold(drop_p),
+                     1.0f / (1.0f - drop_p), reinterpret_cast<uint2*>(out));
+  PCST_LAUNCH_CHECK("dropout_grad_bf16");
+  return PCST_OK;
+}
+
+extern "C" int pcst_linear_wgrad_ex_workspace_size(int64_t M, int64_t I, int64_t O, size_t* bytes) {
+  PCST_CHECK_ARG(M >= 0 && I > 0 && O > 0 && bytes, "linear_wgrad_ex_workspace_size: bad args");
+  const WgradExPlan p = wgrad_ex_plan(std::max<int64_t>(M, 1), I, O);
+  *bytes = sizeof(float) * (size_t)p.chunks * (size_t)(O * I + O);
+  return PCST_OK;
+}
+
+extern "C" int pcst_linear_wgrad_ex(const void* dZ, int dz_bf16, const void* X, int x_bf16,
+                                    int64_t M, int64_t I, int64_t O, float* dW, float* db,
+                                    void* workspace, void* stream) {
+  PCST_CHECK_ARG(M >= 0 && I > 0 && O > 0 && I < (1 << 20) && O < (1 << 20), "linear_wgrad_ex: bad shape");
+  PCST_CHECK_ARG(I % 8 == 0 && O % 8 == 0, "linear_wgrad_ex: I and O must be multiples of 8");
+  PCST_CHECK_ARG(dW && workspace && (M == 0 || (dZ && X)), "linear_wgrad_ex: null pointer");
+  PCST_CHECK_ARG(((uintptr_t)dZ | (uintptr_t)X | (uintptr_t)dW) % 16 == 0, "linear_wgrad_ex: unaligned");
+  hipStream_t s = as_stream(stream);
+  if (M == 0) {
+    PCST_HIP(hipMemsetAsync(dW, 0, sizeof(float) * O * I, s), "memset");
+    if (db) PCST_HIP(hipMemsetAsync(db, 0, sizeof(float) * O, s), "memset");
+    return PCST_OK;
+  }
+  const WgradExPlan p = wgrad_ex_plan(M, I, O);
+  float* partW = static_cast<float*>(workspace);
+  float* partB = db ? partW + (int64_t)p.chunks * O * I : nullptr;
+  const dim3 grid((unsigned)(8 * p.per_xcd));
+#define PCST_WGRAD_EX(TZ, TX)                                                                     \
+  hipLaunchKernelGGL((wgrad_ex_kernel<TZ, TX>), grid, dim3(256), 0, s, static_cast<const TZ*>(dZ), \
+                     static_cast<const TX*>(X), M, (int)I, (int)O, p.rows_per_chunk, p.tiles_i,     \
+                     p.ntile, p.total, p.per_xcd, partW, partB)
+  if (dz_bf16 && x_bf16)
+    PCST_WGRAD_EX(uint16_t, uint16_t);
+  else if (dz_bf16)
+    PCST_WGRAD_EX(uint16_t, float);
+  else if (x_bf16)
+    PCST_WGRAD_EX(float, uint16_t);
+  else
+    PCST_WGRAD_EX(float, float);
+#undef PCST_WGRAD_EX
+  const int64_t n4 = O * I / 4;
+  hipLaunchKernelGGL(wgrad_ex_combine_kernel, dim3((unsigned)std::min<int64_t>(cdiv(n4, 256), 2048)),
+                     dim3(256), 0, s, reinterpret_cast<const float4*>(partW), n4, p.chunks,
+                     reinterpret_cast<float4*>(dW));
+  if (db)
+    hipLaunchKernelGGL(wgrad_ex_combine_kernel, dim3((unsigned)cdiv(O / 4, 256)), dim3(256), 0, s,
+                       reinterpret_cast<const float4*>(partB), O / 4, p.chunks,
+                       reinterpret_cast<float4*>(db));
+  PCST_LAUNCH_CHECK("linear_wgrad_ex");
+  return PCST_OK;
+}

@@ -59,6 +59,172 @@ class LinearFn(torch.autograd.Function):
         return dx, dw, db, None
 
 
+def _bf16(w):
+    return w.detach().to(torch.bfloat16).contiguous()
+
+
+def _bf16_t(w):
+    return w.detach().t().to(torch.bfloat16).contiguous()
+
+
+def _draw_seed(p):
+    """Dropout seed for one layer call: torch's CPU generator (torch.manual_seed governs it)."""
+    return int(torch.randint(0, 2 ** 62, (1,)).item()) if p > 0 else 0
+
+
+def _block_fwd(x, xb, w1, b1, w2, b2, p, seed):
+    """x + Dropout_p(Linear2(ReLU(Linear1(x)))): -> (y fp32, y bf16, h bf16)."""
+    h = _hip.gemm_ex(xb, w1, b1, relu=True, epilogue=_hip.EP_BF16)
+    y, yb = _hip.gemm_ex(h, w2, b2, epilogue=_hip.EP_RESID_DROP, aux=x, seed=seed, p=p,
+                         copy_bf16=True)
+    return y, yb, h
+
+
+def _block_bwd(g, xb, h, w1_t, w2_t, p, seed, bias1=True, bias2=True):
+    """Backward of _block_fwd from the fp32 gradient g of y: -> (gx, dW1, db1, dW2, db2)."""
+    dd = _hip.dropout_grad_bf16(g, seed, p)
+    dz = _hip.gemm_ex(dd, w2_t, epilogue=_hip.EP_RELU_MASK, aux=h)
+    gx = _hip.gemm_ex(dz, w1_t, epilogue=_hip.EP_ADD, aux=g)
+    dw2, db2 = _hip.linear_wgrad_ex(dd, h, bias=bias2)
+    dw1, db1 = _hip.linear_wgrad_ex(dz, xb, bias=bias1)
+    return gx, dw1, db1, dw2, db2
+
+
+class ResidualBlockFn(torch.autograd.Function):
+    """x + Dropout_p(Linear2(ReLU(Linear1(x)))) -- one NoisePredictor layer
+    (diffusion_model.py:48-52, applied at :57-58) -- under autocast, with bf16 activation storage
+    and the elementwise work fused into the GEMM epilogues (csrc/train_mlp.hip):
+
+      forward   h  = bf16(relu(x W1^T + b1))                     EP_BF16
+                y  = x + keep * (h W2^T + b2) / (1-p)           EP_RESID_DROP
+      backward  dd = bf16(g * keep / (1-p))                     pcst_dropout_grad_bf16
+                dz = bf16((dd W2) * [h > 0])                     EP_RELU_MASK
+                gx = g + dz W1                                   EP_ADD
+                dW2, db2 = dd^T h;  dW1, db1 = dz^T x            pcst_linear_wgrad_ex
+
+    Every product rounds its operands to bf16 (LinearFn's autocast GEMMs do the same), so storing
+    x, h, dd and dz as bf16 changes no product; the residual stream x and its gradient stay fp32.
+    The dropout mask is a hash of (seed, element): one seed per call from torch's CPU generator,
+    regenerated in the backward instead of stored."""
+
+    @staticmethod
+    def forward(ctx, x, w1, b1, w2, b2, p):
+        shape = x.shape
+        x2 = x.reshape(-1, shape[-1]).float().contiguous()
+        xb = x2.to(torch.bfloat16)
+        seed = _draw_seed(p)
+        y, _, h = _block_fwd(x2, xb, _bf16(w1), b1, _bf16(w2), b2, p, seed)
+        ctx.save_for_backward(xb, h, w1, w2)
+        ctx.seed, ctx.p, ctx.shape = seed, p, shape
+        ctx.has_b = (b1 is not None, b2 is not None)
+        return y.view(shape)
+
+    @staticmethod
+    def backward(ctx, gy):
+        xb, h, w1, w2 = ctx.saved_tensors
+        g = gy.reshape(xb.shape).float().contiguous()
+        gx, dw1, db1, dw2, db2 = _block_bwd(g, xb, h, _bf16_t(w1), _bf16_t(w2), ctx.p, ctx.seed,
+                                            *ctx.has_b)
+        return gx.view(ctx.shape), dw1, db1, dw2, db2, None
+
+
+def residual_block(x, layer, training):
+    """`layer` = Sequential(Linear(fd, 2fd), ReLU, Linear(2fd, fd), Dropout) applied as
+    x + layer(x) through ResidualBlockFn."""
+    l1, l2, drop = layer[0], layer[2], layer[3]
+    p = float(drop.p) if training else 0.0
+    return ResidualBlockFn.apply(x, l1.weight, l1.bias, l2.weight, l2.bias, p)
+
+
+class NoisePredictorFn(torch.autograd.Function):
+    """The whole per-point network of NoisePredictor.forward (diffusion_model.py:50-61) under
+    autocast, forward and backward, on the fused bf16-storage GEMMs:
+
+      h0 = relu(pts W0^T + b0)             [M,128]  bf16   (pts zero-padded to K = 8)
+      h1 = relu(h0 W2^T + b2)              [M,256]  bf16
+      x  = ((h1 W4^T + b4) + tf) + sf      [M,256]  fp32 + bf16 copy   (EP_COND, per cloud)
+      6 x residual block                   (ResidualBlockFn's kernels)
+      q0 = relu(x Wo0^T + bo0)             [M,256]  bf16
+      q1 = relu(q0 Wo2^T + bo2)            [M,128]  bf16
+      out = q1 Wo4^T + bo4                 [M,3]    fp32
+
+    Inputs: pts [B,N,3], cond [B,2,256] = (time_proj(temb), style_proj(style)) -- the small
+    per-cloud projections stay in autograd -- and the network's 34 weights.  Each ReLU backward
+    is fused into the dX product that produces its gradient (EP_RELU_MASK on the layer's own
+    bf16 output), so no [M,*] elementwise kernel runs outside the GEMMs except the per-cloud
+    column sums of dL/dx for cond's gradient."""
+
+    @staticmethod
+    def forward(ctx, pts, cond, p, *w):
+        B, N, _ = pts.shape
+        M = B * N
+        dev = pts.device
+        xp = torch.zeros(M, 8, dtype=torch.float32, device=dev)
+        xp[:, :3] = pts.reshape(M, 3)
+        w0p = torch.zeros(w[0].shape[0], 8, dtype=torch.float32, device=dev)
+        w0p[:, :3] = w[0].detach()
+        wb = [_bf16(t) if t.dim() == 2 else t.detach() for t in w[2:]]
+        wb = [_bf16(w0p), w[1].detach()] + wb
+        h0 = _hip.gemm_ex(xp, wb[0], wb[1], relu=True, epilogue=_hip.EP_BF16)
+        h1 = _hip.gemm_ex(h0, wb[2], wb[3], relu=True, epilogue=_hip.EP_BF16)
+        x, xb = _hip.gemm_ex(h1, wb[4], wb[5], epilogue=_hip.EP_COND,
+                             aux=cond.detach().float().contiguous(), group_rows=N, copy_bf16=True)
+        saved, seeds = [xp, h0, h1], []
+        for k in range(6):
+            o = 6 + 4 * k
+            seed = _draw_seed(p)
+            seeds.append(seed)
+            saved.append(xb)
+            x, xb, h = _block_fwd(x, xb, wb[o], wb[o + 1], wb[o + 2], wb[o + 3], p, seed)
+            saved.append(h)
+        q0 = _hip.gemm_ex(xb, wb[30], wb[31], relu=True, epilogue=_hip.EP_BF16)
+        q1 = _hip.gemm_ex(q0, wb[32], wb[33], relu=True, epilogue=_hip.EP_BF16)
+        out = _hip.gemm_ex(q1, wb[34], wb[35], epilogue=_hip.EP_F32)
+        saved += [xb, q0, q1]
+        ctx.save_for_backward(*saved, *w)
+        ctx.seeds, ctx.p, ctx.BN = seeds, p, (B, N)
+        return out.view(B, N, 3)
+
+    @staticmethod
+    def backward(ctx, gout):
+        sv = ctx.saved_tensors
+        xp, h0, h1 = sv[0], sv[1], sv[2]
+        blocks = [(sv[3 + 2 * k], sv[4 + 2 * k]) for k in range(6)]
+        xb, q0, q1 = sv[15], sv[16], sv[17]
+        w = sv[18:]
+        B, N = ctx.BN
+        M = B * N
+        dev = gout.device
+        grads = [None] * len(w)
+        # output layer (O = 3): gradient zero-padded to 8 columns for the MFMA kernels
+        g3 = torch.zeros(M, 8, dtype=torch.float32, device=dev)
+        g3[:, :3] = gout.reshape(M, 3)
+        dw, db = _hip.linear_wgrad_ex(g3, q1)
+        grads[34], grads[35] = dw[:3].contiguous(), db[:3].contiguous()
+        wo4p = torch.zeros(8, w[34].shape[1], dtype=torch.float32, device=dev)
+        wo4p[:3] = w[34].detach()
+        dq1 = _hip.gemm_ex(g3, _bf16_t(wo4p), epilogue=_hip.EP_RELU_MASK, aux=q1)
+        grads[32], grads[33] = _hip.linear_wgrad_ex(dq1, q0)
+        dq0 = _hip.gemm_ex(dq1, _bf16_t(w[32]), epilogue=_hip.EP_RELU_MASK, aux=q0)
+        grads[30], grads[31] = _hip.linear_wgrad_ex(dq0, xb)
+        g = _hip.gemm_ex(dq0, _bf16_t(w[30]), epilogue=_hip.EP_F32)
+        for k in reversed(range(6)):
+            o = 6 + 4 * k
+            xbk, hk = blocks[k]
+            g, grads[o], grads[o + 1], grads[o + 2], grads[o + 3] = _block_bwd(
+                g, xbk, hk, _bf16_t(w[o]), _bf16_t(w[o + 2]), ctx.p, ctx.seeds[k])
+        # x = ((pf + tf) + sf): dL/dpf = g, dL/dtf[b] = dL/dsf[b] = sum of g over cloud b's rows
+        gsum = g.view(B, N, -1).sum(1)
+        dcond = torch.stack([gsum, gsum], 1)
+        grads[4], grads[5] = _hip.linear_wgrad_ex(g, h1)
+        dh1 = _hip.gemm_ex(g, _bf16_t(w[4]), epilogue=_hip.EP_RELU_MASK, aux=h1)
+        grads[2], grads[3] = _hip.linear_wgrad_ex(dh1, h0)
+        dh0 = _hip.gemm_ex(dh1, _bf16_t(w[2]), epilogue=_hip.EP_RELU_MASK, aux=h0)
+        dw0, grads[1] = _hip.linear_wgrad_ex(dh0, xp)
+        grads[0] = dw0[:, :3].contiguous()
+        return (None, dcond, None, *grads)
+
+
 class BNReLUFn(torch.autograd.Function):
     """relu(BatchNorm_train(z)) over the rows of z [M, O] (BatchNorm2d on [B, C, S, ns] with
     channel-last rows, pointnet2_encoder.py:108-110), optionally max-pooled over groups of

@@ -124,6 +124,17 @@ class NoisePredictor(nn.Module):
                                ws_t, self.style_proj.bias.detach(),
                                self.point_encoder[4].bias.detach())
 
+    def _fused_params(self):
+        """Weights in NoisePredictorFn's order: point encoder, 6 x (Linear1, Linear2), output."""
+        mods = [self.point_encoder[0], self.point_encoder[2], self.point_encoder[4]]
+        for layer in self.layers:
+            mods += [layer[0], layer[2]]
+        mods += [self.output_mlp[0], self.output_mlp[2], self.output_mlp[4]]
+        out = []
+        for m in mods:
+            out += [m.weight, m.bias]
+        return out
+
     def _dropout_active(self) -> bool:
         return self.training and any(l[3].p > 0 for l in self.layers)
 
@@ -131,11 +142,17 @@ class NoisePredictor(nn.Module):
         """Differentiable path (training): every linear on the MFMA GEMM kernel with its
         backward (models/_autograd.py); residual adds / dropout as device tensor ops."""
         pe = self.point_encoder
+        tf = _ag.linear(self.time_embedding(timestep.to(noisy_points.device)), self.time_proj)
+        sf = _ag.linear(style_feat, self.style_proj)
+        if noisy_points.is_cuda and torch.is_autocast_enabled("cuda"):
+            # the whole per-point network on the bf16-storage fused GEMMs (NoisePredictorFn)
+            p = float(self.layers[0][3].p) if self.training else 0.0
+            cond = torch.stack([tf.float(), sf.float()], 1)
+            return _ag.NoisePredictorFn.apply(noisy_points.float(), cond, p,
+                                              *self._fused_params())
         h = _ag.linear(noisy_points, pe[0], True)
         h = _ag.linear(h, pe[2], True)
         pf = _ag.linear(h, pe[4])
-        tf = _ag.linear(self.time_embedding(timestep.to(noisy_points.device)), self.time_proj)
-        sf = _ag.linear(style_feat, self.style_proj)
         x = pf + tf.unsqueeze(1) + sf.unsqueeze(1)
         for layer in self.layers:
             d = _ag.linear(_ag.linear(x, layer[0], True), layer[2])

@@ -219,3 +219,174 @@ def test_group_gather_fn_backward(H, B, N, C, S, ns):
     pts.grad = None
     ag.GroupGatherFn.apply(xyz, pts, fidx, gidx)[1].backward(gg)
     assert torch.equal(pts.grad, first)
+
+
+# ---- csrc/train_mlp.hip: bf16-storage GEMMs with fused epilogues --------------------------
+def _bf16_ulp_close(a, b, ulps=1.0):
+    """bf16 outputs: within `ulps` bf16 units in the last place of the reference (an ulp of x
+    is at most |x| * 2^-7: 8 significant bits)."""
+    a, b = a.double(), b.double()
+    return ((a - b).abs() <= ulps * (b.abs() * 2.0 ** -7 + 1e-30) + 1e-6 * b.abs().max()).all().item()
+
+
+@pytest.mark.parametrize("M,K,O", [(1, 128, 128), (1000, 256, 512), (4097, 512, 256), (300, 136, 260),
+                                   (60000, 256, 512)])
+@pytest.mark.parametrize("a16,b16", [(False, False), (True, False), (True, True)])
+def test_gemm_ex_epilogues_vs_float64(H, M, K, O, a16, b16):
+    g = torch.Generator(device="cuda").manual_seed(M + K + O + 7 * a16 + 3 * b16)
+    A = torch.randn(M, K, device="cuda", generator=g)
+    B = torch.randn(O, K, device="cuda", generator=g) * K ** -0.5
+    bias = torch.randn(O, device="cuda", generator=g)
+    Ain = A.bfloat16() if a16 else A
+    Bin = B.bfloat16() if b16 else B
+    acc = _bf(A) @ _bf(B).t()
+    tol = lambda ref: 1e-6 * ref.norm().item()  # noqa: E731  fp32 summation order
+    # EP_F32 / EP_BF16 with bias + relu
+    C = H.gemm_ex(Ain, Bin, bias, relu=True, epilogue=H.EP_F32)
+    ref = (acc + bias.double()).clamp_min(0)
+    assert (C.double() - ref).norm().item() <= tol(ref)
+    Cb = H.gemm_ex(Ain, Bin, bias, relu=True, epilogue=H.EP_BF16)
+    assert Cb.dtype == torch.bfloat16 and _bf16_ulp_close(Cb, ref)
+    # EP_ADD
+    aux = torch.randn(M, O, device="cuda", generator=g)
+    C = H.gemm_ex(Ain, Bin, epilogue=H.EP_ADD, aux=aux)
+    ref = acc + aux.double()
+    assert (C.double() - ref).norm().item() <= tol(ref)
+    # EP_RELU_MASK: zero where the bf16 mask is <= 0 (including exact zeros)
+    h = torch.randn(M, O, device="cuda", generator=g)
+    h[:, ::7] = 0.0
+    h = h.bfloat16()
+    C = H.gemm_ex(Ain, Bin, epilogue=H.EP_RELU_MASK, aux=h)
+    ref = acc * (h.double() > 0)
+    assert C.dtype == torch.bfloat16 and _bf16_ulp_close(C, ref)
+    assert torch.equal(C == 0, (h <= 0) | (C == 0))
+
+
+@pytest.mark.parametrize("p", [0.0, 0.1, 0.5])
+def test_gemm_ex_dropout_mask_fwd_bwd_consistent(H, p):
+    """EP_RESID_DROP keeps element e iff hash(seed, e) passes; pcst_dropout_grad_bf16 must
+    regenerate the same mask (read off dropout_grad of ones), the forward must equal
+    x + keep * (acc + b) / (1-p), and the kept fraction must be 1-p."""
+    M, K, O = 20000, 256, 256
+    g = torch.Generator(device="cuda").manual_seed(11)
+    h = torch.randn(M, K, device="cuda", generator=g).bfloat16()
+    W = torch.randn(O, K, device="cuda", generator=g) * K ** -0.5
+    b = torch.randn(O, device="cuda", generator=g)
+    x = torch.randn(M, O, device="cuda", generator=g)
+    seed = 0x1234_5678_9ABC_DEF
+    y = H.gemm_ex(h, W, b, epilogue=H.EP_RESID_DROP, aux=x, seed=seed, p=p)
+    keep = H.dropout_grad_bf16(torch.ones(M, O, device="cuda"), seed, p) != 0
+    frac = keep.double().mean().item()
+    assert abs(frac - (1 - p)) < 4 * np.sqrt(p * (1 - p) / (M * O)) + 1e-12
+    v = _bf(h) @ _bf(W).t() + b.double()
+    ref = x.double() + keep.double() * v * (1.0 / (1.0 - p))
+    assert ((y.double() - ref).norm() / ref.norm()).item() < 1e-6
+    assert torch.equal(y[~keep], x[~keep])  # dropped elements are exactly the residual
+    y2 = H.gemm_ex(h, W, b, epilogue=H.EP_RESID_DROP, aux=x, seed=seed, p=p)
+    assert torch.equal(y, y2)
+    if p > 0:
+        y3 = H.gemm_ex(h, W, b, epilogue=H.EP_RESID_DROP, aux=x, seed=seed + 1, p=p)
+        assert not torch.equal(y, y3)
+    gd = torch.randn(M, O, device="cuda", generator=g)
+    dd = H.dropout_grad_bf16(gd, seed, p)
+    assert _bf16_ulp_close(dd, gd.double() * keep.double() / (1.0 - p), 0.5)
+
+
+@pytest.mark.parametrize("M,I,O", [(1, 256, 512), (100, 136, 264), (5000, 512, 256), (240000, 256, 512),
+                                   (240000, 512, 256)])
+@pytest.mark.parametrize("z16,x16", [(True, True), (True, False), (False, False)])
+def test_linear_wgrad_ex_vs_float64(H, M, I, O, z16, x16):
+    g = torch.Generator(device="cuda").manual_seed(M + I + 3 * O + z16 + 2 * x16)
+    dz = torch.randn(M, O, device="cuda", generator=g)
+    x = torch.randn(M, I, device="cuda", generator=g)
+    dzi = dz.bfloat16() if z16 else dz
+    xi = x.bfloat16() if x16 else x
+    dw, db = H.linear_wgrad_ex(dzi, xi, bias=True)
+    ref = _bf(dz).t() @ _bf(x)
+    assert ((dw.double() - ref).norm() / ref.norm()).item() < 1e-6
+    ref_b = dzi.double().sum(0)  # bias from the operand as stored (bf16 values or fp32)
+    assert ((db.double() - ref_b).abs().max() / ref_b.abs().max()).item() < 1e-5
+    dw2, db2 = H.linear_wgrad_ex(dzi, xi, bias=True)
+    assert torch.equal(dw, dw2) and torch.equal(db, db2), "must be deterministic"
+
+
+@pytest.mark.parametrize("p", [0.0, 0.1])
+def test_residual_block_fn_vs_float64(H, p):
+    """ResidualBlockFn forward and backward against a float64 restatement with the kernel's
+    roundings (bf16 operands, bf16 h/dd/dz storage) and the kernel's own dropout mask."""
+    from pointcloud_style_transfer_amd.models import _autograd as ag
+
+    torch.manual_seed(3)
+    layer = torch.nn.Sequential(torch.nn.Linear(256, 512), torch.nn.ReLU(), torch.nn.Linear(512, 256),
+                                torch.nn.Dropout(p)).cuda()
+    x = torch.randn(4, 3000, 256, device="cuda", requires_grad=True)
+    torch.manual_seed(9)
+    y = ag.residual_block(x, layer, training=True)
+    gy = torch.randn_like(y)
+    y.backward(gy)
+    torch.manual_seed(9)
+    seed = int(torch.randint(0, 2 ** 62, (1,)).item()) if p > 0 else 0
+    M = x.numel() // 256
+    keep = (H.dropout_grad_bf16(torch.ones(M, 256, device="cuda"), seed, p) != 0).double()
+    s = 1.0 / (1.0 - p)
+    w1, b1 = layer[0].weight.detach(), layer[0].bias.detach().double()
+    w2, b2 = layer[2].weight.detach(), layer[2].bias.detach().double()
+    x2 = x.detach().reshape(M, 256)
+    h = (_bf(x2) @ _bf(w1).t() + b1).clamp_min(0)
+    hb = h.bfloat16().double()
+    y_ref = x2.double() + keep * (hb @ _bf(w2).t() + b2) * s
+    rel = lambda a, b: ((a.double() - b).norm() / b.norm()).item()  # noqa: E731
+    assert rel(y.detach().reshape(M, 256), y_ref) < 1e-5
+    g = gy.reshape(M, 256).double()
+    dd = (g * keep * s).float().bfloat16().double()
+    dz = ((dd @ _bf(w2)) * (hb > 0)).float().bfloat16().double()
+    gx = g + dz @ _bf(w1)
+    assert rel(x.grad.reshape(M, 256), gx) < 1e-3
+    assert rel(layer[2].weight.grad, dd.t() @ hb) < 1e-3
+    assert rel(layer[2].bias.grad, dd.sum(0)) < 1e-3
+    assert rel(layer[0].weight.grad, dz.t() @ _bf(x2)) < 1e-3
+    assert rel(layer[0].bias.grad, dz.sum(0)) < 1e-3
+
+
+def test_noise_predictor_fused_blocks_match_unfused(H):
+    """Under autocast with dropout off, the fused residual blocks give the same forward and
+    gradients as the per-linear LinearFn path within bf16 storage error."""
+    from pointcloud_style_transfer_amd.config.config import Config
+    from pointcloud_style_transfer_amd.models.diffusion_model import NoisePredictor
+
+    torch.manual_seed(0)
+    npred = NoisePredictor(Config(make_dirs=False)).cuda().train()
+    for l in npred.layers:
+        l[3].p = 0.0
+    x = torch.randn(2, 4000, 3, device="cuda")
+    t = torch.tensor([10, 500], device="cuda")
+    sf = torch.randn(2, 256, device="cuda")
+    outs, grads = [], []
+    for fused in (True, False):
+        npred.zero_grad()
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            out = npred(x, t, sf) if fused else _unfused_forward(npred, x, t, sf)
+        out.float().pow(2).sum().backward()
+        outs.append(out.detach().float())
+        grads.append([p.grad.detach().clone() for p in npred.parameters()])
+    rel = lambda a, b: ((a.double() - b.double()).norm() / b.double().norm()).item()  # noqa: E731
+    assert rel(outs[0], outs[1]) < 2e-2
+    for a, b in zip(grads[0], grads[1]):
+        assert rel(a, b) < 5e-2
+
+
+def _unfused_forward(npred, noisy_points, timestep, style_feat):
+    from pointcloud_style_transfer_amd.models import _autograd as ag
+
+    pe = npred.point_encoder
+    h = ag.linear(noisy_points, pe[0], True)
+    h = ag.linear(h, pe[2], True)
+    pf = ag.linear(h, pe[4])
+    tf = ag.linear(npred.time_embedding(timestep), npred.time_proj)
+    sf = ag.linear(style_feat, npred.style_proj)
+    x = pf + tf.unsqueeze(1) + sf.unsqueeze(1)
+    for layer in npred.layers:
+        x = ag.linear(ag.linear(x, layer[0], True), layer[2]) + x
+    h = ag.linear(x, npred.output_mlp[0], True)
+    h = ag.linear(h, npred.output_mlp[2], True)
+    return ag.linear(h, npred.output_mlp[4])
