@@ -210,6 +210,9 @@ int pcst_knn3_build(const float* orig, const int64_t* idx, int64_t B, int64_t N,
                     void* workspace, void* stream);
 int pcst_knn3_query(const float* coarse, const float* orig, int64_t B, int64_t N, int64_t M,
                     float* out, void* workspace, void* stream);
+/* diagnostics of the last query on a workspace: out[0] error flag, out[1..B] query chunks per
+ * cloud, out[1+B..2B] outlier queries per cloud (device int32 buffer of 1 + 2B) */
+int pcst_knn_stats(void* workspace, int64_t B, int64_t N, int64_t M, int32_t* out, void* stream);
 int pcst_knn_error(void* workspace, int64_t B, int64_t N, int64_t M, int32_t* err_out,
                    void* stream);
 

@@ -51,6 +51,7 @@ SIGNATURES = {
     "pcst_voxel_downsample_copies_dseed": [_P, _I, _I, _I, _I, _P, _P, _P, _P, _P],
     "pcst_knn3_query": [_P, _P, _I, _I, _I, _P, _P, _P],
     "pcst_knn_error": [_P, _I, _I, _I, _P, _P],
+    "pcst_knn_stats": [_P, _I, _I, _I, _P, _P],
     "pcst_noise_mlp_blob_bytes": [ctypes.c_int],
     "pcst_noise_cond": [_P, _P, _I, _P, _P, _P, _P, _P, _P, _P, _P],
     "pcst_noise_mlp": [_P, _I, _I, _P, _I, _P, _I, _P, ctypes.c_int, _P, _P],
@@ -339,8 +340,9 @@ def knn3_query(coarse, handle):
     return out
 
 
-def knn3_interp(coarse, orig, idx, check=False):
-    """HierarchicalProcessor.upsample_knn: coarse [B,M,3], orig [B,N,3], idx [B,M] -> [B,N,3]."""
+def knn3_interp(coarse, orig, idx, check=False, stats=None):
+    """HierarchicalProcessor.upsample_knn: coarse [B,M,3], orig [B,N,3], idx [B,M] -> [B,N,3].
+    stats (a list): appends {"chunks": [...], "outliers": [...]} per call (diagnostics)."""
     require_device(coarse, orig, idx)
     coarse, orig, idx = _f32(coarse), _f32(orig), _i64(idx)
     B, N, _ = orig.shape
@@ -354,6 +356,11 @@ def knn3_interp(coarse, orig, idx, check=False):
         _call("pcst_knn_error", _ptr(ws), B, N, M, _ptr(err), _stream())
         if int(err.item()):
             raise RuntimeError("knn3_interp: coarse index outside [0, N)")
+    if stats is not None:
+        st = torch.zeros(1 + 2 * B, dtype=torch.int32, device=orig.device)
+        _call("pcst_knn_stats", _ptr(ws), B, N, M, _ptr(st), _stream())
+        st = st.cpu().tolist()
+        stats.append({"chunks": st[1:1 + B], "outliers": st[1 + B:]})
     return out
 
 

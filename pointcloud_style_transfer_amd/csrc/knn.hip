@@ -43,15 +43,20 @@ namespace pcst {
 #endif
 constexpr double kRefsPerCell = KNN_REFS_PER_CELL;  // refs per cell at the cloud's peak density
 constexpr int kCandCap = 512;            // LDS candidates per wave
-constexpr int kBallCells = 512;          // largest cell box one lane's ball may ask for
-constexpr int kBallUnion = 1024;         // largest union box of a ball pass
-constexpr uint32_t kBallBudget = 2048;   // refs the ball pass may stage
+#ifndef KNN_BALL_CELLS  // experiment builds may override
+#define KNN_BALL_CELLS 512
+#define KNN_BALL_UNION 1024
+#define KNN_BALL_BUDGET 2048
+#endif
+constexpr int kBallCells = KNN_BALL_CELLS;         // largest cell box one lane's ball may ask for
+constexpr int kBallUnion = KNN_BALL_UNION;         // largest union box of a ball pass
+constexpr uint32_t kBallBudget = KNN_BALL_BUDGET;  // refs the ball pass may stage
 constexpr int kKnnTile = 4096;           // scan tile (256 threads x 16)
 constexpr int kKnnMaxTiles = 1024;       // per-block LDS tile histogram in the count kernel
 constexpr int kPreKnownBlocks = 64;      // known-row scatter blocks per cloud in the pre kernel
 constexpr int kCountPerBlock = 1024;     // elements per count-kernel block (4 per thread)
 constexpr int kQueryBlocks = 1024;       // query workgroups per cloud (grid-stride over chunks)
-constexpr int kOutlierThreads = 1024;    // one outlier query per workgroup
+constexpr int kOutlierThreads = 1024;    // outlier-pass workgroup
 constexpr int kOutlierBlocks = 128;      // outlier workgroups per cloud
 
 #ifdef KNN_TRACE  // experiment builds only: per-chunk pass timings (tools/knn_trace.py)
@@ -453,7 +458,7 @@ __device__ __forceinline__ float dist1(const Win& W, int i, float ax, float ay, 
 }
 
 // One query: an fp32 screen and the exact (float64) top-3.
-//   consider(): one candidate at a time (outlier pass): screen against the exact 3rd best.
+//   consider(): one candidate at a time: screen against the exact 3rd best.
 //   window():   a staged window of candidates in two phases.  Phase 1 keeps the fp32 three
 //               smallest distances branch-free (min / med3 / med3); phase 2 screens the window
 //               against that fp32 3rd best into a register mask per 64 refs; the survivors
@@ -784,9 +789,59 @@ __device__ __forceinline__ void wave_merge_top3(Top3& t, int top = 32) {
   }
 }
 
-// Exhaustive 3-NN of the outlier queries: one workgroup per query, thread i scans refs i,
-// i+1024, ... (8 loads in flight), then a wave butterfly and a 16-lane butterfly over the
-// waves' results.
+// Exhaustive 3-NN of the outlier queries, kOutPB queries per workgroup iteration: thread i
+// takes refs i, i+1024, ... (kOutLd loads in flight) and scores each against all kOutPB queries, so
+// a ref is read from L2 once per kOutPB queries.
+//   phase 1: the fp32 three smallest per thread and query (branch-free), merged by a wave
+//            butterfly and one wave per query over the 16 waves: the query's fp32 kk-th
+//            smallest, and from it the query pass's screen (fp32 error margin);
+//   phase 2: the refs within the screen (a handful) are appended to the query's LDS list;
+//   rank:    one wave per query ranks its list in float64 (Top3's (distance, j) order is
+//            independent of the visiting order, so the atomic appends stay deterministic).
+// A list that overflows (many refs at exactly the screen distance) falls back to the
+// block-wide float64 scan of that query.  With at most one query per workgroup (the common
+// case after the first steps of a trajectory) each workgroup scans its query alone in one
+// pass (outlier_full: fewest dependent steps per query); the two-phase batch pays off once
+// the L2 re-reads of one-query-per-block dominate (the noisy first steps: ~500 per cloud).
+constexpr int kOutPB = 4;        // queries per workgroup iteration (even: packed pairs)
+constexpr int kOutLd = 4;        // ref loads in flight per thread (multi-query path)
+constexpr int kOutCap = 1024;    // LDS candidates per query
+
+template <int kk>
+__device__ void outlier_full(const float4* __restrict__ R, const float* __restrict__ V, int64_t M,
+                             float x, float y, float z, float* __restrict__ o, double (*sd)[3],
+                             int (*sj)[3]) {
+  constexpr int W = kOutlierThreads / 64, Q = kOutlierThreads;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  Query me;
+  me.init(x, y, z);
+  for (int64_t i = threadIdx.x; i < M; i += Q) me.consider(R[i], kk);
+  wave_merge_top3(me.t);
+  if (lane == 0) {
+    sd[wv][0] = me.t.d0; sd[wv][1] = me.t.d1; sd[wv][2] = me.t.d2;
+    sj[wv][0] = me.t.j0; sj[wv][1] = me.t.j1; sj[wv][2] = me.t.j2;
+  }
+  __syncthreads();
+  if (wv == 0) {
+    Top3 t;
+    t.init();
+    if (lane < W) {
+      t.d0 = sd[lane][0]; t.d1 = sd[lane][1]; t.d2 = sd[lane][2];
+      t.j0 = sj[lane][0]; t.j1 = sj[lane][1]; t.j2 = sj[lane][2];
+    }
+    wave_merge_top3(t, W / 2);
+    if (lane == 0) idw_write(t, kk, V, o);
+  }
+  __syncthreads();
+}
+
+__device__ __forceinline__ void top3f(float& c0, float& c1, float& c2, float d) {
+  const float n0 = fminf(c0, d);
+  const float n1 = __builtin_amdgcn_fmed3f(c0, c1, d);
+  const float n2 = __builtin_amdgcn_fmed3f(c1, c2, d);
+  c0 = n0; c1 = n1; c2 = n2;
+}
+
 template <int kk>
 __global__ __launch_bounds__(kOutlierThreads) void knn_outlier_kernel(
     const float* __restrict__ vals, int64_t N, int64_t M, const float* __restrict__ orig,
@@ -795,8 +850,14 @@ __global__ __launch_bounds__(kOutlierThreads) void knn_outlier_kernel(
     float* __restrict__ out) {
   constexpr int W = kOutlierThreads / 64;
   constexpr int Q = kOutlierThreads;
+  constexpr int P = kOutPB;
   __shared__ double sd[W][3];
   __shared__ int sj[W][3];
+  __shared__ float sc3[P][W][3];
+  __shared__ float s_q[P][4];  // query x, y, z, screen
+  __shared__ int64_t s_n[P];
+  __shared__ int s_cnt[P];
+  __shared__ int s_cand[P][kOutCap];
   const int b = blockIdx.y;
   // rows that are coarse points take the coarse value (result[idx] = coarse; the last coarse
   // row writing a point wins, as in the reference's index assignment)
@@ -812,44 +873,122 @@ __global__ __launch_bounds__(kOutlierThreads) void knn_outlier_kernel(
   const float4* R = refs + b * M;
   const float* V = vals + b * M * 3;
   const int cnt = ocount[b];
-  for (int q = blockIdx.x; q < cnt; q += gridDim.x) {
-    const int64_t n = olist[b * N + q];
-    const float* p = orig + (b * N + n) * 3;
-    Query me;
-    me.init(p[0], p[1], p[2]);
-    int64_t i = threadIdx.x;
-    for (; i + 7 * Q < M; i += 8 * Q) {  // 8 loads in flight per thread
-      float4 r[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) r[u] = R[i + u * Q];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) me.consider(r[u], kk);
+  if (cnt <= (int)gridDim.x) {  // at most one query per workgroup
+    for (int q = blockIdx.x; q < cnt; q += gridDim.x) {
+      const int64_t n = olist[b * N + q];
+      const float* p = orig + (b * N + n) * 3;
+      outlier_full<kk>(R, V, M, p[0], p[1], p[2], out + (b * N + n) * 3, sd, sj);
     }
-    {
-      float4 r[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u)
-        if (i + u * Q < M) r[u] = R[i + u * Q];
-#pragma unroll
-      for (int u = 0; u < 8; ++u)
-        if (i + u * Q < M) me.consider(r[u], kk);
-    }
-    wave_merge_top3(me.t);
-    if (lane == 0) {
-      sd[wv][0] = me.t.d0; sd[wv][1] = me.t.d1; sd[wv][2] = me.t.d2;
-      sj[wv][0] = me.t.j0; sj[wv][1] = me.t.j1; sj[wv][2] = me.t.j2;
+    return;
+  }
+  for (int q0 = blockIdx.x * P; q0 < cnt; q0 += gridDim.x * P) {
+    if (threadIdx.x < P) {  // the iteration's queries; padding slots repeat the last one
+      const int qi = min(q0 + (int)threadIdx.x, cnt - 1);
+      const int64_t n = olist[b * N + qi];
+      const float* p = orig + (b * N + n) * 3;
+      s_n[threadIdx.x] = n;
+      s_q[threadIdx.x][0] = p[0]; s_q[threadIdx.x][1] = p[1]; s_q[threadIdx.x][2] = p[2];
+      s_cnt[threadIdx.x] = 0;
     }
     __syncthreads();
-    if (wv == 0) {  // the 16 wave results, merged by a 16-lane butterfly of wave 0
-      Top3 t;
-      t.init();
-      if (lane < W) {
-        t.d0 = sd[lane][0]; t.d1 = sd[lane][1]; t.d2 = sd[lane][2];
-        t.j0 = sj[lane][0]; t.j1 = sj[lane][1]; t.j2 = sj[lane][2];
-      }
-      wave_merge_top3(t, W / 2);
-      if (lane == 0) idw_write(t, kk, V, out + (b * N + n) * 3);
+    // query pairs in packed registers: one v_pk op scores a ref against two queries (the ref
+    // coordinate is broadcast to both halves); the same IEEE operations as dist32
+    f2 qx2[P / 2], qy2[P / 2], qz2[P / 2];
+    float c0[P], c1[P], c2[P];
+#pragma unroll
+    for (int u = 0; u < P / 2; ++u) {
+      qx2[u] = f2{s_q[2 * u][0], s_q[2 * u + 1][0]};
+      qy2[u] = f2{s_q[2 * u][1], s_q[2 * u + 1][1]};
+      qz2[u] = f2{s_q[2 * u][2], s_q[2 * u + 1][2]};
     }
+#pragma unroll
+    for (int u = 0; u < P; ++u) c0[u] = c1[u] = c2[u] = INFINITY;
+    // phase 1
+    for (int64_t i = threadIdx.x; i < M; i += kOutLd * Q) {
+      float4 r[kOutLd];
+#pragma unroll
+      for (int k = 0; k < kOutLd; ++k)
+        if (i + k * Q < M) r[k] = R[i + k * Q];
+#pragma unroll
+      for (int k = 0; k < kOutLd; ++k)
+        if (i + k * Q < M) {
+          const f2 rx = {r[k].x, r[k].x}, ry = {r[k].y, r[k].y}, rz = {r[k].z, r[k].z};
+#pragma unroll
+          for (int u = 0; u < P / 2; ++u) {
+            const f2 d = dist2(qx2[u], qy2[u], qz2[u], rx, ry, rz);
+            top3f(c0[2 * u], c1[2 * u], c2[2 * u], d.x);
+            top3f(c0[2 * u + 1], c1[2 * u + 1], c2[2 * u + 1], d.y);
+          }
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < P; ++u) {
+#pragma unroll
+      for (int off = 32; off >= 1; off >>= 1) {
+        const float o0 = __shfl_xor(c0[u], off), o1 = __shfl_xor(c1[u], off), o2 = __shfl_xor(c2[u], off);
+        top3f(c0[u], c1[u], c2[u], o0);
+        top3f(c0[u], c1[u], c2[u], o1);
+        top3f(c0[u], c1[u], c2[u], o2);
+      }
+      if (lane == 0) { sc3[u][wv][0] = c0[u]; sc3[u][wv][1] = c1[u]; sc3[u][wv][2] = c2[u]; }
+    }
+    __syncthreads();
+    if (wv < P) {  // wave u merges query u's 16 wave triples
+      float a0 = INFINITY, a1 = INFINITY, a2 = INFINITY;
+      if (lane < W) { a0 = sc3[wv][lane][0]; a1 = sc3[wv][lane][1]; a2 = sc3[wv][lane][2]; }
+#pragma unroll
+      for (int off = W / 2; off >= 1; off >>= 1) {
+        const float o0 = __shfl_xor(a0, off), o1 = __shfl_xor(a1, off), o2 = __shfl_xor(a2, off);
+        top3f(a0, a1, a2, o0);
+        top3f(a0, a1, a2, o1);
+        top3f(a0, a1, a2, o2);
+      }
+      if (lane == 0) {
+        const float ck = kk >= 3 ? a2 : (kk == 2 ? a1 : a0);
+        s_q[wv][3] = ck * 1.000002f + 1e-30f;  // the query pass's screen (fp32 error margin)
+      }
+    }
+    __syncthreads();
+    // phase 2: the screened-in refs of each query into its LDS list
+    f2 scr[P / 2];
+#pragma unroll
+    for (int u = 0; u < P / 2; ++u) scr[u] = f2{s_q[2 * u][3], s_q[2 * u + 1][3]};
+    for (int64_t i = threadIdx.x; i < M; i += kOutLd * Q) {
+      float4 r[kOutLd];
+#pragma unroll
+      for (int k = 0; k < kOutLd; ++k)
+        if (i + k * Q < M) r[k] = R[i + k * Q];
+#pragma unroll
+      for (int k = 0; k < kOutLd; ++k)
+        if (i + k * Q < M) {
+          const f2 rx = {r[k].x, r[k].x}, ry = {r[k].y, r[k].y}, rz = {r[k].z, r[k].z};
+#pragma unroll
+          for (int u = 0; u < P / 2; ++u) {
+            const f2 d = dist2(qx2[u], qy2[u], qz2[u], rx, ry, rz);
+#pragma unroll
+            for (int e = 0; e < 2; ++e)
+              if (d[e] <= scr[u][e]) {
+                const int slot = atomicAdd(&s_cnt[2 * u + e], 1);
+                if (slot < kOutCap) s_cand[2 * u + e][slot] = (int)(i + k * Q);
+              }
+          }
+        }
+    }
+    __syncthreads();
+    // rank: wave u, query u (a padding slot repeats a query: skipped)
+    if (wv < P && q0 + wv < cnt && s_cnt[wv] <= kOutCap) {
+      Query me;
+      me.init(s_q[wv][0], s_q[wv][1], s_q[wv][2]);
+      const int c = s_cnt[wv];
+      for (int k = lane; k < c; k += 64) me.exact(R[s_cand[wv][k]]);
+      wave_merge_top3(me.t);
+      if (lane == 0) idw_write(me.t, kk, V, out + (b * N + s_n[wv]) * 3);
+    }
+    // overflowed lists: the block-wide float64 scan (block-uniform condition)
+#pragma unroll 1
+    for (int u = 0; u < P; ++u)
+      if (q0 + u < cnt && s_cnt[u] > kOutCap)
+        outlier_full<kk>(R, V, M, s_q[u][0], s_q[u][1], s_q[u][2], out + (b * N + s_n[u]) * 3, sd, sj);
     __syncthreads();
   }
 }
@@ -937,6 +1076,19 @@ extern "C" int pcst_knn_trace_dump(void* host, size_t bytes) {
   return PCST_OK;
 }
 #endif
+
+// diagnostics: out[0] = error flag, out[1..B] = query chunks, out[1+B..2B] = outlier queries of
+// the last pcst_knn3_query on this workspace
+extern "C" int pcst_knn_stats(void* workspace, int64_t B, int64_t N, int64_t M, int32_t* out,
+                              void* stream) {
+  KnnWS w = carve_knn(workspace, B, N, M);
+  hipStream_t s = as_stream(stream);
+  PCST_HIP(hipMemcpyAsync(out, w.err, sizeof(int32_t), hipMemcpyDeviceToDevice, s), "knn_stats");
+  PCST_HIP(hipMemcpyAsync(out + 1, w.nchunk, sizeof(int32_t) * B, hipMemcpyDeviceToDevice, s), "knn_stats");
+  PCST_HIP(hipMemcpyAsync(out + 1 + B, w.ocount, sizeof(int32_t) * B, hipMemcpyDeviceToDevice, s),
+           "knn_stats");
+  return PCST_OK;
+}
 
 extern "C" int pcst_knn_error(void* workspace, int64_t B, int64_t N, int64_t M, int32_t* err_out,
                               void* stream) {
