@@ -71,15 +71,26 @@ class DiffusionLoss(nn.Module):
     def forward(self, predicted_noise: torch.Tensor, actual_noise: torch.Tensor,
                 predicted_points_coarse: torch.Tensor = None,
                 target_points_coarse: torch.Tensor = None) -> Tuple[torch.Tensor, Dict[str, float]]:
-        loss_dict = {}
+        total, terms = self.forward_tensors(predicted_noise, actual_noise, predicted_points_coarse,
+                                            target_points_coarse)
+        return total, {k: v.item() for k, v in terms.items()}
+
+    def forward_tensors(self, predicted_noise: torch.Tensor, actual_noise: torch.Tensor,
+                        predicted_points_coarse: torch.Tensor = None,
+                        target_points_coarse: torch.Tensor = None
+                        ) -> Tuple[torch.Tensor, Dict[str, torch.Tensor]]:
+        """forward() with the loss dict still as 0-d device tensors: the trainer converts them
+        after the backward is queued, so the reference's three `.item()` syncs do not stall
+        the GPU between the forward and the backward."""
+        terms = {}
         noise_loss = l1_loss(predicted_noise, actual_noise)
         total = self.noise_weight * noise_loss
-        loss_dict["noise_loss"] = noise_loss.item()
+        terms["noise_loss"] = noise_loss.detach()
         if (self.chamfer_weight > 0 and predicted_points_coarse is not None
                 and target_points_coarse is not None):
             cl = torch.mean(chamfer_distance_chunked_optimized(predicted_points_coarse,
                                                                target_points_coarse))
             total = total + self.chamfer_weight * cl
-            loss_dict["chamfer_loss"] = cl.item()
-        loss_dict["total_loss"] = total.item()
-        return total, loss_dict
+            terms["chamfer_loss"] = cl.detach()
+        terms["total_loss"] = total.detach()
+        return total, terms

@@ -103,8 +103,11 @@ class DiffusionTrainer:
         self.model = PointCloudDiffusionModel(config).to(self.device)
         self.diffusion_process = DiffusionProcess(config, device=str(self.device))
         self.loss_fn = DiffusionLoss(noise_weight=1.0, chamfer_weight=config.lambda_chamfer)
+        # fused AdamW on the GPU: one kernel for all parameters, and GradScaler hands it
+        # found_inf on the device instead of synchronising on it (torch's amp-scaling protocol)
         self.optimizer = optim.AdamW(self.model.parameters(), lr=config.learning_rate,
-                                     weight_decay=config.weight_decay, betas=(0.9, 0.95))
+                                     weight_decay=config.weight_decay, betas=(0.9, 0.95),
+                                     fused=self.device_type == "cuda")
         if config.lr_scheduler == "cosine_with_warmup":
             self.scheduler = CosineWithWarmupLR(self.optimizer, config.warmup_epochs,
                                                 config.num_epochs, config.min_lr_ratio)
@@ -144,7 +147,7 @@ class DiffusionTrainer:
         ctx = (self.ddp_model.no_sync() if self.distributed and not sync
                else contextlib.nullcontext())
         with ctx:
-            loss, loss_dict = self._forward_backward(batch)
+            loss, terms = self._forward_backward(batch)
         if sync:
             self.scaler.unscale_(self.optimizer)
             torch.nn.utils.clip_grad_norm_(self.model.parameters(), self.gradient_clip_norm)
@@ -152,6 +155,9 @@ class DiffusionTrainer:
             self.scaler.update()
             self.optimizer.zero_grad()
             self.ema.update()
+        # the reference's loss dict of python floats (losses.py:93-102), read once the whole
+        # step is queued: its syncs then wait on work already in flight
+        loss_dict = {k: v.item() for k, v in terms.items()}
         return loss, loss_dict
 
     def _forward_backward(self, batch):
@@ -175,14 +181,15 @@ class DiffusionTrainer:
                     a = self.diffusion_process.sqrt_alphas_cumprod[t].view(B, 1, 1)
                     b = self.diffusion_process.sqrt_one_minus_alphas_cumprod[t].view(B, 1, 1)
                     pred_x0_coarse = (noisy_coarse - b * pred) / (a + 1e-8)
-                loss, loss_dict = self.loss_fn(predicted_noise=pred, actual_noise=actual_coarse,
-                                               predicted_points_coarse=pred_x0_coarse,
-                                               target_points_coarse=sim_coarse)
+                loss, terms = self.loss_fn.forward_tensors(
+                    predicted_noise=pred, actual_noise=actual_coarse,
+                    predicted_points_coarse=pred_x0_coarse, target_points_coarse=sim_coarse)
             else:
-                loss, loss_dict = self.loss_fn(predicted_noise=pred, actual_noise=actual_noise)
+                loss, terms = self.loss_fn.forward_tensors(predicted_noise=pred,
+                                                           actual_noise=actual_noise)
             loss = loss / self.gradient_accumulation_steps
         self.scaler.scale(loss).backward()
-        return loss, loss_dict
+        return loss, terms
 
     def train_one_epoch(self, data_loader):
         self.model.train()
