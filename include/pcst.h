@@ -254,8 +254,13 @@ int pcst_voxel_downsample_copies_dseed(const float* pts, int64_t B, int64_t N, i
 /* chamfer_distance_chunked_optimized (losses.py:8-63), never materialising N x M:
  * min1/arg1 [B,N] = row minima pred->target of clamp((|p|^2+|q|^2) + (-2 p.q), 0) (first index
  * on ties), min2/arg2 [B,M] target->pred, out [B] = mean(min1) + mean(min2) (may be NULL).
- * workspace: both clouds repacked as point pairs for the packed-fp32 row-min kernel. */
+ * workspace: the clouds repacked as point pairs (exhaustive row-min) or counting-sorted into
+ * uniform grids (grid-pruned row-min). */
 int pcst_chamfer_fwd_workspace_size(int64_t B, int64_t N, int64_t M, size_t* bytes);
+/* forward path: 0 default (= exhaustive), 1 exhaustive, 2 grid-pruned (fast for overlapping
+ * clouds, slow for rows far outside the other cloud); all give bit-identical minima and
+ * first-index argmins */
+int pcst_chamfer_set_mode(int mode);
 int pcst_chamfer_fwd(const float* pred, const float* target, int64_t B, int64_t N, int64_t M,
                      float* min1, int32_t* arg1, float* min2, int32_t* arg2, float* out,
                      void* workspace, void* stream);

@@ -75,6 +75,7 @@ SIGNATURES = {
     "pcst_channel_stats": [_P, _I, _I, _P, _P, _P, _P],
     "pcst_affine_act": [_P, _I, _I, _P, _P, ctypes.c_int, _I, _P, _P],
     "pcst_chamfer_fwd_workspace_size": [_I, _I, _I, _SZ],
+    "pcst_chamfer_set_mode": [ctypes.c_int],
     "pcst_chamfer_fwd": [_P, _P, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P],
     "pcst_chamfer_bwd_workspace_size": [_I, _I, _I, _SZ],
     "pcst_chamfer_bwd": [_P, _P, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P],
@@ -647,6 +648,11 @@ def chamfer_fwd(pred, target):
     _call("pcst_chamfer_fwd", _ptr(pred), _ptr(target), B, N, M, _ptr(min1), _ptr(arg1),
           _ptr(min2), _ptr(arg2), _ptr(out), _ptr(ws), _stream())
     return out, arg1, arg2
+
+
+def chamfer_set_mode(mode):
+    """Chamfer forward path: 0 auto, 1 exhaustive, 2 grid-pruned (tests force one)."""
+    _call("pcst_chamfer_set_mode", int(mode))
 
 
 def chamfer_bwd(pred, target, arg1, arg2, grad_out, need_pred=True, need_target=False):

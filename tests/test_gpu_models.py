@@ -168,12 +168,14 @@ def test_chamfer_and_loss(mods, golden):
     assert abs(float(total) - float(g["dl_total"])) < 1e-5 * float(g["dl_total"])
 
 
+@pytest.mark.parametrize("mode", [1, 2])
 @pytest.mark.parametrize("N,M", [(3000, 2500), (257, 1), (1, 700), (4096, 4096)])
-def test_chamfer_rowmin_exact_vs_oracle(N, M):
-    """Row minima and first-index argmins of the packed-math kernel, bit-exact against the
-    oracle's scalar restatement (losses.py:36-41), on clouds with duplicated target points and
-    query points equal to targets (raw D <= 0 ties broken by the clamp's first index), sizes
-    that leave the last 256-point chunk ragged, and single-point clouds."""
+def test_chamfer_rowmin_exact_vs_oracle(N, M, mode):
+    """Row minima and first-index argmins of both forward paths (1: packed exhaustive, 2:
+    grid-pruned), bit-exact against the oracle's scalar restatement (losses.py:36-41), on clouds
+    with duplicated target points and query points equal to targets (raw D <= 0 ties broken by
+    the clamp's first index), sizes that leave the last 256-point chunk ragged, and single-point
+    clouds."""
     from pointcloud_style_transfer_amd import _hip
 
     import oracle.oracle as orc
@@ -184,7 +186,11 @@ def test_chamfer_rowmin_exact_vs_oracle(N, M):
     if M > 8:
         q[:, M // 2:M // 2 + 4] = q[:, 1:5]      # duplicates at later indices
         p[:, :min(N, M) // 3] = q[:, :min(N, M) // 3]  # exact hits: raw D may round below 0
-    out, a1, a2 = _hip.chamfer_fwd(dev(p), dev(q))
+    _hip.chamfer_set_mode(mode)
+    try:
+        out, a1, a2 = _hip.chamfer_fwd(dev(p), dev(q))
+    finally:
+        _hip.chamfer_set_mode(0)
     a1, a2 = a1.cpu().numpy(), a2.cpu().numpy()
     ref = []
     for b in range(2):
@@ -194,6 +200,44 @@ def test_chamfer_rowmin_exact_vs_oracle(N, M):
         np.testing.assert_array_equal(a2[b], r2)
         ref.append(m1.astype(np.float64).mean() + m2.astype(np.float64).mean())
     np.testing.assert_allclose(out.cpu().numpy(), np.array(ref), rtol=1e-6)
+
+
+@pytest.mark.parametrize("kind", ["lidar", "gauss_aniso", "far_apart", "dup_heavy"])
+def test_chamfer_grid_equals_exhaustive_30k(kind):
+    """The grid-pruned forward against the exhaustive one at the trainer's size (8 x 30000 per
+    side): minima, argmins and means bit-equal.  Cloud kinds: LiDAR-like rings scaled to tens
+    of metres (the trainer's coarse clouds), an anisotropic Gaussian, two clouds offset far from
+    each other (rows outside the other grid), and heavy duplication (many exact ties)."""
+    from pointcloud_style_transfer_amd import _hip
+    from pointcloud_style_transfer_amd.synthetic import lidar_like_cloud
+
+    rng = np.random.default_rng(11)
+    B, N, M = 8, 30000, 30000
+    if kind == "lidar":
+        p = np.stack([lidar_like_cloud(100 + i, N) * 20 + 5 for i in range(B)]).astype(np.float32)
+        q = np.stack([lidar_like_cloud(200 + i, M) * 30 - 2 for i in range(B)]).astype(np.float32)
+    elif kind == "gauss_aniso":
+        p = (rng.standard_normal((B, N, 3)) * [10, 10, 0.5]).astype(np.float32)
+        q = (rng.standard_normal((B, M, 3)) * [10, 10, 0.5]).astype(np.float32)
+    elif kind == "far_apart":
+        p = rng.standard_normal((B, N, 3)).astype(np.float32)
+        q = (rng.standard_normal((B, M, 3)) + 40.0).astype(np.float32)
+    else:
+        base = rng.standard_normal((B, 600, 3)).astype(np.float32)
+        p = base[:, rng.integers(0, 600, N)]
+        q = base[:, rng.integers(0, 600, M)]
+    res = {}
+    for mode in (1, 2):
+        _hip.chamfer_set_mode(mode)
+        try:
+            P, Q = dev(p), dev(q)
+            out, a1, a2 = _hip.chamfer_fwd(P, Q)
+            torch.cuda.synchronize()
+            res[mode] = (out.cpu().numpy(), a1.cpu().numpy(), a2.cpu().numpy())
+        finally:
+            _hip.chamfer_set_mode(0)
+    for x, y in zip(res[1], res[2]):
+        np.testing.assert_array_equal(x, y)
 
 
 def test_chamfer_determinism(mods):
