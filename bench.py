@@ -26,6 +26,7 @@ Prints ONE JSON line on rank 0 (driver contract), including
 from __future__ import annotations
 
 import argparse
+import contextlib
 import json
 import os
 import socket
@@ -281,6 +282,7 @@ def main():
     device = torch.device("cuda", torch.cuda.current_device())
     from pointcloud_style_transfer_amd import _hip
     from pointcloud_style_transfer_amd.distributed import max_over_ranks, shard
+    from pointcloud_style_transfer_amd.models import diffusion_model as dmod
     from pointcloud_style_transfer_amd.synthetic import lidar_like_cloud, standard_normal
 
     cfg, model, dp = build_model(args.precision, device)
@@ -323,43 +325,63 @@ def main():
         x_cat = torch.cat([x, x]).contiguous()
         ev = []
 
+        # the product loop's stream layout (DiffusionProcess.guided_sample_loop): the step on a
+        # high-priority stream, the kNN build on a side stream during the noise MLP
+        overlap = dmod._OVERLAP_KNN_BUILD
+        loop_stream, side = dmod.step_streams(device) if overlap else (None, None)
+        if overlap:
+            loop_stream.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(loop_stream):
+                knn_ws = _hip.knn_workspace(2 * C, args.points, cfg.global_points, device=device)
+            _hip.knn_set_build_lds_pad(dmod._KNN_BUILD_LDS_PAD)
+        else:
+            knn_ws = None
+
         def step(i, timed):
             nonlocal x
             t = timesteps[i % len(timesteps)]
             t_prev = timesteps[i % len(timesteps) + 1] if t > 0 else -1
             t_in = t_rows[i % len(timesteps)]
             xc, xi = hp.downsample_copies(x, 2)
-            if timed:
-                e0 = torch.cuda.Event(enable_timing=True)
+
+            def mlp(xc_):
+                if not timed:
+                    return npred(xc_, t_in, style_in)
+                e0 = torch.cuda.Event(enable_timing=True)  # on the stream the MLP runs on
                 e1 = torch.cuda.Event(enable_timing=True)
                 blob, bias = npred.packed()[:2]
                 cnd = npred.cond(t_in, style_in)
                 e0.record()
-                nc = _hip.noise_mlp(xc.reshape(-1, 3), cfg.global_points, cnd, blob, bias,
-                                    npred.precision_code).view(2 * C, -1, 3)
+                nc_ = _hip.noise_mlp(xc_.reshape(-1, 3), cfg.global_points, cnd, blob, bias,
+                                     npred.precision_code).view(2 * C, -1, 3)
                 e1.record()
                 ev.append((e0, e1))
-            else:
-                nc = npred(xc, t_in, style_in)
-            eps = hp.upsample_knn(nc, x_cat, xi)
+                return nc_
+
+            eps = dmod.hierarchical_eps(hp, mlp, xc, xi, x_cat, knn_ws, side)
             x = _hip.cfg_ddim_step(x, eps[:C], eps[C:], src, 7.5, dp._coeffs(t, t_prev),
                                    x_cat=x_cat)
 
-        for i in range(args.warmup):
-            step(i, False)
-        # the timed region restarts the sampling trajectory at t = 999 from x_T
-        x = torch.from_numpy(xT_np).to(device)
-        x_cat.copy_(torch.cat([x, x]))
+        lctx = torch.cuda.stream(loop_stream) if overlap else contextlib.nullcontext()
+        with lctx:
+            for i in range(args.warmup):
+                step(i, False)
+            # the timed region restarts the sampling trajectory at t = 999 from x_T
+            x = torch.from_numpy(xT_np).to(device)
+            x_cat.copy_(torch.cat([x, x]))
         if world > 1:
             import torch.distributed as dist
 
             dist.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        for i in range(args.steps):
-            step(i, True)
+        with lctx:
+            for i in range(args.steps):
+                step(i, True)
         torch.cuda.synchronize()
         elapsed = time.perf_counter() - t0
+        if overlap:
+            _hip.knn_set_build_lds_pad(0)
         if world > 1:
             dist.barrier()
             elapsed = max_over_ranks(elapsed, device=device)

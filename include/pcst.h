@@ -213,6 +213,9 @@ int pcst_knn3_query(const float* coarse, const float* orig, int64_t B, int64_t N
 /* diagnostics of the last query on a workspace: out[0] error flag, out[1..B] query chunks per
  * cloud, out[1+B..2B] outlier queries per cloud (device int32 buffer of 1 + 2B) */
 int pcst_knn_stats(void* workspace, int64_t B, int64_t N, int64_t M, int32_t* out, void* stream);
+/* dynamic LDS (bytes, <= 96 KiB) added to the build-phase workgroups: a build on a side stream
+ * then runs only on CUs the noise MLP leaves idle (see pcst_knn3_build) */
+int pcst_knn_set_build_lds_pad(int64_t bytes);
 int pcst_knn_error(void* workspace, int64_t B, int64_t N, int64_t M, int32_t* err_out,
                    void* stream);
 

@@ -52,6 +52,7 @@ SIGNATURES = {
     "pcst_knn3_query": [_P, _P, _I, _I, _I, _P, _P, _P],
     "pcst_knn_error": [_P, _I, _I, _I, _P, _P],
     "pcst_knn_stats": [_P, _I, _I, _I, _P, _P],
+    "pcst_knn_set_build_lds_pad": [_I],
     "pcst_noise_mlp_blob_bytes": [ctypes.c_int],
     "pcst_noise_cond": [_P, _P, _I, _P, _P, _P, _P, _P, _P, _P, _P],
     "pcst_noise_mlp": [_P, _I, _I, _P, _I, _P, _I, _P, ctypes.c_int, _P, _P],
@@ -315,14 +316,25 @@ def voxel_stats(points, target):
 
 
 # ----------------------------------------------------------------------------- kNN upsample
-def knn3_build(orig, idx):
+def knn_workspace(B, N, M, device):
+    """A workspace for knn3_build/knn3_query (allocate it on the stream that outlives both)."""
+    return _workspace("pcst_knn_workspace_size", B, N, M, device=device)
+
+
+def knn_set_build_lds_pad(nbytes):
+    _call("pcst_knn_set_build_lds_pad", int(nbytes))
+
+
+def knn3_build(orig, idx, ws=None):
     """Phase 1 of knn3_interp (positions only) on the current stream -> workspace handle
-    (orig, idx, workspace) for knn3_query."""
+    (orig, idx, workspace) for knn3_query.  `ws` (knn_workspace) may be preallocated, e.g. on
+    the stream that runs the query when the build runs on a side stream."""
     require_device(orig, idx)
     orig, idx = _f32(orig), _i64(idx)
     B, N, _ = orig.shape
     M = idx.shape[1]
-    ws = _workspace("pcst_knn_workspace_size", B, N, M, device=orig.device)
+    if ws is None:
+        ws = _workspace("pcst_knn_workspace_size", B, N, M, device=orig.device)
     _call("pcst_knn3_build", _ptr(orig), _ptr(idx), B, N, M, _ptr(ws), _stream())
     return (orig, idx, ws)
 
@@ -765,7 +777,7 @@ _GUARDED = ("square_distance", "index_points", "fps", "ball_query", "group_gathe
             "chamfer_bwd", "l1_fwd", "l1_bwd", "knn_dist", "emd_greedy", "voxel_center_dist",
             "cfg_ddim_step_dcoef", "voxel_downsample_copies_dseed", "bn_train_coeffs",
             "bn_relu_maxpool", "bn_relu_bwd", "group_gather_bwd", "gemm_ex", "dropout_grad_bf16",
-            "linear_wgrad_ex")
+            "linear_wgrad_ex", "knn_workspace", "knn_set_build_lds_pad", "chamfer_set_mode")
 for _name in _GUARDED:
     globals()[_name] = _on_tensor_device(globals()[_name])
 del _name

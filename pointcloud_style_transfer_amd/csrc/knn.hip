@@ -1003,6 +1003,17 @@ extern "C" int pcst_knn_workspace_size(int64_t B, int64_t N, int64_t M, size_t* 
   return PCST_OK;
 }
 
+// Dynamic LDS added to every build workgroup (pcst_knn_set_build_lds_pad).  A build that runs
+// on a side stream during the noise MLP then cannot co-reside with an MLP workgroup (~130 KiB
+// of LDS): it only takes the CUs the MLP leaves idle in its last partial round.
+static unsigned g_knn_build_lds_pad = 0;
+
+extern "C" int pcst_knn_set_build_lds_pad(int64_t bytes) {
+  PCST_CHECK_ARG(bytes >= 0 && bytes <= 98304, "knn_set_build_lds_pad: 0..98304 bytes");
+  g_knn_build_lds_pad = (unsigned)bytes;
+  return PCST_OK;
+}
+
 // Phase 1 (positions only: the coarse set's points and the full cloud): grid statistics, the
 // packed cell counts, scan, fill.  Phase 2 (needs the coarse values, i.e. the noise MLP's
 // output): known rows, the query passes and the outlier pass.  Splitting them lets a caller run
@@ -1017,19 +1028,20 @@ extern "C" int pcst_knn3_build(const float* orig, const int64_t* idx, int64_t B,
   hipStream_t s = as_stream(stream);
   KnnWS w = carve_knn(workspace, B, N, M);
   const int b = (int)B;
+  const unsigned lds_pad = g_knn_build_lds_pad;
   // error word, counters, known rows, tile sums and packed counts are contiguous in the carve
   PCST_HIP(hipMemsetAsync(w.err, 0, (size_t)(w.bytes - ((char*)w.err - (char*)workspace)), s),
            "knn: memset");
-  hipLaunchKernelGGL(knn_pre_kernel, dim3(kStatBlocks + kPreKnownBlocks, b), dim3(256), 0, s,
+  hipLaunchKernelGGL(knn_pre_kernel, dim3(kStatBlocks + kPreKnownBlocks, b), dim3(256), lds_pad, s,
                      orig, idx, (int)N, M, w.stats, w.known, w.err);
   const unsigned gc = (unsigned)cdiv(M + N, kCountPerBlock);
-  hipLaunchKernelGGL(knn_count_kernel, dim3(gc, b), dim3(256), 0, s, orig, idx, w.stats, w.known,
-                     N, M, w.Cmax, w.T, w.Cpad, w.gp, w.cnt, w.tsum, w.crank);
-  hipLaunchKernelGGL(knn_scan_kernel, dim3((unsigned)w.T, b), dim3(256), 0, s, w.cnt, w.tsum, w.T,
-                     w.Cpad, w.chunks, w.maxch, w.nchunk);
+  hipLaunchKernelGGL(knn_count_kernel, dim3(gc, b), dim3(256), lds_pad, s, orig, idx, w.stats,
+                     w.known, N, M, w.Cmax, w.T, w.Cpad, w.gp, w.cnt, w.tsum, w.crank);
+  hipLaunchKernelGGL(knn_scan_kernel, dim3((unsigned)w.T, b), dim3(256), lds_pad, s, w.cnt, w.tsum,
+                     w.T, w.Cpad, w.chunks, w.maxch, w.nchunk);
   const unsigned gf = (unsigned)std::min<int64_t>(cdiv(M + N, 256), 2048);
-  hipLaunchKernelGGL(knn_fill_kernel, dim3(gf, b), dim3(256), 0, s, orig, idx, N, M, w.Cpad, w.cnt,
-                     w.crank, w.refs, w.qorder);
+  hipLaunchKernelGGL(knn_fill_kernel, dim3(gf, b), dim3(256), lds_pad, s, orig, idx, N, M, w.Cpad,
+                     w.cnt, w.crank, w.refs, w.qorder);
   PCST_LAUNCH_CHECK("knn3_build");
   return PCST_OK;
 }

@@ -14,7 +14,9 @@ reference's draws; on the perf path the voxel subset is drawn on the device.
 """
 from __future__ import annotations
 
+import contextlib
 import math
+import os
 from typing import Dict, Optional, Tuple
 
 import numpy as np
@@ -211,6 +213,47 @@ class HierarchicalProcessor:
         return _hip.knn3_interp(coarse_points, original_points, coarse_indices)
 
 
+# The kNN upsample's build phase (grid, counts, sort: positions only) does not depend on the
+# noise MLP's output, so the sampling loop runs it on a side stream during the MLP.  The loop
+# itself moves to a high-priority stream and the build's workgroups carry extra LDS
+# (pcst_knn_set_build_lds_pad), so they cannot co-reside with an MLP workgroup and only take
+# the CUs the MLP leaves idle in its last partial round (469 workgroups on 256 CUs).  Measured
+# 0.493 -> 0.468 ms/step over the first 20 steps, 0.421 -> 0.408 over 300
+# (tools/overlap_probe.py); results are bit-identical.  PCST_KNN_OVERLAP=0 turns it off.
+_OVERLAP_KNN_BUILD = os.environ.get("PCST_KNN_OVERLAP", "1") != "0"
+_KNN_BUILD_LDS_PAD = 65536
+_STEP_STREAMS: Dict[int, Tuple[torch.cuda.Stream, torch.cuda.Stream]] = {}
+
+
+def step_streams(device) -> Tuple[torch.cuda.Stream, torch.cuda.Stream]:
+    """(high-priority loop stream, default-priority side stream) of a device, created once."""
+    idx = torch.device(device).index
+    idx = torch.cuda.current_device() if idx is None else idx
+    if idx not in _STEP_STREAMS:
+        with torch.cuda.device(idx):
+            _STEP_STREAMS[idx] = (torch.cuda.Stream(priority=-1), torch.cuda.Stream(priority=0))
+    return _STEP_STREAMS[idx]
+
+
+def hierarchical_eps(hp, mlp, xc, xi, x_cat, knn_ws=None, side=None):
+    """eps for the CFG batch: mlp(xc) on the current stream, upsampled to the full clouds by
+    kNN-3 (HierarchicalProcessor.upsample_knn).  With a side stream (and a preallocated
+    workspace) the kNN build runs there, overlapping the MLP; the query waits for it."""
+    if side is None:
+        return hp.upsample_knn(mlp(xc), x_cat, xi)
+    main = torch.cuda.current_stream()
+    ready = torch.cuda.Event()
+    ready.record(main)
+    side.wait_event(ready)
+    with torch.cuda.stream(side):
+        handle = _hip.knn3_build(x_cat, xi, knn_ws)
+        built = torch.cuda.Event()
+        built.record(side)
+    nc = mlp(xc)
+    main.wait_event(built)
+    return _hip.knn3_query(nc, handle)
+
+
 class PointCloudDiffusionModel(nn.Module):
     """`PointCloudDiffusionModel` (diffusion_model.py:156-190)."""
 
@@ -329,16 +372,35 @@ class DiffusionProcess:
         t_rows = t_rows.view(len(timesteps), 2 * B).to(device)
         # the reference's t_prev lookup (first occurrence of t, diffusion_model.py:252)
         t_prevs = [timesteps[timesteps.index(t) + 1] if t > 0 else -1 for t in timesteps]
-        for i, t in enumerate(timesteps):
-            t_in = t_rows[i]
-            if use_hierarchical:
-                xc, xi = hp.downsample_copies(x, 2)
-                eps = hp.upsample_knn(npred(xc, t_in, style_in), x_cat, xi)
-            else:
-                eps = npred(x_cat, t_in, style_in)
-            t_prev = t_prevs[i]
-            x = _hip.cfg_ddim_step(x, eps[:B], eps[B:], source, guidance_scale,
-                                   self._coeffs(t, t_prev), x_cat=x_cat)
+        overlap = use_hierarchical and _OVERLAP_KNN_BUILD
+        side = ws = None
+        ctx = contextlib.nullcontext()
+        if overlap:
+            loop, side = step_streams(device)
+            caller = torch.cuda.current_stream(device)
+            loop.wait_stream(caller)
+            ctx = torch.cuda.stream(loop)
+        with ctx:
+            if overlap:
+                ws = _hip.knn_workspace(2 * B, shape[1], model.config.global_points, device=device)
+                _hip.knn_set_build_lds_pad(_KNN_BUILD_LDS_PAD)
+            try:
+                for i, t in enumerate(timesteps):
+                    t_in = t_rows[i]
+                    if use_hierarchical:
+                        xc, xi = hp.downsample_copies(x, 2)
+                        eps = hierarchical_eps(hp, lambda c: npred(c, t_in, style_in), xc, xi,
+                                               x_cat, ws, side)
+                    else:
+                        eps = npred(x_cat, t_in, style_in)
+                    t_prev = t_prevs[i]
+                    x = _hip.cfg_ddim_step(x, eps[:B], eps[B:], source, guidance_scale,
+                                           self._coeffs(t, t_prev), x_cat=x_cat)
+            finally:
+                if overlap:
+                    _hip.knn_set_build_lds_pad(0)
+        if overlap:
+            caller.wait_stream(loop)
         return x
 
     def _guided_sample_graph(self, model, source_points, condition_points, num_inference_steps,
