@@ -327,7 +327,7 @@ def main():
 
         # the product loop's stream layout (DiffusionProcess.guided_sample_loop): the step on a
         # high-priority stream, the kNN build on a side stream during the noise MLP
-        overlap = dmod._OVERLAP_KNN_BUILD
+        overlap = dmod.overlap_knn_build(2 * C * cfg.global_points)
         loop_stream, side = dmod.step_streams(device) if overlap else (None, None)
         if overlap:
             loop_stream.wait_stream(torch.cuda.current_stream())

@@ -219,9 +219,18 @@ class HierarchicalProcessor:
 # (pcst_knn_set_build_lds_pad), so they cannot co-reside with an MLP workgroup and only take
 # the CUs the MLP leaves idle in its last partial round (469 workgroups on 256 CUs).  Measured
 # 0.493 -> 0.468 ms/step over the first 20 steps, 0.421 -> 0.408 over 300
-# (tools/overlap_probe.py); results are bit-identical.  PCST_KNN_OVERLAP=0 turns it off.
+# (tools/overlap_probe.py, one cloud); results are bit-identical.  PCST_KNN_OVERLAP=0 turns it
+# off.
+# Only small batches leave idle CUs in the MLP's last round: with many rounds (e.g. 32 clouds per
+# GPU, 15000 MLP work-groups) the padded build only runs after the MLP, slower than inline
+# (9.6 -> 10.4 ms per 32-cloud step), so the overlap applies up to two MLP rounds of points.
 _OVERLAP_KNN_BUILD = os.environ.get("PCST_KNN_OVERLAP", "1") != "0"
+_OVERLAP_MAX_MLP_POINTS = 2 * 128 * 256
 _KNN_BUILD_LDS_PAD = 65536
+
+
+def overlap_knn_build(mlp_points: int) -> bool:
+    return _OVERLAP_KNN_BUILD and mlp_points <= _OVERLAP_MAX_MLP_POINTS
 _STEP_STREAMS: Dict[int, Tuple[torch.cuda.Stream, torch.cuda.Stream]] = {}
 
 
@@ -372,7 +381,7 @@ class DiffusionProcess:
         t_rows = t_rows.view(len(timesteps), 2 * B).to(device)
         # the reference's t_prev lookup (first occurrence of t, diffusion_model.py:252)
         t_prevs = [timesteps[timesteps.index(t) + 1] if t > 0 else -1 for t in timesteps]
-        overlap = use_hierarchical and _OVERLAP_KNN_BUILD
+        overlap = use_hierarchical and overlap_knn_build(2 * B * model.config.global_points)
         side = ws = None
         ctx = contextlib.nullcontext()
         if overlap:
