@@ -33,7 +33,8 @@ constexpr int kCondSlots = 4;
 
 // Perf-experiment knobs, compiled only by tools/nm_variants.sh; the product build uses the
 // defaults.  PCST_NM_EXPERIMENT bits: 1 = no weight DMA after the first two parts,
-// 2 = no barrier between parts (both give wrong results; they time the overheads),
+// 2 = no barrier between parts (both give wrong results; they time the overheads;
+// tools/nm_quad.hip defines more for its experiment kernel),
 // 8 = compiler-scheduled LDS fragment reads instead of the asm reads.
 #ifndef PCST_NM_EXPERIMENT
 #define PCST_NM_EXPERIMENT 0
