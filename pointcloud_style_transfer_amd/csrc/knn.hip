@@ -57,7 +57,8 @@ constexpr int kPreKnownBlocks = 64;      // known-row scatter blocks per cloud i
 constexpr int kCountPerBlock = 1024;     // elements per count-kernel block (4 per thread)
 constexpr int kQueryBlocks = 1024;       // query workgroups per cloud (grid-stride over chunks)
 constexpr int kOutlierThreads = 1024;    // outlier-pass workgroup
-constexpr int kOutlierBlocks = 128;      // outlier workgroups per cloud
+constexpr int kOutlierBlocks = 128;      // outlier workgroups per cloud (exhaustive pass)
+constexpr int kOutlierBrickBlocks = 256; // outlier workgroups per cloud (brick search, 4 queries)
 
 #ifdef KNN_TRACE  // experiment builds only: per-chunk pass timings (tools/knn_trace.py)
 __device__ unsigned long long g_knn_trace[2 * 32768 * 8];
@@ -568,28 +569,12 @@ struct Box {
 // offsets) and every lane screens every staged ref.
 // Returns false (abandoned: the open lanes then go to the outlier pass, never to another
 // pass) once more than `budget` refs would be staged; otherwise charges them to `budget`.
-__device__ __forceinline__ bool scan_box(const Box& bx, const Box& prev, const Grid& g,
-                                         const uint64_t* __restrict__ S,
-                                         const float4* __restrict__ R, const Win& W, Query& me,
-                                         int kk, uint32_t& budget) {
+// The staging loop over `vol` units; unit(li, lo, hi) gives the packed start words bounding
+// unit li's contiguous ref range (lo == hi: nothing to scan).
+template <class Unit>
+__device__ __forceinline__ bool scan_units(int vol, const Unit& unit, const float4* __restrict__ R,
+                                           const Win& W, Query& me, int kk, uint32_t& budget) {
   const int lane = threadIdx.x & 63;
-  const int nx = bx.x1 - bx.x0 + 1, ny = bx.y1 - bx.y0 + 1;
-  const int vol = bx.volume();
-  const float rnx = 1.0f / nx, rnxy = 1.0f / (nx * ny);  // exact quotients for li < 2^20
-  // packed start words of cell li and of its successor (empty if outside bx or inside prev)
-  auto unit = [&](int li, uint64_t& lo, uint64_t& hi) {
-    lo = hi = 0;
-    if (li < vol) {
-      const int qz = (int)(((float)li + 0.5f) * rnxy), rz = li - qz * nx * ny;
-      const int qy = (int)(((float)rz + 0.5f) * rnx), qx = rz - qy * nx;
-      const int x = bx.x0 + qx, y = bx.y0 + qy, z = bx.z0 + qz;
-      if (!prev.has(x, y, z)) {
-        const int u0 = cell_id(x, y, z, g);
-        lo = S[u0];
-        hi = S[u0 + 1];
-      }
-    }
-  };
   uint64_t nlo, nhi;
   unit(lane, nlo, nhi);
   int fill = 0;
@@ -640,6 +625,30 @@ __device__ __forceinline__ bool scan_box(const Box& bx, const Box& prev, const G
   lds_order();
   budget -= staged;
   return true;
+}
+
+__device__ __forceinline__ bool scan_box(const Box& bx, const Box& prev, const Grid& g,
+                                         const uint64_t* __restrict__ S,
+                                         const float4* __restrict__ R, const Win& W, Query& me,
+                                         int kk, uint32_t& budget) {
+  const int nx = bx.x1 - bx.x0 + 1, ny = bx.y1 - bx.y0 + 1;
+  const int vol = bx.volume();
+  const float rnx = 1.0f / nx, rnxy = 1.0f / (nx * ny);  // exact quotients for li < 2^20
+  // packed start words of cell li and of its successor (empty if outside bx or inside prev)
+  auto unit = [&](int li, uint64_t& lo, uint64_t& hi) {
+    lo = hi = 0;
+    if (li < vol) {
+      const int qz = (int)(((float)li + 0.5f) * rnxy), rz = li - qz * nx * ny;
+      const int qy = (int)(((float)rz + 0.5f) * rnx), qx = rz - qy * nx;
+      const int x = bx.x0 + qx, y = bx.y0 + qy, z = bx.z0 + qz;
+      if (!prev.has(x, y, z)) {
+        const int u0 = cell_id(x, y, z, g);
+        lo = S[u0];
+        hi = S[u0 + 1];
+      }
+    }
+  };
+  return scan_units(vol, unit, R, W, me, kk, budget);
 }
 
 // Distance from q to the region outside the box of cells [x0,x1]x[y0,y1]x[z0,z1] (faces on
@@ -993,6 +1002,106 @@ __global__ __launch_bounds__(kOutlierThreads) void knn_outlier_kernel(
   }
 }
 
+// Brick-shell search of the outlier queries: one wave per query.  Bricks (4x4x4 cells) are the
+// grid's coarse level for free: a brick's refs are one contiguous range of the cell-sorted refs,
+// [start(64 id), start(64 id + 64)).  The wave scans the box of bricks within Chebyshev brick
+// distance R of the query's brick, R = 1, 2, ..., each step only the new shell, skipping every
+// brick whose box lies farther than the current 3rd-best distance; it stops once that distance
+// is below the distance to everything outside the scanned box (outside_bound, the query pass's
+// settled test) or the box covers the grid.  Refs are staged and screened exactly as in the
+// query pass (scan_units), so the float64 top-3 is the exhaustive one: every ref not scanned is
+// provably farther than the 3rd best (brick lower bounds carry the same cell-rounding slack).
+// After every shell the lanes' lists are merged into lane 0 (the others restart empty with the
+// merged screen): no ref is offered twice.
+template <int kk>
+__global__ __launch_bounds__(256) void knn_outlier_brick_kernel(
+    const float* __restrict__ vals, int64_t N, int64_t M, const float* __restrict__ orig,
+    const float* __restrict__ gp, int64_t Cpad, const uint64_t* __restrict__ start,
+    const float4* __restrict__ refs, const int32_t* __restrict__ olist,
+    const int32_t* __restrict__ ocount, const uint32_t* __restrict__ known,
+    float* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) float cand[4][4][kCandCap];
+  const int b = blockIdx.y;
+  // rows that are coarse points take the coarse value (result[idx] = coarse; the last coarse
+  // row writing a point wins, as in the reference's index assignment)
+  for (int64_t n = (int64_t)blockIdx.x * 256 + threadIdx.x; n < N; n += (int64_t)gridDim.x * 256) {
+    const uint32_t kn = known[b * N + n];
+    if (kn) {
+      const float* v = vals + (b * M + (int64_t)(kn - 1)) * 3;
+      float* o = out + (b * N + n) * 3;
+      o[0] = v[0]; o[1] = v[1]; o[2] = v[2];
+    }
+  }
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  Grid g;
+  g.load(gp + b * 8);
+  const int nbx = g.bx, nby = g.by, nbz = (g.d[2] + 3) >> 2;
+  const uint64_t* S = start + b * Cpad;
+  const float4* R = refs + b * M;
+  const float* V = vals + b * M * 3;
+  const Win W = {cand[wv][0], cand[wv][1], cand[wv][2], reinterpret_cast<int*>(cand[wv][3])};
+  const int cnt = ocount[b];
+  const double bs = 4.0 * (double)g.s;  // brick edge
+  for (int q = blockIdx.x * 4 + wv; q < cnt; q += gridDim.x * 4) {
+    const int64_t n = olist[b * N + q];
+    const float* qp = orig + (b * N + n) * 3;
+    Query me;
+    me.init(qp[0], qp[1], qp[2]);
+    const int qbx = cell_coord(me.fx, g.o[0], g.inv, g.d[0]) >> 2;
+    const int qby = cell_coord(me.fy, g.o[1], g.inv, g.d[1]) >> 2;
+    const int qbz = cell_coord(me.fz, g.o[2], g.inv, g.d[2]) >> 2;
+    Box prev = {1, 0, 1, 0, 1, 0};
+    double best = INFINITY;  // merged kk-th best (exact), the pruning radius^2
+    for (int r = 1;; ++r) {
+      const Box bx = {max(qbx - r, 0), min(qbx + r, nbx - 1), max(qby - r, 0), min(qby + r, nby - 1),
+                      max(qbz - r, 0), min(qbz + r, nbz - 1)};
+      const int nx = bx.x1 - bx.x0 + 1, ny = bx.y1 - bx.y0 + 1;
+      const int vol = bx.volume();
+      const float rnx = 1.0f / nx, rnxy = 1.0f / (nx * ny);
+      const double lim = best;
+      auto unit = [&](int li, uint64_t& lo, uint64_t& hi) {
+        lo = hi = 0;
+        if (li < vol) {
+          const int qz = (int)(((float)li + 0.5f) * rnxy), rz = li - qz * nx * ny;
+          const int qy = (int)(((float)rz + 0.5f) * rnx), qx = rz - qy * nx;
+          const int x = bx.x0 + qx, y = bx.y0 + qy, z = bx.z0 + qz;
+          if (prev.has(x, y, z)) return;
+          // squared distance from the query to the brick's box, less the cell-rounding slack
+          const double x0 = g.o[0] + x * bs, y0 = g.o[1] + y * bs, z0 = g.o[2] + z * bs;
+          const double ex = fmax(fmax(x0 - me.qx, me.qx - (x0 + bs)), 0.0);
+          const double ey = fmax(fmax(y0 - me.qy, me.qy - (y0 + bs)), 0.0);
+          const double ez = fmax(fmax(z0 - me.qz, me.qz - (z0 + bs)), 0.0);
+          const double e = fmax(sqrt(ex * ex + ey * ey + ez * ez) - 1e-5 * g.s, 0.0);
+          if (e * e > lim) return;
+          const int u0 = ((z * nby + y) * nbx + x) << 6;
+          lo = S[u0];
+          hi = S[u0 + 64];
+        }
+      };
+      uint32_t unlimited = 0xffffffffu;
+      scan_units(vol, unit, R, W, me, kk, unlimited);
+      // merge the lanes' lists into lane 0; the others restart empty with the merged screen
+      Top3 t = me.t;
+      wave_merge_top3(t);
+      best = t.last(kk);
+      if (lane == 0) me.t = t;
+      else me.t.init();
+      if (best != INFINITY) me.thr = fminf(me.thr, (float)(best * (1.0 + 2e-6)) + 1e-30f);
+      if (bx.x0 == 0 && bx.y0 == 0 && bx.z0 == 0 && bx.x1 == nbx - 1 && bx.y1 == nby - 1 &&
+          bx.z1 == nbz - 1)
+        break;
+      const Box cells = {bx.x0 * 4, min(bx.x1 * 4 + 3, g.d[0] - 1), bx.y0 * 4,
+                         min(bx.y1 * 4 + 3, g.d[1] - 1), bx.z0 * 4, min(bx.z1 * 4 + 3, g.d[2] - 1)};
+      if (best != INFINITY) {  // wave-uniform: the merged list, the query's own box
+        const double ob = outside_bound(me, cells, g);
+        if (ob == INFINITY || (ob > 0 && best < ob * ob)) break;
+      }
+      prev = bx;
+    }
+    if (lane == 0) idw_write(me.t, kk, V, out + (b * N + n) * 3);
+  }
+}
+
 }  // namespace pcst
 
 using namespace pcst;
@@ -1046,6 +1155,14 @@ extern "C" int pcst_knn3_build(const float* orig, const int64_t* idx, int64_t B,
   return PCST_OK;
 }
 
+static int outlier_mode() {
+  static const int m = [] {
+    const char* e = getenv("PCST_KNN_OUTLIER");
+    return e ? atoi(e) : 0;
+  }();
+  return m;
+}
+
 extern "C" int pcst_knn3_query(const float* coarse, const float* orig, int64_t B, int64_t N,
                                int64_t M, float* out, void* workspace, void* stream) {
   PCST_CHECK_ARG(B >= 0 && N > 0 && M > 0 && N < (1ll << 31) && M < (1ll << 27) &&
@@ -1061,10 +1178,17 @@ extern "C" int pcst_knn3_query(const float* coarse, const float* orig, int64_t B
   auto qk = M >= 3 ? knn_query_kernel<3> : (M == 2 ? knn_query_kernel<2> : knn_query_kernel<1>);
   hipLaunchKernelGGL(qk, dim3(gq, b), dim3(256), 0, s, orig, coarse, N, M, w.Cpad, w.gp, w.cnt,
                      w.refs, w.qorder, w.chunks, w.maxch, w.nchunk, w.olist, w.ocount, out);
-  auto ok = M >= 3 ? knn_outlier_kernel<3>
-                   : (M == 2 ? knn_outlier_kernel<2> : knn_outlier_kernel<1>);
-  hipLaunchKernelGGL(ok, dim3(kOutlierBlocks, b), dim3(kOutlierThreads), 0, s, coarse, N, M, orig,
-                     w.refs, w.olist, w.ocount, w.known, out);
+  if (outlier_mode() == 0) {  // PCST_KNN_OUTLIER=0: the exhaustive pass (A/B experiments)
+    auto ok = M >= 3 ? knn_outlier_kernel<3>
+                     : (M == 2 ? knn_outlier_kernel<2> : knn_outlier_kernel<1>);
+    hipLaunchKernelGGL(ok, dim3(kOutlierBlocks, b), dim3(kOutlierThreads), 0, s, coarse, N, M, orig,
+                       w.refs, w.olist, w.ocount, w.known, out);
+  } else {
+    auto ok = M >= 3 ? knn_outlier_brick_kernel<3>
+                     : (M == 2 ? knn_outlier_brick_kernel<2> : knn_outlier_brick_kernel<1>);
+    hipLaunchKernelGGL(ok, dim3(kOutlierBrickBlocks, b), dim3(256), 0, s, coarse, N, M, orig, w.gp,
+                       w.Cpad, w.cnt, w.refs, w.olist, w.ocount, w.known, out);
+  }
   PCST_LAUNCH_CHECK("knn3_query");
   return PCST_OK;
 }

@@ -100,8 +100,13 @@ class NoisePredictor(nn.Module):
 
     @property
     def precision_code(self) -> int:
+        """ABI precision code: "bf16" runs the 16x16x32 pair kernel (PAIR16), "fp32" the
+        exact-f32 parity kernel.  PCST_NM_BF16_KERNEL=1 selects the 32x32x16 pair kernel
+        (same arithmetic, other MFMA shape; A/B timing)."""
         p = getattr(self.config, "precision", "fp32")
-        return packing.BF16 if p == "bf16" else packing.F32
+        if p != "bf16":
+            return packing.F32
+        return packing.BF16 if os.environ.get("PCST_NM_BF16_KERNEL") == "1" else packing.PAIR16
 
     def packed(self):
         """Packed MFMA weight stream + bias table, rebuilt when any weight changes."""

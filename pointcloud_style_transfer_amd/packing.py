@@ -29,6 +29,18 @@ fragments of BOTH wave roles, role 0 in its first half and role 1 in its second:
       W2 part = [for blocks 0-3: k-steps (2it, 2it+1, 2(8+it), 2(8+it)+1) |
                  the same for blocks 4-7];
   output_mlp.4 (one block): one part, read by both roles.
+
+bf16 16x16x32 order (noise_mlp_pair16_kernel, precision code PAIR16 = 2): the pair layout with
+16-row fragments.  Fragment (rb, s) = 1 KiB:
+     lane l = (r = l & 15, g = l >> 4), element j  ->  W[16 rb + r, k]
+     k = 32 s + 16 (j >> 2) + 4 g + (j & 3)
+(the operand of k-step s is the accumulators of row blocks 2s, 2s+1: C/D row = 4 g + i).
+Parts hold the same weights as the 32x32x16 pair layout, re-cut into 16-row blocks:
+  dense layer: part q = [role 0: row blocks q*k .. q*k+k-1 (each all k-steps) | role 1: ...],
+      k = 16 / NKS own row blocks per role and part;
+  residual W1 part = [row blocks 2it, 2it+1 | row blocks 2(8+it), 2(8+it)+1], all k-steps;
+  residual W2 part = [for row blocks 0-7: k-steps (it, 8+it) | the same for row blocks 8-15];
+  output_mlp.4: one part, row block 0 (rows 3..15 zero), 4 k-steps.
 """
 from __future__ import annotations
 
@@ -36,7 +48,7 @@ import numpy as np
 import torch
 
 PART = 32768
-BF16, F32 = 1, 0
+BF16, F32, PAIR16 = 1, 0, 2
 
 # bias table offsets (floats) -- must match csrc/noise_mlp.hip
 OFF_W0, OFF_B0, OFF_B2, OFF_B1, OFF_BB2, OFF_O0, OFF_O2, OFF_O4, BIAS_FLOATS = (
@@ -94,6 +106,8 @@ def pack_blob(sd, precision, pre="noise_predictor"):
     g = lambda n: np.asarray(sd[f"{pre}.{n}"], np.float32)  # noqa: E731
     if precision == BF16:
         return _pack_pair(g)
+    if precision == PAIR16:
+        return _pack_pair16(g)
     parts = []
 
     def layer(W):
@@ -144,6 +158,58 @@ def _pack_pair(g):
     dense(g("output_mlp.0.weight"))
     dense(g("output_mlp.2.weight"))
     emit([_frags(g("output_mlp.4.weight"), BF16)])
+    return np.concatenate(parts)
+
+
+def _kmap16(nsteps):
+    """k index [s, lane, j] of the 16x16x32 fragments / operands for K = 32*nsteps."""
+    g = (np.arange(64) >> 4)[None, :, None]
+    s = np.arange(nsteps)[:, None, None]
+    j = np.arange(8)[None, None, :]
+    return 32 * s + 16 * (j >> 2) + 4 * g + (j & 3)
+
+
+def _frags16(W):
+    """W [O, K] float32 -> [ceil(O/16), K/32, 512] fragments of v_mfma_f32_16x16x32_bf16."""
+    O, K = W.shape
+    km = _kmap16(K // 32)
+    r = np.arange(64) & 15
+    nrb = (O + 15) // 16
+    Wp = np.zeros((nrb * 16, K), np.float32)
+    Wp[:O] = W
+    return np.stack([Wp[(rb * 16 + r)[None, :, None], km].reshape(K // 32, -1) for rb in range(nrb)])
+
+
+def _pack_pair16(g):
+    """bf16 16x16x32 pair layout of noise_mlp_pair16_kernel (module docstring)."""
+    parts = []
+    fpp = PART // 1024
+
+    def emit(frags):
+        b = _to_bytes(np.concatenate([f.reshape(-1) for f in frags]), BF16)
+        assert len(b) <= PART
+        parts.append(_pad_part(b))
+
+    def dense(W):
+        F = _frags16(W)                      # [NRB, NKS, 512]
+        nrb, nks = F.shape[:2]
+        k = fpp // nks // 2                  # own row blocks per role and part
+        half = nrb // 2
+        for q in range(half // k):
+            emit([F[q * k:(q + 1) * k], F[half + q * k:half + (q + 1) * k]])
+
+    dense(g("point_encoder.2.weight"))
+    dense(g("point_encoder.4.weight"))
+    for i in range(6):
+        F1 = _frags16(g(f"layers.{i}.0.weight"))  # [32 row blocks, 8, 512]
+        F2 = _frags16(g(f"layers.{i}.2.weight"))  # [16 row blocks, 16, 512]
+        for it in range(8):
+            emit([F1[2 * it:2 * it + 2], F1[2 * (8 + it):2 * (8 + it) + 2]])
+            steps = [it, 8 + it]
+            emit([F2[0:8][:, steps], F2[8:16][:, steps]])
+    dense(g("output_mlp.0.weight"))
+    dense(g("output_mlp.2.weight"))
+    emit([_frags16(g("output_mlp.4.weight"))])
     return np.concatenate(parts)
 
 

@@ -291,17 +291,18 @@ def test_noise_mlp_bf16_per_element_60000(det_state):
     cond = _hip.noise_cond(t, style, *cp)
     bias = torch.from_numpy(packing.pack_bias(det_state)).cuda()
     outs = []
-    for prec in (0, 1):
+    for prec in (0, 1, 2):   # f32, bf16 on 32x32x16, bf16 on 16x16x32
         blob = torch.from_numpy(packing.pack_blob(det_state, prec)).cuda()
         outs.append(_hip.noise_mlp(pts, 30000, cond, blob, bias, prec).cpu().numpy())
-    f32, bf = outs
+    f32 = outs[0]
     scale = np.abs(f32).max()
-    d = np.abs(bf - f32)
-    ok = d <= 0.05 * (np.abs(f32) + 0.1 * scale)
-    print(f"bf16 vs f32 at 60000 pts: frac ok {ok.mean():.6f}, max {d.max() / scale:.3e} of "
-          f"max|f32|, median rel {np.median(d / (np.abs(f32) + 1e-30)):.3e}")
-    assert ok.mean() >= 0.999
-    assert d.max() <= 0.25 * scale
+    for prec, bf in ((1, outs[1]), (2, outs[2])):
+        d = np.abs(bf - f32)
+        ok = d <= 0.05 * (np.abs(f32) + 0.1 * scale)
+        print(f"bf16 (code {prec}) vs f32 at 60000 pts: frac ok {ok.mean():.6f}, max "
+              f"{d.max() / scale:.3e} of max|f32|, median rel {np.median(d / (np.abs(f32) + 1e-30)):.3e}")
+        assert ok.mean() >= 0.999
+        assert d.max() <= 0.25 * scale
 
 
 def test_chamfer_vs_oracle_10_steps_120k(det_state):

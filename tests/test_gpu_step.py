@@ -152,6 +152,21 @@ def test_knn_vs_oracle(H, N, M, B, sig):
     np.testing.assert_array_equal(out, O.upsample_knn(coarse, orig, idx))
 
 
+def test_knn_outlier_pass_gaussian_vs_oracle(H):
+    """A noisy-step cloud (isotropic Gaussian, the sampler's x at t = 999; 60000 rows, 15000
+    coarse): its tail queries leave the query pass (sparse shells) and are answered by the
+    brick-shell outlier search -- bit-exact vs the oracle's brute-force float64 3-NN."""
+    rng = np.random.default_rng(999)
+    N, M, B = 60000, 15000, 2
+    orig = rng.standard_normal((B, N, 3)).astype(np.float32)
+    idx = np.stack([rng.choice(N, M, replace=False) for _ in range(B)]).astype(np.int64)
+    coarse = rng.standard_normal((B, M, 3)).astype(np.float32)
+    st = []
+    out = H.knn3_interp(dev(coarse), dev(orig), dev(idx), check=True, stats=st).cpu().numpy()
+    assert min(st[0]["outliers"]) > 20, st
+    np.testing.assert_array_equal(out, O.upsample_knn(coarse, orig, idx))
+
+
 def _clustered(rng, N):
     """tight clusters, a uniform halo and far outliers (sparse shells, exhaustive fallback)"""
     centers = rng.uniform(-2, 2, (12, 3))
@@ -201,7 +216,7 @@ def _noise_params(det_state, H, precision):
                         g("style_proj.bias"), g("point_encoder.4.bias"))
 
 
-@pytest.mark.parametrize("precision", [0, 1])
+@pytest.mark.parametrize("precision", [0, 1, 2])
 def test_noise_mlp_golden(H, golden, det_state, precision):
     g = golden("noise_predictor.npz")
     blob, bias, cp = _noise_params(det_state, H, precision)

@@ -341,3 +341,75 @@ def test_bf16_pair_packing_follows_the_kernel_read_schedule():
         np.testing.assert_array_equal(seen[:O], ref, err_msg=name)
         if O < 32:
             assert (seen[O:] == 0).all(), name
+
+
+def test_bf16_pair16_packing_follows_the_kernel_read_schedule():
+    """packing.pack_blob(PAIR16), the 16x16x32 layout of noise_mlp_pair16_kernel: replaying
+    that kernel's read schedule (csrc/noise_mlp.hip pair16_wave / dense16 / run16: part order,
+    role halves at fragment 16, fragment i = (row block i // NKS, k-step i % NKS)) over the blob
+    recovers every weight of every layer exactly (as bf16)."""
+    import torch
+
+    from pointcloud_style_transfer_amd import packing
+    from pointcloud_style_transfer_amd.model_spec import state_dict_shapes
+    from detweights import deterministic_state
+
+    sd = deterministic_state(state_dict_shapes())
+    pre = "noise_predictor"
+    blob = packing.pack_blob(sd, packing.PAIR16)
+    vals = torch.from_numpy(blob.copy()).view(torch.bfloat16).float().numpy()
+    parts = vals.reshape(-1, packing.PART // 2)
+    km = packing._kmap16(16)                    # [S, 64, 8]
+    r = np.arange(64) & 15
+    q = [0]
+    got = {}
+
+    def put(name, rb, step, f):
+        W = got.setdefault(name, {})
+        fr = parts[q[0], f * 512:(f + 1) * 512].reshape(64, 8)
+        for lane in range(64):
+            for j in range(8):
+                W[(rb * 16 + r[lane], int(km[step, lane, j]))] = fr[lane, j]
+
+    def dense(name, nown, nks):
+        ownpp = 32 // nks // 2
+        done = 0
+        while done < nown:
+            now = min(nown - done, ownpp)
+            for role in (0, 1):
+                for i in range(now * nks):
+                    put(name, role * nown + done + i // nks, i % nks, role * ownpp * nks + i)
+            done += now
+            if done < nown:
+                q[0] += 1
+
+    dense("point_encoder.2", 8, 4)
+    q[0] += 1
+    dense("point_encoder.4", 8, 8)
+    for layer in range(6):
+        for it in range(8):
+            q[0] += 1
+            for role in (0, 1):
+                for i in range(16):
+                    put(f"layers.{layer}.0", 2 * (it + 8 * role) + i // 8, i % 8, role * 16 + i)
+            q[0] += 1
+            for role in (0, 1):
+                for i in range(16):
+                    put(f"layers.{layer}.2", 8 * role + i // 2, (it, 8 + it)[i % 2], role * 16 + i)
+    q[0] += 1
+    dense("output_mlp.0", 8, 8)
+    q[0] += 1
+    dense("output_mlp.2", 4, 8)
+    q[0] += 1
+    for i in range(4):
+        put("output_mlp.4", 0, i, i)
+    assert q[0] + 1 == parts.shape[0]
+    for name, W in got.items():
+        ref = torch.from_numpy(sd[f"{pre}.{name}.weight"]).bfloat16().float().numpy()
+        O, K = ref.shape
+        seen = np.full((max(O, 16), K), np.nan, np.float32)
+        for (o, k), v in W.items():
+            seen[o, k] = v
+        np.testing.assert_array_equal(seen[:O], ref, err_msg=name)
+        if O < 16:
+            assert (seen[O:] == 0).all(), name
