@@ -62,6 +62,8 @@ constexpr int kOutlierBrickBlocks = 256; // outlier workgroups per cloud (brick 
 
 #ifdef KNN_TRACE  // experiment builds only: per-chunk pass timings (tools/knn_trace.py)
 __device__ unsigned long long g_knn_trace[2 * 32768 * 8];
+// per outlier query of the brick search: realtime start/end, shells, refs staged, bricks
+__device__ unsigned long long g_knn_otrace[2 * 4096 * 4];
 #endif
 
 struct KnnWS {
@@ -72,6 +74,7 @@ struct KnnWS {
   int2* crank;       // [B][M+N] (cell, rank in cell); cell -1 for known rows
   uint2* chunks;     // [B][maxch] query ranges [q0, q1) of <= 64 queries inside one brick
   int32_t* olist;    // [B][N]   outlier query rows
+  float* obound;     // [B][N]   their kk-th best squared distance so far (rounded up; inf: none)
   // zeroed every call (contiguous):
   int32_t* err;
   int32_t* nchunk;   // [B]
@@ -101,6 +104,7 @@ static KnnWS carve_knn(void* base, int64_t B, int64_t N, int64_t M) {
   w.crank = c.take<int2>(B * (M + N));
   w.chunks = c.take<uint2>(B * w.maxch);
   w.olist = c.take<int32_t>(B * N);
+  w.obound = c.take<float>(B * N);
   w.err = c.take<int32_t>(4);
   w.nchunk = c.take<int32_t>(B);
   w.ocount = c.take<int32_t>(B);
@@ -627,6 +631,49 @@ __device__ __forceinline__ bool scan_units(int vol, const Unit& unit, const floa
   return true;
 }
 
+// One query per wave: the units' refs are split over the lanes (slot v of the round's
+// concatenated ranges goes to lane v % 64, found by the same binary search over the lanes'
+// offsets), loaded straight into registers four slots at a time and offered to the lane's own
+// top-3 (Query::consider: fp32 screen against the lane's exact 3rd best, then float64).
+template <class Unit>
+__device__ __forceinline__ void scan_units_1q(int vol, const Unit& unit, const float4* __restrict__ R,
+                                              Query& me, int kk, uint32_t& staged) {
+  const int lane = threadIdx.x & 63;
+  uint64_t nlo, nhi;
+  unit(lane, nlo, nhi);
+  for (int c0 = 0; c0 < vol; c0 += 64) {
+    const uint32_t a = (uint32_t)nlo, cnt = (uint32_t)nhi - a;
+    if (c0 + 64 < vol) unit(c0 + 64 + lane, nlo, nhi);
+    uint32_t off = cnt;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = __shfl_up(off, o);
+      if (lane >= o) off += y;
+    }
+    const uint32_t tot = __shfl(off, 63);
+    off -= cnt;
+    staged += tot;
+    for (uint32_t t0 = 0; t0 < tot; t0 += 256) {
+      float4 r[4];
+      bool ok[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const uint32_t v = t0 + 64 * k + lane;
+        int l = 0;  // last lane whose offset <= v
+#pragma unroll
+        for (int st = 32; st >= 1; st >>= 1)
+          if (__shfl(off, l + st) <= v) l += st;
+        const uint32_t src = __shfl(a, l) + (v - __shfl(off, l));
+        ok[k] = v < tot;
+        if (ok[k]) r[k] = R[src];
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        if (ok[k]) me.consider(r[k], kk);
+    }
+  }
+}
+
 __device__ __forceinline__ bool scan_box(const Box& bx, const Box& prev, const Grid& g,
                                          const uint64_t* __restrict__ S,
                                          const float4* __restrict__ R, const Win& W, Query& me,
@@ -678,7 +725,8 @@ __global__ __launch_bounds__(256) void knn_query_kernel(
     int64_t Cpad, const float* __restrict__ gp, const uint64_t* __restrict__ start,
     const float4* __restrict__ refs, const int32_t* __restrict__ qorder,
     const uint2* __restrict__ chunks, int64_t maxch, const int32_t* __restrict__ nchunk,
-    int32_t* __restrict__ olist, int32_t* __restrict__ ocount, float* __restrict__ out) {
+    int32_t* __restrict__ olist, float* __restrict__ obound, int32_t* __restrict__ ocount,
+    float* __restrict__ out) {
   __shared__ __attribute__((aligned(16))) float cand[4][4][kCandCap];
   const int b = blockIdx.y;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -769,7 +817,12 @@ __global__ __launch_bounds__(256) void knn_query_kernel(
       int at = 0;
       if (lane == 0) at = atomicAdd(&ocount[b], (int)__popcll(rest));
       at = __shfl(at, 0);
-      if (open) olist[b * N + at + (int)__popcll(rest & lanemask_lt())] = (int32_t)n;
+      if (open) {
+        const int64_t o = b * N + at + (int)__popcll(rest & lanemask_lt());
+        olist[o] = (int32_t)n;
+        const double dk = me.t.last(kk);  // exact, from refs already seen: >= the true kk-th
+        obound[o] = dk == INFINITY ? INFINITY : (float)(dk * (1.0 + 1e-6)) * 1.000001f;
+      }
     }
     if (valid && !open) idw_write(me.t, kk, V, out + (b * N + n) * 3);
 #ifdef KNN_TRACE
@@ -1005,22 +1058,22 @@ __global__ __launch_bounds__(kOutlierThreads) void knn_outlier_kernel(
 // Brick-shell search of the outlier queries: one wave per query.  Bricks (4x4x4 cells) are the
 // grid's coarse level for free: a brick's refs are one contiguous range of the cell-sorted refs,
 // [start(64 id), start(64 id + 64)).  The wave scans the box of bricks within Chebyshev brick
-// distance R of the query's brick, R = 1, 2, ..., each step only the new shell, skipping every
-// brick whose box lies farther than the current 3rd-best distance; it stops once that distance
-// is below the distance to everything outside the scanned box (outside_bound, the query pass's
-// settled test) or the box covers the grid.  Refs are staged and screened exactly as in the
-// query pass (scan_units), so the float64 top-3 is the exhaustive one: every ref not scanned is
-// provably farther than the 3rd best (brick lower bounds carry the same cell-rounding slack).
-// After every shell the lanes' lists are merged into lane 0 (the others restart empty with the
-// merged screen): no ref is offered twice.
+// distance R of the query's brick, each step only the new shell, skipping every brick whose box
+// lies farther than the current 3rd-best distance; it stops once that distance is below the
+// distance to everything outside the scanned box (outside_bound, the query pass's settled test)
+// or the box covers the grid.  R grows by one until kk refs are known, then jumps to the radius
+// whose box faces lie beyond the kk-th distance (normally the last shell).  The float64 top-3 is
+// the exhaustive one: every ref not scanned is provably farther than the 3rd best (brick lower
+// bounds carry the same cell-rounding slack).  A shell's refs are split over the lanes
+// (scan_units_1q); after every shell the lanes' lists are merged into lane 0 (the others restart
+// empty with the merged screen), so no ref is offered twice.
 template <int kk>
 __global__ __launch_bounds__(256) void knn_outlier_brick_kernel(
     const float* __restrict__ vals, int64_t N, int64_t M, const float* __restrict__ orig,
     const float* __restrict__ gp, int64_t Cpad, const uint64_t* __restrict__ start,
     const float4* __restrict__ refs, const int32_t* __restrict__ olist,
-    const int32_t* __restrict__ ocount, const uint32_t* __restrict__ known,
-    float* __restrict__ out) {
-  __shared__ __attribute__((aligned(16))) float cand[4][4][kCandCap];
+    const float* __restrict__ obound, const int32_t* __restrict__ ocount,
+    const uint32_t* __restrict__ known, float* __restrict__ out) {
   const int b = blockIdx.y;
   // rows that are coarse points take the coarse value (result[idx] = coarse; the last coarse
   // row writing a point wins, as in the reference's index assignment)
@@ -1039,7 +1092,6 @@ __global__ __launch_bounds__(256) void knn_outlier_brick_kernel(
   const uint64_t* S = start + b * Cpad;
   const float4* R = refs + b * M;
   const float* V = vals + b * M * 3;
-  const Win W = {cand[wv][0], cand[wv][1], cand[wv][2], reinterpret_cast<int*>(cand[wv][3])};
   const int cnt = ocount[b];
   const double bs = 4.0 * (double)g.s;  // brick edge
   for (int q = blockIdx.x * 4 + wv; q < cnt; q += gridDim.x * 4) {
@@ -1051,8 +1103,17 @@ __global__ __launch_bounds__(256) void knn_outlier_brick_kernel(
     const int qby = cell_coord(me.fy, g.o[1], g.inv, g.d[1]) >> 2;
     const int qbz = cell_coord(me.fz, g.o[2], g.inv, g.d[2]) >> 2;
     Box prev = {1, 0, 1, 0, 1, 0};
-    double best = INFINITY;  // merged kk-th best (exact), the pruning radius^2
-    for (int r = 1;; ++r) {
+    // the pruning radius^2: the query pass's kk-th best so far (an upper bound of the true
+    // kk-th distance: the refs behind it lie inside it and are found again), then the merged
+    // kk-th best of this search
+    double best = (double)obound[b * N + q];
+    int r = 1;
+    if (best != INFINITY) r = max(1, (int)fmin(floor(sqrt(best) * (1.0 + 1e-6) / bs) + 1.0, 4096.0));
+#ifdef KNN_TRACE
+    const unsigned long long ot0 = __builtin_amdgcn_s_memrealtime();
+    uint32_t oshells = 0, ostaged = 0, olastr = 0;
+#endif
+    for (;;) {
       const Box bx = {max(qbx - r, 0), min(qbx + r, nbx - 1), max(qby - r, 0), min(qby + r, nby - 1),
                       max(qbz - r, 0), min(qbz + r, nbz - 1)};
       const int nx = bx.x1 - bx.x0 + 1, ny = bx.y1 - bx.y0 + 1;
@@ -1078,12 +1139,15 @@ __global__ __launch_bounds__(256) void knn_outlier_brick_kernel(
           hi = S[u0 + 64];
         }
       };
-      uint32_t unlimited = 0xffffffffu;
-      scan_units(vol, unit, R, W, me, kk, unlimited);
+      uint32_t staged = 0;
+      scan_units_1q(vol, unit, R, me, kk, staged);
+#ifdef KNN_TRACE
+      ++oshells; ostaged += staged; olastr = r;
+#endif
       // merge the lanes' lists into lane 0; the others restart empty with the merged screen
       Top3 t = me.t;
       wave_merge_top3(t);
-      best = t.last(kk);
+      best = fmin(best, t.last(kk));
       if (lane == 0) me.t = t;
       else me.t.init();
       if (best != INFINITY) me.thr = fminf(me.thr, (float)(best * (1.0 + 2e-6)) + 1e-30f);
@@ -1097,8 +1161,26 @@ __global__ __launch_bounds__(256) void knn_outlier_brick_kernel(
         if (ob == INFINITY || (ob > 0 && best < ob * ob)) break;
       }
       prev = bx;
+      // next box: once kk refs are known, the one whose faces (R bricks from the query's brick)
+      // lie beyond the current kk-th distance -- the last shell unless rounding says otherwise;
+      // before that, double the radius
+      if (best != INFINITY) {
+        const double need = floor(sqrt(best) * (1.0 + 1e-6) / bs) + 1.0;
+        r = max(r + 1, (int)fmin(need, 4096.0));
+      } else {
+        r += 1;  // sparse shells are cheap; a doubled box can reach into the dense core unpruned
+      }
     }
     if (lane == 0) idw_write(me.t, kk, V, out + (b * N + n) * 3);
+#ifdef KNN_TRACE
+    if (lane == 0 && b < 2 && q < 4096) {
+      unsigned long long* tr = g_knn_otrace + ((int64_t)b * 4096 + q) * 4;
+      tr[0] = ot0;
+      tr[1] = __builtin_amdgcn_s_memrealtime();
+      tr[2] = ((unsigned long long)oshells << 32) | olastr;
+      tr[3] = ostaged;
+    }
+#endif
   }
 }
 
@@ -1158,7 +1240,7 @@ extern "C" int pcst_knn3_build(const float* orig, const int64_t* idx, int64_t B,
 static int outlier_mode() {
   static const int m = [] {
     const char* e = getenv("PCST_KNN_OUTLIER");
-    return e ? atoi(e) : 0;
+    return e ? atoi(e) : 1;
   }();
   return m;
 }
@@ -1177,7 +1259,7 @@ extern "C" int pcst_knn3_query(const float* coarse, const float* orig, int64_t B
   const unsigned gq = (unsigned)std::min<int64_t>(cdiv(w.maxch, 4), kQueryBlocks);
   auto qk = M >= 3 ? knn_query_kernel<3> : (M == 2 ? knn_query_kernel<2> : knn_query_kernel<1>);
   hipLaunchKernelGGL(qk, dim3(gq, b), dim3(256), 0, s, orig, coarse, N, M, w.Cpad, w.gp, w.cnt,
-                     w.refs, w.qorder, w.chunks, w.maxch, w.nchunk, w.olist, w.ocount, out);
+                     w.refs, w.qorder, w.chunks, w.maxch, w.nchunk, w.olist, w.obound, w.ocount, out);
   if (outlier_mode() == 0) {  // PCST_KNN_OUTLIER=0: the exhaustive pass (A/B experiments)
     auto ok = M >= 3 ? knn_outlier_kernel<3>
                      : (M == 2 ? knn_outlier_kernel<2> : knn_outlier_kernel<1>);
@@ -1187,7 +1269,7 @@ extern "C" int pcst_knn3_query(const float* coarse, const float* orig, int64_t B
     auto ok = M >= 3 ? knn_outlier_brick_kernel<3>
                      : (M == 2 ? knn_outlier_brick_kernel<2> : knn_outlier_brick_kernel<1>);
     hipLaunchKernelGGL(ok, dim3(kOutlierBrickBlocks, b), dim3(256), 0, s, coarse, N, M, orig, w.gp,
-                       w.Cpad, w.cnt, w.refs, w.olist, w.ocount, w.known, out);
+                       w.Cpad, w.cnt, w.refs, w.olist, w.obound, w.ocount, w.known, out);
   }
   PCST_LAUNCH_CHECK("knn3_query");
   return PCST_OK;
@@ -1202,6 +1284,16 @@ extern "C" int pcst_knn3_interp(const float* coarse, const float* orig, const in
 }
 
 #ifdef KNN_TRACE
+extern "C" int pcst_knn_otrace_dump(void* host, size_t bytes) {
+  void* d = nullptr;
+  PCST_HIP(hipGetSymbolAddress(&d, HIP_SYMBOL(g_knn_otrace)), "knn_otrace: symbol");
+  PCST_HIP(hipDeviceSynchronize(), "knn_otrace: sync");
+  if (host) PCST_HIP(hipMemcpy(host, d, std::min(bytes, sizeof(g_knn_otrace)), hipMemcpyDeviceToHost), "knn_otrace: copy");
+  PCST_HIP(hipMemset(d, 0, sizeof(g_knn_otrace)), "knn_otrace: reset");
+  PCST_HIP(hipDeviceSynchronize(), "knn_otrace: sync");
+  return PCST_OK;
+}
+
 extern "C" int pcst_knn_trace_dump(void* host, size_t bytes) {
   void* d = nullptr;
   PCST_HIP(hipGetSymbolAddress(&d, HIP_SYMBOL(g_knn_trace)), "knn_trace: symbol");
