@@ -96,7 +96,7 @@ static KnnWS carve_knn(void* base, int64_t B, int64_t N, int64_t M) {
   w.Cmax = knn_cells(M);
   w.T = cdiv(w.Cmax + 1, kKnnTile);
   w.Cpad = w.T * kKnnTile;
-  w.maxch = cdiv(N, 64) + w.Cmax / 64 + 1;
+  w.maxch = cdiv(N, 64) + 8 * (w.Cmax / 64) + 1;  // <= ceil(q/64) + 8 chunks per brick
   w.stats = c.take<StatRec>(B * kStatBlocks);
   w.gp = c.take<float>(B * 8);
   w.refs = c.take<float4>(B * M);
@@ -291,8 +291,8 @@ __device__ __forceinline__ uint64_t block_excl_scan_256_u64(uint64_t v, unsigned
 
 // Exclusive scan of the packed counts in place (the tile offset is the sum of the earlier
 // tiles' sums: at most kKnnMaxTiles words, read by the whole block), then the tile's 64
-// bricks are cut into chunks of <= 64 queries appended to the cloud's chunk list (order free:
-// chunks are independent).
+// bricks are cut into chunks of <= 64 queries (by octant, below) appended to the cloud's chunk
+// list (order free: chunks are independent).
 __global__ __launch_bounds__(256) void knn_scan_kernel(uint64_t* __restrict__ cnt,
                                                        const uint64_t* __restrict__ tsum,
                                                        int64_t T, int64_t Cpad,
@@ -329,10 +329,35 @@ __global__ __launch_bounds__(256) void knn_scan_kernel(uint64_t* __restrict__ cn
 #pragma unroll
   for (int k = 0; k < 16; ++k) D[k * 256 + threadIdx.x] = buf[pad(k * 256 + threadIdx.x)];
   if (threadIdx.x < 64) {
+    // brick t's queries by octant (2x2x2 cells: Morton cells [8o, 8o + 8)).  A chunk is a run of
+    // whole consecutive octants holding <= 64 queries, or a balanced part of one octant that
+    // holds more, so a dense chunk's cell box stays within 2x2x2 cells (the query pass stages
+    // the box grown by one cell: at most 4x4x4).
     const int t = threadIdx.x;
-    const uint32_t q0 = (uint32_t)(buf[pad(t * 64)] >> 32);
-    const uint32_t q1 = (uint32_t)((t < 63 ? buf[pad(t * 64 + 64)] : base + tot) >> 32);
-    const uint32_t nch = (q1 - q0 + 63) / 64;
+    uint32_t qo[9];
+#pragma unroll
+    for (int o = 0; o < 8; ++o) qo[o] = (uint32_t)(buf[pad(t * 64 + 8 * o)] >> 32);
+    qo[8] = (uint32_t)((t < 63 ? buf[pad(t * 64 + 64)] : base + tot) >> 32);
+    // walk the octants; emit(a, b) is called for every chunk [a, b) in order
+    auto walk = [&](auto&& emit) {
+      uint32_t cs = qo[0];  // start of the open run of octants
+#pragma unroll
+      for (int o = 0; o < 8; ++o) {
+        const uint32_t a = qo[o], n = qo[o + 1] - a;
+        if (n > 64) {
+          if (a > cs) emit(cs, a);
+          const uint32_t k = (n + 63) / 64;
+          for (uint32_t i = 0; i < k; ++i) emit(a + (uint32_t)((uint64_t)n * i / k), a + (uint32_t)((uint64_t)n * (i + 1) / k));
+          cs = a + n;
+        } else if (a + n - cs > 64) {
+          emit(cs, a);
+          cs = a;
+        }
+      }
+      if (qo[8] > cs) emit(cs, qo[8]);
+    };
+    uint32_t nch = 0;
+    walk([&](uint32_t, uint32_t) { ++nch; });
     uint32_t off = nch;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
@@ -345,8 +370,8 @@ __global__ __launch_bounds__(256) void knn_scan_kernel(uint64_t* __restrict__ cn
     if (t == 0 && all) at = (uint32_t)atomicAdd(&nchunk[b], (int32_t)all);
     at = __shfl(at, 0);
     uint2* Ch = chunks + b * maxch + at + off;
-    for (uint32_t i = 0; i < nch; ++i)
-      Ch[i] = make_uint2(q0 + 64 * i, min(q0 + 64 * (i + 1), q1));
+    uint32_t i = 0;
+    walk([&](uint32_t a, uint32_t e) { Ch[i++] = make_uint2(a, e); });
   }
 }
 
