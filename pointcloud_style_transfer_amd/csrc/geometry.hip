@@ -237,6 +237,321 @@ __global__ __launch_bounds__(kFps2Threads) void fps_key_kernel(const float* __re
   }
 }
 
+// Spatially culled FPS (the default for 8192 < N <= 30720).  Same arithmetic, keys and
+// result as fps_key_kernel; the points are laid out so that a round can skip most waves.
+//   Layout: the cloud is cut into 16 regions, one per wave: contiguous runs of a 14-bit Morton
+//   order of the points (5/5/4 bits over the cloud's bounding box), filled greedily up to a
+//   wave's 64*R register slots (R = min(PPT, 28): registers hold point pairs, and 15 pairs per
+//   lane would not leave the loop its temporaries in 128 VGPRs); the points past 16 full
+//   regions (at most 4096) form an overflow set kept in LDS (in the histogram's space), four
+//   per lane of the first waves, updated every round.  Inside a
+//   region the points keep ascending index order (a stable counting sort by region), so slot s
+//   of wave w is lane s % 64, register k = s / 64, and a lane's registers hold ascending
+//   indices: the lowest k holding the lane's maximum is still its lowest index (Q3).  perm[]
+//   (LDS, 16-bit) maps a slot back to the point index.
+//   Culling: a wave whose bounding box is at least its current maximum distance away from the
+//   new centroid cannot change any running minimum (fl() is monotone, so the box distance
+//   computed with the points' own operation sequence bounds every point's computed distance
+//   from below) and keeps last round's key, (distance bits << 32) | ~index.  If the greedy fill
+//   leaves more than 4096 points over (a degenerate cloud), the regions are plain index ranges:
+//   the same result, little culling.
+constexpr int kCullBins = 16384;
+constexpr int kCullRegions = kFps2Waves;  // + 1: the overflow set
+constexpr int kCullOver = 4096;           // overflow capacity (the histogram's LDS)
+
+__device__ __forceinline__ uint32_t spread3(uint32_t v) {  // 5 bits -> every third bit
+  uint32_t r = 0;
+#pragma unroll
+  for (int b = 0; b < 5; ++b) r |= ((v >> b) & 1u) << (3 * b);
+  return r;
+}
+
+__device__ __forceinline__ float wave_minf(float v) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) v = fminf(v, __shfl_xor(v, off));
+  return v;
+}
+__device__ __forceinline__ float wave_maxf(float v) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) v = fmaxf(v, __shfl_xor(v, off));
+  return v;
+}
+__device__ __forceinline__ float uni(float v) {  // a wave-uniform value into an SGPR
+  return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v)));
+}
+
+template <int PPT>
+__global__ __launch_bounds__(kFps2Threads) void fps_cull_kernel(const float* __restrict__ xyz,
+                                                                int N, int npoint,
+                                                                const int64_t* __restrict__ start,
+                                                                int64_t* __restrict__ out) {
+  constexpr int R = PPT < 28 ? PPT : 28;  // register slots per lane (an even count)
+  constexpr int H = (R + 1) / 2;
+  constexpr int W = kFps2Waves;
+  constexpr int G = kCullRegions + 1;
+  const int b = blockIdx.x;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const float* P = xyz + (int64_t)b * N * 3;
+  __shared__ uint16_t perm[kFps2Threads * PPT];
+  __shared__ __attribute__((aligned(16))) uint32_t hist[kCullBins];
+  // after the layout is built the histogram's space holds the overflow points: x, y, z, and
+  // the running distance bits
+  float4* s_over = reinterpret_cast<float4*>(hist);
+  static_assert(kCullOver * 16 <= kCullBins * 4, "overflow set must fit the histogram's space");
+  __shared__ float s_red[W][6];
+  __shared__ int s_rs[G + 1];
+  __shared__ int s_cur[G];
+  __shared__ int s_cnt[2][W][G];  // [buffer][wave][region]
+  __shared__ int s_ok;
+  __shared__ uint64_t s_key[2][W];
+
+  // ---- bounding box and Morton bins of the points in index order (n = tid + 1024 k)
+  float mn[3] = {INFINITY, INFINITY, INFINITY}, mx[3] = {-INFINITY, -INFINITY, -INFINITY};
+#pragma unroll 2
+  for (int k = 0; k < PPT; ++k) {
+    const int n = tid + k * kFps2Threads;
+    if (n < N) {
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        const float v = P[n * 3 + c];
+        mn[c] = fminf(mn[c], v);
+        mx[c] = fmaxf(mx[c], v);
+      }
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    mn[c] = wave_minf(mn[c]);
+    mx[c] = wave_maxf(mx[c]);
+    if (lane == 0) { s_red[wid][c] = mn[c]; s_red[wid][3 + c] = mx[c]; }
+  }
+  for (int i = tid; i < kCullBins; i += kFps2Threads) hist[i] = 0;
+  __syncthreads();
+  float lo[3], sc[3];
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    float a = s_red[0][c], z = s_red[0][3 + c];
+    for (int w = 1; w < W; ++w) { a = fminf(a, s_red[w][c]); z = fmaxf(z, s_red[w][3 + c]); }
+    lo[c] = a;
+    const float ext = z - a;
+    sc[c] = ext > 0.0f ? (c == 2 ? 16.0f : 32.0f) / ext : 0.0f;
+  }
+  // 14-bit Morton bin: x and y 5 bits, z 4
+  auto bin_of = [&](int n) {
+    const uint32_t qx = min((uint32_t)((P[n * 3 + 0] - lo[0]) * sc[0]), 31u);
+    const uint32_t qy = min((uint32_t)((P[n * 3 + 1] - lo[1]) * sc[1]), 31u);
+    const uint32_t qz = min((uint32_t)((P[n * 3 + 2] - lo[2]) * sc[2]), 15u);
+    return (spread3(qx) | (spread3(qy) << 1) | (spread3(qz) << 2)) & (uint32_t)(kCullBins - 1);
+  };
+#pragma unroll 2
+  for (int k = 0; k < PPT; ++k) {
+    const int n = tid + k * kFps2Threads;
+    if (n < N) atomicAdd(&hist[bin_of(n)], 1u);
+  }
+  __syncthreads();
+  // ---- exclusive scan of the histogram (16 bins per thread)
+  {
+    uint32_t v[16], sum = 0;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) { v[i] = hist[tid * 16 + i]; sum += v[i]; }
+    uint32_t incl = sum;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = __shfl_up(incl, o);
+      if (lane >= o) incl += y;
+    }
+    if (lane == 63) s_cnt[0][0][wid] = incl;
+    __syncthreads();
+    uint32_t base = 0;
+    for (int w = 0; w < wid; ++w) base += s_cnt[0][0][w];
+    uint32_t run = base + incl - sum;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) { hist[tid * 16 + i] = run; run += v[i]; }
+  }
+  __syncthreads();
+  // ---- region boundaries (wave 0): region r = bins [e_r, e_{r+1}), greedy up to 64*R points;
+  // the overflow set is everything after region 15
+  const uint32_t cap = 64u * R;
+  if (wid == 0) {
+    uint32_t e = 0;  // bin where the current region starts
+    for (int r = 0; r < kCullRegions; ++r) {
+      const uint32_t s0 = e >= kCullBins ? (uint32_t)N : hist[e];
+      // last bin boundary f in [e, kCullBins] with start(f) - s0 <= cap (start(kCullBins) = N)
+      uint32_t lo_b = e, hi_b = kCullBins;
+      while (hi_b > lo_b) {
+        const uint32_t span = hi_b - lo_b;
+        const uint32_t f = lo_b + (uint32_t)(((uint64_t)span * (lane + 1) + 63) / 64);
+        const uint32_t sf = f >= kCullBins ? (uint32_t)N : hist[f];
+        const uint64_t fits = __ballot(sf - s0 <= cap);  // a prefix of the lanes (monotone)
+        const int last = fits ? 63 - __builtin_clzll(fits) : -1;
+        const uint32_t flast = last < 0 ? lo_b : lo_b + (uint32_t)(((uint64_t)span * (last + 1) + 63) / 64);
+        const uint32_t fnext = lo_b + (uint32_t)(((uint64_t)span * (last + 2) + 63) / 64);
+        lo_b = flast;
+        hi_b = last == 63 ? flast : (fnext > lo_b ? fnext - 1 : lo_b);
+      }
+      if (lane == 0) s_rs[r] = (int)s0;
+      e = lo_b;
+    }
+    const uint32_t s16 = e >= kCullBins ? (uint32_t)N : hist[e];
+    if (lane == 0) {
+      const bool ok = (uint32_t)N - s16 <= (uint32_t)kCullOver;
+      s_ok = ok;
+      s_rs[kCullRegions] = ok ? (int)s16 : (int)min((uint32_t)N, cap * kCullRegions);
+      s_rs[G] = N;
+      if (!ok)  // plain index ranges
+        for (int r = 0; r < kCullRegions; ++r) s_rs[r] = (int)min((uint32_t)N, cap * r);
+    }
+  }
+  if (tid < G) s_cur[tid] = 0;
+  __syncthreads();
+  const bool morton = s_ok != 0;
+  // ---- stable counting sort by region, chunk k = the points tid + 1024 k (ascending index)
+#pragma unroll 1
+  for (int k = 0; k < PPT; ++k) {
+    const int n = tid + k * kFps2Threads;
+    int reg = -1;
+    if (n < N) {
+      if (morton) {
+        const uint32_t pos = hist[bin_of(n)];  // region of the bin: its start's region
+        reg = 0;
+#pragma unroll
+        for (int r = 1; r < G; ++r) reg += pos >= (uint32_t)s_rs[r] ? 1 : 0;
+      } else {
+        reg = min(n / (int)cap, kCullRegions);
+      }
+    }
+    uint64_t mine = 0;
+    int cnt_lane = 0;
+#pragma unroll
+    for (int r = 0; r < G; ++r) {
+      const uint64_t m = __ballot(reg == r);
+      if (reg == r) mine = m;
+      if (lane == r) cnt_lane = __popcll(m);
+    }
+    const int buf = k & 1;
+    if (lane < G) s_cnt[buf][wid][lane] = cnt_lane;
+    __syncthreads();
+    if (reg >= 0) {
+      int pre = s_cur[reg];
+      for (int w = 0; w < wid; ++w) pre += s_cnt[buf][w][reg];
+      perm[s_rs[reg] + pre + __popcll(mine & lanemask_lt())] = (uint16_t)n;
+    }
+    __syncthreads();
+    if (tid < G) {
+      int t = 0;
+      for (int w = 0; w < W; ++w) t += s_cnt[buf][w][tid];
+      s_cur[tid] += t;
+    }
+  }
+  __syncthreads();
+  // ---- overflow points into LDS (slot i: wave i >> 8, lane i & 63, m = (i >> 6) & 3), this
+  // wave's region into registers (pairs k, k+1)
+  const int o0 = __builtin_amdgcn_readfirstlane(s_rs[kCullRegions]);
+  const int nover = N - o0;
+  for (int i = tid; i < nover; i += kFps2Threads) {
+    const int n = perm[o0 + i];
+    s_over[i] = make_float4(P[n * 3 + 0], P[n * 3 + 1], P[n * 3 + 2], 1e10f);
+  }
+  const int r0 = __builtin_amdgcn_readfirstlane(s_rs[wid]);
+  const int r1 = __builtin_amdgcn_readfirstlane(s_rs[wid + 1]);
+  fps_f2 X[H], Y[H], Z[H];
+  fps_i2 D[H];
+#pragma unroll
+  for (int j = 0; j < H; ++j) {
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const int p = r0 + (2 * j + e) * 64 + lane;
+      const bool ok = 2 * j + e < R && p < r1;
+      const int n = ok ? (int)perm[p] : 0;
+      X[j][e] = ok ? P[n * 3 + 0] : 0.0f;
+      Y[j][e] = ok ? P[n * 3 + 1] : 0.0f;
+      Z[j][e] = ok ? P[n * 3 + 2] : 0.0f;
+      D[j][e] = __float_as_int(ok ? 1e10f : -1.0f);
+    }
+  }
+  // the wave's bounding box (uniform)
+  float bmn[3], bmx[3];
+  {
+    float a0 = INFINITY, a1 = INFINITY, a2 = INFINITY, z0 = -INFINITY, z1 = -INFINITY, z2 = -INFINITY;
+#pragma unroll
+    for (int j = 0; j < H; ++j)
+#pragma unroll
+      for (int e = 0; e < 2; ++e)
+        if (D[j][e] >= 0) {
+          a0 = fminf(a0, X[j][e]); z0 = fmaxf(z0, X[j][e]);
+          a1 = fminf(a1, Y[j][e]); z1 = fmaxf(z1, Y[j][e]);
+          a2 = fminf(a2, Z[j][e]); z2 = fmaxf(z2, Z[j][e]);
+        }
+    bmn[0] = uni(wave_minf(a0)); bmn[1] = uni(wave_minf(a1)); bmn[2] = uni(wave_minf(a2));
+    bmx[0] = uni(wave_maxf(z0)); bmx[1] = uni(wave_maxf(z1)); bmx[2] = uni(wave_maxf(z2));
+  }
+  const bool has_over = wid * 256 < nover;  // this wave carries overflow points (uniform)
+  // cached region state: key and maximum distance (-1: no point)
+  uint64_t rkey = 0;
+  float rmax = r1 > r0 ? 1e10f : -1.0f;
+  int far = (int)start[b];
+  int64_t* o = out + (int64_t)b * npoint;
+  __syncthreads();
+  for (int it = 0; it < npoint; ++it) {
+    if (tid == 0) o[it] = far;
+    const float cx = uni(P[far * 3 + 0]), cy = uni(P[far * 3 + 1]), cz = uni(P[far * 3 + 2]);
+    // box distance with the points' own operation sequence (a lower bound of every point's)
+    const float ex = cx < bmn[0] ? fsub(bmn[0], cx) : (cx > bmx[0] ? fsub(cx, bmx[0]) : 0.0f);
+    const float ey = cy < bmn[1] ? fsub(bmn[1], cy) : (cy > bmx[1] ? fsub(cy, bmx[1]) : 0.0f);
+    const float ez = cz < bmn[2] ? fsub(bmn[2], cz) : (cz > bmx[2] ? fsub(cz, bmx[2]) : 0.0f);
+    const float lb = fadd(fadd(fmul(ex, ex), fmul(ey, ey)), fmul(ez, ez));
+    if (!(lb >= rmax)) {  // wave-uniform
+      const fps_f2 c2x = {cx, cx}, c2y = {cy, cy}, c2z = {cz, cz};
+#pragma unroll
+      for (int j = 0; j < H; ++j) {
+        const fps_f2 dx = X[j] - c2x, dy = Y[j] - c2y, dz = Z[j] - c2z;
+        const fps_f2 d = (dx * dx + dy * dy) + dz * dz;
+        D[j][0] = min(__float_as_int(d[0]), D[j][0]);
+        D[j][1] = min(__float_as_int(d[1]), D[j][1]);
+      }
+      int best = D[0][0];
+#pragma unroll
+      for (int k = 1; k < 2 * H; ++k) best = max(best, D[k >> 1][k & 1]);
+      int bestk = 2 * H - 1;
+#pragma unroll
+      for (int k = 2 * H - 2; k >= 0; --k) bestk = D[k >> 1][k & 1] == best ? k : bestk;
+      uint64_t key = 0;
+      if (best >= 0) {
+        const uint32_t n = perm[r0 + bestk * 64 + lane];
+        key = ((uint64_t)(uint32_t)best << 32) | (0xFFFFFFFFu - n);
+      }
+      rkey = wave_max_u64(key);
+      rmax = r1 > r0 ? __int_as_float((int)(uint32_t)(rkey >> 32)) : -1.0f;
+    }
+    uint64_t wkey = rkey;
+    if (has_over) {  // the overflow points of this wave: every round
+      uint64_t key = 0;
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        const int i = wid * 256 + m * 64 + lane;
+        if (i < nover) {
+          const float4 q = s_over[i];
+          const float dx = fsub(q.x, cx), dy = fsub(q.y, cy), dz = fsub(q.z, cz);
+          const float d = fadd(fadd(fmul(dx, dx), fmul(dy, dy)), fmul(dz, dz));
+          const int dd = min(__float_as_int(d), __float_as_int(q.w));
+          s_over[i].w = __int_as_float(dd);
+          key = u64max(key, ((uint64_t)(uint32_t)dd << 32) | (0xFFFFFFFFu - (uint32_t)perm[o0 + i]));
+        }
+      }
+      wkey = u64max(wkey, wave_max_u64(key));
+    }
+    const int slot = it & 1;
+    if (lane == 0) s_key[slot][wid] = wkey;
+    __syncthreads();
+    uint64_t g = lane < W ? s_key[slot][lane] : 0ull;
+    g = row_max_u64(g);
+    const uint32_t glo = __builtin_amdgcn_readlane((uint32_t)g, 0);
+    far = (int)(0xFFFFFFFFu - glo);
+  }
+}
+
 // Fallback for N > 512*60: running distances in global memory (caller workspace), one
 // workgroup per cloud streaming the cloud every iteration.
 __global__ __launch_bounds__(1024) void fps_global_kernel(const float* __restrict__ xyz, int N,
@@ -478,6 +793,21 @@ static void launch_fps2(const float* xyz, int B, int N, int npoint, const int64_
                      out);
 }
 
+template <int PPT>
+static void launch_fps_cull(const float* xyz, int B, int N, int npoint, const int64_t* start,
+                            int64_t* out, hipStream_t s) {
+  hipLaunchKernelGGL(fps_cull_kernel<PPT>, dim3(B), dim3(kFps2Threads), 0, s, xyz, N, npoint, start,
+                     out);
+}
+
+static bool fps_cull_enabled() {  // PCST_FPS_CULL=0: fps_key_kernel for every size (A/B)
+  static const bool on = [] {
+    const char* e = getenv("PCST_FPS_CULL");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 extern "C" int pcst_fps_workspace_size(int64_t B, int64_t N, size_t* bytes) {
   *bytes = (N > (int64_t)kFpsThreads * 60) ? (size_t)(B * N) * sizeof(float) : 0;
   return PCST_OK;
@@ -492,6 +822,13 @@ extern "C" int pcst_fps_ws(const float* xyz, int64_t B, int64_t N, int64_t npoin
   hipStream_t s = as_stream(stream);
   const int b = (int)B, n = (int)N, np = (int)npoint;
   const int64_t ppt2 = cdiv(N, kFps2Threads);
+  if (ppt2 > 8 && ppt2 <= 30 && fps_cull_enabled()) {
+    if (ppt2 <= 16) launch_fps_cull<16>(xyz, b, n, np, start_idx, out_idx, s);
+    else if (ppt2 <= 24) launch_fps_cull<24>(xyz, b, n, np, start_idx, out_idx, s);
+    else launch_fps_cull<30>(xyz, b, n, np, start_idx, out_idx, s);
+    PCST_LAUNCH_CHECK("fps");
+    return PCST_OK;
+  }
   if (ppt2 <= 30) {
     if (ppt2 <= 1) launch_fps2<1>(xyz, b, n, np, start_idx, out_idx, s);
     else if (ppt2 <= 2) launch_fps2<2>(xyz, b, n, np, start_idx, out_idx, s);
