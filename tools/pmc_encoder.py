@@ -11,7 +11,7 @@ import os
 import sys
 from collections import defaultdict
 
-KERNELS = {"fps": "fps_key_kernel<30>", "ball_query": "ball_query_split_kernel"}
+KERNELS = {"fps": "fps_cull_kernel<30>", "ball_query": "ball_query_split_kernel"}
 
 
 def main():
