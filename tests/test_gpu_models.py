@@ -89,6 +89,12 @@ def test_guided_loop_direct_cfg1(mods, golden):
 
 
 def test_guided_loop_hierarchical(mods, golden):
+    """3-step hierarchical guided loop (4096 points, 1024 coarse) free-running against the
+    reference's output.  Every step is parity-exact when teacher-forced (next test); free running,
+    fp32 reordering in the noise MLP (1e-4 rel) can flip one query's kNN neighbour set (SURVEY
+    Q13), which moves that row by the distance between two candidate values.  Measured: max abs
+    1.3e-3 in ONE row, 99.967 % of the elements within 1e-4 rel.  Bounds: >= 99.9 % within
+    1e-4 rel, every element within 5e-3 abs (about 4x the measured flip)."""
     g = golden("sampling.npz")
     c, m = make_model(mods, total_points=4096, global_points=1024)
     m.eval()
@@ -97,7 +103,11 @@ def test_guided_loop_hierarchical(mods, golden):
     with mods["rng"].replay(rp):
         out = dp.guided_sample_loop(m, dev(g["b_src"]), dev(g["b_cond"]), 3, 7.5)
     assert rp.exhausted
-    assert_mostly_close(out.cpu().numpy(), g["b_out"], max_abs=5e-2)
+    o, r = out.cpu().numpy(), g["b_out"]
+    d = np.abs(o - r)
+    print(f"hierarchical 3-step: max abs {d.max():.3e}, rows with max > 1e-3: {(d.max(-1) > 1e-3).sum()}, "
+          f"frac within 1e-4 rel {np.mean(d <= 1e-4 * (np.abs(r) + 0.1 * np.abs(r).max())):.5f}")
+    assert_mostly_close(o, r, max_abs=5e-3)
 
 
 def test_guided_step_teacher_forced(mods, golden):
