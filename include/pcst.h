@@ -220,7 +220,9 @@ int pcst_knn_error(void* workspace, int64_t B, int64_t N, int64_t M, int32_t* er
                    void* stream);
 
 /* NoisePredictor.forward (diffusion_model.py:38-61), fused.  precision: 0 = exact f32 MFMA
- * (parity), 1 = bf16 MFMA with fp32 accumulation and fp32 residual stream.  blob/bias are the
+ * (parity); 1 = bf16 MFMA (v_mfma_f32_32x32x16_bf16) with fp32 accumulation and fp32 residual
+ * stream; 2 = the same arithmetic on v_mfma_f32_16x16x32_bf16 (the product bf16 path; its own
+ * fragment layout, packing.PAIR16, same blob size as 1).  blob/bias are the
  * packed weights of packing.py (blob 16-byte aligned, pcst_noise_mlp_blob_bytes() bytes).
  * pcst_noise_cond computes cond[c] = b4 + time_proj(TimeEmbedding(t_c)) + style_proj(style_c)
  * (freqs = the reference's 64-entry exp table; wt = time_proj.weight^T [128,256] and
