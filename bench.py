@@ -337,20 +337,25 @@ def main():
         else:
             knn_ws = None
 
+        S = len(timesteps)
+        conds = None  # every step's conditioning rows, one launch per loop (as guided_sample_loop)
+
+        def all_conds():
+            return npred.cond(t_rows.reshape(-1), style_in.repeat(S, 1)).view(S, 2 * C, -1)
+
         def step(i, timed):
             nonlocal x
             t = timesteps[i % len(timesteps)]
             t_prev = timesteps[i % len(timesteps) + 1] if t > 0 else -1
-            t_in = t_rows[i % len(timesteps)]
+            cnd = conds[i % len(timesteps)]
             xc, xi = hp.downsample_copies(x, 2)
 
             def mlp(xc_):
                 if not timed:
-                    return npred(xc_, t_in, style_in)
+                    return npred.forward_cond(xc_, cnd)
                 e0 = torch.cuda.Event(enable_timing=True)  # on the stream the MLP runs on
                 e1 = torch.cuda.Event(enable_timing=True)
                 blob, bias = npred.packed()[:2]
-                cnd = npred.cond(t_in, style_in)
                 e0.record()
                 nc_ = _hip.noise_mlp(xc_.reshape(-1, 3), cfg.global_points, cnd, blob, bias,
                                      npred.precision_code).view(2 * C, -1, 3)
@@ -364,6 +369,7 @@ def main():
 
         lctx = torch.cuda.stream(loop_stream) if overlap else contextlib.nullcontext()
         with lctx:
+            conds = all_conds()
             for i in range(args.warmup):
                 step(i, False)
             # the timed region restarts the sampling trajectory at t = 999 from x_T
@@ -376,6 +382,7 @@ def main():
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         with lctx:
+            conds = all_conds()  # the loop's one-time conditioning launch, inside the timed region
             for i in range(args.steps):
                 step(i, True)
         torch.cuda.synchronize()

@@ -168,17 +168,27 @@ class NoisePredictor(nn.Module):
         h = _ag.linear(h, self.output_mlp[2], True)
         return _ag.linear(h, self.output_mlp[4])
 
-    def forward(self, noisy_points: torch.Tensor, timestep: torch.Tensor,
-                style_feat: torch.Tensor) -> torch.Tensor:
+    def fused_inference(self, style_feat: torch.Tensor) -> bool:
+        """True when forward() runs the fused inference kernel (no autograd, no dropout)."""
+        return not (_ag.needs_grad(self) or self._dropout_active()
+                    or (style_feat.requires_grad and torch.is_grad_enabled()))
+
+    def forward_cond(self, noisy_points: torch.Tensor, cond: torch.Tensor) -> torch.Tensor:
+        """The fused inference forward with precomputed conditioning rows (`cond()` of the
+        same timesteps and style features): the sampling loops compute every step's rows in one
+        launch before the loop."""
         B, N, _ = noisy_points.shape
-        if (_ag.needs_grad(self) or self._dropout_active()
-                or (style_feat.requires_grad and torch.is_grad_enabled())):
-            return self._forward_autograd(noisy_points, timestep, style_feat)
         blob, bias = self.packed()[:2]
-        cond = self.cond(timestep.to(noisy_points.device), style_feat)
         out = _hip.noise_mlp(noisy_points.reshape(B * N, 3), N, cond, blob, bias,
                              self.precision_code)
         return out.view(B, N, 3)
+
+    def forward(self, noisy_points: torch.Tensor, timestep: torch.Tensor,
+                style_feat: torch.Tensor) -> torch.Tensor:
+        if not self.fused_inference(style_feat):
+            return self._forward_autograd(noisy_points, timestep, style_feat)
+        cond = self.cond(timestep.to(noisy_points.device), style_feat)
+        return self.forward_cond(noisy_points, cond)
 
 
 class HierarchicalProcessor:
@@ -386,6 +396,12 @@ class DiffusionProcess:
         t_rows = t_rows.view(len(timesteps), 2 * B).to(device)
         # the reference's t_prev lookup (first occurrence of t, diffusion_model.py:252)
         t_prevs = [timesteps[timesteps.index(t) + 1] if t > 0 else -1 for t in timesteps]
+        # every step's conditioning rows (time_proj + style_proj + b4, per CFG row) in one launch:
+        # they depend only on t and the style features, not on x
+        conds = None
+        if npred.fused_inference(style_in):
+            S = len(timesteps)
+            conds = npred.cond(t_rows.reshape(-1), style_in.repeat(S, 1)).view(S, 2 * B, -1)
         overlap = use_hierarchical and overlap_knn_build(2 * B * model.config.global_points)
         side = ws = None
         ctx = contextlib.nullcontext()
@@ -401,12 +417,16 @@ class DiffusionProcess:
             try:
                 for i, t in enumerate(timesteps):
                     t_in = t_rows[i]
+                    if conds is not None:
+                        cond_i = conds[i]
+                        mlp = lambda c: npred.forward_cond(c, cond_i)  # noqa: E731
+                    else:
+                        mlp = lambda c: npred(c, t_in, style_in)  # noqa: E731
                     if use_hierarchical:
                         xc, xi = hp.downsample_copies(x, 2)
-                        eps = hierarchical_eps(hp, lambda c: npred(c, t_in, style_in), xc, xi,
-                                               x_cat, ws, side)
+                        eps = hierarchical_eps(hp, mlp, xc, xi, x_cat, ws, side)
                     else:
-                        eps = npred(x_cat, t_in, style_in)
+                        eps = mlp(x_cat)
                     t_prev = t_prevs[i]
                     x = _hip.cfg_ddim_step(x, eps[:B], eps[B:], source, guidance_scale,
                                            self._coeffs(t, t_prev), x_cat=x_cat)
