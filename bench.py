@@ -338,6 +338,9 @@ def main():
             knn_ws = None
 
         S = len(timesteps)
+        timing_event = ((lambda: _hip.DeviceEvent(timing=True))
+                        if os.environ.get("PCST_DEVICE_EVENTS", "1") != "0"
+                        else (lambda: torch.cuda.Event(enable_timing=True)))
         conds = None  # every step's conditioning rows, one launch per loop (as guided_sample_loop)
 
         def all_conds():
@@ -353,8 +356,9 @@ def main():
             def mlp(xc_):
                 if not timed:
                     return npred.forward_cond(xc_, cnd)
-                e0 = torch.cuda.Event(enable_timing=True)  # on the stream the MLP runs on
-                e1 = torch.cuda.Event(enable_timing=True)
+                # on the stream the MLP runs on; device-scope fences (no L2 writeback bubble
+                # around the timed kernel) unless PCST_DEVICE_EVENTS=0
+                e0, e1 = timing_event(), timing_event()
                 blob, bias = npred.packed()[:2]
                 e0.record()
                 nc_ = _hip.noise_mlp(xc_.reshape(-1, 3), cfg.global_points, cnd, blob, bias,

@@ -213,8 +213,9 @@ int pcst_knn3_query(const float* coarse, const float* orig, int64_t B, int64_t N
 /* diagnostics of the last query on a workspace: out[0] error flag, out[1..B] query chunks per
  * cloud, out[1+B..2B] outlier queries per cloud (device int32 buffer of 1 + 2B) */
 int pcst_knn_stats(void* workspace, int64_t B, int64_t N, int64_t M, int32_t* out, void* stream);
-/* dynamic LDS (bytes, <= 96 KiB) added to the build-phase workgroups: a build on a side stream
- * then runs only on CUs the noise MLP leaves idle (see pcst_knn3_build) */
+/* LDS floor (bytes, <= 96 KiB) of the build-phase workgroups (a kernel whose static LDS is below
+ * it gets the difference as dynamic LDS): a build on a side stream then runs only on CUs the noise
+ * MLP leaves idle (see pcst_knn3_build); 0 = no floor */
 int pcst_knn_set_build_lds_pad(int64_t bytes);
 int pcst_knn_error(void* workspace, int64_t B, int64_t N, int64_t M, int32_t* err_out,
                    void* stream);
@@ -307,7 +308,17 @@ int pcst_knn_dist(const float* P, const float* Q, int64_t B, int64_t N, int64_t 
 int pcst_emd_greedy(const float* P, const float* Q, int64_t B, int64_t N, int64_t M, float* out,
                     void* stream);
 
+/* Stream-ordering events with device-scope fences only (hipEventDisableSystemFence; timing = 0
+ * also disables timing).  Used by the Python host for the sampling loop's cross-stream
+ * dependencies and the bench's kernel timing; plain HIP, no kernel. */
+int pcst_event_create(int timing, void** event);
+int pcst_event_destroy(void* event);
+int pcst_event_record(void* event, void* stream);
+int pcst_stream_wait_event(void* stream, void* event);
+int pcst_event_elapsed_ms(void* start, void* end, float* ms);
+
 #ifdef __cplusplus
 }
 #endif
+
 #endif /* PCST_H_ */

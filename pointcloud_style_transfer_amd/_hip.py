@@ -89,6 +89,11 @@ SIGNATURES = {
     "pcst_l1_workspace_size": [_SZ],
     "pcst_l1_fwd": [_P, _P, _I, _P, _P, _P],
     "pcst_l1_bwd": [_P, _P, _I, _P, _P, _P],
+    "pcst_event_create": [ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)],
+    "pcst_event_destroy": [_P],
+    "pcst_event_record": [_P, _P],
+    "pcst_stream_wait_event": [_P, _P],
+    "pcst_event_elapsed_ms": [_P, _P, ctypes.POINTER(ctypes.c_float)],
 }
 _RESTYPES = {"pcst_version": ctypes.c_char_p, "pcst_last_error": ctypes.c_char_p,
              "pcst_noise_mlp_blob_bytes": ctypes.c_int64}
@@ -319,6 +324,39 @@ def voxel_stats(points, target):
 def knn_workspace(B, N, M, device):
     """A workspace for knn3_build/knn3_query (allocate it on the stream that outlives both)."""
     return _workspace("pcst_knn_workspace_size", B, N, M, device=device)
+
+
+class DeviceEvent:
+    """A stream-ordering event with device-scope fences only (pcst_event_*: hipEventDisableSystemFence).
+    The default (torch.cuda.Event) records and waits with system-scope release/acquire, a ~10 us
+    bubble per cross-stream dependency in the sampling step; nothing here needs the host to see
+    device memory.  timing=True keeps timing (the bench's kernel timing)."""
+
+    def __init__(self, timing=False):
+        h = ctypes.c_void_p()
+        _call("pcst_event_create", 1 if timing else 0, ctypes.byref(h))
+        self._h = h
+
+    def record(self, stream=None):
+        s = stream if stream is not None else torch.cuda.current_stream()
+        _call("pcst_event_record", self._h, ctypes.c_void_p(s.cuda_stream))
+
+    def wait(self, stream=None):
+        """Make `stream` (default: the current stream) wait for this event."""
+        s = stream if stream is not None else torch.cuda.current_stream()
+        _call("pcst_stream_wait_event", ctypes.c_void_p(s.cuda_stream), self._h)
+
+    def elapsed_time(self, end):
+        ms = ctypes.c_float()
+        _call("pcst_event_elapsed_ms", self._h, end._h, ctypes.byref(ms))
+        return float(ms.value)
+
+    def __del__(self):
+        try:
+            if _lib is not None and self._h:
+                _lib.pcst_event_destroy(self._h)
+        except Exception:  # noqa: BLE001  (interpreter shutdown)
+            pass
 
 
 def knn_set_build_lds_pad(nbytes):

@@ -17,3 +17,43 @@ void set_error(const char* fmt, ...) {
 
 extern "C" const char* pcst_version(void) { return "pcst 0.1.0 gfx950"; }
 extern "C" const char* pcst_last_error(void) { return pcst::g_last_error; }
+
+// Stream-ordering events with device-scope fences only (hipEventDisableSystemFence): the
+// sampling loop's cross-stream dependencies (kNN build on a side stream) and the bench's kernel
+// timing need no host visibility of device memory, and the default system-scope release/acquire
+// (an L2 writeback + invalidate at every record and wait) costs a ~10 us bubble per dependency.
+extern "C" int pcst_event_create(int timing, void** event) {
+  PCST_CHECK_ARG(event != nullptr, "event_create: null pointer");
+  hipEvent_t e = nullptr;
+  const unsigned flags = hipEventDisableSystemFence | (timing ? 0u : (unsigned)hipEventDisableTiming);
+  PCST_HIP(hipEventCreateWithFlags(&e, flags), "event_create");
+  *event = e;
+  return PCST_OK;
+}
+
+extern "C" int pcst_event_destroy(void* event) {
+  if (event) PCST_HIP(hipEventDestroy(static_cast<hipEvent_t>(event)), "event_destroy");
+  return PCST_OK;
+}
+
+extern "C" int pcst_event_record(void* event, void* stream) {
+  PCST_CHECK_ARG(event != nullptr, "event_record: null event");
+  PCST_HIP(hipEventRecord(static_cast<hipEvent_t>(event), pcst::as_stream(stream)), "event_record");
+  return PCST_OK;
+}
+
+extern "C" int pcst_stream_wait_event(void* stream, void* event) {
+  PCST_CHECK_ARG(event != nullptr, "stream_wait_event: null event");
+  PCST_HIP(hipStreamWaitEvent(pcst::as_stream(stream), static_cast<hipEvent_t>(event), 0),
+           "stream_wait_event");
+  return PCST_OK;
+}
+
+// milliseconds between two recorded timing events (synchronises with the second)
+extern "C" int pcst_event_elapsed_ms(void* start, void* end, float* ms) {
+  PCST_CHECK_ARG(start && end && ms, "event_elapsed_ms: null pointer");
+  PCST_HIP(hipEventSynchronize(static_cast<hipEvent_t>(end)), "event_elapsed_ms: sync");
+  PCST_HIP(hipEventElapsedTime(ms, static_cast<hipEvent_t>(start), static_cast<hipEvent_t>(end)),
+           "event_elapsed_ms");
+  return PCST_OK;
+}

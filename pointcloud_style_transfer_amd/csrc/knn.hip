@@ -1219,14 +1219,27 @@ extern "C" int pcst_knn_workspace_size(int64_t B, int64_t N, int64_t M, size_t* 
   return PCST_OK;
 }
 
-// Dynamic LDS added to every build workgroup (pcst_knn_set_build_lds_pad).  A build that runs
-// on a side stream during the noise MLP then cannot co-reside with an MLP workgroup (~130 KiB
-// of LDS): it only takes the CUs the MLP leaves idle in its last partial round.
-static unsigned g_knn_build_lds_pad = 0;
+// LDS floor of every build workgroup (pcst_knn_set_build_lds_pad): a kernel whose own static
+// LDS is below it gets the difference as dynamic LDS.  A build that runs on a side stream during
+// the noise MLP then cannot co-reside with an MLP workgroup (155 KiB of the CU's 160): it only
+// takes the CUs the MLP leaves idle in its last partial round, and a floor just above the MLP's
+// leftover (8 KiB) keeps as many build workgroups per idle CU as their own LDS allows.
+static unsigned g_pad_pre = 0, g_pad_count = 0, g_pad_scan = 0, g_pad_fill = 0;
+
+static unsigned pad_for(const void* kernel, unsigned floor_bytes) {
+  if (!floor_bytes) return 0;
+  hipFuncAttributes a{};
+  if (hipFuncGetAttributes(&a, kernel) != hipSuccess) return floor_bytes;
+  return a.sharedSizeBytes >= floor_bytes ? 0u : floor_bytes - (unsigned)a.sharedSizeBytes;
+}
 
 extern "C" int pcst_knn_set_build_lds_pad(int64_t bytes) {
   PCST_CHECK_ARG(bytes >= 0 && bytes <= 98304, "knn_set_build_lds_pad: 0..98304 bytes");
-  g_knn_build_lds_pad = (unsigned)bytes;
+  const unsigned f = (unsigned)bytes;
+  g_pad_pre = pad_for((const void*)knn_pre_kernel, f);
+  g_pad_count = pad_for((const void*)knn_count_kernel, f);
+  g_pad_scan = pad_for((const void*)knn_scan_kernel, f);
+  g_pad_fill = pad_for((const void*)knn_fill_kernel, f);
   return PCST_OK;
 }
 
@@ -1244,19 +1257,20 @@ extern "C" int pcst_knn3_build(const float* orig, const int64_t* idx, int64_t B,
   hipStream_t s = as_stream(stream);
   KnnWS w = carve_knn(workspace, B, N, M);
   const int b = (int)B;
-  const unsigned lds_pad = g_knn_build_lds_pad;
+  const unsigned pad_pre = g_pad_pre, pad_count = g_pad_count, pad_scan = g_pad_scan,
+                 pad_fill = g_pad_fill;
   // error word, counters, known rows, tile sums and packed counts are contiguous in the carve
   PCST_HIP(hipMemsetAsync(w.err, 0, (size_t)(w.bytes - ((char*)w.err - (char*)workspace)), s),
            "knn: memset");
-  hipLaunchKernelGGL(knn_pre_kernel, dim3(kStatBlocks + kPreKnownBlocks, b), dim3(256), lds_pad, s,
+  hipLaunchKernelGGL(knn_pre_kernel, dim3(kStatBlocks + kPreKnownBlocks, b), dim3(256), pad_pre, s,
                      orig, idx, (int)N, M, w.stats, w.known, w.err);
   const unsigned gc = (unsigned)cdiv(M + N, kCountPerBlock);
-  hipLaunchKernelGGL(knn_count_kernel, dim3(gc, b), dim3(256), lds_pad, s, orig, idx, w.stats,
+  hipLaunchKernelGGL(knn_count_kernel, dim3(gc, b), dim3(256), pad_count, s, orig, idx, w.stats,
                      w.known, N, M, w.Cmax, w.T, w.Cpad, w.gp, w.cnt, w.tsum, w.crank);
-  hipLaunchKernelGGL(knn_scan_kernel, dim3((unsigned)w.T, b), dim3(256), lds_pad, s, w.cnt, w.tsum,
+  hipLaunchKernelGGL(knn_scan_kernel, dim3((unsigned)w.T, b), dim3(256), pad_scan, s, w.cnt, w.tsum,
                      w.T, w.Cpad, w.chunks, w.maxch, w.nchunk);
   const unsigned gf = (unsigned)std::min<int64_t>(cdiv(M + N, 256), 2048);
-  hipLaunchKernelGGL(knn_fill_kernel, dim3(gf, b), dim3(256), lds_pad, s, orig, idx, N, M, w.Cpad,
+  hipLaunchKernelGGL(knn_fill_kernel, dim3(gf, b), dim3(256), pad_fill, s, orig, idx, N, M, w.Cpad,
                      w.cnt, w.crank, w.refs, w.qorder);
   PCST_LAUNCH_CHECK("knn3_build");
   return PCST_OK;

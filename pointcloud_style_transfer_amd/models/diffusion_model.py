@@ -241,7 +241,12 @@ class HierarchicalProcessor:
 # (9.6 -> 10.4 ms per 32-cloud step), so the overlap applies up to two MLP rounds of points.
 _OVERLAP_KNN_BUILD = os.environ.get("PCST_KNN_OVERLAP", "1") != "0"
 _OVERLAP_MAX_MLP_POINTS = 2 * 128 * 256
-_KNN_BUILD_LDS_PAD = 65536
+# LDS floor of the build's work-groups (pcst_knn_set_build_lds_pad): just above what an MLP
+# work-group leaves free on its CU (160 - 154.6 KiB), so the build never co-resides with the MLP
+# but packs as many work-groups per idle CU as their own LDS allows (round 2 used a flat 64 KiB
+# pad on every build kernel: 1-2 work-groups per idle CU).  PCST_KNN_BUILD_LDS_FLOOR overrides
+# (A/B runs).
+_KNN_BUILD_LDS_PAD = int(os.environ.get("PCST_KNN_BUILD_LDS_FLOOR", "8192"))
 
 
 def overlap_knn_build(mlp_points: int) -> bool:
@@ -266,16 +271,42 @@ def hierarchical_eps(hp, mlp, xc, xi, x_cat, knn_ws=None, side=None):
     if side is None:
         return hp.upsample_knn(mlp(xc), x_cat, xi)
     main = torch.cuda.current_stream()
-    ready = torch.cuda.Event()
+    ready, built = _step_events(main.device)
     ready.record(main)
-    side.wait_event(ready)
+    ready.wait(side)
     with torch.cuda.stream(side):
         handle = _hip.knn3_build(x_cat, xi, knn_ws)
-        built = torch.cuda.Event()
         built.record(side)
     nc = mlp(xc)
-    main.wait_event(built)
+    built.wait(main)
     return _hip.knn3_query(nc, handle)
+
+
+_STEP_EVENTS: Dict[int, tuple] = {}
+_DEVICE_EVENTS = os.environ.get("PCST_DEVICE_EVENTS", "1") != "0"
+
+
+class _TorchEvent:
+    """torch.cuda.Event with the DeviceEvent interface (PCST_DEVICE_EVENTS=0: A/B runs)."""
+
+    def __init__(self):
+        self.e = torch.cuda.Event()
+
+    def record(self, stream):
+        self.e.record(stream)
+
+    def wait(self, stream):
+        stream.wait_event(self.e)
+
+
+def _step_events(device):
+    """The two cross-stream events of the overlapped step (reused every step: a wait captures
+    the event's state when it is enqueued)."""
+    key = torch.device(device).index or 0
+    if key not in _STEP_EVENTS:
+        mk = _hip.DeviceEvent if _DEVICE_EVENTS else _TorchEvent
+        _STEP_EVENTS[key] = (mk(), mk())
+    return _STEP_EVENTS[key]
 
 
 class PointCloudDiffusionModel(nn.Module):
