@@ -284,3 +284,32 @@ def test_knn_build_query_phases_match_interp(H):
     handle[2].record_stream(torch.cuda.current_stream())
     assert torch.equal(H.knn3_query(coarse, handle), ref)
     assert torch.equal(H.knn3_query(coarse, H.knn3_build(orig, idx)), ref)
+
+
+def test_device_events_order_streams(H):
+    """pcst_event_* (device-scope fences, the sampling step's cross-stream dependencies): a
+    consumer stream that waits on the event sees the producer stream's writes, here behind a
+    long producer chain that would otherwise still be running."""
+    prod, cons = torch.cuda.Stream(), torch.cuda.Stream()
+    a = torch.randn(2048, 2048, device="cuda")
+    out = torch.empty_like(a)
+    ev = H.DeviceEvent()
+    for rep in range(3):
+        prod.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(prod):
+            x = a.clone()
+            for _ in range(20):
+                x = torch.tanh(x @ a * 1e-3)
+            flag = x.sum().reshape(1)
+            ev.record(prod)
+        ev.wait(cons)
+        with torch.cuda.stream(cons):
+            out.copy_(x)
+            got = flag.clone()
+        torch.cuda.synchronize()
+        assert torch.equal(out, x) and torch.equal(got, x.sum().reshape(1)), rep
+    t0, t1 = H.DeviceEvent(timing=True), H.DeviceEvent(timing=True)
+    t0.record()
+    torch.tanh(a @ a)
+    t1.record()
+    assert t0.elapsed_time(t1) > 0.0
