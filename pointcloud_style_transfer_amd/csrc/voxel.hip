@@ -341,7 +341,6 @@ __global__ void vox_select_kernel(const float* __restrict__ pts, int N, int64_t 
 // read positions in this list, so the order matters there).
 constexpr int kSelBins = 4096;
 constexpr int kTieCap = 8192;
-constexpr int kTieLds = 1024;  // boundary-bin entries ranked from LDS (more: device-scope loads)
 #ifndef VOX_CHUNK  // experiment builds may override
 #define VOX_CHUNK 512
 #endif
@@ -365,7 +364,7 @@ struct VoxelFastWS {
   uint32_t* rhash;        // [B][N]
   unsigned long long* ties;  // [R][kTieCap] (key<<32 | id)
   // zeroed every call (one memset): counters, histograms, tables, rep flags
-  int32_t* cnt4;          // [R][4]: U (of cloud r, rows r < B), select workgroups done, ties, err
+  int32_t* cnt4;          // [R][4]: U (of cloud r, rows r < B), selected, ties, err
   uint32_t* hist;         // [R][kSelBins]
   unsigned long long* tkey;  // [B][H]  0 = empty, else (1<<32)|hash
   unsigned long long* tsum;  // [B][H]
@@ -580,9 +579,9 @@ __device__ __forceinline__ void voxf_flush_tiles(int row, int64_t tiles, const u
 }
 
 // Every workgroup first finds the row's boundary bin b* (the bin holding the need-th smallest
-// key) from the histogram; workgroup 0 records it (sel, diagnostics).  Then, over one
+// key) from the histogram; workgroup 0 records it for the ties kernel.  Then, over one
 // contiguous candidate range per workgroup: U <= T keeps every representative; keys below b*
-// are kept, keys in b* go to the tie list (its order is irrelevant: the last workgroup ranks).
+// are kept, keys in b* go to the tie list (its order is irrelevant: the ties kernel ranks).
 __global__ __launch_bounds__(256) void voxf_select_kernel(
     int N, int64_t T, int B, uint64_t seed_v, const uint64_t* __restrict__ seed_p,
     const uint32_t* __restrict__ hist, int32_t* __restrict__ sel, int32_t* __restrict__ cnt4,
@@ -647,36 +646,30 @@ __global__ __launch_bounds__(256) void voxf_select_kernel(
     }
   }
   voxf_flush_tiles(row, tiles, lt, ktile);
-  // The row's last workgroup to finish ranks the boundary bin exactly by (key, id) and keeps
-  // the first `rem` (what a separate ties kernel did): every workgroup fences its tie appends
-  // and marks, then counts itself done (cnt4[row][1], zeroed per call); the one that completes
-  // the count reads the ties with device-scope loads.
-  __shared__ int s_last;
-  __threadfence();
-  __syncthreads();
-  if (threadIdx.x == 0) s_last = atomicAdd(&cnt4[row * 4 + 1], 1) == (int)gridDim.x - 1;
-  __syncthreads();
-  if (!s_last || bstar < 0) return;
-  __threadfence();
-  const int rem = s_rem;
-  const int nt = min(__hip_atomic_load(&cnt4[row * 4 + 2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
-                     kTieCap);
+}
+
+// boundary bin: exact order by (key, id), keep the first `rem` (one workgroup per row)
+__global__ __launch_bounds__(1024) void voxf_ties_kernel(int N, int64_t T, int B,
+                                                         const int32_t* __restrict__ sel,
+                                                         const int32_t* __restrict__ cnt4,
+                                                         const unsigned long long* __restrict__ ties,
+                                                         const int64_t* __restrict__ reps,
+                                                         uint32_t* __restrict__ kcnt,
+                                                         uint32_t* __restrict__ ktile,
+                                                         int64_t tiles) {
+  const int row = blockIdx.x, cl = row % B;
+  if (sel[row * 4 + 0] < 0) return;
+  const int rem = sel[row * 4 + 1];
+  const int U = cnt4[cl * 4];
+  const int nt = min(cnt4[row * 4 + 2], kTieCap);
   const unsigned long long* Tb = ties + (int64_t)row * kTieCap;
-  __shared__ unsigned long long st[kTieLds];
-  const bool in_lds = nt <= kTieLds;
-  if (in_lds)
-    for (int i = threadIdx.x; i < nt; i += 256)
-      st[i] = __hip_atomic_load(&Tb[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  __syncthreads();
-  for (int i = threadIdx.x; i < nt; i += 256) {
-    const unsigned long long v =
-        in_lds ? st[i] : __hip_atomic_load(&Tb[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  for (int i = threadIdx.x; i < nt; i += 1024) {
+    const unsigned long long v = Tb[i];
     int rank = 0;
-    for (int k = 0; k < nt; ++k)
-      rank += (in_lds ? st[k] : __hip_atomic_load(&Tb[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) < v;
+    for (int k = 0; k < nt; ++k) rank += Tb[k] < v;
     if (rank < rem) {
       const uint32_t id = (uint32_t)v;
-      const int64_t n = U > T ? R[id] : (int64_t)id;
+      const int64_t n = U > T ? reps[(int64_t)cl * N + id] : (int64_t)id;
       atomicAdd(&kcnt[(int64_t)row * N + n], 1u);
       atomicAdd(&ktile[row * tiles + n / kEmitTile], 1u);
     }
@@ -748,6 +741,8 @@ static int voxel_fast(const float* pts, int64_t B, int64_t N, int64_t copies, in
   hipLaunchKernelGGL(voxf_select_kernel, dim3(128, rows), dim3(256), 0, s, n, T, b, seed, seed_p,
                      w.hist, w.sel, w.cnt4, w.rhash, w.isrep, w.reps, w.ties, w.kcnt, w.ktile,
                      w.tiles);
+  hipLaunchKernelGGL(voxf_ties_kernel, dim3(rows), dim3(1024), 0, s, n, T, b, w.sel, w.cnt4,
+                     w.ties, w.reps, w.kcnt, w.ktile, w.tiles);
   hipLaunchKernelGGL(voxf_emit_kernel, dim3((unsigned)w.tiles, rows), dim3(256), 0, s, pts, n, T,
                      b, w.kcnt, w.ktile, w.tiles, w.cnt4, out_idx, out_pts);
   PCST_LAUNCH_CHECK("voxel_downsample");
