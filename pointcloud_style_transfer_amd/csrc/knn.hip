@@ -744,8 +744,11 @@ __device__ __forceinline__ bool settled(const Query& me, const Box& cells, const
 }
 
 // One wave per chunk of <= 64 queries of one brick; the passes of the header comment.
+// amdgpu_waves_per_eu(4): 128 VGPRs (4 spilled) instead of 138, so 4 waves per SIMD (the LDS
+// allows 4 work-groups per CU) instead of 3: the ~5000 chunks of a step run in fewer rounds
+// (driver window 2379-2398 -> 2400-2429 steps/s, A/B on one box).
 template <int kk>  // min(M, 3), a compile-time constant so the top-3 stays in registers
-__global__ __launch_bounds__(256) void knn_query_kernel(
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) void knn_query_kernel(
     const float* __restrict__ orig, const float* __restrict__ vals, int64_t N, int64_t M,
     int64_t Cpad, const float* __restrict__ gp, const uint64_t* __restrict__ start,
     const float4* __restrict__ refs, const int32_t* __restrict__ qorder,
