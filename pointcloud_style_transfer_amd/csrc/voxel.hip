@@ -342,7 +342,7 @@ __global__ void vox_select_kernel(const float* __restrict__ pts, int N, int64_t 
 constexpr int kSelBins = 4096;
 constexpr int kTieCap = 8192;
 #ifndef VOX_CHUNK  // experiment builds may override
-#define VOX_CHUNK 512
+#define VOX_CHUNK 1024
 #endif
 #ifndef VOX_REPS_BLOCKS
 #define VOX_REPS_BLOCKS 512
