@@ -158,6 +158,15 @@ __device__ __forceinline__ uint64_t row_max_u64(uint64_t k) {
   return k;
 }
 
+__device__ __forceinline__ int wave_max_i32(int v) {  // wave-uniform result
+  v = max(v, __builtin_amdgcn_update_dpp(0, v, 0xB1, 0xf, 0xf, false));   // quad_perm [1,0,3,2]
+  v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x4E, 0xf, 0xf, false));   // quad_perm [2,3,0,1]
+  v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x141, 0xf, 0xf, false));  // row_half_mirror
+  v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x140, 0xf, 0xf, false));  // row_mirror
+  return max(max(__builtin_amdgcn_readlane(v, 0), __builtin_amdgcn_readlane(v, 16)),
+             max(__builtin_amdgcn_readlane(v, 32), __builtin_amdgcn_readlane(v, 48)));
+}
+
 __device__ __forceinline__ uint64_t wave_max_u64(uint64_t k) {
   k = row_max_u64(k);
   uint64_t m = 0;
@@ -511,19 +520,22 @@ __global__ __launch_bounds__(kFps2Threads) void fps_cull_kernel(const float* __r
         D[j][0] = min(__float_as_int(d[0]), D[j][0]);
         D[j][1] = min(__float_as_int(d[1]), D[j][1]);
       }
+      // the wave's maximum distance m (32-bit), then its lowest slot s = 64 k + lane holding m:
+      // slots are in ascending point index inside a region, so that is the lowest index (Q3)
       int best = D[0][0];
 #pragma unroll
       for (int k = 1; k < 2 * H; ++k) best = max(best, D[k >> 1][k & 1]);
-      int bestk = 2 * H - 1;
+      const int m = wave_max_i32(best);  // >= 0: the region has a point (else it is culled)
+      int ks = 2 * H - 1;
+      uint64_t lanes = 0;
 #pragma unroll
-      for (int k = 2 * H - 2; k >= 0; --k) bestk = D[k >> 1][k & 1] == best ? k : bestk;
-      uint64_t key = 0;
-      if (best >= 0) {
-        const uint32_t n = perm[r0 + bestk * 64 + lane];
-        key = ((uint64_t)(uint32_t)best << 32) | (0xFFFFFFFFu - n);
+      for (int k = 0; k < 2 * H; ++k) {
+        const uint64_t hit = __ballot(D[k >> 1][k & 1] == m);
+        if (hit) { ks = k; lanes = hit; break; }
       }
-      rkey = wave_max_u64(key);
-      rmax = r1 > r0 ? __int_as_float((int)(uint32_t)(rkey >> 32)) : -1.0f;
+      const uint32_t n = perm[r0 + ks * 64 + (__builtin_ffsll((long long)lanes) - 1)];
+      rkey = ((uint64_t)(uint32_t)m << 32) | (0xFFFFFFFFu - n);
+      rmax = __int_as_float(m);
     }
     uint64_t wkey = rkey;
     if (has_over) {  // the overflow points of this wave: every round
