@@ -53,7 +53,8 @@ def test_fps_vs_oracle_sizes(H, N, npoint, B):
     np.testing.assert_array_equal(out, O.farthest_point_sample(xyz, npoint, start))
 
 
-@pytest.mark.parametrize("case", ["lidar", "duplicates", "one_bin", "lattice", "small_cluster"])
+@pytest.mark.parametrize("case", ["lidar", "duplicates", "one_bin", "lattice", "small_cluster",
+                                  "empty_regions"])
 def test_fps_culled_vs_oracle(H, case):
     """The spatially culled FPS (8192 < N <= 30720: Morton regions per wave, an LDS overflow
     set, skipped waves) against the oracle: clouds with exact distance ties (duplicated points,
@@ -73,6 +74,8 @@ def test_fps_culled_vs_oracle(H, case):
     elif case == "lattice":
         g = np.arange(32, dtype=np.float32)
         xyz = np.stack(np.meshgrid(g, g, g[:29], indexing="ij"), -1).reshape(1, -1, 3)
+    elif case == "empty_regions":  # 8200 points over 16 regions of 576 slots: the last ones empty
+        xyz = rng.standard_normal((2, 8200, 3)).astype(np.float32)
     else:
         xyz = rng.standard_normal((2, 9000, 3)).astype(np.float32)
     B, N = xyz.shape[:2]
