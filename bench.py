@@ -61,6 +61,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true",
                     help="skip the oracle leg (cpu_baseline and quality)")
     ap.add_argument("--no-encoder", action="store_true")
+    ap.add_argument("--no-other-precision", action="store_true",
+                    help="skip timing the other noise-MLP precision mode after the headline")
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "noise_mlp_traffic.json"))
     ap.add_argument("--encoder-traffic-json",
                     default=os.path.join(REPO, "profiles", "encoder_traffic.json"))
@@ -109,7 +111,9 @@ def build_model(precision, device):
 
 def host_cpu():
     """CPU model, physical cores, the CPUs this process may run on, and the BLAS threads the
-    oracle uses (= min of the affinity set, OMP_NUM_THREADS and the physical cores)."""
+    oracle uses (= min of the affinity set, OMP_NUM_THREADS and the physical cores).  On the GPU
+    box the harness exports OMP_NUM_THREADS=16: one GPU's share of the 8-GPU host's cores, which
+    other GPUs' jobs use at the same time.  The cap is recorded with its source."""
     model = "unknown"
     try:
         with open("/proc/cpuinfo") as f:
@@ -126,10 +130,17 @@ def host_cpu():
     except Exception:  # noqa: BLE001
         physical = os.cpu_count()
     visible = len(os.sched_getaffinity(0))
-    cap = int(os.environ.get("OMP_NUM_THREADS", str(visible)))
+    omp = os.environ.get("OMP_NUM_THREADS")
+    cap = int(omp) if omp else visible
     threads = max(1, min(visible, cap, physical or visible))
-    return {"cpu_model": model, "physical_cores_on_host": physical,
-            "cpus_visible_to_process": visible, "threads": threads}
+    rec = {"cpu_model": model, "physical_cores_on_host": physical,
+           "cpus_visible_to_process": visible, "OMP_NUM_THREADS": omp, "threads": threads}
+    if threads < (physical or threads):
+        rec["cap"] = {"threads": threads,
+                      "source": "OMP_NUM_THREADS as found in the environment (the GPU box "
+                                "exports 16: one GPU's share of the host CPUs)" if omp else
+                                "CPU affinity set of this process"}
+    return rec
 
 
 def oracle_leg(args, cfg, model, dp, src_np, cond_np, xT_np, device):
@@ -191,6 +202,10 @@ def oracle_leg(args, cfg, model, dp, src_np, cond_np, xT_np, device):
     per = float(np.median(step_s[1:])) if len(step_s) > 1 else step_s[0]
     base = {"value": round(1.0 / per, 4), "unit": "denoising-steps/s", "cores": cpu["threads"],
             "kind": "port",
+            # not measured: what the same run would give if it scaled linearly to every
+            # physical core of the host (an upper bound; the oracle's BLAS does not scale so)
+            "linear_upper_bound_all_physical_cores": round(
+                (1.0 / per) * (cpu["physical_cores_on_host"] or cpu["threads"]) / cpu["threads"], 3),
             "sample": f"oracle (numpy/OpenBLAS fp32 MLP + C voxel/kNN, port of the reference "
                       f"path) guided loop on 1 x {args.points}-pt cloud, CFG x2, 30k coarse, "
                       f"{S}-step schedule; median of steps 2..{S}: {per:.3f} s/step "
@@ -333,13 +348,11 @@ def main():
             loop_stream.wait_stream(torch.cuda.current_stream())
             with torch.cuda.stream(loop_stream):
                 knn_ws = _hip.knn_workspace(2 * C, args.points, cfg.global_points, device=device)
-            _hip.knn_set_build_lds_pad(dmod._KNN_BUILD_LDS_PAD)
         else:
             knn_ws = None
 
         S = len(timesteps)
-        timing_event = ((lambda: _hip.DeviceEvent(timing=True))
-                        if os.environ.get("PCST_DEVICE_EVENTS", "1") != "0"
+        timing_event = ((lambda: _hip.DeviceEvent(timing=True)) if dmod.DEVICE_EVENTS
                         else (lambda: torch.cuda.Event(enable_timing=True)))
         conds = None  # every step's conditioning rows, one launch per loop (as guided_sample_loop)
 
@@ -357,7 +370,7 @@ def main():
                 if not timed:
                     return npred.forward_cond(xc_, cnd)
                 # on the stream the MLP runs on; device-scope fences (no L2 writeback bubble
-                # around the timed kernel) unless PCST_DEVICE_EVENTS=0
+                # around the timed kernel) unless tools/knobs.py turned them off
                 e0, e1 = timing_event(), timing_event()
                 blob, bias = npred.packed()[:2]
                 e0.record()
@@ -391,11 +404,37 @@ def main():
                 step(i, True)
         torch.cuda.synchronize()
         elapsed = time.perf_counter() - t0
-        if overlap:
-            _hip.knn_set_build_lds_pad(0)
         if world > 1:
             dist.barrier()
             elapsed = max_over_ranks(elapsed, device=device)
+
+        # the other precision mode, same loop and stream layout, outside the timed region
+        # (N = 1 only): the fp32 (parity) mode's steps/s beside the bf16 headline
+        other = None
+        if world == 1 and not args.no_other_precision:
+            prec0 = cfg.precision
+            cfg.precision = "fp32" if prec0 == "bf16" else "bf16"
+            try:
+                with lctx:
+                    x = torch.from_numpy(xT_np).to(device)
+                    x_cat.copy_(torch.cat([x, x]))
+                    conds = all_conds()
+                    for i in range(2):
+                        step(i, False)
+                torch.cuda.synchronize()
+                t1 = time.perf_counter()
+                with lctx:
+                    conds = all_conds()
+                    for i in range(args.steps):
+                        step(i, False)
+                torch.cuda.synchronize()
+                el = time.perf_counter() - t1
+                other = {"precision": cfg.precision, "value": round(C * args.steps / el, 3),
+                         "ms_per_step": round(el / args.steps * 1e3, 4),
+                         "note": "same loop, steps and stream layout as the headline, timed "
+                                 "after it (not part of value)"}
+            finally:
+                cfg.precision = prec0
 
     mlp_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
     flop = FLOP_PER_POINT * 2 * C * cfg.global_points
@@ -440,6 +479,7 @@ def main():
                          "frac": round(achieved / peak, 4), "traffic": traffic,
                          "algorithmic": f"{FLOP_PER_POINT} FLOP/pt x {2 * C * cfg.global_points} pts",
                          "avg_launch_ms": round(mlp_ms, 4)},
+            "other_precision": other,
             "cpu_baseline": base,
             "quality": quality,
             "encoder_rooflines": enc,

@@ -10,7 +10,8 @@
  * Conventions:
  *   - every pointer is a DEVICE pointer owned by the caller; the library never
  *     allocates or frees, and keeps no global mutable state except a
- *     thread-local last-error string;
+ *     thread-local last-error string (no setters, no environment variables:
+ *     every choice a call makes is one of its arguments);
  *   - index tensors are int64 at the boundary;
  *   - `stream` is a hipStream_t passed as void*; no call synchronises the host,
  *     so every call can be captured into a hipGraph;
@@ -205,18 +206,17 @@ int pcst_knn3_interp(const float* coarse, const float* orig, const int64_t* idx,
 /* The same computation in two phases on one workspace (knn3_interp = build then query):
  * build reads only positions (orig, idx) -- the grid statistics, cell counts, scan and fill --
  * so it can run on a second stream while the noise MLP produces `coarse`; query reads `coarse`
- * and writes out.  The caller orders query after build on the workspace. */
+ * and writes out.  The caller orders query after build on the workspace.
+ * lds_floor (bytes, 0..96 KiB): LDS floor of the build-phase workgroups (a kernel whose static LDS
+ * is below it gets the difference as dynamic LDS), so that a build on a side stream runs only on
+ * CUs the noise MLP leaves idle; 0 = no floor (knn3_interp passes 0). */
 int pcst_knn3_build(const float* orig, const int64_t* idx, int64_t B, int64_t N, int64_t M,
-                    void* workspace, void* stream);
+                    int64_t lds_floor, void* workspace, void* stream);
 int pcst_knn3_query(const float* coarse, const float* orig, int64_t B, int64_t N, int64_t M,
                     float* out, void* workspace, void* stream);
 /* diagnostics of the last query on a workspace: out[0] error flag, out[1..B] query chunks per
  * cloud, out[1+B..2B] outlier queries per cloud (device int32 buffer of 1 + 2B) */
 int pcst_knn_stats(void* workspace, int64_t B, int64_t N, int64_t M, int32_t* out, void* stream);
-/* LDS floor (bytes, <= 96 KiB) of the build-phase workgroups (a kernel whose static LDS is below
- * it gets the difference as dynamic LDS): a build on a side stream then runs only on CUs the noise
- * MLP leaves idle (see pcst_knn3_build); 0 = no floor */
-int pcst_knn_set_build_lds_pad(int64_t bytes);
 int pcst_knn_error(void* workspace, int64_t B, int64_t N, int64_t M, int32_t* err_out,
                    void* stream);
 
@@ -263,12 +263,11 @@ int pcst_voxel_downsample_copies_dseed(const float* pts, int64_t B, int64_t N, i
  * workspace: the clouds repacked as point pairs (exhaustive row-min) or counting-sorted into
  * uniform grids (grid-pruned row-min). */
 int pcst_chamfer_fwd_workspace_size(int64_t B, int64_t N, int64_t M, size_t* bytes);
-/* forward path: 0 default (= exhaustive), 1 exhaustive, 2 grid-pruned (fast for overlapping
- * clouds, slow for rows far outside the other cloud); all give bit-identical minima and
- * first-index argmins */
-int pcst_chamfer_set_mode(int mode);
+/* mode: 0 default (= exhaustive), 1 exhaustive, 2 grid-pruned (fast for overlapping clouds,
+ * slow for rows far outside the other cloud); all give bit-identical minima and first-index
+ * argmins. */
 int pcst_chamfer_fwd(const float* pred, const float* target, int64_t B, int64_t N, int64_t M,
-                     float* min1, int32_t* arg1, float* min2, int32_t* arg2, float* out,
+                     float* min1, int32_t* arg1, float* min2, int32_t* arg2, float* out, int mode,
                      void* workspace, void* stream);
 /* Gradient of sum_b grad_out[b]*chamfer[b]; ACCUMULATES into grad_pred [B,N,3] and/or
  * grad_target [B,M,3] (either may be NULL).  Deterministic (sorted scatter, no float atomics). */

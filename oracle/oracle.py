@@ -363,6 +363,44 @@ def guided_sample_loop(sd, source, cond, steps, scale, replay, global_points=300
     return x
 
 
+def guided_loop_counter(sd, source, cond, x_T, steps, ctr, scale=7.5, global_points=30000,
+                        num_timesteps=1000):
+    """`guided_sample_loop` (diffusion_model.py:224-261) on ONE cloud with the draws of a
+    counter-keyed generator `ctr` (`rng.CounterRNG`: the k-th draw comes from PCG64 seeded with
+    (seed, k)), made in the order the product loop makes them under `rng.replay(ctr)`: the
+    condition cloud's voxel permutation, the two FPS starts (SA1, SA2), then per step one
+    permutation per CFG row.  x_T is passed in (the product's keyword-only `x_T=`)."""
+    T = global_points
+    sched = Schedule(num_timesteps)
+
+    def down(rows):
+        outs, idxs = [], []
+        for b in range(rows.shape[0]):
+            reps = voxel_reps(rows[b], T)[0]
+            U = len(reps)   # reps may repeat an index (two voxels with the same mean index)
+            n = U if U > T else (rows.shape[1] - len(np.unique(reps)) if U < T else 0)
+            draws = [("randperm", ctr.generator().permutation(n))] if n else []
+            p, ix = voxel_downsample(rows[b:b + 1], T, Replay(draws))
+            outs.append(p[0])
+            idxs.append(ix[0])
+        return np.stack(outs), np.stack(idxs)
+
+    cdown, _ = down(_f32(cond))
+    starts = [("randint", ctr.generator().integers(0, cdown.shape[1], (1,), dtype=np.int64)),
+              ("randint", ctr.generator().integers(0, 512, (1,), dtype=np.int64))]
+    style = style_encoder(sd, cdown, Replay(starts))
+    style_in = np.concatenate([style, np.zeros_like(style)])
+    ts = timesteps_for(num_timesteps, steps)
+    x = _f32(x_T).copy()
+    for i, t in enumerate(ts):
+        x_in = np.concatenate([x, x])
+        xc, xi = down(x_in)
+        eps = upsample_knn(noise_predictor(sd, xc, np.full(2, t), style_in), x_in, xi)
+        x = guided_update(sched, x, eps[:1], eps[1:], source, int(t),
+                          int(ts[i + 1]) if t > 0 else -1, scale)
+    return x
+
+
 # ------------------------------------------------------------------ losses.py
 def chamfer_rowmin(P, Q):
     P, Q = _f32(P), _f32(Q)

@@ -46,13 +46,12 @@ SIGNATURES = {
     "pcst_voxel_downsample_copies": [_P, _I, _I, _I, _I, _P, ctypes.c_uint64, _P, _P, _P],
     "pcst_knn_workspace_size": [_I, _I, _I, _SZ],
     "pcst_knn3_interp": [_P, _P, _P, _I, _I, _I, _P, _P, _P],
-    "pcst_knn3_build": [_P, _P, _I, _I, _I, _P, _P],
+    "pcst_knn3_build": [_P, _P, _I, _I, _I, _I, _P, _P],
     "pcst_cfg_ddim_step_dcoef": [_P, _P, _P, _P, _I, ctypes.c_float, _P, _P, _P, _P],
     "pcst_voxel_downsample_copies_dseed": [_P, _I, _I, _I, _I, _P, _P, _P, _P, _P],
     "pcst_knn3_query": [_P, _P, _I, _I, _I, _P, _P, _P],
     "pcst_knn_error": [_P, _I, _I, _I, _P, _P],
     "pcst_knn_stats": [_P, _I, _I, _I, _P, _P],
-    "pcst_knn_set_build_lds_pad": [_I],
     "pcst_noise_mlp_blob_bytes": [ctypes.c_int],
     "pcst_noise_cond": [_P, _P, _I, _P, _P, _P, _P, _P, _P, _P, _P],
     "pcst_noise_mlp": [_P, _I, _I, _P, _I, _P, _I, _P, ctypes.c_int, _P, _P],
@@ -76,8 +75,7 @@ SIGNATURES = {
     "pcst_channel_stats": [_P, _I, _I, _P, _P, _P, _P],
     "pcst_affine_act": [_P, _I, _I, _P, _P, ctypes.c_int, _I, _P, _P],
     "pcst_chamfer_fwd_workspace_size": [_I, _I, _I, _SZ],
-    "pcst_chamfer_set_mode": [ctypes.c_int],
-    "pcst_chamfer_fwd": [_P, _P, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P],
+    "pcst_chamfer_fwd": [_P, _P, _I, _I, _I, _P, _P, _P, _P, _P, ctypes.c_int, _P, _P],
     "pcst_chamfer_bwd_workspace_size": [_I, _I, _I, _SZ],
     "pcst_chamfer_bwd": [_P, _P, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P],
     "pcst_bn_train_coeffs": [_P, _P, _I, _I, _P, _P, _D, _D, _P, _P, _P, _P, _P, _P],
@@ -359,21 +357,18 @@ class DeviceEvent:
             pass
 
 
-def knn_set_build_lds_pad(nbytes):
-    _call("pcst_knn_set_build_lds_pad", int(nbytes))
-
-
-def knn3_build(orig, idx, ws=None):
+def knn3_build(orig, idx, ws=None, lds_floor=0):
     """Phase 1 of knn3_interp (positions only) on the current stream -> workspace handle
     (orig, idx, workspace) for knn3_query.  `ws` (knn_workspace) may be preallocated, e.g. on
-    the stream that runs the query when the build runs on a side stream."""
+    the stream that runs the query when the build runs on a side stream; `lds_floor` (bytes)
+    keeps the build's work-groups off CUs that hold a noise-MLP work-group (pcst.h)."""
     require_device(orig, idx)
     orig, idx = _f32(orig), _i64(idx)
     B, N, _ = orig.shape
     M = idx.shape[1]
     if ws is None:
         ws = _workspace("pcst_knn_workspace_size", B, N, M, device=orig.device)
-    _call("pcst_knn3_build", _ptr(orig), _ptr(idx), B, N, M, _ptr(ws), _stream())
+    _call("pcst_knn3_build", _ptr(orig), _ptr(idx), B, N, M, int(lds_floor), _ptr(ws), _stream())
     return (orig, idx, ws)
 
 
@@ -682,8 +677,9 @@ def group_gather_bwd(dgrouped, group_idx, N):
 
 
 # ----------------------------------------------------------------------------- losses
-def chamfer_fwd(pred, target):
-    """-> (chamfer [B], arg1 [B,N] int32, arg2 [B,M] int32)."""
+def chamfer_fwd(pred, target, mode=0):
+    """-> (chamfer [B], arg1 [B,N] int32, arg2 [B,M] int32).  mode: 0 auto, 1 exhaustive,
+    2 grid-pruned (bit-identical results; pcst.h)."""
     require_device(pred, target)
     pred, target = _f32(pred), _f32(target)
     B, N, _ = pred.shape
@@ -696,13 +692,8 @@ def chamfer_fwd(pred, target):
     out = torch.empty(B, dtype=torch.float32, device=dev)
     ws = _workspace("pcst_chamfer_fwd_workspace_size", B, N, M, device=dev)
     _call("pcst_chamfer_fwd", _ptr(pred), _ptr(target), B, N, M, _ptr(min1), _ptr(arg1),
-          _ptr(min2), _ptr(arg2), _ptr(out), _ptr(ws), _stream())
+          _ptr(min2), _ptr(arg2), _ptr(out), int(mode), _ptr(ws), _stream())
     return out, arg1, arg2
-
-
-def chamfer_set_mode(mode):
-    """Chamfer forward path: 0 auto, 1 exhaustive, 2 grid-pruned (tests force one)."""
-    _call("pcst_chamfer_set_mode", int(mode))
 
 
 def chamfer_bwd(pred, target, arg1, arg2, grad_out, need_pred=True, need_target=False):
@@ -815,7 +806,7 @@ _GUARDED = ("square_distance", "index_points", "fps", "ball_query", "group_gathe
             "chamfer_bwd", "l1_fwd", "l1_bwd", "knn_dist", "emd_greedy", "voxel_center_dist",
             "cfg_ddim_step_dcoef", "voxel_downsample_copies_dseed", "bn_train_coeffs",
             "bn_relu_maxpool", "bn_relu_bwd", "group_gather_bwd", "gemm_ex", "dropout_grad_bf16",
-            "linear_wgrad_ex", "knn_workspace", "knn_set_build_lds_pad", "chamfer_set_mode")
+            "linear_wgrad_ex", "knn_workspace")
 for _name in _GUARDED:
     globals()[_name] = _on_tensor_device(globals()[_name])
 del _name

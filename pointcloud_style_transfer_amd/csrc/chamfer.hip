@@ -717,26 +717,18 @@ static CgWS carve_cg(void* base, int64_t B, int64_t N, int64_t M) {
   return w;
 }
 
-static int g_cd_mode = 0;  // 0 auto, 1 exhaustive, 2 grid (tests force a path)
-
 }  // namespace pcst
 
 using namespace pcst;
 
 static inline int64_t cd_padded(int64_t n) { return cdiv(n, kCdChunk) * kCdChunk; }
 
-extern "C" int pcst_chamfer_set_mode(int mode) {
-  PCST_CHECK_ARG(mode >= 0 && mode <= 2, "chamfer_set_mode: mode is 0 (auto), 1 (exhaustive) or 2 (grid)");
-  g_cd_mode = mode;
-  return PCST_OK;
-}
-
 // The grid path wins when the two clouds overlap (8 x 30000 lidar-like pairs 2.0 -> 0.32 ms),
 // but a row far outside the other cloud's grid has to search the thin shell of points within
 // its nearest distance, which grows with the distance: a noisy predicted x0 against its target
 // (the trainer's early timesteps) measured 46-60 ms.  The exhaustive path's cost does not
 // depend on the data, so it stays the default; the grid path is opt-in (mode 2).
-static bool cd_use_grid(int64_t, int64_t) { return g_cd_mode == 2; }
+static bool cd_use_grid(int mode) { return mode == 2; }
 
 extern "C" int pcst_chamfer_fwd_workspace_size(int64_t B, int64_t N, int64_t M, size_t* bytes) {
   PCST_CHECK_ARG(B >= 0 && N > 0 && M > 0 && bytes, "chamfer_fwd_workspace_size: bad args");
@@ -747,11 +739,13 @@ extern "C" int pcst_chamfer_fwd_workspace_size(int64_t B, int64_t N, int64_t M, 
 
 extern "C" int pcst_chamfer_fwd(const float* pred, const float* target, int64_t B, int64_t N,
                                 int64_t M, float* min1, int32_t* arg1, float* min2,
-                                int32_t* arg2, float* out, void* workspace, void* stream) {
+                                int32_t* arg2, float* out, int mode, void* workspace,
+                                void* stream) {
   PCST_CHECK_ARG(B >= 0 && N > 0 && M > 0 && N < (1ll << 30) && M < (1ll << 30), "chamfer_fwd: bad shape");
+  PCST_CHECK_ARG(mode >= 0 && mode <= 2, "chamfer_fwd: mode is 0 (auto), 1 (exhaustive) or 2 (grid)");
   if (B == 0) return PCST_OK;
   PCST_CHECK_ARG(pred && target && min1 && arg1 && min2 && arg2 && workspace, "chamfer_fwd: null pointer");
-  if (cd_use_grid(N, M)) {
+  if (cd_use_grid(mode)) {
     hipStream_t s = as_stream(stream);
     CgWS w = carve_cg(workspace, B, N, M);
     const unsigned b = (unsigned)B;
@@ -784,10 +778,11 @@ extern "C" int pcst_chamfer_fwd(const float* pred, const float* target, int64_t 
                      pred, (int)N, (int)Np, Pp);
   hipLaunchKernelGGL(chamfer_pack_kernel, dim3((unsigned)cdiv(Mp / 2, 256), b), dim3(256), 0, s,
                      target, (int)M, (int)Mp, Tp);
-  static const int variant = [] {  // S x R experiment knob: 11, 21, 41, 12, 22, 14
-    const char* e = getenv("PCST_CD_VARIANT");
-    return e ? atoi(e) : 21;
-  }();
+  // S x R shape of the row-min launch (experiment builds: XDEF=-DPCST_X_CD_VARIANT=11|41|12|22|14|42)
+#ifndef PCST_X_CD_VARIANT
+#define PCST_X_CD_VARIANT 21
+#endif
+  constexpr int variant = PCST_X_CD_VARIANT;
   auto rowmin = [&](const float* P, const float4* Qp, int64_t n, int64_t m, int64_t mp, float* md,
                     int32_t* am) {
 #define PCST_CD_LAUNCH(S_, R_)                                                                  \

@@ -812,13 +812,11 @@ static void launch_fps_cull(const float* xyz, int B, int N, int npoint, const in
                      out);
 }
 
-static bool fps_cull_enabled() {  // PCST_FPS_CULL=0: fps_key_kernel for every size (A/B)
-  static const bool on = [] {
-    const char* e = getenv("PCST_FPS_CULL");
-    return !(e && e[0] == '0');
-  }();
-  return on;
-}
+// experiment builds: XDEF=-DPCST_X_FPS_CULL=0 runs fps_key_kernel for every size (A/B)
+#ifndef PCST_X_FPS_CULL
+#define PCST_X_FPS_CULL 1
+#endif
+static constexpr bool fps_cull_enabled() { return PCST_X_FPS_CULL != 0; }
 
 extern "C" int pcst_fps_workspace_size(int64_t B, int64_t N, size_t* bytes) {
   *bytes = (N > (int64_t)kFpsThreads * 60) ? (size_t)(B * N) * sizeof(float) : 0;

@@ -1222,13 +1222,12 @@ extern "C" int pcst_knn_workspace_size(int64_t B, int64_t N, int64_t M, size_t* 
   return PCST_OK;
 }
 
-// LDS floor of every build workgroup (pcst_knn_set_build_lds_pad): a kernel whose own static
-// LDS is below it gets the difference as dynamic LDS.  A build that runs on a side stream during
-// the noise MLP then cannot co-reside with an MLP workgroup (155 KiB of the CU's 160): it only
-// takes the CUs the MLP leaves idle in its last partial round, and a floor just above the MLP's
-// leftover (8 KiB) keeps as many build workgroups per idle CU as their own LDS allows.
-static unsigned g_pad_pre = 0, g_pad_count = 0, g_pad_scan = 0, g_pad_fill = 0;
-
+// LDS floor of the build workgroups (the `lds_floor` argument of pcst_knn3_build): a kernel
+// whose own static LDS is below it gets the difference as dynamic LDS.  A build that runs on a
+// side stream during the noise MLP then cannot co-reside with an MLP workgroup (155 KiB of the
+// CU's 160): it only takes the CUs the MLP leaves idle in its last partial round, and a floor just
+// above the MLP's leftover (8 KiB) keeps as many build workgroups per idle CU as their own LDS
+// allows.  A pure function of the kernel and the floor (no state kept between calls).
 static unsigned pad_for(const void* kernel, unsigned floor_bytes) {
   if (!floor_bytes) return 0;
   hipFuncAttributes a{};
@@ -1236,32 +1235,26 @@ static unsigned pad_for(const void* kernel, unsigned floor_bytes) {
   return a.sharedSizeBytes >= floor_bytes ? 0u : floor_bytes - (unsigned)a.sharedSizeBytes;
 }
 
-extern "C" int pcst_knn_set_build_lds_pad(int64_t bytes) {
-  PCST_CHECK_ARG(bytes >= 0 && bytes <= 98304, "knn_set_build_lds_pad: 0..98304 bytes");
-  const unsigned f = (unsigned)bytes;
-  g_pad_pre = pad_for((const void*)knn_pre_kernel, f);
-  g_pad_count = pad_for((const void*)knn_count_kernel, f);
-  g_pad_scan = pad_for((const void*)knn_scan_kernel, f);
-  g_pad_fill = pad_for((const void*)knn_fill_kernel, f);
-  return PCST_OK;
-}
-
 // Phase 1 (positions only: the coarse set's points and the full cloud): grid statistics, the
 // packed cell counts, scan, fill.  Phase 2 (needs the coarse values, i.e. the noise MLP's
 // output): known rows, the query passes and the outlier pass.  Splitting them lets a caller run
 // phase 1 on a second stream while the MLP runs (guided_sample_loop).
 extern "C" int pcst_knn3_build(const float* orig, const int64_t* idx, int64_t B, int64_t N,
-                               int64_t M, void* workspace, void* stream) {
+                               int64_t M, int64_t lds_floor, void* workspace, void* stream) {
   PCST_CHECK_ARG(B >= 0 && N > 0 && M > 0 && N < (1ll << 31) && M < (1ll << 27) &&
                      M + N < (1ll << 31),
                  "knn3_build: bad shape");
+  PCST_CHECK_ARG(lds_floor >= 0 && lds_floor <= 98304, "knn3_build: lds_floor is 0..98304 bytes");
   if (B == 0) return PCST_OK;
   PCST_CHECK_ARG(orig && idx && workspace, "knn3_build: null pointer");
   hipStream_t s = as_stream(stream);
   KnnWS w = carve_knn(workspace, B, N, M);
   const int b = (int)B;
-  const unsigned pad_pre = g_pad_pre, pad_count = g_pad_count, pad_scan = g_pad_scan,
-                 pad_fill = g_pad_fill;
+  const unsigned f = (unsigned)lds_floor;
+  const unsigned pad_pre = pad_for((const void*)knn_pre_kernel, f),
+                 pad_count = pad_for((const void*)knn_count_kernel, f),
+                 pad_scan = pad_for((const void*)knn_scan_kernel, f),
+                 pad_fill = pad_for((const void*)knn_fill_kernel, f);
   // error word, counters, known rows, tile sums and packed counts are contiguous in the carve
   PCST_HIP(hipMemsetAsync(w.err, 0, (size_t)(w.bytes - ((char*)w.err - (char*)workspace)), s),
            "knn: memset");
@@ -1279,13 +1272,11 @@ extern "C" int pcst_knn3_build(const float* orig, const int64_t* idx, int64_t B,
   return PCST_OK;
 }
 
-static int outlier_mode() {
-  static const int m = [] {
-    const char* e = getenv("PCST_KNN_OUTLIER");
-    return e ? atoi(e) : 1;
-  }();
-  return m;
-}
+// PCST_X_KNN_OUTLIER_EXHAUSTIVE (experiment builds, Makefile XDEF): the exhaustive outlier pass
+// instead of the brick-shell search (A/B only)
+#ifndef PCST_X_KNN_OUTLIER_EXHAUSTIVE
+#define PCST_X_KNN_OUTLIER_EXHAUSTIVE 0
+#endif
 
 extern "C" int pcst_knn3_query(const float* coarse, const float* orig, int64_t B, int64_t N,
                                int64_t M, float* out, void* workspace, void* stream) {
@@ -1302,7 +1293,7 @@ extern "C" int pcst_knn3_query(const float* coarse, const float* orig, int64_t B
   auto qk = M >= 3 ? knn_query_kernel<3> : (M == 2 ? knn_query_kernel<2> : knn_query_kernel<1>);
   hipLaunchKernelGGL(qk, dim3(gq, b), dim3(256), 0, s, orig, coarse, N, M, w.Cpad, w.gp, w.cnt,
                      w.refs, w.qorder, w.chunks, w.maxch, w.nchunk, w.olist, w.obound, w.ocount, out);
-  if (outlier_mode() == 0) {  // PCST_KNN_OUTLIER=0: the exhaustive pass (A/B experiments)
+  if (PCST_X_KNN_OUTLIER_EXHAUSTIVE) {  // the exhaustive pass (A/B experiments)
     auto ok = M >= 3 ? knn_outlier_kernel<3>
                      : (M == 2 ? knn_outlier_kernel<2> : knn_outlier_kernel<1>);
     hipLaunchKernelGGL(ok, dim3(kOutlierBlocks, b), dim3(kOutlierThreads), 0, s, coarse, N, M, orig,
@@ -1320,7 +1311,7 @@ extern "C" int pcst_knn3_query(const float* coarse, const float* orig, int64_t B
 extern "C" int pcst_knn3_interp(const float* coarse, const float* orig, const int64_t* idx,
                                 int64_t B, int64_t N, int64_t M, float* out, void* workspace,
                                 void* stream) {
-  int rc = pcst_knn3_build(orig, idx, B, N, M, workspace, stream);
+  int rc = pcst_knn3_build(orig, idx, B, N, M, 0, workspace, stream);
   if (rc) return rc;
   return pcst_knn3_query(coarse, orig, B, N, M, out, workspace, stream);
 }

@@ -962,14 +962,13 @@ static void launch_gemm_dma(int ep, int stages, const void* A, int64_t M, int64_
 }
 #undef PCST_GEMM_DMA
 
-// bf16 kernel choice (experiment knob PCST_GEMM_KERNEL: 0 register-staged, 3/4 LDS-DMA stages)
-static int gemm_kernel_choice() {
-  static const int v = [] {
-    const char* e = getenv("PCST_GEMM_KERNEL");
-    return e ? atoi(e) : 0;  // measured: register staging 140 us vs DMA 146 (3) / 173 (4), K=256
-  }();
-  return v;
-}
+// bf16 kernel choice (experiment builds: XDEF=-DPCST_X_GEMM_KERNEL=3|4 selects the LDS-DMA
+// kernel with that many stages; 0 = register staging, measured 140 us vs DMA 146 (3) / 173 (4)
+// at K = 256)
+#ifndef PCST_X_GEMM_KERNEL
+#define PCST_X_GEMM_KERNEL 0
+#endif
+static constexpr int gemm_kernel_choice() { return PCST_X_GEMM_KERNEL; }
 
 static void launch_gemm_bf(int ep, bool fast, const void* A, int64_t M, int64_t K, const void* B,
                            int64_t O, int tiles_o, int ntiles, int per, const GemmExArgs& args,

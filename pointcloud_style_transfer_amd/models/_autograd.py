@@ -149,14 +149,17 @@ class NoisePredictorFn(torch.autograd.Function):
       out = q1 Wo4^T + bo4                 [M,3]    fp32
 
     Inputs: pts [B,N,3], cond [B,2,256] = (time_proj(temb), style_proj(style)) -- the small
-    per-cloud projections stay in autograd -- and the network's 34 weights.  Each ReLU backward
+    per-cloud projections stay in autograd --, ps = the six residual blocks' dropout rates (each
+    block its own, as nn.Dropout per layer does), and the network's 36 weights and biases.  Each ReLU backward
     is fused into the dX product that produces its gradient (EP_RELU_MASK on the layer's own
     bf16 output), so no [M,*] elementwise kernel runs outside the GEMMs except the per-cloud
     column sums of dL/dx for cond's gradient."""
 
     @staticmethod
-    def forward(ctx, pts, cond, p, *w):
+    def forward(ctx, pts, cond, ps, *w):
         B, N, _ = pts.shape
+        if len(ps) != 6:
+            raise ValueError(f"NoisePredictorFn: 6 dropout rates expected, got {len(ps)}")
         M = B * N
         dev = pts.device
         xp = torch.zeros(M, 8, dtype=torch.float32, device=dev)
@@ -172,17 +175,17 @@ class NoisePredictorFn(torch.autograd.Function):
         saved, seeds = [xp, h0, h1], []
         for k in range(6):
             o = 6 + 4 * k
-            seed = _draw_seed(p)
+            seed = _draw_seed(ps[k])
             seeds.append(seed)
             saved.append(xb)
-            x, xb, h = _block_fwd(x, xb, wb[o], wb[o + 1], wb[o + 2], wb[o + 3], p, seed)
+            x, xb, h = _block_fwd(x, xb, wb[o], wb[o + 1], wb[o + 2], wb[o + 3], ps[k], seed)
             saved.append(h)
         q0 = _hip.gemm_ex(xb, wb[30], wb[31], relu=True, epilogue=_hip.EP_BF16)
         q1 = _hip.gemm_ex(q0, wb[32], wb[33], relu=True, epilogue=_hip.EP_BF16)
         out = _hip.gemm_ex(q1, wb[34], wb[35], epilogue=_hip.EP_F32)
         saved += [xb, q0, q1]
         ctx.save_for_backward(*saved, *w)
-        ctx.seeds, ctx.p, ctx.BN = seeds, p, (B, N)
+        ctx.seeds, ctx.ps, ctx.BN = seeds, tuple(ps), (B, N)
         return out.view(B, N, 3)
 
     @staticmethod
@@ -212,7 +215,7 @@ class NoisePredictorFn(torch.autograd.Function):
             o = 6 + 4 * k
             xbk, hk = blocks[k]
             g, grads[o], grads[o + 1], grads[o + 2], grads[o + 3] = _block_bwd(
-                g, xbk, hk, _bf16_t(w[o]), _bf16_t(w[o + 2]), ctx.p, ctx.seeds[k])
+                g, xbk, hk, _bf16_t(w[o]), _bf16_t(w[o + 2]), ctx.ps[k], ctx.seeds[k])
         # x = ((pf + tf) + sf): dL/dpf = g, dL/dtf[b] = dL/dsf[b] = sum of g over cloud b's rows
         # per-cloud row sums as one batched GEMV (ones [B,1,N] @ g [B,N,256]): torch's
         # middle-dimension sum reduced this at ~40 % of the HBM rate (254 vs 82 us at B = 8)
@@ -264,16 +267,21 @@ class BNReLUFn(torch.autograd.Function):
 
 
 def bn_relu(z, bn, pool_ns=0):
-    """Train-mode `bn` (BatchNorm2d) + ReLU (+ max-pool) on the HIP kernels."""
+    """Train-mode `bn` (BatchNorm2d) + ReLU (+ max-pool) on the HIP kernels.  The reference's
+    layers use the default momentum 0.1 (pointnet2_encoder.py:75-78); momentum=None (cumulative
+    average, factor 1/num_batches_tracked) reads the counter on the host -- off the fast path.
+    The counter is bumped after the forward is queued, so a failing call leaves it and the
+    running statistics consistent."""
     momentum = bn.momentum
-    if bn.track_running_stats:
-        bn.num_batches_tracked.add_(1)
-        if momentum is None:  # cumulative moving average
-            momentum = 1.0 / float(bn.num_batches_tracked.item())
+    if bn.track_running_stats and momentum is None:
+        momentum = 1.0 / (float(bn.num_batches_tracked.item()) + 1.0)
     rm = bn.running_mean if bn.track_running_stats else None
     rv = bn.running_var if bn.track_running_stats else None
-    return BNReLUFn.apply(z, bn.weight, bn.bias, rm, rv, bn.eps,
-                          0.0 if momentum is None else momentum, pool_ns)
+    y = BNReLUFn.apply(z, bn.weight, bn.bias, rm, rv, bn.eps,
+                       0.0 if momentum is None else momentum, pool_ns)
+    if bn.track_running_stats:
+        bn.num_batches_tracked.add_(1)
+    return y
 
 
 class GroupGatherFn(torch.autograd.Function):

@@ -16,7 +16,6 @@ from __future__ import annotations
 
 import contextlib
 import math
-import os
 from typing import Dict, Optional, Tuple
 
 import numpy as np
@@ -98,15 +97,16 @@ class NoisePredictor(nn.Module):
         self._pack_key = None
         self._packed = None
 
+    # ABI precision code of the "bf16" mode: the 16x16x32 pair kernel (PAIR16).  tools/ may set
+    # it to packing.BF16 (the 32x32x16 pair kernel: same arithmetic, other MFMA shape) for A/B
+    # timing; the product never changes it.
+    bf16_code = packing.PAIR16
+
     @property
     def precision_code(self) -> int:
-        """ABI precision code: "bf16" runs the 16x16x32 pair kernel (PAIR16), "fp32" the
-        exact-f32 parity kernel.  PCST_NM_BF16_KERNEL=1 selects the 32x32x16 pair kernel
-        (same arithmetic, other MFMA shape; A/B timing)."""
+        """ABI precision code: "bf16" runs `bf16_code`, "fp32" the exact-f32 parity kernel."""
         p = getattr(self.config, "precision", "fp32")
-        if p != "bf16":
-            return packing.F32
-        return packing.BF16 if os.environ.get("PCST_NM_BF16_KERNEL") == "1" else packing.PAIR16
+        return self.bf16_code if p == "bf16" else packing.F32
 
     def packed(self):
         """Packed MFMA weight stream + bias table, rebuilt when any weight changes."""
@@ -152,10 +152,11 @@ class NoisePredictor(nn.Module):
         tf = _ag.linear(self.time_embedding(timestep.to(noisy_points.device)), self.time_proj)
         sf = _ag.linear(style_feat, self.style_proj)
         if noisy_points.is_cuda and torch.is_autocast_enabled("cuda"):
-            # the whole per-point network on the bf16-storage fused GEMMs (NoisePredictorFn)
-            p = float(self.layers[0][3].p) if self.training else 0.0
+            # the whole per-point network on the bf16-storage fused GEMMs (NoisePredictorFn);
+            # each residual block keeps its own Dropout rate
+            ps = tuple(float(l[3].p) if self.training else 0.0 for l in self.layers)
             cond = torch.stack([tf.float(), sf.float()], 1)
-            return _ag.NoisePredictorFn.apply(noisy_points.float(), cond, p,
+            return _ag.NoisePredictorFn.apply(noisy_points.float(), cond, ps,
                                               *self._fused_params())
         h = _ag.linear(noisy_points, pe[0], True)
         h = _ag.linear(h, pe[2], True)
@@ -231,26 +232,25 @@ class HierarchicalProcessor:
 # The kNN upsample's build phase (grid, counts, sort: positions only) does not depend on the
 # noise MLP's output, so the sampling loop runs it on a side stream during the MLP.  The loop
 # itself moves to a high-priority stream and the build's workgroups carry extra LDS
-# (pcst_knn_set_build_lds_pad), so they cannot co-reside with an MLP workgroup and only take
+# (pcst_knn3_build's lds_floor), so they cannot co-reside with an MLP workgroup and only take
 # the CUs the MLP leaves idle in its last partial round (469 workgroups on 256 CUs).  Measured
 # 0.493 -> 0.468 ms/step over the first 20 steps, 0.421 -> 0.408 over 300
-# (tools/overlap_probe.py, one cloud); results are bit-identical.  PCST_KNN_OVERLAP=0 turns it
-# off.
+# (tools/overlap_probe.py, one cloud); results are bit-identical.  These module constants are
+# the design's fixed choices; tools/knobs.py overrides them for A/B runs only.
 # Only small batches leave idle CUs in the MLP's last round: with many rounds (e.g. 32 clouds per
 # GPU, 15000 MLP work-groups) the padded build only runs after the MLP, slower than inline
 # (9.6 -> 10.4 ms per 32-cloud step), so the overlap applies up to two MLP rounds of points.
-_OVERLAP_KNN_BUILD = os.environ.get("PCST_KNN_OVERLAP", "1") != "0"
+OVERLAP_KNN_BUILD = True
 _OVERLAP_MAX_MLP_POINTS = 2 * 128 * 256
-# LDS floor of the build's work-groups (pcst_knn_set_build_lds_pad): just above what an MLP
+# LDS floor of the build's work-groups (pcst_knn3_build's lds_floor): just above what an MLP
 # work-group leaves free on its CU (160 - 154.6 KiB), so the build never co-resides with the MLP
 # but packs as many work-groups per idle CU as their own LDS allows (round 2 used a flat 64 KiB
-# pad on every build kernel: 1-2 work-groups per idle CU).  PCST_KNN_BUILD_LDS_FLOOR overrides
-# (A/B runs).
-_KNN_BUILD_LDS_PAD = int(os.environ.get("PCST_KNN_BUILD_LDS_FLOOR", "8192"))
+# pad on every build kernel: 1-2 work-groups per idle CU).
+KNN_BUILD_LDS_FLOOR = 8192
 
 
 def overlap_knn_build(mlp_points: int) -> bool:
-    return _OVERLAP_KNN_BUILD and mlp_points <= _OVERLAP_MAX_MLP_POINTS
+    return OVERLAP_KNN_BUILD and mlp_points <= _OVERLAP_MAX_MLP_POINTS
 _STEP_STREAMS: Dict[int, Tuple[torch.cuda.Stream, torch.cuda.Stream]] = {}
 
 
@@ -267,7 +267,8 @@ def step_streams(device) -> Tuple[torch.cuda.Stream, torch.cuda.Stream]:
 def hierarchical_eps(hp, mlp, xc, xi, x_cat, knn_ws=None, side=None):
     """eps for the CFG batch: mlp(xc) on the current stream, upsampled to the full clouds by
     kNN-3 (HierarchicalProcessor.upsample_knn).  With a side stream (and a preallocated
-    workspace) the kNN build runs there, overlapping the MLP; the query waits for it."""
+    workspace) the kNN build runs there, overlapping the MLP, with its work-groups held to an
+    LDS floor of KNN_BUILD_LDS_FLOOR bytes; the query waits for it."""
     if side is None:
         return hp.upsample_knn(mlp(xc), x_cat, xi)
     main = torch.cuda.current_stream()
@@ -275,7 +276,7 @@ def hierarchical_eps(hp, mlp, xc, xi, x_cat, knn_ws=None, side=None):
     ready.record(main)
     ready.wait(side)
     with torch.cuda.stream(side):
-        handle = _hip.knn3_build(x_cat, xi, knn_ws)
+        handle = _hip.knn3_build(x_cat, xi, knn_ws, KNN_BUILD_LDS_FLOOR)
         built.record(side)
     nc = mlp(xc)
     built.wait(main)
@@ -283,11 +284,12 @@ def hierarchical_eps(hp, mlp, xc, xi, x_cat, knn_ws=None, side=None):
 
 
 _STEP_EVENTS: Dict[int, tuple] = {}
-_DEVICE_EVENTS = os.environ.get("PCST_DEVICE_EVENTS", "1") != "0"
+# device-scope events for the step's cross-stream dependencies (tools/knobs.py: A/B only)
+DEVICE_EVENTS = True
 
 
 class _TorchEvent:
-    """torch.cuda.Event with the DeviceEvent interface (PCST_DEVICE_EVENTS=0: A/B runs)."""
+    """torch.cuda.Event with the DeviceEvent interface (DEVICE_EVENTS = False: A/B runs)."""
 
     def __init__(self):
         self.e = torch.cuda.Event()
@@ -304,7 +306,7 @@ def _step_events(device):
     the event's state when it is enqueued)."""
     key = torch.device(device).index or 0
     if key not in _STEP_EVENTS:
-        mk = _hip.DeviceEvent if _DEVICE_EVENTS else _TorchEvent
+        mk = _hip.DeviceEvent if DEVICE_EVENTS else _TorchEvent
         _STEP_EVENTS[key] = (mk(), mk())
     return _STEP_EVENTS[key]
 
@@ -444,7 +446,6 @@ class DiffusionProcess:
         with ctx:
             if overlap:
                 ws = _hip.knn_workspace(2 * B, shape[1], model.config.global_points, device=device)
-                _hip.knn_set_build_lds_pad(_KNN_BUILD_LDS_PAD)
             try:
                 for i, t in enumerate(timesteps):
                     t_in = t_rows[i]
@@ -462,10 +463,10 @@ class DiffusionProcess:
                     x = _hip.cfg_ddim_step(x, eps[:B], eps[B:], source, guidance_scale,
                                            self._coeffs(t, t_prev), x_cat=x_cat)
             finally:
+                # also when a step raises: tensors the caller frees must not be reused while
+                # loop-stream and side-stream kernels still run
                 if overlap:
-                    _hip.knn_set_build_lds_pad(0)
-        if overlap:
-            caller.wait_stream(loop)
+                    caller.wait_stream(loop)
         return x
 
     def _guided_sample_graph(self, model, source_points, condition_points, num_inference_steps,

@@ -8,6 +8,9 @@ Differences from the reference, all deliberate:
     GPU, or `--device cpu`, raises instead of silently switching device (the reference
     falls back to the CPU at `:65`; BASELINE configs[0] is that CPU plumbing run, which this
     build serves on the GPU instead).
+Keyword-only addition: `precision=` on DiffusionInference and the `--precision {fp32,bf16}`
+flag (default "fp32", the checkpoint's parity mode; "bf16" runs the noise MLP on the bf16 MFMA
+kernel -- the mode bench.py measures).
 Kept quirks: EMA weights are copied into the trainable parameters only and the BN buffers
 stay at their init values (Q9, `:98-113`); `.txt` delimiters differ for source (',') and
 reference (' ') (`:151-152`).
@@ -65,7 +68,9 @@ class PointCloudVisualizer:
 class DiffusionInference:
     """`DiffusionInference` (inference.py:62-171)."""
 
-    def __init__(self, checkpoint_path: str, device: str = "cuda"):
+    def __init__(self, checkpoint_path: str, device: str = "cuda", *, precision: str = None):
+        if precision not in (None, "fp32", "bf16"):
+            raise ValueError(f"precision must be 'fp32' or 'bf16', got {precision!r}")
         dev = torch.device(device)
         if dev.type != "cuda":
             raise RuntimeError(f"DiffusionInference runs on the MI355X HIP path only; device "
@@ -78,6 +83,8 @@ class DiffusionInference:
         self.logger = Logger(name="Inference", log_dir="logs/inference",
                              experiment_name=experiment_name, file_output=True)
         self.config, self.model = self.load_model(checkpoint_path)
+        if precision is not None:  # None keeps the checkpoint's (a reference pickle: "fp32")
+            self.config.precision = precision
         self.diffusion_process = DiffusionProcess(self.config, device=str(self.device))
         self.preprocessor = PointCloudPreprocessor(total_points=self.config.total_points,
                                                    global_points=self.config.global_points)
@@ -147,9 +154,12 @@ def main(argv=None):
     p.add_argument("--visualize", action="store_true")
     p.add_argument("--num_steps", type=int, default=50)
     p.add_argument("--guidance_scale", type=float, default=7.5)
+    p.add_argument("--precision", choices=["fp32", "bf16"], default=None,
+                   help="noise-MLP arithmetic: fp32 (exact, the default of a reference "
+                        "checkpoint) or bf16 (the bf16 MFMA kernel bench.py measures)")
     args = p.parse_args(argv)
     try:
-        eng = DiffusionInference(args.checkpoint, args.device)
+        eng = DiffusionInference(args.checkpoint, args.device, precision=args.precision)
         eng.process_file(args.source, args.reference, args.output, args.visualize,
                          args.num_steps, args.guidance_scale)
         print("Inference completed successfully!")

@@ -80,6 +80,18 @@ class CosineWithWarmupLR:
             g["lr"] = base * scale
 
 
+def keep_fused(optimizer, state_dict):
+    """load_state_dict pre-hook of the fused AdamW: Optimizer.load_state_dict replaces the
+    param groups with the saved ones, and a checkpoint written by the reference (or by a
+    non-fused optimizer) carries fused=None.  The optimizer would then step with the foreach
+    kernel while GradScaler, seeing a fused optimizer, hands it found_inf -- which that kernel
+    rejects.  Keep the groups fused; `step` is then loaded onto the device as float32 (torch's
+    rule for fused state)."""
+    sd = dict(state_dict)
+    sd["param_groups"] = [dict(g, fused=True, foreach=None) for g in state_dict["param_groups"]]
+    return sd
+
+
 def _progress(it, desc):
     try:
         from tqdm import tqdm
@@ -105,9 +117,12 @@ class DiffusionTrainer:
         self.loss_fn = DiffusionLoss(noise_weight=1.0, chamfer_weight=config.lambda_chamfer)
         # fused AdamW on the GPU: one kernel for all parameters, and GradScaler hands it
         # found_inf on the device instead of synchronising on it (torch's amp-scaling protocol)
+        fused = self.device_type == "cuda"
         self.optimizer = optim.AdamW(self.model.parameters(), lr=config.learning_rate,
                                      weight_decay=config.weight_decay, betas=(0.9, 0.95),
-                                     fused=self.device_type == "cuda")
+                                     fused=fused)
+        if fused:
+            self.optimizer.register_load_state_dict_pre_hook(keep_fused)
         if config.lr_scheduler == "cosine_with_warmup":
             self.scheduler = CosineWithWarmupLR(self.optimizer, config.warmup_epochs,
                                                 config.num_epochs, config.min_lr_ratio)

@@ -1,13 +1,16 @@
 """Worker of tests/test_gpu_ddp.py (not a test module): one DiffusionTrainer process.
 
-    python tests/ddp_worker.py OUT.npz ACCUM MICRO_BATCHES_PER_RANK CLOUDS_PER_MICRO POINTS
+    python tests/ddp_worker.py OUT.npz ACCUM MICRO_BATCHES_PER_RANK CLOUDS_PER_MICRO POINTS \
+        [AMP GLOBAL_POINTS]
 
 Under torch.distributed (RANK / WORLD_SIZE in the environment, gloo backend, every rank on
 cuda:0) the trainer wraps the model in DDP; without it the same code is the single-process
 reference.  Global micro-batch g (rank r, local step b: g = r * MICRO + b) trains on clouds
 [g * CLOUDS, (g + 1) * CLOUDS) with the draws of rng.CounterRNG(100 + g), so both set-ups see
 the same samples and the same t / noise / cond-drop / voxel / FPS draws.  The gradient each
-optimizer step applies (after clipping) and the parameters after the step are saved.
+optimizer step applies (after clipping) and the parameters after the step are saved (every
+rank's parameters: OUT.rankR.npz for R > 0).  AMP=1 runs the trainer under use_amp (the bf16
+fused NoisePredictor and GEMMs) with the GradScaler disabled, so gradients compare unscaled.
 """
 import os
 import sys
@@ -21,6 +24,8 @@ sys.path.insert(0, REPO)
 
 def main():
     out, accum, micro, clouds, points = sys.argv[1], *map(int, sys.argv[2:6])
+    amp = len(sys.argv) > 6 and sys.argv[6] == "1"
+    global_points = int(sys.argv[7]) if len(sys.argv) > 7 else 2048
     from pointcloud_style_transfer_amd import distributed as D
     from pointcloud_style_transfer_amd import rng
     from pointcloud_style_transfer_amd.config.config import Config
@@ -31,8 +36,9 @@ def main():
     torch.cuda.set_device(0)
     tmp = os.path.dirname(os.path.abspath(out))
     os.chdir(tmp)
-    cfg = Config(make_dirs=False, log_dir=tmp, checkpoint_dir=tmp, use_amp=False,
-                 gradient_accumulation_steps=accum, global_points=2048, precision="fp32")
+    cfg = Config(make_dirs=False, log_dir=tmp, checkpoint_dir=tmp, use_amp=amp,
+                 gradient_accumulation_steps=accum, global_points=global_points,
+                 precision="fp32")
     torch.manual_seed(0)
     tr = DiffusionTrainer(cfg, device="cuda:0")
     assert tr.distributed == (world > 1)
@@ -40,6 +46,8 @@ def main():
         if isinstance(m, torch.nn.Dropout):
             m.p = 0.0
     tr.model.train()
+    if amp:
+        tr.scaler = torch.amp.GradScaler(enabled=False)
     grads = {}
     o_step = tr.optimizer.step
 
@@ -59,10 +67,12 @@ def main():
             loss, _ = tr.train_step({"sim_full": sim.cuda(), "real_full": real.cuda()}, b, micro)
         losses.append(float(loss.detach()))
     torch.cuda.synchronize()
+    params = {f"param:{n}": p.detach().cpu().numpy() for n, p in tr.model.named_parameters()}
     if rank == 0:
-        params = {f"param:{n}": p.detach().cpu().numpy() for n, p in tr.model.named_parameters()}
         np.savez(out, losses=np.array(losses), **{f"grad:{k}": v for k, v in grads.items()},
                  **params)
+    else:
+        np.savez(f"{out[:-4]}.rank{rank}.npz", **params)
     if world > 1:
         torch.distributed.barrier()
         torch.distributed.destroy_process_group()

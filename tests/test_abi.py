@@ -54,6 +54,32 @@ def test_ctypes_binding_covers_header(built):
     assert _hip.noise_mlp_blob_bytes(0) == 217 * 32768
 
 
+def test_no_process_global_mutable_state(built):
+    """pcst.h's contract: no global mutable state except the thread-local last-error string,
+    and no environment variables -- every choice a call makes is one of its arguments.  The
+    writable .data/.bss symbols of the library may only be what the toolchain emits (HIP
+    code-object registration handles, CRT init/fini flags); the only TLS is the error string;
+    getenv/setenv are not imported."""
+    out = subprocess.check_output(["objdump", "-t", built], text=True)
+    allowed = re.compile(r"^(__hip_cuid_|__hip_gpubin_handle_|__hip_fatbin_wrapper$|__dso_handle$|"
+                         r"__do_init\.|__do_fini\.|completed\.|_GLOBAL_OFFSET_TABLE_$|__TMC_END__$|"
+                         r"\.(data|bss|tbss)$)")
+    writable, tls = [], []
+    for line in out.splitlines():
+        parts = line.split()
+        if len(parts) < 5 or parts[-3] not in (".data", ".bss", ".tbss", ".tdata"):
+            continue
+        name = parts[-1]
+        if parts[-3] in (".tbss", ".tdata"):
+            tls.append(name)
+        elif not allowed.match(name):
+            writable.append(name)
+    assert not writable, writable
+    assert all(n in (".tbss", ".tdata") or "g_last_error" in n for n in tls), tls
+    undef = subprocess.check_output(["nm", "-D", "--undefined-only", built], text=True)
+    assert not re.search(r"\b(getenv|secure_getenv|setenv|putenv)\b", undef)
+
+
 def test_gfx950_code_object(built):
     out = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-objdump", "--offloading", built],
                          capture_output=True, text=True)

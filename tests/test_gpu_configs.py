@@ -308,13 +308,13 @@ def test_noise_mlp_bf16_per_element_60000(det_state):
 def test_chamfer_vs_oracle_10_steps_120k(det_state):
     """configs[1]'s quality figure at a test-sized schedule: the HIP guided loop (fp32 noise
     MLP) against the oracle loop on one 120k cloud, 10 steps, same x_T and counter-keyed
-    draws.  Per step the two agree to fp32 summation order (1e-4 rel, the teacher-forced
-    tests), but the loop amplifies that: the first update divides by sqrt(a_999) = 3.1e-4 and
-    CFG multiplies eps differences by 7.5, and kNN neighbour sets flip under 1e-6 changes
-    (two runs of the reference itself differ by ~1.4e-3 abs over 50 steps).
-    Measured here: Chamfer 1.5e-4, max abs 2.4e-3, 47 % of the elements within 1e-4 rel.
-    Bounds: Chamfer (metrics.py:20-44) <= 1e-3, every element within 1e-2 abs, >= 99 % within
-    1e-3 abs."""
+    draws, the oracle computed live.  Per step the two agree to fp32 summation order (1e-4
+    rel, the teacher-forced tests); the loop amplifies that.  The 10-step chaos floor (oracle
+    vs itself from x_T moved by 1 ulp, CHAOS_FLOOR_10, profiles/r03/chaos_floor.json) is
+    large -- the first update divides by sqrt(a_999) = 3.1e-4, and a voxel size moved by one
+    ulp re-draws the subset -- so the bounds are fractions of it: Chamfer (metrics.py:20-44)
+    and the 99.9th percentile within 0.25x the floor, the maximum within 0.005x (round 2
+    measured Chamfer 1.5e-4 = 0.13x and max 2.4e-3 = 0.003x)."""
     from detweights import load_into
     from oracle import oracle as O
     from pointcloud_style_transfer_amd import rng
@@ -372,6 +372,57 @@ def test_chamfer_vs_oracle_10_steps_120k(det_state):
     print(f"10-step 120k fp32: chamfer_vs_ref {ch:.3e}, within 1e-4 rel {within:.6f}, "
           f"within 1e-3 abs {w3:.6f}, median abs {d.median().item():.3e}, "
           f"max abs {d.max().item():.3e}")
-    assert ch <= 1e-3
-    assert d.max().item() <= 1e-2
+    p999 = float(torch.quantile(d.flatten().double(), 0.999))
+    print(f"  vs the 10-step floor: chamfer {ch / CHAOS_FLOOR_10['chamfer']:.3f} x, p999 "
+          f"{p999 / CHAOS_FLOOR_10['p999_abs']:.3f} x, max "
+          f"{d.max().item() / CHAOS_FLOOR_10['max_abs']:.4f} x")
+    assert ch <= 0.25 * CHAOS_FLOOR_10["chamfer"]
+    assert p999 <= 0.25 * CHAOS_FLOOR_10["p999_abs"]
+    assert d.max().item() <= 0.005 * CHAOS_FLOOR_10["max_abs"]
     assert w3 >= 0.99
+
+
+# The loop's own chaos floor (tools/chaos_floor.py -> profiles/r03/chaos_floor.json): the oracle
+# loop against itself from x_T moved by one ulp per element, same cloud / weights / draws as
+# below, 50-step schedule.  tests/test_host.py checks these constants against the JSON.
+CHAOS_FLOOR_50 = {"chamfer": 1.0649e-4, "p999_abs": 9.448e-4, "max_abs": 9.332e-3}
+CHAOS_FLOOR_10 = {"chamfer": 1.1634e-3, "p999_abs": 1.8010e-2, "max_abs": 7.4255e-1}
+
+
+@pytest.mark.parametrize("precision,mult", [("fp32", 1.0), ("bf16", 3.0)])
+def test_loop_vs_oracle_50_steps_120k(det_state, golden, precision, mult):
+    """BASELINE configs[1]'s quality gate ("Chamfer vs ref"), for the mode bench.py measures
+    (bf16 noise MLP) and the parity mode (fp32): the HIP guided loop on the 120k lidar-like
+    cloud, 50 steps, guidance 7.5, the same x_T and counter-keyed draws as the committed oracle
+    output (tests/golden/gen_oracle_loop.py).  Bounds are a stated multiple of the chaos floor
+    -- what a 1-ulp change of x_T does to the oracle itself over the same loop: fp32 within
+    1x the floor, bf16 within 3x, for the metrics.py:20-44 Chamfer, the 99.9th percentile
+    and the maximum of |hip - oracle|."""
+    from detweights import load_into
+    from pointcloud_style_transfer_amd import rng
+    from pointcloud_style_transfer_amd.config.config import Config
+    from pointcloud_style_transfer_amd.evaluation.metrics import PointCloudMetrics
+    from pointcloud_style_transfer_amd.models.diffusion_model import (DiffusionProcess,
+                                                                        PointCloudDiffusionModel)
+    from pointcloud_style_transfer_amd.synthetic import standard_normal
+
+    ref = torch.from_numpy(golden("oracle_loop120k.npz")["x_50"]).cuda()
+    cfg = Config(make_dirs=False, precision=precision)
+    model = PointCloudDiffusionModel(cfg)
+    load_into(model)
+    model = model.cuda().eval()
+    dp = DiffusionProcess(cfg, device="cuda")
+    src, cond = _clouds(1000, 1, 120000).cuda(), _clouds(2000, 1, 120000).cuda()
+    xT = torch.from_numpy(standard_normal(3000, (1, 120000, 3))).cuda()
+    with rng.replay(rng.CounterRNG(6000)):
+        out = dp.guided_sample_loop(model, src, cond, 50, 7.5, x_T=xT)
+    ch = float(PointCloudMetrics().chamfer_distance(out, ref)[0])
+    d = (out - ref).abs().flatten().double()
+    p999 = float(torch.quantile(d, 0.999))
+    mx = float(d.max())
+    print(f"50-step 120k {precision}: chamfer_vs_oracle {ch:.3e} ({ch / CHAOS_FLOOR_50['chamfer']:.2f}"
+          f" x floor), p999 {p999:.3e} ({p999 / CHAOS_FLOOR_50['p999_abs']:.2f} x), max {mx:.3e} "
+          f"({mx / CHAOS_FLOOR_50['max_abs']:.2f} x), within 1e-3 abs {(d <= 1e-3).double().mean():.6f}")
+    assert ch <= mult * CHAOS_FLOOR_50["chamfer"]
+    assert p999 <= mult * CHAOS_FLOOR_50["p999_abs"]
+    assert mx <= mult * CHAOS_FLOOR_50["max_abs"]

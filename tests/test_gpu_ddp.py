@@ -27,7 +27,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _run(tmp, tag, world, accum, micro, clouds=2, points=8192):
+def _run(tmp, tag, world, accum, micro, clouds=2, points=8192, amp=False, global_points=2048):
     out = os.path.join(tmp, f"{tag}.npz")
     port = _free_port()
     procs = []
@@ -40,15 +40,16 @@ def _run(tmp, tag, world, accum, micro, clouds=2, points=8192):
             for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE"):
                 env.pop(k, None)
         procs.append(subprocess.Popen(
-            [sys.executable, WORKER, out, str(accum), str(micro), str(clouds), str(points)],
+            [sys.executable, WORKER, out, str(accum), str(micro), str(clouds), str(points),
+             "1" if amp else "0", str(global_points)],
             env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT))
     return procs, out
 
 
-def _wait(procs):
+def _wait(procs, timeout=100):
     logs = []
     for p in procs:
-        o, _ = p.communicate(timeout=100)
+        o, _ = p.communicate(timeout=timeout)
         logs.append(o.decode(errors="replace")[-3000:])
     for p, lg in zip(procs, logs):
         assert p.returncode == 0, lg
@@ -85,3 +86,41 @@ def test_ddp_gradient_equals_accumulation(tmp_path, accum):
     for k in zd.files:
         if k.startswith("param:"):
             np.testing.assert_allclose(zd[k], zo[k], rtol=0, atol=1e-6 if accum > 1 else 0)
+
+
+def test_ddp_configs3_per_rank_size_amp(tmp_path):
+    """BASELINE configs[3] at its per-rank size: 8 x 120000-point clouds per rank, use_amp (the
+    bf16 fused NoisePredictor, bf16 GEMMs; GradScaler disabled so the gradients compare
+    unscaled), the real 2,549,827-gradient (10.2 MB) bucketed all-reduce through DDP's reducer.
+    World 2 x 1 micro-batch against one process accumulating the same 2 micro-batches
+    (trainer.py:115-125; counter-keyed draws, dropout off).  Each rank's gradient is its
+    micro-batch gradient (loss / 1), DDP averages the two; the single process adds the two
+    micro-batch gradients of loss / 2: (a + b) / 2 vs a / 2 + b / 2, equal in fp32 (halving is
+    exact), so the bound is the accum-2 summation-order bound 4e-7 max|g| and the measured
+    difference is expected to be 0.  Every rank's post-step parameters must be identical."""
+    tmp = str(tmp_path)
+    kw = dict(clouds=8, points=120000, amp=True, global_points=30000)
+    ddp, out_ddp = _run(tmp, "ddp", 2, 1, 1, **kw)
+    _wait(ddp, timeout=400)
+    one, out_one = _run(tmp, "one", 1, 2, 2, **kw)
+    _wait(one, timeout=400)
+    zd, zo = np.load(out_ddp), np.load(out_one)
+    z1 = np.load(out_ddp[:-4] + ".rank1.npz")
+    gd, go = _grads(zd), _grads(zo)
+    assert gd.keys() == go.keys() and len(gd) == 80
+    assert sum(v.size for v in gd.values()) == 2549827
+    bad, exact = [], 0
+    for n in gd:
+        a, b = gd[n].astype(np.float64), go[n].astype(np.float64)
+        assert np.isfinite(a).all() and np.abs(b).max() > 0, n
+        scale = np.abs(b).max()
+        err = np.abs(a - b).max()
+        exact += int(err == 0)
+        if err > 4e-7 * scale + 1e-30:
+            bad.append(f"{n}: max|ddp - accum| {err:.3e} (max|g| {scale:.3e})")
+    print(f"configs[3] per-rank size: {exact}/80 gradients bit-identical")
+    assert not bad, "\n".join(bad[:20])
+    for k in zd.files:
+        if k.startswith("param:"):
+            np.testing.assert_array_equal(zd[k], z1[k])          # ranks identical
+            np.testing.assert_allclose(zd[k], zo[k], rtol=0, atol=1e-6)

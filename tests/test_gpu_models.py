@@ -196,11 +196,7 @@ def test_chamfer_rowmin_exact_vs_oracle(N, M, mode):
     if M > 8:
         q[:, M // 2:M // 2 + 4] = q[:, 1:5]      # duplicates at later indices
         p[:, :min(N, M) // 3] = q[:, :min(N, M) // 3]  # exact hits: raw D may round below 0
-    _hip.chamfer_set_mode(mode)
-    try:
-        out, a1, a2 = _hip.chamfer_fwd(dev(p), dev(q))
-    finally:
-        _hip.chamfer_set_mode(0)
+    out, a1, a2 = _hip.chamfer_fwd(dev(p), dev(q), mode)
     a1, a2 = a1.cpu().numpy(), a2.cpu().numpy()
     ref = []
     for b in range(2):
@@ -238,14 +234,10 @@ def test_chamfer_grid_equals_exhaustive_30k(kind):
         q = base[:, rng.integers(0, 600, M)]
     res = {}
     for mode in (1, 2):
-        _hip.chamfer_set_mode(mode)
-        try:
-            P, Q = dev(p), dev(q)
-            out, a1, a2 = _hip.chamfer_fwd(P, Q)
-            torch.cuda.synchronize()
-            res[mode] = (out.cpu().numpy(), a1.cpu().numpy(), a2.cpu().numpy())
-        finally:
-            _hip.chamfer_set_mode(0)
+        P, Q = dev(p), dev(q)
+        out, a1, a2 = _hip.chamfer_fwd(P, Q, mode)
+        torch.cuda.synchronize()
+        res[mode] = (out.cpu().numpy(), a1.cpu().numpy(), a2.cpu().numpy())
     for x, y in zip(res[1], res[2]):
         np.testing.assert_array_equal(x, y)
 

@@ -154,3 +154,88 @@ def test_guided_sample_graph_matches_eager(B):
         torch.manual_seed(7)
         outs.append(dp.guided_sample_loop(model, src, cond, num_inference_steps=2, graph=graph))
     assert torch.equal(outs[0], outs[1]), (outs[1] - outs[0]).abs().max().item()
+
+
+def test_inference_entry_point_bf16(golden, tmp_path, monkeypatch):
+    """`scripts/inference.py --precision bf16` reaches the measured mode: the noise MLP runs
+    the bf16 pair kernel (precision code 2) on every step, and the result stays within the
+    bf16 mode's distance of the fp32 run (same draws)."""
+    from detweights import load_into
+    from pointcloud_style_transfer_amd import _hip, packing, rng
+    from pointcloud_style_transfer_amd.config.config import Config
+    from pointcloud_style_transfer_amd.models.diffusion_model import PointCloudDiffusionModel
+    from pointcloud_style_transfer_amd.scripts import inference as inf
+    from pointcloud_style_transfer_amd.utils.checkpoint import CheckpointManager
+    from pointcloud_style_transfer_amd.utils.ema import ExponentialMovingAverage
+
+    monkeypatch.chdir(tmp_path)
+    g = golden("inference_cfg1.npz")
+    cfg = Config(experiment_name="cfg1")   # precision left at its default (fp32)
+    m = PointCloudDiffusionModel(cfg)
+    load_into(m)
+    CheckpointManager(cfg.checkpoint_dir, cfg.experiment_name).save(
+        m, torch.optim.AdamW(m.parameters(), lr=1e-4),
+        ExponentialMovingAverage(m.parameters(), decay=0.999), epoch=0)
+    np.save("src.npy", g["src"])
+    np.save("ref.npy", g["ref"])
+    ck = os.path.join(cfg.checkpoint_dir, "cfg1", "ckpt_epoch_0000.pth")
+    codes = []
+    orig = _hip.noise_mlp
+
+    def spy(*a, **k):
+        codes.append(a[5] if len(a) > 5 else k.get("precision"))
+        return orig(*a, **k)
+
+    monkeypatch.setattr(_hip, "noise_mlp", spy)
+    outs = {}
+    for prec in ("fp32", "bf16"):
+        codes.clear()
+        with rng.replay(rng.ReplayRNG.from_npz(g, "rng")):
+            inf.main(["--checkpoint", ck, "--source", "src.npy", "--reference", "ref.npy",
+                      "--output", f"out/{prec}.npy", "--num_steps", "10", "--precision", prec])
+        assert len(codes) == 10, codes
+        assert set(codes) == {packing.F32 if prec == "fp32" else packing.PAIR16}, codes
+        outs[prec] = np.load(f"out/{prec}.npy")
+    # 2048-point clouds (no hierarchy), 10 steps, outputs denormalised (x25): bf16 moves the
+    # trajectory by well under the cloud's point spacing
+    d = np.abs(outs["bf16"] - outs["fp32"])
+    print(f"entry point bf16 vs fp32: mean {d.mean():.3e}, p99 {np.quantile(d, 0.99):.3e}, "
+          f"max {d.max():.3e} (cloud extent {np.ptp(outs['fp32'], 0)})")
+    assert d.mean() <= 2e-2 and np.quantile(d, 0.99) <= 0.25, (d.mean(), d.max())
+
+
+def test_trainer_resumes_reference_checkpoint_under_amp(tmp_path, monkeypatch):
+    """DiffusionTrainer.train() loads the latest checkpoint into its fused
+    AdamW; a checkpoint whose optimizer state came from a non-fused AdamW (the reference's)
+    must resume and take a use_amp step with the GradScaler enabled (found_inf handed to the
+    fused kernel on the device)."""
+    from pointcloud_style_transfer_amd.config.config import Config
+    from pointcloud_style_transfer_amd.synthetic import lidar_like_cloud
+    from pointcloud_style_transfer_amd.training.trainer import DiffusionTrainer
+    from pointcloud_style_transfer_amd.utils.ema import ExponentialMovingAverage
+
+    monkeypatch.chdir(tmp_path)
+    cfg = Config(total_points=8192, global_points=2048, use_amp=True,
+                 gradient_accumulation_steps=1, experiment_name="resume")
+    torch.manual_seed(0)
+    tr = DiffusionTrainer(cfg, device="cuda")
+    ref_opt = torch.optim.AdamW(tr.model.parameters(), lr=cfg.learning_rate,
+                                weight_decay=cfg.weight_decay, betas=(0.9, 0.95))
+    for p in tr.model.parameters():
+        p.grad = torch.randn_like(p) * 1e-3
+    ref_opt.step()
+    tr.checkpoint_manager.save(tr.model, ref_opt, ExponentialMovingAverage(tr.model.parameters()),
+                               epoch=3)
+    assert tr.checkpoint_manager.load(tr.model, tr.optimizer, tr.ema) == 4
+    assert all(g["fused"] for g in tr.optimizer.param_groups)
+    assert tr.scaler.is_enabled()
+    sim = torch.from_numpy(np.stack([lidar_like_cloud(1000 + i, 8192) for i in range(2)]))
+    real = torch.from_numpy(np.stack([lidar_like_cloud(2000 + i, 8192) for i in range(2)]))
+    tr.model.train()
+    tr.optimizer.zero_grad()
+    before = [p.detach().clone() for p in tr.model.parameters()]
+    loss, _ = tr.train_step({"sim_full": sim, "real_full": real}, 0, 1)
+    torch.cuda.synchronize()
+    assert np.isfinite(float(loss))
+    moved = sum(not torch.equal(b, p.detach()) for b, p in zip(before, tr.model.parameters()))
+    assert moved > 70, moved

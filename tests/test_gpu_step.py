@@ -286,6 +286,36 @@ def test_knn_build_query_phases_match_interp(H):
     assert torch.equal(H.knn3_query(coarse, H.knn3_build(orig, idx)), ref)
 
 
+def test_per_call_choices_on_concurrent_streams(H):
+    """The ABI keeps no process-global switches (pcst.h conventions; tests/test_abi.py checks the
+    symbol table): the kNN build's LDS floor and the Chamfer forward path are arguments, so two
+    streams running the same calls with different choices at the same time cannot leak them
+    into each other.  Results are bit-identical to the one-stream, default-argument calls."""
+    rng = np.random.default_rng(5)
+    orig = dev(rng.standard_normal((2, 40000, 3)).astype(np.float32))
+    idx = dev(np.stack([rng.choice(40000, 10000, replace=False) for _ in range(2)]).astype(np.int64))
+    coarse = dev(rng.standard_normal((2, 10000, 3)).astype(np.float32))
+    p = dev((rng.standard_normal((4, 30000, 3)) * [1, 1, 0.2]).astype(np.float32))
+    q = dev((rng.standard_normal((4, 30000, 3)) * [1, 1, 0.2]).astype(np.float32))
+    ref_knn = H.knn3_interp(coarse, orig, idx)
+    ref_cd = H.chamfer_fwd(p, q)
+    torch.cuda.synchronize()
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    for s in (s1, s2):
+        s.wait_stream(torch.cuda.current_stream())
+    res = {}
+    for rep in range(3):   # interleave the enqueues so the two streams' kernels overlap
+        for name, s, floor, mode in (("a", s1, 8192, 2), ("b", s2, 0, 1)):
+            with torch.cuda.stream(s):
+                h = H.knn3_build(orig, idx, lds_floor=floor)
+                res[name, rep] = (H.knn3_query(coarse, h), H.chamfer_fwd(p, q, mode))
+    torch.cuda.synchronize()
+    for (name, rep), (knn, cd) in res.items():
+        assert torch.equal(knn, ref_knn), (name, rep)
+        for x, y in zip(cd, ref_cd):
+            assert torch.equal(x, y), (name, rep)
+
+
 def test_device_events_order_streams(H):
     """pcst_event_* (device-scope fences, the sampling step's cross-stream dependencies): a
     consumer stream that waits on the event sees the producer stream's writes, here behind a

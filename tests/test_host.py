@@ -413,3 +413,50 @@ def test_bf16_pair16_packing_follows_the_kernel_read_schedule():
         np.testing.assert_array_equal(seen[:O], ref, err_msg=name)
         if O < 16:
             assert (seen[O:] == 0).all(), name
+
+
+def test_chaos_floor_constants_match_profile():
+    """The end-to-end gates of tests/test_gpu_configs.py quote the chaos floor measured by
+    tools/chaos_floor.py (profiles/r03/chaos_floor.json); keep the two in step."""
+    import json
+
+    import test_gpu_configs as G
+
+    from conftest import REPO
+
+    rec = json.load(open(os.path.join(REPO, "profiles", "r03", "chaos_floor.json")))
+    assert rec["weights"] == "det"
+    for steps, consts in (("50", G.CHAOS_FLOOR_50), ("10", G.CHAOS_FLOOR_10)):
+        for k, v in consts.items():
+            assert abs(rec["runs"][steps][k] - v) <= 1e-3 * v, (steps, k)
+
+
+def test_fused_adamw_resumes_a_non_fused_checkpoint():
+    """the trainer's AdamW is fused, and load_state_dict takes the saved
+    param groups -- a checkpoint written by the reference (non-fused AdamW) carries fused=None.
+    The trainer's pre-hook (trainer.keep_fused) keeps the groups fused and loads `step` as
+    float32 (torch's rule for fused state), so GradScaler's found_inf protocol still applies.
+    CPU fused AdamW exercises the same torch code path as the device one."""
+    import torch.optim as optim
+
+    from pointcloud_style_transfer_amd.training.trainer import keep_fused
+
+    p = [torch.nn.Parameter(torch.randn(8, 4)), torch.nn.Parameter(torch.randn(4))]
+    ref_opt = optim.AdamW(p, lr=1e-3, betas=(0.9, 0.95))   # the reference's optimizer
+    for q in p:
+        q.grad = torch.randn_like(q)
+    ref_opt.step()
+    saved = ref_opt.state_dict()
+    assert saved["param_groups"][0].get("fused") is None
+    opt = optim.AdamW(p, lr=1e-3, betas=(0.9, 0.95), fused=True)
+    opt.register_load_state_dict_pre_hook(keep_fused)
+    opt.load_state_dict(saved)
+    g = opt.param_groups[0]
+    assert g["fused"] is True and g["foreach"] is None
+    assert opt.state[p[0]]["step"].dtype == torch.float32
+    # the amp-scaling protocol GradScaler uses with a fused optimizer
+    opt.grad_scale, opt.found_inf = torch.ones(()), torch.zeros(())
+    before = p[0].detach().clone()
+    opt.step()
+    assert float(opt.state[p[0]]["step"]) == 2.0
+    assert not torch.equal(before, p[0].detach())

@@ -29,14 +29,12 @@ else:  # the trainer's pair: a predicted x0 (noisy, spread) against the lidar-li
     q = np.stack([lidar_like_cloud(100 + i, a.N) for i in range(a.B)]).astype(np.float32)
     p = (q + rng.standard_normal(q.shape) * a.noise).astype(np.float32)
 p, q = torch.from_numpy(p).cuda(), torch.from_numpy(q).cuda()
-if a.mode:
-    _hip.chamfer_set_mode(a.mode)
-_hip.chamfer_fwd(p, q)
+_hip.chamfer_fwd(p, q, a.mode)
 torch.cuda.synchronize()
 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
 e0.record()
 for _ in range(a.reps):
-    out, _, _ = _hip.chamfer_fwd(p, q)
+    out, _, _ = _hip.chamfer_fwd(p, q, a.mode)
 e1.record()
 torch.cuda.synchronize()
 ms = e0.elapsed_time(e1) / a.reps

@@ -1,5 +1,6 @@
 """FPS timing (the SA1 shape: N = 30000, 512 samples) on a lidar-like and a Gaussian cloud, B = 1
-and B = 32, HIP events over 20 calls.  PCST_FPS_CULL=0 times fps_key_kernel instead."""
+and B = 32, HIP events over 20 calls.  An experiment build with XDEF=-DPCST_X_FPS_CULL=0 (loaded through
+PCST_LIB) times fps_key_kernel instead."""
 import os
 import sys
 
@@ -10,7 +11,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from pointcloud_style_transfer_amd import _hip  # noqa: E402
 from pointcloud_style_transfer_amd.synthetic import lidar_like_cloud  # noqa: E402
 
-mode = os.environ.get("PCST_FPS_CULL", "1")
+mode = os.path.basename(_hip.LIB_PATH)
 for name in ("lidar", "gauss"):
     for B in (1, 32):
         if name == "lidar":

@@ -65,11 +65,11 @@ def main():
     ev = []
     orig = _hip.chamfer_fwd
 
-    def timed_chamfer(pred, target):
+    def timed_chamfer(pred, target, mode=0):
         e0 = torch.cuda.Event(enable_timing=True)
         e1 = torch.cuda.Event(enable_timing=True)
         e0.record()
-        out = orig(pred, target)
+        out = orig(pred, target, mode)
         e1.record()
         ev.append((e0, e1, pred.shape[0] * pred.shape[1] * target.shape[1]))
         return out

@@ -34,7 +34,6 @@ with torch.no_grad():
     loop.wait_stream(torch.cuda.current_stream())
     with torch.cuda.stream(loop):
         ws = _hip.knn_workspace(2, 120000, cfg.global_points, device="cuda")
-    _hip.knn_set_build_lds_pad(dmod._KNN_BUILD_LDS_PAD)
 
     def step(i):
         global x
@@ -62,4 +61,3 @@ with torch.no_grad():
         t2 = time.perf_counter()
         print(f"host enqueue {1e6 * np.mean(host):.0f} us/step (max {1e6 * np.max(host):.0f}); "
               f"wall {1e6 * (t2 - t0) / 20:.0f} us/step; waited at sync {1e6 * (t2 - t1):.0f} us", flush=True)
-    _hip.knn_set_build_lds_pad(0)

@@ -1,5 +1,5 @@
 """Experiment harness: per-query records of the brick-shell outlier search on the bench's first
-trajectory steps.  PCST_LIB=pointcloud_style_transfer_amd/libpcst_hip_v_trace.so PCST_KNN_OUTLIER=1
+trajectory steps.  PCST_LIB=pointcloud_style_transfer_amd/libpcst_hip_v_trace.so 
 python tools/knn_otrace.py   (library built with -DKNN_TRACE)."""
 import ctypes
 import os

@@ -1,0 +1,27 @@
+"""A/B knobs for experiment runs (tools/ only; the product modules read no environment).
+
+    import knobs; knobs.apply()
+
+reads PCST_KNN_OVERLAP=0|1, PCST_KNN_BUILD_LDS_FLOOR=<bytes>, PCST_DEVICE_EVENTS=0|1 and
+PCST_NM_BF16_KERNEL=1 (the 32x32x16 pair kernel) and sets the matching module constants of
+models.diffusion_model.  Kernel-side variants are experiment builds (csrc/Makefile XDEF,
+loaded through PCST_LIB)."""
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def apply():
+    from pointcloud_style_transfer_amd import packing
+    from pointcloud_style_transfer_amd.models import diffusion_model as dm
+
+    e = os.environ
+    if "PCST_KNN_OVERLAP" in e:
+        dm.OVERLAP_KNN_BUILD = e["PCST_KNN_OVERLAP"] != "0"
+    if "PCST_KNN_BUILD_LDS_FLOOR" in e:
+        dm.KNN_BUILD_LDS_FLOOR = int(e["PCST_KNN_BUILD_LDS_FLOOR"])
+    if "PCST_DEVICE_EVENTS" in e:
+        dm.DEVICE_EVENTS = e["PCST_DEVICE_EVENTS"] != "0"
+    if e.get("PCST_NM_BF16_KERNEL") == "1":
+        dm.NoisePredictor.bf16_code = packing.BF16
