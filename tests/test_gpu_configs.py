@@ -389,15 +389,17 @@ CHAOS_FLOOR_50 = {"chamfer": 1.0649e-4, "p999_abs": 9.448e-4, "max_abs": 9.332e-
 CHAOS_FLOOR_10 = {"chamfer": 1.1634e-3, "p999_abs": 1.8010e-2, "max_abs": 7.4255e-1}
 
 
-@pytest.mark.parametrize("precision,mult", [("fp32", 1.0), ("bf16", 3.0)])
+@pytest.mark.parametrize("precision,mult", [("fp32", 1.0), ("bf16", 1.5)])
 def test_loop_vs_oracle_50_steps_120k(det_state, golden, precision, mult):
     """BASELINE configs[1]'s quality gate ("Chamfer vs ref"), for the mode bench.py measures
     (bf16 noise MLP) and the parity mode (fp32): the HIP guided loop on the 120k lidar-like
     cloud, 50 steps, guidance 7.5, the same x_T and counter-keyed draws as the committed oracle
     output (tests/golden/gen_oracle_loop.py).  Bounds are a stated multiple of the chaos floor
     -- what a 1-ulp change of x_T does to the oracle itself over the same loop: fp32 within
-    1x the floor, bf16 within 3x, for the metrics.py:20-44 Chamfer, the 99.9th percentile
-    and the maximum of |hip - oracle|."""
+    1x the floor, bf16 within 1.5x, for the metrics.py:20-44 Chamfer, the 99.9th percentile
+    and the maximum of |hip - oracle|.  Measured (round 3): fp32 0.39 / 0.18 / 0.05 x the
+    floor, bf16 0.95 / 0.35 / 0.94 x; the loop is deterministic (replayed draws), so these
+    figures repeat run to run."""
     from detweights import load_into
     from pointcloud_style_transfer_amd import rng
     from pointcloud_style_transfer_amd.config.config import Config
