@@ -24,6 +24,7 @@ namespace pcst {
 
 typedef __attribute__((ext_vector_type(16))) float f32x16;
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
 
 constexpr int kPart = 32768;  // bytes per streamed weight part
 // bias table offsets (floats) -- must match packing.py
@@ -35,12 +36,20 @@ constexpr int kCondSlots = 4;
 // defaults.  PCST_NM_EXPERIMENT bits: 1 = no weight DMA after the first two parts,
 // 2 = no barrier between parts (both give wrong results; they time the overheads;
 // tools/nm_quad.hip defines more for its experiment kernel),
+// 4 = no LDS fragment reads in the pair16 kernel (A operands from registers), 16 = the same for
+// the first group of 4 fragments of every run16 call only, 32 = no residual chunk hand-off,
 // 8 = compiler-scheduled LDS fragment reads instead of the asm reads.
 #ifndef PCST_NM_EXPERIMENT
 #define PCST_NM_EXPERIMENT 0
 #endif
 #ifndef PCST_NM_NCB
 #define PCST_NM_NCB 1
+#endif
+#ifndef PCST_NM_EPI_GROUP  // pair16 residual loop: the W2 fragment group after which the next
+#define PCST_NM_EPI_GROUP 3    // hidden chunk's epilogue + hand-off run (0..3; 3 measured best)
+#endif
+#ifndef PCST_NM_RD  // pair16 kernel: fragment groups read ahead of their MFMAs
+#define PCST_NM_RD 1
 #endif
 #ifndef PCST_NM_PAIRX  // pair kernel: partner = wave ^ PAIRX (4: the partner shares the SIMD)
 #define PCST_NM_PAIRX 4
@@ -161,6 +170,24 @@ template <int OFF>
 __device__ __forceinline__ bf16x8 lds_read_b128(uint32_t addr) {
   bf16x8 v;
   asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(v) : "v"(addr), "i"(OFF));
+  return v;
+}
+// one fragment read at byte offset `off` from `addr` (off is a compile-time constant after
+// unrolling; it goes into the instruction's offset field when it fits)
+__device__ __forceinline__ bf16x8 lds_read_one(uint32_t addr, int off) {
+  bf16x8 v;
+  if (__builtin_constant_p(off) && off >= 0 && off < 65536)
+    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(v) : "v"(addr), "i"(off));
+  else
+    asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(addr + off));
+  return v;
+}
+// f32x4 read from LDS in asm (bias rows in the hot loop): like the fragment reads, invisible to
+// the compiler's lgkmcnt accounting, so no compiler-inserted lgkmcnt(0) drains the fragment
+// read pipeline at their first use; covered by the counted waits (LDS ops complete in order)
+__device__ __forceinline__ f32x4 lds_read_f4(const float* p) {
+  f32x4 v;
+  asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"((uint32_t)(uintptr_t)p) : "memory");
   return v;
 }
 template <int N>
@@ -546,6 +573,23 @@ __device__ __forceinline__ void xput(char* X, int area, const bf16x8* ops) {
 #pragma unroll
   for (int i = 0; i < N; ++i) d[i * 64] = ops[i];
 }
+// the same at operand offset `at` (1 KiB units) of the area
+template <int N>
+__device__ __forceinline__ void xput_at(char* X, int area, int at, const bf16x8* ops) {
+  if constexpr ((PCST_NM_EXPERIMENT & 32) != 0) return;  // timing only: no chunk hand-off
+  bf16x8* d = reinterpret_cast<bf16x8*>(X + area * kXBytes) + at * 64 + (threadIdx.x & 63);
+#pragma unroll
+  for (int i = 0; i < N; ++i) d[i * 64] = ops[i];
+}
+// asm reads (see lds_read_f4): the hand-off registers are waited for by the next counted wait
+template <int N>
+__device__ __forceinline__ void xget_at(const char* X, int area, int at, bf16x8* ops) {
+  if constexpr ((PCST_NM_EXPERIMENT & 32) != 0) return;
+  const uint32_t a = (uint32_t)(uintptr_t)(X + area * kXBytes + at * 1024 + (threadIdx.x & 63) * 16);
+#pragma unroll
+  for (int i = 0; i < N; ++i)
+    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(ops[i]) : "v"(a), "i"(i * 1024) : "memory");
+}
 template <int N>
 __device__ __forceinline__ void xget(const char* X, int area, bf16x8* ops) {
   const bf16x8* d = reinterpret_cast<const bf16x8*>(X + area * kXBytes) + (threadIdx.x & 63);
@@ -737,26 +781,55 @@ __device__ __forceinline__ f32x4 mfma16(bf16x8 a, bf16x8 b, f32x4 c) {
 
 // N fragments from LDS part q starting at fragment base; fragment i is (row block i / NKS,
 // k-step i % NKS) and feeds both column blocks.  Same counted-wait read pipeline as run_seq.
-template <int N, int NKS>
+template <int N, int NKS, class Hook = NoHook>
 __device__ __forceinline__ void run16(const Streamer2& st, int q, int base, const bf16x8* in,
-                                      f32x4* acc) {
+                                      f32x4* acc, const Hook& hook = Hook()) {
   static_assert(N % 4 == 0, "groups of 4 fragments");
-  const uint32_t a0 = st.frag_addr(q, base);
-  bf16x8 cur[4], nxt[4];
-  cur[0] = lds_read_b128<0 * 1024>(a0);
-  cur[1] = lds_read_b128<1 * 1024>(a0);
-  cur[2] = lds_read_b128<2 * 1024>(a0);
-  cur[3] = lds_read_b128<3 * 1024>(a0);
+  if constexpr ((PCST_NM_EXPERIMENT & 4) != 0) {  // timing only: no LDS fragment reads
 #pragma unroll
-  for (int g = 0; g < N; g += 4) {
-    if (g + 4 < N) {
-      nxt[0] = lds_read_b128<0>(a0 + (g + 4) * 1024);
-      nxt[1] = lds_read_b128<1024>(a0 + (g + 4) * 1024);
-      nxt[2] = lds_read_b128<2 * 1024>(a0 + (g + 4) * 1024);
-      nxt[3] = lds_read_b128<3 * 1024>(a0 + (g + 4) * 1024);
-      lgkm_wait4<4>(cur[0], cur[1], cur[2], cur[3]);
+    for (int i = 0; i < N; ++i) {
+      const int rb = i / NKS, ks = i % NKS;
+      acc[rb * 2 + 0] = mfma16(in[(ks + 1) % NKS * 2], in[ks * 2 + 0], acc[rb * 2 + 0]);
+      acc[rb * 2 + 1] = mfma16(in[(ks + 1) % NKS * 2], in[ks * 2 + 1], acc[rb * 2 + 1]);
+    }
+    return;
+  }
+  const uint32_t a0 = st.frag_addr(q, base);
+  constexpr int NG = N / 4;
+  // groups of 4 fragments read PCST_NM_RD groups ahead of their MFMAs (1: cur + nxt; 2: + nn)
+  bf16x8 cur[4], nxt[4], nn[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    if constexpr ((PCST_NM_EXPERIMENT & 16) != 0)   // timing only: first group from registers
+      cur[j] = in[(j + 1) % NKS * 2];
+    else
+      cur[j] = lds_read_one(a0, j * 1024);
+  }
+  if constexpr (PCST_NM_RD >= 2 && NG > 1) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) nxt[j] = lds_read_one(a0, 4096 + j * 1024);
+  }
+#pragma unroll
+  for (int gg = 0; gg < NG; ++gg) {
+    const int g = gg * 4;
+    if constexpr (PCST_NM_RD >= 2) {
+      if (gg + 2 < NG) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) nn[j] = lds_read_one(a0, (g + 8) * 1024 + j * 1024);
+        lgkm_wait4<8>(cur[0], cur[1], cur[2], cur[3]);
+      } else if (gg + 1 < NG) {
+        lgkm_wait4<4>(cur[0], cur[1], cur[2], cur[3]);
+      } else {
+        lgkm_wait4<0>(cur[0], cur[1], cur[2], cur[3]);
+      }
     } else {
-      lgkm_wait4<0>(cur[0], cur[1], cur[2], cur[3]);
+      if (gg + 1 < NG) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) nxt[j] = lds_read_one(a0, (g + 4) * 1024 + j * 1024);
+        lgkm_wait4<4>(cur[0], cur[1], cur[2], cur[3]);
+      } else {
+        lgkm_wait4<0>(cur[0], cur[1], cur[2], cur[3]);
+      }
     }
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -764,9 +837,13 @@ __device__ __forceinline__ void run16(const Streamer2& st, int q, int base, cons
       acc[rb * 2 + 0] = mfma16(cur[j], in[ks * 2 + 0], acc[rb * 2 + 0]);
       acc[rb * 2 + 1] = mfma16(cur[j], in[ks * 2 + 1], acc[rb * 2 + 1]);
     }
-    if (g + 4 < N) {
+    hook(gg);  // VALU / LDS-store work placed in this group's MFMA shadow
+    if (gg + 1 < NG) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) cur[j] = nxt[j];
+      for (int j = 0; j < 4; ++j) {
+        cur[j] = nxt[j];
+        if constexpr (PCST_NM_RD >= 2) nxt[j] = nn[j];
+      }
     }
   }
 }
@@ -872,24 +949,57 @@ __device__ __forceinline__ void pair16_wave(const float* __restrict__ cond, cons
   put_own(x, false);
 
   // ---- 6 residual blocks; per pair of hidden chunks (it, 8 + it): W1 part (own chunk it + 8R,
-  // 2 row blocks x 8 k-steps), W2 part (own 8 row blocks x k-steps {chunk it, chunk 8 + it})
+  // 2 row blocks x 8 k-steps), W2 part (own 8 row blocks x k-steps {chunk it, chunk 8 + it}).
+  // Software-pipelined (parts packed W1(0), W1(1), W2(0), W1(2), W2(1), ...): W1 of chunk it + 1
+  // runs before W2 of chunk it, so the partner's chunk it -- written before the barrier that
+  // opens W1(it + 1) -- is read at the start of that part and is in registers when W2(it)
+  // starts, and chunk it + 1's ReLU/bf16 epilogue and hand-off run after the W2 MFMAs are
+  // issued.  The hand-off alternates between two 2 KiB slots of the partner's area (chunk c in
+  // slot c & 1): a wave writes chunk it + 1 while its partner may still read chunk it.
   for (int layer = 0; layer < 6; ++layer) {
     const float* b1 = sb + kOffB1 + layer * 512;
     const float* b2 = sb + kOffBB2 + layer * 256;
     st.next();
     get_mate();
-    for (int it = 0; it < 8; ++it) {
-      if (it) st.next();
+    Op hb[4];  // [chunk it: cb 0, cb 1 | chunk 8 + it: cb 0, cb 1]
+    {
       f32x4 hc[4];
-      hc[0] = hc[1] = bias4(b1 + (it + 8 * R) * 32, g);
-      hc[2] = hc[3] = bias4(b1 + (it + 8 * R) * 32 + 16, g);
+      hc[0] = hc[1] = bias4(b1 + (8 * R) * 32, g);
+      hc[2] = hc[3] = bias4(b1 + (8 * R) * 32 + 16, g);
       run16<16, 8>(st, st.part, R * 16, xb, hc);
-      Op hb[4];  // [chunk it: cb 0, cb 1 | chunk 8 + it: cb 0, cb 1]
       ops16<2>(hc, true, &hb[2 * R]);
-      xput<2>(X, mate, &hb[2 * R]);       // into the partner's area
-      st.next();
-      xget<2>(X, wid, &hb[2 * (1 - R)]);  // the partner's chunk, from this wave's area
-      run16<16, 2>(st, st.part, R * 16, hb, x);
+      xput_at<2>(X, mate, 0, &hb[2 * R]);
+    }
+    for (int it = 0; it < 8; ++it) {
+      f32x4 hn[4];
+      if (it < 7) {
+        st.next();                                           // part W1(it + 1)
+        xget_at<2>(X, wid, (it & 1) * 2, &hb[2 * (1 - R)]);  // the partner's chunk it
+        hn[0] = hn[1] = lds_read_f4(b1 + (it + 1 + 8 * R) * 32 + 4 * g);
+        hn[2] = hn[3] = lds_read_f4(b1 + (it + 1 + 8 * R) * 32 + 16 + 4 * g);
+        run16<16, 8>(st, st.part, R * 16, xb, hn);
+        st.next();                                           // part W2(it)
+      } else {
+        st.next();                                           // part W2(7)
+        xget_at<2>(X, wid, (it & 1) * 2, &hb[2 * (1 - R)]);
+      }
+      if (it < 7) {
+        // chunk it + 1's epilogue and hand-off in the MFMA shadow of W2's fragment group
+        // PCST_NM_EPI_GROUP (after the last: measured 1-4 % faster than after the first or
+        // second, where the VALU and LDS stores compete with the fragment reads)
+        Op hbn[2];
+        auto epi = [&](int gg) {
+          if (gg == PCST_NM_EPI_GROUP) {
+            ops16<2>(hn, true, hbn);
+            xput_at<2>(X, mate, ((it + 1) & 1) * 2, hbn);
+          }
+        };
+        run16<16, 2>(st, st.part, R * 16, hb, x, epi);
+        hb[2 * R] = hbn[0];
+        hb[2 * R + 1] = hbn[1];
+      } else {
+        run16<16, 2>(st, st.part, R * 16, hb, x);
+      }
     }
 #pragma unroll
     for (int rb = 0; rb < 8; ++rb) {

@@ -41,6 +41,10 @@ Parts hold the same weights as the 32x32x16 pair layout, re-cut into 16-row bloc
   residual W1 part = [row blocks 2it, 2it+1 | row blocks 2(8+it), 2(8+it)+1], all k-steps;
   residual W2 part = [for row blocks 0-7: k-steps (it, 8+it) | the same for row blocks 8-15];
   output_mlp.4: one part, row block 0 (rows 3..15 zero), 4 k-steps.
+The residual parts are in the kernel's software-pipelined order: W1(0), then per it = 0..7
+W1(it+1) (it < 7) before W2(it) -- the kernel computes the next hidden chunk before the W2
+product of the current one, so the partner's chunk exchange and the ReLU/bf16 epilogue sit in
+the MFMA shadow of the other part.
 """
 from __future__ import annotations
 
@@ -203,8 +207,11 @@ def _pack_pair16(g):
     for i in range(6):
         F1 = _frags16(g(f"layers.{i}.0.weight"))  # [32 row blocks, 8, 512]
         F2 = _frags16(g(f"layers.{i}.2.weight"))  # [16 row blocks, 16, 512]
+        w1 = lambda it: emit([F1[2 * it:2 * it + 2], F1[2 * (8 + it):2 * (8 + it) + 2]])  # noqa: E731
+        w1(0)
         for it in range(8):
-            emit([F1[2 * it:2 * it + 2], F1[2 * (8 + it):2 * (8 + it) + 2]])
+            if it < 7:
+                w1(it + 1)
             steps = [it, 8 + it]
             emit([F2[0:8][:, steps], F2[8:16][:, steps]])
     dense(g("output_mlp.0.weight"))

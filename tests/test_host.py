@@ -386,12 +386,17 @@ def test_bf16_pair16_packing_follows_the_kernel_read_schedule():
     dense("point_encoder.2", 8, 4)
     q[0] += 1
     dense("point_encoder.4", 8, 8)
-    for layer in range(6):
+    def w1(layer, it):
+        q[0] += 1
+        for role in (0, 1):
+            for i in range(16):
+                put(f"layers.{layer}.0", 2 * (it + 8 * role) + i // 8, i % 8, role * 16 + i)
+
+    for layer in range(6):   # software-pipelined: W1(0), then W1(it + 1) before W2(it)
+        w1(layer, 0)
         for it in range(8):
-            q[0] += 1
-            for role in (0, 1):
-                for i in range(16):
-                    put(f"layers.{layer}.0", 2 * (it + 8 * role) + i // 8, i % 8, role * 16 + i)
+            if it < 7:
+                w1(layer, it + 1)
             q[0] += 1
             for role in (0, 1):
                 for i in range(16):

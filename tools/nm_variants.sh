@@ -8,10 +8,11 @@ SETS=${2:-"0:1"}
 OUT=tools/nm_bin
 mkdir -p $OUT
 for s in $SETS; do
-  # SET = EXP:NCB[:PAIRX]
+  # SET = EXP:NCB[:PAIRX[:RD[:EPI]]]
   e=$(echo $s | cut -d: -f1); n=$(echo $s | cut -d: -f2); x=$(echo $s | cut -s -d: -f3)
-  bin=$OUT/nm_${e}_${n}${x:+_x$x}
-  extra="-DPCST_NM_EXPERIMENT=$e -DPCST_NM_NCB=$n ${x:+-DPCST_NM_PAIRX=$x}"
+  rd=$(echo $s | cut -s -d: -f4); ep=$(echo $s | cut -s -d: -f5)
+  bin=$OUT/nm_${e}_${n}${x:+_x$x}${rd:+_rd$rd}${ep:+_ep$ep}
+  extra="-DPCST_NM_EXPERIMENT=$e -DPCST_NM_NCB=$n ${x:+-DPCST_NM_PAIRX=$x} ${rd:+-DPCST_NM_RD=$rd} ${ep:+-DPCST_NM_EPI_GROUP=$ep}"
   # "v0:0" = a saved earlier kernel (tools/_scratch/noise_mlp_v0.hip)
   if [ "$e" = v0 ]; then extra='-DNM_SRC="_scratch/noise_mlp_v0.hip"'; fi
   if [ "$MODE" = build ]; then
