@@ -579,9 +579,9 @@ __device__ __forceinline__ void voxf_flush_tiles(int row, int64_t tiles, const u
 }
 
 // Every workgroup first finds the row's boundary bin b* (the bin holding the need-th smallest
-// key) from the histogram; workgroup 0 records it for the ties kernel.  Then, over one
+// key) from the histogram; workgroup 0 records it for the emit kernel's tie ranking.  Then, over one
 // contiguous candidate range per workgroup: U <= T keeps every representative; keys below b*
-// are kept, keys in b* go to the tie list (its order is irrelevant: the ties kernel ranks).
+// are kept, keys in b* go to the tie list (its order is irrelevant: the emit kernel ranks).
 __global__ __launch_bounds__(256) void voxf_select_kernel(
     int N, int64_t T, int B, uint64_t seed_v, const uint64_t* __restrict__ seed_p,
     const uint32_t* __restrict__ hist, int32_t* __restrict__ sel, int32_t* __restrict__ cnt4,
@@ -648,48 +648,29 @@ __global__ __launch_bounds__(256) void voxf_select_kernel(
   voxf_flush_tiles(row, tiles, lt, ktile);
 }
 
-// boundary bin: exact order by (key, id), keep the first `rem` (one workgroup per row)
-__global__ __launch_bounds__(1024) void voxf_ties_kernel(int N, int64_t T, int B,
-                                                         const int32_t* __restrict__ sel,
-                                                         const int32_t* __restrict__ cnt4,
-                                                         const unsigned long long* __restrict__ ties,
-                                                         const int64_t* __restrict__ reps,
-                                                         uint32_t* __restrict__ kcnt,
-                                                         uint32_t* __restrict__ ktile,
-                                                         int64_t tiles) {
-  const int row = blockIdx.x, cl = row % B;
-  if (sel[row * 4 + 0] < 0) return;
-  const int rem = sel[row * 4 + 1];
-  const int U = cnt4[cl * 4];
-  const int nt = min(cnt4[row * 4 + 2], kTieCap);
-  const unsigned long long* Tb = ties + (int64_t)row * kTieCap;
-  for (int i = threadIdx.x; i < nt; i += 1024) {
-    const unsigned long long v = Tb[i];
-    int rank = 0;
-    for (int k = 0; k < nt; ++k) rank += Tb[k] < v;
-    if (rank < rem) {
-      const uint32_t id = (uint32_t)v;
-      const int64_t n = U > T ? reps[(int64_t)cl * N + id] : (int64_t)id;
-      atomicAdd(&kcnt[(int64_t)row * N + n], 1u);
-      atomicAdd(&ktile[row * tiles + n / kEmitTile], 1u);
-    }
-  }
-}
-
 // Row emit in ascending point-index order: tile j's offset is the sum of the earlier tiles'
 // keep counts; inside the tile a block scan places each index kcnt[n] times (index + point).
-// The 16 points of a thread are loaded before any store, so their latencies overlap.
+// The boundary bin's ties (select's list, one per row) are ranked exactly by (key, id) here, by
+// every workgroup of the row (the list holds about candidates / 4096 entries), instead of by a
+// launch of their own: the kept ties in this tile add to its counts, those in earlier tiles to
+// its offset.  The 16 points of a thread are loaded before any store, so their latencies overlap.
+constexpr int kTieLds = 2048;  // ties ranked from LDS up to this many (else from L2)
 __global__ __launch_bounds__(256) void voxf_emit_kernel(const float* __restrict__ pts, int N,
                                                         int64_t T, int B,
                                                         const uint32_t* __restrict__ kcnt,
                                                         const uint32_t* __restrict__ ktile,
                                                         int64_t tiles, int32_t* __restrict__ cnt4,
+                                                        const int32_t* __restrict__ sel,
+                                                        const unsigned long long* __restrict__ ties,
+                                                        const int64_t* __restrict__ reps,
                                                         int64_t* __restrict__ out_idx,
                                                         float* __restrict__ out_pts) {
   constexpr int kPer = kEmitTile / 256;
   const int row = blockIdx.y, cl = row % B;
   const int64_t tile = blockIdx.x;
   __shared__ uint32_t sh[260];
+  __shared__ uint32_t add[kEmitTile];
+  __shared__ unsigned long long tl[kTieLds];
   const int64_t n0 = tile * kEmitTile + threadIdx.x * kPer;
   const uint32_t* C = kcnt + (int64_t)row * N;
   const float* P = pts + (int64_t)cl * N * 3;
@@ -702,13 +683,45 @@ __global__ __launch_bounds__(256) void voxf_emit_kernel(const float* __restrict_
     const int64_t n = n0 + k < N ? n0 + k : N - 1;
     q[3 * k] = P[n * 3]; q[3 * k + 1] = P[n * 3 + 1]; q[3 * k + 2] = P[n * 3 + 2];
   }
-  uint32_t before = 0;
+  // the boundary bin: keep the `rem` smallest (key, id) of the row's tie list
+  for (int i = threadIdx.x; i < kEmitTile; i += 256) add[i] = 0u;
+  const int bstar = sel[row * 4 + 0];
+  uint32_t tie_before = 0;
+  if (bstar >= 0) {
+    const int rem = sel[row * 4 + 1];
+    const int U = cnt4[(row % B) * 4];
+    const int nt = min(cnt4[row * 4 + 2], kTieCap);
+    const unsigned long long* Tb = ties + (int64_t)row * kTieCap;
+    const bool in_lds = nt <= kTieLds;
+    if (in_lds)
+      for (int i = threadIdx.x; i < nt; i += 256) tl[i] = Tb[i];
+    __syncthreads();
+    for (int i = threadIdx.x; i < nt; i += 256) {
+      const unsigned long long v = in_lds ? tl[i] : Tb[i];
+      int rank = 0;
+      if (in_lds)
+        for (int k = 0; k < nt; ++k) rank += tl[k] < v;
+      else
+        for (int k = 0; k < nt; ++k) rank += Tb[k] < v;
+      if (rank < rem) {
+        const uint32_t id = (uint32_t)v;
+        const int64_t n = U > T ? reps[(int64_t)cl * N + id] : (int64_t)id;
+        const int64_t tn = n / kEmitTile;
+        if (tn < tile) ++tie_before;
+        else if (tn == tile) atomicAdd(&add[n - tile * kEmitTile], 1u);
+      }
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < kPer; ++k) c[k] += add[threadIdx.x * kPer + k];
+  uint32_t before = tie_before;
   for (int64_t i = threadIdx.x; i < tile; i += 256) before += ktile[row * tiles + i];
   uint32_t s = 0;
 #pragma unroll
   for (int k = 0; k < kPer; ++k) s += c[k];
   uint32_t tot0, tot;
-  block_excl_scan_256(before, sh, tot0);  // tot0 = sum over the earlier tiles
+  block_excl_scan_256(before, sh, tot0);  // tot0 = everything kept in the earlier tiles
   int64_t pos = (int64_t)tot0 + block_excl_scan_256(s, sh, tot);
 #pragma unroll
   for (int k = 0; k < kPer; ++k) {
@@ -721,8 +734,8 @@ __global__ __launch_bounds__(256) void voxf_emit_kernel(const float* __restrict_
   }
 }
 
-// stats (+ zeroing), insert (+ voxel parameters), reps, hist, select (+ boundary bin, marks),
-// ties (+ marks), emit (rows in point-index order): 7 launches.
+// stats (+ zeroing), insert (+ voxel parameters), reps, hist, select (+ boundary bin, marks,
+// tie list), emit (+ tie ranking; rows in point-index order): 6 launches.
 static int voxel_fast(const float* pts, int64_t B, int64_t N, int64_t copies, int64_t T,
                       void* workspace, uint64_t seed, const uint64_t* seed_p, int64_t* out_idx,
                       float* out_pts, hipStream_t s) {
@@ -741,10 +754,8 @@ static int voxel_fast(const float* pts, int64_t B, int64_t N, int64_t copies, in
   hipLaunchKernelGGL(voxf_select_kernel, dim3(128, rows), dim3(256), 0, s, n, T, b, seed, seed_p,
                      w.hist, w.sel, w.cnt4, w.rhash, w.isrep, w.reps, w.ties, w.kcnt, w.ktile,
                      w.tiles);
-  hipLaunchKernelGGL(voxf_ties_kernel, dim3(rows), dim3(1024), 0, s, n, T, b, w.sel, w.cnt4,
-                     w.ties, w.reps, w.kcnt, w.ktile, w.tiles);
   hipLaunchKernelGGL(voxf_emit_kernel, dim3((unsigned)w.tiles, rows), dim3(256), 0, s, pts, n, T,
-                     b, w.kcnt, w.ktile, w.tiles, w.cnt4, out_idx, out_pts);
+                     b, w.kcnt, w.ktile, w.tiles, w.cnt4, w.sel, w.ties, w.reps, out_idx, out_pts);
   PCST_LAUNCH_CHECK("voxel_downsample");
   return PCST_OK;
 }

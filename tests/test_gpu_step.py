@@ -123,6 +123,43 @@ def test_voxel_copies_matches_concat(H, N, T, B, copies, sig):
     np.testing.assert_array_equal(p1.cpu().numpy(), np.stack([allp[r][i1[r]] for r in range(copies * B)]))
 
 
+def test_voxel_pad_subset_is_uniform(H):
+    """The device-drawn pad subset (U < T: T - U of the P non-representatives, chosen by a
+    keyed Feistel permutation of the pool, csrc/voxel.hip voxf_keep_kernel) is a uniform
+    random subset: over 400 seeds every pool point's inclusion frequency is (T - U) / P within
+    a binomial 5-sigma band, the count per seed is exact, the per-seed sets differ, and the
+    frequencies of the pool's first and second halves agree (no positional bias)."""
+    rng = np.random.default_rng(5)
+    N, T = 6000, 3000
+    pts = (rng.standard_normal((1, N, 3)) * np.array([1, 1, 0.2])).astype(np.float32)
+    x = dev(pts)
+    from oracle import oracle as O
+    reps = O.voxel_reps(pts[0], T)[0]
+    U = len(reps)
+    assert U < T
+    pool = np.setdiff1d(np.arange(N), reps)
+    P, need = len(pool), T - U
+    S = 400
+    hits = np.zeros(N, np.int64)
+    prev = None
+    for seed in range(S):
+        _, idx = H.voxel_downsample(x, T, seed=1000 + seed)
+        i = idx[0].cpu().numpy()
+        extra = np.setdiff1d(i, reps)
+        assert len(extra) == need and len(np.unique(extra)) == need
+        hits[extra] += 1
+        if prev is not None:
+            assert not np.array_equal(prev, extra)
+        prev = extra
+    f = hits[pool] / S
+    p = need / P
+    sd = np.sqrt(p * (1 - p) / S)
+    assert np.abs(f - p).max() <= 5 * sd + 1e-12, (np.abs(f - p).max(), sd)
+    h = len(pool) // 2
+    assert abs(f[:h].mean() - f[h:].mean()) <= 5 * sd / np.sqrt(h)
+    assert hits[reps].sum() == 0
+
+
 def test_knn_golden(H, golden):
     g = golden("hierarchical.npz")
     out = H.knn3_interp(dev(g["knn_coarse"]), dev(g["knn_orig"]), dev(g["knn_idx"]), check=True)
