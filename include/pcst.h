@@ -130,20 +130,24 @@ int pcst_linear_wgrad_workspace_size(int64_t M, int64_t I, int64_t O, size_t* by
 int pcst_linear_wgrad(const float* dZ, const float* X, int64_t M, int64_t I, int64_t O, float* dW,
                       float* db, void* workspace, void* stream);
 
-/* bf16-MFMA variants for the training path under torch.autocast (trainer.py:81-106; the
+/* 16-bit-MFMA variants for the training path under torch.autocast (trainer.py:81-106; the
  * reference's CUDA autocast runs Linear layers in half precision): operands are fp32 tensors
- * rounded to bf16 in LDS, accumulation and outputs fp32.
+ * rounded in LDS to bf16 (f16 = 0) or fp16 (f16 = 1, torch's default CUDA autocast dtype),
+ * accumulation and outputs fp32.
  * gemm_nt: C [M,O] = act(scale*(A [M,K] . B [O,K]^T) + shift) (scale/shift may be NULL).
  * linear_wgrad_bf16: as pcst_linear_wgrad (db from the unrounded fp32 dZ). */
 int pcst_gemm_nt_bf16(const float* A, int64_t M, int64_t K, const float* B, int64_t O,
-                      const float* scale, const float* shift, int relu, float* C, void* stream);
+                      const float* scale, const float* shift, int relu, float* C, int f16,
+                      void* stream);
 int pcst_linear_wgrad_bf16_workspace_size(int64_t M, int64_t I, int64_t O, size_t* bytes);
 int pcst_linear_wgrad_bf16(const float* dZ, const float* X, int64_t M, int64_t I, int64_t O,
-                           float* dW, float* db, void* workspace, void* stream);
+                           float* dW, float* db, void* workspace, int f16, void* stream);
 
-/* Training GEMMs with bf16 activation storage and fused epilogues (csrc/train_mlp.hip): the
+/* Training GEMMs with 16-bit activation storage and fused epilogues (csrc/train_mlp.hip): the
  * NoisePredictor residual block x + Dropout(Linear2(ReLU(Linear1(x)))) (diffusion_model.py:48-52,
- * 57-58) and its backward.  bf16 buffers are uint16_t (raw bfloat16 bits).  A [M,K] and B [O,K]
+ * 57-58) and its backward.  16-bit buffers are uint16_t raw bits, bfloat16 (f16 = 0) or IEEE
+ * half (f16 = 1: the reference trainer's CUDA autocast dtype, trainer.py:50,78); "bf16" in the
+ * names and flags below means "16-bit" in either format.  A [M,K] and B [O,K]
  * are fp32 (rounded to bf16 when staged) or bf16 per a_bf16/b_bf16; O % 4 == 0, K % 8 == 0 for a
  * bf16 operand (% 4 for fp32); all pointers 16-byte aligned.  epilogue:
  *   0 EP_F32         C fp32 = act(acc + bias)
@@ -158,15 +162,16 @@ int pcst_linear_wgrad_bf16(const float* dZ, const float* X, int64_t M, int64_t I
  * bf16 A with bf16 B runs the pipelined kernel (64-deep K slices, two in flight). */
 int pcst_gemm_ex(const void* A, int a_bf16, int64_t M, int64_t K, const void* B, int b_bf16,
                  int64_t O, const float* bias, int relu, int epilogue, const void* aux,
-                 uint64_t seed, float drop_p, int64_t group_rows, void* C, uint16_t* C2,
+                 uint64_t seed, float drop_p, int64_t group_rows, void* C, uint16_t* C2, int f16,
                  void* stream);
 int pcst_dropout_grad_bf16(const float* g, int64_t n, uint64_t seed, float drop_p, uint16_t* out,
-                           void* stream);
+                           int f16, void* stream);
 /* dW [O,I] = dZ^T X, db [O] = column sums of dZ (may be NULL), dZ [M,O] / X [M,I] fp32 or bf16;
  * I % 8 == 0, O % 8 == 0.  Deterministic (chunk partials combined in order). */
 int pcst_linear_wgrad_ex_workspace_size(int64_t M, int64_t I, int64_t O, size_t* bytes);
 int pcst_linear_wgrad_ex(const void* dZ, int dz_bf16, const void* X, int x_bf16, int64_t M,
-                         int64_t I, int64_t O, float* dW, float* db, void* workspace, void* stream);
+                         int64_t I, int64_t O, float* dW, float* db, void* workspace, int f16,
+                         void* stream);
 
 /* ---- models/diffusion_model.py --------------------------------------------------------- */
 

@@ -60,14 +60,15 @@ SIGNATURES = {
     "pcst_voxel_center_dist": [_P, _I, _P, ctypes.c_float, _P, _P, _P, _P],
     "pcst_knn_dist": [_P, _P, _I, _I, _I, _I, _P, _P, _P],
     "pcst_emd_greedy": [_P, _P, _I, _I, _I, _P, _P],
-    "pcst_gemm_nt_bf16": [_P, _I, _I, _P, _I, _P, _P, ctypes.c_int, _P, _P],
+    "pcst_gemm_nt_bf16": [_P, _I, _I, _P, _I, _P, _P, ctypes.c_int, _P, ctypes.c_int, _P],
     "pcst_linear_wgrad_bf16_workspace_size": [_I, _I, _I, _SZ],
-    "pcst_linear_wgrad_bf16": [_P, _P, _I, _I, _I, _P, _P, _P, _P],
+    "pcst_linear_wgrad_bf16": [_P, _P, _I, _I, _I, _P, _P, _P, ctypes.c_int, _P],
     "pcst_gemm_ex": [_P, ctypes.c_int, _I, _I, _P, ctypes.c_int, _I, _P, ctypes.c_int,
-                     ctypes.c_int, _P, ctypes.c_uint64, _F, _I, _P, _P, _P],
-    "pcst_dropout_grad_bf16": [_P, _I, ctypes.c_uint64, _F, _P, _P],
+                     ctypes.c_int, _P, ctypes.c_uint64, _F, _I, _P, _P, ctypes.c_int, _P],
+    "pcst_dropout_grad_bf16": [_P, _I, ctypes.c_uint64, _F, _P, ctypes.c_int, _P],
     "pcst_linear_wgrad_ex_workspace_size": [_I, _I, _I, _SZ],
-    "pcst_linear_wgrad_ex": [_P, ctypes.c_int, _P, ctypes.c_int, _I, _I, _I, _P, _P, _P, _P],
+    "pcst_linear_wgrad_ex": [_P, ctypes.c_int, _P, ctypes.c_int, _I, _I, _I, _P, _P, _P,
+                             ctypes.c_int, _P],
     "pcst_relu_bwd": [_P, _P, _I, _P, _P],
     "pcst_linear_wgrad_workspace_size": [_I, _I, _I, _SZ],
     "pcst_linear_wgrad": [_P, _P, _I, _I, _I, _P, _P, _P, _P],
@@ -479,9 +480,20 @@ def relu_bwd(dy, y):
     return dz
 
 
-def linear_wgrad(dZ, X, bias=True, bf16=False):
+_HALVES = (torch.bfloat16, torch.float16)
+
+
+def _f16_flag(half):
+    """ABI format flag of a 16-bit dtype: 0 bfloat16, 1 float16 (pcst.h)."""
+    if half not in _HALVES:
+        raise RuntimeError(f"16-bit operand dtype must be bfloat16 or float16, got {half}")
+    return 1 if half == torch.float16 else 0
+
+
+def linear_wgrad(dZ, X, bias=True, bf16=False, half=torch.bfloat16):
     """dZ [M,O], X [M,I] -> (dW = dZ^T X [O,I], db = dZ^T 1 [O] or None); deterministic.
-    bf16: operands rounded to bf16 for the MFMA (autocast training), fp32 accumulation."""
+    bf16: operands rounded to the 16-bit `half` dtype (bfloat16 or float16) for the MFMA
+    (autocast training), fp32 accumulation."""
     require_device(dZ, X)
     dZ, X = _f32(dZ), _f32(X)
     M, O = dZ.shape
@@ -492,12 +504,17 @@ def linear_wgrad(dZ, X, bias=True, bf16=False):
     ws = _workspace(fn + "_workspace_size", M, I, O, device=dZ.device)
     dW = torch.empty(O, I, dtype=torch.float32, device=dZ.device)
     db = torch.empty(O, dtype=torch.float32, device=dZ.device) if bias else None
-    _call(fn, _ptr(dZ), _ptr(X), M, I, O, _ptr(dW), _ptr(db), _ptr(ws), _stream())
+    if bf16:
+        _call(fn, _ptr(dZ), _ptr(X), M, I, O, _ptr(dW), _ptr(db), _ptr(ws), _f16_flag(half),
+              _stream())
+    else:
+        _call(fn, _ptr(dZ), _ptr(X), M, I, O, _ptr(dW), _ptr(db), _ptr(ws), _stream())
     return dW, db
 
 
-def gemm_nt_bf16(A, B, scale=None, shift=None, relu=False):
-    """A [M,K], B [O,K] -> act(scale*(A B^T)+shift) [M,O] on bf16 MFMA (fp32 accumulation)."""
+def gemm_nt_bf16(A, B, scale=None, shift=None, relu=False, half=torch.bfloat16):
+    """A [M,K], B [O,K] -> act(scale*(A B^T)+shift) [M,O] on 16-bit MFMA (operands rounded to
+    `half`: bfloat16 or float16; fp32 accumulation)."""
     require_device(A, B, scale, shift)
     A, B = _f32(A), _f32(B)
     M, K = A.shape
@@ -508,7 +525,7 @@ def gemm_nt_bf16(A, B, scale=None, shift=None, relu=False):
     scale = None if scale is None else _f32(scale)
     shift = None if shift is None else _f32(shift)
     _call("pcst_gemm_nt_bf16", _ptr(A), M, K, _ptr(B), O, _ptr(scale), _ptr(shift),
-          int(relu), _ptr(C), _stream())
+          int(relu), _ptr(C), _f16_flag(half), _stream())
     return C
 
 
@@ -516,63 +533,78 @@ EP_F32, EP_BF16, EP_RESID_DROP, EP_RELU_MASK, EP_ADD, EP_COND = range(6)
 _EP_BF16_OUT = (EP_BF16, EP_RELU_MASK)
 
 
-def _f32_or_bf16(t):
-    if t.dtype == torch.bfloat16:
+def _f32_or_16(t, half):
+    """(tensor, 16-bit flag): 16-bit tensors must be of the call's `half` dtype."""
+    if t.dtype in _HALVES:
+        if t.dtype != half:
+            raise RuntimeError(f"16-bit operand is {t.dtype}, the call's format is {half}")
         return t.contiguous(), 1
     return _f32(t), 0
 
 
+def _half_of(*ts, default=torch.bfloat16):
+    """The 16-bit format of a call: that of its 16-bit tensors (all alike), else `default`."""
+    hs = {t.dtype for t in ts if t is not None and t.dtype in _HALVES}
+    if len(hs) > 1:
+        raise RuntimeError(f"mixed 16-bit operand formats {hs}")
+    return hs.pop() if hs else default
+
+
 def gemm_ex(A, B, bias=None, relu=False, epilogue=EP_F32, aux=None, seed=0, p=0.0,
-            group_rows=0, copy_bf16=False):
-    """A [M,K], B [O,K] (fp32 or bf16) -> epilogue(A B^T) on bf16 MFMA (csrc/train_mlp.hip):
-    EP_F32/EP_BF16 act(acc+bias) as fp32/bf16, EP_RESID_DROP aux + dropout_p(acc+bias) (fp32),
-    EP_RELU_MASK acc*[aux>0] (bf16, aux bf16), EP_ADD acc + aux (fp32), EP_COND
+            group_rows=0, copy_bf16=False, half=None):
+    """A [M,K], B [O,K] (fp32 or 16-bit) -> epilogue(A B^T) on 16-bit MFMA (csrc/train_mlp.hip):
+    EP_F32/EP_BF16 act(acc+bias) as fp32/16-bit, EP_RESID_DROP aux + dropout_p(acc+bias) (fp32),
+    EP_RELU_MASK acc*[aux>0] (16-bit, aux 16-bit), EP_ADD acc + aux (fp32), EP_COND
     ((acc+bias) + aux[g,0]) + aux[g,1] with g = row // group_rows (fp32).  copy_bf16 (fp32
-    outputs): also return a bf16 copy, (C, C_bf16)."""
+    outputs): also return a 16-bit copy, (C, C_16).  `half` (bfloat16 or float16) is the 16-bit
+    format; default: that of the 16-bit operands, else bfloat16."""
     require_device(A, B, bias, aux)
-    A, a16 = _f32_or_bf16(A)
-    B, b16 = _f32_or_bf16(B)
+    half = half or _half_of(A, B, aux if epilogue == EP_RELU_MASK else None)
+    A, a16 = _f32_or_16(A, half)
+    B, b16 = _f32_or_16(B, half)
     M, K = A.shape
     O = B.shape[0]
     if B.shape[1] != K:
         raise RuntimeError(f"gemm_ex: K mismatch {tuple(A.shape)} vs {tuple(B.shape)}")
     bias = None if bias is None else _f32(bias)
     if aux is not None:
-        want = torch.bfloat16 if epilogue == EP_RELU_MASK else torch.float32
+        want = half if epilogue == EP_RELU_MASK else torch.float32
         shape = (M // max(group_rows, 1), 2, O) if epilogue == EP_COND else (M, O)
         if aux.dtype != want or tuple(aux.shape) != shape:
             raise RuntimeError(f"gemm_ex: aux must be {want} {list(shape)}, got "
                                f"{aux.dtype} {list(aux.shape)}")
         aux = aux.contiguous()
-    out_dtype = torch.bfloat16 if epilogue in _EP_BF16_OUT else torch.float32
+    out_dtype = half if epilogue in _EP_BF16_OUT else torch.float32
     C = torch.empty(M, O, dtype=out_dtype, device=A.device)
     C2 = None
     if copy_bf16:
         if out_dtype != torch.float32:
             raise RuntimeError("gemm_ex: copy_bf16 needs an fp32 epilogue")
-        C2 = torch.empty(M, O, dtype=torch.bfloat16, device=A.device)
+        C2 = torch.empty(M, O, dtype=half, device=A.device)
     _call("pcst_gemm_ex", _ptr(A), a16, M, K, _ptr(B), b16, O, _ptr(bias), int(relu),
           int(epilogue), _ptr(aux), int(seed) & (2**64 - 1), float(p), int(group_rows), _ptr(C),
-          _ptr(C2), _stream())
+          _ptr(C2), _f16_flag(half), _stream())
     return (C, C2) if copy_bf16 else C
 
 
-def dropout_grad_bf16(g, seed, p):
-    """Dropout backward with the mask regenerated from (seed, element index): bf16(g*keep/(1-p))."""
+def dropout_grad_bf16(g, seed, p, half=torch.bfloat16):
+    """Dropout backward with the mask regenerated from (seed, element index):
+    half(g*keep/(1-p)), `half` bfloat16 or float16."""
     require_device(g)
     g = _f32(g)
-    out = torch.empty(g.shape, dtype=torch.bfloat16, device=g.device)
+    out = torch.empty(g.shape, dtype=half, device=g.device)
     _call("pcst_dropout_grad_bf16", _ptr(g), g.numel(), int(seed) & (2**64 - 1), float(p),
-          _ptr(out), _stream())
+          _ptr(out), _f16_flag(half), _stream())
     return out
 
 
-def linear_wgrad_ex(dZ, X, bias=True):
-    """dZ [M,O], X [M,I] (fp32 or bf16) -> (dW = dZ^T X [O,I], db [O] or None) on bf16 MFMA,
-    deterministic."""
+def linear_wgrad_ex(dZ, X, bias=True, half=None):
+    """dZ [M,O], X [M,I] (fp32 or 16-bit) -> (dW = dZ^T X [O,I], db [O] or None) on 16-bit MFMA,
+    deterministic; `half` as in gemm_ex."""
     require_device(dZ, X)
-    dZ, z16 = _f32_or_bf16(dZ)
-    X, x16 = _f32_or_bf16(X)
+    half = half or _half_of(dZ, X)
+    dZ, z16 = _f32_or_16(dZ, half)
+    X, x16 = _f32_or_16(X, half)
     M, O = dZ.shape
     I = X.shape[1]
     if X.shape[0] != M:
@@ -581,7 +613,7 @@ def linear_wgrad_ex(dZ, X, bias=True):
     dW = torch.empty(O, I, dtype=torch.float32, device=dZ.device)
     db = torch.empty(O, dtype=torch.float32, device=dZ.device) if bias else None
     _call("pcst_linear_wgrad_ex", _ptr(dZ), z16, _ptr(X), x16, M, I, O, _ptr(dW), _ptr(db),
-          _ptr(ws), _stream())
+          _ptr(ws), _f16_flag(half), _stream())
     return dW, db
 
 

@@ -3,9 +3,11 @@ defaults and order), so pickled configs in reference checkpoints map onto it and
 field the hot path reads (feature_dim, time_embed_dim, global_points, num_timesteps, schedule,
 cond_drop_prob, lambda_chamfer, use_amp, use_hierarchical, ...) means the same thing.
 
-Two additions, both keyword fields with defaults that keep the reference behaviour:
+Three additions, keyword fields with defaults that keep the reference behaviour:
 `precision` ("fp32": exact-f32 MFMA, the parity default; "bf16": bf16 MFMA perf mode of the
-noise MLP, what bench.py measures) and
+noise MLP, what bench.py measures),
+`amp_dtype` (the 16-bit operand format of the training GEMMs under `use_amp`: "float16", the
+reference's CUDA autocast default, trainer.py:50,78, or "bfloat16"; same MFMA rate) and
 `make_dirs` (the reference creates log/result/checkpoint directories in the CWD on
 construction, config.py:64-67; set False to skip)."""
 from dataclasses import dataclass
@@ -70,6 +72,7 @@ class Config:
 
     # MI355X build additions
     precision: str = "fp32"
+    amp_dtype: str = "float16"
     make_dirs: bool = True
 
     def __post_init__(self):
@@ -80,6 +83,6 @@ class Config:
             os.makedirs(d, exist_ok=True)
 
     def __setstate__(self, state):
-        # reference pickles carry no `precision` / `make_dirs`: fill the defaults
-        self.__dict__.update({"precision": "fp32", "make_dirs": True})
+        # reference pickles carry no `precision` / `amp_dtype` / `make_dirs`: fill the defaults
+        self.__dict__.update({"precision": "fp32", "amp_dtype": "float16", "make_dirs": True})
         self.__dict__.update(state)

@@ -7,45 +7,65 @@
 //   wgrad:    C[o, i] = sum_m dZ[m, o] X[m, i]  (+ db[o] = sum_m dZ[m, o])  weight gradient
 //
 // Tile 128 x 128 per 256-thread workgroup: 2 x 2 waves, each 64 x 64 = 2 x 2 blocks of
-// v_mfma_f32_32x32x16_bf16.  K is staged 32 deep; an LDS row holds the 32 k-values of one
+// v_mfma_f32_32x32x16_bf16 (or _f16: the file is compiled twice, see train_mlp.hip).  K is staged 32 deep; an LDS row holds the 32 k-values of one
 // output row or column as bf16 (64 B) padded to 80 B, so the 16-byte fragment reads of
 // consecutive rows fall on distinct banks.  The weight gradient splits its reduction over the
 // M rows into chunks (as csrc/sa_mlp.hip's exact-f32 wgrad) and combines them in order.
 #include "common.h"
 
+#include "train_h16.h"
+
+#ifndef PCST_H16_F16
+#define PCST_H16_F16 0
+#endif
+
 namespace pcst {
+namespace PCST_H16_NS {
+
+#if PCST_H16_F16
+typedef _Float16 h16;
+#else
+typedef __bf16 h16;
+#endif
 
 typedef __attribute__((ext_vector_type(16))) float f32x16;
-typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
-typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+typedef __attribute__((ext_vector_type(8))) h16 h16x8;
+__device__ __forceinline__ auto mfma32_h16(h16x8 a, h16x8 b, __attribute__((ext_vector_type(16))) float c) {
+#if PCST_H16_F16
+  return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+#else
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+#endif
+}
+typedef __attribute__((ext_vector_type(4))) h16 h16x4;
 
 constexpr int kGT = 128, kGK = 32, kGLd = 40;  // tile, k slice, LDS row (bf16 elements)
 
 __device__ __forceinline__ int grow(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
 
 // one 32-deep k slice: 2 x 2 blocks x 2 k-steps of 32x32x16
-__device__ __forceinline__ void mma_slice(const __bf16 (*As)[kGLd], const __bf16 (*Bs)[kGLd],
+__device__ __forceinline__ void mma_slice(const h16 (*As)[kGLd], const h16 (*Bs)[kGLd],
                                           int wr, int wc, int l32, int h, f32x16 (&acc)[2][2]) {
 #pragma unroll
   for (int ks = 0; ks < 2; ++ks) {
-    bf16x8 a[2], b[2];
+    h16x8 a[2], b[2];
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
-      a[t] = *reinterpret_cast<const bf16x8*>(&As[wr * 64 + t * 32 + l32][ks * 16 + h * 8]);
-      b[t] = *reinterpret_cast<const bf16x8*>(&Bs[wc * 64 + t * 32 + l32][ks * 16 + h * 8]);
+      a[t] = *reinterpret_cast<const h16x8*>(&As[wr * 64 + t * 32 + l32][ks * 16 + h * 8]);
+      b[t] = *reinterpret_cast<const h16x8*>(&Bs[wc * 64 + t * 32 + l32][ks * 16 + h * 8]);
     }
 #pragma unroll
     for (int bm = 0; bm < 2; ++bm)
 #pragma unroll
       for (int bn = 0; bn < 2; ++bn)
-        acc[bm][bn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[bm], b[bn], acc[bm][bn], 0, 0, 0);
+        acc[bm][bn] = mfma32_h16(a[bm], b[bn], acc[bm][bn]);
   }
 }
 
 // stage rows [r0, r0+128) x k [k0, k0+32) of a row-major [R, K] fp32 matrix as bf16
 template <bool VEC>
 __device__ __forceinline__ void stage_rows(const float* __restrict__ S, int64_t R, int K,
-                                           int64_t r0, int k0, __bf16 (*D)[kGLd], int tid) {
+                                           int64_t r0, int k0, h16 (*D)[kGLd], int tid) {
   if (VEC) {  // K % 4 == 0: float4 loads, 4 per thread
 #pragma unroll
     for (int it = 0; it < 4; ++it) {
@@ -54,12 +74,12 @@ __device__ __forceinline__ void stage_rows(const float* __restrict__ S, int64_t 
       const int64_t row = r0 + r;
       float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
       if (row < R && k0 + kc < K) v = *reinterpret_cast<const float4*>(S + row * K + k0 + kc);
-      bf16x4 o;
-      o[0] = (__bf16)v.x;
-      o[1] = (__bf16)v.y;
-      o[2] = (__bf16)v.z;
-      o[3] = (__bf16)v.w;
-      *reinterpret_cast<bf16x4*>(&D[r][kc]) = o;
+      h16x4 o;
+      o[0] = (h16)v.x;
+      o[1] = (h16)v.y;
+      o[2] = (h16)v.z;
+      o[3] = (h16)v.w;
+      *reinterpret_cast<h16x4*>(&D[r][kc]) = o;
     }
   } else {
 #pragma unroll 4
@@ -68,7 +88,7 @@ __device__ __forceinline__ void stage_rows(const float* __restrict__ S, int64_t 
       const int r = e >> 5, k = e & 31;
       const int64_t row = r0 + r;
       const float v = (row < R && k0 + k < K) ? S[row * K + k0 + k] : 0.0f;
-      D[r][k] = (__bf16)v;
+      D[r][k] = (h16)v;
     }
   }
 }
@@ -91,17 +111,17 @@ __device__ __forceinline__ void load_rows(const float* __restrict__ S, int64_t R
   }
 }
 
-__device__ __forceinline__ void store_rows(const RowRegs& g, __bf16 (*D)[kGLd], int tid) {
+__device__ __forceinline__ void store_rows(const RowRegs& g, h16 (*D)[kGLd], int tid) {
 #pragma unroll
   for (int it = 0; it < 4; ++it) {
     const int f = tid + 256 * it;
     const int r = f >> 3, kc = (f & 7) * 4;
-    bf16x4 o;
-    o[0] = (__bf16)g.v[it].x;
-    o[1] = (__bf16)g.v[it].y;
-    o[2] = (__bf16)g.v[it].z;
-    o[3] = (__bf16)g.v[it].w;
-    *reinterpret_cast<bf16x4*>(&D[r][kc]) = o;
+    h16x4 o;
+    o[0] = (h16)g.v[it].x;
+    o[1] = (h16)g.v[it].y;
+    o[2] = (h16)g.v[it].z;
+    o[3] = (h16)g.v[it].w;
+    *reinterpret_cast<h16x4*>(&D[r][kc]) = o;
   }
 }
 
@@ -111,8 +131,8 @@ __global__ __launch_bounds__(256) void gemm_nt_bf16_kernel(const float* __restri
                                                            int O, const float* __restrict__ scale,
                                                            const float* __restrict__ shift,
                                                            int relu, float* __restrict__ C) {
-  __shared__ __attribute__((aligned(16))) __bf16 As[kGT][kGLd];
-  __shared__ __attribute__((aligned(16))) __bf16 Bs[kGT][kGLd];
+  __shared__ __attribute__((aligned(16))) h16 As[kGT][kGLd];
+  __shared__ __attribute__((aligned(16))) h16 Bs[kGT][kGLd];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wr = wid >> 1, wc = wid & 1, h = lane >> 5, l32 = lane & 31;
   const int64_t m0 = (int64_t)blockIdx.x * kGT;
@@ -179,18 +199,18 @@ __device__ __forceinline__ void load_cols(const float* __restrict__ S, int64_t M
   }
 }
 
-__device__ __forceinline__ void store_cols(const ColRegs& g, __bf16 (*D)[kGLd], int tid,
+__device__ __forceinline__ void store_cols(const ColRegs& g, h16 (*D)[kGLd], int tid,
                                            float* colsum) {
   const int c = tid & 127, half = tid >> 7;
-  bf16x8 f[2];
+  h16x8 f[2];
   float s = 0.0f;
 #pragma unroll
   for (int j = 0; j < 16; ++j) {
     s += g.v[j];
-    f[j >> 3][j & 7] = (__bf16)g.v[j];
+    f[j >> 3][j & 7] = (h16)g.v[j];
   }
-  *reinterpret_cast<bf16x8*>(&D[c][half * 16]) = f[0];
-  *reinterpret_cast<bf16x8*>(&D[c][half * 16 + 8]) = f[1];
+  *reinterpret_cast<h16x8*>(&D[c][half * 16]) = f[0];
+  *reinterpret_cast<h16x8*>(&D[c][half * 16 + 8]) = f[1];
   if (colsum) *colsum += s;
 }
 
@@ -199,8 +219,8 @@ __global__ __launch_bounds__(256) void wgrad_bf16_kernel(const float* __restrict
                                                          int I, int O, int64_t rows_per_chunk,
                                                          int tiles_i, float* __restrict__ partW,
                                                          float* __restrict__ partB) {
-  __shared__ __attribute__((aligned(16))) __bf16 As[kGT][kGLd];  // dZ^T: [o][m]
-  __shared__ __attribute__((aligned(16))) __bf16 Bs[kGT][kGLd];  // X^T:  [i][m]
+  __shared__ __attribute__((aligned(16))) h16 As[kGT][kGLd];  // dZ^T: [o][m]
+  __shared__ __attribute__((aligned(16))) h16 Bs[kGT][kGLd];  // X^T:  [i][m]
   __shared__ float bred[kGT];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wr = wid >> 1, wc = wid & 1, h = lane >> 5, l32 = lane & 31;
@@ -314,13 +334,8 @@ static Bf16WgradPlan bf16_wgrad_plan(int64_t M, int64_t I, int64_t O) {
   return p;
 }
 
-}  // namespace pcst
-
-using namespace pcst;
-
-extern "C" int pcst_gemm_nt_bf16(const float* A, int64_t M, int64_t K, const float* B, int64_t O,
-                                 const float* scale, const float* shift, int relu, float* C,
-                                 void* stream) {
+int gemm_nt_impl(const float* A, int64_t M, int64_t K, const float* B, int64_t O,
+                 const float* scale, const float* shift, int relu, float* C, void* stream) {
   PCST_CHECK_ARG(M >= 0 && K > 0 && O > 0 && K < (1 << 20) && O < (1 << 20),
                  "gemm_nt_bf16: bad shape");
   if (M == 0) return PCST_OK;
@@ -337,17 +352,15 @@ extern "C" int pcst_gemm_nt_bf16(const float* A, int64_t M, int64_t K, const flo
   return PCST_OK;
 }
 
-extern "C" int pcst_linear_wgrad_bf16_workspace_size(int64_t M, int64_t I, int64_t O,
-                                                     size_t* bytes) {
+int wgrad16_workspace_impl(int64_t M, int64_t I, int64_t O, size_t* bytes) {
   PCST_CHECK_ARG(M >= 0 && I > 0 && O > 0 && bytes, "linear_wgrad_bf16_workspace_size: bad args");
   const Bf16WgradPlan p = bf16_wgrad_plan(std::max<int64_t>(M, 1), I, O);
   *bytes = sizeof(float) * (size_t)p.chunks * (size_t)(O * I + O);
   return PCST_OK;
 }
 
-extern "C" int pcst_linear_wgrad_bf16(const float* dZ, const float* X, int64_t M, int64_t I,
-                                      int64_t O, float* dW, float* db, void* workspace,
-                                      void* stream) {
+int wgrad16_impl(const float* dZ, const float* X, int64_t M, int64_t I, int64_t O, float* dW,
+                 float* db, void* workspace, void* stream) {
   PCST_CHECK_ARG(M >= 0 && I > 0 && O > 0 && I < (1 << 20) && O < (1 << 20),
                  "linear_wgrad_bf16: bad shape");
   PCST_CHECK_ARG(dW && workspace && (M == 0 || (dZ && X)), "linear_wgrad_bf16: null pointer");
@@ -379,3 +392,29 @@ extern "C" int pcst_linear_wgrad_bf16(const float* dZ, const float* X, int64_t M
   PCST_LAUNCH_CHECK("linear_wgrad_bf16");
   return PCST_OK;
 }
+
+}  // namespace PCST_H16_NS
+}  // namespace pcst
+
+#if !PCST_H16_F16
+// C entry points (include/pcst.h): `f16` picks the operand format the fp32 inputs are rounded
+// to -- 0 bf16, 1 fp16 (the reference trainer's autocast dtype).
+extern "C" int pcst_gemm_nt_bf16(const float* A, int64_t M, int64_t K, const float* B, int64_t O,
+                                 const float* scale, const float* shift, int relu, float* C,
+                                 int f16, void* stream) {
+  return f16 ? pcst::f16m::gemm_nt_impl(A, M, K, B, O, scale, shift, relu, C, stream)
+             : pcst::bf16m::gemm_nt_impl(A, M, K, B, O, scale, shift, relu, C, stream);
+}
+
+extern "C" int pcst_linear_wgrad_bf16_workspace_size(int64_t M, int64_t I, int64_t O,
+                                                     size_t* bytes) {
+  return pcst::bf16m::wgrad16_workspace_impl(M, I, O, bytes);
+}
+
+extern "C" int pcst_linear_wgrad_bf16(const float* dZ, const float* X, int64_t M, int64_t I,
+                                      int64_t O, float* dW, float* db, void* workspace, int f16,
+                                      void* stream) {
+  return f16 ? pcst::f16m::wgrad16_impl(dZ, X, M, I, O, dW, db, workspace, stream)
+             : pcst::bf16m::wgrad16_impl(dZ, X, M, I, O, dW, db, workspace, stream);
+}
+#endif

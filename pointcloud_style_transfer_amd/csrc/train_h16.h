@@ -1,0 +1,37 @@
+// The 16-bit-operand training GEMMs (train_mlp.hip, train_gemm.hip) are compiled twice: as
+// themselves for bf16 (namespace pcst::bf16m) and through train_*_f16.hip for fp16
+// (pcst::f16m).  The C entry points, defined in the bf16 build, dispatch on their `f16` argument.
+#pragma once
+#include <stddef.h>
+#include <stdint.h>
+
+#if defined(PCST_H16_F16) && PCST_H16_F16
+#define PCST_H16_NS f16m
+#else
+#define PCST_H16_NS bf16m
+#endif
+
+namespace pcst {
+#define PCST_H16_DECLS                                                                              \
+  int gemm_ex_impl(const void* A, int a_bf16, int64_t M, int64_t K, const void* B, int b_bf16,     \
+                   int64_t O, const float* bias, int relu, int epilogue, const void* aux,          \
+                   uint64_t seed, float drop_p, int64_t group_rows, void* C, uint16_t* C2,         \
+                   void* stream);                                                                  \
+  int dropout_grad_impl(const float* g, int64_t n, uint64_t seed, float drop_p, uint16_t* out,     \
+                        void* stream);                                                             \
+  int wgrad_ex_workspace_impl(int64_t M, int64_t I, int64_t O, size_t* bytes);                     \
+  int wgrad_ex_impl(const void* dZ, int dz_bf16, const void* X, int x_bf16, int64_t M, int64_t I, \
+                    int64_t O, float* dW, float* db, void* workspace, void* stream);               \
+  int gemm_nt_impl(const float* A, int64_t M, int64_t K, const float* B, int64_t O,               \
+                   const float* scale, const float* shift, int relu, float* C, void* stream);      \
+  int wgrad16_workspace_impl(int64_t M, int64_t I, int64_t O, size_t* bytes);                      \
+  int wgrad16_impl(const float* dZ, const float* X, int64_t M, int64_t I, int64_t O, float* dW,    \
+                   float* db, void* workspace, void* stream);
+namespace bf16m {
+PCST_H16_DECLS
+}
+namespace f16m {
+PCST_H16_DECLS
+}
+#undef PCST_H16_DECLS
+}  // namespace pcst

@@ -23,14 +23,46 @@
 // wgrad_ex stages dZ and X row-major (coalesced) and feeds both MFMA operands with
 // ds_read_b64_tr_b16 transposed reads; the M reduction is split into chunks whose partials are
 // combined in chunk order (deterministic), as csrc/train_gemm.hip does.
+//
+// 16-bit operand format: this file is compiled twice (Makefile), as itself for bf16 and through
+// train_mlp_f16.hip (PCST_H16_F16 = 1) for fp16 -- the autocast dtype of the reference's CUDA
+// trainer (training/trainer.py:50,78; v_mfma_f32_32x32x16_f16 runs at the bf16 rate).  The
+// kernels live in pcst::bf16m / pcst::f16m; the C entry points (bf16 build) dispatch on `f16`.
 #include "common.h"
+#include "train_h16.h"
+
+#ifndef PCST_H16_F16
+#define PCST_H16_F16 0
+#endif
 
 namespace pcst {
+namespace PCST_H16_NS {
 
 typedef __attribute__((ext_vector_type(16))) float f32x16;
-typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
-typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+#if PCST_H16_F16
+typedef _Float16 h16;
+#else
+typedef __bf16 h16;
+#endif
+typedef __attribute__((ext_vector_type(8))) h16 h16x8;
+typedef __attribute__((ext_vector_type(4))) h16 h16x4;
 typedef short v4i16 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ f32x16 mfma32_h16(h16x8 a, h16x8 b, f32x16 c) {
+#if PCST_H16_F16
+  return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+#else
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+#endif
+}
+// 16-bit storage bits -> float
+__device__ __forceinline__ float h16_to_f32(uint32_t bits16) {
+#if PCST_H16_F16
+  return (float)__builtin_bit_cast(_Float16, (uint16_t)bits16);
+#else
+  return __uint_as_float(bits16 << 16);
+#endif
+}
 
 enum { EP_F32 = 0, EP_BF16 = 1, EP_RESID_DROP = 2, EP_RELU_MASK = 3, EP_ADD = 4, EP_COND = 5 };
 
@@ -70,17 +102,17 @@ struct XStage<float> {  // K % 4 == 0
                                        : make_float4(0.f, 0.f, 0.f, 0.f);
     }
   }
-  __device__ __forceinline__ void store(__bf16 (*D)[kXLd], int tid) const {
+  __device__ __forceinline__ void store(h16 (*D)[kXLd], int tid) const {
 #pragma unroll
     for (int it = 0; it < 4; ++it) {
       const int f = tid + 256 * it;
       const int r = f >> 3, kc = (f & 7) * 4;
-      bf16x4 o;
-      o[0] = (__bf16)v[it].x;
-      o[1] = (__bf16)v[it].y;
-      o[2] = (__bf16)v[it].z;
-      o[3] = (__bf16)v[it].w;
-      *reinterpret_cast<bf16x4*>(&D[r][kc]) = o;
+      h16x4 o;
+      o[0] = (h16)v[it].x;
+      o[1] = (h16)v[it].y;
+      o[2] = (h16)v[it].z;
+      o[3] = (h16)v[it].w;
+      *reinterpret_cast<h16x4*>(&D[r][kc]) = o;
     }
   }
 };
@@ -99,7 +131,7 @@ struct XStage<uint16_t> {  // bf16 storage, K % 8 == 0
                                        : make_uint4(0u, 0u, 0u, 0u);
     }
   }
-  __device__ __forceinline__ void store(__bf16 (*D)[kXLd], int tid) const {
+  __device__ __forceinline__ void store(h16 (*D)[kXLd], int tid) const {
 #pragma unroll
     for (int it = 0; it < 2; ++it) {
       const int f = tid + 256 * it;
@@ -110,21 +142,21 @@ struct XStage<uint16_t> {  // bf16 storage, K % 8 == 0
 };
 
 // one 32-deep k slice: 2 x 2 blocks x 2 k-steps of 32x32x16
-__device__ __forceinline__ void xmma_slice(const __bf16 (*As)[kXLd], const __bf16 (*Bs)[kXLd],
+__device__ __forceinline__ void xmma_slice(const h16 (*As)[kXLd], const h16 (*Bs)[kXLd],
                                            int wr, int wc, int l32, int h, f32x16 (&acc)[2][2]) {
 #pragma unroll
   for (int ks = 0; ks < 2; ++ks) {
-    bf16x8 a[2], b[2];
+    h16x8 a[2], b[2];
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
-      a[t] = *reinterpret_cast<const bf16x8*>(&As[wr * 64 + t * 32 + l32][ks * 16 + h * 8]);
-      b[t] = *reinterpret_cast<const bf16x8*>(&Bs[wc * 64 + t * 32 + l32][ks * 16 + h * 8]);
+      a[t] = *reinterpret_cast<const h16x8*>(&As[wr * 64 + t * 32 + l32][ks * 16 + h * 8]);
+      b[t] = *reinterpret_cast<const h16x8*>(&Bs[wc * 64 + t * 32 + l32][ks * 16 + h * 8]);
     }
 #pragma unroll
     for (int bm = 0; bm < 2; ++bm)
 #pragma unroll
       for (int bn = 0; bn < 2; ++bn)
-        acc[bm][bn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[bm], b[bn], acc[bm][bn], 0, 0, 0);
+        acc[bm][bn] = mfma32_h16(a[bm], b[bn], acc[bm][bn]);
   }
 }
 
@@ -141,12 +173,12 @@ struct GemmExArgs {
 };
 
 __device__ __forceinline__ void store4_bf16(uint16_t* p, float a, float b, float c, float d) {
-  bf16x4 o;
-  o[0] = (__bf16)a;
-  o[1] = (__bf16)b;
-  o[2] = (__bf16)c;
-  o[3] = (__bf16)d;
-  *reinterpret_cast<bf16x4*>(p) = o;
+  h16x4 o;
+  o[0] = (h16)a;
+  o[1] = (h16)b;
+  o[2] = (h16)c;
+  o[3] = (h16)d;
+  *reinterpret_cast<h16x4*>(p) = o;
 }
 
 // epilogue: two passes of 64 rows through LDS; thread -> (column quad tid % 32, rows
@@ -239,7 +271,7 @@ __device__ __forceinline__ void gemm_epilogue(const f32x16 (&acc)[2][2], float (
           store4_bf16(out, y[0], y[1], y[2], y[3]);
         } else {
           for (int u = 0; u < nv; ++u) {
-            const __bf16 b = (__bf16)y[u];
+            const h16 b = (h16)y[u];
             out[u] = __builtin_bit_cast(uint16_t, b);
           }
         }
@@ -251,7 +283,7 @@ __device__ __forceinline__ void gemm_epilogue(const f32x16 (&acc)[2][2], float (
         } else {
           for (int u = 0; u < nv; ++u) {
             out[u] = y[u];
-            if (args.C2) args.C2[e + u] = __builtin_bit_cast(uint16_t, (__bf16)y[u]);
+            if (args.C2) args.C2[e + u] = __builtin_bit_cast(uint16_t, (h16)y[u]);
           }
         }
       }
@@ -267,8 +299,8 @@ __global__ __launch_bounds__(256) void gemm_ex_kernel(const TA* __restrict__ A, 
   constexpr int kStageBytes = 2 * kXT * kXLd * 2;  // As + Bs
   constexpr int kEpiBytes = 64 * kCLd * 4;         // half the C tile, fp32
   __shared__ __attribute__((aligned(16))) char smem[kStageBytes > kEpiBytes ? kStageBytes : kEpiBytes];
-  __bf16 (*As)[kXLd] = reinterpret_cast<__bf16 (*)[kXLd]>(smem);
-  __bf16 (*Bs)[kXLd] = reinterpret_cast<__bf16 (*)[kXLd]>(smem + kXT * kXLd * 2);
+  h16 (*As)[kXLd] = reinterpret_cast<h16 (*)[kXLd]>(smem);
+  h16 (*Bs)[kXLd] = reinterpret_cast<h16 (*)[kXLd]>(smem + kXT * kXLd * 2);
   float (*Cs)[kCLd] = reinterpret_cast<float (*)[kCLd]>(smem);
 
   // XCD-aware tile order: workgroup L runs on XCD L % 8; tile t = xcd * per_xcd + L / 8, so the
@@ -342,7 +374,7 @@ __device__ __forceinline__ void bf_load(rsrc_t ra, rsrc_t rb, const uint32_t (&v
   }
 }
 
-__device__ __forceinline__ void bf_store(const BfRegs& g, __bf16 (*As)[kBLd], __bf16 (*Bs)[kBLd],
+__device__ __forceinline__ void bf_store(const BfRegs& g, h16 (*As)[kBLd], h16 (*Bs)[kBLd],
                                          int tid) {
 #pragma unroll
   for (int it = 0; it < kBIt; ++it) {
@@ -358,30 +390,30 @@ __device__ __forceinline__ void lds_barrier() {
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
-__device__ __forceinline__ void bf_mma(const __bf16 (*As)[kBLd], const __bf16 (*Bs)[kBLd], int wr,
+__device__ __forceinline__ void bf_mma(const h16 (*As)[kBLd], const h16 (*Bs)[kBLd], int wr,
                                        int wc, int l32, int h, f32x16 (&acc)[2][2]) {
 #pragma unroll
   for (int ks = 0; ks < kBK / 16; ++ks) {
-    bf16x8 a[2], b[2];
+    h16x8 a[2], b[2];
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
-      a[t] = *reinterpret_cast<const bf16x8*>(&As[wr * 64 + t * 32 + l32][ks * 16 + h * 8]);
-      b[t] = *reinterpret_cast<const bf16x8*>(&Bs[wc * 64 + t * 32 + l32][ks * 16 + h * 8]);
+      a[t] = *reinterpret_cast<const h16x8*>(&As[wr * 64 + t * 32 + l32][ks * 16 + h * 8]);
+      b[t] = *reinterpret_cast<const h16x8*>(&Bs[wc * 64 + t * 32 + l32][ks * 16 + h * 8]);
     }
 #pragma unroll
     for (int bm = 0; bm < 2; ++bm)
 #pragma unroll
       for (int bn = 0; bn < 2; ++bn)
-        acc[bm][bn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[bm], b[bn], acc[bm][bn], 0, 0, 0);
+        acc[bm][bn] = mfma32_h16(a[bm], b[bn], acc[bm][bn]);
   }
 }
 
 __device__ __forceinline__ uint2 pack4_bf16(float a, float b, float c, float d) {
-  bf16x4 o;
-  o[0] = (__bf16)a;
-  o[1] = (__bf16)b;
-  o[2] = (__bf16)c;
-  o[3] = (__bf16)d;
+  h16x4 o;
+  o[0] = (h16)a;
+  o[1] = (h16)b;
+  o[2] = (h16)c;
+  o[3] = (h16)d;
   return *reinterpret_cast<const uint2*>(&o);
 }
 
@@ -476,7 +508,7 @@ __global__ __launch_bounds__(256) void gemm_bf_kernel(const uint16_t* __restrict
   constexpr int kStage = 4 * kBuf;      // A, B x two buffers
   constexpr int kEpi = 64 * kCLd * 4;
   __shared__ __attribute__((aligned(16))) char smem[kStage > kEpi ? kStage : kEpi];
-  typedef __bf16 Row[kBLd];
+  typedef h16 Row[kBLd];
   Row* As0 = reinterpret_cast<Row*>(smem);
   Row* Bs0 = reinterpret_cast<Row*>(smem + kBuf);
   Row* As1 = reinterpret_cast<Row*>(smem + 2 * kBuf);
@@ -552,13 +584,13 @@ __device__ __forceinline__ void dma_slice(rsrc_t ra, rsrc_t rb, uint32_t va0, ui
 // counted lgkmcnt tied to the registers it guards (as csrc/noise_mlp.hip does), so no MFMA
 // is scheduled above it; the vm_barrier before the reads makes the slice's DMA complete.
 template <int OFF>
-__device__ __forceinline__ bf16x8 dma_read(uint32_t addr) {
-  bf16x8 v;
+__device__ __forceinline__ h16x8 dma_read(uint32_t addr) {
+  h16x8 v;
   asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(v) : "v"(addr), "i"(OFF));
   return v;
 }
 template <int N>
-__device__ __forceinline__ void dma_wait4(bf16x8& a, bf16x8& b, bf16x8& c, bf16x8& d) {
+__device__ __forceinline__ void dma_wait4(h16x8& a, h16x8& b, h16x8& c, h16x8& d) {
   asm volatile("s_waitcnt lgkmcnt(%4)" : "+v"(a), "+v"(b), "+v"(c), "+v"(d) : "n"(N));
 }
 
@@ -576,21 +608,21 @@ __device__ __forceinline__ DmaLane dma_lane_offsets(int wr, int wc, int l32, int
 
 __device__ __forceinline__ void dma_mma(const char* stage, const DmaLane& ln, f32x16 (&acc)[2][2]) {
   const uint32_t base = (uint32_t)(uintptr_t)stage;
-  bf16x8 a0 = dma_read<0>(base + ln.a0), a1 = dma_read<2048>(base + ln.a0);
-  bf16x8 b0 = dma_read<0>(base + ln.b0), b1 = dma_read<2048>(base + ln.b0);
-  bf16x8 c0 = dma_read<0>(base + ln.a1), c1 = dma_read<2048>(base + ln.a1);
-  bf16x8 d0 = dma_read<0>(base + ln.b1), d1 = dma_read<2048>(base + ln.b1);
+  h16x8 a0 = dma_read<0>(base + ln.a0), a1 = dma_read<2048>(base + ln.a0);
+  h16x8 b0 = dma_read<0>(base + ln.b0), b1 = dma_read<2048>(base + ln.b0);
+  h16x8 c0 = dma_read<0>(base + ln.a1), c1 = dma_read<2048>(base + ln.a1);
+  h16x8 d0 = dma_read<0>(base + ln.b1), d1 = dma_read<2048>(base + ln.b1);
   dma_wait4<4>(a0, a1, b0, b1);
-  acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b0, acc[0][0], 0, 0, 0);
-  acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b1, acc[0][1], 0, 0, 0);
-  acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b0, acc[1][0], 0, 0, 0);
-  acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b1, acc[1][1], 0, 0, 0);
+  acc[0][0] = mfma32_h16(a0, b0, acc[0][0]);
+  acc[0][1] = mfma32_h16(a0, b1, acc[0][1]);
+  acc[1][0] = mfma32_h16(a1, b0, acc[1][0]);
+  acc[1][1] = mfma32_h16(a1, b1, acc[1][1]);
   __builtin_amdgcn_sched_barrier(0);  // k-step 0's MFMAs stay above k-step 1's wait
   dma_wait4<0>(c0, c1, d0, d1);
-  acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(c0, d0, acc[0][0], 0, 0, 0);
-  acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(c0, d1, acc[0][1], 0, 0, 0);
-  acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(c1, d0, acc[1][0], 0, 0, 0);
-  acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(c1, d1, acc[1][1], 0, 0, 0);
+  acc[0][0] = mfma32_h16(c0, d0, acc[0][0]);
+  acc[0][1] = mfma32_h16(c0, d1, acc[0][1]);
+  acc[1][0] = mfma32_h16(c1, d0, acc[1][0]);
+  acc[1][1] = mfma32_h16(c1, d1, acc[1][1]);
 }
 
 template <int S>
@@ -670,11 +702,11 @@ __global__ void dropout_grad_kernel(const float4* __restrict__ g, int64_t n4, ui
       const bool keep = drop_hash(slo, shi, (uint64_t)(4 * q + u)) >= thr;
       y[u] = keep ? vs[u] * scale : 0.0f;
     }
-    bf16x4 o;
-    o[0] = (__bf16)y[0];
-    o[1] = (__bf16)y[1];
-    o[2] = (__bf16)y[2];
-    o[3] = (__bf16)y[3];
+    h16x4 o;
+    o[0] = (h16)y[0];
+    o[1] = (h16)y[1];
+    o[2] = (h16)y[2];
+    o[3] = (h16)y[3];
     out[q] = *reinterpret_cast<const uint2*>(&o);
   }
 }
@@ -705,12 +737,12 @@ struct WStage<float> {  // Cn % 4 == 0: thread -> (column quad tid % 32, rows ti
 #pragma unroll
     for (int it = 0; it < 4; ++it) {
       const int r = (tid >> 5) + 8 * it;
-      bf16x4 o;
-      o[0] = (__bf16)v[it].x;
-      o[1] = (__bf16)v[it].y;
-      o[2] = (__bf16)v[it].z;
-      o[3] = (__bf16)v[it].w;
-      *reinterpret_cast<bf16x4*>(D + r * kWLdB + cq * 2) = o;
+      h16x4 o;
+      o[0] = (h16)v[it].x;
+      o[1] = (h16)v[it].y;
+      o[2] = (h16)v[it].z;
+      o[3] = (h16)v[it].w;
+      *reinterpret_cast<h16x4*>(D + r * kWLdB + cq * 2) = o;
       if (csum) {  // unrounded fp32 column sums
         csum[0] += v[it].x;
         csum[1] += v[it].y;
@@ -745,8 +777,8 @@ struct WStage<uint16_t> {  // Cn % 8 == 0: thread -> (column octet tid % 16, row
         const uint32_t w[4] = {v[it].x, v[it].y, v[it].z, v[it].w};
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
-          csum[2 * u] += __uint_as_float(w[u] << 16);
-          csum[2 * u + 1] += __uint_as_float(w[u] & 0xffff0000u);
+          csum[2 * u] += h16_to_f32(w[u] & 0xffffu);
+          csum[2 * u + 1] += h16_to_f32(w[u] >> 16);
         }
       }
     }
@@ -756,16 +788,16 @@ struct WStage<uint16_t> {  // Cn % 8 == 0: thread -> (column octet tid % 16, row
 
 // 32x32x16 operand fragment of columns [c, c+32) x rows [k, k+16) of a [row][col] bf16 image:
 // lane l gets column c + l % 32, rows k + 8 (l / 32) + 0..7 (two ds_read_b64_tr_b16)
-__device__ __forceinline__ bf16x8 tr_frag(const char* img, int c, int k, int lane) {
+__device__ __forceinline__ h16x8 tr_frag(const char* img, int c, int k, int lane) {
   const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
   const char* base = img + (k + 8 * (g >> 1) + q) * kWLdB + (c + 16 * (g & 1) + 4 * p) * 2;
   typedef __attribute__((address_space(3))) v4i16 lds_v4i16;
   const v4i16 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(base));
   const v4i16 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(base + 4 * kWLdB));
-  bf16x8 f;
+  h16x8 f;
   const short s[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
 #pragma unroll
-  for (int u = 0; u < 8; ++u) f[u] = __builtin_bit_cast(__bf16, s[u]);
+  for (int u = 0; u < 8; ++u) f[u] = __builtin_bit_cast(h16, s[u]);
   return f;
 }
 
@@ -811,7 +843,7 @@ __global__ __launch_bounds__(256) void wgrad_ex_kernel(const TZ* __restrict__ dZ
     }
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
-      bf16x8 a[2], b[2];
+      h16x8 a[2], b[2];
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
         a[u] = tr_frag(Zs, wr * 64 + u * 32, ks * 16, lane);
@@ -821,7 +853,7 @@ __global__ __launch_bounds__(256) void wgrad_ex_kernel(const TZ* __restrict__ dZ
       for (int bm = 0; bm < 2; ++bm)
 #pragma unroll
         for (int bn = 0; bn < 2; ++bn)
-          acc[bm][bn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[bm], b[bn], acc[bm][bn], 0, 0, 0);
+          acc[bm][bn] = mfma32_h16(a[bm], b[bn], acc[bm][bn]);
     }
     __syncthreads();
   }
@@ -906,10 +938,6 @@ static uint32_t drop_threshold(float p) {
   return t <= 0.0 ? 0u : (t >= 4294967295.0 ? 0xffffffffu : (uint32_t)t);
 }
 
-}  // namespace pcst
-
-using namespace pcst;
-
 #define PCST_GEMM_EX(TA, TB, EPV)                                                                  \
   hipLaunchKernelGGL((gemm_ex_kernel<TA, TB, EPV>), dim3((unsigned)(8 * per)), dim3(256), 0, s,     \
                      static_cast<const TA*>(A), M, (int)K, static_cast<const TB*>(B), (int)O,        \
@@ -984,10 +1012,10 @@ static void launch_gemm_bf(int ep, bool fast, const void* A, int64_t M, int64_t 
 }
 #undef PCST_GEMM_BF
 
-extern "C" int pcst_gemm_ex(const void* A, int a_bf16, int64_t M, int64_t K, const void* B,
-                            int b_bf16, int64_t O, const float* bias, int relu, int epilogue,
-                            const void* aux, uint64_t seed, float drop_p, int64_t group_rows,
-                            void* C, uint16_t* C2, void* stream) {
+int gemm_ex_impl(const void* A, int a_bf16, int64_t M, int64_t K, const void* B, int b_bf16,
+                 int64_t O, const float* bias, int relu, int epilogue, const void* aux,
+                 uint64_t seed, float drop_p, int64_t group_rows, void* C, uint16_t* C2,
+                 void* stream) {
   PCST_CHECK_ARG(M >= 0 && K > 0 && O > 0 && K < (1 << 20) && O < (1 << 20), "gemm_ex: bad shape");
   PCST_CHECK_ARG(epilogue >= EP_F32 && epilogue <= EP_COND, "gemm_ex: bad epilogue");
   PCST_CHECK_ARG(K % (a_bf16 ? 8 : 4) == 0 && K % (b_bf16 ? 8 : 4) == 0,
@@ -1037,8 +1065,8 @@ extern "C" int pcst_gemm_ex(const void* A, int a_bf16, int64_t M, int64_t K, con
   return PCST_OK;
 }
 
-extern "C" int pcst_dropout_grad_bf16(const float* g, int64_t n, uint64_t seed, float drop_p,
-                                      uint16_t* out, void* stream) {
+int dropout_grad_impl(const float* g, int64_t n, uint64_t seed, float drop_p, uint16_t* out,
+                      void* stream) {
   PCST_CHECK_ARG(n >= 0 && n % 4 == 0, "dropout_grad_bf16: n must be a multiple of 4");
   PCST_CHECK_ARG(drop_p >= 0.0f && drop_p < 1.0f, "dropout_grad_bf16: p must be in [0, 1)");
   if (n == 0) return PCST_OK;
@@ -1052,16 +1080,15 @@ extern "C" int pcst_dropout_grad_bf16(const float* g, int64_t n, uint64_t seed, 
   return PCST_OK;
 }
 
-extern "C" int pcst_linear_wgrad_ex_workspace_size(int64_t M, int64_t I, int64_t O, size_t* bytes) {
+int wgrad_ex_workspace_impl(int64_t M, int64_t I, int64_t O, size_t* bytes) {
   PCST_CHECK_ARG(M >= 0 && I > 0 && O > 0 && bytes, "linear_wgrad_ex_workspace_size: bad args");
   const WgradExPlan p = wgrad_ex_plan(std::max<int64_t>(M, 1), I, O);
   *bytes = sizeof(float) * (size_t)p.chunks * (size_t)(O * I + O);
   return PCST_OK;
 }
 
-extern "C" int pcst_linear_wgrad_ex(const void* dZ, int dz_bf16, const void* X, int x_bf16,
-                                    int64_t M, int64_t I, int64_t O, float* dW, float* db,
-                                    void* workspace, void* stream) {
+int wgrad_ex_impl(const void* dZ, int dz_bf16, const void* X, int x_bf16, int64_t M, int64_t I,
+                  int64_t O, float* dW, float* db, void* workspace, void* stream) {
   PCST_CHECK_ARG(M >= 0 && I > 0 && O > 0 && I < (1 << 20) && O < (1 << 20), "linear_wgrad_ex: bad shape");
   PCST_CHECK_ARG(I % 8 == 0 && O % 8 == 0, "linear_wgrad_ex: I and O must be multiples of 8");
   PCST_CHECK_ARG(dW && workspace && (M == 0 || (dZ && X)), "linear_wgrad_ex: null pointer");
@@ -1100,3 +1127,37 @@ extern "C" int pcst_linear_wgrad_ex(const void* dZ, int dz_bf16, const void* X, 
   PCST_LAUNCH_CHECK("linear_wgrad_ex");
   return PCST_OK;
 }
+
+}  // namespace PCST_H16_NS
+}  // namespace pcst
+
+#if !PCST_H16_F16
+// C entry points (include/pcst.h): the 16-bit storage flags (a_bf16, ...) mark 16-bit operands,
+// `f16` picks their format -- 0 bf16, 1 fp16 -- for the operands rounded while staged too.
+extern "C" int pcst_gemm_ex(const void* A, int a_bf16, int64_t M, int64_t K, const void* B,
+                            int b_bf16, int64_t O, const float* bias, int relu, int epilogue,
+                            const void* aux, uint64_t seed, float drop_p, int64_t group_rows,
+                            void* C, uint16_t* C2, int f16, void* stream) {
+  return f16 ? pcst::f16m::gemm_ex_impl(A, a_bf16, M, K, B, b_bf16, O, bias, relu, epilogue, aux,
+                                        seed, drop_p, group_rows, C, C2, stream)
+             : pcst::bf16m::gemm_ex_impl(A, a_bf16, M, K, B, b_bf16, O, bias, relu, epilogue, aux,
+                                         seed, drop_p, group_rows, C, C2, stream);
+}
+
+extern "C" int pcst_dropout_grad_bf16(const float* g, int64_t n, uint64_t seed, float drop_p,
+                                      uint16_t* out, int f16, void* stream) {
+  return f16 ? pcst::f16m::dropout_grad_impl(g, n, seed, drop_p, out, stream)
+             : pcst::bf16m::dropout_grad_impl(g, n, seed, drop_p, out, stream);
+}
+
+extern "C" int pcst_linear_wgrad_ex_workspace_size(int64_t M, int64_t I, int64_t O, size_t* bytes) {
+  return pcst::bf16m::wgrad_ex_workspace_impl(M, I, O, bytes);  // the same plan in both formats
+}
+
+extern "C" int pcst_linear_wgrad_ex(const void* dZ, int dz_bf16, const void* X, int x_bf16,
+                                    int64_t M, int64_t I, int64_t O, float* dW, float* db,
+                                    void* workspace, int f16, void* stream) {
+  return f16 ? pcst::f16m::wgrad_ex_impl(dZ, dz_bf16, X, x_bf16, M, I, O, dW, db, workspace, stream)
+             : pcst::bf16m::wgrad_ex_impl(dZ, dz_bf16, X, x_bf16, M, I, O, dW, db, workspace, stream);
+}
+#endif

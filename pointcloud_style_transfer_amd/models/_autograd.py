@@ -7,7 +7,9 @@
             dW = dZ^T X, db = dZ^T 1                  pcst_linear_wgrad (split over row chunks)
 All products are exact-f32 MFMA; the row reduction combines fixed chunks in order (no
 atomics), so gradients are deterministic.  Under torch.autocast (the trainer's use_amp) the same
-three products run on bf16 MFMA (pcst_gemm_nt_bf16 / pcst_linear_wgrad_bf16, csrc/train_gemm.hip).
+three products run on 16-bit MFMA in autocast's dtype -- float16 by default on CUDA, the
+reference trainer's (training/trainer.py:50,78), or bfloat16 (pcst_gemm_nt_bf16 /
+pcst_linear_wgrad_bf16, csrc/train_gemm.hip, f16 flag).
 
 The SetAbstraction training half (csrc/sa_train.hip):
   BNReLUFn       train-mode BatchNorm2d + ReLU (+ max over nsample with its argmax), forward
@@ -23,16 +25,26 @@ import torch
 from .. import _hip
 
 
+def autocast_half():
+    """The 16-bit operand dtype of the CUDA autocast region this runs in (float16 unless the
+    caller asked autocast for bfloat16), or None outside one."""
+    if not torch.is_autocast_enabled("cuda"):
+        return None
+    h = torch.get_autocast_dtype("cuda")
+    return h if h in (torch.float16, torch.bfloat16) else torch.float16
+
+
 class LinearFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, relu):
         x2 = x.reshape(-1, x.shape[-1]).float().contiguous()
         W = weight.reshape(weight.shape[0], -1).float().contiguous()
         b = None if bias is None else bias.float()
-        # under torch.autocast (the trainer's use_amp) the GEMMs run on bf16 MFMA
-        ctx.bf16 = x2.is_cuda and torch.is_autocast_enabled("cuda")
+        # under torch.autocast (the trainer's use_amp) the GEMMs run on 16-bit MFMA
+        ctx.half = autocast_half() if x2.is_cuda else None
+        ctx.bf16 = ctx.half is not None
         if ctx.bf16:
-            y = _hip.gemm_nt_bf16(x2, W, None, b, relu)
+            y = _hip.gemm_nt_bf16(x2, W, None, b, relu, half=ctx.half)
         else:
             y = _hip.pointwise_linear(x2, W, None, b, relu, 0)
         ctx.relu = relu
@@ -50,21 +62,24 @@ class LinearFn(torch.autograd.Function):
             dz = _hip.relu_bwd(dz, y)
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
-            gemm = _hip.gemm_nt_bf16 if ctx.bf16 else _hip.pointwise_linear
-            dx = gemm(dz, W.t().contiguous()).view(ctx.xshape)
+            if ctx.bf16:
+                dx = _hip.gemm_nt_bf16(dz, W.t().contiguous(), half=ctx.half).view(ctx.xshape)
+            else:
+                dx = _hip.pointwise_linear(dz, W.t().contiguous()).view(ctx.xshape)
         need_b = ctx.has_bias and ctx.needs_input_grad[2]
         if ctx.needs_input_grad[1] or need_b:
-            dw, db = _hip.linear_wgrad(dz, x2, bias=need_b, bf16=ctx.bf16)
+            dw, db = _hip.linear_wgrad(dz, x2, bias=need_b, bf16=ctx.bf16,
+                                       half=ctx.half or torch.bfloat16)
             dw = dw.view(ctx.wshape) if ctx.needs_input_grad[1] else None
         return dx, dw, db, None
 
 
-def _bf16(w):
-    return w.detach().to(torch.bfloat16).contiguous()
+def _h(w, half):
+    return w.detach().to(half).contiguous()
 
 
-def _bf16_t(w):
-    return w.detach().t().to(torch.bfloat16).contiguous()
+def _h_t(w, half):
+    return w.detach().t().to(half).contiguous()
 
 
 def _draw_seed(p):
@@ -73,7 +88,8 @@ def _draw_seed(p):
 
 
 def _block_fwd(x, xb, w1, b1, w2, b2, p, seed):
-    """x + Dropout_p(Linear2(ReLU(Linear1(x)))): -> (y fp32, y bf16, h bf16)."""
+    """x + Dropout_p(Linear2(ReLU(Linear1(x)))): -> (y fp32, y 16-bit, h 16-bit); the 16-bit
+    format is that of xb / w1 / w2."""
     h = _hip.gemm_ex(xb, w1, b1, relu=True, epilogue=_hip.EP_BF16)
     y, yb = _hip.gemm_ex(h, w2, b2, epilogue=_hip.EP_RESID_DROP, aux=x, seed=seed, p=p,
                          copy_bf16=True)
@@ -82,7 +98,7 @@ def _block_fwd(x, xb, w1, b1, w2, b2, p, seed):
 
 def _block_bwd(g, xb, h, w1_t, w2_t, p, seed, bias1=True, bias2=True):
     """Backward of _block_fwd from the fp32 gradient g of y: -> (gx, dW1, db1, dW2, db2)."""
-    dd = _hip.dropout_grad_bf16(g, seed, p)
+    dd = _hip.dropout_grad_bf16(g, seed, p, half=xb.dtype)
     dz = _hip.gemm_ex(dd, w2_t, epilogue=_hip.EP_RELU_MASK, aux=h)
     gx = _hip.gemm_ex(dz, w1_t, epilogue=_hip.EP_ADD, aux=g)
     dw2, db2 = _hip.linear_wgrad_ex(dd, h, bias=bias2)
@@ -92,8 +108,9 @@ def _block_bwd(g, xb, h, w1_t, w2_t, p, seed, bias1=True, bias2=True):
 
 class ResidualBlockFn(torch.autograd.Function):
     """x + Dropout_p(Linear2(ReLU(Linear1(x)))) -- one NoisePredictor layer
-    (diffusion_model.py:48-52, applied at :57-58) -- under autocast, with bf16 activation storage
-    and the elementwise work fused into the GEMM epilogues (csrc/train_mlp.hip):
+    (diffusion_model.py:48-52, applied at :57-58) -- under autocast, with 16-bit activation
+    storage in autocast's dtype (written bf16 below; float16 by default) and the elementwise work
+    fused into the GEMM epilogues (csrc/train_mlp.hip):
 
       forward   h  = bf16(relu(x W1^T + b1))                     EP_BF16
                 y  = x + keep * (h W2^T + b2) / (1-p)           EP_RESID_DROP
@@ -110,10 +127,11 @@ class ResidualBlockFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w1, b1, w2, b2, p):
         shape = x.shape
+        half = autocast_half() or torch.bfloat16
         x2 = x.reshape(-1, shape[-1]).float().contiguous()
-        xb = x2.to(torch.bfloat16)
+        xb = x2.to(half)
         seed = _draw_seed(p)
-        y, _, h = _block_fwd(x2, xb, _bf16(w1), b1, _bf16(w2), b2, p, seed)
+        y, _, h = _block_fwd(x2, xb, _h(w1, half), b1, _h(w2, half), b2, p, seed)
         ctx.save_for_backward(xb, h, w1, w2)
         ctx.seed, ctx.p, ctx.shape = seed, p, shape
         ctx.has_b = (b1 is not None, b2 is not None)
@@ -123,8 +141,8 @@ class ResidualBlockFn(torch.autograd.Function):
     def backward(ctx, gy):
         xb, h, w1, w2 = ctx.saved_tensors
         g = gy.reshape(xb.shape).float().contiguous()
-        gx, dw1, db1, dw2, db2 = _block_bwd(g, xb, h, _bf16_t(w1), _bf16_t(w2), ctx.p, ctx.seed,
-                                            *ctx.has_b)
+        gx, dw1, db1, dw2, db2 = _block_bwd(g, xb, h, _h_t(w1, xb.dtype), _h_t(w2, xb.dtype),
+                                            ctx.p, ctx.seed, *ctx.has_b)
         return gx.view(ctx.shape), dw1, db1, dw2, db2, None
 
 
@@ -138,7 +156,8 @@ def residual_block(x, layer, training):
 
 class NoisePredictorFn(torch.autograd.Function):
     """The whole per-point network of NoisePredictor.forward (diffusion_model.py:50-61) under
-    autocast, forward and backward, on the fused bf16-storage GEMMs:
+    autocast, forward and backward, on the fused 16-bit-storage GEMMs (autocast's dtype: float16
+    by default, the reference trainer's; "bf16" below stands for it):
 
       h0 = relu(pts W0^T + b0)             [M,128]  bf16   (pts zero-padded to K = 8)
       h1 = relu(h0 W2^T + b2)              [M,256]  bf16
@@ -166,8 +185,9 @@ class NoisePredictorFn(torch.autograd.Function):
         xp[:, :3] = pts.reshape(M, 3)
         w0p = torch.zeros(w[0].shape[0], 8, dtype=torch.float32, device=dev)
         w0p[:, :3] = w[0].detach()
-        wb = [_bf16(t) if t.dim() == 2 else t.detach() for t in w[2:]]
-        wb = [_bf16(w0p), w[1].detach()] + wb
+        half = autocast_half() or torch.bfloat16
+        wb = [_h(t, half) if t.dim() == 2 else t.detach() for t in w[2:]]
+        wb = [_h(w0p, half), w[1].detach()] + wb
         h0 = _hip.gemm_ex(xp, wb[0], wb[1], relu=True, epilogue=_hip.EP_BF16)
         h1 = _hip.gemm_ex(h0, wb[2], wb[3], relu=True, epilogue=_hip.EP_BF16)
         x, xb = _hip.gemm_ex(h1, wb[4], wb[5], epilogue=_hip.EP_COND,
@@ -185,7 +205,7 @@ class NoisePredictorFn(torch.autograd.Function):
         out = _hip.gemm_ex(q1, wb[34], wb[35], epilogue=_hip.EP_F32)
         saved += [xb, q0, q1]
         ctx.save_for_backward(*saved, *w)
-        ctx.seeds, ctx.ps, ctx.BN = seeds, tuple(ps), (B, N)
+        ctx.seeds, ctx.ps, ctx.BN, ctx.half = seeds, tuple(ps), (B, N), half
         return out.view(B, N, 3)
 
     @staticmethod
@@ -196,6 +216,7 @@ class NoisePredictorFn(torch.autograd.Function):
         xb, q0, q1 = sv[15], sv[16], sv[17]
         w = sv[18:]
         B, N = ctx.BN
+        half = ctx.half
         M = B * N
         dev = gout.device
         grads = [None] * len(w)
@@ -206,16 +227,16 @@ class NoisePredictorFn(torch.autograd.Function):
         grads[34], grads[35] = dw[:3].contiguous(), db[:3].contiguous()
         wo4p = torch.zeros(8, w[34].shape[1], dtype=torch.float32, device=dev)
         wo4p[:3] = w[34].detach()
-        dq1 = _hip.gemm_ex(g3, _bf16_t(wo4p), epilogue=_hip.EP_RELU_MASK, aux=q1)
+        dq1 = _hip.gemm_ex(g3, _h_t(wo4p, half), epilogue=_hip.EP_RELU_MASK, aux=q1)
         grads[32], grads[33] = _hip.linear_wgrad_ex(dq1, q0)
-        dq0 = _hip.gemm_ex(dq1, _bf16_t(w[32]), epilogue=_hip.EP_RELU_MASK, aux=q0)
+        dq0 = _hip.gemm_ex(dq1, _h_t(w[32], half), epilogue=_hip.EP_RELU_MASK, aux=q0)
         grads[30], grads[31] = _hip.linear_wgrad_ex(dq0, xb)
-        g = _hip.gemm_ex(dq0, _bf16_t(w[30]), epilogue=_hip.EP_F32)
+        g = _hip.gemm_ex(dq0, _h_t(w[30], half), epilogue=_hip.EP_F32)
         for k in reversed(range(6)):
             o = 6 + 4 * k
             xbk, hk = blocks[k]
             g, grads[o], grads[o + 1], grads[o + 2], grads[o + 3] = _block_bwd(
-                g, xbk, hk, _bf16_t(w[o]), _bf16_t(w[o + 2]), ctx.ps[k], ctx.seeds[k])
+                g, xbk, hk, _h_t(w[o], half), _h_t(w[o + 2], half), ctx.ps[k], ctx.seeds[k])
         # x = ((pf + tf) + sf): dL/dpf = g, dL/dtf[b] = dL/dsf[b] = sum of g over cloud b's rows
         # per-cloud row sums as one batched GEMV (ones [B,1,N] @ g [B,N,256]): torch's
         # middle-dimension sum reduced this at ~40 % of the HBM rate (254 vs 82 us at B = 8)
@@ -223,9 +244,9 @@ class NoisePredictorFn(torch.autograd.Function):
                          g.view(B, N, -1)).squeeze(1)
         dcond = torch.stack([gsum, gsum], 1)
         grads[4], grads[5] = _hip.linear_wgrad_ex(g, h1)
-        dh1 = _hip.gemm_ex(g, _bf16_t(w[4]), epilogue=_hip.EP_RELU_MASK, aux=h1)
+        dh1 = _hip.gemm_ex(g, _h_t(w[4], half), epilogue=_hip.EP_RELU_MASK, aux=h1)
         grads[2], grads[3] = _hip.linear_wgrad_ex(dh1, h0)
-        dh0 = _hip.gemm_ex(dh1, _bf16_t(w[2]), epilogue=_hip.EP_RELU_MASK, aux=h0)
+        dh0 = _hip.gemm_ex(dh1, _h_t(w[2], half), epilogue=_hip.EP_RELU_MASK, aux=h0)
         dw0, grads[1] = _hip.linear_wgrad_ex(dh0, xp)
         grads[0] = dw0[:, :3].contiguous()
         return (None, dcond, None, *grads)

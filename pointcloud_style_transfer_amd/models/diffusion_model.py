@@ -152,7 +152,8 @@ class NoisePredictor(nn.Module):
         tf = _ag.linear(self.time_embedding(timestep.to(noisy_points.device)), self.time_proj)
         sf = _ag.linear(style_feat, self.style_proj)
         if noisy_points.is_cuda and torch.is_autocast_enabled("cuda"):
-            # the whole per-point network on the bf16-storage fused GEMMs (NoisePredictorFn);
+            # the whole per-point network on the 16-bit-storage fused GEMMs (NoisePredictorFn,
+            # autocast's dtype);
             # each residual block keeps its own Dropout rate
             ps = tuple(float(l[3].p) if self.training else 0.0 for l in self.layers)
             cond = torch.stack([tf.float(), sf.float()], 1)

@@ -17,11 +17,13 @@ and voxel subsets; the EMA is built after the DDP wrap, from rank 0's broadcast 
 validation loss is averaged over ranks before the best/patience decision, so every rank stops
 at the same epoch; the train sampler's epoch is set every epoch.
 
-Precision under `use_amp` (the reference's default): the per-point linear layers run on bf16
-MFMA with fp32 accumulation (models/_autograd.py -> pcst_gemm_nt_bf16 /
-pcst_linear_wgrad_bf16).  That keeps 8 mantissa bits per operand against the 11 of the
-reference's fp16 autocast, with fp32's exponent range; geometry, BN statistics, Chamfer and L1
-stay fp32.  `use_amp=False` runs every product in exact f32 (the gradient parity tests).
+Precision under `use_amp` (the reference's default): the per-point linear layers run on 16-bit
+MFMA with fp32 accumulation (models/_autograd.py -> pcst_gemm_ex / pcst_gemm_nt_bf16 /
+pcst_linear_wgrad_bf16) in `Config.amp_dtype`: float16 by default, the reference's CUDA
+autocast (trainer.py:50,78; 11 mantissa bits, the GradScaler guards the range), or bfloat16
+(8 bits, fp32's exponent range); both run at the same MFMA rate.  Geometry, BN statistics,
+Chamfer and L1 stay fp32.  `use_amp=False` runs every product in exact f32 (the gradient
+parity tests).
 The GradScaler logic is kept as is.  TensorBoard is optional (not installed here).
 """
 from __future__ import annotations
@@ -175,6 +177,12 @@ class DiffusionTrainer:
         loss_dict = {k: v.item() for k, v in terms.items()}
         return loss, loss_dict
 
+    def _amp_dtype(self):
+        name = getattr(self.config, "amp_dtype", "float16")
+        if name not in ("float16", "bfloat16"):
+            raise ValueError(f"Config.amp_dtype must be 'float16' or 'bfloat16', got {name!r}")
+        return getattr(torch, name)
+
     def _forward_backward(self, batch):
         sim = batch["sim_full"].to(self.device)
         real = batch["real_full"].to(self.device)
@@ -182,7 +190,8 @@ class DiffusionTrainer:
         src = _rng.source()
         t = src.randint(0, self.config.num_timesteps, (B,), device=self.device).long()
         noisy, actual_noise = self.diffusion_process.q_sample(sim, t)
-        with autocast(device_type=self.device_type, enabled=self.config.use_amp):
+        with autocast(device_type=self.device_type, enabled=self.config.use_amp,
+                      dtype=self._amp_dtype()):
             pred, indices = self.ddp_model(noisy_points=noisy, timestep=t, condition_points=real,
                                            cond_drop_prob=self.config.cond_drop_prob,
                                            use_hierarchical=self.config.use_hierarchical)

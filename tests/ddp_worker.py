@@ -9,8 +9,10 @@ reference.  Global micro-batch g (rank r, local step b: g = r * MICRO + b) train
 [g * CLOUDS, (g + 1) * CLOUDS) with the draws of rng.CounterRNG(100 + g), so both set-ups see
 the same samples and the same t / noise / cond-drop / voxel / FPS draws.  The gradient each
 optimizer step applies (after clipping) and the parameters after the step are saved (every
-rank's parameters: OUT.rankR.npz for R > 0).  AMP=1 runs the trainer under use_amp (the bf16
-fused NoisePredictor and GEMMs) with the GradScaler disabled, so gradients compare unscaled.
+rank's parameters: OUT.rankR.npz for R > 0).  AMP=1 (or bf16) runs the trainer under use_amp
+with Config.amp_dtype "bfloat16" (the bf16 fused NoisePredictor and GEMMs) and the GradScaler
+disabled, so gradients compare unscaled; AMP=fp16 runs the reference's float16 autocast with the
+GradScaler at a fixed scale (its unscale_ is exact: a power of two).
 """
 import os
 import sys
@@ -24,7 +26,9 @@ sys.path.insert(0, REPO)
 
 def main():
     out, accum, micro, clouds, points = sys.argv[1], *map(int, sys.argv[2:6])
-    amp = len(sys.argv) > 6 and sys.argv[6] == "1"
+    amp_arg = sys.argv[6] if len(sys.argv) > 6 else "0"
+    amp = amp_arg != "0"
+    amp_dtype = "float16" if amp_arg == "fp16" else "bfloat16"
     global_points = int(sys.argv[7]) if len(sys.argv) > 7 else 2048
     from pointcloud_style_transfer_amd import distributed as D
     from pointcloud_style_transfer_amd import rng
@@ -38,7 +42,7 @@ def main():
     os.chdir(tmp)
     cfg = Config(make_dirs=False, log_dir=tmp, checkpoint_dir=tmp, use_amp=amp,
                  gradient_accumulation_steps=accum, global_points=global_points,
-                 precision="fp32")
+                 precision="fp32", amp_dtype=amp_dtype)
     torch.manual_seed(0)
     tr = DiffusionTrainer(cfg, device="cuda:0")
     assert tr.distributed == (world > 1)
@@ -47,7 +51,8 @@ def main():
             m.p = 0.0
     tr.model.train()
     if amp:
-        tr.scaler = torch.amp.GradScaler(enabled=False)
+        tr.scaler = (torch.amp.GradScaler(init_scale=2.0 ** 14, growth_interval=10 ** 9)
+                     if amp_dtype == "float16" else torch.amp.GradScaler(enabled=False))
     grads = {}
     o_step = tr.optimizer.step
 

@@ -1,7 +1,8 @@
 """BASELINE configs at their own sizes on one MI355X:
 
-  configs[2]  DiffusionTrainer.train_step on 8 x 120k-point clouds under use_amp (bf16 MFMA
-              GEMMs) against the same step in exact f32, same draws (rng.CounterRNG);
+  configs[2]  DiffusionTrainer.train_step on 8 x 120k-point clouds under use_amp (16-bit MFMA
+              GEMMs, fp16 by default as the reference, and bf16) against the same step in
+              exact f32, same draws (rng.CounterRNG);
   configs[4]  the per-GPU share of the 256-cloud batch inference: 32 x 120k clouds through the
               hipGraph-captured guided step vs the eager loop; the device-drawn voxel subset of
               all 64 CFG rows (every representative kept, pad points distinct); and one
@@ -31,7 +32,7 @@ def _clouds(seed0, n, points):
     return torch.from_numpy(np.stack([lidar_like_cloud(seed0 + i, points) for i in range(n)]))
 
 
-def _trainer_step_grads(tmp_path, sim, real, amp, lambda_chamfer):
+def _trainer_step_grads(tmp_path, sim, real, amp, lambda_chamfer, amp_dtype="float16"):
     """One DiffusionTrainer.train_step with counter-keyed draws and dropout off -> (loss, the
     gradient as the step computed it, before clipping)."""
     from pointcloud_style_transfer_amd import rng
@@ -40,14 +41,19 @@ def _trainer_step_grads(tmp_path, sim, real, amp, lambda_chamfer):
 
     cfg = Config(make_dirs=False, log_dir=str(tmp_path), checkpoint_dir=str(tmp_path),
                  use_amp=amp, gradient_accumulation_steps=1, batch_size=8,
-                 lambda_chamfer=lambda_chamfer)
+                 lambda_chamfer=lambda_chamfer, amp_dtype=amp_dtype)
     torch.manual_seed(0)
     tr = T.DiffusionTrainer(cfg, device="cuda")
     tr.model.train()
     for m in tr.model.modules():
         if isinstance(m, torch.nn.Dropout):
             m.p = 0.0
-    tr.scaler = torch.amp.GradScaler(enabled=False)  # compare unscaled gradients
+    if not amp or amp_dtype == "bfloat16":
+        tr.scaler = torch.amp.GradScaler(enabled=False)  # compare unscaled gradients
+    else:
+        # fp16 (the reference's autocast) needs the loss scale: the L1 gradient 1/numel sits
+        # in fp16's subnormal range.  Fixed scale; unscale_ (before the snapshot) is exact
+        tr.scaler = torch.amp.GradScaler(init_scale=2.0 ** 14, growth_interval=10 ** 9)
     grads = {}
     clip = torch.nn.utils.clip_grad_norm_
 
@@ -67,9 +73,9 @@ def _trainer_step_grads(tmp_path, sim, real, amp, lambda_chamfer):
 
 
 def test_trainer_step_8x120k_amp_vs_fp32(tmp_path):
-    """configs[2]: one trainer step at B = 8 x 120000 under use_amp (bf16 GEMMs) and in f32,
-    same draws, dropout off: both losses finite, within 2e-2 relative, gradient norms (before
-    clipping) within 10 %.  The gradient DIRECTION is not a bf16-vs-f32 invariant of this
+    """configs[2]: one trainer step at B = 8 x 120000 under use_amp (16-bit GEMMs: fp16, the
+    default, and bf16) and in f32, same draws, dropout off: losses finite, within 2e-2
+    relative, gradient norms (before clipping) within 10 %.  The gradient DIRECTION is not a bf16-vs-f32 invariant of this
     loss: L1's gradient is sign(eps_hat - eps) (bf16 rounding flips the sign of the ~0.4 % of
     elements within its error: |dg|/|g| ~ 2 sqrt(0.004) ~ 0.13) and the Chamfer term acts on
     pred_x0 = (x_t - sqrt(1-a) eps_hat)/sqrt(a), amplifying eps_hat by up to 3e3 and flipping
@@ -79,12 +85,13 @@ def test_trainer_step_8x120k_amp_vs_fp32(tmp_path):
     norm = lambda g: torch.sqrt(sum((v ** 2).sum() for v in g.values())).item()  # noqa: E731
     for lam in (0.1, 0.0):
         l32, g32 = _trainer_step_grads(tmp_path, sim, real, False, lam)
-        l16, g16 = _trainer_step_grads(tmp_path, sim, real, True, lam)
-        print(f"configs[2] lambda_chamfer {lam}: loss f32 {l32:.6f} amp {l16:.6f}; grad norm "
-              f"f32 {norm(g32):.4e} amp {norm(g16):.4e}")
-        assert np.isfinite(l32) and np.isfinite(l16)
-        assert abs(l16 - l32) <= 2e-2 * abs(l32), (l16, l32)
-        assert abs(norm(g16) - norm(g32)) <= 0.10 * norm(g32)
+        for dt in ("float16", "bfloat16"):
+            l16, g16 = _trainer_step_grads(tmp_path, sim, real, True, lam, dt)
+            print(f"configs[2] lambda_chamfer {lam} {dt}: loss f32 {l32:.6f} amp {l16:.6f}; "
+                  f"grad norm f32 {norm(g32):.4e} amp {norm(g16):.4e}")
+            assert np.isfinite(l32) and np.isfinite(l16)
+            assert abs(l16 - l32) <= 2e-2 * abs(l32), (dt, l16, l32)
+            assert abs(norm(g16) - norm(g32)) <= 0.10 * norm(g32), dt
 
 
 def test_model_backward_8x120k_amp_vs_fp32():
@@ -93,15 +100,19 @@ def test_model_backward_8x120k_amp_vs_fp32():
     upstream gradient G on the coarse noise prediction:
 
     * f32 twice: bit-identical gradients (no float atomics anywhere in the backward);
-    * autocast (bf16 GEMMs) vs f32: the prediction within 2e-2 (measured 7.7e-3); the last
-      layer's weight gradient (no ReLU behind it) within 2e-2 (measured 7.6e-3).  Deeper
-      layers differ by what bf16 does to the ReLU masks: a pre-activation within bf16's error
-      of zero (~3 % of the units at K = 256: 2^-9 sqrt(K) of the spread) flips its mask, which
-      moves the gradient by ~sqrt(0.03) ~ 0.15 of its norm; measured 0.13-0.19 on the noise
+    * autocast vs f32, in both 16-bit formats -- float16 (the reference's CUDA autocast,
+      trainer.py:50,78, and Config.amp_dtype's default) and bfloat16: the prediction within
+      2e-2 (bf16 measured 7.7e-3); the last layer's weight gradient (no ReLU behind it) within
+      2e-2 (bf16 measured 7.6e-3).  Deeper layers differ by what rounding does to the ReLU
+      masks: a pre-activation within the format's error of zero (~3 % of the units at K = 256
+      for bf16: 2^-9 sqrt(K) of the spread; 8x fewer for fp16) flips its mask, which moves the
+      gradient by ~sqrt(0.03) ~ 0.15 of its norm for bf16; measured 0.13-0.19 on the noise
       predictor, 0.36-0.59 on the SA layers (train-mode BN over the flipped units), 0.27 for
       the whole gradient.  Regression bounds above those: whole gradient <= 0.35, noise
       predictor cos >= 0.975, style encoder cos >= 0.8 (pre-BN conv biases aside:
-      analytically zero gradient, rounding noise on both sides)."""
+      analytically zero gradient, rounding noise on both sides);
+    * fp16 tracks the f32 step at least as closely as bf16 (3 more mantissa bits, same MFMA
+      rate): prediction, last-layer gradient and whole gradient each no further from f32."""
     from pointcloud_style_transfer_amd import rng
     from pointcloud_style_transfer_amd.config.config import Config
     from pointcloud_style_transfer_amd.models.diffusion_model import PointCloudDiffusionModel
@@ -110,40 +121,48 @@ def test_model_backward_8x120k_amp_vs_fp32():
     real = _clouds(2000, 8, 120000).cuda()
     t = torch.arange(8, device="cuda") * 120 + 3
     grads, preds = [], []
-    for amp in (False, False, True):
+    modes = [None, None, torch.float16, torch.bfloat16]
+    for half in modes:
         torch.manual_seed(0)
         m = PointCloudDiffusionModel(Config(make_dirs=False)).cuda().train()
         for mod in m.modules():
             if isinstance(mod, torch.nn.Dropout):
                 mod.p = 0.0
-        with rng.replay(rng.CounterRNG(4100)), torch.autocast("cuda", enabled=amp):
+        with rng.replay(rng.CounterRNG(4100)), \
+                torch.autocast("cuda", enabled=half is not None, dtype=half or torch.float16):
             pred, idx = m(noisy, t, real, cond_drop_prob=0.1)
         G = torch.randn(pred.shape, generator=torch.Generator(device="cuda").manual_seed(9),
                         device="cuda")
         pred.backward(G)
         preds.append(pred.detach())
         grads.append({n: p.grad.detach().double() for n, p in m.named_parameters()})
-    g32, g32b, g16 = grads
+        del m, pred, idx
+    g32, g32b = grads[0], grads[1]
     assert all(torch.equal(g32[n], g32b[n]) for n in g32), "f32 backward not deterministic"
-    rel = ((preds[2] - preds[0]).norm() / preds[0].norm()).item()
     keep = [n for n in g32 if not PRE_BN_BIAS.search(n)]
     n32 = torch.sqrt(sum((g32[n] ** 2).sum() for n in keep)).item()
-    nd = torch.sqrt(sum(((g16[n] - g32[n]) ** 2).sum() for n in keep)).item()
-    print(f"model fwd+bwd 8x120k: |pred16 - pred32|/|pred32| {rel:.3e}, "
-          f"|g16 - g32| / |g32| {nd / n32:.3e}")
-    bad = []
-    for n in keep:
-        a, b = g16[n].flatten(), g32[n].flatten()
-        cos = float((a @ b) / (a.norm() * b.norm() + 1e-300))
-        floor = 0.975 if n.startswith("noise_predictor.") else 0.8
-        if cos < floor:
-            bad.append(f"{n}: cos {cos:.4f} < {floor}")
     last = "noise_predictor.output_mlp.4.weight"
-    last_rel = ((g16[last] - g32[last]).norm() / g32[last].norm()).item()
-    assert rel <= 2e-2
-    assert last_rel <= 2e-2, last_rel
-    assert nd <= 0.35 * n32, (nd, n32)
-    assert not bad, bad
+    stats = {}
+    for name, pred16, g16 in (("fp16", preds[2], grads[2]), ("bf16", preds[3], grads[3])):
+        rel = ((pred16 - preds[0]).norm() / preds[0].norm()).item()
+        nd = torch.sqrt(sum(((g16[n] - g32[n]) ** 2).sum() for n in keep)).item() / n32
+        last_rel = ((g16[last] - g32[last]).norm() / g32[last].norm()).item()
+        stats[name] = (rel, last_rel, nd)
+        print(f"model fwd+bwd 8x120k {name}: |pred16 - pred32|/|pred32| {rel:.3e}, "
+              f"last-layer dW {last_rel:.3e}, |g16 - g32| / |g32| {nd:.3e}")
+        bad = []
+        for n in keep:
+            a, b = g16[n].flatten(), g32[n].flatten()
+            cos = float((a @ b) / (a.norm() * b.norm() + 1e-300))
+            floor = 0.975 if n.startswith("noise_predictor.") else 0.8
+            if cos < floor:
+                bad.append(f"{n}: cos {cos:.4f} < {floor}")
+        assert rel <= 2e-2, (name, rel)
+        assert last_rel <= 2e-2, (name, last_rel)
+        assert nd <= 0.35, (name, nd)
+        assert not bad, (name, bad)
+    for k, what in enumerate(("prediction", "last-layer dW", "whole gradient")):
+        assert stats["fp16"][k] <= stats["bf16"][k], (what, stats)
 
 
 @pytest.fixture(scope="module")

@@ -41,7 +41,7 @@ def _run(tmp, tag, world, accum, micro, clouds=2, points=8192, amp=False, global
                 env.pop(k, None)
         procs.append(subprocess.Popen(
             [sys.executable, WORKER, out, str(accum), str(micro), str(clouds), str(points),
-             "1" if amp else "0", str(global_points)],
+             amp if isinstance(amp, str) else ("1" if amp else "0"), str(global_points)],
             env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT))
     return procs, out
 
@@ -89,9 +89,10 @@ def test_ddp_gradient_equals_accumulation(tmp_path, accum):
 
 
 def test_ddp_configs3_per_rank_size_amp(tmp_path):
-    """BASELINE configs[3] at its per-rank size: 8 x 120000-point clouds per rank, use_amp (the
-    bf16 fused NoisePredictor, bf16 GEMMs; GradScaler disabled so the gradients compare
-    unscaled), the real 2,549,827-gradient (10.2 MB) bucketed all-reduce through DDP's reducer.
+    """BASELINE configs[3] at its per-rank size: 8 x 120000-point clouds per rank, use_amp with
+    Config.amp_dtype "bfloat16" (the bf16 fused NoisePredictor, bf16 GEMMs; GradScaler disabled
+    so the gradients compare unscaled -- bf16's fp32 exponent range keeps the halving below
+    exact; the float16 case is test_ddp_fp16_amp_matches_accumulation), the real 2,549,827-gradient (10.2 MB) bucketed all-reduce through DDP's reducer.
     World 2 x 1 micro-batch against one process accumulating the same 2 micro-batches
     (trainer.py:115-125; counter-keyed draws, dropout off).  Each rank's gradient is its
     micro-batch gradient (loss / 1), DDP averages the two; the single process adds the two
@@ -124,3 +125,35 @@ def test_ddp_configs3_per_rank_size_amp(tmp_path):
         if k.startswith("param:"):
             np.testing.assert_array_equal(zd[k], z1[k])          # ranks identical
             np.testing.assert_allclose(zd[k], zo[k], rtol=0, atol=1e-6)
+
+
+def test_ddp_fp16_amp_matches_accumulation(tmp_path):
+    """The reference's float16 autocast (Config.amp_dtype default, trainer.py:50,78) under DDP,
+    with the GradScaler on at a fixed scale 2^14 (its unscale_ is exact): world 2 x 1
+    micro-batch against one process accumulating the same 2.  The 16-bit activation gradients
+    of loss/2 are exact halves of those of loss/1 unless they fall into fp16's subnormal range,
+    which the loss scale keeps them out of: bound 1e-3 max|g|, expected bit-identical (the
+    count is printed).  Ranks' post-step parameters identical; no inf/nan (the scaler would
+    have skipped the step)."""
+    tmp = str(tmp_path)
+    ddp, out_ddp = _run(tmp, "ddp", 2, 1, 1, amp="fp16")
+    one, out_one = _run(tmp, "one", 1, 2, 2, amp="fp16")
+    _wait(ddp + one)
+    zd, zo = np.load(out_ddp), np.load(out_one)
+    z1 = np.load(out_ddp[:-4] + ".rank1.npz")
+    gd, go = _grads(zd), _grads(zo)
+    assert gd.keys() == go.keys() and len(gd) == 80
+    bad, exact = [], 0
+    for n in gd:
+        a, b = gd[n].astype(np.float64), go[n].astype(np.float64)
+        assert np.isfinite(a).all() and np.isfinite(b).all(), n
+        scale = np.abs(b).max()
+        err = np.abs(a - b).max()
+        exact += int(err == 0)
+        if err > 1e-3 * scale + 1e-30:
+            bad.append(f"{n}: max|ddp - accum| {err:.3e} (max|g| {scale:.3e})")
+    print(f"fp16 amp DDP: {exact}/80 gradients bit-identical")
+    assert not bad, "\n".join(bad[:20])
+    for k in zd.files:
+        if k.startswith("param:"):
+            np.testing.assert_array_equal(zd[k], z1[k])

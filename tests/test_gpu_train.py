@@ -57,50 +57,66 @@ def test_linear_fn_backward_matches_autograd(H):
         assert err.item() < 1e-5
 
 
-def _bf(t):
-    return t.bfloat16().double()
+def _bf(t, half=torch.bfloat16):
+    return t.to(half).double()
 
 
+HALVES = [torch.bfloat16, torch.float16]
+HALF_IDS = ["bf16", "fp16"]
+
+
+@pytest.mark.parametrize("half", HALVES, ids=HALF_IDS)
 @pytest.mark.parametrize("M,K,O,relu", [(1, 3, 64, True), (1000, 3, 128, True), (4097, 131, 256, False),
                                         (60000, 256, 512, True), (60000, 512, 256, False),
                                         (300, 259, 3, False)])
-def test_gemm_nt_bf16_vs_float64(H, M, K, O, relu):
-    """bf16-rounded operands, fp32 accumulation: matches the float64 product of the same
-    rounded operands up to fp32 summation order."""
+def test_gemm_nt_bf16_vs_float64(H, M, K, O, relu, half):
+    """16-bit-rounded operands (bfloat16, or float16 -- the reference's autocast format),
+    fp32 accumulation: matches the float64 product of the same rounded operands up to fp32
+    summation order."""
     g = torch.Generator(device="cuda").manual_seed(M + K + O)
     A = torch.randn(M, K, device="cuda", generator=g)
     B = torch.randn(O, K, device="cuda", generator=g)
     shift = torch.randn(O, device="cuda", generator=g)
-    C = H.gemm_nt_bf16(A, B, None, shift, relu)
-    ref = _bf(A) @ _bf(B).t() + shift.double()
+    C = H.gemm_nt_bf16(A, B, None, shift, relu, half=half)
+    ref = _bf(A, half) @ _bf(B, half).t() + shift.double()
     if relu:
         ref = ref.clamp_min(0)
     err = (C.double() - ref).norm() / ref.norm()
     assert err.item() < 1e-6, err.item()
 
 
+@pytest.mark.parametrize("half", HALVES, ids=HALF_IDS)
 @pytest.mark.parametrize("M,I,O", [(37, 3, 64), (4097, 259, 256), (240000, 256, 512), (8, 256, 512)])
-def test_linear_wgrad_bf16_vs_float64(H, M, I, O):
+def test_linear_wgrad_bf16_vs_float64(H, M, I, O, half):
     g = torch.Generator(device="cuda").manual_seed(M * 3 + I + O)
     dz = torch.randn(M, O, device="cuda", generator=g)
     x = torch.randn(M, I, device="cuda", generator=g)
-    dw, db = H.linear_wgrad(dz, x, bias=True, bf16=True)
-    ref = _bf(dz).t() @ _bf(x)
+    dw, db = H.linear_wgrad(dz, x, bias=True, bf16=True, half=half)
+    ref = _bf(dz, half).t() @ _bf(x, half)
     assert ((dw.double() - ref).norm() / ref.norm()).item() < 1e-6
     ref_b = dz.double().sum(0)
     assert ((db.double() - ref_b).norm() / ref_b.norm()).item() < 1e-6
-    dw2, _ = H.linear_wgrad(dz, x, bias=False, bf16=True)
+    dw2, _ = H.linear_wgrad(dz, x, bias=False, bf16=True, half=half)
     assert torch.equal(dw, dw2)
 
 
-def test_linear_fn_uses_bf16_under_autocast(H):
+@pytest.mark.parametrize("half", HALVES, ids=HALF_IDS)
+def test_linear_fn_uses_bf16_under_autocast(H, half):
+    """LinearFn under autocast runs the 16-bit GEMMs in autocast's dtype: the output matches
+    the float64 product of operands rounded to THAT dtype (and not the other one)."""
     from pointcloud_style_transfer_amd.models import _autograd as ag
 
     torch.manual_seed(1)
     lin = torch.nn.Linear(256, 512).cuda()
     x = torch.randn(3000, 256, device="cuda", requires_grad=True)
-    with torch.autocast("cuda", dtype=torch.bfloat16):
+    with torch.autocast("cuda", dtype=half):
         y = ag.linear(x, lin, relu=True)
+    other = torch.float16 if half == torch.bfloat16 else torch.bfloat16
+    rounded = lambda h: (_bf(x.detach(), h) @ _bf(lin.weight.detach(), h).t()  # noqa: E731
+                         + lin.bias.detach().double()).clamp_min(0)
+    r_own, r_other = rounded(half), rounded(other)
+    assert (y.double() - r_own).norm() < 1e-5 * r_own.norm()
+    assert (y.double() - r_other).norm() > 1e-4 * r_own.norm()
     assert y.dtype == torch.float32
     y.sum().backward()
     x64 = x.detach().double().requires_grad_()
@@ -108,8 +124,8 @@ def test_linear_fn_uses_bf16_under_autocast(H):
     y64 = torch.relu(x64 @ w64.t() + lin.bias.detach().double())
     y64.sum().backward()
     rel = lambda a, b: ((a.double() - b).norm() / b.norm()).item()  # noqa: E731
-    assert 1e-7 < rel(y, y64) < 1e-2          # bf16 operands: not the f32 path, within bf16 error
-    # backward products against float64 with the kernel's own ReLU mask (bf16 rounding flips
+    assert 1e-7 < rel(y, y64) < 1e-2          # 16-bit operands: not the f32 path, within their error
+    # backward products against float64 with the kernel's own ReLU mask (16-bit rounding flips
     # the mask of near-zero pre-activations; that is not a GEMM error)
     mask = (y.detach() > 0).double()
     assert rel(x.grad, mask @ w64.detach()) < 1e-2
@@ -223,62 +239,68 @@ def test_group_gather_fn_backward(H, B, N, C, S, ns):
 
 # ---- csrc/train_mlp.hip: bf16-storage GEMMs with fused epilogues --------------------------
 def _bf16_ulp_close(a, b, ulps=1.0):
-    """bf16 outputs: within `ulps` bf16 units in the last place of the reference (an ulp of x
-    is at most |x| * 2^-7: 8 significant bits)."""
+    """16-bit outputs: within `ulps` units in the last place of the reference (an ulp of x is
+    at most |x| * 2^-7 for bfloat16's 8 significant bits, |x| * 2^-10 for float16's 11)."""
+    rel = 2.0 ** -10 if a.dtype == torch.float16 else 2.0 ** -7
     a, b = a.double(), b.double()
-    return ((a - b).abs() <= ulps * (b.abs() * 2.0 ** -7 + 1e-30) + 1e-6 * b.abs().max()).all().item()
+    return ((a - b).abs() <= ulps * (b.abs() * rel + 1e-30) + 1e-6 * b.abs().max()).all().item()
 
 
+@pytest.mark.parametrize("half", HALVES, ids=HALF_IDS)
 @pytest.mark.parametrize("M,K,O", [(1, 128, 128), (1000, 256, 512), (4097, 512, 256), (300, 136, 260),
                                    (60000, 256, 512)])
 @pytest.mark.parametrize("a16,b16", [(False, False), (True, False), (True, True)])
-def test_gemm_ex_epilogues_vs_float64(H, M, K, O, a16, b16):
+def test_gemm_ex_epilogues_vs_float64(H, M, K, O, a16, b16, half):
     g = torch.Generator(device="cuda").manual_seed(M + K + O + 7 * a16 + 3 * b16)
     A = torch.randn(M, K, device="cuda", generator=g)
     B = torch.randn(O, K, device="cuda", generator=g) * K ** -0.5
     bias = torch.randn(O, device="cuda", generator=g)
-    Ain = A.bfloat16() if a16 else A
-    Bin = B.bfloat16() if b16 else B
-    acc = _bf(A) @ _bf(B).t()
+    Ain = A.to(half) if a16 else A
+    Bin = B.to(half) if b16 else B
+    acc = _bf(A, half) @ _bf(B, half).t()
     tol = lambda ref: 1e-6 * ref.norm().item()  # noqa: E731  fp32 summation order
     # EP_F32 / EP_BF16 with bias + relu
-    C = H.gemm_ex(Ain, Bin, bias, relu=True, epilogue=H.EP_F32)
+    C = H.gemm_ex(Ain, Bin, bias, relu=True, epilogue=H.EP_F32, half=half)
     ref = (acc + bias.double()).clamp_min(0)
     assert (C.double() - ref).norm().item() <= tol(ref)
-    Cb = H.gemm_ex(Ain, Bin, bias, relu=True, epilogue=H.EP_BF16)
-    assert Cb.dtype == torch.bfloat16 and _bf16_ulp_close(Cb, ref)
+    Cb = H.gemm_ex(Ain, Bin, bias, relu=True, epilogue=H.EP_BF16, half=half)
+    assert Cb.dtype == half and _bf16_ulp_close(Cb, ref)
+    # EP_F32 with the 16-bit copy (EP_COND's copy path uses the same conversion)
+    C, C2 = H.gemm_ex(Ain, Bin, bias, epilogue=H.EP_F32, copy_bf16=True, half=half)
+    assert C2.dtype == half and torch.equal(C2, C.to(half))
     # EP_ADD
     aux = torch.randn(M, O, device="cuda", generator=g)
-    C = H.gemm_ex(Ain, Bin, epilogue=H.EP_ADD, aux=aux)
+    C = H.gemm_ex(Ain, Bin, epilogue=H.EP_ADD, aux=aux, half=half)
     ref = acc + aux.double()
     assert (C.double() - ref).norm().item() <= tol(ref)
     # EP_RELU_MASK: zero where the bf16 mask is <= 0 (including exact zeros)
     h = torch.randn(M, O, device="cuda", generator=g)
     h[:, ::7] = 0.0
-    h = h.bfloat16()
+    h = h.to(half)
     C = H.gemm_ex(Ain, Bin, epilogue=H.EP_RELU_MASK, aux=h)
     ref = acc * (h.double() > 0)
-    assert C.dtype == torch.bfloat16 and _bf16_ulp_close(C, ref)
+    assert C.dtype == half and _bf16_ulp_close(C, ref)
     assert torch.equal(C == 0, (h <= 0) | (C == 0))
 
 
+@pytest.mark.parametrize("half", HALVES, ids=HALF_IDS)
 @pytest.mark.parametrize("p", [0.0, 0.1, 0.5])
-def test_gemm_ex_dropout_mask_fwd_bwd_consistent(H, p):
+def test_gemm_ex_dropout_mask_fwd_bwd_consistent(H, p, half):
     """EP_RESID_DROP keeps element e iff hash(seed, e) passes; pcst_dropout_grad_bf16 must
     regenerate the same mask (read off dropout_grad of ones), the forward must equal
     x + keep * (acc + b) / (1-p), and the kept fraction must be 1-p."""
     M, K, O = 20000, 256, 256
     g = torch.Generator(device="cuda").manual_seed(11)
-    h = torch.randn(M, K, device="cuda", generator=g).bfloat16()
+    h = torch.randn(M, K, device="cuda", generator=g).to(half)
     W = torch.randn(O, K, device="cuda", generator=g) * K ** -0.5
     b = torch.randn(O, device="cuda", generator=g)
     x = torch.randn(M, O, device="cuda", generator=g)
     seed = 0x1234_5678_9ABC_DEF
     y = H.gemm_ex(h, W, b, epilogue=H.EP_RESID_DROP, aux=x, seed=seed, p=p)
-    keep = H.dropout_grad_bf16(torch.ones(M, O, device="cuda"), seed, p) != 0
+    keep = H.dropout_grad_bf16(torch.ones(M, O, device="cuda"), seed, p, half=half) != 0
     frac = keep.double().mean().item()
     assert abs(frac - (1 - p)) < 4 * np.sqrt(p * (1 - p) / (M * O)) + 1e-12
-    v = _bf(h) @ _bf(W).t() + b.double()
+    v = _bf(h, half) @ _bf(W, half).t() + b.double()
     ref = x.double() + keep.double() * v * (1.0 / (1.0 - p))
     assert ((y.double() - ref).norm() / ref.norm()).item() < 1e-6
     assert torch.equal(y[~keep], x[~keep])  # dropped elements are exactly the residual
@@ -288,25 +310,27 @@ def test_gemm_ex_dropout_mask_fwd_bwd_consistent(H, p):
         y3 = H.gemm_ex(h, W, b, epilogue=H.EP_RESID_DROP, aux=x, seed=seed + 1, p=p)
         assert not torch.equal(y, y3)
     gd = torch.randn(M, O, device="cuda", generator=g)
-    dd = H.dropout_grad_bf16(gd, seed, p)
+    dd = H.dropout_grad_bf16(gd, seed, p, half=half)
+    assert dd.dtype == half
     assert _bf16_ulp_close(dd, gd.double() * keep.double() / (1.0 - p), 0.5)
 
 
 @pytest.mark.parametrize("M,I,O", [(1, 256, 512), (100, 136, 264), (5000, 512, 256), (240000, 256, 512),
                                    (240000, 512, 256)])
 @pytest.mark.parametrize("z16,x16", [(True, True), (True, False), (False, False)])
-def test_linear_wgrad_ex_vs_float64(H, M, I, O, z16, x16):
+@pytest.mark.parametrize("half", HALVES, ids=HALF_IDS)
+def test_linear_wgrad_ex_vs_float64(H, M, I, O, z16, x16, half):
     g = torch.Generator(device="cuda").manual_seed(M + I + 3 * O + z16 + 2 * x16)
     dz = torch.randn(M, O, device="cuda", generator=g)
     x = torch.randn(M, I, device="cuda", generator=g)
-    dzi = dz.bfloat16() if z16 else dz
-    xi = x.bfloat16() if x16 else x
-    dw, db = H.linear_wgrad_ex(dzi, xi, bias=True)
-    ref = _bf(dz).t() @ _bf(x)
+    dzi = dz.to(half) if z16 else dz
+    xi = x.to(half) if x16 else x
+    dw, db = H.linear_wgrad_ex(dzi, xi, bias=True, half=half)
+    ref = _bf(dz, half).t() @ _bf(x, half)
     assert ((dw.double() - ref).norm() / ref.norm()).item() < 1e-6
     ref_b = dzi.double().sum(0)  # bias from the operand as stored (bf16 values or fp32)
     assert ((db.double() - ref_b).abs().max() / ref_b.abs().max()).item() < 1e-5
-    dw2, db2 = H.linear_wgrad_ex(dzi, xi, bias=True)
+    dw2, db2 = H.linear_wgrad_ex(dzi, xi, bias=True, half=half)
     assert torch.equal(dw, dw2) and torch.equal(db, db2), "must be deterministic"
 
 
