@@ -12,6 +12,8 @@ import socket
 import subprocess
 import sys
 
+import re
+
 import numpy as np
 import pytest
 
@@ -19,6 +21,7 @@ pytestmark = pytest.mark.gpu
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 WORKER = os.path.join(HERE, "ddp_worker.py")
+PRE_BN_BIAS = re.compile(r"style_encoder\.encoder\.sa\d\.mlp_convs\.\d+\.bias$")
 
 
 def _free_port():
@@ -129,12 +132,14 @@ def test_ddp_configs3_per_rank_size_amp(tmp_path):
 
 def test_ddp_fp16_amp_matches_accumulation(tmp_path):
     """The reference's float16 autocast (Config.amp_dtype default, trainer.py:50,78) under DDP,
-    with the GradScaler on at a fixed scale 2^14 (its unscale_ is exact): world 2 x 1
-    micro-batch against one process accumulating the same 2.  The 16-bit activation gradients
-    of loss/2 are exact halves of those of loss/1 unless they fall into fp16's subnormal range,
-    which the loss scale keeps them out of: bound 1e-3 max|g|, expected bit-identical (the
-    count is printed).  Ranks' post-step parameters identical; no inf/nan (the scaler would
-    have skipped the step)."""
+    with the GradScaler on at a fixed scale 2^16 (its default init; unscale_ is exact): world
+    2 x 1 micro-batch against one process accumulating the same 2.  The 16-bit activation
+    gradients of loss/2 are exact halves of those of loss/1 except where they fall into fp16's
+    subnormal range (the style branch's, deep behind style_proj, do even at 2^16: round-3
+    measurement at 2^14, 0/80 bit-identical, all within 1e-3), so the bound is 1e-3 max|g|.
+    Pre-BN conv biases are skipped: their gradient is analytically zero (train-mode BN
+    removes any shift) and both sides hold rounding noise.  Ranks' post-step parameters
+    identical; no inf/nan (the scaler would have skipped the step)."""
     tmp = str(tmp_path)
     ddp, out_ddp = _run(tmp, "ddp", 2, 1, 1, amp="fp16")
     one, out_one = _run(tmp, "one", 1, 2, 2, amp="fp16")
@@ -143,16 +148,20 @@ def test_ddp_fp16_amp_matches_accumulation(tmp_path):
     z1 = np.load(out_ddp[:-4] + ".rank1.npz")
     gd, go = _grads(zd), _grads(zo)
     assert gd.keys() == go.keys() and len(gd) == 80
-    bad, exact = [], 0
+    bad, exact, worst = [], 0, 0.0
     for n in gd:
         a, b = gd[n].astype(np.float64), go[n].astype(np.float64)
         assert np.isfinite(a).all() and np.isfinite(b).all(), n
+        if PRE_BN_BIAS.search(n):
+            continue
         scale = np.abs(b).max()
         err = np.abs(a - b).max()
         exact += int(err == 0)
+        worst = max(worst, err / scale)
         if err > 1e-3 * scale + 1e-30:
             bad.append(f"{n}: max|ddp - accum| {err:.3e} (max|g| {scale:.3e})")
-    print(f"fp16 amp DDP: {exact}/80 gradients bit-identical")
+    print(f"fp16 amp DDP: {exact}/71 gradients bit-identical, worst max|ddp - accum|/max|g| "
+          f"{worst:.3e}")
     assert not bad, "\n".join(bad[:20])
     for k in zd.files:
         if k.startswith("param:"):
