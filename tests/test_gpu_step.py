@@ -124,9 +124,9 @@ def test_voxel_copies_matches_concat(H, N, T, B, copies, sig):
 
 
 def test_voxel_pad_subset_is_uniform(H):
-    """The device-drawn pad subset (U < T: T - U of the P non-representatives, chosen by a
-    keyed Feistel permutation of the pool, csrc/voxel.hip voxf_keep_kernel) is a uniform
-    random subset: over 400 seeds every pool point's inclusion frequency is (T - U) / P within
+    """The device-drawn pad subset (U < T: T - U of the P non-representatives, the ones with
+    the smallest counter-based random keys: csrc/voxel.hip voxf_hist/select radix select and
+    the boundary bin's exact tie ranking in voxf_emit) is a uniform random subset: over 400 seeds every pool point's inclusion frequency is (T - U) / P within
     a binomial 5-sigma band, the count per seed is exact, the per-seed sets differ, and the
     frequencies of the pool's first and second halves agree (no positional bias)."""
     rng = np.random.default_rng(5)
