@@ -83,22 +83,34 @@ __device__ __forceinline__ void cd_minpairs(const float4 (&q)[8], const cd_f2 (&
 // against segment s's chunks [s*per, (s+1)*per).  R rows share every scalar load; S segments
 // put more waves in flight.  The block combines the segments' (best, first chunk) in segment
 // order, and the winning chunk's re-scan is split over the S segments the same way.
-template <int S, int R>
+// kList: the rows are the first *rcount entries of rlist (the grid search's overflow rows of
+// cloud b, side `side`: list (b * 2 + side) of stride `lstride`) instead of 0..N-1.
+template <int S, int R, bool kList = false>
 __global__ __launch_bounds__(256 * S) void chamfer_rowmin_kernel(const float* __restrict__ P,
                                                                  const float4* __restrict__ Qp,
                                                                  int N, int M, int Mp,
                                                                  float* __restrict__ mind,
-                                                                 int32_t* __restrict__ argm) {
+                                                                 int32_t* __restrict__ argm,
+                                                                 const int* __restrict__ rlist = nullptr,
+                                                                 const int* __restrict__ rcount = nullptr,
+                                                                 int side = 0, int64_t lstride = 0) {
   __shared__ float sbest[S][256 * R];
   __shared__ int sidx[S][256 * R];
   const int b = blockIdx.y;
   const int r = threadIdx.x & 255;
   const int seg = __builtin_amdgcn_readfirstlane(threadIdx.x >> 8);  // wave-uniform
+  const int* L = kList ? rlist + ((int64_t)b * 2 + side) * lstride : nullptr;
+  const int nrows = kList ? rcount[b * 2 + side] : N;
+  if (kList && blockIdx.x * 256 * R >= nrows) return;  // block-uniform: no barrier skipped
+  auto row_of = [&](int w) {  // the row of slot w, or N (none)
+    const int k = blockIdx.x * 256 * R + w * 256 + r;
+    return k < nrows ? (kList ? L[k] : k) : N;
+  };
   float mx[R], my[R], mz[R], np_[R];
   cd_f2 mx2[R], my2[R], mz2[R], np2[R];
 #pragma unroll
   for (int w = 0; w < R; ++w) {
-    const int i = blockIdx.x * 256 * R + w * 256 + r;
+    const int i = row_of(w);
     const float* p = P + ((int64_t)b * N + (i < N ? i : 0)) * 3;
     const float px = p[0], py = p[1], pz = p[2];
     np_[w] = sqnorm3(px, py, pz);
@@ -200,7 +212,7 @@ __global__ __launch_bounds__(256 * S) void chamfer_rowmin_kernel(const float* __
   }
 #pragma unroll
   for (int w = 0; w < R; ++w) {
-    const int i = blockIdx.x * 256 * R + w * 256 + r;
+    const int i = row_of(w);
     const int bj = bchunk[w] * kCdChunk + (found[w] < kCdChunk ? found[w] : 0);
     if (i < N) {
       mind[(int64_t)b * N + i] = best[w];
@@ -586,6 +598,10 @@ __device__ __forceinline__ float cg_axis_gap(float p, float lo, float hi) {
 }
 
 // rows: side s's sorted points; grid: side 1-s.  Writes min/arg at the row's original index.
+// ring_budget > 0 (the hybrid mode): a row still open after that many rings around its cell
+// (a row far from the other cloud, whose search would sweep a thin shell of the whole grid)
+// is appended to its overflow list instead (ovf_rows[b*2+side][*], count ovf_count[b*2+side];
+// list order is irrelevant) and the exhaustive row-min serves it.
 __global__ __launch_bounds__(256) void cg_rowmin_kernel(int N, int M,
                                                         const CgGrid* __restrict__ grids,
                                                         const int* __restrict__ starts,
@@ -594,7 +610,10 @@ __global__ __launch_bounds__(256) void cg_rowmin_kernel(int N, int M,
                                                         float* __restrict__ min1,
                                                         int32_t* __restrict__ arg1,
                                                         float* __restrict__ min2,
-                                                        int32_t* __restrict__ arg2) {
+                                                        int32_t* __restrict__ arg2,
+                                                        int ring_budget,
+                                                        int* __restrict__ ovf_count,
+                                                        int* __restrict__ ovf_rows) {
   const int b = blockIdx.y, side = blockIdx.z;  // side 0: pred rows vs target grid
   const int n = side ? M : N;
   const int r = blockIdx.x * blockDim.x + threadIdx.x;
@@ -650,6 +669,11 @@ __global__ __launch_bounds__(256) void cg_rowmin_kernel(int N, int M,
       if (!any) break;  // the rings so far cover the whole grid
       if (lb * shrink - err > best) break;
     }
+    if (ring_budget > 0 && ring > ring_budget) {  // over budget: the exhaustive pass takes it
+      const int at = atomicAdd(&ovf_count[rs], 1);
+      ovf_rows[rs * NM + at] = row;
+      return;
+    }
     const int z0 = max(cz - ring, 0), z1 = min(cz + ring, g.d[2] - 1);
     const int y0 = max(cy - ring, 0), y1 = min(cy + ring, g.d[1] - 1);
     const int x0 = max(cx - ring, 0), x1 = min(cx + ring, g.d[0] - 1);
@@ -700,6 +724,8 @@ struct CgWS {
   int2* crank;     // [B][2][NM]
   float4* sorted;  // [B][2][NM]
   int* sidx;       // [B][2][NM]
+  int* ovf_count;  // [B][2]       hybrid mode: rows over the ring budget
+  int* ovf_rows;   // [B][2][NM]
   size_t bytes;
 };
 static CgWS carve_cg(void* base, int64_t B, int64_t N, int64_t M) {
@@ -713,6 +739,8 @@ static CgWS carve_cg(void* base, int64_t B, int64_t N, int64_t M) {
   w.crank = c.take<int2>(B * 2 * NM);
   w.sorted = c.take<float4>(B * 2 * NM);
   w.sidx = c.take<int>(B * 2 * NM);
+  w.ovf_count = c.take<int>(B * 2);
+  w.ovf_rows = c.take<int>(B * 2 * NM);
   w.bytes = c.bytes();
   return w;
 }
@@ -726,14 +754,22 @@ static inline int64_t cd_padded(int64_t n) { return cdiv(n, kCdChunk) * kCdChunk
 // The grid path wins when the two clouds overlap (8 x 30000 lidar-like pairs 2.0 -> 0.32 ms),
 // but a row far outside the other cloud's grid has to search the thin shell of points within
 // its nearest distance, which grows with the distance: a noisy predicted x0 against its target
-// (the trainer's early timesteps) measured 46-60 ms.  The exhaustive path's cost does not
-// depend on the data, so it stays the default; the grid path is opt-in (mode 2).
-static bool cd_use_grid(int mode) { return mode == 2; }
+// (the trainer's early timesteps) measured 46-60 ms.  The hybrid mode (3) bounds that: the grid
+// search gives up after kCgRingBudget rings and the exhaustive row-min serves the rows it gave
+// up on (a list per cloud and side), so a direction costs at most about the exhaustive pass plus
+// the budgeted rings.  All modes give bit-identical minima and first-index argmins.
+#ifndef PCST_X_CG_RING_BUDGET  // experiment builds may override
+#define PCST_X_CG_RING_BUDGET 2
+#endif
+constexpr int kCgRingBudget = PCST_X_CG_RING_BUDGET;
+static bool cd_use_grid(int mode) { return mode == 2 || mode == 3; }
+static size_t cd_exh_bytes(int64_t B, int64_t N, int64_t M) {
+  return (sizeof(float) * 4 * (size_t)B * (size_t)(cd_padded(N) + cd_padded(M)) + 255) / 256 * 256;
+}
 
 extern "C" int pcst_chamfer_fwd_workspace_size(int64_t B, int64_t N, int64_t M, size_t* bytes) {
   PCST_CHECK_ARG(B >= 0 && N > 0 && M > 0 && bytes, "chamfer_fwd_workspace_size: bad args");
-  const size_t exh = sizeof(float) * 4 * (size_t)B * (size_t)(cd_padded(N) + cd_padded(M));
-  *bytes = std::max(exh, carve_cg(nullptr, B, N, M).bytes);
+  *bytes = cd_exh_bytes(B, N, M) + carve_cg(nullptr, B, N, M).bytes;
   return PCST_OK;
 }
 
@@ -742,15 +778,30 @@ extern "C" int pcst_chamfer_fwd(const float* pred, const float* target, int64_t 
                                 int32_t* arg2, float* out, int mode, void* workspace,
                                 void* stream) {
   PCST_CHECK_ARG(B >= 0 && N > 0 && M > 0 && N < (1ll << 30) && M < (1ll << 30), "chamfer_fwd: bad shape");
-  PCST_CHECK_ARG(mode >= 0 && mode <= 2, "chamfer_fwd: mode is 0 (auto), 1 (exhaustive) or 2 (grid)");
+  PCST_CHECK_ARG(mode >= 0 && mode <= 3,
+                 "chamfer_fwd: mode is 0 (auto), 1 (exhaustive), 2 (grid) or 3 (hybrid)");
   if (B == 0) return PCST_OK;
   PCST_CHECK_ARG(pred && target && min1 && arg1 && min2 && arg2 && workspace, "chamfer_fwd: null pointer");
+  hipStream_t s = as_stream(stream);
+  const unsigned b = (unsigned)B;
+  const int64_t Np = cd_padded(N), Mp = cd_padded(M);
+  float4* Pp = static_cast<float4*>(workspace);  // pred packed, B x Np/2 pairs x 2
+  float4* Tp = Pp + B * Np;                       // target packed
+  auto pack = [&]() {
+    hipLaunchKernelGGL(chamfer_pack_kernel, dim3((unsigned)cdiv(Np / 2, 256), b), dim3(256), 0, s,
+                       pred, (int)N, (int)Np, Pp);
+    hipLaunchKernelGGL(chamfer_pack_kernel, dim3((unsigned)cdiv(Mp / 2, 256), b), dim3(256), 0, s,
+                       target, (int)M, (int)Mp, Tp);
+  };
   if (cd_use_grid(mode)) {
-    hipStream_t s = as_stream(stream);
-    CgWS w = carve_cg(workspace, B, N, M);
-    const unsigned b = (unsigned)B;
+    const bool hybrid = mode == 3;
+    CgWS w = carve_cg(static_cast<char*>(workspace) + cd_exh_bytes(B, N, M), B, N, M);
     const int64_t NM = std::max(N, M);
     PCST_HIP(hipMemsetAsync(w.counts, 0, sizeof(int) * B * 2 * (kCgMaxCells + 1), s), "memset");
+    if (hybrid) {
+      PCST_HIP(hipMemsetAsync(w.ovf_count, 0, sizeof(int) * B * 2, s), "memset");
+      pack();
+    }
     hipLaunchKernelGGL(cg_stats_kernel, dim3(b, 2), dim3(1024), 0, s, pred, target, (int)N, (int)M,
                        w.grids);
     const dim3 pg((unsigned)cdiv(NM, 256), b, 2);
@@ -762,22 +813,23 @@ extern "C" int pcst_chamfer_fwd(const float* pred, const float* target, int64_t 
     hipLaunchKernelGGL(cg_fill_kernel, pg, dim3(256), 0, s, pred, target, (int)N, (int)M, w.starts,
                        w.crank, w.sorted, w.sidx);
     hipLaunchKernelGGL(cg_rowmin_kernel, pg, dim3(256), 0, s, (int)N, (int)M, w.grids, w.starts,
-                       w.sorted, w.sidx, min1, arg1, min2, arg2);
+                       w.sorted, w.sidx, min1, arg1, min2, arg2, hybrid ? kCgRingBudget : 0,
+                       w.ovf_count, w.ovf_rows);
+    if (hybrid) {  // the rows over budget, exhaustively (grid over the list's upper bound)
+      hipLaunchKernelGGL((chamfer_rowmin_kernel<2, 1, true>), dim3((unsigned)cdiv(N, 256), b),
+                         dim3(512), 0, s, pred, Tp, (int)N, (int)M, (int)Mp, min1, arg1,
+                         w.ovf_rows, w.ovf_count, 0, NM);
+      hipLaunchKernelGGL((chamfer_rowmin_kernel<2, 1, true>), dim3((unsigned)cdiv(M, 256), b),
+                         dim3(512), 0, s, target, Pp, (int)M, (int)N, (int)Np, min2, arg2,
+                         w.ovf_rows, w.ovf_count, 1, NM);
+    }
     if (out)
       hipLaunchKernelGGL(chamfer_mean_kernel, dim3(b), dim3(1024), 0, s, min1, (int)N, min2, (int)M,
                          out);
     PCST_LAUNCH_CHECK("chamfer_fwd");
     return PCST_OK;
   }
-  hipStream_t s = as_stream(stream);
-  const int64_t Np = cd_padded(N), Mp = cd_padded(M);
-  float4* Pp = static_cast<float4*>(workspace);  // pred packed, B x Np/2 pairs x 2
-  float4* Tp = Pp + B * Np;                       // target packed
-  const unsigned b = (unsigned)B;
-  hipLaunchKernelGGL(chamfer_pack_kernel, dim3((unsigned)cdiv(Np / 2, 256), b), dim3(256), 0, s,
-                     pred, (int)N, (int)Np, Pp);
-  hipLaunchKernelGGL(chamfer_pack_kernel, dim3((unsigned)cdiv(Mp / 2, 256), b), dim3(256), 0, s,
-                     target, (int)M, (int)Mp, Tp);
+  pack();
   // S x R shape of the row-min launch (experiment builds: XDEF=-DPCST_X_CD_VARIANT=11|41|12|22|14|42)
 #ifndef PCST_X_CD_VARIANT
 #define PCST_X_CD_VARIANT 21
@@ -787,7 +839,8 @@ extern "C" int pcst_chamfer_fwd(const float* pred, const float* target, int64_t 
                     int32_t* am) {
 #define PCST_CD_LAUNCH(S_, R_)                                                                  \
   hipLaunchKernelGGL((chamfer_rowmin_kernel<S_, R_>), dim3((unsigned)cdiv(n, 256 * R_), b),    \
-                     dim3(256 * S_), 0, s, P, Qp, (int)n, (int)m, (int)mp, md, am)
+                     dim3(256 * S_), 0, s, P, Qp, (int)n, (int)m, (int)mp, md, am, nullptr,     \
+                     nullptr, 0, 0)
     switch (variant) {
       case 11: PCST_CD_LAUNCH(1, 1); break;
       case 41: PCST_CD_LAUNCH(4, 1); break;

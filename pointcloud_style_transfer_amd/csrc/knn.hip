@@ -14,7 +14,7 @@
 // compact box and a brick's refs are one contiguous range.  Refs and the unknown rows
 // (queries) are counting-sorted by cell.
 //
-// Query pass (wave-cooperative).  One wave per chunk of <= 64 queries of one brick (the scan
+// Query pass (wave-cooperative).  One wave per chunk of <= 64 queries of a few x-adjacent bricks (the scan
 // kernel cuts the chunks).  Two passes, the second over refs the first did not visit:
 //   1. the cells of the chunk's cell bounding box grown by one cell;
 //   2. for lanes not yet settled that hold 3 refs: the cells of the union of their balls (the
@@ -72,7 +72,7 @@ struct KnnWS {
   float4* refs;      // [B][M]   (x, y, z, j) cell-sorted
   int32_t* qorder;   // [B][N]   query row index in cell order
   int2* crank;       // [B][M+N] (cell, rank in cell); cell -1 for known rows
-  uint2* chunks;     // [B][maxch] query ranges [q0, q1) of <= 64 queries inside one brick
+  uint2* chunks;     // [B][maxch] query ranges [q0, q1) of <= 64 queries (one brick group)
   int32_t* olist;    // [B][N]   outlier query rows
   float* obound;     // [B][N]   their kk-th best squared distance so far (rounded up; inf: none)
   // zeroed every call (contiguous):
@@ -290,11 +290,26 @@ __device__ __forceinline__ uint64_t block_excl_scan_256_u64(uint64_t v, unsigned
 }
 
 // Exclusive scan of the packed counts in place (the tile offset is the sum of the earlier
-// tiles' sums: at most kKnnMaxTiles words, read by the whole block), then the tile's 64
-// bricks are cut into chunks of <= 64 queries (by octant, below) appended to the cloud's chunk
-// list (order free: chunks are independent).
+// tiles' sums: at most kKnnMaxTiles words, read by the whole block), then the tile's 64 bricks
+// are cut into chunks of <= 64 queries (below) appended to the cloud's chunk list (order free:
+// chunks are independent).
+//
+// Chunks.  Lane t of the first wave walks the octants (2x2x2 cells: Morton cells [8o, 8o + 8))
+// of kChunkGroup consecutive bricks (x-neighbours: a group never crosses the start of a brick
+// row).  A chunk is a run of whole consecutive octants holding <= 64 queries, or a balanced part
+// of one octant that holds more, so a dense chunk's cell box stays within 2x2x2 cells (the query
+// pass stages the box grown by one cell).  Runs continue across the bricks of a group: sparse
+// bricks share a wave instead of each taking a mostly idle one, so a step has fewer chunks than
+// the chip has wave slots (one round of the query kernel instead of 1.2).
+#ifndef KNN_CHUNK_GROUP  // experiment builds may override (1 = one brick per walk)
+#define KNN_CHUNK_GROUP 4
+#endif
+constexpr int kChunkGroup = KNN_CHUNK_GROUP;
+static_assert(64 % kChunkGroup == 0, "bricks per tile must split into whole groups");
+
 __global__ __launch_bounds__(256) void knn_scan_kernel(uint64_t* __restrict__ cnt,
                                                        const uint64_t* __restrict__ tsum,
+                                                       const float* __restrict__ gp,
                                                        int64_t T, int64_t Cpad,
                                                        uint2* __restrict__ chunks, int64_t maxch,
                                                        int32_t* __restrict__ nchunk) {
@@ -329,21 +344,25 @@ __global__ __launch_bounds__(256) void knn_scan_kernel(uint64_t* __restrict__ cn
 #pragma unroll
   for (int k = 0; k < 16; ++k) D[k * 256 + threadIdx.x] = buf[pad(k * 256 + threadIdx.x)];
   if (threadIdx.x < 64) {
-    // brick t's queries by octant (2x2x2 cells: Morton cells [8o, 8o + 8)).  A chunk is a run of
-    // whole consecutive octants holding <= 64 queries, or a balanced part of one octant that
-    // holds more, so a dense chunk's cell box stays within 2x2x2 cells (the query pass stages
-    // the box grown by one cell: at most 4x4x4).
+    constexpr int kGroups = 64 / kChunkGroup, kOct = 8 * kChunkGroup;
     const int t = threadIdx.x;
-    uint32_t qo[9];
+    const bool walker = t < kGroups;
+    const int bx = (__float_as_int(gp[b * 8 + 5]) + 3) >> 2;  // bricks per row
+    const int64_t brick0 = (int64_t)tile * 64 + (int64_t)t * kChunkGroup;
+    uint32_t qo[kOct + 1];
 #pragma unroll
-    for (int o = 0; o < 8; ++o) qo[o] = (uint32_t)(buf[pad(t * 64 + 8 * o)] >> 32);
-    qo[8] = (uint32_t)((t < 63 ? buf[pad(t * 64 + 64)] : base + tot) >> 32);
+    for (int o = 0; o < kOct; ++o) qo[o] = walker ? (uint32_t)(buf[pad(t * kOct * 8 + 8 * o)] >> 32) : 0u;
+    qo[kOct] = walker ? (uint32_t)((t < kGroups - 1 ? buf[pad((t + 1) * kOct * 8)] : base + tot) >> 32) : 0u;
     // walk the octants; emit(a, b) is called for every chunk [a, b) in order
     auto walk = [&](auto&& emit) {
       uint32_t cs = qo[0];  // start of the open run of octants
 #pragma unroll
-      for (int o = 0; o < 8; ++o) {
+      for (int o = 0; o < kOct; ++o) {
         const uint32_t a = qo[o], n = qo[o + 1] - a;
+        if (o % 8 == 0 && o > 0 && (brick0 + o / 8) % bx == 0) {  // a new brick row: close the run
+          if (a > cs) emit(cs, a);
+          cs = a;
+        }
         if (n > 64) {
           if (a > cs) emit(cs, a);
           const uint32_t k = (n + 63) / 64;
@@ -354,10 +373,10 @@ __global__ __launch_bounds__(256) void knn_scan_kernel(uint64_t* __restrict__ cn
           cs = a;
         }
       }
-      if (qo[8] > cs) emit(cs, qo[8]);
+      if (qo[kOct] > cs) emit(cs, qo[kOct]);
     };
     uint32_t nch = 0;
-    walk([&](uint32_t, uint32_t) { ++nch; });
+    if (walker) walk([&](uint32_t, uint32_t) { ++nch; });
     uint32_t off = nch;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
@@ -371,7 +390,7 @@ __global__ __launch_bounds__(256) void knn_scan_kernel(uint64_t* __restrict__ cn
     at = __shfl(at, 0);
     uint2* Ch = chunks + b * maxch + at + off;
     uint32_t i = 0;
-    walk([&](uint32_t a, uint32_t e) { Ch[i++] = make_uint2(a, e); });
+    if (walker) walk([&](uint32_t a, uint32_t e) { Ch[i++] = make_uint2(a, e); });
   }
 }
 
@@ -743,7 +762,7 @@ __device__ __forceinline__ bool settled(const Query& me, const Box& cells, const
   return bound == INFINITY || (bound > 0 && me.t.last(kk) < bound * bound);
 }
 
-// One wave per chunk of <= 64 queries of one brick; the passes of the header comment.
+// One wave per chunk of <= 64 queries (knn_scan_kernel); the passes of the header comment.
 // amdgpu_waves_per_eu(4): 128 VGPRs (4 spilled) instead of 138, so 4 waves per SIMD (the LDS
 // allows 4 work-groups per CU) instead of 3: the ~5000 chunks of a step run in fewer rounds
 // (driver window 2379-2398 -> 2400-2429 steps/s, A/B on one box).
@@ -1264,7 +1283,7 @@ extern "C" int pcst_knn3_build(const float* orig, const int64_t* idx, int64_t B,
   hipLaunchKernelGGL(knn_count_kernel, dim3(gc, b), dim3(256), pad_count, s, orig, idx, w.stats,
                      w.known, N, M, w.Cmax, w.T, w.Cpad, w.gp, w.cnt, w.tsum, w.crank);
   hipLaunchKernelGGL(knn_scan_kernel, dim3((unsigned)w.T, b), dim3(256), pad_scan, s, w.cnt, w.tsum,
-                     w.T, w.Cpad, w.chunks, w.maxch, w.nchunk);
+                     w.gp, w.T, w.Cpad, w.chunks, w.maxch, w.nchunk);
   const unsigned gf = (unsigned)std::min<int64_t>(cdiv(M + N, 256), 2048);
   hipLaunchKernelGGL(knn_fill_kernel, dim3(gf, b), dim3(256), pad_fill, s, orig, idx, N, M, w.Cpad,
                      w.cnt, w.crank, w.refs, w.qorder);

@@ -178,11 +178,11 @@ def test_chamfer_and_loss(mods, golden):
     assert abs(float(total) - float(g["dl_total"])) < 1e-5 * float(g["dl_total"])
 
 
-@pytest.mark.parametrize("mode", [1, 2])
+@pytest.mark.parametrize("mode", [1, 2, 3])
 @pytest.mark.parametrize("N,M", [(3000, 2500), (257, 1), (1, 700), (4096, 4096)])
 def test_chamfer_rowmin_exact_vs_oracle(N, M, mode):
-    """Row minima and first-index argmins of both forward paths (1: packed exhaustive, 2:
-    grid-pruned), bit-exact against the oracle's scalar restatement (losses.py:36-41), on clouds
+    """Row minima and first-index argmins of the forward paths (1: packed exhaustive, 2:
+    grid-pruned, 3: hybrid -- budgeted grid, exhaustive overflow rows), bit-exact against the oracle's scalar restatement (losses.py:36-41), on clouds
     with duplicated target points and query points equal to targets (raw D <= 0 ties broken by
     the clamp's first index), sizes that leave the last 256-point chunk ragged, and single-point
     clouds."""
@@ -208,12 +208,14 @@ def test_chamfer_rowmin_exact_vs_oracle(N, M, mode):
     np.testing.assert_allclose(out.cpu().numpy(), np.array(ref), rtol=1e-6)
 
 
-@pytest.mark.parametrize("kind", ["lidar", "gauss_aniso", "far_apart", "dup_heavy"])
+@pytest.mark.parametrize("kind", ["lidar", "gauss_aniso", "far_apart", "dup_heavy", "noisy_x0"])
 def test_chamfer_grid_equals_exhaustive_30k(kind):
-    """The grid-pruned forward against the exhaustive one at the trainer's size (8 x 30000 per
-    side): minima, argmins and means bit-equal.  Cloud kinds: LiDAR-like rings scaled to tens
-    of metres (the trainer's coarse clouds), an anisotropic Gaussian, two clouds offset far from
-    each other (rows outside the other grid), and heavy duplication (many exact ties)."""
+    """The grid-pruned and hybrid forwards against the exhaustive one at the trainer's size
+    (8 x 30000 per side): argmins and means bit-equal.  Cloud kinds: LiDAR-like rings scaled to
+    tens of metres (the trainer's coarse clouds), an anisotropic Gaussian, two clouds offset far
+    from each other (rows outside the other grid), heavy duplication (many exact ties), and the
+    trainer's high-timestep case: pred_x0 = target + noise / sqrt(a_t) with per-cloud noise
+    scales 0.05..8 (the hybrid's overflow rows)."""
     from pointcloud_style_transfer_amd import _hip
     from pointcloud_style_transfer_amd.synthetic import lidar_like_cloud
 
@@ -228,18 +230,23 @@ def test_chamfer_grid_equals_exhaustive_30k(kind):
     elif kind == "far_apart":
         p = rng.standard_normal((B, N, 3)).astype(np.float32)
         q = (rng.standard_normal((B, M, 3)) + 40.0).astype(np.float32)
+    elif kind == "noisy_x0":
+        q = np.stack([lidar_like_cloud(300 + i, M) for i in range(B)]).astype(np.float32)
+        scale = np.geomspace(0.05, 8.0, B).astype(np.float32)[:, None, None]
+        p = (q[:, rng.permutation(M)[:N]] + rng.standard_normal((B, N, 3)) * scale).astype(np.float32)
     else:
         base = rng.standard_normal((B, 600, 3)).astype(np.float32)
         p = base[:, rng.integers(0, 600, N)]
         q = base[:, rng.integers(0, 600, M)]
     res = {}
-    for mode in (1, 2):
+    for mode in (1, 2, 3):
         P, Q = dev(p), dev(q)
         out, a1, a2 = _hip.chamfer_fwd(P, Q, mode)
         torch.cuda.synchronize()
         res[mode] = (out.cpu().numpy(), a1.cpu().numpy(), a2.cpu().numpy())
-    for x, y in zip(res[1], res[2]):
-        np.testing.assert_array_equal(x, y)
+    for mode in (2, 3):
+        for x, y in zip(res[1], res[mode]):
+            np.testing.assert_array_equal(x, y)
 
 
 def test_chamfer_determinism(mods):
