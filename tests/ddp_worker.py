@@ -51,7 +51,7 @@ def main():
             m.p = 0.0
     tr.model.train()
     if amp:
-        tr.scaler = (torch.amp.GradScaler(init_scale=2.0 ** 16, growth_interval=10 ** 9)
+        tr.scaler = (torch.amp.GradScaler(init_scale=2.0 ** 14, growth_interval=10 ** 9)
                      if amp_dtype == "float16" else torch.amp.GradScaler(enabled=False))
     grads = {}
     o_step = tr.optimizer.step

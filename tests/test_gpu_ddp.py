@@ -132,11 +132,12 @@ def test_ddp_configs3_per_rank_size_amp(tmp_path):
 
 def test_ddp_fp16_amp_matches_accumulation(tmp_path):
     """The reference's float16 autocast (Config.amp_dtype default, trainer.py:50,78) under DDP,
-    with the GradScaler on at a fixed scale 2^16 (its default init; unscale_ is exact): world
+    with the GradScaler on at a fixed scale 2^14 (unscale_ is exact; the default init 2^16
+    overflows fp16 in this first step -- the scaler would skip it and halve the scale): world
     2 x 1 micro-batch against one process accumulating the same 2.  The 16-bit activation
     gradients of loss/2 are exact halves of those of loss/1 except where they fall into fp16's
-    subnormal range (the style branch's, deep behind style_proj, do even at 2^16: round-3
-    measurement at 2^14, 0/80 bit-identical, all within 1e-3), so the bound is 1e-3 max|g|.
+    subnormal range (the style branch's, deep behind style_proj, do: round-3 measurement 0/80
+    bit-identical, all within 1e-3), so the bound is 1e-3 max|g|.
     Pre-BN conv biases are skipped: their gradient is analytically zero (train-mode BN
     removes any shift) and both sides hold rounding noise.  Ranks' post-step parameters
     identical; no inf/nan (the scaler would have skipped the step)."""
