@@ -710,7 +710,7 @@ def group_gather_bwd(dgrouped, group_idx, N):
 
 # ----------------------------------------------------------------------------- losses
 def chamfer_fwd(pred, target, mode=0):
-    """-> (chamfer [B], arg1 [B,N] int32, arg2 [B,M] int32).  mode: 0 auto, 1 exhaustive,
+    """-> (chamfer [B], arg1 [B,N] int32, arg2 [B,M] int32).  mode: 0 auto (= 3), 1 exhaustive,
     2 grid-pruned, 3 hybrid (budgeted grid + exhaustive overflow rows); bit-identical results
     (pcst.h)."""
     require_device(pred, target)

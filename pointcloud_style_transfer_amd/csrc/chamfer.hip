@@ -754,15 +754,18 @@ static inline int64_t cd_padded(int64_t n) { return cdiv(n, kCdChunk) * kCdChunk
 // The grid path wins when the two clouds overlap (8 x 30000 lidar-like pairs 2.0 -> 0.32 ms),
 // but a row far outside the other cloud's grid has to search the thin shell of points within
 // its nearest distance, which grows with the distance: a noisy predicted x0 against its target
-// (the trainer's early timesteps) measured 46-60 ms.  The hybrid mode (3) bounds that: the grid
-// search gives up after kCgRingBudget rings and the exhaustive row-min serves the rows it gave
-// up on (a list per cloud and side), so a direction costs at most about the exhaustive pass plus
-// the budgeted rings.  All modes give bit-identical minima and first-index argmins.
+// (the trainer's early timesteps) measured 46-60 ms.  The hybrid mode (3, and the default 0)
+// bounds that: the grid search gives up after kCgRingBudget rings and the exhaustive row-min
+// serves the rows it gave up on (a list per cloud and side), so a direction costs at most about
+// the exhaustive pass plus the budgeted rings.  Measured on the trainer's pair (a predicted x0
+// = lidar-like target + noise, 8 x 30000 per side, tools/cd_sweep.sh): noise 0.02: exhaustive
+// 2.08 ms, grid 0.32, hybrid 0.34; noise 0.2: 2.10 / 1.34 / 1.43; noise 1: 2.09 / 16.9 / 1.25;
+// noise 4: 2.10 / 62.5 / 1.28.  All modes give bit-identical minima and first-index argmins.
 #ifndef PCST_X_CG_RING_BUDGET  // experiment builds may override
 #define PCST_X_CG_RING_BUDGET 2
 #endif
 constexpr int kCgRingBudget = PCST_X_CG_RING_BUDGET;
-static bool cd_use_grid(int mode) { return mode == 2 || mode == 3; }
+static bool cd_use_grid(int mode) { return mode == 0 || mode == 2 || mode == 3; }
 static size_t cd_exh_bytes(int64_t B, int64_t N, int64_t M) {
   return (sizeof(float) * 4 * (size_t)B * (size_t)(cd_padded(N) + cd_padded(M)) + 255) / 256 * 256;
 }
@@ -794,7 +797,7 @@ extern "C" int pcst_chamfer_fwd(const float* pred, const float* target, int64_t 
                        target, (int)M, (int)Mp, Tp);
   };
   if (cd_use_grid(mode)) {
-    const bool hybrid = mode == 3;
+    const bool hybrid = mode != 2;
     CgWS w = carve_cg(static_cast<char*>(workspace) + cd_exh_bytes(B, N, M), B, N, M);
     const int64_t NM = std::max(N, M);
     PCST_HIP(hipMemsetAsync(w.counts, 0, sizeof(int) * B * 2 * (kCgMaxCells + 1), s), "memset");

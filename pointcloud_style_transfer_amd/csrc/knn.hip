@@ -14,7 +14,7 @@
 // compact box and a brick's refs are one contiguous range.  Refs and the unknown rows
 // (queries) are counting-sorted by cell.
 //
-// Query pass (wave-cooperative).  One wave per chunk of <= 64 queries of a few x-adjacent bricks (the scan
+// Query pass (wave-cooperative).  One wave per chunk of <= 64 queries of one brick (the scan
 // kernel cuts the chunks).  Two passes, the second over refs the first did not visit:
 //   1. the cells of the chunk's cell bounding box grown by one cell;
 //   2. for lanes not yet settled that hold 3 refs: the cells of the union of their balls (the
@@ -70,9 +70,9 @@ struct KnnWS {
   StatRec* stats;    // [B][kStatBlocks]
   float* gp;         // [B][8]: origin xyz, cell size, inv size, dims xyz (int bits)
   float4* refs;      // [B][M]   (x, y, z, j) cell-sorted
-  float4* qpts;      // [B][N]   (x, y, z, row n) of the queries, cell-sorted
+  int32_t* qorder;   // [B][N]   query row index in cell order
   int2* crank;       // [B][M+N] (cell, rank in cell); cell -1 for known rows
-  uint4* chunks;     // [B][maxch] {q0, q1, first brick, cell box}: <= 64 queries (knn_scan_kernel)
+  uint2* chunks;     // [B][maxch] query ranges [q0, q1) of <= 64 queries inside one brick
   int32_t* olist;    // [B][N]   outlier query rows
   float* obound;     // [B][N]   their kk-th best squared distance so far (rounded up; inf: none)
   // zeroed every call (contiguous):
@@ -100,9 +100,9 @@ static KnnWS carve_knn(void* base, int64_t B, int64_t N, int64_t M) {
   w.stats = c.take<StatRec>(B * kStatBlocks);
   w.gp = c.take<float>(B * 8);
   w.refs = c.take<float4>(B * M);
-  w.qpts = c.take<float4>(B * N);
+  w.qorder = c.take<int32_t>(B * N);
   w.crank = c.take<int2>(B * (M + N));
-  w.chunks = c.take<uint4>(B * w.maxch);
+  w.chunks = c.take<uint2>(B * w.maxch);
   w.olist = c.take<int32_t>(B * N);
   w.obound = c.take<float>(B * N);
   w.err = c.take<int32_t>(4);
@@ -290,30 +290,13 @@ __device__ __forceinline__ uint64_t block_excl_scan_256_u64(uint64_t v, unsigned
 }
 
 // Exclusive scan of the packed counts in place (the tile offset is the sum of the earlier
-// tiles' sums: at most kKnnMaxTiles words, read by the whole block), then the tile's 64 bricks
-// are cut into chunks of <= 64 queries (below) appended to the cloud's chunk list (order free:
-// chunks are independent).
-//
-// Chunks.  Lane t of the first wave walks the octants (2x2x2 cells: Morton cells [8o, 8o + 8))
-// of kChunkGroup consecutive bricks.  A chunk is a run of whole consecutive octants holding <= 64
-// queries, or a balanced part of one octant that holds more, so a dense chunk's cell box stays
-// within 2x2x2 cells (the query pass stages the box grown by one cell).  Runs continue across the
-// bricks of a group (x-neighbours; a run is cut at the start of a brick row): sparse bricks share
-// a wave instead of each taking a mostly idle one.  Each chunk carries the bounding box of the
-// cells holding its queries (from the per-cell query counts the scan has in LDS), relative to its
-// first brick: the query kernel starts loading the box's ref ranges with the chunk descriptor,
-// without waiting for the query coordinates.
-#ifndef KNN_CHUNK_GROUP  // experiment builds may override (1 = one brick per walk)
-#define KNN_CHUNK_GROUP 4
-#endif
-constexpr int kChunkGroup = KNN_CHUNK_GROUP;
-static_assert(64 % kChunkGroup == 0, "bricks per tile must split into whole groups");
-
+// tiles' sums: at most kKnnMaxTiles words, read by the whole block), then the tile's 64
+// bricks are cut into chunks of <= 64 queries (by octant, below) appended to the cloud's chunk
+// list (order free: chunks are independent).
 __global__ __launch_bounds__(256) void knn_scan_kernel(uint64_t* __restrict__ cnt,
                                                        const uint64_t* __restrict__ tsum,
-                                                       const float* __restrict__ gp,
                                                        int64_t T, int64_t Cpad,
-                                                       uint4* __restrict__ chunks, int64_t maxch,
+                                                       uint2* __restrict__ chunks, int64_t maxch,
                                                        int32_t* __restrict__ nchunk) {
   const int b = blockIdx.y, tile = blockIdx.x;
   __shared__ unsigned long long buf[kKnnTile + kKnnTile / 32];
@@ -345,82 +328,36 @@ __global__ __launch_bounds__(256) void knn_scan_kernel(uint64_t* __restrict__ cn
   __syncthreads();
 #pragma unroll
   for (int k = 0; k < 16; ++k) D[k * 256 + threadIdx.x] = buf[pad(k * 256 + threadIdx.x)];
-  // per octant of the tile (Morton cells [8q, 8q + 8)): bit l = cell 8q + l holds a query
-  __shared__ uint8_t occs[kKnnTile / 8];
-  for (int q = threadIdx.x; q < kKnnTile / 8; q += 256) {
-    uint32_t m = 0, prev = (uint32_t)(buf[pad(8 * q)] >> 32);
-    for (int l = 1; l <= 8; ++l) {
-      const int c = 8 * q + l;
-      const uint32_t nxt = (uint32_t)((c < kKnnTile ? buf[pad(c)] : base + tot) >> 32);
-      m |= (nxt > prev ? 1u : 0u) << (l - 1);
-      prev = nxt;
-    }
-    occs[q] = (uint8_t)m;
-  }
-  __syncthreads();
   if (threadIdx.x < 64) {
-    constexpr int kGroups = 64 / kChunkGroup, kOct = 8 * kChunkGroup;
+    // brick t's queries by octant (2x2x2 cells: Morton cells [8o, 8o + 8)).  A chunk is a run of
+    // whole consecutive octants holding <= 64 queries, or a balanced part of one octant that
+    // holds more, so a dense chunk's cell box stays within 2x2x2 cells (the query pass stages
+    // the box grown by one cell: at most 4x4x4).
     const int t = threadIdx.x;
-    const bool walker = t < kGroups;
-    const int bx = (__float_as_int(gp[b * 8 + 5]) + 3) >> 2;  // bricks per row
-    const int64_t brick0 = (int64_t)tile * 64 + (int64_t)t * kChunkGroup;
-    // query start of the group's octant o (o = kOct: the group's end)
-    auto qo = [&](int o) -> uint32_t {
-      const int c = t * kOct * 8 + 8 * o;
-      return (uint32_t)((c < kKnnTile ? buf[pad(c)] : base + tot) >> 32);
-    };
-    // cell box of octant o's occupied cells relative to the run's first brick kb: x 0..4G-1
-    // (5 bits each end), y and z 0..3 (2 bits each end); packed x0|x1<<5|y0<<10|y1<<12|z0<<14|z1<<16
-    auto obox = [&](int o, int kb) -> uint32_t {
-      const uint32_t m = occs[t * kOct + o], k = (uint32_t)(o / 8 - kb), oc = (uint32_t)(o % 8);
-      const uint32_t xb = 4 * k + 2 * (oc & 1), yb = 2 * ((oc >> 1) & 1), zb = 2 * ((oc >> 2) & 1);
-      const uint32_t x0 = xb + ((m & 0x55u) ? 0 : 1), x1 = xb + ((m & 0xAAu) ? 1 : 0);
-      const uint32_t y0 = yb + ((m & 0x33u) ? 0 : 1), y1 = yb + ((m & 0xCCu) ? 1 : 0);
-      const uint32_t z0 = zb + ((m & 0x0Fu) ? 0 : 1), z1 = zb + ((m & 0xF0u) ? 1 : 0);
-      return x0 | x1 << 5 | y0 << 10 | y1 << 12 | z0 << 14 | z1 << 16;
-    };
-    auto box_union = [](uint32_t u, uint32_t v) -> uint32_t {
-      if (u == 0xffffffffu) return v;
-      const uint32_t x0 = min(u & 31u, v & 31u), x1 = max((u >> 5) & 31u, (v >> 5) & 31u);
-      const uint32_t y0 = min((u >> 10) & 3u, (v >> 10) & 3u), y1 = max((u >> 12) & 3u, (v >> 12) & 3u);
-      const uint32_t z0 = min((u >> 14) & 3u, (v >> 14) & 3u), z1 = max((u >> 16) & 3u, (v >> 16) & 3u);
-      return x0 | x1 << 5 | y0 << 10 | y1 << 12 | z0 << 14 | z1 << 16;
-    };
-    // walk the octants; emit(a, e, first brick of the chunk, box) for every chunk [a, e) in order
+    uint32_t qo[9];
+#pragma unroll
+    for (int o = 0; o < 8; ++o) qo[o] = (uint32_t)(buf[pad(t * 64 + 8 * o)] >> 32);
+    qo[8] = (uint32_t)((t < 63 ? buf[pad(t * 64 + 64)] : base + tot) >> 32);
+    // walk the octants; emit(a, b) is called for every chunk [a, b) in order
     auto walk = [&](auto&& emit) {
-      uint32_t cs = qo(0);          // start of the open run of octants
-      int kb = 0;                   // the run's first brick (group-relative)
-      uint32_t rbox = 0xffffffffu;  // the run's box (none yet)
-      uint32_t a = cs;
-      for (int o = 0; o < kOct; ++o) {
-        const uint32_t e1 = qo(o + 1), n = e1 - a;
-        if (o % 8 == 0 && o > 0 && (brick0 + o / 8) % bx == 0) {  // a new brick row: close the run
-          if (a > cs) emit(cs, a, kb, rbox);
-          cs = a;
-          rbox = 0xffffffffu;
-        }
-        if (a == cs) kb = o / 8;  // the run is empty so far: it starts in this brick
+      uint32_t cs = qo[0];  // start of the open run of octants
+#pragma unroll
+      for (int o = 0; o < 8; ++o) {
+        const uint32_t a = qo[o], n = qo[o + 1] - a;
         if (n > 64) {
-          if (a > cs) emit(cs, a, kb, rbox);
-          const uint32_t k = (n + 63) / 64, ob = obox(o, o / 8);
-          for (uint32_t i = 0; i < k; ++i)
-            emit(a + (uint32_t)((uint64_t)n * i / k), a + (uint32_t)((uint64_t)n * (i + 1) / k), o / 8, ob);
+          if (a > cs) emit(cs, a);
+          const uint32_t k = (n + 63) / 64;
+          for (uint32_t i = 0; i < k; ++i) emit(a + (uint32_t)((uint64_t)n * i / k), a + (uint32_t)((uint64_t)n * (i + 1) / k));
           cs = a + n;
-          rbox = 0xffffffffu;
         } else if (a + n - cs > 64) {
-          emit(cs, a, kb, rbox);
+          emit(cs, a);
           cs = a;
-          kb = o / 8;
-          rbox = n ? obox(o, kb) : 0xffffffffu;
-        } else if (n) {
-          rbox = box_union(rbox, obox(o, kb));
         }
-        a = e1;
       }
-      if (a > cs) emit(cs, a, kb, rbox);
+      if (qo[8] > cs) emit(cs, qo[8]);
     };
     uint32_t nch = 0;
-    if (walker) walk([&](uint32_t, uint32_t, int, uint32_t) { ++nch; });
+    walk([&](uint32_t, uint32_t) { ++nch; });
     uint32_t off = nch;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
@@ -432,12 +369,9 @@ __global__ __launch_bounds__(256) void knn_scan_kernel(uint64_t* __restrict__ cn
     uint32_t at = 0;
     if (t == 0 && all) at = (uint32_t)atomicAdd(&nchunk[b], (int32_t)all);
     at = __shfl(at, 0);
-    uint4* Ch = chunks + b * maxch + at + off;
+    uint2* Ch = chunks + b * maxch + at + off;
     uint32_t i = 0;
-    if (walker)
-      walk([&](uint32_t a, uint32_t e, int kb, uint32_t box) {
-        Ch[i++] = make_uint4(a, e, (uint32_t)(brick0 + kb), box);
-      });
+    walk([&](uint32_t a, uint32_t e) { Ch[i++] = make_uint2(a, e); });
   }
 }
 
@@ -447,7 +381,7 @@ __global__ __launch_bounds__(256) void knn_fill_kernel(const float* __restrict__
                                                        const uint64_t* __restrict__ start,
                                                        const int2* __restrict__ crank,
                                                        float4* __restrict__ refs,
-                                                       float4* __restrict__ qpts) {
+                                                       int32_t* __restrict__ qorder) {
   const int b = blockIdx.y;
   const uint64_t* S = start + b * Cpad;
   for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < M + N; e += gridDim.x * 256) {
@@ -461,8 +395,7 @@ __global__ __launch_bounds__(256) void knn_fill_kernel(const float* __restrict__
       refs[b * M + pos] = make_float4(p[0], p[1], p[2], __int_as_float((int)e));
     } else {
       const uint32_t pos = (uint32_t)(S[cr.x] >> 32) + (uint32_t)cr.y;
-      const float* p = orig + (b * N + (e - M)) * 3;
-      qpts[b * N + pos] = make_float4(p[0], p[1], p[2], __int_as_float((int)(e - M)));
+      qorder[b * N + pos] = (int32_t)(e - M);
     }
   }
 }
@@ -810,7 +743,7 @@ __device__ __forceinline__ bool settled(const Query& me, const Box& cells, const
   return bound == INFINITY || (bound > 0 && me.t.last(kk) < bound * bound);
 }
 
-// One wave per chunk of <= 64 queries (knn_scan_kernel); the passes of the header comment.
+// One wave per chunk of <= 64 queries of one brick; the passes of the header comment.
 // amdgpu_waves_per_eu(4): 128 VGPRs (4 spilled) instead of 138, so 4 waves per SIMD (the LDS
 // allows 4 work-groups per CU) instead of 3: the ~5000 chunks of a step run in fewer rounds
 // (driver window 2379-2398 -> 2400-2429 steps/s, A/B on one box).
@@ -818,8 +751,8 @@ template <int kk>  // min(M, 3), a compile-time constant so the top-3 stays in r
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) void knn_query_kernel(
     const float* __restrict__ orig, const float* __restrict__ vals, int64_t N, int64_t M,
     int64_t Cpad, const float* __restrict__ gp, const uint64_t* __restrict__ start,
-    const float4* __restrict__ refs, const float4* __restrict__ qpts,
-    const uint4* __restrict__ chunks, int64_t maxch, const int32_t* __restrict__ nchunk,
+    const float4* __restrict__ refs, const int32_t* __restrict__ qorder,
+    const uint2* __restrict__ chunks, int64_t maxch, const int32_t* __restrict__ nchunk,
     int32_t* __restrict__ olist, float* __restrict__ obound, int32_t* __restrict__ ocount,
     float* __restrict__ out) {
   __shared__ __attribute__((aligned(16))) float cand[4][4][kCandCap];
@@ -834,24 +767,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
   const Box none = {1, 0, 1, 0, 1, 0};
   const int nch = nchunk[b];
   for (int item = blockIdx.x * 4 + wv; item < nch; item += gridDim.x * 4) {
-    const uint4 ch = chunks[b * maxch + item];
+    const uint2 ch = chunks[b * maxch + item];
     const bool valid = ch.x + lane < ch.y;
 #ifdef KNN_TRACE
     const unsigned long long kt0 = clock64();
     unsigned long long kt1 = 0, kt2 = 0;
     uint32_t ks1 = 0, ks2 = 0, ks3 = 0, ko1 = 0, ko2 = 0, kvol = 0;
 #endif
-    // the query and the box of its chunk's cells arrive together (the box from the descriptor:
-    // the ref ranges of pass 1 load without waiting for the query coordinates)
-    const float4 qp = qpts[b * N + (valid ? ch.x + lane : ch.x)];
-    const int bid = (int)ch.z, bxi = bid % g.bx, byi = (bid / g.bx) % g.by, bzi = bid / (g.bx * g.by);
-    const uint32_t cb = ch.w;
-    const int lx = 4 * bxi + (int)(cb & 31u), hx = 4 * bxi + (int)((cb >> 5) & 31u);
-    const int ly = 4 * byi + (int)((cb >> 10) & 3u), hy = 4 * byi + (int)((cb >> 12) & 3u);
-    const int lz = 4 * bzi + (int)((cb >> 14) & 3u), hz = 4 * bzi + (int)((cb >> 16) & 3u);
-    const int64_t n = __float_as_int(qp.w);
+    const int64_t n = qorder[b * N + (valid ? ch.x + lane : ch.x)];
+    const float* qp = orig + (b * N + n) * 3;
     Query me;
-    me.init(qp.x, qp.y, qp.z);
+    me.init(qp[0], qp[1], qp[2]);
+    const int cx = cell_coord(me.fx, g.o[0], g.inv, g.d[0]);
+    const int cy = cell_coord(me.fy, g.o[1], g.inv, g.d[1]);
+    const int cz = cell_coord(me.fz, g.o[2], g.inv, g.d[2]);
+    const int lx = wave_min(cx), hx = wave_max(cx), ly = wave_min(cy), hy = wave_max(cy),
+              lz = wave_min(cz), hz = wave_max(cz);
     // 1. the chunk's cell box grown by one cell
     Box pb = {max(lx - 1, 0), min(hx + 1, g.d[0] - 1), max(ly - 1, 0), min(hy + 1, g.d[1] - 1),
               max(lz - 1, 0), min(hz + 1, g.d[2] - 1)};
@@ -1333,10 +1264,10 @@ extern "C" int pcst_knn3_build(const float* orig, const int64_t* idx, int64_t B,
   hipLaunchKernelGGL(knn_count_kernel, dim3(gc, b), dim3(256), pad_count, s, orig, idx, w.stats,
                      w.known, N, M, w.Cmax, w.T, w.Cpad, w.gp, w.cnt, w.tsum, w.crank);
   hipLaunchKernelGGL(knn_scan_kernel, dim3((unsigned)w.T, b), dim3(256), pad_scan, s, w.cnt, w.tsum,
-                     w.gp, w.T, w.Cpad, w.chunks, w.maxch, w.nchunk);
+                     w.T, w.Cpad, w.chunks, w.maxch, w.nchunk);
   const unsigned gf = (unsigned)std::min<int64_t>(cdiv(M + N, 256), 2048);
   hipLaunchKernelGGL(knn_fill_kernel, dim3(gf, b), dim3(256), pad_fill, s, orig, idx, N, M, w.Cpad,
-                     w.cnt, w.crank, w.refs, w.qpts);
+                     w.cnt, w.crank, w.refs, w.qorder);
   PCST_LAUNCH_CHECK("knn3_build");
   return PCST_OK;
 }
@@ -1361,7 +1292,7 @@ extern "C" int pcst_knn3_query(const float* coarse, const float* orig, int64_t B
   const unsigned gq = (unsigned)std::min<int64_t>(cdiv(w.maxch, 4), kQueryBlocks);
   auto qk = M >= 3 ? knn_query_kernel<3> : (M == 2 ? knn_query_kernel<2> : knn_query_kernel<1>);
   hipLaunchKernelGGL(qk, dim3(gq, b), dim3(256), 0, s, orig, coarse, N, M, w.Cpad, w.gp, w.cnt,
-                     w.refs, w.qpts, w.chunks, w.maxch, w.nchunk, w.olist, w.obound, w.ocount, out);
+                     w.refs, w.qorder, w.chunks, w.maxch, w.nchunk, w.olist, w.obound, w.ocount, out);
   if (PCST_X_KNN_OUTLIER_EXHAUSTIVE) {  // the exhaustive pass (A/B experiments)
     auto ok = M >= 3 ? knn_outlier_kernel<3>
                      : (M == 2 ? knn_outlier_kernel<2> : knn_outlier_kernel<1>);

@@ -37,6 +37,8 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--amp", type=int, default=1, help="Config.use_amp (reference default 1)")
+    ap.add_argument("--amp-dtype", default="float16", choices=["float16", "bfloat16"],
+                    help="Config.amp_dtype (float16: the reference's CUDA autocast)")
     args = ap.parse_args()
 
     from pointcloud_style_transfer_amd import _hip
@@ -50,7 +52,7 @@ def main():
     device = torch.device("cuda", torch.cuda.current_device())
     logdir = tempfile.mkdtemp(prefix="pcst_train_")
     cfg = Config(make_dirs=False, log_dir=logdir, checkpoint_dir=logdir, use_amp=bool(args.amp),
-                 gradient_accumulation_steps=1, batch_size=args.batch)
+                 gradient_accumulation_steps=1, batch_size=args.batch, amp_dtype=args.amp_dtype)
     torch.manual_seed(0)
     trainer = DiffusionTrainer(cfg, device=str(device))
     trainer.model.train()
@@ -109,13 +111,16 @@ def main():
             "ms_per_step": round(elapsed / args.steps * 1e3, 2),
             "higher_is_better": True,
             "scaling": "weak",
-            "dtype": "fp32 (autocast on)" if args.amp else "fp32",
+            "dtype": f"fp32 (autocast {args.amp_dtype})" if args.amp else "fp32",
             "data": "synthetic (numpy PCG64 anisotropic Gaussian clouds, random-init weights)",
             "config": {"workload": "DiffusionTrainer.train_step, accumulation 1 "
                                    "(BASELINE configs[2]; configs[3] under torchrun)",
                        "clouds_per_gpu": B, "global_batch": world * B, "points": args.points,
                        "parallelism": f"ddp{world}" if world > 1 else "single"},
-            "chamfer_fwd": {"bound": "valu fp32", "avg_launch_ms": round(ch_ms, 3) if ch_ms else None,
+            "chamfer_fwd": {"bound": "valu fp32", "mode": "0 (hybrid: budgeted grid + exhaustive "
+                                                          "overflow rows; achieved counts every pair "
+                                                          "of the exhaustive product)",
+                            "avg_launch_ms": round(ch_ms, 3) if ch_ms else None,
                             "pairs_per_direction": pairs,
                             "achieved": round(ch_tflops, 2) if ch_tflops else None,
                             "peak": VALU_F32_PEAK_TFLOPS, "unit": "TFLOP/s",
