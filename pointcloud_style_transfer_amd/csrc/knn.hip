@@ -124,7 +124,13 @@ struct Grid {
     d[0] = __float_as_int(G[5]); d[1] = __float_as_int(G[6]); d[2] = __float_as_int(G[7]);
     bx = (d[0] + 3) >> 2;
     by = (d[1] + 3) >> 2;
+    // A point's computed cell floor((p - o) * inv) can differ from its exact cell when p lies
+    // within this distance of a cell face: fp32 rounding of p - o and of the product (|p - o| <=
+    // (d + 1) s, 2^-24 relative each) and inv = fl(1/s) against s (2^-24 each side) give at most
+    // ~(d + 1) * 2.4e-7 cells.  Every lower bound of a distance to unscanned cells subtracts it.
+    slack = (double)s * (3e-7 * (double)(max(d[0], max(d[1], d[2])) + 1) + 1e-5);
   }
+  double slack;
 };
 
 __device__ __forceinline__ int cell_coord(float p, float o, float inv, int d) {
@@ -734,7 +740,7 @@ __device__ __forceinline__ double outside_bound(const Query& me, const Box& c, c
   if (c.y1 + 1 < g.d[1]) bound = fmin(bound, (oy + (c.y1 + 1) * s) - me.qy);
   if (c.z0 > 0) bound = fmin(bound, me.qz - (oz + c.z0 * s));
   if (c.z1 + 1 < g.d[2]) bound = fmin(bound, (oz + (c.z1 + 1) * s) - me.qz);
-  return bound - 1e-5 * s;  // covers fp32 cell-assignment rounding
+  return bound - g.slack;  // covers fp32 cell-assignment rounding
 }
 
 __device__ __forceinline__ bool settled(const Query& me, const Box& cells, const Grid& g, int kk) {
@@ -801,7 +807,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
       bool ball = open && dk != INFINITY;
       int bx0 = 0x7fffffff, bx1 = -1, by0 = 0x7fffffff, by1 = -1, bz0 = 0x7fffffff, bz1 = -1;
       if (ball) {
-        const float r = (float)(sqrt(dk) * (1.0 + 1e-5)) + 1e-4f * g.s;
+        const float r = (float)(sqrt(dk) * (1.0 + 1e-5) + 2.0 * g.slack);
         const Box lb = {cell_coord(me.fx - r, g.o[0], g.inv, g.d[0]),
                         cell_coord(me.fx + r, g.o[0], g.inv, g.d[0]),
                         cell_coord(me.fy - r, g.o[1], g.inv, g.d[1]),
@@ -1160,7 +1166,7 @@ __global__ __launch_bounds__(256) void knn_outlier_brick_kernel(
           const double ex = fmax(fmax(x0 - me.qx, me.qx - (x0 + bs)), 0.0);
           const double ey = fmax(fmax(y0 - me.qy, me.qy - (y0 + bs)), 0.0);
           const double ez = fmax(fmax(z0 - me.qz, me.qz - (z0 + bs)), 0.0);
-          const double e = fmax(sqrt(ex * ex + ey * ey + ez * ez) - 1e-5 * g.s, 0.0);
+          const double e = fmax(sqrt(ex * ex + ey * ey + ez * ez) - g.slack, 0.0);
           if (e * e > lim) return;
           const int u0 = ((z * nby + y) * nbx + x) << 6;
           lo = S[u0];
