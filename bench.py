@@ -351,6 +351,8 @@ def main():
         else:
             knn_ws = None
 
+        vws = _hip.voxel_copies_workspace(C, args.points, 2, device=device)
+        pk = npred.packed()  # the loop changes no weight (as guided_sample_loop)
         S = len(timesteps)
         timing_event = ((lambda: _hip.DeviceEvent(timing=True)) if dmod.DEVICE_EVENTS
                         else (lambda: torch.cuda.Event(enable_timing=True)))
@@ -364,15 +366,15 @@ def main():
             t = timesteps[i % len(timesteps)]
             t_prev = timesteps[i % len(timesteps) + 1] if t > 0 else -1
             cnd = conds[i % len(timesteps)]
-            xc, xi = hp.downsample_copies(x, 2)
+            xc, xi = hp.downsample_copies(x, 2, vws)
 
             def mlp(xc_):
                 if not timed:
-                    return npred.forward_cond(xc_, cnd)
+                    return npred.forward_cond(xc_, cnd, pk)
                 # on the stream the MLP runs on; device-scope fences (no L2 writeback bubble
                 # around the timed kernel) unless tools/knobs.py turned them off
                 e0, e1 = timing_event(), timing_event()
-                blob, bias = npred.packed()[:2]
+                blob, bias = pk[:2]
                 e0.record()
                 nc_ = _hip.noise_mlp(xc_.reshape(-1, 3), cfg.global_points, cnd, blob, bias,
                                      npred.precision_code).view(2 * C, -1, 3)
@@ -414,6 +416,7 @@ def main():
         if world == 1 and not args.no_other_precision:
             prec0 = cfg.precision
             cfg.precision = "fp32" if prec0 == "bf16" else "bf16"
+            pk = npred.packed()  # the other mode's weight stream
             try:
                 with lctx:
                     x = torch.from_numpy(xT_np).to(device)
@@ -435,6 +438,7 @@ def main():
                                  "after it (not part of value)"}
             finally:
                 cfg.precision = prec0
+                pk = npred.packed()
 
     mlp_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
     flop = FLOP_PER_POINT * 2 * C * cfg.global_points

@@ -254,7 +254,12 @@ def _workspace(fn, *dims, device):
 
 
 # ----------------------------------------------------------------------------- voxel downsample
-def voxel_downsample(points, target, seed=0, perm_provider=None, copies=1):
+def voxel_copies_workspace(B, N, copies, device):
+    """A workspace for voxel_downsample(..., copies=copies, ws=) of B clouds of N points."""
+    return _workspace("pcst_voxel_copies_workspace_size", B, N, copies, device=device)
+
+
+def voxel_downsample(points, target, seed=0, perm_provider=None, copies=1, ws=None):
     """HierarchicalProcessor._voxel_grid_downsample_torch for N > target, all clouds at once.
 
     perm_provider=None: the random subset is drawn on the device from `seed`.
@@ -272,7 +277,13 @@ def voxel_downsample(points, target, seed=0, perm_provider=None, copies=1):
     B, N, _ = points.shape
     dev = points.device
     if perm_provider is None:
-        ws = _workspace("pcst_voxel_copies_workspace_size", B, N, copies, device=dev)
+        if ws is None:
+            ws = voxel_copies_workspace(B, N, copies, dev)
+        else:
+            need = ctypes.c_size_t(0)
+            _call("pcst_voxel_copies_workspace_size", B, N, copies, ctypes.byref(need))
+            if ws.numel() < need.value or ws.device != dev:
+                raise RuntimeError("voxel_downsample: workspace too small or on another device")
         out_idx = torch.empty(copies * B, target, dtype=torch.int64, device=dev)
         out_pts = torch.empty(copies * B, target, 3, dtype=torch.float32, device=dev)
         _call("pcst_voxel_downsample_copies", _ptr(points), B, N, copies, target, _ptr(ws),

@@ -1234,11 +1234,14 @@ extern "C" int pcst_knn_workspace_size(int64_t B, int64_t N, int64_t M, size_t* 
 // CU's 160): it only takes the CUs the MLP leaves idle in its last partial round, and a floor just
 // above the MLP's leftover (8 KiB) keeps as many build workgroups per idle CU as their own LDS
 // allows.  A pure function of the kernel and the floor (no state kept between calls).
-static unsigned pad_for(const void* kernel, unsigned floor_bytes) {
-  if (!floor_bytes) return 0;
-  hipFuncAttributes a{};
-  if (hipFuncGetAttributes(&a, kernel) != hipSuccess) return floor_bytes;
-  return a.sharedSizeBytes >= floor_bytes ? 0u : floor_bytes - (unsigned)a.sharedSizeBytes;
+// The kernels' static LDS is a compile-time constant (their __shared__ arrays), so no runtime
+// attribute query sits on the launch path (hipFuncGetAttributes cost ~5 us of host time each).
+constexpr unsigned kLdsPre = 0;
+constexpr unsigned kLdsCount = 8 * sizeof(float) + kKnnMaxTiles * sizeof(unsigned long long);
+constexpr unsigned kLdsScan = (kKnnTile + kKnnTile / 32 + 8) * sizeof(unsigned long long);
+constexpr unsigned kLdsFill = 0;
+static unsigned pad_for(unsigned static_lds, unsigned floor_bytes) {
+  return static_lds >= floor_bytes ? 0u : floor_bytes - static_lds;
 }
 
 // Phase 1 (positions only: the coarse set's points and the full cloud): grid statistics, the
@@ -1257,10 +1260,8 @@ extern "C" int pcst_knn3_build(const float* orig, const int64_t* idx, int64_t B,
   KnnWS w = carve_knn(workspace, B, N, M);
   const int b = (int)B;
   const unsigned f = (unsigned)lds_floor;
-  const unsigned pad_pre = pad_for((const void*)knn_pre_kernel, f),
-                 pad_count = pad_for((const void*)knn_count_kernel, f),
-                 pad_scan = pad_for((const void*)knn_scan_kernel, f),
-                 pad_fill = pad_for((const void*)knn_fill_kernel, f);
+  const unsigned pad_pre = pad_for(kLdsPre, f), pad_count = pad_for(kLdsCount, f),
+                 pad_scan = pad_for(kLdsScan, f), pad_fill = pad_for(kLdsFill, f);
   // error word, counters, known rows, tile sums and packed counts are contiguous in the carve
   PCST_HIP(hipMemsetAsync(w.err, 0, (size_t)(w.bytes - ((char*)w.err - (char*)workspace)), s),
            "knn: memset");

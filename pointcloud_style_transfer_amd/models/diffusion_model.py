@@ -175,12 +175,14 @@ class NoisePredictor(nn.Module):
         return not (_ag.needs_grad(self) or self._dropout_active()
                     or (style_feat.requires_grad and torch.is_grad_enabled()))
 
-    def forward_cond(self, noisy_points: torch.Tensor, cond: torch.Tensor) -> torch.Tensor:
+    def forward_cond(self, noisy_points: torch.Tensor, cond: torch.Tensor,
+                     packed: Optional[tuple] = None) -> torch.Tensor:
         """The fused inference forward with precomputed conditioning rows (`cond()` of the
         same timesteps and style features): the sampling loops compute every step's rows in one
-        launch before the loop."""
+        launch before the loop.  `packed` (this module's `packed()`, fetched once before a loop
+        that does not change the weights) skips the per-call weight-version check."""
         B, N, _ = noisy_points.shape
-        blob, bias = self.packed()[:2]
+        blob, bias = (packed if packed is not None else self.packed())[:2]
         out = _hip.noise_mlp(noisy_points.reshape(B * N, 3), N, cond, blob, bias,
                              self.precision_code)
         return out.view(B, N, 3)
@@ -214,16 +216,17 @@ class HierarchicalProcessor:
     def downsample(self, points: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
         return self._voxel_grid_downsample_torch(points, self.global_points)
 
-    def downsample_copies(self, points: torch.Tensor,
-                          copies: int) -> Tuple[torch.Tensor, torch.Tensor]:
+    def downsample_copies(self, points: torch.Tensor, copies: int,
+                          ws: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, torch.Tensor]:
         """downsample(torch.cat([points] * copies)) -- the CFG batch of guided_sample_loop
         (diffusion_model.py:244-247) -- without building or re-hashing the copies.  Replay runs
-        take the concatenated path: the reference draws one permutation per row."""
+        take the concatenated path: the reference draws one permutation per row.  `ws`
+        (_hip.voxel_copies_workspace of the same shape) is reused instead of allocated."""
         src = _rng.source()
         if points.shape[1] <= self.global_points or src.replaying:
             return self.downsample(torch.cat([points] * copies))
         return _hip.voxel_downsample(points, self.global_points, seed=src.device_seed(),
-                                     copies=copies)
+                                     copies=copies, ws=ws)
 
     def upsample_knn(self, coarse_points: torch.Tensor, original_points: torch.Tensor,
                      coarse_indices: torch.Tensor) -> torch.Tensor:
@@ -437,7 +440,8 @@ class DiffusionProcess:
             S = len(timesteps)
             conds = npred.cond(t_rows.reshape(-1), style_in.repeat(S, 1)).view(S, 2 * B, -1)
         overlap = use_hierarchical and overlap_knn_build(2 * B * model.config.global_points)
-        side = ws = None
+        side = ws = vws = None
+        pk = npred.packed() if conds is not None else None  # the loop changes no weight
         ctx = contextlib.nullcontext()
         if overlap:
             loop, side = step_streams(device)
@@ -447,16 +451,18 @@ class DiffusionProcess:
         with ctx:
             if overlap:
                 ws = _hip.knn_workspace(2 * B, shape[1], model.config.global_points, device=device)
+            if use_hierarchical:
+                vws = _hip.voxel_copies_workspace(B, shape[1], 2, device=device)
             try:
                 for i, t in enumerate(timesteps):
                     t_in = t_rows[i]
                     if conds is not None:
                         cond_i = conds[i]
-                        mlp = lambda c: npred.forward_cond(c, cond_i)  # noqa: E731
+                        mlp = lambda c: npred.forward_cond(c, cond_i, pk)  # noqa: E731
                     else:
                         mlp = lambda c: npred(c, t_in, style_in)  # noqa: E731
                     if use_hierarchical:
-                        xc, xi = hp.downsample_copies(x, 2)
+                        xc, xi = hp.downsample_copies(x, 2, vws)
                         eps = hierarchical_eps(hp, mlp, xc, xi, x_cat, ws, side)
                     else:
                         eps = mlp(x_cat)

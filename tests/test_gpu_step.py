@@ -60,7 +60,9 @@ def test_voxel_golden_120k(H, golden):
 
 
 @pytest.mark.parametrize("N,T,B,sig", [(5000, 1000, 3, (1, 1, 0.15)), (20000, 3000, 2, (1, 1, 1e-3)),
-                                        (70000, 30000, 2, (1, 1, 0.15)), (9000, 8000, 1, (1, 1, 1))])
+                                        (70000, 30000, 2, (1, 1, 0.15)), (9000, 8000, 1, (1, 1, 1)),
+                                        (300, 250, 2, (1, 1, 1)), (1025, 1000, 1, (1, 1, 1)),
+                                        (3000, 2999, 1, (1, 1, 1))])
 def test_voxel_vs_oracle_random_perm(H, N, T, B, sig):
     """Reps/pool bit-exact vs the oracle; the device-drawn subset is a valid draw."""
     rng = np.random.default_rng(N)
