@@ -322,6 +322,17 @@ int pcst_event_record(void* event, void* stream);
 int pcst_stream_wait_event(void* stream, void* event);
 int pcst_event_elapsed_ms(void* start, void* end, float* ms);
 
+/* Kernel-side stream signal: a one-lane kernel on `stream` publishes *flag = value (agent-scope
+ * release, after everything enqueued before it on that stream); pcst_signal_wait enqueues a
+ * one-workgroup kernel that polls *flag until it is >= value (agent-scope acquire), so the
+ * work enqueued after it on ITS stream starts after the signal.  A cross-stream dependency
+ * without an event marker on the producer's queue (an event that another queue waits on costs
+ * that queue ~17 us; this ~3 us, tools/sync_probe.hip).  The wait gives up after ~10 s of
+ * polling and then sets *err = 1 (err may be NULL).  Values must grow monotonically per flag.
+ * flag: one uint32 of device memory, zero-initialised by the caller. */
+int pcst_signal_write(uint32_t* flag, uint32_t value, void* stream);
+int pcst_signal_wait(const uint32_t* flag, uint32_t value, int32_t* err, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -74,3 +74,50 @@ extern "C" int pcst_cfg_ddim_step_dcoef(const float* x, const float* eps_c, cons
   PCST_LAUNCH_CHECK("cfg_ddim_step_dcoef");
   return PCST_OK;
 }
+
+// ---- kernel-side stream signal (pcst.h: pcst_signal_write / pcst_signal_wait) -------------
+namespace pcst {
+// one lane: the stream's earlier kernels have completed and released at their end; the fence
+// makes this kernel's view current before the flag (vector store, agent scope) is published
+__global__ void signal_write_kernel(uint32_t* flag, uint32_t value) {
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __hip_atomic_store(flag, value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+// one lane polls (agent-scope loads, L2-served, with s_sleep between polls) until the flag
+// reaches `value`, at most kSignalPolls times (~10 s); then an agent-scope acquire
+constexpr int kSignalPolls = 1 << 26;
+__global__ void signal_wait_kernel(const uint32_t* flag, uint32_t value, int32_t* err) {
+  if (threadIdx.x == 0) {
+    bool ok = false;
+    for (int i = 0; i < kSignalPolls; ++i) {
+      if (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= value) {
+        ok = true;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(4);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    if (!ok && err) __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+}  // namespace pcst
+
+extern "C" int pcst_signal_write(uint32_t* flag, uint32_t value, void* stream) {
+  PCST_CHECK_ARG(flag != nullptr, "signal_write: null flag");
+  hipLaunchKernelGGL(pcst::signal_write_kernel, dim3(1), dim3(64), 0, pcst::as_stream(stream), flag,
+                     value);
+  PCST_LAUNCH_CHECK("signal_write");
+  return PCST_OK;
+}
+
+extern "C" int pcst_signal_wait(const uint32_t* flag, uint32_t value, int32_t* err, void* stream) {
+  PCST_CHECK_ARG(flag != nullptr, "signal_wait: null flag");
+  hipLaunchKernelGGL(pcst::signal_wait_kernel, dim3(1), dim3(64), 0, pcst::as_stream(stream), flag,
+                     value, err);
+  PCST_LAUNCH_CHECK("signal_wait");
+  return PCST_OK;
+}

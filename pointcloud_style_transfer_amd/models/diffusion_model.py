@@ -277,7 +277,11 @@ def hierarchical_eps(hp, mlp, xc, xi, x_cat, knn_ws=None, side=None):
         return hp.upsample_knn(mlp(xc), x_cat, xi)
     main = torch.cuda.current_stream()
     ready, built = _step_events(main.device)
-    ready.record(main)
+    if KERNEL_SIGNAL:  # main -> side by a kernel-side flag: no event marker on the loop's queue
+        ready = _step_signal(main.device)
+        ready.signal(main)
+    else:
+        ready.record(main)
     ready.wait(side)
     with torch.cuda.stream(side):
         handle = _hip.knn3_build(x_cat, xi, knn_ws, KNN_BUILD_LDS_FLOOR)
@@ -290,6 +294,19 @@ def hierarchical_eps(hp, mlp, xc, xi, x_cat, knn_ws=None, side=None):
 _STEP_EVENTS: Dict[int, tuple] = {}
 # device-scope events for the step's cross-stream dependencies (tools/knobs.py: A/B only)
 DEVICE_EVENTS = True
+# The loop -> side dependency (the voxel output is ready) by kernel-side signalling instead of an
+# event: an event that another queue waits on stalls the recording queue ~17 us, a one-lane flag
+# kernel ~3 us (tools/sync_probe.hip).  The side -> loop one (the kNN build is done) stays an
+# event: waiting on an event that has already completed costs the waiting queue ~0.3 us.
+KERNEL_SIGNAL = True
+_STEP_SIGNALS: Dict[int, "_hip.DeviceSignal"] = {}
+
+
+def _step_signal(device):
+    key = torch.device(device).index or 0
+    if key not in _STEP_SIGNALS:
+        _STEP_SIGNALS[key] = _hip.DeviceSignal(device)
+    return _STEP_SIGNALS[key]
 
 
 class _TorchEvent:

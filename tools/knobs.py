@@ -2,7 +2,8 @@
 
     import knobs; knobs.apply()
 
-reads PCST_KNN_OVERLAP=0|1, PCST_KNN_BUILD_LDS_FLOOR=<bytes>, PCST_DEVICE_EVENTS=0|1 and
+reads PCST_KNN_OVERLAP=0|1, PCST_KNN_BUILD_LDS_FLOOR=<bytes>, PCST_DEVICE_EVENTS=0|1,
+PCST_KERNEL_SIGNAL=0|1 and
 PCST_NM_BF16_KERNEL=1 (the 32x32x16 pair kernel) and sets the matching module constants of
 models.diffusion_model.  Kernel-side variants are experiment builds (csrc/Makefile XDEF,
 loaded through PCST_LIB)."""
@@ -23,5 +24,7 @@ def apply():
         dm.KNN_BUILD_LDS_FLOOR = int(e["PCST_KNN_BUILD_LDS_FLOOR"])
     if "PCST_DEVICE_EVENTS" in e:
         dm.DEVICE_EVENTS = e["PCST_DEVICE_EVENTS"] != "0"
+    if "PCST_KERNEL_SIGNAL" in e:
+        dm.KERNEL_SIGNAL = e["PCST_KERNEL_SIGNAL"] != "0"
     if e.get("PCST_NM_BF16_KERNEL") == "1":
         dm.NoisePredictor.bf16_code = packing.BF16

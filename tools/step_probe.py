@@ -10,6 +10,7 @@ median ms/step of each:
   noev    the same without the timing events
   seq     one stream: the kNN build inline before the MLP, no events at all
   seq_ev  seq with the timing events around the MLP
+  evready noev with the loop -> side dependency as an event instead of the kernel-side signal
 A development tool (tools/ only)."""
 import argparse
 import os
@@ -52,6 +53,7 @@ def main():
         ws = _hip.knn_workspace(2, 120000, cfg.global_points, device=dev)
 
         def run(mode, n):
+            dmod.KERNEL_SIGNAL = mode != "evready"  # evready: the loop -> side dependency as an event
             x = xT.clone()
             x_cat = torch.cat([x, x]).contiguous()
             timed = mode.endswith("ev") or mode == "bench"
