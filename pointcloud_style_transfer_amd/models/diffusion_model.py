@@ -40,7 +40,14 @@ class TimeEmbedding(nn.Module):
         self.dim = dim
 
     def freqs(self, device) -> torch.Tensor:
-        return packing.time_freqs(self.dim).to(device)
+        # kept per device: a pageable host->device copy synchronises the stream (every training
+        # step would wait for the work queued before it); not a buffer, so the state_dict stays
+        # the reference's
+        cache = self.__dict__.setdefault("_freqs", {})
+        key = str(torch.device(device))
+        if key not in cache:
+            cache[key] = packing.time_freqs(self.dim).to(device)
+        return cache[key]
 
     def forward(self, t: torch.Tensor) -> torch.Tensor:
         _hip.require_device(t)
@@ -62,8 +69,8 @@ class StyleEncoder(nn.Module):
         self.style_mlp = nn.Sequential(nn.Linear(feature_dim, 512), nn.ReLU(), nn.Dropout(0.1),
                                        nn.Linear(512, feature_dim), nn.ReLU())
 
-    def forward(self, points: torch.Tensor) -> torch.Tensor:
-        f = self.encoder(points)
+    def forward(self, points: torch.Tensor, geometry: Optional[list] = None) -> torch.Tensor:
+        f = self.encoder(points, geometry)
         if _ag.needs_grad(self):
             h = _ag.linear(f, self.style_mlp[0], True)
             h = self.style_mlp[2](h)
@@ -343,11 +350,24 @@ class PointCloudDiffusionModel(nn.Module):
         self.hierarchical_processor = HierarchicalProcessor(total_points=config.total_points,
                                                             global_points=config.global_points)
 
+    def style_geometry(self, condition_points: torch.Tensor, use_hierarchical: bool = True):
+        """The positions-only part of the style branch of forward(): the condition cloud's
+        downsample and the encoder's FPS / ball-query indices, in forward()'s draw order.
+        Passing it back as forward(style_geometry=...) skips recomputing it."""
+        if use_hierarchical and condition_points.shape[1] > self.config.global_points:
+            xyz = self.hierarchical_processor.downsample(condition_points)[0]
+        else:
+            xyz = condition_points
+        return xyz, self.style_encoder.encoder.geometry(xyz)
+
     def forward(self, noisy_points: torch.Tensor, timestep: torch.Tensor,
                 condition_points: torch.Tensor, cond_drop_prob: float = 0.0,
-                use_hierarchical: bool = True) -> Tuple[torch.Tensor, Optional[torch.Tensor]]:
+                use_hierarchical: bool = True,
+                style_geometry: Optional[tuple] = None) -> Tuple[torch.Tensor, Optional[torch.Tensor]]:
         hp = self.hierarchical_processor
-        if use_hierarchical and condition_points.shape[1] > self.config.global_points:
+        if style_geometry is not None:  # style_geometry(condition_points, use_hierarchical)
+            style_feat = self.style_encoder(*style_geometry)
+        elif use_hierarchical and condition_points.shape[1] > self.config.global_points:
             style_feat = self.style_encoder(hp.downsample(condition_points)[0])
         else:
             style_feat = self.style_encoder(condition_points)

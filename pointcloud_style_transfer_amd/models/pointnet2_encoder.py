@@ -37,6 +37,10 @@ def farthest_point_sample(xyz: torch.Tensor, npoint: int, *,
     B, N, _ = xyz.shape
     if start_idx is None:
         start_idx = _rng.source().randint(0, N, (B,))
+    if not start_idx.is_cuda and xyz.is_cuda:
+        # through pinned memory, asynchronously: a pageable host->device copy synchronises the
+        # stream, which would stall the host on all the work queued before this forward
+        start_idx = start_idx.pin_memory().to(xyz.device, non_blocking=True)
     return _hip.fps(xyz, npoint, start_idx.to(xyz.device))
 
 
@@ -64,17 +68,24 @@ class SetAbstraction(nn.Module):
             last = out
         self.group_all = group_all
 
-    def forward(self, xyz: torch.Tensor,
-                points: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, torch.Tensor]:
+    def geometry(self, xyz: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
+        """The layer's sampling and grouping (pointnet2_encoder.py:85-91): (FPS indices, their
+        points, ball-query indices).  Positions only -- no parameter enters -- so a trainer can
+        compute it ahead of the forward (DiffusionTrainer.prefetch_style_geometry)."""
+        fidx = farthest_point_sample(xyz, self.npoint)
+        new_xyz = index_points(xyz, fidx)
+        gidx = query_ball_point(self.radius, self.nsample, xyz, new_xyz)
+        return fidx, new_xyz, gidx
+
+    def forward(self, xyz: torch.Tensor, points: Optional[torch.Tensor] = None,
+                geometry: Optional[tuple] = None) -> Tuple[torch.Tensor, torch.Tensor]:
         B, N, _ = xyz.shape
         if self.group_all:
             new_xyz = torch.zeros(B, 1, 3, device=xyz.device)
             grouped = xyz if points is None else torch.cat([xyz, points], dim=-1)
             feats = self.apply_mlp(grouped.reshape(B * N, -1), pool_ns=N)  # [B, C]
             return new_xyz, feats
-        fidx = farthest_point_sample(xyz, self.npoint)
-        new_xyz = index_points(xyz, fidx)
-        gidx = query_ball_point(self.radius, self.nsample, xyz, new_xyz)
+        fidx, new_xyz, gidx = geometry if geometry is not None else self.geometry(xyz)
         if points is not None and points.requires_grad and torch.is_grad_enabled():
             # training: the same fused gather, with its deterministic scatter backward
             new_xyz, grouped = _ag.GroupGatherFn.apply(xyz, points, fidx, gidx)
@@ -140,9 +151,15 @@ class PointNet2Encoder(nn.Module):
         self.sa3 = SetAbstraction(npoint=None, radius=None, nsample=None, in_channel=256,
                                   mlp=[256, 512, feature_dim], group_all=True)
 
-    def forward(self, xyz: torch.Tensor) -> torch.Tensor:
+    def geometry(self, xyz: torch.Tensor) -> list:
+        """SA1's and SA2's sampling and grouping for `xyz`, in the forward's draw order."""
+        g1 = self.sa1.geometry(xyz)
+        return [g1, self.sa2.geometry(g1[1])]
+
+    def forward(self, xyz: torch.Tensor, geometry: Optional[list] = None) -> torch.Tensor:
         B = xyz.shape[0]
-        l1_xyz, l1_points = self.sa1(xyz, None)
-        l2_xyz, l2_points = self.sa2(l1_xyz, l1_points.permute(0, 2, 1))
+        g1, g2 = geometry if geometry is not None else (None, None)
+        l1_xyz, l1_points = self.sa1(xyz, None, g1)
+        l2_xyz, l2_points = self.sa2(l1_xyz, l1_points.permute(0, 2, 1), g2)
         _, g = self.sa3(l2_xyz, l2_points.permute(0, 2, 1))
         return g.view(B, -1)

@@ -141,6 +141,13 @@ class DiffusionTrainer:
         self.gradient_accumulation_steps = config.gradient_accumulation_steps
         self.gradient_clip_norm = 1.0
         self.ddp_model = self.model
+        # train_step(next_batch=...): the next batch's style geometry (condition-cloud downsample,
+        # FPS, ball query: positions only) is queued on a side stream at the start of a step and
+        # runs beside it; the next step's forward then starts at the SA MLPs.  Off while draws
+        # are replayed (the parity tests follow the reference's draw order).
+        self.prefetch_style_geometry = self.device_type == "cuda"
+        self._geo_next = None  # (condition tensor it was computed for, geometry, ready event)
+        self._geo_stream = None
         if self.distributed:
             from torch.nn.parallel import DistributedDataParallel as DDP
 
@@ -157,14 +164,24 @@ class DiffusionTrainer:
         return ((batch_idx + 1) % self.gradient_accumulation_steps == 0
                 or batch_idx == num_batches - 1)
 
-    def train_step(self, batch, batch_idx: int, num_batches: int):
-        """Body of the per-batch loop of train_one_epoch (trainer.py:70-127)."""
+    def train_step(self, batch, batch_idx: int, num_batches: int, *, host_sync: bool = True,
+                   next_batch=None):
+        """Body of the per-batch loop of train_one_epoch (trainer.py:70-127).
+
+        host_sync=False (keyword-only) returns the loss terms as device scalars instead of the
+        reference's python floats: nothing waits for the device, so the caller can queue the
+        next step before reading this one's values (train_one_epoch does; see _log_step).
+        next_batch (keyword-only): the batch the next call will get; its style geometry is
+        computed beside this step (prefetch_style_geometry)."""
         sync = self._is_sync_step(batch_idx, num_batches)
+        geo = self._take_geometry(batch)
+        if next_batch is not None:
+            self._queue_geometry(next_batch)
         # DDP: all-reduce only on the micro-step that ends the accumulation window
         ctx = (self.ddp_model.no_sync() if self.distributed and not sync
                else contextlib.nullcontext())
         with ctx:
-            loss, terms = self._forward_backward(batch)
+            loss, terms = self._forward_backward(batch, geo)
         if sync:
             self.scaler.unscale_(self.optimizer)
             torch.nn.utils.clip_grad_norm_(self.model.parameters(), self.gradient_clip_norm)
@@ -172,10 +189,56 @@ class DiffusionTrainer:
             self.scaler.update()
             self.optimizer.zero_grad()
             self.ema.update()
+        if not host_sync:
+            return loss.detach(), {k: v.detach() for k, v in terms.items()}
         # the reference's loss dict of python floats (losses.py:93-102), read once the whole
         # step is queued: its syncs then wait on work already in flight
         loss_dict = {k: v.item() for k, v in terms.items()}
         return loss, loss_dict
+
+    def _prefetching(self) -> bool:
+        return (self.prefetch_style_geometry and self.device_type == "cuda"
+                and not _rng.source().replaying)
+
+    def _queue_geometry(self, batch):
+        """Queue batch's style geometry on the side stream, ordered after the work queued so far
+        (not after this step's forward and backward, which are queued next)."""
+        if not self._prefetching():
+            return
+        real = batch["real_full"]
+        main = torch.cuda.current_stream(self.device)
+        if self._geo_stream is None:
+            self._geo_stream = torch.cuda.Stream(device=self.device)
+        side = self._geo_stream
+        side.wait_stream(main)
+        with torch.cuda.stream(side), torch.no_grad():
+            real_dev = real.to(self.device, non_blocking=True)
+            geo = self.model.style_geometry(real_dev, self.config.use_hierarchical)
+            ready = torch.cuda.Event()
+            ready.record(side)
+        self._geo_next = (real, (real_dev, geo), ready)
+
+    def _take_geometry(self, batch):
+        """The prefetched geometry if it was computed for this batch's condition cloud."""
+        pending, self._geo_next = self._geo_next, None
+        if pending is None or pending[0] is not batch["real_full"] or not self._prefetching():
+            return None
+        real_dev, (xyz, geo) = pending[1]
+        main = torch.cuda.current_stream(self.device)
+        main.wait_event(pending[2])
+        for t in [real_dev, xyz] + [u for g in geo for u in g]:
+            t.record_stream(main)  # made on the side stream, used and freed on this one
+        return real_dev, (xyz, geo)
+
+    def _log_step(self, pbar, loss, terms) -> float:
+        """One step's contribution to the epoch's loss sum and its progress-bar line."""
+        loss_dict = {k: v.item() for k, v in terms.items()}
+        if hasattr(pbar, "set_postfix"):
+            pbar.set_postfix({"Loss": f"{loss_dict.get('total_loss', 0):.4f}",
+                              "L1": f"{loss_dict.get('noise_loss', 0):.4f}",
+                              "CD": f"{loss_dict.get('chamfer_loss', 0):.4f}",
+                              "LR": f"{self.optimizer.param_groups[0]['lr']:.2e}"})
+        return loss.item() * self.gradient_accumulation_steps
 
     def _amp_dtype(self):
         name = getattr(self.config, "amp_dtype", "float16")
@@ -183,9 +246,10 @@ class DiffusionTrainer:
             raise ValueError(f"Config.amp_dtype must be 'float16' or 'bfloat16', got {name!r}")
         return getattr(torch, name)
 
-    def _forward_backward(self, batch):
-        sim = batch["sim_full"].to(self.device)
-        real = batch["real_full"].to(self.device)
+    def _forward_backward(self, batch, geo=None):
+        # non_blocking: from a pinned loader batch the copies do not stall the host
+        sim = batch["sim_full"].to(self.device, non_blocking=True)
+        real = batch["real_full"].to(self.device, non_blocking=True) if geo is None else geo[0]
         B, N, C = sim.shape
         src = _rng.source()
         t = src.randint(0, self.config.num_timesteps, (B,), device=self.device).long()
@@ -194,7 +258,8 @@ class DiffusionTrainer:
                       dtype=self._amp_dtype()):
             pred, indices = self.ddp_model(noisy_points=noisy, timestep=t, condition_points=real,
                                            cond_drop_prob=self.config.cond_drop_prob,
-                                           use_hierarchical=self.config.use_hierarchical)
+                                           use_hierarchical=self.config.use_hierarchical,
+                                           style_geometry=None if geo is None else geo[1])
             if indices is not None:
                 ie = indices.unsqueeze(-1).expand(-1, -1, C)
                 actual_coarse = torch.gather(actual_noise, 1, ie)
@@ -221,14 +286,24 @@ class DiffusionTrainer:
         pbar = _progress(data_loader, f"Epoch {self.current_epoch}/{self.config.num_epochs} [Train]")
         self.optimizer.zero_grad()
         n = len(data_loader)
-        for batch_idx, batch in enumerate(pbar):
-            loss, loss_dict = self.train_step(batch, batch_idx, n)
-            total += loss.item() * self.gradient_accumulation_steps
-            if hasattr(pbar, "set_postfix"):
-                pbar.set_postfix({"Loss": f"{loss_dict.get('total_loss', 0):.4f}",
-                                  "L1": f"{loss_dict.get('noise_loss', 0):.4f}",
-                                  "CD": f"{loss_dict.get('chamfer_loss', 0):.4f}",
-                                  "LR": f"{self.optimizer.param_groups[0]['lr']:.2e}"})
+        # The reference reads each step's loss with .item() right after the step (a device sync
+        # that leaves the GPU idle while the host queues the next step's many small launches).
+        # Here step k's values are read after step k + 1 is queued: the same sum and the same
+        # progress-bar values, one step later.
+        pending = None
+        items = enumerate(pbar)
+        cur = next(items, None)
+        while cur is not None:
+            nxt = next(items, None)  # one batch ahead: its style geometry runs beside this step
+            batch_idx, batch = cur
+            step = self.train_step(batch, batch_idx, n, host_sync=False,
+                                   next_batch=None if nxt is None else nxt[1])
+            if pending is not None:
+                total += self._log_step(pbar, *pending)
+            pending = step
+            cur = nxt
+        if pending is not None:
+            total += self._log_step(pbar, *pending)
         avg = total / n
         self.writer.add_scalar("Loss/Train", avg, self.current_epoch)
         return avg

@@ -239,3 +239,73 @@ def test_trainer_resumes_reference_checkpoint_under_amp(tmp_path, monkeypatch):
     assert np.isfinite(float(loss))
     moved = sum(not torch.equal(b, p.detach()) for b, p in zip(before, tr.model.parameters()))
     assert moved > 70, moved
+
+
+def test_train_one_epoch_pipelined_readback_matches_per_step(tmp_path, monkeypatch):
+    """train_one_epoch reads step k's loss after queueing step k + 1 (train_step(host_sync=False))
+    and hands each step the next batch (style-geometry prefetch): the epoch average and the final
+    weights equal those of a loop that makes the same train_step calls but reads every step's
+    floats right away (the reference's order, trainer.py:70-127)."""
+    from pointcloud_style_transfer_amd.config.config import Config
+    from pointcloud_style_transfer_amd.synthetic import lidar_like_cloud
+    from pointcloud_style_transfer_amd.training.trainer import DiffusionTrainer
+
+    monkeypatch.chdir(tmp_path)
+    batches = [{"sim_full": torch.from_numpy(np.stack([lidar_like_cloud(10 * i + j, 4096)
+                                                       for j in range(2)])),
+                "real_full": torch.from_numpy(np.stack([lidar_like_cloud(500 + 10 * i + j, 4096)
+                                                        for j in range(2)]))}
+               for i in range(3)]
+
+    def fresh():
+        torch.manual_seed(0)
+        cfg = Config(total_points=4096, global_points=1024, use_amp=True,
+                     gradient_accumulation_steps=1, experiment_name="pipe", precision="fp32")
+        return DiffusionTrainer(cfg, device="cuda")
+
+    a = fresh()
+    torch.manual_seed(1)
+    avg_a = a.train_one_epoch(batches)
+    b = fresh()
+    torch.manual_seed(1)
+    b.model.train()
+    b.optimizer.zero_grad()
+    total = 0.0
+    for i, batch in enumerate(batches):
+        nxt = batches[i + 1] if i + 1 < len(batches) else None
+        loss, d = b.train_step(batch, i, len(batches), next_batch=nxt)
+        total += loss.item()
+        assert set(d) >= {"total_loss", "noise_loss"} and all(isinstance(v, float) for v in d.values())
+    assert avg_a == total / len(batches)
+    for (n, pa), (_, pb) in zip(a.model.named_parameters(), b.model.named_parameters()):
+        assert torch.equal(pa, pb), n
+
+
+@pytest.mark.parametrize("train", [False, True])
+def test_style_geometry_prefetch_equals_inline(train):
+    """forward(style_geometry=style_geometry(cond)) -- the trainer's prefetched style branch --
+    gives the forward's own result: same downsample, FPS and ball-query draws in the same order,
+    so with the generators reset the prediction and indices are bit-identical."""
+    from pointcloud_style_transfer_amd.config.config import Config
+    from pointcloud_style_transfer_amd.models.diffusion_model import PointCloudDiffusionModel
+    from pointcloud_style_transfer_amd.synthetic import lidar_like_cloud
+
+    torch.manual_seed(0)
+    cfg = Config(total_points=8192, global_points=2048, make_dirs=False, precision="fp32")
+    m = PointCloudDiffusionModel(cfg).cuda().train(train)
+    for mod in m.modules():
+        if isinstance(mod, torch.nn.Dropout):
+            mod.p = 0.0
+    noisy = torch.from_numpy(np.stack([lidar_like_cloud(7 + j, 8192) for j in range(2)])).cuda()
+    real = torch.from_numpy(np.stack([lidar_like_cloud(70 + j, 8192) for j in range(2)])).cuda()
+    t = torch.tensor([10, 500], device="cuda")
+    outs = []
+    for pre in (False, True):
+        torch.manual_seed(123)
+        torch.cuda.manual_seed(123)
+        with torch.no_grad():
+            geo = m.style_geometry(real) if pre else None
+            outs.append(m(noisy, t, real, 0.0, True, style_geometry=geo))
+    assert torch.equal(outs[0][1], outs[1][1])
+    assert torch.equal(outs[0][0], outs[1][0])
+

@@ -77,8 +77,10 @@ def main():
         return out
 
     _hip.chamfer_fwd = timed_chamfer
+    # as DiffusionTrainer.train_one_epoch: every step is handed the next batch (here the same
+    # one), whose style geometry then runs beside it
     for i in range(args.warmup):
-        trainer.train_step(batch, i, 1 << 30)
+        trainer.train_step(batch, i, 1 << 30, next_batch=batch)
     ev.clear()
     if world > 1:
         import torch.distributed as dist
@@ -86,8 +88,19 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    # as DiffusionTrainer.train_one_epoch: each step's loss values are read (.item()) after the
+    # next step is queued, not right after the step
+    def read(step):  # train_one_epoch's per-step readback (DiffusionTrainer._log_step)
+        return step[0].item(), {k: v.item() for k, v in step[1].items()}
+
+    pending = None
     for i in range(args.steps):
-        loss, _ = trainer.train_step(batch, i, 1 << 30)
+        step = trainer.train_step(batch, i, 1 << 30, host_sync=False,
+                                  next_batch=batch if i + 1 < args.steps else None)
+        if pending is not None:
+            loss, _ = read(pending)
+        pending = step
+    loss, _ = read(pending)
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     if world > 1:
