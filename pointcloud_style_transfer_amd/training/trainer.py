@@ -103,6 +103,27 @@ def _progress(it, desc):
         return it
 
 
+class DeferredLosses:
+    """One step's loss values, copied to pinned host memory behind the step (no host wait):
+    read() waits for that copy only -- a `.item()` on the step's tensors would be ordered behind
+    everything queued after the step as well."""
+
+    def __init__(self, loss: torch.Tensor, terms: dict):
+        self.keys = list(terms)
+        vals = torch.stack([loss.detach().float().reshape(())]
+                           + [terms[k].detach().float().reshape(()) for k in self.keys])
+        self.buf = torch.empty(len(self.keys) + 1, dtype=torch.float32, pin_memory=True)
+        self.buf.copy_(vals, non_blocking=True)
+        self.ready = torch.cuda.Event()
+        self.ready.record()
+
+    def read(self):
+        """(loss, {term: value}) as python floats (the values `.item()` gives)."""
+        self.ready.synchronize()
+        v = self.buf.tolist()
+        return v[0], dict(zip(self.keys, v[1:]))
+
+
 class DiffusionTrainer:
     """`DiffusionTrainer` (trainer.py:36-232)."""
 
@@ -168,7 +189,7 @@ class DiffusionTrainer:
                    next_batch=None):
         """Body of the per-batch loop of train_one_epoch (trainer.py:70-127).
 
-        host_sync=False (keyword-only) returns the loss terms as device scalars instead of the
+        host_sync=False (keyword-only) returns (loss tensor, DeferredLosses) instead of the
         reference's python floats: nothing waits for the device, so the caller can queue the
         next step before reading this one's values (train_one_epoch does; see _log_step).
         next_batch (keyword-only): the batch the next call will get; its style geometry is
@@ -190,7 +211,7 @@ class DiffusionTrainer:
             self.optimizer.zero_grad()
             self.ema.update()
         if not host_sync:
-            return loss.detach(), {k: v.detach() for k, v in terms.items()}
+            return loss.detach(), DeferredLosses(loss, terms)
         # the reference's loss dict of python floats (losses.py:93-102), read once the whole
         # step is queued: its syncs then wait on work already in flight
         loss_dict = {k: v.item() for k, v in terms.items()}
@@ -230,15 +251,15 @@ class DiffusionTrainer:
             t.record_stream(main)  # made on the side stream, used and freed on this one
         return real_dev, (xyz, geo)
 
-    def _log_step(self, pbar, loss, terms) -> float:
+    def _log_step(self, pbar, loss, deferred) -> float:
         """One step's contribution to the epoch's loss sum and its progress-bar line."""
-        loss_dict = {k: v.item() for k, v in terms.items()}
+        loss_value, loss_dict = deferred.read()
         if hasattr(pbar, "set_postfix"):
             pbar.set_postfix({"Loss": f"{loss_dict.get('total_loss', 0):.4f}",
                               "L1": f"{loss_dict.get('noise_loss', 0):.4f}",
                               "CD": f"{loss_dict.get('chamfer_loss', 0):.4f}",
                               "LR": f"{self.optimizer.param_groups[0]['lr']:.2e}"})
-        return loss.item() * self.gradient_accumulation_steps
+        return loss_value * self.gradient_accumulation_steps
 
     def _amp_dtype(self):
         name = getattr(self.config, "amp_dtype", "float16")

@@ -91,7 +91,7 @@ def main():
     # as DiffusionTrainer.train_one_epoch: each step's loss values are read (.item()) after the
     # next step is queued, not right after the step
     def read(step):  # train_one_epoch's per-step readback (DiffusionTrainer._log_step)
-        return step[0].item(), {k: v.item() for k, v in step[1].items()}
+        return step[1].read()
 
     pending = None
     for i in range(args.steps):
