@@ -359,7 +359,7 @@ def main():
         conds = None  # every step's conditioning rows, one launch per loop (as guided_sample_loop)
 
         def all_conds():
-            return npred.cond(t_rows.reshape(-1), style_in.repeat(S, 1)).view(S, 2 * C, -1)
+            return npred.cond(t_rows.reshape(-1), style_in.repeat(S, 1), pk).view(S, 2 * C, -1)
 
         def step(i, timed):
             nonlocal x

@@ -132,8 +132,9 @@ class NoisePredictor(nn.Module):
             self._pack_key = key
         return self._packed
 
-    def cond(self, timestep: torch.Tensor, style_feat: torch.Tensor) -> torch.Tensor:
-        _, _, freqs, wt_t, ws_t = self.packed()
+    def cond(self, timestep: torch.Tensor, style_feat: torch.Tensor,
+             packed: Optional[tuple] = None) -> torch.Tensor:
+        _, _, freqs, wt_t, ws_t = packed if packed is not None else self.packed()
         return _hip.noise_cond(timestep, style_feat, freqs, wt_t, self.time_proj.bias.detach(),
                                ws_t, self.style_proj.bias.detach(),
                                self.point_encoder[4].bias.detach())
@@ -472,13 +473,13 @@ class DiffusionProcess:
         t_prevs = [timesteps[timesteps.index(t) + 1] if t > 0 else -1 for t in timesteps]
         # every step's conditioning rows (time_proj + style_proj + b4, per CFG row) in one launch:
         # they depend only on t and the style features, not on x
-        conds = None
+        conds = pk = None
         if npred.fused_inference(style_in):
             S = len(timesteps)
-            conds = npred.cond(t_rows.reshape(-1), style_in.repeat(S, 1)).view(S, 2 * B, -1)
+            pk = npred.packed()  # the loop changes no weight
+            conds = npred.cond(t_rows.reshape(-1), style_in.repeat(S, 1), pk).view(S, 2 * B, -1)
         overlap = use_hierarchical and overlap_knn_build(2 * B * model.config.global_points)
         side = ws = vws = None
-        pk = npred.packed() if conds is not None else None  # the loop changes no weight
         ctx = contextlib.nullcontext()
         if overlap:
             loop, side = step_streams(device)
