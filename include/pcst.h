@@ -214,9 +214,11 @@ int pcst_knn3_interp(const float* coarse, const float* orig, const int64_t* idx,
  * and writes out.  The caller orders query after build on the workspace.
  * lds_floor (bytes, 0..96 KiB): LDS floor of the build-phase workgroups (a kernel whose static LDS
  * is below it gets the difference as dynamic LDS), so that a build on a side stream runs only on
- * CUs the noise MLP leaves idle; 0 = no floor (knn3_interp passes 0). */
+ * CUs the noise MLP leaves idle; 0 = no floor (knn3_interp passes 0).  max_wg (> 0): at most
+ * this many workgroups per build launch over all clouds (each kernel strides over its work), so a
+ * side-stream build holds few CUs; 0 = the natural grids (knn3_interp passes 0). */
 int pcst_knn3_build(const float* orig, const int64_t* idx, int64_t B, int64_t N, int64_t M,
-                    int64_t lds_floor, void* workspace, void* stream);
+                    int64_t lds_floor, int64_t max_wg, void* workspace, void* stream);
 int pcst_knn3_query(const float* coarse, const float* orig, int64_t B, int64_t N, int64_t M,
                     float* out, void* workspace, void* stream);
 /* diagnostics of the last query on a workspace: out[0] error flag, out[1..B] query chunks per

@@ -192,12 +192,13 @@ __global__ __launch_bounds__(256) void knn_pre_kernel(const float* __restrict__ 
                                                       uint32_t* __restrict__ known,
                                                       int32_t* __restrict__ err) {
   const int b = blockIdx.y;
-  if (blockIdx.x < kStatBlocks) {
-    cloud_stats_block(orig + (int64_t)b * N * 3, N, blockIdx.x, stats + b * kStatBlocks);
-    return;
+  // any grid size (a capped side-stream build has few workgroups): the stats partials and the
+  // known rows are strided over the workgroups
+  for (int sb = blockIdx.x; sb < kStatBlocks; sb += gridDim.x) {
+    cloud_stats_block(orig + (int64_t)b * N * 3, N, sb, stats + b * kStatBlocks);
+    __syncthreads();  // the block helper's LDS is reused by the next partial
   }
-  const int blk = blockIdx.x - kStatBlocks;
-  for (int64_t j = (int64_t)blk * 256 + threadIdx.x; j < M; j += kPreKnownBlocks * 256) {
+  for (int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x; j < M; j += (int64_t)gridDim.x * 256) {
     const int64_t n = idx[b * M + j];
     if (n < 0 || n >= N) { atomicOr(err, 1); continue; }
     atomicMax(&known[b * (int64_t)N + n], (uint32_t)(j + 1));
@@ -217,35 +218,41 @@ __global__ __launch_bounds__(256) void knn_count_kernel(
   const int b = blockIdx.y;
   __shared__ float Gs[8];
   __shared__ unsigned long long th[kKnnMaxTiles];
-  // the elements' coordinates are loaded first: their latency overlaps the grid parameters
-  const int64_t e0 = (int64_t)blockIdx.x * kCountPerBlock + threadIdx.x;
+  // element blocks of kCountPerBlock strided over the workgroups (a capped side-stream build has
+  // few); the first block's coordinates are loaded before the grid parameters are folded, so
+  // their latency overlaps
+  const int64_t nblk = (M + N + kCountPerBlock - 1) / kCountPerBlock;
   float px[U], py[U], pz[U];
   bool need[U];
   unsigned long long inc[U], old[U];
+  auto load = [&](int64_t blk) {
+    const int64_t e0 = blk * kCountPerBlock + threadIdx.x;
 #pragma unroll
-  for (int u = 0; u < U; ++u) {
-    const int64_t e = e0 + u * 256;
-    need[u] = false;
-    inc[u] = 0ull;
-    px[u] = py[u] = pz[u] = 0.0f;
-    if (e < M) {
-      int64_t n = idx[b * M + e];
-      n = n < 0 ? 0 : (n >= N ? N - 1 : n);
-      const float* p = orig + (b * N + n) * 3;
-      px[u] = p[0]; py[u] = p[1]; pz[u] = p[2];
-      need[u] = true;
-      inc[u] = 1ull;
-    } else if (e < M + N) {
-      const int64_t n = e - M;
-      const uint32_t kn = known[b * N + n];
-      if (!kn) {  // known rows take the coarse value in the outlier pass (after the MLP)
+    for (int u = 0; u < U; ++u) {
+      const int64_t e = e0 + u * 256;
+      need[u] = false;
+      inc[u] = 0ull;
+      px[u] = py[u] = pz[u] = 0.0f;
+      if (e < M) {
+        int64_t n = idx[b * M + e];
+        n = n < 0 ? 0 : (n >= N ? N - 1 : n);
         const float* p = orig + (b * N + n) * 3;
         px[u] = p[0]; py[u] = p[1]; pz[u] = p[2];
         need[u] = true;
-        inc[u] = 1ull << 32;
+        inc[u] = 1ull;
+      } else if (e < M + N) {
+        const int64_t n = e - M;
+        const uint32_t kn = known[b * N + n];
+        if (!kn) {  // known rows take the coarse value in the outlier pass (after the MLP)
+          const float* p = orig + (b * N + n) * 3;
+          px[u] = p[0]; py[u] = p[1]; pz[u] = p[2];
+          need[u] = true;
+          inc[u] = 1ull << 32;
+        }
       }
     }
-  }
+  };
+  load(blockIdx.x);
   if (threadIdx.x < 64) knn_grid_params(stats, b, N, M, Cmax, Gs);
   for (int t = threadIdx.x; t < T; t += 256) th[t] = 0ull;
   __syncthreads();
@@ -253,25 +260,29 @@ __global__ __launch_bounds__(256) void knn_count_kernel(
   Grid g;
   g.load(Gs);
   uint64_t* Cn = cnt + b * Cpad;
-  int cell[U];
+  for (int64_t blk = blockIdx.x; blk < nblk; blk += gridDim.x) {
+    if (blk != blockIdx.x) load(blk);
+    const int64_t e0 = blk * kCountPerBlock + threadIdx.x;
+    int cell[U];
 #pragma unroll
-  for (int u = 0; u < U; ++u) {
-    const float p[3] = {px[u], py[u], pz[u]};
-    cell[u] = need[u] ? cell_of(p, g) : -1;
-  }
-#pragma unroll
-  for (int u = 0; u < U; ++u)
-    old[u] = cell[u] >= 0 ? atomicAdd((unsigned long long*)&Cn[cell[u]], inc[u]) : 0ull;
-#pragma unroll
-  for (int u = 0; u < U; ++u) {
-    const int64_t e = e0 + u * 256;
-    if (e >= M + N) continue;
-    int2 cr = make_int2(-1, 0);
-    if (cell[u] >= 0) {
-      atomicAdd(&th[cell[u] / kKnnTile], inc[u]);
-      cr = make_int2(cell[u], (int)(uint32_t)(e < M ? old[u] : old[u] >> 32));
+    for (int u = 0; u < U; ++u) {
+      const float p[3] = {px[u], py[u], pz[u]};
+      cell[u] = need[u] ? cell_of(p, g) : -1;
     }
-    crank[b * (M + N) + e] = cr;
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      old[u] = cell[u] >= 0 ? atomicAdd((unsigned long long*)&Cn[cell[u]], inc[u]) : 0ull;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t e = e0 + u * 256;
+      if (e >= M + N) continue;
+      int2 cr = make_int2(-1, 0);
+      if (cell[u] >= 0) {
+        atomicAdd(&th[cell[u] / kKnnTile], inc[u]);
+        cr = make_int2(cell[u], (int)(uint32_t)(e < M ? old[u] : old[u] >> 32));
+      }
+      crank[b * (M + N) + e] = cr;
+    }
   }
   __syncthreads();
   for (int t = threadIdx.x; t < T; t += 256)
@@ -304,81 +315,85 @@ __global__ __launch_bounds__(256) void knn_scan_kernel(uint64_t* __restrict__ cn
                                                        int64_t T, int64_t Cpad,
                                                        uint2* __restrict__ chunks, int64_t maxch,
                                                        int32_t* __restrict__ nchunk) {
-  const int b = blockIdx.y, tile = blockIdx.x;
+  const int b = blockIdx.y;
   __shared__ unsigned long long buf[kKnnTile + kKnnTile / 32];
   __shared__ unsigned long long sh[8];
   auto pad = [](int i) { return i + (i >> 5); };
-  uint64_t* D = cnt + b * Cpad + (int64_t)tile * kKnnTile;
-  uint64_t pre = 0;
-  for (int t = threadIdx.x; t < tile; t += 256) pre += tsum[b * T + t];
+  // tiles strided over the workgroups (a capped side-stream build has few)
+  for (int tile = blockIdx.x; tile < (int)T; tile += gridDim.x) {
+    __syncthreads();  // the previous tile's buf / sh readers are done
+    uint64_t* D = cnt + b * Cpad + (int64_t)tile * kKnnTile;
+    uint64_t pre = 0;
+    for (int t = threadIdx.x; t < tile; t += 256) pre += tsum[b * T + t];
 #pragma unroll
-  for (int off = 32; off >= 1; off >>= 1) pre += __shfl_xor(pre, off);
-  if ((threadIdx.x & 63) == 0) sh[4 + (threadIdx.x >> 6)] = pre;
+    for (int off = 32; off >= 1; off >>= 1) pre += __shfl_xor(pre, off);
+    if ((threadIdx.x & 63) == 0) sh[4 + (threadIdx.x >> 6)] = pre;
 #pragma unroll
-  for (int k = 0; k < 16; ++k) buf[pad(k * 256 + threadIdx.x)] = D[k * 256 + threadIdx.x];
-  __syncthreads();
-  const uint64_t base = sh[4] + sh[5] + sh[6] + sh[7];
-  uint64_t v[16], s = 0;
+    for (int k = 0; k < 16; ++k) buf[pad(k * 256 + threadIdx.x)] = D[k * 256 + threadIdx.x];
+    __syncthreads();
+    const uint64_t base = sh[4] + sh[5] + sh[6] + sh[7];
+    uint64_t v[16], s = 0;
 #pragma unroll
-  for (int k = 0; k < 16; ++k) {
-    v[k] = buf[pad(threadIdx.x * 16 + k)];
-    s += v[k];
-  }
-  uint64_t tot;
-  uint64_t run = block_excl_scan_256_u64(s, sh, tot) + base;
-#pragma unroll
-  for (int k = 0; k < 16; ++k) {
-    buf[pad(threadIdx.x * 16 + k)] = run;
-    run += v[k];
-  }
-  __syncthreads();
-#pragma unroll
-  for (int k = 0; k < 16; ++k) D[k * 256 + threadIdx.x] = buf[pad(k * 256 + threadIdx.x)];
-  if (threadIdx.x < 64) {
-    // brick t's queries by octant (2x2x2 cells: Morton cells [8o, 8o + 8)).  A chunk is a run of
-    // whole consecutive octants holding <= 64 queries, or a balanced part of one octant that
-    // holds more, so a dense chunk's cell box stays within 2x2x2 cells (the query pass stages
-    // the box grown by one cell: at most 4x4x4).
-    const int t = threadIdx.x;
-    uint32_t qo[9];
-#pragma unroll
-    for (int o = 0; o < 8; ++o) qo[o] = (uint32_t)(buf[pad(t * 64 + 8 * o)] >> 32);
-    qo[8] = (uint32_t)((t < 63 ? buf[pad(t * 64 + 64)] : base + tot) >> 32);
-    // walk the octants; emit(a, b) is called for every chunk [a, b) in order
-    auto walk = [&](auto&& emit) {
-      uint32_t cs = qo[0];  // start of the open run of octants
-#pragma unroll
-      for (int o = 0; o < 8; ++o) {
-        const uint32_t a = qo[o], n = qo[o + 1] - a;
-        if (n > 64) {
-          if (a > cs) emit(cs, a);
-          const uint32_t k = (n + 63) / 64;
-          for (uint32_t i = 0; i < k; ++i) emit(a + (uint32_t)((uint64_t)n * i / k), a + (uint32_t)((uint64_t)n * (i + 1) / k));
-          cs = a + n;
-        } else if (a + n - cs > 64) {
-          emit(cs, a);
-          cs = a;
-        }
-      }
-      if (qo[8] > cs) emit(cs, qo[8]);
-    };
-    uint32_t nch = 0;
-    walk([&](uint32_t, uint32_t) { ++nch; });
-    uint32_t off = nch;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const uint32_t y = __shfl_up(off, o);
-      if (t >= o) off += y;
+    for (int k = 0; k < 16; ++k) {
+      v[k] = buf[pad(threadIdx.x * 16 + k)];
+      s += v[k];
     }
-    const uint32_t all = __shfl(off, 63);
-    off -= nch;
-    uint32_t at = 0;
-    if (t == 0 && all) at = (uint32_t)atomicAdd(&nchunk[b], (int32_t)all);
-    at = __shfl(at, 0);
-    uint2* Ch = chunks + b * maxch + at + off;
-    uint32_t i = 0;
-    walk([&](uint32_t a, uint32_t e) { Ch[i++] = make_uint2(a, e); });
-  }
+    uint64_t tot;
+    uint64_t run = block_excl_scan_256_u64(s, sh, tot) + base;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      buf[pad(threadIdx.x * 16 + k)] = run;
+      run += v[k];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 16; ++k) D[k * 256 + threadIdx.x] = buf[pad(k * 256 + threadIdx.x)];
+    if (threadIdx.x < 64) {
+      // brick t's queries by octant (2x2x2 cells: Morton cells [8o, 8o + 8)).  A chunk is a run of
+      // whole consecutive octants holding <= 64 queries, or a balanced part of one octant that
+      // holds more, so a dense chunk's cell box stays within 2x2x2 cells (the query pass stages
+      // the box grown by one cell: at most 4x4x4).
+      const int t = threadIdx.x;
+      uint32_t qo[9];
+#pragma unroll
+      for (int o = 0; o < 8; ++o) qo[o] = (uint32_t)(buf[pad(t * 64 + 8 * o)] >> 32);
+      qo[8] = (uint32_t)((t < 63 ? buf[pad(t * 64 + 64)] : base + tot) >> 32);
+      // walk the octants; emit(a, b) is called for every chunk [a, b) in order
+      auto walk = [&](auto&& emit) {
+        uint32_t cs = qo[0];  // start of the open run of octants
+#pragma unroll
+        for (int o = 0; o < 8; ++o) {
+          const uint32_t a = qo[o], n = qo[o + 1] - a;
+          if (n > 64) {
+            if (a > cs) emit(cs, a);
+            const uint32_t k = (n + 63) / 64;
+            for (uint32_t i = 0; i < k; ++i) emit(a + (uint32_t)((uint64_t)n * i / k), a + (uint32_t)((uint64_t)n * (i + 1) / k));
+            cs = a + n;
+          } else if (a + n - cs > 64) {
+            emit(cs, a);
+            cs = a;
+          }
+        }
+        if (qo[8] > cs) emit(cs, qo[8]);
+      };
+      uint32_t nch = 0;
+      walk([&](uint32_t, uint32_t) { ++nch; });
+      uint32_t off = nch;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(off, o);
+        if (t >= o) off += y;
+      }
+      const uint32_t all = __shfl(off, 63);
+      off -= nch;
+      uint32_t at = 0;
+      if (t == 0 && all) at = (uint32_t)atomicAdd(&nchunk[b], (int32_t)all);
+      at = __shfl(at, 0);
+      uint2* Ch = chunks + b * maxch + at + off;
+      uint32_t i = 0;
+      walk([&](uint32_t a, uint32_t e) { Ch[i++] = make_uint2(a, e); });
+    }
+  }  // tile
 }
 
 __global__ __launch_bounds__(256) void knn_fill_kernel(const float* __restrict__ orig,
@@ -1248,12 +1263,18 @@ static unsigned pad_for(unsigned static_lds, unsigned floor_bytes) {
 // packed cell counts, scan, fill.  Phase 2 (needs the coarse values, i.e. the noise MLP's
 // output): known rows, the query passes and the outlier pass.  Splitting them lets a caller run
 // phase 1 on a second stream while the MLP runs (guided_sample_loop).
+// max_wg (> 0): at most this many work-groups per build launch over all clouds (each kernel
+// strides over its work), so a build on a side stream holds at most max_wg CUs -- the noise MLP's
+// last partial round of work-groups leaves ~40 of 256 idle and never waits for one held by the
+// build.  0 = the kernels' natural grids.
 extern "C" int pcst_knn3_build(const float* orig, const int64_t* idx, int64_t B, int64_t N,
-                               int64_t M, int64_t lds_floor, void* workspace, void* stream) {
+                               int64_t M, int64_t lds_floor, int64_t max_wg, void* workspace,
+                               void* stream) {
   PCST_CHECK_ARG(B >= 0 && N > 0 && M > 0 && N < (1ll << 31) && M < (1ll << 27) &&
                      M + N < (1ll << 31),
                  "knn3_build: bad shape");
   PCST_CHECK_ARG(lds_floor >= 0 && lds_floor <= 98304, "knn3_build: lds_floor is 0..98304 bytes");
+  PCST_CHECK_ARG(max_wg >= 0, "knn3_build: max_wg < 0");
   if (B == 0) return PCST_OK;
   PCST_CHECK_ARG(orig && idx && workspace, "knn3_build: null pointer");
   hipStream_t s = as_stream(stream);
@@ -1265,14 +1286,17 @@ extern "C" int pcst_knn3_build(const float* orig, const int64_t* idx, int64_t B,
   // error word, counters, known rows, tile sums and packed counts are contiguous in the carve
   PCST_HIP(hipMemsetAsync(w.err, 0, (size_t)(w.bytes - ((char*)w.err - (char*)workspace)), s),
            "knn: memset");
-  hipLaunchKernelGGL(knn_pre_kernel, dim3(kStatBlocks + kPreKnownBlocks, b), dim3(256), pad_pre, s,
-                     orig, idx, (int)N, M, w.stats, w.known, w.err);
-  const unsigned gc = (unsigned)cdiv(M + N, kCountPerBlock);
-  hipLaunchKernelGGL(knn_count_kernel, dim3(gc, b), dim3(256), pad_count, s, orig, idx, w.stats,
-                     w.known, N, M, w.Cmax, w.T, w.Cpad, w.gp, w.cnt, w.tsum, w.crank);
-  hipLaunchKernelGGL(knn_scan_kernel, dim3((unsigned)w.T, b), dim3(256), pad_scan, s, w.cnt, w.tsum,
+  // per-cloud grid of each launch: natural size, capped at max_wg / B (at least one)
+  const int64_t cap = max_wg > 0 ? std::max<int64_t>(1, max_wg / B) : (int64_t)1 << 30;
+  auto grid = [&](int64_t natural) { return (unsigned)std::min<int64_t>(natural, cap); };
+  hipLaunchKernelGGL(knn_pre_kernel, dim3(grid(kStatBlocks + kPreKnownBlocks), b), dim3(256), pad_pre,
+                     s, orig, idx, (int)N, M, w.stats, w.known, w.err);
+  hipLaunchKernelGGL(knn_count_kernel, dim3(grid(cdiv(M + N, kCountPerBlock)), b), dim3(256),
+                     pad_count, s, orig, idx, w.stats, w.known, N, M, w.Cmax, w.T, w.Cpad, w.gp,
+                     w.cnt, w.tsum, w.crank);
+  hipLaunchKernelGGL(knn_scan_kernel, dim3(grid(w.T), b), dim3(256), pad_scan, s, w.cnt, w.tsum,
                      w.T, w.Cpad, w.chunks, w.maxch, w.nchunk);
-  const unsigned gf = (unsigned)std::min<int64_t>(cdiv(M + N, 256), 2048);
+  const unsigned gf = grid(std::min<int64_t>(cdiv(M + N, 256), 2048));
   hipLaunchKernelGGL(knn_fill_kernel, dim3(gf, b), dim3(256), pad_fill, s, orig, idx, N, M, w.Cpad,
                      w.cnt, w.crank, w.refs, w.qorder);
   PCST_LAUNCH_CHECK("knn3_build");
@@ -1318,7 +1342,7 @@ extern "C" int pcst_knn3_query(const float* coarse, const float* orig, int64_t B
 extern "C" int pcst_knn3_interp(const float* coarse, const float* orig, const int64_t* idx,
                                 int64_t B, int64_t N, int64_t M, float* out, void* workspace,
                                 void* stream) {
-  int rc = pcst_knn3_build(orig, idx, B, N, M, 0, workspace, stream);
+  int rc = pcst_knn3_build(orig, idx, B, N, M, 0, 0, workspace, stream);
   if (rc) return rc;
   return pcst_knn3_query(coarse, orig, B, N, M, out, workspace, stream);
 }

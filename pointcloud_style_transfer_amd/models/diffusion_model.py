@@ -259,6 +259,10 @@ _OVERLAP_MAX_MLP_POINTS = 2 * 128 * 256
 # but packs as many work-groups per idle CU as their own LDS allows (round 2 used a flat 64 KiB
 # pad on every build kernel: 1-2 work-groups per idle CU).
 KNN_BUILD_LDS_FLOOR = 8192
+# Work-groups per build launch on the side stream (pcst_knn3_build's max_wg): the MLP's last
+# round (469 work-groups on 256 CUs) leaves ~43 CUs idle; a build confined to fewer work-groups
+# than that never holds a CU an MLP work-group of that round is waiting for.
+KNN_BUILD_MAX_WG = 0
 
 
 def overlap_knn_build(mlp_points: int) -> bool:
@@ -292,7 +296,7 @@ def hierarchical_eps(hp, mlp, xc, xi, x_cat, knn_ws=None, side=None):
         ready.record(main)
     ready.wait(side)
     with torch.cuda.stream(side):
-        handle = _hip.knn3_build(x_cat, xi, knn_ws, KNN_BUILD_LDS_FLOOR)
+        handle = _hip.knn3_build(x_cat, xi, knn_ws, KNN_BUILD_LDS_FLOOR, KNN_BUILD_MAX_WG)
         built.record(side)
     nc = mlp(xc)
     built.wait(main)

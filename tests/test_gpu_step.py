@@ -325,6 +325,19 @@ def test_knn_build_query_phases_match_interp(H):
     assert torch.equal(H.knn3_query(coarse, H.knn3_build(orig, idx)), ref)
 
 
+@pytest.mark.parametrize("max_wg,floor", [(1, 0), (2, 8192), (32, 8192), (7, 0)])
+def test_knn_build_workgroup_cap_is_exact(H, max_wg, floor):
+    """pcst_knn3_build's max_wg only changes how many work-groups stride over the build's work
+    (stats partials, element blocks, scan tiles, fill): the result is bit-identical to the
+    natural grids, down to one work-group per cloud."""
+    rng = np.random.default_rng(max_wg)
+    orig = dev((rng.standard_normal((2, 60000, 3)) * [1, 0.5, 0.2]).astype(np.float32))
+    idx = dev(np.stack([rng.choice(60000, 15000, replace=False) for _ in range(2)]).astype(np.int64))
+    coarse = dev(rng.standard_normal((2, 15000, 3)).astype(np.float32))
+    ref = H.knn3_interp(coarse, orig, idx)
+    assert torch.equal(H.knn3_query(coarse, H.knn3_build(orig, idx, None, floor, max_wg)), ref)
+
+
 def test_per_call_choices_on_concurrent_streams(H):
     """The ABI keeps no process-global switches (pcst.h conventions; tests/test_abi.py checks the
     symbol table): the kNN build's LDS floor and the Chamfer forward path are arguments, so two

@@ -24,6 +24,8 @@ def apply():
         dm.KNN_BUILD_LDS_FLOOR = int(e["PCST_KNN_BUILD_LDS_FLOOR"])
     if "PCST_DEVICE_EVENTS" in e:
         dm.DEVICE_EVENTS = e["PCST_DEVICE_EVENTS"] != "0"
+    if "PCST_KNN_BUILD_MAX_WG" in e:
+        dm.KNN_BUILD_MAX_WG = int(e["PCST_KNN_BUILD_MAX_WG"])
     if "PCST_KERNEL_SIGNAL" in e:
         dm.KERNEL_SIGNAL = e["PCST_KERNEL_SIGNAL"] != "0"
     if e.get("PCST_NM_BF16_KERNEL") == "1":

@@ -11,6 +11,8 @@ median ms/step of each:
   seq     one stream: the kNN build inline before the MLP, no events at all
   seq_ev  seq with the timing events around the MLP
   evready noev with the loop -> side dependency as an event instead of the kernel-side signal
+  nocap   noev with the side-stream build at its natural grids (no max_wg cap)
+  capK    noev with the side-stream build capped at K work-groups per launch
 A development tool (tools/ only)."""
 import argparse
 import os
@@ -51,9 +53,13 @@ def main():
         conds = npred.cond(t_rows.reshape(-1), style_in.repeat(1000, 1)).view(1000, 2, -1)
         blob, bias = npred.packed()[:2]
         ws = _hip.knn_workspace(2, 120000, cfg.global_points, device=dev)
+        cap0 = dmod.KNN_BUILD_MAX_WG
 
         def run(mode, n):
             dmod.KERNEL_SIGNAL = mode != "evready"  # evready: the loop -> side dependency as an event
+            # nocap: natural build grids; capK: at most K build work-groups per launch
+            dmod.KNN_BUILD_MAX_WG = (0 if mode == "nocap" else
+                                     int(mode[3:]) if mode.startswith("cap") else cap0)
             x = xT.clone()
             x_cat = torch.cat([x, x]).contiguous()
             timed = mode.endswith("ev") or mode == "bench"
