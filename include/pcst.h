@@ -156,7 +156,13 @@ int pcst_linear_wgrad_bf16(const float* dZ, const float* X, int64_t M, int64_t I
  *   3 EP_RELU_MASK   C bf16 = acc * [aux_bf16 > 0]
  *   4 EP_ADD         C fp32 = acc + aux_fp32
  *   5 EP_COND        C fp32 = ((acc + bias) + aux[g,0,:]) + aux[g,1,:],  g = m / group_rows
- * C2 (may be NULL): bf16 copy of an fp32 C.  O % 4 == 0 except for EP_F32/EP_BF16.
+ *   6 EP_RESID_DROP16 C bf16 = aux_bf16 + keep(e) * (acc + bias) / (1 - drop_p)
+ *   7 EP_ADD16       C bf16 = acc + aux_bf16
+ *     (6, 7: the residual stream in the autocast format, as the reference's autocast keeps it)
+ * C2 (may be NULL): bf16 copy of an fp32 C (EP_F32, EP_RESID_DROP, EP_COND -- C may then be NULL
+ * for EP_COND), or for EP_BF16 / EP_ADD16 the next Dropout backward fused: C2 = bf16(C * keep(e)
+ * / (1 - drop_p)) from the stored bf16 C, pcst_dropout_grad_bf16's result on it (those two
+ * epilogues apply no dropout of their own).  O % 4 == 0 except for EP_F32/EP_BF16.
  * keep(e) for element e = m*O + o is hash(seed, e) >= drop_p * 2^32: a pure function of
  * (seed, e), regenerated by pcst_dropout_grad_bf16 (out bf16 = g * keep * 1/(1-p), n % 4 == 0).
  * bf16 A with bf16 B runs the pipelined kernel (64-deep K slices, two in flight). */

@@ -568,8 +568,9 @@ def gemm_nt_bf16(A, B, scale=None, shift=None, relu=False, half=torch.bfloat16):
     return C
 
 
-EP_F32, EP_BF16, EP_RESID_DROP, EP_RELU_MASK, EP_ADD, EP_COND = range(6)
-_EP_BF16_OUT = (EP_BF16, EP_RELU_MASK)
+EP_F32, EP_BF16, EP_RESID_DROP, EP_RELU_MASK, EP_ADD, EP_COND, EP_RESID_DROP16, EP_ADD16 = range(8)
+_EP_BF16_OUT = (EP_BF16, EP_RELU_MASK, EP_RESID_DROP16, EP_ADD16)
+_EP_AUX16 = (EP_RELU_MASK, EP_RESID_DROP16, EP_ADD16)
 
 
 def _f32_or_16(t, half):
@@ -590,15 +591,18 @@ def _half_of(*ts, default=torch.bfloat16):
 
 
 def gemm_ex(A, B, bias=None, relu=False, epilogue=EP_F32, aux=None, seed=0, p=0.0,
-            group_rows=0, copy_bf16=False, half=None):
+            group_rows=0, copy_bf16=False, half=None, dropout_copy=False, fp32_out=True):
     """A [M,K], B [O,K] (fp32 or 16-bit) -> epilogue(A B^T) on 16-bit MFMA (csrc/train_mlp.hip):
     EP_F32/EP_BF16 act(acc+bias) as fp32/16-bit, EP_RESID_DROP aux + dropout_p(acc+bias) (fp32),
     EP_RELU_MASK acc*[aux>0] (16-bit, aux 16-bit), EP_ADD acc + aux (fp32), EP_COND
     ((acc+bias) + aux[g,0]) + aux[g,1] with g = row // group_rows (fp32).  copy_bf16 (fp32
-    outputs): also return a 16-bit copy, (C, C_16).  `half` (bfloat16 or float16) is the 16-bit
-    format; default: that of the 16-bit operands, else bfloat16."""
+    outputs): also return a 16-bit copy, (C, C_16); with fp32_out=False (EP_COND) only C_16.
+    EP_RESID_DROP16 / EP_ADD16: EP_RESID_DROP / EP_ADD with a 16-bit aux and output.
+    dropout_copy (EP_BF16, EP_ADD16): also return half(C * keep / (1-p)) under (seed, p) --
+    dropout_grad_bf16 of the stored C, fused -- as (C, dD).  `half` (bfloat16 or float16) is
+    the 16-bit format; default: that of the 16-bit operands, else bfloat16."""
     require_device(A, B, bias, aux)
-    half = half or _half_of(A, B, aux if epilogue == EP_RELU_MASK else None)
+    half = half or _half_of(A, B, aux if epilogue in _EP_AUX16 else None)
     A, a16 = _f32_or_16(A, half)
     B, b16 = _f32_or_16(B, half)
     M, K = A.shape
@@ -607,23 +611,31 @@ def gemm_ex(A, B, bias=None, relu=False, epilogue=EP_F32, aux=None, seed=0, p=0.
         raise RuntimeError(f"gemm_ex: K mismatch {tuple(A.shape)} vs {tuple(B.shape)}")
     bias = None if bias is None else _f32(bias)
     if aux is not None:
-        want = half if epilogue == EP_RELU_MASK else torch.float32
+        want = half if epilogue in _EP_AUX16 else torch.float32
         shape = (M // max(group_rows, 1), 2, O) if epilogue == EP_COND else (M, O)
         if aux.dtype != want or tuple(aux.shape) != shape:
             raise RuntimeError(f"gemm_ex: aux must be {want} {list(shape)}, got "
                                f"{aux.dtype} {list(aux.shape)}")
         aux = aux.contiguous()
     out_dtype = half if epilogue in _EP_BF16_OUT else torch.float32
-    C = torch.empty(M, O, dtype=out_dtype, device=A.device)
+    if not fp32_out and not (epilogue == EP_COND and copy_bf16):
+        raise RuntimeError("gemm_ex: fp32_out=False is for EP_COND with copy_bf16")
+    C = torch.empty(M, O, dtype=out_dtype, device=A.device) if fp32_out else None
     C2 = None
     if copy_bf16:
         if out_dtype != torch.float32:
             raise RuntimeError("gemm_ex: copy_bf16 needs an fp32 epilogue")
         C2 = torch.empty(M, O, dtype=half, device=A.device)
+    if dropout_copy:
+        if epilogue not in (EP_BF16, EP_ADD16) or copy_bf16:
+            raise RuntimeError("gemm_ex: dropout_copy is for EP_BF16 / EP_ADD16")
+        C2 = torch.empty(M, O, dtype=half, device=A.device)
     _call("pcst_gemm_ex", _ptr(A), a16, M, K, _ptr(B), b16, O, _ptr(bias), int(relu),
           int(epilogue), _ptr(aux), int(seed) & (2**64 - 1), float(p), int(group_rows), _ptr(C),
           _ptr(C2), _f16_flag(half), _stream())
-    return (C, C2) if copy_bf16 else C
+    if not fp32_out:
+        return C2
+    return (C, C2) if copy_bf16 or dropout_copy else C
 
 
 def dropout_grad_bf16(g, seed, p, half=torch.bfloat16):

@@ -10,6 +10,10 @@
 //     EP_RESID_DROP  resid + keep(m, o) * (acc + bias) * s -> fp32  (x + Dropout(Linear2(h)))
 //     EP_RELU_MASK   acc * [h > 0]                       -> bf16  (ReLU backward of Linear1)
 //     EP_ADD         acc + add                           -> fp32  (residual gradient sum)
+//     EP_RESID_DROP16, EP_ADD16: the same with a 16-bit residual operand and output (the residual
+//                    stream in autocast's 16-bit format, as the reference's autocast keeps it)
+//   EP_BF16 / EP_ADD16 with C2: also C2 = 16-bit(C * keep(e) / (1 - p)), the next Dropout
+//   backward's dD from the stored 16-bit C (the dropout_grad kernel's result, fused)
 //   wgrad_ex:  dW[o, i] = sum_m dZ[m, o] X[m, i],  db[o] = sum_m dZ[m, o]
 //   dropout_grad: dD = bf16(g * keep * s)  (Dropout backward, the mask regenerated)
 //
@@ -64,7 +68,22 @@ __device__ __forceinline__ float h16_to_f32(uint32_t bits16) {
 #endif
 }
 
-enum { EP_F32 = 0, EP_BF16 = 1, EP_RESID_DROP = 2, EP_RELU_MASK = 3, EP_ADD = 4, EP_COND = 5 };
+enum {
+  EP_F32 = 0, EP_BF16 = 1, EP_RESID_DROP = 2, EP_RELU_MASK = 3, EP_ADD = 4, EP_COND = 5,
+  EP_RESID_DROP16 = 6, EP_ADD16 = 7
+};
+// 16-bit output / 16-bit aux operand / the C2 dropout copy of a 16-bit output
+__host__ __device__ constexpr bool ep_out16(int ep) {
+  return ep == EP_BF16 || ep == EP_RELU_MASK || ep == EP_RESID_DROP16 || ep == EP_ADD16;
+}
+__host__ __device__ constexpr bool ep_aux16(int ep) {
+  return ep == EP_RELU_MASK || ep == EP_RESID_DROP16 || ep == EP_ADD16;
+}
+__host__ __device__ constexpr bool ep_drop_copy(int ep) { return ep == EP_BF16 || ep == EP_ADD16; }
+__host__ __device__ constexpr bool ep_dropout(int ep) { return ep == EP_RESID_DROP || ep == EP_RESID_DROP16; }
+__host__ __device__ constexpr bool ep_no_bias(int ep) {
+  return ep == EP_RELU_MASK || ep == EP_ADD || ep == EP_ADD16;
+}
 
 constexpr int kXT = 128, kXK = 32, kXLd = 40;  // tile, k slice, LDS row (bf16 elements, 80 B)
 constexpr int kCLd = 132;                      // epilogue LDS row (floats)
@@ -164,11 +183,13 @@ struct GemmExArgs {
   const float* bias;
   int relu;
   const void* aux;  // EP_RESID_DROP: resid fp32 [M,O]; EP_RELU_MASK: h bf16 [M,O]; EP_ADD: fp32;
-                    // EP_COND: [G, 2, O] fp32 (two per-group row vectors added in turn)
+                    // EP_COND: [G, 2, O] fp32 (two per-group row vectors added in turn);
+                    // EP_RESID_DROP16 / EP_ADD16: 16-bit [M,O]
   uint32_t seed_lo, seed_hi, thr;
   float scale;
   void* C;
-  uint16_t* C2;     // optional bf16 copy of an fp32 output (EP_F32, EP_RESID_DROP, EP_COND)
+  uint16_t* C2;     // optional bf16 copy of an fp32 output (EP_F32, EP_RESID_DROP, EP_COND; C may
+                    // then be null for EP_COND), or the dropout copy (EP_BF16, EP_ADD16)
   int64_t group_rows;  // EP_COND: rows per group
 };
 
@@ -216,7 +237,7 @@ __device__ __forceinline__ void gemm_epilogue(const f32x16 (&acc)[2][2], float (
       const float4 c = *reinterpret_cast<const float4*>(&Cs[rr][cq]);
       const int64_t e = m * O + o;
       float v[4] = {c.x + bias4[0], c.y + bias4[1], c.z + bias4[2], c.w + bias4[3]};
-      if (EP == EP_RELU_MASK || EP == EP_ADD) {  // no bias on the gradient products
+      if (ep_no_bias(EP)) {  // no bias on the gradient products
         v[0] = c.x;
         v[1] = c.y;
         v[2] = c.z;
@@ -227,7 +248,7 @@ __device__ __forceinline__ void gemm_epilogue(const f32x16 (&acc)[2][2], float (
         for (int u = 0; u < 4; ++u) v[u] = fmaxf(v[u], 0.0f);
       }
       float y[4];
-      if (EP == EP_RESID_DROP) {
+      if (ep_dropout(EP)) {
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
           const bool keep = drop_hash(args.seed_lo, args.seed_hi, (uint64_t)(e + u)) >= args.thr;
@@ -240,6 +261,10 @@ __device__ __forceinline__ void gemm_epilogue(const f32x16 (&acc)[2][2], float (
       } else {
 #pragma unroll
         for (int u = 0; u < 4; ++u) y[u] = v[u];
+      }
+      if (EP == EP_RESID_DROP16 || EP == EP_ADD16) {  // 16-bit residual operand
+        const uint16_t* a16 = static_cast<const uint16_t*>(args.aux) + e;
+        for (int u = 0; u < nv; ++u) y[u] += h16_to_f32(a16[u]);
       }
       if (EP == EP_RESID_DROP || EP == EP_ADD || EP == EP_RELU_MASK) {
         if (vec) {
@@ -265,7 +290,7 @@ __device__ __forceinline__ void gemm_epilogue(const f32x16 (&acc)[2][2], float (
           }
         }
       }
-      if (EP == EP_BF16 || EP == EP_RELU_MASK) {
+      if (ep_out16(EP)) {
         uint16_t* out = static_cast<uint16_t*>(args.C) + e;
         if (vec) {
           store4_bf16(out, y[0], y[1], y[2], y[3]);
@@ -275,14 +300,21 @@ __device__ __forceinline__ void gemm_epilogue(const f32x16 (&acc)[2][2], float (
             out[u] = __builtin_bit_cast(uint16_t, b);
           }
         }
+        if (ep_drop_copy(EP) && args.C2) {  // dD = 16-bit(C16 * keep / (1 - p))
+          for (int u = 0; u < nv; ++u) {
+            const bool keep = drop_hash(args.seed_lo, args.seed_hi, (uint64_t)(e + u)) >= args.thr;
+            const float yr = (float)(h16)y[u];
+            args.C2[e + u] = __builtin_bit_cast(uint16_t, (h16)(keep ? yr * args.scale : 0.0f));
+          }
+        }
       } else {
         float* out = static_cast<float*>(args.C) + e;
         if (vec) {
-          *reinterpret_cast<float4*>(out) = make_float4(y[0], y[1], y[2], y[3]);
+          if (EP != EP_COND || args.C) *reinterpret_cast<float4*>(out) = make_float4(y[0], y[1], y[2], y[3]);
           if (args.C2) store4_bf16(args.C2 + e, y[0], y[1], y[2], y[3]);
         } else {
           for (int u = 0; u < nv; ++u) {
-            out[u] = y[u];
+            if (EP != EP_COND || args.C) out[u] = y[u];
             if (args.C2) args.C2[e + u] = __builtin_bit_cast(uint16_t, (h16)y[u]);
           }
         }
@@ -427,13 +459,13 @@ __device__ __forceinline__ void gemm_epilogue_fast(const f32x16 (&acc)[2][2], fl
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wr = wid >> 1, wc = wid & 1, h = lane >> 5, l32 = lane & 31;
   const int cq = (tid & 31) * 4, rl = tid >> 5;
-  constexpr bool kOutBf16 = EP == EP_BF16 || EP == EP_RELU_MASK;
+  constexpr bool kOutBf16 = ep_out16(EP);
   const uint32_t nel = (uint32_t)(M * O);
   const rsrc_t rc = make_rsrc(args.C, nel * (kOutBf16 ? 2u : 4u));
   const rsrc_t rc2 = make_rsrc(args.C2, args.C2 ? nel * 2u : 0u);
-  const rsrc_t rx = make_rsrc(args.aux, args.aux ? nel * (EP == EP_RELU_MASK ? 2u : 4u) : 0u);
+  const rsrc_t rx = make_rsrc(args.aux, args.aux ? nel * (ep_aux16(EP) ? 2u : 4u) : 0u);
   float bias4[4] = {0.f, 0.f, 0.f, 0.f};
-  if (args.bias && EP != EP_RELU_MASK && EP != EP_ADD) {
+  if (args.bias && !ep_no_bias(EP)) {
     const float4 b = *reinterpret_cast<const float4*>(args.bias + o0 + cq);
     bias4[0] = b.x;
     bias4[1] = b.y;
@@ -464,12 +496,19 @@ __device__ __forceinline__ void gemm_epilogue_fast(const f32x16 (&acc)[2][2], fl
 #pragma unroll
         for (int u = 0; u < 4; ++u) y[u] = fmaxf(y[u], 0.0f);
       }
-      if (EP == EP_RESID_DROP) {
+      if (ep_dropout(EP)) {
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
           const bool keep = drop_hash(args.seed_lo, args.seed_hi, (uint64_t)(e + u)) >= args.thr;
           y[u] = keep ? y[u] * args.scale : 0.0f;
         }
+      }
+      if (EP == EP_RESID_DROP16 || EP == EP_ADD16) {
+        const v2i32 hb = __builtin_amdgcn_raw_buffer_load_b64(rx, (int)(e * 2u), 0, 0);
+        y[0] += h16_to_f32((uint32_t)hb.x & 0xffffu);
+        y[1] += h16_to_f32((uint32_t)hb.x >> 16);
+        y[2] += h16_to_f32((uint32_t)hb.y & 0xffffu);
+        y[3] += h16_to_f32((uint32_t)hb.y >> 16);
       }
       if (EP == EP_RESID_DROP || EP == EP_ADD) {
         const v4i32 a = __builtin_amdgcn_raw_buffer_load_b128(rx, (int)(e * 4u), 0, 0);
@@ -486,6 +525,18 @@ __device__ __forceinline__ void gemm_epilogue_fast(const f32x16 (&acc)[2][2], fl
       if (kOutBf16) {
         const uint2 pk = pack4_bf16(y[0], y[1], y[2], y[3]);
         __builtin_amdgcn_raw_buffer_store_b64(v2i32{(int)pk.x, (int)pk.y}, rc, (int)(e * 2u), 0, 0);
+        if (ep_drop_copy(EP) && args.C2) {  // dD = 16-bit(C16 * keep / (1 - p))
+          const uint32_t w[2] = {pk.x, pk.y};
+          float d[4];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const bool keep = drop_hash(args.seed_lo, args.seed_hi, (uint64_t)(e + u)) >= args.thr;
+            const float yr = h16_to_f32((w[u >> 1] >> (16 * (u & 1))) & 0xffffu);
+            d[u] = keep ? yr * args.scale : 0.0f;
+          }
+          const uint2 pd = pack4_bf16(d[0], d[1], d[2], d[3]);
+          __builtin_amdgcn_raw_buffer_store_b64(v2i32{(int)pd.x, (int)pd.y}, rc2, (int)(e * 2u), 0, 0);
+        }
       } else {
         __builtin_amdgcn_raw_buffer_store_b128(
             v4i32{__float_as_int(y[0]), __float_as_int(y[1]), __float_as_int(y[2]), __float_as_int(y[3])},
@@ -952,6 +1003,8 @@ static void launch_gemm_ex(int ep, const void* A, int64_t M, int64_t K, const vo
     case EP_RESID_DROP: PCST_GEMM_EX(TA, TB, EP_RESID_DROP); break;
     case EP_RELU_MASK: PCST_GEMM_EX(TA, TB, EP_RELU_MASK); break;
     case EP_ADD: PCST_GEMM_EX(TA, TB, EP_ADD); break;
+    case EP_RESID_DROP16: PCST_GEMM_EX(TA, TB, EP_RESID_DROP16); break;
+    case EP_ADD16: PCST_GEMM_EX(TA, TB, EP_ADD16); break;
     default: PCST_GEMM_EX(TA, TB, EP_COND); break;
   }
 }
@@ -985,6 +1038,8 @@ static void launch_gemm_dma(int ep, int stages, const void* A, int64_t M, int64_
     case EP_BF16: PCST_GEMM_DMA(EP_BF16); break;
     case EP_RESID_DROP: PCST_GEMM_DMA(EP_RESID_DROP); break;
     case EP_RELU_MASK: PCST_GEMM_DMA(EP_RELU_MASK); break;
+    case EP_RESID_DROP16: PCST_GEMM_DMA(EP_RESID_DROP16); break;
+    case EP_ADD16: PCST_GEMM_DMA(EP_ADD16); break;
     default: PCST_GEMM_DMA(EP_ADD); break;
   }
 }
@@ -1007,6 +1062,8 @@ static void launch_gemm_bf(int ep, bool fast, const void* A, int64_t M, int64_t 
     case EP_RESID_DROP: PCST_GEMM_BF(EP_RESID_DROP); break;
     case EP_RELU_MASK: PCST_GEMM_BF(EP_RELU_MASK); break;
     case EP_ADD: PCST_GEMM_BF(EP_ADD); break;
+    case EP_RESID_DROP16: PCST_GEMM_BF(EP_RESID_DROP16); break;
+    case EP_ADD16: PCST_GEMM_BF(EP_ADD16); break;
     default: PCST_GEMM_BF(EP_COND); break;
   }
 }
@@ -1017,7 +1074,7 @@ int gemm_ex_impl(const void* A, int a_bf16, int64_t M, int64_t K, const void* B,
                  uint64_t seed, float drop_p, int64_t group_rows, void* C, uint16_t* C2,
                  void* stream) {
   PCST_CHECK_ARG(M >= 0 && K > 0 && O > 0 && K < (1 << 20) && O < (1 << 20), "gemm_ex: bad shape");
-  PCST_CHECK_ARG(epilogue >= EP_F32 && epilogue <= EP_COND, "gemm_ex: bad epilogue");
+  PCST_CHECK_ARG(epilogue >= EP_F32 && epilogue <= EP_ADD16, "gemm_ex: bad epilogue");
   PCST_CHECK_ARG(K % (a_bf16 ? 8 : 4) == 0 && K % (b_bf16 ? 8 : 4) == 0,
                  "gemm_ex: K must be a multiple of 8 (bf16 operand) or 4 (fp32 operand)");
   PCST_CHECK_ARG(O % 4 == 0 || epilogue == EP_F32 || epilogue == EP_BF16,
@@ -1025,7 +1082,10 @@ int gemm_ex_impl(const void* A, int a_bf16, int64_t M, int64_t K, const void* B,
   PCST_CHECK_ARG(drop_p >= 0.0f && drop_p < 1.0f, "gemm_ex: dropout p must be in [0, 1)");
   PCST_CHECK_ARG(epilogue != EP_COND || group_rows > 0, "gemm_ex: EP_COND needs group_rows > 0");
   if (M == 0) return PCST_OK;
-  PCST_CHECK_ARG(A && B && C, "gemm_ex: null pointer");
+  PCST_CHECK_ARG(A && B && (C || (epilogue == EP_COND && C2)), "gemm_ex: null pointer");
+  PCST_CHECK_ARG(!C2 || epilogue == EP_F32 || epilogue == EP_RESID_DROP || epilogue == EP_COND ||
+                     ep_drop_copy(epilogue),
+                 "gemm_ex: C2 is not defined for this epilogue");
   PCST_CHECK_ARG(epilogue == EP_F32 || epilogue == EP_BF16 || aux, "gemm_ex: epilogue needs aux");
   PCST_CHECK_ARG(((uintptr_t)A | (uintptr_t)B | (uintptr_t)C | (uintptr_t)C2 | (uintptr_t)aux) % 16 == 0,
                  "gemm_ex: pointers must be 16-byte aligned");

@@ -154,6 +154,13 @@ def residual_block(x, layer, training):
     return ResidualBlockFn.apply(x, l1.weight, l1.bias, l2.weight, l2.bias, p)
 
 
+# The residual stream x and its gradient in NoisePredictorFn: in autocast's 16-bit format (True,
+# as the reference's autocast keeps them: every Linear output there is half precision) or fp32
+# (False, the stricter round-2 layout).  16-bit halves the bytes of the residual epilogues and
+# lets each Dropout backward ride on the epilogue that produces its gradient.
+RESIDUAL_16BIT = True
+
+
 class NoisePredictorFn(torch.autograd.Function):
     """The whole per-point network of NoisePredictor.forward (diffusion_model.py:50-61) under
     autocast, forward and backward, on the fused 16-bit-storage GEMMs (autocast's dtype: float16
@@ -163,6 +170,9 @@ class NoisePredictorFn(torch.autograd.Function):
       h1 = relu(h0 W2^T + b2)              [M,256]  bf16
       x  = ((h1 W4^T + b4) + tf) + sf      [M,256]  fp32 + bf16 copy   (EP_COND, per cloud)
       6 x residual block                   (ResidualBlockFn's kernels)
+    With RESIDUAL_16BIT (default) x and its gradient g are stored in the 16-bit format only:
+    blocks run EP_BF16 + EP_RESID_DROP16 forward and EP_RELU_MASK + EP_ADD16 backward, and each
+    block's Dropout backward is the dropout copy of the epilogue that produced its g.
       q0 = relu(x Wo0^T + bo0)             [M,256]  bf16
       q1 = relu(q0 Wo2^T + bo2)            [M,128]  bf16
       out = q1 Wo4^T + bo4                 [M,3]    fp32
@@ -190,22 +200,33 @@ class NoisePredictorFn(torch.autograd.Function):
         wb = [_h(w0p, half), w[1].detach()] + wb
         h0 = _hip.gemm_ex(xp, wb[0], wb[1], relu=True, epilogue=_hip.EP_BF16)
         h1 = _hip.gemm_ex(h0, wb[2], wb[3], relu=True, epilogue=_hip.EP_BF16)
-        x, xb = _hip.gemm_ex(h1, wb[4], wb[5], epilogue=_hip.EP_COND,
-                             aux=cond.detach().float().contiguous(), group_rows=N, copy_bf16=True)
+        r16 = RESIDUAL_16BIT
+        cnd = cond.detach().float().contiguous()
+        if r16:
+            xb = _hip.gemm_ex(h1, wb[4], wb[5], epilogue=_hip.EP_COND, aux=cnd, group_rows=N,
+                              copy_bf16=True, fp32_out=False)
+        else:
+            x, xb = _hip.gemm_ex(h1, wb[4], wb[5], epilogue=_hip.EP_COND, aux=cnd, group_rows=N,
+                                 copy_bf16=True)
         saved, seeds = [xp, h0, h1], []
         for k in range(6):
             o = 6 + 4 * k
             seed = _draw_seed(ps[k])
             seeds.append(seed)
             saved.append(xb)
-            x, xb, h = _block_fwd(x, xb, wb[o], wb[o + 1], wb[o + 2], wb[o + 3], ps[k], seed)
+            if r16:
+                h = _hip.gemm_ex(xb, wb[o], wb[o + 1], relu=True, epilogue=_hip.EP_BF16)
+                xb = _hip.gemm_ex(h, wb[o + 2], wb[o + 3], epilogue=_hip.EP_RESID_DROP16, aux=xb,
+                                  seed=seed, p=ps[k])
+            else:
+                x, xb, h = _block_fwd(x, xb, wb[o], wb[o + 1], wb[o + 2], wb[o + 3], ps[k], seed)
             saved.append(h)
         q0 = _hip.gemm_ex(xb, wb[30], wb[31], relu=True, epilogue=_hip.EP_BF16)
         q1 = _hip.gemm_ex(q0, wb[32], wb[33], relu=True, epilogue=_hip.EP_BF16)
         out = _hip.gemm_ex(q1, wb[34], wb[35], epilogue=_hip.EP_F32)
         saved += [xb, q0, q1]
         ctx.save_for_backward(*saved, *w)
-        ctx.seeds, ctx.ps, ctx.BN, ctx.half = seeds, tuple(ps), (B, N), half
+        ctx.seeds, ctx.ps, ctx.BN, ctx.half, ctx.r16 = seeds, tuple(ps), (B, N), half, r16
         return out.view(B, N, 3)
 
     @staticmethod
@@ -231,17 +252,34 @@ class NoisePredictorFn(torch.autograd.Function):
         grads[32], grads[33] = _hip.linear_wgrad_ex(dq1, q0)
         dq0 = _hip.gemm_ex(dq1, _h_t(w[32], half), epilogue=_hip.EP_RELU_MASK, aux=q0)
         grads[30], grads[31] = _hip.linear_wgrad_ex(dq0, xb)
-        g = _hip.gemm_ex(dq0, _h_t(w[30], half), epilogue=_hip.EP_F32)
-        for k in reversed(range(6)):
-            o = 6 + 4 * k
-            xbk, hk = blocks[k]
-            g, grads[o], grads[o + 1], grads[o + 2], grads[o + 3] = _block_bwd(
-                g, xbk, hk, _h_t(w[o], half), _h_t(w[o + 2], half), ctx.ps[k], ctx.seeds[k])
+        if ctx.r16:
+            # g and the last block's dD from one epilogue; each block's EP_ADD16 then emits the
+            # next (earlier) block's dD beside its g
+            g, dd = _hip.gemm_ex(dq0, _h_t(w[30], half), epilogue=_hip.EP_BF16, seed=ctx.seeds[5],
+                                 p=ctx.ps[5], dropout_copy=True)
+            for k in reversed(range(6)):
+                o = 6 + 4 * k
+                xbk, hk = blocks[k]
+                dz = _hip.gemm_ex(dd, _h_t(w[o + 2], half), epilogue=_hip.EP_RELU_MASK, aux=hk)
+                grads[o + 2], grads[o + 3] = _hip.linear_wgrad_ex(dd, hk)
+                if k:
+                    g, dd = _hip.gemm_ex(dz, _h_t(w[o], half), epilogue=_hip.EP_ADD16, aux=g,
+                                         seed=ctx.seeds[k - 1], p=ctx.ps[k - 1], dropout_copy=True)
+                else:
+                    g = _hip.gemm_ex(dz, _h_t(w[o], half), epilogue=_hip.EP_ADD16, aux=g)
+                grads[o], grads[o + 1] = _hip.linear_wgrad_ex(dz, xbk)
+        else:
+            g = _hip.gemm_ex(dq0, _h_t(w[30], half), epilogue=_hip.EP_F32)
+            for k in reversed(range(6)):
+                o = 6 + 4 * k
+                xbk, hk = blocks[k]
+                g, grads[o], grads[o + 1], grads[o + 2], grads[o + 3] = _block_bwd(
+                    g, xbk, hk, _h_t(w[o], half), _h_t(w[o + 2], half), ctx.ps[k], ctx.seeds[k])
         # x = ((pf + tf) + sf): dL/dpf = g, dL/dtf[b] = dL/dsf[b] = sum of g over cloud b's rows
         # per-cloud row sums as one batched GEMV (ones [B,1,N] @ g [B,N,256]): torch's
         # middle-dimension sum reduced this at ~40 % of the HBM rate (254 vs 82 us at B = 8)
         gsum = torch.bmm(torch.ones(B, 1, N, dtype=g.dtype, device=g.device),
-                         g.view(B, N, -1)).squeeze(1)
+                         g.view(B, N, -1)).squeeze(1).float()
         dcond = torch.stack([gsum, gsum], 1)
         grads[4], grads[5] = _hip.linear_wgrad_ex(g, h1)
         dh1 = _hip.gemm_ex(g, _h_t(w[4], half), epilogue=_hip.EP_RELU_MASK, aux=h1)

@@ -284,6 +284,70 @@ def test_gemm_ex_epilogues_vs_float64(H, M, K, O, a16, b16, half):
 
 
 @pytest.mark.parametrize("half", HALVES, ids=HALF_IDS)
+@pytest.mark.parametrize("M,K,O", [(1, 128, 128), (4097, 512, 256), (300, 136, 260), (60000, 256, 512)])
+@pytest.mark.parametrize("p", [0.0, 0.3])
+def test_gemm_ex_16bit_residual_epilogues(H, M, K, O, p, half):
+    """EP_RESID_DROP16 / EP_ADD16 (16-bit residual operand and output) against float64 products
+    of the rounded operands; the dropout copy of EP_BF16 / EP_ADD16 equals dropout_grad_bf16 of
+    the stored 16-bit output bit for bit; EP_COND's 16-bit-only output equals its copy."""
+    g = torch.Generator(device="cuda").manual_seed(M + K + O + int(10 * p))
+    A = torch.randn(M, K, device="cuda", generator=g).to(half)
+    B = (torch.randn(O, K, device="cuda", generator=g) * K ** -0.5).to(half)
+    bias = torch.randn(O, device="cuda", generator=g)
+    acc = A.double() @ B.double().t()
+    x16 = torch.randn(M, O, device="cuda", generator=g).to(half)
+    seed = 0x0DDB_A11_5EED + M
+    y = H.gemm_ex(A, B, bias, epilogue=H.EP_RESID_DROP16, aux=x16, seed=seed, p=p)
+    keep = (H.dropout_grad_bf16(torch.ones(M, O, device="cuda"), seed, p, half=half) != 0).double()
+    ref = x16.double() + keep * (acc + bias.double()) / (1.0 - p)
+    assert y.dtype == half and _bf16_ulp_close(y, ref)
+    assert torch.equal(H.gemm_ex(A, B, bias, epilogue=H.EP_RESID_DROP16, aux=x16, seed=seed, p=p), y)
+    gx = H.gemm_ex(A, B, epilogue=H.EP_ADD16, aux=x16)
+    assert gx.dtype == half and _bf16_ulp_close(gx, acc + x16.double())
+    for ep, aux in ((H.EP_ADD16, x16), (H.EP_BF16, None)):
+        c, dd = H.gemm_ex(A, B, epilogue=ep, aux=aux, seed=seed, p=p, dropout_copy=True)
+        assert torch.equal(c, H.gemm_ex(A, B, epilogue=ep, aux=aux))
+        assert torch.equal(dd, H.dropout_grad_bf16(c.float(), seed, p, half=half))
+    if O % 4 == 0 and M % 3 == 0:
+        cond = torch.randn(M // 3, 2, O, device="cuda", generator=g)
+        c32, c16 = H.gemm_ex(A, B, bias, epilogue=H.EP_COND, aux=cond, group_rows=3, copy_bf16=True)
+        only = H.gemm_ex(A, B, bias, epilogue=H.EP_COND, aux=cond, group_rows=3, copy_bf16=True,
+                         fp32_out=False)
+        assert torch.equal(only, c16)
+
+
+@pytest.mark.parametrize("half", HALVES, ids=HALF_IDS)
+def test_noise_predictor_16bit_residual_matches_fp32_residual(H, half, monkeypatch):
+    """NoisePredictorFn with the 16-bit residual stream (default) against the fp32-stream
+    layout, dropout on (the same seeds): forward and every gradient within 16-bit storage
+    error of the residual stream."""
+    from pointcloud_style_transfer_amd.config.config import Config
+    from pointcloud_style_transfer_amd.models import _autograd as ag
+    from pointcloud_style_transfer_amd.models.diffusion_model import NoisePredictor
+
+    torch.manual_seed(0)
+    npred = NoisePredictor(Config(make_dirs=False)).cuda().train()
+    x = torch.randn(2, 4000, 3, device="cuda")
+    t = torch.tensor([10, 500], device="cuda")
+    sf = torch.randn(2, 256, device="cuda")
+    outs, grads = [], []
+    for r16 in (True, False):
+        monkeypatch.setattr(ag, "RESIDUAL_16BIT", r16)
+        npred.zero_grad()
+        torch.manual_seed(5)  # the same dropout seeds
+        with torch.autocast("cuda", dtype=half):
+            out = npred(x, t, sf)
+        out.float().pow(2).sum().backward()
+        outs.append(out.detach().float())
+        grads.append([p.grad.detach().clone() for p in npred.parameters()])
+    rel = lambda a, b: ((a.double() - b.double()).norm() / b.double().norm()).item()  # noqa: E731
+    tol = 2e-2 if half == torch.bfloat16 else 4e-3
+    assert rel(outs[0], outs[1]) < tol
+    for a, b in zip(grads[0], grads[1]):
+        assert rel(a, b) < 2.5 * tol
+
+
+@pytest.mark.parametrize("half", HALVES, ids=HALF_IDS)
 @pytest.mark.parametrize("p", [0.0, 0.1, 0.5])
 def test_gemm_ex_dropout_mask_fwd_bwd_consistent(H, p, half):
     """EP_RESID_DROP keeps element e iff hash(seed, e) passes; pcst_dropout_grad_bf16 must
