@@ -92,47 +92,88 @@ __global__ __launch_bounds__(256) void pw_linear_kernel(const float* __restrict_
   }
 }
 
-// Deterministic per-channel statistics of Z [M, O]: partial float64 sums over row chunks,
-// then an in-order combine.  mean[o], var[o] (biased, as BatchNorm normalises with).
-// A 256-thread block covers TO = min(O, 64) channels x (256 / TO) row lanes of one chunk
-// (coalesced rows, every lane busy for narrow layers); the lanes fold in a fixed order.
+// Deterministic per-channel statistics of Z [M, O]: one pass of float64 partial sums and sums
+// of squares over row chunks (an fp32 value's square is exact in float64), then a fixed-order
+// combine.  mean[o], var[o] = E[z^2] - mean^2 (biased, as BatchNorm normalises with; in float64
+// the cancellation costs ~1e-16 * (mean^2 + var) / var relative, far below the fp32 outputs).
+// A 256-thread block covers TQ = min(O / W, 64) groups of W channels (W = 4: float4 loads when
+// O % 4 == 0) x (256 / TQ) row lanes of one chunk; the lanes fold in a fixed order.
 constexpr int kStatChunks = 256;
 
+template <int W>
 __global__ __launch_bounds__(256) void channel_partial_kernel(const float* __restrict__ Z, int64_t M,
-                                                              int O, const double* __restrict__ mean,
-                                                              double* __restrict__ part) {
-  const int TO = O < 64 ? O : 64;
-  const int RL = 256 / TO;
-  const int oc = threadIdx.x % TO, rl = threadIdx.x / TO;
-  const int o = blockIdx.y * TO + oc;
+                                                              int O, double* __restrict__ part) {
+  const int G = O / W;  // channel groups (O % W == 0)
+  const int TQ = G < 64 ? G : 64;
+  const int RL = 256 / TQ;
+  const int cg = threadIdx.x % TQ, rl = threadIdx.x / TQ;
+  const int o0 = (blockIdx.y * TQ + cg) * W;
   const int chunk = blockIdx.x;
   const int64_t per = (M + kStatChunks - 1) / kStatChunks;
   const int64_t a = chunk * per, e = a + per < M ? a + per : M;
-  __shared__ double sh[256];
-  double s = 0.0;
-  if (rl < RL && o < O) {
-    const double mu = mean ? mean[o] : 0.0;
+  __shared__ double s1[W][256], s2[W][256];
+  double t1[W], t2[W];
+#pragma unroll
+  for (int w = 0; w < W; ++w) t1[w] = t2[w] = 0.0;
+  if (rl < RL && o0 < O) {
     for (int64_t m = a + rl; m < e; m += RL) {
-      const double v = (double)Z[m * O + o] - mu;
-      s += mean ? v * v : v;
+      float v[W];
+      if constexpr (W == 4) {
+        const float4 q = *reinterpret_cast<const float4*>(Z + m * O + o0);
+        v[0] = q.x, v[1] = q.y, v[2] = q.z, v[3] = q.w;
+      } else {
+        v[0] = Z[m * O + o0];
+      }
+#pragma unroll
+      for (int w = 0; w < W; ++w) {
+        const double d = (double)v[w];
+        t1[w] += d;
+        t2[w] = fma(d, d, t2[w]);
+      }
     }
   }
-  sh[threadIdx.x] = s;
+#pragma unroll
+  for (int w = 0; w < W; ++w) {
+    s1[w][threadIdx.x] = t1[w];
+    s2[w][threadIdx.x] = t2[w];
+  }
   __syncthreads();
-  if (rl == 0 && o < O) {
-    double t = 0.0;
-    for (int q = 0; q < RL; ++q) t += sh[q * TO + oc];
-    part[(int64_t)chunk * O + o] = t;
+  if (rl == 0 && o0 < O) {
+#pragma unroll
+    for (int w = 0; w < W; ++w) {
+      double u1 = 0.0, u2 = 0.0;
+      for (int q = 0; q < RL; ++q) {
+        u1 += s1[w][q * TQ + cg];
+        u2 += s2[w][q * TQ + cg];
+      }
+      part[((int64_t)chunk * 2 + 0) * O + o0 + w] = u1;
+      part[((int64_t)chunk * 2 + 1) * O + o0 + w] = u2;
+    }
   }
 }
 
-__global__ void channel_combine_kernel(const double* __restrict__ part, int64_t M, int O,
-                                       double* __restrict__ out) {
-  const int o = blockIdx.x * 256 + threadIdx.x;
+// one wave per channel: lane j folds chunks j, j + 64, ... in order, then a fixed butterfly
+__device__ __forceinline__ double chunk_fold(const double* __restrict__ part, int64_t stride, int lane) {
+  double t = 0.0;
+  for (int c = lane; c < kStatChunks; c += 64) t += part[(int64_t)c * stride];
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) t += __shfl_xor(t, d);
+  return t;
+}
+
+__global__ __launch_bounds__(256) void channel_combine_kernel(const double* __restrict__ part, int64_t M,
+                                                              int O, double* __restrict__ mean,
+                                                              double* __restrict__ var) {
+  const int o = blockIdx.x * 4 + (int)(threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (o >= O) return;
-  double s = 0.0;
-  for (int c = 0; c < kStatChunks; ++c) s += part[(int64_t)c * O + o];
-  out[o] = s / (double)M;
+  const double s = chunk_fold(part + o, 2 * (int64_t)O, lane);
+  const double q = chunk_fold(part + O + o, 2 * (int64_t)O, lane);
+  if (lane == 0) {
+    const double mu = s / (double)M;
+    const double v = q / (double)M - mu * mu;
+    mean[o] = mu;
+    var[o] = v > 0.0 ? v : 0.0;
+  }
 }
 
 __global__ void affine_act_kernel(const float* __restrict__ Z, int64_t M, int O,
@@ -284,7 +325,7 @@ extern "C" int pcst_pointwise_linear(const float* X, int64_t M, int64_t K, const
 }
 
 extern "C" int pcst_channel_stats_workspace_size(int64_t O, size_t* bytes) {
-  *bytes = sizeof(double) * (size_t)(kStatChunks * O);
+  *bytes = sizeof(double) * (size_t)(2 * kStatChunks * O);
   return PCST_OK;
 }
 
@@ -293,11 +334,16 @@ extern "C" int pcst_channel_stats(const float* Z, int64_t M, int64_t O, double* 
   PCST_CHECK_ARG(M > 0 && O > 0, "channel_stats: bad shape");
   hipStream_t s = as_stream(stream);
   double* part = static_cast<double*>(workspace);
-  dim3 g(kStatChunks, (unsigned)cdiv(O, O < 64 ? O : 64));
-  hipLaunchKernelGGL(channel_partial_kernel, g, dim3(256), 0, s, Z, M, (int)O, (const double*)nullptr, part);
-  hipLaunchKernelGGL(channel_combine_kernel, dim3((unsigned)cdiv(O, 256)), dim3(256), 0, s, part, M, (int)O, mean);
-  hipLaunchKernelGGL(channel_partial_kernel, g, dim3(256), 0, s, Z, M, (int)O, (const double*)mean, part);
-  hipLaunchKernelGGL(channel_combine_kernel, dim3((unsigned)cdiv(O, 256)), dim3(256), 0, s, part, M, (int)O, var);
+  if (O % 4 == 0 && (uintptr_t)Z % 16 == 0) {
+    const int64_t G = O / 4;
+    hipLaunchKernelGGL(channel_partial_kernel<4>, dim3(kStatChunks, (unsigned)cdiv(G, G < 64 ? G : 64)),
+                       dim3(256), 0, s, Z, M, (int)O, part);
+  } else {
+    hipLaunchKernelGGL(channel_partial_kernel<1>, dim3(kStatChunks, (unsigned)cdiv(O, O < 64 ? O : 64)),
+                       dim3(256), 0, s, Z, M, (int)O, part);
+  }
+  hipLaunchKernelGGL(channel_combine_kernel, dim3((unsigned)cdiv(O, 4)), dim3(256), 0, s, part, M,
+                     (int)O, mean, var);
   PCST_LAUNCH_CHECK("channel_stats");
   return PCST_OK;
 }

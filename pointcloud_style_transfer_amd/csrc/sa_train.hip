@@ -69,73 +69,130 @@ __global__ void bn_relu_maxpool_kernel(const float* __restrict__ Z, int64_t G, i
   }
 }
 
-// Per-channel partial sums over row chunks: a 256-thread block covers TO = min(O, 64) channels
-// x (256 / TO) row lanes; lanes are folded in a fixed order, chunks combined in order later.
-__device__ __forceinline__ float bn_dyp(const float* __restrict__ Z, const float* __restrict__ dY,
-                                        const float* __restrict__ dP, const int32_t* __restrict__ arg,
-                                        int64_t ns, int O, int64_t m, int o, float sc, float sh,
-                                        float& z) {
-  z = Z[m * O + o];
-  float dy;
+// Per-channel partial sums over row chunks: a 256-thread block covers TQ = min(O / W, 64)
+// groups of W channels (W = 4: 16-byte loads when O % 4 == 0) x (256 / TQ) row lanes; lanes are
+// folded in a fixed order, chunks combined in a fixed order later.
+template <int W>
+struct Vec;
+template <>
+struct Vec<4> {
+  float v[4];
+  __device__ __forceinline__ void load(const float* __restrict__ p) {
+    const float4 q = *reinterpret_cast<const float4*>(p);
+    v[0] = q.x, v[1] = q.y, v[2] = q.z, v[3] = q.w;
+  }
+};
+template <>
+struct Vec<1> {
+  float v[1];
+  __device__ __forceinline__ void load(const float* __restrict__ p) { v[0] = *p; }
+};
+
+// dyp[w] = dY * [scale z + shift > 0] for channels o..o+W-1 of row m (z returned)
+template <int W>
+__device__ __forceinline__ void bn_dyp(const float* __restrict__ Z, const float* __restrict__ dY,
+                                       const float* __restrict__ dP, const int32_t* __restrict__ arg,
+                                       int64_t ns, int O, int64_t m, int o, const float* sc,
+                                       const float* sh, float (&z)[W], float (&dyp)[W]) {
+  Vec<W> zv, dv;
+  zv.load(Z + m * O + o);
   if (dY) {
-    dy = dY[m * O + o];
+    dv.load(dY + m * O + o);
   } else {
     const int64_t g = m / ns;
-    dy = arg[g * O + o] == (int)(m - g * ns) ? dP[g * O + o] : 0.0f;
+    const int r = (int)(m - g * ns);
+    dv.load(dP + g * O + o);
+#pragma unroll
+    for (int w = 0; w < W; ++w)
+      if (arg[g * O + o + w] != r) dv.v[w] = 0.0f;
   }
-  return fmaf(z, sc, sh) > 0.0f ? dy : 0.0f;
+#pragma unroll
+  for (int w = 0; w < W; ++w) {
+    z[w] = zv.v[w];
+    dyp[w] = fmaf(z[w], sc[w], sh[w]) > 0.0f ? dv.v[w] : 0.0f;
+  }
 }
 
+template <int W>
 __global__ __launch_bounds__(256) void bn_bwd_partial_kernel(
     const float* __restrict__ Z, const float* __restrict__ dY, const float* __restrict__ dP,
     const int32_t* __restrict__ arg, int64_t M, int64_t ns, int O, const float* __restrict__ scale,
     const float* __restrict__ shift, const double* __restrict__ mean,
     const double* __restrict__ invstd, double* __restrict__ part) {
-  const int TO = O < 64 ? O : 64;
-  const int RL = 256 / TO;                 // row lanes
-  const int oc = threadIdx.x % TO, rl = threadIdx.x / TO;
-  const int o = blockIdx.y * TO + oc;
+  const int G = O / W;
+  const int TQ = G < 64 ? G : 64;
+  const int RL = 256 / TQ;                 // row lanes
+  const int cg = threadIdx.x % TQ, rl = threadIdx.x / TQ;
+  const int o = (blockIdx.y * TQ + cg) * W;
   const int chunk = blockIdx.x;
   const int64_t per = (M + kBnChunks - 1) / kBnChunks;
   const int64_t a = chunk * per, e = a + per < M ? a + per : M;
-  __shared__ double s1[256], s2[256];
-  double t1 = 0.0, t2 = 0.0;
+  __shared__ double s1[W][256], s2[W][256];
+  double t1[W], t2[W];
+#pragma unroll
+  for (int w = 0; w < W; ++w) t1[w] = t2[w] = 0.0;
   if (rl < RL && o < O) {
-    const float sc = scale[o], sh = shift[o];
-    const double mu = mean[o], is = invstd[o];
+    float sc[W], sh[W];
+    double mu[W], is[W];
+#pragma unroll
+    for (int w = 0; w < W; ++w) {
+      sc[w] = scale[o + w];
+      sh[w] = shift[o + w];
+      mu[w] = mean[o + w];
+      is[w] = invstd[o + w];
+    }
     for (int64_t m = a + rl; m < e; m += RL) {
-      float z;
-      const double dyp = bn_dyp(Z, dY, dP, arg, ns, O, m, o, sc, sh, z);
-      t1 += dyp;
-      t2 += dyp * (((double)z - mu) * is);
+      float z[W], dyp[W];
+      bn_dyp<W>(Z, dY, dP, arg, ns, O, m, o, sc, sh, z, dyp);
+#pragma unroll
+      for (int w = 0; w < W; ++w) {
+        t1[w] += dyp[w];
+        t2[w] += dyp[w] * (((double)z[w] - mu[w]) * is[w]);
+      }
     }
   }
-  s1[threadIdx.x] = t1;
-  s2[threadIdx.x] = t2;
+#pragma unroll
+  for (int w = 0; w < W; ++w) {
+    s1[w][threadIdx.x] = t1[w];
+    s2[w][threadIdx.x] = t2[w];
+  }
   __syncthreads();
   if (rl == 0 && o < O) {
-    double u1 = 0.0, u2 = 0.0;
-    for (int q = 0; q < RL; ++q) {
-      u1 += s1[q * TO + oc];
-      u2 += s2[q * TO + oc];
+#pragma unroll
+    for (int w = 0; w < W; ++w) {
+      double u1 = 0.0, u2 = 0.0;
+      for (int q = 0; q < RL; ++q) {
+        u1 += s1[w][q * TQ + cg];
+        u2 += s2[w][q * TQ + cg];
+      }
+      part[((int64_t)chunk * 2 + 0) * O + o + w] = u1;
+      part[((int64_t)chunk * 2 + 1) * O + o + w] = u2;
     }
-    part[((int64_t)chunk * 2 + 0) * O + o] = u1;
-    part[((int64_t)chunk * 2 + 1) * O + o] = u2;
   }
 }
 
-// S1, S2 in chunk order -> dgamma = S2, dbeta = S1 and the per-channel coefficients of dZ
-__global__ void bn_bwd_combine_kernel(const double* __restrict__ part, int64_t M, int O,
-                                      const float* __restrict__ gamma,
-                                      const double* __restrict__ invstd, double* __restrict__ coef,
-                                      float* __restrict__ dgamma, float* __restrict__ dbeta) {
-  const int o = blockIdx.x * 256 + threadIdx.x;
+// one wave per channel: lane j folds chunks j, j + 64, ... in order, then a fixed butterfly
+__device__ __forceinline__ double bn_chunk_fold(const double* __restrict__ part, int64_t stride,
+                                                int lane) {
+  double t = 0.0;
+  for (int c = lane; c < kBnChunks; c += 64) t += part[(int64_t)c * stride];
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) t += __shfl_xor(t, d);
+  return t;
+}
+
+// S1, S2 over the chunks -> dgamma = S2, dbeta = S1 and the per-channel coefficients of dZ
+__global__ __launch_bounds__(256) void bn_bwd_combine_kernel(const double* __restrict__ part, int64_t M,
+                                                             int O, const float* __restrict__ gamma,
+                                                             const double* __restrict__ invstd,
+                                                             double* __restrict__ coef,
+                                                             float* __restrict__ dgamma,
+                                                             float* __restrict__ dbeta) {
+  const int o = blockIdx.x * 4 + (int)(threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (o >= O) return;
-  double u1 = 0.0, u2 = 0.0;
-  for (int c = 0; c < kBnChunks; ++c) {
-    u1 += part[((int64_t)c * 2 + 0) * O + o];
-    u2 += part[((int64_t)c * 2 + 1) * O + o];
-  }
+  const double u1 = bn_chunk_fold(part + o, 2 * (int64_t)O, lane);
+  const double u2 = bn_chunk_fold(part + O + o, 2 * (int64_t)O, lane);
+  if (lane) return;
   if (dgamma) dgamma[o] = (float)u2;
   if (dbeta) dbeta[o] = (float)u1;
   coef[o * 3 + 0] = (double)gamma[o] * invstd[o];
@@ -143,20 +200,36 @@ __global__ void bn_bwd_combine_kernel(const double* __restrict__ part, int64_t M
   coef[o * 3 + 2] = u2 / (double)M;
 }
 
+// dZ = g invstd (dyp - S1/M - xhat S2/M), W channels of one row per thread
+template <int W>
 __global__ void bn_bwd_apply_kernel(const float* __restrict__ Z, const float* __restrict__ dY,
                                     const float* __restrict__ dP, const int32_t* __restrict__ arg,
                                     int64_t M, int64_t ns, int O, const float* __restrict__ scale,
                                     const float* __restrict__ shift, const double* __restrict__ mean,
                                     const double* __restrict__ invstd,
                                     const double* __restrict__ coef, float* __restrict__ dZ) {
-  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < M * O;
-       e += (int64_t)gridDim.x * blockDim.x) {
-    const int o = (int)(e % O);
-    const int64_t m = e / O;
-    float z;
-    const double dyp = bn_dyp(Z, dY, dP, arg, ns, O, m, o, scale[o], shift[o], z);
-    const double xh = ((double)z - mean[o]) * invstd[o];
-    dZ[e] = (float)(coef[o * 3 + 0] * (dyp - coef[o * 3 + 1] - xh * coef[o * 3 + 2]));
+  const int G = O / W;
+  for (int64_t q = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; q < M * G;
+       q += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t m = q / G;
+    const int o = (int)(q - m * G) * W;
+    float sc[W], sh[W], z[W], dyp[W], out[W];
+#pragma unroll
+    for (int w = 0; w < W; ++w) {
+      sc[w] = scale[o + w];
+      sh[w] = shift[o + w];
+    }
+    bn_dyp<W>(Z, dY, dP, arg, ns, O, m, o, sc, sh, z, dyp);
+#pragma unroll
+    for (int w = 0; w < W; ++w) {
+      const double xh = ((double)z[w] - mean[o + w]) * invstd[o + w];
+      out[w] = (float)(coef[(o + w) * 3 + 0] *
+                       ((double)dyp[w] - coef[(o + w) * 3 + 1] - xh * coef[(o + w) * 3 + 2]));
+    }
+    if constexpr (W == 4)
+      *reinterpret_cast<float4*>(dZ + m * O + o) = make_float4(out[0], out[1], out[2], out[3]);
+    else
+      dZ[m * O + o] = out[0];
   }
 }
 
@@ -274,13 +347,23 @@ extern "C" int pcst_bn_relu_bwd(const float* Z, int64_t M, int64_t O, const floa
   hipStream_t s = as_stream(stream);
   double* part = static_cast<double*>(workspace);
   double* coef = part + 2 * kBnChunks * O;
-  const int TO = O < 64 ? (int)O : 64;
-  hipLaunchKernelGGL(bn_bwd_partial_kernel, dim3(kBnChunks, (unsigned)cdiv(O, TO)), dim3(256), 0, s,
-                     Z, dY, dP, arg, M, ns, (int)O, scale, shift, mean, invstd, part);
-  hipLaunchKernelGGL(bn_bwd_combine_kernel, dim3((unsigned)cdiv(O, 256)), dim3(256), 0, s, part, M,
+  const bool vec = O % 4 == 0 && ((uintptr_t)Z | (uintptr_t)dY | (uintptr_t)dP | (uintptr_t)dZ) % 16 == 0;
+  if (vec) {
+    const int64_t G = O / 4;
+    hipLaunchKernelGGL(bn_bwd_partial_kernel<4>, dim3(kBnChunks, (unsigned)cdiv(G, G < 64 ? G : 64)),
+                       dim3(256), 0, s, Z, dY, dP, arg, M, ns, (int)O, scale, shift, mean, invstd, part);
+  } else {
+    hipLaunchKernelGGL(bn_bwd_partial_kernel<1>, dim3(kBnChunks, (unsigned)cdiv(O, O < 64 ? O : 64)),
+                       dim3(256), 0, s, Z, dY, dP, arg, M, ns, (int)O, scale, shift, mean, invstd, part);
+  }
+  hipLaunchKernelGGL(bn_bwd_combine_kernel, dim3((unsigned)cdiv(O, 4)), dim3(256), 0, s, part, M,
                      (int)O, gamma, invstd, coef, dgamma, dbeta);
-  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(grid1d(M * O)), dim3(256), 0, s, Z, dY, dP, arg, M,
-                     ns, (int)O, scale, shift, mean, invstd, coef, dZ);
+  if (vec)
+    hipLaunchKernelGGL(bn_bwd_apply_kernel<4>, dim3(grid1d(M * O / 4)), dim3(256), 0, s, Z, dY, dP,
+                       arg, M, ns, (int)O, scale, shift, mean, invstd, coef, dZ);
+  else
+    hipLaunchKernelGGL(bn_bwd_apply_kernel<1>, dim3(grid1d(M * O)), dim3(256), 0, s, Z, dY, dP, arg,
+                       M, ns, (int)O, scale, shift, mean, invstd, coef, dZ);
   PCST_LAUNCH_CHECK("bn_relu_bwd");
   return PCST_OK;
 }
