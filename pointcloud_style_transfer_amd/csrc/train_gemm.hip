@@ -269,51 +269,40 @@ __global__ __launch_bounds__(256) void wgrad_bf16_kernel(const float* __restrict
   }
 }
 
-__global__ void wgrad_bf16_combine_kernel(const float* __restrict__ part, int64_t n, int chunks,
-                                          float* __restrict__ out) {
-  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < n;
-       e += (int64_t)gridDim.x * blockDim.x) {
-    double s = 0.0;
-    int c = 0;
-    for (; c + 8 <= chunks; c += 8) {  // 8 loads in flight, summed in chunk order
-      float v[8];
+// Chunk partials -> dW and db in one launch: a 256-thread block covers 64 outputs (of dW, then
+// of db); wave w folds its quarter of the chunks in order into float64 with its loads in flight
+// together, and the four quarters meet in LDS in order -- a fixed reduction tree (deterministic).
+constexpr int kCombLoads = 32;
+__global__ __launch_bounds__(256) void wgrad_bf16_combine_kernel(
+    const float* __restrict__ partW, int64_t nW, const float* __restrict__ partB, int64_t nB,
+    int chunks, float* __restrict__ outW, float* __restrict__ outB) {
+  __shared__ double red[3][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t q = (int64_t)blockIdx.x * 64 + lane;
+  const bool isW = q < nW;
+  const bool valid = q < nW + nB;
+  const float* part = isW ? partW : partB;
+  const int64_t n = isW ? nW : nB;
+  const int64_t e = isW ? q : q - nW;
+  const int lo = (w * chunks) / 4, hi = ((w + 1) * chunks) / 4;
+  double s = 0.0;
+  if (valid) {
+    for (int c0 = lo; c0 < hi; c0 += kCombLoads) {
+      float v[kCombLoads];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) v[u] = part[(int64_t)(c + u) * n + e];
+      for (int u = 0; u < kCombLoads; ++u)
+        if (c0 + u < hi) v[u] = part[(int64_t)(c0 + u) * n + e];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) s += (double)v[u];
+      for (int u = 0; u < kCombLoads; ++u)
+        if (c0 + u < hi) s += (double)v[u];
     }
-    for (; c < chunks; ++c) s += (double)part[(int64_t)c * n + e];
-    out[e] = (float)s;
   }
-}
-
-// n % 4 == 0: four consecutive outputs per thread, 8 chunk loads in flight, same in-order sums
-__global__ void wgrad_bf16_combine4_kernel(const float4* __restrict__ part, int64_t n4, int chunks,
-                                           float4* __restrict__ out) {
-  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < n4;
-       e += (int64_t)gridDim.x * blockDim.x) {
-    double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
-    int c = 0;
-    for (; c + 8 <= chunks; c += 8) {
-      float4 v[8];
+  if (w) red[w - 1][lane] = s;
+  __syncthreads();
+  if (w == 0 && valid) {
 #pragma unroll
-      for (int u = 0; u < 8; ++u) v[u] = part[(int64_t)(c + u) * n4 + e];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        s0 += (double)v[u].x;
-        s1 += (double)v[u].y;
-        s2 += (double)v[u].z;
-        s3 += (double)v[u].w;
-      }
-    }
-    for (; c < chunks; ++c) {
-      const float4 v = part[(int64_t)c * n4 + e];
-      s0 += (double)v.x;
-      s1 += (double)v.y;
-      s2 += (double)v.z;
-      s3 += (double)v.w;
-    }
-    out[e] = make_float4((float)s0, (float)s1, (float)s2, (float)s3);
+    for (int k = 0; k < 3; ++k) s += red[k][lane];
+    if (isW) outW[e] = (float)s; else outB[e] = (float)s;
   }
 }
 
@@ -376,19 +365,9 @@ int wgrad16_impl(const float* dZ, const float* X, int64_t M, int64_t I, int64_t 
   hipLaunchKernelGGL(wgrad_bf16_kernel, dim3((unsigned)(p.tiles_i * p.tiles_o), (unsigned)p.chunks),
                      dim3(256), 0, s, dZ, X, M, (int)I, (int)O, p.rows_per_chunk, p.tiles_i, partW,
                      partB);
-  const int64_t n = O * I;
-  if (n % 4 == 0 && (uintptr_t)dW % 16 == 0)
-    hipLaunchKernelGGL(wgrad_bf16_combine4_kernel,
-                       dim3((unsigned)std::min<int64_t>(cdiv(n / 4, 256), 2048)), dim3(256), 0, s,
-                       reinterpret_cast<const float4*>(partW), n / 4, p.chunks,
-                       reinterpret_cast<float4*>(dW));
-  else
-    hipLaunchKernelGGL(wgrad_bf16_combine_kernel,
-                       dim3((unsigned)std::min<int64_t>(cdiv(n, 256), 2048)), dim3(256), 0, s,
-                       partW, n, p.chunks, dW);
-  if (db)
-    hipLaunchKernelGGL(wgrad_bf16_combine_kernel, dim3((unsigned)cdiv(O, 256)), dim3(256), 0, s,
-                       partB, O, p.chunks, db);
+  const int64_t nW = O * I, nB = db ? O : 0;
+  hipLaunchKernelGGL(wgrad_bf16_combine_kernel, dim3((unsigned)cdiv(nW + nB, 64)), dim3(256), 0, s,
+                     partW, nW, partB, nB, p.chunks, dW, db);
   PCST_LAUNCH_CHECK("linear_wgrad_bf16");
   return PCST_OK;
 }

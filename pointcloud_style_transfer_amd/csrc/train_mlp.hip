@@ -936,34 +936,59 @@ __global__ __launch_bounds__(256) void wgrad_ex_kernel(const TZ* __restrict__ dZ
   }
 }
 
-__global__ void wgrad_ex_combine_kernel(const float4* __restrict__ part, int64_t n4, int chunks,
-                                        float4* __restrict__ out) {
-  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < n4;
-       e += (int64_t)gridDim.x * blockDim.x) {
-    double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
-    int c = 0;
-    for (; c + 8 <= chunks; c += 8) {  // 8 loads in flight, summed in chunk order
-      float4 v[8];
+// Chunk partials -> dW and db in one launch: a 256-thread block covers 64 float4 elements (of
+// dW, then of db); wave w folds its quarter of the chunks in order into float64 (all its loads in
+// flight together), and the four quarters meet in LDS in order -- a fixed reduction tree, so the
+// gradient is deterministic.
+constexpr int kCombLoads = 32;  // float4 loads in flight per thread
+__global__ __launch_bounds__(256) void wgrad_ex_combine_kernel(
+    const float4* __restrict__ partW, int64_t nW4, const float4* __restrict__ partB, int64_t nB4,
+    int chunks, float4* __restrict__ outW, float4* __restrict__ outB) {
+  __shared__ double red[3][64][4];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t q = (int64_t)blockIdx.x * 64 + lane;
+  const bool isW = q < nW4;
+  const bool valid = q < nW4 + nB4;
+  const float4* part = isW ? partW : partB;
+  const int64_t n4 = isW ? nW4 : nB4;
+  const int64_t e = isW ? q : q - nW4;
+  const int lo = (w * chunks) / 4, hi = ((w + 1) * chunks) / 4;
+  double s[4] = {0.0, 0.0, 0.0, 0.0};
+  if (valid) {
+    for (int c0 = lo; c0 < hi; c0 += kCombLoads) {
+      float4 v[kCombLoads];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) v[u] = part[(int64_t)(c + u) * n4 + e];
+      for (int u = 0; u < kCombLoads; ++u)
+        if (c0 + u < hi) v[u] = part[(int64_t)(c0 + u) * n4 + e];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        s0 += (double)v[u].x;
-        s1 += (double)v[u].y;
-        s2 += (double)v[u].z;
-        s3 += (double)v[u].w;
-      }
+      for (int u = 0; u < kCombLoads; ++u)
+        if (c0 + u < hi) {
+          s[0] += (double)v[u].x;
+          s[1] += (double)v[u].y;
+          s[2] += (double)v[u].z;
+          s[3] += (double)v[u].w;
+        }
     }
-    for (; c < chunks; ++c) {
-      const float4 v = part[(int64_t)c * n4 + e];
-      s0 += (double)v.x;
-      s1 += (double)v.y;
-      s2 += (double)v.z;
-      s3 += (double)v.w;
-    }
-    out[e] = make_float4((float)s0, (float)s1, (float)s2, (float)s3);
+  }
+  if (w) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) red[w - 1][lane][u] = s[u];
+  }
+  __syncthreads();
+  if (w == 0 && valid) {
+#pragma unroll
+    for (int k = 0; k < 3; ++k)
+#pragma unroll
+      for (int u = 0; u < 4; ++u) s[u] += red[k][lane][u];
+    const float4 r = make_float4((float)s[0], (float)s[1], (float)s[2], (float)s[3]);
+    if (isW) outW[e] = r; else outB[e] = r;
   }
 }
+
+// workgroups of one weight-gradient launch (experiment builds: XDEF=-DPCST_X_WGRAD_WG=N)
+#ifndef PCST_X_WGRAD_WG
+#define PCST_X_WGRAD_WG 512
+#endif
 
 struct WgradExPlan {
   int tiles_i, tiles_o, ntile, chunks, total, per_xcd;
@@ -975,7 +1000,7 @@ static WgradExPlan wgrad_ex_plan(int64_t M, int64_t I, int64_t O) {
   p.tiles_i = (int)cdiv(I, kXT);
   p.tiles_o = (int)cdiv(O, kXT);
   p.ntile = p.tiles_i * p.tiles_o;
-  int64_t chunks = cdiv(512, p.ntile);  // ~2 workgroups per CU
+  int64_t chunks = cdiv(PCST_X_WGRAD_WG, p.ntile);  // ~2 workgroups per CU
   chunks = std::max<int64_t>(1, std::min<int64_t>(chunks, cdiv(M, 512)));
   p.rows_per_chunk = cdiv(cdiv(M, chunks), kWS) * kWS;
   p.chunks = (int)cdiv(M, p.rows_per_chunk);
@@ -1176,14 +1201,11 @@ int wgrad_ex_impl(const void* dZ, int dz_bf16, const void* X, int x_bf16, int64_
   else
     PCST_WGRAD_EX(float, float);
 #undef PCST_WGRAD_EX
-  const int64_t n4 = O * I / 4;
-  hipLaunchKernelGGL(wgrad_ex_combine_kernel, dim3((unsigned)std::min<int64_t>(cdiv(n4, 256), 2048)),
-                     dim3(256), 0, s, reinterpret_cast<const float4*>(partW), n4, p.chunks,
-                     reinterpret_cast<float4*>(dW));
-  if (db)
-    hipLaunchKernelGGL(wgrad_ex_combine_kernel, dim3((unsigned)cdiv(O / 4, 256)), dim3(256), 0, s,
-                       reinterpret_cast<const float4*>(partB), O / 4, p.chunks,
-                       reinterpret_cast<float4*>(db));
+  const int64_t nW4 = O * I / 4, nB4 = db ? O / 4 : 0;
+  hipLaunchKernelGGL(wgrad_ex_combine_kernel, dim3((unsigned)cdiv(nW4 + nB4, 64)), dim3(256), 0, s,
+                     reinterpret_cast<const float4*>(partW), nW4,
+                     reinterpret_cast<const float4*>(partB), nB4, p.chunks,
+                     reinterpret_cast<float4*>(dW), reinterpret_cast<float4*>(db));
   PCST_LAUNCH_CHECK("linear_wgrad_ex");
   return PCST_OK;
 }
