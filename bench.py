@@ -382,9 +382,8 @@ def main():
                 ev.append((e0, e1))
                 return nc_
 
-            eps = dmod.hierarchical_eps(hp, mlp, xc, xi, x_cat, knn_ws, side)
-            x = _hip.cfg_ddim_step(x, eps[:C], eps[C:], src, 7.5, dp._coeffs(t, t_prev),
-                                   x_cat=x_cat)
+            x = dmod.hierarchical_step(hp, mlp, xc, xi, x_cat, x, src, 7.5, dp._coeffs(t, t_prev),
+                                       knn_ws, side)
 
         lctx = torch.cuda.stream(loop_stream) if overlap else contextlib.nullcontext()
         with lctx:

@@ -227,6 +227,20 @@ int pcst_knn3_build(const float* orig, const int64_t* idx, int64_t B, int64_t N,
                     int64_t lds_floor, int64_t max_wg, void* workspace, void* stream);
 int pcst_knn3_query(const float* coarse, const float* orig, int64_t B, int64_t N, int64_t M,
                     float* out, void* workspace, void* stream);
+/* The query in two halves (the same bits as pcst_knn3_query).  search (after build; positions
+ * only): every unknown row's three neighbours and float64 IDW weights into the workspace, so it
+ * can run beside the noise MLP too; finish: out [B,N,3] from coarse [B,M,3] (the gathers and the
+ * weighted sums).  finish_cfg_ddim: the finish of a CFG batch (B = 2C clouds: rows c and C + c are
+ * the conditional and unconditional eps of cloud c) fused with pcst_cfg_ddim_step's update of x
+ * [C,N,3] (source [C,N,3] or NULL, x_cat [2C,N,3] or NULL). */
+int pcst_knn3_search(const float* orig, int64_t B, int64_t N, int64_t M, void* workspace,
+                     void* stream);
+int pcst_knn3_finish(const float* coarse, int64_t B, int64_t N, int64_t M, float* out,
+                     void* workspace, void* stream);
+int pcst_knn3_finish_cfg_ddim(const float* coarse, int64_t B, int64_t N, int64_t M, void* workspace,
+                              const float* x, const float* source, float guidance_scale,
+                              float sqrt_1m_at, float sqrt_at_eps, float sqrt_aprev,
+                              float sqrt_1m_aprev, float* x_out, float* x_cat, void* stream);
 /* diagnostics of the last query on a workspace: out[0] error flag, out[1..B] query chunks per
  * cloud, out[1+B..2B] outlier queries per cloud (device int32 buffer of 1 + 2B) */
 int pcst_knn_stats(void* workspace, int64_t B, int64_t N, int64_t M, int32_t* out, void* stream);

@@ -50,6 +50,9 @@ SIGNATURES = {
     "pcst_cfg_ddim_step_dcoef": [_P, _P, _P, _P, _I, ctypes.c_float, _P, _P, _P, _P],
     "pcst_voxel_downsample_copies_dseed": [_P, _I, _I, _I, _I, _P, _P, _P, _P, _P],
     "pcst_knn3_query": [_P, _P, _I, _I, _I, _P, _P, _P],
+    "pcst_knn3_search": [_P, _I, _I, _I, _P, _P],
+    "pcst_knn3_finish": [_P, _I, _I, _I, _P, _P, _P],
+    "pcst_knn3_finish_cfg_ddim": [_P, _I, _I, _I, _P, _P, _P, _F, _F, _F, _F, _F, _P, _P, _P],
     "pcst_knn_error": [_P, _I, _I, _I, _P, _P],
     "pcst_knn_stats": [_P, _I, _I, _I, _P, _P],
     "pcst_noise_mlp_blob_bytes": [ctypes.c_int],
@@ -423,6 +426,56 @@ def knn3_query(coarse, handle):
         raise RuntimeError(f"knn3_query: coarse {tuple(coarse.shape)} != {(B, M, 3)}")
     out = torch.empty(B, N, 3, dtype=torch.float32, device=orig.device)
     _call("pcst_knn3_query", _ptr(coarse), _ptr(orig), B, N, M, _ptr(out), _ptr(ws), _stream())
+    return out
+
+
+def knn3_search(handle):
+    """The positions-only half of knn3_query on the current stream (after knn3_build on the
+    handle's workspace): every row's three neighbours and IDW weights into the workspace, so
+    that only the gather of the coarse values (knn3_finish / knn3_finish_cfg_ddim) waits for
+    the noise MLP.  Returns the handle."""
+    orig, idx, ws = handle
+    B, N, _ = orig.shape
+    _call("pcst_knn3_search", _ptr(orig), B, N, idx.shape[1], _ptr(ws), _stream())
+    return handle
+
+
+def _coarse_for(coarse, handle, name):
+    orig, idx, _ = handle
+    require_device(coarse)
+    coarse = _f32(coarse)
+    B, N, _ = orig.shape
+    M = idx.shape[1]
+    if coarse.shape != (B, M, 3):
+        raise RuntimeError(f"{name}: coarse {tuple(coarse.shape)} != {(B, M, 3)}")
+    return coarse, B, N, M
+
+
+def knn3_finish(coarse, handle):
+    """After knn3_search: coarse [B,M,3] -> [B,N,3], the same bits as knn3_query."""
+    coarse, B, N, M = _coarse_for(coarse, handle, "knn3_finish")
+    out = torch.empty(B, N, 3, dtype=torch.float32, device=coarse.device)
+    _call("pcst_knn3_finish", _ptr(coarse), B, N, M, _ptr(out), _ptr(handle[2]), _stream())
+    return out
+
+
+def knn3_finish_cfg_ddim(coarse, handle, x, source, guidance_scale, coeffs, x_cat=None, out=None):
+    """After knn3_search on the CFG batch (2C clouds): cfg_ddim_step(x, eps[:C], eps[C:], ...)
+    with eps = knn3_finish(coarse, handle), in one launch and with the same bits."""
+    coarse, B, N, M = _coarse_for(coarse, handle, "knn3_finish_cfg_ddim")
+    require_device(x, source, x_cat)
+    x = _f32(x)
+    if B % 2 or x.shape != (B // 2, N, 3):
+        raise RuntimeError(f"knn3_finish_cfg_ddim: x {tuple(x.shape)} != {(B // 2, N, 3)}")
+    if source is not None and source.shape != x.shape:
+        raise RuntimeError("knn3_finish_cfg_ddim: source shape != x shape")
+    if x_cat is not None and x_cat.shape != (B, N, 3):
+        raise RuntimeError("knn3_finish_cfg_ddim: x_cat shape != (2C, N, 3)")
+    if out is None:
+        out = torch.empty_like(x)
+    c1, c2, c3, c4 = (float(c) for c in coeffs)
+    _call("pcst_knn3_finish_cfg_ddim", _ptr(coarse), B, N, M, _ptr(handle[2]), _ptr(x),
+          _ptr(source), float(guidance_scale), c1, c2, c3, c4, _ptr(out), _ptr(x_cat), _stream())
     return out
 
 
@@ -885,6 +938,7 @@ def voxel_downsample_copies_dseed(points, target, seed_dev, copies):
 # every public wrapper launches on its tensors' device (see _on_tensor_device)
 _GUARDED = ("square_distance", "index_points", "fps", "ball_query", "group_gather",
             "voxel_downsample", "voxel_stats", "knn3_build", "knn3_query", "knn3_interp",
+            "knn3_search", "knn3_finish", "knn3_finish_cfg_ddim",
             "noise_cond", "noise_mlp", "cfg_ddim_step", "pointwise_linear", "relu_bwd",
             "linear_wgrad", "gemm_nt_bf16", "channel_stats", "affine_act", "chamfer_fwd",
             "chamfer_bwd", "l1_fwd", "l1_bwd", "knn_dist", "emd_greedy", "voxel_center_dist",

@@ -65,6 +65,23 @@ __device__ __forceinline__ float fsub(float a, float b) { return __fsub_rn(a, b)
 __device__ __forceinline__ float ffma(float a, float b, float c) { return __fmaf_rn(a, b, c); }
 __device__ __forceinline__ double dmul(double a, double b) { return __dmul_rn(a, b); }
 __device__ __forceinline__ double dadd(double a, double b) { return __dadd_rn(a, b); }
+
+// One element of the fused CFG + DDIM update (sampler.hip: diffusion_model.py:248-260):
+//   eps = eps_u + s*(eps_c - eps_u) (eps_u given), x0 = (x - c1*eps)/c2, x0 += 0.1*(src - x0)
+//   (src given), x0 = tanh(x0/1.8)*1.8, x' = c3*x0 + c4*eps.  Shared by cfg_ddim_kernel and the
+//   fused kNN finish (knn.hip), so both give the same bits.
+__device__ __forceinline__ float cfg_ddim_value(float x, float eps, const float* eps_u,
+                                                const float* src, float scale, float c1, float c2,
+                                                float c3, float c4) {
+  if (eps_u) {
+    const float u = *eps_u;
+    eps = __fadd_rn(u, __fmul_rn(scale, __fsub_rn(eps, u)));
+  }
+  float x0 = __fdiv_rn(__fsub_rn(x, __fmul_rn(c1, eps)), c2);
+  if (src) x0 = __fadd_rn(x0, __fmul_rn(0.1f, __fsub_rn(*src, x0)));
+  x0 = __fmul_rn(tanhf(__fdiv_rn(x0, 1.8f)), 1.8f);
+  return __fadd_rn(__fmul_rn(c3, x0), __fmul_rn(c4, eps));
+}
 __device__ __forceinline__ double dsub(double a, double b) { return __dsub_rn(a, b); }
 
 // Unfused squared norm ((x^2 + y^2) + z^2)   (SURVEY Q2).

@@ -66,6 +66,14 @@ __device__ unsigned long long g_knn_trace[2 * 32768 * 8];
 __device__ unsigned long long g_knn_otrace[2 * 4096 * 4];
 #endif
 
+// A query row's IDW weights and ref indices (kk of them used), written by the deferred search
+// and applied to the coarse values by the finish pass (pcst_knn3_search / pcst_knn3_finish).
+struct NbrRec {
+  double u0, u1, u2;
+  int j0, j1;
+  int j2, kk;
+};
+
 struct KnnWS {
   StatRec* stats;    // [B][kStatBlocks]
   float* gp;         // [B][8]: origin xyz, cell size, inv size, dims xyz (int bits)
@@ -75,6 +83,7 @@ struct KnnWS {
   uint2* chunks;     // [B][maxch] query ranges [q0, q1) of <= 64 queries inside one brick
   int32_t* olist;    // [B][N]   outlier query rows
   float* obound;     // [B][N]   their kk-th best squared distance so far (rounded up; inf: none)
+  NbrRec* nbr;       // [B][N]   a query row's IDW weights (the deferred search: pcst_knn3_search)
   // zeroed every call (contiguous):
   int32_t* err;
   int32_t* nchunk;   // [B]
@@ -105,6 +114,7 @@ static KnnWS carve_knn(void* base, int64_t B, int64_t N, int64_t M) {
   w.chunks = c.take<uint2>(B * w.maxch);
   w.olist = c.take<int32_t>(B * N);
   w.obound = c.take<float>(B * N);
+  w.nbr = c.take<NbrRec>(B * N);
   w.err = c.take<int32_t>(4);
   w.nchunk = c.take<int32_t>(B);
   w.ocount = c.take<int32_t>(B);
@@ -452,25 +462,52 @@ struct Top3 {
   }
 };
 
-// IDW of the reference (float64, sequential sums), rounded to float32
-__device__ __forceinline__ void idw_write(const Top3& t, int kk, const float* __restrict__ V,
-                                          float* __restrict__ O) {
+// IDW of the reference (float64, sequential sums), rounded to float32, in two halves: the
+// weights (positions only) and their application to the coarse values
+__device__ __forceinline__ NbrRec idw_weights(const Top3& t, int kk) {
   const double w0 = __ddiv_rn(1.0, dadd(__dsqrt_rn(t.d0), 1e-8));
   const double w1 = kk > 1 ? __ddiv_rn(1.0, dadd(__dsqrt_rn(t.d1), 1e-8)) : 0.0;
   const double w2 = kk > 2 ? __ddiv_rn(1.0, dadd(__dsqrt_rn(t.d2), 1e-8)) : 0.0;
   double wsum = w0;
   if (kk > 1) wsum = dadd(wsum, w1);
   if (kk > 2) wsum = dadd(wsum, w2);
-  const double u0 = __ddiv_rn(w0, wsum), u1 = __ddiv_rn(w1, wsum), u2 = __ddiv_rn(w2, wsum);
-  const float* v0 = V + (int64_t)t.j0 * 3;
-  const float* v1 = V + (int64_t)(kk > 1 ? t.j1 : t.j0) * 3;
-  const float* v2 = V + (int64_t)(kk > 2 ? t.j2 : t.j0) * 3;
+  NbrRec r;
+  r.u0 = __ddiv_rn(w0, wsum);
+  r.u1 = __ddiv_rn(w1, wsum);
+  r.u2 = __ddiv_rn(w2, wsum);
+  r.j0 = t.j0;
+  r.j1 = kk > 1 ? t.j1 : t.j0;
+  r.j2 = kk > 2 ? t.j2 : t.j0;
+  r.kk = kk;
+  return r;
+}
+__device__ __forceinline__ void idw_apply(const NbrRec& r, const float* __restrict__ V, float (&o)[3]) {
+  const float* v0 = V + (int64_t)r.j0 * 3;
+  const float* v1 = V + (int64_t)r.j1 * 3;
+  const float* v2 = V + (int64_t)r.j2 * 3;
 #pragma unroll
   for (int c = 0; c < 3; ++c) {
-    double acc = dmul((double)v0[c], u0);
-    if (kk > 1) acc = dadd(acc, dmul((double)v1[c], u1));
-    if (kk > 2) acc = dadd(acc, dmul((double)v2[c], u2));
-    O[c] = (float)acc;
+    double acc = dmul((double)v0[c], r.u0);
+    if (r.kk > 1) acc = dadd(acc, dmul((double)v1[c], r.u1));
+    if (r.kk > 2) acc = dadd(acc, dmul((double)v2[c], r.u2));
+    o[c] = (float)acc;
+  }
+}
+__device__ __forceinline__ void idw_write(const Top3& t, int kk, const float* __restrict__ V,
+                                          float* __restrict__ O) {
+  float o[3];
+  idw_apply(idw_weights(t, kk), V, o);
+  O[0] = o[0]; O[1] = o[1]; O[2] = o[2];
+}
+
+// the row's result: the IDW now (vals given) or its top-3 for the finish pass (deferred search)
+__device__ __forceinline__ void row_write(const Top3& t, int kk, const float* __restrict__ V,
+                                          float* __restrict__ out, NbrRec* __restrict__ nbr,
+                                          int64_t row) {
+  if (nbr) {
+    nbr[row] = idw_weights(t, kk);
+  } else {
+    idw_write(t, kk, V, out + row * 3);
   }
 }
 
@@ -768,14 +805,16 @@ __device__ __forceinline__ bool settled(const Query& me, const Box& cells, const
 // amdgpu_waves_per_eu(4): 128 VGPRs (4 spilled) instead of 138, so 4 waves per SIMD (the LDS
 // allows 4 work-groups per CU) instead of 3: the ~5000 chunks of a step run in fewer rounds
 // (driver window 2379-2398 -> 2400-2429 steps/s, A/B on one box).
-template <int kk>  // min(M, 3), a compile-time constant so the top-3 stays in registers
+// DEFER: the deferred search (positions only): the rows' IDW weights into nbr instead of the IDW
+// of vals into out.
+template <int kk, bool DEFER>  // kk = min(M, 3), a compile-time constant so the top-3 stays in registers
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) void knn_query_kernel(
     const float* __restrict__ orig, const float* __restrict__ vals, int64_t N, int64_t M,
     int64_t Cpad, const float* __restrict__ gp, const uint64_t* __restrict__ start,
     const float4* __restrict__ refs, const int32_t* __restrict__ qorder,
     const uint2* __restrict__ chunks, int64_t maxch, const int32_t* __restrict__ nchunk,
     int32_t* __restrict__ olist, float* __restrict__ obound, int32_t* __restrict__ ocount,
-    float* __restrict__ out) {
+    float* __restrict__ out, NbrRec* __restrict__ nbr) {
   __shared__ __attribute__((aligned(16))) float cand[4][4][kCandCap];
   const int b = blockIdx.y;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -783,7 +822,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
   g.load(gp + b * 8);
   const uint64_t* S = start + b * Cpad;
   const float4* R = refs + b * M;
-  const float* V = vals + b * M * 3;
+  const float* V = DEFER ? nullptr : vals + b * M * 3;
   const Win W = {cand[wv][0], cand[wv][1], cand[wv][2], reinterpret_cast<int*>(cand[wv][3])};
   const Box none = {1, 0, 1, 0, 1, 0};
   const int nch = nchunk[b];
@@ -873,7 +912,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
         obound[o] = dk == INFINITY ? INFINITY : (float)(dk * (1.0 + 1e-6)) * 1.000001f;
       }
     }
-    if (valid && !open) idw_write(me.t, kk, V, out + (b * N + n) * 3);
+    if (valid && !open) row_write(me.t, kk, V, out, DEFER ? nbr : nullptr, b * N + n);
 #ifdef KNN_TRACE
     const unsigned long long kt3 = clock64();
     if (lane == 0 && item < 32768) {
@@ -1122,11 +1161,13 @@ __global__ __launch_bounds__(256) void knn_outlier_brick_kernel(
     const float* __restrict__ gp, int64_t Cpad, const uint64_t* __restrict__ start,
     const float4* __restrict__ refs, const int32_t* __restrict__ olist,
     const float* __restrict__ obound, const int32_t* __restrict__ ocount,
-    const uint32_t* __restrict__ known, float* __restrict__ out) {
+    const uint32_t* __restrict__ known, float* __restrict__ out, NbrRec* __restrict__ nbr) {
   const int b = blockIdx.y;
   // rows that are coarse points take the coarse value (result[idx] = coarse; the last coarse
-  // row writing a point wins, as in the reference's index assignment)
-  for (int64_t n = (int64_t)blockIdx.x * 256 + threadIdx.x; n < N; n += (int64_t)gridDim.x * 256) {
+  // row writing a point wins, as in the reference's index assignment); the deferred search
+  // leaves them to the finish pass
+  for (int64_t n = (int64_t)blockIdx.x * 256 + threadIdx.x; !nbr && n < N;
+       n += (int64_t)gridDim.x * 256) {
     const uint32_t kn = known[b * N + n];
     if (kn) {
       const float* v = vals + (b * M + (int64_t)(kn - 1)) * 3;
@@ -1140,7 +1181,7 @@ __global__ __launch_bounds__(256) void knn_outlier_brick_kernel(
   const int nbx = g.bx, nby = g.by, nbz = (g.d[2] + 3) >> 2;
   const uint64_t* S = start + b * Cpad;
   const float4* R = refs + b * M;
-  const float* V = vals + b * M * 3;
+  const float* V = vals ? vals + b * M * 3 : nullptr;
   const int cnt = ocount[b];
   const double bs = 4.0 * (double)g.s;  // brick edge
   for (int q = blockIdx.x * 4 + wv; q < cnt; q += gridDim.x * 4) {
@@ -1220,7 +1261,7 @@ __global__ __launch_bounds__(256) void knn_outlier_brick_kernel(
         r += 1;  // sparse shells are cheap; a doubled box can reach into the dense core unpruned
       }
     }
-    if (lane == 0) idw_write(me.t, kk, V, out + (b * N + n) * 3);
+    if (lane == 0) row_write(me.t, kk, V, out, nbr, b * N + n);
 #ifdef KNN_TRACE
     if (lane == 0 && b < 2 && q < 4096) {
       unsigned long long* tr = g_knn_otrace + ((int64_t)b * 4096 + q) * 4;
@@ -1230,6 +1271,63 @@ __global__ __launch_bounds__(256) void knn_outlier_brick_kernel(
       tr[3] = ostaged;
     }
 #endif
+  }
+}
+
+// Finish pass of the deferred search: row n of cloud b takes the coarse value of the last coarse
+// row that is the point itself (known), else the IDW of its neighbour record.
+__device__ __forceinline__ void finish_row(const float* __restrict__ vals, int64_t N, int64_t M,
+                                           const uint32_t* __restrict__ known,
+                                           const NbrRec* __restrict__ nbr, int64_t b, int64_t n,
+                                           float (&o)[3]) {
+  const uint32_t kn = known[b * N + n];
+  const float* V = vals + b * M * 3;
+  if (kn) {
+    const float* v = V + (int64_t)(kn - 1) * 3;
+    o[0] = v[0]; o[1] = v[1]; o[2] = v[2];
+  } else {
+    idw_apply(nbr[b * N + n], V, o);
+  }
+}
+
+__global__ __launch_bounds__(256) void knn_finish_kernel(const float* __restrict__ vals, int64_t B,
+                                                         int64_t N, int64_t M,
+                                                         const uint32_t* __restrict__ known,
+                                                         const NbrRec* __restrict__ nbr,
+                                                         float* __restrict__ out) {
+  for (int64_t r = blockIdx.x * 256ll + threadIdx.x; r < B * N; r += (int64_t)gridDim.x * 256) {
+    float o[3];
+    finish_row(vals, N, M, known, nbr, r / N, r % N, o);
+    out[r * 3 + 0] = o[0]; out[r * 3 + 1] = o[1]; out[r * 3 + 2] = o[2];
+  }
+}
+
+// The finish pass fused with the CFG + DDIM update (sampler.hip) over a CFG batch of 2C clouds:
+// eps_c is row n of cloud c, eps_u the same row of cloud C + c; x, src, x_out are [C, N, 3] and
+// x_cat [2C, N, 3] takes the new x twice.  Same operations as knn_finish_kernel followed by
+// cfg_ddim_kernel.
+__global__ __launch_bounds__(256) void knn_finish_cfg_ddim_kernel(
+    const float* __restrict__ vals, int64_t C, int64_t N, int64_t M,
+    const uint32_t* __restrict__ known, const NbrRec* __restrict__ nbr, const float* __restrict__ x,
+    const float* __restrict__ src, float scale, float c1, float c2, float c3, float c4,
+    float* __restrict__ x_out, float* __restrict__ x_cat) {
+  const int64_t rows = C * N;
+  for (int64_t r = blockIdx.x * 256ll + threadIdx.x; r < rows; r += (int64_t)gridDim.x * 256) {
+    const int64_t c = r / N, n = r % N;
+    float ec[3], eu[3];
+    finish_row(vals, N, M, known, nbr, c, n, ec);
+    finish_row(vals, N, M, known, nbr, C + c, n, eu);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      const int64_t e = r * 3 + k;
+      const float xn = cfg_ddim_value(x[e], ec[k], &eu[k], src ? src + e : nullptr, scale, c1, c2,
+                                      c3, c4);
+      x_out[e] = xn;
+      if (x_cat) {
+        x_cat[e] = xn;
+        x_cat[rows * 3 + e] = xn;
+      }
+    }
   }
 }
 
@@ -1309,22 +1407,21 @@ extern "C" int pcst_knn3_build(const float* orig, const int64_t* idx, int64_t B,
 #define PCST_X_KNN_OUTLIER_EXHAUSTIVE 0
 #endif
 
-extern "C" int pcst_knn3_query(const float* coarse, const float* orig, int64_t B, int64_t N,
-                               int64_t M, float* out, void* workspace, void* stream) {
-  PCST_CHECK_ARG(B >= 0 && N > 0 && M > 0 && N < (1ll << 31) && M < (1ll << 27) &&
-                     M + N < (1ll << 31),
-                 "knn3_query: bad shape");
-  if (B == 0) return PCST_OK;
-  PCST_CHECK_ARG(coarse && orig && out && workspace, "knn3_query: null pointer");
-  hipStream_t s = as_stream(stream);
-  KnnWS w = carve_knn(workspace, B, N, M);
+// The query and outlier launches: vals/out given -> IDW written to out; nbr given (deferred
+// search, positions only) -> every query row's weights into the workspace's neighbour records.
+static void launch_knn_query(const KnnWS& w, const float* coarse, const float* orig, int64_t B,
+                             int64_t N, int64_t M, float* out, NbrRec* nbr, hipStream_t s) {
   const int b = (int)B;
   // fixed grids stride over the chunk and outlier lists (their lengths live on the device)
   const unsigned gq = (unsigned)std::min<int64_t>(cdiv(w.maxch, 4), kQueryBlocks);
-  auto qk = M >= 3 ? knn_query_kernel<3> : (M == 2 ? knn_query_kernel<2> : knn_query_kernel<1>);
+  auto qk = nbr ? (M >= 3 ? knn_query_kernel<3, true>
+                          : (M == 2 ? knn_query_kernel<2, true> : knn_query_kernel<1, true>))
+                : (M >= 3 ? knn_query_kernel<3, false>
+                          : (M == 2 ? knn_query_kernel<2, false> : knn_query_kernel<1, false>));
   hipLaunchKernelGGL(qk, dim3(gq, b), dim3(256), 0, s, orig, coarse, N, M, w.Cpad, w.gp, w.cnt,
-                     w.refs, w.qorder, w.chunks, w.maxch, w.nchunk, w.olist, w.obound, w.ocount, out);
-  if (PCST_X_KNN_OUTLIER_EXHAUSTIVE) {  // the exhaustive pass (A/B experiments)
+                     w.refs, w.qorder, w.chunks, w.maxch, w.nchunk, w.olist, w.obound, w.ocount, out,
+                     nbr);
+  if (PCST_X_KNN_OUTLIER_EXHAUSTIVE && !nbr) {  // the exhaustive pass (A/B experiments)
     auto ok = M >= 3 ? knn_outlier_kernel<3>
                      : (M == 2 ? knn_outlier_kernel<2> : knn_outlier_kernel<1>);
     hipLaunchKernelGGL(ok, dim3(kOutlierBlocks, b), dim3(kOutlierThreads), 0, s, coarse, N, M, orig,
@@ -1333,9 +1430,66 @@ extern "C" int pcst_knn3_query(const float* coarse, const float* orig, int64_t B
     auto ok = M >= 3 ? knn_outlier_brick_kernel<3>
                      : (M == 2 ? knn_outlier_brick_kernel<2> : knn_outlier_brick_kernel<1>);
     hipLaunchKernelGGL(ok, dim3(kOutlierBrickBlocks, b), dim3(256), 0, s, coarse, N, M, orig, w.gp,
-                       w.Cpad, w.cnt, w.refs, w.olist, w.obound, w.ocount, w.known, out);
+                       w.Cpad, w.cnt, w.refs, w.olist, w.obound, w.ocount, w.known, out, nbr);
   }
+}
+
+#define PCST_KNN_SHAPE_CHECK(name)                                                      \
+  PCST_CHECK_ARG(B >= 0 && N > 0 && M > 0 && N < (1ll << 31) && M < (1ll << 27) &&      \
+                     M + N < (1ll << 31),                                               \
+                 name ": bad shape")
+
+extern "C" int pcst_knn3_query(const float* coarse, const float* orig, int64_t B, int64_t N,
+                               int64_t M, float* out, void* workspace, void* stream) {
+  PCST_KNN_SHAPE_CHECK("knn3_query");
+  if (B == 0) return PCST_OK;
+  PCST_CHECK_ARG(coarse && orig && out && workspace, "knn3_query: null pointer");
+  KnnWS w = carve_knn(workspace, B, N, M);
+  launch_knn_query(w, coarse, orig, B, N, M, out, nullptr, as_stream(stream));
   PCST_LAUNCH_CHECK("knn3_query");
+  return PCST_OK;
+}
+
+extern "C" int pcst_knn3_search(const float* orig, int64_t B, int64_t N, int64_t M,
+                                void* workspace, void* stream) {
+  PCST_KNN_SHAPE_CHECK("knn3_search");
+  if (B == 0) return PCST_OK;
+  PCST_CHECK_ARG(orig && workspace, "knn3_search: null pointer");
+  KnnWS w = carve_knn(workspace, B, N, M);
+  launch_knn_query(w, nullptr, orig, B, N, M, nullptr, w.nbr, as_stream(stream));
+  PCST_LAUNCH_CHECK("knn3_search");
+  return PCST_OK;
+}
+
+extern "C" int pcst_knn3_finish(const float* coarse, int64_t B, int64_t N, int64_t M, float* out,
+                                void* workspace, void* stream) {
+  PCST_KNN_SHAPE_CHECK("knn3_finish");
+  if (B == 0) return PCST_OK;
+  PCST_CHECK_ARG(coarse && out && workspace, "knn3_finish: null pointer");
+  KnnWS w = carve_knn(workspace, B, N, M);
+  const unsigned g = (unsigned)std::min<int64_t>(cdiv(B * N, 256), 4096);
+  hipLaunchKernelGGL(knn_finish_kernel, dim3(g), dim3(256), 0, as_stream(stream), coarse, B, N, M,
+                     w.known, w.nbr, out);
+  PCST_LAUNCH_CHECK("knn3_finish");
+  return PCST_OK;
+}
+
+extern "C" int pcst_knn3_finish_cfg_ddim(const float* coarse, int64_t B, int64_t N, int64_t M,
+                                         void* workspace, const float* x, const float* source,
+                                         float guidance_scale, float sqrt_1m_at, float sqrt_at_eps,
+                                         float sqrt_aprev, float sqrt_1m_aprev, float* x_out,
+                                         float* x_cat, void* stream) {
+  PCST_KNN_SHAPE_CHECK("knn3_finish_cfg_ddim");
+  PCST_CHECK_ARG(B % 2 == 0, "knn3_finish_cfg_ddim: B must be the CFG batch (2 x clouds)");
+  if (B == 0) return PCST_OK;
+  PCST_CHECK_ARG(coarse && workspace && x && x_out, "knn3_finish_cfg_ddim: null pointer");
+  KnnWS w = carve_knn(workspace, B, N, M);
+  const int64_t C = B / 2;
+  const unsigned g = (unsigned)std::min<int64_t>(cdiv(C * N, 256), 4096);
+  hipLaunchKernelGGL(knn_finish_cfg_ddim_kernel, dim3(g), dim3(256), 0, as_stream(stream), coarse,
+                     C, N, M, w.known, w.nbr, x, source, guidance_scale, sqrt_1m_at, sqrt_at_eps,
+                     sqrt_aprev, sqrt_1m_aprev, x_out, x_cat);
+  PCST_LAUNCH_CHECK("knn3_finish_cfg_ddim");
   return PCST_OK;
 }
 

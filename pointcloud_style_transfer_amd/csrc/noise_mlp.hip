@@ -48,6 +48,9 @@ constexpr int kCondSlots = 4;
 #ifndef PCST_NM_EPI_GROUP  // pair16 residual loop: the W2 fragment group after which the next
 #define PCST_NM_EPI_GROUP 3    // hidden chunk's epilogue + hand-off run (0..3; 3 measured best)
 #endif
+#ifndef PCST_NM_EARLY  // pair16: issue weight parts 0 and 1 before the prologue loads (0: after)
+#define PCST_NM_EARLY 1
+#endif
 #ifndef PCST_NM_RD  // pair16 kernel: fragment groups read ahead of their MFMAs
 #define PCST_NM_RD 1
 #endif
@@ -554,6 +557,12 @@ struct Streamer2 {
     __syncthreads();
     issue(1);
   }
+  // both slots are free at kernel start: parts 0 and 1 in flight before the caller's own
+  // prologue loads; the caller's next __syncthreads (vmcnt 0 first) then has both landed
+  __device__ void begin_early() {
+    issue(0);
+    issue(1);
+  }
   __device__ void next() {
     if (!(PCST_NM_EXPERIMENT & 2)) __syncthreads();
     ++part;
@@ -1058,6 +1067,8 @@ __global__ __launch_bounds__(kPairThreads) void noise_mlp_pair16_kernel(
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int64_t p0 = (int64_t)blockIdx.x * 128;
   const int64_t c0 = p0 / T;
+  Streamer2 st{blob, smem, 0, nparts, wid};
+  if (PCST_NM_EARLY) st.begin_early();  // the first two weight parts under the prologue loads
   for (int i = tid; i < kBiasFloats; i += kPairThreads) sb[i] = bias[i];
   for (int i = tid; i < kCondSlots * 256; i += kPairThreads) {
     const int64_t c = c0 + i / 256;
@@ -1078,8 +1089,7 @@ __global__ __launch_bounds__(kPairThreads) void noise_mlp_pair16_kernel(
     slot[cb] = (int)(pc / T - c0);
   }
   __syncthreads();
-  Streamer2 st{blob, smem, 0, nparts, wid};
-  st.begin();
+  if (!PCST_NM_EARLY) st.begin();
   if ((wid & PX) == 0)
     pair16_wave<0>(cond, sb, sc, X, st, wid, c0, slot, px, py, pz, p, P, out);
   else

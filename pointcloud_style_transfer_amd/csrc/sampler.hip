@@ -25,15 +25,8 @@ __global__ void cfg_ddim_kernel(const float* __restrict__ x, const float* __rest
   }
   for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < n;
        e += (int64_t)gridDim.x * blockDim.x) {
-    float eps = eps_c[e];
-    if (eps_u) {
-      const float u = eps_u[e];
-      eps = fadd(u, fmul(scale, fsub(eps, u)));
-    }
-    float x0 = __fdiv_rn(fsub(x[e], fmul(c1, eps)), c2);
-    if (src) x0 = fadd(x0, fmul(0.1f, fsub(src[e], x0)));
-    x0 = fmul(tanhf(__fdiv_rn(x0, 1.8f)), 1.8f);
-    const float xn = fadd(fmul(c3, x0), fmul(c4, eps));
+    const float xn = cfg_ddim_value(x[e], eps_c[e], eps_u ? eps_u + e : nullptr,
+                                    src ? src + e : nullptr, scale, c1, c2, c3, c4);
     x_out[e] = xn;
     if (x_cat) {
       x_cat[e] = xn;

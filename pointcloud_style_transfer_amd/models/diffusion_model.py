@@ -249,9 +249,11 @@ class HierarchicalProcessor:
 # 0.493 -> 0.468 ms/step over the first 20 steps, 0.421 -> 0.408 over 300
 # (tools/overlap_probe.py, one cloud); results are bit-identical.  These module constants are
 # the design's fixed choices; tools/knobs.py overrides them for A/B runs only.
-# Only small batches leave idle CUs in the MLP's last round: with many rounds (e.g. 32 clouds per
-# GPU, 15000 MLP work-groups) the padded build only runs after the MLP, slower than inline
-# (9.6 -> 10.4 ms per 32-cloud step), so the overlap applies up to two MLP rounds of points.
+# Only small batches leave idle CUs in the MLP's last round, so the LDS floor below applies up to
+# two MLP rounds of points.  With many rounds (e.g. 32 clouds per GPU, 15000 MLP work-groups) the
+# build runs unpadded beside the MLP, taking CUs as MLP work-groups retire: 8.78 -> 8.31 ms per
+# 32-cloud step against the build inline before the MLP (8.36 with the floor: it then waits for
+# the MLP's last round; tools/b32_probe.py, one box).
 OVERLAP_KNN_BUILD = True
 _OVERLAP_MAX_MLP_POINTS = 2 * 128 * 256
 # LDS floor of the build's work-groups (pcst_knn3_build's lds_floor): just above what an MLP
@@ -266,7 +268,12 @@ KNN_BUILD_MAX_WG = 0
 
 
 def overlap_knn_build(mlp_points: int) -> bool:
-    return OVERLAP_KNN_BUILD and mlp_points <= _OVERLAP_MAX_MLP_POINTS
+    return OVERLAP_KNN_BUILD
+
+
+def knn_build_lds_floor(mlp_points: int) -> int:
+    """The side-stream build's LDS floor for an MLP launch over `mlp_points` points."""
+    return KNN_BUILD_LDS_FLOOR if mlp_points <= _OVERLAP_MAX_MLP_POINTS else 0
 _STEP_STREAMS: Dict[int, Tuple[torch.cuda.Stream, torch.cuda.Stream]] = {}
 
 
@@ -296,11 +303,48 @@ def hierarchical_eps(hp, mlp, xc, xi, x_cat, knn_ws=None, side=None):
         ready.record(main)
     ready.wait(side)
     with torch.cuda.stream(side):
-        handle = _hip.knn3_build(x_cat, xi, knn_ws, KNN_BUILD_LDS_FLOOR, KNN_BUILD_MAX_WG)
+        handle = _hip.knn3_build(x_cat, xi, knn_ws, knn_build_lds_floor(xc.shape[0] * xc.shape[1]),
+                                 KNN_BUILD_MAX_WG)
         built.record(side)
     nc = mlp(xc)
     built.wait(main)
     return _hip.knn3_query(nc, handle)
+
+
+# The query's neighbour search is positions-only too: with SEARCH_BESIDE_MLP the side stream runs
+# it after the build (pcst_knn3_search: each row's three neighbours and IDW weights), and after
+# the MLP only the gather of the coarse values remains, fused with the CFG + DDIM update
+# (pcst_knn3_finish_cfg_ddim).  Bit-identical to the query path (test_gpu_step.py).  Off: at one
+# cloud the search takes the CUs of the MLP's last round and the step is slower (0.3707 vs
+# 0.3615 ms, tools/step_probe.py srch/nosrch, one box).
+SEARCH_BESIDE_MLP = False
+
+
+def hierarchical_step(hp, mlp, xc, xi, x_cat, x, source, guidance_scale, coeffs, knn_ws=None,
+                      side=None):
+    """One guided step of the hierarchical branch (diffusion_model.py:240-260): eps of the CFG
+    batch (mlp(xc) upsampled by kNN-3), then the fused CFG + DDIM update of x (x_cat takes the
+    new x twice).  Returns the new x."""
+    C = x.shape[0]
+    if side is None or not SEARCH_BESIDE_MLP:
+        eps = hierarchical_eps(hp, mlp, xc, xi, x_cat, knn_ws, side)
+        return _hip.cfg_ddim_step(x, eps[:C], eps[C:], source, guidance_scale, coeffs, x_cat=x_cat)
+    main = torch.cuda.current_stream()
+    ready, built = _step_events(main.device)
+    if KERNEL_SIGNAL:
+        ready = _step_signal(main.device)
+        ready.signal(main)
+    else:
+        ready.record(main)
+    ready.wait(side)
+    with torch.cuda.stream(side):
+        handle = _hip.knn3_build(x_cat, xi, knn_ws, knn_build_lds_floor(xc.shape[0] * xc.shape[1]),
+                                 KNN_BUILD_MAX_WG)
+        _hip.knn3_search(handle)
+        built.record(side)
+    nc = mlp(xc)
+    built.wait(main)
+    return _hip.knn3_finish_cfg_ddim(nc, handle, x, source, guidance_scale, coeffs, x_cat=x_cat)
 
 
 _STEP_EVENTS: Dict[int, tuple] = {}
@@ -503,14 +547,15 @@ class DiffusionProcess:
                         mlp = lambda c: npred.forward_cond(c, cond_i, pk)  # noqa: E731
                     else:
                         mlp = lambda c: npred(c, t_in, style_in)  # noqa: E731
+                    coeffs = self._coeffs(t, t_prevs[i])
                     if use_hierarchical:
                         xc, xi = hp.downsample_copies(x, 2, vws)
-                        eps = hierarchical_eps(hp, mlp, xc, xi, x_cat, ws, side)
+                        x = hierarchical_step(hp, mlp, xc, xi, x_cat, x, source, guidance_scale,
+                                              coeffs, ws, side)
                     else:
                         eps = mlp(x_cat)
-                    t_prev = t_prevs[i]
-                    x = _hip.cfg_ddim_step(x, eps[:B], eps[B:], source, guidance_scale,
-                                           self._coeffs(t, t_prev), x_cat=x_cat)
+                        x = _hip.cfg_ddim_step(x, eps[:B], eps[B:], source, guidance_scale,
+                                               coeffs, x_cat=x_cat)
             finally:
                 # also when a step raises: tensors the caller frees must not be reused while
                 # loop-stream and side-stream kernels still run

@@ -325,6 +325,78 @@ def test_knn_build_query_phases_match_interp(H):
     assert torch.equal(H.knn3_query(coarse, H.knn3_build(orig, idx)), ref)
 
 
+def _search_case(kind, rng):
+    """(orig [2,N,3], idx [2,M]) for the deferred-search tests: a Gaussian cloud, one with far
+    outliers (rows the query pass sends to the outlier pass), repeated indices (known rows written
+    by several coarse rows) and the kk < 3 kernels (M = 1, 2)."""
+    N, M = {"gauss": (20000, 5000), "outliers": (30000, 7500), "repeat": (8000, 3000),
+            "m1": (500, 1), "m2": (500, 2)}[kind]
+    orig = rng.standard_normal((2, N, 3)).astype(np.float32)
+    if kind == "outliers":
+        far = rng.choice(N, 300, replace=False)
+        orig[:, far] *= 40.0
+    if kind == "repeat":
+        idx = rng.integers(0, N, (2, M))
+    else:
+        idx = np.stack([rng.choice(N, M, replace=False) for _ in range(2)])
+    return dev(orig), dev(idx.astype(np.int64))
+
+
+@pytest.mark.parametrize("kind", ["gauss", "outliers", "repeat", "m1", "m2"])
+def test_knn_search_finish_match_query(H, kind):
+    """pcst_knn3_search (positions only, on a side stream after the build) + pcst_knn3_finish give
+    the bit-identical result of pcst_knn3_query; pcst_knn3_finish_cfg_ddim gives the bits of
+    pcst_cfg_ddim_step over that eps (x_cat both halves)."""
+    rng = np.random.default_rng(len(kind))
+    orig, idx = _search_case(kind, rng)
+    M = idx.shape[1]
+    coarse = dev(rng.standard_normal((2, M, 3)).astype(np.float32))
+    ref = H.knn3_query(coarse, H.knn3_build(orig, idx))
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        handle = H.knn3_search(H.knn3_build(orig, idx))
+    torch.cuda.current_stream().wait_stream(side)
+    handle[2].record_stream(torch.cuda.current_stream())
+    assert torch.equal(H.knn3_finish(coarse, handle), ref)
+    x = orig[:1].clone() * 0.5
+    src = dev(rng.standard_normal(tuple(x.shape)).astype(np.float32))
+    coeffs = (np.float32(0.3), np.float32(0.95), np.float32(0.97), np.float32(0.24))
+    xc_ref = torch.empty_like(orig)
+    want = H.cfg_ddim_step(x, ref[:1], ref[1:], src, 7.5, coeffs, x_cat=xc_ref)
+    xc = torch.empty_like(orig)
+    got = H.knn3_finish_cfg_ddim(coarse, handle, x, src, 7.5, coeffs, x_cat=xc)
+    assert torch.equal(got, want) and torch.equal(xc, xc_ref)
+    got2 = H.knn3_finish_cfg_ddim(coarse, handle, x, None, 3.0, coeffs)
+    want2 = H.cfg_ddim_step(x, ref[:1], ref[1:], None, 3.0, coeffs)
+    assert torch.equal(got2, want2)
+
+
+def test_guided_loop_search_beside_mlp_bit_identical():
+    """The sampling loop with the kNN search on the side stream and the fused finish + CFG/DDIM
+    (SEARCH_BESIDE_MLP, the product layout) gives the bits of the build-only overlap with the
+    query after the MLP, on the bench's 120k cloud (5 steps from t = 999)."""
+    import bench
+    from pointcloud_style_transfer_amd.models import diffusion_model as dm
+    from pointcloud_style_transfer_amd.synthetic import lidar_like_cloud, standard_normal
+
+    dev0 = torch.device("cuda", 0)
+    cfg, model, dp = bench.build_model("bf16", dev0)
+    src = torch.from_numpy(lidar_like_cloud(1000, 120000)[None]).to(dev0)
+    cond = torch.from_numpy(lidar_like_cloud(2000, 120000)[None]).to(dev0)
+    xT = torch.from_numpy(standard_normal(3000, (1, 120000, 3))).to(dev0)
+    outs = []
+    saved = dm.SEARCH_BESIDE_MLP
+    try:
+        for on in (True, False):
+            dm.SEARCH_BESIDE_MLP = on
+            torch.manual_seed(7)
+            outs.append(dp.guided_sample_loop(model, src, cond, 5, 7.5, x_T=xT))
+    finally:
+        dm.SEARCH_BESIDE_MLP = saved
+    assert torch.equal(outs[0], outs[1])
+
+
 @pytest.mark.parametrize("max_wg,floor", [(1, 0), (2, 8192), (32, 8192), (7, 0)])
 def test_knn_build_workgroup_cap_is_exact(H, max_wg, floor):
     """pcst_knn3_build's max_wg only changes how many work-groups stride over the build's work

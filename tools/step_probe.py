@@ -13,6 +13,9 @@ median ms/step of each:
   evready noev with the loop -> side dependency as an event instead of the kernel-side signal
   nocap   noev with the side-stream build at its natural grids (no max_wg cap)
   capK    noev with the side-stream build capped at K work-groups per launch
+  srch    the product step (diffusion_model.hierarchical_step): build + neighbour search on the
+          side stream, the fused finish + CFG/DDIM after the MLP
+  nosrch  hierarchical_step with SEARCH_BESIDE_MLP off (build-only overlap, query after the MLP)
 A development tool (tools/ only)."""
 import argparse
 import os
@@ -77,6 +80,11 @@ def main():
                         e1.record()
                     return out
 
+                if mode in ("srch", "nosrch"):
+                    dmod.SEARCH_BESIDE_MLP = mode == "srch"
+                    x = dmod.hierarchical_step(hp, mlp, xc, xi, x_cat, x, src, 7.5, dp._coeffs(t, tp),
+                                               ws, side)
+                    continue
                 if mode.startswith("seq"):
                     h = _hip.knn3_build(x_cat, xi, ws, 0)
                     eps = _hip.knn3_query(mlp(xc), h)
