@@ -302,10 +302,12 @@ def hierarchical_eps(hp, mlp, xc, xi, x_cat, knn_ws=None, side=None):
     else:
         ready.record(main)
     ready.wait(side)
+    if BUILT_SIGNAL:
+        built = _step_signal(main.device, 1)
     with torch.cuda.stream(side):
         handle = _hip.knn3_build(x_cat, xi, knn_ws, knn_build_lds_floor(xc.shape[0] * xc.shape[1]),
                                  KNN_BUILD_MAX_WG)
-        built.record(side)
+        built.signal(side) if BUILT_SIGNAL else built.record(side)
     nc = mlp(xc)
     built.wait(main)
     return _hip.knn3_query(nc, handle)
@@ -355,11 +357,18 @@ DEVICE_EVENTS = True
 # kernel ~3 us (tools/sync_probe.hip).  The side -> loop one (the kNN build is done) stays an
 # event: waiting on an event that has already completed costs the waiting queue ~0.3 us.
 KERNEL_SIGNAL = True
-_STEP_SIGNALS: Dict[int, "_hip.DeviceSignal"] = {}
+# The side -> loop dependency (the kNN build is done) by the same kind of flag (BUILT_SIGNAL): in
+# the driver-window trace the event wait left ~10 us between the MLP's end and the query's start
+# although the build had finished ~16 us earlier (profiles/r03/s8_*); a one-workgroup wait kernel
+# that finds the flag already set costs a few us.
+BUILT_SIGNAL = True
+_STEP_SIGNALS: Dict[tuple, "_hip.DeviceSignal"] = {}
 
 
-def _step_signal(device):
-    key = torch.device(device).index or 0
+def _step_signal(device, which=0):
+    """The step's device flags: 0 loop -> side (the voxel output is ready), 1 side -> loop (the
+    kNN build is done)."""
+    key = (torch.device(device).index or 0, which)
     if key not in _STEP_SIGNALS:
         _STEP_SIGNALS[key] = _hip.DeviceSignal(device)
     return _STEP_SIGNALS[key]

@@ -16,6 +16,7 @@ median ms/step of each:
   srch    the product step (diffusion_model.hierarchical_step): build + neighbour search on the
           side stream, the fused finish + CFG/DDIM after the MLP
   nosrch  hierarchical_step with SEARCH_BESIDE_MLP off (build-only overlap, query after the MLP)
+  bev     noev with the side -> loop dependency as an event instead of the kernel-side flag
 A development tool (tools/ only)."""
 import argparse
 import os
@@ -60,6 +61,7 @@ def main():
 
         def run(mode, n):
             dmod.KERNEL_SIGNAL = mode != "evready"  # evready: the loop -> side dependency as an event
+            dmod.BUILT_SIGNAL = mode != "bev"  # bev: the side -> loop dependency as an event
             # nocap: natural build grids; capK: at most K build work-groups per launch
             dmod.KNN_BUILD_MAX_WG = (0 if mode == "nocap" else
                                      int(mode[3:]) if mode.startswith("cap") else cap0)
