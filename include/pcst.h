@@ -263,6 +263,17 @@ int pcst_noise_cond(const int64_t* t, const float* style, int64_t nclouds, const
 int pcst_noise_mlp(const float* pts, int64_t P, int64_t points_per_cloud, const float* cond,
                    int64_t nclouds, const void* blob, int64_t blob_bytes, const float* bias,
                    int precision, float* out, void* stream);
+/* pcst_noise_mlp at precision 2 whose launch completes only once *flag >= value as well: after
+ * writing its rows, the MLP's last work-group (a caller-owned uint32 counter, zero before the
+ * call and zero again after it, counts the work-groups out) polls the flag with agent-scope loads
+ * (the producer on another stream writes it with pcst_signal_write), bounded at ~10 s (then *err
+ * = 1, err may be NULL).  Work queued after it on the stream is ordered after the flag's producer
+ * without a separate wait launch. */
+int pcst_noise_mlp_then_wait(const float* pts, int64_t P, int64_t points_per_cloud,
+                             const float* cond, int64_t nclouds, const void* blob,
+                             int64_t blob_bytes, const float* bias, float* out,
+                             const uint32_t* flag, uint32_t value, uint32_t* counter, int32_t* err,
+                             void* stream);
 
 /* CFG + DDIM update of guided_sample_loop (diffusion_model.py:248-260); eps_u == NULL gives
  * ddim_sample_loop's update (:283-290), source == NULL skips the source pull.  x_cat (optional,

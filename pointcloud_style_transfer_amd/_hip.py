@@ -58,6 +58,7 @@ SIGNATURES = {
     "pcst_noise_mlp_blob_bytes": [ctypes.c_int],
     "pcst_noise_cond": [_P, _P, _I, _P, _P, _P, _P, _P, _P, _P, _P],
     "pcst_noise_mlp": [_P, _I, _I, _P, _I, _P, _I, _P, ctypes.c_int, _P, _P],
+    "pcst_noise_mlp_then_wait": [_P, _I, _I, _P, _I, _P, _I, _P, _P, _P, ctypes.c_uint32, _P, _P, _P],
     "pcst_cfg_ddim_step": [_P, _P, _P, _P, _I, _F, _F, _F, _F, _F, _P, _P, _P],
     "pcst_pointwise_linear": [_P, _I, _I, _P, _I, _P, _P, ctypes.c_int, _I, _P, _P],
     "pcst_voxel_center_dist": [_P, _I, _P, ctypes.c_float, _P, _P, _P, _P],
@@ -350,7 +351,8 @@ class DeviceSignal:
     counter of this flag (no library state)."""
 
     def __init__(self, device):
-        self.flag = torch.zeros(2, dtype=torch.int32, device=device)  # [flag, timeout error]
+        # [flag, timeout error, work-group counter of pcst_noise_mlp_then_wait, pad]
+        self.flag = torch.zeros(4, dtype=torch.int32, device=device)
         self.value = 0
 
     def signal(self, stream):
@@ -360,6 +362,12 @@ class DeviceSignal:
     def wait(self, stream):
         _call("pcst_signal_wait", _ptr(self.flag), self.value, ctypes.c_void_p(self.flag.data_ptr() + 4),
               ctypes.c_void_p(stream.cuda_stream))
+
+    def wait_args(self):
+        """(flag, value, counter, err) for pcst_noise_mlp_then_wait: wait for the last signal."""
+        base = self.flag.data_ptr()
+        return (ctypes.c_void_p(base), ctypes.c_uint32(self.value), ctypes.c_void_p(base + 8),
+                ctypes.c_void_p(base + 4))
 
     def timed_out(self) -> bool:
         return bool(int(self.flag[1].item()))
@@ -518,15 +526,24 @@ def noise_cond(t, style, freqs, wt, bt, ws_, bs, b4):
     return cond
 
 
-def noise_mlp(pts, points_per_cloud, cond, blob, bias, precision, out=None):
-    """pts [P,3] (P = clouds*points_per_cloud, cloud-major) -> eps [P,3]."""
+def noise_mlp(pts, points_per_cloud, cond, blob, bias, precision, out=None, wait=None):
+    """pts [P,3] (P = clouds*points_per_cloud, cloud-major) -> eps [P,3].
+    wait (a DeviceSignal signalled on another stream): work queued after the MLP on this stream
+    is also ordered after that signal -- at precision 2 by the MLP's last work-group
+    (pcst_noise_mlp_then_wait), otherwise by a wait launch after it."""
     require_device(pts, cond, blob, bias)
     pts = _f32(pts)
     P = pts.shape[0]
     if out is None:
         out = torch.empty(P, 3, dtype=torch.float32, device=pts.device)
+    if wait is not None and precision == 2 and P > 0:
+        _call("pcst_noise_mlp_then_wait", _ptr(pts), P, points_per_cloud, _ptr(cond), cond.shape[0],
+              _ptr(blob), blob.numel(), _ptr(bias), _ptr(out), *wait.wait_args(), _stream())
+        return out
     _call("pcst_noise_mlp", _ptr(pts), P, points_per_cloud, _ptr(cond), cond.shape[0], _ptr(blob),
           blob.numel(), _ptr(bias), precision, _ptr(out), _stream())
+    if wait is not None:
+        wait.wait(torch.cuda.current_stream(pts.device))
     return out
 
 

@@ -184,15 +184,16 @@ class NoisePredictor(nn.Module):
                     or (style_feat.requires_grad and torch.is_grad_enabled()))
 
     def forward_cond(self, noisy_points: torch.Tensor, cond: torch.Tensor,
-                     packed: Optional[tuple] = None) -> torch.Tensor:
+                     packed: Optional[tuple] = None, wait=None) -> torch.Tensor:
         """The fused inference forward with precomputed conditioning rows (`cond()` of the
         same timesteps and style features): the sampling loops compute every step's rows in one
         launch before the loop.  `packed` (this module's `packed()`, fetched once before a loop
-        that does not change the weights) skips the per-call weight-version check."""
+        that does not change the weights) skips the per-call weight-version check.  `wait` (a
+        DeviceSignal): later work on this stream also waits for it (_hip.noise_mlp)."""
         B, N, _ = noisy_points.shape
         blob, bias = (packed if packed is not None else self.packed())[:2]
         out = _hip.noise_mlp(noisy_points.reshape(B * N, 3), N, cond, blob, bias,
-                             self.precision_code)
+                             self.precision_code, wait=wait)
         return out.view(B, N, 3)
 
     def forward(self, noisy_points: torch.Tensor, timestep: torch.Tensor,
@@ -287,7 +288,7 @@ def step_streams(device) -> Tuple[torch.cuda.Stream, torch.cuda.Stream]:
     return _STEP_STREAMS[idx]
 
 
-def hierarchical_eps(hp, mlp, xc, xi, x_cat, knn_ws=None, side=None):
+def hierarchical_eps(hp, mlp, xc, xi, x_cat, knn_ws=None, side=None, mlp_waits=False):
     """eps for the CFG batch: mlp(xc) on the current stream, upsampled to the full clouds by
     kNN-3 (HierarchicalProcessor.upsample_knn).  With a side stream (and a preallocated
     workspace) the kNN build runs there, overlapping the MLP, with its work-groups held to an
@@ -308,8 +309,11 @@ def hierarchical_eps(hp, mlp, xc, xi, x_cat, knn_ws=None, side=None):
         handle = _hip.knn3_build(x_cat, xi, knn_ws, knn_build_lds_floor(xc.shape[0] * xc.shape[1]),
                                  KNN_BUILD_MAX_WG)
         built.signal(side) if BUILT_SIGNAL else built.record(side)
-    nc = mlp(xc)
-    built.wait(main)
+    if BUILT_SIGNAL and mlp_waits:  # the MLP's last work-group waits for the build's flag
+        nc = mlp(xc, built)
+    else:
+        nc = mlp(xc)
+        built.wait(main)
     return _hip.knn3_query(nc, handle)
 
 
@@ -323,13 +327,13 @@ SEARCH_BESIDE_MLP = False
 
 
 def hierarchical_step(hp, mlp, xc, xi, x_cat, x, source, guidance_scale, coeffs, knn_ws=None,
-                      side=None):
+                      side=None, mlp_waits=False):
     """One guided step of the hierarchical branch (diffusion_model.py:240-260): eps of the CFG
     batch (mlp(xc) upsampled by kNN-3), then the fused CFG + DDIM update of x (x_cat takes the
     new x twice).  Returns the new x."""
     C = x.shape[0]
     if side is None or not SEARCH_BESIDE_MLP:
-        eps = hierarchical_eps(hp, mlp, xc, xi, x_cat, knn_ws, side)
+        eps = hierarchical_eps(hp, mlp, xc, xi, x_cat, knn_ws, side, mlp_waits)
         return _hip.cfg_ddim_step(x, eps[:C], eps[C:], source, guidance_scale, coeffs, x_cat=x_cat)
     main = torch.cuda.current_stream()
     ready, built = _step_events(main.device)
@@ -360,8 +364,10 @@ KERNEL_SIGNAL = True
 # The side -> loop dependency (the kNN build is done) by the same kind of flag (BUILT_SIGNAL): in
 # the driver-window trace the event wait left ~10 us between the MLP's end and the query's start
 # although the build had finished ~16 us earlier (profiles/r03/s8_*); a one-workgroup wait kernel
-# that finds the flag already set costs a few us.
+# that finds the flag already set costs a few us.  With the fused MLP (mlp_waits) the MLP's last
+# work-group waits for the flag itself (pcst_noise_mlp_then_wait): no wait launch at all.
 BUILT_SIGNAL = True
+MLP_WAITS = True
 _STEP_SIGNALS: Dict[tuple, "_hip.DeviceSignal"] = {}
 
 
@@ -553,14 +559,15 @@ class DiffusionProcess:
                     t_in = t_rows[i]
                     if conds is not None:
                         cond_i = conds[i]
-                        mlp = lambda c: npred.forward_cond(c, cond_i, pk)  # noqa: E731
+                        mlp = lambda c, wait=None: npred.forward_cond(c, cond_i, pk, wait)  # noqa: E731
                     else:
                         mlp = lambda c: npred(c, t_in, style_in)  # noqa: E731
                     coeffs = self._coeffs(t, t_prevs[i])
                     if use_hierarchical:
                         xc, xi = hp.downsample_copies(x, 2, vws)
                         x = hierarchical_step(hp, mlp, xc, xi, x_cat, x, source, guidance_scale,
-                                              coeffs, ws, side)
+                                              coeffs, ws, side,
+                                              mlp_waits=MLP_WAITS and conds is not None)
                     else:
                         eps = mlp(x_cat)
                         x = _hip.cfg_ddim_step(x, eps[:B], eps[B:], source, guidance_scale,

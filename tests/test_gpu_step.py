@@ -467,3 +467,68 @@ def test_device_events_order_streams(H):
     torch.tanh(a @ a)
     t1.record()
     assert t0.elapsed_time(t1) > 0.0
+
+
+def test_noise_mlp_then_wait_orders_after_the_signal(H):
+    """pcst_noise_mlp_then_wait: the MLP's rows are the bits of pcst_noise_mlp, work queued after
+    it on the stream sees what the signalling stream wrote before its pcst_signal_write (here a
+    side stream that fills a 64 MB buffer after a delay), and the work-group counter is back to 0
+    with no timeout."""
+    from pointcloud_style_transfer_amd import packing
+    from pointcloud_style_transfer_amd.config.config import Config
+    from pointcloud_style_transfer_amd.models.diffusion_model import NoisePredictor
+
+    torch.manual_seed(4)
+    cfg = Config(make_dirs=False, precision="bf16")
+    npred = NoisePredictor(cfg).cuda().eval()
+    assert npred.precision_code == packing.PAIR16
+    rng = np.random.default_rng(8)
+    pts = dev(rng.standard_normal((2 * 30000, 3)).astype(np.float32))
+    t = torch.tensor([999, 999], device="cuda")
+    style = dev(rng.standard_normal((2, 256)).astype(np.float32))
+    with torch.no_grad():
+        cond = npred.cond(t, style)
+        blob, bias = npred.packed()[:2]
+        ref = H.noise_mlp(pts, 30000, cond, blob, bias, npred.precision_code)
+        sig = H.DeviceSignal("cuda")
+        side = torch.cuda.Stream()
+        big = torch.zeros(16 << 20, device="cuda")
+        side.wait_stream(torch.cuda.current_stream())
+        for rep in range(3):
+            with torch.cuda.stream(side):
+                a = torch.randn(4096, 4096, device="cuda")
+                for _ in range(4):
+                    a = a @ a.T / 4096.0  # a delay on the side stream
+                big.fill_(float(rep + 1))
+                sig.signal(side)
+            out = H.noise_mlp(pts, 30000, cond, blob, bias, npred.precision_code, wait=sig)
+            seen = big.clone()  # ordered after the MLP, hence after the side's fill
+            torch.cuda.synchronize()
+            assert torch.equal(out, ref)
+            assert bool((seen == float(rep + 1)).all())
+            assert int(sig.flag[2].item()) == 0 and not sig.timed_out()
+
+
+def test_guided_loop_mlp_waits_bit_identical():
+    """The sampling loop with the MLP's last work-group waiting for the kNN build's flag
+    (MLP_WAITS, the product layout) gives the bits of the separate wait launch, on the bench's
+    120k cloud (5 steps from t = 999)."""
+    import bench
+    from pointcloud_style_transfer_amd.models import diffusion_model as dm
+    from pointcloud_style_transfer_amd.synthetic import lidar_like_cloud, standard_normal
+
+    dev0 = torch.device("cuda", 0)
+    cfg, model, dp = bench.build_model("bf16", dev0)
+    src = torch.from_numpy(lidar_like_cloud(1000, 120000)[None]).to(dev0)
+    cond = torch.from_numpy(lidar_like_cloud(2000, 120000)[None]).to(dev0)
+    xT = torch.from_numpy(standard_normal(3000, (1, 120000, 3))).to(dev0)
+    outs = []
+    saved = dm.MLP_WAITS
+    try:
+        for on in (True, False):
+            dm.MLP_WAITS = on
+            torch.manual_seed(7)
+            outs.append(dp.guided_sample_loop(model, src, cond, 5, 7.5, x_T=xT))
+    finally:
+        dm.MLP_WAITS = saved
+    assert torch.equal(outs[0], outs[1])

@@ -17,6 +17,7 @@ median ms/step of each:
           side stream, the fused finish + CFG/DDIM after the MLP
   nosrch  hierarchical_step with SEARCH_BESIDE_MLP off (build-only overlap, query after the MLP)
   bev     noev with the side -> loop dependency as an event instead of the kernel-side flag
+  mw      noev with the MLP's last work-group waiting for the build's flag (mlp_waits: the product)
 A development tool (tools/ only)."""
 import argparse
 import os
@@ -72,12 +73,12 @@ def main():
                 t, tp = ts[i], ts[i + 1]
                 xc, xi = hp.downsample_copies(x, 2)
 
-                def mlp(c):
+                def mlp(c, wait=None):
                     if timed:
                         e0, e1 = _hip.DeviceEvent(timing=True), _hip.DeviceEvent(timing=True)
                         e0.record()
                     out = _hip.noise_mlp(c.reshape(-1, 3), cfg.global_points, conds[i], blob, bias,
-                                         npred.precision_code).view(2, -1, 3)
+                                         npred.precision_code, wait=wait).view(2, -1, 3)
                     if timed:
                         e1.record()
                     return out
@@ -91,7 +92,7 @@ def main():
                     h = _hip.knn3_build(x_cat, xi, ws, 0)
                     eps = _hip.knn3_query(mlp(xc), h)
                 else:
-                    eps = dmod.hierarchical_eps(hp, mlp, xc, xi, x_cat, ws, side)
+                    eps = dmod.hierarchical_eps(hp, mlp, xc, xi, x_cat, ws, side, mlp_waits=mode == "mw")
                 x = _hip.cfg_ddim_step(x, eps[:1], eps[1:], src, 7.5, dp._coeffs(t, tp), x_cat=x_cat)
             return x
 
