@@ -364,10 +364,12 @@ KERNEL_SIGNAL = True
 # The side -> loop dependency (the kNN build is done) by the same kind of flag (BUILT_SIGNAL): in
 # the driver-window trace the event wait left ~10 us between the MLP's end and the query's start
 # although the build had finished ~16 us earlier (profiles/r03/s8_*); a one-workgroup wait kernel
-# that finds the flag already set costs a few us.  With the fused MLP (mlp_waits) the MLP's last
-# work-group waits for the flag itself (pcst_noise_mlp_then_wait): no wait launch at all.
+# that finds the flag already set costs a few us.  MLP_WAITS: the MLP's last work-group waits for
+# the flag itself (pcst_noise_mlp_then_wait), no wait launch at all: 0.3765 -> 0.3740 ms/step
+# (profiles/r03/s15_*), within run-to-run noise, and the MLP's launch then also holds the build's
+# tail, so its measured duration (the bench's roofline) is no longer the MLP's own.  Off.
 BUILT_SIGNAL = True
-MLP_WAITS = True
+MLP_WAITS = False
 _STEP_SIGNALS: Dict[tuple, "_hip.DeviceSignal"] = {}
 
 
