@@ -56,6 +56,11 @@ constexpr int kKnnMaxTiles = 1024;       // per-block LDS tile histogram in the 
 constexpr int kPreKnownBlocks = 64;      // known-row scatter blocks per cloud in the pre kernel
 constexpr int kCountPerBlock = 1024;     // elements per count-kernel block (4 per thread)
 constexpr int kQueryBlocks = 1024;       // query workgroups per cloud (grid-stride over chunks)
+#ifndef KNN_QUERY_TOTAL  // experiment builds may override
+#define KNN_QUERY_TOTAL (1 << 30)
+#endif
+constexpr int64_t kQueryBlocksTotal = KNN_QUERY_TOTAL;  // cap over all clouds of a launch
+constexpr int kQueryBlocksMin = 16;
 constexpr int kOutlierThreads = 1024;    // outlier-pass workgroup
 constexpr int kOutlierBlocks = 128;      // outlier workgroups per cloud (exhaustive pass)
 constexpr int kOutlierBrickBlocks = 256; // outlier workgroups per cloud (brick search, 4 queries)
@@ -1413,7 +1418,8 @@ static void launch_knn_query(const KnnWS& w, const float* coarse, const float* o
                              int64_t N, int64_t M, float* out, NbrRec* nbr, hipStream_t s) {
   const int b = (int)B;
   // fixed grids stride over the chunk and outlier lists (their lengths live on the device)
-  const unsigned gq = (unsigned)std::min<int64_t>(cdiv(w.maxch, 4), kQueryBlocks);
+  const unsigned gq = (unsigned)std::min<int64_t>(
+      cdiv(w.maxch, 4), std::max<int64_t>(kQueryBlocksMin, std::min<int64_t>(kQueryBlocks, kQueryBlocksTotal / B)));
   auto qk = nbr ? (M >= 3 ? knn_query_kernel<3, true>
                           : (M == 2 ? knn_query_kernel<2, true> : knn_query_kernel<1, true>))
                 : (M >= 3 ? knn_query_kernel<3, false>
