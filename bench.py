@@ -343,9 +343,10 @@ def main():
         # the product loop's stream layout (DiffusionProcess.guided_sample_loop): the step on a
         # high-priority stream, the kNN build on a side stream during the noise MLP
         overlap = dmod.overlap_knn_build(2 * C * cfg.global_points)
-        loop_stream, side = dmod.step_streams(device) if overlap else (None, None)
+        state = dmod.StepState(device) if overlap else None
+        loop_stream = state.loop if overlap else None
         if overlap:
-            loop_stream.wait_stream(torch.cuda.current_stream())
+            state.begin(torch.cuda.current_stream())
             with torch.cuda.stream(loop_stream):
                 knn_ws = _hip.knn_workspace(2 * C, args.points, cfg.global_points, device=device)
         else:
@@ -383,7 +384,7 @@ def main():
                 return nc_
 
             x = dmod.hierarchical_step(hp, mlp, xc, xi, x_cat, x, src, 7.5, dp._coeffs(t, t_prev),
-                                       knn_ws, side, mlp_waits=dmod.MLP_WAITS)
+                                       knn_ws, state, mlp_waits=dmod.MLP_WAITS)
 
         lctx = torch.cuda.stream(loop_stream) if overlap else contextlib.nullcontext()
         with lctx:
@@ -405,6 +406,8 @@ def main():
                 step(i, True)
         torch.cuda.synchronize()
         elapsed = time.perf_counter() - t0
+        if overlap:
+            state.check()  # a timed-out cross-stream wait invalidates the run: raise
         if world > 1:
             dist.barrier()
             elapsed = max_over_ranks(elapsed, device=device)
@@ -438,6 +441,8 @@ def main():
             finally:
                 cfg.precision = prec0
                 pk = npred.packed()
+            if overlap:
+                state.check()
 
     mlp_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
     flop = FLOP_PER_POINT * 2 * C * cfg.global_points

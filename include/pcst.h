@@ -118,6 +118,14 @@ int pcst_group_gather_bwd_workspace_size(int64_t B, int64_t E, size_t* bytes);
 int pcst_group_gather_bwd(const float* dgrouped, const int64_t* group_idx, int64_t B, int64_t S,
                           int64_t ns, int64_t N, int64_t C, float* dpoints, void* workspace,
                           void* stream);
+/* Per-cloud column sums of a 16-bit matrix G [B*N, C] (f16 = 1: float16, 0: bfloat16 storage):
+ * out [B, C] float32 = 16-bit-rounded float sum over cloud b's N rows -- autograd's reduction of
+ * the broadcast time / style rows of x = (pf + tf) + sf under autocast (diffusion_model.py:56-58,
+ * trainer.py:78-106 backward).  Deterministic (row slices combined in slice order); C % 8 == 0,
+ * G 16-byte aligned.  workspace: pcst_group_colsum16_workspace_size() bytes. */
+int pcst_group_colsum16_workspace_size(int64_t B, int64_t C, size_t* bytes);
+int pcst_group_colsum16(const uint16_t* G, int f16, int64_t B, int64_t N, int64_t C, float* out,
+                        void* workspace, void* stream);
 
 /* Weight / bias gradient of a per-point linear layer for the training path (autograd of
  * nn.Linear / Conv2d-1x1, trainer.py:106 backward): dW [O,I] = dZ^T X, db [O] = column sums of
@@ -266,14 +274,15 @@ int pcst_noise_mlp(const float* pts, int64_t P, int64_t points_per_cloud, const 
 /* pcst_noise_mlp at precision 2 whose launch completes only once *flag >= value as well: after
  * writing its rows, the MLP's last work-group (a caller-owned uint32 counter, zero before the
  * call and zero again after it, counts the work-groups out) polls the flag with agent-scope loads
- * (the producer on another stream writes it with pcst_signal_write), bounded at ~10 s (then *err
- * = 1, err may be NULL).  Work queued after it on the stream is ordered after the flag's producer
+ * (the producer on another stream writes it with pcst_signal_write), at most max_polls times
+ * (<= 0: the default, ~10 s; then *err = 1 and the launch completes anyway: the caller must read
+ * *err, err may be NULL).  Work queued after it on the stream is ordered after the flag's producer
  * without a separate wait launch. */
 int pcst_noise_mlp_then_wait(const float* pts, int64_t P, int64_t points_per_cloud,
                              const float* cond, int64_t nclouds, const void* blob,
                              int64_t blob_bytes, const float* bias, float* out,
                              const uint32_t* flag, uint32_t value, uint32_t* counter, int32_t* err,
-                             void* stream);
+                             int64_t max_polls, void* stream);
 
 /* CFG + DDIM update of guided_sample_loop (diffusion_model.py:248-260); eps_u == NULL gives
  * ddim_sample_loop's update (:283-290), source == NULL skips the source pull.  x_cat (optional,
@@ -360,11 +369,20 @@ int pcst_event_elapsed_ms(void* start, void* end, float* ms);
  * one-workgroup kernel that polls *flag until it is >= value (agent-scope acquire), so the
  * work enqueued after it on ITS stream starts after the signal.  A cross-stream dependency
  * without an event marker on the producer's queue (an event that another queue waits on costs
- * that queue ~17 us; this ~3 us, tools/sync_probe.hip).  The wait gives up after ~10 s of
- * polling and then sets *err = 1 (err may be NULL).  Values must grow monotonically per flag.
- * flag: one uint32 of device memory, zero-initialised by the caller. */
+ * that queue ~17 us; this ~3 us, tools/sync_probe.hip).  The wait gives up after max_polls polls
+ * (<= 0: the default, ~10 s) and then sets *err = 1 (err may be NULL) and lets its stream go on:
+ * the caller must read *err after the stream's work (the Python host raises, _hip.DeviceSignal).
+ * Values must grow monotonically per flag.  flag: one uint32 of device memory, zero-initialised
+ * by the caller. */
 int pcst_signal_write(uint32_t* flag, uint32_t value, void* stream);
-int pcst_signal_wait(const uint32_t* flag, uint32_t value, int32_t* err, void* stream);
+int pcst_signal_wait(const uint32_t* flag, uint32_t value, int32_t* err, int64_t max_polls,
+                     void* stream);
+
+/* Caller-owned streams for the sampling loop (one pair per loop invocation / host thread, so two
+ * loops on one device never share a queue).  priority < 0: the device's greatest priority, else
+ * its default; non-blocking w.r.t. the null stream.  Plain HIP, no kernel. */
+int pcst_stream_create(int priority, void** stream);
+int pcst_stream_destroy(void* stream);
 
 #ifdef __cplusplus
 }

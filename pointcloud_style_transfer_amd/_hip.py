@@ -58,7 +58,8 @@ SIGNATURES = {
     "pcst_noise_mlp_blob_bytes": [ctypes.c_int],
     "pcst_noise_cond": [_P, _P, _I, _P, _P, _P, _P, _P, _P, _P, _P],
     "pcst_noise_mlp": [_P, _I, _I, _P, _I, _P, _I, _P, ctypes.c_int, _P, _P],
-    "pcst_noise_mlp_then_wait": [_P, _I, _I, _P, _I, _P, _I, _P, _P, _P, ctypes.c_uint32, _P, _P, _P],
+    "pcst_noise_mlp_then_wait": [_P, _I, _I, _P, _I, _P, _I, _P, _P, _P, ctypes.c_uint32, _P, _P, _I,
+                                 _P],
     "pcst_cfg_ddim_step": [_P, _P, _P, _P, _I, _F, _F, _F, _F, _F, _P, _P, _P],
     "pcst_pointwise_linear": [_P, _I, _I, _P, _I, _P, _P, ctypes.c_int, _I, _P, _P],
     "pcst_voxel_center_dist": [_P, _I, _P, ctypes.c_float, _P, _P, _P, _P],
@@ -89,6 +90,8 @@ SIGNATURES = {
     "pcst_bn_relu_bwd": [_P, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _I, _P, _P, _P, _P, _P],
     "pcst_group_gather_bwd_workspace_size": [_I, _I, _SZ],
     "pcst_group_gather_bwd": [_P, _P, _I, _I, _I, _I, _I, _P, _P, _P],
+    "pcst_group_colsum16_workspace_size": [_I, _I, _SZ],
+    "pcst_group_colsum16": [_P, ctypes.c_int, _I, _I, _I, _P, _P, _P],
     "pcst_l1_workspace_size": [_SZ],
     "pcst_l1_fwd": [_P, _P, _I, _P, _P, _P],
     "pcst_l1_bwd": [_P, _P, _I, _P, _P, _P],
@@ -97,7 +100,9 @@ SIGNATURES = {
     "pcst_event_record": [_P, _P],
     "pcst_stream_wait_event": [_P, _P],
     "pcst_signal_write": [_P, ctypes.c_uint32, _P],
-    "pcst_signal_wait": [_P, ctypes.c_uint32, _P, _P],
+    "pcst_signal_wait": [_P, ctypes.c_uint32, _P, _I, _P],
+    "pcst_stream_create": [ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)],
+    "pcst_stream_destroy": [_P],
     "pcst_event_elapsed_ms": [_P, _P, ctypes.POINTER(ctypes.c_float)],
 }
 _RESTYPES = {"pcst_version": ctypes.c_char_p, "pcst_last_error": ctypes.c_char_p,
@@ -342,35 +347,83 @@ def knn_workspace(B, N, M, device):
     return _workspace("pcst_knn_workspace_size", B, N, M, device=device)
 
 
+class SignalTimeout(RuntimeError):
+    """A device-side wait on a DeviceSignal gave up (the flag's producer never signalled within
+    the poll bound): the work ordered behind the wait may have read unfinished data."""
+
+
 class DeviceSignal:
     """A cross-stream dependency by kernel-side signalling (pcst_signal_write / pcst_signal_wait):
     `signal(stream)` publishes the next value of a device flag after the work enqueued so far on
     `stream`; `wait(stream)` makes `stream`'s later work wait for that value.  Unlike an event
     that another queue waits on, it puts no marker packet on the producer's queue (~3 us there
     instead of ~17 us, tools/sync_probe.hip).  Values grow monotonically; the host holds the
-    counter of this flag (no library state)."""
+    counter of this flag (no library state).
 
-    def __init__(self, device):
+    A wait that polls `max_polls` times (0: the library's default, ~10 s) without seeing its
+    value gives up, sets the flag's error word and lets its stream go on; `check()` (after the
+    waiting stream's work) raises SignalTimeout then.  Owners call it once per sampling loop.
+    `storage` (optional): an int32 device tensor of 4 elements to live in (so several signals
+    can share one allocation and one error read)."""
+
+    # the host counter is passed to the kernels as uint32: a flag retires well before it wraps
+    VALUE_LIMIT = 1 << 31
+
+    def __init__(self, device, max_polls=0, storage=None):
         # [flag, timeout error, work-group counter of pcst_noise_mlp_then_wait, pad]
-        self.flag = torch.zeros(4, dtype=torch.int32, device=device)
+        self.flag = (storage if storage is not None
+                     else torch.zeros(4, dtype=torch.int32, device=device))
+        if self.flag.dtype != torch.int32 or self.flag.numel() != 4 or not self.flag.is_contiguous():
+            raise ValueError("DeviceSignal storage must be 4 contiguous int32")
         self.value = 0
+        self.max_polls = int(max_polls)
 
     def signal(self, stream):
+        if self.value + 1 >= self.VALUE_LIMIT:
+            raise RuntimeError("DeviceSignal: value would wrap; use a fresh signal")
         self.value += 1
         _call("pcst_signal_write", _ptr(self.flag), self.value, ctypes.c_void_p(stream.cuda_stream))
 
     def wait(self, stream):
         _call("pcst_signal_wait", _ptr(self.flag), self.value, ctypes.c_void_p(self.flag.data_ptr() + 4),
-              ctypes.c_void_p(stream.cuda_stream))
+              self.max_polls, ctypes.c_void_p(stream.cuda_stream))
 
     def wait_args(self):
-        """(flag, value, counter, err) for pcst_noise_mlp_then_wait: wait for the last signal."""
+        """(flag, value, counter, err, max_polls) for pcst_noise_mlp_then_wait: wait for the last
+        signal."""
         base = self.flag.data_ptr()
         return (ctypes.c_void_p(base), ctypes.c_uint32(self.value), ctypes.c_void_p(base + 8),
-                ctypes.c_void_p(base + 4))
+                ctypes.c_void_p(base + 4), ctypes.c_int64(self.max_polls))
 
     def timed_out(self) -> bool:
+        """Whether any wait on this flag gave up (reads the device: call after the waits ran)."""
         return bool(int(self.flag[1].item()))
+
+    def check(self):
+        if self.timed_out():
+            raise SignalTimeout("pcst: a cross-stream device wait timed out (its producer never "
+                                "signalled); results ordered behind it are invalid")
+
+
+class DeviceStream:
+    """A HIP stream owned by the caller (pcst_stream_create), usable as a torch stream
+    (torch.cuda.ExternalStream).  priority < 0: the device's greatest priority."""
+
+    def __init__(self, device, priority=0):
+        dev = torch.device(device)
+        idx = dev.index if dev.index is not None else torch.cuda.current_device()
+        h = ctypes.c_void_p()
+        with torch.cuda.device(idx):
+            _call("pcst_stream_create", int(priority), ctypes.byref(h))
+        self._h = h
+        self.stream = torch.cuda.ExternalStream(h.value, device=torch.device("cuda", idx))
+
+    def __del__(self):
+        try:
+            if _lib is not None and self._h:
+                _lib.pcst_stream_destroy(self._h)
+        except Exception:  # noqa: BLE001  (interpreter shutdown)
+            pass
 
 
 class DeviceEvent:
@@ -829,6 +882,24 @@ def group_gather_bwd(dgrouped, group_idx, N):
     return dP
 
 
+def group_colsum16(g, B):
+    """g [B*N, C] float16 / bfloat16 -> [B, C] float32: each cloud's column sums, rounded to g's
+    16-bit type (the autocast reduction of a broadcast row; deterministic)."""
+    require_device(g)
+    if g.dtype not in (torch.float16, torch.bfloat16) or g.dim() != 2:
+        raise RuntimeError(f"group_colsum16: need a 2-d float16/bfloat16 tensor, got {g.dtype} "
+                           f"{tuple(g.shape)}")
+    g = g.contiguous()
+    M, C = g.shape
+    if M % B:
+        raise RuntimeError(f"group_colsum16: {M} rows do not split into {B} clouds")
+    ws = _workspace("pcst_group_colsum16_workspace_size", B, C, device=g.device)
+    out = torch.empty(B, C, dtype=torch.float32, device=g.device)
+    _call("pcst_group_colsum16", _ptr(g), 1 if g.dtype == torch.float16 else 0, B, M // B, C,
+          _ptr(out), _ptr(ws), _stream())
+    return out
+
+
 # ----------------------------------------------------------------------------- losses
 def chamfer_fwd(pred, target, mode=0):
     """-> (chamfer [B], arg1 [B,N] int32, arg2 [B,M] int32).  mode: 0 auto (= 3), 1 exhaustive,
@@ -960,7 +1031,7 @@ _GUARDED = ("square_distance", "index_points", "fps", "ball_query", "group_gathe
             "linear_wgrad", "gemm_nt_bf16", "channel_stats", "affine_act", "chamfer_fwd",
             "chamfer_bwd", "l1_fwd", "l1_bwd", "knn_dist", "emd_greedy", "voxel_center_dist",
             "cfg_ddim_step_dcoef", "voxel_downsample_copies_dseed", "bn_train_coeffs",
-            "bn_relu_maxpool", "bn_relu_bwd", "group_gather_bwd", "gemm_ex", "dropout_grad_bf16",
+            "bn_relu_maxpool", "bn_relu_bwd", "group_gather_bwd", "group_colsum16", "gemm_ex", "dropout_grad_bf16",
             "linear_wgrad_ex", "knn_workspace")
 for _name in _GUARDED:
     globals()[_name] = _on_tensor_device(globals()[_name])

@@ -57,3 +57,22 @@ extern "C" int pcst_event_elapsed_ms(void* start, void* end, float* ms) {
            "event_elapsed_ms");
   return PCST_OK;
 }
+
+// Streams owned by the caller (one pair per sampling loop and host thread, so two loops on one
+// device never share a queue: their cross-stream flag waits could otherwise interleave on it and
+// wait on each other).  priority < 0 is the device's greatest priority, else its default.
+extern "C" int pcst_stream_create(int priority, void** stream) {
+  PCST_CHECK_ARG(stream != nullptr, "stream_create: null pointer");
+  int least = 0, greatest = 0;
+  PCST_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest), "stream_create: priority range");
+  hipStream_t s = nullptr;
+  PCST_HIP(hipStreamCreateWithPriority(&s, hipStreamNonBlocking, priority < 0 ? greatest : least),
+           "stream_create");
+  *stream = s;
+  return PCST_OK;
+}
+
+extern "C" int pcst_stream_destroy(void* stream) {
+  if (stream) PCST_HIP(hipStreamDestroy(static_cast<hipStream_t>(stream)), "stream_destroy");
+  return PCST_OK;
+}

@@ -1062,7 +1062,7 @@ __device__ __forceinline__ void pair16_wave(const float* __restrict__ cond, cons
 // producer always finds free CUs.
 constexpr int kMlpWaitPolls = 1 << 26;
 __device__ __forceinline__ void last_group_wait(const uint32_t* flag, uint32_t value,
-                                                uint32_t* counter, int32_t* err) {
+                                                uint32_t* counter, int32_t* err, int64_t max_polls) {
   __syncthreads();  // this work-group's rows are written
   if (threadIdx.x == 0) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
@@ -1071,7 +1071,7 @@ __device__ __forceinline__ void last_group_wait(const uint32_t* flag, uint32_t v
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       bool ok = false;
-      for (int i = 0; i < kMlpWaitPolls; ++i) {
+      for (int64_t i = 0; i < max_polls; ++i) {
         if (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= value) {
           ok = true;
           break;
@@ -1088,7 +1088,7 @@ __global__ __launch_bounds__(kPairThreads) void noise_mlp_pair16_kernel(
     const float* __restrict__ pts, int64_t P, int64_t T, const float* __restrict__ cond,
     int64_t nclouds, const char* __restrict__ blob, int nparts, const float* __restrict__ bias,
     float* __restrict__ out, const uint32_t* __restrict__ wflag, uint32_t wvalue,
-    uint32_t* __restrict__ wcount, int32_t* __restrict__ werr) {
+    uint32_t* __restrict__ wcount, int32_t* __restrict__ werr, int64_t wpolls) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* X = smem + Streamer2::kSlots * kPart;
   float* sb = reinterpret_cast<float*>(X + Streamer2::kWaves * kXBytes);
@@ -1124,7 +1124,7 @@ __global__ __launch_bounds__(kPairThreads) void noise_mlp_pair16_kernel(
     pair16_wave<0>(cond, sb, sc, X, st, wid, c0, slot, px, py, pz, p, P, out);
   else
     pair16_wave<1>(cond, sb, sc, X, st, wid, c0, slot, px, py, pz, p, P, out);
-  if (wflag) last_group_wait(wflag, wvalue, wcount, werr);
+  if (wflag) last_group_wait(wflag, wvalue, wcount, werr, wpolls);
 }
 
 // cond[c] = b4 + time_proj(emb(t_c)) + style_proj(style_c)   (diffusion_model.py:15-26, 56-58)
@@ -1231,7 +1231,7 @@ extern "C" int pcst_noise_mlp(const float* pts, int64_t P, int64_t points_per_cl
     hipLaunchKernelGGL(noise_mlp_pair16_kernel, dim3((unsigned)cdiv(P, 128)), dim3(kPairThreads),
                        lds, s, pts, P, points_per_cloud, cond, nclouds, (const char*)blob,
                        (int)(blob_bytes / kPart), bias, out, (const uint32_t*)nullptr, 0u,
-                       (uint32_t*)nullptr, (int32_t*)nullptr);
+                       (uint32_t*)nullptr, (int32_t*)nullptr, (int64_t)0);
   } else if (precision == 1) {
     const size_t lds = Streamer2::kSlots * kPart + Streamer2::kWaves * kXBytes +
                        (kBiasFloats + kCondSlots * 256) * sizeof(float);
@@ -1248,7 +1248,7 @@ extern "C" int pcst_noise_mlp_then_wait(const float* pts, int64_t P, int64_t poi
                                         const float* cond, int64_t nclouds, const void* blob,
                                         int64_t blob_bytes, const float* bias, float* out,
                                         const uint32_t* flag, uint32_t value, uint32_t* counter,
-                                        int32_t* err, void* stream) {
+                                        int32_t* err, int64_t max_polls, void* stream) {
   PCST_CHECK_ARG(P > 0 && points_per_cloud > 0 && nclouds > 0, "noise_mlp_then_wait: bad shape");
   PCST_CHECK_ARG(P <= points_per_cloud * nclouds, "noise_mlp_then_wait: P exceeds clouds*points");
   PCST_CHECK_ARG(blob_bytes == pcst_noise_mlp_blob_bytes(2), "noise_mlp_then_wait: blob size %lld != %lld",
@@ -1259,7 +1259,8 @@ extern "C" int pcst_noise_mlp_then_wait(const float* pts, int64_t P, int64_t poi
                      (kBiasFloats + kCondSlots * 256) * sizeof(float);
   hipLaunchKernelGGL(noise_mlp_pair16_kernel, dim3((unsigned)cdiv(P, 128)), dim3(kPairThreads), lds,
                      as_stream(stream), pts, P, points_per_cloud, cond, nclouds, (const char*)blob,
-                     (int)(blob_bytes / kPart), bias, out, flag, value, counter, err);
+                     (int)(blob_bytes / kPart), bias, out, flag, value, counter, err,
+                     max_polls > 0 ? max_polls : (int64_t)kMlpWaitPolls);
   PCST_LAUNCH_CHECK("noise_mlp_then_wait");
   return PCST_OK;
 }

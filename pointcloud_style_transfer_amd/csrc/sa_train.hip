@@ -18,6 +18,8 @@
 //   gather    grouped[b, s, k, 3 + c] = P[b, clamp(idx[b, s, k]), c]  (pcst_group_gather)
 //             dP[b, n, c] = sum over entries e with idx == n of dG[b, e, 3 + c]
 //                                                                    pcst_group_gather_bwd
+#include <hip/hip_fp16.h>
+
 #include "common.h"
 #include "sort.h"
 
@@ -397,5 +399,95 @@ extern "C" int pcst_group_gather_bwd(const float* dgrouped, const int64_t* group
   hipLaunchKernelGGL(gather_bwd_kernel, dim3((unsigned)N, (unsigned)B), dim3(C >= 128 ? 128 : 64), 0, s,
                      dgrouped, w.k, w.v, E, C, N, dpoints);
   PCST_LAUNCH_CHECK("group_gather_bwd");
+  return PCST_OK;
+}
+
+// ---- per-cloud column sums of a 16-bit matrix (NoisePredictorFn's dL/dtf = dL/dsf) ----------
+// out[b][c] = f32(h16(sum over the N rows of cloud b of G[b*N + n][c])): the reduction autograd
+// makes for the broadcast time / style rows of x = (pf + tf) + sf (diffusion_model.py:56-58)
+// under autocast -- float accumulation, the 16-bit output rounding of torch's half sum.
+// Deterministic: slice s of cloud b sums rows [s*rows_per, ...) in row order per lane, the 8
+// row lanes of a work-group meet in LDS in lane order, and the slices are combined in slice order.
+namespace pcst {
+constexpr int kColsumSlices = 64;
+constexpr int kColsumCols = 256;  // columns per work-group: 32 lanes x 8 (16-byte loads)
+
+__device__ __forceinline__ float h16_to_f(uint16_t v, int f16) {
+  if (f16) return __half2float(__ushort_as_half(v));
+  return __uint_as_float((uint32_t)v << 16);
+}
+__device__ __forceinline__ float h16_round(float v, int f16) {
+  if (f16) return __half2float(__float2half_rn(v));
+  return (float)(__bf16)v;
+}
+
+__global__ __launch_bounds__(256) void colsum16_partial_kernel(const uint16_t* __restrict__ G,
+                                                               int f16, int64_t N, int64_t C,
+                                                               float* __restrict__ part) {
+  const int b = blockIdx.z, s = blockIdx.y;
+  const int64_t c0 = (int64_t)blockIdx.x * kColsumCols + (threadIdx.x & 31) * 8;
+  const int rl = threadIdx.x >> 5;  // row lane 0..7
+  const int64_t per = (N + kColsumSlices - 1) / kColsumSlices;
+  const int64_t r0 = s * per, r1 = r0 + per < N ? r0 + per : N;
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (c0 < C) {
+    const uint16_t* base = G + ((int64_t)b * N) * C + c0;
+    for (int64_t r = r0 + rl; r < r1; r += 8) {
+      const uint4 v = *reinterpret_cast<const uint4*>(base + r * C);
+      const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        acc[2 * j] += h16_to_f((uint16_t)(w[j] & 0xffffu), f16);
+        acc[2 * j + 1] += h16_to_f((uint16_t)(w[j] >> 16), f16);
+      }
+    }
+  }
+  __shared__ float sh[8][kColsumCols + 4];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) sh[rl][(threadIdx.x & 31) * 8 + j] = acc[j];
+  __syncthreads();
+  const int64_t c = (int64_t)blockIdx.x * kColsumCols + threadIdx.x;
+  if (c < C) {
+    float t = sh[0][threadIdx.x];
+#pragma unroll
+    for (int k = 1; k < 8; ++k) t += sh[k][threadIdx.x];
+    part[((int64_t)b * kColsumSlices + s) * C + c] = t;
+  }
+}
+
+__global__ __launch_bounds__(256) void colsum16_combine_kernel(const float* __restrict__ part,
+                                                               int f16, int64_t B, int64_t C,
+                                                               float* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= B * C) return;
+  const int64_t b = i / C, c = i % C;
+  float t = 0.f;
+  for (int s = 0; s < kColsumSlices; ++s) t += part[(b * kColsumSlices + s) * C + c];
+  out[i] = h16_round(t, f16);
+}
+}  // namespace pcst
+
+extern "C" int pcst_group_colsum16_workspace_size(int64_t B, int64_t C, size_t* bytes) {
+  PCST_CHECK_ARG(bytes && B >= 0 && C >= 0, "group_colsum16_workspace_size: bad arguments");
+  *bytes = (size_t)(B * pcst::kColsumSlices * C) * sizeof(float);
+  return PCST_OK;
+}
+
+extern "C" int pcst_group_colsum16(const uint16_t* G, int f16, int64_t B, int64_t N, int64_t C,
+                                   float* out, void* workspace, void* stream) {
+  PCST_CHECK_ARG(B >= 0 && N >= 0 && C >= 0, "group_colsum16: bad shape");
+  PCST_CHECK_ARG(C % 8 == 0, "group_colsum16: C must be a multiple of 8 (16-byte rows)");
+  if (B == 0 || C == 0) return PCST_OK;
+  PCST_CHECK_ARG(G && out && workspace, "group_colsum16: null pointer");
+  PCST_CHECK_ARG(((uintptr_t)G & 15) == 0, "group_colsum16: G must be 16-byte aligned");
+  PCST_CHECK_ARG(B <= 65535, "group_colsum16: too many clouds");
+  hipStream_t s = pcst::as_stream(stream);
+  float* part = static_cast<float*>(workspace);
+  hipLaunchKernelGGL(pcst::colsum16_partial_kernel,
+                     dim3((unsigned)pcst::cdiv(C, pcst::kColsumCols), pcst::kColsumSlices, (unsigned)B),
+                     dim3(256), 0, s, G, f16, N, C, part);
+  hipLaunchKernelGGL(pcst::colsum16_combine_kernel, dim3((unsigned)pcst::cdiv(B * C, 256)), dim3(256),
+                     0, s, part, f16, B, C, out);
+  PCST_LAUNCH_CHECK("group_colsum16");
   return PCST_OK;
 }

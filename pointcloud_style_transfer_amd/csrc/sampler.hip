@@ -81,12 +81,14 @@ __global__ void signal_write_kernel(uint32_t* flag, uint32_t value) {
 }
 
 // one lane polls (agent-scope loads, L2-served, with s_sleep between polls) until the flag
-// reaches `value`, at most kSignalPolls times (~10 s); then an agent-scope acquire
+// reaches `value`, at most max_polls times (default kSignalPolls, ~10 s); then an agent-scope
+// acquire.  A wait that gives up sets *err: the caller must read it (the stream goes on).
 constexpr int kSignalPolls = 1 << 26;
-__global__ void signal_wait_kernel(const uint32_t* flag, uint32_t value, int32_t* err) {
+__global__ void signal_wait_kernel(const uint32_t* flag, uint32_t value, int32_t* err,
+                                   int64_t max_polls) {
   if (threadIdx.x == 0) {
     bool ok = false;
-    for (int i = 0; i < kSignalPolls; ++i) {
+    for (int64_t i = 0; i < max_polls; ++i) {
       if (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= value) {
         ok = true;
         break;
@@ -107,10 +109,11 @@ extern "C" int pcst_signal_write(uint32_t* flag, uint32_t value, void* stream) {
   return PCST_OK;
 }
 
-extern "C" int pcst_signal_wait(const uint32_t* flag, uint32_t value, int32_t* err, void* stream) {
+extern "C" int pcst_signal_wait(const uint32_t* flag, uint32_t value, int32_t* err, int64_t max_polls,
+                                void* stream) {
   PCST_CHECK_ARG(flag != nullptr, "signal_wait: null flag");
   hipLaunchKernelGGL(pcst::signal_wait_kernel, dim3(1), dim3(64), 0, pcst::as_stream(stream), flag,
-                     value, err);
+                     value, err, max_polls > 0 ? max_polls : (int64_t)pcst::kSignalPolls);
   PCST_LAUNCH_CHECK("signal_wait");
   return PCST_OK;
 }

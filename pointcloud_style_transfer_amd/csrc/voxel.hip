@@ -365,7 +365,8 @@ struct VoxelFastWS {
   unsigned long long* ties;  // [R][kTieCap] (key<<32 | id)
   // zeroed every call (one memset): counters, histograms, tables, rep flags
   int32_t* cnt4;          // [R][4]: U (of cloud r, rows r < B), selected, ties, err
-  uint32_t* hist;         // [R][kSelBins]
+  uint32_t* hist;         // [R][kSelBins] pool keys (U < T): every point's, less the reps'
+  uint32_t* hist2;        // [R][kSelBins] representative keys (U > T)
   unsigned long long* tkey;  // [B][H]  0 = empty, else (1<<32)|hash
   unsigned long long* tsum;  // [B][H]
   uint32_t* tcnt;         // [B][H]
@@ -397,6 +398,7 @@ static VoxelFastWS carve_voxel_fast(void* base, int64_t B, int64_t N, int64_t co
   w.ties = c.take<unsigned long long>(R * kTieCap);
   w.cnt4 = c.take<int32_t>(R * 4);
   w.hist = c.take<uint32_t>(R * kSelBins);
+  w.hist2 = c.take<uint32_t>(R * kSelBins);
   w.tkey = c.take<unsigned long long>(B * w.H);
   w.tsum = c.take<unsigned long long>(B * w.H);
   w.tcnt = c.take<uint32_t>(B * w.H);
@@ -437,7 +439,10 @@ __global__ __launch_bounds__(256) void voxf_insert_kernel(const float* __restric
                                                           int64_t T, int64_t H,
                                                           unsigned long long* __restrict__ tkey,
                                                           unsigned long long* __restrict__ tsum,
-                                                          uint32_t* __restrict__ tcnt) {
+                                                          uint32_t* __restrict__ tcnt, int B,
+                                                          int copies, uint64_t seed_v,
+                                                          const uint64_t* __restrict__ seed_p,
+                                                          uint32_t* __restrict__ hist) {
   // Each workgroup first aggregates its kVoxChunk points in an LDS table (LDS atomics), then
   // publishes one global (sum, count) per distinct voxel: dense voxels see at most one global
   // atomic per workgroup instead of one per point.
@@ -485,14 +490,37 @@ __global__ __launch_bounds__(256) void voxf_insert_kernel(const float* __restric
     atomicAdd(&tsum[b * H + slot], lsum[i]);
     atomicAdd(&tcnt[b * H + slot], lcnt[i]);
   }
+  // The pool-key histogram of every row of this cloud over EVERY point of the chunk (a pool
+  // key depends on (seed, row, index) only); voxf_reps_kernel takes the representatives' keys
+  // back out, leaving the histogram of the pool (the U < T candidates) without a launch of its
+  // own.  The LDS table above is reused as the 4096 bins (kVoxLds * 8 B >= 16 KiB).
+  static_assert(kVoxLds * 2 >= kSelBins, "LDS table too small for the key histogram");
+  uint32_t* lh = reinterpret_cast<uint32_t*>(lkey);
+  const uint64_t seed = seed_p ? *seed_p : seed_v;
+  for (int c = 0; c < copies; ++c) {
+    const int row = c * B + b;
+    __syncthreads();
+    for (int i = threadIdx.x; i < kSelBins; i += 256) lh[i] = 0u;
+    __syncthreads();
+    for (int n = n0 + threadIdx.x; n < n1; n += 256)
+      atomicAdd(&lh[rand_key(seed, row + 0x10000, n) >> 20], 1u);
+    __syncthreads();
+    for (int i = threadIdx.x; i < kSelBins; i += 256)
+      if (lh[i]) atomicAdd(&hist[(int64_t)row * kSelBins + i], lh[i]);
+  }
 }
 
 // occupied slot -> representative trunc(f32(sum)/f32(count)) (Q6); list order = arrival order
 // (only the SET matters downstream: rows are emitted in point-index order).
+// Each representative also updates both selection histograms of every row of its cloud: its
+// voxel's key into hist2 (the U > T candidates), and its index's pool key out of hist (once per
+// distinct index: the first voxel to flag the index does it).
 __global__ __launch_bounds__(256) void voxf_reps_kernel(
     const unsigned long long* __restrict__ tkey, const unsigned long long* __restrict__ tsum,
     const uint32_t* __restrict__ tcnt, int64_t H, int N, int32_t* __restrict__ cnt4,
-    int64_t* __restrict__ reps, uint32_t* __restrict__ rhash, uint32_t* __restrict__ isrep) {
+    int64_t* __restrict__ reps, uint32_t* __restrict__ rhash, uint32_t* __restrict__ isrep,
+    int B, int copies, uint64_t seed_v, const uint64_t* __restrict__ seed_p,
+    uint32_t* __restrict__ hist, uint32_t* __restrict__ hist2) {
   // one contiguous slot range per workgroup, one counter atomic per workgroup
   const int b = blockIdx.y;
   const int64_t chunk = (H + gridDim.x - 1) / gridDim.x;
@@ -507,6 +535,7 @@ __global__ __launch_bounds__(256) void voxf_reps_kernel(
   if (threadIdx.x == 0) base = tot ? atomicAdd(&cnt4[b * 4 + 0], (int)tot) : 0;
   __syncthreads();
   int k = base + (int)off;
+  const uint64_t seed = seed_p ? *seed_p : seed_v;
   for (int64_t s = s0 + threadIdx.x; s < s1; s += 256) {
     const unsigned long long kw = K[s];
     if (!kw) continue;
@@ -515,7 +544,12 @@ __global__ __launch_bounds__(256) void voxf_reps_kernel(
     const int64_t r = (int64_t)__fdiv_rn(fs, fc);
     reps[(int64_t)b * N + k] = r;
     rhash[(int64_t)b * N + k] = (uint32_t)kw;
-    isrep[(int64_t)b * N + r] = 1u;
+    const bool first = atomicExch(&isrep[(int64_t)b * N + r], 1u) == 0u;
+    for (int c = 0; c < copies; ++c) {
+      const int row = c * B + b;
+      atomicAdd(&hist2[(int64_t)row * kSelBins + (rand_key(seed, row, (int)((uint32_t)kw & 0x7fffffff)) >> 20)], 1u);
+      if (first) atomicSub(&hist[(int64_t)row * kSelBins + (rand_key(seed, row + 0x10000, (int)r) >> 20)], 1u);
+    }
     ++k;
   }
 }
@@ -536,27 +570,6 @@ __device__ __forceinline__ bool voxf_cand(int row, int cl, int e, int N, int U, 
   id = (uint32_t)e;
   key = rand_key(seed, row + 0x10000, e);
   return true;
-}
-
-__global__ __launch_bounds__(256) void voxf_hist_kernel(int N, int64_t T, int B, uint64_t seed_v,
-                                                        const uint64_t* __restrict__ seed_p,
-                                                        const int32_t* __restrict__ cnt4,
-                                                        const uint32_t* __restrict__ rhash,
-                                                        const uint32_t* __restrict__ isrep,
-                                                        uint32_t* __restrict__ hist) {
-  const uint64_t seed = seed_p ? *seed_p : seed_v;  // device seed: hipGraph-replayable
-  const int row = blockIdx.y, cl = row % B;
-  const int U = cnt4[cl * 4];
-  __shared__ uint32_t h[kSelBins];
-  for (int i = threadIdx.x; i < kSelBins; i += 256) h[i] = 0;
-  __syncthreads();
-  for (int e = blockIdx.x * 256 + threadIdx.x; e < N; e += gridDim.x * 256) {
-    uint32_t key, id;
-    if (voxf_cand(row, cl, e, N, U, T, seed, rhash, isrep, key, id)) atomicAdd(&h[key >> 20], 1u);
-  }
-  __syncthreads();
-  for (int i = threadIdx.x; i < kSelBins; i += 256)
-    if (h[i]) atomicAdd(&hist[row * kSelBins + i], h[i]);
 }
 
 // kept candidate -> one more keep of its point index in this row (index n = the rep's index if
@@ -584,7 +597,8 @@ __device__ __forceinline__ void voxf_flush_tiles(int row, int64_t tiles, const u
 // are kept, keys in b* go to the tie list (its order is irrelevant: the emit kernel ranks).
 __global__ __launch_bounds__(256) void voxf_select_kernel(
     int N, int64_t T, int B, uint64_t seed_v, const uint64_t* __restrict__ seed_p,
-    const uint32_t* __restrict__ hist, int32_t* __restrict__ sel, int32_t* __restrict__ cnt4,
+    const uint32_t* __restrict__ hist, const uint32_t* __restrict__ hist2,
+    int32_t* __restrict__ sel, int32_t* __restrict__ cnt4,
     const uint32_t* __restrict__ rhash, const uint32_t* __restrict__ isrep,
     const int64_t* __restrict__ reps, unsigned long long* __restrict__ ties,
     uint32_t* __restrict__ kcnt, uint32_t* __restrict__ ktile, int64_t tiles) {
@@ -599,9 +613,10 @@ __global__ __launch_bounds__(256) void voxf_select_kernel(
   {
     constexpr int per = kSelBins / 256;
     uint32_t v[per], s = 0;
+    const uint32_t* hs = (U > T ? hist2 : hist) + (int64_t)row * kSelBins;
 #pragma unroll
     for (int k = 0; k < per; ++k) {
-      v[k] = hist[row * kSelBins + threadIdx.x * per + k];
+      v[k] = hs[threadIdx.x * per + k];
       s += v[k];
     }
     if (threadIdx.x == 0) { s_bstar = -1; s_rem = 0; }
@@ -734,8 +749,9 @@ __global__ __launch_bounds__(256) void voxf_emit_kernel(const float* __restrict_
   }
 }
 
-// stats (+ zeroing), insert (+ voxel parameters), reps, hist, select (+ boundary bin, marks,
-// tie list), emit (+ tie ranking; rows in point-index order): 6 launches.
+// stats (+ zeroing), insert (+ voxel parameters, every point's pool-key histogram), reps (+ the
+// representatives' keys into / out of the histograms), select (+ boundary bin, marks, tie list),
+// emit (+ tie ranking; rows in point-index order): 5 launches.
 static int voxel_fast(const float* pts, int64_t B, int64_t N, int64_t copies, int64_t T,
                       void* workspace, uint64_t seed, const uint64_t* seed_p, int64_t* out_idx,
                       float* out_pts, hipStream_t s) {
@@ -744,16 +760,15 @@ static int voxel_fast(const float* pts, int64_t B, int64_t N, int64_t copies, in
   const size_t zero = (size_t)((char*)(w.ktile + rows * w.tiles) - (char*)w.cnt4);
   hipLaunchKernelGGL(voxf_stats_zero_kernel, dim3(kStatBlocks + kVoxZeroBlocks, b), dim3(256), 0, s,
                      pts, n, w.mm, reinterpret_cast<uint4*>(w.cnt4), (int64_t)cdiv(zero, 16));
+  const int cp = (int)copies;
   hipLaunchKernelGGL(voxf_insert_kernel, dim3((unsigned)cdiv(N, kVoxChunk), b), dim3(256), 0, s,
-                     pts, n, w.mm, T, w.H, w.tkey, w.tsum, w.tcnt);
+                     pts, n, w.mm, T, w.H, w.tkey, w.tsum, w.tcnt, b, cp, seed, seed_p, w.hist);
   hipLaunchKernelGGL(voxf_reps_kernel, dim3(kVoxRepsBlocks, b), dim3(256), 0, s, w.tkey, w.tsum,
-                     w.tcnt, w.H, n, w.cnt4, w.reps, w.rhash, w.isrep);
-  const unsigned gs = (unsigned)std::min<int64_t>(cdiv(N, 256), 256);
-  hipLaunchKernelGGL(voxf_hist_kernel, dim3(gs, rows), dim3(256), 0, s, n, T, b, seed, seed_p,
-                     w.cnt4, w.rhash, w.isrep, w.hist);
+                     w.tcnt, w.H, n, w.cnt4, w.reps, w.rhash, w.isrep, b, cp, seed, seed_p, w.hist,
+                     w.hist2);
   hipLaunchKernelGGL(voxf_select_kernel, dim3(128, rows), dim3(256), 0, s, n, T, b, seed, seed_p,
-                     w.hist, w.sel, w.cnt4, w.rhash, w.isrep, w.reps, w.ties, w.kcnt, w.ktile,
-                     w.tiles);
+                     w.hist, w.hist2, w.sel, w.cnt4, w.rhash, w.isrep, w.reps, w.ties, w.kcnt,
+                     w.ktile, w.tiles);
   hipLaunchKernelGGL(voxf_emit_kernel, dim3((unsigned)w.tiles, rows), dim3(256), 0, s, pts, n, T,
                      b, w.kcnt, w.ktile, w.tiles, w.cnt4, w.sel, w.ties, w.reps, out_idx, out_pts);
   PCST_LAUNCH_CHECK("voxel_downsample");

@@ -276,10 +276,10 @@ class NoisePredictorFn(torch.autograd.Function):
                 g, grads[o], grads[o + 1], grads[o + 2], grads[o + 3] = _block_bwd(
                     g, xbk, hk, _h_t(w[o], half), _h_t(w[o + 2], half), ctx.ps[k], ctx.seeds[k])
         # x = ((pf + tf) + sf): dL/dpf = g, dL/dtf[b] = dL/dsf[b] = sum of g over cloud b's rows
-        # per-cloud row sums as one batched GEMV (ones [B,1,N] @ g [B,N,256]): torch's
-        # middle-dimension sum reduced this at ~40 % of the HBM rate (254 vs 82 us at B = 8)
-        gsum = torch.bmm(torch.ones(B, 1, N, dtype=g.dtype, device=g.device),
-                         g.view(B, N, -1)).squeeze(1).float()
+        # per-cloud row sums (pcst_group_colsum16: float accumulation, rounded to g's 16-bit
+        # type as autocast's sum; replaces a hipBLASLt batched GEMV, ones [B,1,N] @ g [B,N,256])
+        gsum = (_hip.group_colsum16(g, B) if g.dtype in (torch.float16, torch.bfloat16)
+                else g.view(B, N, -1).sum(1).float())
         dcond = torch.stack([gsum, gsum], 1)
         grads[4], grads[5] = _hip.linear_wgrad_ex(g, h1)
         dh1 = _hip.gemm_ex(g, _h_t(w[4], half), epilogue=_hip.EP_RELU_MASK, aux=h1)

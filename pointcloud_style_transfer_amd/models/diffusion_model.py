@@ -16,7 +16,8 @@ from __future__ import annotations
 
 import contextlib
 import math
-from typing import Dict, Optional, Tuple
+import threading
+from typing import Optional, Tuple
 
 import numpy as np
 import torch
@@ -275,36 +276,83 @@ def overlap_knn_build(mlp_points: int) -> bool:
 def knn_build_lds_floor(mlp_points: int) -> int:
     """The side-stream build's LDS floor for an MLP launch over `mlp_points` points."""
     return KNN_BUILD_LDS_FLOOR if mlp_points <= _OVERLAP_MAX_MLP_POINTS else 0
-_STEP_STREAMS: Dict[int, Tuple[torch.cuda.Stream, torch.cuda.Stream]] = {}
+_THREAD_STREAMS = threading.local()
 
 
 def step_streams(device) -> Tuple[torch.cuda.Stream, torch.cuda.Stream]:
-    """(high-priority loop stream, default-priority side stream) of a device, created once."""
+    """(high-priority loop stream, default-priority side stream) of the calling host thread on a
+    device, created once per thread (pcst_stream_create).  Two sampling loops running at the same
+    time from two threads never share a queue: their flag waits, interleaved on one queue, could
+    wait on each other."""
     idx = torch.device(device).index
     idx = torch.cuda.current_device() if idx is None else idx
-    if idx not in _STEP_STREAMS:
-        with torch.cuda.device(idx):
-            _STEP_STREAMS[idx] = (torch.cuda.Stream(priority=-1), torch.cuda.Stream(priority=0))
-    return _STEP_STREAMS[idx]
+    per_dev = getattr(_THREAD_STREAMS, "by_device", None)
+    if per_dev is None:
+        per_dev = _THREAD_STREAMS.by_device = {}
+    if idx not in per_dev:
+        per_dev[idx] = (_hip.DeviceStream(idx, priority=-1), _hip.DeviceStream(idx, priority=0))
+    loop, side = per_dev[idx]
+    return loop.stream, side.stream
 
 
-def hierarchical_eps(hp, mlp, xc, xi, x_cat, knn_ws=None, side=None, mlp_waits=False):
+# Poll bound of the step's device waits (0: the library's default, ~10 s).  Tests lower it.
+SIGNAL_MAX_POLLS = 0
+
+
+class StepState:
+    """The overlapped step's streams and cross-stream dependencies for ONE sampling loop (or one
+    bench run): the calling thread's loop / side streams, two events and two device flags (0:
+    loop -> side, the voxel output is ready; 1: side -> loop, the kNN build is done).  The flags
+    share one allocation, so `check()` reads both timeout words with one copy; it raises
+    _hip.SignalTimeout when a wait gave up (the loop's results are then invalid).  Per loop, so
+    concurrent loops never share a flag and a flag's host counter starts at zero every loop."""
+
+    def __init__(self, device, max_polls=None):
+        self.loop, self.side = step_streams(device)
+        mk = _hip.DeviceEvent if DEVICE_EVENTS else _TorchEvent
+        self.ready_ev, self.built_ev = mk(), mk()
+        polls = SIGNAL_MAX_POLLS if max_polls is None else max_polls
+        self._flags = torch.zeros(2, 4, dtype=torch.int32, device=device)
+        self.ready_sig = _hip.DeviceSignal(device, polls, self._flags[0])
+        self.built_sig = _hip.DeviceSignal(device, polls, self._flags[1])
+
+    def begin(self, caller):
+        """Order both streams after the caller's work so far (the flags' zero fill included)."""
+        self.loop.wait_stream(caller)
+        self.side.wait_stream(caller)
+
+    def end(self, caller):
+        """Order the caller after every loop- and side-stream kernel (also on an exception: the
+        tensors the caller frees must not be reused while they run)."""
+        caller.wait_stream(self.loop)
+        caller.wait_stream(self.side)
+
+    def check(self):
+        """After end(): raise if any of the step's device waits timed out."""
+        if bool(self._flags[:, 1].cpu().any()):
+            raise _hip.SignalTimeout(
+                "pcst: a cross-stream device wait of the sampling step timed out (the kNN build or "
+                "the voxel output it waited for never signalled); the loop's output is invalid")
+
+
+def hierarchical_eps(hp, mlp, xc, xi, x_cat, knn_ws=None, state=None, mlp_waits=False):
     """eps for the CFG batch: mlp(xc) on the current stream, upsampled to the full clouds by
-    kNN-3 (HierarchicalProcessor.upsample_knn).  With a side stream (and a preallocated
-    workspace) the kNN build runs there, overlapping the MLP, with its work-groups held to an
-    LDS floor of KNN_BUILD_LDS_FLOOR bytes; the query waits for it."""
-    if side is None:
+    kNN-3 (HierarchicalProcessor.upsample_knn).  With a StepState (and a preallocated
+    workspace) the kNN build runs on its side stream, overlapping the MLP, with its work-groups
+    held to an LDS floor of KNN_BUILD_LDS_FLOOR bytes; the query waits for it."""
+    if state is None:
         return hp.upsample_knn(mlp(xc), x_cat, xi)
     main = torch.cuda.current_stream()
-    ready, built = _step_events(main.device)
+    side = state.side
+    ready, built = state.ready_ev, state.built_ev
     if KERNEL_SIGNAL:  # main -> side by a kernel-side flag: no event marker on the loop's queue
-        ready = _step_signal(main.device)
+        ready = state.ready_sig
         ready.signal(main)
     else:
         ready.record(main)
     ready.wait(side)
     if BUILT_SIGNAL:
-        built = _step_signal(main.device, 1)
+        built = state.built_sig
     with torch.cuda.stream(side):
         handle = _hip.knn3_build(x_cat, xi, knn_ws, knn_build_lds_floor(xc.shape[0] * xc.shape[1]),
                                  KNN_BUILD_MAX_WG)
@@ -327,18 +375,19 @@ SEARCH_BESIDE_MLP = False
 
 
 def hierarchical_step(hp, mlp, xc, xi, x_cat, x, source, guidance_scale, coeffs, knn_ws=None,
-                      side=None, mlp_waits=False):
+                      state=None, mlp_waits=False):
     """One guided step of the hierarchical branch (diffusion_model.py:240-260): eps of the CFG
     batch (mlp(xc) upsampled by kNN-3), then the fused CFG + DDIM update of x (x_cat takes the
-    new x twice).  Returns the new x."""
+    new x twice).  Returns the new x.  state: a StepState (overlapped layout) or None."""
     C = x.shape[0]
-    if side is None or not SEARCH_BESIDE_MLP:
-        eps = hierarchical_eps(hp, mlp, xc, xi, x_cat, knn_ws, side, mlp_waits)
+    if state is None or not SEARCH_BESIDE_MLP:
+        eps = hierarchical_eps(hp, mlp, xc, xi, x_cat, knn_ws, state, mlp_waits)
         return _hip.cfg_ddim_step(x, eps[:C], eps[C:], source, guidance_scale, coeffs, x_cat=x_cat)
     main = torch.cuda.current_stream()
-    ready, built = _step_events(main.device)
+    side = state.side
+    ready, built = state.ready_ev, state.built_ev
     if KERNEL_SIGNAL:
-        ready = _step_signal(main.device)
+        ready = state.ready_sig
         ready.signal(main)
     else:
         ready.record(main)
@@ -353,7 +402,6 @@ def hierarchical_step(hp, mlp, xc, xi, x_cat, x, source, guidance_scale, coeffs,
     return _hip.knn3_finish_cfg_ddim(nc, handle, x, source, guidance_scale, coeffs, x_cat=x_cat)
 
 
-_STEP_EVENTS: Dict[int, tuple] = {}
 # device-scope events for the step's cross-stream dependencies (tools/knobs.py: A/B only)
 DEVICE_EVENTS = True
 # The loop -> side dependency (the voxel output is ready) by kernel-side signalling instead of an
@@ -370,18 +418,6 @@ KERNEL_SIGNAL = True
 # tail, so its measured duration (the bench's roofline) is no longer the MLP's own.  Off.
 BUILT_SIGNAL = True
 MLP_WAITS = False
-_STEP_SIGNALS: Dict[tuple, "_hip.DeviceSignal"] = {}
-
-
-def _step_signal(device, which=0):
-    """The step's device flags: 0 loop -> side (the voxel output is ready), 1 side -> loop (the
-    kNN build is done)."""
-    key = (torch.device(device).index or 0, which)
-    if key not in _STEP_SIGNALS:
-        _STEP_SIGNALS[key] = _hip.DeviceSignal(device)
-    return _STEP_SIGNALS[key]
-
-
 class _TorchEvent:
     """torch.cuda.Event with the DeviceEvent interface (DEVICE_EVENTS = False: A/B runs)."""
 
@@ -393,16 +429,6 @@ class _TorchEvent:
 
     def wait(self, stream):
         stream.wait_event(self.e)
-
-
-def _step_events(device):
-    """The two cross-stream events of the overlapped step (reused every step: a wait captures
-    the event's state when it is enqueued)."""
-    key = torch.device(device).index or 0
-    if key not in _STEP_EVENTS:
-        mk = _hip.DeviceEvent if DEVICE_EVENTS else _TorchEvent
-        _STEP_EVENTS[key] = (mk(), mk())
-    return _STEP_EVENTS[key]
 
 
 class PointCloudDiffusionModel(nn.Module):
@@ -544,13 +570,13 @@ class DiffusionProcess:
             pk = npred.packed()  # the loop changes no weight
             conds = npred.cond(t_rows.reshape(-1), style_in.repeat(S, 1), pk).view(S, 2 * B, -1)
         overlap = use_hierarchical and overlap_knn_build(2 * B * model.config.global_points)
-        side = ws = vws = None
+        state = ws = vws = None
         ctx = contextlib.nullcontext()
         if overlap:
-            loop, side = step_streams(device)
+            state = StepState(device)
             caller = torch.cuda.current_stream(device)
-            loop.wait_stream(caller)
-            ctx = torch.cuda.stream(loop)
+            state.begin(caller)
+            ctx = torch.cuda.stream(state.loop)
         with ctx:
             if overlap:
                 ws = _hip.knn_workspace(2 * B, shape[1], model.config.global_points, device=device)
@@ -568,7 +594,7 @@ class DiffusionProcess:
                     if use_hierarchical:
                         xc, xi = hp.downsample_copies(x, 2, vws)
                         x = hierarchical_step(hp, mlp, xc, xi, x_cat, x, source, guidance_scale,
-                                              coeffs, ws, side,
+                                              coeffs, ws, state,
                                               mlp_waits=MLP_WAITS and conds is not None)
                     else:
                         eps = mlp(x_cat)
@@ -578,7 +604,9 @@ class DiffusionProcess:
                 # also when a step raises: tensors the caller frees must not be reused while
                 # loop-stream and side-stream kernels still run
                 if overlap:
-                    caller.wait_stream(loop)
+                    state.end(caller)
+        if overlap:
+            state.check()  # a timed-out device wait is an error, never a silent wrong result
         return x
 
     def _guided_sample_graph(self, model, source_points, condition_points, num_inference_steps,

@@ -16,6 +16,7 @@ seeded from `device_seed()`.
 from __future__ import annotations
 
 import contextlib
+import threading
 
 import numpy as np
 import torch
@@ -129,20 +130,58 @@ class CounterRNG:
         return 0
 
 
-_source = TorchRNG()
+class GeneratorRNG(TorchRNG):
+    """torch's draws from a private, seeded CPU generator (moved to the device), on the
+    non-replay (device) paths: the draws of one sampling loop do not depend on what other host
+    threads draw at the same time (tests of concurrent loops).  Installed with `use(...)`."""
+
+    def __init__(self, seed: int):
+        self.g = torch.Generator().manual_seed(int(seed))
+
+    def randint(self, low, high, size, device=None):
+        return torch.randint(low, high, size, dtype=torch.long, generator=self.g).to(device)
+
+    def randperm(self, n, device=None):
+        return torch.randperm(n, generator=self.g).to(device)
+
+    def randn(self, shape, device=None):
+        return torch.randn(shape, generator=self.g).to(device)
+
+    def rand(self, shape, device=None):
+        return torch.rand(shape, generator=self.g).to(device)
+
+    def randn_like(self, x):
+        return torch.randn(tuple(x.shape), generator=self.g).to(x.device)
+
+    def device_seed(self):
+        return int(torch.randint(0, 2**62, (1,), dtype=torch.long, generator=self.g).item())
+
+
+_default = TorchRNG()
+# the installed source is per host thread (a loop in one thread never consumes another
+# thread's replayed or seeded draws); threads without one use torch's global generators
+_local = threading.local()
 
 
 def source():
-    return _source
+    return getattr(_local, "source", None) or _default
+
+
+@contextlib.contextmanager
+def use(rng):
+    """Install `rng` as the calling thread's source for the duration of the block."""
+    prev = getattr(_local, "source", None)
+    _local.source = rng
+    try:
+        yield rng
+    finally:
+        _local.source = prev
 
 
 @contextlib.contextmanager
 def replay(draws_or_rng):
-    global _source
-    prev = _source
-    _source = (draws_or_rng if isinstance(draws_or_rng, (ReplayRNG, CounterRNG))
-               else ReplayRNG(draws_or_rng))
-    try:
-        yield _source
-    finally:
-        _source = prev
+    """Install a replay source (recorded draws, a ReplayRNG or a CounterRNG) for this thread."""
+    rng = (draws_or_rng if isinstance(draws_or_rng, (ReplayRNG, CounterRNG))
+           else ReplayRNG(draws_or_rng))
+    with use(rng):
+        yield rng

@@ -31,6 +31,7 @@ from __future__ import annotations
 import contextlib
 import math
 import os
+from typing import Optional
 
 import numpy as np
 import torch
@@ -127,11 +128,16 @@ class DeferredLosses:
 class DiffusionTrainer:
     """`DiffusionTrainer` (trainer.py:36-232)."""
 
-    def __init__(self, config: Config, device: str = "cuda"):
+    def __init__(self, config: Config, device: str = "cuda", *, ddp: Optional[bool] = None):
+        """ddp (keyword-only): None wraps the model in DDP when a process group of world size
+        > 1 is initialised; True wraps it whenever a process group is initialised, world size 1
+        included (the RCCL smoke test: DDP's reducer then all-reduces through a one-rank
+        communicator)."""
         self.config = config
         self.device = torch.device(device)
         self.device_type = "cuda" if "cuda" in str(self.device) else "cpu"
-        self.distributed = dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
+        group = dist.is_available() and dist.is_initialized()
+        self.distributed = group and (dist.get_world_size() > 1 or bool(ddp))
         self.rank = dist.get_rank() if self.distributed else 0
         self.logger = Logger(name="DiffusionTrainer", log_dir=config.log_dir,
                              experiment_name=config.experiment_name, file_output=self.rank == 0)
@@ -166,6 +172,13 @@ class DiffusionTrainer:
         # FPS, ball query: positions only) is queued on a side stream at the start of a step and
         # runs beside it; the next step's forward then starts at the SA MLPs.  Off while draws
         # are replayed (the parity tests follow the reference's draw order).
+        # Draw order: with prefetch on, batch k+1's geometry draws (the condition cloud's voxel
+        # subset seed, the SA1/SA2 FPS starts) are made at the start of step k, BEFORE step k's
+        # timestep / noise / cond-drop / dropout draws.  A seeded epoch therefore consumes the
+        # global generator in a different order than the same train_step calls without
+        # next_batch (and than the reference, trainer.py:70-127): the runs are equally valid
+        # samples but intentionally not draw-for-draw identical.  Set this to False for the
+        # reference's order (every parity test runs with it off or under a replay source).
         self.prefetch_style_geometry = self.device_type == "cuda"
         self._geo_next = None  # (condition tensor it was computed for, geometry, ready event)
         self._geo_stream = None

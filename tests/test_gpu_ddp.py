@@ -30,13 +30,14 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _run(tmp, tag, world, accum, micro, clouds=2, points=8192, amp=False, global_points=2048):
+def _run(tmp, tag, world, accum, micro, clouds=2, points=8192, amp=False, global_points=2048,
+         backend="gloo", extra_env=None):
     out = os.path.join(tmp, f"{tag}.npz")
     port = _free_port()
     procs = []
     for r in range(world):
         env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", MASTER_ADDR="127.0.0.1",
-                   MASTER_PORT=str(port))
+                   MASTER_PORT=str(port), **(extra_env or {}))
         if world > 1:
             env.update(RANK=str(r), LOCAL_RANK="0", WORLD_SIZE=str(world))
         else:
@@ -44,7 +45,7 @@ def _run(tmp, tag, world, accum, micro, clouds=2, points=8192, amp=False, global
                 env.pop(k, None)
         procs.append(subprocess.Popen(
             [sys.executable, WORKER, out, str(accum), str(micro), str(clouds), str(points),
-             amp if isinstance(amp, str) else ("1" if amp else "0"), str(global_points)],
+             amp if isinstance(amp, str) else ("1" if amp else "0"), str(global_points), backend],
             env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT))
     return procs, out
 
@@ -53,9 +54,10 @@ def _wait(procs, timeout=100):
     logs = []
     for p in procs:
         o, _ = p.communicate(timeout=timeout)
-        logs.append(o.decode(errors="replace")[-3000:])
+        logs.append(o.decode(errors="replace"))
     for p, lg in zip(procs, logs):
-        assert p.returncode == 0, lg
+        assert p.returncode == 0, lg[-3000:]
+    return logs
 
 
 def _grads(z):
@@ -167,3 +169,31 @@ def test_ddp_fp16_amp_matches_accumulation(tmp_path):
     for k in zd.files:
         if k.startswith("param:"):
             np.testing.assert_array_equal(zd[k], z1[k])
+
+
+def test_rccl_one_rank_ddp_step_matches_plain_step(tmp_path):
+    """The RCCL transport itself (the 8-GPU node's all-reduce; one GPU here): a fresh child
+    process with a one-rank "nccl" process group runs DiffusionTrainer(ddp=True) for one
+    optimizer step (2 micro-batches, no_sync on the first), so DDP's reducer all-reduces the
+    2,549,827 gradients through RCCL.  A sum over one rank is the identity, so the gradients
+    and the parameters after the step equal the plain single-process step's bit for bit
+    (/root/reference/training/trainer.py:115-125).  RCCL's collective log (NCCL_DEBUG=INFO,
+    subsystem COLL) must show the reducer's AllReduce calls."""
+    tmp = str(tmp_path)
+    rc, out_rc = _run(tmp, "rccl", 1, 2, 2, backend="nccl",
+                      extra_env={"NCCL_DEBUG": "INFO", "NCCL_DEBUG_SUBSYS": "COLL"})
+    log = _wait(rc, timeout=200)[0]
+    one, out_one = _run(tmp, "plain", 1, 2, 2)
+    _wait(one)
+    zr, zo = np.load(out_rc), np.load(out_one)
+    n_ar = sum("AllReduce" in ln for ln in log.splitlines())
+    print(f"RCCL AllReduce log lines: {n_ar}")
+    assert n_ar >= 1, log[-3000:]
+    gr, go = _grads(zr), _grads(zo)
+    assert gr.keys() == go.keys() and len(gr) == 80
+    assert np.array_equal(zr["losses"], zo["losses"])
+    for n in gr:
+        assert np.array_equal(gr[n], go[n]), n
+    for k in zr.files:
+        if k.startswith("param:"):
+            assert np.array_equal(zr[k], zo[k]), k

@@ -51,3 +51,116 @@ def test_signal_values_are_monotonic_per_flag():
         sig.wait(s)  # the same stream: already satisfied when it runs
     torch.cuda.synchronize()
     assert int(sig.flag[0].item()) == 5 and sig.value == 5 and not sig.timed_out()
+
+
+def test_wait_that_times_out_is_reported():
+    """A wait whose value is never signalled gives up after its poll bound (an argument of the
+    call), lets its stream go on, and check() raises SignalTimeout; the MLP's last-group wait
+    (pcst_noise_mlp_then_wait) reports through the same error word."""
+    from pointcloud_style_transfer_amd import _hip
+
+    dev = torch.device("cuda", 0)
+    s = torch.cuda.Stream(device=dev)
+    sig = _hip.DeviceSignal(dev, max_polls=2000)
+    sig.value = 1  # a value no kernel will ever write
+    sig.wait(s)
+    torch.cuda.synchronize()
+    assert sig.timed_out()
+    with pytest.raises(_hip.SignalTimeout):
+        sig.check()
+
+    from pointcloud_style_transfer_amd import packing
+    from pointcloud_style_transfer_amd.config.config import Config
+    from pointcloud_style_transfer_amd.models.diffusion_model import NoisePredictor
+
+    torch.manual_seed(4)
+    npred = NoisePredictor(Config(make_dirs=False, precision="bf16")).to(dev).eval()
+    assert npred.precision_code == packing.PAIR16
+    pts = torch.randn(2 * 4096, 3, device=dev)
+    with torch.no_grad():
+        cond = npred.cond(torch.tensor([5, 5], device=dev), torch.randn(2, 256, device=dev))
+        blob, bias = npred.packed()[:2]
+        ref = _hip.noise_mlp(pts, 4096, cond, blob, bias, npred.precision_code)
+        sig2 = _hip.DeviceSignal(dev, max_polls=2000)
+        sig2.value = 1
+        out = _hip.noise_mlp(pts, 4096, cond, blob, bias, npred.precision_code, wait=sig2)
+    torch.cuda.synchronize()
+    assert torch.equal(out, ref)  # the rows are written before the wait
+    with pytest.raises(_hip.SignalTimeout):
+        sig2.check()
+    assert int(sig2.flag[2].item()) == 0  # the work-group counter is reset for the next call
+
+
+def _small_model(dev, precision="bf16"):
+    from pointcloud_style_transfer_amd.config.config import Config
+    from pointcloud_style_transfer_amd.models.diffusion_model import (DiffusionProcess,
+                                                                        PointCloudDiffusionModel)
+
+    cfg = Config(make_dirs=False, precision=precision, global_points=4096)
+    torch.manual_seed(11)
+    model = PointCloudDiffusionModel(cfg).to(dev).eval()
+    return cfg, model, DiffusionProcess(cfg, device=str(dev))
+
+
+def test_guided_loop_raises_when_a_step_wait_times_out(monkeypatch):
+    """The sampling loop reads its flags' timeout words once at its end: a producer that never
+    signals (simulated: signal() bumps the host value but writes nothing) makes the loop raise
+    instead of returning what the unsynchronised kNN query computed."""
+    from pointcloud_style_transfer_amd import _hip
+    from pointcloud_style_transfer_amd.models import diffusion_model as dm
+    from pointcloud_style_transfer_amd.synthetic import lidar_like_cloud
+
+    dev = torch.device("cuda", 0)
+    cfg, model, dp = _small_model(dev)
+    src = torch.from_numpy(lidar_like_cloud(1000, 16384)[None]).to(dev)
+    cond = torch.from_numpy(lidar_like_cloud(2000, 16384)[None]).to(dev)
+    with torch.no_grad():
+        dp.guided_sample_loop(model, src, cond, 3, 7.5)  # healthy: no raise
+        monkeypatch.setattr(dm, "SIGNAL_MAX_POLLS", 2000)
+
+        def silent(self, stream):
+            self.value += 1
+
+        monkeypatch.setattr(_hip.DeviceSignal, "signal", silent)
+        with pytest.raises(_hip.SignalTimeout):
+            dp.guided_sample_loop(model, src, cond, 3, 7.5)
+
+
+def test_two_loops_on_two_threads_match_serial():
+    """Two guided loops running at the same time from two host threads on one device (each with
+    its own seeded draws, rng.GeneratorRNG) give the bits of the same loops run one after the
+    other: the loop's streams are per thread and its flags and events per call."""
+    import threading
+
+    from pointcloud_style_transfer_amd import rng
+    from pointcloud_style_transfer_amd.synthetic import lidar_like_cloud, standard_normal
+
+    dev = torch.device("cuda", 0)
+    cfg, model, dp = _small_model(dev)
+    model.noise_predictor.packed()  # pack once, before the threads
+    n = 16384
+    jobs = []
+    for k in range(2):
+        jobs.append(tuple(torch.from_numpy(a).to(dev) for a in (
+            lidar_like_cloud(1000 + k, n)[None], lidar_like_cloud(2000 + k, n)[None],
+            standard_normal(3000 + k, (1, n, 3)))))
+
+    def run(k, out):
+        src, cond, xT = jobs[k]
+        with torch.no_grad(), rng.use(rng.GeneratorRNG(100 + k)):
+            out[k] = dp.guided_sample_loop(model, src, cond, 12, 7.5, x_T=xT)
+        torch.cuda.current_stream(dev).synchronize()
+
+    serial = {}
+    for k in range(2):
+        run(k, serial)
+    conc = {}
+    ths = [threading.Thread(target=run, args=(k, conc)) for k in range(2)]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join(timeout=120)
+    assert all(not t.is_alive() for t in ths)
+    torch.cuda.synchronize()
+    for k in range(2):
+        assert torch.equal(conc[k], serial[k]), k

@@ -478,3 +478,21 @@ def _unfused_forward(npred, noisy_points, timestep, style_feat):
     h = ag.linear(x, npred.output_mlp[0], True)
     h = ag.linear(h, npred.output_mlp[2], True)
     return ag.linear(h, npred.output_mlp[4])
+
+
+@pytest.mark.parametrize("B,N,C", [(8, 30000, 256), (1, 1, 8), (3, 1001, 264), (2, 7, 256)])
+@pytest.mark.parametrize("half", [torch.float16, torch.bfloat16])
+def test_group_colsum16_vs_float64(H, B, N, C, half):
+    """pcst_group_colsum16 (NoisePredictorFn's dL/dtf = dL/dsf, no hipBLASLt GEMV): each cloud's
+    column sums in float, rounded to the 16-bit type.  Against the float64 sum of the same 16-bit
+    values rounded the same way: within one 16-bit ulp (a float32 sum of N terms is within
+    N * 2^-24 relative of the float64 one, far below the 16-bit rounding step); deterministic."""
+    torch.manual_seed(B * 1000 + N + C)
+    g = (torch.randn(B * N, C, device="cuda") * 0.01).to(half)
+    out = H.group_colsum16(g, B)
+    ref = g.double().view(B, N, C).sum(1).to(half).float()
+    assert out.shape == (B, C) and out.dtype == torch.float32
+    ulp = torch.finfo(half).eps * ref.abs().clamp_min(torch.finfo(half).tiny)
+    assert bool(((out - ref).abs() <= ulp * 1.01).all())
+    assert bool((out == ref).double().mean() >= 0.99)
+    assert torch.equal(out, H.group_colsum16(g, B))

@@ -1,0 +1,60 @@
+#!/bin/bash
+# Round-4 GPU check: tools/r4_check.sh TAG [STAGES...]
+#   tests=EXPR   pytest -m gpu -k EXPR (tests=all: the whole GPU suite)
+#   smoke        __graft_entry__.smoke()
+#   bench        the driver's invocation (bench.py --gpus 1 --steps 20 --warmup 5)
+#   prof         rocprofv3 kernel trace + stats of the driver's window (tools/kstats.py summary)
+#   pmc          noise-MLP counters over the driver's window: one SQ pass (MFMA count, MFMA-busy
+#                cycles, LDS waits), FETCH_SIZE and WRITE_SIZE passes (tools/pmc_summary.py)
+#   b32          the 32-cloud bench (configs[4]'s per-GPU share)
+#   train        tools/bench_train.py (configs[2]) plain
+# Every GPU step has its own time limit; the script stops at the first failure.
+set -u
+TAG=$1; shift; OUT=gpurun_out/$TAG; mkdir -p "$OUT"
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+BENCH="bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline --no-encoder --no-other-precision"
+for st in "$@"; do
+  case $st in
+    tests=*)
+      K=${st#tests=}
+      if [ "$K" = all ]; then SEL=(); else SEL=(-k "$K"); fi
+      timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread \
+          "${SEL[@]}" > "$OUT/pytest.log" 2>&1
+      rc=$?; echo "pytest rc=$rc"; grep -E "FAILED|ERROR" "$OUT/pytest.log" | head; tail -1 "$OUT/pytest.log"
+      if [ $rc -ne 0 ]; then exit $rc; fi ;;
+    smoke)
+      timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > "$OUT/smoke.log" 2>&1
+      rc=$?; tail -1 "$OUT/smoke.log"; if [ $rc -ne 0 ]; then exit $rc; fi ;;
+    bench)
+      timeout -k 10 400 python -u bench.py --gpus 1 --steps 20 --warmup 5 > "$OUT/bench.json" 2> "$OUT/bench.err"
+      rc=$?; echo "bench rc=$rc"; if [ $rc -ne 0 ]; then tail -3 "$OUT/bench.err"; exit $rc; fi
+      python -c "import json;d=json.loads(open('$OUT/bench.json').read().strip().splitlines()[-1]);print('bench', d['value'],d['ms_per_step'],d['roofline']['frac'],d['roofline']['avg_launch_ms'])" ;;
+    prof)
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- \
+          python $BENCH > "$OUT/pbench.json" 2> "$OUT/pbench.err"
+      rc=$?; echo "prof rc=$rc"; if [ $rc -ne 0 ]; then tail -5 "$OUT/pbench.err"; exit $rc; fi
+      python tools/kstats.py "$OUT/prof/run_kernel_stats.csv" 25 | tee "$OUT/kernel_top.txt" ;;
+    pmc)
+      timeout -s KILL 150 rocprofv3 --pmc SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_INST_LDS SQ_INSTS_LDS \
+          SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --output-format csv -d "$OUT/p1" -o pmc -- \
+          python $BENCH > "$OUT/p1.log" 2>&1
+      rc=$?; echo "pmc sq rc=$rc"; if [ $rc -ne 0 ]; then tail -5 "$OUT/p1.log"; exit $rc; fi
+      for C in FETCH_SIZE WRITE_SIZE; do
+        timeout -s KILL 150 rocprofv3 --pmc $C --output-format csv -d "$OUT/pmc_$C" -o pmc -- \
+            python $BENCH > "$OUT/pmc_$C.log" 2>&1
+        rc=$?; echo "pmc $C rc=$rc"; if [ $rc -ne 0 ]; then tail -5 "$OUT/pmc_$C.log"; exit $rc; fi
+      done
+      python tools/pmc_sq.py "$OUT" noise_mlp | tee "$OUT/noise_mlp_sq_counters.txt"
+      python tools/pmc_summary.py "$OUT" noise_mlp --json "$OUT/noise_mlp_traffic.json" | tail -4 ;;
+    b32)
+      timeout -k 10 300 python bench.py --gpus 1 --clouds-per-gpu 32 --steps 20 --warmup 3 --no-cpu-baseline \
+          --no-encoder --no-other-precision > "$OUT/bench_b32.json" 2> "$OUT/bench_b32.err"
+      rc=$?; echo "b32 rc=$rc"; if [ $rc -ne 0 ]; then tail -3 "$OUT/bench_b32.err"; exit $rc; fi
+      python -c "import json;d=json.loads(open('$OUT/bench_b32.json').read().strip().splitlines()[-1]);print('b32', d['value'], d['ms_per_step'], d['roofline']['avg_launch_ms'], d['roofline']['frac'])" ;;
+    train)
+      timeout -k 10 300 python tools/bench_train.py > "$OUT/train.json" 2> "$OUT/train.err"
+      rc=$?; echo "train rc=$rc"; if [ $rc -ne 0 ]; then tail -3 "$OUT/train.err"; exit $rc; fi
+      tail -c 600 "$OUT/train.json"; echo ;;
+    *) echo "unknown stage $st"; exit 2 ;;
+  esac
+done
