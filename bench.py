@@ -369,22 +369,23 @@ def main():
             cnd = conds[i % len(timesteps)]
             xc, xi = hp.downsample_copies(x, 2, vws)
 
-            def mlp(xc_, wait=None):
+            def mlp(xc_, wait=None, start=None):
                 if not timed:
-                    return npred.forward_cond(xc_, cnd, pk, wait)
+                    return npred.forward_cond(xc_, cnd, pk, wait, start)
                 # on the stream the MLP runs on; device-scope fences (no L2 writeback bubble
                 # around the timed kernel) unless tools/knobs.py turned them off
                 e0, e1 = timing_event(), timing_event()
                 blob, bias = pk[:2]
                 e0.record()
                 nc_ = _hip.noise_mlp(xc_.reshape(-1, 3), cfg.global_points, cnd, blob, bias,
-                                     npred.precision_code, wait=wait).view(2 * C, -1, 3)
+                                     npred.precision_code, wait=wait, signal=start).view(2 * C, -1, 3)
                 e1.record()
                 ev.append((e0, e1))
                 return nc_
 
             x = dmod.hierarchical_step(hp, mlp, xc, xi, x_cat, x, src, 7.5, dp._coeffs(t, t_prev),
-                                       knn_ws, state, mlp_waits=dmod.MLP_WAITS)
+                                       knn_ws, state, mlp_waits=dmod.MLP_WAITS,
+                                       mlp_signals=dmod.MLP_SIGNALS)
 
         lctx = torch.cuda.stream(loop_stream) if overlap else contextlib.nullcontext()
         with lctx:

@@ -283,6 +283,17 @@ int pcst_noise_mlp_then_wait(const float* pts, int64_t P, int64_t points_per_clo
                              int64_t blob_bytes, const float* bias, float* out,
                              const uint32_t* flag, uint32_t value, uint32_t* counter, int32_t* err,
                              int64_t max_polls, void* stream);
+/* pcst_noise_mlp with optional cross-stream signalling folded into the launch (all optional):
+ * start_flag: *start_flag = start_value (agent-scope store) as the launch begins, i.e. once every
+ * kernel queued before it on `stream` has completed -- the producer side of pcst_signal_wait
+ * without a pcst_signal_write launch; wait_flag/value/counter/err/max_polls: as
+ * pcst_noise_mlp_then_wait.  Precision 2 folds both into the MLP kernel; other precisions use
+ * separate one-lane launches (same ordering). */
+int pcst_noise_mlp_ex(const float* pts, int64_t P, int64_t points_per_cloud, const float* cond,
+                      int64_t nclouds, const void* blob, int64_t blob_bytes, const float* bias,
+                      int precision, float* out, uint32_t* start_flag, uint32_t start_value,
+                      const uint32_t* wait_flag, uint32_t wait_value, uint32_t* wait_counter,
+                      int32_t* wait_err, int64_t max_polls, void* stream);
 
 /* CFG + DDIM update of guided_sample_loop (diffusion_model.py:248-260); eps_u == NULL gives
  * ddim_sample_loop's update (:283-290), source == NULL skips the source pull.  x_cat (optional,

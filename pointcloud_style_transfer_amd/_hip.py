@@ -60,6 +60,8 @@ SIGNATURES = {
     "pcst_noise_mlp": [_P, _I, _I, _P, _I, _P, _I, _P, ctypes.c_int, _P, _P],
     "pcst_noise_mlp_then_wait": [_P, _I, _I, _P, _I, _P, _I, _P, _P, _P, ctypes.c_uint32, _P, _P, _I,
                                  _P],
+    "pcst_noise_mlp_ex": [_P, _I, _I, _P, _I, _P, _I, _P, ctypes.c_int, _P, _P, ctypes.c_uint32, _P,
+                          ctypes.c_uint32, _P, _P, _I, _P],
     "pcst_cfg_ddim_step": [_P, _P, _P, _P, _I, _F, _F, _F, _F, _F, _P, _P, _P],
     "pcst_pointwise_linear": [_P, _I, _I, _P, _I, _P, _P, ctypes.c_int, _I, _P, _P],
     "pcst_voxel_center_dist": [_P, _I, _P, ctypes.c_float, _P, _P, _P, _P],
@@ -388,6 +390,14 @@ class DeviceSignal:
         _call("pcst_signal_wait", _ptr(self.flag), self.value, ctypes.c_void_p(self.flag.data_ptr() + 4),
               self.max_polls, ctypes.c_void_p(stream.cuda_stream))
 
+    def next_value(self):
+        """Advance the host counter for a write made by another launch (pcst_noise_mlp_ex's start
+        signal): returns (flag pointer, value) to pass to it."""
+        if self.value + 1 >= self.VALUE_LIMIT:
+            raise RuntimeError("DeviceSignal: value would wrap; use a fresh signal")
+        self.value += 1
+        return ctypes.c_void_p(self.flag.data_ptr()), ctypes.c_uint32(self.value)
+
     def wait_args(self):
         """(flag, value, counter, err, max_polls) for pcst_noise_mlp_then_wait: wait for the last
         signal."""
@@ -579,16 +589,26 @@ def noise_cond(t, style, freqs, wt, bt, ws_, bs, b4):
     return cond
 
 
-def noise_mlp(pts, points_per_cloud, cond, blob, bias, precision, out=None, wait=None):
+def noise_mlp(pts, points_per_cloud, cond, blob, bias, precision, out=None, wait=None,
+              signal=None):
     """pts [P,3] (P = clouds*points_per_cloud, cloud-major) -> eps [P,3].
     wait (a DeviceSignal signalled on another stream): work queued after the MLP on this stream
     is also ordered after that signal -- at precision 2 by the MLP's last work-group
-    (pcst_noise_mlp_then_wait), otherwise by a wait launch after it."""
+    (pcst_noise_mlp_then_wait), otherwise by a wait launch after it.
+    signal ((flag, value) from DeviceSignal.next_value()): the value is published as the MLP
+    launch begins (everything queued before it on this stream is then done) --
+    pcst_noise_mlp_ex's start signal."""
     require_device(pts, cond, blob, bias)
     pts = _f32(pts)
     P = pts.shape[0]
     if out is None:
         out = torch.empty(P, 3, dtype=torch.float32, device=pts.device)
+    if signal is not None:
+        fl, val = signal
+        w = wait.wait_args() if wait is not None else (None, 0, None, None, 0)
+        _call("pcst_noise_mlp_ex", _ptr(pts), P, points_per_cloud, _ptr(cond), cond.shape[0],
+              _ptr(blob), blob.numel(), _ptr(bias), precision, _ptr(out), fl, val, *w, _stream())
+        return out
     if wait is not None and precision == 2 and P > 0:
         _call("pcst_noise_mlp_then_wait", _ptr(pts), P, points_per_cloud, _ptr(cond), cond.shape[0],
               _ptr(blob), blob.numel(), _ptr(bias), _ptr(out), *wait.wait_args(), _stream())

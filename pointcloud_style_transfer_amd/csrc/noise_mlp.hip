@@ -1088,8 +1088,14 @@ __global__ __launch_bounds__(kPairThreads) void noise_mlp_pair16_kernel(
     const float* __restrict__ pts, int64_t P, int64_t T, const float* __restrict__ cond,
     int64_t nclouds, const char* __restrict__ blob, int nparts, const float* __restrict__ bias,
     float* __restrict__ out, const uint32_t* __restrict__ wflag, uint32_t wvalue,
-    uint32_t* __restrict__ wcount, int32_t* __restrict__ werr, int64_t wpolls) {
+    uint32_t* __restrict__ wcount, int32_t* __restrict__ werr, int64_t wpolls,
+    uint32_t* __restrict__ sflag, uint32_t svalue) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  // start signal (pcst_noise_mlp_ex): the launch has begun, so every kernel queued before it on
+  // this stream has completed (and released its writes at its end): one agent-scope store
+  // publishes that to a waiter on another stream without a signal launch of its own
+  if (sflag && blockIdx.x == 0 && threadIdx.x == 0)
+    __hip_atomic_store(sflag, svalue, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   char* X = smem + Streamer2::kSlots * kPart;
   float* sb = reinterpret_cast<float*>(X + Streamer2::kWaves * kXBytes);
   float* sc = sb + kBiasFloats;
@@ -1231,7 +1237,7 @@ extern "C" int pcst_noise_mlp(const float* pts, int64_t P, int64_t points_per_cl
     hipLaunchKernelGGL(noise_mlp_pair16_kernel, dim3((unsigned)cdiv(P, 128)), dim3(kPairThreads),
                        lds, s, pts, P, points_per_cloud, cond, nclouds, (const char*)blob,
                        (int)(blob_bytes / kPart), bias, out, (const uint32_t*)nullptr, 0u,
-                       (uint32_t*)nullptr, (int32_t*)nullptr, (int64_t)0);
+                       (uint32_t*)nullptr, (int32_t*)nullptr, (int64_t)0, (uint32_t*)nullptr, 0u);
   } else if (precision == 1) {
     const size_t lds = Streamer2::kSlots * kPart + Streamer2::kWaves * kXBytes +
                        (kBiasFloats + kCondSlots * 256) * sizeof(float);
@@ -1260,7 +1266,48 @@ extern "C" int pcst_noise_mlp_then_wait(const float* pts, int64_t P, int64_t poi
   hipLaunchKernelGGL(noise_mlp_pair16_kernel, dim3((unsigned)cdiv(P, 128)), dim3(kPairThreads), lds,
                      as_stream(stream), pts, P, points_per_cloud, cond, nclouds, (const char*)blob,
                      (int)(blob_bytes / kPart), bias, out, flag, value, counter, err,
-                     max_polls > 0 ? max_polls : (int64_t)kMlpWaitPolls);
+                     max_polls > 0 ? max_polls : (int64_t)kMlpWaitPolls, (uint32_t*)nullptr, 0u);
   PCST_LAUNCH_CHECK("noise_mlp_then_wait");
+  return PCST_OK;
+}
+
+namespace pcst {
+__global__ void mlp_start_signal_kernel(uint32_t* flag, uint32_t value) {
+  if (threadIdx.x == 0) __hip_atomic_store(flag, value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+}  // namespace pcst
+
+extern "C" int pcst_noise_mlp_ex(const float* pts, int64_t P, int64_t points_per_cloud,
+                                 const float* cond, int64_t nclouds, const void* blob,
+                                 int64_t blob_bytes, const float* bias, int precision, float* out,
+                                 uint32_t* start_flag, uint32_t start_value,
+                                 const uint32_t* wait_flag, uint32_t wait_value,
+                                 uint32_t* wait_counter, int32_t* wait_err, int64_t max_polls,
+                                 void* stream) {
+  if (precision != 2 || P == 0) {  // no fused form: the same ordering by separate launches
+    if (start_flag) {
+      hipLaunchKernelGGL(mlp_start_signal_kernel, dim3(1), dim3(64), 0, as_stream(stream), start_flag,
+                         start_value);
+      PCST_LAUNCH_CHECK("noise_mlp_ex: start signal");
+    }
+    const int rc = pcst_noise_mlp(pts, P, points_per_cloud, cond, nclouds, blob, blob_bytes, bias,
+                                  precision, out, stream);
+    if (rc != PCST_OK || !wait_flag) return rc;
+    return pcst_signal_wait(wait_flag, wait_value, wait_err, max_polls, stream);
+  }
+  PCST_CHECK_ARG(P > 0 && points_per_cloud > 0 && nclouds > 0, "noise_mlp_ex: bad shape");
+  PCST_CHECK_ARG(P <= points_per_cloud * nclouds, "noise_mlp_ex: P exceeds clouds*points");
+  PCST_CHECK_ARG(blob_bytes == pcst_noise_mlp_blob_bytes(2), "noise_mlp_ex: blob size %lld != %lld",
+                 (long long)blob_bytes, (long long)pcst_noise_mlp_blob_bytes(2));
+  PCST_CHECK_ARG(((uintptr_t)blob & 15) == 0, "noise_mlp_ex: blob must be 16-byte aligned");
+  PCST_CHECK_ARG(!wait_flag || wait_counter, "noise_mlp_ex: a wait needs its counter");
+  const size_t lds = Streamer2::kSlots * kPart + Streamer2::kWaves * kXBytes +
+                     (kBiasFloats + kCondSlots * 256) * sizeof(float);
+  hipLaunchKernelGGL(noise_mlp_pair16_kernel, dim3((unsigned)cdiv(P, 128)), dim3(kPairThreads), lds,
+                     as_stream(stream), pts, P, points_per_cloud, cond, nclouds, (const char*)blob,
+                     (int)(blob_bytes / kPart), bias, out, wait_flag, wait_value, wait_counter,
+                     wait_err, max_polls > 0 ? max_polls : (int64_t)kMlpWaitPolls, start_flag,
+                     start_value);
+  PCST_LAUNCH_CHECK("noise_mlp_ex");
   return PCST_OK;
 }

@@ -185,16 +185,17 @@ class NoisePredictor(nn.Module):
                     or (style_feat.requires_grad and torch.is_grad_enabled()))
 
     def forward_cond(self, noisy_points: torch.Tensor, cond: torch.Tensor,
-                     packed: Optional[tuple] = None, wait=None) -> torch.Tensor:
+                     packed: Optional[tuple] = None, wait=None, signal=None) -> torch.Tensor:
         """The fused inference forward with precomputed conditioning rows (`cond()` of the
         same timesteps and style features): the sampling loops compute every step's rows in one
         launch before the loop.  `packed` (this module's `packed()`, fetched once before a loop
         that does not change the weights) skips the per-call weight-version check.  `wait` (a
-        DeviceSignal): later work on this stream also waits for it (_hip.noise_mlp)."""
+        DeviceSignal): later work on this stream also waits for it; `signal` (a DeviceSignal's
+        next_value()): published as the launch begins (_hip.noise_mlp)."""
         B, N, _ = noisy_points.shape
         blob, bias = (packed if packed is not None else self.packed())[:2]
         out = _hip.noise_mlp(noisy_points.reshape(B * N, 3), N, cond, blob, bias,
-                             self.precision_code, wait=wait)
+                             self.precision_code, wait=wait, signal=signal)
         return out.view(B, N, 3)
 
     def forward(self, noisy_points: torch.Tensor, timestep: torch.Tensor,
@@ -335,19 +336,25 @@ class StepState:
                 "the voxel output it waited for never signalled); the loop's output is invalid")
 
 
-def hierarchical_eps(hp, mlp, xc, xi, x_cat, knn_ws=None, state=None, mlp_waits=False):
+def hierarchical_eps(hp, mlp, xc, xi, x_cat, knn_ws=None, state=None, mlp_waits=False,
+                     mlp_signals=False):
     """eps for the CFG batch: mlp(xc) on the current stream, upsampled to the full clouds by
     kNN-3 (HierarchicalProcessor.upsample_knn).  With a StepState (and a preallocated
     workspace) the kNN build runs on its side stream, overlapping the MLP, with its work-groups
-    held to an LDS floor of KNN_BUILD_LDS_FLOOR bytes; the query waits for it."""
+    held to an LDS floor of KNN_BUILD_LDS_FLOOR bytes; the query waits for it.  mlp_signals: the
+    MLP launch itself publishes the loop -> side flag as it begins (mlp takes start=)."""
     if state is None:
         return hp.upsample_knn(mlp(xc), x_cat, xi)
     main = torch.cuda.current_stream()
     side = state.side
     ready, built = state.ready_ev, state.built_ev
+    start = None
     if KERNEL_SIGNAL:  # main -> side by a kernel-side flag: no event marker on the loop's queue
         ready = state.ready_sig
-        ready.signal(main)
+        if mlp_signals:
+            start = ready.next_value()  # written by the MLP launch (pcst_noise_mlp_ex)
+        else:
+            ready.signal(main)
     else:
         ready.record(main)
     ready.wait(side)
@@ -357,10 +364,11 @@ def hierarchical_eps(hp, mlp, xc, xi, x_cat, knn_ws=None, state=None, mlp_waits=
         handle = _hip.knn3_build(x_cat, xi, knn_ws, knn_build_lds_floor(xc.shape[0] * xc.shape[1]),
                                  KNN_BUILD_MAX_WG)
         built.signal(side) if BUILT_SIGNAL else built.record(side)
+    kw = {"start": start} if start is not None else {}
     if BUILT_SIGNAL and mlp_waits:  # the MLP's last work-group waits for the build's flag
-        nc = mlp(xc, built)
+        nc = mlp(xc, built, **kw)
     else:
-        nc = mlp(xc)
+        nc = mlp(xc, **kw)
         built.wait(main)
     return _hip.knn3_query(nc, handle)
 
@@ -375,13 +383,13 @@ SEARCH_BESIDE_MLP = False
 
 
 def hierarchical_step(hp, mlp, xc, xi, x_cat, x, source, guidance_scale, coeffs, knn_ws=None,
-                      state=None, mlp_waits=False):
+                      state=None, mlp_waits=False, mlp_signals=False):
     """One guided step of the hierarchical branch (diffusion_model.py:240-260): eps of the CFG
     batch (mlp(xc) upsampled by kNN-3), then the fused CFG + DDIM update of x (x_cat takes the
     new x twice).  Returns the new x.  state: a StepState (overlapped layout) or None."""
     C = x.shape[0]
     if state is None or not SEARCH_BESIDE_MLP:
-        eps = hierarchical_eps(hp, mlp, xc, xi, x_cat, knn_ws, state, mlp_waits)
+        eps = hierarchical_eps(hp, mlp, xc, xi, x_cat, knn_ws, state, mlp_waits, mlp_signals)
         return _hip.cfg_ddim_step(x, eps[:C], eps[C:], source, guidance_scale, coeffs, x_cat=x_cat)
     main = torch.cuda.current_stream()
     side = state.side
@@ -418,6 +426,9 @@ KERNEL_SIGNAL = True
 # tail, so its measured duration (the bench's roofline) is no longer the MLP's own.  Off.
 BUILT_SIGNAL = True
 MLP_WAITS = False
+# The loop -> side flag written by the MLP launch as it begins (pcst_noise_mlp_ex's start signal)
+# instead of a one-lane signal launch between the voxel emit and the MLP on the loop's queue.
+MLP_SIGNALS = True
 class _TorchEvent:
     """torch.cuda.Event with the DeviceEvent interface (DEVICE_EVENTS = False: A/B runs)."""
 
@@ -587,7 +598,8 @@ class DiffusionProcess:
                     t_in = t_rows[i]
                     if conds is not None:
                         cond_i = conds[i]
-                        mlp = lambda c, wait=None: npred.forward_cond(c, cond_i, pk, wait)  # noqa: E731
+                        mlp = lambda c, wait=None, start=None: npred.forward_cond(  # noqa: E731
+                            c, cond_i, pk, wait, start)
                     else:
                         mlp = lambda c: npred(c, t_in, style_in)  # noqa: E731
                     coeffs = self._coeffs(t, t_prevs[i])
@@ -595,7 +607,8 @@ class DiffusionProcess:
                         xc, xi = hp.downsample_copies(x, 2, vws)
                         x = hierarchical_step(hp, mlp, xc, xi, x_cat, x, source, guidance_scale,
                                               coeffs, ws, state,
-                                              mlp_waits=MLP_WAITS and conds is not None)
+                                              mlp_waits=MLP_WAITS and conds is not None,
+                                              mlp_signals=MLP_SIGNALS and conds is not None)
                     else:
                         eps = mlp(x_cat)
                         x = _hip.cfg_ddim_step(x, eps[:B], eps[B:], source, guidance_scale,

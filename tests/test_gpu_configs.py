@@ -447,3 +447,43 @@ def test_loop_vs_oracle_50_steps_120k(det_state, golden, precision, mult):
     assert ch <= mult * CHAOS_FLOOR_50["chamfer"]
     assert p999 <= mult * CHAOS_FLOOR_50["p999_abs"]
     assert mx <= mult * CHAOS_FLOOR_50["max_abs"]
+
+
+@pytest.mark.parametrize("precision,mult", [("bf16", 1.5)])
+def test_loop_vs_oracle_1000_steps_120k(det_state, golden, precision, mult):
+    """BASELINE configs[1] as written -- the full 1000-step schedule (every t from 999 to 0,
+    /root/reference/models/diffusion_model.py:224-261), bf16 noise MLP (the mode bench.py
+    measures), 120k lidar-like cloud, guidance 7.5 -- against the committed 1000-step oracle output
+    (tests/golden/gen_oracle_loop.py 1000) on the same x_T and counter-keyed draws.  Bound: 1.5x
+    the loop's own 1000-step chaos floor (the oracle against itself from x_T moved by one ulp,
+    tools/chaos_floor.py -> profiles/r04/chaos_floor.json) for the metrics.py:20-44 Chamfer, the
+    99.9th percentile and the maximum of |hip - oracle|."""
+    from detweights import load_into
+    from pointcloud_style_transfer_amd import rng
+    from pointcloud_style_transfer_amd.config.config import Config
+    from pointcloud_style_transfer_amd.evaluation.metrics import PointCloudMetrics
+    from pointcloud_style_transfer_amd.models.diffusion_model import (DiffusionProcess,
+                                                                        PointCloudDiffusionModel)
+    from pointcloud_style_transfer_amd.synthetic import standard_normal
+
+    ref = torch.from_numpy(golden("oracle_loop120k_1000.npz")["x_1000"]).cuda()
+    cfg = Config(make_dirs=False, precision=precision)
+    model = PointCloudDiffusionModel(cfg)
+    load_into(model)
+    model = model.cuda().eval()
+    dp = DiffusionProcess(cfg, device="cuda")
+    src, cond = _clouds(1000, 1, 120000).cuda(), _clouds(2000, 1, 120000).cuda()
+    xT = torch.from_numpy(standard_normal(3000, (1, 120000, 3))).cuda()
+    with rng.replay(rng.CounterRNG(6000)):
+        out = dp.guided_sample_loop(model, src, cond, 1000, 7.5, x_T=xT)
+    ch = float(PointCloudMetrics().chamfer_distance(out, ref)[0])
+    d = (out - ref).abs().flatten().double()
+    p999 = float(torch.quantile(d, 0.999))
+    mx = float(d.max())
+    fl = CHAOS_FLOOR_1000
+    print(f"1000-step 120k {precision}: chamfer_vs_oracle {ch:.3e} ({ch / fl['chamfer']:.2f} x floor), "
+          f"p999 {p999:.3e} ({p999 / fl['p999_abs']:.2f} x), max {mx:.3e} ({mx / fl['max_abs']:.2f} x), "
+          f"within 1e-3 abs {(d <= 1e-3).double().mean():.6f}")
+    assert ch <= mult * fl["chamfer"]
+    assert p999 <= mult * fl["p999_abs"]
+    assert mx <= mult * fl["max_abs"]

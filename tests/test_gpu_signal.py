@@ -164,3 +164,68 @@ def test_two_loops_on_two_threads_match_serial():
     torch.cuda.synchronize()
     for k in range(2):
         assert torch.equal(conc[k], serial[k]), k
+
+
+def test_mlp_start_signal_orders_the_side_stream():
+    """pcst_noise_mlp_ex's start signal (the MLP launch publishes the loop -> side flag as it
+    begins): the side stream's work waits for it and sees what the loop stream wrote before the
+    MLP; the MLP's rows equal the plain launch's; f32 precision takes the separate-launch form."""
+    from pointcloud_style_transfer_amd import _hip
+    from pointcloud_style_transfer_amd.config.config import Config
+    from pointcloud_style_transfer_amd.models.diffusion_model import NoisePredictor
+
+    dev = torch.device("cuda", 0)
+    loop = torch.cuda.Stream(device=dev)
+    side = torch.cuda.Stream(device=dev)
+    for prec in ("bf16", "fp32"):
+        torch.manual_seed(5)
+        npred = NoisePredictor(Config(make_dirs=False, precision=prec)).to(dev).eval()
+        pts = torch.randn(2 * 4096, 3, device=dev)
+        with torch.no_grad():
+            cond = npred.cond(torch.tensor([7, 7], device=dev), torch.randn(2, 256, device=dev))
+            blob, bias = npred.packed()[:2]
+            ref = _hip.noise_mlp(pts, 4096, cond, blob, bias, npred.precision_code)
+            sig = _hip.DeviceSignal(dev, max_polls=1 << 24)
+            buf = torch.zeros(8 << 20, device=dev)
+            loop.wait_stream(torch.cuda.current_stream())
+            side.wait_stream(torch.cuda.current_stream())
+            outs = []
+            for rep in range(3):
+                with torch.cuda.stream(loop):
+                    a = torch.randn(2048, 2048, device=dev)
+                    for _ in range(3):
+                        a = a @ a.T / 2048.0  # a delay on the loop stream before the MLP
+                    buf.fill_(float(rep + 1))
+                    start = sig.next_value()
+                    sig.wait(side)
+                    with torch.cuda.stream(side):
+                        seen = buf.clone()  # ordered after the flag, hence after the fill
+                    out = _hip.noise_mlp(pts, 4096, cond, blob, bias, npred.precision_code,
+                                         signal=start)
+                outs.append((out, seen, rep))
+            torch.cuda.synchronize()
+        sig.check()
+        assert int(sig.flag[0].item()) == 3
+        for out, seen, rep in outs:
+            assert torch.equal(out, ref)
+            assert bool((seen == float(rep + 1)).all()), (prec, rep)
+
+
+def test_guided_loop_mlp_start_signal_bit_identical(monkeypatch):
+    """The sampling loop with the loop -> side flag written by the MLP launch (MLP_SIGNALS, the
+    product) gives the bits of the separate signal launch."""
+    from pointcloud_style_transfer_amd.models import diffusion_model as dm
+    from pointcloud_style_transfer_amd.synthetic import lidar_like_cloud, standard_normal
+
+    dev = torch.device("cuda", 0)
+    cfg, model, dp = _small_model(dev)
+    src = torch.from_numpy(lidar_like_cloud(1000, 16384)[None]).to(dev)
+    cond = torch.from_numpy(lidar_like_cloud(2000, 16384)[None]).to(dev)
+    xT = torch.from_numpy(standard_normal(3000, (1, 16384, 3))).to(dev)
+    outs = []
+    with torch.no_grad():
+        for on in (True, False):
+            monkeypatch.setattr(dm, "MLP_SIGNALS", on)
+            torch.manual_seed(7)
+            outs.append(dp.guided_sample_loop(model, src, cond, 8, 7.5, x_T=xT))
+    assert torch.equal(outs[0], outs[1])

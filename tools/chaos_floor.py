@@ -8,6 +8,10 @@ from the oracle is measured against.
 CPU only (test infrastructure: imports oracle/).  Writes profiles/r03/chaos_floor.json.
 
     python tools/chaos_floor.py [--steps 10 50] [--weights det|seed0]
+    python tools/chaos_floor.py --steps 1000 --base-npz tests/golden/oracle_loop120k_1000.npz \
+        --out profiles/r04/chaos_floor.json
+(--base-npz: the unperturbed run is the committed oracle output `x_S` of that file -- the same
+oracle, inputs and draws -- so only the perturbed run is computed.)
 """
 from __future__ import annotations
 
@@ -46,6 +50,7 @@ def main():
     ap.add_argument("--steps", type=int, nargs="+", default=[10, 50])
     ap.add_argument("--weights", default="det", choices=["det", "seed0"])
     ap.add_argument("--out", default=os.path.join(REPO, "profiles", "r03", "chaos_floor.json"))
+    ap.add_argument("--base-npz", default=None)
     args = ap.parse_args()
     from oracle import oracle as O
     from pointcloud_style_transfer_amd import rng
@@ -83,8 +88,11 @@ def main():
             res["runs"] = old.get("runs", {})
     for S in args.steps:
         t0 = time.perf_counter()
-        base = O.guided_loop_counter(sd, src, cond, xT, S, rng.CounterRNG(6000))
         pert = O.guided_loop_counter(sd, src, cond, xT_p, S, rng.CounterRNG(6000))
+        if args.base_npz:
+            base = np.load(args.base_npz)[f"x_{S}"]
+        else:
+            base = O.guided_loop_counter(sd, src, cond, xT, S, rng.CounterRNG(6000))
         r = metrics(pert, base)
         r["seconds"] = round(time.perf_counter() - t0, 1)
         res["runs"][str(S)] = r

@@ -36,7 +36,8 @@ def main():
     G = cfg.global_points
     src = torch.from_numpy(lidar_like_cloud(1000, 120000)[None]).to(dev)
     x = torch.from_numpy(standard_normal(3000, (1, 120000, 3))).to(dev)
-    loop, side = dmod.step_streams(dev)
+    state = dmod.StepState(dev)
+    loop, side = state.loop, state.side
     loop.wait_stream(torch.cuda.current_stream())
     with torch.no_grad(), torch.cuda.stream(loop):
         style_in = torch.zeros(2, 256, device=dev)
@@ -64,7 +65,7 @@ def main():
         timeit("event record", lambda: ev.record(loop))
         timeit("event wait", lambda: ev.wait(side))
         timeit("hierarchical_eps", lambda: dmod.hierarchical_eps(
-            hp, lambda c: npred.forward_cond(c, conds[0]), xc, xi, x_cat, ws, side))
+            hp, lambda c: npred.forward_cond(c, conds[0]), xc, xi, x_cat, ws, state))
 
 
 if __name__ == "__main__":

@@ -30,7 +30,8 @@ with torch.no_grad():
     t_rows = torch.tensor(ts).repeat_interleave(2).view(S, 2).cuda()
     conds = npred.cond(t_rows.reshape(-1), style_in.repeat(S, 1)).view(S, 2, -1)
     x_cat = torch.cat([x, x]).contiguous()
-    loop, side = dmod.step_streams("cuda")
+    state = dmod.StepState("cuda")
+    loop, side = state.loop, state.side
     loop.wait_stream(torch.cuda.current_stream())
     with torch.cuda.stream(loop):
         ws = _hip.knn_workspace(2, 120000, cfg.global_points, device="cuda")
@@ -41,7 +42,7 @@ with torch.no_grad():
         tp = ts[i + 1] if t > 0 else -1
         xc, xi = hp.downsample_copies(x, 2)
         c = conds[i]
-        eps = dmod.hierarchical_eps(hp, lambda a: npred.forward_cond(a, c), xc, xi, x_cat, ws, side)
+        eps = dmod.hierarchical_eps(hp, lambda a: npred.forward_cond(a, c), xc, xi, x_cat, ws, state)
         x = _hip.cfg_ddim_step(x, eps[:1], eps[1:], src, 7.5, dp._coeffs(t, tp), x_cat=x_cat)
 
     with torch.cuda.stream(loop):

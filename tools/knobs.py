@@ -26,6 +26,8 @@ def apply():
         dm.DEVICE_EVENTS = e["PCST_DEVICE_EVENTS"] != "0"
     if "PCST_KNN_BUILD_MAX_WG" in e:
         dm.KNN_BUILD_MAX_WG = int(e["PCST_KNN_BUILD_MAX_WG"])
+    if "PCST_MLP_SIGNALS" in e:
+        dm.MLP_SIGNALS = e["PCST_MLP_SIGNALS"] != "0"
     if "PCST_MLP_WAITS" in e:
         dm.MLP_WAITS = e["PCST_MLP_WAITS"] != "0"
     if "PCST_BUILT_SIGNAL" in e:

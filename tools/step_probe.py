@@ -5,9 +5,10 @@
 Runs the bench's loop (120k cloud, CFG x2, 30k coarse, bf16, the first `steps` steps from t = 999,
 as the driver's invocation) in several layouts, interleaved over `reps` rounds, and prints the
 median ms/step of each:
-  bench   the product layout (loop stream + side-stream kNN build, device-scope events) with the
-          bench's two timing events around every MLP launch
-  noev    the same without the timing events
+  bench   the product layout (loop stream + side-stream kNN build, device-scope events, the loop ->
+          side flag written by the MLP launch) with the bench's two timing events around every MLP
+  msig    noev with the loop -> side flag written by the MLP launch (pcst_noise_mlp_ex)
+  noev    the same without the timing events, the loop -> side flag by a signal launch
   seq     one stream: the kNN build inline before the MLP, no events at all
   seq_ev  seq with the timing events around the MLP
   evready noev with the loop -> side dependency as an event instead of the kernel-side signal
@@ -47,8 +48,9 @@ def main():
     src = torch.from_numpy(lidar_like_cloud(1000, 120000)[None]).to(dev)
     cond = torch.from_numpy(lidar_like_cloud(2000, 120000)[None]).to(dev)
     xT = torch.from_numpy(standard_normal(3000, (1, 120000, 3))).to(dev)
-    loop, side = dmod.step_streams(dev)
-    loop.wait_stream(torch.cuda.current_stream())
+    state = dmod.StepState(dev)
+    loop = state.loop
+    state.begin(torch.cuda.current_stream())
     res = {m: [] for m in a.modes.split(",")}
     with torch.no_grad(), torch.cuda.stream(loop):
         style = model.style_encoder(hp.downsample(cond)[0])
@@ -73,12 +75,12 @@ def main():
                 t, tp = ts[i], ts[i + 1]
                 xc, xi = hp.downsample_copies(x, 2)
 
-                def mlp(c, wait=None):
+                def mlp(c, wait=None, start=None):
                     if timed:
                         e0, e1 = _hip.DeviceEvent(timing=True), _hip.DeviceEvent(timing=True)
                         e0.record()
                     out = _hip.noise_mlp(c.reshape(-1, 3), cfg.global_points, conds[i], blob, bias,
-                                         npred.precision_code, wait=wait).view(2, -1, 3)
+                                         npred.precision_code, wait=wait, signal=start).view(2, -1, 3)
                     if timed:
                         e1.record()
                     return out
@@ -86,13 +88,14 @@ def main():
                 if mode in ("srch", "nosrch"):
                     dmod.SEARCH_BESIDE_MLP = mode == "srch"
                     x = dmod.hierarchical_step(hp, mlp, xc, xi, x_cat, x, src, 7.5, dp._coeffs(t, tp),
-                                               ws, side)
+                                               ws, state)
                     continue
                 if mode.startswith("seq"):
                     h = _hip.knn3_build(x_cat, xi, ws, 0)
                     eps = _hip.knn3_query(mlp(xc), h)
                 else:
-                    eps = dmod.hierarchical_eps(hp, mlp, xc, xi, x_cat, ws, side, mlp_waits=mode == "mw")
+                    eps = dmod.hierarchical_eps(hp, mlp, xc, xi, x_cat, ws, state, mlp_waits=mode == "mw",
+                                                mlp_signals=mode in ("msig", "bench"))
                 x = _hip.cfg_ddim_step(x, eps[:1], eps[1:], src, 7.5, dp._coeffs(t, tp), x_cat=x_cat)
             return x
 
