@@ -230,11 +230,17 @@ int pcst_knn3_interp(const float* coarse, const float* orig, const int64_t* idx,
  * is below it gets the difference as dynamic LDS), so that a build on a side stream runs only on
  * CUs the noise MLP leaves idle; 0 = no floor (knn3_interp passes 0).  max_wg (> 0): at most
  * this many workgroups per build launch over all clouds (each kernel strides over its work), so a
- * side-stream build holds few CUs; 0 = the natural grids (knn3_interp passes 0). */
+ * side-stream build holds few CUs; 0 = the natural grids (knn3_interp passes 0).
+ * built_flag / built_value (query, finish, finish_cfg_ddim; NULL: none): the flag the build's
+ * producer publishes (pcst_signal_write) -- the consumer reads the workspace only if the flag
+ * holds the value when its work-groups start; otherwise (a cross-stream wait that gave up) it
+ * leaves the workspace alone and writes 0 for eps, so a timed-out wait can never make it read a
+ * half-built workspace.  The caller reports the wait's error word. */
 int pcst_knn3_build(const float* orig, const int64_t* idx, int64_t B, int64_t N, int64_t M,
                     int64_t lds_floor, int64_t max_wg, void* workspace, void* stream);
 int pcst_knn3_query(const float* coarse, const float* orig, int64_t B, int64_t N, int64_t M,
-                    float* out, void* workspace, void* stream);
+                    float* out, void* workspace, const uint32_t* built_flag, uint32_t built_value,
+                    void* stream);
 /* The query in two halves (the same bits as pcst_knn3_query).  search (after build; positions
  * only): every unknown row's three neighbours and float64 IDW weights into the workspace, so it
  * can run beside the noise MLP too; finish: out [B,N,3] from coarse [B,M,3] (the gathers and the
@@ -244,11 +250,13 @@ int pcst_knn3_query(const float* coarse, const float* orig, int64_t B, int64_t N
 int pcst_knn3_search(const float* orig, int64_t B, int64_t N, int64_t M, void* workspace,
                      void* stream);
 int pcst_knn3_finish(const float* coarse, int64_t B, int64_t N, int64_t M, float* out,
-                     void* workspace, void* stream);
+                     void* workspace, const uint32_t* built_flag, uint32_t built_value,
+                     void* stream);
 int pcst_knn3_finish_cfg_ddim(const float* coarse, int64_t B, int64_t N, int64_t M, void* workspace,
                               const float* x, const float* source, float guidance_scale,
                               float sqrt_1m_at, float sqrt_at_eps, float sqrt_aprev,
-                              float sqrt_1m_aprev, float* x_out, float* x_cat, void* stream);
+                              float sqrt_1m_aprev, float* x_out, float* x_cat,
+                              const uint32_t* built_flag, uint32_t built_value, void* stream);
 /* diagnostics of the last query on a workspace: out[0] error flag, out[1..B] query chunks per
  * cloud, out[1+B..2B] outlier queries per cloud (device int32 buffer of 1 + 2B) */
 int pcst_knn_stats(void* workspace, int64_t B, int64_t N, int64_t M, int32_t* out, void* stream);

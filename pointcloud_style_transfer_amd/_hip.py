@@ -49,10 +49,11 @@ SIGNATURES = {
     "pcst_knn3_build": [_P, _P, _I, _I, _I, _I, _I, _P, _P],
     "pcst_cfg_ddim_step_dcoef": [_P, _P, _P, _P, _I, ctypes.c_float, _P, _P, _P, _P],
     "pcst_voxel_downsample_copies_dseed": [_P, _I, _I, _I, _I, _P, _P, _P, _P, _P],
-    "pcst_knn3_query": [_P, _P, _I, _I, _I, _P, _P, _P],
+    "pcst_knn3_query": [_P, _P, _I, _I, _I, _P, _P, _P, ctypes.c_uint32, _P],
     "pcst_knn3_search": [_P, _I, _I, _I, _P, _P],
-    "pcst_knn3_finish": [_P, _I, _I, _I, _P, _P, _P],
-    "pcst_knn3_finish_cfg_ddim": [_P, _I, _I, _I, _P, _P, _P, _F, _F, _F, _F, _F, _P, _P, _P],
+    "pcst_knn3_finish": [_P, _I, _I, _I, _P, _P, _P, ctypes.c_uint32, _P],
+    "pcst_knn3_finish_cfg_ddim": [_P, _I, _I, _I, _P, _P, _P, _F, _F, _F, _F, _F, _P, _P, _P,
+                                  ctypes.c_uint32, _P],
     "pcst_knn_error": [_P, _I, _I, _I, _P, _P],
     "pcst_knn_stats": [_P, _I, _I, _I, _P, _P],
     "pcst_noise_mlp_blob_bytes": [ctypes.c_int],
@@ -486,8 +487,18 @@ def knn3_build(orig, idx, ws=None, lds_floor=0, max_wg=0):
     return (orig, idx, ws)
 
 
-def knn3_query(coarse, handle):
-    """Phase 2 of knn3_interp on the current stream: coarse [B,M,3] -> [B,N,3]."""
+def _built_args(built):
+    """(flag pointer, value) of the DeviceSignal the build's producer signals, or (NULL, 0)."""
+    if built is None:
+        return None, 0
+    return ctypes.c_void_p(built.flag.data_ptr()), ctypes.c_uint32(built.value)
+
+
+def knn3_query(coarse, handle, built=None):
+    """Phase 2 of knn3_interp on the current stream: coarse [B,M,3] -> [B,N,3].  built (the
+    DeviceSignal the side-stream build signalled): the query reads the workspace only if that
+    flag holds its last value (pcst.h: a timed-out wait then yields eps = 0, reported by the
+    signal's error word, instead of a read of a half-built workspace)."""
     orig, idx, ws = handle
     require_device(coarse)
     coarse = _f32(coarse)
@@ -496,7 +507,8 @@ def knn3_query(coarse, handle):
     if coarse.shape != (B, M, 3):
         raise RuntimeError(f"knn3_query: coarse {tuple(coarse.shape)} != {(B, M, 3)}")
     out = torch.empty(B, N, 3, dtype=torch.float32, device=orig.device)
-    _call("pcst_knn3_query", _ptr(coarse), _ptr(orig), B, N, M, _ptr(out), _ptr(ws), _stream())
+    _call("pcst_knn3_query", _ptr(coarse), _ptr(orig), B, N, M, _ptr(out), _ptr(ws),
+          *_built_args(built), _stream())
     return out
 
 
@@ -522,15 +534,18 @@ def _coarse_for(coarse, handle, name):
     return coarse, B, N, M
 
 
-def knn3_finish(coarse, handle):
-    """After knn3_search: coarse [B,M,3] -> [B,N,3], the same bits as knn3_query."""
+def knn3_finish(coarse, handle, built=None):
+    """After knn3_search: coarse [B,M,3] -> [B,N,3], the same bits as knn3_query (built: as
+    knn3_query)."""
     coarse, B, N, M = _coarse_for(coarse, handle, "knn3_finish")
     out = torch.empty(B, N, 3, dtype=torch.float32, device=coarse.device)
-    _call("pcst_knn3_finish", _ptr(coarse), B, N, M, _ptr(out), _ptr(handle[2]), _stream())
+    _call("pcst_knn3_finish", _ptr(coarse), B, N, M, _ptr(out), _ptr(handle[2]),
+          *_built_args(built), _stream())
     return out
 
 
-def knn3_finish_cfg_ddim(coarse, handle, x, source, guidance_scale, coeffs, x_cat=None, out=None):
+def knn3_finish_cfg_ddim(coarse, handle, x, source, guidance_scale, coeffs, x_cat=None, out=None,
+                         built=None):
     """After knn3_search on the CFG batch (2C clouds): cfg_ddim_step(x, eps[:C], eps[C:], ...)
     with eps = knn3_finish(coarse, handle), in one launch and with the same bits."""
     coarse, B, N, M = _coarse_for(coarse, handle, "knn3_finish_cfg_ddim")
@@ -546,7 +561,8 @@ def knn3_finish_cfg_ddim(coarse, handle, x, source, guidance_scale, coeffs, x_ca
         out = torch.empty_like(x)
     c1, c2, c3, c4 = (float(c) for c in coeffs)
     _call("pcst_knn3_finish_cfg_ddim", _ptr(coarse), B, N, M, _ptr(handle[2]), _ptr(x),
-          _ptr(source), float(guidance_scale), c1, c2, c3, c4, _ptr(out), _ptr(x_cat), _stream())
+          _ptr(source), float(guidance_scale), c1, c2, c3, c4, _ptr(out), _ptr(x_cat),
+          *_built_args(built), _stream())
     return out
 
 

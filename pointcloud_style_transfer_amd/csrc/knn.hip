@@ -807,6 +807,21 @@ __device__ __forceinline__ bool settled(const Query& me, const Box& cells, const
 }
 
 // One wave per chunk of <= 64 queries of one brick; the passes of the header comment.
+// The consumer side of the build -> query dependency (the `built_flag` / `built_value` of
+// pcst_knn3_query / _finish): the workspace is read only once the build's flag holds its value.
+// The stream waited for the flag before this launch (pcst_signal_wait, or the MLP's last
+// work-group); a wait that gave up lets the launch run anyway, and then every work-group finds
+// the flag short and leaves the workspace alone (its rows of the output get 0) instead of reading
+// a half-built one.  The caller raises on the wait's error word after the loop.
+__device__ __forceinline__ bool build_pending(const uint32_t* flag, uint32_t value) {
+  __shared__ int s_pending;
+  if (threadIdx.x == 0)
+    s_pending = flag != nullptr &&
+                __hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < value;
+  __syncthreads();
+  return s_pending != 0;
+}
+
 // amdgpu_waves_per_eu(4): 128 VGPRs (4 spilled) instead of 138, so 4 waves per SIMD (the LDS
 // allows 4 work-groups per CU) instead of 3: the ~5000 chunks of a step run in fewer rounds
 // (driver window 2379-2398 -> 2400-2429 steps/s, A/B on one box).
@@ -819,9 +834,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
     const float4* __restrict__ refs, const int32_t* __restrict__ qorder,
     const uint2* __restrict__ chunks, int64_t maxch, const int32_t* __restrict__ nchunk,
     int32_t* __restrict__ olist, float* __restrict__ obound, int32_t* __restrict__ ocount,
-    float* __restrict__ out, NbrRec* __restrict__ nbr) {
+    float* __restrict__ out, NbrRec* __restrict__ nbr, const uint32_t* __restrict__ bflag,
+    uint32_t bvalue) {
   __shared__ __attribute__((aligned(16))) float cand[4][4][kCandCap];
   const int b = blockIdx.y;
+  if (build_pending(bflag, bvalue)) {
+    if (!DEFER)
+      for (int64_t n = (int64_t)blockIdx.x * 256 + threadIdx.x; n < N * 3; n += (int64_t)gridDim.x * 256)
+        out[b * N * 3 + n] = 0.0f;
+    return;
+  }
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   Grid g;
   g.load(gp + b * 8);
@@ -1002,7 +1024,8 @@ __global__ __launch_bounds__(kOutlierThreads) void knn_outlier_kernel(
     const float* __restrict__ vals, int64_t N, int64_t M, const float* __restrict__ orig,
     const float4* __restrict__ refs, const int32_t* __restrict__ olist,
     const int32_t* __restrict__ ocount, const uint32_t* __restrict__ known,
-    float* __restrict__ out) {
+    float* __restrict__ out, const uint32_t* __restrict__ bflag, uint32_t bvalue) {
+  if (build_pending(bflag, bvalue)) return;
   constexpr int W = kOutlierThreads / 64;
   constexpr int Q = kOutlierThreads;
   constexpr int P = kOutPB;
@@ -1166,8 +1189,10 @@ __global__ __launch_bounds__(256) void knn_outlier_brick_kernel(
     const float* __restrict__ gp, int64_t Cpad, const uint64_t* __restrict__ start,
     const float4* __restrict__ refs, const int32_t* __restrict__ olist,
     const float* __restrict__ obound, const int32_t* __restrict__ ocount,
-    const uint32_t* __restrict__ known, float* __restrict__ out, NbrRec* __restrict__ nbr) {
+    const uint32_t* __restrict__ known, float* __restrict__ out, NbrRec* __restrict__ nbr,
+    const uint32_t* __restrict__ bflag, uint32_t bvalue) {
   const int b = blockIdx.y;
+  if (build_pending(bflag, bvalue)) return;
   // rows that are coarse points take the coarse value (result[idx] = coarse; the last coarse
   // row writing a point wins, as in the reference's index assignment); the deferred search
   // leaves them to the finish pass
@@ -1299,10 +1324,13 @@ __global__ __launch_bounds__(256) void knn_finish_kernel(const float* __restrict
                                                          int64_t N, int64_t M,
                                                          const uint32_t* __restrict__ known,
                                                          const NbrRec* __restrict__ nbr,
-                                                         float* __restrict__ out) {
+                                                         float* __restrict__ out,
+                                                         const uint32_t* __restrict__ bflag,
+                                                         uint32_t bvalue) {
+  const bool pending = build_pending(bflag, bvalue);
   for (int64_t r = blockIdx.x * 256ll + threadIdx.x; r < B * N; r += (int64_t)gridDim.x * 256) {
-    float o[3];
-    finish_row(vals, N, M, known, nbr, r / N, r % N, o);
+    float o[3] = {0.0f, 0.0f, 0.0f};
+    if (!pending) finish_row(vals, N, M, known, nbr, r / N, r % N, o);
     out[r * 3 + 0] = o[0]; out[r * 3 + 1] = o[1]; out[r * 3 + 2] = o[2];
   }
 }
@@ -1315,13 +1343,17 @@ __global__ __launch_bounds__(256) void knn_finish_cfg_ddim_kernel(
     const float* __restrict__ vals, int64_t C, int64_t N, int64_t M,
     const uint32_t* __restrict__ known, const NbrRec* __restrict__ nbr, const float* __restrict__ x,
     const float* __restrict__ src, float scale, float c1, float c2, float c3, float c4,
-    float* __restrict__ x_out, float* __restrict__ x_cat) {
+    float* __restrict__ x_out, float* __restrict__ x_cat, const uint32_t* __restrict__ bflag,
+    uint32_t bvalue) {
   const int64_t rows = C * N;
+  const bool pending = build_pending(bflag, bvalue);
   for (int64_t r = blockIdx.x * 256ll + threadIdx.x; r < rows; r += (int64_t)gridDim.x * 256) {
     const int64_t c = r / N, n = r % N;
-    float ec[3], eu[3];
-    finish_row(vals, N, M, known, nbr, c, n, ec);
-    finish_row(vals, N, M, known, nbr, C + c, n, eu);
+    float ec[3] = {0.0f, 0.0f, 0.0f}, eu[3] = {0.0f, 0.0f, 0.0f};
+    if (!pending) {
+      finish_row(vals, N, M, known, nbr, c, n, ec);
+      finish_row(vals, N, M, known, nbr, C + c, n, eu);
+    }
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
       const int64_t e = r * 3 + k;
@@ -1415,7 +1447,8 @@ extern "C" int pcst_knn3_build(const float* orig, const int64_t* idx, int64_t B,
 // The query and outlier launches: vals/out given -> IDW written to out; nbr given (deferred
 // search, positions only) -> every query row's weights into the workspace's neighbour records.
 static void launch_knn_query(const KnnWS& w, const float* coarse, const float* orig, int64_t B,
-                             int64_t N, int64_t M, float* out, NbrRec* nbr, hipStream_t s) {
+                             int64_t N, int64_t M, float* out, NbrRec* nbr, const uint32_t* bflag,
+                             uint32_t bvalue, hipStream_t s) {
   const int b = (int)B;
   // fixed grids stride over the chunk and outlier lists (their lengths live on the device)
   const unsigned gq = (unsigned)std::min<int64_t>(
@@ -1426,17 +1459,18 @@ static void launch_knn_query(const KnnWS& w, const float* coarse, const float* o
                           : (M == 2 ? knn_query_kernel<2, false> : knn_query_kernel<1, false>));
   hipLaunchKernelGGL(qk, dim3(gq, b), dim3(256), 0, s, orig, coarse, N, M, w.Cpad, w.gp, w.cnt,
                      w.refs, w.qorder, w.chunks, w.maxch, w.nchunk, w.olist, w.obound, w.ocount, out,
-                     nbr);
+                     nbr, bflag, bvalue);
   if (PCST_X_KNN_OUTLIER_EXHAUSTIVE && !nbr) {  // the exhaustive pass (A/B experiments)
     auto ok = M >= 3 ? knn_outlier_kernel<3>
                      : (M == 2 ? knn_outlier_kernel<2> : knn_outlier_kernel<1>);
     hipLaunchKernelGGL(ok, dim3(kOutlierBlocks, b), dim3(kOutlierThreads), 0, s, coarse, N, M, orig,
-                       w.refs, w.olist, w.ocount, w.known, out);
+                       w.refs, w.olist, w.ocount, w.known, out, bflag, bvalue);
   } else {
     auto ok = M >= 3 ? knn_outlier_brick_kernel<3>
                      : (M == 2 ? knn_outlier_brick_kernel<2> : knn_outlier_brick_kernel<1>);
     hipLaunchKernelGGL(ok, dim3(kOutlierBrickBlocks, b), dim3(256), 0, s, coarse, N, M, orig, w.gp,
-                       w.Cpad, w.cnt, w.refs, w.olist, w.obound, w.ocount, w.known, out, nbr);
+                       w.Cpad, w.cnt, w.refs, w.olist, w.obound, w.ocount, w.known, out, nbr, bflag,
+                       bvalue);
   }
 }
 
@@ -1446,12 +1480,13 @@ static void launch_knn_query(const KnnWS& w, const float* coarse, const float* o
                  name ": bad shape")
 
 extern "C" int pcst_knn3_query(const float* coarse, const float* orig, int64_t B, int64_t N,
-                               int64_t M, float* out, void* workspace, void* stream) {
+                               int64_t M, float* out, void* workspace, const uint32_t* built_flag,
+                               uint32_t built_value, void* stream) {
   PCST_KNN_SHAPE_CHECK("knn3_query");
   if (B == 0) return PCST_OK;
   PCST_CHECK_ARG(coarse && orig && out && workspace, "knn3_query: null pointer");
   KnnWS w = carve_knn(workspace, B, N, M);
-  launch_knn_query(w, coarse, orig, B, N, M, out, nullptr, as_stream(stream));
+  launch_knn_query(w, coarse, orig, B, N, M, out, nullptr, built_flag, built_value, as_stream(stream));
   PCST_LAUNCH_CHECK("knn3_query");
   return PCST_OK;
 }
@@ -1462,20 +1497,21 @@ extern "C" int pcst_knn3_search(const float* orig, int64_t B, int64_t N, int64_t
   if (B == 0) return PCST_OK;
   PCST_CHECK_ARG(orig && workspace, "knn3_search: null pointer");
   KnnWS w = carve_knn(workspace, B, N, M);
-  launch_knn_query(w, nullptr, orig, B, N, M, nullptr, w.nbr, as_stream(stream));
+  launch_knn_query(w, nullptr, orig, B, N, M, nullptr, w.nbr, nullptr, 0u, as_stream(stream));
   PCST_LAUNCH_CHECK("knn3_search");
   return PCST_OK;
 }
 
 extern "C" int pcst_knn3_finish(const float* coarse, int64_t B, int64_t N, int64_t M, float* out,
-                                void* workspace, void* stream) {
+                                void* workspace, const uint32_t* built_flag, uint32_t built_value,
+                                void* stream) {
   PCST_KNN_SHAPE_CHECK("knn3_finish");
   if (B == 0) return PCST_OK;
   PCST_CHECK_ARG(coarse && out && workspace, "knn3_finish: null pointer");
   KnnWS w = carve_knn(workspace, B, N, M);
   const unsigned g = (unsigned)std::min<int64_t>(cdiv(B * N, 256), 4096);
   hipLaunchKernelGGL(knn_finish_kernel, dim3(g), dim3(256), 0, as_stream(stream), coarse, B, N, M,
-                     w.known, w.nbr, out);
+                     w.known, w.nbr, out, built_flag, built_value);
   PCST_LAUNCH_CHECK("knn3_finish");
   return PCST_OK;
 }
@@ -1484,7 +1520,8 @@ extern "C" int pcst_knn3_finish_cfg_ddim(const float* coarse, int64_t B, int64_t
                                          void* workspace, const float* x, const float* source,
                                          float guidance_scale, float sqrt_1m_at, float sqrt_at_eps,
                                          float sqrt_aprev, float sqrt_1m_aprev, float* x_out,
-                                         float* x_cat, void* stream) {
+                                         float* x_cat, const uint32_t* built_flag,
+                                         uint32_t built_value, void* stream) {
   PCST_KNN_SHAPE_CHECK("knn3_finish_cfg_ddim");
   PCST_CHECK_ARG(B % 2 == 0, "knn3_finish_cfg_ddim: B must be the CFG batch (2 x clouds)");
   if (B == 0) return PCST_OK;
@@ -1494,7 +1531,7 @@ extern "C" int pcst_knn3_finish_cfg_ddim(const float* coarse, int64_t B, int64_t
   const unsigned g = (unsigned)std::min<int64_t>(cdiv(C * N, 256), 4096);
   hipLaunchKernelGGL(knn_finish_cfg_ddim_kernel, dim3(g), dim3(256), 0, as_stream(stream), coarse,
                      C, N, M, w.known, w.nbr, x, source, guidance_scale, sqrt_1m_at, sqrt_at_eps,
-                     sqrt_aprev, sqrt_1m_aprev, x_out, x_cat);
+                     sqrt_aprev, sqrt_1m_aprev, x_out, x_cat, built_flag, built_value);
   PCST_LAUNCH_CHECK("knn3_finish_cfg_ddim");
   return PCST_OK;
 }
@@ -1504,7 +1541,7 @@ extern "C" int pcst_knn3_interp(const float* coarse, const float* orig, const in
                                 void* stream) {
   int rc = pcst_knn3_build(orig, idx, B, N, M, 0, 0, workspace, stream);
   if (rc) return rc;
-  return pcst_knn3_query(coarse, orig, B, N, M, out, workspace, stream);
+  return pcst_knn3_query(coarse, orig, B, N, M, out, workspace, nullptr, 0u, stream);
 }
 
 #ifdef KNN_TRACE

@@ -763,7 +763,10 @@ __global__ void dropout_grad_kernel(const float4* __restrict__ g, int64_t n4, ui
 }
 
 // ---- weight gradient with transposed LDS reads
-constexpr int kWS = 32;                 // m rows per slice
+#ifndef PCST_WGRAD_WS  // experiment builds may override (32 or 64)
+#define PCST_WGRAD_WS 32
+#endif
+constexpr int kWS = PCST_WGRAD_WS;      // m rows per slice
 constexpr int kWLdB = 2 * kXT + 64;     // LDS row bytes: 256 + 64 (row stride = 64 mod 256 B)
 
 // slice rows [m, m+32) x columns [c0, c0+128) of a row-major [*, Cn] matrix -> bf16 LDS image
@@ -772,12 +775,13 @@ struct WStage;
 
 template <>
 struct WStage<float> {  // Cn % 4 == 0: thread -> (column quad tid % 32, rows tid / 32 + 8 it)
-  float4 v[4];
+  static constexpr int kIt = kWS / 8;
+  float4 v[kIt];
   __device__ __forceinline__ void load(const float* __restrict__ S, int64_t mend, int Cn,
                                        int64_t m, int c0, int tid) {
     const int cq = (tid & 31) * 4;
 #pragma unroll
-    for (int it = 0; it < 4; ++it) {
+    for (int it = 0; it < kIt; ++it) {
       const int64_t row = m + (tid >> 5) + 8 * it;
       v[it] = (row < mend && c0 + cq < Cn) ? *reinterpret_cast<const float4*>(S + row * Cn + c0 + cq)
                                            : make_float4(0.f, 0.f, 0.f, 0.f);
@@ -786,7 +790,7 @@ struct WStage<float> {  // Cn % 4 == 0: thread -> (column quad tid % 32, rows ti
   __device__ __forceinline__ void store(char* D, int tid, float* csum) const {
     const int cq = (tid & 31) * 4;
 #pragma unroll
-    for (int it = 0; it < 4; ++it) {
+    for (int it = 0; it < kIt; ++it) {
       const int r = (tid >> 5) + 8 * it;
       h16x4 o;
       o[0] = (h16)v[it].x;
@@ -807,12 +811,13 @@ struct WStage<float> {  // Cn % 4 == 0: thread -> (column quad tid % 32, rows ti
 
 template <>
 struct WStage<uint16_t> {  // Cn % 8 == 0: thread -> (column octet tid % 16, rows tid / 16 + 16 it)
-  uint4 v[2];
+  static constexpr int kIt = kWS / 16;
+  uint4 v[kIt];
   __device__ __forceinline__ void load(const uint16_t* __restrict__ S, int64_t mend, int Cn,
                                        int64_t m, int c0, int tid) {
     const int co = (tid & 15) * 8;
 #pragma unroll
-    for (int it = 0; it < 2; ++it) {
+    for (int it = 0; it < kIt; ++it) {
       const int64_t row = m + (tid >> 4) + 16 * it;
       v[it] = (row < mend && c0 + co < Cn) ? *reinterpret_cast<const uint4*>(S + row * Cn + c0 + co)
                                            : make_uint4(0u, 0u, 0u, 0u);
@@ -821,7 +826,7 @@ struct WStage<uint16_t> {  // Cn % 8 == 0: thread -> (column octet tid % 16, row
   __device__ __forceinline__ void store(char* D, int tid, float* csum) const {
     const int co = (tid & 15) * 8;
 #pragma unroll
-    for (int it = 0; it < 2; ++it) {
+    for (int it = 0; it < kIt; ++it) {
       const int r = (tid >> 4) + 16 * it;
       *reinterpret_cast<uint4*>(D + r * kWLdB + co * 2) = v[it];
       if (csum) {
@@ -893,7 +898,7 @@ __global__ __launch_bounds__(256) void wgrad_ex_kernel(const TZ* __restrict__ dZ
       gx.load(X, me, I, k0 + kWS, i0, tid);
     }
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
+    for (int ks = 0; ks < kWS / 16; ++ks) {
       h16x8 a[2], b[2];
 #pragma unroll
       for (int u = 0; u < 2; ++u) {

@@ -370,7 +370,7 @@ def hierarchical_eps(hp, mlp, xc, xi, x_cat, knn_ws=None, state=None, mlp_waits=
     else:
         nc = mlp(xc, **kw)
         built.wait(main)
-    return _hip.knn3_query(nc, handle)
+    return _hip.knn3_query(nc, handle, built if BUILT_SIGNAL else None)
 
 
 # The query's neighbour search is positions-only too: with SEARCH_BESIDE_MLP the side stream runs

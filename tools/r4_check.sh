@@ -55,6 +55,35 @@ for st in "$@"; do
       timeout -k 10 300 python tools/bench_train.py > "$OUT/train.json" 2> "$OUT/train.err"
       rc=$?; echo "train rc=$rc"; if [ $rc -ne 0 ]; then tail -3 "$OUT/train.err"; exit $rc; fi
       tail -c 600 "$OUT/train.json"; echo ;;
+    trainpmc)
+      TB="tools/bench_train.py --steps 3 --warmup 1"
+      timeout -s KILL 200 rocprofv3 --pmc SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY \
+          SQ_ACTIVE_INST_ANY SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES --output-format csv -d "$OUT/psq" -o pmc -- \
+          python $TB > "$OUT/psq.log" 2>&1
+      rc=$?; echo "trainpmc sq rc=$rc"; if [ $rc -ne 0 ]; then tail -5 "$OUT/psq.log"; exit $rc; fi
+      for C in FETCH_SIZE WRITE_SIZE; do
+        timeout -s KILL 200 rocprofv3 --pmc $C --output-format csv -d "$OUT/pmc_$C" -o pmc -- \
+            python $TB > "$OUT/tpmc_$C.log" 2>&1
+        rc=$?; echo "trainpmc $C rc=$rc"; if [ $rc -ne 0 ]; then tail -5 "$OUT/tpmc_$C.log"; exit $rc; fi
+      done
+      python tools/pmc_summary.py "$OUT" gemm_bf | head -30 | tee "$OUT/train_traffic.txt"
+      for k in "gemm_bf_kernel<1" "gemm_bf_kernel<3" "gemm_bf_kernel<6" "gemm_bf_kernel<7" wgrad_ex_kernel; do
+        echo "== $k"; python tools/pmc_sq.py "$OUT" "$k"
+      done | tee "$OUT/train_sq.txt" ;;
+    trainab=*)
+      # trainab=v_a,v_b: bench_train.py with the product library and each experiment library
+      # pointcloud_style_transfer_amd/libpcst_hip_<v>.so, two alternating passes
+      VS=${st#trainab=}
+      for pass in 1 2; do
+        for v in prod ${VS//,/ }; do
+          if [ "$v" = prod ]; then lib=pointcloud_style_transfer_amd/libpcst_hip.so; else lib=pointcloud_style_transfer_amd/libpcst_hip_$v.so; fi
+          PCST_LIB=$lib timeout -k 10 300 python tools/bench_train.py > "$OUT/train_$v.$pass.json" 2> "$OUT/train_$v.$pass.err"
+          rc=$?; if [ $rc -ne 0 ]; then tail -3 "$OUT/train_$v.$pass.err"; exit $rc; fi
+          python -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print(sys.argv[2], d['ms_per_step'], d['final_loss'])" "$OUT/train_$v.$pass.json" "$v.$pass"
+        done
+      done ;;
+    qcap)
+      bash tools/knn_qcap_ab.sh "$TAG/qcap" || exit 1 ;;
     *) echo "unknown stage $st"; exit 2 ;;
   esac
 done
