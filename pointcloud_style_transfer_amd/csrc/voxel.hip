@@ -345,11 +345,11 @@ constexpr int kTieCap = 8192;
 #define VOX_CHUNK 1024
 #endif
 #ifndef VOX_REPS_BLOCKS
-#define VOX_REPS_BLOCKS 512
+#define VOX_REPS_BLOCKS 64
 #endif
 constexpr int kVoxChunk = VOX_CHUNK;      // points aggregated per workgroup in LDS
 constexpr int kVoxLds = 2 * kVoxChunk;    // LDS table slots (load factor <= 1/2)
-constexpr int kVoxRepsBlocks = VOX_REPS_BLOCKS;  // slot-range workgroups per cloud
+constexpr int kVoxRepsBlocks = VOX_REPS_BLOCKS;  // workgroups per cloud over the voxel list
 
 // Copies.  guided_sample_loop downsamples the CFG batch cat([x] * 2) (diffusion_model.py:244-247):
 // identical clouds.  With copies = k the input is the B distinct clouds and the output has the
@@ -362,6 +362,7 @@ struct VoxelFastWS {
   int32_t* sel;           // [R][4]: bin*, rem, need, U>T flag  (R = copies * B rows)
   int64_t* reps;          // [B][N]
   uint32_t* rhash;        // [B][N]
+  int32_t* vlist;         // [B][N]    occupied table slots in arrival order (cnt4[b][0] of them)
   unsigned long long* ties;  // [R][kTieCap] (key<<32 | id)
   // zeroed every call (one memset): counters, histograms, tables, rep flags
   int32_t* cnt4;          // [R][4]: U (of cloud r, rows r < B), selected, ties, err
@@ -395,6 +396,7 @@ static VoxelFastWS carve_voxel_fast(void* base, int64_t B, int64_t N, int64_t co
   w.sel = c.take<int32_t>(R * 4);
   w.reps = c.take<int64_t>(B * N);
   w.rhash = c.take<uint32_t>(B * N);
+  w.vlist = c.take<int32_t>(B * N);
   w.ties = c.take<unsigned long long>(R * kTieCap);
   w.cnt4 = c.take<int32_t>(R * 4);
   w.hist = c.take<uint32_t>(R * kSelBins);
@@ -442,7 +444,9 @@ __global__ __launch_bounds__(256) void voxf_insert_kernel(const float* __restric
                                                           uint32_t* __restrict__ tcnt, int B,
                                                           int copies, uint64_t seed_v,
                                                           const uint64_t* __restrict__ seed_p,
-                                                          uint32_t* __restrict__ hist) {
+                                                          uint32_t* __restrict__ hist,
+                                                          int32_t* __restrict__ cnt4,
+                                                          int32_t* __restrict__ vlist, int pack) {
   // Each workgroup first aggregates its kVoxChunk points in an LDS table (LDS atomics), then
   // publishes one global (sum, count) per distinct voxel: dense voxels see at most one global
   // atomic per workgroup instead of one per point.
@@ -484,11 +488,19 @@ __global__ __launch_bounds__(256) void voxf_insert_kernel(const float* __restric
     int64_t slot = mix32((uint32_t)kw) & (H - 1);
     for (;;) {
       const unsigned long long old = atomicCAS(&K[slot], 0ull, kw);
-      if (old == 0ull || old == kw) break;
+      if (old == 0ull) {  // a new voxel: list its slot (U = the list length, U <= N)
+        vlist[(int64_t)b * N + atomicAdd(&cnt4[b * 4 + 0], 1)] = (int32_t)slot;
+        break;
+      }
+      if (old == kw) break;
       slot = (slot + 1) & (H - 1);
     }
-    atomicAdd(&tsum[b * H + slot], lsum[i]);
-    atomicAdd(&tcnt[b * H + slot], lcnt[i]);
+    if (pack) {  // N < 2^20: (index sum << 20) | count in one 64-bit add (sum < 2^40)
+      atomicAdd(&tsum[b * H + slot], (lsum[i] << 20) | (unsigned long long)lcnt[i]);
+    } else {
+      atomicAdd(&tsum[b * H + slot], lsum[i]);
+      atomicAdd(&tcnt[b * H + slot], lcnt[i]);
+    }
   }
   // The pool-key histogram of every row of this cloud over EVERY point of the chunk (a pool
   // key depends on (seed, row, index) only); voxf_reps_kernel takes the representatives' keys
@@ -512,35 +524,26 @@ __global__ __launch_bounds__(256) void voxf_insert_kernel(const float* __restric
 
 // occupied slot -> representative trunc(f32(sum)/f32(count)) (Q6); list order = arrival order
 // (only the SET matters downstream: rows are emitted in point-index order).
-// Each representative also updates both selection histograms of every row of its cloud: its
-// voxel's key into hist2 (the U > T candidates), and its index's pool key out of hist (once per
-// distinct index: the first voxel to flag the index does it).
+// One listed voxel (voxf_insert_kernel's slot list) -> representative trunc(f32(sum)/f32(count))
+// (Q6) at its list position (arrival order: only the SET matters downstream, rows are emitted in
+// point-index order).  Each representative also updates both selection histograms of every row
+// of its cloud: its voxel's key into hist2 (the U > T candidates), and its index's pool key out of
+// hist (once per distinct index: the first voxel to flag the index does it).
 __global__ __launch_bounds__(256) void voxf_reps_kernel(
     const unsigned long long* __restrict__ tkey, const unsigned long long* __restrict__ tsum,
-    const uint32_t* __restrict__ tcnt, int64_t H, int N, int32_t* __restrict__ cnt4,
-    int64_t* __restrict__ reps, uint32_t* __restrict__ rhash, uint32_t* __restrict__ isrep,
-    int B, int copies, uint64_t seed_v, const uint64_t* __restrict__ seed_p,
-    uint32_t* __restrict__ hist, uint32_t* __restrict__ hist2) {
-  // one contiguous slot range per workgroup, one counter atomic per workgroup
+    const uint32_t* __restrict__ tcnt, int64_t H, int N, const int32_t* __restrict__ cnt4,
+    const int32_t* __restrict__ vlist, int pack, int64_t* __restrict__ reps,
+    uint32_t* __restrict__ rhash, uint32_t* __restrict__ isrep, int B, int copies, uint64_t seed_v,
+    const uint64_t* __restrict__ seed_p, uint32_t* __restrict__ hist, uint32_t* __restrict__ hist2) {
   const int b = blockIdx.y;
-  const int64_t chunk = (H + gridDim.x - 1) / gridDim.x;
-  const int64_t s0 = blockIdx.x * chunk, s1 = s0 + chunk < H ? s0 + chunk : H;
-  const unsigned long long* K = tkey + b * H;
-  uint32_t mine = 0;
-  for (int64_t s = s0 + threadIdx.x; s < s1; s += 256) mine += K[s] != 0ull;
-  __shared__ uint32_t sh[260];
-  __shared__ int base;
-  uint32_t tot;
-  uint32_t off = block_excl_scan_256(mine, sh, tot);
-  if (threadIdx.x == 0) base = tot ? atomicAdd(&cnt4[b * 4 + 0], (int)tot) : 0;
-  __syncthreads();
-  int k = base + (int)off;
+  const int U = cnt4[b * 4 + 0];
   const uint64_t seed = seed_p ? *seed_p : seed_v;
-  for (int64_t s = s0 + threadIdx.x; s < s1; s += 256) {
-    const unsigned long long kw = K[s];
-    if (!kw) continue;
-    const float fs = (float)(long long)tsum[b * H + s];
-    const float fc = (float)tcnt[b * H + s];
+  for (int k = blockIdx.x * 256 + threadIdx.x; k < U; k += gridDim.x * 256) {
+    const int64_t s = vlist[(int64_t)b * N + k];
+    const unsigned long long kw = tkey[b * H + s];
+    const unsigned long long v = tsum[b * H + s];
+    const float fs = (float)(long long)(pack ? (v >> 20) : v);
+    const float fc = (float)(pack ? (uint32_t)(v & 0xFFFFFull) : tcnt[b * H + s]);
     const int64_t r = (int64_t)__fdiv_rn(fs, fc);
     reps[(int64_t)b * N + k] = r;
     rhash[(int64_t)b * N + k] = (uint32_t)kw;
@@ -550,7 +553,6 @@ __global__ __launch_bounds__(256) void voxf_reps_kernel(
       atomicAdd(&hist2[(int64_t)row * kSelBins + (rand_key(seed, row, (int)((uint32_t)kw & 0x7fffffff)) >> 20)], 1u);
       if (first) atomicSub(&hist[(int64_t)row * kSelBins + (rand_key(seed, row + 0x10000, (int)r) >> 20)], 1u);
     }
-    ++k;
   }
 }
 
@@ -761,11 +763,13 @@ static int voxel_fast(const float* pts, int64_t B, int64_t N, int64_t copies, in
   hipLaunchKernelGGL(voxf_stats_zero_kernel, dim3(kStatBlocks + kVoxZeroBlocks, b), dim3(256), 0, s,
                      pts, n, w.mm, reinterpret_cast<uint4*>(w.cnt4), (int64_t)cdiv(zero, 16));
   const int cp = (int)copies;
+  const int pack = N < (1 << 20) ? 1 : 0;
   hipLaunchKernelGGL(voxf_insert_kernel, dim3((unsigned)cdiv(N, kVoxChunk), b), dim3(256), 0, s,
-                     pts, n, w.mm, T, w.H, w.tkey, w.tsum, w.tcnt, b, cp, seed, seed_p, w.hist);
-  hipLaunchKernelGGL(voxf_reps_kernel, dim3(kVoxRepsBlocks, b), dim3(256), 0, s, w.tkey, w.tsum,
-                     w.tcnt, w.H, n, w.cnt4, w.reps, w.rhash, w.isrep, b, cp, seed, seed_p, w.hist,
-                     w.hist2);
+                     pts, n, w.mm, T, w.H, w.tkey, w.tsum, w.tcnt, b, cp, seed, seed_p, w.hist, w.cnt4,
+                     w.vlist, pack);
+  hipLaunchKernelGGL(voxf_reps_kernel, dim3((unsigned)std::min<int64_t>(cdiv(N, 256), kVoxRepsBlocks), b),
+                     dim3(256), 0, s, w.tkey, w.tsum, w.tcnt, w.H, n, w.cnt4, w.vlist, pack, w.reps,
+                     w.rhash, w.isrep, b, cp, seed, seed_p, w.hist, w.hist2);
   hipLaunchKernelGGL(voxf_select_kernel, dim3(128, rows), dim3(256), 0, s, n, T, b, seed, seed_p,
                      w.hist, w.hist2, w.sel, w.cnt4, w.rhash, w.isrep, w.reps, w.ties, w.kcnt,
                      w.ktile, w.tiles);

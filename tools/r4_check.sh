@@ -82,6 +82,12 @@ for st in "$@"; do
           python -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print(sys.argv[2], d['ms_per_step'], d['final_loss'])" "$OUT/train_$v.$pass.json" "$v.$pass"
         done
       done ;;
+    b32prof)
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/b32prof" -o run -- \
+          python bench.py --gpus 1 --clouds-per-gpu 32 --steps 10 --warmup 3 --no-cpu-baseline --no-encoder \
+          --no-other-precision > "$OUT/b32prof.json" 2> "$OUT/b32prof.err"
+      rc=$?; echo "b32prof rc=$rc"; if [ $rc -ne 0 ]; then tail -5 "$OUT/b32prof.err"; exit $rc; fi
+      python tools/kstats.py "$OUT/b32prof/run_kernel_stats.csv" 25 | tee "$OUT/b32_kernel_top.txt" ;;
     qcap)
       bash tools/knn_qcap_ab.sh "$TAG/qcap" || exit 1 ;;
     *) echo "unknown stage $st"; exit 2 ;;
