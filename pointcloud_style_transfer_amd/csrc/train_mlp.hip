@@ -767,6 +767,9 @@ __global__ void dropout_grad_kernel(const float4* __restrict__ g, int64_t n4, ui
 #define PCST_WGRAD_WS 32
 #endif
 constexpr int kWS = PCST_WGRAD_WS;      // m rows per slice
+#ifndef PCST_WGRAD_PF  // experiment builds: 2 = two slices in flight (two register stages)
+#define PCST_WGRAD_PF 1
+#endif
 constexpr int kWLdB = 2 * kXT + 64;     // LDS row bytes: 256 + 64 (row stride = 64 mod 256 B)
 
 // slice rows [m, m+32) x columns [c0, c0+128) of a row-major [*, Cn] matrix -> bf16 LDS image
@@ -885,18 +888,7 @@ __global__ __launch_bounds__(256) void wgrad_ex_kernel(const TZ* __restrict__ dZ
   float csum[WStage<TZ>::kSumCols];
 #pragma unroll
   for (int u = 0; u < WStage<TZ>::kSumCols; ++u) csum[u] = 0.0f;
-  WStage<TZ> gz;
-  WStage<TX> gx;
-  gz.load(dZ, me, O, mb, o0, tid);
-  gx.load(X, me, I, mb, i0, tid);
-  for (int64_t k0 = mb; k0 < me; k0 += kWS) {
-    gz.store(Zs, tid, bias ? csum : nullptr);
-    gx.store(Xs, tid, nullptr);
-    __syncthreads();
-    if (k0 + kWS < me) {
-      gz.load(dZ, me, O, k0 + kWS, o0, tid);
-      gx.load(X, me, I, k0 + kWS, i0, tid);
-    }
+  auto mma = [&]() {
 #pragma unroll
     for (int ks = 0; ks < kWS / 16; ++ks) {
       h16x8 a[2], b[2];
@@ -911,8 +903,51 @@ __global__ __launch_bounds__(256) void wgrad_ex_kernel(const TZ* __restrict__ dZ
         for (int bn = 0; bn < 2; ++bn)
           acc[bm][bn] = mfma32_h16(a[bm], b[bn], acc[bm][bn]);
     }
+  };
+  WStage<TZ> gz;
+  WStage<TX> gx;
+  gz.load(dZ, me, O, mb, o0, tid);
+  gx.load(X, me, I, mb, i0, tid);
+#if PCST_WGRAD_PF == 2
+  // two slices in flight: the register stages alternate, each loaded two slices ahead
+  WStage<TZ> gz1;
+  WStage<TX> gx1;
+  gz1.load(dZ, me, O, mb + kWS, o0, tid);
+  gx1.load(X, me, I, mb + kWS, i0, tid);
+  for (int64_t k0 = mb; k0 < me; k0 += 2 * kWS) {
+    gz.store(Zs, tid, bias ? csum : nullptr);
+    gx.store(Xs, tid, nullptr);
+    __syncthreads();
+    if (k0 + 2 * kWS < me) {
+      gz.load(dZ, me, O, k0 + 2 * kWS, o0, tid);
+      gx.load(X, me, I, k0 + 2 * kWS, i0, tid);
+    }
+    mma();
+    __syncthreads();
+    // the odd slice (rows past me in the last one load as zeros: the MFMAs add nothing)
+    gz1.store(Zs, tid, bias ? csum : nullptr);
+    gx1.store(Xs, tid, nullptr);
+    __syncthreads();
+    if (k0 + 3 * kWS < me) {
+      gz1.load(dZ, me, O, k0 + 3 * kWS, o0, tid);
+      gx1.load(X, me, I, k0 + 3 * kWS, i0, tid);
+    }
+    mma();
     __syncthreads();
   }
+#else
+  for (int64_t k0 = mb; k0 < me; k0 += kWS) {
+    gz.store(Zs, tid, bias ? csum : nullptr);
+    gx.store(Xs, tid, nullptr);
+    __syncthreads();
+    if (k0 + kWS < me) {
+      gz.load(dZ, me, O, k0 + kWS, o0, tid);
+      gx.load(X, me, I, k0 + kWS, i0, tid);
+    }
+    mma();
+    __syncthreads();
+  }
+#endif
   float* pw = partW + (int64_t)chunk * O * I;
 #pragma unroll
   for (int bn = 0; bn < 2; ++bn) {
