@@ -375,6 +375,9 @@ __global__ __launch_bounds__(256) void gemm_ex_kernel(const TA* __restrict__ A, 
 #define PCST_GEMM_BK 32
 #endif
 constexpr int kBK = PCST_GEMM_BK;   // k slice (32 or 64)
+#ifndef PCST_GEMM_PF  // experiment builds: 2 = two slices in flight (two register stages)
+#define PCST_GEMM_PF 1
+#endif
 constexpr int kBLd = kBK + 8;       // LDS row, bf16 elements (+16 B pad: conflict-free row reads)
 constexpr int kCPR = kBK / 8;       // 16-byte chunks per row slice
 constexpr int kBIt = kCPR / 2;      // loads per thread per operand per slice
@@ -590,6 +593,22 @@ __global__ __launch_bounds__(256) void gemm_bf_kernel(const uint16_t* __restrict
   const int nk = K / kBK;
   BfRegs g;
   bf_load(ra, rb, va, vb, 0, g);
+#if PCST_GEMM_PF == 2
+  // two slices in flight (K % 64 == 0: nk is even): the register stages alternate, each loaded
+  // two slices ahead of its LDS store
+  BfRegs g1;
+  bf_load(ra, rb, va, vb, (uint32_t)(kBK * 2), g1);
+  for (int k = 0; k < nk; k += 2) {
+    bf_store(g, As0, Bs0, tid);
+    lds_barrier();
+    if (k + 2 < nk) bf_load(ra, rb, va, vb, (uint32_t)((k + 2) * kBK * 2), g);
+    bf_mma(As0, Bs0, wr, wc, l32, h, acc);
+    bf_store(g1, As1, Bs1, tid);
+    lds_barrier();
+    if (k + 3 < nk) bf_load(ra, rb, va, vb, (uint32_t)((k + 3) * kBK * 2), g1);
+    bf_mma(As1, Bs1, wr, wc, l32, h, acc);
+  }
+#else
   for (int k = 0; k < nk; ++k) {
     Row* As = (k & 1) ? As1 : As0;
     Row* Bs = (k & 1) ? Bs1 : Bs0;
@@ -598,6 +617,7 @@ __global__ __launch_bounds__(256) void gemm_bf_kernel(const uint16_t* __restrict
     if (k + 1 < nk) bf_load(ra, rb, va, vb, (uint32_t)((k + 1) * kBK * 2), g);
     bf_mma(As, Bs, wr, wc, l32, h, acc);
   }
+#endif
   __syncthreads();  // every wave's MFMA reads done before the epilogue reuses the LDS
   if (FAST)
     gemm_epilogue_fast<EP>(acc, reinterpret_cast<float (*)[kCLd]>(smem), M, O, m0, o0, args);
