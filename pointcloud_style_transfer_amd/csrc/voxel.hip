@@ -339,7 +339,12 @@ __global__ void vox_select_kernel(const float* __restrict__ pts, int N, int64_t 
 // The kept multiset is fixed by the seed, and so is the row order: the result does not
 // depend on the arrival order of any atomic (the style encoder's FPS start and ball query
 // read positions in this list, so the order matters there).
-constexpr int kSelBins = 4096;
+// Radix-select bins of the 32-bit subset keys (bin = key >> shift).  The kept set is the `need`
+// smallest (key, id) whatever the bin width.  Up to 4M points a row uses 1024 bins (shift 22;
+// round 4, was 4096): 4x fewer global histogram adds, ~candidates / 1024 boundary-bin ties per
+// row for emit to rank; larger clouds keep 4096 (the tie list holds kTieCap).
+constexpr int kSelBins = 4096;  // histogram stride per row (the most bins)
+static int vox_sel_shift(int64_t N) { return N <= (4ll << 20) ? 22 : 20; }
 constexpr int kTieCap = 8192;
 #ifndef VOX_CHUNK  // experiment builds may override
 #define VOX_CHUNK 1024
@@ -446,7 +451,9 @@ __global__ __launch_bounds__(256) void voxf_insert_kernel(const float* __restric
                                                           const uint64_t* __restrict__ seed_p,
                                                           uint32_t* __restrict__ hist,
                                                           int32_t* __restrict__ cnt4,
-                                                          int32_t* __restrict__ vlist, int pack) {
+                                                          int32_t* __restrict__ vlist, int pack,
+                                                          int sshift) {
+  const int nbins = 1 << (32 - sshift);
   // Each workgroup first aggregates its kVoxChunk points in an LDS table (LDS atomics), then
   // publishes one global (sum, count) per distinct voxel: dense voxels see at most one global
   // atomic per workgroup instead of one per point.
@@ -505,19 +512,19 @@ __global__ __launch_bounds__(256) void voxf_insert_kernel(const float* __restric
   // The pool-key histogram of every row of this cloud over EVERY point of the chunk (a pool
   // key depends on (seed, row, index) only); voxf_reps_kernel takes the representatives' keys
   // back out, leaving the histogram of the pool (the U < T candidates) without a launch of its
-  // own.  The LDS table above is reused as the 4096 bins (kVoxLds * 8 B >= 16 KiB).
+  // own.  The LDS table above is reused as the (at most 4096) bins (kVoxLds * 8 B >= 16 KiB).
   static_assert(kVoxLds * 2 >= kSelBins, "LDS table too small for the key histogram");
   uint32_t* lh = reinterpret_cast<uint32_t*>(lkey);
   const uint64_t seed = seed_p ? *seed_p : seed_v;
   for (int c = 0; c < copies; ++c) {
     const int row = c * B + b;
     __syncthreads();
-    for (int i = threadIdx.x; i < kSelBins; i += 256) lh[i] = 0u;
+    for (int i = threadIdx.x; i < nbins; i += 256) lh[i] = 0u;
     __syncthreads();
     for (int n = n0 + threadIdx.x; n < n1; n += 256)
-      atomicAdd(&lh[rand_key(seed, row + 0x10000, n) >> 20], 1u);
+      atomicAdd(&lh[rand_key(seed, row + 0x10000, n) >> sshift], 1u);
     __syncthreads();
-    for (int i = threadIdx.x; i < kSelBins; i += 256)
+    for (int i = threadIdx.x; i < nbins; i += 256)
       if (lh[i]) atomicAdd(&hist[(int64_t)row * kSelBins + i], lh[i]);
   }
 }
@@ -534,7 +541,8 @@ __global__ __launch_bounds__(256) void voxf_reps_kernel(
     const uint32_t* __restrict__ tcnt, int64_t H, int N, const int32_t* __restrict__ cnt4,
     const int32_t* __restrict__ vlist, int pack, int64_t* __restrict__ reps,
     uint32_t* __restrict__ rhash, uint32_t* __restrict__ isrep, int B, int copies, uint64_t seed_v,
-    const uint64_t* __restrict__ seed_p, uint32_t* __restrict__ hist, uint32_t* __restrict__ hist2) {
+    const uint64_t* __restrict__ seed_p, uint32_t* __restrict__ hist, uint32_t* __restrict__ hist2,
+    int sshift) {
   const int b = blockIdx.y;
   const int U = cnt4[b * 4 + 0];
   const uint64_t seed = seed_p ? *seed_p : seed_v;
@@ -550,8 +558,8 @@ __global__ __launch_bounds__(256) void voxf_reps_kernel(
     const bool first = atomicExch(&isrep[(int64_t)b * N + r], 1u) == 0u;
     for (int c = 0; c < copies; ++c) {
       const int row = c * B + b;
-      atomicAdd(&hist2[(int64_t)row * kSelBins + (rand_key(seed, row, (int)((uint32_t)kw & 0x7fffffff)) >> 20)], 1u);
-      if (first) atomicSub(&hist[(int64_t)row * kSelBins + (rand_key(seed, row + 0x10000, (int)r) >> 20)], 1u);
+      atomicAdd(&hist2[(int64_t)row * kSelBins + (rand_key(seed, row, (int)((uint32_t)kw & 0x7fffffff)) >> sshift)], 1u);
+      if (first) atomicSub(&hist[(int64_t)row * kSelBins + (rand_key(seed, row + 0x10000, (int)r) >> sshift)], 1u);
     }
   }
 }
@@ -603,7 +611,7 @@ __global__ __launch_bounds__(256) void voxf_select_kernel(
     int32_t* __restrict__ sel, int32_t* __restrict__ cnt4,
     const uint32_t* __restrict__ rhash, const uint32_t* __restrict__ isrep,
     const int64_t* __restrict__ reps, unsigned long long* __restrict__ ties,
-    uint32_t* __restrict__ kcnt, uint32_t* __restrict__ ktile, int64_t tiles) {
+    uint32_t* __restrict__ kcnt, uint32_t* __restrict__ ktile, int64_t tiles, int sshift) {
   const uint64_t seed = seed_p ? *seed_p : seed_v;
   const int row = blockIdx.y, cl = row % B;
   const int U = cnt4[cl * 4];
@@ -614,11 +622,12 @@ __global__ __launch_bounds__(256) void voxf_select_kernel(
   for (int i = threadIdx.x; i < kMarkTiles; i += 256) lt[i] = 0u;
   {
     constexpr int per = kSelBins / 256;
+    const int nbins = 1 << (32 - sshift);  // bins past nbins read as empty
     uint32_t v[per], s = 0;
     const uint32_t* hs = (U > T ? hist2 : hist) + (int64_t)row * kSelBins;
 #pragma unroll
     for (int k = 0; k < per; ++k) {
-      v[k] = hs[threadIdx.x * per + k];
+      v[k] = threadIdx.x * per + k < nbins ? hs[threadIdx.x * per + k] : 0u;
       s += v[k];
     }
     if (threadIdx.x == 0) { s_bstar = -1; s_rem = 0; }
@@ -652,7 +661,7 @@ __global__ __launch_bounds__(256) void voxf_select_kernel(
     for (int e = e0 + threadIdx.x; e < e1; e += 256) {
       uint32_t key, id;
       if (!voxf_cand(row, cl, e, N, U, T, seed, rhash, isrep, key, id)) continue;
-      const int bin = (int)(key >> 20);
+      const int bin = (int)(key >> sshift);
       if (bin < bstar) {
         voxf_mark(row, N, U > T ? R[id] : (int64_t)id, kcnt, ktile, tiles, lt);
       } else if (bin == bstar) {
@@ -764,15 +773,16 @@ static int voxel_fast(const float* pts, int64_t B, int64_t N, int64_t copies, in
                      pts, n, w.mm, reinterpret_cast<uint4*>(w.cnt4), (int64_t)cdiv(zero, 16));
   const int cp = (int)copies;
   const int pack = N < (1 << 20) ? 1 : 0;
+  const int sshift = vox_sel_shift(N);
   hipLaunchKernelGGL(voxf_insert_kernel, dim3((unsigned)cdiv(N, kVoxChunk), b), dim3(256), 0, s,
                      pts, n, w.mm, T, w.H, w.tkey, w.tsum, w.tcnt, b, cp, seed, seed_p, w.hist, w.cnt4,
-                     w.vlist, pack);
+                     w.vlist, pack, sshift);
   hipLaunchKernelGGL(voxf_reps_kernel, dim3((unsigned)std::min<int64_t>(cdiv(N, 256), kVoxRepsBlocks), b),
                      dim3(256), 0, s, w.tkey, w.tsum, w.tcnt, w.H, n, w.cnt4, w.vlist, pack, w.reps,
-                     w.rhash, w.isrep, b, cp, seed, seed_p, w.hist, w.hist2);
+                     w.rhash, w.isrep, b, cp, seed, seed_p, w.hist, w.hist2, sshift);
   hipLaunchKernelGGL(voxf_select_kernel, dim3(128, rows), dim3(256), 0, s, n, T, b, seed, seed_p,
                      w.hist, w.hist2, w.sel, w.cnt4, w.rhash, w.isrep, w.reps, w.ties, w.kcnt,
-                     w.ktile, w.tiles);
+                     w.ktile, w.tiles, sshift);
   hipLaunchKernelGGL(voxf_emit_kernel, dim3((unsigned)w.tiles, rows), dim3(256), 0, s, pts, n, T,
                      b, w.kcnt, w.ktile, w.tiles, w.cnt4, w.sel, w.ties, w.reps, out_idx, out_pts);
   PCST_LAUNCH_CHECK("voxel_downsample");

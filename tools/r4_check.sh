@@ -35,13 +35,16 @@ for st in "$@"; do
       rc=$?; echo "prof rc=$rc"; if [ $rc -ne 0 ]; then tail -5 "$OUT/pbench.err"; exit $rc; fi
       python tools/kstats.py "$OUT/prof/run_kernel_stats.csv" 25 | tee "$OUT/kernel_top.txt" ;;
     pmc)
-      timeout -s KILL 150 rocprofv3 --pmc SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_INST_LDS SQ_INSTS_LDS \
-          SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --output-format csv -d "$OUT/p1" -o pmc -- \
-          python $BENCH > "$OUT/p1.log" 2>&1
+      # counter passes serialise every queue's dispatches: the single-stream step layout (no
+      # cross-stream flag waits, which would spin to their poll bound), 10 steps
+      PB="tools/bench_knobs.py --gpus 1 --steps 10 --warmup 2 --no-cpu-baseline --no-encoder --no-other-precision"
+      PCST_KNN_OVERLAP=0 timeout -s KILL 300 rocprofv3 --pmc SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_INST_LDS \
+          SQ_INSTS_LDS SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --output-format csv -d "$OUT/p1" -o pmc -- \
+          python $PB > "$OUT/p1.log" 2>&1
       rc=$?; echo "pmc sq rc=$rc"; if [ $rc -ne 0 ]; then tail -5 "$OUT/p1.log"; exit $rc; fi
       for C in FETCH_SIZE WRITE_SIZE; do
-        timeout -s KILL 150 rocprofv3 --pmc $C --output-format csv -d "$OUT/pmc_$C" -o pmc -- \
-            python $BENCH > "$OUT/pmc_$C.log" 2>&1
+        PCST_KNN_OVERLAP=0 timeout -s KILL 300 rocprofv3 --pmc $C --output-format csv -d "$OUT/pmc_$C" -o pmc -- \
+            python $PB > "$OUT/pmc_$C.log" 2>&1
         rc=$?; echo "pmc $C rc=$rc"; if [ $rc -ne 0 ]; then tail -5 "$OUT/pmc_$C.log"; exit $rc; fi
       done
       python tools/pmc_sq.py "$OUT" noise_mlp | tee "$OUT/noise_mlp_sq_counters.txt"
@@ -57,12 +60,12 @@ for st in "$@"; do
       tail -c 600 "$OUT/train.json"; echo ;;
     trainpmc)
       TB="tools/bench_train.py --steps 3 --warmup 1"
-      timeout -s KILL 200 rocprofv3 --pmc SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY \
+      timeout -s KILL 300 rocprofv3 --pmc SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY \
           SQ_ACTIVE_INST_ANY SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES --output-format csv -d "$OUT/psq" -o pmc -- \
           python $TB > "$OUT/psq.log" 2>&1
       rc=$?; echo "trainpmc sq rc=$rc"; if [ $rc -ne 0 ]; then tail -5 "$OUT/psq.log"; exit $rc; fi
       for C in FETCH_SIZE WRITE_SIZE; do
-        timeout -s KILL 200 rocprofv3 --pmc $C --output-format csv -d "$OUT/pmc_$C" -o pmc -- \
+        timeout -s KILL 300 rocprofv3 --pmc $C --output-format csv -d "$OUT/pmc_$C" -o pmc -- \
             python $TB > "$OUT/tpmc_$C.log" 2>&1
         rc=$?; echo "trainpmc $C rc=$rc"; if [ $rc -ne 0 ]; then tail -5 "$OUT/tpmc_$C.log"; exit $rc; fi
       done
