@@ -362,12 +362,14 @@ def main():
         def all_conds():
             return npred.cond(t_rows.reshape(-1), style_in.repeat(S, 1), pk).view(S, 2 * C, -1)
 
+        prepped = False
+
         def step(i, timed):
-            nonlocal x
+            nonlocal x, prepped
             t = timesteps[i % len(timesteps)]
             t_prev = timesteps[i % len(timesteps) + 1] if t > 0 else -1
             cnd = conds[i % len(timesteps)]
-            xc, xi = hp.downsample_copies(x, 2, vws)
+            xc, xi = hp.downsample_copies(x, 2, vws, prepped)
 
             def mlp(xc_, wait=None, start=None):
                 if not timed:
@@ -383,9 +385,12 @@ def main():
                 ev.append((e0, e1))
                 return nc_
 
+            # the update prepares the next step's downsample (as guided_sample_loop does)
+            prep = dmod.VOXEL_PREP and hp.step_prep(x)
             x = dmod.hierarchical_step(hp, mlp, xc, xi, x_cat, x, src, 7.5, dp._coeffs(t, t_prev),
                                        knn_ws, state, mlp_waits=dmod.MLP_WAITS,
-                                       mlp_signals=dmod.MLP_SIGNALS)
+                                       mlp_signals=dmod.MLP_SIGNALS, vox_ws=vws if prep else None)
+            prepped = prep
 
         lctx = torch.cuda.stream(loop_stream) if overlap else contextlib.nullcontext()
         with lctx:
@@ -395,6 +400,7 @@ def main():
             # the timed region restarts the sampling trajectory at t = 999 from x_T
             x = torch.from_numpy(xT_np).to(device)
             x_cat.copy_(torch.cat([x, x]))
+            prepped = False
         if world > 1:
             import torch.distributed as dist
 
@@ -424,6 +430,7 @@ def main():
                 with lctx:
                     x = torch.from_numpy(xT_np).to(device)
                     x_cat.copy_(torch.cat([x, x]))
+                    prepped = False
                     conds = all_conds()
                     for i in range(2):
                         step(i, False)

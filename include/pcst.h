@@ -213,6 +213,20 @@ int pcst_voxel_copies_workspace_size(int64_t B, int64_t N, int64_t copies, size_
 int pcst_voxel_downsample_copies(const float* pts, int64_t B, int64_t N, int64_t copies,
                                  int64_t target, void* workspace, uint64_t seed, int64_t* out_idx,
                                  float* out_pts, void* stream);
+/* The sampling step's CFG + DDIM update (pcst_cfg_ddim_step over a CFG batch: eps [2C,N,3] whose
+ * rows c and C + c are cloud c's conditional and unconditional eps; source [C,N,3] or NULL; x_out
+ * [C,N,3] and x_cat [2C,N,3] = the new x and the next CFG batch) fused with the first stage of the
+ * next downsample of x_out on vox_workspace (a pcst_voxel_copies_workspace_size(C, N, copies)
+ * workspace): the new points' min / max partials and the zeroing of the per-call state.  The next
+ * call on that workspace must then be pcst_voxel_downsample_copies_prepped with pts = x_out (the
+ * same arguments as pcst_voxel_downsample_copies, one launch fewer; the same result bit for bit). */
+int pcst_cfg_ddim_voxel_prep(const float* x, const float* eps, const float* source, int64_t C,
+                             int64_t N, float guidance_scale, float sqrt_1m_at, float sqrt_at_eps,
+                             float sqrt_aprev, float sqrt_1m_aprev, float* x_out, float* x_cat,
+                             void* vox_workspace, int64_t copies, void* stream);
+int pcst_voxel_downsample_copies_prepped(const float* pts, int64_t B, int64_t N, int64_t copies,
+                                         int64_t target, void* workspace, uint64_t seed,
+                                         int64_t* out_idx, float* out_pts, void* stream);
 /* Copies the replay-validation error word (0 = ok) to err_out (device int32). */
 int pcst_voxel_error(void* workspace, int64_t B, int64_t N, int32_t* err_out, void* stream);
 

@@ -44,6 +44,8 @@ SIGNATURES = {
     "pcst_voxel_error": [_P, _I, _I, _P, _P],
     "pcst_voxel_copies_workspace_size": [_I, _I, _I, _SZ],
     "pcst_voxel_downsample_copies": [_P, _I, _I, _I, _I, _P, ctypes.c_uint64, _P, _P, _P],
+    "pcst_voxel_downsample_copies_prepped": [_P, _I, _I, _I, _I, _P, ctypes.c_uint64, _P, _P, _P],
+    "pcst_cfg_ddim_voxel_prep": [_P, _P, _P, _I, _I, _F, _F, _F, _F, _F, _P, _P, _P, _I, _P],
     "pcst_knn_workspace_size": [_I, _I, _I, _SZ],
     "pcst_knn3_interp": [_P, _P, _P, _I, _I, _I, _P, _P, _P],
     "pcst_knn3_build": [_P, _P, _I, _I, _I, _I, _I, _P, _P],
@@ -273,7 +275,8 @@ def voxel_copies_workspace(B, N, copies, device):
     return _workspace("pcst_voxel_copies_workspace_size", B, N, copies, device=device)
 
 
-def voxel_downsample(points, target, seed=0, perm_provider=None, copies=1, ws=None):
+def voxel_downsample(points, target, seed=0, perm_provider=None, copies=1, ws=None,
+                     prepped=False):
     """HierarchicalProcessor._voxel_grid_downsample_torch for N > target, all clouds at once.
 
     perm_provider=None: the random subset is drawn on the device from `seed`.
@@ -282,6 +285,8 @@ def voxel_downsample(points, target, seed=0, perm_provider=None, copies=1, ws=No
     copies=k: the result for torch.cat([points] * k) (rows c*B + b) -- on the device-drawn path
     without building or re-hashing the copies (each row keeps the set the concatenated call
     keeps for the same seed); the replay path concatenates, as the reference's draws are per row.
+    prepped=True: `ws` was prepared by cfg_ddim_voxel_prep for these points (the device-drawn
+    path skips its statistics / zeroing launch).
     Returns (points [k*B,T,3], idx [k*B,T] int64)."""
     require_device(points)
     points = _f32(points)
@@ -291,6 +296,8 @@ def voxel_downsample(points, target, seed=0, perm_provider=None, copies=1, ws=No
     B, N, _ = points.shape
     dev = points.device
     if perm_provider is None:
+        if prepped and ws is None:
+            raise RuntimeError("voxel_downsample: prepped=True needs the prepared workspace")
         if ws is None:
             ws = voxel_copies_workspace(B, N, copies, dev)
         else:
@@ -300,8 +307,9 @@ def voxel_downsample(points, target, seed=0, perm_provider=None, copies=1, ws=No
                 raise RuntimeError("voxel_downsample: workspace too small or on another device")
         out_idx = torch.empty(copies * B, target, dtype=torch.int64, device=dev)
         out_pts = torch.empty(copies * B, target, 3, dtype=torch.float32, device=dev)
-        _call("pcst_voxel_downsample_copies", _ptr(points), B, N, copies, target, _ptr(ws),
-              seed & (2**64 - 1), _ptr(out_idx), _ptr(out_pts), _stream())
+        _call("pcst_voxel_downsample_copies_prepped" if prepped else "pcst_voxel_downsample_copies",
+              _ptr(points), B, N, copies, target, _ptr(ws), seed & (2**64 - 1), _ptr(out_idx),
+              _ptr(out_pts), _stream())
         return out_pts, out_idx
     ws = _workspace("pcst_voxel_workspace_size", B, N, device=dev)
     out_idx = torch.empty(B, target, dtype=torch.int64, device=dev)
@@ -637,6 +645,29 @@ def noise_mlp(pts, points_per_cloud, cond, blob, bias, precision, out=None, wait
 
 
 # ----------------------------------------------------------------------------- CFG / DDIM update
+def cfg_ddim_voxel_prep(x, eps, source, guidance_scale, coeffs, x_cat, vox_ws, copies=2, out=None):
+    """cfg_ddim_step(x, eps[:C], eps[C:], source, ...) of a CFG batch (x [C,N,3], eps [2C,N,3],
+    x_cat [2C,N,3] receives the new x twice) fused with the first stage of the next
+    voxel_downsample(new x, copies=copies, ws=vox_ws, prepped=True) (pcst.h)."""
+    require_device(x, eps, source, x_cat, vox_ws)
+    x, eps = _f32(x), _f32(eps)
+    C, N, _ = x.shape
+    if eps.shape != (2 * C, N, 3) or x_cat is None or x_cat.shape != (2 * C, N, 3):
+        raise RuntimeError(f"cfg_ddim_voxel_prep: eps {tuple(eps.shape)} / x_cat must be {(2 * C, N, 3)}")
+    if source is not None and source.shape != x.shape:
+        raise RuntimeError("cfg_ddim_voxel_prep: source shape != x shape")
+    need = ctypes.c_size_t(0)
+    _call("pcst_voxel_copies_workspace_size", C, N, copies, ctypes.byref(need))
+    if vox_ws.numel() < need.value:
+        raise RuntimeError("cfg_ddim_voxel_prep: voxel workspace too small")
+    if out is None:
+        out = torch.empty_like(x)
+    c1, c2, c3, c4 = (float(c) for c in coeffs)
+    _call("pcst_cfg_ddim_voxel_prep", _ptr(x), _ptr(eps), _ptr(source), C, N, float(guidance_scale),
+          c1, c2, c3, c4, _ptr(out), _ptr(x_cat), _ptr(vox_ws), copies, _stream())
+    return out
+
+
 def cfg_ddim_step(x, eps_c, eps_u, source, guidance_scale, coeffs, x_cat=None, out=None):
     """coeffs = (sqrt(1-a_t), sqrt(a_t)+1e-8, sqrt(a_prev), sqrt(1-a_prev)) as fp32 values."""
     require_device(x, eps_c, eps_u, source, x_cat)
@@ -1063,7 +1094,7 @@ def voxel_downsample_copies_dseed(points, target, seed_dev, copies):
 _GUARDED = ("square_distance", "index_points", "fps", "ball_query", "group_gather",
             "voxel_downsample", "voxel_stats", "knn3_build", "knn3_query", "knn3_interp",
             "knn3_search", "knn3_finish", "knn3_finish_cfg_ddim",
-            "noise_cond", "noise_mlp", "cfg_ddim_step", "pointwise_linear", "relu_bwd",
+            "noise_cond", "noise_mlp", "cfg_ddim_step", "cfg_ddim_voxel_prep", "pointwise_linear", "relu_bwd",
             "linear_wgrad", "gemm_nt_bf16", "channel_stats", "affine_act", "chamfer_fwd",
             "chamfer_bwd", "l1_fwd", "l1_bwd", "knn_dist", "emd_greedy", "voxel_center_dist",
             "cfg_ddim_step_dcoef", "voxel_downsample_copies_dseed", "bn_train_coeffs",

@@ -362,8 +362,10 @@ constexpr int kVoxRepsBlocks = VOX_REPS_BLOCKS;  // workgroups per cloud over th
 // representatives are built once per cloud, only the random subset is drawn per row, with
 // the row's own keys -- the kept SET of every row equals the one the concatenated call draws
 // from the same seed.
+constexpr int kPrepMaxBlocks = 1024;  // min/max partials of pcst_cfg_ddim_voxel_prep per cloud
 struct VoxelFastWS {
   StatRec* mm;            // [B][kStatBlocks]
+  float* pmm;             // [B][kPrepMaxBlocks][6]  min xyz, max xyz partials (prepped calls)
   int32_t* sel;           // [R][4]: bin*, rem, need, U>T flag  (R = copies * B rows)
   int64_t* reps;          // [B][N]
   uint32_t* rhash;        // [B][N]
@@ -398,6 +400,7 @@ static VoxelFastWS carve_voxel_fast(void* base, int64_t B, int64_t N, int64_t co
   const int64_t R = B * copies;
   w.H = vox_table_size(N);
   w.mm = c.take<StatRec>(B * kStatBlocks);
+  w.pmm = c.take<float>(B * kPrepMaxBlocks * 6);
   w.sel = c.take<int32_t>(R * 4);
   w.reps = c.take<int64_t>(B * N);
   w.rhash = c.take<uint32_t>(B * N);
@@ -439,6 +442,88 @@ __global__ __launch_bounds__(256) void voxf_stats_zero_kernel(const float* __res
   for (int64_t i = z0; i < zero_words; i += stride) zero[i] = make_uint4(0u, 0u, 0u, 0u);
 }
 
+// min / max partials [b][kPrepMaxBlocks][6] of cloud b folded by one wave (s, ss left 0: the
+// voxel parameters do not use them)
+__device__ __forceinline__ StatRec fold_minmax_wave(const float* __restrict__ pmm, int b, int n) {
+  StatRec r;
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    r.mn[c] = 3.4e38f;
+    r.mx[c] = -3.4e38f;
+    r.s[c] = r.ss[c] = 0.0;
+  }
+  for (int q = threadIdx.x & 63; q < n; q += 64) {
+    const float* v = pmm + ((int64_t)b * kPrepMaxBlocks + q) * 6;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      r.mn[c] = fminf(r.mn[c], v[c]);
+      r.mx[c] = fmaxf(r.mx[c], v[3 + c]);
+    }
+  }
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1)
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      r.mn[c] = fminf(r.mn[c], __shfl_xor(r.mn[c], off));
+      r.mx[c] = fmaxf(r.mx[c], __shfl_xor(r.mx[c], off));
+    }
+  return r;
+}
+
+static int vox_prep_blocks(int64_t N) { return (int)std::min<int64_t>(cdiv(N, 256), kPrepMaxBlocks); }
+
+// pcst_cfg_ddim_voxel_prep: the CFG + DDIM update of C clouds (eps [2C,N,3]: rows c and C + c,
+// the elementwise update of sampler.hip's cfg_ddim_kernel through cfg_ddim_value), x_out and
+// x_cat [2C,N,3] written, fused with what the next downsample of x_out would launch first: the
+// min / max partials of the new points (blocks [0, nprep) of cloud y) and the zeroing of the
+// voxel workspace's per-call state (the other blocks).  One launch fewer per sampling step.
+__global__ __launch_bounds__(256) void voxf_cfg_prep_kernel(
+    const float* __restrict__ x, const float* __restrict__ eps, const float* __restrict__ src,
+    int64_t C, int N, float scale, float c1, float c2, float c3, float c4,
+    float* __restrict__ x_out, float* __restrict__ x_cat, float* __restrict__ pmm, int nprep,
+    uint4* __restrict__ zero, int64_t zero_words) {
+  const int c = blockIdx.y;
+  if ((int)blockIdx.x < nprep) {
+    float mn[3] = {3.4e38f, 3.4e38f, 3.4e38f}, mx[3] = {-3.4e38f, -3.4e38f, -3.4e38f};
+    const int64_t half = C * (int64_t)N * 3;
+    for (int n = blockIdx.x * 256 + threadIdx.x; n < N; n += nprep * 256) {
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        const int64_t e = ((int64_t)c * N + n) * 3 + j;
+        const float xn = cfg_ddim_value(x[e], eps[e], eps + half + e, src ? src + e : nullptr,
+                                        scale, c1, c2, c3, c4);
+        x_out[e] = xn;
+        x_cat[e] = xn;
+        x_cat[half + e] = xn;
+        mn[j] = fminf(mn[j], xn);
+        mx[j] = fmaxf(mx[j], xn);
+      }
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1)
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        mn[j] = fminf(mn[j], __shfl_xor(mn[j], off));
+        mx[j] = fmaxf(mx[j], __shfl_xor(mx[j], off));
+      }
+    __shared__ float w[4][6];
+    const int wid = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0)
+      for (int j = 0; j < 3; ++j) { w[wid][j] = mn[j]; w[wid][3 + j] = mx[j]; }
+    __syncthreads();
+    if (threadIdx.x < 6) {
+      float v = w[0][threadIdx.x];
+      for (int q = 1; q < 4; ++q)
+        v = threadIdx.x < 3 ? fminf(v, w[q][threadIdx.x]) : fmaxf(v, w[q][threadIdx.x]);
+      pmm[((int64_t)c * kPrepMaxBlocks + blockIdx.x) * 6 + threadIdx.x] = v;
+    }
+    return;
+  }
+  const int64_t stride = (int64_t)kVoxZeroBlocks * gridDim.y * 256;
+  const int64_t z0 = ((int64_t)c * kVoxZeroBlocks + (blockIdx.x - nprep)) * 256 + threadIdx.x;
+  for (int64_t i = z0; i < zero_words; i += stride) zero[i] = make_uint4(0u, 0u, 0u, 0u);
+}
+
 // Voxel table insert; the first wave also folds the cloud's min/max partials into the voxel
 // parameters (min xyz, voxel size) for its workgroup.
 __global__ __launch_bounds__(256) void voxf_insert_kernel(const float* __restrict__ pts, int N,
@@ -452,7 +537,8 @@ __global__ __launch_bounds__(256) void voxf_insert_kernel(const float* __restric
                                                           uint32_t* __restrict__ hist,
                                                           int32_t* __restrict__ cnt4,
                                                           int32_t* __restrict__ vlist, int pack,
-                                                          int sshift) {
+                                                          int sshift, const float* __restrict__ pmm,
+                                                          int npm) {
   const int nbins = 1 << (32 - sshift);
   // Each workgroup first aggregates its kVoxChunk points in an LDS table (LDS atomics), then
   // publishes one global (sum, count) per distinct voxel: dense voxels see at most one global
@@ -465,7 +551,9 @@ __global__ __launch_bounds__(256) void voxf_insert_kernel(const float* __restric
   __shared__ uint32_t lcnt[kVoxLds];
   __shared__ float4 vps;
   if (threadIdx.x < 64) {
-    const StatRec M = fold_stats_wave(mm, b);
+    // the voxel parameters use only min / max (order-free folds): from the stats partials, or
+    // from pcst_cfg_ddim_voxel_prep's min / max partials on a prepped call
+    const StatRec M = pmm ? fold_minmax_wave(pmm, b, npm) : fold_stats_wave(mm, b);
     if (threadIdx.x == 0) vps = make_float4(M.mn[0], M.mn[1], M.mn[2], voxel_size(M, T));
   }
   for (int i = threadIdx.x; i < kVoxLds; i += 256) { lkey[i] = 0ull; lsum[i] = 0ull; lcnt[i] = 0u; }
@@ -763,20 +851,25 @@ __global__ __launch_bounds__(256) void voxf_emit_kernel(const float* __restrict_
 // stats (+ zeroing), insert (+ voxel parameters, every point's pool-key histogram), reps (+ the
 // representatives' keys into / out of the histograms), select (+ boundary bin, marks, tie list),
 // emit (+ tie ranking; rows in point-index order): 5 launches.
+static size_t vox_zero_bytes(const VoxelFastWS& w, int64_t rows) {
+  return (size_t)((char*)(w.ktile + rows * w.tiles) - (char*)w.cnt4);
+}
+
 static int voxel_fast(const float* pts, int64_t B, int64_t N, int64_t copies, int64_t T,
                       void* workspace, uint64_t seed, const uint64_t* seed_p, int64_t* out_idx,
-                      float* out_pts, hipStream_t s) {
+                      float* out_pts, hipStream_t s, bool prepped = false) {
   VoxelFastWS w = carve_voxel_fast(workspace, B, N, copies);
   const int b = (int)B, n = (int)N, rows = (int)(B * copies);
-  const size_t zero = (size_t)((char*)(w.ktile + rows * w.tiles) - (char*)w.cnt4);
-  hipLaunchKernelGGL(voxf_stats_zero_kernel, dim3(kStatBlocks + kVoxZeroBlocks, b), dim3(256), 0, s,
-                     pts, n, w.mm, reinterpret_cast<uint4*>(w.cnt4), (int64_t)cdiv(zero, 16));
+  if (!prepped)  // (a prepped call: pcst_cfg_ddim_voxel_prep made the partials and zeroed)
+    hipLaunchKernelGGL(voxf_stats_zero_kernel, dim3(kStatBlocks + kVoxZeroBlocks, b), dim3(256), 0,
+                       s, pts, n, w.mm, reinterpret_cast<uint4*>(w.cnt4),
+                       (int64_t)cdiv(vox_zero_bytes(w, rows), 16));
   const int cp = (int)copies;
   const int pack = N < (1 << 20) ? 1 : 0;
   const int sshift = vox_sel_shift(N);
   hipLaunchKernelGGL(voxf_insert_kernel, dim3((unsigned)cdiv(N, kVoxChunk), b), dim3(256), 0, s,
                      pts, n, w.mm, T, w.H, w.tkey, w.tsum, w.tcnt, b, cp, seed, seed_p, w.hist, w.cnt4,
-                     w.vlist, pack, sshift);
+                     w.vlist, pack, sshift, prepped ? w.pmm : nullptr, vox_prep_blocks(N));
   hipLaunchKernelGGL(voxf_reps_kernel, dim3((unsigned)std::min<int64_t>(cdiv(N, 256), kVoxRepsBlocks), b),
                      dim3(256), 0, s, w.tkey, w.tsum, w.tcnt, w.H, n, w.cnt4, w.vlist, pack, w.reps,
                      w.rhash, w.isrep, b, cp, seed, seed_p, w.hist, w.hist2, sshift);
@@ -901,6 +994,37 @@ extern "C" int pcst_voxel_downsample_copies(const float* pts, int64_t B, int64_t
   PCST_CHECK_ARG(pts && workspace && out_idx && out_pts, "voxel_downsample_copies: null pointer");
   return voxel_fast(pts, B, N, copies, target, workspace, seed, nullptr, out_idx, out_pts,
                     as_stream(stream));
+}
+
+extern "C" int pcst_voxel_downsample_copies_prepped(const float* pts, int64_t B, int64_t N,
+                                                    int64_t copies, int64_t target, void* workspace,
+                                                    uint64_t seed, int64_t* out_idx, float* out_pts,
+                                                    void* stream) {
+  PCST_CHECK_ARG(B > 0 && copies >= 1 && B * copies < (1 << 15) && N > target && target > 0 &&
+                     N < (1ll << 30),
+                 "voxel_downsample_copies_prepped: bad shape");
+  PCST_CHECK_ARG(pts && workspace && out_idx && out_pts, "voxel_downsample_copies_prepped: null pointer");
+  return voxel_fast(pts, B, N, copies, target, workspace, seed, nullptr, out_idx, out_pts,
+                    as_stream(stream), true);
+}
+
+extern "C" int pcst_cfg_ddim_voxel_prep(const float* x, const float* eps, const float* source,
+                                        int64_t C, int64_t N, float guidance_scale,
+                                        float sqrt_1m_at, float sqrt_at_eps, float sqrt_aprev,
+                                        float sqrt_1m_aprev, float* x_out, float* x_cat,
+                                        void* vox_workspace, int64_t copies, void* stream) {
+  PCST_CHECK_ARG(C > 0 && N > 0 && copies >= 1 && C * copies < (1 << 15) && N < (1ll << 30),
+                 "cfg_ddim_voxel_prep: bad shape");
+  PCST_CHECK_ARG(x && eps && x_out && x_cat && vox_workspace, "cfg_ddim_voxel_prep: null pointer");
+  VoxelFastWS w = carve_voxel_fast(vox_workspace, C, N, copies);
+  const int nprep = vox_prep_blocks(N);
+  hipLaunchKernelGGL(voxf_cfg_prep_kernel, dim3(nprep + kVoxZeroBlocks, (unsigned)C), dim3(256), 0,
+                     as_stream(stream), x, eps, source, C, (int)N, guidance_scale, sqrt_1m_at,
+                     sqrt_at_eps, sqrt_aprev, sqrt_1m_aprev, x_out, x_cat, w.pmm, nprep,
+                     reinterpret_cast<uint4*>(w.cnt4),
+                     (int64_t)cdiv(vox_zero_bytes(w, C * copies), 16));
+  PCST_LAUNCH_CHECK("cfg_ddim_voxel_prep");
+  return PCST_OK;
 }
 
 extern "C" int pcst_voxel_downsample_copies_dseed(const float* pts, int64_t B, int64_t N,

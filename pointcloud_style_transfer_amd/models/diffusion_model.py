@@ -228,16 +228,24 @@ class HierarchicalProcessor:
         return self._voxel_grid_downsample_torch(points, self.global_points)
 
     def downsample_copies(self, points: torch.Tensor, copies: int,
-                          ws: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, torch.Tensor]:
+                          ws: Optional[torch.Tensor] = None,
+                          prepped: bool = False) -> Tuple[torch.Tensor, torch.Tensor]:
         """downsample(torch.cat([points] * copies)) -- the CFG batch of guided_sample_loop
         (diffusion_model.py:244-247) -- without building or re-hashing the copies.  Replay runs
         take the concatenated path: the reference draws one permutation per row.  `ws`
-        (_hip.voxel_copies_workspace of the same shape) is reused instead of allocated."""
+        (_hip.voxel_copies_workspace of the same shape) is reused instead of allocated;
+        prepped: `ws` was prepared for `points` by the previous step's update
+        (_hip.cfg_ddim_voxel_prep)."""
         src = _rng.source()
         if points.shape[1] <= self.global_points or src.replaying:
             return self.downsample(torch.cat([points] * copies))
         return _hip.voxel_downsample(points, self.global_points, seed=src.device_seed(),
-                                     copies=copies, ws=ws)
+                                     copies=copies, ws=ws, prepped=prepped)
+
+    def step_prep(self, points: torch.Tensor) -> bool:
+        """Whether the next downsample_copies of `points` can take a workspace prepared by the
+        step's update (the device-drawn path; replay runs concatenate)."""
+        return points.shape[1] > self.global_points and not _rng.source().replaying
 
     def upsample_knn(self, coarse_points: torch.Tensor, original_points: torch.Tensor,
                      coarse_indices: torch.Tensor) -> torch.Tensor:
@@ -383,13 +391,17 @@ SEARCH_BESIDE_MLP = False
 
 
 def hierarchical_step(hp, mlp, xc, xi, x_cat, x, source, guidance_scale, coeffs, knn_ws=None,
-                      state=None, mlp_waits=False, mlp_signals=False):
+                      state=None, mlp_waits=False, mlp_signals=False, vox_ws=None):
     """One guided step of the hierarchical branch (diffusion_model.py:240-260): eps of the CFG
     batch (mlp(xc) upsampled by kNN-3), then the fused CFG + DDIM update of x (x_cat takes the
-    new x twice).  Returns the new x.  state: a StepState (overlapped layout) or None."""
+    new x twice).  Returns the new x.  state: a StepState (overlapped layout) or None.
+    vox_ws: the voxel workspace of the next step's downsample_copies, prepared by this update
+    (_hip.cfg_ddim_voxel_prep: one launch fewer); that call must then pass prepped=True."""
     C = x.shape[0]
     if state is None or not SEARCH_BESIDE_MLP:
         eps = hierarchical_eps(hp, mlp, xc, xi, x_cat, knn_ws, state, mlp_waits, mlp_signals)
+        if vox_ws is not None:
+            return _hip.cfg_ddim_voxel_prep(x, eps, source, guidance_scale, coeffs, x_cat, vox_ws)
         return _hip.cfg_ddim_step(x, eps[:C], eps[C:], source, guidance_scale, coeffs, x_cat=x_cat)
     main = torch.cuda.current_stream()
     side = state.side
@@ -429,6 +441,9 @@ MLP_WAITS = False
 # The loop -> side flag written by the MLP launch as it begins (pcst_noise_mlp_ex's start signal)
 # instead of a one-lane signal launch between the voxel emit and the MLP on the loop's queue.
 MLP_SIGNALS = True
+# The step's CFG + DDIM update also prepares the next step's voxel downsample (its statistics and
+# zeroing: pcst_cfg_ddim_voxel_prep), one launch fewer per step; bit-identical.
+VOXEL_PREP = True
 class _TorchEvent:
     """torch.cuda.Event with the DeviceEvent interface (DEVICE_EVENTS = False: A/B runs)."""
 
@@ -593,6 +608,7 @@ class DiffusionProcess:
                 ws = _hip.knn_workspace(2 * B, shape[1], model.config.global_points, device=device)
             if use_hierarchical:
                 vws = _hip.voxel_copies_workspace(B, shape[1], 2, device=device)
+            prepped = False
             try:
                 for i, t in enumerate(timesteps):
                     t_in = t_rows[i]
@@ -604,11 +620,14 @@ class DiffusionProcess:
                         mlp = lambda c: npred(c, t_in, style_in)  # noqa: E731
                     coeffs = self._coeffs(t, t_prevs[i])
                     if use_hierarchical:
-                        xc, xi = hp.downsample_copies(x, 2, vws)
+                        xc, xi = hp.downsample_copies(x, 2, vws, prepped)
+                        prep = VOXEL_PREP and i + 1 < len(timesteps) and hp.step_prep(x)
                         x = hierarchical_step(hp, mlp, xc, xi, x_cat, x, source, guidance_scale,
                                               coeffs, ws, state,
                                               mlp_waits=MLP_WAITS and conds is not None,
-                                              mlp_signals=MLP_SIGNALS and conds is not None)
+                                              mlp_signals=MLP_SIGNALS and conds is not None,
+                                              vox_ws=vws if prep else None)
+                        prepped = prep
                     else:
                         eps = mlp(x_cat)
                         x = _hip.cfg_ddim_step(x, eps[:B], eps[B:], source, guidance_scale,

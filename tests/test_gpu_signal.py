@@ -1,6 +1,7 @@
 """Kernel-side cross-stream signal (pcst_signal_write / pcst_signal_wait, _hip.DeviceSignal): the
 sampling loop's loop -> side dependency.  Work enqueued after a wait must see everything the
 producer stream wrote before the matching signal, under load and across many rounds."""
+import numpy as np
 import pytest
 import torch
 
@@ -229,3 +230,25 @@ def test_guided_loop_mlp_start_signal_bit_identical(monkeypatch):
             torch.manual_seed(7)
             outs.append(dp.guided_sample_loop(model, src, cond, 8, 7.5, x_T=xT))
     assert torch.equal(outs[0], outs[1])
+
+
+def test_guided_loop_voxel_prep_bit_identical(monkeypatch):
+    """The step's CFG + DDIM update fused with the next downsample's statistics and zeroing
+    (pcst_cfg_ddim_voxel_prep + pcst_voxel_downsample_copies_prepped, VOXEL_PREP) gives the bits
+    of the separate update and full downsample, at 1 and 3 clouds."""
+    from pointcloud_style_transfer_amd.models import diffusion_model as dm
+    from pointcloud_style_transfer_amd.synthetic import lidar_like_cloud, standard_normal
+
+    dev = torch.device("cuda", 0)
+    cfg, model, dp = _small_model(dev)
+    for B in (1, 3):
+        src = torch.from_numpy(np.stack([lidar_like_cloud(1000 + i, 16384) for i in range(B)])).to(dev)
+        cond = torch.from_numpy(np.stack([lidar_like_cloud(2000 + i, 16384) for i in range(B)])).to(dev)
+        xT = torch.from_numpy(np.stack([standard_normal(3000 + i, (16384, 3)) for i in range(B)])).to(dev)
+        outs = []
+        with torch.no_grad():
+            for on in (True, False):
+                monkeypatch.setattr(dm, "VOXEL_PREP", on)
+                torch.manual_seed(9)
+                outs.append(dp.guided_sample_loop(model, src, cond, 6, 7.5, x_T=xT))
+        assert torch.equal(outs[0], outs[1]), B

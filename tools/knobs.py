@@ -26,6 +26,8 @@ def apply():
         dm.DEVICE_EVENTS = e["PCST_DEVICE_EVENTS"] != "0"
     if "PCST_KNN_BUILD_MAX_WG" in e:
         dm.KNN_BUILD_MAX_WG = int(e["PCST_KNN_BUILD_MAX_WG"])
+    if "PCST_VOXEL_PREP" in e:
+        dm.VOXEL_PREP = e["PCST_VOXEL_PREP"] != "0"
     if "PCST_MLP_SIGNALS" in e:
         dm.MLP_SIGNALS = e["PCST_MLP_SIGNALS"] != "0"
     if "PCST_MLP_WAITS" in e:
