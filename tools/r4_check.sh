@@ -79,7 +79,7 @@ for st in "$@"; do
       VS=${st#trainab=}
       for pass in 1 2; do
         for v in prod ${VS//,/ }; do
-          if [ "$v" = prod ]; then lib=pointcloud_style_transfer_amd/libpcst_hip.so; else lib=pointcloud_style_transfer_amd/libpcst_hip_$v.so; fi
+          if [ "$v" = prod ]; then lib=$PWD/pointcloud_style_transfer_amd/libpcst_hip.so; else lib=$PWD/pointcloud_style_transfer_amd/libpcst_hip_$v.so; fi
           PCST_LIB=$lib timeout -k 10 300 python tools/bench_train.py > "$OUT/train_$v.$pass.json" 2> "$OUT/train_$v.$pass.err"
           rc=$?; if [ $rc -ne 0 ]; then tail -3 "$OUT/train_$v.$pass.err"; exit $rc; fi
           python -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print(sys.argv[2], d['ms_per_step'], d['final_loss'])" "$OUT/train_$v.$pass.json" "$v.$pass"
@@ -94,7 +94,7 @@ for st in "$@"; do
     libtests=*)
       # libtests=v_name,EXPR: pytest -m gpu -k EXPR against pointcloud_style_transfer_amd/libpcst_hip_<v_name>.so
       A=${st#libtests=}; V=${A%%,*}; K=${A#*,}
-      PCST_LIB=pointcloud_style_transfer_amd/libpcst_hip_$V.so timeout -k 10 600 python -u -m pytest tests -m gpu -x -v \
+      PCST_LIB=$PWD/pointcloud_style_transfer_amd/libpcst_hip_$V.so timeout -k 10 600 python -u -m pytest tests -m gpu -x -v \
           --timeout 300 --timeout-method thread -k "$K" > "$OUT/libtests_$V.log" 2>&1
       rc=$?; echo "libtests $V rc=$rc"; grep -E "FAILED|ERROR" "$OUT/libtests_$V.log" | head; tail -1 "$OUT/libtests_$V.log"
       if [ $rc -ne 0 ]; then exit $rc; fi ;;
@@ -103,7 +103,7 @@ for st in "$@"; do
       VS=${st#benchlib=}
       for pass in 1 2; do
         for v in prod ${VS//,/ }; do
-          if [ "$v" = prod ]; then lib=pointcloud_style_transfer_amd/libpcst_hip.so; else lib=pointcloud_style_transfer_amd/libpcst_hip_$v.so; fi
+          if [ "$v" = prod ]; then lib=$PWD/pointcloud_style_transfer_amd/libpcst_hip.so; else lib=$PWD/pointcloud_style_transfer_amd/libpcst_hip_$v.so; fi
           PCST_LIB=$lib timeout -k 10 200 python $BENCH > "$OUT/bench_$v.$pass.json" 2> "$OUT/bench_$v.$pass.err"
           rc=$?; if [ $rc -ne 0 ]; then tail -3 "$OUT/bench_$v.$pass.err"; exit $rc; fi
           PCST_LIB=$lib timeout -k 10 200 python bench.py --gpus 1 --clouds-per-gpu 32 --steps 10 --warmup 3 \
