@@ -386,7 +386,7 @@ def main():
                 return nc_
 
             # the update prepares the next step's downsample (as guided_sample_loop does)
-            prep = dmod.VOXEL_PREP and hp.step_prep(x)
+            prep = dmod.voxel_prep_ok(hp, x, state)
             x = dmod.hierarchical_step(hp, mlp, xc, xi, x_cat, x, src, 7.5, dp._coeffs(t, t_prev),
                                        knn_ws, state, mlp_waits=dmod.MLP_WAITS,
                                        mlp_signals=dmod.MLP_SIGNALS, vox_ws=vws if prep else None)

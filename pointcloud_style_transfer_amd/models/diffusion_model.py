@@ -381,6 +381,13 @@ def hierarchical_eps(hp, mlp, xc, xi, x_cat, knn_ws=None, state=None, mlp_waits=
     return _hip.knn3_query(nc, handle, built if BUILT_SIGNAL else None)
 
 
+def voxel_prep_ok(hp, x, state) -> bool:
+    """Whether hierarchical_step's update prepares the next downsample_copies of x (VOXEL_PREP;
+    the fused update exists on the query-after-MLP layout, not with SEARCH_BESIDE_MLP's fused
+    finish)."""
+    return VOXEL_PREP and (state is None or not SEARCH_BESIDE_MLP) and hp.step_prep(x)
+
+
 # The query's neighbour search is positions-only too: with SEARCH_BESIDE_MLP the side stream runs
 # it after the build (pcst_knn3_search: each row's three neighbours and IDW weights), and after
 # the MLP only the gather of the coarse values remains, fused with the CFG + DDIM update
@@ -396,13 +403,16 @@ def hierarchical_step(hp, mlp, xc, xi, x_cat, x, source, guidance_scale, coeffs,
     batch (mlp(xc) upsampled by kNN-3), then the fused CFG + DDIM update of x (x_cat takes the
     new x twice).  Returns the new x.  state: a StepState (overlapped layout) or None.
     vox_ws: the voxel workspace of the next step's downsample_copies, prepared by this update
-    (_hip.cfg_ddim_voxel_prep: one launch fewer); that call must then pass prepped=True."""
+    (_hip.cfg_ddim_voxel_prep: one launch fewer); that call must then pass prepped=True.  Only
+    on the query-after-MLP layout (voxel_prep_ok)."""
     C = x.shape[0]
     if state is None or not SEARCH_BESIDE_MLP:
         eps = hierarchical_eps(hp, mlp, xc, xi, x_cat, knn_ws, state, mlp_waits, mlp_signals)
         if vox_ws is not None:
             return _hip.cfg_ddim_voxel_prep(x, eps, source, guidance_scale, coeffs, x_cat, vox_ws)
         return _hip.cfg_ddim_step(x, eps[:C], eps[C:], source, guidance_scale, coeffs, x_cat=x_cat)
+    if vox_ws is not None:
+        raise RuntimeError("hierarchical_step: the voxel prep needs the query-after-MLP layout")
     main = torch.cuda.current_stream()
     side = state.side
     ready, built = state.ready_ev, state.built_ev
@@ -621,7 +631,7 @@ class DiffusionProcess:
                     coeffs = self._coeffs(t, t_prevs[i])
                     if use_hierarchical:
                         xc, xi = hp.downsample_copies(x, 2, vws, prepped)
-                        prep = VOXEL_PREP and i + 1 < len(timesteps) and hp.step_prep(x)
+                        prep = i + 1 < len(timesteps) and voxel_prep_ok(hp, x, state)
                         x = hierarchical_step(hp, mlp, xc, xi, x_cat, x, source, guidance_scale,
                                               coeffs, ws, state,
                                               mlp_waits=MLP_WAITS and conds is not None,
