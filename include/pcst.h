@@ -123,6 +123,15 @@ int pcst_group_gather_bwd(const float* dgrouped, const int64_t* group_idx, int64
  * the broadcast time / style rows of x = (pf + tf) + sf under autocast (diffusion_model.py:56-58,
  * trainer.py:78-106 backward).  Deterministic (row slices combined in slice order); C % 8 == 0,
  * G 16-byte aligned.  workspace: pcst_group_colsum16_workspace_size() bytes. */
+/* One residual block of NoisePredictorFn's 16-bit residual stream (diffusion_model.py:48-52,57-58
+ * under autocast) in one launch: h [M,512] = 16-bit(relu(x W1^T + b1)), x_out [M,256] =
+ * 16-bit(x + Dropout_p(h W2^T + b2)); x [M,256], W1 [512,256], W2 [256,512] in the 16-bit format
+ * f16 selects (1 float16, 0 bfloat16), b1 / b2 fp32.  The bits of pcst_gemm_ex EP_BF16 followed
+ * by EP_RESID_DROP16 with the same (seed, p); h is written for the backward but never re-read.
+ * 16-byte aligned pointers, x_out != x, M * 1024 < 2^31. */
+int pcst_resblock_fwd16(const uint16_t* x, int64_t M, const uint16_t* w1, const float* b1,
+                        const uint16_t* w2, const float* b2, uint64_t seed, float drop_p,
+                        uint16_t* h, uint16_t* x_out, int f16, void* stream);
 int pcst_group_colsum16_workspace_size(int64_t B, int64_t C, size_t* bytes);
 int pcst_group_colsum16(const uint16_t* G, int f16, int64_t B, int64_t N, int64_t C, float* out,
                         void* workspace, void* stream);

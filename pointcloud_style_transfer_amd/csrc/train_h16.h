@@ -19,6 +19,9 @@ namespace pcst {
                    void* stream);                                                                  \
   int dropout_grad_impl(const float* g, int64_t n, uint64_t seed, float drop_p, uint16_t* out,     \
                         void* stream);                                                             \
+  int resblock_fwd_impl(const uint16_t* x, int64_t M, const uint16_t* w1, const float* b1,         \
+                        const uint16_t* w2, const float* b2, uint64_t seed, float drop_p,          \
+                        uint16_t* h, uint16_t* xo, void* stream);                                  \
   int wgrad_ex_workspace_impl(int64_t M, int64_t I, int64_t O, size_t* bytes);                     \
   int wgrad_ex_impl(const void* dZ, int dz_bf16, const void* X, int x_bf16, int64_t M, int64_t I, \
                     int64_t O, float* dW, float* db, void* workspace, void* stream);               \

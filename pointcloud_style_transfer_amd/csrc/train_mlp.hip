@@ -1270,6 +1270,199 @@ int wgrad_ex_impl(const void* dZ, int dz_bf16, const void* X, int x_bf16, int64_
   return PCST_OK;
 }
 
+// ---- fused residual block forward (NoisePredictorFn's 16-bit residual stream):
+//   h  = 16-bit(relu(x W1^T + b1))          [M, 512]   (written: the backward's mask and dW2 operand)
+//   x' = 16-bit(x + Dropout(h W2^T + b2))   [M, 256]
+// = gemm_ex EP_BF16 followed by EP_RESID_DROP16 in one pass over the rows: a work-group keeps its
+// 128-row x tile in LDS for all four 128-wide hidden chunks and the residual add, and each chunk
+// of h goes from the accumulators through LDS straight into the second product, so h is written
+// once and never read back (the two-kernel form reads it again: 246 MB per block at M = 240 000).
+// Bit-identical to the two gemm_ex calls: the same 32x32x16 MFMA roles (activation rows x weight
+// rows), every output's k ascending in steps of 16, the same bias / ReLU / dropout / rounding.
+// 512 threads = 8 waves, wave (wr, wc) = (w & 3, w >> 2): rows [32 wr, +32) x cols [64 wc, +64) of
+// each 128 x 128 output tile.  The weights stream through a double-buffered 64-deep B slice:
+// per chunk 4 slices of W1 (K = 256) then 2 x 2 slices of W2 (the two output halves, K = 128).
+constexpr int kRbK = 64;                 // weight slice depth
+constexpr int kRbBLd = kRbK + 8;         // B image row (16-bit elements): 144 B, conflict-free
+constexpr int kRbXLd = 256 + 8;          // x tile row: 528 B
+constexpr int kRbHLd = 128 + 8;          // h chunk row: 272 B
+constexpr int kRbXBytes = 128 * kRbXLd * 2;
+constexpr int kRbHBytes = 128 * kRbHLd * 2;
+constexpr int kRbBBytes = 128 * kRbBLd * 2;
+constexpr int kRbLds = kRbXBytes + kRbHBytes + 2 * kRbBBytes;
+
+struct RbArgs {
+  const uint16_t* x;   // [M, 256]
+  const uint16_t* w1;  // [512, 256]
+  const float* b1;     // [512]
+  const uint16_t* w2;  // [256, 512]
+  const float* b2;     // [256]
+  uint16_t* h;         // [M, 512]
+  uint16_t* xo;        // [M, 256]
+  int64_t M;
+  uint32_t seed_lo, seed_hi, thr;
+  float scale;
+};
+
+__global__ __launch_bounds__(512) void resblock_fwd_kernel(RbArgs a, int per_xcd, int ntiles) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  h16* Xs = reinterpret_cast<h16*>(smem);                                   // [128][kRbXLd]
+  h16* Hs = reinterpret_cast<h16*>(smem + kRbXBytes);                       // [128][kRbHLd]
+  h16* Bs0 = reinterpret_cast<h16*>(smem + kRbXBytes + kRbHBytes);          // [128][kRbBLd]
+  h16* Bs1 = reinterpret_cast<h16*>(smem + kRbXBytes + kRbHBytes + kRbBBytes);
+  const int L = blockIdx.x;
+  const int t = (L & 7) * per_xcd + (L >> 3);
+  if (t >= ntiles) return;
+  const int64_t m0 = (int64_t)t * 128;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wr = wid & 3, wc = wid >> 2, h = lane >> 5, l32 = lane & 31;
+  const int64_t M = a.M;
+  // x tile -> Xs (rows past M read 0 through the buffer bound)
+  const rsrc_t rx = make_rsrc(a.x, (uint32_t)(M * 256 * 2));
+#pragma unroll
+  for (int it = 0; it < 8; ++it) {  // 128 rows x 32 chunks of 16 B
+    const int q = it * 512 + tid, r = q >> 5, cch = (q & 31) * 8;
+    const uint4 v = bload16(rx, (uint32_t)(((m0 + r) * 256 + cch) * 2), 0);
+    *reinterpret_cast<uint4*>(Xs + r * kRbXLd + cch) = v;
+  }
+  // B slice i: chunk c = i / 8, j = i % 8: j < 4 -> W1 rows [128c, +128) k [64j, +64);
+  // j >= 4 -> W2 rows [128 oh, +128) k [128c + 64s, +64) with oh = (j - 4) / 2, s = (j - 4) % 2.
+  // Thread -> (row tid / 4, 16 elements at (tid % 4) * 16): two 16-byte loads.
+  const rsrc_t rw1 = make_rsrc(a.w1, 512u * 256u * 2u), rw2 = make_rsrc(a.w2, 256u * 512u * 2u);
+  const int br = tid >> 2, bk = (tid & 3) * 16;
+  auto load_slice = [&](int i, uint4& g0, uint4& g1) {
+    const int c = i >> 3, j = i & 7;
+    uint32_t off;
+    rsrc_t r;
+    if (j < 4) {
+      off = (uint32_t)(((128 * c + br) * 256 + 64 * j + bk) * 2);
+      r = rw1;
+    } else {
+      const int oh = (j - 4) >> 1, sl = (j - 4) & 1;
+      off = (uint32_t)(((128 * oh + br) * 512 + 128 * c + 64 * sl + bk) * 2);
+      r = rw2;
+    }
+    g0 = bload16(r, off, 0);
+    g1 = bload16(r, off + 16, 0);
+  };
+  f32x16 acc1[2], acc2[4];
+#pragma unroll
+  for (int u = 0; u < 2; ++u) acc1[u] = f32x16{};
+#pragma unroll
+  for (int u = 0; u < 4; ++u) acc2[u] = f32x16{};
+  uint4 g0, g1;
+  load_slice(0, g0, g1);
+  const int arow = 32 * wr + l32;
+  for (int i = 0; i < 32; ++i) {
+    h16* Bs = (i & 1) ? Bs1 : Bs0;
+    *reinterpret_cast<uint4*>(Bs + br * kRbBLd + bk) = g0;
+    *reinterpret_cast<uint4*>(Bs + br * kRbBLd + bk + 8) = g1;
+    __syncthreads();  // this slice landed; the previous slice's (and epilogue's) readers are done
+    if (i + 1 < 32) load_slice(i + 1, g0, g1);
+    const int c = i >> 3, j = i & 7;
+    if (j == 4) {
+      // chunk c's h (written to Hs by every wave after slice 8c + 3) -> global h, coalesced:
+      // 128 rows x 16 chunks of 16 B, 4 per thread
+      const rsrc_t rh = make_rsrc(a.h, (uint32_t)(M * 512 * 2));
+#pragma unroll
+      for (int it = 0; it < 4; ++it) {
+        const int q = it * 512 + tid, r = q >> 4, cch = (q & 15) * 8;
+        const uint4 v = *reinterpret_cast<const uint4*>(Hs + r * kRbHLd + cch);
+        const v4i32 vv = {(int)v.x, (int)v.y, (int)v.z, (int)v.w};
+        __builtin_amdgcn_raw_buffer_store_b128(vv, rh, (int)(((m0 + r) * 512 + 128 * c + cch) * 2), 0, 0);
+      }
+    }
+#pragma unroll
+    for (int ks = 0; ks < kRbK / 16; ++ks) {
+      h16x8 av, b[2];
+      if (j < 4)
+        av = *reinterpret_cast<const h16x8*>(Xs + arow * kRbXLd + 64 * j + 16 * ks + 8 * h);
+      else
+        av = *reinterpret_cast<const h16x8*>(Hs + arow * kRbHLd + 64 * ((j - 4) & 1) + 16 * ks + 8 * h);
+#pragma unroll
+      for (int bn = 0; bn < 2; ++bn)
+        b[bn] = *reinterpret_cast<const h16x8*>(Bs + (64 * wc + 32 * bn + l32) * kRbBLd + 16 * ks + 8 * h);
+      if (j < 4) {
+#pragma unroll
+        for (int bn = 0; bn < 2; ++bn) acc1[bn] = mfma32_h16(av, b[bn], acc1[bn]);
+      } else {
+        const int oh = (j - 4) >> 1;
+#pragma unroll
+        for (int bn = 0; bn < 2; ++bn) {
+          if (oh == 0) acc2[bn] = mfma32_h16(av, b[bn], acc2[bn]);
+          else acc2[2 + bn] = mfma32_h16(av, b[bn], acc2[2 + bn]);
+        }
+      }
+    }
+    if (j == 3) {
+      // chunk c's epilogue: h = 16-bit(relu(acc1 + b1)) into Hs (read by every wave after the
+      // next slice's barrier); the accumulators restart for chunk c + 1
+#pragma unroll
+      for (int bn = 0; bn < 2; ++bn) {
+        const int col = 64 * wc + 32 * bn + l32;
+        const float bb = a.b1[128 * c + col];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float v = fmaxf(acc1[bn][r] + bb, 0.0f);
+          Hs[(32 * wr + xrow(r, h)) * kRbHLd + col] = (h16)v;
+        }
+        acc1[bn] = f32x16{};
+      }
+    }
+  }
+  __syncthreads();  // every wave's W2 products done; Xs is read below only by its owner lanes
+  // x' = 16-bit(x + Dropout(acc2 + b2)), in place in Xs, then a coalesced copy out
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int oh = u >> 1, bn = u & 1;
+    const int col = 128 * oh + 64 * wc + 32 * bn + l32;
+    const float bb = a.b2[col];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int row = 32 * wr + xrow(r, h);
+      const uint32_t e = (uint32_t)((m0 + row) * 256 + col);
+      float y = acc2[u][r] + bb;
+      const bool keep = drop_hash(a.seed_lo, a.seed_hi, (uint64_t)e) >= a.thr;
+      y = keep ? y * a.scale : 0.0f;
+      h16* px = Xs + row * kRbXLd + col;
+      y += (float)*px;
+      *px = (h16)y;
+    }
+  }
+  __syncthreads();
+  const rsrc_t ro = make_rsrc(a.xo, (uint32_t)(M * 256 * 2));
+#pragma unroll
+  for (int it = 0; it < 8; ++it) {
+    const int q = it * 512 + tid, r = q >> 5, cch = (q & 31) * 8;
+    const uint4 v = *reinterpret_cast<const uint4*>(Xs + r * kRbXLd + cch);
+    const v4i32 vv = {(int)v.x, (int)v.y, (int)v.z, (int)v.w};
+    __builtin_amdgcn_raw_buffer_store_b128(vv, ro, (int)(((m0 + r) * 256 + cch) * 2), 0, 0);
+  }
+}
+
+int resblock_fwd_impl(const uint16_t* x, int64_t M, const uint16_t* w1, const float* b1,
+                      const uint16_t* w2, const float* b2, uint64_t seed, float drop_p,
+                      uint16_t* h, uint16_t* xo, void* stream) {
+  PCST_CHECK_ARG(M >= 0 && M * 512 * 2 < (1ll << 31), "resblock_fwd: bad M");
+  PCST_CHECK_ARG(drop_p >= 0.0f && drop_p < 1.0f, "resblock_fwd: dropout p must be in [0, 1)");
+  if (M == 0) return PCST_OK;
+  PCST_CHECK_ARG(x && w1 && b1 && w2 && b2 && h && xo, "resblock_fwd: null pointer");
+  PCST_CHECK_ARG(((uintptr_t)x | (uintptr_t)w1 | (uintptr_t)w2 | (uintptr_t)h | (uintptr_t)xo) % 16 == 0,
+                 "resblock_fwd: pointers must be 16-byte aligned");
+  PCST_CHECK_ARG(xo != x, "resblock_fwd: out of place only");
+  RbArgs a;
+  a.x = x; a.w1 = w1; a.b1 = b1; a.w2 = w2; a.b2 = b2; a.h = h; a.xo = xo; a.M = M;
+  a.seed_lo = (uint32_t)seed;
+  a.seed_hi = (uint32_t)(seed >> 32);
+  a.thr = drop_threshold(drop_p);
+  a.scale = 1.0f / (1.0f - drop_p);
+  const int ntiles = (int)cdiv(M, 128), per = (int)cdiv(ntiles, 8);
+  hipLaunchKernelGGL(resblock_fwd_kernel, dim3((unsigned)(8 * per)), dim3(512), kRbLds,
+                     as_stream(stream), a, per, ntiles);
+  PCST_LAUNCH_CHECK("resblock_fwd");
+  return PCST_OK;
+}
+
 }  // namespace PCST_H16_NS
 }  // namespace pcst
 
@@ -1284,6 +1477,13 @@ extern "C" int pcst_gemm_ex(const void* A, int a_bf16, int64_t M, int64_t K, con
                                         seed, drop_p, group_rows, C, C2, stream)
              : pcst::bf16m::gemm_ex_impl(A, a_bf16, M, K, B, b_bf16, O, bias, relu, epilogue, aux,
                                          seed, drop_p, group_rows, C, C2, stream);
+}
+
+extern "C" int pcst_resblock_fwd16(const uint16_t* x, int64_t M, const uint16_t* w1, const float* b1,
+                                   const uint16_t* w2, const float* b2, uint64_t seed, float drop_p,
+                                   uint16_t* h, uint16_t* x_out, int f16, void* stream) {
+  return f16 ? pcst::f16m::resblock_fwd_impl(x, M, w1, b1, w2, b2, seed, drop_p, h, x_out, stream)
+             : pcst::bf16m::resblock_fwd_impl(x, M, w1, b1, w2, b2, seed, drop_p, h, x_out, stream);
 }
 
 extern "C" int pcst_dropout_grad_bf16(const float* g, int64_t n, uint64_t seed, float drop_p,

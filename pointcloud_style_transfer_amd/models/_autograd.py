@@ -159,6 +159,9 @@ def residual_block(x, layer, training):
 # (False, the stricter round-2 layout).  16-bit halves the bytes of the residual epilogues and
 # lets each Dropout backward ride on the epilogue that produces its gradient.
 RESIDUAL_16BIT = True
+# Each residual block's forward as one launch (pcst_resblock_fwd16: h never re-read from HBM;
+# bit-identical to the EP_BF16 + EP_RESID_DROP16 pair).  tools/knobs.py may turn it off (A/B).
+FUSED_BLOCK_FWD = True
 
 
 class NoisePredictorFn(torch.autograd.Function):
@@ -214,7 +217,10 @@ class NoisePredictorFn(torch.autograd.Function):
             seed = _draw_seed(ps[k])
             seeds.append(seed)
             saved.append(xb)
-            if r16:
+            if r16 and FUSED_BLOCK_FWD and xb.shape[1] == 256 and wb[o].shape == (512, 256):
+                h, xb = _hip.resblock_fwd16(xb, wb[o], wb[o + 1], wb[o + 2], wb[o + 3], seed=seed,
+                                            p=ps[k])
+            elif r16:
                 h = _hip.gemm_ex(xb, wb[o], wb[o + 1], relu=True, epilogue=_hip.EP_BF16)
                 xb = _hip.gemm_ex(h, wb[o + 2], wb[o + 3], epilogue=_hip.EP_RESID_DROP16, aux=xb,
                                   seed=seed, p=ps[k])

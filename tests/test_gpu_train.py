@@ -498,3 +498,25 @@ def test_group_colsum16_vs_float64(H, B, N, C, half):
     assert bool(((out - ref).abs() <= step + 2 * f32_bound).all())
     assert bool((out == ref).double().mean() >= 0.95)
     assert torch.equal(out, H.group_colsum16(g, B))
+
+
+@pytest.mark.parametrize("M", [240000, 1000, 129, 1])
+@pytest.mark.parametrize("p", [0.0, 0.3])
+@pytest.mark.parametrize("half", [torch.float16, torch.bfloat16])
+def test_resblock_fwd16_matches_two_gemms(H, M, p, half):
+    """pcst_resblock_fwd16 (one residual block forward, h never re-read) gives the bits of
+    gemm_ex EP_BF16 followed by EP_RESID_DROP16 with the same (seed, p): h and x' bit-equal, for
+    ragged M, with and without dropout, in both 16-bit formats."""
+    torch.manual_seed(M + int(p * 10))
+    x = (torch.randn(M, 256, device="cuda")).to(half)
+    w1 = (torch.randn(512, 256, device="cuda") * 0.06).to(half)
+    w2 = (torch.randn(256, 512, device="cuda") * 0.04).to(half)
+    b1 = torch.randn(512, device="cuda") * 0.1
+    b2 = torch.randn(256, device="cuda") * 0.1
+    seed = 123456789123
+    h_ref = H.gemm_ex(x, w1, b1, relu=True, epilogue=H.EP_BF16)
+    x_ref = H.gemm_ex(h_ref, w2, b2, epilogue=H.EP_RESID_DROP16, aux=x, seed=seed, p=p)
+    h, xo = H.resblock_fwd16(x, w1, b1, w2, b2, seed=seed, p=p)
+    assert h.dtype == half and xo.dtype == half
+    assert torch.equal(h, h_ref)
+    assert torch.equal(xo, x_ref)
