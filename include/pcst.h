@@ -258,12 +258,15 @@ int pcst_knn3_interp(const float* coarse, const float* orig, const int64_t* idx,
  * producer publishes (pcst_signal_write) -- the consumer reads the workspace only if the flag
  * holds the value when its work-groups start; otherwise (a cross-stream wait that gave up) it
  * leaves the workspace alone and writes 0 for eps, so a timed-out wait can never make it read a
- * half-built workspace.  The caller reports the wait's error word. */
+ * half-built workspace.  The caller reports the wait's error word.
+ * grid_cap (query, search): the query grid's workgroups over all clouds of the launch (each
+ * strides over its cloud's chunks; the result does not depend on it); <= 0: 16384, the winner
+ * of the round-4 A/B at 32 clouds (profiles/r04/a5). */
 int pcst_knn3_build(const float* orig, const int64_t* idx, int64_t B, int64_t N, int64_t M,
                     int64_t lds_floor, int64_t max_wg, void* workspace, void* stream);
 int pcst_knn3_query(const float* coarse, const float* orig, int64_t B, int64_t N, int64_t M,
                     float* out, void* workspace, const uint32_t* built_flag, uint32_t built_value,
-                    void* stream);
+                    int64_t grid_cap, void* stream);
 /* The query in two halves (the same bits as pcst_knn3_query).  search (after build; positions
  * only): every unknown row's three neighbours and float64 IDW weights into the workspace, so it
  * can run beside the noise MLP too; finish: out [B,N,3] from coarse [B,M,3] (the gathers and the
@@ -271,7 +274,7 @@ int pcst_knn3_query(const float* coarse, const float* orig, int64_t B, int64_t N
  * the conditional and unconditional eps of cloud c) fused with pcst_cfg_ddim_step's update of x
  * [C,N,3] (source [C,N,3] or NULL, x_cat [2C,N,3] or NULL). */
 int pcst_knn3_search(const float* orig, int64_t B, int64_t N, int64_t M, void* workspace,
-                     void* stream);
+                     int64_t grid_cap, void* stream);
 int pcst_knn3_finish(const float* coarse, int64_t B, int64_t N, int64_t M, float* out,
                      void* workspace, const uint32_t* built_flag, uint32_t built_value,
                      void* stream);

@@ -51,8 +51,8 @@ SIGNATURES = {
     "pcst_knn3_build": [_P, _P, _I, _I, _I, _I, _I, _P, _P],
     "pcst_cfg_ddim_step_dcoef": [_P, _P, _P, _P, _I, ctypes.c_float, _P, _P, _P, _P],
     "pcst_voxel_downsample_copies_dseed": [_P, _I, _I, _I, _I, _P, _P, _P, _P, _P],
-    "pcst_knn3_query": [_P, _P, _I, _I, _I, _P, _P, _P, ctypes.c_uint32, _P],
-    "pcst_knn3_search": [_P, _I, _I, _I, _P, _P],
+    "pcst_knn3_query": [_P, _P, _I, _I, _I, _P, _P, _P, ctypes.c_uint32, _I, _P],
+    "pcst_knn3_search": [_P, _I, _I, _I, _P, _I, _P],
     "pcst_knn3_finish": [_P, _I, _I, _I, _P, _P, _P, ctypes.c_uint32, _P],
     "pcst_knn3_finish_cfg_ddim": [_P, _I, _I, _I, _P, _P, _P, _F, _F, _F, _F, _F, _P, _P, _P,
                                   ctypes.c_uint32, _P],
@@ -510,11 +510,13 @@ def _built_args(built):
     return ctypes.c_void_p(built.flag.data_ptr()), ctypes.c_uint32(built.value)
 
 
-def knn3_query(coarse, handle, built=None):
+def knn3_query(coarse, handle, built=None, grid_cap=0):
     """Phase 2 of knn3_interp on the current stream: coarse [B,M,3] -> [B,N,3].  built (the
     DeviceSignal the side-stream build signalled): the query reads the workspace only if that
     flag holds its last value (pcst.h: a timed-out wait then yields eps = 0, reported by the
-    signal's error word, instead of a read of a half-built workspace)."""
+    signal's error word, instead of a read of a half-built workspace).  grid_cap: the query
+    grid's workgroups over all clouds (0: the library default; the result never depends on
+    it)."""
     orig, idx, ws = handle
     require_device(coarse)
     coarse = _f32(coarse)
@@ -524,18 +526,18 @@ def knn3_query(coarse, handle, built=None):
         raise RuntimeError(f"knn3_query: coarse {tuple(coarse.shape)} != {(B, M, 3)}")
     out = torch.empty(B, N, 3, dtype=torch.float32, device=orig.device)
     _call("pcst_knn3_query", _ptr(coarse), _ptr(orig), B, N, M, _ptr(out), _ptr(ws),
-          *_built_args(built), _stream())
+          *_built_args(built), int(grid_cap), _stream())
     return out
 
 
-def knn3_search(handle):
+def knn3_search(handle, grid_cap=0):
     """The positions-only half of knn3_query on the current stream (after knn3_build on the
     handle's workspace): every row's three neighbours and IDW weights into the workspace, so
     that only the gather of the coarse values (knn3_finish / knn3_finish_cfg_ddim) waits for
     the noise MLP.  Returns the handle."""
     orig, idx, ws = handle
     B, N, _ = orig.shape
-    _call("pcst_knn3_search", _ptr(orig), B, N, idx.shape[1], _ptr(ws), _stream())
+    _call("pcst_knn3_search", _ptr(orig), B, N, idx.shape[1], _ptr(ws), int(grid_cap), _stream())
     return handle
 
 

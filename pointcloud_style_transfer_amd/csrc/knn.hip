@@ -59,10 +59,10 @@ constexpr int kCountPerBlock = 1024;     // elements per count-kernel block (4 p
 #define PCST_KNN_SORT 0
 #endif
 constexpr int kQueryBlocks = 1024;       // query workgroups per cloud (grid-stride over chunks)
-#ifndef KNN_QUERY_TOTAL  // experiment builds may override
-#define KNN_QUERY_TOTAL (1 << 30)
-#endif
-constexpr int64_t kQueryBlocksTotal = KNN_QUERY_TOTAL;  // cap over all clouds of a launch
+// the query grid's cap over all clouds of one launch, when the caller passes grid_cap <= 0: at
+// 32 clouds (64 CFG rows) 16384 workgroups let each wave stride over several chunks (r04 A/B,
+// profiles/r04/a5: b32 8.79 -> 8.67 ms); at one cloud the per-cloud cap (kQueryBlocks) binds first
+constexpr int64_t kQueryGridCapDefault = 16384;
 constexpr int kQueryBlocksMin = 16;
 constexpr int kOutlierThreads = 1024;    // outlier-pass workgroup
 constexpr int kOutlierBlocks = 128;      // outlier workgroups per cloud (exhaustive pass)
@@ -1703,11 +1703,12 @@ extern "C" int pcst_knn3_build(const float* orig, const int64_t* idx, int64_t B,
 // search, positions only) -> every query row's weights into the workspace's neighbour records.
 static void launch_knn_query(const KnnWS& w, const float* coarse, const float* orig, int64_t B,
                              int64_t N, int64_t M, float* out, NbrRec* nbr, const uint32_t* bflag,
-                             uint32_t bvalue, hipStream_t s) {
+                             uint32_t bvalue, int64_t grid_cap, hipStream_t s) {
   const int b = (int)B;
+  if (grid_cap <= 0) grid_cap = kQueryGridCapDefault;
   // fixed grids stride over the chunk and outlier lists (their lengths live on the device)
   const unsigned gq = (unsigned)std::min<int64_t>(
-      cdiv(w.maxch, 4), std::max<int64_t>(kQueryBlocksMin, std::min<int64_t>(kQueryBlocks, kQueryBlocksTotal / B)));
+      cdiv(w.maxch, 4), std::max<int64_t>(kQueryBlocksMin, std::min<int64_t>(kQueryBlocks, grid_cap / B)));
   auto qk = nbr ? (M >= 3 ? knn_query_kernel<3, true>
                           : (M == 2 ? knn_query_kernel<2, true> : knn_query_kernel<1, true>))
                 : (M >= 3 ? knn_query_kernel<3, false>
@@ -1736,23 +1737,25 @@ static void launch_knn_query(const KnnWS& w, const float* coarse, const float* o
 
 extern "C" int pcst_knn3_query(const float* coarse, const float* orig, int64_t B, int64_t N,
                                int64_t M, float* out, void* workspace, const uint32_t* built_flag,
-                               uint32_t built_value, void* stream) {
+                               uint32_t built_value, int64_t grid_cap, void* stream) {
   PCST_KNN_SHAPE_CHECK("knn3_query");
   if (B == 0) return PCST_OK;
   PCST_CHECK_ARG(coarse && orig && out && workspace, "knn3_query: null pointer");
   KnnWS w = carve_knn(workspace, B, N, M);
-  launch_knn_query(w, coarse, orig, B, N, M, out, nullptr, built_flag, built_value, as_stream(stream));
+  launch_knn_query(w, coarse, orig, B, N, M, out, nullptr, built_flag, built_value, grid_cap,
+                   as_stream(stream));
   PCST_LAUNCH_CHECK("knn3_query");
   return PCST_OK;
 }
 
 extern "C" int pcst_knn3_search(const float* orig, int64_t B, int64_t N, int64_t M,
-                                void* workspace, void* stream) {
+                                void* workspace, int64_t grid_cap, void* stream) {
   PCST_KNN_SHAPE_CHECK("knn3_search");
   if (B == 0) return PCST_OK;
   PCST_CHECK_ARG(orig && workspace, "knn3_search: null pointer");
   KnnWS w = carve_knn(workspace, B, N, M);
-  launch_knn_query(w, nullptr, orig, B, N, M, nullptr, w.nbr, nullptr, 0u, as_stream(stream));
+  launch_knn_query(w, nullptr, orig, B, N, M, nullptr, w.nbr, nullptr, 0u, grid_cap,
+                   as_stream(stream));
   PCST_LAUNCH_CHECK("knn3_search");
   return PCST_OK;
 }
@@ -1796,7 +1799,7 @@ extern "C" int pcst_knn3_interp(const float* coarse, const float* orig, const in
                                 void* stream) {
   int rc = pcst_knn3_build(orig, idx, B, N, M, 0, 0, workspace, stream);
   if (rc) return rc;
-  return pcst_knn3_query(coarse, orig, B, N, M, out, workspace, nullptr, 0u, stream);
+  return pcst_knn3_query(coarse, orig, B, N, M, out, workspace, nullptr, 0u, 0, stream);
 }
 
 #ifdef KNN_TRACE

@@ -325,6 +325,21 @@ def test_knn_build_query_phases_match_interp(H):
     assert torch.equal(H.knn3_query(coarse, H.knn3_build(orig, idx)), ref)
 
 
+@pytest.mark.parametrize("kind", ["gauss", "outliers", "m1"])
+def test_knn_query_grid_cap_does_not_change_bits(H, kind):
+    """pcst_knn3_query / pcst_knn3_search's grid_cap (workgroups over all clouds) only changes
+    how many chunks each wave strides over: 16 (the floor), 64, the default and 2^30 give the
+    same bits."""
+    rng = np.random.default_rng(100 + len(kind))
+    orig, idx = _search_case(kind, rng)
+    coarse = dev(rng.standard_normal((2, idx.shape[1], 3)).astype(np.float32))
+    h = H.knn3_build(orig, idx)
+    ref = H.knn3_query(coarse, h)
+    for cap in (16, 64, 1 << 30):
+        assert torch.equal(H.knn3_query(coarse, h, grid_cap=cap), ref), cap
+        assert torch.equal(H.knn3_finish(coarse, H.knn3_search(h, grid_cap=cap)), ref), cap
+
+
 def _search_case(kind, rng):
     """(orig [2,N,3], idx [2,M]) for the deferred-search tests: a Gaussian cloud, one with far
     outliers (rows the query pass sends to the outlier pass), repeated indices (known rows written

@@ -422,16 +422,18 @@ def test_bf16_pair16_packing_follows_the_kernel_read_schedule():
 
 def test_chaos_floor_constants_match_profile():
     """The end-to-end gates of tests/test_gpu_configs.py quote the chaos floor measured by
-    tools/chaos_floor.py (profiles/r03/chaos_floor.json); keep the two in step."""
+    tools/chaos_floor.py (profiles/r04/chaos_floor.json: 10, 50 and 1000 steps); keep the two in
+    step."""
     import json
 
     import test_gpu_configs as G
 
     from conftest import REPO
 
-    rec = json.load(open(os.path.join(REPO, "profiles", "r03", "chaos_floor.json")))
+    rec = json.load(open(os.path.join(REPO, "profiles", "r04", "chaos_floor.json")))
     assert rec["weights"] == "det"
-    for steps, consts in (("50", G.CHAOS_FLOOR_50), ("10", G.CHAOS_FLOOR_10)):
+    for steps, consts in (("50", G.CHAOS_FLOOR_50), ("10", G.CHAOS_FLOOR_10),
+                          ("1000", G.CHAOS_FLOOR_1000)):
         for k, v in consts.items():
             assert abs(rec["runs"][steps][k] - v) <= 1e-3 * v, (steps, k)
 
