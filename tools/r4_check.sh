@@ -115,8 +115,6 @@ for st in "$@"; do
     loop1000)
       timeout -k 10 600 python -u tools/loop1000_probe.py > "$OUT/loop1000.jsonl" 2> "$OUT/loop1000.err"
       rc=$?; echo "loop1000 rc=$rc"; cat "$OUT/loop1000.jsonl"; if [ $rc -ne 0 ]; then tail -3 "$OUT/loop1000.err"; exit $rc; fi ;;
-    qcap)
-      bash tools/knn_qcap_ab.sh "$TAG/qcap" || exit 1 ;;
     *) echo "unknown stage $st"; exit 2 ;;
   esac
 done
