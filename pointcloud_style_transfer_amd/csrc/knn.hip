@@ -58,6 +58,9 @@ constexpr int kCountPerBlock = 1024;     // elements per count-kernel block (4 p
 #ifndef PCST_KNN_SORT  // 1: the sort build (no global atomic per element); 0: the atomic build
 #define PCST_KNN_SORT 0
 #endif
+#ifndef PCST_KNN_SLOTKEY  // 1: the one-pass slot-keyed query window (Query::window); 0: two-pass
+#define PCST_KNN_SLOTKEY 1
+#endif
 constexpr int kQueryBlocks = 1024;       // query workgroups per cloud (grid-stride over chunks)
 // the query grid's cap over all clouds of one launch, when the caller passes grid_cap <= 0: at
 // 32 clouds (64 CFG rows) 16384 workgroups let each wave stride over several chunks (r04 A/B,
@@ -824,6 +827,81 @@ struct Query {
     const float n2 = __builtin_amdgcn_fmed3f(c1, c2, d);
     c0 = n0; c1 = n1; c2 = n2;
   }
+#if PCST_KNN_SLOTKEY
+  // Slot-keyed window (one pass over the staged refs): each fp32 distance with its low 9
+  // mantissa bits replaced by the ref's window slot (< kCandCap = 512) is a key whose order is
+  // the distances' order up to 2^-14 relative; the four smallest keys are kept branch-free
+  // (min / med3, on the keys as non-negative floats).  Ranked exactly: the three smallest keys'
+  // refs (all three whatever kk: extra candidates are harmless).  Screen sc = min(upper(kk-th
+  // key) (1 + 2e-6), thr) bounds every exact top-kk member's
+  // fp32 distance (at least kk refs lie at or below the kk-th key's upper end), and every ref
+  // within sc that is not among the three ranked has a key >= the fourth, so lanes whose fourth
+  // key's lower end lies within sc (near-ties: ~1e-3 of the lanes) re-screen the window the
+  // two-pass way.  The exact top-3 is order-independent and repeats are rejected, so the result
+  // is the bit-identical one of the two-pass window.
+  static __device__ __forceinline__ float key_lo(float k) { return __uint_as_float(__float_as_uint(k) & ~511u); }
+  static __device__ __forceinline__ float key_hi(float k) {
+    return k == INFINITY ? INFINITY : __uint_as_float(__float_as_uint(k) | 511u);
+  }
+  __device__ __forceinline__ void window(const Win& W, int fill, int kk) {
+    const float ax = fx, ay = fy, az = fz;  // by value: keeps the query out of private memory
+    const f2 qx = {ax, ax}, qy = {ay, ay}, qz = {az, az};
+    float k0 = INFINITY, k1 = INFINITY, k2 = INFINITY, k3 = INFINITY;
+    auto put = [&](float d, int slot) {
+      const float key = __uint_as_float((__float_as_uint(d) & ~511u) | (unsigned)slot);
+      const float n0 = fminf(k0, key);
+      const float n1 = __builtin_amdgcn_fmed3f(k0, k1, key);
+      const float n2 = __builtin_amdgcn_fmed3f(k1, k2, key);
+      const float n3 = __builtin_amdgcn_fmed3f(k2, k3, key);
+      k0 = n0; k1 = n1; k2 = n2; k3 = n3;
+    };
+    int i = 0;
+    for (; i + 4 <= fill; i += 4) {
+      f2 d01, d23;
+      dist4(W, i, qx, qy, qz, d01, d23);
+      put(d01.x, i);
+      put(d01.y, i + 1);
+      put(d23.x, i + 2);
+      put(d23.y, i + 3);
+    }
+    for (; i < fill; ++i) put(dist1(W, i, ax, ay, az), i);
+    const float ck = kk >= 3 ? k2 : (kk == 2 ? k1 : k0);
+    const float sc = fminf(key_hi(ck) * 1.000002f + 1e-30f, thr);
+    const bool again = k3 != INFINITY && key_lo(k3) <= sc;
+    auto rank = [&](float k) {
+      if (k == INFINITY) return;
+      const int s = (int)(__float_as_uint(k) & 511u);
+      exact(make_float4(W.x[s], W.y[s], W.z[s], __int_as_float(W.j[s])));
+    };
+    rank(k0);
+    rank(k1);
+    rank(k2);
+    if (__any(again)) rescreen(W, fill, again ? sc : -1.0f);
+    if (t.last(kk) != INFINITY) thr = fminf(thr, (float)(t.last(kk) * (1.0 + 2e-6)) + 1e-30f);
+  }
+  // the two-pass window's second pass for the lanes that need it (sc < 0: none)
+  __device__ __forceinline__ void rescreen(const Win& W, int fill, float sc) {
+    const float ax = fx, ay = fy, az = fz;
+    const f2 qx = {ax, ax}, qy = {ay, ay}, qz = {az, az};
+    for (int b0 = 0; b0 < fill; b0 += 64) {
+      const int nb = min(64, fill - b0);
+      uint64_t m = 0;
+      int u = 0;
+      for (; u + 4 <= nb; u += 4) {
+        f2 d01, d23;
+        dist4(W, b0 + u, qx, qy, qz, d01, d23);
+        m |= ((uint64_t)(d01.x <= sc) | ((uint64_t)(d01.y <= sc) << 1) |
+              ((uint64_t)(d23.x <= sc) << 2) | ((uint64_t)(d23.y <= sc) << 3)) << u;
+      }
+      for (; u < nb; ++u) m |= (uint64_t)(dist1(W, b0 + u, ax, ay, az) <= sc) << u;
+      while (m) {
+        const int k = b0 + __builtin_ctzll(m);
+        m &= m - 1;
+        exact(make_float4(W.x[k], W.y[k], W.z[k], __int_as_float(W.j[k])));
+      }
+    }
+  }
+#else
   __device__ __forceinline__ void window(const Win& W, int fill, int kk) {
     const float ax = fx, ay = fy, az = fz;  // by value: keeps the query out of private memory
     const f2 qx = {ax, ax}, qy = {ay, ay}, qz = {az, az};
@@ -860,6 +938,7 @@ struct Query {
     }
     if (t.last(kk) != INFINITY) thr = fminf(thr, (float)(t.last(kk) * (1.0 + 2e-6)) + 1e-30f);
   }
+#endif
 };
 
 // LDS reads/writes of this wave done (before the window is overwritten or read)

@@ -1283,6 +1283,11 @@ int wgrad_ex_impl(const void* dZ, int dz_bf16, const void* X, int x_bf16, int64_
 // each 128 x 128 output tile.  The weights stream through a double-buffered 64-deep B slice:
 // per chunk 4 slices of W1 (K = 256) then 2 x 2 slices of W2 (the two output halves, K = 128).
 constexpr int kRbK = 64;                 // weight slice depth
+#ifndef PCST_RB_PF  // experiment builds: weight slices in flight (1, 2 or 4; divides 32)
+#define PCST_RB_PF 4
+#endif
+constexpr int kRbPF = PCST_RB_PF;
+static_assert(32 % kRbPF == 0, "kRbPF must divide 32");
 constexpr int kRbBLd = kRbK + 8;         // B image row (16-bit elements): 144 B, conflict-free
 constexpr int kRbXLd = 256 + 8;          // x tile row: 528 B
 constexpr int kRbHLd = 128 + 8;          // h chunk row: 272 B
@@ -1350,15 +1355,21 @@ __global__ __launch_bounds__(512) void resblock_fwd_kernel(RbArgs a, int per_xcd
   for (int u = 0; u < 2; ++u) acc1[u] = f32x16{};
 #pragma unroll
   for (int u = 0; u < 4; ++u) acc2[u] = f32x16{};
-  uint4 g0, g1;
-  load_slice(0, g0, g1);
+  // kRbPF register stages: slice i is loaded kRbPF slices before its LDS store, so the L2
+  // latency of the weight stream hides behind kRbPF slices of MFMAs (one stage exposed it)
+  uint4 g[kRbPF][2];
+#pragma unroll
+  for (int u = 0; u < kRbPF; ++u) load_slice(u, g[u][0], g[u][1]);
   const int arow = 32 * wr + l32;
-  for (int i = 0; i < 32; ++i) {
+  for (int i0 = 0; i0 < 32; i0 += kRbPF)
+#pragma unroll
+  for (int u = 0; u < kRbPF; ++u) {
+    const int i = i0 + u;
     h16* Bs = (i & 1) ? Bs1 : Bs0;
-    *reinterpret_cast<uint4*>(Bs + br * kRbBLd + bk) = g0;
-    *reinterpret_cast<uint4*>(Bs + br * kRbBLd + bk + 8) = g1;
+    *reinterpret_cast<uint4*>(Bs + br * kRbBLd + bk) = g[u][0];
+    *reinterpret_cast<uint4*>(Bs + br * kRbBLd + bk + 8) = g[u][1];
     __syncthreads();  // this slice landed; the previous slice's (and epilogue's) readers are done
-    if (i + 1 < 32) load_slice(i + 1, g0, g1);
+    if (i + kRbPF < 32) load_slice(i + kRbPF, g[u][0], g[u][1]);
     const int c = i >> 3, j = i & 7;
     if (j == 4) {
       // chunk c's h (written to Hs by every wave after slice 8c + 3) -> global h, coalesced:

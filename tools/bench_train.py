@@ -41,6 +41,10 @@ def main():
                     help="Config.amp_dtype (float16: the reference's CUDA autocast)")
     args = ap.parse_args()
 
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    import knobs  # A/B knobs (environment), tools/ only
+
+    knobs.apply()
     from pointcloud_style_transfer_amd import _hip
     from pointcloud_style_transfer_amd.config.config import Config
     from pointcloud_style_transfer_amd.distributed import init_from_env, max_over_ranks, shard

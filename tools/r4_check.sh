@@ -73,14 +73,21 @@ for st in "$@"; do
       for k in "gemm_bf_kernel<1" "gemm_bf_kernel<3" "gemm_bf_kernel<6" "gemm_bf_kernel<7" wgrad_ex_kernel; do
         echo "== $k"; python tools/pmc_sq.py "$OUT" "$k"
       done | tee "$OUT/train_sq.txt" ;;
+    trainprof)
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/tprof" -o run -- \
+          python tools/bench_train.py --steps 4 --warmup 2 > "$OUT/tprof.json" 2> "$OUT/tprof.err"
+      rc=$?; echo "trainprof rc=$rc"; if [ $rc -ne 0 ]; then tail -5 "$OUT/tprof.err"; exit $rc; fi
+      python tools/kstats.py "$OUT/tprof/run_kernel_stats.csv" 40 | tee "$OUT/train_kernel_top.txt" ;;
     trainab=*)
       # trainab=v_a,v_b: bench_train.py with the product library and each experiment library
       # pointcloud_style_transfer_amd/libpcst_hip_<v>.so, two alternating passes
       VS=${st#trainab=}
       for pass in 1 2; do
         for v in prod ${VS//,/ }; do
-          if [ "$v" = prod ]; then lib=$PWD/pointcloud_style_transfer_amd/libpcst_hip.so; else lib=$PWD/pointcloud_style_transfer_amd/libpcst_hip_$v.so; fi
-          PCST_LIB=$lib timeout -k 10 300 python tools/bench_train.py > "$OUT/train_$v.$pass.json" 2> "$OUT/train_$v.$pass.err"
+          # v_name: experiment library; NAME=VAL: the product library with that knob (tools/knobs.py)
+          lib=$PWD/pointcloud_style_transfer_amd/libpcst_hip.so; kv=PCST_NONE=1
+          case $v in prod) ;; *=*) kv=$v ;; *) lib=$PWD/pointcloud_style_transfer_amd/libpcst_hip_$v.so ;; esac
+          env "$kv" PCST_LIB=$lib timeout -k 10 300 python tools/bench_train.py > "$OUT/train_$v.$pass.json" 2> "$OUT/train_$v.$pass.err"
           rc=$?; if [ $rc -ne 0 ]; then tail -3 "$OUT/train_$v.$pass.err"; exit $rc; fi
           python -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print(sys.argv[2], d['ms_per_step'], d['final_loss'])" "$OUT/train_$v.$pass.json" "$v.$pass"
         done
