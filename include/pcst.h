@@ -132,6 +132,16 @@ int pcst_group_gather_bwd(const float* dgrouped, const int64_t* group_idx, int64
 int pcst_resblock_fwd16(const uint16_t* x, int64_t M, const uint16_t* w1, const float* b1,
                         const uint16_t* w2, const float* b2, uint64_t seed, float drop_p,
                         uint16_t* h, uint16_t* x_out, int f16, void* stream);
+/* The same block's backward products in one launch (the autograd backward of the block above,
+ * trainer.py:106): dz [M,512] = 16-bit((dd W2) * [h > 0]), g_out [M,256] = 16-bit(g + dz W1) and,
+ * if dd_out is not NULL, dd_out [M,256] = 16-bit(g_out keep / (1 - p)) with keep the dropout mask
+ * of (seed, p) -- the previous block's, as pcst_gemm_ex's EP_ADD16 dropout copy.  w2t = W2^T
+ * [512,256] and w1t = W1^T [256,512] in the 16-bit format.  The bits of pcst_gemm_ex EP_RELU_MASK
+ * (aux h) followed by EP_ADD16 (aux g); dz is written for dW1 = dz^T x but never re-read here.
+ * 16-byte aligned pointers, g_out != dd, dz != h, M * 1024 < 2^31. */
+int pcst_resblock_bwd16(const uint16_t* dd, int64_t M, const uint16_t* w2t, const uint16_t* w1t,
+                        const uint16_t* h, const uint16_t* g, uint64_t seed, float drop_p,
+                        uint16_t* dz, uint16_t* g_out, uint16_t* dd_out, int f16, void* stream);
 int pcst_group_colsum16_workspace_size(int64_t B, int64_t C, size_t* bytes);
 int pcst_group_colsum16(const uint16_t* G, int f16, int64_t B, int64_t N, int64_t C, float* out,
                         void* workspace, void* stream);

@@ -74,6 +74,7 @@ SIGNATURES = {
     "pcst_linear_wgrad_bf16_workspace_size": [_I, _I, _I, _SZ],
     "pcst_linear_wgrad_bf16": [_P, _P, _I, _I, _I, _P, _P, _P, ctypes.c_int, _P],
     "pcst_resblock_fwd16": [_P, _I, _P, _P, _P, _P, ctypes.c_uint64, _F, _P, _P, ctypes.c_int, _P],
+    "pcst_resblock_bwd16": [_P, _I, _P, _P, _P, _P, ctypes.c_uint64, _F, _P, _P, _P, ctypes.c_int, _P],
     "pcst_gemm_ex": [_P, ctypes.c_int, _I, _I, _P, ctypes.c_int, _I, _P, ctypes.c_int,
                      ctypes.c_int, _P, ctypes.c_uint64, _F, _I, _P, _P, ctypes.c_int, _P],
     "pcst_dropout_grad_bf16": [_P, _I, ctypes.c_uint64, _F, _P, ctypes.c_int, _P],
@@ -814,6 +815,33 @@ def resblock_fwd16(x, w1, b1, w2, b2, seed=0, p=0.0):
     return h, out
 
 
+def resblock_bwd16(dd, w2t, w1t, h, g, seed=0, p=0.0, dropout_copy=False):
+    """The backward products of one residual block in one launch (pcst_resblock_bwd16): dd, g
+    [M,256] and h [M,512] 16-bit, w2t = W2^T [512,256] / w1t = W1^T [256,512] 16-bit ->
+    (dz [M,512] = (dd W2) * [h > 0], g' [M,256] = g + dz W1, and with dropout_copy the previous
+    block's dD' = g' keep / (1 - p) under (seed, p), else None), all 16-bit: the bits of gemm_ex
+    EP_RELU_MASK (aux h) followed by EP_ADD16 (aux g, dropout_copy)."""
+    require_device(dd, w2t, w1t, h, g)
+    half = dd.dtype
+    if half not in (torch.float16, torch.bfloat16):
+        raise RuntimeError(f"resblock_bwd16: dd must be float16 or bfloat16, got {dd.dtype}")
+    M = dd.shape[0]
+    if (dd.dim() != 2 or dd.shape[1] != 256 or tuple(w2t.shape) != (512, 256)
+            or tuple(w1t.shape) != (256, 512) or tuple(h.shape) != (M, 512)
+            or tuple(g.shape) != (M, 256)
+            or any(t.dtype != half for t in (w2t, w1t, h, g))):
+        raise RuntimeError("resblock_bwd16: shapes are dd [M,256], w2t [512,256], w1t [256,512], "
+                           "h [M,512], g [M,256] in dd's 16-bit format")
+    dd, w2t, w1t, h, g = (t.contiguous() for t in (dd, w2t, w1t, h, g))
+    dz = torch.empty(M, 512, dtype=half, device=dd.device)
+    g_out = torch.empty(M, 256, dtype=half, device=dd.device)
+    dd_out = torch.empty(M, 256, dtype=half, device=dd.device) if dropout_copy else None
+    _call("pcst_resblock_bwd16", _ptr(dd), M, _ptr(w2t), _ptr(w1t), _ptr(h), _ptr(g),
+          int(seed) & (2**64 - 1), float(p), _ptr(dz), _ptr(g_out), _ptr(dd_out),
+          1 if half == torch.float16 else 0, _stream())
+    return dz, g_out, dd_out
+
+
 def gemm_ex(A, B, bias=None, relu=False, epilogue=EP_F32, aux=None, seed=0, p=0.0,
             group_rows=0, copy_bf16=False, half=None, dropout_copy=False, fp32_out=True):
     """A [M,K], B [O,K] (fp32 or 16-bit) -> epilogue(A B^T) on 16-bit MFMA (csrc/train_mlp.hip):
@@ -1132,7 +1160,7 @@ _GUARDED = ("square_distance", "index_points", "fps", "ball_query", "group_gathe
             "linear_wgrad", "gemm_nt_bf16", "channel_stats", "affine_act", "chamfer_fwd",
             "chamfer_bwd", "l1_fwd", "l1_bwd", "knn_dist", "emd_greedy", "voxel_center_dist",
             "cfg_ddim_step_dcoef", "voxel_downsample_copies_dseed", "bn_train_coeffs",
-            "bn_relu_maxpool", "bn_relu_bwd", "group_gather_bwd", "group_colsum16", "resblock_fwd16",
+            "bn_relu_maxpool", "bn_relu_bwd", "group_gather_bwd", "group_colsum16", "resblock_fwd16", "resblock_bwd16",
             "gemm_ex", "dropout_grad_bf16",
             "linear_wgrad_ex", "knn_workspace")
 for _name in _GUARDED:

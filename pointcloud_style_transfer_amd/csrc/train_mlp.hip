@@ -50,6 +50,7 @@ typedef __bf16 h16;
 #endif
 typedef __attribute__((ext_vector_type(8))) h16 h16x8;
 typedef __attribute__((ext_vector_type(4))) h16 h16x4;
+typedef __attribute__((ext_vector_type(2))) h16 h16x2;
 typedef short v4i16 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ f32x16 mfma32_h16(h16x8 a, h16x8 b, f32x16 c) {
@@ -1297,19 +1298,31 @@ constexpr int kRbBBytes = 128 * kRbBLd * 2;
 constexpr int kRbLds = kRbXBytes + kRbHBytes + 2 * kRbBBytes;
 
 struct RbArgs {
-  const uint16_t* x;   // [M, 256]
-  const uint16_t* w1;  // [512, 256]
-  const float* b1;     // [512]
-  const uint16_t* w2;  // [256, 512]
-  const float* b2;     // [256]
-  uint16_t* h;         // [M, 512]
-  uint16_t* xo;        // [M, 256]
+  const uint16_t* x;   // [M, 256]   the A operand: x (forward) / dD (backward)
+  const uint16_t* w1;  // [512, 256] first product's weight rows: W1 / W2^T
+  const float* b1;     // [512]      (forward only)
+  const uint16_t* w2;  // [256, 512] second product's weight rows: W2 / W1^T
+  const float* b2;     // [256]      (forward only)
+  uint16_t* h;         // [M, 512]   written: h (forward) / dZ (backward)
+  uint16_t* xo;        // [M, 256]   written: x' (forward) / g' (backward)
+  const uint16_t* hm;  // [M, 512]   backward: the block's h (ReLU mask)
+  const uint16_t* g;   // [M, 256]   backward: the residual gradient
+  uint16_t* ddo;       // [M, 256]   backward, optional: dropout copy of g' (previous block's rate)
   int64_t M;
   uint32_t seed_lo, seed_hi, thr;
   float scale;
 };
 
-__global__ __launch_bounds__(512) void resblock_fwd_kernel(RbArgs a, int per_xcd, int ntiles) {
+// BWD = false: the forward above.  BWD = true: the block's backward products in the same pass,
+//   dZ = 16-bit((dD W2) * [h > 0])          [M, 512]   (EP_RELU_MASK; written for dW1 = dZ^T x)
+//   g' = 16-bit(g + dZ W1)                   [M, 256]   (EP_ADD16)
+//   dD' = 16-bit(g' keep / (1 - p))          [M, 256]   (EP_ADD16's dropout copy, optional)
+// with dD in the x tile, W2^T / W1^T as the two weight streams, each chunk's mask read into the
+// chunk buffer two slices before its epilogue, and g loaded into the x tile once the last
+// first-product slice has read it.  Bit-identical to the two gemm_ex calls (the fast epilogue's
+// "+ 0" bias included: it turns a -0 product into +0).
+template <bool BWD>
+__global__ __launch_bounds__(512) void resblock_kernel(RbArgs a, int per_xcd, int ntiles) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   h16* Xs = reinterpret_cast<h16*>(smem);                                   // [128][kRbXLd]
   h16* Hs = reinterpret_cast<h16*>(smem + kRbXBytes);                       // [128][kRbHLd]
@@ -1350,31 +1363,77 @@ __global__ __launch_bounds__(512) void resblock_fwd_kernel(RbArgs a, int per_xcd
     g0 = bload16(r, off, 0);
     g1 = bload16(r, off + 16, 0);
   };
+  const rsrc_t rh = make_rsrc(a.h, (uint32_t)(M * 512 * 2));
+  const rsrc_t rm = make_rsrc(BWD ? a.hm : nullptr, BWD ? (uint32_t)(M * 512 * 2) : 0u);
+  const rsrc_t rg = make_rsrc(BWD ? a.g : nullptr, BWD ? (uint32_t)(M * 256 * 2) : 0u);
+  uint4 mk[4], gr[8];  // backward: a chunk's mask rows, the residual gradient tile
+  // the lane's biases, loaded up front: a load issued at its use would wait (in-order vmcnt)
+  // for every weight slice in flight as well
+  float bb1[4][2], bb2[4];
+#pragma unroll
+  for (int c = 0; c < 4; ++c)
+#pragma unroll
+    for (int bn = 0; bn < 2; ++bn) bb1[c][bn] = BWD ? 0.0f : a.b1[128 * c + 64 * wc + 32 * bn + l32];
+#pragma unroll
+  for (int u = 0; u < 4; ++u)
+    bb2[u] = BWD ? 0.0f : a.b2[128 * (u >> 1) + 64 * wc + 32 * (u & 1) + l32];
   f32x16 acc1[2], acc2[4];
 #pragma unroll
   for (int u = 0; u < 2; ++u) acc1[u] = f32x16{};
 #pragma unroll
   for (int u = 0; u < 4; ++u) acc2[u] = f32x16{};
-  // kRbPF register stages: slice i is loaded kRbPF slices before its LDS store, so the L2
-  // latency of the weight stream hides behind kRbPF slices of MFMAs (one stage exposed it)
+  // kRbPF register stages: slice s lives in g[s % kRbPF] from its load, kRbPF slices ahead,
+  // until its LDS store, one slice ahead: iteration i stores slice i + 1 into the other buffer
+  // after the barrier, so the store overlaps slice i's MFMAs instead of preceding them
   uint4 g[kRbPF][2];
 #pragma unroll
   for (int u = 0; u < kRbPF; ++u) load_slice(u, g[u][0], g[u][1]);
+  *reinterpret_cast<uint4*>(Bs0 + br * kRbBLd + bk) = g[0][0];
+  *reinterpret_cast<uint4*>(Bs0 + br * kRbBLd + bk + 8) = g[0][1];
+  if (kRbPF < 32) load_slice(kRbPF, g[0][0], g[0][1]);
   const int arow = 32 * wr + l32;
   for (int i0 = 0; i0 < 32; i0 += kRbPF)
 #pragma unroll
   for (int u = 0; u < kRbPF; ++u) {
     const int i = i0 + u;
     h16* Bs = (i & 1) ? Bs1 : Bs0;
-    *reinterpret_cast<uint4*>(Bs + br * kRbBLd + bk) = g[u][0];
-    *reinterpret_cast<uint4*>(Bs + br * kRbBLd + bk + 8) = g[u][1];
-    __syncthreads();  // this slice landed; the previous slice's (and epilogue's) readers are done
-    if (i + kRbPF < 32) load_slice(i + kRbPF, g[u][0], g[u][1]);
+    __syncthreads();  // slice i landed; slice i - 1's (and the epilogue's) readers are done
+    if (i + 1 < 32) {
+      const int un = (u + 1) % kRbPF;
+      h16* Bn = (i & 1) ? Bs0 : Bs1;
+      *reinterpret_cast<uint4*>(Bn + br * kRbBLd + bk) = g[un][0];
+      *reinterpret_cast<uint4*>(Bn + br * kRbBLd + bk + 8) = g[un][1];
+      if (i + 1 + kRbPF < 32) load_slice(i + 1 + kRbPF, g[un][0], g[un][1]);
+    }
     const int c = i >> 3, j = i & 7;
+    if (BWD && j == 0) {
+      // chunk c's mask rows, coalesced (128 rows x 16 chunks of 16 B, 4 per thread)
+#pragma unroll
+      for (int it = 0; it < 4; ++it) {
+        const int q = it * 512 + tid, r = q >> 4, cch = (q & 15) * 8;
+        mk[it] = bload16(rm, (uint32_t)(((m0 + r) * 512 + 128 * c + cch) * 2), 0);
+      }
+    }
+    if (BWD && j == 2) {
+      // -> Hs: the previous chunk's second-product readers passed this slice's barrier; the
+      // epilogue reads it after the next one
+#pragma unroll
+      for (int it = 0; it < 4; ++it) {
+        const int q = it * 512 + tid, r = q >> 4, cch = (q & 15) * 8;
+        *reinterpret_cast<uint4*>(Hs + r * kRbHLd + cch) = mk[it];
+      }
+    }
+    if (BWD && i == 28) {
+      // g tile: Xs is read for the last time by slice 27's first product
+#pragma unroll
+      for (int it = 0; it < 8; ++it) {
+        const int q = it * 512 + tid, r = q >> 5, cch = (q & 31) * 8;
+        gr[it] = bload16(rg, (uint32_t)(((m0 + r) * 256 + cch) * 2), 0);
+      }
+    }
     if (j == 4) {
       // chunk c's h (written to Hs by every wave after slice 8c + 3) -> global h, coalesced:
       // 128 rows x 16 chunks of 16 B, 4 per thread
-      const rsrc_t rh = make_rsrc(a.h, (uint32_t)(M * 512 * 2));
 #pragma unroll
       for (int it = 0; it < 4; ++it) {
         const int q = it * 512 + tid, r = q >> 4, cch = (q & 15) * 8;
@@ -1406,35 +1465,49 @@ __global__ __launch_bounds__(512) void resblock_fwd_kernel(RbArgs a, int per_xcd
       }
     }
     if (j == 3) {
-      // chunk c's epilogue: h = 16-bit(relu(acc1 + b1)) into Hs (read by every wave after the
-      // next slice's barrier); the accumulators restart for chunk c + 1
+      // chunk c's epilogue into Hs (read by every wave after the next slice's barrier): forward
+      // h = 16-bit(relu(acc1 + b1)); backward dZ = 16-bit(acc1 + 0 masked by h > 0), the mask
+      // read from the lane's own element.  The accumulators restart for chunk c + 1.
 #pragma unroll
       for (int bn = 0; bn < 2; ++bn) {
         const int col = 64 * wc + 32 * bn + l32;
-        const float bb = a.b1[128 * c + col];
+        const float bb = bb1[c][bn];
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const float v = fmaxf(acc1[bn][r] + bb, 0.0f);
-          Hs[(32 * wr + xrow(r, h)) * kRbHLd + col] = (h16)v;
+          h16* ph = Hs + (32 * wr + xrow(r, h)) * kRbHLd + col;
+          float v = acc1[bn][r] + bb;
+          if (BWD) v = __builtin_bit_cast(int16_t, *ph) > 0 ? v : 0.0f;
+          else v = fmaxf(v, 0.0f);
+          *ph = (h16)v;
         }
         acc1[bn] = f32x16{};
       }
     }
   }
+  if (BWD) {
+#pragma unroll
+    for (int it = 0; it < 8; ++it) {
+      const int q = it * 512 + tid, r = q >> 5, cch = (q & 31) * 8;
+      *reinterpret_cast<uint4*>(Xs + r * kRbXLd + cch) = gr[it];
+    }
+  }
   __syncthreads();  // every wave's W2 products done; Xs is read below only by its owner lanes
-  // x' = 16-bit(x + Dropout(acc2 + b2)), in place in Xs, then a coalesced copy out
+  // forward x' = 16-bit(x + Dropout(acc2 + b2)); backward g' = 16-bit((acc2 + 0) + g): in place
+  // in Xs, then a coalesced copy out
 #pragma unroll
   for (int u = 0; u < 4; ++u) {
     const int oh = u >> 1, bn = u & 1;
     const int col = 128 * oh + 64 * wc + 32 * bn + l32;
-    const float bb = a.b2[col];
+    const float bb = bb2[u];
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int row = 32 * wr + xrow(r, h);
-      const uint32_t e = (uint32_t)((m0 + row) * 256 + col);
       float y = acc2[u][r] + bb;
-      const bool keep = drop_hash(a.seed_lo, a.seed_hi, (uint64_t)e) >= a.thr;
-      y = keep ? y * a.scale : 0.0f;
+      if (!BWD) {
+        const uint32_t e = (uint32_t)((m0 + row) * 256 + col);
+        const bool keep = drop_hash(a.seed_lo, a.seed_hi, (uint64_t)e) >= a.thr;
+        y = keep ? y * a.scale : 0.0f;
+      }
       h16* px = Xs + row * kRbXLd + col;
       y += (float)*px;
       *px = (h16)y;
@@ -1442,12 +1515,34 @@ __global__ __launch_bounds__(512) void resblock_fwd_kernel(RbArgs a, int per_xcd
   }
   __syncthreads();
   const rsrc_t ro = make_rsrc(a.xo, (uint32_t)(M * 256 * 2));
+  const rsrc_t rd = make_rsrc(BWD ? a.ddo : nullptr, BWD && a.ddo ? (uint32_t)(M * 256 * 2) : 0u);
 #pragma unroll
   for (int it = 0; it < 8; ++it) {
     const int q = it * 512 + tid, r = q >> 5, cch = (q & 31) * 8;
     const uint4 v = *reinterpret_cast<const uint4*>(Xs + r * kRbXLd + cch);
-    const v4i32 vv = {(int)v.x, (int)v.y, (int)v.z, (int)v.w};
-    __builtin_amdgcn_raw_buffer_store_b128(vv, ro, (int)(((m0 + r) * 256 + cch) * 2), 0, 0);
+    const int off = (int)(((m0 + r) * 256 + cch) * 2);
+    __builtin_amdgcn_raw_buffer_store_b128(v4i32{(int)v.x, (int)v.y, (int)v.z, (int)v.w}, ro, off, 0, 0);
+    if (BWD && a.ddo) {  // dD' = 16-bit(g' keep / (1 - p)), element e = (m0 + r) * 256 + cch + u
+      const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+      uint32_t o[4];
+      const uint32_t e0 = (uint32_t)((m0 + r) * 256 + cch);
+#pragma unroll
+      for (int u2 = 0; u2 < 4; ++u2) {
+        float d[2];
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          const uint32_t e = e0 + 2 * u2 + s2;
+          const bool keep = drop_hash(a.seed_lo, a.seed_hi, (uint64_t)e) >= a.thr;
+          const float yr = h16_to_f32((w[u2] >> (16 * s2)) & 0xffffu);
+          d[s2] = keep ? yr * a.scale : 0.0f;
+        }
+        h16x2 pk;
+        pk[0] = (h16)d[0];
+        pk[1] = (h16)d[1];
+        o[u2] = __builtin_bit_cast(uint32_t, pk);
+      }
+      __builtin_amdgcn_raw_buffer_store_b128(v4i32{(int)o[0], (int)o[1], (int)o[2], (int)o[3]}, rd, off, 0, 0);
+    }
   }
 }
 
@@ -1468,9 +1563,35 @@ int resblock_fwd_impl(const uint16_t* x, int64_t M, const uint16_t* w1, const fl
   a.thr = drop_threshold(drop_p);
   a.scale = 1.0f / (1.0f - drop_p);
   const int ntiles = (int)cdiv(M, 128), per = (int)cdiv(ntiles, 8);
-  hipLaunchKernelGGL(resblock_fwd_kernel, dim3((unsigned)(8 * per)), dim3(512), kRbLds,
+  a.hm = nullptr; a.g = nullptr; a.ddo = nullptr;
+  hipLaunchKernelGGL(resblock_kernel<false>, dim3((unsigned)(8 * per)), dim3(512), kRbLds,
                      as_stream(stream), a, per, ntiles);
   PCST_LAUNCH_CHECK("resblock_fwd");
+  return PCST_OK;
+}
+
+int resblock_bwd_impl(const uint16_t* dd, int64_t M, const uint16_t* w2t, const uint16_t* w1t,
+                      const uint16_t* h, const uint16_t* g, uint64_t seed, float drop_p,
+                      uint16_t* dz, uint16_t* g_out, uint16_t* dd_out, void* stream) {
+  PCST_CHECK_ARG(M >= 0 && M * 512 * 2 < (1ll << 31), "resblock_bwd: bad M");
+  PCST_CHECK_ARG(drop_p >= 0.0f && drop_p < 1.0f, "resblock_bwd: dropout p must be in [0, 1)");
+  if (M == 0) return PCST_OK;
+  PCST_CHECK_ARG(dd && w2t && w1t && h && g && dz && g_out, "resblock_bwd: null pointer");
+  PCST_CHECK_ARG(((uintptr_t)dd | (uintptr_t)w2t | (uintptr_t)w1t | (uintptr_t)h | (uintptr_t)g |
+                  (uintptr_t)dz | (uintptr_t)g_out | (uintptr_t)dd_out) % 16 == 0,
+                 "resblock_bwd: pointers must be 16-byte aligned");
+  PCST_CHECK_ARG(g_out != dd && dz != h, "resblock_bwd: out of place only");
+  RbArgs a;
+  a.x = dd; a.w1 = w2t; a.b1 = nullptr; a.w2 = w1t; a.b2 = nullptr; a.h = dz; a.xo = g_out;
+  a.hm = h; a.g = g; a.ddo = dd_out; a.M = M;
+  a.seed_lo = (uint32_t)seed;
+  a.seed_hi = (uint32_t)(seed >> 32);
+  a.thr = drop_threshold(drop_p);
+  a.scale = 1.0f / (1.0f - drop_p);
+  const int ntiles = (int)cdiv(M, 128), per = (int)cdiv(ntiles, 8);
+  hipLaunchKernelGGL(resblock_kernel<true>, dim3((unsigned)(8 * per)), dim3(512), kRbLds,
+                     as_stream(stream), a, per, ntiles);
+  PCST_LAUNCH_CHECK("resblock_bwd");
   return PCST_OK;
 }
 
@@ -1495,6 +1616,14 @@ extern "C" int pcst_resblock_fwd16(const uint16_t* x, int64_t M, const uint16_t*
                                    uint16_t* h, uint16_t* x_out, int f16, void* stream) {
   return f16 ? pcst::f16m::resblock_fwd_impl(x, M, w1, b1, w2, b2, seed, drop_p, h, x_out, stream)
              : pcst::bf16m::resblock_fwd_impl(x, M, w1, b1, w2, b2, seed, drop_p, h, x_out, stream);
+}
+
+extern "C" int pcst_resblock_bwd16(const uint16_t* dd, int64_t M, const uint16_t* w2t,
+                                   const uint16_t* w1t, const uint16_t* h, const uint16_t* g,
+                                   uint64_t seed, float drop_p, uint16_t* dz, uint16_t* g_out,
+                                   uint16_t* dd_out, int f16, void* stream) {
+  return f16 ? pcst::f16m::resblock_bwd_impl(dd, M, w2t, w1t, h, g, seed, drop_p, dz, g_out, dd_out, stream)
+             : pcst::bf16m::resblock_bwd_impl(dd, M, w2t, w1t, h, g, seed, drop_p, dz, g_out, dd_out, stream);
 }
 
 extern "C" int pcst_dropout_grad_bf16(const float* g, int64_t n, uint64_t seed, float drop_p,

@@ -162,6 +162,9 @@ RESIDUAL_16BIT = True
 # Each residual block's forward as one launch (pcst_resblock_fwd16: h never re-read from HBM;
 # bit-identical to the EP_BF16 + EP_RESID_DROP16 pair).  tools/knobs.py may turn it off (A/B).
 FUSED_BLOCK_FWD = True
+# Each residual block's backward products (EP_RELU_MASK then EP_ADD16) as one launch
+# (pcst_resblock_bwd16: dZ written once for dW1, never re-read; bit-identical).
+FUSED_BLOCK_BWD = True
 
 
 class NoisePredictorFn(torch.autograd.Function):
@@ -266,6 +269,15 @@ class NoisePredictorFn(torch.autograd.Function):
             for k in reversed(range(6)):
                 o = 6 + 4 * k
                 xbk, hk = blocks[k]
+                if FUSED_BLOCK_BWD and dd.shape[1] == 256 and hk.shape[1] == 512:
+                    w2t, w1t = _h_t(w[o + 2], half), _h_t(w[o], half)
+                    grads[o + 2], grads[o + 3] = _hip.linear_wgrad_ex(dd, hk)
+                    dz, g, dd = _hip.resblock_bwd16(dd, w2t, w1t, hk, g,
+                                                    seed=ctx.seeds[k - 1] if k else 0,
+                                                    p=ctx.ps[k - 1] if k else 0.0,
+                                                    dropout_copy=k > 0)
+                    grads[o], grads[o + 1] = _hip.linear_wgrad_ex(dz, xbk)
+                    continue
                 dz = _hip.gemm_ex(dd, _h_t(w[o + 2], half), epilogue=_hip.EP_RELU_MASK, aux=hk)
                 grads[o + 2], grads[o + 3] = _hip.linear_wgrad_ex(dd, hk)
                 if k:

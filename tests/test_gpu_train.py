@@ -520,3 +520,31 @@ def test_resblock_fwd16_matches_two_gemms(H, M, p, half):
     assert h.dtype == half and xo.dtype == half
     assert torch.equal(h, h_ref)
     assert torch.equal(xo, x_ref)
+
+
+@pytest.mark.parametrize("M", [240000, 1000, 129, 1])
+@pytest.mark.parametrize("p", [0.0, 0.3])
+@pytest.mark.parametrize("half", [torch.float16, torch.bfloat16])
+def test_resblock_bwd16_matches_two_gemms(H, M, p, half):
+    """pcst_resblock_bwd16 (one residual block's backward products, dZ never re-read) gives the
+    bits of gemm_ex EP_RELU_MASK (aux h) followed by EP_ADD16 (aux g) with the previous block's
+    dropout copy under the same (seed, p): dZ, g' and dD' bit-equal, for ragged M, with and
+    without dropout, in both 16-bit formats; without the copy dD' is None."""
+    torch.manual_seed(M + int(p * 10) + 7)
+    dd = (torch.randn(M, 256, device="cuda")).to(half)
+    h = torch.relu(torch.randn(M, 512, device="cuda")).to(half)
+    g = (torch.randn(M, 256, device="cuda")).to(half)
+    w2t = (torch.randn(512, 256, device="cuda") * 0.04).to(half)
+    w1t = (torch.randn(256, 512, device="cuda") * 0.06).to(half)
+    seed = 987654321987
+    dz_ref = H.gemm_ex(dd, w2t, epilogue=H.EP_RELU_MASK, aux=h)
+    g_ref, dd_ref = H.gemm_ex(dz_ref, w1t, epilogue=H.EP_ADD16, aux=g, seed=seed, p=p,
+                              dropout_copy=True)
+    dz, g2, dd2 = H.resblock_bwd16(dd, w2t, w1t, h, g, seed=seed, p=p, dropout_copy=True)
+    assert dz.dtype == half and g2.dtype == half and dd2.dtype == half
+    assert torch.equal(dz, dz_ref)
+    assert torch.equal(g2, g_ref)
+    assert torch.equal(dd2, dd_ref)
+    dz3, g3, none = H.resblock_bwd16(dd, w2t, w1t, h, g)
+    assert none is None and torch.equal(dz3, dz_ref)
+    assert torch.equal(g3, H.gemm_ex(dz_ref, w1t, epilogue=H.EP_ADD16, aux=g))

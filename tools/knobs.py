@@ -3,7 +3,7 @@
     import knobs; knobs.apply()
 
 reads PCST_KNN_OVERLAP=0|1, PCST_KNN_BUILD_LDS_FLOOR=<bytes>, PCST_DEVICE_EVENTS=0|1,
-PCST_KERNEL_SIGNAL=0|1, PCST_FUSED_BLOCK_FWD=0|1 (models._autograd) and
+PCST_KERNEL_SIGNAL=0|1, PCST_FUSED_BLOCK_FWD / _BWD=0|1 (models._autograd) and
 PCST_NM_BF16_KERNEL=1 (the 32x32x16 pair kernel) and sets the matching module constants of
 models.diffusion_model.  Kernel-side variants are experiment builds (csrc/Makefile XDEF,
 loaded through PCST_LIB)."""
@@ -41,5 +41,8 @@ def apply():
     if "PCST_FUSED_BLOCK_FWD" in e:
         from pointcloud_style_transfer_amd.models import _autograd
         _autograd.FUSED_BLOCK_FWD = e["PCST_FUSED_BLOCK_FWD"] != "0"
+    if "PCST_FUSED_BLOCK_BWD" in e:
+        from pointcloud_style_transfer_amd.models import _autograd
+        _autograd.FUSED_BLOCK_BWD = e["PCST_FUSED_BLOCK_BWD"] != "0"
     if e.get("PCST_NM_BF16_KERNEL") == "1":
         dm.NoisePredictor.bf16_code = packing.BF16

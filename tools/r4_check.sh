@@ -78,6 +78,16 @@ for st in "$@"; do
           python tools/bench_train.py --steps 4 --warmup 2 > "$OUT/tprof.json" 2> "$OUT/tprof.err"
       rc=$?; echo "trainprof rc=$rc"; if [ $rc -ne 0 ]; then tail -5 "$OUT/tprof.err"; exit $rc; fi
       python tools/kstats.py "$OUT/tprof/run_kernel_stats.csv" 40 | tee "$OUT/train_kernel_top.txt" ;;
+    trainpmc2)
+      # the fused residual-block kernels: LDS, MFMA and wait counters (one SQ pass)
+      TB="tools/bench_train.py --steps 3 --warmup 1"
+      timeout -s KILL 300 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_LDS SQ_INSTS_LDS \
+          SQ_LDS_BANK_CONFLICT SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_ANY --output-format csv -d "$OUT/psq2" -o pmc -- \
+          python $TB > "$OUT/psq2.log" 2>&1
+      rc=$?; echo "trainpmc2 rc=$rc"; if [ $rc -ne 0 ]; then tail -5 "$OUT/psq2.log"; exit $rc; fi
+      for k in "resblock_kernel<false" "resblock_kernel<true" "wgrad_ex_kernel<unsigned short, unsigned short"; do
+        echo "== $k"; python tools/pmc_sq.py "$OUT" "$k" psq2
+      done | tee "$OUT/train_sq2.txt" ;;
     trainab=*)
       # trainab=v_a,v_b: bench_train.py with the product library and each experiment library
       # pointcloud_style_transfer_amd/libpcst_hip_<v>.so, two alternating passes
