@@ -811,6 +811,18 @@ struct WStage<float> {  // Cn % 4 == 0: thread -> (column quad tid % 32, rows ti
                                            : make_float4(0.f, 0.f, 0.f, 0.f);
     }
   }
+  // the same slice by raw buffer loads: rows past the buffer read 0, a column quad past Cn is
+  // sent past the buffer too -- no branch, so the compiler counts the loads in flight exactly
+  __device__ __forceinline__ void load_buf(rsrc_t r, int64_t m, int c0, int Cn, int tid, bool ok) {
+    const int cq = (tid & 31) * 4;
+#pragma unroll
+    for (int it = 0; it < kIt; ++it) {
+      const int64_t row = m + (tid >> 5) + 8 * it;
+      const uint32_t off = ok && c0 + cq < Cn ? (uint32_t)((row * Cn + c0 + cq) * 4) : 0xfffffff0u;
+      const v4i32 q = __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 0);
+      v[it] = make_float4(__int_as_float(q.x), __int_as_float(q.y), __int_as_float(q.z), __int_as_float(q.w));
+    }
+  }
   __device__ __forceinline__ void store(char* D, int tid, float* csum) const {
     const int cq = (tid & 31) * 4;
 #pragma unroll
@@ -847,6 +859,15 @@ struct WStage<uint16_t> {  // Cn % 8 == 0: thread -> (column octet tid % 16, row
                                            : make_uint4(0u, 0u, 0u, 0u);
     }
   }
+  __device__ __forceinline__ void load_buf(rsrc_t r, int64_t m, int c0, int Cn, int tid, bool ok) {
+    const int co = (tid & 15) * 8;
+#pragma unroll
+    for (int it = 0; it < kIt; ++it) {
+      const int64_t row = m + (tid >> 4) + 16 * it;
+      const uint32_t off = ok && c0 + co < Cn ? (uint32_t)((row * Cn + c0 + co) * 2) : 0xfffffff0u;
+      v[it] = bload16(r, off, 0);
+    }
+  }
   __device__ __forceinline__ void store(char* D, int tid, float* csum) const {
     const int co = (tid & 15) * 8;
 #pragma unroll
@@ -881,15 +902,25 @@ __device__ __forceinline__ h16x8 tr_frag(const char* img, int c, int k, int lane
   return f;
 }
 
-template <typename TZ, typename TX>
+// BUF (operands < 2 GiB): branch-free buffer loads, kWPF slices in flight in registers, the LDS
+// image double-buffered with one barrier per slice (slice s + 1 is stored after slice s's
+// barrier, beside slice s's MFMAs).  !BUF: the pointer loads, one slice ahead, two barriers.
+#ifndef PCST_WGRAD_BPF
+#define PCST_WGRAD_BPF 3
+#endif
+#ifndef PCST_X_WGRAD_BUF  // 0: the pointer-load kernel only (A/B)
+#define PCST_X_WGRAD_BUF 1
+#endif
+constexpr int kWPF = PCST_WGRAD_BPF;
+template <typename TZ, typename TX, bool BUF = false>
 __global__ __launch_bounds__(256) void wgrad_ex_kernel(const TZ* __restrict__ dZ,
                                                        const TX* __restrict__ X, int64_t M, int I,
                                                        int O, int64_t rows_per_chunk, int tiles_i,
                                                        int ntile, int total, int per_xcd,
                                                        float* __restrict__ partW,
                                                        float* __restrict__ partB) {
-  __shared__ __attribute__((aligned(16))) char Zs[kWS * kWLdB];
-  __shared__ __attribute__((aligned(16))) char Xs[kWS * kWLdB];
+  __shared__ __attribute__((aligned(16))) char Zs[(BUF ? 2 : 1) * kWS * kWLdB];
+  __shared__ __attribute__((aligned(16))) char Xs[(BUF ? 2 : 1) * kWS * kWLdB];
   __shared__ float bred[WStage<TZ>::kRowLanes][kXT + 1];
   const int L = blockIdx.x;
   const int t = (L & 7) * per_xcd + (L >> 3);  // XCD-aware: one chunk's tiles share an L2
@@ -909,14 +940,14 @@ __global__ __launch_bounds__(256) void wgrad_ex_kernel(const TZ* __restrict__ dZ
   float csum[WStage<TZ>::kSumCols];
 #pragma unroll
   for (int u = 0; u < WStage<TZ>::kSumCols; ++u) csum[u] = 0.0f;
-  auto mma = [&]() {
+  auto mma = [&](const char* Zb, const char* Xb) {
 #pragma unroll
     for (int ks = 0; ks < kWS / 16; ++ks) {
       h16x8 a[2], b[2];
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
-        a[u] = tr_frag(Zs, wr * 64 + u * 32, ks * 16, lane);
-        b[u] = tr_frag(Xs, wc * 64 + u * 32, ks * 16, lane);
+        a[u] = tr_frag(Zb, wr * 64 + u * 32, ks * 16, lane);
+        b[u] = tr_frag(Xb, wc * 64 + u * 32, ks * 16, lane);
       }
 #pragma unroll
       for (int bm = 0; bm < 2; ++bm)
@@ -925,6 +956,40 @@ __global__ __launch_bounds__(256) void wgrad_ex_kernel(const TZ* __restrict__ dZ
           acc[bm][bn] = mfma32_h16(a[bm], b[bn], acc[bm][bn]);
     }
   };
+  if (BUF) {
+    const rsrc_t rz = make_rsrc(dZ, (uint32_t)(M * O * (int64_t)sizeof(TZ)));
+    const rsrc_t rx = make_rsrc(X, (uint32_t)(M * I * (int64_t)sizeof(TX)));
+    // slices, padded to whole groups of kWPF: a padding slice loads zeros (out-of-range
+    // offsets), so the loop body has no branch and the loads' counts stay exact
+    const int ns = (int)((me - mb + kWS - 1) / kWS);
+    const int np = (ns + kWPF - 1) / kWPF * kWPF;
+    WStage<TZ> gz[kWPF];
+    WStage<TX> gx[kWPF];
+    float* cs = csum;  // column sums of every staged dZ slice (kept for the bias tiles only)
+#pragma unroll
+    for (int u = 0; u < kWPF; ++u) {
+      gz[u].load_buf(rz, mb + (int64_t)u * kWS, o0, O, tid, u < ns);
+      gx[u].load_buf(rx, mb + (int64_t)u * kWS, i0, I, tid, u < ns);
+    }
+    gz[0].store(Zs, tid, cs);
+    gx[0].store(Xs, tid, nullptr);
+    gz[0].load_buf(rz, mb + (int64_t)kWPF * kWS, o0, O, tid, kWPF < ns);
+    gx[0].load_buf(rx, mb + (int64_t)kWPF * kWS, i0, I, tid, kWPF < ns);
+    for (int s0 = 0; s0 < np; s0 += kWPF) {
+#pragma unroll
+      for (int u = 0; u < kWPF; ++u) {
+        const int sl = s0 + u;
+        __syncthreads();  // slice sl landed; slice sl - 1's readers are done
+        const int un = (u + 1) % kWPF, nb = (sl + 1) & 1;
+        gz[un].store(Zs + nb * kWS * kWLdB, tid, cs);
+        gx[un].store(Xs + nb * kWS * kWLdB, tid, nullptr);
+        const int ln = sl + 1 + kWPF;
+        gz[un].load_buf(rz, mb + (int64_t)ln * kWS, o0, O, tid, ln < ns);
+        gx[un].load_buf(rx, mb + (int64_t)ln * kWS, i0, I, tid, ln < ns);
+        mma(Zs + (sl & 1) * kWS * kWLdB, Xs + (sl & 1) * kWS * kWLdB);
+      }
+    }
+  } else {
   WStage<TZ> gz;
   WStage<TX> gx;
   gz.load(dZ, me, O, mb, o0, tid);
@@ -943,7 +1008,7 @@ __global__ __launch_bounds__(256) void wgrad_ex_kernel(const TZ* __restrict__ dZ
       gz.load(dZ, me, O, k0 + 2 * kWS, o0, tid);
       gx.load(X, me, I, k0 + 2 * kWS, i0, tid);
     }
-    mma();
+    mma(Zs, Xs);
     __syncthreads();
     // the odd slice (rows past me in the last one load as zeros: the MFMAs add nothing)
     gz1.store(Zs, tid, bias ? csum : nullptr);
@@ -953,7 +1018,7 @@ __global__ __launch_bounds__(256) void wgrad_ex_kernel(const TZ* __restrict__ dZ
       gz1.load(dZ, me, O, k0 + 3 * kWS, o0, tid);
       gx1.load(X, me, I, k0 + 3 * kWS, i0, tid);
     }
-    mma();
+    mma(Zs, Xs);
     __syncthreads();
   }
 #else
@@ -965,10 +1030,11 @@ __global__ __launch_bounds__(256) void wgrad_ex_kernel(const TZ* __restrict__ dZ
       gz.load(dZ, me, O, k0 + kWS, o0, tid);
       gx.load(X, me, I, k0 + kWS, i0, tid);
     }
-    mma();
+    mma(Zs, Xs);
     __syncthreads();
   }
 #endif
+  }
   float* pw = partW + (int64_t)chunk * O * I;
 #pragma unroll
   for (int bn = 0; bn < 2; ++bn) {
@@ -1249,10 +1315,18 @@ int wgrad_ex_impl(const void* dZ, int dz_bf16, const void* X, int x_bf16, int64_
   float* partW = static_cast<float*>(workspace);
   float* partB = db ? partW + (int64_t)p.chunks * O * I : nullptr;
   const dim3 grid((unsigned)(8 * p.per_xcd));
+  const int64_t lim = 1ll << 31;
 #define PCST_WGRAD_EX(TZ, TX)                                                                     \
-  hipLaunchKernelGGL((wgrad_ex_kernel<TZ, TX>), grid, dim3(256), 0, s, static_cast<const TZ*>(dZ), \
-                     static_cast<const TX*>(X), M, (int)I, (int)O, p.rows_per_chunk, p.tiles_i,     \
-                     p.ntile, p.total, p.per_xcd, partW, partB)
+  do {                                                                                            \
+  if (PCST_X_WGRAD_BUF && M * O * (int64_t)sizeof(TZ) < lim && M * I * (int64_t)sizeof(TX) < lim) \
+    hipLaunchKernelGGL((wgrad_ex_kernel<TZ, TX, true>), grid, dim3(256), 0, s,                     \
+                       static_cast<const TZ*>(dZ), static_cast<const TX*>(X), M, (int)I, (int)O,  \
+                       p.rows_per_chunk, p.tiles_i, p.ntile, p.total, p.per_xcd, partW, partB);   \
+  else                                                                                            \
+    hipLaunchKernelGGL((wgrad_ex_kernel<TZ, TX, false>), grid, dim3(256), 0, s,                    \
+                       static_cast<const TZ*>(dZ), static_cast<const TX*>(X), M, (int)I, (int)O,  \
+                       p.rows_per_chunk, p.tiles_i, p.ntile, p.total, p.per_xcd, partW, partB); \
+  } while (0)
   if (dz_bf16 && x_bf16)
     PCST_WGRAD_EX(uint16_t, uint16_t);
   else if (dz_bf16)

@@ -601,7 +601,7 @@ __global__ __launch_bounds__(256) void voxf_insert_kernel(const float* __restric
   // key depends on (seed, row, index) only); voxf_reps_kernel takes the representatives' keys
   // back out, leaving the histogram of the pool (the U < T candidates) without a launch of its
   // own.  The LDS table above is reused as the (at most 4096) bins (kVoxLds * 8 B >= 16 KiB).
-  static_assert(kVoxLds * 2 >= kSelBins, "LDS table too small for the key histogram");
+  static_assert(kVoxLds * 2 >= 1024, "LDS table too small for the key histogram");
   uint32_t* lh = reinterpret_cast<uint32_t*>(lkey);
   const uint64_t seed = seed_p ? *seed_p : seed_v;
   for (int c = 0; c < copies; ++c) {
@@ -867,6 +867,7 @@ static int voxel_fast(const float* pts, int64_t B, int64_t N, int64_t copies, in
   const int cp = (int)copies;
   const int pack = N < (1 << 20) ? 1 : 0;
   const int sshift = vox_sel_shift(N);
+  PCST_CHECK_ARG((1 << (32 - sshift)) <= 2 * kVoxLds, "voxel_downsample: cloud too large for this build");
   hipLaunchKernelGGL(voxf_insert_kernel, dim3((unsigned)cdiv(N, kVoxChunk), b), dim3(256), 0, s,
                      pts, n, w.mm, T, w.H, w.tkey, w.tsum, w.tcnt, b, cp, seed, seed_p, w.hist, w.cnt4,
                      w.vlist, pack, sshift, prepped ? w.pmm : nullptr, vox_prep_blocks(N));

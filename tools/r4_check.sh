@@ -78,6 +78,10 @@ for st in "$@"; do
           python tools/bench_train.py --steps 4 --warmup 2 > "$OUT/tprof.json" 2> "$OUT/tprof.err"
       rc=$?; echo "trainprof rc=$rc"; if [ $rc -ne 0 ]; then tail -5 "$OUT/tprof.err"; exit $rc; fi
       python tools/kstats.py "$OUT/tprof/run_kernel_stats.csv" 40 | tee "$OUT/train_kernel_top.txt" ;;
+    split=*)
+      # split=G: the 32-cloud step as G concurrent groups (tools/split_probe.py)
+      timeout -k 10 500 python tools/split_probe.py --clouds 32 --groups ${st#split=} > "$OUT/split.json" 2> "$OUT/split.err"
+      rc=$?; echo "split rc=$rc"; cat "$OUT/split.json"; if [ $rc -ne 0 ]; then tail -5 "$OUT/split.err"; exit $rc; fi ;;
     trainpmc2)
       # the fused residual-block kernels: LDS, MFMA and wait counters (one SQ pass)
       TB="tools/bench_train.py --steps 3 --warmup 1"
