@@ -55,9 +55,6 @@ constexpr int kKnnTile = 4096;           // scan tile (256 threads x 16)
 constexpr int kKnnMaxTiles = 1024;       // per-block LDS tile histogram in the count kernel
 constexpr int kPreKnownBlocks = 64;      // known-row scatter blocks per cloud in the pre kernel
 constexpr int kCountPerBlock = 1024;     // elements per count-kernel block (4 per thread)
-#ifndef PCST_KNN_SORT  // 1: the sort build (no global atomic per element); 0: the atomic build
-#define PCST_KNN_SORT 0
-#endif
 #ifndef PCST_KNN_SLOTKEY  // 1: the one-pass slot-keyed query window (Query::window); 0: two-pass
 #define PCST_KNN_SLOTKEY 1
 #endif
@@ -95,11 +92,6 @@ struct KnnWS {
   int32_t* olist;    // [B][N]   outlier query rows
   float* obound;     // [B][N]   their kk-th best squared distance so far (rounded up; inf: none)
   NbrRec* nbr;       // [B][N]   a query row's IDW weights (the deferred search: pcst_knn3_search)
-  // sort build (PCST_KNN_SORT): elements bucketed by tile, no global atomics
-  uint64_t* wgh;     // [B][nblk][T] per count-block tile counts (refs | queries << 32) -> bucket offsets
-  uint64_t* toff;    // [B][T+1]  tile starts (refs | queries << 32)
-  int2* rbkt;        // [B][M]    (ref j, cell) in tile order
-  int2* qbkt;        // [B][N]    (query row n, cell) in tile order
   // zeroed every call (contiguous):
   int32_t* err;
   int32_t* nchunk;   // [B]
@@ -107,7 +99,7 @@ struct KnnWS {
   uint32_t* known;   // [B][N]  (j+1 of the last coarse row writing n, 0 = query)
   uint64_t* tsum;    // [B][T]  per-tile sums of the packed counts
   uint64_t* cnt;     // [B][T*kKnnTile] packed counts (refs | queries << 32) -> starts
-  int64_t Cmax, T, Cpad, maxch, nblk;
+  int64_t Cmax, T, Cpad, maxch;
   size_t bytes;
 };
 
@@ -131,12 +123,7 @@ static KnnWS carve_knn(void* base, int64_t B, int64_t N, int64_t M) {
   w.olist = c.take<int32_t>(B * N);
   w.obound = c.take<float>(B * N);
   w.nbr = c.take<NbrRec>(B * N);
-  w.nblk = cdiv(M + N, kCountPerBlock);
-  w.wgh = c.take<uint64_t>(B * w.nblk * w.T);
-  w.toff = c.take<uint64_t>(B * (w.T + 1));
-  w.rbkt = c.take<int2>(B * M);
-  w.qbkt = c.take<int2>(B * N);
-  w.err = c.take<int32_t>(4);
+  w.err = c.take<int32_t>(4);  // [0] error flags, [2] fill work-groups done (built signal)
   w.nchunk = c.take<int32_t>(B);
   w.ocount = c.take<int32_t>(B);
   w.known = c.take<uint32_t>(B * N);
@@ -433,7 +420,10 @@ __global__ __launch_bounds__(256) void knn_fill_kernel(const float* __restrict__
                                                        const uint64_t* __restrict__ start,
                                                        const int2* __restrict__ crank,
                                                        float4* __restrict__ refs,
-                                                       int32_t* __restrict__ qorder) {
+                                                       int32_t* __restrict__ qorder,
+                                                       uint32_t* __restrict__ sig_flag,
+                                                       uint32_t sig_value,
+                                                       uint32_t* __restrict__ done) {
   const int b = blockIdx.y;
   const uint64_t* S = start + b * Cpad;
   for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < M + N; e += gridDim.x * 256) {
@@ -450,226 +440,19 @@ __global__ __launch_bounds__(256) void knn_fill_kernel(const float* __restrict__
       qorder[b * N + pos] = (int32_t)(e - M);
     }
   }
-}
-
-// ---- sort build (PCST_KNN_SORT): the cell-sorted layout of count/scan/fill without a global
-// atomic per element.  At many clouds the count kernel's 64-bit returning atomics (one per ref and
-// query row, scattered over the cells) run at the memory-side atomic rate; here every rank comes
-// from an LDS atomic and the global arrays are written with plain stores:
-//   bin    per 1024-element block: cell, rank within (block, tile) from an LDS tile histogram,
-//          the block's histogram stored to wgh[block][tile]
-//   bscan  per cloud: tile totals, tile starts (toff), and each (block, tile)'s bucket offset
-//   scatter  each element to its tile bucket (rbkt / qbkt) at its block offset + rank
-//   tile   per tile: LDS counting sort of the bucket by cell (ranks from LDS atomics), the packed
-//          cell starts (cnt), the brick chunks (as knn_scan_kernel), refs / qorder written in place
-// Same layout as the atomic build; only the order inside a cell differs, which the exact top-3
-// (distance, index) does not see.
-__global__ __launch_bounds__(256) void knn_bin_kernel(
-    const float* __restrict__ orig, const int64_t* __restrict__ idx,
-    const StatRec* __restrict__ stats, const uint32_t* __restrict__ known, int64_t N, int64_t M,
-    int64_t Cmax, int64_t T, int64_t nblk, float* __restrict__ gp, uint64_t* __restrict__ wgh,
-    int2* __restrict__ crank) {
-  constexpr int U = kCountPerBlock / 256;
-  const int b = blockIdx.y;
-  __shared__ float Gs[8];
-  __shared__ unsigned long long th[kKnnMaxTiles];
-  if (threadIdx.x < 64) knn_grid_params(stats, b, N, M, Cmax, Gs);
-  __syncthreads();
-  if (blockIdx.x == 0 && threadIdx.x < 8) gp[b * 8 + threadIdx.x] = Gs[threadIdx.x];
-  Grid g;
-  g.load(Gs);
-  for (int64_t blk = blockIdx.x; blk < nblk; blk += gridDim.x) {
-    for (int t = threadIdx.x; t < T; t += 256) th[t] = 0ull;
+  if (sig_flag) {
+    // the build's completion flag (pcst_knn3_build's built_flag): every thread's stores released
+    // at agent scope, then the last work-group to count itself out publishes the value -- the
+    // one-lane signal launch it replaces sat on the side stream's critical path
+    __threadfence();
     __syncthreads();
-    const int64_t e0 = blk * kCountPerBlock + threadIdx.x;
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int64_t e = e0 + u * 256;
-      if (e >= M + N) continue;
-      const float* p = nullptr;
-      unsigned long long inc = 0ull;
-      if (e < M) {
-        int64_t n = idx[b * M + e];
-        n = n < 0 ? 0 : (n >= N ? N - 1 : n);
-        p = orig + (b * N + n) * 3;
-        inc = 1ull;
-      } else if (!known[b * N + (e - M)]) {
-        p = orig + (b * N + (e - M)) * 3;
-        inc = 1ull << 32;
+    if (threadIdx.x == 0) {
+      const uint32_t total = gridDim.x * gridDim.y;
+      if (atomicAdd(done, 1u) == total - 1) {
+        __threadfence();
+        __hip_atomic_store(sig_flag, sig_value, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
       }
-      int2 cr = make_int2(-1, 0);
-      if (p) {
-        const int cell = cell_of(p, g);
-        const unsigned long long old = atomicAdd(&th[cell / kKnnTile], inc);
-        cr = make_int2(cell, (int)(uint32_t)(e < M ? old : old >> 32));
-      }
-      crank[b * (M + N) + e] = cr;
     }
-    __syncthreads();
-    for (int t = threadIdx.x; t < T; t += 256) wgh[((int64_t)b * nblk + blk) * T + t] = th[t];
-    __syncthreads();
-  }
-}
-
-// One work-group per cloud: tile totals over the blocks, tile starts, and wgh[blk][t] ->
-// bucket offset of block blk inside tile t (exclusive over blocks, tile start included).
-__global__ __launch_bounds__(256) void knn_bscan_kernel(uint64_t* __restrict__ wgh, int64_t T,
-                                                        int64_t nblk, uint64_t* __restrict__ toff) {
-  const int b = blockIdx.x;
-  uint64_t* W = wgh + (int64_t)b * nblk * T;
-  __shared__ unsigned long long sh[8];
-  __shared__ unsigned long long tot_t[kKnnMaxTiles];
-  for (int t = threadIdx.x; t < T; t += 256) {
-    uint64_t s = 0;
-    for (int64_t k = 0; k < nblk; ++k) s += W[k * T + t];
-    tot_t[t] = s;
-  }
-  __syncthreads();
-  // exclusive scan of the tile totals: thread i takes tiles [4i, 4i + 4)
-  uint64_t v[4], run = 0;
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int t = threadIdx.x * 4 + j;
-    v[j] = t < T ? tot_t[t] : 0ull;
-    run += v[j];
-  }
-  uint64_t total;
-  uint64_t ex = block_excl_scan_256_u64(run, sh, total);
-  __syncthreads();
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int t = threadIdx.x * 4 + j;
-    if (t < T) tot_t[t] = ex;  // now the tile's start
-    ex += v[j];
-  }
-  __syncthreads();
-  for (int t = threadIdx.x; t <= T; t += 256) toff[(int64_t)b * (T + 1) + t] = t < T ? tot_t[t] : total;
-  for (int t = threadIdx.x; t < T; t += 256) {
-    uint64_t r = tot_t[t];
-    for (int64_t k = 0; k < nblk; ++k) {
-      const uint64_t c = W[k * T + t];
-      W[k * T + t] = r;
-      r += c;
-    }
-  }
-}
-
-__global__ __launch_bounds__(256) void knn_scatter_kernel(const int2* __restrict__ crank, int64_t N,
-                                                          int64_t M, int64_t T, int64_t nblk,
-                                                          const uint64_t* __restrict__ wgh,
-                                                          int2* __restrict__ rbkt,
-                                                          int2* __restrict__ qbkt) {
-  const int b = blockIdx.y;
-  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < M + N; e += (int64_t)gridDim.x * 256) {
-    const int2 cr = crank[b * (M + N) + e];
-    if (cr.x < 0) continue;
-    const int64_t blk = e / kCountPerBlock;
-    const uint64_t o = wgh[((int64_t)b * nblk + blk) * T + cr.x / kKnnTile];
-    if (e < M) rbkt[b * M + (uint32_t)o + (uint32_t)cr.y] = make_int2((int)e, cr.x);
-    else qbkt[b * N + (uint32_t)(o >> 32) + (uint32_t)cr.y] = make_int2((int)(e - M), cr.x);
-  }
-}
-
-// One work-group per (tile, cloud): counting sort of the tile's bucket by cell in LDS, the packed
-// cell starts, the chunk list of the tile's 64 bricks, then refs / qorder at their final places.
-// A thread re-reads exactly the rank words it wrote (crank[.].y), so no fence is needed between.
-__global__ __launch_bounds__(256) void knn_tile_kernel(
-    const float* __restrict__ orig, const int64_t* __restrict__ idx, int64_t N, int64_t M,
-    int64_t T, int64_t Cpad, const uint64_t* __restrict__ toff, const int2* __restrict__ rbkt,
-    const int2* __restrict__ qbkt, int2* __restrict__ crank, uint64_t* __restrict__ cnt,
-    uint2* __restrict__ chunks, int64_t maxch, int32_t* __restrict__ nchunk,
-    float4* __restrict__ refs, int32_t* __restrict__ qorder) {
-  const int b = blockIdx.y, tile = blockIdx.x;
-  __shared__ unsigned long long buf[kKnnTile + kKnnTile / 32];
-  __shared__ unsigned long long sh[8];
-  auto pad = [](int i) { return i + (i >> 5); };
-  const uint64_t t0 = toff[(int64_t)b * (T + 1) + tile], t1 = toff[(int64_t)b * (T + 1) + tile + 1];
-  const uint32_t r0 = (uint32_t)t0, r1 = (uint32_t)t1;
-  const uint32_t q0 = (uint32_t)(t0 >> 32), q1 = (uint32_t)(t1 >> 32);
-  const int cbase = tile * kKnnTile;
-  for (int k = threadIdx.x; k < kKnnTile; k += 256) buf[pad(k)] = 0ull;
-  __syncthreads();
-  int2* CR = crank + b * (M + N);
-  for (uint32_t i = r0 + threadIdx.x; i < r1; i += 256) {
-    const int2 it = rbkt[b * M + i];
-    CR[it.x].y = (int)(uint32_t)atomicAdd(&buf[pad(it.y - cbase)], 1ull);
-  }
-  for (uint32_t i = q0 + threadIdx.x; i < q1; i += 256) {
-    const int2 it = qbkt[b * N + i];
-    CR[M + it.x].y = (int)(uint32_t)(atomicAdd(&buf[pad(it.y - cbase)], 1ull << 32) >> 32);
-  }
-  __syncthreads();
-  // exclusive scan of the packed counts + the tile start -> cell starts
-  uint64_t v[16], s = 0;
-#pragma unroll
-  for (int k = 0; k < 16; ++k) {
-    v[k] = buf[pad(threadIdx.x * 16 + k)];
-    s += v[k];
-  }
-  uint64_t tot;
-  uint64_t run = block_excl_scan_256_u64(s, sh, tot) + t0;
-#pragma unroll
-  for (int k = 0; k < 16; ++k) {
-    buf[pad(threadIdx.x * 16 + k)] = run;
-    run += v[k];
-  }
-  __syncthreads();
-  uint64_t* D = cnt + b * Cpad + (int64_t)tile * kKnnTile;
-#pragma unroll
-  for (int k = 0; k < 16; ++k) D[k * 256 + threadIdx.x] = buf[pad(k * 256 + threadIdx.x)];
-  if (threadIdx.x < 64) {  // the tile's bricks by octant (knn_scan_kernel's chunking)
-    const int t = threadIdx.x;
-    uint32_t qo[9];
-#pragma unroll
-    for (int o = 0; o < 8; ++o) qo[o] = (uint32_t)(buf[pad(t * 64 + 8 * o)] >> 32);
-    qo[8] = (uint32_t)((t < 63 ? buf[pad(t * 64 + 64)] : t1) >> 32);
-    auto walk = [&](auto&& emit) {
-      uint32_t cs = qo[0];
-#pragma unroll
-      for (int o = 0; o < 8; ++o) {
-        const uint32_t a = qo[o], n = qo[o + 1] - a;
-        if (n > 64) {
-          if (a > cs) emit(cs, a);
-          const uint32_t k = (n + 63) / 64;
-          for (uint32_t i = 0; i < k; ++i) emit(a + (uint32_t)((uint64_t)n * i / k), a + (uint32_t)((uint64_t)n * (i + 1) / k));
-          cs = a + n;
-        } else if (a + n - cs > 64) {
-          emit(cs, a);
-          cs = a;
-        }
-      }
-      if (qo[8] > cs) emit(cs, qo[8]);
-    };
-    uint32_t nch = 0;
-    walk([&](uint32_t, uint32_t) { ++nch; });
-    uint32_t off = nch;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const uint32_t y = __shfl_up(off, o);
-      if (t >= o) off += y;
-    }
-    const uint32_t all = __shfl(off, 63);
-    off -= nch;
-    uint32_t at = 0;
-    if (t == 0 && all) at = (uint32_t)atomicAdd(&nchunk[b], (int32_t)all);
-    at = __shfl(at, 0);
-    uint2* Ch = chunks + b * maxch + at + off;
-    uint32_t i = 0;
-    walk([&](uint32_t a, uint32_t e) { Ch[i++] = make_uint2(a, e); });
-  }
-  // final places (the rank words are this thread's own writes of the first loops)
-  for (uint32_t i = r0 + threadIdx.x; i < r1; i += 256) {
-    const int2 it = rbkt[b * M + i];
-    const uint32_t pos = (uint32_t)buf[pad(it.y - cbase)] + (uint32_t)CR[it.x].y;
-    int64_t n = idx[b * M + it.x];
-    n = n < 0 ? 0 : (n >= N ? N - 1 : n);
-    const float* p = orig + (b * N + n) * 3;
-    refs[b * M + pos] = make_float4(p[0], p[1], p[2], __int_as_float(it.x));
-  }
-  for (uint32_t i = q0 + threadIdx.x; i < q1; i += 256) {
-    const int2 it = qbkt[b * N + i];
-    const uint32_t pos = (uint32_t)(buf[pad(it.y - cbase)] >> 32) + (uint32_t)CR[M + it.x].y;
-    qorder[b * N + pos] = it.x;
   }
 }
 
@@ -1703,9 +1486,6 @@ constexpr unsigned kLdsPre = 0;
 constexpr unsigned kLdsCount = 8 * sizeof(float) + kKnnMaxTiles * sizeof(unsigned long long);
 constexpr unsigned kLdsScan = (kKnnTile + kKnnTile / 32 + 8) * sizeof(unsigned long long);
 constexpr unsigned kLdsFill = 0;
-constexpr unsigned kLdsBin = kLdsCount;
-constexpr unsigned kLdsBscan = (8 + kKnnMaxTiles) * sizeof(unsigned long long);
-constexpr unsigned kLdsTile = (kKnnTile + kKnnTile / 32 + 8) * sizeof(unsigned long long);
 static unsigned pad_for(unsigned static_lds, unsigned floor_bytes) {
   return static_lds >= floor_bytes ? 0u : floor_bytes - static_lds;
 }
@@ -1720,7 +1500,7 @@ static unsigned pad_for(unsigned static_lds, unsigned floor_bytes) {
 // build.  0 = the kernels' natural grids.
 extern "C" int pcst_knn3_build(const float* orig, const int64_t* idx, int64_t B, int64_t N,
                                int64_t M, int64_t lds_floor, int64_t max_wg, void* workspace,
-                               void* stream) {
+                               uint32_t* built_flag, uint32_t built_value, void* stream) {
   PCST_CHECK_ARG(B >= 0 && N > 0 && M > 0 && N < (1ll << 31) && M < (1ll << 27) &&
                      M + N < (1ll << 31),
                  "knn3_build: bad shape");
@@ -1737,24 +1517,6 @@ extern "C" int pcst_knn3_build(const float* orig, const int64_t* idx, int64_t B,
   // per-cloud grid of each launch: natural size, capped at max_wg / B (at least one)
   const int64_t cap = max_wg > 0 ? std::max<int64_t>(1, max_wg / B) : (int64_t)1 << 30;
   auto grid = [&](int64_t natural) { return (unsigned)std::min<int64_t>(natural, cap); };
-  if (PCST_KNN_SORT) {
-    // error word, counters and known rows are contiguous in the carve (the sort build writes
-    // every tile sum and cell start itself: no memset of the ~4 MB per cloud of packed counts)
-    PCST_HIP(hipMemsetAsync(w.err, 0, (size_t)((char*)w.tsum - (char*)w.err), s), "knn: memset");
-    hipLaunchKernelGGL(knn_pre_kernel, dim3(grid(kStatBlocks + kPreKnownBlocks), b), dim3(256),
-                       pad_pre, s, orig, idx, (int)N, M, w.stats, w.known, w.err);
-    hipLaunchKernelGGL(knn_bin_kernel, dim3(grid(w.nblk), b), dim3(256), pad_for(kLdsBin, f), s,
-                       orig, idx, w.stats, w.known, N, M, w.Cmax, w.T, w.nblk, w.gp, w.wgh, w.crank);
-    hipLaunchKernelGGL(knn_bscan_kernel, dim3(b), dim3(256), pad_for(kLdsBscan, f), s, w.wgh, w.T,
-                       w.nblk, w.toff);
-    hipLaunchKernelGGL(knn_scatter_kernel, dim3(grid(std::min<int64_t>(cdiv(M + N, 256), 2048)), b),
-                       dim3(256), pad_fill, s, w.crank, N, M, w.T, w.nblk, w.wgh, w.rbkt, w.qbkt);
-    hipLaunchKernelGGL(knn_tile_kernel, dim3((unsigned)w.T, b), dim3(256), pad_for(kLdsTile, f), s,
-                       orig, idx, N, M, w.T, w.Cpad, w.toff, w.rbkt, w.qbkt, w.crank, w.cnt,
-                       w.chunks, w.maxch, w.nchunk, w.refs, w.qorder);
-    PCST_LAUNCH_CHECK("knn3_build");
-    return PCST_OK;
-  }
   // error word, counters, known rows, tile sums and packed counts are contiguous in the carve
   PCST_HIP(hipMemsetAsync(w.err, 0, (size_t)(w.bytes - ((char*)w.err - (char*)workspace)), s),
            "knn: memset");
@@ -1767,7 +1529,8 @@ extern "C" int pcst_knn3_build(const float* orig, const int64_t* idx, int64_t B,
                      w.T, w.Cpad, w.chunks, w.maxch, w.nchunk);
   const unsigned gf = grid(std::min<int64_t>(cdiv(M + N, 256), 2048));
   hipLaunchKernelGGL(knn_fill_kernel, dim3(gf, b), dim3(256), pad_fill, s, orig, idx, N, M, w.Cpad,
-                     w.cnt, w.crank, w.refs, w.qorder);
+                     w.cnt, w.crank, w.refs, w.qorder, built_flag, built_value,
+                     reinterpret_cast<uint32_t*>(w.err + 2));
   PCST_LAUNCH_CHECK("knn3_build");
   return PCST_OK;
 }
@@ -1876,7 +1639,7 @@ extern "C" int pcst_knn3_finish_cfg_ddim(const float* coarse, int64_t B, int64_t
 extern "C" int pcst_knn3_interp(const float* coarse, const float* orig, const int64_t* idx,
                                 int64_t B, int64_t N, int64_t M, float* out, void* workspace,
                                 void* stream) {
-  int rc = pcst_knn3_build(orig, idx, B, N, M, 0, 0, workspace, stream);
+  int rc = pcst_knn3_build(orig, idx, B, N, M, 0, 0, workspace, nullptr, 0u, stream);
   if (rc) return rc;
   return pcst_knn3_query(coarse, orig, B, N, M, out, workspace, nullptr, 0u, 0, stream);
 }

@@ -133,6 +133,22 @@ for st in "$@"; do
           python -c "import json,sys; f=lambda p: json.loads(open(p).read().strip().splitlines()[-1]); a=f(sys.argv[1]); b=f(sys.argv[2]); print(sys.argv[3], 'b1', a['value'], a['ms_per_step'], a['roofline']['avg_launch_ms'], 'b32', b['ms_per_step'])" "$OUT/bench_$v.$pass.json" "$OUT/b32_$v.$pass.json" "$v.$pass"
         done
       done ;;
+    benchknob=*)
+      # benchknob=NAME=VAL,...: the driver-window bench (and the 32-cloud bench) with the product
+      # library plain and with each knob (tools/knobs.py through tools/bench_knobs.py), two passes
+      VS=${st#benchknob=}
+      for pass in 1 2; do
+        for v in prod ${VS//,/ }; do
+          kv=PCST_NONE=1; if [ "$v" != prod ]; then kv=$v; fi
+          env "$kv" timeout -k 10 200 python tools/bench_knobs.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline \
+              --no-encoder --no-other-precision > "$OUT/bench_$v.$pass.json" 2> "$OUT/bench_$v.$pass.err"
+          rc=$?; if [ $rc -ne 0 ]; then tail -3 "$OUT/bench_$v.$pass.err"; exit $rc; fi
+          env "$kv" timeout -k 10 200 python tools/bench_knobs.py --gpus 1 --clouds-per-gpu 32 --steps 10 --warmup 3 \
+              --no-cpu-baseline --no-encoder --no-other-precision > "$OUT/b32_$v.$pass.json" 2> "$OUT/b32_$v.$pass.err"
+          rc=$?; if [ $rc -ne 0 ]; then tail -3 "$OUT/b32_$v.$pass.err"; exit $rc; fi
+          python -c "import json,sys; f=lambda p: json.loads(open(p).read().strip().splitlines()[-1]); a=f(sys.argv[1]); b=f(sys.argv[2]); print(sys.argv[3], 'b1', a['value'], a['ms_per_step'], a['roofline']['avg_launch_ms'], 'b32', b['ms_per_step'])" "$OUT/bench_$v.$pass.json" "$OUT/b32_$v.$pass.json" "$v.$pass"
+        done
+      done ;;
     loop1000)
       timeout -k 10 600 python -u tools/loop1000_probe.py > "$OUT/loop1000.jsonl" 2> "$OUT/loop1000.err"
       rc=$?; echo "loop1000 rc=$rc"; cat "$OUT/loop1000.jsonl"; if [ $rc -ne 0 ]; then tail -3 "$OUT/loop1000.err"; exit $rc; fi ;;
