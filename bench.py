@@ -296,6 +296,7 @@ def main():
     world, rank, local = setup_dist(args)
     device = torch.device("cuda", torch.cuda.current_device())
     from pointcloud_style_transfer_amd import _hip
+    from pointcloud_style_transfer_amd import rng as _rng
     from pointcloud_style_transfer_amd.distributed import max_over_ranks, shard
     from pointcloud_style_transfer_amd.models import diffusion_model as dmod
     from pointcloud_style_transfer_amd.synthetic import lidar_like_cloud, standard_normal
@@ -362,14 +363,15 @@ def main():
         def all_conds():
             return npred.cond(t_rows.reshape(-1), style_in.repeat(S, 1), pk).view(S, 2 * C, -1)
 
-        prepped = False
+        prepped = pool = False
+        next_seed = None
 
         def step(i, timed):
-            nonlocal x, prepped
+            nonlocal x, prepped, pool, next_seed
             t = timesteps[i % len(timesteps)]
             t_prev = timesteps[i % len(timesteps) + 1] if t > 0 else -1
             cnd = conds[i % len(timesteps)]
-            xc, xi = hp.downsample_copies(x, 2, vws, prepped)
+            xc, xi = hp.downsample_copies(x, 2, vws, prepped, next_seed, pool)
 
             def mlp(xc_, wait=None, start=None):
                 if not timed:
@@ -385,12 +387,16 @@ def main():
                 ev.append((e0, e1))
                 return nc_
 
-            # the update prepares the next step's downsample (as guided_sample_loop does)
+            # the update prepares the next step's downsample, its pool histogram for the next
+            # subset seed drawn one step ahead included (as guided_sample_loop does)
             prep = dmod.voxel_prep_ok(hp, x, state)
+            next_seed = (_rng.source().device_seed() & (2**64 - 1)
+                         if prep and dmod.pool_prep_ok(x) else None)
             x = dmod.hierarchical_step(hp, mlp, xc, xi, x_cat, x, src, 7.5, dp._coeffs(t, t_prev),
                                        knn_ws, state, mlp_waits=dmod.MLP_WAITS,
-                                       mlp_signals=dmod.MLP_SIGNALS, vox_ws=vws if prep else None)
-            prepped = prep
+                                       mlp_signals=dmod.MLP_SIGNALS, vox_ws=vws if prep else None,
+                                       pool_seed=next_seed)
+            prepped, pool = prep, next_seed is not None
 
         lctx = torch.cuda.stream(loop_stream) if overlap else contextlib.nullcontext()
         with lctx:
@@ -400,7 +406,8 @@ def main():
             # the timed region restarts the sampling trajectory at t = 999 from x_T
             x = torch.from_numpy(xT_np).to(device)
             x_cat.copy_(torch.cat([x, x]))
-            prepped = False
+            prepped = pool = False
+            next_seed = None
         if world > 1:
             import torch.distributed as dist
 
@@ -430,7 +437,8 @@ def main():
                 with lctx:
                     x = torch.from_numpy(xT_np).to(device)
                     x_cat.copy_(torch.cat([x, x]))
-                    prepped = False
+                    prepped = pool = False
+                    next_seed = None
                     conds = all_conds()
                     for i in range(2):
                         step(i, False)

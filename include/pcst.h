@@ -238,13 +238,18 @@ int pcst_voxel_downsample_copies(const float* pts, int64_t B, int64_t N, int64_t
  * next downsample of x_out on vox_workspace (a pcst_voxel_copies_workspace_size(C, N, copies)
  * workspace): the new points' min / max partials and the zeroing of the per-call state.  The next
  * call on that workspace must then be pcst_voxel_downsample_copies_prepped with pts = x_out (the
- * same arguments as pcst_voxel_downsample_copies, one launch fewer; the same result bit for bit). */
+ * same arguments as pcst_voxel_downsample_copies, one launch fewer; the same result bit for bit).
+ * pool != 0 (N <= 4M): the update also makes that downsample's pool-key histogram for the seed
+ * pool_seed it will be called with (the keys depend on (seed, row, index) only), which the
+ * downsample's insert otherwise makes on the step's critical path; that call must then pass
+ * pool = 1 and seed = pool_seed. */
 int pcst_cfg_ddim_voxel_prep(const float* x, const float* eps, const float* source, int64_t C,
                              int64_t N, float guidance_scale, float sqrt_1m_at, float sqrt_at_eps,
                              float sqrt_aprev, float sqrt_1m_aprev, float* x_out, float* x_cat,
-                             void* vox_workspace, int64_t copies, void* stream);
+                             void* vox_workspace, int64_t copies, uint64_t pool_seed, int pool,
+                             void* stream);
 int pcst_voxel_downsample_copies_prepped(const float* pts, int64_t B, int64_t N, int64_t copies,
-                                         int64_t target, void* workspace, uint64_t seed,
+                                         int64_t target, void* workspace, uint64_t seed, int pool,
                                          int64_t* out_idx, float* out_pts, void* stream);
 /* Copies the replay-validation error word (0 = ok) to err_out (device int32). */
 int pcst_voxel_error(void* workspace, int64_t B, int64_t N, int32_t* err_out, void* stream);

@@ -44,8 +44,10 @@ SIGNATURES = {
     "pcst_voxel_error": [_P, _I, _I, _P, _P],
     "pcst_voxel_copies_workspace_size": [_I, _I, _I, _SZ],
     "pcst_voxel_downsample_copies": [_P, _I, _I, _I, _I, _P, ctypes.c_uint64, _P, _P, _P],
-    "pcst_voxel_downsample_copies_prepped": [_P, _I, _I, _I, _I, _P, ctypes.c_uint64, _P, _P, _P],
-    "pcst_cfg_ddim_voxel_prep": [_P, _P, _P, _I, _I, _F, _F, _F, _F, _F, _P, _P, _P, _I, _P],
+    "pcst_voxel_downsample_copies_prepped": [_P, _I, _I, _I, _I, _P, ctypes.c_uint64, ctypes.c_int,
+                                             _P, _P, _P],
+    "pcst_cfg_ddim_voxel_prep": [_P, _P, _P, _I, _I, _F, _F, _F, _F, _F, _P, _P, _P, _I,
+                                 ctypes.c_uint64, ctypes.c_int, _P],
     "pcst_knn_workspace_size": [_I, _I, _I, _SZ],
     "pcst_knn3_interp": [_P, _P, _P, _I, _I, _I, _P, _P, _P],
     "pcst_knn3_build": [_P, _P, _I, _I, _I, _I, _I, _P, _P, ctypes.c_uint32, _P],
@@ -280,12 +282,15 @@ def _workspace(fn, *dims, device):
 
 # ----------------------------------------------------------------------------- voxel downsample
 def voxel_copies_workspace(B, N, copies, device):
-    """A workspace for voxel_downsample(..., copies=copies, ws=) of B clouds of N points."""
-    return _workspace("pcst_voxel_copies_workspace_size", B, N, copies, device=device)
+    """A workspace for voxel_downsample(..., copies=copies, ws=) of B clouds of N points (zeroed
+    once: its pool histogram is kept zero between calls, see cfg_ddim_voxel_prep's pool_seed)."""
+    need = ctypes.c_size_t(0)
+    _call("pcst_voxel_copies_workspace_size", B, N, copies, ctypes.byref(need))
+    return torch.zeros(max(int(need.value), 1), dtype=torch.uint8, device=device)
 
 
 def voxel_downsample(points, target, seed=0, perm_provider=None, copies=1, ws=None,
-                     prepped=False):
+                     prepped=False, pool=False):
     """HierarchicalProcessor._voxel_grid_downsample_torch for N > target, all clouds at once.
 
     perm_provider=None: the random subset is drawn on the device from `seed`.
@@ -295,7 +300,8 @@ def voxel_downsample(points, target, seed=0, perm_provider=None, copies=1, ws=No
     without building or re-hashing the copies (each row keeps the set the concatenated call
     keeps for the same seed); the replay path concatenates, as the reference's draws are per row.
     prepped=True: `ws` was prepared by cfg_ddim_voxel_prep for these points (the device-drawn
-    path skips its statistics / zeroing launch).
+    path skips its statistics / zeroing launch); pool=True: that prep also made the pool-key
+    histogram for this `seed` (its pool_seed), so the insert skips it.
     Returns (points [k*B,T,3], idx [k*B,T] int64)."""
     require_device(points)
     points = _f32(points)
@@ -316,9 +322,15 @@ def voxel_downsample(points, target, seed=0, perm_provider=None, copies=1, ws=No
                 raise RuntimeError("voxel_downsample: workspace too small or on another device")
         out_idx = torch.empty(copies * B, target, dtype=torch.int64, device=dev)
         out_pts = torch.empty(copies * B, target, 3, dtype=torch.float32, device=dev)
-        _call("pcst_voxel_downsample_copies_prepped" if prepped else "pcst_voxel_downsample_copies",
-              _ptr(points), B, N, copies, target, _ptr(ws), seed & (2**64 - 1), _ptr(out_idx),
-              _ptr(out_pts), _stream())
+        if prepped:
+            _call("pcst_voxel_downsample_copies_prepped", _ptr(points), B, N, copies, target,
+                  _ptr(ws), seed & (2**64 - 1), 1 if pool else 0, _ptr(out_idx), _ptr(out_pts),
+                  _stream())
+        else:
+            if pool:
+                raise RuntimeError("voxel_downsample: pool=True needs prepped=True")
+            _call("pcst_voxel_downsample_copies", _ptr(points), B, N, copies, target, _ptr(ws),
+                  seed & (2**64 - 1), _ptr(out_idx), _ptr(out_pts), _stream())
         return out_pts, out_idx
     ws = _workspace("pcst_voxel_workspace_size", B, N, device=dev)
     out_idx = torch.empty(B, target, dtype=torch.int64, device=dev)
@@ -658,10 +670,12 @@ def noise_mlp(pts, points_per_cloud, cond, blob, bias, precision, out=None, wait
 
 
 # ----------------------------------------------------------------------------- CFG / DDIM update
-def cfg_ddim_voxel_prep(x, eps, source, guidance_scale, coeffs, x_cat, vox_ws, copies=2, out=None):
+def cfg_ddim_voxel_prep(x, eps, source, guidance_scale, coeffs, x_cat, vox_ws, copies=2, out=None,
+                        pool_seed=None):
     """cfg_ddim_step(x, eps[:C], eps[C:], source, ...) of a CFG batch (x [C,N,3], eps [2C,N,3],
     x_cat [2C,N,3] receives the new x twice) fused with the first stage of the next
-    voxel_downsample(new x, copies=copies, ws=vox_ws, prepped=True) (pcst.h)."""
+    voxel_downsample(new x, copies=copies, ws=vox_ws, prepped=True) (pcst.h).  pool_seed (the
+    seed that downsample will take): also its pool-key histogram; it must then pass pool=True."""
     require_device(x, eps, source, x_cat, vox_ws)
     x, eps = _f32(x), _f32(eps)
     C, N, _ = x.shape
@@ -677,7 +691,8 @@ def cfg_ddim_voxel_prep(x, eps, source, guidance_scale, coeffs, x_cat, vox_ws, c
         out = torch.empty_like(x)
     c1, c2, c3, c4 = (float(c) for c in coeffs)
     _call("pcst_cfg_ddim_voxel_prep", _ptr(x), _ptr(eps), _ptr(source), C, N, float(guidance_scale),
-          c1, c2, c3, c4, _ptr(out), _ptr(x_cat), _ptr(vox_ws), copies, _stream())
+          c1, c2, c3, c4, _ptr(out), _ptr(x_cat), _ptr(vox_ws), copies,
+          (pool_seed or 0) & (2**64 - 1), 0 if pool_seed is None else 1, _stream())
     return out
 
 
@@ -1164,7 +1179,7 @@ _GUARDED = ("square_distance", "index_points", "fps", "ball_query", "group_gathe
             "cfg_ddim_step_dcoef", "voxel_downsample_copies_dseed", "bn_train_coeffs",
             "bn_relu_maxpool", "bn_relu_bwd", "group_gather_bwd", "group_colsum16", "resblock_fwd16", "resblock_bwd16",
             "gemm_ex", "dropout_grad_bf16",
-            "linear_wgrad_ex", "knn_workspace")
+            "linear_wgrad_ex", "knn_workspace", "voxel_copies_workspace")
 for _name in _GUARDED:
     globals()[_name] = _on_tensor_device(globals()[_name])
 del _name

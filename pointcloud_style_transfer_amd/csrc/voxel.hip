@@ -373,6 +373,9 @@ struct VoxelFastWS {
   unsigned long long* ties;  // [R][kTieCap] (key<<32 | id)
   // zeroed every call (one memset): counters, histograms, tables, rep flags
   int32_t* cnt4;          // [R][4]: U (of cloud r, rows r < B), selected, ties, err
+  uint32_t* phist;        // [R][kSelBins] the pool-key histogram of every point made ahead by
+                          // pcst_cfg_ddim_voxel_prep (pool calls), outside the zeroed state:
+                          // emit zeroes it after its readers (reps, select) are done
   uint32_t* hist;         // [R][kSelBins] pool keys (U < T): every point's, less the reps'
   uint32_t* hist2;        // [R][kSelBins] representative keys (U > T)
   unsigned long long* tkey;  // [B][H]  0 = empty, else (1<<32)|hash
@@ -405,6 +408,7 @@ static VoxelFastWS carve_voxel_fast(void* base, int64_t B, int64_t N, int64_t co
   w.reps = c.take<int64_t>(B * N);
   w.rhash = c.take<uint32_t>(B * N);
   w.vlist = c.take<int32_t>(B * N);
+  w.phist = c.take<uint32_t>(R * kSelBins);
   w.ties = c.take<unsigned long long>(R * kTieCap);
   w.cnt4 = c.take<int32_t>(R * 4);
   w.hist = c.take<uint32_t>(R * kSelBins);
@@ -428,6 +432,7 @@ __device__ __forceinline__ uint32_t mix32(uint32_t x) {
 // Cloud statistics (blocks [0, kStatBlocks) of row y) and, in the other blocks, the zeroing of
 // the counters / histograms / tables / rep flags of this call (instead of a separate memset).
 constexpr int kVoxZeroBlocks = 128;
+constexpr int kPoolBlocks = 16;  // pool-histogram work-groups per row in the prep kernel
 __global__ __launch_bounds__(256) void voxf_stats_zero_kernel(const float* __restrict__ pts, int N,
                                                               StatRec* __restrict__ part,
                                                               uint4* __restrict__ zero,
@@ -481,8 +486,29 @@ __global__ __launch_bounds__(256) void voxf_cfg_prep_kernel(
     const float* __restrict__ x, const float* __restrict__ eps, const float* __restrict__ src,
     int64_t C, int N, float scale, float c1, float c2, float c3, float c4,
     float* __restrict__ x_out, float* __restrict__ x_cat, float* __restrict__ pmm, int nprep,
-    uint4* __restrict__ zero, int64_t zero_words) {
+    uint4* __restrict__ zero, int64_t zero_words, uint32_t* __restrict__ phist, uint64_t pool_seed,
+    int copies, int sshift) {
   const int c = blockIdx.y;
+  if ((int)blockIdx.x >= nprep + kVoxZeroBlocks) {
+    // the next downsample's pool-key histogram (every point of this cloud, each copy's row):
+    // it depends on (seed, row, index) only, so it is made here instead of in the insert
+    const int q = (int)blockIdx.x - nprep - kVoxZeroBlocks;
+    const int cp = q / kPoolBlocks, part = q % kPoolBlocks;
+    const int row = cp * (int)C + c;
+    const int nbins = 1 << (32 - sshift);
+    __shared__ uint32_t lh[1024];
+    for (int i = threadIdx.x; i < nbins; i += 256) lh[i] = 0u;
+    __syncthreads();
+    const int per = (N + kPoolBlocks - 1) / kPoolBlocks;
+    const int n0 = part * per, n1 = min(n0 + per, N);
+    for (int n = n0 + threadIdx.x; n < n1; n += 256)
+      atomicAdd(&lh[rand_key(pool_seed, row + 0x10000, n) >> sshift], 1u);
+    __syncthreads();
+    for (int i = threadIdx.x; i < nbins; i += 256)
+      if (lh[i]) atomicAdd(&phist[(int64_t)row * kSelBins + i], lh[i]);
+    (void)copies;
+    return;
+  }
   if ((int)blockIdx.x < nprep) {
     float mn[3] = {3.4e38f, 3.4e38f, 3.4e38f}, mx[3] = {-3.4e38f, -3.4e38f, -3.4e38f};
     const int64_t half = C * (int64_t)N * 3;
@@ -538,7 +564,7 @@ __global__ __launch_bounds__(256) void voxf_insert_kernel(const float* __restric
                                                           int32_t* __restrict__ cnt4,
                                                           int32_t* __restrict__ vlist, int pack,
                                                           int sshift, const float* __restrict__ pmm,
-                                                          int npm) {
+                                                          int npm, int pool_made) {
   const int nbins = 1 << (32 - sshift);
   // Each workgroup first aggregates its kVoxChunk points in an LDS table (LDS atomics), then
   // publishes one global (sum, count) per distinct voxel: dense voxels see at most one global
@@ -604,7 +630,7 @@ __global__ __launch_bounds__(256) void voxf_insert_kernel(const float* __restric
   static_assert(kVoxLds * 2 >= 1024, "LDS table too small for the key histogram");
   uint32_t* lh = reinterpret_cast<uint32_t*>(lkey);
   const uint64_t seed = seed_p ? *seed_p : seed_v;
-  for (int c = 0; c < copies; ++c) {
+  for (int c = 0; c < (pool_made ? 0 : copies); ++c) {  // (a pool call: the prep made it)
     const int row = c * B + b;
     __syncthreads();
     for (int i = threadIdx.x; i < nbins; i += 256) lh[i] = 0u;
@@ -778,10 +804,13 @@ __global__ __launch_bounds__(256) void voxf_emit_kernel(const float* __restrict_
                                                         const unsigned long long* __restrict__ ties,
                                                         const int64_t* __restrict__ reps,
                                                         int64_t* __restrict__ out_idx,
-                                                        float* __restrict__ out_pts) {
+                                                        float* __restrict__ out_pts,
+                                                        uint32_t* __restrict__ phist) {
   constexpr int kPer = kEmitTile / 256;
   const int row = blockIdx.y, cl = row % B;
   const int64_t tile = blockIdx.x;
+  if (tile == 0)  // the row's pool histogram is read (reps, select) before this launch: clear it
+    for (int i = threadIdx.x; i < kSelBins; i += 256) phist[(int64_t)row * kSelBins + i] = 0u;
   __shared__ uint32_t sh[260];
   __shared__ uint32_t add[kEmitTile];
   __shared__ unsigned long long tl[kTieLds];
@@ -857,7 +886,7 @@ static size_t vox_zero_bytes(const VoxelFastWS& w, int64_t rows) {
 
 static int voxel_fast(const float* pts, int64_t B, int64_t N, int64_t copies, int64_t T,
                       void* workspace, uint64_t seed, const uint64_t* seed_p, int64_t* out_idx,
-                      float* out_pts, hipStream_t s, bool prepped = false) {
+                      float* out_pts, hipStream_t s, bool prepped = false, bool pool = false) {
   VoxelFastWS w = carve_voxel_fast(workspace, B, N, copies);
   const int b = (int)B, n = (int)N, rows = (int)(B * copies);
   if (!prepped)  // (a prepped call: pcst_cfg_ddim_voxel_prep made the partials and zeroed)
@@ -870,15 +899,17 @@ static int voxel_fast(const float* pts, int64_t B, int64_t N, int64_t copies, in
   PCST_CHECK_ARG((1 << (32 - sshift)) <= 2 * kVoxLds, "voxel_downsample: cloud too large for this build");
   hipLaunchKernelGGL(voxf_insert_kernel, dim3((unsigned)cdiv(N, kVoxChunk), b), dim3(256), 0, s,
                      pts, n, w.mm, T, w.H, w.tkey, w.tsum, w.tcnt, b, cp, seed, seed_p, w.hist, w.cnt4,
-                     w.vlist, pack, sshift, prepped ? w.pmm : nullptr, vox_prep_blocks(N));
+                     w.vlist, pack, sshift, prepped ? w.pmm : nullptr, vox_prep_blocks(N), pool ? 1 : 0);
+  uint32_t* hist = pool ? w.phist : w.hist;  // the pool histogram: made ahead, or by the insert
   hipLaunchKernelGGL(voxf_reps_kernel, dim3((unsigned)std::min<int64_t>(cdiv(N, 256), kVoxRepsBlocks), b),
                      dim3(256), 0, s, w.tkey, w.tsum, w.tcnt, w.H, n, w.cnt4, w.vlist, pack, w.reps,
-                     w.rhash, w.isrep, b, cp, seed, seed_p, w.hist, w.hist2, sshift);
+                     w.rhash, w.isrep, b, cp, seed, seed_p, hist, w.hist2, sshift);
   hipLaunchKernelGGL(voxf_select_kernel, dim3(128, rows), dim3(256), 0, s, n, T, b, seed, seed_p,
-                     w.hist, w.hist2, w.sel, w.cnt4, w.rhash, w.isrep, w.reps, w.ties, w.kcnt,
+                     hist, w.hist2, w.sel, w.cnt4, w.rhash, w.isrep, w.reps, w.ties, w.kcnt,
                      w.ktile, w.tiles, sshift);
   hipLaunchKernelGGL(voxf_emit_kernel, dim3((unsigned)w.tiles, rows), dim3(256), 0, s, pts, n, T,
-                     b, w.kcnt, w.ktile, w.tiles, w.cnt4, w.sel, w.ties, w.reps, out_idx, out_pts);
+                     b, w.kcnt, w.ktile, w.tiles, w.cnt4, w.sel, w.ties, w.reps, out_idx, out_pts,
+                     w.phist);
   PCST_LAUNCH_CHECK("voxel_downsample");
   return PCST_OK;
 }
@@ -999,31 +1030,36 @@ extern "C" int pcst_voxel_downsample_copies(const float* pts, int64_t B, int64_t
 
 extern "C" int pcst_voxel_downsample_copies_prepped(const float* pts, int64_t B, int64_t N,
                                                     int64_t copies, int64_t target, void* workspace,
-                                                    uint64_t seed, int64_t* out_idx, float* out_pts,
-                                                    void* stream) {
+                                                    uint64_t seed, int pool, int64_t* out_idx,
+                                                    float* out_pts, void* stream) {
   PCST_CHECK_ARG(B > 0 && copies >= 1 && B * copies < (1 << 15) && N > target && target > 0 &&
                      N < (1ll << 30),
                  "voxel_downsample_copies_prepped: bad shape");
   PCST_CHECK_ARG(pts && workspace && out_idx && out_pts, "voxel_downsample_copies_prepped: null pointer");
   return voxel_fast(pts, B, N, copies, target, workspace, seed, nullptr, out_idx, out_pts,
-                    as_stream(stream), true);
+                    as_stream(stream), true, pool != 0);
 }
 
 extern "C" int pcst_cfg_ddim_voxel_prep(const float* x, const float* eps, const float* source,
                                         int64_t C, int64_t N, float guidance_scale,
                                         float sqrt_1m_at, float sqrt_at_eps, float sqrt_aprev,
                                         float sqrt_1m_aprev, float* x_out, float* x_cat,
-                                        void* vox_workspace, int64_t copies, void* stream) {
+                                        void* vox_workspace, int64_t copies, uint64_t pool_seed,
+                                        int pool, void* stream) {
   PCST_CHECK_ARG(C > 0 && N > 0 && copies >= 1 && C * copies < (1 << 15) && N < (1ll << 30),
                  "cfg_ddim_voxel_prep: bad shape");
   PCST_CHECK_ARG(x && eps && x_out && x_cat && vox_workspace, "cfg_ddim_voxel_prep: null pointer");
   VoxelFastWS w = carve_voxel_fast(vox_workspace, C, N, copies);
   const int nprep = vox_prep_blocks(N);
-  hipLaunchKernelGGL(voxf_cfg_prep_kernel, dim3(nprep + kVoxZeroBlocks, (unsigned)C), dim3(256), 0,
-                     as_stream(stream), x, eps, source, C, (int)N, guidance_scale, sqrt_1m_at,
+  const int sshift = vox_sel_shift(N);
+  PCST_CHECK_ARG(!pool || (1 << (32 - sshift)) <= 1024, "cfg_ddim_voxel_prep: pool histogram needs N <= 4M");
+  const unsigned npool = pool ? (unsigned)(kPoolBlocks * copies) : 0u;
+  hipLaunchKernelGGL(voxf_cfg_prep_kernel, dim3(nprep + kVoxZeroBlocks + npool, (unsigned)C), dim3(256),
+                     0, as_stream(stream), x, eps, source, C, (int)N, guidance_scale, sqrt_1m_at,
                      sqrt_at_eps, sqrt_aprev, sqrt_1m_aprev, x_out, x_cat, w.pmm, nprep,
                      reinterpret_cast<uint4*>(w.cnt4),
-                     (int64_t)cdiv(vox_zero_bytes(w, C * copies), 16));
+                     (int64_t)cdiv(vox_zero_bytes(w, C * copies), 16), w.phist, pool_seed,
+                     (int)copies, sshift);
   PCST_LAUNCH_CHECK("cfg_ddim_voxel_prep");
   return PCST_OK;
 }

@@ -229,18 +229,21 @@ class HierarchicalProcessor:
 
     def downsample_copies(self, points: torch.Tensor, copies: int,
                           ws: Optional[torch.Tensor] = None,
-                          prepped: bool = False) -> Tuple[torch.Tensor, torch.Tensor]:
+                          prepped: bool = False, seed: Optional[int] = None,
+                          pool: bool = False) -> Tuple[torch.Tensor, torch.Tensor]:
         """downsample(torch.cat([points] * copies)) -- the CFG batch of guided_sample_loop
         (diffusion_model.py:244-247) -- without building or re-hashing the copies.  Replay runs
         take the concatenated path: the reference draws one permutation per row.  `ws`
         (_hip.voxel_copies_workspace of the same shape) is reused instead of allocated;
         prepped: `ws` was prepared for `points` by the previous step's update
-        (_hip.cfg_ddim_voxel_prep)."""
+        (_hip.cfg_ddim_voxel_prep).  seed: the subset seed drawn ahead by the loop (the one the
+        previous step's update made the pool histogram for: pool=True); None draws it here."""
         src = _rng.source()
         if points.shape[1] <= self.global_points or src.replaying:
             return self.downsample(torch.cat([points] * copies))
-        return _hip.voxel_downsample(points, self.global_points, seed=src.device_seed(),
-                                     copies=copies, ws=ws, prepped=prepped)
+        return _hip.voxel_downsample(points, self.global_points,
+                                     seed=src.device_seed() if seed is None else seed,
+                                     copies=copies, ws=ws, prepped=prepped, pool=pool)
 
     def step_prep(self, points: torch.Tensor) -> bool:
         """Whether the next downsample_copies of `points` can take a workspace prepared by the
@@ -385,6 +388,12 @@ def hierarchical_eps(hp, mlp, xc, xi, x_cat, knn_ws=None, state=None, mlp_waits=
     return _hip.knn3_query(nc, handle, built if BUILT_SIGNAL else None)
 
 
+def pool_prep_ok(x) -> bool:
+    """Whether a prepared update also makes the next downsample's pool histogram (POOL_PREP;
+    the prep kernel's histogram holds the 1024 bins of clouds up to 4M points)."""
+    return POOL_PREP and x.shape[1] <= (4 << 20)
+
+
 def voxel_prep_ok(hp, x, state) -> bool:
     """Whether hierarchical_step's update prepares the next downsample_copies of x (VOXEL_PREP;
     the fused update exists on the query-after-MLP layout, not with SEARCH_BESIDE_MLP's fused
@@ -402,18 +411,21 @@ SEARCH_BESIDE_MLP = False
 
 
 def hierarchical_step(hp, mlp, xc, xi, x_cat, x, source, guidance_scale, coeffs, knn_ws=None,
-                      state=None, mlp_waits=False, mlp_signals=False, vox_ws=None):
+                      state=None, mlp_waits=False, mlp_signals=False, vox_ws=None, pool_seed=None):
     """One guided step of the hierarchical branch (diffusion_model.py:240-260): eps of the CFG
     batch (mlp(xc) upsampled by kNN-3), then the fused CFG + DDIM update of x (x_cat takes the
     new x twice).  Returns the new x.  state: a StepState (overlapped layout) or None.
     vox_ws: the voxel workspace of the next step's downsample_copies, prepared by this update
     (_hip.cfg_ddim_voxel_prep: one launch fewer); that call must then pass prepped=True.  Only
-    on the query-after-MLP layout (voxel_prep_ok)."""
+    on the query-after-MLP layout (voxel_prep_ok).  pool_seed (with vox_ws): the seed of that
+    downsample, drawn ahead; the update also makes its pool-key histogram (POOL_PREP), and the
+    downsample must then pass seed=pool_seed, pool=True."""
     C = x.shape[0]
     if state is None or not SEARCH_BESIDE_MLP:
         eps = hierarchical_eps(hp, mlp, xc, xi, x_cat, knn_ws, state, mlp_waits, mlp_signals)
         if vox_ws is not None:
-            return _hip.cfg_ddim_voxel_prep(x, eps, source, guidance_scale, coeffs, x_cat, vox_ws)
+            return _hip.cfg_ddim_voxel_prep(x, eps, source, guidance_scale, coeffs, x_cat, vox_ws,
+                                            pool_seed=pool_seed)
         return _hip.cfg_ddim_step(x, eps[:C], eps[C:], source, guidance_scale, coeffs, x_cat=x_cat)
     if vox_ws is not None:
         raise RuntimeError("hierarchical_step: the voxel prep needs the query-after-MLP layout")
@@ -462,6 +474,11 @@ MLP_SIGNALS = True
 # The step's CFG + DDIM update also prepares the next step's voxel downsample (its statistics and
 # zeroing: pcst_cfg_ddim_voxel_prep), one launch fewer per step; bit-identical.
 VOXEL_PREP = True
+# The update also makes the next downsample's pool-key histogram (its keys depend on the subset
+# seed, the row and the point index only), so the voxel insert on the step's critical path skips
+# it; the loop draws each step's subset seed one step ahead (one draw per step either way, in the
+# same order: the draws, hence the results, are unchanged).  POOL_PREP needs VOXEL_PREP.
+POOL_PREP = True
 class _TorchEvent:
     """torch.cuda.Event with the DeviceEvent interface (DEVICE_EVENTS = False: A/B runs)."""
 
@@ -626,7 +643,8 @@ class DiffusionProcess:
                 ws = _hip.knn_workspace(2 * B, shape[1], model.config.global_points, device=device)
             if use_hierarchical:
                 vws = _hip.voxel_copies_workspace(B, shape[1], 2, device=device)
-            prepped = False
+            prepped = pool = False
+            next_seed = None
             try:
                 for i, t in enumerate(timesteps):
                     t_in = t_rows[i]
@@ -638,14 +656,17 @@ class DiffusionProcess:
                         mlp = lambda c: npred(c, t_in, style_in)  # noqa: E731
                     coeffs = self._coeffs(t, t_prevs[i])
                     if use_hierarchical:
-                        xc, xi = hp.downsample_copies(x, 2, vws, prepped)
+                        xc, xi = hp.downsample_copies(x, 2, vws, prepped, next_seed, pool)
                         prep = i + 1 < len(timesteps) and voxel_prep_ok(hp, x, state)
+                        # the next step's subset seed, drawn one step ahead for its pool histogram
+                        next_seed = (_rng.source().device_seed() & (2**64 - 1)
+                                     if prep and pool_prep_ok(x) else None)
                         x = hierarchical_step(hp, mlp, xc, xi, x_cat, x, source, guidance_scale,
                                               coeffs, ws, state,
                                               mlp_waits=MLP_WAITS and conds is not None,
                                               mlp_signals=MLP_SIGNALS and conds is not None,
-                                              vox_ws=vws if prep else None)
-                        prepped = prep
+                                              vox_ws=vws if prep else None, pool_seed=next_seed)
+                        prepped, pool = prep, next_seed is not None
                     else:
                         eps = mlp(x_cat)
                         x = _hip.cfg_ddim_step(x, eps[:B], eps[B:], source, guidance_scale,

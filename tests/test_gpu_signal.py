@@ -139,8 +139,12 @@ def _small_model(dev, precision="bf16"):
 
 def test_guided_loop_raises_when_a_step_wait_times_out(monkeypatch):
     """The sampling loop reads its flags' timeout words once at its end: a producer that never
-    signals (simulated: signal() bumps the host value but writes nothing) makes the loop raise
-    instead of returning what the unsynchronised kNN query computed."""
+    signals (simulated: signal() bumps the host value but writes nothing, and the values handed
+    to producing launches -- the MLP's start signal, the kNN build's completion flag -- go to a
+    scratch word instead of the flag) makes the loop raise instead of returning what the
+    unsynchronised kNN query computed."""
+    import ctypes
+
     from pointcloud_style_transfer_amd import _hip
     from pointcloud_style_transfer_amd.models import diffusion_model as dm
     from pointcloud_style_transfer_amd.synthetic import lidar_like_cloud
@@ -156,7 +160,15 @@ def test_guided_loop_raises_when_a_step_wait_times_out(monkeypatch):
         def silent(self, stream):
             self.value += 1
 
+        scratch = torch.zeros(4, dtype=torch.int32, device=dev)
+        real_next = _hip.DeviceSignal.next_value
+
+        def silent_next(self):
+            _, v = real_next(self)
+            return ctypes.c_void_p(scratch.data_ptr()), v
+
         monkeypatch.setattr(_hip.DeviceSignal, "signal", silent)
+        monkeypatch.setattr(_hip.DeviceSignal, "next_value", silent_next)
         with pytest.raises(_hip.SignalTimeout):
             dp.guided_sample_loop(model, src, cond, 3, 7.5)
 
@@ -286,3 +298,52 @@ def test_guided_loop_voxel_prep_bit_identical(monkeypatch):
                 torch.manual_seed(9)
                 outs.append(dp.guided_sample_loop(model, src, cond, 6, 7.5, x_T=xT))
         assert torch.equal(outs[0], outs[1]), B
+
+
+def test_guided_loop_pool_prep_bit_identical(monkeypatch):
+    """The next downsample's pool-key histogram made by the step's update from the subset seed
+    drawn one step ahead (POOL_PREP: pcst_cfg_ddim_voxel_prep's pool_seed, the insert skips the
+    histogram) gives the bits of the loop that draws each seed at its downsample and builds the
+    histogram in the insert, at 1 and 3 clouds; with VOXEL_PREP off the loop draws nothing ahead."""
+    from pointcloud_style_transfer_amd.models import diffusion_model as dm
+    from pointcloud_style_transfer_amd.synthetic import lidar_like_cloud, standard_normal
+
+    dev = torch.device("cuda", 0)
+    cfg, model, dp = _small_model(dev)
+    for B in (1, 3):
+        src = torch.from_numpy(np.stack([lidar_like_cloud(1100 + i, 16384) for i in range(B)])).to(dev)
+        cond = torch.from_numpy(np.stack([lidar_like_cloud(2100 + i, 16384) for i in range(B)])).to(dev)
+        xT = torch.from_numpy(np.stack([standard_normal(3100 + i, (16384, 3)) for i in range(B)])).to(dev)
+        outs = []
+        with torch.no_grad():
+            for pool, prep in ((True, True), (False, True), (False, False)):
+                monkeypatch.setattr(dm, "POOL_PREP", pool)
+                monkeypatch.setattr(dm, "VOXEL_PREP", prep)
+                torch.manual_seed(9)
+                outs.append(dp.guided_sample_loop(model, src, cond, 6, 7.5, x_T=xT))
+        assert torch.equal(outs[0], outs[1]), B
+        assert torch.equal(outs[0], outs[2]), B
+
+
+def test_pool_prepped_downsample_matches_plain():
+    """pcst_voxel_downsample_copies_prepped with the pool histogram made by the update for its
+    seed (pool = 1) keeps the same rows as the plain downsample of the same points and seed,
+    over consecutive calls on one workspace (the emit clears the histogram between them)."""
+    from pointcloud_style_transfer_amd import _hip
+
+    dev = torch.device("cuda", 0)
+    rng = np.random.default_rng(3)
+    C, N, T = 2, 60000, 15000
+    ws = _hip.voxel_copies_workspace(C, N, 2, dev)
+    x = torch.from_numpy(rng.standard_normal((C, N, 3)).astype(np.float32)).to(dev)
+    src = torch.from_numpy(rng.standard_normal((C, N, 3)).astype(np.float32)).to(dev)
+    coeffs = (np.float32(0.3), np.float32(0.95), np.float32(0.97), np.float32(0.24))
+    for r in range(4):
+        eps = torch.from_numpy(rng.standard_normal((2 * C, N, 3)).astype(np.float32)).to(dev)
+        x_cat = torch.empty(2 * C, N, 3, device=dev)
+        seed = 1234567 + 1000003 * r
+        _hip.voxel_downsample(x, T, seed=seed, copies=2, ws=ws)  # the previous step's downsample
+        x = _hip.cfg_ddim_voxel_prep(x, eps, src, 7.5, coeffs, x_cat, ws, pool_seed=seed)
+        got = _hip.voxel_downsample(x, T, seed=seed, copies=2, ws=ws, prepped=True, pool=True)
+        want = _hip.voxel_downsample(x, T, seed=seed, copies=2)
+        assert torch.equal(got[1], want[1]) and torch.equal(got[0], want[0]), r

@@ -28,6 +28,8 @@ def apply():
         dm.KNN_BUILD_MAX_WG = int(e["PCST_KNN_BUILD_MAX_WG"])
     if "PCST_VOXEL_PREP" in e:
         dm.VOXEL_PREP = e["PCST_VOXEL_PREP"] != "0"
+    if "PCST_POOL_PREP" in e:
+        dm.POOL_PREP = e["PCST_POOL_PREP"] != "0"
     if "PCST_MLP_SIGNALS" in e:
         dm.MLP_SIGNALS = e["PCST_MLP_SIGNALS"] != "0"
     if "PCST_MLP_WAITS" in e:
