@@ -274,15 +274,11 @@ int pcst_knn3_interp(const float* coarse, const float* orig, const int64_t* idx,
  * holds the value when its work-groups start; otherwise (a cross-stream wait that gave up) it
  * leaves the workspace alone and writes 0 for eps, so a timed-out wait can never make it read a
  * half-built workspace.  The caller reports the wait's error word.
- * built_flag / built_value (build; NULL: none): the build's last kernel publishes the value to
- * the flag (release, agent scope) once all its work-groups are done -- the producer side of
- * the query's built_flag, without a signal launch of its own (pcst_signal_write).
  * grid_cap (query, search): the query grid's workgroups over all clouds of the launch (each
  * strides over its cloud's chunks; the result does not depend on it); <= 0: 16384, the winner
  * of the round-4 A/B at 32 clouds (profiles/r04/a5). */
 int pcst_knn3_build(const float* orig, const int64_t* idx, int64_t B, int64_t N, int64_t M,
-                    int64_t lds_floor, int64_t max_wg, void* workspace, uint32_t* built_flag,
-                    uint32_t built_value, void* stream);
+                    int64_t lds_floor, int64_t max_wg, void* workspace, void* stream);
 int pcst_knn3_query(const float* coarse, const float* orig, int64_t B, int64_t N, int64_t M,
                     float* out, void* workspace, const uint32_t* built_flag, uint32_t built_value,
                     int64_t grid_cap, void* stream);

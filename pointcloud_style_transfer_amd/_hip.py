@@ -50,7 +50,7 @@ SIGNATURES = {
                                  ctypes.c_uint64, ctypes.c_int, _P],
     "pcst_knn_workspace_size": [_I, _I, _I, _SZ],
     "pcst_knn3_interp": [_P, _P, _P, _I, _I, _I, _P, _P, _P],
-    "pcst_knn3_build": [_P, _P, _I, _I, _I, _I, _I, _P, _P, ctypes.c_uint32, _P],
+    "pcst_knn3_build": [_P, _P, _I, _I, _I, _I, _I, _P, _P],
     "pcst_cfg_ddim_step_dcoef": [_P, _P, _P, _P, _I, ctypes.c_float, _P, _P, _P, _P],
     "pcst_voxel_downsample_copies_dseed": [_P, _I, _I, _I, _I, _P, _P, _P, _P, _P],
     "pcst_knn3_query": [_P, _P, _I, _I, _I, _P, _P, _P, ctypes.c_uint32, _I, _P],
@@ -499,22 +499,20 @@ class DeviceEvent:
             pass
 
 
-def knn3_build(orig, idx, ws=None, lds_floor=0, max_wg=0, signal=None):
+def knn3_build(orig, idx, ws=None, lds_floor=0, max_wg=0):
     """Phase 1 of knn3_interp (positions only) on the current stream -> workspace handle
     (orig, idx, workspace) for knn3_query.  `ws` (knn_workspace) may be preallocated, e.g. on
     the stream that runs the query when the build runs on a side stream; `lds_floor` (bytes)
     keeps the build's work-groups off CUs that hold a noise-MLP work-group and `max_wg` caps
-    the work-groups of each build launch (pcst.h).  signal ((flag, value) from
-    DeviceSignal.next_value()): published by the build's last kernel when it completes."""
+    the work-groups of each build launch (pcst.h)."""
     require_device(orig, idx)
     orig, idx = _f32(orig), _i64(idx)
     B, N, _ = orig.shape
     M = idx.shape[1]
     if ws is None:
         ws = _workspace("pcst_knn_workspace_size", B, N, M, device=orig.device)
-    fl, val = signal if signal is not None else (None, 0)
     _call("pcst_knn3_build", _ptr(orig), _ptr(idx), B, N, M, int(lds_floor), int(max_wg), _ptr(ws),
-          fl, val, _stream())
+          _stream())
     return (orig, idx, ws)
 
 

@@ -123,7 +123,7 @@ static KnnWS carve_knn(void* base, int64_t B, int64_t N, int64_t M) {
   w.olist = c.take<int32_t>(B * N);
   w.obound = c.take<float>(B * N);
   w.nbr = c.take<NbrRec>(B * N);
-  w.err = c.take<int32_t>(4);  // [0] error flags, [2] fill work-groups done (built signal)
+  w.err = c.take<int32_t>(4);
   w.nchunk = c.take<int32_t>(B);
   w.ocount = c.take<int32_t>(B);
   w.known = c.take<uint32_t>(B * N);
@@ -420,10 +420,7 @@ __global__ __launch_bounds__(256) void knn_fill_kernel(const float* __restrict__
                                                        const uint64_t* __restrict__ start,
                                                        const int2* __restrict__ crank,
                                                        float4* __restrict__ refs,
-                                                       int32_t* __restrict__ qorder,
-                                                       uint32_t* __restrict__ sig_flag,
-                                                       uint32_t sig_value,
-                                                       uint32_t* __restrict__ done) {
+                                                       int32_t* __restrict__ qorder) {
   const int b = blockIdx.y;
   const uint64_t* S = start + b * Cpad;
   for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < M + N; e += gridDim.x * 256) {
@@ -438,20 +435,6 @@ __global__ __launch_bounds__(256) void knn_fill_kernel(const float* __restrict__
     } else {
       const uint32_t pos = (uint32_t)(S[cr.x] >> 32) + (uint32_t)cr.y;
       qorder[b * N + pos] = (int32_t)(e - M);
-    }
-  }
-  if (sig_flag) {
-    // the build's completion flag (pcst_knn3_build's built_flag): every thread's stores released
-    // at agent scope, then the last work-group to count itself out publishes the value -- the
-    // one-lane signal launch it replaces sat on the side stream's critical path
-    __threadfence();
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      const uint32_t total = gridDim.x * gridDim.y;
-      if (atomicAdd(done, 1u) == total - 1) {
-        __threadfence();
-        __hip_atomic_store(sig_flag, sig_value, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-      }
     }
   }
 }
@@ -1500,7 +1483,7 @@ static unsigned pad_for(unsigned static_lds, unsigned floor_bytes) {
 // build.  0 = the kernels' natural grids.
 extern "C" int pcst_knn3_build(const float* orig, const int64_t* idx, int64_t B, int64_t N,
                                int64_t M, int64_t lds_floor, int64_t max_wg, void* workspace,
-                               uint32_t* built_flag, uint32_t built_value, void* stream) {
+                               void* stream) {
   PCST_CHECK_ARG(B >= 0 && N > 0 && M > 0 && N < (1ll << 31) && M < (1ll << 27) &&
                      M + N < (1ll << 31),
                  "knn3_build: bad shape");
@@ -1529,8 +1512,7 @@ extern "C" int pcst_knn3_build(const float* orig, const int64_t* idx, int64_t B,
                      w.T, w.Cpad, w.chunks, w.maxch, w.nchunk);
   const unsigned gf = grid(std::min<int64_t>(cdiv(M + N, 256), 2048));
   hipLaunchKernelGGL(knn_fill_kernel, dim3(gf, b), dim3(256), pad_fill, s, orig, idx, N, M, w.Cpad,
-                     w.cnt, w.crank, w.refs, w.qorder, built_flag, built_value,
-                     reinterpret_cast<uint32_t*>(w.err + 2));
+                     w.cnt, w.crank, w.refs, w.qorder);
   PCST_LAUNCH_CHECK("knn3_build");
   return PCST_OK;
 }
@@ -1639,7 +1621,7 @@ extern "C" int pcst_knn3_finish_cfg_ddim(const float* coarse, int64_t B, int64_t
 extern "C" int pcst_knn3_interp(const float* coarse, const float* orig, const int64_t* idx,
                                 int64_t B, int64_t N, int64_t M, float* out, void* workspace,
                                 void* stream) {
-  int rc = pcst_knn3_build(orig, idx, B, N, M, 0, 0, workspace, nullptr, 0u, stream);
+  int rc = pcst_knn3_build(orig, idx, B, N, M, 0, 0, workspace, stream);
   if (rc) return rc;
   return pcst_knn3_query(coarse, orig, B, N, M, out, workspace, nullptr, 0u, 0, stream);
 }

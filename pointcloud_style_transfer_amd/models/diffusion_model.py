@@ -372,13 +372,9 @@ def hierarchical_eps(hp, mlp, xc, xi, x_cat, knn_ws=None, state=None, mlp_waits=
     if BUILT_SIGNAL:
         built = state.built_sig
     with torch.cuda.stream(side):
-        floor = knn_build_lds_floor(xc.shape[0] * xc.shape[1])
-        if BUILT_SIGNAL:  # published by the build's last kernel (no signal launch)
-            handle = _hip.knn3_build(x_cat, xi, knn_ws, floor, KNN_BUILD_MAX_WG,
-                                     signal=built.next_value())
-        else:
-            handle = _hip.knn3_build(x_cat, xi, knn_ws, floor, KNN_BUILD_MAX_WG)
-            built.record(side)
+        handle = _hip.knn3_build(x_cat, xi, knn_ws, knn_build_lds_floor(xc.shape[0] * xc.shape[1]),
+                                 KNN_BUILD_MAX_WG)
+        built.signal(side) if BUILT_SIGNAL else built.record(side)
     kw = {"start": start} if start is not None else {}
     if BUILT_SIGNAL and mlp_waits:  # the MLP's last work-group waits for the build's flag
         nc = mlp(xc, built, **kw)
@@ -461,13 +457,13 @@ KERNEL_SIGNAL = True
 # that finds the flag already set costs a few us.  MLP_WAITS: the MLP's last work-group waits for
 # the flag itself (pcst_noise_mlp_then_wait), no wait launch at all: 0.3765 -> 0.3740 ms/step
 # (profiles/r03/s15_*), within run-to-run noise, and the MLP's launch then also holds the build's
-# tail, so its measured duration (the bench's roofline) is no longer the MLP's own.  Round 4: the
-# build's last kernel publishes the flag itself (pcst_knn3_build's built_flag: no signal launch on
-# the side stream, whose chain ended ~2 us after the MLP plus a 7 us signal launch), so the
-# build now ends before the MLP and the MLP's wait costs nothing; MLP_WAITS on (A/B in
-# profiles/r04).
+# tail, so its measured duration (the bench's roofline) is no longer the MLP's own.  Off.
+# Round 4 tried publishing the flag from the build's last kernel (a counter over the fill
+# kernel's work-groups): every work-group then needs an agent-scope release, i.e. an L2
+# writeback on this multi-XCD part, and the fill went 21 -> 159 us (bench 2700 -> 2030
+# steps/s, profiles/r04/a15): the one-lane signal launch stays.
 BUILT_SIGNAL = True
-MLP_WAITS = True
+MLP_WAITS = False
 # The loop -> side flag written by the MLP launch as it begins (pcst_noise_mlp_ex's start signal)
 # instead of a one-lane signal launch between the voxel emit and the MLP on the loop's queue.
 MLP_SIGNALS = True

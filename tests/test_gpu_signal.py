@@ -41,40 +41,6 @@ def test_signal_orders_consumer_after_producer():
         torch.testing.assert_close(got, y + float(r), rtol=0, atol=0)
 
 
-def test_knn_build_publishes_its_signal():
-    """pcst_knn3_build's built_flag: the fill kernel's last work-group publishes the value once
-    every work-group is done; a query waiting for it on another stream (pcst_signal_wait, then
-    the query's own flag check) gives the bits of the serial build + query, over many rounds
-    with the build queued behind a long producer chain."""
-    from pointcloud_style_transfer_amd import _hip
-
-    dev = torch.device("cuda", 0)
-    rng = np.random.default_rng(5)
-    orig = torch.from_numpy(rng.standard_normal((2, 40000, 3)).astype(np.float32)).to(dev)
-    idx = torch.from_numpy(np.stack([rng.choice(40000, 10000, replace=False)
-                                     for _ in range(2)]).astype(np.int64)).to(dev)
-    coarse = torch.from_numpy(rng.standard_normal((2, 10000, 3)).astype(np.float32)).to(dev)
-    ref = _hip.knn3_query(coarse, _hip.knn3_build(orig, idx))
-    side = torch.cuda.Stream(device=dev)
-    sig = _hip.DeviceSignal(dev)
-    ws = _hip.knn_workspace(2, 40000, 10000, device=dev)
-    a = torch.randn(1024, 1024, device=dev)
-    for r in range(10):
-        side.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(side):
-            y = a
-            for _ in range(3):
-                y = torch.tanh(y @ a)
-            h = _hip.knn3_build(orig, idx, ws, signal=sig.next_value())
-        sig.wait(torch.cuda.current_stream())
-        got = _hip.knn3_query(coarse, h, sig)
-        assert torch.equal(got, ref), r
-        torch.cuda.current_stream().wait_stream(side)
-    torch.cuda.synchronize()
-    assert not sig.timed_out()
-    assert int(sig.flag[0].item()) == sig.value
-
-
 def test_signal_values_are_monotonic_per_flag():
     from pointcloud_style_transfer_amd import _hip
 
