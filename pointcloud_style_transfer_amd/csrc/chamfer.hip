@@ -765,6 +765,11 @@ static inline int64_t cd_padded(int64_t n) { return cdiv(n, kCdChunk) * kCdChunk
 #define PCST_X_CG_RING_BUDGET 2
 #endif
 constexpr int kCgRingBudget = PCST_X_CG_RING_BUDGET;
+// S x R shape of the overflow-list row-min launches (experiment builds may override)
+#ifndef PCST_X_CD_LIST_S
+#define PCST_X_CD_LIST_S 2
+#define PCST_X_CD_LIST_R 1
+#endif
 static bool cd_use_grid(int mode) { return mode == 0 || mode == 2 || mode == 3; }
 static size_t cd_exh_bytes(int64_t B, int64_t N, int64_t M) {
   return (sizeof(float) * 4 * (size_t)B * (size_t)(cd_padded(N) + cd_padded(M)) + 255) / 256 * 256;
@@ -819,11 +824,12 @@ extern "C" int pcst_chamfer_fwd(const float* pred, const float* target, int64_t 
                        w.sorted, w.sidx, min1, arg1, min2, arg2, hybrid ? kCgRingBudget : 0,
                        w.ovf_count, w.ovf_rows);
     if (hybrid) {  // the rows over budget, exhaustively (grid over the list's upper bound)
-      hipLaunchKernelGGL((chamfer_rowmin_kernel<2, 1, true>), dim3((unsigned)cdiv(N, 256), b),
-                         dim3(512), 0, s, pred, Tp, (int)N, (int)M, (int)Mp, min1, arg1,
+      constexpr int LS = PCST_X_CD_LIST_S, LR = PCST_X_CD_LIST_R;
+      hipLaunchKernelGGL((chamfer_rowmin_kernel<LS, LR, true>), dim3((unsigned)cdiv(N, 256 * LR), b),
+                         dim3(256 * LS), 0, s, pred, Tp, (int)N, (int)M, (int)Mp, min1, arg1,
                          w.ovf_rows, w.ovf_count, 0, NM);
-      hipLaunchKernelGGL((chamfer_rowmin_kernel<2, 1, true>), dim3((unsigned)cdiv(M, 256), b),
-                         dim3(512), 0, s, target, Pp, (int)M, (int)N, (int)Np, min2, arg2,
+      hipLaunchKernelGGL((chamfer_rowmin_kernel<LS, LR, true>), dim3((unsigned)cdiv(M, 256 * LR), b),
+                         dim3(256 * LS), 0, s, target, Pp, (int)M, (int)N, (int)Np, min2, arg2,
                          w.ovf_rows, w.ovf_count, 1, NM);
     }
     if (out)
