@@ -1357,17 +1357,27 @@ int wgrad_ex_impl(const void* dZ, int dz_bf16, const void* X, int x_bf16, int64_
 // 512 threads = 8 waves, wave (wr, wc) = (w & 3, w >> 2): rows [32 wr, +32) x cols [64 wc, +64) of
 // each 128 x 128 output tile.  The weights stream through a double-buffered 64-deep B slice:
 // per chunk 4 slices of W1 (K = 256) then 2 x 2 slices of W2 (the two output halves, K = 128).
-constexpr int kRbK = 64;                 // weight slice depth
+#ifndef PCST_RB_TILE  // rows per tile: 128 (512 threads, 64-deep weight slices, one work-group
+#define PCST_RB_TILE 128  // per CU) or 64 (256 threads, 32-deep slices, two work-groups per CU)
+#endif
+constexpr int kRbRows = PCST_RB_TILE;
+constexpr int kRbThreads = kRbRows * 4;          // (rows / 32) x 2 waves
+constexpr int kRbNWR = kRbRows / 32;             // wave rows
+constexpr int kRbK = kRbRows == 128 ? 64 : 32;   // weight slice depth
+constexpr int kRbW1S = 256 / kRbK;               // first-product slices per hidden chunk (K = 256)
+constexpr int kRbW2S = 128 / kRbK;               // second-product slices per output half (K = 128)
+constexpr int kRbSPC = kRbW1S + 2 * kRbW2S;      // slices per chunk
+constexpr int kRbSlices = 4 * kRbSPC;
 #ifndef PCST_RB_PF  // experiment builds: weight slices in flight (1, 2 or 4; divides 32)
 #define PCST_RB_PF 4
 #endif
 constexpr int kRbPF = PCST_RB_PF;
-static_assert(32 % kRbPF == 0, "kRbPF must divide 32");
+static_assert(kRbSlices % kRbPF == 0, "kRbPF must divide the slice count");
 constexpr int kRbBLd = kRbK + 8;         // B image row (16-bit elements): 144 B, conflict-free
 constexpr int kRbXLd = 256 + 8;          // x tile row: 528 B
 constexpr int kRbHLd = 128 + 8;          // h chunk row: 272 B
-constexpr int kRbXBytes = 128 * kRbXLd * 2;
-constexpr int kRbHBytes = 128 * kRbHLd * 2;
+constexpr int kRbXBytes = kRbRows * kRbXLd * 2;
+constexpr int kRbHBytes = kRbRows * kRbHLd * 2;
 constexpr int kRbBBytes = 128 * kRbBLd * 2;
 constexpr int kRbLds = kRbXBytes + kRbHBytes + 2 * kRbBBytes;
 
@@ -1396,24 +1406,26 @@ struct RbArgs {
 // first-product slice has read it.  Bit-identical to the two gemm_ex calls (the fast epilogue's
 // "+ 0" bias included: it turns a -0 product into +0).
 template <bool BWD>
-__global__ __launch_bounds__(512) void resblock_kernel(RbArgs a, int per_xcd, int ntiles) {
+// two waves per SIMD: two 256-thread work-groups per CU (64-row tiles), or one of 512 threads
+__global__ __launch_bounds__(kRbThreads) __attribute__((amdgpu_waves_per_eu(2, 2))) void resblock_kernel(
+    RbArgs a, int per_xcd, int ntiles) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  h16* Xs = reinterpret_cast<h16*>(smem);                                   // [128][kRbXLd]
-  h16* Hs = reinterpret_cast<h16*>(smem + kRbXBytes);                       // [128][kRbHLd]
+  h16* Xs = reinterpret_cast<h16*>(smem);                                   // [rows][kRbXLd]
+  h16* Hs = reinterpret_cast<h16*>(smem + kRbXBytes);                       // [rows][kRbHLd]
   h16* Bs0 = reinterpret_cast<h16*>(smem + kRbXBytes + kRbHBytes);          // [128][kRbBLd]
   h16* Bs1 = reinterpret_cast<h16*>(smem + kRbXBytes + kRbHBytes + kRbBBytes);
   const int L = blockIdx.x;
   const int t = (L & 7) * per_xcd + (L >> 3);
   if (t >= ntiles) return;
-  const int64_t m0 = (int64_t)t * 128;
+  const int64_t m0 = (int64_t)t * kRbRows;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wr = wid & 3, wc = wid >> 2, h = lane >> 5, l32 = lane & 31;
+  const int wr = wid % kRbNWR, wc = wid / kRbNWR, h = lane >> 5, l32 = lane & 31;
   const int64_t M = a.M;
   // x tile -> Xs (rows past M read 0 through the buffer bound)
   const rsrc_t rx = make_rsrc(a.x, (uint32_t)(M * 256 * 2));
 #pragma unroll
-  for (int it = 0; it < 8; ++it) {  // 128 rows x 32 chunks of 16 B
-    const int q = it * 512 + tid, r = q >> 5, cch = (q & 31) * 8;
+  for (int it = 0; it < 8; ++it) {  // rows x 32 chunks of 16 B
+    const int q = it * kRbThreads + tid, r = q >> 5, cch = (q & 31) * 8;
     const uint4 v = bload16(rx, (uint32_t)(((m0 + r) * 256 + cch) * 2), 0);
     *reinterpret_cast<uint4*>(Xs + r * kRbXLd + cch) = v;
   }
@@ -1421,17 +1433,17 @@ __global__ __launch_bounds__(512) void resblock_kernel(RbArgs a, int per_xcd, in
   // j >= 4 -> W2 rows [128 oh, +128) k [128c + 64s, +64) with oh = (j - 4) / 2, s = (j - 4) % 2.
   // Thread -> (row tid / 4, 16 elements at (tid % 4) * 16): two 16-byte loads.
   const rsrc_t rw1 = make_rsrc(a.w1, 512u * 256u * 2u), rw2 = make_rsrc(a.w2, 256u * 512u * 2u);
-  const int br = tid >> 2, bk = (tid & 3) * 16;
+  const int br = tid / (kRbK / 16), bk = (tid % (kRbK / 16)) * 16;
   auto load_slice = [&](int i, uint4& g0, uint4& g1) {
-    const int c = i >> 3, j = i & 7;
+    const int c = i / kRbSPC, j = i % kRbSPC;
     uint32_t off;
     rsrc_t r;
-    if (j < 4) {
-      off = (uint32_t)(((128 * c + br) * 256 + 64 * j + bk) * 2);
+    if (j < kRbW1S) {
+      off = (uint32_t)(((128 * c + br) * 256 + kRbK * j + bk) * 2);
       r = rw1;
     } else {
-      const int oh = (j - 4) >> 1, sl = (j - 4) & 1;
-      off = (uint32_t)(((128 * oh + br) * 512 + 128 * c + 64 * sl + bk) * 2);
+      const int oh = (j - kRbW1S) / kRbW2S, sl = (j - kRbW1S) % kRbW2S;
+      off = (uint32_t)(((128 * oh + br) * 512 + 128 * c + kRbK * sl + bk) * 2);
       r = rw2;
     }
     g0 = bload16(r, off, 0);
@@ -1464,53 +1476,53 @@ __global__ __launch_bounds__(512) void resblock_kernel(RbArgs a, int per_xcd, in
   for (int u = 0; u < kRbPF; ++u) load_slice(u, g[u][0], g[u][1]);
   *reinterpret_cast<uint4*>(Bs0 + br * kRbBLd + bk) = g[0][0];
   *reinterpret_cast<uint4*>(Bs0 + br * kRbBLd + bk + 8) = g[0][1];
-  if (kRbPF < 32) load_slice(kRbPF, g[0][0], g[0][1]);
+  if (kRbPF < kRbSlices) load_slice(kRbPF, g[0][0], g[0][1]);
   const int arow = 32 * wr + l32;
-  for (int i0 = 0; i0 < 32; i0 += kRbPF)
+  for (int i0 = 0; i0 < kRbSlices; i0 += kRbPF)
 #pragma unroll
   for (int u = 0; u < kRbPF; ++u) {
     const int i = i0 + u;
     h16* Bs = (i & 1) ? Bs1 : Bs0;
     __syncthreads();  // slice i landed; slice i - 1's (and the epilogue's) readers are done
-    if (i + 1 < 32) {
+    if (i + 1 < kRbSlices) {
       const int un = (u + 1) % kRbPF;
       h16* Bn = (i & 1) ? Bs0 : Bs1;
       *reinterpret_cast<uint4*>(Bn + br * kRbBLd + bk) = g[un][0];
       *reinterpret_cast<uint4*>(Bn + br * kRbBLd + bk + 8) = g[un][1];
-      if (i + 1 + kRbPF < 32) load_slice(i + 1 + kRbPF, g[un][0], g[un][1]);
+      if (i + 1 + kRbPF < kRbSlices) load_slice(i + 1 + kRbPF, g[un][0], g[un][1]);
     }
-    const int c = i >> 3, j = i & 7;
+    const int c = i / kRbSPC, j = i % kRbSPC;
     if (BWD && j == 0) {
-      // chunk c's mask rows, coalesced (128 rows x 16 chunks of 16 B, 4 per thread)
+      // chunk c's mask rows, coalesced (rows x 16 chunks of 16 B, 4 per thread)
 #pragma unroll
       for (int it = 0; it < 4; ++it) {
-        const int q = it * 512 + tid, r = q >> 4, cch = (q & 15) * 8;
+        const int q = it * kRbThreads + tid, r = q >> 4, cch = (q & 15) * 8;
         mk[it] = bload16(rm, (uint32_t)(((m0 + r) * 512 + 128 * c + cch) * 2), 0);
       }
     }
-    if (BWD && j == 2) {
+    if (BWD && j == kRbW1S - 2) {
       // -> Hs: the previous chunk's second-product readers passed this slice's barrier; the
       // epilogue reads it after the next one
 #pragma unroll
       for (int it = 0; it < 4; ++it) {
-        const int q = it * 512 + tid, r = q >> 4, cch = (q & 15) * 8;
+        const int q = it * kRbThreads + tid, r = q >> 4, cch = (q & 15) * 8;
         *reinterpret_cast<uint4*>(Hs + r * kRbHLd + cch) = mk[it];
       }
     }
-    if (BWD && i == 28) {
+    if (BWD && i == kRbSlices - 2 * kRbW2S) {
       // g tile: Xs is read for the last time by slice 27's first product
 #pragma unroll
       for (int it = 0; it < 8; ++it) {
-        const int q = it * 512 + tid, r = q >> 5, cch = (q & 31) * 8;
+        const int q = it * kRbThreads + tid, r = q >> 5, cch = (q & 31) * 8;
         gr[it] = bload16(rg, (uint32_t)(((m0 + r) * 256 + cch) * 2), 0);
       }
     }
-    if (j == 4) {
+    if (j == kRbW1S) {
       // chunk c's h (written to Hs by every wave after slice 8c + 3) -> global h, coalesced:
-      // 128 rows x 16 chunks of 16 B, 4 per thread
+      // rows x 16 chunks of 16 B, 4 per thread
 #pragma unroll
       for (int it = 0; it < 4; ++it) {
-        const int q = it * 512 + tid, r = q >> 4, cch = (q & 15) * 8;
+        const int q = it * kRbThreads + tid, r = q >> 4, cch = (q & 15) * 8;
         const uint4 v = *reinterpret_cast<const uint4*>(Hs + r * kRbHLd + cch);
         const v4i32 vv = {(int)v.x, (int)v.y, (int)v.z, (int)v.w};
         __builtin_amdgcn_raw_buffer_store_b128(vv, rh, (int)(((m0 + r) * 512 + 128 * c + cch) * 2), 0, 0);
@@ -1519,18 +1531,19 @@ __global__ __launch_bounds__(512) void resblock_kernel(RbArgs a, int per_xcd, in
 #pragma unroll
     for (int ks = 0; ks < kRbK / 16; ++ks) {
       h16x8 av, b[2];
-      if (j < 4)
-        av = *reinterpret_cast<const h16x8*>(Xs + arow * kRbXLd + 64 * j + 16 * ks + 8 * h);
+      if (j < kRbW1S)
+        av = *reinterpret_cast<const h16x8*>(Xs + arow * kRbXLd + kRbK * j + 16 * ks + 8 * h);
       else
-        av = *reinterpret_cast<const h16x8*>(Hs + arow * kRbHLd + 64 * ((j - 4) & 1) + 16 * ks + 8 * h);
+        av = *reinterpret_cast<const h16x8*>(Hs + arow * kRbHLd + kRbK * ((j - kRbW1S) % kRbW2S) +
+                                             16 * ks + 8 * h);
 #pragma unroll
       for (int bn = 0; bn < 2; ++bn)
         b[bn] = *reinterpret_cast<const h16x8*>(Bs + (64 * wc + 32 * bn + l32) * kRbBLd + 16 * ks + 8 * h);
-      if (j < 4) {
+      if (j < kRbW1S) {
 #pragma unroll
         for (int bn = 0; bn < 2; ++bn) acc1[bn] = mfma32_h16(av, b[bn], acc1[bn]);
       } else {
-        const int oh = (j - 4) >> 1;
+        const int oh = (j - kRbW1S) / kRbW2S;
 #pragma unroll
         for (int bn = 0; bn < 2; ++bn) {
           if (oh == 0) acc2[bn] = mfma32_h16(av, b[bn], acc2[bn]);
@@ -1538,7 +1551,7 @@ __global__ __launch_bounds__(512) void resblock_kernel(RbArgs a, int per_xcd, in
         }
       }
     }
-    if (j == 3) {
+    if (j == kRbW1S - 1) {
       // chunk c's epilogue into Hs (read by every wave after the next slice's barrier): forward
       // h = 16-bit(relu(acc1 + b1)); backward dZ = 16-bit(acc1 + 0 masked by h > 0), the mask
       // read from the lane's own element.  The accumulators restart for chunk c + 1.
@@ -1561,7 +1574,7 @@ __global__ __launch_bounds__(512) void resblock_kernel(RbArgs a, int per_xcd, in
   if (BWD) {
 #pragma unroll
     for (int it = 0; it < 8; ++it) {
-      const int q = it * 512 + tid, r = q >> 5, cch = (q & 31) * 8;
+      const int q = it * kRbThreads + tid, r = q >> 5, cch = (q & 31) * 8;
       *reinterpret_cast<uint4*>(Xs + r * kRbXLd + cch) = gr[it];
     }
   }
@@ -1592,7 +1605,7 @@ __global__ __launch_bounds__(512) void resblock_kernel(RbArgs a, int per_xcd, in
   const rsrc_t rd = make_rsrc(BWD ? a.ddo : nullptr, BWD && a.ddo ? (uint32_t)(M * 256 * 2) : 0u);
 #pragma unroll
   for (int it = 0; it < 8; ++it) {
-    const int q = it * 512 + tid, r = q >> 5, cch = (q & 31) * 8;
+    const int q = it * kRbThreads + tid, r = q >> 5, cch = (q & 31) * 8;
     const uint4 v = *reinterpret_cast<const uint4*>(Xs + r * kRbXLd + cch);
     const int off = (int)(((m0 + r) * 256 + cch) * 2);
     __builtin_amdgcn_raw_buffer_store_b128(v4i32{(int)v.x, (int)v.y, (int)v.z, (int)v.w}, ro, off, 0, 0);
@@ -1636,9 +1649,9 @@ int resblock_fwd_impl(const uint16_t* x, int64_t M, const uint16_t* w1, const fl
   a.seed_hi = (uint32_t)(seed >> 32);
   a.thr = drop_threshold(drop_p);
   a.scale = 1.0f / (1.0f - drop_p);
-  const int ntiles = (int)cdiv(M, 128), per = (int)cdiv(ntiles, 8);
+  const int ntiles = (int)cdiv(M, kRbRows), per = (int)cdiv(ntiles, 8);
   a.hm = nullptr; a.g = nullptr; a.ddo = nullptr;
-  hipLaunchKernelGGL(resblock_kernel<false>, dim3((unsigned)(8 * per)), dim3(512), kRbLds,
+  hipLaunchKernelGGL(resblock_kernel<false>, dim3((unsigned)(8 * per)), dim3(kRbThreads), kRbLds,
                      as_stream(stream), a, per, ntiles);
   PCST_LAUNCH_CHECK("resblock_fwd");
   return PCST_OK;
@@ -1662,8 +1675,8 @@ int resblock_bwd_impl(const uint16_t* dd, int64_t M, const uint16_t* w2t, const 
   a.seed_hi = (uint32_t)(seed >> 32);
   a.thr = drop_threshold(drop_p);
   a.scale = 1.0f / (1.0f - drop_p);
-  const int ntiles = (int)cdiv(M, 128), per = (int)cdiv(ntiles, 8);
-  hipLaunchKernelGGL(resblock_kernel<true>, dim3((unsigned)(8 * per)), dim3(512), kRbLds,
+  const int ntiles = (int)cdiv(M, kRbRows), per = (int)cdiv(ntiles, 8);
+  hipLaunchKernelGGL(resblock_kernel<true>, dim3((unsigned)(8 * per)), dim3(kRbThreads), kRbLds,
                      as_stream(stream), a, per, ntiles);
   PCST_LAUNCH_CHECK("resblock_bwd");
   return PCST_OK;
