@@ -293,6 +293,9 @@ __global__ void chamfer_keys_kernel(const int32_t* __restrict__ argm, int R, uin
 // deterministic and a destination with many sources (a point many rows collapse onto) costs
 // len/16 rounds instead of len.
 constexpr int kGatherLanes = 16;
+#ifndef PCST_X_CD_GATHER16
+#define PCST_X_CD_GATHER16 0
+#endif
 __global__ void chamfer_gather_kernel(const float* __restrict__ Dp, int ND,
                                       const float* __restrict__ Sp, int NR,
                                       const uint32_t* __restrict__ skeys,
@@ -337,6 +340,173 @@ __global__ void chamfer_gather_kernel(const float* __restrict__ Dp, int ND,
   }
 }
 
+// The same sums as a segmented reduction over the sorted (destination, row) pairs, so a
+// destination that many rows share (a noisy predicted x0: thousands of target rows on one
+// predicted point) costs one pass over its entries in parallel instead of a serial loop of 16
+// lanes.  chamfer_segsum_kernel: kSegE consecutive entries per block; a segmented inclusive scan
+// (thread-serial over 4 entries, then a block scan of (head seen, sum) pairs) gives every
+// segment end its sum since max(segment head, block start).  A segment that starts and ends in
+// the block is written by it (its only writer).  The block records its first segment's partial
+// when that segment began in an earlier block and ends here, and its last segment's partial when
+// that segment runs on past the block.  chamfer_segfix_kernel: the block holding a spanning
+// segment's end adds the earlier blocks' partials, walking back to the segment's head.  The
+// summation order is fixed, so the gradient is deterministic.
+constexpr int kSegPer = 4;
+constexpr int kSegE = 256 * kSegPer;  // entries per block
+__device__ __forceinline__ void seg_op(int& f, float (&a)[3], int f2, const float (&b)[3]) {
+  // (f, a) (+) (f2, b): b restarts at a head
+#pragma unroll
+  for (int c = 0; c < 3; ++c) a[c] = f2 ? b[c] : a[c] + b[c];
+  f |= f2;
+}
+__global__ __launch_bounds__(256) void chamfer_segsum_kernel(
+    const float* __restrict__ Dp, int ND, const float* __restrict__ Sp, int NR,
+    const uint32_t* __restrict__ skeys, const uint32_t* __restrict__ svals,
+    const float* __restrict__ gout, float sign, float* __restrict__ grad, int nblk,
+    float4* __restrict__ part, int* __restrict__ pflag) {
+  const int b = blockIdx.y, blk = blockIdx.x, tid = threadIdx.x;
+  const int base = blk * kSegE;
+  const uint32_t* K = skeys + (int64_t)b * NR;
+  const uint32_t* V = svals + (int64_t)b * NR;
+  const float g = gout[b] * 2.0f / (float)NR;
+  // this thread's entries: values and head flags
+  float v[kSegPer][3];
+  int hd[kSegPer];
+  uint32_t key[kSegPer];
+  const int k0 = base + tid * kSegPer;
+#pragma unroll
+  for (int u = 0; u < kSegPer; ++u) {
+    const int k = k0 + u;
+    v[u][0] = v[u][1] = v[u][2] = 0.0f;
+    hd[u] = 1;
+    key[u] = 0xffffffffu;
+    if (k < NR) {
+      key[u] = K[k];
+      hd[u] = k == 0 || K[k - 1] != key[u];
+      const int d = (int)key[u], r = (int)V[k];
+      const float* q = Dp + ((int64_t)b * ND + (d < ND ? d : 0)) * 3;
+      const float* p = Sp + ((int64_t)b * NR + r) * 3;
+      if (raw_pair(p, q) >= 0.0f) {
+        v[u][0] = g * (p[0] - q[0]);
+        v[u][1] = g * (p[1] - q[1]);
+        v[u][2] = g * (p[2] - q[2]);
+      }
+    }
+  }
+  // thread-serial segmented scan, then the thread aggregates across the block
+  float s[kSegPer][3];
+  int f = hd[0];
+  float acc[3] = {v[0][0], v[0][1], v[0][2]};
+#pragma unroll
+  for (int c = 0; c < 3; ++c) s[0][c] = acc[c];
+#pragma unroll
+  for (int u = 1; u < kSegPer; ++u) {
+    seg_op(f, acc, hd[u], v[u]);
+#pragma unroll
+    for (int c = 0; c < 3; ++c) s[u][c] = acc[c];
+  }
+  // inclusive block scan of (f, acc) over threads (wave shuffles, then the waves in LDS)
+  const int lane = tid & 63, wv = tid >> 6;
+  int fi = f;
+  float ai[3] = {acc[0], acc[1], acc[2]};
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const int fo = __shfl_up(fi, off);
+    float ao[3];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) ao[c] = __shfl_up(ai[c], off);
+    if (lane >= off) {  // (fo, ao) (+) (fi, ai)
+      float r[3] = {ao[0], ao[1], ao[2]};
+      int fr = fo;
+      seg_op(fr, r, fi, ai);
+      fi = fr;
+#pragma unroll
+      for (int c = 0; c < 3; ++c) ai[c] = r[c];
+    }
+  }
+  __shared__ float wsum[4][3];
+  __shared__ int wflag[4];
+  if (lane == 63) {
+    wflag[wv] = fi;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) wsum[wv][c] = ai[c];
+  }
+  __syncthreads();
+  // exclusive prefix for this thread: the waves before, then the lanes before
+  int fx = 0;
+  float ax[3] = {0.0f, 0.0f, 0.0f};
+  for (int w = 0; w < wv; ++w) {
+    float t[3] = {wsum[w][0], wsum[w][1], wsum[w][2]};
+    seg_op(fx, ax, wflag[w], t);
+  }
+  {
+    const int fl = __shfl_up(fi, 1);
+    float al[3];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) al[c] = __shfl_up(ai[c], 1);
+    if (lane > 0) seg_op(fx, ax, fl, al);
+  }
+  // the block's first segment began in an earlier block and ends in this one: segfix completes
+  // it (a flag per block, written every call)
+  if (tid == 0 && base < NR) {
+    const uint32_t k0key = K[base];
+    const int last = min(base + kSegE, NR) - 1;
+    const bool spans_in = base > 0 && K[base - 1] == k0key;
+    const bool runs_on = K[last] == k0key && last + 1 < NR && K[last + 1] == k0key;
+    pflag[b * nblk + blk] = spans_in && !runs_on;
+  }
+  // entries: carry-in until the thread's first head
+#pragma unroll
+  for (int u = 0; u < kSegPer; ++u) {
+    const int k = k0 + u;
+    if (k >= NR) break;
+    // sum of this entry's segment since max(head, block start) up to k
+    bool head_seen = false;  // a head among this thread's entries 0..u
+#pragma unroll
+    for (int w = 0; w <= u; ++w) head_seen |= hd[w] != 0;
+    float tot[3];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) tot[c] = head_seen ? s[u][c] : ax[c] + s[u][c];
+    const bool head_in_block = head_seen || fx != 0;  // the segment's head lies in this block
+    const bool seg_end = k == NR - 1 || K[k + 1] != key[u];
+    if (seg_end) {
+      if (head_in_block) {
+        float* o = grad + ((int64_t)b * ND + key[u]) * 3;
+        o[0] += -sign * tot[0];
+        o[1] += -sign * tot[1];
+        o[2] += -sign * tot[2];
+      } else {  // began in an earlier block: this block holds its end (segfix completes it)
+        part[((int64_t)b * nblk + blk) * 2] = make_float4(tot[0], tot[1], tot[2], 0.0f);
+      }
+    } else if (k == base + kSegE - 1) {  // runs on past the block: this block's portion
+      part[((int64_t)b * nblk + blk) * 2 + 1] = make_float4(tot[0], tot[1], tot[2], 0.0f);
+    }
+  }
+}
+
+__global__ void chamfer_segfix_kernel(int ND, int NR, const uint32_t* __restrict__ skeys, float sign,
+                                      float* __restrict__ grad, int nblk,
+                                      const float4* __restrict__ part, int* __restrict__ pflag) {
+  const int b = blockIdx.y, blk = blockIdx.x * 256 + threadIdx.x;
+  if (blk >= nblk || !pflag[b * nblk + blk]) return;
+  const uint32_t* K = skeys + (int64_t)b * NR;
+  const float4 e = part[((int64_t)b * nblk + blk) * 2];
+  float t[3] = {e.x, e.y, e.z};
+  const uint32_t key = K[blk * kSegE];
+  // walk back over the blocks the segment runs through: each contributes its last portion
+  for (int j = blk - 1; j >= 0; --j) {
+    const float4 q = part[((int64_t)b * nblk + j) * 2 + 1];
+    t[0] += q.x;
+    t[1] += q.y;
+    t[2] += q.z;
+    if (j == 0 || K[j * kSegE - 1] != key) break;  // the segment's head is in block j
+  }
+  float* o = grad + ((int64_t)b * ND + key) * 3;
+  o[0] += -sign * t[0];
+  o[1] += -sign * t[1];
+  o[2] += -sign * t[2];
+}
+
 // ---- L1 (F.l1_loss, mean reduction): deterministic two-level float64 sum
 constexpr int kL1Blocks = 512;
 __global__ __launch_bounds__(256) void l1_partial_kernel(const float* __restrict__ a,
@@ -374,6 +544,8 @@ __global__ void l1_bwd_kernel(const float* __restrict__ a, const float* __restri
 
 struct CdWS {
   uint32_t *kA, *vA, *kB, *vB, *hist;
+  float4* part;  // [B][blocks][2] segmented-sum partials (chamfer_segsum_kernel)
+  int* pflag;    // [B][blocks]
   size_t bytes;
 };
 static CdWS carve_cd(void* base, int64_t B, int64_t R) {
@@ -384,6 +556,8 @@ static CdWS carve_cd(void* base, int64_t B, int64_t R) {
   w.kB = c.take<uint32_t>(B * R);
   w.vB = c.take<uint32_t>(B * R);
   w.hist = c.take<uint32_t>(radix_hist_words((int)B, R));
+  w.part = c.take<float4>(B * cdiv(R, kSegE) * 2);
+  w.pflag = c.take<int>(B * cdiv(R, kSegE));
   w.bytes = c.bytes();
   return w;
 }
@@ -886,6 +1060,20 @@ extern "C" int pcst_chamfer_bwd(const float* pred, const float* target, int64_t 
   hipStream_t s = as_stream(stream);
   CdWS w = carve_cd(workspace, B, std::max(N, M));
   const unsigned b = (unsigned)B;
+  // the scatter onto the argmin side from the sorted (destination, row) pairs: segmented sums
+  // (PCST_X_CD_GATHER16 = 1: the 16-lane gather per destination, A/B)
+  auto seg_gather = [&](const float* D, int ND, const float* S, int NR, const float* go, float* gr) {
+    if (PCST_X_CD_GATHER16) {
+      hipLaunchKernelGGL(chamfer_gather_kernel, dim3((unsigned)cdiv((int64_t)ND * kGatherLanes, 256), b),
+                         dim3(256), 0, s, D, ND, S, NR, w.kA, w.vA, go, 1.0f, gr);
+      return;
+    }
+    const int nblk = (int)cdiv(NR, kSegE);
+    hipLaunchKernelGGL(chamfer_segsum_kernel, dim3((unsigned)nblk, b), dim3(256), 0, s, D, ND, S, NR,
+                       w.kA, w.vA, go, 1.0f, gr, nblk, w.part, w.pflag);
+    hipLaunchKernelGGL(chamfer_segfix_kernel, dim3((unsigned)cdiv(nblk, 256), b), dim3(256), 0, s, ND,
+                       NR, w.kA, 1.0f, gr, nblk, w.part, w.pflag);
+  };
   // direction 1 (pred rows -> target argmin): direct on pred, scattered on target
   if (grad_pred)
     hipLaunchKernelGGL(chamfer_direct_kernel, dim3((unsigned)cdiv(N, 256), b), dim3(256), 0, s,
@@ -896,9 +1084,7 @@ extern "C" int pcst_chamfer_bwd(const float* pred, const float* target, int64_t 
     int rc = radix_sort_pairs(w.kA, w.vA, w.kB, w.vB, w.hist, (int)B, N, SegCounts{nullptr, (int32_t)N},
                               0, 32, s);
     if (rc) return rc;
-    hipLaunchKernelGGL(chamfer_gather_kernel, dim3((unsigned)cdiv(M * kGatherLanes, 256), b),
-                       dim3(256), 0, s, target, (int)M, pred, (int)N, w.kA, w.vA, grad_out, 1.0f,
-                       grad_target);
+    seg_gather(target, (int)M, pred, (int)N, grad_out, grad_target);
   }
   // direction 2 (target rows -> pred argmin): direct on target, scattered on pred
   if (grad_target)
@@ -910,9 +1096,7 @@ extern "C" int pcst_chamfer_bwd(const float* pred, const float* target, int64_t 
     int rc = radix_sort_pairs(w.kA, w.vA, w.kB, w.vB, w.hist, (int)B, M, SegCounts{nullptr, (int32_t)M},
                               0, 32, s);
     if (rc) return rc;
-    hipLaunchKernelGGL(chamfer_gather_kernel, dim3((unsigned)cdiv(N * kGatherLanes, 256), b),
-                       dim3(256), 0, s, pred, (int)N, target, (int)M, w.kA, w.vA, grad_out, 1.0f,
-                       grad_pred);
+    seg_gather(pred, (int)N, target, (int)M, grad_out, grad_pred);
   }
   PCST_LAUNCH_CHECK("chamfer_bwd");
   return PCST_OK;

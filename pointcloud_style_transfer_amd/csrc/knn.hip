@@ -58,9 +58,6 @@ constexpr int kCountPerBlock = 1024;     // elements per count-kernel block (4 p
 #ifndef PCST_KNN_SLOTKEY  // 1: the one-pass slot-keyed query window (Query::window); 0: two-pass
 #define PCST_KNN_SLOTKEY 1
 #endif
-#ifndef PCST_X_KNN_FLOOR_MASK  // build kernels the LDS floor applies to (see pcst_knn3_build)
-#define PCST_X_KNN_FLOOR_MASK 14
-#endif
 constexpr int kQueryBlocks = 1024;       // query workgroups per cloud (grid-stride over chunks)
 // the query grid's cap over all clouds of one launch, when the caller passes grid_cap <= 0: at
 // 32 clouds (64 CFG rows) 16384 workgroups let each wave stride over several chunks (r04 A/B,
@@ -1498,15 +1495,8 @@ extern "C" int pcst_knn3_build(const float* orig, const int64_t* idx, int64_t B,
   KnnWS w = carve_knn(workspace, B, N, M);
   const int b = (int)B;
   const unsigned f = (unsigned)lds_floor;
-  // the floor holds count / scan / fill off CUs an MLP work-group occupies; the pre kernel
-  // (cloud statistics, known rows: a few us of work) runs unpadded, beside the MLP's first round,
-  // instead of waiting for a CU with the rest (PCST_X_KNN_FLOOR_MASK: bit 0 pre, 1 count,
-  // 2 scan, 3 fill; experiment builds may override)
-  const int fm = PCST_X_KNN_FLOOR_MASK;
-  const unsigned pad_pre = (fm & 1) ? pad_for(kLdsPre, f) : 0u,
-                 pad_count = (fm & 2) ? pad_for(kLdsCount, f) : 0u,
-                 pad_scan = (fm & 4) ? pad_for(kLdsScan, f) : 0u,
-                 pad_fill = (fm & 8) ? pad_for(kLdsFill, f) : 0u;
+  const unsigned pad_pre = pad_for(kLdsPre, f), pad_count = pad_for(kLdsCount, f),
+                 pad_scan = pad_for(kLdsScan, f), pad_fill = pad_for(kLdsFill, f);
   // per-cloud grid of each launch: natural size, capped at max_wg / B (at least one)
   const int64_t cap = max_wg > 0 ? std::max<int64_t>(1, max_wg / B) : (int64_t)1 << 30;
   auto grid = [&](int64_t natural) { return (unsigned)std::min<int64_t>(natural, cap); };

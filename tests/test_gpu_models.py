@@ -276,3 +276,39 @@ def test_ddim_loop_hierarchical(mods, golden):
         out = dp.ddim_sample_loop(m, (1, 4096, 3), dev(g["cond"]), 3)
     assert rp.exhausted
     assert_mostly_close(out.cpu().numpy(), g["out"])
+
+
+@pytest.mark.parametrize("heavy", [0, 1, 20000])
+def test_chamfer_bwd_segmented_scatter_vs_float64(heavy):
+    """pcst_chamfer_bwd's scatter onto the argmin side (segmented sums over the sorted
+    (destination, row) pairs, partials of segments that span blocks completed in order) against a
+    float64 restatement of the autograd gradient, with `heavy` target rows sharing one predicted
+    point as their nearest (a segment spanning ~20 of the 1024-entry blocks), ragged sizes, and
+    twice the same call for determinism."""
+    from pointcloud_style_transfer_amd import _hip
+
+    rng = np.random.default_rng(17 + heavy)
+    B, N, M = 2, 3001, 40003
+    p = (rng.standard_normal((B, N, 3)) * 4).astype(np.float32)
+    q = (rng.standard_normal((B, M, 3)) * 4).astype(np.float32)
+    if heavy:
+        p[:, 7] = (40.0, 40.0, 40.0)
+        q[:, :heavy] = (40.0 + rng.standard_normal((B, heavy, 3)) * 0.05).astype(np.float32)
+    P, Q = dev(p), dev(q)
+    out, a1, a2 = _hip.chamfer_fwd(P, Q, 1)
+    gout = dev(np.array([0.7, 1.3], np.float32))
+    gp, gt = _hip.chamfer_bwd(P, Q, a1, a2, gout, need_pred=True, need_target=True)
+    gp2, gt2 = _hip.chamfer_bwd(P, Q, a1, a2, gout, need_pred=True, need_target=True)
+    assert torch.equal(gp, gp2) and torch.equal(gt, gt2)
+    a1, a2 = a1.cpu().numpy(), a2.cpu().numpy()
+    p64, q64 = p.astype(np.float64), q.astype(np.float64)
+    for b in range(B):
+        g = float(gout[b])
+        want_p = 2 * g / N * (p64[b] - q64[b][a1[b]])
+        np.add.at(want_p, a2[b], 2 * g / M * (p64[b][a2[b]] - q64[b]))
+        want_q = 2 * g / M * (q64[b] - p64[b][a2[b]])
+        np.add.at(want_q, a1[b], 2 * g / N * (q64[b][a1[b]] - p64[b]))
+        for got, want in ((gp[b], want_p), (gt[b], want_q)):
+            got = got.cpu().numpy().astype(np.float64)
+            scale = np.abs(want).max() + 1e-30
+            assert np.abs(got - want).max() <= 2e-5 * scale, (heavy, np.abs(got - want).max(), scale)
