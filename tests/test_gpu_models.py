@@ -291,9 +291,10 @@ def test_chamfer_bwd_segmented_scatter_vs_float64(heavy):
     B, N, M = 2, 3001, 40003
     p = (rng.standard_normal((B, N, 3)) * 4).astype(np.float32)
     q = (rng.standard_normal((B, M, 3)) * 4).astype(np.float32)
-    if heavy:
-        p[:, 7] = (40.0, 40.0, 40.0)
-        q[:, :heavy] = (40.0 + rng.standard_normal((B, heavy, 3)) * 0.05).astype(np.float32)
+    if heavy:  # (away from the other points, and no pair close enough for the expanded fp32
+        # distance to round below 0, where the gradient is dropped -- the reference's clamp)
+        p[:, 7] = (12.0, 0.0, 0.0)
+        q[:, :heavy] = ((12.0, 0.0, 0.0) + rng.standard_normal((B, heavy, 3)) * 0.5).astype(np.float32)
     P, Q = dev(p), dev(q)
     out, a1, a2 = _hip.chamfer_fwd(P, Q, 1)
     gout = dev(np.array([0.7, 1.3], np.float32))
