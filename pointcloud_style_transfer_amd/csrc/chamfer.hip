@@ -661,9 +661,9 @@ __global__ __launch_bounds__(1024) void cg_stats_kernel(const float* __restrict_
     const float dens = (float)fmax(hsq / fmax((double)n, 1.0), 1.0) / bin_vol;
     float h = cbrtf((float)kCgPerCell / dens);
     if (!(h > 1e-30f) || !(h < INFINITY)) h = fmaxf(emax, 1.0f);  // degenerate cloud
-    for (int it = 0; it < 64; ++it) {  // grow h until the (bricked) cell count fits
-      int64_t c = 64;
-      for (int a = 0; a < 3; ++a) c *= ((int64_t)fminf(ceilf(ext[a] / h) + 1.0f, 4096.0f) + 3) / 4;
+    for (int it = 0; it < 64; ++it) {  // grow h until the cell count fits
+      int64_t c = 1;
+      for (int a = 0; a < 3; ++a) c *= (int64_t)fminf(ceilf(ext[a] / h) + 1.0f, 4096.0f);
       if (c <= kCgMaxCells) break;
       h *= 1.25f;
     }
@@ -675,15 +675,6 @@ __global__ __launch_bounds__(1024) void cg_stats_kernel(const float* __restrict_
     g.nmax = -r[6];
     grids[b * 2 + side] = g;
   }
-}
-
-// brick-major cell id: 4x4x4-cell bricks in row-major order, Morton order inside a brick, so a
-// run of consecutive cell-sorted points is a compact box (the overflow search's runs)
-__device__ __forceinline__ int cg_cell(int x, int y, int z, const CgGrid& g) {
-  const int bx = (g.d[0] + 3) >> 2, by = (g.d[1] + 3) >> 2;
-  const int m = (x & 1) | ((y & 1) << 1) | ((z & 1) << 2) | ((x & 2) << 2) | ((y & 2) << 3) |
-                ((z & 2) << 4);
-  return ((((z >> 2) * by + (y >> 2)) * bx + (x >> 2)) << 6) + m;
 }
 
 __device__ __forceinline__ int cg_cell_coord(float x, float o, float inv_h, int d) {
@@ -704,7 +695,7 @@ __global__ void cg_count_kernel(const float* __restrict__ P, const float* __rest
   const int cx = cg_cell_coord(X[0], g.o[0], g.inv_h, g.d[0]);
   const int cy = cg_cell_coord(X[1], g.o[1], g.inv_h, g.d[1]);
   const int cz = cg_cell_coord(X[2], g.o[2], g.inv_h, g.d[2]);
-  const int cell = cg_cell(cx, cy, cz, g);
+  const int cell = (cz * g.d[1] + cy) * g.d[0] + cx;
   const int rank = atomicAdd(&counts[(int64_t)(b * 2 + side) * (kCgMaxCells + 1) + cell], 1);
   crank[(int64_t)(b * 2 + side) * (N > M ? N : M) + i] = make_int2(cell, rank);
 }
@@ -796,9 +787,7 @@ __global__ __launch_bounds__(256) void cg_rowmin_kernel(int N, int M,
                                                         int32_t* __restrict__ arg2,
                                                         int ring_budget,
                                                         int* __restrict__ ovf_count,
-                                                        int* __restrict__ ovf_rows,
-                                                        float* __restrict__ ovf_best,
-                                                        int* __restrict__ ovf_bi) {
+                                                        int* __restrict__ ovf_rows) {
   const int b = blockIdx.y, side = blockIdx.z;  // side 0: pred rows vs target grid
   const int n = side ? M : N;
   const int r = blockIdx.x * blockDim.x + threadIdx.x;
@@ -854,13 +843,9 @@ __global__ __launch_bounds__(256) void cg_rowmin_kernel(int N, int M,
       if (!any) break;  // the rings so far cover the whole grid
       if (lb * shrink - err > best) break;
     }
-    if (ring_budget > 0 && ring > ring_budget) {  // over budget: the overflow pass takes it
+    if (ring_budget > 0 && ring > ring_budget) {  // over budget: the exhaustive pass takes it
       const int at = atomicAdd(&ovf_count[rs], 1);
       ovf_rows[rs * NM + at] = row;
-      if (ovf_best) {  // the rings' best so far: where the pruned overflow search starts
-        ovf_best[rs * NM + at] = best;
-        ovf_bi[rs * NM + at] = bi;
-      }
       return;
     }
     const int z0 = max(cz - ring, 0), z1 = min(cz + ring, g.d[2] - 1);
@@ -871,7 +856,7 @@ __global__ __launch_bounds__(256) void cg_rowmin_kernel(int N, int M,
       const float gy = cg_axis_gap(py, g.o[1] + y * g.h - g.slack, g.o[1] + (y + 1) * g.h + g.slack);
       const float gz = cg_axis_gap(pz, g.o[2] + z * g.h - g.slack, g.o[2] + (z + 1) * g.h + g.slack);
       if (best != INFINITY && (gx * gx + gy * gy + gz * gz) * shrink - err > best) return;
-      const int cell = cg_cell(x, y, z, g);
+      const int cell = (z * g.d[1] + y) * g.d[0] + x;
       const int k1 = S[cell + 1];
       for (int k = S[cell]; k < k1; ++k) {
         const float4 q = T[k];
@@ -905,113 +890,6 @@ __global__ __launch_bounds__(256) void cg_rowmin_kernel(int N, int M,
   }
 }
 
-// ---- Box-pruned search of the overflow rows (the hybrid mode's rows still open after the ring
-// budget: rows far outside the other cloud).  The other cloud's cell-sorted points are cut into
-// runs of kCgRun consecutive points with their exact bounding boxes (cg_runbox_kernel).  One lane
-// per overflow row, the list in the order the grid search appended it (spatially coherent; cells
-// are brick-major, so a run is a compact box): every
-// run whose box lies nearer (by the same conservative computed-distance bound as the rings) than
-// some lane's best so far is scored by every lane of the wave; the others are skipped whole.
-// Each lane starts from its rings' best, keeps (clamped D, original index) lexicographically --
-// bit-identical to the exhaustive first-index argmin -- and visits the runs in sorted order.
-constexpr int kCgRun = 64;
-__global__ __launch_bounds__(256) void cg_runbox_kernel(int N, int M, const float4* __restrict__ sorted,
-                                                        float4* __restrict__ boxes) {
-  const int b = blockIdx.y, side = blockIdx.z;
-  const int n = side ? M : N, NM = N > M ? N : M;
-  const int run = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
-  const int nrun = (n + kCgRun - 1) / kCgRun, mrun = (NM + kCgRun - 1) / kCgRun;
-  if (run >= nrun) return;
-  const int64_t slot = (int64_t)(b * 2 + side);
-  const int k = run * kCgRun + lane;
-  const float4 q = sorted[slot * NM + (k < n ? k : run * kCgRun)];
-  float lo[3] = {q.x, q.y, q.z}, hi[3] = {q.x, q.y, q.z};
-#pragma unroll
-  for (int off = 32; off >= 1; off >>= 1)
-#pragma unroll
-    for (int a = 0; a < 3; ++a) {
-      lo[a] = fminf(lo[a], __shfl_xor(lo[a], off));
-      hi[a] = fmaxf(hi[a], __shfl_xor(hi[a], off));
-    }
-  if (lane == 0) {
-    boxes[(slot * mrun + run) * 2] = make_float4(lo[0], lo[1], lo[2], 0.0f);
-    boxes[(slot * mrun + run) * 2 + 1] = make_float4(hi[0], hi[1], hi[2], 0.0f);
-  }
-}
-
-__global__ __launch_bounds__(256) void cg_prune_kernel(const float* __restrict__ P,
-                                                       const float* __restrict__ Q, int N, int M,
-                                                       const CgGrid* __restrict__ grids,
-                                                       const float4* __restrict__ sorted,
-                                                       const int* __restrict__ sidx,
-                                                       const float4* __restrict__ boxes,
-                                                       const int* __restrict__ ovf_count,
-                                                       const int* __restrict__ ovf_rows,
-                                                       const float* __restrict__ ovf_best,
-                                                       const int* __restrict__ ovf_bi,
-                                                       float* __restrict__ min1, int32_t* __restrict__ arg1,
-                                                       float* __restrict__ min2, int32_t* __restrict__ arg2) {
-  const int b = blockIdx.y, side = blockIdx.z;  // side 0: pred rows vs the target's runs
-  const int NM = N > M ? N : M;
-  const int64_t rs = (int64_t)(b * 2 + side), ts = (int64_t)(b * 2 + 1 - side);
-  const int cnt = ovf_count[rs];
-  if (blockIdx.x * 256 >= cnt) return;  // block-uniform
-  const int k = blockIdx.x * 256 + threadIdx.x;
-  const bool live = k < cnt;
-  const int kk = live ? k : blockIdx.x * 256;  // a dead lane shadows a live row of its block
-  const int row = ovf_rows[rs * NM + kk];
-  const int nr = side ? M : N, nt = side ? N : M;
-  const float* X = (side ? Q : P) + ((int64_t)b * nr + row) * 3;
-  const float px = X[0], py = X[1], pz = X[2], np_ = sqnorm3(px, py, pz);
-  const CgGrid g = grids[ts];
-  const float err = 16.0f * kCgU * (np_ + g.nmax) + 1e-30f;
-  const float shrink = 1.0f - 8.0f * kCgU;
-  float best = ovf_best[rs * NM + kk];
-  int bi = ovf_bi[rs * NM + kk];
-  const float4* T = sorted + ts * NM;
-  const int* TI = sidx + ts * NM;
-  const int nrun = (nt + kCgRun - 1) / kCgRun, mrun = (NM + kCgRun - 1) / kCgRun;
-  const float4* BX = boxes + ts * mrun * 2;
-  // a bound on the row's computed minimum before any run is scored: every point of a run lies
-  // within the box's farthest corner, and a computed D exceeds the true squared distance by at
-  // most err (so a row whose rings found nothing still prunes)
-  float thr = best;
-  for (int run = 0; run < nrun; ++run) {
-    const float4 lo = BX[2 * run], hi = BX[2 * run + 1];
-    const float fx = fmaxf(fabsf(px - lo.x), fabsf(px - hi.x)),
-                fy = fmaxf(fabsf(py - lo.y), fabsf(py - hi.y)),
-                fz = fmaxf(fabsf(pz - lo.z), fabsf(pz - hi.z));
-    thr = fminf(thr, (fx * fx + fy * fy + fz * fz) * (1.0f + 16.0f * kCgU) + err);
-  }
-  for (int run = 0; run < nrun; ++run) {
-    const float4 lo = BX[2 * run], hi = BX[2 * run + 1];
-    const float gx = cg_axis_gap(px, lo.x, hi.x), gy = cg_axis_gap(py, lo.y, hi.y),
-                gz = cg_axis_gap(pz, lo.z, hi.z);
-    const bool need = (gx * gx + gy * gy + gz * gz) * shrink - err <= fminf(thr, best);
-    if (!__any(need)) continue;
-    const int k0 = run * kCgRun, k1 = min(k0 + kCgRun, nt);
-    for (int q = k0; q < k1; ++q) {
-      const float4 t = T[q];
-      float v = cd_dist(px, py, pz, np_, t.x, t.y, t.z, t.w);
-      v = v < 0.0f ? 0.0f : v;
-      const int j = TI[q];
-      if (v < best || (v == best && j < bi)) {
-        best = v;
-        bi = j;
-      }
-    }
-  }
-  if (!live) return;
-  if (bi == 0x7fffffff) bi = 0;  // no comparable pair (NaN row): the exhaustive kernel's answer
-  if (side == 0) {
-    min1[(int64_t)b * N + row] = best;
-    arg1[(int64_t)b * N + row] = bi;
-  } else {
-    min2[(int64_t)b * M + row] = best;
-    arg2[(int64_t)b * M + row] = bi;
-  }
-}
-
 struct CgWS {
   CgGrid* grids;
   int* counts;     // [B][2][kCgMaxCells + 1]
@@ -1022,9 +900,6 @@ struct CgWS {
   int* sidx;       // [B][2][NM]
   int* ovf_count;  // [B][2]       hybrid mode: rows over the ring budget
   int* ovf_rows;   // [B][2][NM]
-  float* ovf_best; // [B][2][NM]  the rings' best of each overflow row (pruned search)
-  int* ovf_bi;     // [B][2][NM]
-  float4* boxes;   // [B][2][runs][2] the sorted runs' bounding boxes (pruned search)
   size_t bytes;
 };
 static CgWS carve_cg(void* base, int64_t B, int64_t N, int64_t M) {
@@ -1040,9 +915,6 @@ static CgWS carve_cg(void* base, int64_t B, int64_t N, int64_t M) {
   w.sidx = c.take<int>(B * 2 * NM);
   w.ovf_count = c.take<int>(B * 2);
   w.ovf_rows = c.take<int>(B * 2 * NM);
-  w.ovf_best = c.take<float>(B * 2 * NM);
-  w.ovf_bi = c.take<int>(B * 2 * NM);
-  w.boxes = c.take<float4>(B * 2 * cdiv(NM, kCgRun) * 2);
   w.bytes = c.bytes();
   return w;
 }
@@ -1067,10 +939,6 @@ static inline int64_t cd_padded(int64_t n) { return cdiv(n, kCdChunk) * kCdChunk
 #define PCST_X_CG_RING_BUDGET 2
 #endif
 constexpr int kCgRingBudget = PCST_X_CG_RING_BUDGET;
-#ifndef PCST_X_CG_PRUNE  // 0: the overflow rows by the exhaustive row-min (A/B)
-#define PCST_X_CG_PRUNE 1
-#endif
-constexpr bool kCgPrune = PCST_X_CG_PRUNE != 0;
 // S x R shape of the overflow-list row-min launches (experiment builds may override; r04 a17:
 // 4 x 1 11.31-11.36 ms per trainer step vs 2 x 1 11.42-11.75, 2 x 2 11.72, 1 x 2 12.3-12.45)
 #ifndef PCST_X_CD_LIST_S
@@ -1115,7 +983,7 @@ extern "C" int pcst_chamfer_fwd(const float* pred, const float* target, int64_t 
     PCST_HIP(hipMemsetAsync(w.counts, 0, sizeof(int) * B * 2 * (kCgMaxCells + 1), s), "memset");
     if (hybrid) {
       PCST_HIP(hipMemsetAsync(w.ovf_count, 0, sizeof(int) * B * 2, s), "memset");
-      if (!kCgPrune) pack();  // the exhaustive overflow pass reads the packed pairs
+      pack();
     }
     hipLaunchKernelGGL(cg_stats_kernel, dim3(b, 2), dim3(1024), 0, s, pred, target, (int)N, (int)M,
                        w.grids);
@@ -1127,17 +995,10 @@ extern "C" int pcst_chamfer_fwd(const float* pred, const float* target, int64_t 
     hipLaunchKernelGGL(cg_scan_kernel, tg, dim3(kCgTile), 0, s, w.counts, w.tsum, w.starts);
     hipLaunchKernelGGL(cg_fill_kernel, pg, dim3(256), 0, s, pred, target, (int)N, (int)M, w.starts,
                        w.crank, w.sorted, w.sidx);
-    const bool prune = hybrid && kCgPrune;
     hipLaunchKernelGGL(cg_rowmin_kernel, pg, dim3(256), 0, s, (int)N, (int)M, w.grids, w.starts,
                        w.sorted, w.sidx, min1, arg1, min2, arg2, hybrid ? kCgRingBudget : 0,
-                       w.ovf_count, w.ovf_rows, prune ? w.ovf_best : nullptr, w.ovf_bi);
-    if (prune) {  // the rows over budget, by the box-pruned search (grid over the list's bound)
-      hipLaunchKernelGGL(cg_runbox_kernel, dim3((unsigned)cdiv(cdiv(NM, kCgRun), 4), b, 2), dim3(256),
-                         0, s, (int)N, (int)M, w.sorted, w.boxes);
-      hipLaunchKernelGGL(cg_prune_kernel, pg, dim3(256), 0, s, pred, target, (int)N, (int)M, w.grids,
-                         w.sorted, w.sidx, w.boxes, w.ovf_count, w.ovf_rows, w.ovf_best, w.ovf_bi,
-                         min1, arg1, min2, arg2);
-    } else if (hybrid) {  // the rows over budget, exhaustively (grid over the list's upper bound)
+                       w.ovf_count, w.ovf_rows);
+    if (hybrid) {  // the rows over budget, exhaustively (grid over the list's upper bound)
       constexpr int LS = PCST_X_CD_LIST_S, LR = PCST_X_CD_LIST_R;
       hipLaunchKernelGGL((chamfer_rowmin_kernel<LS, LR, true>), dim3((unsigned)cdiv(N, 256 * LR), b),
                          dim3(256 * LS), 0, s, pred, Tp, (int)N, (int)M, (int)Mp, min1, arg1,
