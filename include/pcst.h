@@ -142,6 +142,11 @@ int pcst_resblock_fwd16(const uint16_t* x, int64_t M, const uint16_t* w1, const 
 int pcst_resblock_bwd16(const uint16_t* dd, int64_t M, const uint16_t* w2t, const uint16_t* w1t,
                         const uint16_t* h, const uint16_t* g, uint64_t seed, float drop_p,
                         uint16_t* dz, uint16_t* g_out, uint16_t* dd_out, int f16, void* stream);
+/* The step's 2-D fp32 weights to the 16-bit format f16 selects, n <= 64 tensors in one launch:
+ * dst[i] = 16-bit(src[i]) [rows, cols] row-major, or its transpose [cols, rows] if transpose[i]
+ * (round to nearest even, as torch's .to(dtype)).  Host arrays of n entries. */
+int pcst_cast16_batch(const float* const* src, uint16_t* const* dst, const int32_t* rows,
+                      const int32_t* cols, const int32_t* transpose, int n, int f16, void* stream);
 int pcst_group_colsum16_workspace_size(int64_t B, int64_t C, size_t* bytes);
 int pcst_group_colsum16(const uint16_t* G, int f16, int64_t B, int64_t N, int64_t C, float* out,
                         void* workspace, void* stream);

@@ -76,6 +76,7 @@ SIGNATURES = {
     "pcst_linear_wgrad_bf16_workspace_size": [_I, _I, _I, _SZ],
     "pcst_linear_wgrad_bf16": [_P, _P, _I, _I, _I, _P, _P, _P, ctypes.c_int, _P],
     "pcst_resblock_fwd16": [_P, _I, _P, _P, _P, _P, ctypes.c_uint64, _F, _P, _P, ctypes.c_int, _P],
+    "pcst_cast16_batch": [_P, _P, _P, _P, _P, ctypes.c_int, ctypes.c_int, _P],
     "pcst_resblock_bwd16": [_P, _I, _P, _P, _P, _P, ctypes.c_uint64, _F, _P, _P, _P, ctypes.c_int, _P],
     "pcst_gemm_ex": [_P, ctypes.c_int, _I, _I, _P, ctypes.c_int, _I, _P, ctypes.c_int,
                      ctypes.c_int, _P, ctypes.c_uint64, _F, _I, _P, _P, ctypes.c_int, _P],
@@ -830,6 +831,34 @@ def resblock_fwd16(x, w1, b1, w2, b2, seed=0, p=0.0):
     return h, out
 
 
+def cast16_batch(tensors, half, transpose=None):
+    """fp32 2-D tensors -> their 16-bit copies in `half` (float16 / bfloat16), each transposed where
+    transpose[i], all in one launch (pcst_cast16_batch; the bits of t.to(half) / t.t().to(half))."""
+    n = len(tensors)
+    if n == 0:
+        return []
+    transpose = list(transpose) if transpose is not None else [False] * n
+    if n > 64 or len(transpose) != n:
+        raise RuntimeError("cast16_batch: at most 64 tensors, one transpose flag each")
+    require_device(*tensors)
+    src = [_f32(t.detach()) for t in tensors]
+    if any(t.dim() != 2 for t in src):
+        raise RuntimeError("cast16_batch: 2-D tensors only")
+    sizes = [t.numel() for t in src]
+    offs = np.cumsum([0] + [(z + 7) // 8 * 8 for z in sizes])  # 16-byte aligned slices
+    flat = torch.empty(int(offs[-1]), dtype=half, device=src[0].device)
+    outs = []
+    for t, o, tr in zip(src, offs, transpose):
+        r, c = t.shape
+        outs.append(flat[int(o):int(o) + r * c].view(c, r) if tr else flat[int(o):int(o) + r * c].view(r, c))
+    P = ctypes.c_void_p * n
+    I32 = ctypes.c_int32 * n
+    _call("pcst_cast16_batch", P(*[t.data_ptr() for t in src]), P(*[o.data_ptr() for o in outs]),
+          I32(*[t.shape[0] for t in src]), I32(*[t.shape[1] for t in src]),
+          I32(*[1 if tr else 0 for tr in transpose]), n, 1 if half == torch.float16 else 0, _stream())
+    return outs
+
+
 def resblock_bwd16(dd, w2t, w1t, h, g, seed=0, p=0.0, dropout_copy=False):
     """The backward products of one residual block in one launch (pcst_resblock_bwd16): dd, g
     [M,256] and h [M,512] 16-bit, w2t = W2^T [512,256] / w1t = W1^T [256,512] 16-bit ->
@@ -1175,7 +1204,7 @@ _GUARDED = ("square_distance", "index_points", "fps", "ball_query", "group_gathe
             "linear_wgrad", "gemm_nt_bf16", "channel_stats", "affine_act", "chamfer_fwd",
             "chamfer_bwd", "l1_fwd", "l1_bwd", "knn_dist", "emd_greedy", "voxel_center_dist",
             "cfg_ddim_step_dcoef", "voxel_downsample_copies_dseed", "bn_train_coeffs",
-            "bn_relu_maxpool", "bn_relu_bwd", "group_gather_bwd", "group_colsum16", "resblock_fwd16", "resblock_bwd16",
+            "bn_relu_maxpool", "bn_relu_bwd", "group_gather_bwd", "group_colsum16", "resblock_fwd16", "resblock_bwd16", "cast16_batch",
             "gemm_ex", "dropout_grad_bf16",
             "linear_wgrad_ex", "knn_workspace", "voxel_copies_workspace")
 for _name in _GUARDED:

@@ -1633,6 +1633,50 @@ __global__ __launch_bounds__(kRbThreads) __attribute__((amdgpu_waves_per_eu(2, 2
   }
 }
 
+// ---- batched weight casts: every 2-D weight of a step to the 16-bit format (optionally
+// transposed) in one launch, instead of one cast (and, transposed, one more copy) per tensor
+struct CastBatch {
+  const float* src[kCastMax];
+  uint16_t* dst[kCastMax];
+  int32_t rows[kCastMax], cols[kCastMax], trans[kCastMax];
+  int n;
+};
+__global__ __launch_bounds__(256) void cast16_batch_kernel(CastBatch cb) {
+  const int m = blockIdx.y;
+  const float* S = cb.src[m];
+  uint16_t* D = cb.dst[m];
+  const int R = cb.rows[m], C = cb.cols[m];
+  const int64_t n = (int64_t)R * C;
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < n; e += (int64_t)gridDim.x * 256) {
+    const h16 v = (h16)S[e];
+    const int64_t o = cb.trans[m] ? (e % C) * R + e / C : e;  // [R,C] -> [C,R]
+    D[o] = __builtin_bit_cast(uint16_t, v);
+  }
+}
+
+int cast16_batch_impl(const float* const* src, uint16_t* const* dst, const int32_t* rows,
+                      const int32_t* cols, const int32_t* trans, int n, void* stream) {
+  PCST_CHECK_ARG(n >= 0 && n <= kCastMax, "cast16_batch: 0..64 tensors");
+  if (n == 0) return PCST_OK;
+  CastBatch cb;
+  int64_t most = 0;
+  for (int i = 0; i < n; ++i) {
+    PCST_CHECK_ARG(rows[i] >= 0 && cols[i] >= 0 && ((src[i] && dst[i]) || (int64_t)rows[i] * cols[i] == 0),
+                   "cast16_batch: bad tensor");
+    cb.src[i] = src[i];
+    cb.dst[i] = dst[i];
+    cb.rows[i] = rows[i];
+    cb.cols[i] = cols[i];
+    cb.trans[i] = trans[i] ? 1 : 0;
+    most = std::max<int64_t>(most, (int64_t)rows[i] * cols[i]);
+  }
+  cb.n = n;
+  const unsigned gx = (unsigned)std::max<int64_t>(1, std::min<int64_t>(cdiv(most, 256), 64));
+  hipLaunchKernelGGL(cast16_batch_kernel, dim3(gx, (unsigned)n), dim3(256), 0, as_stream(stream), cb);
+  PCST_LAUNCH_CHECK("cast16_batch");
+  return PCST_OK;
+}
+
 int resblock_fwd_impl(const uint16_t* x, int64_t M, const uint16_t* w1, const float* b1,
                       const uint16_t* w2, const float* b2, uint64_t seed, float drop_p,
                       uint16_t* h, uint16_t* xo, void* stream) {
@@ -1703,6 +1747,13 @@ extern "C" int pcst_resblock_fwd16(const uint16_t* x, int64_t M, const uint16_t*
                                    uint16_t* h, uint16_t* x_out, int f16, void* stream) {
   return f16 ? pcst::f16m::resblock_fwd_impl(x, M, w1, b1, w2, b2, seed, drop_p, h, x_out, stream)
              : pcst::bf16m::resblock_fwd_impl(x, M, w1, b1, w2, b2, seed, drop_p, h, x_out, stream);
+}
+
+extern "C" int pcst_cast16_batch(const float* const* src, uint16_t* const* dst, const int32_t* rows,
+                                 const int32_t* cols, const int32_t* transpose, int n, int f16,
+                                 void* stream) {
+  return f16 ? pcst::f16m::cast16_batch_impl(src, dst, rows, cols, transpose, n, stream)
+             : pcst::bf16m::cast16_batch_impl(src, dst, rows, cols, transpose, n, stream);
 }
 
 extern "C" int pcst_resblock_bwd16(const uint16_t* dd, int64_t M, const uint16_t* w2t,

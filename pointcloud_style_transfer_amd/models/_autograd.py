@@ -82,6 +82,16 @@ def _h_t(w, half):
     return w.detach().t().to(half).contiguous()
 
 
+BATCH_CAST = True   # one pcst_cast16_batch launch for a layer stack's 16-bit weight copies
+
+
+def _cast_all(ts, half, transpose=False):
+    """`_h` (or `_h_t`) of every tensor of `ts`: one launch when BATCH_CAST, else one each."""
+    if BATCH_CAST:
+        return _hip.cast16_batch(ts, half, [transpose] * len(ts))
+    return [(_h_t if transpose else _h)(t, half) for t in ts]
+
+
 def _draw_seed(p):
     """Dropout seed for one layer call: torch's CPU generator (torch.manual_seed governs it)."""
     return int(torch.randint(0, 2 ** 62, (1,)).item()) if p > 0 else 0
@@ -202,8 +212,12 @@ class NoisePredictorFn(torch.autograd.Function):
         w0p = torch.zeros(w[0].shape[0], 8, dtype=torch.float32, device=dev)
         w0p[:, :3] = w[0].detach()
         half = autocast_half() or torch.bfloat16
-        wb = [_h(t, half) if t.dim() == 2 else t.detach() for t in w[2:]]
-        wb = [_h(w0p, half), w[1].detach()] + wb
+        # every 2-D weight to the 16-bit format in one launch (pcst_cast16_batch)
+        mats = [w0p] + [t for t in w[2:] if t.dim() == 2]
+        cast = iter(_cast_all(mats, half))
+        w0b = next(cast)
+        wb = [next(cast) if t.dim() == 2 else t.detach() for t in w[2:]]
+        wb = [w0b, w[1].detach()] + wb
         h0 = _hip.gemm_ex(xp, wb[0], wb[1], relu=True, epilogue=_hip.EP_BF16)
         h1 = _hip.gemm_ex(h0, wb[2], wb[3], relu=True, epilogue=_hip.EP_BF16)
         r16 = RESIDUAL_16BIT
@@ -257,20 +271,23 @@ class NoisePredictorFn(torch.autograd.Function):
         grads[34], grads[35] = dw[:3].contiguous(), db[:3].contiguous()
         wo4p = torch.zeros(8, w[34].shape[1], dtype=torch.float32, device=dev)
         wo4p[:3] = w[34].detach()
-        dq1 = _hip.gemm_ex(g3, _h_t(wo4p, half), epilogue=_hip.EP_RELU_MASK, aux=q1)
+        # the transposed 16-bit weights of the whole backward in one launch (pcst_cast16_batch)
+        tidx = [32, 30] + [i for k in reversed(range(6)) for i in (6 + 4 * k + 2, 6 + 4 * k)] + [4, 2]
+        tw = dict(zip(["o4"] + tidx, _cast_all([wo4p] + [w[i] for i in tidx], half, True)))
+        dq1 = _hip.gemm_ex(g3, tw["o4"], epilogue=_hip.EP_RELU_MASK, aux=q1)
         grads[32], grads[33] = _hip.linear_wgrad_ex(dq1, q0)
-        dq0 = _hip.gemm_ex(dq1, _h_t(w[32], half), epilogue=_hip.EP_RELU_MASK, aux=q0)
+        dq0 = _hip.gemm_ex(dq1, tw[32], epilogue=_hip.EP_RELU_MASK, aux=q0)
         grads[30], grads[31] = _hip.linear_wgrad_ex(dq0, xb)
         if ctx.r16:
             # g and the last block's dD from one epilogue; each block's EP_ADD16 then emits the
             # next (earlier) block's dD beside its g
-            g, dd = _hip.gemm_ex(dq0, _h_t(w[30], half), epilogue=_hip.EP_BF16, seed=ctx.seeds[5],
+            g, dd = _hip.gemm_ex(dq0, tw[30], epilogue=_hip.EP_BF16, seed=ctx.seeds[5],
                                  p=ctx.ps[5], dropout_copy=True)
             for k in reversed(range(6)):
                 o = 6 + 4 * k
                 xbk, hk = blocks[k]
                 if FUSED_BLOCK_BWD and dd.shape[1] == 256 and hk.shape[1] == 512:
-                    w2t, w1t = _h_t(w[o + 2], half), _h_t(w[o], half)
+                    w2t, w1t = tw[o + 2], tw[o]
                     grads[o + 2], grads[o + 3] = _hip.linear_wgrad_ex(dd, hk)
                     dz, g, dd = _hip.resblock_bwd16(dd, w2t, w1t, hk, g,
                                                     seed=ctx.seeds[k - 1] if k else 0,
@@ -278,21 +295,21 @@ class NoisePredictorFn(torch.autograd.Function):
                                                     dropout_copy=k > 0)
                     grads[o], grads[o + 1] = _hip.linear_wgrad_ex(dz, xbk)
                     continue
-                dz = _hip.gemm_ex(dd, _h_t(w[o + 2], half), epilogue=_hip.EP_RELU_MASK, aux=hk)
+                dz = _hip.gemm_ex(dd, tw[o + 2], epilogue=_hip.EP_RELU_MASK, aux=hk)
                 grads[o + 2], grads[o + 3] = _hip.linear_wgrad_ex(dd, hk)
                 if k:
-                    g, dd = _hip.gemm_ex(dz, _h_t(w[o], half), epilogue=_hip.EP_ADD16, aux=g,
+                    g, dd = _hip.gemm_ex(dz, tw[o], epilogue=_hip.EP_ADD16, aux=g,
                                          seed=ctx.seeds[k - 1], p=ctx.ps[k - 1], dropout_copy=True)
                 else:
-                    g = _hip.gemm_ex(dz, _h_t(w[o], half), epilogue=_hip.EP_ADD16, aux=g)
+                    g = _hip.gemm_ex(dz, tw[o], epilogue=_hip.EP_ADD16, aux=g)
                 grads[o], grads[o + 1] = _hip.linear_wgrad_ex(dz, xbk)
         else:
-            g = _hip.gemm_ex(dq0, _h_t(w[30], half), epilogue=_hip.EP_F32)
+            g = _hip.gemm_ex(dq0, tw[30], epilogue=_hip.EP_F32)
             for k in reversed(range(6)):
                 o = 6 + 4 * k
                 xbk, hk = blocks[k]
                 g, grads[o], grads[o + 1], grads[o + 2], grads[o + 3] = _block_bwd(
-                    g, xbk, hk, _h_t(w[o], half), _h_t(w[o + 2], half), ctx.ps[k], ctx.seeds[k])
+                    g, xbk, hk, tw[o], tw[o + 2], ctx.ps[k], ctx.seeds[k])
         # x = ((pf + tf) + sf): dL/dpf = g, dL/dtf[b] = dL/dsf[b] = sum of g over cloud b's rows
         # per-cloud row sums (pcst_group_colsum16: float accumulation, rounded to g's 16-bit
         # type as autocast's sum; replaces a hipBLASLt batched GEMV, ones [B,1,N] @ g [B,N,256])
@@ -300,9 +317,9 @@ class NoisePredictorFn(torch.autograd.Function):
                 else g.view(B, N, -1).sum(1).float())
         dcond = torch.stack([gsum, gsum], 1)
         grads[4], grads[5] = _hip.linear_wgrad_ex(g, h1)
-        dh1 = _hip.gemm_ex(g, _h_t(w[4], half), epilogue=_hip.EP_RELU_MASK, aux=h1)
+        dh1 = _hip.gemm_ex(g, tw[4], epilogue=_hip.EP_RELU_MASK, aux=h1)
         grads[2], grads[3] = _hip.linear_wgrad_ex(dh1, h0)
-        dh0 = _hip.gemm_ex(dh1, _h_t(w[2], half), epilogue=_hip.EP_RELU_MASK, aux=h0)
+        dh0 = _hip.gemm_ex(dh1, tw[2], epilogue=_hip.EP_RELU_MASK, aux=h0)
         dw0, grads[1] = _hip.linear_wgrad_ex(dh0, xp)
         grads[0] = dw0[:, :3].contiguous()
         return (None, dcond, None, *grads)

@@ -548,3 +548,22 @@ def test_resblock_bwd16_matches_two_gemms(H, M, p, half):
     dz3, g3, none = H.resblock_bwd16(dd, w2t, w1t, h, g)
     assert none is None and torch.equal(dz3, dz_ref)
     assert torch.equal(g3, H.gemm_ex(dz_ref, w1t, epilogue=H.EP_ADD16, aux=g))
+
+
+@pytest.mark.parametrize("half", [torch.float16, torch.bfloat16])
+def test_cast16_batch_matches_per_tensor_casts(H, half):
+    """pcst_cast16_batch (a layer stack's 16-bit weight copies in one launch) gives the bits of
+    t.to(half) and t.t().to(half) for every tensor, ragged shapes included (odd sizes, one row,
+    an empty tensor), with values that round, overflow float16 and underflow to subnormals."""
+    torch.manual_seed(11)
+    shapes = [(512, 256), (256, 512), (8, 128), (3, 5), (1, 7), (0, 4), (259, 33), (128, 3)]
+    ts = [torch.randn(r, c, device="cuda") * 10.0 ** (i - 3) for i, (r, c) in enumerate(shapes)]
+    ts[1][0, :4] = torch.tensor([7e4, -7e4, 1e-8, float("inf")], device="cuda")
+    flags = [i % 2 == 1 for i in range(len(ts))]
+    outs = H.cast16_batch(ts, half, flags)
+    for t, o, tr in zip(ts, outs, flags):
+        ref = (t.t() if tr else t).to(half).contiguous()
+        assert o.dtype == half and o.shape == ref.shape and o.is_contiguous()
+        assert torch.equal(o.view(torch.int16), ref.view(torch.int16))
+    plain = H.cast16_batch(ts[:3], half)
+    assert all(torch.equal(o, t.to(half)) for o, t in zip(plain, ts[:3]))

@@ -46,5 +46,8 @@ def apply():
     if "PCST_FUSED_BLOCK_BWD" in e:
         from pointcloud_style_transfer_amd.models import _autograd
         _autograd.FUSED_BLOCK_BWD = e["PCST_FUSED_BLOCK_BWD"] != "0"
+    if "PCST_BATCH_CAST" in e:
+        from pointcloud_style_transfer_amd.models import _autograd
+        _autograd.BATCH_CAST = e["PCST_BATCH_CAST"] != "0"
     if e.get("PCST_NM_BF16_KERNEL") == "1":
         dm.NoisePredictor.bf16_code = packing.BF16
