@@ -1633,6 +1633,454 @@ __global__ __launch_bounds__(kRbThreads) __attribute__((amdgpu_waves_per_eu(2, 2
   }
 }
 
+// ---- fused residual block, version 2 (PCST_RB_V2=1; bit-identical to the kernel above and to
+// gemm_ex, not yet faster than the kernel above, so not the default -- DESIGN.md §6a): one
+// wave per SIMD, each wave keeping its 64 rows' A operand (x / dD, 64 x 256) in registers for the
+// whole block, so the MFMAs read only weight fragments from LDS (one 1 KiB fragment feeds two
+// MFMAs, against 1.5 fragment reads per MFMA above).  The products run transposed,
+//   h^T [512, rows] = W1 x^T,   x'^T [256, rows] = W2 h^T
+// (A = a weight fragment, B = the rows), so each hidden chunk's accumulators (lane = row, registers
+// = 16 hidden units) become the second product's B operand in registers: v_permlane32_swap moves
+// the accumulator layout (lane half h holds units {4h..4h+3, 8+4h..8+4h+3} of a 16-block) to the
+// operand layout (8h..8h+7), so every output still sums k ascending in steps of 16 with the same
+// products as gemm_ex -- bit-identical, as the kernel above.  Work-group = 4 waves = 256 rows; the
+// weights stream per 32-unit hidden chunk (32 fragments, 32 KiB: W1 rows [32c, +32) x K 256 and
+// W2 rows 0..255 x k [32c, +32)) straight into LDS (global_load_lds from the row-major weights,
+// 16 B per lane), double-buffered, one barrier per chunk.
+#ifndef PCST_RB_V2
+#define PCST_RB_V2 0
+#endif
+#ifndef PCST_X_RB2_EPI_PREFETCH  // the next tile's A rows loaded block by block in the final
+#define PCST_X_RB2_EPI_PREFETCH 0  // epilogue (1) or after it (0)
+#endif
+#ifndef PCST_X_RB2_NOFILL  // timing experiments only: no weight refills (wrong results)
+#define PCST_X_RB2_NOFILL 0
+#endif
+#ifndef PCST_X_RB2_NOHASH  // timing experiments only: no dropout draws (wrong results)
+#define PCST_X_RB2_NOHASH 0
+#endif
+#ifndef PCST_X_RB2_NOSTORE  // timing experiments only: the chunk h / dZ stores left out
+#define PCST_X_RB2_NOSTORE 0
+#endif
+#ifndef PCST_X_RB2_STAMPS  // timing probe builds only: wave 0 of tiles 0 and ntiles / 2 writes
+#define PCST_X_RB2_STAMPS 0  // s_memtime stamps over its first h row (tools/rb_probe.py)
+#endif
+constexpr int kR2Rows = 256;               // rows per work-group tile
+constexpr int kR2Slab = 32 * 1024;         // one hidden chunk's fragments
+constexpr int kR2Keep = 8 * 256 * 4;       // dropout keep bits: [8 output blocks][256 lanes] words
+constexpr int kR2Slabs = 3;                // weight ring: chunk gc + 2 loads while gc runs
+constexpr int kR2Lds = kR2Slabs * kR2Slab + (512 + 256) * 4 + kR2Keep;
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) void lds_void;
+
+// exchange lo's lanes 32..63 with hi's lanes 0..31
+__device__ __forceinline__ void swap_halves(uint32_t& lo, uint32_t& hi) {
+  const auto r = __builtin_amdgcn_permlane32_swap(lo, hi, false, false);
+  lo = r[0];
+  hi = r[1];
+}
+// a 16-block of 16-bit values, 8 per lane: MFMA-output layout (lane half h: {4h..4h+3, 8+4h..})
+// <-> operand layout (lane half h: 8h..8h+7); the same exchange both ways
+__device__ __forceinline__ u32x4 relayout(u32x4 v) {
+  uint32_t a = v[0], b = v[1], c = v[2], d = v[3];
+  swap_halves(a, c);
+  swap_halves(b, d);
+  return u32x4{a, b, c, d};
+}
+__device__ __forceinline__ uint32_t pack16(float lo, float hi) {
+  h16x2 p;
+  p[0] = (h16)lo;
+  p[1] = (h16)hi;
+  return __builtin_bit_cast(uint32_t, p);
+}
+__device__ __forceinline__ h16x8 as_h16x8(u32x4 v) { return __builtin_bit_cast(h16x8, v); }
+__device__ __forceinline__ u32x4 as_u32x4(uint4 v) { return u32x4{v.x, v.y, v.z, v.w}; }
+
+// one group of four fragment reads (asm: invisible to the compiler's LDS-DMA tracking; each
+// group's wait is a counted lgkmcnt tied to its registers, as the dma_read path above)
+template <int G>
+__device__ __forceinline__ void r2_read4(uint32_t a0, h16x8 (&v)[4]) {
+  v[0] = dma_read<(4 * G + 0) * 1024>(a0);
+  v[1] = dma_read<(4 * G + 1) * 1024>(a0);
+  v[2] = dma_read<(4 * G + 2) * 1024>(a0);
+  v[3] = dma_read<(4 * G + 3) * 1024>(a0);
+}
+__device__ __forceinline__ f32x4 r2_read_f4(uint32_t addr) {
+  f32x4 v;
+  asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(addr));
+  return v;
+}
+
+__device__ __forceinline__ h16x8 r2_read_one(uint32_t addr, int off) {
+  h16x8 v;
+  if (__builtin_constant_p(off) && off >= 0 && off < 65536)
+    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(v) : "v"(addr), "i"(off));
+  else
+    asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(addr + off));
+  return v;
+}
+template <int N>
+__device__ __forceinline__ void r2_wait1(h16x8& a) {
+  asm volatile("s_waitcnt lgkmcnt(%1)" : "+v"(a) : "n"(N));
+}
+// LDS-DMA of 16 B per lane (buffer_load_dwordx4 ... lds) in asm: the compiler, which does not
+// see it, then inserts no vmcnt wait for it before barriers (it would drain the chunk-after-next
+// load at every chunk); its completion is covered by the explicit counted waits.  M0 (the LDS
+// destination) is saved and restored around it.
+__device__ __forceinline__ void r2_dma16(rsrc_t r, uint32_t voff, uint32_t soff, uint32_t lds) {
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %4 offen lds\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(voff), "s"(r), "s"(lds), "s"(soff)
+               : "memory");
+}
+__device__ __forceinline__ uint32_t r2_read_u32(uint32_t addr) {
+  uint32_t v;
+  asm volatile("ds_read_b32 %0, %1" : "=v"(v) : "v"(addr));
+  return v;
+}
+__device__ __forceinline__ void r2_write_u32(uint32_t addr, uint32_t v) {
+  asm volatile("ds_write_b32 %0, %1" : : "v"(addr), "v"(v) : "memory");
+}
+
+// Persistent: one work-group per CU walks tiles t = blockIdx.x, + gridDim.x, ...; the weight
+// stream runs on across tiles (every tile reads the same 16 chunks), and the next tile's A rows
+// load into the registers the final epilogue frees, output block by output block.
+template <bool BWD>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void resblock2_kernel(
+    RbArgs a, int ntiles) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float* sb1 = reinterpret_cast<float*>(smem + kR2Slabs * kR2Slab);  // [512]
+  float* sb2 = sb1 + 512;                                             // [256]
+  uint32_t* skeep = reinterpret_cast<uint32_t*>(sb2 + 256);           // [8][256]
+  int t = blockIdx.x;
+  if (t >= ntiles) return;
+  const int G = gridDim.x;
+  const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, l32 = lane & 31;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int64_t M = a.M;
+  const bool drop = !PCST_X_RB2_NOHASH && (BWD ? a.ddo != nullptr : true);  // a dropout draw in the final epilogue
+#if PCST_X_RB2_STAMPS
+  uint64_t stamp[24];
+  stamp[0] = __builtin_amdgcn_s_memtime();
+#define R2_STAMP(i) stamp[i] = __builtin_amdgcn_s_memtime()
+#else
+#define R2_STAMP(i) (void)0
+#endif
+  if (!BWD) {
+    sb1[tid] = a.b1[tid];
+    sb1[256 + tid] = a.b1[256 + tid];
+    sb2[tid] = a.b2[tid];
+  }
+  // chunk c's fragments -> slab: f < 16: W1 rows [32c, +32) k [16f, +16); f = 16 + 2 ob + kk:
+  // W2 rows [32 ob, +32) k [32c + 16kk, +16).  Waves 0, 1 load the W1 half, 2, 3 the W2 half.
+  const rsrc_t rw1 = make_rsrc(a.w1, 512u * 256u * 2u), rw2 = make_rsrc(a.w2, 256u * 512u * 2u);
+  const uint32_t vw = wid < 2 ? (uint32_t)((l32 * 256 + 8 * h) * 2) : (uint32_t)((l32 * 512 + 8 * h) * 2);
+  const rsrc_t rwv = wid < 2 ? rw1 : rw2;
+  const uint32_t lds_slab0 = (uint32_t)(uintptr_t)smem + wid * 8 * 1024;
+  auto fill = [&](int c, int slab) {
+    const uint32_t dst = lds_slab0 + slab * kR2Slab;
+    // wave-uniform: W1 fragment f at (32c * 256 + 16 f) * 2 bytes, W2 fragment (ob, kk) at
+    // (32 ob * 512 + 32c + 16 kk) * 2
+    const int base = wid < 2 ? (32 * c * 256 + 16 * 8 * wid) * 2 : (32 * 4 * (wid - 2) * 512 + 32 * c) * 2;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int so = base + (wid < 2 ? i * 32 : (32 * (i >> 1) * 512 + 16 * (i & 1)) * 2);
+      r2_dma16(rwv, vw, __builtin_amdgcn_readfirstlane(so), __builtin_amdgcn_readfirstlane(dst + i * 1024));
+    }
+  };
+  fill(0, 0);
+  fill(1, 1);
+  // the A rows in operand layout: xb[p][kb] = row r0 + 32p, k [16kb + 8h, +8).  Per-lane byte
+  // offsets of the rows (the columns go into the instructions' offset fields or soffset; rows
+  // past M fail the buffer range check: loads read 0, stores drop)
+  const rsrc_t rx = make_rsrc(a.x, (uint32_t)(M * 256 * 2));
+  int64_t r0 = (int64_t)t * kR2Rows + 64 * wid + l32;  // the lane's row in set 0 (set 1: +32)
+  uint32_t v256 = (uint32_t)((r0 * 256 + 8 * h) * 2);  // set p: + p * 32 * 512 bytes
+  uint32_t v512 = (uint32_t)((r0 * 512 + 8 * h) * 2);  // set p: + p * 32 * 1024 bytes
+  const uint32_t vstep256 = (uint32_t)G * kR2Rows * 256 * 2, vstep512 = (uint32_t)G * kR2Rows * 512 * 2;
+  u32x4 xb[2][16];
+#pragma unroll
+  for (int p = 0; p < 2; ++p)
+#pragma unroll
+    for (int kb = 0; kb < 16; ++kb)
+      xb[p][kb] = as_u32x4(bload16(rx, v256 + p * 16384 + kb * 32, 0));
+  const rsrc_t rh = make_rsrc(a.h, (uint32_t)(M * 512 * 2));
+  const rsrc_t rm = make_rsrc(BWD ? a.hm : nullptr, BWD ? (uint32_t)(M * 512 * 2) : 0u);
+  const rsrc_t ro = make_rsrc(a.xo, (uint32_t)(M * 256 * 2));
+  const rsrc_t rg = make_rsrc(BWD ? a.g : nullptr, BWD ? (uint32_t)(M * 256 * 2) : 0u);
+  const rsrc_t rd = make_rsrc(BWD ? a.ddo : nullptr, BWD && a.ddo ? (uint32_t)(M * 256 * 2) : 0u);
+  u32x4 mk[2][2];  // backward: the next chunk's mask rows (h), operand layout
+  if (BWD) {
+#pragma unroll
+    for (int p = 0; p < 2; ++p)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+        mk[p][kk] = as_u32x4(bload16(rm, v512 + p * 32768 + kk * 32, 0));
+  }
+  const uint32_t lds0 = (uint32_t)(uintptr_t)smem + lane * 16;
+  const uint32_t lb1 = (uint32_t)(uintptr_t)sb1 + 16 * h;  // + 4 (32c + 8q) bytes
+  const uint32_t lb2 = (uint32_t)(uintptr_t)sb2 + 16 * h;  // + 4 (32ob + 8q) bytes
+  const uint32_t lkeep = (uint32_t)(uintptr_t)skeep + 4 * tid;  // + 1024 ob bytes
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();  // slab 0 and the biases landed
+  R2_STAMP(1);
+  int gc = 0;  // chunks done by this work-group
+  int slab0 = 0, slab2 = 2;  // the running chunk's slab, the slab chunk gc + 2 loads into
+#pragma unroll 1
+  for (;;) {
+    const bool more = __builtin_amdgcn_readfirstlane(t + G < ntiles ? 1 : 0) != 0;  // another tile follows
+    f32x16 acc2[8][2];
+#pragma unroll
+    for (int ob = 0; ob < 8; ++ob)
+#pragma unroll
+      for (int p = 0; p < 2; ++p) acc2[ob][p] = f32x16{};
+    uint32_t keep2 = 0;  // the final epilogue's dropout draws, made in the loop's MFMA shadow
+#pragma unroll 1
+    for (int c = 0; c < 16; ++c, ++gc) {
+      const uint32_t a0 = lds0 + slab0 * kR2Slab;
+      uint32_t mbits = 0;  // backward: bit 16p + r = [h > 0] of accumulator element (p, r)
+      if (BWD) {
+#pragma unroll
+        for (int p = 0; p < 2; ++p)
+#pragma unroll
+          for (int kk = 0; kk < 2; ++kk) {
+            const u32x4 v = relayout(mk[p][kk]);
+#pragma unroll
+            for (int d = 0; d < 4; ++d) {
+              const int r = 8 * kk + 2 * d;
+              mbits |= (uint32_t)((int16_t)(v[d] & 0xffffu) > 0) << (16 * p + r);
+              mbits |= (uint32_t)((int16_t)(v[d] >> 16) > 0) << (16 * p + r + 1);
+            }
+          }
+      }
+      // backward: the next chunk's mask rows (this tile's c + 1, or the next tile's chunk 0)
+      if (BWD && (c + 1 < 16 || more)) {
+        const uint32_t vn = c + 1 < 16 ? v512 : v512 + vstep512;
+#pragma unroll
+        for (int p = 0; p < 2; ++p)
+#pragma unroll
+          for (int kk = 0; kk < 2; ++kk)
+            mk[p][kk] = as_u32x4(bload16(rm, vn + p * 32768 + kk * 32, (uint32_t)(64 * ((c + 1) & 15))));
+      }
+      // the chunk after next (this tile's c + 2 or the next tile's: the same weights) into the
+      // slab chunk gc - 1 used
+      const bool fill2 = c + 2 < 16 || more;
+      if (fill2 && !PCST_X_RB2_NOFILL) fill((c + 2) & 15, slab2);
+      // the chunk's 32 fragments in order: f < 16 the first product (acc1[p] += W1[32c.., 16f..]
+      // x^T, k ascending), f >= 16 the second (acc2[ob][p] += W2[32ob.., 32c + 16kk ..] h^T, f =
+      // 16 + 2 ob + kk); a ring of four reads in flight, the wait for fragment f counted over the
+      // reads issued after it (and the forward's bias reads, issued between fragments 15 and 16)
+      h16x8 fr[4];
+      fr[0] = dma_read<0>(a0);
+      fr[1] = dma_read<1024>(a0);
+      fr[2] = dma_read<2048>(a0);
+      fr[3] = dma_read<3072>(a0);
+      f32x16 acc1[2] = {f32x16{}, f32x16{}};
+      f32x4 bq[4];
+      u32x4 hb[2][2];
+      const uint32_t e0 = (uint32_t)((r0 + 32 * (c & 1)) * 256 + 32 * (c >> 1) + 4 * h);
+      if (!(c & 1)) keep2 = 0;
+#pragma unroll
+      for (int f = 0; f < 32; ++f) {
+        if (f == 16) {
+#if PCST_X_RB2_STAMPS
+          if (c == 9 && gc < 16) R2_STAMP(7);
+#endif
+          // epilogue: forward h = 16-bit(relu(acc1 + b1)), backward dZ = 16-bit((acc1 + 0)
+          // [h > 0]); to the second product's operand layout and out to global (16 B per lane)
+          if (!BWD) asm volatile("s_waitcnt lgkmcnt(4)" : "+v"(bq[0]), "+v"(bq[1]), "+v"(bq[2]), "+v"(bq[3]));
+#pragma unroll
+          for (int p = 0; p < 2; ++p) {
+            float v[16];
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+              v[r] = acc1[p][r] + (BWD ? 0.0f : bq[r >> 2][r & 3]);
+              if (BWD) v[r] = (mbits >> (16 * p + r)) & 1u ? v[r] : 0.0f;
+              else v[r] = fmaxf(v[r], 0.0f);
+            }
+#pragma unroll
+            for (int kk = 0; kk < 2; ++kk) {
+              const u32x4 o = {pack16(v[8 * kk + 0], v[8 * kk + 1]), pack16(v[8 * kk + 2], v[8 * kk + 3]),
+                               pack16(v[8 * kk + 4], v[8 * kk + 5]), pack16(v[8 * kk + 6], v[8 * kk + 7])};
+              hb[p][kk] = relayout(o);
+              if (!PCST_X_RB2_NOSTORE)
+                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i32, hb[p][kk]), rh,
+                                                       (int)(v512 + p * 32768 + kk * 32), 64 * c, 0);
+            }
+          }
+#if PCST_X_RB2_STAMPS
+          if (c == 9 && gc < 16) R2_STAMP(8);
+#endif
+        }
+        const int younger = (31 - f < 3 ? 31 - f : 3) + (!BWD && f >= 12 && f < 16 ? 4 : 0);
+        if (younger == 7) r2_wait1<7>(fr[f & 3]);
+        else if (younger == 3) r2_wait1<3>(fr[f & 3]);
+        else if (younger == 2) r2_wait1<2>(fr[f & 3]);
+        else if (younger == 1) r2_wait1<1>(fr[f & 3]);
+        else r2_wait1<0>(fr[f & 3]);
+        if (f < 16) {
+#pragma unroll
+          for (int p = 0; p < 2; ++p) acc1[p] = mfma32_h16(fr[f & 3], as_h16x8(xb[p][f]), acc1[p]);
+        } else {
+          const int ob = (f - 16) >> 1, kk = f & 1;
+#pragma unroll
+          for (int p = 0; p < 2; ++p) acc2[ob][p] = mfma32_h16(fr[f & 3], as_h16x8(hb[p][kk]), acc2[ob][p]);
+          // the final epilogue's dropout draw for output block c / 2, row set c % 2, element
+          // r = f - 16 (no data dependence: it fills the MFMA shadow): bit 16 (c & 1) + r
+          if (drop) {
+            const int r = f - 16;
+            keep2 |= (uint32_t)(drop_hash(a.seed_lo, a.seed_hi, (uint64_t)(e0 + (r & 3) + 8 * (r >> 2))) >= a.thr)
+                     << (16 * (c & 1) + r);
+          }
+        }
+        // the MFMAs of fragment f stay ahead of the next read and wait (asm statements keep
+        // their order; without this the scheduler sinks MFMAs below later waits)
+        __builtin_amdgcn_sched_barrier(0);
+        if (f + 4 < 32) fr[f & 3] = r2_read_one(a0, (f + 4) * 1024);
+        if (!BWD && f == 11) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) bq[q] = r2_read_f4(lb1 + 4 * (32 * c + 8 * q));
+        }
+      }
+#if PCST_X_RB2_STAMPS
+      if (c == 9 && gc < 16) R2_STAMP(9);
+#endif
+      if (drop && (c & 1)) r2_write_u32(lkeep + 1024 * (c >> 1), keep2);
+      // this wave's DMA of the next chunk (issued a chunk ago) and backward its mask rows landed;
+      // the chunk-after-next DMA (8) and this chunk's h stores (4) may still be in flight
+      if (fill2) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+#if PCST_X_RB2_STAMPS
+      if (c == 9 && gc < 16) R2_STAMP(10);
+#endif
+      __syncthreads();  // every wave's DMA of chunk gc + 1 landed; every wave is done with slab0
+      slab0 = slab0 == kR2Slabs - 1 ? 0 : slab0 + 1;
+      slab2 = slab2 == kR2Slabs - 1 ? 0 : slab2 + 1;
+#if PCST_X_RB2_STAMPS
+      if (gc == 0) R2_STAMP(2);
+      if (gc == 1) R2_STAMP(3);
+      if (gc == 7) R2_STAMP(4);
+      if (gc == 15) R2_STAMP(5);
+      if (gc == 9) R2_STAMP(11);
+      if (gc == 8) R2_STAMP(12);
+#endif
+    }
+    // final epilogue: forward x' = 16-bit(x + Dropout(acc2 + b2)); backward g' = 16-bit((acc2 +
+    // 0) + g) and the dropout copy dD' = 16-bit(g' keep / (1 - p)); 16 B stores in operand
+    // layout.  Output block ob frees xb[.][2ob, 2ob + 1], which then takes the next tile's rows.
+    u32x4 gres[2][2][2];  // backward: the residual gradient of blocks ob, ob + 1 (ring of two)
+    if (BWD) {
+#pragma unroll
+      for (int p = 0; p < 2; ++p)
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk)
+          gres[0][p][kk] = as_u32x4(bload16(rg, v256 + p * 16384 + kk * 32, 0));
+    }
+#pragma unroll
+    for (int ob = 0; ob < 8; ++ob) {
+      if (BWD && ob + 1 < 8) {
+#pragma unroll
+        for (int p = 0; p < 2; ++p)
+#pragma unroll
+          for (int kk = 0; kk < 2; ++kk)
+            gres[(ob + 1) & 1][p][kk] = as_u32x4(bload16(rg, v256 + p * 16384 + (ob + 1) * 64 + kk * 32, 0));
+      }
+      // LDS addresses recomputed per block (opaque bases): hoisted out of the tile loop they
+      // would be 40 loop-invariant registers
+      uint32_t lb2o = lb2, lko = lkeep;
+      asm volatile("" : "+v"(lb2o), "+v"(lko));
+      f32x4 bq[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) bq[q] = BWD ? f32x4{0.f, 0.f, 0.f, 0.f} : r2_read_f4(lb2o + 4 * (32 * ob + 8 * q));
+      uint32_t kw = drop ? r2_read_u32(lko + 1024 * ob) : 0u;
+      asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(bq[0]), "+v"(bq[1]), "+v"(bq[2]), "+v"(bq[3]), "+v"(kw));
+#pragma unroll
+      for (int p = 0; p < 2; ++p) {
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) {
+          // one 8-element piece at a time: no accumulator read hoisted ahead of its piece (the
+          // scheduler would otherwise read a whole block's accumulators out at once)
+          __builtin_amdgcn_sched_barrier(0);
+          // x (forward) / g (backward) in the accumulator layout
+          const u32x4 res = relayout(BWD ? gres[ob & 1][p][kk] : xb[p][2 * ob + kk]);
+          uint32_t o[4], od[4];
+#pragma unroll
+          for (int d = 0; d < 4; ++d) {
+            float y2[2];
+#pragma unroll
+            for (int s2 = 0; s2 < 2; ++s2) {
+              const int r = 8 * kk + 2 * d + s2;
+              float y = acc2[ob][p][r] + bq[r >> 2][r & 3];
+              if (!BWD) y = (kw >> (16 * p + r)) & 1u ? y * a.scale : 0.0f;
+              y += h16_to_f32((res[d] >> (16 * s2)) & 0xffffu);
+              y2[s2] = y;
+            }
+            o[d] = pack16(y2[0], y2[1]);
+            if (BWD) {
+              float dv[2];
+#pragma unroll
+              for (int s2 = 0; s2 < 2; ++s2) {
+                const int r = 8 * kk + 2 * d + s2;
+                const float yr = h16_to_f32((o[d] >> (16 * s2)) & 0xffffu);
+                dv[s2] = (kw >> (16 * p + r)) & 1u ? yr * a.scale : 0.0f;
+              }
+              od[d] = pack16(dv[0], dv[1]);
+            }
+          }
+          const int off = (int)(v256 + p * 16384 + ob * 64 + kk * 32);
+          const u32x4 on = relayout(u32x4{o[0], o[1], o[2], o[3]});
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i32, on), ro, off, 0, 0);
+          if (BWD && drop) {
+            const u32x4 dn = relayout(u32x4{od[0], od[1], od[2], od[3]});
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i32, dn), rd, off, 0, 0);
+          }
+        }
+      }
+#if PCST_X_RB2_EPI_PREFETCH
+      // not above this block's stores: the residual registers are free only after them
+      asm volatile("" ::: "memory");
+      if (more) {  // the next tile's A rows, k [32 ob, +32)
+#pragma unroll
+        for (int p = 0; p < 2; ++p)
+#pragma unroll
+          for (int kk = 0; kk < 2; ++kk)
+            xb[p][2 * ob + kk] = as_u32x4(bload16(rx, v256 + vstep256 + p * 16384 + ob * 64 + kk * 32, 0));
+      }
+#endif
+    }
+#if !PCST_X_RB2_EPI_PREFETCH
+    if (more) {  // the next tile's A rows
+#pragma unroll
+      for (int p = 0; p < 2; ++p)
+#pragma unroll
+        for (int kb = 0; kb < 16; ++kb)
+          xb[p][kb] = as_u32x4(bload16(rx, v256 + vstep256 + p * 16384 + kb * 32, 0));
+    }
+#endif
+#if PCST_X_RB2_STAMPS
+    if (gc == 16) R2_STAMP(13);
+#endif
+    if (!more) break;
+    t += G;
+    r0 += (int64_t)G * kR2Rows;
+    v256 += vstep256;
+    v512 += vstep512;
+  }
+#if PCST_X_RB2_STAMPS
+  R2_STAMP(6);
+  if (wid == 0 && lane == 0) {
+    uint64_t* o = reinterpret_cast<uint64_t*>(a.h + (int64_t)blockIdx.x * kR2Rows * 512);
+#pragma unroll
+    for (int i = 0; i < 7; ++i) o[i] = stamp[i];
+    o[7] = (uint64_t)blockIdx.x;
+#pragma unroll
+    for (int i = 7; i < 14; ++i) o[i + 1] = stamp[i];
+  }
+#endif
+}
+
 // ---- batched weight casts: every 2-D weight of a step to the 16-bit format (optionally
 // transposed) in one launch, instead of one cast (and, transposed, one more copy) per tensor
 struct CastBatch {
@@ -1677,6 +2125,18 @@ int cast16_batch_impl(const float* const* src, uint16_t* const* dst, const int32
   return PCST_OK;
 }
 
+// persistent grid of the fused residual-block kernel: one work-group per CU of the current device
+static int r2_grid() {
+  static int cus[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  if (!cus[dev]) {
+    int n = 0;
+    cus[dev] = hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n > 0 ? n : 256;
+  }
+  return cus[dev];
+}
+
 int resblock_fwd_impl(const uint16_t* x, int64_t M, const uint16_t* w1, const float* b1,
                       const uint16_t* w2, const float* b2, uint64_t seed, float drop_p,
                       uint16_t* h, uint16_t* xo, void* stream) {
@@ -1693,10 +2153,16 @@ int resblock_fwd_impl(const uint16_t* x, int64_t M, const uint16_t* w1, const fl
   a.seed_hi = (uint32_t)(seed >> 32);
   a.thr = drop_threshold(drop_p);
   a.scale = 1.0f / (1.0f - drop_p);
-  const int ntiles = (int)cdiv(M, kRbRows), per = (int)cdiv(ntiles, 8);
   a.hm = nullptr; a.g = nullptr; a.ddo = nullptr;
-  hipLaunchKernelGGL(resblock_kernel<false>, dim3((unsigned)(8 * per)), dim3(kRbThreads), kRbLds,
-                     as_stream(stream), a, per, ntiles);
+  if (PCST_RB_V2) {
+    const int ntiles = (int)cdiv(M, kR2Rows);
+    hipLaunchKernelGGL(resblock2_kernel<false>, dim3((unsigned)std::min(ntiles, r2_grid())), dim3(256),
+                       kR2Lds, as_stream(stream), a, ntiles);
+  } else {
+    const int ntiles = (int)cdiv(M, kRbRows), per = (int)cdiv(ntiles, 8);
+    hipLaunchKernelGGL(resblock_kernel<false>, dim3((unsigned)(8 * per)), dim3(kRbThreads), kRbLds,
+                       as_stream(stream), a, per, ntiles);
+  }
   PCST_LAUNCH_CHECK("resblock_fwd");
   return PCST_OK;
 }
@@ -1719,9 +2185,15 @@ int resblock_bwd_impl(const uint16_t* dd, int64_t M, const uint16_t* w2t, const 
   a.seed_hi = (uint32_t)(seed >> 32);
   a.thr = drop_threshold(drop_p);
   a.scale = 1.0f / (1.0f - drop_p);
-  const int ntiles = (int)cdiv(M, kRbRows), per = (int)cdiv(ntiles, 8);
-  hipLaunchKernelGGL(resblock_kernel<true>, dim3((unsigned)(8 * per)), dim3(kRbThreads), kRbLds,
-                     as_stream(stream), a, per, ntiles);
+  if (PCST_RB_V2) {
+    const int ntiles = (int)cdiv(M, kR2Rows);
+    hipLaunchKernelGGL(resblock2_kernel<true>, dim3((unsigned)std::min(ntiles, r2_grid())), dim3(256),
+                       kR2Lds, as_stream(stream), a, ntiles);
+  } else {
+    const int ntiles = (int)cdiv(M, kRbRows), per = (int)cdiv(ntiles, 8);
+    hipLaunchKernelGGL(resblock_kernel<true>, dim3((unsigned)(8 * per)), dim3(kRbThreads), kRbLds,
+                       as_stream(stream), a, per, ntiles);
+  }
   PCST_LAUNCH_CHECK("resblock_bwd");
   return PCST_OK;
 }
