@@ -1633,8 +1633,9 @@ __global__ __launch_bounds__(kRbThreads) __attribute__((amdgpu_waves_per_eu(2, 2
   }
 }
 
-// ---- fused residual block, version 2 (PCST_RB_V2=1; bit-identical to the kernel above and to
-// gemm_ex, not yet faster than the kernel above, so not the default -- DESIGN.md §6a): one
+// ---- fused residual block, version 2 (the forward's default, PCST_RB_V2_FWD; the backward's with
+// PCST_RB_V2_BWD=1, slower there -- DESIGN.md §6a; bit-identical to the kernel above and to
+// gemm_ex): one
 // wave per SIMD, each wave keeping its 64 rows' A operand (x / dD, 64 x 256) in registers for the
 // whole block, so the MFMAs read only weight fragments from LDS (one 1 KiB fragment feeds two
 // MFMAs, against 1.5 fragment reads per MFMA above).  The products run transposed,
@@ -1647,8 +1648,14 @@ __global__ __launch_bounds__(kRbThreads) __attribute__((amdgpu_waves_per_eu(2, 2
 // weights stream per 32-unit hidden chunk (32 fragments, 32 KiB: W1 rows [32c, +32) x K 256 and
 // W2 rows 0..255 x k [32c, +32)) straight into LDS (global_load_lds from the row-major weights,
 // 16 B per lane), double-buffered, one barrier per chunk.
-#ifndef PCST_RB_V2
+#ifndef PCST_RB_V2  // 1: both directions on version 2 (experiment builds)
 #define PCST_RB_V2 0
+#endif
+#ifndef PCST_RB_V2_FWD  // the forward on version 2: 245 vs 274 us at M = 245760 (a31)
+#define PCST_RB_V2_FWD 1
+#endif
+#ifndef PCST_RB_V2_BWD  // the backward stays on the kernel above: 385 vs 337 us (HBM-write bound)
+#define PCST_RB_V2_BWD PCST_RB_V2
 #endif
 #ifndef PCST_X_RB2_EPI_PREFETCH  // the next tile's A rows loaded block by block in the final
 #define PCST_X_RB2_EPI_PREFETCH 0  // epilogue (1) or after it (0)
@@ -1735,6 +1742,14 @@ __device__ __forceinline__ void r2_dma16(rsrc_t r, uint32_t voff, uint32_t soff,
                : "v"(voff), "s"(r), "s"(lds), "s"(soff)
                : "memory");
 }
+// 16-byte buffer load in asm (the backward's mask rows): the compiler does not track it, so it
+// inserts no wait for it (its own would also drain the weight DMA behind it); the chunk-end wait
+// covers it, tied to these registers
+__device__ __forceinline__ u32x4 r2_load16(rsrc_t r, uint32_t voff, uint32_t soff) {
+  u32x4 v;
+  asm volatile("buffer_load_dwordx4 %0, %1, %2, %3 offen" : "=v"(v) : "v"(voff), "s"(r), "s"(soff) : "memory");
+  return v;
+}
 __device__ __forceinline__ uint32_t r2_read_u32(uint32_t addr) {
   uint32_t v;
   asm volatile("ds_read_b32 %0, %1" : "=v"(v) : "v"(addr));
@@ -1760,7 +1775,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, l32 = lane & 31;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int64_t M = a.M;
-  const bool drop = !PCST_X_RB2_NOHASH && (BWD ? a.ddo != nullptr : true);  // a dropout draw in the final epilogue
+  // the dropout draws are made in the loop whether or not the backward writes its dropout copy:
+  // a run-time condition there would cut the loop body into blocks the scheduler cannot
+  // interleave with the MFMAs (measured: the backward 88 us slower with it)
+  const bool drop = !PCST_X_RB2_NOHASH;
+  const bool ddo = BWD && a.ddo != nullptr;  // backward: the dropout copy is written
 #if PCST_X_RB2_STAMPS
   uint64_t stamp[24];
   stamp[0] = __builtin_amdgcn_s_memtime();
@@ -1862,7 +1881,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         for (int p = 0; p < 2; ++p)
 #pragma unroll
           for (int kk = 0; kk < 2; ++kk)
-            mk[p][kk] = as_u32x4(bload16(rm, vn + p * 32768 + kk * 32, (uint32_t)(64 * ((c + 1) & 15))));
+            mk[p][kk] = r2_load16(rm, vn + p * 32768 + kk * 32,
+                                  __builtin_amdgcn_readfirstlane((uint32_t)(64 * ((c + 1) & 15))));
       }
       // the chunk after next (this tile's c + 2 or the next tile's: the same weights) into the
       // slab chunk gc - 1 used
@@ -1950,8 +1970,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       if (drop && (c & 1)) r2_write_u32(lkeep + 1024 * (c >> 1), keep2);
       // this wave's DMA of the next chunk (issued a chunk ago) and backward its mask rows landed;
       // the chunk-after-next DMA (8) and this chunk's h stores (4) may still be in flight
-      if (fill2) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      if (BWD) {  // tied to the mask registers it guards
+        if (fill2)
+          asm volatile("s_waitcnt vmcnt(12)" : "+v"(mk[0][0]), "+v"(mk[0][1]), "+v"(mk[1][0]), "+v"(mk[1][1]) : : "memory");
+        else
+          asm volatile("s_waitcnt vmcnt(4)" : "+v"(mk[0][0]), "+v"(mk[0][1]), "+v"(mk[1][0]), "+v"(mk[1][1]) : : "memory");
+      } else {
+        if (fill2) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      }
 #if PCST_X_RB2_STAMPS
       if (c == 9 && gc < 16) R2_STAMP(10);
 #endif
@@ -2032,7 +2059,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
           const int off = (int)(v256 + p * 16384 + ob * 64 + kk * 32);
           const u32x4 on = relayout(u32x4{o[0], o[1], o[2], o[3]});
           __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i32, on), ro, off, 0, 0);
-          if (BWD && drop) {
+          if (ddo) {
             const u32x4 dn = relayout(u32x4{od[0], od[1], od[2], od[3]});
             __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i32, dn), rd, off, 0, 0);
           }
@@ -2154,7 +2181,7 @@ int resblock_fwd_impl(const uint16_t* x, int64_t M, const uint16_t* w1, const fl
   a.thr = drop_threshold(drop_p);
   a.scale = 1.0f / (1.0f - drop_p);
   a.hm = nullptr; a.g = nullptr; a.ddo = nullptr;
-  if (PCST_RB_V2) {
+  if (PCST_RB_V2_FWD) {
     const int ntiles = (int)cdiv(M, kR2Rows);
     hipLaunchKernelGGL(resblock2_kernel<false>, dim3((unsigned)std::min(ntiles, r2_grid())), dim3(256),
                        kR2Lds, as_stream(stream), a, ntiles);
@@ -2185,7 +2212,7 @@ int resblock_bwd_impl(const uint16_t* dd, int64_t M, const uint16_t* w2t, const 
   a.seed_hi = (uint32_t)(seed >> 32);
   a.thr = drop_threshold(drop_p);
   a.scale = 1.0f / (1.0f - drop_p);
-  if (PCST_RB_V2) {
+  if (PCST_RB_V2_BWD) {
     const int ntiles = (int)cdiv(M, kR2Rows);
     hipLaunchKernelGGL(resblock2_kernel<true>, dim3((unsigned)std::min(ntiles, r2_grid())), dim3(256),
                        kR2Lds, as_stream(stream), a, ntiles);

@@ -77,7 +77,7 @@ for st in "$@"; do
       timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/tprof" -o run -- \
           python tools/bench_train.py --steps 4 --warmup 2 > "$OUT/tprof.json" 2> "$OUT/tprof.err"
       rc=$?; echo "trainprof rc=$rc"; if [ $rc -ne 0 ]; then tail -5 "$OUT/tprof.err"; exit $rc; fi
-      python tools/kstats.py "$OUT/tprof/run_kernel_stats.csv" 40 | tee "$OUT/train_kernel_top.txt" ;;
+      python tools/kstats.py "$OUT/tprof/run_kernel_stats.csv" 40 | tee "$OUT/train_kernel_top.txt"; python tools/kstats.py "$OUT/tprof/run_kernel_stats.csv" 400 > "$OUT/train_kernel_all.txt" ;;
     split=*)
       # split=G: the 32-cloud step as G concurrent groups (tools/split_probe.py)
       timeout -k 10 500 python tools/split_probe.py --clouds 32 --groups ${st#split=} > "$OUT/split.json" 2> "$OUT/split.err"
