@@ -2153,15 +2153,11 @@ int cast16_batch_impl(const float* const* src, uint16_t* const* dst, const int32
 }
 
 // persistent grid of the fused residual-block kernel: one work-group per CU of the current device
+// (queried per call: the library keeps no process-global state)
 static int r2_grid() {
-  static int cus[64] = {0};
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
-  if (!cus[dev]) {
-    int n = 0;
-    cus[dev] = hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n > 0 ? n : 256;
-  }
-  return cus[dev];
+  int dev = 0, n = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 256;
+  return hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n > 0 ? n : 256;
 }
 
 int resblock_fwd_impl(const uint16_t* x, int64_t M, const uint16_t* w1, const float* b1,
