@@ -107,6 +107,14 @@ int pcst_bn_train_coeffs(const double* mean, const double* var, int64_t M, int64
                          const float* gamma, const float* beta, double eps, double momentum,
                          float* running_mean, float* running_var, float* scale, float* shift,
                          double* invstd, void* stream);
+/* pcst_channel_stats followed by pcst_bn_train_coeffs in two launches instead of three (the
+ * statistics' combine and the coefficients in one kernel), the same bits: mean / var (float64),
+ * scale / shift / invstd and the running-stat update.  workspace:
+ * pcst_channel_stats_workspace_size() bytes.  (Round 4.) */
+int pcst_bn_train_stats(const float* Z, int64_t M, int64_t O, const float* gamma,
+                        const float* beta, double eps, double momentum, float* running_mean,
+                        float* running_var, double* mean, double* var, float* scale, float* shift,
+                        double* invstd, void* workspace, void* stream);
 int pcst_bn_relu_maxpool(const float* Z, int64_t M, int64_t O, const float* scale,
                          const float* shift, int64_t ns, float* Y, int32_t* arg, void* stream);
 int pcst_bn_relu_bwd_workspace_size(int64_t O, size_t* bytes);

@@ -95,6 +95,7 @@ SIGNATURES = {
     "pcst_chamfer_bwd_workspace_size": [_I, _I, _I, _SZ],
     "pcst_chamfer_bwd": [_P, _P, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P],
     "pcst_bn_train_coeffs": [_P, _P, _I, _I, _P, _P, _D, _D, _P, _P, _P, _P, _P, _P],
+    "pcst_bn_train_stats": [_P, _I, _I, _P, _P, _D, _D, _P, _P, _P, _P, _P, _P, _P, _P, _P],
     "pcst_bn_relu_maxpool": [_P, _I, _I, _P, _P, _I, _P, _P, _P],
     "pcst_bn_relu_bwd_workspace_size": [_I, _SZ],
     "pcst_bn_relu_bwd": [_P, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _I, _P, _P, _P, _P, _P],
@@ -1008,6 +1009,30 @@ def bn_train_coeffs(mean, var, M, gamma, beta, eps, momentum, running_mean=None,
     return scale, shift, invstd
 
 
+def bn_train_stats(Z, gamma, beta, eps, momentum, running_mean=None, running_var=None):
+    """channel_stats then bn_train_coeffs in two launches (pcst_bn_train_stats, the same bits):
+    -> (mean f64 [O], var f64 [O], scale f32 [O], shift f32 [O], invstd f64 [O]); running stats
+    updated in place."""
+    require_device(Z, gamma, beta)
+    Z = _f32(Z)
+    M, O = Z.shape
+    gamma, beta = _f32(gamma), _f32(beta)
+    for t in (running_mean, running_var):
+        if t is not None and (t.dtype != torch.float32 or not t.is_contiguous()):
+            raise RuntimeError("bn_train_stats: running stats must be contiguous fp32")
+    ws = _workspace("pcst_channel_stats_workspace_size", O, device=Z.device)
+    dev = Z.device
+    mean = torch.empty(O, dtype=torch.float64, device=dev)
+    var = torch.empty(O, dtype=torch.float64, device=dev)
+    scale = torch.empty(O, dtype=torch.float32, device=dev)
+    shift = torch.empty_like(scale)
+    invstd = torch.empty(O, dtype=torch.float64, device=dev)
+    _call("pcst_bn_train_stats", _ptr(Z), M, O, _ptr(gamma), _ptr(beta), float(eps), float(momentum),
+          _ptr(running_mean), _ptr(running_var), _ptr(mean), _ptr(var), _ptr(scale), _ptr(shift),
+          _ptr(invstd), _ptr(ws), _stream())
+    return mean, var, scale, shift, invstd
+
+
 def bn_relu_maxpool(Z, scale, shift, ns):
     """-> (pooled [M/ns, O], arg int32 [M/ns, O]) of relu(scale*Z + shift)."""
     require_device(Z, scale, shift)
@@ -1201,7 +1226,7 @@ _GUARDED = ("square_distance", "index_points", "fps", "ball_query", "group_gathe
             "voxel_downsample", "voxel_stats", "knn3_build", "knn3_query", "knn3_interp",
             "knn3_search", "knn3_finish", "knn3_finish_cfg_ddim",
             "noise_cond", "noise_mlp", "cfg_ddim_step", "cfg_ddim_voxel_prep", "pointwise_linear", "relu_bwd",
-            "linear_wgrad", "gemm_nt_bf16", "channel_stats", "affine_act", "chamfer_fwd",
+            "linear_wgrad", "gemm_nt_bf16", "channel_stats", "bn_train_stats", "affine_act", "chamfer_fwd",
             "chamfer_bwd", "l1_fwd", "l1_bwd", "knn_dist", "emd_greedy", "voxel_center_dist",
             "cfg_ddim_step_dcoef", "voxel_downsample_copies_dseed", "bn_train_coeffs",
             "bn_relu_maxpool", "bn_relu_bwd", "group_gather_bwd", "group_colsum16", "resblock_fwd16", "resblock_bwd16", "cast16_batch",

@@ -176,6 +176,40 @@ __global__ __launch_bounds__(256) void channel_combine_kernel(const double* __re
   }
 }
 
+// channel_combine_kernel followed by sa_train.hip's bn_coeffs_kernel in one launch (the
+// BatchNorm forward's statistics, affine coefficients and running-stat update): the same
+// operations, fp contraction off as in that file, so the same bits
+__global__ __launch_bounds__(256) void bn_stats_coeffs_kernel(
+    const double* __restrict__ part, int64_t M, int O, double* __restrict__ mean,
+    double* __restrict__ var, const float* __restrict__ gamma, const float* __restrict__ beta,
+    double eps, double momentum, float* __restrict__ run_mean, float* __restrict__ run_var,
+    float* __restrict__ scale, float* __restrict__ shift, double* __restrict__ invstd) {
+  const int o = blockIdx.x * 4 + (int)(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (o >= O) return;
+  const double s = chunk_fold(part + o, 2 * (int64_t)O, lane);
+  const double q = chunk_fold(part + O + o, 2 * (int64_t)O, lane);
+  if (lane) return;
+  // the statistics as channel_combine_kernel (this file's flags)
+  const double mu = s / (double)M;
+  const double v0 = q / (double)M - mu * mu;
+  const double vd = v0 > 0.0 ? v0 : 0.0;
+  mean[o] = mu;
+  var[o] = vd;
+  {  // the coefficients as bn_coeffs_kernel (sa_train.hip: fp contraction off)
+#pragma clang fp contract(off)
+    const float v = (float)vd, muf = (float)mu;
+    const float sc = gamma[o] / sqrtf(v + (float)eps);
+    scale[o] = sc;
+    shift[o] = beta[o] - muf * sc;
+    invstd[o] = 1.0 / sqrt(vd + eps);
+    if (run_mean) {
+      const double unb = M > 1 ? vd * ((double)M / (double)(M - 1)) : vd;
+      run_mean[o] = (float)((1.0 - momentum) * run_mean[o] + momentum * mu);
+      run_var[o] = (float)((1.0 - momentum) * run_var[o] + momentum * unb);
+    }
+  }
+}
+
 __global__ void affine_act_kernel(const float* __restrict__ Z, int64_t M, int O,
                                   const float* __restrict__ scale, const float* __restrict__ shift,
                                   int relu, int64_t ns, float* __restrict__ Y) {
@@ -345,6 +379,33 @@ extern "C" int pcst_channel_stats(const float* Z, int64_t M, int64_t O, double* 
   hipLaunchKernelGGL(channel_combine_kernel, dim3((unsigned)cdiv(O, 4)), dim3(256), 0, s, part, M,
                      (int)O, mean, var);
   PCST_LAUNCH_CHECK("channel_stats");
+  return PCST_OK;
+}
+
+extern "C" int pcst_bn_train_stats(const float* Z, int64_t M, int64_t O, const float* gamma,
+                                   const float* beta, double eps, double momentum,
+                                   float* running_mean, float* running_var, double* mean, double* var,
+                                   float* scale, float* shift, double* invstd, void* workspace,
+                                   void* stream) {
+  PCST_CHECK_ARG(M > 0 && O > 0, "bn_train_stats: bad shape");
+  PCST_CHECK_ARG(Z && gamma && beta && mean && var && scale && shift && invstd && workspace,
+                 "bn_train_stats: null pointer");
+  PCST_CHECK_ARG((running_mean == nullptr) == (running_var == nullptr),
+                 "bn_train_stats: running mean and var go together");
+  hipStream_t s = as_stream(stream);
+  double* part = static_cast<double*>(workspace);
+  if (O % 4 == 0 && (uintptr_t)Z % 16 == 0) {
+    const int64_t G = O / 4;
+    hipLaunchKernelGGL(channel_partial_kernel<4>, dim3(kStatChunks, (unsigned)cdiv(G, G < 64 ? G : 64)),
+                       dim3(256), 0, s, Z, M, (int)O, part);
+  } else {
+    hipLaunchKernelGGL(channel_partial_kernel<1>, dim3(kStatChunks, (unsigned)cdiv(O, O < 64 ? O : 64)),
+                       dim3(256), 0, s, Z, M, (int)O, part);
+  }
+  hipLaunchKernelGGL(bn_stats_coeffs_kernel, dim3((unsigned)cdiv(O, 4)), dim3(256), 0, s, part, M,
+                     (int)O, mean, var, gamma, beta, eps, momentum, running_mean, running_var, scale,
+                     shift, invstd);
+  PCST_LAUNCH_CHECK("bn_train_stats");
   return PCST_OK;
 }
 

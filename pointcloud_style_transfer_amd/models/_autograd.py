@@ -82,6 +82,7 @@ def _h_t(w, half):
     return w.detach().t().to(half).contiguous()
 
 
+FUSED_BN_STATS = True  # BatchNorm forward: pcst_bn_train_stats instead of channel_stats + coeffs
 BATCH_CAST = True   # one pcst_cast16_batch launch for a layer stack's 16-bit weight copies
 
 
@@ -334,9 +335,13 @@ class BNReLUFn(torch.autograd.Function):
     def forward(ctx, z, gamma, beta, running_mean, running_var, eps, momentum, pool_ns):
         z2 = z.reshape(-1, z.shape[-1]).float().contiguous()
         M = z2.shape[0]
-        mean, var = _hip.channel_stats(z2)
-        scale, shift, invstd = _hip.bn_train_coeffs(mean, var, M, gamma.detach(), beta.detach(),
-                                                    eps, momentum, running_mean, running_var)
+        if FUSED_BN_STATS:  # statistics and coefficients in two launches (the same bits)
+            mean, var, scale, shift, invstd = _hip.bn_train_stats(
+                z2, gamma.detach(), beta.detach(), eps, momentum, running_mean, running_var)
+        else:
+            mean, var = _hip.channel_stats(z2)
+            scale, shift, invstd = _hip.bn_train_coeffs(mean, var, M, gamma.detach(), beta.detach(),
+                                                        eps, momentum, running_mean, running_var)
         arg = None
         if pool_ns:
             y, arg = _hip.bn_relu_maxpool(z2, scale, shift, pool_ns)

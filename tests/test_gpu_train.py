@@ -567,3 +567,28 @@ def test_cast16_batch_matches_per_tensor_casts(H, half):
         assert torch.equal(o.view(torch.int16), ref.view(torch.int16))
     plain = H.cast16_batch(ts[:3], half)
     assert all(torch.equal(o, t.to(half)) for o, t in zip(plain, ts[:3]))
+
+
+@pytest.mark.parametrize("O", [64, 128, 3])
+def test_bn_train_stats_matches_stats_then_coeffs(H, O):
+    """pcst_bn_train_stats (statistics + coefficients in two launches) gives the bits of
+    pcst_channel_stats followed by pcst_bn_train_coeffs: mean / var, scale / shift / invstd and
+    the running-stat update, with and without running stats, vectorised and scalar channel
+    counts."""
+    torch.manual_seed(O)
+    M = 40961
+    z = torch.randn(M, O, device="cuda") * 3.0 + 0.5
+    g = torch.rand(O, device="cuda") + 0.5
+    b = torch.randn(O, device="cuda")
+    for with_run in (True, False):
+        rm1 = torch.randn(O, device="cuda") if with_run else None
+        rv1 = (torch.rand(O, device="cuda") + 0.1) if with_run else None
+        rm2 = rm1.clone() if with_run else None
+        rv2 = rv1.clone() if with_run else None
+        mean, var = H.channel_stats(z)
+        ref = H.bn_train_coeffs(mean, var, M, g, b, 1e-5, 0.1, rm1, rv1)
+        got = H.bn_train_stats(z, g, b, 1e-5, 0.1, rm2, rv2)
+        for x, y in zip((mean, var) + tuple(ref), got):
+            assert torch.equal(x, y)
+        if with_run:
+            assert torch.equal(rm1, rm2) and torch.equal(rv1, rv2)
