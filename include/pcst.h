@@ -136,20 +136,24 @@ int pcst_group_gather_bwd(const float* dgrouped, const int64_t* group_idx, int64
  * 16-bit(x + Dropout_p(h W2^T + b2)); x [M,256], W1 [512,256], W2 [256,512] in the 16-bit format
  * f16 selects (1 float16, 0 bfloat16), b1 / b2 fp32.  The bits of pcst_gemm_ex EP_BF16 followed
  * by EP_RESID_DROP16 with the same (seed, p); h is written for the backward but never re-read.
+ * hbits (may be NULL): [M,16] uint32, bit j of word w of row m = [h[m, 32w + j] > 0] (the ReLU
+ * mask the backward needs, 64 B per row instead of h's 1 KiB).
  * 16-byte aligned pointers, x_out != x, M * 1024 < 2^31. */
 int pcst_resblock_fwd16(const uint16_t* x, int64_t M, const uint16_t* w1, const float* b1,
                         const uint16_t* w2, const float* b2, uint64_t seed, float drop_p,
-                        uint16_t* h, uint16_t* x_out, int f16, void* stream);
+                        uint16_t* h, uint16_t* x_out, uint32_t* hbits, int f16, void* stream);
 /* The same block's backward products in one launch (the autograd backward of the block above,
  * trainer.py:106): dz [M,512] = 16-bit((dd W2) * [h > 0]), g_out [M,256] = 16-bit(g + dz W1) and,
  * if dd_out is not NULL, dd_out [M,256] = 16-bit(g_out keep / (1 - p)) with keep the dropout mask
  * of (seed, p) -- the previous block's, as pcst_gemm_ex's EP_ADD16 dropout copy.  w2t = W2^T
  * [512,256] and w1t = W1^T [256,512] in the 16-bit format.  The bits of pcst_gemm_ex EP_RELU_MASK
  * (aux h) followed by EP_ADD16 (aux g); dz is written for dW1 = dz^T x but never re-read here.
+ * hbits (may be NULL): the forward's mask bits, read instead of h (h may then be NULL).
  * 16-byte aligned pointers, g_out != dd, dz != h, M * 1024 < 2^31. */
 int pcst_resblock_bwd16(const uint16_t* dd, int64_t M, const uint16_t* w2t, const uint16_t* w1t,
                         const uint16_t* h, const uint16_t* g, uint64_t seed, float drop_p,
-                        uint16_t* dz, uint16_t* g_out, uint16_t* dd_out, int f16, void* stream);
+                        uint16_t* dz, uint16_t* g_out, uint16_t* dd_out, const uint32_t* hbits,
+                        int f16, void* stream);
 /* The step's 2-D fp32 weights to the 16-bit format f16 selects, n <= 64 tensors in one launch:
  * dst[i] = 16-bit(src[i]) [rows, cols] row-major, or its transpose [cols, rows] if transpose[i]
  * (round to nearest even, as torch's .to(dtype)).  Host arrays of n entries. */

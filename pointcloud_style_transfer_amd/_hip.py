@@ -75,9 +75,9 @@ SIGNATURES = {
     "pcst_gemm_nt_bf16": [_P, _I, _I, _P, _I, _P, _P, ctypes.c_int, _P, ctypes.c_int, _P],
     "pcst_linear_wgrad_bf16_workspace_size": [_I, _I, _I, _SZ],
     "pcst_linear_wgrad_bf16": [_P, _P, _I, _I, _I, _P, _P, _P, ctypes.c_int, _P],
-    "pcst_resblock_fwd16": [_P, _I, _P, _P, _P, _P, ctypes.c_uint64, _F, _P, _P, ctypes.c_int, _P],
+    "pcst_resblock_fwd16": [_P, _I, _P, _P, _P, _P, ctypes.c_uint64, _F, _P, _P, _P, ctypes.c_int, _P],
     "pcst_cast16_batch": [_P, _P, _P, _P, _P, ctypes.c_int, ctypes.c_int, _P],
-    "pcst_resblock_bwd16": [_P, _I, _P, _P, _P, _P, ctypes.c_uint64, _F, _P, _P, _P, ctypes.c_int, _P],
+    "pcst_resblock_bwd16": [_P, _I, _P, _P, _P, _P, ctypes.c_uint64, _F, _P, _P, _P, _P, ctypes.c_int, _P],
     "pcst_gemm_ex": [_P, ctypes.c_int, _I, _I, _P, ctypes.c_int, _I, _P, ctypes.c_int,
                      ctypes.c_int, _P, ctypes.c_uint64, _F, _I, _P, _P, ctypes.c_int, _P],
     "pcst_dropout_grad_bf16": [_P, _I, ctypes.c_uint64, _F, _P, ctypes.c_int, _P],
@@ -808,11 +808,13 @@ def _half_of(*ts, default=torch.bfloat16):
     return hs.pop() if hs else default
 
 
-def resblock_fwd16(x, w1, b1, w2, b2, seed=0, p=0.0):
+def resblock_fwd16(x, w1, b1, w2, b2, seed=0, p=0.0, mask_bits=False):
     """One residual block of the 16-bit residual stream in one launch (pcst_resblock_fwd16):
     x [M,256] 16-bit, w1 [512,256] / w2 [256,512] 16-bit (x's format), b1 [512] / b2 [256] fp32 ->
     (h [M,512] = relu(x w1^T + b1), x' [M,256] = x + Dropout_p(h w2^T + b2)), both 16-bit: the
-    bits of gemm_ex EP_BF16 followed by EP_RESID_DROP16 under the same (seed, p)."""
+    bits of gemm_ex EP_BF16 followed by EP_RESID_DROP16 under the same (seed, p).
+    mask_bits=True: also the ReLU mask [h > 0] as int32 [M,16] bits (bit j of word w of row m =
+    unit 32w + j), returned third, for resblock_bwd16(hbits=)."""
     require_device(x, w1, b1, w2, b2)
     half = x.dtype
     if half not in (torch.float16, torch.bfloat16):
@@ -826,10 +828,11 @@ def resblock_fwd16(x, w1, b1, w2, b2, seed=0, p=0.0):
     x, w1, w2 = x.contiguous(), w1.contiguous(), w2.contiguous()
     h = torch.empty(M, 512, dtype=half, device=x.device)
     out = torch.empty(M, 256, dtype=half, device=x.device)
+    hbits = torch.empty(M, 16, dtype=torch.int32, device=x.device) if mask_bits else None
     _call("pcst_resblock_fwd16", _ptr(x), M, _ptr(w1), _ptr(_f32(b1)), _ptr(w2), _ptr(_f32(b2)),
-          int(seed) & (2**64 - 1), float(p), _ptr(h), _ptr(out),
+          int(seed) & (2**64 - 1), float(p), _ptr(h), _ptr(out), _ptr(hbits),
           1 if half == torch.float16 else 0, _stream())
-    return h, out
+    return (h, out, hbits) if mask_bits else (h, out)
 
 
 def cast16_batch(tensors, half, transpose=None):
@@ -860,29 +863,35 @@ def cast16_batch(tensors, half, transpose=None):
     return outs
 
 
-def resblock_bwd16(dd, w2t, w1t, h, g, seed=0, p=0.0, dropout_copy=False):
+def resblock_bwd16(dd, w2t, w1t, h, g, seed=0, p=0.0, dropout_copy=False, hbits=None):
     """The backward products of one residual block in one launch (pcst_resblock_bwd16): dd, g
     [M,256] and h [M,512] 16-bit, w2t = W2^T [512,256] / w1t = W1^T [256,512] 16-bit ->
     (dz [M,512] = (dd W2) * [h > 0], g' [M,256] = g + dz W1, and with dropout_copy the previous
     block's dD' = g' keep / (1 - p) under (seed, p), else None), all 16-bit: the bits of gemm_ex
-    EP_RELU_MASK (aux h) followed by EP_ADD16 (aux g, dropout_copy)."""
-    require_device(dd, w2t, w1t, h, g)
+    EP_RELU_MASK (aux h) followed by EP_ADD16 (aux g, dropout_copy).  hbits: resblock_fwd16's
+    mask bits [M,16], read instead of h (h may then be None)."""
+    if h is None and hbits is None:
+        raise RuntimeError("resblock_bwd16: give h or hbits")
+    require_device(dd, w2t, w1t, g, *([h] if h is not None else []), *([hbits] if hbits is not None else []))
     half = dd.dtype
     if half not in (torch.float16, torch.bfloat16):
         raise RuntimeError(f"resblock_bwd16: dd must be float16 or bfloat16, got {dd.dtype}")
     M = dd.shape[0]
     if (dd.dim() != 2 or dd.shape[1] != 256 or tuple(w2t.shape) != (512, 256)
-            or tuple(w1t.shape) != (256, 512) or tuple(h.shape) != (M, 512)
+            or tuple(w1t.shape) != (256, 512) or (h is not None and tuple(h.shape) != (M, 512))
             or tuple(g.shape) != (M, 256)
-            or any(t.dtype != half for t in (w2t, w1t, h, g))):
+            or (hbits is not None and (tuple(hbits.shape) != (M, 16) or hbits.dtype != torch.int32))
+            or any(t.dtype != half for t in (w2t, w1t, g) + ((h,) if h is not None else ()))):
         raise RuntimeError("resblock_bwd16: shapes are dd [M,256], w2t [512,256], w1t [256,512], "
                            "h [M,512], g [M,256] in dd's 16-bit format")
-    dd, w2t, w1t, h, g = (t.contiguous() for t in (dd, w2t, w1t, h, g))
+    dd, w2t, w1t, g = (t.contiguous() for t in (dd, w2t, w1t, g))
+    h = h.contiguous() if h is not None else None
+    hbits = hbits.contiguous() if hbits is not None else None
     dz = torch.empty(M, 512, dtype=half, device=dd.device)
     g_out = torch.empty(M, 256, dtype=half, device=dd.device)
     dd_out = torch.empty(M, 256, dtype=half, device=dd.device) if dropout_copy else None
     _call("pcst_resblock_bwd16", _ptr(dd), M, _ptr(w2t), _ptr(w1t), _ptr(h), _ptr(g),
-          int(seed) & (2**64 - 1), float(p), _ptr(dz), _ptr(g_out), _ptr(dd_out),
+          int(seed) & (2**64 - 1), float(p), _ptr(dz), _ptr(g_out), _ptr(dd_out), _ptr(hbits),
           1 if half == torch.float16 else 0, _stream())
     return dz, g_out, dd_out
 

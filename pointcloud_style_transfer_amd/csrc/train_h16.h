@@ -22,12 +22,13 @@ constexpr int kCastMax = 64;  // tensors per pcst_cast16_batch call
                         void* stream);                                                             \
   int resblock_fwd_impl(const uint16_t* x, int64_t M, const uint16_t* w1, const float* b1,         \
                         const uint16_t* w2, const float* b2, uint64_t seed, float drop_p,          \
-                        uint16_t* h, uint16_t* xo, void* stream);                                  \
+                        uint16_t* h, uint16_t* xo, uint32_t* hbits, void* stream);                 \
   int cast16_batch_impl(const float* const* src, uint16_t* const* dst, const int32_t* rows,         \
                         const int32_t* cols, const int32_t* trans, int n, void* stream);           \
   int resblock_bwd_impl(const uint16_t* dd, int64_t M, const uint16_t* w2t, const uint16_t* w1t,   \
                         const uint16_t* h, const uint16_t* g, uint64_t seed, float drop_p,         \
-                        uint16_t* dz, uint16_t* g_out, uint16_t* dd_out, void* stream);            \
+                        uint16_t* dz, uint16_t* g_out, uint16_t* dd_out, const uint32_t* hbits,    \
+                        void* stream);                                                             \
   int wgrad_ex_workspace_impl(int64_t M, int64_t I, int64_t O, size_t* bytes);                     \
   int wgrad_ex_impl(const void* dZ, int dz_bf16, const void* X, int x_bf16, int64_t M, int64_t I, \
                     int64_t O, float* dW, float* db, void* workspace, void* stream);               \

@@ -1379,7 +1379,7 @@ constexpr int kRbHLd = 128 + 8;          // h chunk row: 272 B
 constexpr int kRbXBytes = kRbRows * kRbXLd * 2;
 constexpr int kRbHBytes = kRbRows * kRbHLd * 2;
 constexpr int kRbBBytes = 128 * kRbBLd * 2;
-constexpr int kRbLds = kRbXBytes + kRbHBytes + 2 * kRbBBytes;
+constexpr int kRbLds = kRbXBytes + kRbHBytes + 2 * kRbBBytes + kRbRows * 4 * 4;  // + mask bits
 
 struct RbArgs {
   const uint16_t* x;   // [M, 256]   the A operand: x (forward) / dD (backward)
@@ -1392,6 +1392,9 @@ struct RbArgs {
   const uint16_t* hm;  // [M, 512]   backward: the block's h (ReLU mask)
   const uint16_t* g;   // [M, 256]   backward: the residual gradient
   uint16_t* ddo;       // [M, 256]   backward, optional: dropout copy of g' (previous block's rate)
+  uint32_t* hbo;       // [M, 16]    forward (v2), optional: the ReLU mask of h as bits (bit j of word
+                       //            w of row m = [h[m, 32w + j] > 0])
+  const uint32_t* hbi; // [M, 16]    backward, optional: that mask, read instead of h
   int64_t M;
   uint32_t seed_lo, seed_hi, thr;
   float scale;
@@ -1405,7 +1408,9 @@ struct RbArgs {
 // chunk buffer two slices before its epilogue, and g loaded into the x tile once the last
 // first-product slice has read it.  Bit-identical to the two gemm_ex calls (the fast epilogue's
 // "+ 0" bias included: it turns a -0 product into +0).
-template <bool BWD>
+// MB (backward): the ReLU mask from the forward's bit array (a.hbi, 2 KiB per 128-row chunk of
+// 128 units) instead of h (32 KiB): 16x fewer mask bytes
+template <bool BWD, bool MB = false>
 // two waves per SIMD: two 256-thread work-groups per CU (64-row tiles), or one of 512 threads
 __global__ __launch_bounds__(kRbThreads) __attribute__((amdgpu_waves_per_eu(2, 2))) void resblock_kernel(
     RbArgs a, int per_xcd, int ntiles) {
@@ -1414,6 +1419,7 @@ __global__ __launch_bounds__(kRbThreads) __attribute__((amdgpu_waves_per_eu(2, 2
   h16* Hs = reinterpret_cast<h16*>(smem + kRbXBytes);                       // [rows][kRbHLd]
   h16* Bs0 = reinterpret_cast<h16*>(smem + kRbXBytes + kRbHBytes);          // [128][kRbBLd]
   h16* Bs1 = reinterpret_cast<h16*>(smem + kRbXBytes + kRbHBytes + kRbBBytes);
+  uint32_t* Mb = reinterpret_cast<uint32_t*>(smem + kRbXBytes + kRbHBytes + 2 * kRbBBytes);  // [rows][4]
   const int L = blockIdx.x;
   const int t = (L & 7) * per_xcd + (L >> 3);
   if (t >= ntiles) return;
@@ -1450,9 +1456,11 @@ __global__ __launch_bounds__(kRbThreads) __attribute__((amdgpu_waves_per_eu(2, 2
     g1 = bload16(r, off + 16, 0);
   };
   const rsrc_t rh = make_rsrc(a.h, (uint32_t)(M * 512 * 2));
-  const rsrc_t rm = make_rsrc(BWD ? a.hm : nullptr, BWD ? (uint32_t)(M * 512 * 2) : 0u);
+  const rsrc_t rm = make_rsrc(BWD && !MB ? a.hm : nullptr, BWD && !MB ? (uint32_t)(M * 512 * 2) : 0u);
+  const rsrc_t rmb = make_rsrc(MB ? a.hbi : nullptr, MB ? (uint32_t)(M * 16 * 4) : 0u);
   const rsrc_t rg = make_rsrc(BWD ? a.g : nullptr, BWD ? (uint32_t)(M * 256 * 2) : 0u);
   uint4 mk[4], gr[8];  // backward: a chunk's mask rows, the residual gradient tile
+  uint32_t mbw = 0;    // MB: one word of a chunk's mask bits (row tid / 4, word tid % 4)
   // the lane's biases, loaded up front: a load issued at its use would wait (in-order vmcnt)
   // for every weight slice in flight as well
   float bb1[4][2], bb2[4];
@@ -1492,7 +1500,13 @@ __global__ __launch_bounds__(kRbThreads) __attribute__((amdgpu_waves_per_eu(2, 2
       if (i + 1 + kRbPF < kRbSlices) load_slice(i + 1 + kRbPF, g[un][0], g[un][1]);
     }
     const int c = i / kRbSPC, j = i % kRbSPC;
-    if (BWD && j == 0) {
+    if (MB && j == 0 && tid < 4 * kRbRows) {
+      // chunk c's mask bits: rows x 4 words (units 128c .. 128c + 127)
+      const int r = tid >> 2, w = tid & 3;
+      mbw = __builtin_amdgcn_raw_buffer_load_b32(rmb, (int)(((m0 + r) * 16 + 4 * c + w) * 4), 0, 0);
+    }
+    if (MB && j == kRbW1S - 2 && tid < 4 * kRbRows) Mb[tid] = mbw;  // read by the epilogue after the next barrier
+    if (BWD && !MB && j == 0) {
       // chunk c's mask rows, coalesced (rows x 16 chunks of 16 B, 4 per thread)
 #pragma unroll
       for (int it = 0; it < 4; ++it) {
@@ -1500,7 +1514,7 @@ __global__ __launch_bounds__(kRbThreads) __attribute__((amdgpu_waves_per_eu(2, 2
         mk[it] = bload16(rm, (uint32_t)(((m0 + r) * 512 + 128 * c + cch) * 2), 0);
       }
     }
-    if (BWD && j == kRbW1S - 2) {
+    if (BWD && !MB && j == kRbW1S - 2) {
       // -> Hs: the previous chunk's second-product readers passed this slice's barrier; the
       // epilogue reads it after the next one
 #pragma unroll
@@ -1563,7 +1577,8 @@ __global__ __launch_bounds__(kRbThreads) __attribute__((amdgpu_waves_per_eu(2, 2
         for (int r = 0; r < 16; ++r) {
           h16* ph = Hs + (32 * wr + xrow(r, h)) * kRbHLd + col;
           float v = acc1[bn][r] + bb;
-          if (BWD) v = __builtin_bit_cast(int16_t, *ph) > 0 ? v : 0.0f;
+          if (MB) v = (Mb[(32 * wr + xrow(r, h)) * 4 + (col >> 5)] >> (col & 31)) & 1u ? v : 0.0f;
+          else if (BWD) v = __builtin_bit_cast(int16_t, *ph) > 0 ? v : 0.0f;
           else v = fmaxf(v, 0.0f);
           *ph = (h16)v;
         }
@@ -1818,6 +1833,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   int64_t r0 = (int64_t)t * kR2Rows + 64 * wid + l32;  // the lane's row in set 0 (set 1: +32)
   uint32_t v256 = (uint32_t)((r0 * 256 + 8 * h) * 2);  // set p: + p * 32 * 512 bytes
   uint32_t v512 = (uint32_t)((r0 * 512 + 8 * h) * 2);  // set p: + p * 32 * 1024 bytes
+  uint32_t vrow16 = (uint32_t)(r0 * 64);               // the mask-bit row (16 words): + p * 32 * 64
   const uint32_t vstep256 = (uint32_t)G * kR2Rows * 256 * 2, vstep512 = (uint32_t)G * kR2Rows * 512 * 2;
   u32x4 xb[2][16];
 #pragma unroll
@@ -1826,6 +1842,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     for (int kb = 0; kb < 16; ++kb)
       xb[p][kb] = as_u32x4(bload16(rx, v256 + p * 16384 + kb * 32, 0));
   const rsrc_t rh = make_rsrc(a.h, (uint32_t)(M * 512 * 2));
+  const rsrc_t rhb = make_rsrc(!BWD ? a.hbo : nullptr, !BWD && a.hbo ? (uint32_t)(M * 16 * 4) : 0u);
   const rsrc_t rm = make_rsrc(BWD ? a.hm : nullptr, BWD ? (uint32_t)(M * 512 * 2) : 0u);
   const rsrc_t ro = make_rsrc(a.xo, (uint32_t)(M * 256 * 2));
   const rsrc_t rg = make_rsrc(BWD ? a.g : nullptr, BWD ? (uint32_t)(M * 256 * 2) : 0u);
@@ -1902,38 +1919,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       u32x4 hb[2][2];
       const uint32_t e0 = (uint32_t)((r0 + 32 * (c & 1)) * 256 + 32 * (c >> 1) + 4 * h);
       if (!(c & 1)) keep2 = 0;
-#pragma unroll
-      for (int f = 0; f < 32; ++f) {
-        if (f == 16) {
-#if PCST_X_RB2_STAMPS
-          if (c == 9 && gc < 16) R2_STAMP(7);
-#endif
-          // epilogue: forward h = 16-bit(relu(acc1 + b1)), backward dZ = 16-bit((acc1 + 0)
-          // [h > 0]); to the second product's operand layout and out to global (16 B per lane)
-          if (!BWD) asm volatile("s_waitcnt lgkmcnt(4)" : "+v"(bq[0]), "+v"(bq[1]), "+v"(bq[2]), "+v"(bq[3]));
-#pragma unroll
-          for (int p = 0; p < 2; ++p) {
-            float v[16];
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-              v[r] = acc1[p][r] + (BWD ? 0.0f : bq[r >> 2][r & 3]);
-              if (BWD) v[r] = (mbits >> (16 * p + r)) & 1u ? v[r] : 0.0f;
-              else v[r] = fmaxf(v[r], 0.0f);
-            }
-#pragma unroll
-            for (int kk = 0; kk < 2; ++kk) {
-              const u32x4 o = {pack16(v[8 * kk + 0], v[8 * kk + 1]), pack16(v[8 * kk + 2], v[8 * kk + 3]),
-                               pack16(v[8 * kk + 4], v[8 * kk + 5]), pack16(v[8 * kk + 6], v[8 * kk + 7])};
-              hb[p][kk] = relayout(o);
-              if (!PCST_X_RB2_NOSTORE)
-                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i32, hb[p][kk]), rh,
-                                                       (int)(v512 + p * 32768 + kk * 32), 64 * c, 0);
-            }
-          }
-#if PCST_X_RB2_STAMPS
-          if (c == 9 && gc < 16) R2_STAMP(8);
-#endif
-        }
+      // one fragment step (f a constant after unrolling): wait, MFMAs, next read
+      auto frag_step = [&](const int f) __attribute__((always_inline)) {
         const int younger = (31 - f < 3 ? 31 - f : 3) + (!BWD && f >= 12 && f < 16 ? 4 : 0);
         if (younger == 7) r2_wait1<7>(fr[f & 3]);
         else if (younger == 3) r2_wait1<3>(fr[f & 3]);
@@ -1963,7 +1950,63 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 #pragma unroll
           for (int q = 0; q < 4; ++q) bq[q] = r2_read_f4(lb1 + 4 * (32 * c + 8 * q));
         }
-      }
+            };
+#pragma unroll
+      for (int f = 0; f < 16; ++f) frag_step(f);
+#if PCST_X_RB2_STAMPS
+        if (c == 9 && gc < 16) R2_STAMP(7);
+#endif
+        // epilogue: forward h = 16-bit(relu(acc1 + b1)), backward dZ = 16-bit((acc1 + 0)
+        // [h > 0]); to the second product's operand layout and out to global (16 B per lane)
+        if (!BWD) asm volatile("s_waitcnt lgkmcnt(4)" : "+v"(bq[0]), "+v"(bq[1]), "+v"(bq[2]), "+v"(bq[3]));
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+          float v[16];
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            v[r] = acc1[p][r] + (BWD ? 0.0f : bq[r >> 2][r & 3]);
+            if (BWD) v[r] = (mbits >> (16 * p + r)) & 1u ? v[r] : 0.0f;
+            else v[r] = fmaxf(v[r], 0.0f);
+          }
+          uint32_t mb = 0;  // forward: this lane's half of the row's mask word for chunk c
+#pragma unroll
+          for (int kk = 0; kk < 2; ++kk) {
+            const u32x4 o = {pack16(v[8 * kk + 0], v[8 * kk + 1]), pack16(v[8 * kk + 2], v[8 * kk + 3]),
+                             pack16(v[8 * kk + 4], v[8 * kk + 5]), pack16(v[8 * kk + 6], v[8 * kk + 7])};
+            if (!BWD) {
+              // [stored 16-bit value > 0] of accumulator register r = 8kk + 2d + s, unit
+              // xrow(r, h) = ((2d + s) & 3) + 16kk + 8(d >> 1) + 4h of the chunk
+#pragma unroll
+              for (int d = 0; d < 4; ++d) {
+#pragma unroll
+                for (int s2 = 0; s2 < 2; ++s2) {
+                  const uint32_t half16 = (o[d] >> (16 * s2)) & 0xffffu;
+                  const int bit = ((2 * d + s2) & 3) + 16 * kk + 8 * (d >> 1);
+                  mb |= (half16 - 1u < 0x7fffu ? 1u : 0u) << bit;  // 1 .. 0x7fff: positive
+                }
+              }
+            }
+            hb[p][kk] = relayout(o);
+            if (!PCST_X_RB2_NOSTORE)
+              __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i32, hb[p][kk]), rh,
+                                                     (int)(v512 + p * 32768 + kk * 32), 64 * c, 0);
+          }
+          if (!BWD) {  // the two halves' bits are disjoint: one word per row, lane half 0 stores
+            // (branch-free: control flow here breaks the register allocation of the loop; the
+            // other half's store, and every store when hbo is NULL, fails the range check)
+            mb <<= 4 * h;  // lane half h holds units + 4h
+            uint32_t lo = mb, hi = mb;
+            swap_halves(lo, hi);  // lo: lanes 32-63 get lanes 0-31's; hi: lanes 0-31 get 32-63's
+            const uint32_t word = mb | (h ? lo : hi);
+            __builtin_amdgcn_raw_buffer_store_b32(word, rhb, (int)(h ? 0x7ffffff0u : vrow16 + p * 32 * 64),
+                                                  4 * c, 0);
+          }
+        }
+#if PCST_X_RB2_STAMPS
+        if (c == 9 && gc < 16) R2_STAMP(8);
+#endif
+#pragma unroll
+      for (int f = 16; f < 32; ++f) frag_step(f);
 #if PCST_X_RB2_STAMPS
       if (c == 9 && gc < 16) R2_STAMP(9);
 #endif
@@ -1975,9 +2018,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
           asm volatile("s_waitcnt vmcnt(12)" : "+v"(mk[0][0]), "+v"(mk[0][1]), "+v"(mk[1][0]), "+v"(mk[1][1]) : : "memory");
         else
           asm volatile("s_waitcnt vmcnt(4)" : "+v"(mk[0][0]), "+v"(mk[0][1]), "+v"(mk[1][0]), "+v"(mk[1][1]) : : "memory");
-      } else {
-        if (fill2) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      } else {  // + the two mask-bit word stores after the h stores
+        if (fill2) asm volatile("s_waitcnt vmcnt(14)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
       }
 #if PCST_X_RB2_STAMPS
       if (c == 9 && gc < 16) R2_STAMP(10);
@@ -2094,6 +2137,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     r0 += (int64_t)G * kR2Rows;
     v256 += vstep256;
     v512 += vstep512;
+    vrow16 += (uint32_t)G * kR2Rows * 64;
   }
 #if PCST_X_RB2_STAMPS
   R2_STAMP(6);
@@ -2162,8 +2206,9 @@ static int r2_grid() {
 
 int resblock_fwd_impl(const uint16_t* x, int64_t M, const uint16_t* w1, const float* b1,
                       const uint16_t* w2, const float* b2, uint64_t seed, float drop_p,
-                      uint16_t* h, uint16_t* xo, void* stream) {
+                      uint16_t* h, uint16_t* xo, uint32_t* hbits, void* stream) {
   PCST_CHECK_ARG(M >= 0 && M * 512 * 2 < (1ll << 31), "resblock_fwd: bad M");
+  PCST_CHECK_ARG(hbits == nullptr || PCST_RB_V2_FWD, "resblock_fwd: hbits needs the v2 forward kernel");
   PCST_CHECK_ARG(drop_p >= 0.0f && drop_p < 1.0f, "resblock_fwd: dropout p must be in [0, 1)");
   if (M == 0) return PCST_OK;
   PCST_CHECK_ARG(x && w1 && b1 && w2 && b2 && h && xo, "resblock_fwd: null pointer");
@@ -2177,6 +2222,7 @@ int resblock_fwd_impl(const uint16_t* x, int64_t M, const uint16_t* w1, const fl
   a.thr = drop_threshold(drop_p);
   a.scale = 1.0f / (1.0f - drop_p);
   a.hm = nullptr; a.g = nullptr; a.ddo = nullptr;
+  a.hbo = hbits; a.hbi = nullptr;
   if (PCST_RB_V2_FWD) {
     const int ntiles = (int)cdiv(M, kR2Rows);
     hipLaunchKernelGGL(resblock2_kernel<false>, dim3((unsigned)std::min(ntiles, r2_grid())), dim3(256),
@@ -2192,11 +2238,14 @@ int resblock_fwd_impl(const uint16_t* x, int64_t M, const uint16_t* w1, const fl
 
 int resblock_bwd_impl(const uint16_t* dd, int64_t M, const uint16_t* w2t, const uint16_t* w1t,
                       const uint16_t* h, const uint16_t* g, uint64_t seed, float drop_p,
-                      uint16_t* dz, uint16_t* g_out, uint16_t* dd_out, void* stream) {
+                      uint16_t* dz, uint16_t* g_out, uint16_t* dd_out, const uint32_t* hbits,
+                      void* stream) {
   PCST_CHECK_ARG(M >= 0 && M * 512 * 2 < (1ll << 31), "resblock_bwd: bad M");
   PCST_CHECK_ARG(drop_p >= 0.0f && drop_p < 1.0f, "resblock_bwd: dropout p must be in [0, 1)");
   if (M == 0) return PCST_OK;
-  PCST_CHECK_ARG(dd && w2t && w1t && h && g && dz && g_out, "resblock_bwd: null pointer");
+  PCST_CHECK_ARG(dd && w2t && w1t && (h || hbits) && g && dz && g_out, "resblock_bwd: null pointer");
+  PCST_CHECK_ARG(hbits == nullptr || !PCST_RB_V2_BWD, "resblock_bwd: hbits needs the round-3 backward kernel");
+  PCST_CHECK_ARG(((uintptr_t)hbits % 4) == 0, "resblock_bwd: hbits must be 4-byte aligned");
   PCST_CHECK_ARG(((uintptr_t)dd | (uintptr_t)w2t | (uintptr_t)w1t | (uintptr_t)h | (uintptr_t)g |
                   (uintptr_t)dz | (uintptr_t)g_out | (uintptr_t)dd_out) % 16 == 0,
                  "resblock_bwd: pointers must be 16-byte aligned");
@@ -2204,6 +2253,7 @@ int resblock_bwd_impl(const uint16_t* dd, int64_t M, const uint16_t* w2t, const 
   RbArgs a;
   a.x = dd; a.w1 = w2t; a.b1 = nullptr; a.w2 = w1t; a.b2 = nullptr; a.h = dz; a.xo = g_out;
   a.hm = h; a.g = g; a.ddo = dd_out; a.M = M;
+  a.hbo = nullptr; a.hbi = hbits;
   a.seed_lo = (uint32_t)seed;
   a.seed_hi = (uint32_t)(seed >> 32);
   a.thr = drop_threshold(drop_p);
@@ -2214,8 +2264,12 @@ int resblock_bwd_impl(const uint16_t* dd, int64_t M, const uint16_t* w2t, const 
                        kR2Lds, as_stream(stream), a, ntiles);
   } else {
     const int ntiles = (int)cdiv(M, kRbRows), per = (int)cdiv(ntiles, 8);
-    hipLaunchKernelGGL(resblock_kernel<true>, dim3((unsigned)(8 * per)), dim3(kRbThreads), kRbLds,
-                       as_stream(stream), a, per, ntiles);
+    if (hbits)
+      hipLaunchKernelGGL((resblock_kernel<true, true>), dim3((unsigned)(8 * per)), dim3(kRbThreads), kRbLds,
+                         as_stream(stream), a, per, ntiles);
+    else
+      hipLaunchKernelGGL(resblock_kernel<true>, dim3((unsigned)(8 * per)), dim3(kRbThreads), kRbLds,
+                         as_stream(stream), a, per, ntiles);
   }
   PCST_LAUNCH_CHECK("resblock_bwd");
   return PCST_OK;
@@ -2239,9 +2293,9 @@ extern "C" int pcst_gemm_ex(const void* A, int a_bf16, int64_t M, int64_t K, con
 
 extern "C" int pcst_resblock_fwd16(const uint16_t* x, int64_t M, const uint16_t* w1, const float* b1,
                                    const uint16_t* w2, const float* b2, uint64_t seed, float drop_p,
-                                   uint16_t* h, uint16_t* x_out, int f16, void* stream) {
-  return f16 ? pcst::f16m::resblock_fwd_impl(x, M, w1, b1, w2, b2, seed, drop_p, h, x_out, stream)
-             : pcst::bf16m::resblock_fwd_impl(x, M, w1, b1, w2, b2, seed, drop_p, h, x_out, stream);
+                                   uint16_t* h, uint16_t* x_out, uint32_t* hbits, int f16, void* stream) {
+  return f16 ? pcst::f16m::resblock_fwd_impl(x, M, w1, b1, w2, b2, seed, drop_p, h, x_out, hbits, stream)
+             : pcst::bf16m::resblock_fwd_impl(x, M, w1, b1, w2, b2, seed, drop_p, h, x_out, hbits, stream);
 }
 
 extern "C" int pcst_cast16_batch(const float* const* src, uint16_t* const* dst, const int32_t* rows,
@@ -2254,9 +2308,9 @@ extern "C" int pcst_cast16_batch(const float* const* src, uint16_t* const* dst, 
 extern "C" int pcst_resblock_bwd16(const uint16_t* dd, int64_t M, const uint16_t* w2t,
                                    const uint16_t* w1t, const uint16_t* h, const uint16_t* g,
                                    uint64_t seed, float drop_p, uint16_t* dz, uint16_t* g_out,
-                                   uint16_t* dd_out, int f16, void* stream) {
-  return f16 ? pcst::f16m::resblock_bwd_impl(dd, M, w2t, w1t, h, g, seed, drop_p, dz, g_out, dd_out, stream)
-             : pcst::bf16m::resblock_bwd_impl(dd, M, w2t, w1t, h, g, seed, drop_p, dz, g_out, dd_out, stream);
+                                   uint16_t* dd_out, const uint32_t* hbits, int f16, void* stream) {
+  return f16 ? pcst::f16m::resblock_bwd_impl(dd, M, w2t, w1t, h, g, seed, drop_p, dz, g_out, dd_out, hbits, stream)
+             : pcst::bf16m::resblock_bwd_impl(dd, M, w2t, w1t, h, g, seed, drop_p, dz, g_out, dd_out, hbits, stream);
 }
 
 extern "C" int pcst_dropout_grad_bf16(const float* g, int64_t n, uint64_t seed, float drop_p,

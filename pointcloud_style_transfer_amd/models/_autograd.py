@@ -82,6 +82,9 @@ def _h_t(w, half):
     return w.detach().t().to(half).contiguous()
 
 
+# the fused blocks' backward reads the ReLU mask from 64 B of bits per row written by the forward
+# (kernel v2) instead of h's 1 KiB per row (h itself is still kept: dW2 = dD^T h)
+MASK_BITS = True
 FUSED_BN_STATS = True  # BatchNorm forward: pcst_bn_train_stats instead of channel_stats + coeffs
 BATCH_CAST = True   # one pcst_cast16_batch launch for a layer stack's 16-bit weight copies
 
@@ -230,14 +233,19 @@ class NoisePredictorFn(torch.autograd.Function):
             x, xb = _hip.gemm_ex(h1, wb[4], wb[5], epilogue=_hip.EP_COND, aux=cnd, group_rows=N,
                                  copy_bf16=True)
         saved, seeds = [xp, h0, h1], []
+        hbits = [None] * 6  # the fused blocks' ReLU masks as bits (MASK_BITS), for the backward
         for k in range(6):
             o = 6 + 4 * k
             seed = _draw_seed(ps[k])
             seeds.append(seed)
             saved.append(xb)
             if r16 and FUSED_BLOCK_FWD and xb.shape[1] == 256 and wb[o].shape == (512, 256):
-                h, xb = _hip.resblock_fwd16(xb, wb[o], wb[o + 1], wb[o + 2], wb[o + 3], seed=seed,
-                                            p=ps[k])
+                if MASK_BITS:
+                    h, xb, hbits[k] = _hip.resblock_fwd16(xb, wb[o], wb[o + 1], wb[o + 2], wb[o + 3],
+                                                          seed=seed, p=ps[k], mask_bits=True)
+                else:
+                    h, xb = _hip.resblock_fwd16(xb, wb[o], wb[o + 1], wb[o + 2], wb[o + 3], seed=seed,
+                                                p=ps[k])
             elif r16:
                 h = _hip.gemm_ex(xb, wb[o], wb[o + 1], relu=True, epilogue=_hip.EP_BF16)
                 xb = _hip.gemm_ex(h, wb[o + 2], wb[o + 3], epilogue=_hip.EP_RESID_DROP16, aux=xb,
@@ -251,6 +259,7 @@ class NoisePredictorFn(torch.autograd.Function):
         saved += [xb, q0, q1]
         ctx.save_for_backward(*saved, *w)
         ctx.seeds, ctx.ps, ctx.BN, ctx.half, ctx.r16 = seeds, tuple(ps), (B, N), half, r16
+        ctx.hbits = hbits
         return out.view(B, N, 3)
 
     @staticmethod
@@ -293,7 +302,7 @@ class NoisePredictorFn(torch.autograd.Function):
                     dz, g, dd = _hip.resblock_bwd16(dd, w2t, w1t, hk, g,
                                                     seed=ctx.seeds[k - 1] if k else 0,
                                                     p=ctx.ps[k - 1] if k else 0.0,
-                                                    dropout_copy=k > 0)
+                                                    dropout_copy=k > 0, hbits=ctx.hbits[k])
                     grads[o], grads[o + 1] = _hip.linear_wgrad_ex(dz, xbk)
                     continue
                 dz = _hip.gemm_ex(dd, tw[o + 2], epilogue=_hip.EP_RELU_MASK, aux=hk)

@@ -592,3 +592,30 @@ def test_bn_train_stats_matches_stats_then_coeffs(H, O):
             assert torch.equal(x, y)
         if with_run:
             assert torch.equal(rm1, rm2) and torch.equal(rv1, rv2)
+
+
+@pytest.mark.parametrize("M", [240000, 1000, 129, 1])
+@pytest.mark.parametrize("half", [torch.float16, torch.bfloat16])
+def test_resblock_mask_bits(H, M, half):
+    """resblock_fwd16(mask_bits=True) writes bit j of word w of row m = [h[m, 32w + j] > 0] of the
+    h it returns (h and x' unchanged), and resblock_bwd16(hbits=) -- the mask from those bits,
+    h not read -- gives the bits of the h-mask backward, ragged M included."""
+    torch.manual_seed(M + 3)
+    x = torch.randn(M, 256, device="cuda").to(half)
+    w1 = (torch.randn(512, 256, device="cuda") * 0.06).to(half)
+    w2 = (torch.randn(256, 512, device="cuda") * 0.04).to(half)
+    b1 = torch.randn(512, device="cuda") * 0.1
+    b2 = torch.randn(256, device="cuda") * 0.1
+    h_ref, xo_ref = H.resblock_fwd16(x, w1, b1, w2, b2, seed=11, p=0.2)
+    h, xo, bits = H.resblock_fwd16(x, w1, b1, w2, b2, seed=11, p=0.2, mask_bits=True)
+    assert torch.equal(h, h_ref) and torch.equal(xo, xo_ref)
+    pos = (h.view(torch.int16) > 0).view(M, 16, 32).to(torch.int64)
+    want = (pos << torch.arange(32, device="cuda")).sum(-1)
+    assert torch.equal(bits.to(torch.int64) & 0xFFFFFFFF, want & 0xFFFFFFFF)
+    dd = torch.randn(M, 256, device="cuda").to(half)
+    g = torch.randn(M, 256, device="cuda").to(half)
+    w2t, w1t = w2.t().contiguous(), w1.t().contiguous()
+    ref = H.resblock_bwd16(dd, w2t, w1t, h, g, seed=5, p=0.3, dropout_copy=True)
+    got = H.resblock_bwd16(dd, w2t, w1t, None, g, seed=5, p=0.3, dropout_copy=True, hbits=bits)
+    for a, b in zip(ref, got):
+        assert torch.equal(a, b)

@@ -46,6 +46,9 @@ def apply():
     if "PCST_FUSED_BLOCK_BWD" in e:
         from pointcloud_style_transfer_amd.models import _autograd
         _autograd.FUSED_BLOCK_BWD = e["PCST_FUSED_BLOCK_BWD"] != "0"
+    if "PCST_MASK_BITS" in e:
+        from pointcloud_style_transfer_amd.models import _autograd
+        _autograd.MASK_BITS = e["PCST_MASK_BITS"] != "0"
     if "PCST_FUSED_BN_STATS" in e:
         from pointcloud_style_transfer_amd.models import _autograd
         _autograd.FUSED_BN_STATS = e["PCST_FUSED_BN_STATS"] != "0"
