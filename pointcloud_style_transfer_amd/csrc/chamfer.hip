@@ -890,6 +890,140 @@ __global__ __launch_bounds__(256) void cg_rowmin_kernel(int N, int M,
   }
 }
 
+// ---- The rows over the ring budget (hybrid mode) by box pruning.  Each cloud's cell-sorted
+// points are cut into boxes of kCgBoxPts consecutive points (a run of neighbouring cells) with
+// their exact bounding boxes.  One wave per row: the boxes' distance lower bounds (lane = box),
+// the nearest box scanned for a first best (lane = point), then every box the ring search's own
+// conservative test (lb * shrink - err > best) cannot rule out.  Pairs are scored by cd_dist and
+// ranked by (clamped value, original index) as in cg_rowmin_kernel: the exhaustive first-index
+// argmin, bit for bit, in any visiting order.  A far row scans a few boxes instead of M points.
+constexpr int kCgBoxPts = 64;
+
+// boxes[slot][box] = {lo.xyz, hi.xyz} of sorted points [64 box, 64 box + 64) (NaN points drop out)
+__global__ __launch_bounds__(256) void cg_box_kernel(int N, int M, const float4* __restrict__ sorted,
+                                                     float4* __restrict__ boxes) {
+  const int b = blockIdx.y, side = blockIdx.z;
+  const int n = side ? M : N;
+  const int NM = N > M ? N : M;
+  const int nbs = (NM + kCgBoxPts - 1) / kCgBoxPts;
+  const int box = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (box * kCgBoxPts >= n) return;  // wave-uniform
+  const int i = box * kCgBoxPts + (threadIdx.x & 63);
+  const int64_t slot = b * 2 + side;
+  float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+  if (i < n) {
+    const float4 q = sorted[slot * NM + i];
+    lo[0] = hi[0] = q.x;
+    lo[1] = hi[1] = q.y;
+    lo[2] = hi[2] = q.z;
+  }
+#pragma unroll
+  for (int a = 0; a < 3; ++a)
+    for (int off = 32; off >= 1; off >>= 1) {
+      lo[a] = fminf(lo[a], __shfl_xor(lo[a], off));
+      hi[a] = fmaxf(hi[a], __shfl_xor(hi[a], off));
+    }
+  if ((threadIdx.x & 63) == 0) {
+    boxes[(slot * nbs + box) * 2] = make_float4(lo[0], lo[1], lo[2], 0.0f);
+    boxes[(slot * nbs + box) * 2 + 1] = make_float4(hi[0], hi[1], hi[2], 0.0f);
+  }
+}
+
+// (v, j) into (best, bi) by (value, index); NaN never enters
+__device__ __forceinline__ void cg_take(float v, int j, float& best, int& bi) {
+  if (v < best || (v == best && j < bi)) {
+    best = v;
+    bi = j;
+  }
+}
+
+__device__ __forceinline__ void cg_wave_argmin(float& best, int& bi) {
+  for (int off = 32; off >= 1; off >>= 1) {
+    const float ov = __shfl_xor(best, off);
+    const int oj = __shfl_xor(bi, off);
+    cg_take(ov, oj, best, bi);
+  }
+}
+
+// grid (blocks, B, 2): the waves of (cloud b, side) stride over that side's overflow list
+__global__ __launch_bounds__(256) void cg_list_box_kernel(
+    const float* __restrict__ P, const float* __restrict__ Q, int N, int M,
+    const CgGrid* __restrict__ grids, const float4* __restrict__ sorted,
+    const int* __restrict__ sidx, const float4* __restrict__ boxes,
+    const int* __restrict__ ovf_count, const int* __restrict__ ovf_rows, float* __restrict__ min1,
+    int32_t* __restrict__ arg1, float* __restrict__ min2, int32_t* __restrict__ arg2) {
+  const int b = blockIdx.y, side = blockIdx.z;  // side 0: pred rows vs the target's boxes
+  const int NM = N > M ? N : M;
+  const int nbs = (NM + kCgBoxPts - 1) / kCgBoxPts;
+  const int64_t rs = b * 2 + side, ts = b * 2 + 1 - side;
+  const int m = side ? N : M;  // the other cloud's points
+  const int nbox = (m + kCgBoxPts - 1) / kCgBoxPts;
+  const int lane = threadIdx.x & 63;
+  const int count = ovf_count[rs];
+  const int* __restrict__ L = ovf_rows + rs * NM;
+  const float4* __restrict__ T = sorted + ts * NM;
+  const int* __restrict__ TI = sidx + ts * NM;
+  const float4* __restrict__ Bx = boxes + ts * nbs * 2;
+  const float gnmax = grids[ts].nmax;
+  const float shrink = 1.0f - 8.0f * kCgU;
+  const int waves = gridDim.x * 4;
+  for (int k = blockIdx.x * 4 + (int)(threadIdx.x >> 6); k < count; k += waves) {
+    const int row = L[k];
+    const float* X = side ? Q + ((int64_t)b * M + row) * 3 : P + ((int64_t)b * N + row) * 3;
+    const float px = X[0], py = X[1], pz = X[2];
+    const float np_ = sqnorm3(px, py, pz);
+    const float err = 16.0f * kCgU * (np_ + gnmax) + 1e-30f;
+    auto box_lb = [&](int c) {
+      const float4 lo = Bx[2 * c], hi = Bx[2 * c + 1];
+      const float gx = cg_axis_gap(px, lo.x, hi.x), gy = cg_axis_gap(py, lo.y, hi.y);
+      const float gz = cg_axis_gap(pz, lo.z, hi.z);
+      return gx * gx + gy * gy + gz * gz;
+    };
+    float best = INFINITY;
+    int bi = 0x7fffffff;
+    auto scan = [&](int c) {  // lane = point of box c
+      const int kk = c * kCgBoxPts + lane;
+      if (kk < m) {
+        const float4 q = T[kk];
+        float v = cd_dist(px, py, pz, np_, q.x, q.y, q.z, q.w);
+        v = v < 0.0f ? 0.0f : v;
+        cg_take(v, TI[kk], best, bi);
+      }
+    };
+    // the box of the smallest lower bound gives the first best
+    float lmin = INFINITY;
+    int cmin = 0;
+    for (int c = lane; c < nbox; c += 64) cg_take(box_lb(c), c, lmin, cmin);
+    cg_wave_argmin(lmin, cmin);
+    cmin = __builtin_amdgcn_readfirstlane(cmin);
+    scan(cmin);
+    // every other box the bound cannot rule out (lane = box, then the candidates in turn)
+    for (int c0 = 0; c0 < nbox; c0 += 64) {
+      cg_wave_argmin(best, bi);
+      const int c = c0 + lane;
+      bool cand = false;
+      if (c < nbox && c != cmin) cand = !(box_lb(c) * shrink - err > best);
+      uint64_t mask = __ballot(cand);
+      while (mask) {
+        const int bit = __builtin_ctzll(mask);
+        mask &= mask - 1;
+        scan(c0 + bit);
+      }
+    }
+    cg_wave_argmin(best, bi);
+    if (lane == 0) {
+      if (bi == 0x7fffffff) bi = 0;  // no comparable pair (NaN row)
+      if (side == 0) {
+        min1[(int64_t)b * N + row] = best;
+        arg1[(int64_t)b * N + row] = bi;
+      } else {
+        min2[(int64_t)b * M + row] = best;
+        arg2[(int64_t)b * M + row] = bi;
+      }
+    }
+  }
+}
+
 struct CgWS {
   CgGrid* grids;
   int* counts;     // [B][2][kCgMaxCells + 1]
@@ -900,6 +1034,7 @@ struct CgWS {
   int* sidx;       // [B][2][NM]
   int* ovf_count;  // [B][2]       hybrid mode: rows over the ring budget
   int* ovf_rows;   // [B][2][NM]
+  float4* boxes;   // [B][2][NM / kCgBoxPts][2]  hybrid mode: sorted-point boxes (lo, hi)
   size_t bytes;
 };
 static CgWS carve_cg(void* base, int64_t B, int64_t N, int64_t M) {
@@ -915,6 +1050,7 @@ static CgWS carve_cg(void* base, int64_t B, int64_t N, int64_t M) {
   w.sidx = c.take<int>(B * 2 * NM);
   w.ovf_count = c.take<int>(B * 2);
   w.ovf_rows = c.take<int>(B * 2 * NM);
+  w.boxes = c.take<float4>(B * 2 * cdiv(NM, kCgBoxPts) * 2);
   w.bytes = c.bytes();
   return w;
 }
@@ -929,12 +1065,15 @@ static inline int64_t cd_padded(int64_t n) { return cdiv(n, kCdChunk) * kCdChunk
 // but a row far outside the other cloud's grid has to search the thin shell of points within
 // its nearest distance, which grows with the distance: a noisy predicted x0 against its target
 // (the trainer's early timesteps) measured 46-60 ms.  The hybrid mode (3, and the default 0)
-// bounds that: the grid search gives up after kCgRingBudget rings and the exhaustive row-min
-// serves the rows it gave up on (a list per cloud and side), so a direction costs at most about
-// the exhaustive pass plus the budgeted rings.  Measured on the trainer's pair (a predicted x0
+// bounds that: the grid search gives up after kCgRingBudget rings and the rows it gave up on (a
+// list per cloud and side) are served by box pruning (cg_list_box_kernel; PCST_X_CD_BOX=0: the
+// exhaustive row-min over the list, which bounds a direction by the exhaustive pass).  Measured on the trainer's pair (a predicted x0
 // = lidar-like target + noise, 8 x 30000 per side, tools/cd_sweep.sh): noise 0.02: exhaustive
 // 2.08 ms, grid 0.32, hybrid 0.34; noise 0.2: 2.10 / 1.34 / 1.43; noise 1: 2.09 / 16.9 / 1.25;
 // noise 4: 2.10 / 62.5 / 1.28.  All modes give bit-identical minima and first-index argmins.
+#ifndef PCST_X_CD_BOX  // the overflow rows by box pruning; 0: the exhaustive list row-min (A/B)
+#define PCST_X_CD_BOX 1
+#endif
 #ifndef PCST_X_CG_RING_BUDGET  // experiment builds may override
 #define PCST_X_CG_RING_BUDGET 2
 #endif
@@ -983,7 +1122,7 @@ extern "C" int pcst_chamfer_fwd(const float* pred, const float* target, int64_t 
     PCST_HIP(hipMemsetAsync(w.counts, 0, sizeof(int) * B * 2 * (kCgMaxCells + 1), s), "memset");
     if (hybrid) {
       PCST_HIP(hipMemsetAsync(w.ovf_count, 0, sizeof(int) * B * 2, s), "memset");
-      pack();
+      if (!PCST_X_CD_BOX) pack();
     }
     hipLaunchKernelGGL(cg_stats_kernel, dim3(b, 2), dim3(1024), 0, s, pred, target, (int)N, (int)M,
                        w.grids);
@@ -998,7 +1137,15 @@ extern "C" int pcst_chamfer_fwd(const float* pred, const float* target, int64_t 
     hipLaunchKernelGGL(cg_rowmin_kernel, pg, dim3(256), 0, s, (int)N, (int)M, w.grids, w.starts,
                        w.sorted, w.sidx, min1, arg1, min2, arg2, hybrid ? kCgRingBudget : 0,
                        w.ovf_count, w.ovf_rows);
-    if (hybrid) {  // the rows over budget, exhaustively (grid over the list's upper bound)
+    if (hybrid && PCST_X_CD_BOX) {  // the rows over budget: box-pruned scans
+      const int nbs = (int)cdiv(NM, kCgBoxPts);
+      hipLaunchKernelGGL(cg_box_kernel, dim3((unsigned)cdiv(nbs, 4), b, 2), dim3(256), 0, s, (int)N,
+                         (int)M, w.sorted, w.boxes);
+      const unsigned lb = (unsigned)std::min<int64_t>(cdiv(NM, 64), 128);
+      hipLaunchKernelGGL(cg_list_box_kernel, dim3(lb, b, 2), dim3(256), 0, s, pred, target, (int)N,
+                         (int)M, w.grids, w.sorted, w.sidx, w.boxes, w.ovf_count, w.ovf_rows, min1,
+                         arg1, min2, arg2);
+    } else if (hybrid) {  // the rows over budget, exhaustively (grid over the list's upper bound)
       constexpr int LS = PCST_X_CD_LIST_S, LR = PCST_X_CD_LIST_R;
       hipLaunchKernelGGL((chamfer_rowmin_kernel<LS, LR, true>), dim3((unsigned)cdiv(N, 256 * LR), b),
                          dim3(256 * LS), 0, s, pred, Tp, (int)N, (int)M, (int)Mp, min1, arg1,
