@@ -892,23 +892,31 @@ __global__ __launch_bounds__(256) void cg_rowmin_kernel(int N, int M,
 
 // ---- The rows over the ring budget (hybrid mode) by box pruning.  Each cloud's cell-sorted
 // points are cut into boxes of kCgBoxPts consecutive points (a run of neighbouring cells) with
-// their exact bounding boxes.  One wave per row: the boxes' distance lower bounds (lane = box),
-// the nearest box scanned for a first best (lane = point), then every box the ring search's own
-// conservative test (lb * shrink - err > best) cannot rule out.  Pairs are scored by cd_dist and
-// ranked by (clamped value, original index) as in cg_rowmin_kernel: the exhaustive first-index
-// argmin, bit for bit, in any visiting order.  A far row scans a few boxes instead of M points.
+// their exact bounding boxes, and the boxes into superboxes of kCgSbBoxes.  One wave per row:
+// the superboxes' distance lower bounds (lane = superbox), the nearest box of the nearest
+// superbox scanned for a first best (lane = point), then, eight kept superboxes at a time (lane =
+// one of their boxes), every box the ring search's own conservative test (lb * shrink - err >
+// best) cannot rule out.  Pairs are scored by cd_dist and ranked by (clamped value, original
+// index) as in cg_rowmin_kernel: the exhaustive first-index argmin, bit for bit, in any visiting
+// order.  A far row scans a few boxes (5-6 on average, tools/cd_box_probe.py) instead of M points.
 constexpr int kCgBoxPts = 64;
+constexpr int kCgSbBoxes = 8;
 
-// boxes[slot][box] = {lo.xyz, hi.xyz} of sorted points [64 box, 64 box + 64) (NaN points drop out)
-__global__ __launch_bounds__(256) void cg_box_kernel(int N, int M, const float4* __restrict__ sorted,
-                                                     float4* __restrict__ boxes) {
+// boxes[slot][box] = {lo.xyz, hi.xyz} of sorted points [64 box, 64 box + 64), sboxes[slot][sb]
+// the same over boxes [8 sb, 8 sb + 8) (NaN points drop out).  One 512-thread block per superbox.
+__global__ __launch_bounds__(512) void cg_box_kernel(int N, int M, const float4* __restrict__ sorted,
+                                                     float4* __restrict__ boxes,
+                                                     float4* __restrict__ sboxes) {
   const int b = blockIdx.y, side = blockIdx.z;
   const int n = side ? M : N;
   const int NM = N > M ? N : M;
   const int nbs = (NM + kCgBoxPts - 1) / kCgBoxPts;
-  const int box = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (box * kCgBoxPts >= n) return;  // wave-uniform
-  const int i = box * kCgBoxPts + (threadIdx.x & 63);
+  const int nss = (nbs + kCgSbBoxes - 1) / kCgSbBoxes;
+  const int sb = blockIdx.x;
+  if (sb * kCgSbBoxes * kCgBoxPts >= n) return;  // block-uniform
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int box = sb * kCgSbBoxes + w;
+  const int i = box * kCgBoxPts + lane;
   const int64_t slot = b * 2 + side;
   float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
   if (i < n) {
@@ -923,9 +931,28 @@ __global__ __launch_bounds__(256) void cg_box_kernel(int N, int M, const float4*
       lo[a] = fminf(lo[a], __shfl_xor(lo[a], off));
       hi[a] = fmaxf(hi[a], __shfl_xor(hi[a], off));
     }
-  if ((threadIdx.x & 63) == 0) {
-    boxes[(slot * nbs + box) * 2] = make_float4(lo[0], lo[1], lo[2], 0.0f);
-    boxes[(slot * nbs + box) * 2 + 1] = make_float4(hi[0], hi[1], hi[2], 0.0f);
+  __shared__ float red[kCgSbBoxes][6];
+  if (lane == 0) {
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+      red[w][a] = lo[a];
+      red[w][3 + a] = hi[a];
+    }
+    if (box * kCgBoxPts < n) {
+      boxes[(slot * nbs + box) * 2] = make_float4(lo[0], lo[1], lo[2], 0.0f);
+      boxes[(slot * nbs + box) * 2 + 1] = make_float4(hi[0], hi[1], hi[2], 0.0f);
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int v = 1; v < kCgSbBoxes; ++v)
+#pragma unroll
+      for (int a = 0; a < 3; ++a) {
+        lo[a] = fminf(lo[a], red[v][a]);
+        hi[a] = fmaxf(hi[a], red[v][3 + a]);
+      }
+    sboxes[(slot * nss + sb) * 2] = make_float4(lo[0], lo[1], lo[2], 0.0f);
+    sboxes[(slot * nss + sb) * 2 + 1] = make_float4(hi[0], hi[1], hi[2], 0.0f);
   }
 }
 
@@ -937,8 +964,9 @@ __device__ __forceinline__ void cg_take(float v, int j, float& best, int& bi) {
   }
 }
 
+template <int kFrom = 32>
 __device__ __forceinline__ void cg_wave_argmin(float& best, int& bi) {
-  for (int off = 32; off >= 1; off >>= 1) {
+  for (int off = kFrom; off >= 1; off >>= 1) {
     const float ov = __shfl_xor(best, off);
     const int oj = __shfl_xor(bi, off);
     cg_take(ov, oj, best, bi);
@@ -950,20 +978,24 @@ __global__ __launch_bounds__(256) void cg_list_box_kernel(
     const float* __restrict__ P, const float* __restrict__ Q, int N, int M,
     const CgGrid* __restrict__ grids, const float4* __restrict__ sorted,
     const int* __restrict__ sidx, const float4* __restrict__ boxes,
-    const int* __restrict__ ovf_count, const int* __restrict__ ovf_rows, float* __restrict__ min1,
-    int32_t* __restrict__ arg1, float* __restrict__ min2, int32_t* __restrict__ arg2) {
+    const float4* __restrict__ sboxes, const int* __restrict__ ovf_count,
+    const int* __restrict__ ovf_rows, float* __restrict__ min1, int32_t* __restrict__ arg1,
+    float* __restrict__ min2, int32_t* __restrict__ arg2) {
   const int b = blockIdx.y, side = blockIdx.z;  // side 0: pred rows vs the target's boxes
   const int NM = N > M ? N : M;
   const int nbs = (NM + kCgBoxPts - 1) / kCgBoxPts;
+  const int nss = (nbs + kCgSbBoxes - 1) / kCgSbBoxes;
   const int64_t rs = b * 2 + side, ts = b * 2 + 1 - side;
   const int m = side ? N : M;  // the other cloud's points
   const int nbox = (m + kCgBoxPts - 1) / kCgBoxPts;
+  const int nsb = (nbox + kCgSbBoxes - 1) / kCgSbBoxes;
   const int lane = threadIdx.x & 63;
   const int count = ovf_count[rs];
   const int* __restrict__ L = ovf_rows + rs * NM;
   const float4* __restrict__ T = sorted + ts * NM;
   const int* __restrict__ TI = sidx + ts * NM;
   const float4* __restrict__ Bx = boxes + ts * nbs * 2;
+  const float4* __restrict__ Sx = sboxes + ts * nss * 2;
   const float gnmax = grids[ts].nmax;
   const float shrink = 1.0f - 8.0f * kCgU;
   const int waves = gridDim.x * 4;
@@ -973,8 +1005,8 @@ __global__ __launch_bounds__(256) void cg_list_box_kernel(
     const float px = X[0], py = X[1], pz = X[2];
     const float np_ = sqnorm3(px, py, pz);
     const float err = 16.0f * kCgU * (np_ + gnmax) + 1e-30f;
-    auto box_lb = [&](int c) {
-      const float4 lo = Bx[2 * c], hi = Bx[2 * c + 1];
+    auto lbound = [&](const float4* __restrict__ Bs, int c) {
+      const float4 lo = Bs[2 * c], hi = Bs[2 * c + 1];
       const float gx = cg_axis_gap(px, lo.x, hi.x), gy = cg_axis_gap(py, lo.y, hi.y);
       const float gz = cg_axis_gap(pz, lo.z, hi.z);
       return gx * gx + gy * gy + gz * gz;
@@ -990,27 +1022,52 @@ __global__ __launch_bounds__(256) void cg_list_box_kernel(
         cg_take(v, TI[kk], best, bi);
       }
     };
-    // the box of the smallest lower bound gives the first best
+    // the first best: the nearest box (by bound) of the nearest superbox
     float lmin = INFINITY;
-    int cmin = 0;
-    for (int c = lane; c < nbox; c += 64) cg_take(box_lb(c), c, lmin, cmin);
-    cg_wave_argmin(lmin, cmin);
+    int smin = 0;
+    for (int c = lane; c < nsb; c += 64) cg_take(lbound(Sx, c), c, lmin, smin);
+    cg_wave_argmin(lmin, smin);
+    smin = __builtin_amdgcn_readfirstlane(smin);
+    lmin = INFINITY;
+    int cmin = smin * kCgSbBoxes;
+    {
+      const int c = smin * kCgSbBoxes + (lane & (kCgSbBoxes - 1));
+      if (c < nbox) cg_take(lbound(Bx, c), c, lmin, cmin);
+    }
+    cg_wave_argmin<kCgSbBoxes / 2>(lmin, cmin);
     cmin = __builtin_amdgcn_readfirstlane(cmin);
     scan(cmin);
-    // every other box the bound cannot rule out (lane = box, then the candidates in turn)
-    for (int c0 = 0; c0 < nbox; c0 += 64) {
+#ifdef PCST_X_CG_BOX_STATS
+    int nscan = 1;
+#endif
+    // the superboxes the bound keeps, eight at a time: lane group g takes the g-th kept one
+    for (int s0 = 0; s0 < nsb; s0 += 64) {
       cg_wave_argmin(best, bi);
-      const int c = c0 + lane;
-      bool cand = false;
-      if (c < nbox && c != cmin) cand = !(box_lb(c) * shrink - err > best);
-      uint64_t mask = __ballot(cand);
-      while (mask) {
-        const int bit = __builtin_ctzll(mask);
-        mask &= mask - 1;
-        scan(c0 + bit);
+      const int sc = s0 + lane;
+      uint64_t smask = __ballot(sc < nsb && !(lbound(Sx, sc) * shrink - err > best));
+      while (smask) {
+        cg_wave_argmin(best, bi);  // the tightest bound so far for this batch's boxes
+        uint64_t mg = smask;
+        for (int g = 0; g < (lane >> 3); ++g) mg &= mg - 1;
+#pragma unroll
+        for (int g = 0; g < 64 / kCgSbBoxes; ++g) smask &= smask - 1;
+        const int c = mg ? (s0 + __builtin_ctzll(mg)) * kCgSbBoxes + (lane & (kCgSbBoxes - 1)) : nbox;
+        uint64_t bmask = __ballot(c < nbox && c != cmin && !(lbound(Bx, c) * shrink - err > best));
+        while (bmask) {
+          const int bit = __builtin_ctzll(bmask);
+          bmask &= bmask - 1;
+#ifdef PCST_X_CG_BOX_STATS
+          ++nscan;
+#endif
+          scan(__builtin_amdgcn_readlane(c, bit));
+        }
       }
     }
     cg_wave_argmin(best, bi);
+#ifdef PCST_X_CG_BOX_STATS  // experiment builds (tools/cd_box_probe.py): -1 and the scanned boxes
+    best = -1.0f;
+    bi = nscan;
+#endif
     if (lane == 0) {
       if (bi == 0x7fffffff) bi = 0;  // no comparable pair (NaN row)
       if (side == 0) {
@@ -1035,6 +1092,7 @@ struct CgWS {
   int* ovf_count;  // [B][2]       hybrid mode: rows over the ring budget
   int* ovf_rows;   // [B][2][NM]
   float4* boxes;   // [B][2][NM / kCgBoxPts][2]  hybrid mode: sorted-point boxes (lo, hi)
+  float4* sboxes;  // [B][2][boxes / kCgSbBoxes][2]  and their superboxes
   size_t bytes;
 };
 static CgWS carve_cg(void* base, int64_t B, int64_t N, int64_t M) {
@@ -1051,6 +1109,7 @@ static CgWS carve_cg(void* base, int64_t B, int64_t N, int64_t M) {
   w.ovf_count = c.take<int>(B * 2);
   w.ovf_rows = c.take<int>(B * 2 * NM);
   w.boxes = c.take<float4>(B * 2 * cdiv(NM, kCgBoxPts) * 2);
+  w.sboxes = c.take<float4>(B * 2 * cdiv(cdiv(NM, kCgBoxPts), kCgSbBoxes) * 2);
   w.bytes = c.bytes();
   return w;
 }
@@ -1139,11 +1198,11 @@ extern "C" int pcst_chamfer_fwd(const float* pred, const float* target, int64_t 
                        w.ovf_count, w.ovf_rows);
     if (hybrid && PCST_X_CD_BOX) {  // the rows over budget: box-pruned scans
       const int nbs = (int)cdiv(NM, kCgBoxPts);
-      hipLaunchKernelGGL(cg_box_kernel, dim3((unsigned)cdiv(nbs, 4), b, 2), dim3(256), 0, s, (int)N,
-                         (int)M, w.sorted, w.boxes);
+      hipLaunchKernelGGL(cg_box_kernel, dim3((unsigned)cdiv(nbs, kCgSbBoxes), b, 2), dim3(512), 0, s,
+                         (int)N, (int)M, w.sorted, w.boxes, w.sboxes);
       const unsigned lb = (unsigned)std::min<int64_t>(cdiv(NM, 64), 128);
       hipLaunchKernelGGL(cg_list_box_kernel, dim3(lb, b, 2), dim3(256), 0, s, pred, target, (int)N,
-                         (int)M, w.grids, w.sorted, w.sidx, w.boxes, w.ovf_count, w.ovf_rows, min1,
+                         (int)M, w.grids, w.sorted, w.sidx, w.boxes, w.sboxes, w.ovf_count, w.ovf_rows, min1,
                          arg1, min2, arg2);
     } else if (hybrid) {  // the rows over budget, exhaustively (grid over the list's upper bound)
       constexpr int LS = PCST_X_CD_LIST_S, LR = PCST_X_CD_LIST_R;
