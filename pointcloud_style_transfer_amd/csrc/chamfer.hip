@@ -1025,7 +1025,12 @@ __global__ __launch_bounds__(256) void cg_list_box_kernel(
     // the first best: the nearest box (by bound) of the nearest superbox
     float lmin = INFINITY;
     int smin = 0;
-    for (int c = lane; c < nsb; c += 64) cg_take(lbound(Sx, c), c, lmin, smin);
+    float slb = INFINITY;  // this lane's superbox bound among the first 64 (reused below)
+    for (int c = lane; c < nsb; c += 64) {
+      const float v = lbound(Sx, c);
+      if (c < 64) slb = v;
+      cg_take(v, c, lmin, smin);
+    }
     cg_wave_argmin(lmin, smin);
     smin = __builtin_amdgcn_readfirstlane(smin);
     lmin = INFINITY;
@@ -1044,7 +1049,7 @@ __global__ __launch_bounds__(256) void cg_list_box_kernel(
     for (int s0 = 0; s0 < nsb; s0 += 64) {
       cg_wave_argmin(best, bi);
       const int sc = s0 + lane;
-      uint64_t smask = __ballot(sc < nsb && !(lbound(Sx, sc) * shrink - err > best));
+      uint64_t smask = __ballot(sc < nsb && !((s0 ? lbound(Sx, sc) : slb) * shrink - err > best));
       while (smask) {
         cg_wave_argmin(best, bi);  // the tightest bound so far for this batch's boxes
         uint64_t mg = smask;
@@ -1130,6 +1135,9 @@ static inline int64_t cd_padded(int64_t n) { return cdiv(n, kCdChunk) * kCdChunk
 // = lidar-like target + noise, 8 x 30000 per side, tools/cd_sweep.sh): noise 0.02: exhaustive
 // 2.08 ms, grid 0.32, hybrid 0.34; noise 0.2: 2.10 / 1.34 / 1.43; noise 1: 2.09 / 16.9 / 1.25;
 // noise 4: 2.10 / 62.5 / 1.28.  All modes give bit-identical minima and first-index argmins.
+#ifndef PCST_X_CG_LIST_BLOCKS  // blocks (4 waves) per cloud and side of cg_list_box_kernel
+#define PCST_X_CG_LIST_BLOCKS 512  // r04 a48: 512 9.61-9.65 ms per trainer step, 128 9.80-9.89
+#endif
 #ifndef PCST_X_CD_BOX  // the overflow rows by box pruning; 0: the exhaustive list row-min (A/B)
 #define PCST_X_CD_BOX 1
 #endif
@@ -1200,7 +1208,7 @@ extern "C" int pcst_chamfer_fwd(const float* pred, const float* target, int64_t 
       const int nbs = (int)cdiv(NM, kCgBoxPts);
       hipLaunchKernelGGL(cg_box_kernel, dim3((unsigned)cdiv(nbs, kCgSbBoxes), b, 2), dim3(512), 0, s,
                          (int)N, (int)M, w.sorted, w.boxes, w.sboxes);
-      const unsigned lb = (unsigned)std::min<int64_t>(cdiv(NM, 64), 128);
+      const unsigned lb = (unsigned)std::min<int64_t>(cdiv(NM, 64), PCST_X_CG_LIST_BLOCKS);
       hipLaunchKernelGGL(cg_list_box_kernel, dim3(lb, b, 2), dim3(256), 0, s, pred, target, (int)N,
                          (int)M, w.grids, w.sorted, w.sidx, w.boxes, w.sboxes, w.ovf_count, w.ovf_rows, min1,
                          arg1, min2, arg2);
