@@ -249,6 +249,28 @@ def test_chamfer_grid_equals_exhaustive_30k(kind):
             np.testing.assert_array_equal(x, y)
 
 
+def test_chamfer_hybrid_nan_and_far_rows_match_exhaustive():
+    """Rows the hybrid's grid search gives up on (far outside the other cloud, and NaN rows whose
+    box bounds prune nothing) and NaN target points: the box-pruned path returns what the
+    exhaustive row-min returns, bit for bit (NaN pairs never win; a row with no comparable pair
+    gets (inf, 0))."""
+    from pointcloud_style_transfer_amd import _hip
+
+    rng = np.random.default_rng(5)
+    B, N, M = 2, 5000, 4000
+    q = rng.standard_normal((B, M, 3)).astype(np.float32)
+    p = (rng.standard_normal((B, N, 3)) * np.array([1.0, 1.0, 60.0])).astype(np.float32)
+    p[:, :7] = np.nan
+    p[1, 100:130, 1] = np.nan
+    q[:, 50:60] = np.nan
+    res = {}
+    for mode in (1, 3):
+        out, a1, a2 = _hip.chamfer_fwd(dev(p), dev(q), mode)
+        res[mode] = (out.cpu().numpy(), a1.cpu().numpy(), a2.cpu().numpy())
+    for x, y in zip(res[1], res[3]):
+        np.testing.assert_array_equal(x, y)
+
+
 def test_chamfer_determinism(mods):
     L = mods["losses"]
     rng = np.random.default_rng(0)
