@@ -154,9 +154,9 @@ def main():
                                    "(BASELINE configs[2]; configs[3] under torchrun)",
                        "clouds_per_gpu": B, "global_batch": world * B, "points": args.points,
                        "parallelism": f"ddp{world}" if world > 1 else "single"},
-            "chamfer_fwd": {"product_mode": "0 (hybrid: budgeted grid search + exhaustive "
-                                            "overflow rows; evaluates a data-dependent subset of "
-                                            "the pairs)",
+            "chamfer_fwd": {"product_mode": "0 (hybrid: budgeted grid search, then a "
+                                            "box-pruned search for the rows it gives up on; "
+                                            "evaluates a data-dependent subset of the pairs)",
                             "product_avg_launch_ms": round(ch_ms, 3) if ch_ms else None,
                             "exhaustive_ms_same_inputs": round(ex_ms, 3) if ex_ms else None,
                             "speedup_vs_exhaustive": round(ex_ms / ch_ms, 2) if ex_ms and ch_ms else None,
