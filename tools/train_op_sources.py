@@ -50,7 +50,7 @@ def main():
     torch.cuda.synchronize()
     from torch.profiler import ProfilerActivity, profile
 
-    with profile(activities=[ProfilerActivity.CPU], with_stack=True, record_shapes=False) as prof:
+    with profile(activities=[ProfilerActivity.CPU], with_stack=True, record_shapes=True) as prof:
         for i in range(a.steps):
             tr.train_step(batch, i, 1 << 30, next_batch=batch if i + 1 < a.steps else None)
         torch.cuda.synchronize()
@@ -65,6 +65,12 @@ def main():
                 break
         counts[(ev.key, frame)] += ev.count
     out = [{"op": k[0], "where": k[1], "per_step": v / a.steps} for k, v in counts.most_common(70)]
+    # without python stacks (some builds record none): the same ops by input shapes
+    shapes = collections.Counter()
+    for ev in prof.key_averages(group_by_input_shape=True):
+        if ev.key in OPS:
+            shapes[(ev.key, str(ev.input_shapes)[:160])] += ev.count
+    out += [{"op": k[0], "shapes": k[1], "per_step": v / a.steps} for k, v in shapes.most_common(60)]
     sys.stdout.write(json.dumps(out, indent=0) + "\n")
 
 
