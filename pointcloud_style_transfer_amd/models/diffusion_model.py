@@ -270,11 +270,13 @@ class HierarchicalProcessor:
 # the MLP's last round; tools/b32_probe.py, one box).
 OVERLAP_KNN_BUILD = True
 _OVERLAP_MAX_MLP_POINTS = 2 * 128 * 256
-# LDS floor of the build's work-groups (pcst_knn3_build's lds_floor): just above what an MLP
-# work-group leaves free on its CU (160 - 154.6 KiB), so the build never co-resides with the MLP
-# but packs as many work-groups per idle CU as their own LDS allows (round 2 used a flat 64 KiB
-# pad on every build kernel: 1-2 work-groups per idle CU).
-KNN_BUILD_LDS_FLOOR = 8192
+# LDS floor of the build's work-groups (pcst_knn3_build's lds_floor): above what an MLP
+# work-group leaves free on its CU (160 - 154.6 KiB), so the build never co-resides with the MLP,
+# and 16 KiB rather than the smallest such floor (8 KiB): the driver window measured 2718 / 2722 /
+# 2733 / 2706 vs 2685 / 2709 / 2717 / 2693 steps/s in four alternating pairs over two boxes
+# (profiles/r04/a56, a57); 24 KiB 2725 / 2715.  Round 2 used a flat 64 KiB pad on every build
+# kernel (1-2 work-groups per idle CU).
+KNN_BUILD_LDS_FLOOR = 16384
 # Work-groups per build launch on the side stream (pcst_knn3_build's max_wg): the MLP's last
 # round (469 work-groups on 256 CUs) leaves ~43 CUs idle; a build confined to fewer work-groups
 # than that never holds a CU an MLP work-group of that round is waiting for.
