@@ -642,8 +642,8 @@ def noise_mlp(pts, points_per_cloud, cond, blob, bias, precision, out=None, wait
               signal=None):
     """pts [P,3] (P = clouds*points_per_cloud, cloud-major) -> eps [P,3].
     wait (a DeviceSignal signalled on another stream): work queued after the MLP on this stream
-    is also ordered after that signal -- at precision 2 by the MLP's last work-group
-    (pcst_noise_mlp_then_wait), otherwise by a wait launch after it.
+    is also ordered after that signal -- at precisions 2 and 3 by the MLP's last work-group
+    (pcst_noise_mlp_ex's wait), otherwise by a wait launch after it.
     signal ((flag, value) from DeviceSignal.next_value()): the value is published as the MLP
     launch begins (everything queued before it on this stream is then done) --
     pcst_noise_mlp_ex's start signal."""
@@ -658,9 +658,10 @@ def noise_mlp(pts, points_per_cloud, cond, blob, bias, precision, out=None, wait
         _call("pcst_noise_mlp_ex", _ptr(pts), P, points_per_cloud, _ptr(cond), cond.shape[0],
               _ptr(blob), blob.numel(), _ptr(bias), precision, _ptr(out), fl, val, *w, _stream())
         return out
-    if wait is not None and precision == 2 and P > 0:
-        _call("pcst_noise_mlp_then_wait", _ptr(pts), P, points_per_cloud, _ptr(cond), cond.shape[0],
-              _ptr(blob), blob.numel(), _ptr(bias), _ptr(out), *wait.wait_args(), _stream())
+    if wait is not None and precision in (2, 3) and P > 0:
+        _call("pcst_noise_mlp_ex", _ptr(pts), P, points_per_cloud, _ptr(cond), cond.shape[0],
+              _ptr(blob), blob.numel(), _ptr(bias), precision, _ptr(out), None, 0,
+              *wait.wait_args(), _stream())
         return out
     _call("pcst_noise_mlp", _ptr(pts), P, points_per_cloud, _ptr(cond), cond.shape[0], _ptr(blob),
           blob.numel(), _ptr(bias), precision, _ptr(out), _stream())

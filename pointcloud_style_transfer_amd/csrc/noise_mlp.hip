@@ -1133,6 +1133,588 @@ __global__ __launch_bounds__(kPairThreads) void noise_mlp_pair16_kernel(
   if (wflag) last_group_wait(wflag, wvalue, wcount, werr, wpolls);
 }
 
+// ============================================================================================
+// bf16 "solo" kernel on v_mfma_f32_16x16x32_bf16 (precision code 3).  Every wave owns 32 points
+// (two 16-point column blocks) and ALL features of every layer, so no wave ever needs another
+// wave's activations: there is no partner exchange, and a 1 KiB weight fragment in LDS feeds all
+// 8 waves of the work-group (2 MFMAs each) instead of the 4 waves of one role.  256 points per
+// work-group, 8 waves = 2 per SIMD.
+//
+// Weights stream through a 2-slot ring of 64 KiB *superparts* (64 fragments, packing.py SOLO16)
+// with ONE barrier per superpart: per barrier each wave runs 128 MFMAs (the pair kernel: 32), and
+// each wave DMAs 8 KiB of the next superpart while computing the current one.  Inside a
+// superpart the fragment reads run kD ahead of the MFMAs (asm reads, counted lgkmcnt waits), and
+// the few other LDS reads (biases) are issued at fixed places in the same count.
+//
+// Register budget at two waves per SIMD (256): the residual stream x (32 points x 256 features,
+// fp32) 128, its bf16 operand xb 64, one hidden chunk (32 rows) hc 16 + its operand hb 8, the
+// fragment window 20, biases 8.
+//
+// Residual layers are software-pipelined by one hidden chunk: part k of a layer = [W1(k) | W2(k-1)]
+// and the ReLU/bf16 epilogue of chunk k runs after W2(k-1)'s MFMAs are issued, so it never waits
+// for an MFMA result; part 0 = [W2(15) of the previous layer | W1(0)], the layer-end conversion
+// x -> xb between them (the stream order of packing.py SOLO16).
+namespace solo {
+
+constexpr int kThreads = 512;
+constexpr int kPts = 256;               // points per work-group
+constexpr int kSP = 65536;              // superpart bytes
+constexpr int kNF = kSP / 1024;         // fragments per superpart
+#ifndef PCST_SOLO_KD
+#define PCST_SOLO_KD 3
+#endif
+#ifndef PCST_SOLO_PRIO
+#define PCST_SOLO_PRIO 0
+#endif
+#ifndef PCST_SOLO_STAMPS  // experiment builds (tools/solo_bench.hip): per-wave clock stamps
+#define PCST_SOLO_STAMPS 0
+#endif
+#ifndef PCST_SOLO_EXP  // timing-only experiment builds (wrong results): 1 no DMA after superpart 1,
+#define PCST_SOLO_EXP 0  // 2 no s_barrier, 4 fragments from registers (no LDS fragment reads)
+#endif
+constexpr int kD = PCST_SOLO_KD;        // fragment reads in flight ahead of their MFMAs
+constexpr int kBiasLds = 2 * kSP;       // LDS byte offset of the bias table
+constexpr int kLds = kBiasLds + kBiasFloats * 4;
+constexpr int kTailSP = 3 + 6 * 8;      // first superpart of the output MLP (after h2, x, 6 layers)
+constexpr int kNSP = kTailSP + 4;       // 55
+
+template <int I, int N, class F>
+__device__ __forceinline__ void sfor(F& f) {
+  if constexpr (I < N) {
+    f(std::integral_constant<int, I>{});
+    sfor<I + 1, N>(f);
+  }
+}
+
+// LDS operations issued after the read of fragment f, at its wait in iteration f.  Iteration j
+// issues S::nx(j) extra reads, then the read of fragment j + kD; fragments 0..kD-1 are read
+// before iteration 0.
+template <class S>
+constexpr int frag_after(int f) {
+  int n = (S::NF - 1 - f) < kD ? (S::NF - 1 - f) : kD;
+  for (int j = (f - kD + 1 > 0 ? f - kD + 1 : 0); j <= f; ++j) n += S::nx(j);
+  return n;
+}
+// LDS operations issued after the extra reads of iteration J, at a wait in iteration f >= J
+template <class S>
+constexpr int extra_after(int J, int f) {
+  int n = 0;
+  for (int j = J; j <= f; ++j) n += (j + kD < S::NF) ? 1 : 0;
+  for (int j = J + 1; j <= f; ++j) n += S::nx(j);
+  return n;
+}
+
+template <int N>
+__device__ __forceinline__ void wait_frag(bf16x8& a) {
+  static_assert(N >= 0 && N <= 15, "lgkmcnt range");
+  asm volatile("s_waitcnt lgkmcnt(%1)" : "+v"(a) : "n"(N));
+}
+template <int N>
+__device__ __forceinline__ void wait_f4(f32x4& a) {
+  static_assert(N >= 0 && N <= 15, "lgkmcnt range");
+  asm volatile("s_waitcnt lgkmcnt(%1)" : "+v"(a) : "n"(N));
+}
+template <int N>
+__device__ __forceinline__ void wait_f4x2(f32x4& a, f32x4& b) {
+  static_assert(N >= 0 && N <= 15, "lgkmcnt range");
+  asm volatile("s_waitcnt lgkmcnt(%2)" : "+v"(a), "+v"(b) : "n"(N));
+}
+// one bias row (f32x4) from the LDS table; `off` is a compile-time byte offset.
+// RULE for every asm LDS read here: its result must reach a tied wait (wait_frag / wait_f4) before
+// anything else.  The compiler sees the read's output as written at the asm statement, so an
+// unused result frees its registers at once -- and the data that lands later overwrites whatever
+// the compiler put there (an unused bias read once clobbered a 64-bit address: a memory fault).
+// tools/asm_hazard.py checks the built kernel for reads whose registers are touched before their
+// wait.
+__device__ __forceinline__ f32x4 lds_f4(uint32_t addr, int off) {
+  f32x4 v;
+  if (__builtin_constant_p(off) && off >= 0 && off < 65536)
+    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(v) : "v"(addr), "i"(off));
+  else
+    asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(addr + off));
+  return v;
+}
+
+// PCST_SOLO_PRIO 2 (experiment): waves 4-7 lead the first half of a superpart, waves 0-3 the second
+__device__ __forceinline__ void prio_start() {
+  if (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6) >= 4) __builtin_amdgcn_s_setprio(1);
+  else __builtin_amdgcn_s_setprio(0);
+}
+__device__ __forceinline__ void prio_flip() {
+  if (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6) >= 4) __builtin_amdgcn_s_setprio(0);
+  else __builtin_amdgcn_s_setprio(1);
+}
+
+// One superpart: S::NF fragments at lane address `a` (fragment f at a + 1024 f).  Iteration f:
+// xr(f) (extra reads), the read of fragment f + kD, the counted wait for fragment f, mf(f, frag),
+// dm(f) (DMA of the next superpart), po(f) (epilogues; a wait for extras uses extra_after).
+template <class S, class XR, class MF, class DM, class PO>
+__device__ __forceinline__ void run_sp(uint32_t a, XR& xr, MF& mf, DM& dm, PO& po) {
+  constexpr int NPRO = kD < S::NF ? kD : S::NF;
+  bf16x8 w[kD + 1];
+  auto pro = [&](auto fc) {
+    constexpr int f = decltype(fc)::value;
+    w[f] = lds_read_one(a, f * 1024);
+  };
+  sfor<0, NPRO>(pro);
+  if constexpr ((PCST_SOLO_EXP & 4) != 0) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    for (int i = 0; i <= kD; ++i) w[i] = w[i % NPRO];
+  }
+  auto it = [&](auto fc) {
+    constexpr int f = decltype(fc)::value;
+    xr(fc);
+    if constexpr ((PCST_SOLO_EXP & 4) == 0) {
+      if constexpr (f + kD < S::NF) w[(f + kD) % (kD + 1)] = lds_read_one(a, (f + kD) * 1024);
+      wait_frag<frag_after<S>(f)>(w[f % (kD + 1)]);
+    }
+    mf(fc, w[f % (kD + 1)]);
+    dm(fc);
+    po(fc);
+    if constexpr (PCST_SOLO_PRIO == 2 && f == 31) prio_flip();
+  };
+  if constexpr (PCST_SOLO_PRIO == 2) prio_start();
+  sfor<0, S::NF>(it);
+}
+
+// every wave: its own DMAs have landed and it is done with the current slot; then the barrier
+__device__ __forceinline__ void sp_barrier() {
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  if (!(PCST_SOLO_EXP & 2)) __builtin_amdgcn_s_barrier();
+}
+
+__device__ __forceinline__ f32x4 relu4(f32x4 v) {
+  f32x4 r;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) r[i] = fmaxf(v[i], 0.0f);
+  return r;
+}
+
+// relu(bf16(v)) on packed bf16 pairs: a bf16 with its sign set is a negative int16, so a signed
+// 16-bit max with 0 is the ReLU (-0 included) -- one v_pk_max_i16 per two values, after the
+// conversion (relu then round == round then relu)
+typedef __attribute__((ext_vector_type(8))) short s16x8;
+typedef __attribute__((ext_vector_type(2))) float f32x2;
+typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2;
+// accumulators of row blocks 2s, 2s+1 -> operand of k-step s, one v_cvt_pk_bf16_f32 per pair
+// (pcst::op16 converts element by element: a convert-with-zero plus a v_perm per pair)
+__device__ __forceinline__ bf16x8 opk(const f32x4& lo, const f32x4& hi) {
+  const bf16x2 p0 = __builtin_convertvector((f32x2){lo[0], lo[1]}, bf16x2);
+  const bf16x2 p1 = __builtin_convertvector((f32x2){lo[2], lo[3]}, bf16x2);
+  const bf16x2 p2 = __builtin_convertvector((f32x2){hi[0], hi[1]}, bf16x2);
+  const bf16x2 p3 = __builtin_convertvector((f32x2){hi[2], hi[3]}, bf16x2);
+  return __builtin_shufflevector(__builtin_shufflevector(p0, p1, 0, 1, 2, 3),
+                                 __builtin_shufflevector(p2, p3, 0, 1, 2, 3), 0, 1, 2, 3, 4, 5, 6, 7);
+}
+__device__ __forceinline__ bf16x8 relu_bf16(bf16x8 v) {
+  // (a per-dword form through u32x4 element bit_casts miscompiled to a splat of dword 0 with this
+  // clang, host builds included -- keep the whole-vector form)
+  const s16x8 h = __builtin_elementwise_max(__builtin_bit_cast(s16x8, v), s16x8{0, 0, 0, 0, 0, 0, 0, 0});
+  return __builtin_bit_cast(bf16x8, h);
+}
+
+// schedules: S::nx(j) = extra LDS reads (biases) issued in iteration j
+struct SchH2 {  // h2: fragment f = (row block f/4, k-step f%4); bias of row block rb >= 1 at 4rb-3
+  static constexpr int NF = kNF;
+  static constexpr int nx(int j) { return j % 4 == 1 && j < 60 ? 1 : 0; }
+};
+struct SchX {  // x = W4 h2 (+ cond, loaded before): no extras
+  static constexpr int NF = kNF;
+  static constexpr int nx(int) { return 0; }
+};
+// A W1 chunk's first fragment of row half r (k-step 0) takes its bias b1 as the MFMA's C operand,
+// read two iterations ahead (at iteration 0 for a fragment 0: the read then has the latency of
+// the superpart's first fragment reads).
+struct SchL0 {  // parts 0, 1 of a layer: W2(15)' 0-15, W1(0) 16-31, W1(1) 32-47, W2(0) 48-63;
+                // b2 of row block rb at 15 + rb, b1 at 14, 22 (chunk 0) and 30, 38 (chunk 1)
+  static constexpr int NF = kNF;
+  static constexpr int nx(int j) {
+    return (j >= 15 && j < 31 ? 1 : 0) + (j == 14 || j == 22 || j == 30 || j == 38 ? 1 : 0);
+  }
+};
+struct SchR {  // parts 2m, 2m+1: W1(2m) 0-15, W2(2m-1) 16-31, W1(2m+1) 32-47, W2(2m) 48-63;
+               // b1 at 0, 6 (chunk 2m) and 30, 38 (chunk 2m+1)
+  static constexpr int NF = kNF;
+  static constexpr int nx(int j) { return j == 0 || j == 6 || j == 30 || j == 38 ? 1 : 0; }
+};
+// output MLP: tail fragment t = 64 K + f: W2(15) of layer 5 [0, 16), out0 [16, 144) (bias of row
+// block rb read at t = 21 + 8rb), out1 [144, 208) (bias at t = 149 + 8rb), out2 [208, 212)
+template <int K>
+struct SchT {
+  static constexpr int NF = K < 3 ? kNF : 212 - 64 * 3;
+  static constexpr int nx(int j) {
+    const int t = 64 * K + j;
+    return ((t >= 16 && t < 144 && (t - 16) % 8 == 5) || (t >= 144 && t < 208 && (t - 144) % 8 == 5)) ? 1 : 0;
+  }
+};
+
+#ifndef PCST_SOLO_DMA  // 0: the next superpart's pieces at fragments 1, 5, .., 29; 1: at 1..8
+#define PCST_SOLO_DMA 0
+#endif
+
+__global__ __launch_bounds__(kThreads) void noise_mlp_solo_kernel(
+    const float* __restrict__ pts, int64_t P, int64_t T, const float* __restrict__ cond,
+    int64_t nclouds, const char* __restrict__ blob, int nsp, const float* __restrict__ bias,
+    float* __restrict__ out, const uint32_t* __restrict__ wflag, uint32_t wvalue,
+    uint32_t* __restrict__ wcount, int32_t* __restrict__ werr, int64_t wpolls,
+    uint32_t* __restrict__ sflag, uint32_t svalue) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  if (sflag && blockIdx.x == 0 && threadIdx.x == 0)  // see noise_mlp_pair16_kernel
+    __hip_atomic_store(sflag, svalue, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  if (PCST_SOLO_PRIO && wid >= 4) __builtin_amdgcn_s_setprio(1);
+  const uint32_t lds0 = (uint32_t)(uintptr_t)smem;
+  const uint32_t ba = lds0 + kBiasLds + 16 * g;  // bias rows 4g..4g+3 of a 16-row block
+  long long st_t0 = 0, st_r0 = 0, st_dma = 0, st_bar = 0, st_head = 0, st_res = 0;
+  if (PCST_SOLO_STAMPS) {
+    st_t0 = __builtin_amdgcn_s_memtime();
+    st_r0 = __builtin_amdgcn_s_memrealtime();
+  }
+  // every wave: its own DMAs have landed and it is done with the current slot; then the barrier
+  int st_nb = 0;  // stamps mode 2: each barrier's arrival time (cycles since the kernel start)
+  auto bar = [&]() {
+    if (PCST_SOLO_STAMPS == 2 && lane == 0) {
+      out[P * 3 + ((int64_t)blockIdx.x * 8 + wid) * 64 + st_nb] = (float)(__builtin_amdgcn_s_memtime() - st_t0);
+      ++st_nb;
+    }
+    if (PCST_SOLO_STAMPS == 1) {
+      const long long t0 = __builtin_amdgcn_s_memtime();
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const long long t1 = __builtin_amdgcn_s_memtime();
+      sp_barrier();
+      const long long t2 = __builtin_amdgcn_s_memtime();
+      st_dma += t1 - t0;
+      st_bar += t2 - t1;
+    } else {
+      sp_barrier();
+    }
+  };
+  const f32x4 zero = {0.0f, 0.0f, 0.0f, 0.0f};
+  int sp = 0;
+  // piece i (1 KiB) of superpart s for this wave
+  // (past the last superpart it re-reads the last one into the free slot: no branch in the stream)
+  auto piece = [&](int s, int i) {
+    const int off = wid * 8192 + i * 1024;
+    const int src = s < nsp ? s : nsp - 1;
+    __builtin_amdgcn_global_load_lds((const void*)(blob + (int64_t)src * kSP + off + lane * 16),
+                                     (__attribute__((address_space(3))) void*)(smem + (s & 1) * kSP + off),
+                                     16, 0, 0);
+  };
+  auto piece2 = [&](int s, int i) {  // PCST_SOLO_PRIO 3: 16 pieces per wave of waves 0-3
+    const int off = wid * 16384 + i * 1024;
+    const int src = s < nsp ? s : nsp - 1;
+    __builtin_amdgcn_global_load_lds((const void*)(blob + (int64_t)src * kSP + off + lane * 16),
+                                     (__attribute__((address_space(3))) void*)(smem + (s & 1) * kSP + off),
+                                     16, 0, 0);
+  };
+  // the next superpart's 8 pieces
+  auto dm = [&](auto fc) {
+    constexpr int f = decltype(fc)::value;
+    if ((PCST_SOLO_EXP & 1) && sp >= 1) return;
+    if constexpr (PCST_SOLO_PRIO == 3) {  // experiment: the older waves (0-3) carry the DMA
+      if constexpr (f % 2 == 1 && f < 32) {
+        if (wid < 4) {
+          piece2(sp + 1, f / 2);
+        }
+      }
+      return;
+    }
+    if constexpr (PCST_SOLO_DMA == 0 && f % 4 == 1 && f < 32) piece(sp + 1, f / 4);
+    if constexpr (PCST_SOLO_DMA == 1 && f >= 1 && f <= 8) piece(sp + 1, f - 1);
+  };
+  auto none = [](auto) {};
+  auto slot = [&]() { return lds0 + (uint32_t)((sp & 1) * kSP) + lane * 16; };
+
+#pragma unroll
+  for (int i = 0; i < 8; ++i) piece(0, i);
+  float* sb = reinterpret_cast<float*>(smem + kBiasLds);
+  for (int i = tid; i < kBiasFloats; i += kThreads) sb[i] = bias[i];
+  const int64_t p0 = (int64_t)blockIdx.x * kPts + wid * 32;
+  int64_t cl[2];
+  float px[2], py[2], pz[2];
+#pragma unroll
+  for (int cb = 0; cb < 2; ++cb) {
+    const int64_t pq = p0 + cb * 16 + (lane & 15);
+    const int64_t pc = pq < P ? pq : (P - 1);
+    px[cb] = pts[pc * 3 + 0];
+    py[cb] = pts[pc * 3 + 1];
+    pz[cb] = pts[pc * 3 + 2];
+    cl[cb] = pc / T;
+  }
+  bar();  // superpart 0 and the bias table are in LDS
+
+  // ---- h1 = relu(W0 p + b0): 128 features = 4 k-steps, both column blocks (VALU)
+  bf16x8 h1[8];
+#pragma unroll
+  for (int s = 0; s < 4; ++s)
+#pragma unroll
+    for (int cb = 0; cb < 2; ++cb) {
+      bf16x8 o;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int f = 32 * s + 16 * (j >> 2) + 4 * g + (j & 3);
+        float v = sb[kOffB0 + f];
+        v = fmaf(sb[kOffW0 + f * 3 + 0], px[cb], v);
+        v = fmaf(sb[kOffW0 + f * 3 + 1], py[cb], v);
+        v = fmaf(sb[kOffW0 + f * 3 + 2], pz[cb], v);
+        o[j] = (__bf16)fmaxf(v, 0.0f);
+      }
+      h1[s * 2 + cb] = o;
+    }
+
+  // ---- h2 = relu(W2 h1 + b2) (superpart 0): row block rb's bias is its accumulator's start
+  bf16x8 xb[16];  // a K = 256 operand [ks*2 + cb]: here h2, later bf16(x)
+  {
+    f32x4 acc[32];
+    f32x4 bq;
+    auto xr = [&](auto fc) {
+      constexpr int f = decltype(fc)::value;
+      if constexpr (f % 4 == 1 && f < 60) bq = lds_f4(ba, (kOffB2 + ((f + 3) / 4) * 16) * 4);
+    };
+    auto mf = [&](auto fc, const bf16x8& a) {
+      constexpr int f = decltype(fc)::value, rb = f / 4, ks = f % 4;
+      if constexpr (ks == 0) {
+        if constexpr (f == 0) {
+          bq = lds_f4(ba, kOffB2 * 4);
+          wait_f4<0>(bq);
+        } else {
+          wait_f4<extra_after<SchH2>(f - 3, f)>(bq);
+        }
+      }
+#pragma unroll
+      for (int cb = 0; cb < 2; ++cb)
+        acc[rb * 2 + cb] = mfma16(a, h1[ks * 2 + cb], ks == 0 ? bq : acc[rb * 2 + cb]);
+    };
+    auto po = [&](auto fc) {
+      constexpr int f = decltype(fc)::value, rb = f / 4;
+      // operand k-step s from row blocks 2s, 2s+1, two fragments after the last one's MFMAs
+      if constexpr (f % 4 == 1 && rb >= 1 && rb % 2 == 0) {
+#pragma unroll
+        for (int cb = 0; cb < 2; ++cb)
+          xb[(rb / 2 - 1) * 2 + cb] = relu_bf16(opk(acc[(rb - 2) * 2 + cb], acc[(rb - 1) * 2 + cb]));
+      }
+      if constexpr (f == 63) {
+#pragma unroll
+        for (int cb = 0; cb < 2; ++cb) xb[7 * 2 + cb] = relu_bf16(opk(acc[14 * 2 + cb], acc[15 * 2 + cb]));
+      }
+    };
+    run_sp<SchH2>(slot(), xr, mf, dm, po);
+  }
+
+  // ---- x = W4 h2 + cond[cloud] (superparts 1, 2); cond enters as the accumulator's start
+  f32x4 x[32];
+#pragma unroll
+  for (int rb = 0; rb < 16; ++rb)
+#pragma unroll
+    for (int cb = 0; cb < 2; ++cb)
+      x[rb * 2 + cb] = *reinterpret_cast<const f32x4*>(cond + cl[cb] * 256 + rb * 16 + 4 * g);
+  auto xhalf = [&](auto hc_) {
+    constexpr int h = decltype(hc_)::value;
+    bar();
+    ++sp;
+    auto mf = [&](auto fc, const bf16x8& a) {
+      constexpr int f = decltype(fc)::value, rb = h * 8 + f / 8, ks = f % 8;
+#pragma unroll
+      for (int cb = 0; cb < 2; ++cb) x[rb * 2 + cb] = mfma16(a, xb[ks * 2 + cb], x[rb * 2 + cb]);
+    };
+    run_sp<SchX>(slot(), none, mf, dm, none);
+  };
+  sfor<0, 2>(xhalf);
+  if (PCST_SOLO_STAMPS) st_head = __builtin_amdgcn_s_memtime();
+
+  // ---- 6 residual blocks x += W2 relu(W1 x + b1) + b2, 8 superparts each.  The epilogue of hidden
+  // chunk c (hb = relu(bf16(hc))) runs after W2(c-1)'s MFMAs are issued: it never waits for an MFMA,
+  // and W1(c+1) (independent of hb) follows it.
+  bf16x8 hb[2] = {bf16x8{}, bf16x8{}};  // zero: layer 0's part 0 has no W2(15) (zero fragments)
+  f32x4 hc[4];
+  f32x4 b1r;  // the bias of the W1 row half whose first fragment comes next
+  auto w1 = [&](auto ic, const bf16x8& a) {  // fragment (r, ks) of a W1 chunk, ic = 8r + ks
+    constexpr int i = decltype(ic)::value, r = i / 8, ks = i % 8;
+#pragma unroll
+    for (int cb = 0; cb < 2; ++cb) hc[r * 2 + cb] = mfma16(a, xb[ks * 2 + cb], ks == 0 ? b1r : hc[r * 2 + cb]);
+  };
+  auto w2 = [&](auto rc, const bf16x8& a) {  // row block rc of a W2 chunk column
+    constexpr int rb = decltype(rc)::value;
+#pragma unroll
+    for (int cb = 0; cb < 2; ++cb) x[rb * 2 + cb] = mfma16(a, hb[cb], x[rb * 2 + cb]);
+  };
+  auto epi = [&]() {
+#pragma unroll
+    for (int cb = 0; cb < 2; ++cb) hb[cb] = relu_bf16(opk(hc[cb], hc[2 + cb]));
+  };
+  for (int layer = 0; layer < 6; ++layer) {
+    const uint32_t b1a = ba + (kOffB1 + layer * 512) * 4;   // chunk c, row half r: + (32c + 16r)*4
+    const uint32_t b2a = ba + (kOffBB2 + layer * 256) * 4;
+    bar();
+    ++sp;
+    {  // parts 0, 1: W2(15) of the previous layer | xb = bf16(x), x += b2 | W1(0) || W1(1) | W2(0)
+      f32x4 bq[2];
+      auto xr = [&](auto fc) {
+        constexpr int f = decltype(fc)::value;
+        if constexpr (f == 14 || f == 22 || f == 30 || f == 38) b1r = lds_f4(b1a, (f - 14) / 8 * 64);
+        if constexpr (f >= 15 && f < 31) bq[(f - 15) % 2] = lds_f4(b2a, (f - 15) * 64);
+      };
+      auto mf = [&](auto fc, const bf16x8& a) {
+        constexpr int f = decltype(fc)::value;
+        if constexpr (f < 16) {
+          w2(std::integral_constant<int, f>{}, a);
+        } else if constexpr (f < 48) {
+          if constexpr (f % 8 == 0) wait_f4<extra_after<SchL0>(f - 2, f)>(b1r);
+          w1(std::integral_constant<int, (f - 16) % 16>{}, a);
+        } else {
+          w2(std::integral_constant<int, f - 48>{}, a);
+        }
+      };
+      auto po = [&](auto fc) {
+        constexpr int f = decltype(fc)::value;
+        // xb k-step s from x row blocks 2s, 2s+1 (final after W2(15) fragment 2s+1), two
+        // fragments later; W1(0) reads k-step s at fragment 16 + s
+        if constexpr (f >= 3 && f <= 17 && f % 2 == 1) {
+          constexpr int s = (f - 3) / 2;
+#pragma unroll
+          for (int cb = 0; cb < 2; ++cb) xb[s * 2 + cb] = opk(x[(2 * s) * 2 + cb], x[(2 * s + 1) * 2 + cb]);
+        }
+        if constexpr (f >= 16 && f < 32) {  // x += b2 (x's W2 products of this layer come later)
+          constexpr int rb = f - 16;
+          wait_f4<extra_after<SchL0>(f - 1, f)>(bq[rb % 2]);
+          x[rb * 2] += bq[rb % 2];
+          x[rb * 2 + 1] += bq[rb % 2];
+        }
+        if constexpr (f == 31 || f == 63) epi();  // chunk 0 / chunk 1
+      };
+      run_sp<SchL0>(slot(), xr, mf, dm, po);
+    }
+    for (int m = 1; m < 8; ++m) {  // parts 2m, 2m + 1: W1(2m) | W2(2m-1) || W1(2m+1) | W2(2m)
+      bar();
+      ++sp;
+      const uint32_t bm = b1a + m * 256;
+      auto xr = [&](auto fc) {
+        constexpr int f = decltype(fc)::value;
+        if constexpr (f == 0 || f == 6) b1r = lds_f4(bm, (f / 6) * 64);
+        if constexpr (f == 30 || f == 38) b1r = lds_f4(bm, 128 + (f - 30) / 8 * 64);
+      };
+      auto mf = [&](auto fc, const bf16x8& a) {
+        constexpr int f = decltype(fc)::value;
+        if constexpr (f % 32 < 16) {
+          if constexpr (f == 0) wait_f4<extra_after<SchR>(0, 0)>(b1r);
+          if constexpr (f == 8 || f == 32 || f == 40) wait_f4<extra_after<SchR>(f - 2, f)>(b1r);
+          w1(std::integral_constant<int, f % 16>{}, a);
+        } else {
+          w2(std::integral_constant<int, f % 16>{}, a);
+        }
+      };
+      auto po = [&](auto fc) {
+        constexpr int f = decltype(fc)::value;
+        if constexpr (f == 31 || f == 63) epi();  // chunk 2m / 2m + 1
+      };
+      run_sp<SchR>(slot(), xr, mf, dm, po);
+    }
+  }
+  if (PCST_SOLO_STAMPS) st_res = __builtin_amdgcn_s_memtime();
+
+  // ---- tail: W2(15) of layer 5, then the output MLP 256 -> 256 -> 128 -> 3
+  f32x4 acc[32];   // out0 (32), then out1 (16)
+  bf16x8 o1[16];   // out0's output: out1's K = 256 operand
+  bf16x8 o2[8];    // out1's output: out2's K = 128 operand
+  f32x4 acc2[2];
+  f32x4 bq[2];
+  auto tail = [&](auto kc) {
+    constexpr int K = decltype(kc)::value;
+    using S = SchT<K>;
+    bar();
+    ++sp;
+    auto xr = [&](auto fc) {
+      constexpr int t = 64 * K + decltype(fc)::value;
+      if constexpr (t >= 16 && t < 144 && (t - 16) % 8 == 5)
+        bq[((t - 16) / 8) % 2] = lds_f4(ba, (kOffO0 + ((t - 16) / 8) * 16) * 4);
+      if constexpr (t >= 144 && t < 208 && (t - 144) % 8 == 5)
+        bq[((t - 144) / 8) % 2] = lds_f4(ba, (kOffO2 + ((t - 144) / 8) * 16) * 4);
+    };
+    auto mf = [&](auto fc, const bf16x8& a) {
+      constexpr int t = 64 * K + decltype(fc)::value;
+      if constexpr (t < 16) {
+        w2(std::integral_constant<int, t>{}, a);
+      } else if constexpr (t < 144) {
+        constexpr int rb = (t - 16) / 8, ks = (t - 16) % 8;
+#pragma unroll
+        for (int cb = 0; cb < 2; ++cb)
+          acc[rb * 2 + cb] = mfma16(a, xb[ks * 2 + cb], ks == 0 ? zero : acc[rb * 2 + cb]);
+      } else if constexpr (t < 208) {
+        constexpr int rb = (t - 144) / 8, ks = (t - 144) % 8;
+#pragma unroll
+        for (int cb = 0; cb < 2; ++cb)
+          acc[rb * 2 + cb] = mfma16(a, o1[ks * 2 + cb], ks == 0 ? zero : acc[rb * 2 + cb]);
+      } else {
+        constexpr int ks = t - 208;
+#pragma unroll
+        for (int cb = 0; cb < 2; ++cb) acc2[cb] = mfma16(a, o2[ks * 2 + cb], ks == 0 ? zero : acc2[cb]);
+      }
+    };
+    auto po = [&](auto fc) {
+      constexpr int f = decltype(fc)::value, t = 64 * K + f;
+      if constexpr (t >= 3 && t <= 17 && t % 2 == 1) {  // xb = bf16(x), as in a layer's part 0
+        constexpr int s = (t - 3) / 2;
+#pragma unroll
+        for (int cb = 0; cb < 2; ++cb) xb[s * 2 + cb] = opk(x[(2 * s) * 2 + cb], x[(2 * s + 1) * 2 + cb]);
+      }
+      if constexpr (t >= 16 && t < 144 && (t - 16) % 8 == 7) {  // out0 row block rb done
+        constexpr int rb = (t - 16) / 8;
+        wait_f4<extra_after<S>(f - 2, f)>(bq[rb % 2]);
+        acc[rb * 2] += bq[rb % 2];
+        acc[rb * 2 + 1] += bq[rb % 2];
+        if constexpr (rb % 2 == 1) {
+#pragma unroll
+          for (int cb = 0; cb < 2; ++cb)
+            o1[(rb / 2) * 2 + cb] = relu_bf16(opk(acc[(rb - 1) * 2 + cb], acc[rb * 2 + cb]));
+        }
+      }
+      if constexpr (t >= 144 && t < 208 && (t - 144) % 8 == 7) {  // out1 row block rb done
+        constexpr int rb = (t - 144) / 8;
+        wait_f4<extra_after<S>(f - 2, f)>(bq[rb % 2]);
+        acc[rb * 2] += bq[rb % 2];
+        acc[rb * 2 + 1] += bq[rb % 2];
+        if constexpr (rb % 2 == 1) {
+#pragma unroll
+          for (int cb = 0; cb < 2; ++cb)
+            o2[(rb / 2) * 2 + cb] = relu_bf16(opk(acc[(rb - 1) * 2 + cb], acc[rb * 2 + cb]));
+        }
+      }
+    };
+    run_sp<S>(slot(), xr, mf, dm, po);
+  };
+  sfor<0, 4>(tail);
+  if (g == 0) {
+    const float o0 = sb[kOffO4 + 0], o1v = sb[kOffO4 + 1], o2v = sb[kOffO4 + 2];
+#pragma unroll
+    for (int cb = 0; cb < 2; ++cb) {
+      const int64_t q = (int64_t)blockIdx.x * kPts + wid * 32 + cb * 16 + (lane & 15);
+      if (q < P) {
+        out[q * 3 + 0] = acc2[cb][0] + o0;
+        out[q * 3 + 1] = acc2[cb][1] + o1v;
+        out[q * 3 + 2] = acc2[cb][2] + o2v;
+      }
+    }
+  }
+  if (PCST_SOLO_STAMPS == 2 && lane == 0)
+    out[P * 3 + ((int64_t)blockIdx.x * 8 + wid) * 64 + 63] = (float)(__builtin_amdgcn_s_memtime() - st_t0);
+  if (PCST_SOLO_STAMPS == 1 && lane == 0) {  // {cycles, DMA wait, barrier, 100 MHz ticks, head, residual, tail, 1}
+    const long long t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+    float* st = out + P * 3 + ((int64_t)blockIdx.x * 8 + wid) * 8;
+    st[0] = (float)(t1 - st_t0);
+    st[1] = (float)st_dma;
+    st[2] = (float)st_bar;
+    st[3] = (float)(r1 - st_r0);
+    st[4] = (float)(st_head - st_t0);
+    st[5] = (float)(st_res - st_head);
+    st[6] = (float)(t1 - st_res);
+    st[7] = 1.0f;
+  }
+  if (wflag) last_group_wait(wflag, wvalue, wcount, werr, wpolls);
+}
+
+}  // namespace solo
+
 // cond[c] = b4 + time_proj(emb(t_c)) + style_proj(style_c)   (diffusion_model.py:15-26, 56-58)
 // freqs[64] is the reference's exp table computed on the host with torch's own CPU exp.
 // Grid (clouds, 8): workgroup y computes outputs [32y, 32y + 32); its 8 row groups split the
@@ -1192,6 +1774,7 @@ using namespace pcst;
 
 // Bytes of the packed weight blob for a precision: 0 = f32 (parity), 1 = bf16.
 extern "C" int64_t pcst_noise_mlp_blob_bytes(int precision) {
+  if (precision == 3) return (int64_t)solo::kNSP * solo::kSP;  // 55 superparts (packing.py SOLO16)
   // every layer starts on a fresh 32 KiB part (see packing.py); residual chunks take one part
   // (bf16: W1c | W2c) or two (f32: W1c, W2c).  The two bf16 layouts (1: 32x32x16 fragments,
   // 2: 16x16x32 fragments) hold the same fragments per part, so their blobs have one size.
@@ -1224,14 +1807,19 @@ extern "C" int pcst_noise_mlp(const float* pts, int64_t P, int64_t points_per_cl
                               void* stream) {
   PCST_CHECK_ARG(P >= 0 && points_per_cloud > 0 && nclouds > 0, "noise_mlp: bad shape");
   PCST_CHECK_ARG(P <= points_per_cloud * nclouds, "noise_mlp: P exceeds clouds*points");
-  PCST_CHECK_ARG(precision >= 0 && precision <= 2,
-                 "noise_mlp: precision must be 0 (f32), 1 (bf16 32x32x16) or 2 (bf16 16x16x32)");
+  PCST_CHECK_ARG(precision >= 0 && precision <= 3,
+                 "noise_mlp: precision must be 0 (f32), 1 (bf16 32x32x16), 2 (bf16 pair16) or 3 (bf16 solo)");
   PCST_CHECK_ARG(blob_bytes == pcst_noise_mlp_blob_bytes(precision), "noise_mlp: blob size %lld != %lld",
                  (long long)blob_bytes, (long long)pcst_noise_mlp_blob_bytes(precision));
   PCST_CHECK_ARG(((uintptr_t)blob & 15) == 0, "noise_mlp: blob must be 16-byte aligned");
   if (P == 0) return PCST_OK;
   hipStream_t s = as_stream(stream);
-  if (precision == 2) {
+  if (precision == 3) {
+    hipLaunchKernelGGL(solo::noise_mlp_solo_kernel, dim3((unsigned)cdiv(P, solo::kPts)), dim3(solo::kThreads),
+                       solo::kLds, s, pts, P, points_per_cloud, cond, nclouds, (const char*)blob,
+                       solo::kNSP, bias, out, (const uint32_t*)nullptr, 0u, (uint32_t*)nullptr,
+                       (int32_t*)nullptr, (int64_t)0, (uint32_t*)nullptr, 0u);
+  } else if (precision == 2) {
     const size_t lds = Streamer2::kSlots * kPart + Streamer2::kWaves * kXBytes +
                        (kBiasFloats + kCondSlots * 256) * sizeof(float);
     hipLaunchKernelGGL(noise_mlp_pair16_kernel, dim3((unsigned)cdiv(P, 128)), dim3(kPairThreads),
@@ -1284,7 +1872,7 @@ extern "C" int pcst_noise_mlp_ex(const float* pts, int64_t P, int64_t points_per
                                  const uint32_t* wait_flag, uint32_t wait_value,
                                  uint32_t* wait_counter, int32_t* wait_err, int64_t max_polls,
                                  void* stream) {
-  if (precision != 2 || P == 0) {  // no fused form: the same ordering by separate launches
+  if ((precision != 2 && precision != 3) || P == 0) {  // no fused form: separate launches
     if (start_flag) {
       hipLaunchKernelGGL(mlp_start_signal_kernel, dim3(1), dim3(64), 0, as_stream(stream), start_flag,
                          start_value);
@@ -1297,10 +1885,19 @@ extern "C" int pcst_noise_mlp_ex(const float* pts, int64_t P, int64_t points_per
   }
   PCST_CHECK_ARG(P > 0 && points_per_cloud > 0 && nclouds > 0, "noise_mlp_ex: bad shape");
   PCST_CHECK_ARG(P <= points_per_cloud * nclouds, "noise_mlp_ex: P exceeds clouds*points");
-  PCST_CHECK_ARG(blob_bytes == pcst_noise_mlp_blob_bytes(2), "noise_mlp_ex: blob size %lld != %lld",
-                 (long long)blob_bytes, (long long)pcst_noise_mlp_blob_bytes(2));
+  PCST_CHECK_ARG(blob_bytes == pcst_noise_mlp_blob_bytes(precision), "noise_mlp_ex: blob size %lld != %lld",
+                 (long long)blob_bytes, (long long)pcst_noise_mlp_blob_bytes(precision));
   PCST_CHECK_ARG(((uintptr_t)blob & 15) == 0, "noise_mlp_ex: blob must be 16-byte aligned");
   PCST_CHECK_ARG(!wait_flag || wait_counter, "noise_mlp_ex: a wait needs its counter");
+  if (precision == 3) {
+    hipLaunchKernelGGL(solo::noise_mlp_solo_kernel, dim3((unsigned)cdiv(P, solo::kPts)), dim3(solo::kThreads),
+                       solo::kLds, as_stream(stream), pts, P, points_per_cloud, cond, nclouds,
+                       (const char*)blob, solo::kNSP, bias, out, wait_flag, wait_value, wait_counter,
+                       wait_err, max_polls > 0 ? max_polls : (int64_t)kMlpWaitPolls, start_flag,
+                       start_value);
+    PCST_LAUNCH_CHECK("noise_mlp_ex");
+    return PCST_OK;
+  }
   const size_t lds = Streamer2::kSlots * kPart + Streamer2::kWaves * kXBytes +
                      (kBiasFloats + kCondSlots * 256) * sizeof(float);
   hipLaunchKernelGGL(noise_mlp_pair16_kernel, dim3((unsigned)cdiv(P, 128)), dim3(kPairThreads), lds,

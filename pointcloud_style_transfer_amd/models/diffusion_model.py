@@ -105,10 +105,10 @@ class NoisePredictor(nn.Module):
         self._pack_key = None
         self._packed = None
 
-    # ABI precision code of the "bf16" mode: the 16x16x32 pair kernel (PAIR16).  tools/ may set
-    # it to packing.BF16 (the 32x32x16 pair kernel: same arithmetic, other MFMA shape) for A/B
-    # timing; the product never changes it.
-    bf16_code = packing.PAIR16
+    # ABI precision code of the "bf16" mode: the 16x16x32 solo kernel (SOLO16, round 5).  tools/
+    # may set it to packing.PAIR16 (the round-2..4 pair kernel: same arithmetic, other work split)
+    # for A/B timing; the product never changes it.
+    bf16_code = packing.SOLO16
 
     @property
     def precision_code(self) -> int:

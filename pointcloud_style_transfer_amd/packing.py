@@ -45,6 +45,18 @@ The residual parts are in the kernel's software-pipelined order: W1(0), then per
 W1(it+1) (it < 7) before W2(it) -- the kernel computes the next hidden chunk before the W2
 product of the current one, so the partner's chunk exchange and the ReLU/bf16 epilogue sit in
 the MFMA shadow of the other part.
+
+bf16 "solo" order (noise_mlp_solo_kernel, precision code SOLO16 = 3): the same 16x16x32 fragments
+as a flat stream in consumption order, read by every wave (no roles), cut into 64 KiB superparts
+(64 fragments; the kernel's DMA and barrier unit) only at the end (padded to whole superparts):
+  point_encoder.2: (row block rb, k-step ks), rb-major        64 fragments
+  point_encoder.4: the same                                   128
+  residual layer i (512 fragments = 8 superparts), chunk c = hidden rows 32c..32c+31:
+      W2(15) of layer i-1 (16 row blocks, k-step 15; zeros for i = 0), W1(0),
+      then for k = 1..15: W1(k), W2(k-1)
+    where W1(k) = (row block 2k + r, ks) r-major (16 fragments) and W2(k) = row blocks 0..15 at
+    k-step k (16 fragments)
+  W2(15) of layer 5, output_mlp.0 (128), output_mlp.2 (64), output_mlp.4 (4)
 """
 from __future__ import annotations
 
@@ -52,7 +64,8 @@ import numpy as np
 import torch
 
 PART = 32768
-BF16, F32, PAIR16 = 1, 0, 2
+BF16, F32, PAIR16, SOLO16 = 1, 0, 2, 3
+SUPERPART = 65536
 
 # bias table offsets (floats) -- must match csrc/noise_mlp.hip
 OFF_W0, OFF_B0, OFF_B2, OFF_B1, OFF_BB2, OFF_O0, OFF_O2, OFF_O4, BIAS_FLOATS = (
@@ -112,6 +125,8 @@ def pack_blob(sd, precision, pre="noise_predictor"):
         return _pack_pair(g)
     if precision == PAIR16:
         return _pack_pair16(g)
+    if precision == SOLO16:
+        return _pack_solo16(g)
     parts = []
 
     def layer(W):
@@ -218,6 +233,36 @@ def _pack_pair16(g):
     dense(g("output_mlp.2.weight"))
     emit([_frags16(g("output_mlp.4.weight"))])
     return np.concatenate(parts)
+
+
+def _pack_solo16(g):
+    """bf16 16x16x32 solo stream of noise_mlp_solo_kernel (module docstring)."""
+    frags = []
+
+    def dense(W):
+        F = _frags16(W)                      # [NRB, NKS, 512]
+        frags.extend(F.reshape(-1, 512))     # rb-major, then k-step
+
+    dense(g("point_encoder.2.weight"))
+    dense(g("point_encoder.4.weight"))
+    prev = np.zeros((16, 16, 512), np.float32)     # "W2 of layer -1": zeros
+    for i in range(6):
+        F1 = _frags16(g(f"layers.{i}.0.weight"))  # [32 row blocks, 8, 512]
+        F2 = _frags16(g(f"layers.{i}.2.weight"))  # [16 row blocks, 16, 512]
+        w1 = lambda k: F1[2 * k:2 * k + 2].reshape(-1, 512)  # noqa: E731  (r, ks) r-major
+        frags.extend(prev[:, 15])
+        frags.extend(w1(0))
+        for k in range(1, 16):
+            frags.extend(w1(k))
+            frags.extend(F2[:, k - 1])
+        prev = F2
+    frags.extend(prev[:, 15])
+    dense(g("output_mlp.0.weight"))
+    dense(g("output_mlp.2.weight"))
+    dense(g("output_mlp.4.weight"))
+    b = _to_bytes(np.stack(frags), BF16)
+    n = (-len(b)) % SUPERPART
+    return np.concatenate([b, np.zeros(n, np.uint8)]) if n else b
 
 
 def pack_bias(sd, pre="noise_predictor"):

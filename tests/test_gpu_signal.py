@@ -76,7 +76,7 @@ def test_wait_that_times_out_is_reported():
 
     torch.manual_seed(4)
     npred = NoisePredictor(Config(make_dirs=False, precision="bf16")).to(dev).eval()
-    assert npred.precision_code == packing.PAIR16
+    assert npred.precision_code == packing.SOLO16
     pts = torch.randn(2 * 4096, 3, device=dev)
     with torch.no_grad():
         cond = npred.cond(torch.tensor([5, 5], device=dev), torch.randn(2, 256, device=dev))

@@ -255,7 +255,7 @@ def _noise_params(det_state, H, precision):
                         g("style_proj.bias"), g("point_encoder.4.bias"))
 
 
-@pytest.mark.parametrize("precision", [0, 1, 2])
+@pytest.mark.parametrize("precision", [0, 1, 2, 3])
 def test_noise_mlp_golden(H, golden, det_state, precision):
     g = golden("noise_predictor.npz")
     blob, bias, cp = _noise_params(det_state, H, precision)
@@ -496,7 +496,7 @@ def test_noise_mlp_then_wait_orders_after_the_signal(H):
     torch.manual_seed(4)
     cfg = Config(make_dirs=False, precision="bf16")
     npred = NoisePredictor(cfg).cuda().eval()
-    assert npred.precision_code == packing.PAIR16
+    assert npred.precision_code == packing.SOLO16
     rng = np.random.default_rng(8)
     pts = dev(rng.standard_normal((2 * 30000, 3)).astype(np.float32))
     t = torch.tensor([999, 999], device="cuda")

@@ -343,6 +343,103 @@ def test_bf16_pair_packing_follows_the_kernel_read_schedule():
             assert (seen[O:] == 0).all(), name
 
 
+def test_bf16_solo16_packing_follows_the_kernel_read_schedule():
+    """packing.pack_blob(SOLO16), the stream of noise_mlp_solo_kernel: replaying that kernel's
+    consumption order (csrc/noise_mlp.hip solo::: h2 rb-major, x, per layer W2(15) of the previous
+    layer then W1(0), then W1(k), W2(k-1) for k = 1..15, the tail W2(15), out0, out1, out2)
+    recovers every weight of every layer exactly (as bf16), the layer-0 W2 slot is zero, and the
+    blob is 55 superparts of 64 fragments (the kernel's DMA unit)."""
+    import torch
+
+    from pointcloud_style_transfer_amd import packing
+    from pointcloud_style_transfer_amd.model_spec import state_dict_shapes
+    from detweights import deterministic_state
+
+    sd = deterministic_state(state_dict_shapes())
+    pre = "noise_predictor"
+    blob = packing.pack_blob(sd, packing.SOLO16)
+    assert len(blob) == 55 * packing.SUPERPART
+    vals = torch.from_numpy(blob.copy()).view(torch.bfloat16).float().numpy()
+    frags = vals.reshape(-1, 512)
+    km = packing._kmap16(16)                    # [S, 64, 8]
+    r = np.arange(64) & 15
+    pos = [0]
+    got = {}
+
+    def take(name, rb, step):
+        fr = frags[pos[0]].reshape(64, 8)
+        pos[0] += 1
+        if name is None:
+            assert (fr == 0).all()
+            return
+        W = got.setdefault(name, {})
+        for lane in range(64):
+            for j in range(8):
+                W[(rb * 16 + r[lane], int(km[step, lane, j]))] = fr[lane, j]
+
+    def dense(name, nrb, nks):
+        for rb in range(nrb):
+            for ks in range(nks):
+                take(name, rb, ks)
+
+    dense("point_encoder.2", 16, 4)
+    dense("point_encoder.4", 16, 8)
+    for layer in range(6):
+        for rb in range(16):
+            take(f"layers.{layer - 1}.2" if layer else None, rb, 15)
+        for k in range(16):
+            for rr in range(2):
+                for ks in range(8):
+                    take(f"layers.{layer}.0", 2 * k + rr, ks)
+            if k:
+                for rb in range(16):
+                    take(f"layers.{layer}.2", rb, k - 1)
+    for rb in range(16):
+        take("layers.5.2", rb, 15)
+    dense("output_mlp.0", 16, 8)
+    dense("output_mlp.2", 8, 8)
+    dense("output_mlp.4", 1, 4)
+    assert pos[0] == 212 + 192 + 6 * 512
+    assert (frags[pos[0]:] == 0).all()
+    for name, W in got.items():
+        ref = torch.from_numpy(sd[f"{pre}.{name}.weight"]).bfloat16().float().numpy()
+        O, K = ref.shape
+        seen = np.full((max(O, 16), K), np.nan, np.float32)
+        for (o, k), v in W.items():
+            seen[o, k] = v
+        np.testing.assert_array_equal(seen[:O], ref, err_msg=name)
+        if O < 16:
+            assert (seen[O:] == 0).all(), name
+
+
+def test_solo16_kernel_schedule_emulated_matches_the_network():
+    """tests/solo_emulator.py replays noise_mlp_solo_kernel's dataflow lane by lane over the packed
+    SOLO16 blob (fragment order, v_mfma_f32_16x16x32_bf16 layouts, bias placement, the hidden-chunk
+    software pipeline, bf16 operand rounding) for one wave's 32 points; it must equal the exact-f32
+    network (oracle.noise_predictor) within the bf16 mode's normwise bound (3e-2, as the GPU
+    tests) -- a schedule or layout error gives O(1) differences."""
+    import solo_emulator as SE
+    from pointcloud_style_transfer_amd import packing
+    from pointcloud_style_transfer_amd.model_spec import state_dict_shapes
+    from detweights import deterministic_state
+    import oracle.oracle as O
+
+    sd = deterministic_state(state_dict_shapes())
+    blob = packing.pack_blob(sd, packing.SOLO16)
+    bias = packing.pack_bias(sd)
+    rng = np.random.default_rng(11)
+    pts = rng.standard_normal((1, 32, 3)).astype(np.float32)
+    t = np.array([731])
+    style = (rng.standard_normal((1, 256)) * 0.3).astype(np.float32)
+    ref = O.noise_predictor(sd, pts, t, style).reshape(-1, 3)
+    pre = "noise_predictor"
+    cond = (sd[pre + ".point_encoder.4.bias"] + O._linear(sd, pre + ".time_proj", O.time_embedding(t, 128))
+            + O._linear(sd, pre + ".style_proj", style)).astype(np.float32)
+    out = SE.run_wave(blob, bias, pts[0], np.repeat(cond, 32, axis=0))
+    err = np.linalg.norm(out - ref) / np.linalg.norm(ref)
+    assert err < 3e-2, err
+
+
 def test_bf16_pair16_packing_follows_the_kernel_read_schedule():
     """packing.pack_blob(PAIR16), the 16x16x32 layout of noise_mlp_pair16_kernel: replaying
     that kernel's read schedule (csrc/noise_mlp.hip pair16_wave / dense16 / run16: part order,

@@ -57,3 +57,5 @@ def apply():
         _autograd.BATCH_CAST = e["PCST_BATCH_CAST"] != "0"
     if e.get("PCST_NM_BF16_KERNEL") == "1":
         dm.NoisePredictor.bf16_code = packing.BF16
+    if "PCST_NM_CODE" in e:   # the bf16 mode's kernel: 1 pair 32x32x16, 2 pair16, 3 solo (product)
+        dm.NoisePredictor.bf16_code = int(e["PCST_NM_CODE"])
