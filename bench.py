@@ -21,7 +21,12 @@ Prints ONE JSON line on rank 0 (driver contract), including
   * `quality` (N=1 only, outside the timed region): "Chamfer vs ref", the second half of
     BASELINE's metric -- the HIP loop (bf16 and fp32 noise MLP) against the oracle loop on
     the same 120k cloud, x_T and counter-keyed draws (rng.CounterRNG);
-  * `encoder_rooflines`: FPS / ball query in the SURVEY §8d scan model AND from PMC counters.
+  * `encoder_rooflines`: FPS / ball query in the SURVEY §8d scan model AND from PMC counters;
+  * `batch32` (N=1 only, after the headline): BASELINE configs[4]'s per-GPU share, 32 clouds x
+    120k through DiffusionProcess.guided_sample_loop eager and with graph=True, ms per step;
+  * `train_step` (N=1 only, after the headline): BASELINE configs[2], DiffusionTrainer.train_step
+    on 8 x 120k clouds under fp16 autocast, ms per step and the top three trainer kernels'
+    rooflines.
 """
 from __future__ import annotations
 
@@ -63,6 +68,8 @@ def parse():
     ap.add_argument("--no-encoder", action="store_true")
     ap.add_argument("--no-other-precision", action="store_true",
                     help="skip timing the other noise-MLP precision mode after the headline")
+    ap.add_argument("--no-extra", action="store_true",
+                    help="skip the batch32 (configs[4]) and train_step (configs[2]) legs")
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "noise_mlp_traffic.json"))
     ap.add_argument("--encoder-traffic-json",
                     default=os.path.join(REPO, "profiles", "encoder_traffic.json"))
@@ -290,6 +297,132 @@ def encoder_rooflines(xc, device, traffic, tag, reps=5):
     return out
 
 
+def batch32_leg(cfg, model, dp, device, clouds=32, points=120000, short=5, long=25):
+    """BASELINE configs[4]'s per-GPU share: `clouds` clouds x `points` through the product
+    sampling loop (DiffusionProcess.guided_sample_loop), eager and graph=True.  Each mode runs a
+    `short`- and a `long`-step schedule on the same inputs; ms per step = the wall difference over
+    the extra steps, so the one-time costs both runs share (style encode, conditioning rows,
+    workspaces, the graph capture) cancel.  Outside the headline's timed region."""
+    from pointcloud_style_transfer_amd.synthetic import lidar_like_cloud, standard_normal
+
+    src = torch.from_numpy(np.stack([lidar_like_cloud(1000 + i, points) for i in range(clouds)])).to(device)
+    cond = torch.from_numpy(np.stack([lidar_like_cloud(2000 + i, points) for i in range(clouds)])).to(device)
+    xT = torch.from_numpy(np.stack([standard_normal(3000 + i, (points, 3)) for i in range(clouds)])).to(device)
+    out = {"workload": f"guided_sample_loop, {clouds} x {points}-pt clouds per GPU, CFG x2, "
+                       f"{cfg.global_points} coarse (BASELINE configs[4]: 256 clouds / 8 GPUs)",
+           "method": f"(wall({long} steps) - wall({short} steps)) / {long - short}, "
+                     "torch.cuda.synchronize() around each loop"}
+    for mode, graph in (("eager", False), ("graph", True)):
+        dp.guided_sample_loop(model, src, cond, 2, 7.5, x_T=xT, graph=graph)  # workspaces, warm-up
+        wall = {}
+        for n in (short, long):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            dp.guided_sample_loop(model, src, cond, n, 7.5, x_T=xT, graph=graph)
+            torch.cuda.synchronize()
+            wall[n] = time.perf_counter() - t0
+        ms = (wall[long] - wall[short]) / (long - short) * 1e3
+        out[mode] = {"ms_per_step": round(ms, 4), "clouds_steps_per_s": round(clouds * 1e3 / ms, 2),
+                     "wall_s": {str(k): round(v, 4) for k, v in wall.items()}}
+    return out
+
+
+def train_leg(device, batch=8, points=120000, steps=5, warmup=2):
+    """BASELINE configs[2]: one DiffusionTrainer.train_step (trainer.py:70-127, accumulation 1) on
+    `batch` x `points` clouds under fp16 autocast (Config defaults), inputs resident in HBM, ms per
+    step over `steps` after `warmup` (each step's loss read after the next is queued, as
+    train_one_epoch).  Then two more steps with HIP events around the three largest trainer
+    kernels (round-4 profile: the fused residual-block backward and forward, the 16-bit weight
+    gradient) on their launch stream: algorithmic FLOP over the summed event time, against the
+    dense fp16 MFMA peak."""
+    import tempfile
+
+    from pointcloud_style_transfer_amd import _hip
+    from pointcloud_style_transfer_amd.config.config import Config
+    from pointcloud_style_transfer_amd.synthetic import lidar_like_cloud
+    from pointcloud_style_transfer_amd.training.trainer import DiffusionTrainer
+
+    logdir = tempfile.mkdtemp(prefix="pcst_bench_train_")
+    cfg = Config(make_dirs=False, log_dir=logdir, checkpoint_dir=logdir, gradient_accumulation_steps=1,
+                 batch_size=batch)
+    torch.manual_seed(0)
+    trainer = DiffusionTrainer(cfg, device=str(device))
+    trainer.model.train()
+    sim = torch.from_numpy(np.stack([lidar_like_cloud(1000 + i, points) for i in range(batch)]))
+    real = torch.from_numpy(np.stack([lidar_like_cloud(2000 + i, points) for i in range(batch)]))
+    data = {"sim_full": sim.to(device), "real_full": real.to(device)}
+    for i in range(warmup):
+        trainer.train_step(data, i, 1 << 30, next_batch=data)
+
+    def run(n):
+        pending = loss = None
+        for i in range(n):
+            step = trainer.train_step(data, i, 1 << 30, host_sync=False,
+                                      next_batch=data if i + 1 < n else None)
+            if pending is not None:
+                loss, _ = pending[1].read()
+            pending = step
+        loss, _ = pending[1].read()
+        return loss
+
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    loss = run(steps)
+    torch.cuda.synchronize()
+    ms = (time.perf_counter() - t0) / steps * 1e3
+
+    # kernel rooflines: wrap the three ABI calls with events on the stream they launch on
+    flops = {"resblock_bwd16": lambda a, k: 4 * a[0].shape[0] * 256 * 512,   # dd W2, dz W1
+             "resblock_fwd16": lambda a, k: 4 * a[0].shape[0] * 256 * 512,   # x W1^T, h W2^T
+             "linear_wgrad_ex": lambda a, k: 2 * a[0].shape[0] * a[0].shape[1] * a[1].shape[1]}
+    kernels = {"resblock_bwd16": "resblock_kernel<true, true> (pcst_resblock_bwd16)",
+               "resblock_fwd16": "resblock2_kernel (pcst_resblock_fwd16)",
+               "linear_wgrad_ex": "wgrad_ex_kernel + combine (pcst_linear_wgrad_ex)"}
+    rec = {k: [] for k in flops}
+    orig = {k: getattr(_hip, k) for k in flops}
+
+    def wrap(name):
+        fn = orig[name]
+
+        def timed(*a, **k):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            r = fn(*a, **k)
+            e1.record()
+            rec[name].append((e0, e1, flops[name](a, k)))
+            return r
+        return timed
+
+    try:
+        for k in flops:
+            setattr(_hip, k, wrap(k))
+        run(2)
+        torch.cuda.synchronize()
+    finally:
+        for k, fn in orig.items():
+            setattr(_hip, k, fn)
+    roof = {}
+    for k, ev in rec.items():
+        if not ev:
+            roof[k] = None
+            continue
+        t = sum(a.elapsed_time(b) for a, b, _ in ev)
+        f = sum(x for _, _, x in ev)
+        tf = f / (t * 1e-3) / 1e12
+        roof[k] = {"kernel": kernels[k], "bound": "mfma", "calls_per_step": len(ev) // 2,
+                   "avg_launch_ms": round(t / len(ev), 4), "achieved": round(tf, 2),
+                   "peak": MFMA_BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
+                   "frac": round(tf / MFMA_BF16_PEAK_TFLOPS, 4),
+                   "algorithmic": "4 M 256 512 FLOP per block" if k != "linear_wgrad_ex" else "2 M I O FLOP"}
+    del trainer
+    torch.cuda.empty_cache()
+    return {"workload": f"DiffusionTrainer.train_step, {batch} x {points}-pt clouds, L1 + Chamfer, "
+                        "accumulation 1 (BASELINE configs[2])",
+            "dtype": f"fp32 master weights, autocast {cfg.amp_dtype}" if cfg.use_amp else "fp32",
+            "steps": steps, "warmup": warmup, "ms_per_step": round(ms, 3),
+            "clouds_per_s": round(batch * 1e3 / ms, 3), "final_loss": float(loss), "rooflines": roof}
+
+
 def main():
     args = parse()
     maybe_spawn(args)
@@ -461,6 +594,13 @@ def main():
                 state.check()
 
     mlp_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    # configs[4] and configs[2], after the headline and outside its timed region (N = 1 only)
+    batch32 = train_step = None
+    if world == 1 and not args.no_extra:
+        with torch.no_grad():
+            batch32 = batch32_leg(cfg, model, dp, device)
+        torch.cuda.empty_cache()
+        train_step = train_leg(device)
     flop = FLOP_PER_POINT * 2 * C * cfg.global_points
     peak = MFMA_BF16_PEAK_TFLOPS if args.precision == "bf16" else MFMA_F32_PEAK_TFLOPS
     achieved = flop / (mlp_ms * 1e-3) / 1e12
@@ -507,6 +647,8 @@ def main():
             "cpu_baseline": base,
             "quality": quality,
             "encoder_rooflines": enc,
+            "batch32": batch32,
+            "train_step": train_step,
         }
         print(json.dumps(line), flush=True)
     if world > 1:

@@ -1062,9 +1062,10 @@ __device__ __forceinline__ void pair16_wave(const float* __restrict__ cond, cons
 // producer always finds free CUs.
 constexpr int kMlpWaitPolls = 1 << 26;
 __device__ __forceinline__ void last_group_wait(const uint32_t* flag, uint32_t value,
-                                                uint32_t* counter, int32_t* err, int64_t max_polls) {
+                                                uint32_t* counter, int32_t* err, int64_t max_polls,
+                                                bool leader) {
   __syncthreads();  // this work-group's rows are written
-  if (threadIdx.x == 0) {
+  if (leader) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     const uint32_t prev = atomicAdd(counter, 1u);
     if (prev == gridDim.x - 1) {
@@ -1130,7 +1131,7 @@ __global__ __launch_bounds__(kPairThreads) void noise_mlp_pair16_kernel(
     pair16_wave<0>(cond, sb, sc, X, st, wid, c0, slot, px, py, pz, p, P, out);
   else
     pair16_wave<1>(cond, sb, sc, X, st, wid, c0, slot, px, py, pz, p, P, out);
-  if (wflag) last_group_wait(wflag, wvalue, wcount, werr, wpolls);
+  if (wflag) last_group_wait(wflag, wvalue, wcount, werr, wpolls, threadIdx.x == 0);
 }
 
 // ============================================================================================
@@ -1156,12 +1157,15 @@ __global__ __launch_bounds__(kPairThreads) void noise_mlp_pair16_kernel(
 // x -> xb between them (the stream order of packing.py SOLO16).
 namespace solo {
 
-constexpr int kThreads = 512;
+#ifndef PCST_SOLO_NCB
+#define PCST_SOLO_NCB 2
+#endif
+constexpr int kNCB = PCST_SOLO_NCB;    // column blocks per wave of the product instantiation
 constexpr int kPts = 256;               // points per work-group
 constexpr int kSP = 65536;              // superpart bytes
 constexpr int kNF = kSP / 1024;         // fragments per superpart
 #ifndef PCST_SOLO_KD
-#define PCST_SOLO_KD 3
+#define PCST_SOLO_KD 2
 #endif
 #ifndef PCST_SOLO_PRIO
 #define PCST_SOLO_PRIO 0
@@ -1219,6 +1223,18 @@ __device__ __forceinline__ void wait_f4x2(f32x4& a, f32x4& b) {
   static_assert(N >= 0 && N <= 15, "lgkmcnt range");
   asm volatile("s_waitcnt lgkmcnt(%2)" : "+v"(a), "+v"(b) : "n"(N));
 }
+// a uniform value re-materialised here (empty asm): address arithmetic that uses it cannot be
+// hoisted out of its loop and kept live (at 256 VGPRs such a hoisted value spills)
+__device__ __forceinline__ uint32_t here(uint32_t v) {
+  v = __builtin_amdgcn_readfirstlane(v);
+  asm volatile("" : "+s"(v));
+  return v;
+}
+// this lane's index without keeping threadIdx.x live (v_mbcnt)
+__device__ __forceinline__ uint32_t lane_id() {
+  return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+}
+
 // one bias row (f32x4) from the LDS table; `off` is a compile-time byte offset.
 // RULE for every asm LDS read here: its result must reach a tied wait (wait_frag / wait_f4) before
 // anything else.  The compiler sees the read's output as written at the asm statement, so an
@@ -1352,12 +1368,14 @@ struct SchT {
 #define PCST_SOLO_DMA 0
 #endif
 
-__global__ __launch_bounds__(kThreads) void noise_mlp_solo_kernel(
+template <int NCB>  // 16-point column blocks per wave: 2 (8 waves, 2 per SIMD) or 4 (4 waves, 1 per SIMD)
+__global__ __launch_bounds__(16 / NCB * 64) void noise_mlp_solo_kernel(
     const float* __restrict__ pts, int64_t P, int64_t T, const float* __restrict__ cond,
     int64_t nclouds, const char* __restrict__ blob, int nsp, const float* __restrict__ bias,
     float* __restrict__ out, const uint32_t* __restrict__ wflag, uint32_t wvalue,
     uint32_t* __restrict__ wcount, int32_t* __restrict__ werr, int64_t wpolls,
     uint32_t* __restrict__ sflag, uint32_t svalue) {
+  constexpr int NW = 16 / NCB;  // waves per work-group
   extern __shared__ __attribute__((aligned(16))) char smem[];
   if (sflag && blockIdx.x == 0 && threadIdx.x == 0)  // see noise_mlp_pair16_kernel
     __hip_atomic_store(sflag, svalue, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1395,7 +1413,7 @@ __global__ __launch_bounds__(kThreads) void noise_mlp_solo_kernel(
   // piece i (1 KiB) of superpart s for this wave
   // (past the last superpart it re-reads the last one into the free slot: no branch in the stream)
   auto piece = [&](int s, int i) {
-    const int off = wid * 8192 + i * 1024;
+    const int off = wid * (kSP / NW) + i * 1024;
     const int src = s < nsp ? s : nsp - 1;
     __builtin_amdgcn_global_load_lds((const void*)(blob + (int64_t)src * kSP + off + lane * 16),
                                      (__attribute__((address_space(3))) void*)(smem + (s & 1) * kSP + off),
@@ -1420,7 +1438,8 @@ __global__ __launch_bounds__(kThreads) void noise_mlp_solo_kernel(
       }
       return;
     }
-    if constexpr (PCST_SOLO_DMA == 0 && f % 4 == 1 && f < 32) piece(sp + 1, f / 4);
+    if constexpr (PCST_SOLO_DMA == 0 && NW == 8 && f % 4 == 1 && f < 32) piece(sp + 1, f / 4);
+    if constexpr (PCST_SOLO_DMA == 0 && NW == 4 && f % 2 == 1 && f < 32) piece(sp + 1, f / 2);
     if constexpr (PCST_SOLO_DMA == 1 && f >= 1 && f <= 8) piece(sp + 1, f - 1);
   };
   auto none = [](auto) {};
@@ -1429,12 +1448,12 @@ __global__ __launch_bounds__(kThreads) void noise_mlp_solo_kernel(
 #pragma unroll
   for (int i = 0; i < 8; ++i) piece(0, i);
   float* sb = reinterpret_cast<float*>(smem + kBiasLds);
-  for (int i = tid; i < kBiasFloats; i += kThreads) sb[i] = bias[i];
-  const int64_t p0 = (int64_t)blockIdx.x * kPts + wid * 32;
-  int64_t cl[2];
-  float px[2], py[2], pz[2];
+  for (int i = tid; i < kBiasFloats; i += NW * 64) sb[i] = bias[i];
+  const int64_t p0 = (int64_t)blockIdx.x * kPts + wid * 16 * NCB;
+  int64_t cl[NCB];
+  float px[NCB], py[NCB], pz[NCB];
 #pragma unroll
-  for (int cb = 0; cb < 2; ++cb) {
+  for (int cb = 0; cb < NCB; ++cb) {
     const int64_t pq = p0 + cb * 16 + (lane & 15);
     const int64_t pc = pq < P ? pq : (P - 1);
     px[cb] = pts[pc * 3 + 0];
@@ -1445,11 +1464,11 @@ __global__ __launch_bounds__(kThreads) void noise_mlp_solo_kernel(
   bar();  // superpart 0 and the bias table are in LDS
 
   // ---- h1 = relu(W0 p + b0): 128 features = 4 k-steps, both column blocks (VALU)
-  bf16x8 h1[8];
+  bf16x8 h1[4 * NCB];
 #pragma unroll
   for (int s = 0; s < 4; ++s)
 #pragma unroll
-    for (int cb = 0; cb < 2; ++cb) {
+    for (int cb = 0; cb < NCB; ++cb) {
       bf16x8 o;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
@@ -1460,13 +1479,13 @@ __global__ __launch_bounds__(kThreads) void noise_mlp_solo_kernel(
         v = fmaf(sb[kOffW0 + f * 3 + 2], pz[cb], v);
         o[j] = (__bf16)fmaxf(v, 0.0f);
       }
-      h1[s * 2 + cb] = o;
+      h1[s * NCB + cb] = o;
     }
 
   // ---- h2 = relu(W2 h1 + b2) (superpart 0): row block rb's bias is its accumulator's start
-  bf16x8 xb[16];  // a K = 256 operand [ks*2 + cb]: here h2, later bf16(x)
+  bf16x8 xb[8 * NCB];  // a K = 256 operand [ks*2 + cb]: here h2, later bf16(x)
   {
-    f32x4 acc[32];
+    f32x4 acc[16 * NCB];
     f32x4 bq;
     auto xr = [&](auto fc) {
       constexpr int f = decltype(fc)::value;
@@ -1483,32 +1502,41 @@ __global__ __launch_bounds__(kThreads) void noise_mlp_solo_kernel(
         }
       }
 #pragma unroll
-      for (int cb = 0; cb < 2; ++cb)
-        acc[rb * 2 + cb] = mfma16(a, h1[ks * 2 + cb], ks == 0 ? bq : acc[rb * 2 + cb]);
+      for (int cb = 0; cb < NCB; ++cb)
+        acc[rb * NCB + cb] = mfma16(a, h1[ks * NCB + cb], ks == 0 ? bq : acc[rb * NCB + cb]);
     };
     auto po = [&](auto fc) {
       constexpr int f = decltype(fc)::value, rb = f / 4;
       // operand k-step s from row blocks 2s, 2s+1, two fragments after the last one's MFMAs
       if constexpr (f % 4 == 1 && rb >= 1 && rb % 2 == 0) {
 #pragma unroll
-        for (int cb = 0; cb < 2; ++cb)
-          xb[(rb / 2 - 1) * 2 + cb] = relu_bf16(opk(acc[(rb - 2) * 2 + cb], acc[(rb - 1) * 2 + cb]));
+        for (int cb = 0; cb < NCB; ++cb)
+          xb[(rb / 2 - 1) * NCB + cb] = relu_bf16(opk(acc[(rb - 2) * NCB + cb], acc[(rb - 1) * NCB + cb]));
       }
       if constexpr (f == 63) {
 #pragma unroll
-        for (int cb = 0; cb < 2; ++cb) xb[7 * 2 + cb] = relu_bf16(opk(acc[14 * 2 + cb], acc[15 * 2 + cb]));
+        for (int cb = 0; cb < NCB; ++cb) xb[7 * NCB + cb] = relu_bf16(opk(acc[14 * NCB + cb], acc[15 * NCB + cb]));
       }
     };
     run_sp<SchH2>(slot(), xr, mf, dm, po);
   }
 
-  // ---- x = W4 h2 + cond[cloud] (superparts 1, 2); cond enters as the accumulator's start
-  f32x4 x[32];
+  // ---- x = W4 h2 + cond[cloud] (superparts 1, 2); cond enters as the accumulator's start.  The
+  // row addresses pass through an empty asm so the loads stay here, after superpart 0 (hoisted
+  // into it they would overlap its accumulators and spill); the barrier's wait covers them.
+  f32x4 x[16 * NCB];
+  {
+    const float* crow[NCB];
 #pragma unroll
-  for (int rb = 0; rb < 16; ++rb)
+    for (int cb = 0; cb < NCB; ++cb) {
+      crow[cb] = cond + cl[cb] * 256 + 4 * g;
+      asm volatile("" : "+v"(crow[cb]));
+    }
 #pragma unroll
-    for (int cb = 0; cb < 2; ++cb)
-      x[rb * 2 + cb] = *reinterpret_cast<const f32x4*>(cond + cl[cb] * 256 + rb * 16 + 4 * g);
+    for (int rb = 0; rb < 16; ++rb)
+#pragma unroll
+      for (int cb = 0; cb < NCB; ++cb) x[rb * NCB + cb] = *reinterpret_cast<const f32x4*>(crow[cb] + rb * 16);
+  }
   auto xhalf = [&](auto hc_) {
     constexpr int h = decltype(hc_)::value;
     bar();
@@ -1516,7 +1544,7 @@ __global__ __launch_bounds__(kThreads) void noise_mlp_solo_kernel(
     auto mf = [&](auto fc, const bf16x8& a) {
       constexpr int f = decltype(fc)::value, rb = h * 8 + f / 8, ks = f % 8;
 #pragma unroll
-      for (int cb = 0; cb < 2; ++cb) x[rb * 2 + cb] = mfma16(a, xb[ks * 2 + cb], x[rb * 2 + cb]);
+      for (int cb = 0; cb < NCB; ++cb) x[rb * NCB + cb] = mfma16(a, xb[ks * NCB + cb], x[rb * NCB + cb]);
     };
     run_sp<SchX>(slot(), none, mf, dm, none);
   };
@@ -1526,34 +1554,36 @@ __global__ __launch_bounds__(kThreads) void noise_mlp_solo_kernel(
   // ---- 6 residual blocks x += W2 relu(W1 x + b1) + b2, 8 superparts each.  The epilogue of hidden
   // chunk c (hb = relu(bf16(hc))) runs after W2(c-1)'s MFMAs are issued: it never waits for an MFMA,
   // and W1(c+1) (independent of hb) follows it.
-  bf16x8 hb[2] = {bf16x8{}, bf16x8{}};  // zero: layer 0's part 0 has no W2(15) (zero fragments)
-  f32x4 hc[4];
+  bf16x8 hb[NCB] = {};  // zero: layer 0's part 0 has no W2(15) (zero fragments)
+  f32x4 hc[2 * NCB];
   f32x4 b1r;  // the bias of the W1 row half whose first fragment comes next
   auto w1 = [&](auto ic, const bf16x8& a) {  // fragment (r, ks) of a W1 chunk, ic = 8r + ks
     constexpr int i = decltype(ic)::value, r = i / 8, ks = i % 8;
 #pragma unroll
-    for (int cb = 0; cb < 2; ++cb) hc[r * 2 + cb] = mfma16(a, xb[ks * 2 + cb], ks == 0 ? b1r : hc[r * 2 + cb]);
+    for (int cb = 0; cb < NCB; ++cb) hc[r * NCB + cb] = mfma16(a, xb[ks * NCB + cb], ks == 0 ? b1r : hc[r * NCB + cb]);
   };
   auto w2 = [&](auto rc, const bf16x8& a) {  // row block rc of a W2 chunk column
     constexpr int rb = decltype(rc)::value;
 #pragma unroll
-    for (int cb = 0; cb < 2; ++cb) x[rb * 2 + cb] = mfma16(a, hb[cb], x[rb * 2 + cb]);
+    for (int cb = 0; cb < NCB; ++cb) x[rb * NCB + cb] = mfma16(a, hb[cb], x[rb * NCB + cb]);
   };
   auto epi = [&]() {
 #pragma unroll
-    for (int cb = 0; cb < 2; ++cb) hb[cb] = relu_bf16(opk(hc[cb], hc[2 + cb]));
+    for (int cb = 0; cb < NCB; ++cb) hb[cb] = relu_bf16(opk(hc[cb], hc[NCB + cb]));
   };
   for (int layer = 0; layer < 6; ++layer) {
-    const uint32_t b1a = ba + (kOffB1 + layer * 512) * 4;   // chunk c, row half r: + (32c + 16r)*4
-    const uint32_t b2a = ba + (kOffBB2 + layer * 256) * 4;
+    // bias byte offsets of this layer (uniform); each read adds its own to ba, so no per-layer
+    // lane address stays live across the layer (it would spill)
+    const uint32_t b1o = (kOffB1 + layer * 512) * 4;   // chunk c, row half r: + (32c + 16r)*4
+    const uint32_t b2o = (kOffBB2 + layer * 256) * 4;
     bar();
     ++sp;
     {  // parts 0, 1: W2(15) of the previous layer | xb = bf16(x), x += b2 | W1(0) || W1(1) | W2(0)
       f32x4 bq[2];
       auto xr = [&](auto fc) {
         constexpr int f = decltype(fc)::value;
-        if constexpr (f == 14 || f == 22 || f == 30 || f == 38) b1r = lds_f4(b1a, (f - 14) / 8 * 64);
-        if constexpr (f >= 15 && f < 31) bq[(f - 15) % 2] = lds_f4(b2a, (f - 15) * 64);
+        if constexpr (f == 14 || f == 22 || f == 30 || f == 38) b1r = lds_f4(ba + here(b1o), (f - 14) / 8 * 64);
+        if constexpr (f >= 15 && f < 31) bq[(f - 15) % 2] = lds_f4(ba + here(b2o), (f - 15) * 64);
       };
       auto mf = [&](auto fc, const bf16x8& a) {
         constexpr int f = decltype(fc)::value;
@@ -1573,13 +1603,12 @@ __global__ __launch_bounds__(kThreads) void noise_mlp_solo_kernel(
         if constexpr (f >= 3 && f <= 17 && f % 2 == 1) {
           constexpr int s = (f - 3) / 2;
 #pragma unroll
-          for (int cb = 0; cb < 2; ++cb) xb[s * 2 + cb] = opk(x[(2 * s) * 2 + cb], x[(2 * s + 1) * 2 + cb]);
+          for (int cb = 0; cb < NCB; ++cb) xb[s * NCB + cb] = opk(x[(2 * s) * NCB + cb], x[(2 * s + 1) * NCB + cb]);
         }
         if constexpr (f >= 16 && f < 32) {  // x += b2 (x's W2 products of this layer come later)
           constexpr int rb = f - 16;
           wait_f4<extra_after<SchL0>(f - 1, f)>(bq[rb % 2]);
-          x[rb * 2] += bq[rb % 2];
-          x[rb * 2 + 1] += bq[rb % 2];
+          for (int cb = 0; cb < NCB; ++cb) x[rb * NCB + cb] += bq[rb % 2];
         }
         if constexpr (f == 31 || f == 63) epi();  // chunk 0 / chunk 1
       };
@@ -1588,11 +1617,11 @@ __global__ __launch_bounds__(kThreads) void noise_mlp_solo_kernel(
     for (int m = 1; m < 8; ++m) {  // parts 2m, 2m + 1: W1(2m) | W2(2m-1) || W1(2m+1) | W2(2m)
       bar();
       ++sp;
-      const uint32_t bm = b1a + m * 256;
+      const uint32_t bmo = b1o + m * 256;
       auto xr = [&](auto fc) {
         constexpr int f = decltype(fc)::value;
-        if constexpr (f == 0 || f == 6) b1r = lds_f4(bm, (f / 6) * 64);
-        if constexpr (f == 30 || f == 38) b1r = lds_f4(bm, 128 + (f - 30) / 8 * 64);
+        if constexpr (f == 0 || f == 6) b1r = lds_f4(ba + here(bmo), (f / 6) * 64);
+        if constexpr (f == 30 || f == 38) b1r = lds_f4(ba + here(bmo), 128 + (f - 30) / 8 * 64);
       };
       auto mf = [&](auto fc, const bf16x8& a) {
         constexpr int f = decltype(fc)::value;
@@ -1614,10 +1643,10 @@ __global__ __launch_bounds__(kThreads) void noise_mlp_solo_kernel(
   if (PCST_SOLO_STAMPS) st_res = __builtin_amdgcn_s_memtime();
 
   // ---- tail: W2(15) of layer 5, then the output MLP 256 -> 256 -> 128 -> 3
-  f32x4 acc[32];   // out0 (32), then out1 (16)
-  bf16x8 o1[16];   // out0's output: out1's K = 256 operand
-  bf16x8 o2[8];    // out1's output: out2's K = 128 operand
-  f32x4 acc2[2];
+  f32x4 acc[16 * NCB];   // out0 (16 row blocks), then out1 (8)
+  bf16x8 o1[8 * NCB];   // out0's output: out1's K = 256 operand
+  bf16x8 o2[4 * NCB];    // out1's output: out2's K = 128 operand
+  f32x4 acc2[NCB];
   f32x4 bq[2];
   auto tail = [&](auto kc) {
     constexpr int K = decltype(kc)::value;
@@ -1638,17 +1667,17 @@ __global__ __launch_bounds__(kThreads) void noise_mlp_solo_kernel(
       } else if constexpr (t < 144) {
         constexpr int rb = (t - 16) / 8, ks = (t - 16) % 8;
 #pragma unroll
-        for (int cb = 0; cb < 2; ++cb)
-          acc[rb * 2 + cb] = mfma16(a, xb[ks * 2 + cb], ks == 0 ? zero : acc[rb * 2 + cb]);
+        for (int cb = 0; cb < NCB; ++cb)
+          acc[rb * NCB + cb] = mfma16(a, xb[ks * NCB + cb], ks == 0 ? zero : acc[rb * NCB + cb]);
       } else if constexpr (t < 208) {
         constexpr int rb = (t - 144) / 8, ks = (t - 144) % 8;
 #pragma unroll
-        for (int cb = 0; cb < 2; ++cb)
-          acc[rb * 2 + cb] = mfma16(a, o1[ks * 2 + cb], ks == 0 ? zero : acc[rb * 2 + cb]);
+        for (int cb = 0; cb < NCB; ++cb)
+          acc[rb * NCB + cb] = mfma16(a, o1[ks * NCB + cb], ks == 0 ? zero : acc[rb * NCB + cb]);
       } else {
         constexpr int ks = t - 208;
 #pragma unroll
-        for (int cb = 0; cb < 2; ++cb) acc2[cb] = mfma16(a, o2[ks * 2 + cb], ks == 0 ? zero : acc2[cb]);
+        for (int cb = 0; cb < NCB; ++cb) acc2[cb] = mfma16(a, o2[ks * NCB + cb], ks == 0 ? zero : acc2[cb]);
       }
     };
     auto po = [&](auto fc) {
@@ -1656,39 +1685,38 @@ __global__ __launch_bounds__(kThreads) void noise_mlp_solo_kernel(
       if constexpr (t >= 3 && t <= 17 && t % 2 == 1) {  // xb = bf16(x), as in a layer's part 0
         constexpr int s = (t - 3) / 2;
 #pragma unroll
-        for (int cb = 0; cb < 2; ++cb) xb[s * 2 + cb] = opk(x[(2 * s) * 2 + cb], x[(2 * s + 1) * 2 + cb]);
+        for (int cb = 0; cb < NCB; ++cb) xb[s * NCB + cb] = opk(x[(2 * s) * NCB + cb], x[(2 * s + 1) * NCB + cb]);
       }
       if constexpr (t >= 16 && t < 144 && (t - 16) % 8 == 7) {  // out0 row block rb done
         constexpr int rb = (t - 16) / 8;
         wait_f4<extra_after<S>(f - 2, f)>(bq[rb % 2]);
-        acc[rb * 2] += bq[rb % 2];
-        acc[rb * 2 + 1] += bq[rb % 2];
+        for (int cb = 0; cb < NCB; ++cb) acc[rb * NCB + cb] += bq[rb % 2];
         if constexpr (rb % 2 == 1) {
 #pragma unroll
-          for (int cb = 0; cb < 2; ++cb)
-            o1[(rb / 2) * 2 + cb] = relu_bf16(opk(acc[(rb - 1) * 2 + cb], acc[rb * 2 + cb]));
+          for (int cb = 0; cb < NCB; ++cb)
+            o1[(rb / 2) * NCB + cb] = relu_bf16(opk(acc[(rb - 1) * NCB + cb], acc[rb * NCB + cb]));
         }
       }
       if constexpr (t >= 144 && t < 208 && (t - 144) % 8 == 7) {  // out1 row block rb done
         constexpr int rb = (t - 144) / 8;
         wait_f4<extra_after<S>(f - 2, f)>(bq[rb % 2]);
-        acc[rb * 2] += bq[rb % 2];
-        acc[rb * 2 + 1] += bq[rb % 2];
+        for (int cb = 0; cb < NCB; ++cb) acc[rb * NCB + cb] += bq[rb % 2];
         if constexpr (rb % 2 == 1) {
 #pragma unroll
-          for (int cb = 0; cb < 2; ++cb)
-            o2[(rb / 2) * 2 + cb] = relu_bf16(opk(acc[(rb - 1) * 2 + cb], acc[rb * 2 + cb]));
+          for (int cb = 0; cb < NCB; ++cb)
+            o2[(rb / 2) * NCB + cb] = relu_bf16(opk(acc[(rb - 1) * NCB + cb], acc[rb * NCB + cb]));
         }
       }
     };
     run_sp<S>(slot(), xr, mf, dm, po);
   };
   sfor<0, 4>(tail);
-  if (g == 0) {
+  const uint32_t ln = lane_id();  // (recomputed: not kept live through the kernel)
+  if (ln < 16) {                   // lane group 0 holds rows 0..3
     const float o0 = sb[kOffO4 + 0], o1v = sb[kOffO4 + 1], o2v = sb[kOffO4 + 2];
 #pragma unroll
-    for (int cb = 0; cb < 2; ++cb) {
-      const int64_t q = (int64_t)blockIdx.x * kPts + wid * 32 + cb * 16 + (lane & 15);
+    for (int cb = 0; cb < NCB; ++cb) {
+      const int64_t q = (int64_t)here(blockIdx.x * kPts + wid * 16 * NCB + cb * 16) + ln;
       if (q < P) {
         out[q * 3 + 0] = acc2[cb][0] + o0;
         out[q * 3 + 1] = acc2[cb][1] + o1v;
@@ -1710,7 +1738,7 @@ __global__ __launch_bounds__(kThreads) void noise_mlp_solo_kernel(
     st[6] = (float)(t1 - st_res);
     st[7] = 1.0f;
   }
-  if (wflag) last_group_wait(wflag, wvalue, wcount, werr, wpolls);
+  if (wflag) last_group_wait(wflag, wvalue, wcount, werr, wpolls, wid == 0 && lane_id() == 0);
 }
 
 }  // namespace solo
@@ -1815,7 +1843,7 @@ extern "C" int pcst_noise_mlp(const float* pts, int64_t P, int64_t points_per_cl
   if (P == 0) return PCST_OK;
   hipStream_t s = as_stream(stream);
   if (precision == 3) {
-    hipLaunchKernelGGL(solo::noise_mlp_solo_kernel, dim3((unsigned)cdiv(P, solo::kPts)), dim3(solo::kThreads),
+    hipLaunchKernelGGL(solo::noise_mlp_solo_kernel<solo::kNCB>, dim3((unsigned)cdiv(P, solo::kPts)), dim3(16 / solo::kNCB * 64),
                        solo::kLds, s, pts, P, points_per_cloud, cond, nclouds, (const char*)blob,
                        solo::kNSP, bias, out, (const uint32_t*)nullptr, 0u, (uint32_t*)nullptr,
                        (int32_t*)nullptr, (int64_t)0, (uint32_t*)nullptr, 0u);
@@ -1890,7 +1918,7 @@ extern "C" int pcst_noise_mlp_ex(const float* pts, int64_t P, int64_t points_per
   PCST_CHECK_ARG(((uintptr_t)blob & 15) == 0, "noise_mlp_ex: blob must be 16-byte aligned");
   PCST_CHECK_ARG(!wait_flag || wait_counter, "noise_mlp_ex: a wait needs its counter");
   if (precision == 3) {
-    hipLaunchKernelGGL(solo::noise_mlp_solo_kernel, dim3((unsigned)cdiv(P, solo::kPts)), dim3(solo::kThreads),
+    hipLaunchKernelGGL(solo::noise_mlp_solo_kernel<solo::kNCB>, dim3((unsigned)cdiv(P, solo::kPts)), dim3(16 / solo::kNCB * 64),
                        solo::kLds, as_stream(stream), pts, P, points_per_cloud, cond, nclouds,
                        (const char*)blob, solo::kNSP, bias, out, wait_flag, wait_value, wait_counter,
                        wait_err, max_polls > 0 ? max_polls : (int64_t)kMlpWaitPolls, start_flag,

@@ -300,23 +300,47 @@ def test_ddim_loop_hierarchical(mods, golden):
     assert_mostly_close(out.cpu().numpy(), g["out"])
 
 
-@pytest.mark.parametrize("heavy", [0, 1, 20000])
-def test_chamfer_bwd_segmented_scatter_vs_float64(heavy):
+def _fma32(a, b, c):
+    """fp32 fma(a, b, c): the product of two fp32 values is exact in float64; the float64 sum is
+    rounded once more before the fp32 rounding (double rounding, off by one fp32 ulp with
+    probability ~2^-29 per operation)."""
+    return (a.astype(np.float64) * b.astype(np.float64) + c.astype(np.float64)).astype(np.float32)
+
+
+def _expanded_d32(p, q):
+    """The reference's fp32 expanded distance of each pair p[k], q[k] (losses.py:24-25,35-37):
+    (|p|^2 + |q|^2) + (-2 p.q) with unfused ((x^2 + y^2) + z^2) norms, the K=3 sgemm dot as an fma
+    chain, and -2 dot exact so the last add is one rounding (csrc/chamfer.hip cd_dist's contract,
+    SURVEY Q1/Q2).  Negative where rounding makes it so: the clamp (losses.py:38,55) then drops
+    the pair's gradient."""
+    p, q = p.astype(np.float32), q.astype(np.float32)
+    n_p = (p[:, 0] * p[:, 0] + p[:, 1] * p[:, 1]) + p[:, 2] * p[:, 2]
+    n_q = (q[:, 0] * q[:, 0] + q[:, 1] * q[:, 1]) + q[:, 2] * q[:, 2]
+    dot = _fma32(p[:, 2], q[:, 2], _fma32(p[:, 1], q[:, 1], p[:, 0] * q[:, 0]))
+    return _fma32(np.full_like(dot, -2.0), dot, n_p + n_q)
+
+
+@pytest.mark.parametrize("heavy,centre,spread", [(0, 12.0, 0.5), (1, 12.0, 0.5), (20000, 12.0, 0.5),
+                                                 (20000, 40.0, 0.05)])
+def test_chamfer_bwd_segmented_scatter_vs_float64(heavy, centre, spread):
     """pcst_chamfer_bwd's scatter onto the argmin side (segmented sums over the sorted
     (destination, row) pairs, partials of segments that span blocks completed in order) against a
     float64 restatement of the autograd gradient, with `heavy` target rows sharing one predicted
     point as their nearest (a segment spanning ~20 of the 1024-entry blocks), ragged sizes, and
-    twice the same call for determinism."""
+    twice the same call for determinism.  The (40, 40, 40) +- 0.05 cluster is the clamp case:
+    |p|^2 = 4800 puts the fp32 ulp of the expanded distance (2^-11) at the size of the true
+    squared distances (~0.0075), so a share of the cluster's pairs round below 0 and the
+    reference's clamp (losses.py:36-41,53-58) zeroes their gradient; the expectation drops exactly
+    the pairs whose fp32 expanded distance (_expanded_d32) is < 0."""
     from pointcloud_style_transfer_amd import _hip
 
-    rng = np.random.default_rng(17 + heavy)
+    rng = np.random.default_rng(17 + heavy + int(centre))
     B, N, M = 2, 3001, 40003
     p = (rng.standard_normal((B, N, 3)) * 4).astype(np.float32)
     q = (rng.standard_normal((B, M, 3)) * 4).astype(np.float32)
-    if heavy:  # (away from the other points, and no pair close enough for the expanded fp32
-        # distance to round below 0, where the gradient is dropped -- the reference's clamp)
-        p[:, 7] = (12.0, 0.0, 0.0)
-        q[:, :heavy] = ((12.0, 0.0, 0.0) + rng.standard_normal((B, heavy, 3)) * 0.5).astype(np.float32)
+    if heavy:  # away from the other points
+        p[:, 7] = (centre, centre, centre)
+        q[:, :heavy] = ((centre, centre, centre) + rng.standard_normal((B, heavy, 3)) * spread).astype(np.float32)
     P, Q = dev(p), dev(q)
     out, a1, a2 = _hip.chamfer_fwd(P, Q, 1)
     gout = dev(np.array([0.7, 1.3], np.float32))
@@ -325,24 +349,32 @@ def test_chamfer_bwd_segmented_scatter_vs_float64(heavy):
     assert torch.equal(gp, gp2) and torch.equal(gt, gt2)
     a1, a2 = a1.cpu().numpy(), a2.cpu().numpy()
     p64, q64 = p.astype(np.float64), q.astype(np.float64)
+    dropped = 0
     for b in range(B):
         g = float(gout[b])
+        keep1 = (_expanded_d32(p[b], q[b][a1[b]]) >= 0).astype(np.float64)[:, None]   # rows of P
+        keep2 = (_expanded_d32(p[b][a2[b]], q[b]) >= 0).astype(np.float64)[:, None]   # rows of Q
+        dropped += int((keep1 == 0).sum() + (keep2 == 0).sum())
         # float64 sums, with each destination's sum of |terms| and term count for the fp32 bound
         # (fp32 sums of n terms in blocks: ~sqrt(n) 2^-24 sum|terms|, with a 4x margin -- a dropped
         # 1024-entry block of the 20000-row destination would exceed it ~20x)
-        d_p = 2 * g / N * (p64[b] - q64[b][a1[b]])
+        d_p = keep1 * 2 * g / N * (p64[b] - q64[b][a1[b]])
         want_p, abs_p, cnt_p = d_p.copy(), np.abs(d_p), np.ones(N)
-        t_p = 2 * g / M * (p64[b][a2[b]] - q64[b])
+        t_p = keep2 * 2 * g / M * (p64[b][a2[b]] - q64[b])
         np.add.at(want_p, a2[b], t_p)
         np.add.at(abs_p, a2[b], np.abs(t_p))
         np.add.at(cnt_p, a2[b], 1.0)
-        d_q = 2 * g / M * (q64[b] - p64[b][a2[b]])
+        d_q = keep2 * 2 * g / M * (q64[b] - p64[b][a2[b]])
         want_q, abs_q, cnt_q = d_q.copy(), np.abs(d_q), np.ones(M)
-        t_q = 2 * g / N * (q64[b][a1[b]] - p64[b])
+        t_q = keep1 * 2 * g / N * (q64[b][a1[b]] - p64[b])
         np.add.at(want_q, a1[b], t_q)
         np.add.at(abs_q, a1[b], np.abs(t_q))
         np.add.at(cnt_q, a1[b], 1.0)
         for got, want, ab, cnt in ((gp[b], want_p, abs_p, cnt_p), (gt[b], want_q, abs_q, cnt_q)):
             got = got.cpu().numpy().astype(np.float64)
             tol = (4 * np.sqrt(cnt[:, None]) + 2) * 2.0 ** -23 * ab + 1e-30
-            assert bool((np.abs(got - want) <= tol).all()), (heavy, np.abs(got - want).max())
+            assert bool((np.abs(got - want) <= tol).all()), (heavy, centre, np.abs(got - want).max())
+    if centre == 40.0:
+        assert dropped >= 4, dropped   # the case exercises the clamp (~8 pairs per cloud)
+    else:
+        assert dropped == 0, dropped

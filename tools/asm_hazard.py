@@ -16,11 +16,12 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def regs(tok):
+    """VGPRs and AGPRs named in an operand string, as ('v'|'a', index)"""
     out = set()
-    for m in re.finditer(r"v\[(\d+):(\d+)\]", tok):
-        out |= set(range(int(m.group(1)), int(m.group(2)) + 1))
-    for m in re.finditer(r"\bv(\d+)\b", tok):
-        out.add(int(m.group(1)))
+    for m in re.finditer(r"\b([va])\[(\d+):(\d+)\]", tok):
+        out |= {(m.group(1), i) for i in range(int(m.group(2)), int(m.group(3)) + 1)}
+    for m in re.finditer(r"\b([va])(\d+)\b", tok):
+        out.add((m.group(1), int(m.group(2))))
     return out
 
 

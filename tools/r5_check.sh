@@ -12,7 +12,7 @@
 set -u
 TAG=$1; shift; OUT=gpurun_out/$TAG; mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-BENCH="bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline --no-encoder --no-other-precision"
+BENCH="bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline --no-encoder --no-other-precision --no-extra"
 for st in "$@"; do
   case $st in
     tests=*)
@@ -37,7 +37,7 @@ for st in "$@"; do
     pmc)
       # counter passes serialise every queue's dispatches: the single-stream step layout (no
       # cross-stream flag waits, which would spin to their poll bound), 10 steps
-      PB="tools/bench_knobs.py --gpus 1 --steps 10 --warmup 2 --no-cpu-baseline --no-encoder --no-other-precision"
+      PB="tools/bench_knobs.py --gpus 1 --steps 10 --warmup 2 --no-cpu-baseline --no-encoder --no-other-precision --no-extra"
       PCST_KNN_OVERLAP=0 timeout -s KILL 300 rocprofv3 --pmc SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_INST_LDS \
           SQ_INSTS_LDS SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --output-format csv -d "$OUT/p1" -o pmc -- \
           python $PB > "$OUT/p1.log" 2>&1
@@ -51,7 +51,7 @@ for st in "$@"; do
       python tools/pmc_summary.py "$OUT" noise_mlp --json "$OUT/noise_mlp_traffic.json" | tail -4 ;;
     b32)
       timeout -k 10 300 python bench.py --gpus 1 --clouds-per-gpu 32 --steps 20 --warmup 3 --no-cpu-baseline \
-          --no-encoder --no-other-precision > "$OUT/bench_b32.json" 2> "$OUT/bench_b32.err"
+          --no-encoder --no-other-precision --no-extra > "$OUT/bench_b32.json" 2> "$OUT/bench_b32.err"
       rc=$?; echo "b32 rc=$rc"; if [ $rc -ne 0 ]; then tail -3 "$OUT/bench_b32.err"; exit $rc; fi
       python -c "import json;d=json.loads(open('$OUT/bench_b32.json').read().strip().splitlines()[-1]);print('b32', d['value'], d['ms_per_step'], d['roofline']['avg_launch_ms'], d['roofline']['frac'])" ;;
     train)
@@ -108,8 +108,8 @@ for st in "$@"; do
       done ;;
     b32prof)
       timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/b32prof" -o run -- \
-          python bench.py --gpus 1 --clouds-per-gpu 32 --steps 10 --warmup 3 --no-cpu-baseline --no-encoder \
-          --no-other-precision > "$OUT/b32prof.json" 2> "$OUT/b32prof.err"
+          python bench.py --gpus 1 --clouds-per-gpu 32 --steps 10 --warmup 3 --no-cpu-baseline --no-encoder --no-extra \
+          --no-other-precision --no-extra > "$OUT/b32prof.json" 2> "$OUT/b32prof.err"
       rc=$?; echo "b32prof rc=$rc"; if [ $rc -ne 0 ]; then tail -5 "$OUT/b32prof.err"; exit $rc; fi
       python tools/kstats.py "$OUT/b32prof/run_kernel_stats.csv" 25 | tee "$OUT/b32_kernel_top.txt" ;;
     libtests=*)
@@ -128,7 +128,7 @@ for st in "$@"; do
           PCST_LIB=$lib timeout -k 10 200 python $BENCH > "$OUT/bench_$v.$pass.json" 2> "$OUT/bench_$v.$pass.err"
           rc=$?; if [ $rc -ne 0 ]; then tail -3 "$OUT/bench_$v.$pass.err"; exit $rc; fi
           PCST_LIB=$lib timeout -k 10 200 python bench.py --gpus 1 --clouds-per-gpu 32 --steps 10 --warmup 3 \
-              --no-cpu-baseline --no-encoder --no-other-precision > "$OUT/b32_$v.$pass.json" 2> "$OUT/b32_$v.$pass.err"
+              --no-cpu-baseline --no-encoder --no-other-precision --no-extra > "$OUT/b32_$v.$pass.json" 2> "$OUT/b32_$v.$pass.err"
           rc=$?; if [ $rc -ne 0 ]; then tail -3 "$OUT/b32_$v.$pass.err"; exit $rc; fi
           python -c "import json,sys; f=lambda p: json.loads(open(p).read().strip().splitlines()[-1]); a=f(sys.argv[1]); b=f(sys.argv[2]); print(sys.argv[3], 'b1', a['value'], a['ms_per_step'], a['roofline']['avg_launch_ms'], 'b32', b['ms_per_step'])" "$OUT/bench_$v.$pass.json" "$OUT/b32_$v.$pass.json" "$v.$pass"
         done
@@ -141,10 +141,10 @@ for st in "$@"; do
         for v in prod ${VS//,/ }; do
           kv=PCST_NONE=1; if [ "$v" != prod ]; then kv=$v; fi
           env "$kv" timeout -k 10 200 python tools/bench_knobs.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline \
-              --no-encoder --no-other-precision > "$OUT/bench_$v.$pass.json" 2> "$OUT/bench_$v.$pass.err"
+              --no-encoder --no-other-precision --no-extra > "$OUT/bench_$v.$pass.json" 2> "$OUT/bench_$v.$pass.err"
           rc=$?; if [ $rc -ne 0 ]; then tail -3 "$OUT/bench_$v.$pass.err"; exit $rc; fi
           env "$kv" timeout -k 10 200 python tools/bench_knobs.py --gpus 1 --clouds-per-gpu 32 --steps 10 --warmup 3 \
-              --no-cpu-baseline --no-encoder --no-other-precision > "$OUT/b32_$v.$pass.json" 2> "$OUT/b32_$v.$pass.err"
+              --no-cpu-baseline --no-encoder --no-other-precision --no-extra > "$OUT/b32_$v.$pass.json" 2> "$OUT/b32_$v.$pass.err"
           rc=$?; if [ $rc -ne 0 ]; then tail -3 "$OUT/b32_$v.$pass.err"; exit $rc; fi
           python -c "import json,sys; f=lambda p: json.loads(open(p).read().strip().splitlines()[-1]); a=f(sys.argv[1]); b=f(sys.argv[2]); print(sys.argv[3], 'b1', a['value'], a['ms_per_step'], a['roofline']['avg_launch_ms'], 'b32', b['ms_per_step'])" "$OUT/bench_$v.$pass.json" "$OUT/b32_$v.$pass.json" "$v.$pass"
         done

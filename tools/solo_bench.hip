@@ -87,7 +87,7 @@ int main(int argc, char** argv) {
         CK(hipEventElapsedTime(&ms, e0, e1));
         const double us = 1e3 * ms / n;
         const double tf = 3540480.0 * P / (us * 1e-6) / 1e12;
-        printf("kd=%d prio=%d dma=%d exp=%d prec=%d clouds=%lld  %.1f us/launch  %.1f TFLOP/s  frac %.4f\n", PCST_SOLO_KD,
+        printf("ncb=%d kd=%d prio=%d dma=%d exp=%d prec=%d clouds=%lld  %.1f us/launch  %.1f TFLOP/s  frac %.4f\n", PCST_SOLO_NCB, PCST_SOLO_KD,
                PCST_SOLO_PRIO, PCST_SOLO_DMA, PCST_SOLO_EXP, prec, (long long)C, us, tf, tf / 2500.0);
         if (PCST_SOLO_STAMPS == 2 && prec == 3 && rep == 1) {
           // per barrier k: arrival spread over the 8 waves and |wave w - wave w+4| (one SIMD), mean
