@@ -483,8 +483,10 @@ def main():
             state.begin(torch.cuda.current_stream())
             with torch.cuda.stream(loop_stream):
                 knn_ws = _hip.knn_workspace(2 * C, args.points, cfg.global_points, device=device)
+                rows_ws = (_hip.knn_rows_workspace(C, 2, args.points, cfg.global_points, device)
+                           if dmod.rows_layout_ok(2 * C * cfg.global_points) else None)
         else:
-            knn_ws = None
+            knn_ws = rows_ws = None
 
         vws = _hip.voxel_copies_workspace(C, args.points, 2, device=device)
         pk = npred.packed()  # the loop changes no weight (as guided_sample_loop)
@@ -504,7 +506,12 @@ def main():
             t = timesteps[i % len(timesteps)]
             t_prev = timesteps[i % len(timesteps) + 1] if t > 0 else -1
             cnd = conds[i % len(timesteps)]
-            xc, xi = hp.downsample_copies(x, 2, vws, prepped, next_seed, pool)
+            # the rows layout: the kNN's positions-only phase on the side stream beside the
+            # downsample (as guided_sample_loop)
+            rows, start = (dmod.knn_rows_begin(x, cfg.global_points, state, rows_ws,
+                                               by_downsample=prepped)
+                           if rows_ws is not None else (None, None))
+            xc, xi = hp.downsample_copies(x, 2, vws, prepped, next_seed, pool, start)
 
             def mlp(xc_, wait=None, start=None):
                 if not timed:
@@ -528,7 +535,7 @@ def main():
             x = dmod.hierarchical_step(hp, mlp, xc, xi, x_cat, x, src, 7.5, dp._coeffs(t, t_prev),
                                        knn_ws, state, mlp_waits=dmod.MLP_WAITS,
                                        mlp_signals=dmod.MLP_SIGNALS, vox_ws=vws if prep else None,
-                                       pool_seed=next_seed)
+                                       pool_seed=next_seed, rows=rows)
             prepped, pool = prep, next_seed is not None
 
         lctx = torch.cuda.stream(loop_stream) if overlap else contextlib.nullcontext()

@@ -259,15 +259,22 @@ int pcst_voxel_downsample_copies(const float* pts, int64_t B, int64_t N, int64_t
  * pool != 0 (N <= 4M): the update also makes that downsample's pool-key histogram for the seed
  * pool_seed it will be called with (the keys depend on (seed, row, index) only), which the
  * downsample's insert otherwise makes on the step's critical path; that call must then pass
- * pool = 1 and seed = pool_seed. */
+ * pool = 1 and seed = pool_seed.  A pool prep adds into the workspace's pool histogram, which only
+ * that downsample clears (its emit, after reading it): every pool prep must be followed by its
+ * matching prepped downsample on the same workspace before the next prep, or the histogram keeps
+ * stale counts (a caller whose step raised in between must re-zero the workspace). */
 int pcst_cfg_ddim_voxel_prep(const float* x, const float* eps, const float* source, int64_t C,
                              int64_t N, float guidance_scale, float sqrt_1m_at, float sqrt_at_eps,
                              float sqrt_aprev, float sqrt_1m_aprev, float* x_out, float* x_cat,
                              void* vox_workspace, int64_t copies, uint64_t pool_seed, int pool,
                              void* stream);
+/* start_flag (NULL: none): written with start_value as the downsample's first launch begins,
+ * i.e. once every launch ahead of it on `stream` has completed -- the pts are final -- for work
+ * on another stream that waits for it (the sampling step's kNN rows build, pcst_signal_wait). */
 int pcst_voxel_downsample_copies_prepped(const float* pts, int64_t B, int64_t N, int64_t copies,
                                          int64_t target, void* workspace, uint64_t seed, int pool,
-                                         int64_t* out_idx, float* out_pts, void* stream);
+                                         int64_t* out_idx, float* out_pts, uint32_t* start_flag,
+                                         uint32_t start_value, void* stream);
 /* Copies the replay-validation error word (0 = ok) to err_out (device int32). */
 int pcst_voxel_error(void* workspace, int64_t B, int64_t N, int32_t* err_out, void* stream);
 
@@ -320,12 +327,48 @@ int pcst_knn3_finish_cfg_ddim(const float* coarse, int64_t B, int64_t N, int64_t
 int pcst_knn_stats(void* workspace, int64_t B, int64_t N, int64_t M, int32_t* out, void* stream);
 int pcst_knn_error(void* workspace, int64_t B, int64_t N, int64_t M, int32_t* err_out,
                    void* stream);
+/* The same upsample in the rows layout (the sampling step's): the CFG batch's B = C * copies rows,
+ * row b a copy of cloud b % C of x [C,N,3] (guided_sample_loop's cat([x, x])).
+ *   rows_build (positions of x only, before the coarse indices exist): every point of every
+ *     cloud binned by cell -- the grid statistics (those of pcst_knn3_build, sized for M refs),
+ *     per-cell counts, scan, the query chunks over all points, the points in cell order.
+ *     refs_flag / done_flag (NULL: none): written with their values once rows_refs may run on
+ *     another stream (after the scan) and once the whole build is done (after the fill);
+ *   rows_refs (idx [B,M] int64): each ref marks its point known (the last j wins) and takes a slot
+ *     at the front of its point's cell range and one at the front of its brick's; a ref beyond
+ *     either range's rows (repeated indices piling up) also goes to the row's overflow list, which
+ *     the query offers wherever its scanned box holds them.  wait_flag (NULL: none): the kernel
+ *     first waits, in every work-group, until the flag holds wait_value (the side stream's
+ *     pcst_signal_write after rows_build), at most max_polls polls (<= 0: ~10 s); a wait that gives
+ *     up sets *wait_err and places nothing (as pcst_signal_wait's error word);
+ *   rows_query (coarse [B,M,3] -> out [B,N,3]): the query and outlier passes of pcst_knn3_query
+ *     over every point, known points copying their coarse value; built_flag (the build's
+ *     done_flag): every query work-group waits for it itself (as rows_refs; on a timeout it sets
+ *     *wait_err and writes eps = 0); grid_cap as pcst_knn3_query.
+ * Same bits as pcst_knn3_interp on cat([x] * copies).  An index outside [0, N) sets bit 1 of the
+ * error word, a chunk or ref range outside the workspace's arrays bits 4 / 8 (the range is then
+ * skipped, never read); pcst_knn_rows_stats copies out[0] = error word, out[1..C] chunks per
+ * cloud, out[1+C..C+B] outlier queries, out[1+C+B..C+2B] overflow refs per row. */
+int pcst_knn_rows_workspace_size(int64_t C, int64_t copies, int64_t N, int64_t M, size_t* bytes);
+int pcst_knn3_rows_build(const float* x, int64_t C, int64_t copies, int64_t N, int64_t M,
+                         void* workspace, uint32_t* refs_flag, uint32_t refs_value,
+                         uint32_t* done_flag, uint32_t done_value, void* stream);
+int pcst_knn3_rows_refs(const float* x, const int64_t* idx, int64_t C, int64_t copies, int64_t N,
+                        int64_t M, void* workspace, const uint32_t* wait_flag, uint32_t wait_value,
+                        int32_t* wait_err, int64_t max_polls, void* stream);
+int pcst_knn3_rows_query(const float* coarse, const float* x, int64_t C, int64_t copies, int64_t N,
+                         int64_t M, float* out, void* workspace, const uint32_t* built_flag,
+                         uint32_t built_value, int32_t* wait_err, int64_t max_polls,
+                         int64_t grid_cap, void* stream);
+int pcst_knn_rows_stats(void* workspace, int64_t C, int64_t copies, int64_t N, int64_t M,
+                        int32_t* out, void* stream);
 
 /* NoisePredictor.forward (diffusion_model.py:38-61), fused.  precision: 0 = exact f32 MFMA
- * (parity); 1 = bf16 MFMA (v_mfma_f32_32x32x16_bf16) with fp32 accumulation and fp32 residual
- * stream; 2 = the same arithmetic on v_mfma_f32_16x16x32_bf16 (the product bf16 path; its own
- * fragment layout, packing.PAIR16, same blob size as 1).  blob/bias are the
- * packed weights of packing.py (blob 16-byte aligned, pcst_noise_mlp_blob_bytes() bytes).
+ * (v_mfma_f32_32x32x2_f32, the parity mode); 1 = bf16 operands on v_mfma_f32_16x16x32_bf16 with
+ * fp32 accumulation and an fp32 residual stream (the product mode).  blob/bias are the packed
+ * weights of packing.py for that precision (blob 16-byte aligned, pcst_noise_mlp_blob_bytes()
+ * bytes; -1 for any other precision).  Any other precision is PCST_EINVAL (codes 2 and 3 of
+ * rounds 2-4 are retired).
  * pcst_noise_cond computes cond[c] = b4 + time_proj(TimeEmbedding(t_c)) + style_proj(style_c)
  * (freqs = the reference's 64-entry exp table; wt = time_proj.weight^T [128,256] and
  * ws = style_proj.weight^T [256,256], transposed for coalesced reads).  pts [P,3] cloud-major with
@@ -337,24 +380,17 @@ int pcst_noise_cond(const int64_t* t, const float* style, int64_t nclouds, const
 int pcst_noise_mlp(const float* pts, int64_t P, int64_t points_per_cloud, const float* cond,
                    int64_t nclouds, const void* blob, int64_t blob_bytes, const float* bias,
                    int precision, float* out, void* stream);
-/* pcst_noise_mlp at precision 2 whose launch completes only once *flag >= value as well: after
- * writing its rows, the MLP's last work-group (a caller-owned uint32 counter, zero before the
- * call and zero again after it, counts the work-groups out) polls the flag with agent-scope loads
- * (the producer on another stream writes it with pcst_signal_write), at most max_polls times
- * (<= 0: the default, ~10 s; then *err = 1 and the launch completes anyway: the caller must read
- * *err, err may be NULL).  Work queued after it on the stream is ordered after the flag's producer
- * without a separate wait launch. */
-int pcst_noise_mlp_then_wait(const float* pts, int64_t P, int64_t points_per_cloud,
-                             const float* cond, int64_t nclouds, const void* blob,
-                             int64_t blob_bytes, const float* bias, float* out,
-                             const uint32_t* flag, uint32_t value, uint32_t* counter, int32_t* err,
-                             int64_t max_polls, void* stream);
 /* pcst_noise_mlp with optional cross-stream signalling folded into the launch (all optional):
  * start_flag: *start_flag = start_value (agent-scope store) as the launch begins, i.e. once every
  * kernel queued before it on `stream` has completed -- the producer side of pcst_signal_wait
- * without a pcst_signal_write launch; wait_flag/value/counter/err/max_polls: as
- * pcst_noise_mlp_then_wait.  Precision 2 folds both into the MLP kernel; other precisions use
- * separate one-lane launches (same ordering). */
+ * without a pcst_signal_write launch; wait_flag: the launch completes only once *wait_flag >=
+ * wait_value as well -- after writing its rows, the MLP's last work-group (counted out by
+ * wait_counter, a caller-owned uint32 that is zero before the call and zero again after it) polls
+ * the flag with agent-scope loads (the producer on another stream writes it with
+ * pcst_signal_write), at most max_polls times (<= 0: ~10 s; then *wait_err = 1 and the launch
+ * completes anyway: the caller must read it); work queued after it on the stream is then ordered
+ * after the flag's producer without a wait launch.  Precision 1 folds both into the MLP kernel;
+ * precision 0 uses separate one-lane launches (same ordering). */
 int pcst_noise_mlp_ex(const float* pts, int64_t P, int64_t points_per_cloud, const float* cond,
                       int64_t nclouds, const void* blob, int64_t blob_bytes, const float* bias,
                       int precision, float* out, uint32_t* start_flag, uint32_t start_value,

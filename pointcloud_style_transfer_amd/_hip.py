@@ -16,9 +16,9 @@ import numpy as np
 import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-# PCST_LIB overrides the library path (experiment builds of tools/ only; the product path and
-# every test load the in-tree libpcst_hip.so)
-LIB_PATH = os.environ.get("PCST_LIB") or os.path.join(_HERE, "libpcst_hip.so")
+# the in-tree library (tools/knobs.py may point an experiment run at another build before the
+# first load; the product reads no environment)
+LIB_PATH = os.path.join(_HERE, "libpcst_hip.so")
 
 _P = ctypes.c_void_p
 _I = ctypes.c_int64
@@ -45,7 +45,7 @@ SIGNATURES = {
     "pcst_voxel_copies_workspace_size": [_I, _I, _I, _SZ],
     "pcst_voxel_downsample_copies": [_P, _I, _I, _I, _I, _P, ctypes.c_uint64, _P, _P, _P],
     "pcst_voxel_downsample_copies_prepped": [_P, _I, _I, _I, _I, _P, ctypes.c_uint64, ctypes.c_int,
-                                             _P, _P, _P],
+                                             _P, _P, _P, ctypes.c_uint32, _P],
     "pcst_cfg_ddim_voxel_prep": [_P, _P, _P, _I, _I, _F, _F, _F, _F, _F, _P, _P, _P, _I,
                                  ctypes.c_uint64, ctypes.c_int, _P],
     "pcst_knn_workspace_size": [_I, _I, _I, _SZ],
@@ -60,11 +60,14 @@ SIGNATURES = {
                                   ctypes.c_uint32, _P],
     "pcst_knn_error": [_P, _I, _I, _I, _P, _P],
     "pcst_knn_stats": [_P, _I, _I, _I, _P, _P],
+    "pcst_knn_rows_workspace_size": [_I, _I, _I, _I, _SZ],
+    "pcst_knn3_rows_build": [_P, _I, _I, _I, _I, _P, _P, ctypes.c_uint32, _P, ctypes.c_uint32, _P],
+    "pcst_knn3_rows_refs": [_P, _P, _I, _I, _I, _I, _P, _P, ctypes.c_uint32, _P, _I, _P],
+    "pcst_knn3_rows_query": [_P, _P, _I, _I, _I, _I, _P, _P, _P, ctypes.c_uint32, _P, _I, _I, _P],
+    "pcst_knn_rows_stats": [_P, _I, _I, _I, _I, _P, _P],
     "pcst_noise_mlp_blob_bytes": [ctypes.c_int],
     "pcst_noise_cond": [_P, _P, _I, _P, _P, _P, _P, _P, _P, _P, _P],
     "pcst_noise_mlp": [_P, _I, _I, _P, _I, _P, _I, _P, ctypes.c_int, _P, _P],
-    "pcst_noise_mlp_then_wait": [_P, _I, _I, _P, _I, _P, _I, _P, _P, _P, ctypes.c_uint32, _P, _P, _I,
-                                 _P],
     "pcst_noise_mlp_ex": [_P, _I, _I, _P, _I, _P, _I, _P, ctypes.c_int, _P, _P, ctypes.c_uint32, _P,
                           ctypes.c_uint32, _P, _P, _I, _P],
     "pcst_cfg_ddim_step": [_P, _P, _P, _P, _I, _F, _F, _F, _F, _F, _P, _P, _P],
@@ -136,14 +139,7 @@ def lib():
                 "`python -c 'import __graft_entry__ as g; g.build()'` (no CPU fallback exists)")
         L = ctypes.CDLL(LIB_PATH)
         for name, args in SIGNATURES.items():
-            try:
-                fn = getattr(L, name)
-            except AttributeError:
-                # an experiment build (PCST_LIB) may predate an entry point; the product library
-                # must export every one (tests/test_abi.py)
-                if os.environ.get("PCST_LIB"):
-                    continue
-                raise
+            fn = getattr(L, name)  # every entry point is exported (tests/test_abi.py)
             fn.argtypes = args
             fn.restype = _RESTYPES.get(name, ctypes.c_int)
         _lib = L
@@ -175,6 +171,8 @@ def _tensor_device_index(args, kwargs):
                     return b.device.index
         elif getattr(a, "is_cuda", False):
             return a.device.index
+        elif isinstance(a, KnnRows):
+            return a.x.device.index
     return None
 
 
@@ -292,7 +290,7 @@ def voxel_copies_workspace(B, N, copies, device):
 
 
 def voxel_downsample(points, target, seed=0, perm_provider=None, copies=1, ws=None,
-                     prepped=False, pool=False):
+                     prepped=False, pool=False, start=None):
     """HierarchicalProcessor._voxel_grid_downsample_torch for N > target, all clouds at once.
 
     perm_provider=None: the random subset is drawn on the device from `seed`.
@@ -303,7 +301,8 @@ def voxel_downsample(points, target, seed=0, perm_provider=None, copies=1, ws=No
     keeps for the same seed); the replay path concatenates, as the reference's draws are per row.
     prepped=True: `ws` was prepared by cfg_ddim_voxel_prep for these points (the device-drawn
     path skips its statistics / zeroing launch); pool=True: that prep also made the pool-key
-    histogram for this `seed` (its pool_seed), so the insert skips it.
+    histogram for this `seed` (its pool_seed), so the insert skips it.  start (prepped only):
+    (flag pointer, value) of a DeviceSignal.next_value() the launch publishes as it begins.
     Returns (points [k*B,T,3], idx [k*B,T] int64)."""
     require_device(points)
     points = _f32(points)
@@ -325,10 +324,13 @@ def voxel_downsample(points, target, seed=0, perm_provider=None, copies=1, ws=No
         out_idx = torch.empty(copies * B, target, dtype=torch.int64, device=dev)
         out_pts = torch.empty(copies * B, target, 3, dtype=torch.float32, device=dev)
         if prepped:
+            sflag, sval = start if start is not None else (None, ctypes.c_uint32(0))
             _call("pcst_voxel_downsample_copies_prepped", _ptr(points), B, N, copies, target,
                   _ptr(ws), seed & (2**64 - 1), 1 if pool else 0, _ptr(out_idx), _ptr(out_pts),
-                  _stream())
+                  sflag, sval, _stream())
         else:
+            if start is not None:
+                raise RuntimeError("voxel_downsample: start= needs prepped=True")
             if pool:
                 raise RuntimeError("voxel_downsample: pool=True needs prepped=True")
             _call("pcst_voxel_downsample_copies", _ptr(points), B, N, copies, target, _ptr(ws),
@@ -404,7 +406,7 @@ class DeviceSignal:
     VALUE_LIMIT = 1 << 31
 
     def __init__(self, device, max_polls=0, storage=None):
-        # [flag, timeout error, work-group counter of pcst_noise_mlp_then_wait, pad]
+        # [flag, timeout error, work-group counter of pcst_noise_mlp_ex's wait, pad]
         self.flag = (storage if storage is not None
                      else torch.zeros(4, dtype=torch.int32, device=device))
         if self.flag.dtype != torch.int32 or self.flag.numel() != 4 or not self.flag.is_contiguous():
@@ -431,7 +433,7 @@ class DeviceSignal:
         return ctypes.c_void_p(self.flag.data_ptr()), ctypes.c_uint32(self.value)
 
     def wait_args(self):
-        """(flag, value, counter, err, max_polls) for pcst_noise_mlp_then_wait: wait for the last
+        """(flag, value, counter, err, max_polls) for pcst_noise_mlp_ex: wait for the last
         signal."""
         base = self.flag.data_ptr()
         return (ctypes.c_void_p(base), ctypes.c_uint32(self.value), ctypes.c_void_p(base + 8),
@@ -623,6 +625,104 @@ def knn3_interp(coarse, orig, idx, check=False, stats=None):
     return out
 
 
+# kNN-3 upsample, rows layout (pcst_knn3_rows_*): the sampling step's split of the build into
+# a positions-only phase over the distinct clouds (beside the voxel downsample) and a one-launch
+# ref placement after it.
+def knn_rows_workspace(C, copies, N, M, device):
+    """A workspace for knn3_rows_build / _refs / _query over C clouds x `copies` CFG rows."""
+    return _workspace("pcst_knn_rows_workspace_size", C, copies, N, M, device=device)
+
+
+class KnnRows:
+    """Handle of a rows-layout build: the clouds x [C,N,3], the CFG copies, M and the workspace."""
+
+    def __init__(self, x, copies, M, ws):
+        self.x, self.copies, self.M, self.ws = x, int(copies), int(M), ws
+
+    @property
+    def dims(self):
+        C, N, _ = self.x.shape
+        return C, self.copies, N, self.M
+
+
+def knn3_rows_build(x, M, copies=1, ws=None, refs_sig=None, done_sig=None):
+    """Phase A on the current stream: bin every point of the clouds x [C,N,3] for the query of the
+    C * copies CFG rows (row b = cloud b % C) against M refs each -> KnnRows handle.  refs_sig /
+    done_sig (DeviceSignals): signalled from this stream once knn3_rows_refs may run (after the
+    scan) and once the build is done (after the fill), for work on other streams."""
+    require_device(x)
+    x = _f32(x)
+    C, N, _ = x.shape
+    if ws is None:
+        ws = knn_rows_workspace(C, copies, N, M, x.device)
+    rf, rv = refs_sig.next_value() if refs_sig is not None else (None, ctypes.c_uint32(0))
+    df, dv = done_sig.next_value() if done_sig is not None else (None, ctypes.c_uint32(0))
+    _call("pcst_knn3_rows_build", _ptr(x), C, int(copies), N, int(M), _ptr(ws), rf, rv, df, dv,
+          _stream())
+    return KnnRows(x, copies, M, ws)
+
+
+def knn3_rows_refs(handle, idx, wait=None):
+    """Phase B on the current stream (after knn3_rows_build on the handle): the coarse indices
+    idx [C * copies, M] into the rows layout.  wait (a DeviceSignal): the launch itself waits for
+    its last signal (phase A on another stream) instead of a wait launch ahead of it; a wait that
+    gives up sets the signal's error word (its check() raises).  Returns the handle."""
+    require_device(idx)
+    idx = _i64(idx)
+    C, copies, N, M = handle.dims
+    if tuple(idx.shape) != (C * copies, M):
+        raise RuntimeError(f"knn3_rows_refs: idx {tuple(idx.shape)} != {(C * copies, M)}")
+    handle.idx = idx  # kept alive until the query
+    if wait is not None:
+        flag, value, _, err, polls = wait.wait_args()
+    else:
+        flag, value, err, polls = None, ctypes.c_uint32(0), None, ctypes.c_int64(0)
+    _call("pcst_knn3_rows_refs", _ptr(handle.x), _ptr(idx), C, copies, N, M, _ptr(handle.ws), flag,
+          value, err, polls, _stream())
+    return handle
+
+
+def knn3_rows_query(coarse, handle, built=None, grid_cap=0):
+    """coarse [C * copies, M, 3] -> [C * copies, N, 3] on the current stream (after
+    knn3_rows_refs).  built (the DeviceSignal of the build's done_sig): the query's work-groups
+    wait for its last value themselves (a timeout sets its error word and yields eps = 0);
+    grid_cap as knn3_query."""
+    require_device(coarse)
+    coarse = _f32(coarse)
+    C, copies, N, M = handle.dims
+    if tuple(coarse.shape) != (C * copies, M, 3):
+        raise RuntimeError(f"knn3_rows_query: coarse {tuple(coarse.shape)} != {(C * copies, M, 3)}")
+    out = torch.empty(C * copies, N, 3, dtype=torch.float32, device=coarse.device)
+    if built is not None:
+        flag, value, _, err, polls = built.wait_args()
+    else:
+        flag, value, err, polls = None, ctypes.c_uint32(0), None, ctypes.c_int64(0)
+    _call("pcst_knn3_rows_query", _ptr(coarse), _ptr(handle.x), C, copies, N, M, _ptr(out),
+          _ptr(handle.ws), flag, value, err, polls, int(grid_cap), _stream())
+    return out
+
+
+def knn_rows_stats(handle):
+    """{"err", "chunks" [C], "outliers" [B], "overflow" [B]} of the handle's last build / query
+    (synchronises)."""
+    C, copies, N, M = handle.dims
+    B = C * copies
+    st = torch.zeros(1 + C + 2 * B, dtype=torch.int32, device=handle.x.device)
+    _call("pcst_knn_rows_stats", _ptr(handle.ws), C, copies, N, M, _ptr(st), _stream())
+    st = st.cpu().tolist()
+    return {"err": st[0], "chunks": st[1:1 + C], "outliers": st[1 + C:1 + C + B],
+            "overflow": st[1 + C + B:]}
+
+
+def knn3_interp_rows(coarse, x, idx, copies=1):
+    """knn3_interp through the rows layout: coarse [C*copies,M,3], the clouds x [C,N,3] (CFG row
+    b is cloud b % C), idx [C*copies,M] -> [C*copies,N,3]; the same bits as
+    knn3_interp(coarse, cat([x] * copies), idx)."""
+    h = knn3_rows_build(x, idx.shape[1], copies)
+    knn3_rows_refs(h, idx)
+    return knn3_rows_query(coarse, h)
+
+
 # ----------------------------------------------------------------------------- noise MLP
 def noise_mlp_blob_bytes(precision):
     return int(lib().pcst_noise_mlp_blob_bytes(precision))
@@ -658,7 +758,7 @@ def noise_mlp(pts, points_per_cloud, cond, blob, bias, precision, out=None, wait
         _call("pcst_noise_mlp_ex", _ptr(pts), P, points_per_cloud, _ptr(cond), cond.shape[0],
               _ptr(blob), blob.numel(), _ptr(bias), precision, _ptr(out), fl, val, *w, _stream())
         return out
-    if wait is not None and precision in (2, 3) and P > 0:
+    if wait is not None and precision == 1 and P > 0:
         _call("pcst_noise_mlp_ex", _ptr(pts), P, points_per_cloud, _ptr(cond), cond.shape[0],
               _ptr(blob), blob.numel(), _ptr(bias), precision, _ptr(out), None, 0,
               *wait.wait_args(), _stream())
@@ -1241,7 +1341,8 @@ _GUARDED = ("square_distance", "index_points", "fps", "ball_query", "group_gathe
             "cfg_ddim_step_dcoef", "voxel_downsample_copies_dseed", "bn_train_coeffs",
             "bn_relu_maxpool", "bn_relu_bwd", "group_gather_bwd", "group_colsum16", "resblock_fwd16", "resblock_bwd16", "cast16_batch",
             "gemm_ex", "dropout_grad_bf16",
-            "linear_wgrad_ex", "knn_workspace", "voxel_copies_workspace")
+            "linear_wgrad_ex", "knn_workspace", "voxel_copies_workspace", "knn3_rows_build",
+            "knn3_rows_refs", "knn3_rows_query", "knn_rows_stats", "knn3_interp_rows")
 for _name in _GUARDED:
     globals()[_name] = _on_tensor_device(globals()[_name])
 del _name

@@ -83,28 +83,20 @@ __device__ __forceinline__ void cd_minpairs(const float4 (&q)[8], const cd_f2 (&
 // against segment s's chunks [s*per, (s+1)*per).  R rows share every scalar load; S segments
 // put more waves in flight.  The block combines the segments' (best, first chunk) in segment
 // order, and the winning chunk's re-scan is split over the S segments the same way.
-// kList: the rows are the first *rcount entries of rlist (the grid search's overflow rows of
-// cloud b, side `side`: list (b * 2 + side) of stride `lstride`) instead of 0..N-1.
-template <int S, int R, bool kList = false>
+template <int S, int R>
 __global__ __launch_bounds__(256 * S) void chamfer_rowmin_kernel(const float* __restrict__ P,
                                                                  const float4* __restrict__ Qp,
                                                                  int N, int M, int Mp,
                                                                  float* __restrict__ mind,
-                                                                 int32_t* __restrict__ argm,
-                                                                 const int* __restrict__ rlist = nullptr,
-                                                                 const int* __restrict__ rcount = nullptr,
-                                                                 int side = 0, int64_t lstride = 0) {
+                                                                 int32_t* __restrict__ argm) {
   __shared__ float sbest[S][256 * R];
   __shared__ int sidx[S][256 * R];
   const int b = blockIdx.y;
   const int r = threadIdx.x & 255;
   const int seg = __builtin_amdgcn_readfirstlane(threadIdx.x >> 8);  // wave-uniform
-  const int* L = kList ? rlist + ((int64_t)b * 2 + side) * lstride : nullptr;
-  const int nrows = kList ? rcount[b * 2 + side] : N;
-  if (kList && blockIdx.x * 256 * R >= nrows) return;  // block-uniform: no barrier skipped
   auto row_of = [&](int w) {  // the row of slot w, or N (none)
     const int k = blockIdx.x * 256 * R + w * 256 + r;
-    return k < nrows ? (kList ? L[k] : k) : N;
+    return k < N ? k : N;
   };
   float mx[R], my[R], mz[R], np_[R];
   cd_f2 mx2[R], my2[R], mz2[R], np2[R];
@@ -283,60 +275,6 @@ __global__ void chamfer_keys_kernel(const int32_t* __restrict__ argm, int R, uin
   for (int r = blockIdx.x * 256 + threadIdx.x; r < R; r += gridDim.x * 256) {
     keys[(int64_t)b * R + r] = (uint32_t)argm[(int64_t)b * R + r];
     vals[(int64_t)b * R + r] = (uint32_t)r;
-  }
-}
-
-// scattered term: destination d (a row of D-side cloud, D_pts [B,ND,3]) sums
-// sign * g/NR * 2(src_r - dst_d) over source rows r with argmin(r) == d.  A group of 16 lanes
-// serves one destination: lane j sums the contributions lo+j, lo+j+16, ... of d's sorted segment
-// in order, then the 16 partials are combined by a fixed xor tree, so the result is
-// deterministic and a destination with many sources (a point many rows collapse onto) costs
-// len/16 rounds instead of len.
-constexpr int kGatherLanes = 16;
-#ifndef PCST_X_CD_GATHER16
-#define PCST_X_CD_GATHER16 0
-#endif
-__global__ void chamfer_gather_kernel(const float* __restrict__ Dp, int ND,
-                                      const float* __restrict__ Sp, int NR,
-                                      const uint32_t* __restrict__ skeys,
-                                      const uint32_t* __restrict__ svals,
-                                      const float* __restrict__ gout, float sign,
-                                      float* __restrict__ grad) {
-  const int b = blockIdx.y;
-  const int t = blockIdx.x * 256 + threadIdx.x;
-  const int d = t / kGatherLanes, j = t % kGatherLanes;
-  const bool valid = d < ND;  // whole 16-lane groups share validity (256 % 16 == 0)
-  const uint32_t* K = skeys + (int64_t)b * NR;
-  int lo = 0, hi = valid ? NR : 0;  // lower bound of d
-  while (lo < hi) {
-    const int mid = (lo + hi) >> 1;
-    if (K[mid] < (uint32_t)d) lo = mid + 1; else hi = mid;
-  }
-  const float* q = Dp + ((int64_t)b * ND + (valid ? d : 0)) * 3;
-  const float g = gout[b] * 2.0f / (float)NR;
-  float a0 = 0.0f, a1 = 0.0f, a2 = 0.0f;
-  if (valid) {
-    for (int k = lo + j; k < NR && K[k] == (uint32_t)d; k += kGatherLanes) {
-      const int r = (int)svals[(int64_t)b * NR + k];
-      const float* p = Sp + ((int64_t)b * NR + r) * 3;
-      if (raw_pair(p, q) >= 0.0f) {
-        a0 += g * (p[0] - q[0]);
-        a1 += g * (p[1] - q[1]);
-        a2 += g * (p[2] - q[2]);
-      }
-    }
-  }
-#pragma unroll
-  for (int off = kGatherLanes / 2; off > 0; off >>= 1) {
-    a0 += __shfl_xor(a0, off);
-    a1 += __shfl_xor(a1, off);
-    a2 += __shfl_xor(a2, off);
-  }
-  if (valid && j == 0) {
-    float* o = grad + ((int64_t)b * ND + d) * 3;
-    o[0] += -sign * a0;
-    o[1] += -sign * a1;
-    o[2] += -sign * a2;
   }
 }
 
@@ -1042,9 +980,6 @@ __global__ __launch_bounds__(256) void cg_list_box_kernel(
     cg_wave_argmin<kCgSbBoxes / 2>(lmin, cmin);
     cmin = __builtin_amdgcn_readfirstlane(cmin);
     scan(cmin);
-#ifdef PCST_X_CG_BOX_STATS
-    int nscan = 1;
-#endif
     // the superboxes the bound keeps, eight at a time: lane group g takes the g-th kept one
     for (int s0 = 0; s0 < nsb; s0 += 64) {
       cg_wave_argmin(best, bi);
@@ -1061,18 +996,11 @@ __global__ __launch_bounds__(256) void cg_list_box_kernel(
         while (bmask) {
           const int bit = __builtin_ctzll(bmask);
           bmask &= bmask - 1;
-#ifdef PCST_X_CG_BOX_STATS
-          ++nscan;
-#endif
           scan(__builtin_amdgcn_readlane(c, bit));
         }
       }
     }
     cg_wave_argmin(best, bi);
-#ifdef PCST_X_CG_BOX_STATS  // experiment builds (tools/cd_box_probe.py): -1 and the scanned boxes
-    best = -1.0f;
-    bi = nscan;
-#endif
     if (lane == 0) {
       if (bi == 0x7fffffff) bi = 0;  // no comparable pair (NaN row)
       if (side == 0) {
@@ -1130,27 +1058,15 @@ static inline int64_t cd_padded(int64_t n) { return cdiv(n, kCdChunk) * kCdChunk
 // its nearest distance, which grows with the distance: a noisy predicted x0 against its target
 // (the trainer's early timesteps) measured 46-60 ms.  The hybrid mode (3, and the default 0)
 // bounds that: the grid search gives up after kCgRingBudget rings and the rows it gave up on (a
-// list per cloud and side) are served by box pruning (cg_list_box_kernel; PCST_X_CD_BOX=0: the
-// exhaustive row-min over the list, which bounds a direction by the exhaustive pass).  Measured on the trainer's pair (a predicted x0
+// list per cloud and side) are served by box pruning (cg_list_box_kernel; round 4 measured it
+// against the exhaustive row-min over the list).  Measured on the trainer's pair (a predicted x0
 // = lidar-like target + noise, 8 x 30000 per side, tools/cd_sweep.sh): noise 0.02: exhaustive
 // 2.08 ms, grid 0.32, hybrid 0.34; noise 0.2: 2.10 / 1.34 / 1.43; noise 1: 2.09 / 16.9 / 1.25;
 // noise 4: 2.10 / 62.5 / 1.28.  All modes give bit-identical minima and first-index argmins.
-#ifndef PCST_X_CG_LIST_BLOCKS  // blocks (4 waves) per cloud and side of cg_list_box_kernel
-#define PCST_X_CG_LIST_BLOCKS 512  // r04 a48: 512 9.61-9.65 ms per trainer step, 128 9.80-9.89
-#endif
-#ifndef PCST_X_CD_BOX  // the overflow rows by box pruning; 0: the exhaustive list row-min (A/B)
-#define PCST_X_CD_BOX 1
-#endif
-#ifndef PCST_X_CG_RING_BUDGET  // experiment builds may override
-#define PCST_X_CG_RING_BUDGET 2
-#endif
-constexpr int kCgRingBudget = PCST_X_CG_RING_BUDGET;
-// S x R shape of the overflow-list row-min launches (experiment builds may override; r04 a17:
-// 4 x 1 11.31-11.36 ms per trainer step vs 2 x 1 11.42-11.75, 2 x 2 11.72, 1 x 2 12.3-12.45)
-#ifndef PCST_X_CD_LIST_S
-#define PCST_X_CD_LIST_S 4
-#define PCST_X_CD_LIST_R 1
-#endif
+// blocks (4 waves) per cloud and side of cg_list_box_kernel (r04 a48: 512 9.61-9.65 ms per trainer
+// step, 128 9.80-9.89)
+constexpr int kCgListBlocks = 512;
+constexpr int kCgRingBudget = 2;  // rings the grid search tries before a row joins the list (r04 a47)
 static bool cd_use_grid(int mode) { return mode == 0 || mode == 2 || mode == 3; }
 static size_t cd_exh_bytes(int64_t B, int64_t N, int64_t M) {
   return (sizeof(float) * 4 * (size_t)B * (size_t)(cd_padded(N) + cd_padded(M)) + 255) / 256 * 256;
@@ -1187,10 +1103,7 @@ extern "C" int pcst_chamfer_fwd(const float* pred, const float* target, int64_t 
     CgWS w = carve_cg(static_cast<char*>(workspace) + cd_exh_bytes(B, N, M), B, N, M);
     const int64_t NM = std::max(N, M);
     PCST_HIP(hipMemsetAsync(w.counts, 0, sizeof(int) * B * 2 * (kCgMaxCells + 1), s), "memset");
-    if (hybrid) {
-      PCST_HIP(hipMemsetAsync(w.ovf_count, 0, sizeof(int) * B * 2, s), "memset");
-      if (!PCST_X_CD_BOX) pack();
-    }
+    if (hybrid) PCST_HIP(hipMemsetAsync(w.ovf_count, 0, sizeof(int) * B * 2, s), "memset");
     hipLaunchKernelGGL(cg_stats_kernel, dim3(b, 2), dim3(1024), 0, s, pred, target, (int)N, (int)M,
                        w.grids);
     const dim3 pg((unsigned)cdiv(NM, 256), b, 2);
@@ -1204,22 +1117,14 @@ extern "C" int pcst_chamfer_fwd(const float* pred, const float* target, int64_t 
     hipLaunchKernelGGL(cg_rowmin_kernel, pg, dim3(256), 0, s, (int)N, (int)M, w.grids, w.starts,
                        w.sorted, w.sidx, min1, arg1, min2, arg2, hybrid ? kCgRingBudget : 0,
                        w.ovf_count, w.ovf_rows);
-    if (hybrid && PCST_X_CD_BOX) {  // the rows over budget: box-pruned scans
+    if (hybrid) {  // the rows over budget: box-pruned scans
       const int nbs = (int)cdiv(NM, kCgBoxPts);
       hipLaunchKernelGGL(cg_box_kernel, dim3((unsigned)cdiv(nbs, kCgSbBoxes), b, 2), dim3(512), 0, s,
                          (int)N, (int)M, w.sorted, w.boxes, w.sboxes);
-      const unsigned lb = (unsigned)std::min<int64_t>(cdiv(NM, 64), PCST_X_CG_LIST_BLOCKS);
+      const unsigned lb = (unsigned)std::min<int64_t>(cdiv(NM, 64), kCgListBlocks);
       hipLaunchKernelGGL(cg_list_box_kernel, dim3(lb, b, 2), dim3(256), 0, s, pred, target, (int)N,
                          (int)M, w.grids, w.sorted, w.sidx, w.boxes, w.sboxes, w.ovf_count, w.ovf_rows, min1,
                          arg1, min2, arg2);
-    } else if (hybrid) {  // the rows over budget, exhaustively (grid over the list's upper bound)
-      constexpr int LS = PCST_X_CD_LIST_S, LR = PCST_X_CD_LIST_R;
-      hipLaunchKernelGGL((chamfer_rowmin_kernel<LS, LR, true>), dim3((unsigned)cdiv(N, 256 * LR), b),
-                         dim3(256 * LS), 0, s, pred, Tp, (int)N, (int)M, (int)Mp, min1, arg1,
-                         w.ovf_rows, w.ovf_count, 0, NM);
-      hipLaunchKernelGGL((chamfer_rowmin_kernel<LS, LR, true>), dim3((unsigned)cdiv(M, 256 * LR), b),
-                         dim3(256 * LS), 0, s, target, Pp, (int)M, (int)N, (int)Np, min2, arg2,
-                         w.ovf_rows, w.ovf_count, 1, NM);
     }
     if (out)
       hipLaunchKernelGGL(chamfer_mean_kernel, dim3(b), dim3(1024), 0, s, min1, (int)N, min2, (int)M,
@@ -1228,27 +1133,11 @@ extern "C" int pcst_chamfer_fwd(const float* pred, const float* target, int64_t 
     return PCST_OK;
   }
   pack();
-  // S x R shape of the row-min launch (experiment builds: XDEF=-DPCST_X_CD_VARIANT=11|41|12|22|14|42)
-#ifndef PCST_X_CD_VARIANT
-#define PCST_X_CD_VARIANT 21
-#endif
-  constexpr int variant = PCST_X_CD_VARIANT;
+  // 2 segments x 1 row per thread (the S x R sweep of round 3: 11 / 41 / 12 / 22 / 14 / 42 slower)
   auto rowmin = [&](const float* P, const float4* Qp, int64_t n, int64_t m, int64_t mp, float* md,
                     int32_t* am) {
-#define PCST_CD_LAUNCH(S_, R_)                                                                  \
-  hipLaunchKernelGGL((chamfer_rowmin_kernel<S_, R_>), dim3((unsigned)cdiv(n, 256 * R_), b),    \
-                     dim3(256 * S_), 0, s, P, Qp, (int)n, (int)m, (int)mp, md, am, nullptr,     \
-                     nullptr, 0, 0)
-    switch (variant) {
-      case 11: PCST_CD_LAUNCH(1, 1); break;
-      case 41: PCST_CD_LAUNCH(4, 1); break;
-      case 12: PCST_CD_LAUNCH(1, 2); break;
-      case 22: PCST_CD_LAUNCH(2, 2); break;
-      case 14: PCST_CD_LAUNCH(1, 4); break;
-      case 42: PCST_CD_LAUNCH(4, 2); break;
-      default: PCST_CD_LAUNCH(2, 1); break;
-    }
-#undef PCST_CD_LAUNCH
+    hipLaunchKernelGGL((chamfer_rowmin_kernel<2, 1>), dim3((unsigned)cdiv(n, 256), b), dim3(512), 0, s,
+                       P, Qp, (int)n, (int)m, (int)mp, md, am);
   };
   rowmin(pred, Tp, N, M, Mp, min1, arg1);
   rowmin(target, Pp, M, N, Np, min2, arg2);
@@ -1275,13 +1164,7 @@ extern "C" int pcst_chamfer_bwd(const float* pred, const float* target, int64_t 
   CdWS w = carve_cd(workspace, B, std::max(N, M));
   const unsigned b = (unsigned)B;
   // the scatter onto the argmin side from the sorted (destination, row) pairs: segmented sums
-  // (PCST_X_CD_GATHER16 = 1: the 16-lane gather per destination, A/B)
   auto seg_gather = [&](const float* D, int ND, const float* S, int NR, const float* go, float* gr) {
-    if (PCST_X_CD_GATHER16) {
-      hipLaunchKernelGGL(chamfer_gather_kernel, dim3((unsigned)cdiv((int64_t)ND * kGatherLanes, 256), b),
-                         dim3(256), 0, s, D, ND, S, NR, w.kA, w.vA, go, 1.0f, gr);
-      return;
-    }
     const int nblk = (int)cdiv(NR, kSegE);
     hipLaunchKernelGGL(chamfer_segsum_kernel, dim3((unsigned)nblk, b), dim3(256), 0, s, D, ND, S, NR,
                        w.kA, w.vA, go, 1.0f, gr, nblk, w.part, w.pflag);

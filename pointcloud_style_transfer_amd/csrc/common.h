@@ -44,6 +44,10 @@ inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s);
 inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
 // Workspace carving: 256-byte aligned sub-buffers of one caller-owned allocation.
+// Default poll bound of the device-side cross-stream waits (pcst_signal_wait and the kernels that
+// wait for a flag themselves): ~10 s.
+constexpr int kSignalPolls = 1 << 26;
+
 struct Carver {
   char* base;
   size_t off = 0;

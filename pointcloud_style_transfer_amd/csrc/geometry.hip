@@ -812,12 +812,6 @@ static void launch_fps_cull(const float* xyz, int B, int N, int npoint, const in
                      out);
 }
 
-// experiment builds: XDEF=-DPCST_X_FPS_CULL=0 runs fps_key_kernel for every size (A/B)
-#ifndef PCST_X_FPS_CULL
-#define PCST_X_FPS_CULL 1
-#endif
-static constexpr bool fps_cull_enabled() { return PCST_X_FPS_CULL != 0; }
-
 extern "C" int pcst_fps_workspace_size(int64_t B, int64_t N, size_t* bytes) {
   *bytes = (N > (int64_t)kFpsThreads * 60) ? (size_t)(B * N) * sizeof(float) : 0;
   return PCST_OK;
@@ -832,7 +826,7 @@ extern "C" int pcst_fps_ws(const float* xyz, int64_t B, int64_t N, int64_t npoin
   hipStream_t s = as_stream(stream);
   const int b = (int)B, n = (int)N, np = (int)npoint;
   const int64_t ppt2 = cdiv(N, kFps2Threads);
-  if (ppt2 > 8 && ppt2 <= 30 && fps_cull_enabled()) {
+  if (ppt2 > 8 && ppt2 <= 30) {
     if (ppt2 <= 16) launch_fps_cull<16>(xyz, b, n, np, start_idx, out_idx, s);
     else if (ppt2 <= 24) launch_fps_cull<24>(xyz, b, n, np, start_idx, out_idx, s);
     else launch_fps_cull<30>(xyz, b, n, np, start_idx, out_idx, s);

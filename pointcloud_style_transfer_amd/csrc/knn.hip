@@ -27,7 +27,8 @@
 // best are ranked in exact float64.  Pass 2 runs under a staging budget (a wave's time is
 // bounded); lanes still open after it (sparse neighbourhoods: in the bench trajectory ~0.05 %
 // of the queries, which a wave-wide staging pass would serve at the cost of the kernel's tail)
-// go to the outlier list: one workgroup per outlier query scans every ref (knn_outlier_kernel).
+// go to the outlier list: one wave per outlier query searches shells of bricks around it
+// (knn_outlier_brick_kernel).
 //
 // Launches: memset, pre (cloud stats + known rows), count (grid params, per-cell counts with
 // each element's rank in its cell, per-tile sums, known-row copies), scan (single pass: tile
@@ -38,41 +39,24 @@
 
 namespace pcst {
 
-#ifndef KNN_REFS_PER_CELL  // experiment builds may override
-#define KNN_REFS_PER_CELL 6.0
-#endif
-constexpr double kRefsPerCell = KNN_REFS_PER_CELL;  // refs per cell at the cloud's peak density
+constexpr double kRefsPerCell = 6.0;     // refs per cell at the cloud's peak density
 constexpr int kCandCap = 512;            // LDS candidates per wave
-#ifndef KNN_BALL_CELLS  // experiment builds may override
-#define KNN_BALL_CELLS 512
-#define KNN_BALL_UNION 1024
-#define KNN_BALL_BUDGET 2048
-#endif
-constexpr int kBallCells = KNN_BALL_CELLS;         // largest cell box one lane's ball may ask for
-constexpr int kBallUnion = KNN_BALL_UNION;         // largest union box of a ball pass
-constexpr uint32_t kBallBudget = KNN_BALL_BUDGET;  // refs the ball pass may stage
+constexpr int kBallCells = 512;          // largest cell box one lane's ball may ask for
+constexpr int kBallUnion = 1024;         // largest union box of a ball pass
+constexpr uint32_t kBallBudget = 2048;   // refs the ball pass may stage
 constexpr int kKnnTile = 4096;           // scan tile (256 threads x 16)
 constexpr int kKnnMaxTiles = 1024;       // per-block LDS tile histogram in the count kernel
 constexpr int kPreKnownBlocks = 64;      // known-row scatter blocks per cloud in the pre kernel
 constexpr int kCountPerBlock = 1024;     // elements per count-kernel block (4 per thread)
-#ifndef PCST_KNN_SLOTKEY  // 1: the one-pass slot-keyed query window (Query::window); 0: two-pass
-#define PCST_KNN_SLOTKEY 1
-#endif
 constexpr int kQueryBlocks = 1024;       // query workgroups per cloud (grid-stride over chunks)
 // the query grid's cap over all clouds of one launch, when the caller passes grid_cap <= 0: at
 // 32 clouds (64 CFG rows) 16384 workgroups let each wave stride over several chunks (r04 A/B,
 // profiles/r04/a5: b32 8.79 -> 8.67 ms); at one cloud the per-cloud cap (kQueryBlocks) binds first
 constexpr int64_t kQueryGridCapDefault = 16384;
 constexpr int kQueryBlocksMin = 16;
-constexpr int kOutlierThreads = 1024;    // outlier-pass workgroup
-constexpr int kOutlierBlocks = 128;      // outlier workgroups per cloud (exhaustive pass)
+constexpr int kOvlLds = 256;             // overflow refs staged in LDS per query work-group
 constexpr int kOutlierBrickBlocks = 256; // outlier workgroups per cloud (brick search, 4 queries)
 
-#ifdef KNN_TRACE  // experiment builds only: per-chunk pass timings (tools/knn_trace.py)
-__device__ unsigned long long g_knn_trace[2 * 32768 * 8];
-// per outlier query of the brick search: realtime start/end, shells, refs staged, bricks
-__device__ unsigned long long g_knn_otrace[2 * 4096 * 4];
-#endif
 
 // A query row's IDW weights and ref indices (kk of them used), written by the deferred search
 // and applied to the coarse values by the finish pass (pcst_knn3_search / pcst_knn3_finish).
@@ -203,13 +187,29 @@ __device__ void knn_grid_params(const StatRec* __restrict__ stats, int b, int64_
   G[5] = __int_as_float(d[0]); G[6] = __int_as_float(d[1]); G[7] = __int_as_float(d[2]);
 }
 
-// blocks [0, kStatBlocks): cloud statistics; the rest: known[n] = max j+1 with idx[j] == n
+// blocks [0, kStatBlocks): cloud statistics; the rest: known[n] = max j+1 with idx[j] == n.
+// zero (rows layout, M = 0): blocks [kStatBlocks, grid) zero zero_words 16-byte words instead of
+// a memset launch (the per-build state; the kernels that read it are later launches).
+constexpr int kPreZeroBlocks = 128;
 __global__ __launch_bounds__(256) void knn_pre_kernel(const float* __restrict__ orig,
                                                       const int64_t* __restrict__ idx, int N,
                                                       int64_t M, StatRec* __restrict__ stats,
                                                       uint32_t* __restrict__ known,
-                                                      int32_t* __restrict__ err) {
+                                                      int32_t* __restrict__ err,
+                                                      uint4* __restrict__ zero = nullptr,
+                                                      int64_t zero_words = 0) {
   const int b = blockIdx.y;
+  if (zero) {
+    if ((int)blockIdx.x >= kStatBlocks) {
+      const int64_t stride = (int64_t)kPreZeroBlocks * gridDim.y * 256;
+      for (int64_t i = ((int64_t)b * kPreZeroBlocks + (blockIdx.x - kStatBlocks)) * 256 + threadIdx.x;
+           i < zero_words; i += stride)
+        zero[i] = make_uint4(0u, 0u, 0u, 0u);
+      return;
+    }
+    cloud_stats_block(orig + (int64_t)b * N * 3, N, blockIdx.x, stats + b * kStatBlocks);
+    return;
+  }
   // any grid size (a capped side-stream build has few workgroups): the stats partials and the
   // known rows are strided over the workgroups
   for (int sb = blockIdx.x; sb < kStatBlocks; sb += gridDim.x) {
@@ -224,13 +224,13 @@ __global__ __launch_bounds__(256) void knn_pre_kernel(const float* __restrict__ 
 }
 
 // Per element e of [refs j < M | rows n = e - M]: its cell and its rank in the cell (the old
-// value of the cell's packed counter), per-tile sums via an LDS histogram; known rows copy
-// their coarse value to the output here.  Each thread handles 4 elements with their atomics
-// in flight together.
+// value of the cell's packed counter), per-tile sums via an LDS histogram.  Known rows are not
+// counted (known == nullptr: every row is, the rows layout's phase A with M = 0).  The grid is
+// sized for Mgrid refs.  Each thread handles 4 elements with their atomics in flight together.
 __global__ __launch_bounds__(256) void knn_count_kernel(
     const float* __restrict__ orig, const int64_t* __restrict__ idx,
     const StatRec* __restrict__ stats, const uint32_t* __restrict__ known, int64_t N, int64_t M,
-    int64_t Cmax, int64_t T, int64_t Cpad, float* __restrict__ gp, uint64_t* __restrict__ cnt,
+    int64_t Mgrid, int64_t Cmax, int64_t T, int64_t Cpad, float* __restrict__ gp, uint64_t* __restrict__ cnt,
     uint64_t* __restrict__ tsum, int2* __restrict__ crank) {
   constexpr int U = kCountPerBlock / 256;
   const int b = blockIdx.y;
@@ -260,7 +260,7 @@ __global__ __launch_bounds__(256) void knn_count_kernel(
         inc[u] = 1ull;
       } else if (e < M + N) {
         const int64_t n = e - M;
-        const uint32_t kn = known[b * N + n];
+        const uint32_t kn = known ? known[b * N + n] : 0u;  // (rows layout: every row)
         if (!kn) {  // known rows take the coarse value in the outlier pass (after the MLP)
           const float* p = orig + (b * N + n) * 3;
           px[u] = p[0]; py[u] = p[1]; pz[u] = p[2];
@@ -271,7 +271,7 @@ __global__ __launch_bounds__(256) void knn_count_kernel(
     }
   };
   load(blockIdx.x);
-  if (threadIdx.x < 64) knn_grid_params(stats, b, N, M, Cmax, Gs);
+  if (threadIdx.x < 64) knn_grid_params(stats, b, N, Mgrid, Cmax, Gs);
   for (int t = threadIdx.x; t < T; t += 256) th[t] = 0ull;
   __syncthreads();
   if (blockIdx.x == 0 && threadIdx.x < 8) gp[b * 8 + threadIdx.x] = Gs[threadIdx.x];
@@ -439,6 +439,188 @@ __global__ __launch_bounds__(256) void knn_fill_kernel(const float* __restrict__
   }
 }
 
+// ---- Rows layout (the sampling loop's step: pcst_knn3_rows_build / _refs / _query) ----
+// Phase A needs the clouds' positions only, so the loop runs it beside the voxel downsample
+// (before the coarse indices exist): every row of cloud cl is binned (statistics, grid, per-cell
+// row counts with each row's rank, the scan -- row starts and the chunk list over ALL rows --
+// and the fill: rows in cell order), shared by the `copies` CFG rows b = c * C + cl of the cloud.
+// Phase B (after the downsample), three short launches: (1) ref j of row b marks its point n
+// known (atomicMax: the last j wins, as the reference's index assignment) and takes a rank in
+// n's cell (atomicAdd); (2) one wave per brick turns its 64 cells' counts into slot offsets: the
+// brick's refs are one contiguous run at the front of the brick's row range, cell after cell
+// (the compact layout's order inside a brick); (3) each ref is stored at its slot.  Distinct refs
+// always fit (a cell has one row per distinct ref); refs repeating an index (the downsample's
+// representatives may share one: ~200 of 30000 per row in the bench) fit while their cell has
+// rows to spare, and the rest go to the row's overflow list, which the query offers wherever its
+// scanned box holds them.  The query skips known rows (copying their coarse value instead).  The
+// grid is the compact layout's (the same statistics and ref count), so both layouts give the
+// same bits.
+struct KnnRowsWS {
+  StatRec* stats;    // [C][kStatBlocks]
+  float* gp;         // [C][8]
+  int32_t* qorder;   // [C][N] rows in cell order
+  int2* crank;       // [C][N] (cell, rank in cell)
+  uint2* chunks;     // [C][maxch] row ranges [q0, q1) of <= 64 rows inside one brick
+  float4* refs;      // [B][N] refs (x, y, z, j), per brick at the front of its row range
+  float4* over;      // [B][M] overflow refs (an index named again)
+  uint32_t* rrank;   // [B][M] ref j's rank in its cell (~0u: overflow or a bad index)
+  uint64_t* cw;      // [B][Cpad] a cell's refs: first slot | count << 32
+  int32_t* olist;    // [B][N] outlier query rows
+  float* obound;     // [B][N]
+  // zeroed every build (contiguous):
+  int32_t* err;
+  int32_t* nchunk;   // [C]
+  int32_t* ocount;   // [B]
+  int32_t* ovn;      // [B] overflow refs
+  uint32_t* known;   // [B][N] j+1 of the last ref naming n, 0 = a query row
+  uint32_t* rcnt;    // [B][Cpad] refs ranked per cell
+  uint64_t* tsum;    // [C][T]
+  uint64_t* cnt;     // [C][Cpad] packed counts (0 | rows << 32) -> starts
+  int64_t B, C, Cmax, T, Cpad, maxch;
+  size_t bytes;
+};
+
+static KnnRowsWS carve_knn_rows(void* base, int64_t C, int64_t copies, int64_t N, int64_t M) {
+  Carver c(base);
+  KnnRowsWS w;
+  w.C = C;
+  w.B = C * copies;
+  w.Cmax = knn_cells(M);
+  w.T = cdiv(w.Cmax + 1, kKnnTile);
+  w.Cpad = w.T * kKnnTile;
+  w.maxch = cdiv(N, 64) + 8 * (w.Cmax / 64) + 1;
+  w.stats = c.take<StatRec>(C * kStatBlocks);
+  w.gp = c.take<float>(C * 8);
+  w.qorder = c.take<int32_t>(C * N);
+  w.crank = c.take<int2>(C * N);
+  w.chunks = c.take<uint2>(C * w.maxch);
+  w.refs = c.take<float4>(w.B * N);
+  w.over = c.take<float4>(w.B * M);
+  w.rrank = c.take<uint32_t>(w.B * M);
+  w.cw = c.take<uint64_t>(w.B * w.Cpad);
+  w.olist = c.take<int32_t>(w.B * N);
+  w.obound = c.take<float>(w.B * N);
+  w.err = c.take<int32_t>(4);
+  w.nchunk = c.take<int32_t>(C);
+  w.ocount = c.take<int32_t>(w.B);
+  w.ovn = c.take<int32_t>(w.B);
+  w.known = c.take<uint32_t>(w.B * N);
+  w.rcnt = c.take<uint32_t>(w.B * w.Cpad);
+  w.tsum = c.take<uint64_t>(C * w.T);
+  w.cnt = c.take<uint64_t>(C * w.Cpad);
+  w.bytes = c.bytes();
+  return w;
+}
+
+// A flag for work on another stream: every launch ahead of this one on its stream has completed.
+__global__ void knn_flag_kernel(uint32_t* flag, uint32_t value) {
+  if (threadIdx.x == 0) __hip_atomic_store(flag, value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// The consumer side of a flag hand-off inside a kernel (MI355X_MICROARCH.md, inter-workgroup
+// visibility): thread 0 polls (relaxed, agent scope) until the flag holds `value`, at most
+// max_polls times, then one agent-scope acquire; the block barrier lets every wave load after it.
+// A wait that gives up sets *werr and returns false for the whole block.
+__device__ bool block_wait_flag(const uint32_t* flag, uint32_t value, int32_t* werr, int64_t max_polls) {
+  __shared__ int s_ok;
+  if (threadIdx.x == 0) {
+    bool ok = false;
+    for (int64_t i = 0; i < max_polls; ++i) {
+      if (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= value) {
+        ok = true;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(4);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (!ok && werr) __hip_atomic_store(werr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_ok = ok;
+  }
+  __syncthreads();
+  return s_ok != 0;
+}
+
+// Phase B (1): ref j of CFG row b (cloud b % C): its known mark and its rank in its cell (both
+// atomics issued together); a rank beyond the cell's rows sends the ref to the overflow list.
+// wflag (optional): the side stream's phase-A flag; every work-group waits until it holds wvalue
+// (the consumer side of the guide's hand-off: one relaxed poll loop, one agent-scope acquire, a
+// barrier), so no wait launch sits in front of this one; a wait that gives up sets werr and the
+// work-group leaves the workspace alone (the query's flag test then yields eps = 0 and the
+// caller raises).
+__global__ __launch_bounds__(256) void knn_rows_rank_kernel(
+    const float* __restrict__ x, const int64_t* __restrict__ idx, int64_t C, int64_t N, int64_t M,
+    int64_t Cpad, const uint64_t* __restrict__ start, const int2* __restrict__ crank,
+    uint32_t* __restrict__ known, uint32_t* __restrict__ rcnt, uint32_t* __restrict__ rrank,
+    float4* __restrict__ over, int32_t* __restrict__ ovn, int32_t* __restrict__ err,
+    const uint32_t* __restrict__ wflag, uint32_t wvalue, int32_t* __restrict__ werr,
+    int64_t max_polls) {
+  if (wflag && !block_wait_flag(wflag, wvalue, werr, max_polls)) return;
+  const int b = blockIdx.y;
+  const int64_t cl = b % C;
+  for (int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x; j < M; j += (int64_t)gridDim.x * 256) {
+    const int64_t n = idx[b * M + j];
+    if (n < 0 || n >= N) {
+      atomicOr(err, 1);
+      rrank[b * M + j] = ~0u;
+      continue;
+    }
+    const int cell = crank[cl * N + n].x;
+    const uint32_t rows = (uint32_t)(start[cl * Cpad + cell + 1] >> 32) -
+                          (uint32_t)(start[cl * Cpad + cell] >> 32);
+    atomicMax(&known[b * N + n], (uint32_t)(j + 1));
+    const uint32_t rank = atomicAdd(&rcnt[b * Cpad + cell], 1u);
+    rrank[b * M + j] = rank < rows ? rank : ~0u;
+    if (rank >= rows) {
+      const float* p = x + (cl * N + n) * 3;
+      over[b * M + atomicAdd(&ovn[b], 1)] = make_float4(p[0], p[1], p[2], __int_as_float((int)j));
+    }
+  }
+}
+
+// Phase B (2): one wave per brick: cell c's refs take slots [cw, cw + count) with count =
+// min(ranked refs, rows of c) and the cells of the brick back to back from the brick's first row.
+__global__ __launch_bounds__(256) void knn_rows_cellscan_kernel(int64_t C, int64_t Cpad,
+                                                                const uint64_t* __restrict__ start,
+                                                                const uint32_t* __restrict__ rcnt,
+                                                                uint64_t* __restrict__ cw) {
+  const int b = blockIdx.y;
+  const int64_t cl = b % C;
+  const int lane = threadIdx.x & 63;
+  const int64_t brick = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (brick * 64 >= Cpad) return;
+  const int64_t c = brick * 64 + lane;
+  const uint64_t* S = start + cl * Cpad;
+  const uint32_t a = (uint32_t)(S[c] >> 32);
+  const uint32_t rows = (c + 1 < Cpad ? (uint32_t)(S[c + 1] >> 32) : a) - a;
+  const uint32_t v = min(rcnt[b * Cpad + c], rows);
+  uint32_t inc = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(inc, o);
+    if (lane >= o) inc += y;
+  }
+  const uint32_t base = (uint32_t)(S[brick * 64] >> 32);
+  cw[b * Cpad + c] = (uint64_t)(base + inc - v) | ((uint64_t)v << 32);
+}
+
+// Phase B (3): every ranked ref to its slot.
+__global__ __launch_bounds__(256) void knn_rows_place_kernel(
+    const float* __restrict__ x, const int64_t* __restrict__ idx, int64_t C, int64_t N, int64_t M,
+    int64_t Cpad, const int2* __restrict__ crank, const uint32_t* __restrict__ rrank,
+    const uint64_t* __restrict__ cw, float4* __restrict__ refs) {
+  const int b = blockIdx.y;
+  const int64_t cl = b % C;
+  for (int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x; j < M; j += (int64_t)gridDim.x * 256) {
+    const uint32_t rank = rrank[b * M + j];
+    if (rank == ~0u) continue;
+    const int64_t n = idx[b * M + j];
+    const float* p = x + (cl * N + n) * 3;
+    const int cell = crank[cl * N + n].x;
+    refs[b * N + (uint32_t)cw[b * Cpad + cell] + rank] = make_float4(p[0], p[1], p[2], __int_as_float((int)j));
+  }
+}
+
 struct Top3 {
   // named fields, not arrays: a runtime index would put an array in scratch
   double d0, d1, d2;
@@ -555,27 +737,22 @@ __device__ __forceinline__ float dist1(const Win& W, int i, float ax, float ay, 
 
 // One query: an fp32 screen and the exact (float64) top-3.
 //   consider(): one candidate at a time: screen against the exact 3rd best.
-//   window():   a staged window of candidates in two phases.  Phase 1 keeps the fp32 three
-//               smallest distances branch-free (min / med3 / med3); phase 2 screens the window
-//               against that fp32 3rd best into a register mask per 64 refs; the survivors
-//               (~3 per lane) are then ranked in float64 by each lane alone.  The window is
-//               four coordinate arrays so both phases use packed fp32 math.  Every member of
-//               the exact top-3 survives
-//               its window's screen: its fp32 distance is within (1 + 3e-7)^2 of its float64
-//               one, and the fp32 3rd best bounds the float64 3rd best the same way (a ref must
-//               never reach phase 1 twice: a repeat would shrink the fp32 3rd best).
+//   window():   a staged window of candidates in one pass of slot-keyed fp32 distances (below),
+//               then float64 ranks of the few candidates that can be in the top 3.  The window
+//               is four coordinate arrays so the pass uses packed fp32 math.  Every member of the
+//               exact top-3 survives its window's screen: its fp32 distance is within
+//               (1 + 3e-7)^2 of its float64 one, and the fp32 kk-th best bounds the float64 one
+//               the same way (a ref must never reach the window twice: a repeat would shrink it).
 struct Query {
   float fx, fy, fz;
   double qx, qy, qz;
   Top3 t;
   float thr;            // exact-path screen (from the float64 3rd best)
-  float c0, c1, c2;     // fp32 three smallest distances seen (window path)
   __device__ void init(float x, float y, float z) {
     fx = x; fy = y; fz = z;
     qx = x; qy = y; qz = z;
     t.init();
     thr = INFINITY;
-    c0 = c1 = c2 = INFINITY;
   }
   __device__ __forceinline__ void exact(float4 ref) {
     const double ux = dsub(qx, (double)ref.x), uy = dsub(qy, (double)ref.y),
@@ -587,13 +764,6 @@ struct Query {
     exact(ref);
     if (t.last(kk) != INFINITY) thr = (float)(t.last(kk) * (1.0 + 2e-6)) + 1e-30f;
   }
-  __device__ __forceinline__ void top3_fp32(float d) {
-    const float n0 = fminf(c0, d);
-    const float n1 = __builtin_amdgcn_fmed3f(c0, c1, d);
-    const float n2 = __builtin_amdgcn_fmed3f(c1, c2, d);
-    c0 = n0; c1 = n1; c2 = n2;
-  }
-#if PCST_KNN_SLOTKEY
   // Slot-keyed window (one pass over the staged refs): each fp32 distance with its low 9
   // mantissa bits replaced by the ref's window slot (< kCandCap = 512) is a key whose order is
   // the distances' order up to 2^-14 relative; the four smallest keys are kept branch-free
@@ -667,44 +837,6 @@ struct Query {
       }
     }
   }
-#else
-  __device__ __forceinline__ void window(const Win& W, int fill, int kk) {
-    const float ax = fx, ay = fy, az = fz;  // by value: keeps the query out of private memory
-    const f2 qx = {ax, ax}, qy = {ay, ay}, qz = {az, az};
-    int i = 0;
-    for (; i + 4 <= fill; i += 4) {
-      f2 d01, d23;
-      dist4(W, i, qx, qy, qz, d01, d23);
-      top3_fp32(d01.x);
-      top3_fp32(d01.y);
-      top3_fp32(d23.x);
-      top3_fp32(d23.y);
-    }
-    for (; i < fill; ++i) top3_fp32(dist1(W, i, ax, ay, az));
-    const float ck = kk >= 3 ? c2 : (kk == 2 ? c1 : c0);
-    const float sc = fminf(ck * 1.000002f + 1e-30f, thr);
-    // phase 2 per block of 64 staged refs: a register mask of the screened-in refs (no LDS
-    // writes, so the reads pipeline), then each lane ranks its own survivors exactly
-    for (int b0 = 0; b0 < fill; b0 += 64) {
-      const int nb = min(64, fill - b0);
-      uint64_t m = 0;
-      int u = 0;
-      for (; u + 4 <= nb; u += 4) {
-        f2 d01, d23;
-        dist4(W, b0 + u, qx, qy, qz, d01, d23);
-        m |= ((uint64_t)(d01.x <= sc) | ((uint64_t)(d01.y <= sc) << 1) |
-              ((uint64_t)(d23.x <= sc) << 2) | ((uint64_t)(d23.y <= sc) << 3)) << u;
-      }
-      for (; u < nb; ++u) m |= (uint64_t)(dist1(W, b0 + u, ax, ay, az) <= sc) << u;
-      while (m) {
-        const int k = b0 + __builtin_ctzll(m);
-        m &= m - 1;
-        exact(make_float4(W.x[k], W.y[k], W.z[k], __int_as_float(W.j[k])));
-      }
-    }
-    if (t.last(kk) != INFINITY) thr = fminf(thr, (float)(t.last(kk) * (1.0 + 2e-6)) + 1e-30f);
-  }
-#endif
 };
 
 // LDS reads/writes of this wave done (before the window is overwritten or read)
@@ -835,31 +967,28 @@ __device__ __forceinline__ void scan_units_1q(int vol, const Unit& unit, const f
         if (ok[k]) r[k] = R[src];
       }
 #pragma unroll
-      for (int k = 0; k < 4; ++k)
-        if (ok[k]) me.consider(r[k], kk);
+      for (int k = 0; k < 4; ++k)  // (j < 0: an empty slot of the rows layout's brick range)
+        if (ok[k] && __float_as_int(r[k].w) >= 0) me.consider(r[k], kk);
     }
   }
 }
 
-__device__ __forceinline__ bool scan_box(const Box& bx, const Box& prev, const Grid& g,
-                                         const uint64_t* __restrict__ S,
+// rng(u0, lo, hi): the ref range [lo, hi) of cell u0 (in the low 32 bits of each word)
+template <class Rng>
+__device__ __forceinline__ bool scan_box(const Box& bx, const Box& prev, const Grid& g, const Rng& rng,
                                          const float4* __restrict__ R, const Win& W, Query& me,
                                          int kk, uint32_t& budget) {
   const int nx = bx.x1 - bx.x0 + 1, ny = bx.y1 - bx.y0 + 1;
   const int vol = bx.volume();
   const float rnx = 1.0f / nx, rnxy = 1.0f / (nx * ny);  // exact quotients for li < 2^20
-  // packed start words of cell li and of its successor (empty if outside bx or inside prev)
+  // ref range of cell li (empty if outside bx or inside prev)
   auto unit = [&](int li, uint64_t& lo, uint64_t& hi) {
     lo = hi = 0;
     if (li < vol) {
       const int qz = (int)(((float)li + 0.5f) * rnxy), rz = li - qz * nx * ny;
       const int qy = (int)(((float)rz + 0.5f) * rnx), qx = rz - qy * nx;
       const int x = bx.x0 + qx, y = bx.y0 + qy, z = bx.z0 + qz;
-      if (!prev.has(x, y, z)) {
-        const int u0 = cell_id(x, y, z, g);
-        lo = S[u0];
-        hi = S[u0 + 1];
-      }
+      if (!prev.has(x, y, z)) rng(cell_id(x, y, z, g), lo, hi);
     }
   };
   return scan_units(vol, unit, R, W, me, kk, budget);
@@ -906,7 +1035,24 @@ __device__ __forceinline__ bool build_pending(const uint32_t* flag, uint32_t val
 // (driver window 2379-2398 -> 2400-2429 steps/s, A/B on one box).
 // DEFER: the deferred search (positions only): the rows' IDW weights into nbr instead of the IDW
 // of vals into out.
-template <int kk, bool DEFER>  // kk = min(M, 3), a compile-time constant so the top-3 stays in registers
+// The layout-specific arrays of the query and outlier launches.  Compact layout (pcst_knn3_build):
+// per CFG row b, refs cell-sorted in [0, M), the packed start words give a cell's ref range.
+// Rows layout (pcst_knn3_rows_*): the cloud cl = b % C holds the grid, the rows in cell order and
+// the chunks; row b's refs sit at the front of their cell's row range (count rcnt[b][cell]), the
+// known rows are skipped by the query (their value is the coarse one, copied there) and the
+// overflow refs (repeated indices) are offered to every query.
+struct KArgs {
+  int64_t C;                  // clouds holding the grid / rows / chunks (compact: B)
+  const uint32_t* known;      // [B][N] (rows layout)
+  const uint64_t* cw;         // [B][Cpad] a cell's refs: first slot | count << 32 (rows layout)
+  const float4* over;         // [B][M] overflow refs (rows layout)
+  const int32_t* ovn;         // [B] their counts (rows layout)
+  int32_t* err;               // bit 4: a chunk outside [0, N], bit 8: a ref range outside the refs
+  int32_t* werr;              // rows layout: the query waits for bflag itself (its timeout word)
+  int64_t max_polls;
+};
+
+template <int kk, bool DEFER, bool ROWS>  // kk = min(M, 3), a compile-time constant so the top-3 stays in registers
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) void knn_query_kernel(
     const float* __restrict__ orig, const float* __restrict__ vals, int64_t N, int64_t M,
     int64_t Cpad, const float* __restrict__ gp, const uint64_t* __restrict__ start,
@@ -914,10 +1060,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
     const uint2* __restrict__ chunks, int64_t maxch, const int32_t* __restrict__ nchunk,
     int32_t* __restrict__ olist, float* __restrict__ obound, int32_t* __restrict__ ocount,
     float* __restrict__ out, NbrRec* __restrict__ nbr, const uint32_t* __restrict__ bflag,
-    uint32_t bvalue) {
+    uint32_t bvalue, const KArgs ka) {
   __shared__ __attribute__((aligned(16))) float cand[4][4][kCandCap];
   const int b = blockIdx.y;
-  if (build_pending(bflag, bvalue)) {
+  const int64_t cl = ROWS ? b % ka.C : b;
+  // compact layout: the stream waited for the build before this launch, the flag is only checked;
+  // rows layout: the work-groups wait for the build's last flag themselves (no wait launch)
+  const bool pending = (ROWS && bflag) ? !block_wait_flag(bflag, bvalue, ka.werr, ka.max_polls)
+                                       : build_pending(bflag, bvalue);
+  if (pending) {
     if (!DEFER)
       for (int64_t n = (int64_t)blockIdx.x * 256 + threadIdx.x; n < N * 3; n += (int64_t)gridDim.x * 256)
         out[b * N * 3 + n] = 0.0f;
@@ -925,23 +1076,99 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
   }
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   Grid g;
-  g.load(gp + b * 8);
-  const uint64_t* S = start + b * Cpad;
-  const float4* R = refs + b * M;
+  g.load(gp + cl * 8);
+  const uint64_t* S = start + cl * Cpad;
+  const float4* R = refs + b * (ROWS ? N : M);
   const float* V = DEFER ? nullptr : vals + b * M * 3;
+  const uint64_t* CW = ROWS ? ka.cw + b * Cpad : nullptr;
+  const uint32_t rlim = (uint32_t)(ROWS ? N : M);
+  // the ref range of cell u0, checked against the ref array (a bad build raises, never faults)
+  auto rng = [&](int u0, uint64_t& lo, uint64_t& hi) {
+    uint32_t a, e;
+    if constexpr (ROWS) {  // the cell's placed refs
+      const uint64_t cwv = CW[u0];
+      a = (uint32_t)cwv;
+      e = a + (uint32_t)(cwv >> 32);
+    } else {
+      a = (uint32_t)S[u0];
+      e = (uint32_t)S[u0 + 1];
+    }
+    if (e < a || e > rlim) {
+      atomicOr(ka.err, 8);
+      a = e = 0;
+    }
+    lo = a;
+    hi = e;
+  };
   const Win W = {cand[wv][0], cand[wv][1], cand[wv][2], reinterpret_cast<int*>(cand[wv][3])};
   const Box none = {1, 0, 1, 0, 1, 0};
-  const int nch = nchunk[b];
+  const int nch = nchunk[cl];
+  // the row's overflow refs (rows layout; a few dozen in the bench), staged once per work-group
+  // with their cell coordinates: a pass offers a query only those inside the box it scanned (the
+  // settled test covers every ref outside it, as for the cell-placed refs)
+  __shared__ float4 ovl[ROWS ? kOvlLds : 1];
+  __shared__ uint64_t ovc[ROWS ? kOvlLds : 1];
+  const int novr = ROWS ? ka.ovn[b] : 0;
+  auto ov_cell = [&](float4 r) {  // cell coordinates x | y << 16 | z << 32 (each < 2048)
+    return (uint64_t)cell_coord(r.x, g.o[0], g.inv, g.d[0]) |
+           ((uint64_t)cell_coord(r.y, g.o[1], g.inv, g.d[1]) << 16) |
+           ((uint64_t)cell_coord(r.z, g.o[2], g.inv, g.d[2]) << 32);
+  };
+  if constexpr (ROWS) {
+    for (int i = threadIdx.x; i < min(novr, kOvlLds); i += 256) {
+      const float4 r = ka.over[b * M + i];
+      ovl[i] = r;
+      ovc[i] = ov_cell(r);
+    }
+    __syncthreads();
+  }
+  // offer every overflow ref whose cell lies in bx but not in prev (wave-uniform)
+  auto offer_overflow = [&](const Box& bx, const Box& prev, Query& me) {
+    for (int o0 = 0; o0 < novr; o0 += 64) {
+      const int i = o0 + lane;
+      float4 r = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+      uint64_t c = 0;
+      if (i < novr) {
+        if (i < kOvlLds) {
+          r = ovl[i];
+          c = ovc[i];
+        } else {
+          r = ka.over[b * M + i];
+          c = ov_cell(r);
+        }
+      }
+      const int x = (int)(c & 0xffffu), y = (int)((c >> 16) & 0xffffu), z = (int)(c >> 32);
+      uint64_t in = __ballot(i < novr && bx.has(x, y, z) && !prev.has(x, y, z));
+      while (in) {
+        const int k = __builtin_ctzll(in);
+        in &= in - 1;
+        float4 rk;
+        rk.x = __shfl(r.x, k); rk.y = __shfl(r.y, k); rk.z = __shfl(r.z, k); rk.w = __shfl(r.w, k);
+        me.consider(rk, kk);
+      }
+    }
+  };
   for (int item = blockIdx.x * 4 + wv; item < nch; item += gridDim.x * 4) {
-    const uint2 ch = chunks[b * maxch + item];
-    const bool valid = ch.x + lane < ch.y;
-#ifdef KNN_TRACE
-    const unsigned long long kt0 = clock64();
-    unsigned long long kt1 = 0, kt2 = 0;
-    uint32_t ks1 = 0, ks2 = 0, ks3 = 0, ko1 = 0, ko2 = 0, kvol = 0;
-#endif
-    const int64_t n = qorder[b * N + (valid ? ch.x + lane : ch.x)];
-    const float* qp = orig + (b * N + n) * 3;
+    const uint2 ch = chunks[cl * maxch + item];
+    if (ch.x > ch.y || ch.y > (uint32_t)N || ch.y - ch.x > 64u) {  // wave-uniform
+      if (lane == 0) atomicOr(ka.err, 4);
+      continue;
+    }
+    bool valid = ch.x + lane < ch.y;
+    const int64_t n = qorder[cl * N + (valid ? ch.x + lane : ch.x)];
+    const float* qp = orig + (cl * N + n) * 3;
+    if constexpr (ROWS) {  // a known row takes its coarse value (the last coarse row naming it)
+      const uint32_t kn = valid ? ka.known[b * N + n] : 0u;
+      if (kn) {
+        if (!DEFER) {
+          const float* v = V + (int64_t)(kn - 1) * 3;
+          float* o = out + (b * N + n) * 3;
+          o[0] = v[0]; o[1] = v[1]; o[2] = v[2];
+        }
+        valid = false;
+      }
+      if (!__any(valid)) continue;
+    }
     Query me;
     me.init(qp[0], qp[1], qp[2]);
     const int cx = cell_coord(me.fx, g.o[0], g.inv, g.d[0]);
@@ -953,14 +1180,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
     Box pb = {max(lx - 1, 0), min(hx + 1, g.d[0] - 1), max(ly - 1, 0), min(hy + 1, g.d[1] - 1),
               max(lz - 1, 0), min(hz + 1, g.d[2] - 1)};
     uint32_t unlimited = 0xffffffffu;
-    scan_box(pb, none, g, S, R, W, me, kk, unlimited);
+    scan_box(pb, none, g, rng, R, W, me, kk, unlimited);
+    if constexpr (ROWS) offer_overflow(pb, none, me);
     bool open = valid && !settled(me, pb, g, kk);
     bool ok = true;
-#ifdef KNN_TRACE
-    kt1 = clock64();
-    ks1 = 0xffffffffu - unlimited;
-    ko1 = (uint32_t)__popcll(__ballot(open));
-#endif
     // 2. the balls of the open lanes that hold kk refs
     if (__any(open)) {
       const double dk = me.t.last(kk);
@@ -984,15 +1207,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
         const Box bb = {min(pb.x0, wave_min(bx0)), max(pb.x1, wave_max(bx1)),
                         min(pb.y0, wave_min(by0)), max(pb.y1, wave_max(by1)),
                         min(pb.z0, wave_min(bz0)), max(pb.z1, wave_max(bz1))};
-#ifdef KNN_TRACE
-        kvol = bb.volume();
-#endif
         if (bb.volume() <= kBallUnion) {
           uint32_t budget = kBallBudget;
-          ok = scan_box(bb, pb, g, S, R, W, me, kk, budget);
-#ifdef KNN_TRACE
-          ks2 = ok ? kBallBudget - budget : 0xffffffffu;
-#endif
+          ok = scan_box(bb, pb, g, rng, R, W, me, kk, budget);
+          if constexpr (ROWS) {
+            if (ok) offer_overflow(bb, pb, me);
+          }
           if (ok) {
             pb = bb;
             open = open && !settled(me, pb, g, kk);
@@ -1000,11 +1220,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
         }
       }
     }
-#ifdef KNN_TRACE
-    kt2 = clock64();
-    ko2 = (uint32_t)__popcll(__ballot(open));
-    ks3 = 0;
-#endif
     // the rest (sparse neighbourhoods, ball too large, budget exceeded): the outlier pass
     const uint64_t rest = __ballot(open);
     if (rest) {
@@ -1019,17 +1234,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
       }
     }
     if (valid && !open) row_write(me.t, kk, V, out, DEFER ? nbr : nullptr, b * N + n);
-#ifdef KNN_TRACE
-    const unsigned long long kt3 = clock64();
-    if (lane == 0 && item < 32768) {
-      unsigned long long* r = g_knn_trace + ((int64_t)b * 32768 + item) * 8;
-      r[0] = ((unsigned long long)(ch.y - ch.x) << 32) | 1u;
-      r[1] = ((unsigned long long)ko1 << 32) | ko2;
-      r[2] = kt0; r[3] = kt1; r[4] = kt2; r[5] = kt3;
-      r[6] = ((unsigned long long)ks1 << 32) | ks2;
-      r[7] = ((unsigned long long)ks3 << 32) | ((unsigned long long)__popcll(rest) << 16) | (kvol & 0xffff);
-    }
-#endif
   }
 }
 
@@ -1045,211 +1249,6 @@ __device__ __forceinline__ void wave_merge_top3(Top3& t, int top = 32) {
   }
 }
 
-// Exhaustive 3-NN of the outlier queries, kOutPB queries per workgroup iteration: thread i
-// takes refs i, i+1024, ... (kOutLd loads in flight) and scores each against all kOutPB queries, so
-// a ref is read from L2 once per kOutPB queries.
-//   phase 1: the fp32 three smallest per thread and query (branch-free), merged by a wave
-//            butterfly and one wave per query over the 16 waves: the query's fp32 kk-th
-//            smallest, and from it the query pass's screen (fp32 error margin);
-//   phase 2: the refs within the screen (a handful) are appended to the query's LDS list;
-//   rank:    one wave per query ranks its list in float64 (Top3's (distance, j) order is
-//            independent of the visiting order, so the atomic appends stay deterministic).
-// A list that overflows (many refs at exactly the screen distance) falls back to the
-// block-wide float64 scan of that query.  With at most one query per workgroup (the common
-// case after the first steps of a trajectory) each workgroup scans its query alone in one
-// pass (outlier_full: fewest dependent steps per query); the two-phase batch pays off once
-// the L2 re-reads of one-query-per-block dominate (the noisy first steps: ~500 per cloud).
-constexpr int kOutPB = 4;        // queries per workgroup iteration (even: packed pairs)
-constexpr int kOutLd = 4;        // ref loads in flight per thread (multi-query path)
-constexpr int kOutCap = 1024;    // LDS candidates per query
-
-template <int kk>
-__device__ void outlier_full(const float4* __restrict__ R, const float* __restrict__ V, int64_t M,
-                             float x, float y, float z, float* __restrict__ o, double (*sd)[3],
-                             int (*sj)[3]) {
-  constexpr int W = kOutlierThreads / 64, Q = kOutlierThreads;
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  Query me;
-  me.init(x, y, z);
-  for (int64_t i = threadIdx.x; i < M; i += Q) me.consider(R[i], kk);
-  wave_merge_top3(me.t);
-  if (lane == 0) {
-    sd[wv][0] = me.t.d0; sd[wv][1] = me.t.d1; sd[wv][2] = me.t.d2;
-    sj[wv][0] = me.t.j0; sj[wv][1] = me.t.j1; sj[wv][2] = me.t.j2;
-  }
-  __syncthreads();
-  if (wv == 0) {
-    Top3 t;
-    t.init();
-    if (lane < W) {
-      t.d0 = sd[lane][0]; t.d1 = sd[lane][1]; t.d2 = sd[lane][2];
-      t.j0 = sj[lane][0]; t.j1 = sj[lane][1]; t.j2 = sj[lane][2];
-    }
-    wave_merge_top3(t, W / 2);
-    if (lane == 0) idw_write(t, kk, V, o);
-  }
-  __syncthreads();
-}
-
-__device__ __forceinline__ void top3f(float& c0, float& c1, float& c2, float d) {
-  const float n0 = fminf(c0, d);
-  const float n1 = __builtin_amdgcn_fmed3f(c0, c1, d);
-  const float n2 = __builtin_amdgcn_fmed3f(c1, c2, d);
-  c0 = n0; c1 = n1; c2 = n2;
-}
-
-template <int kk>
-__global__ __launch_bounds__(kOutlierThreads) void knn_outlier_kernel(
-    const float* __restrict__ vals, int64_t N, int64_t M, const float* __restrict__ orig,
-    const float4* __restrict__ refs, const int32_t* __restrict__ olist,
-    const int32_t* __restrict__ ocount, const uint32_t* __restrict__ known,
-    float* __restrict__ out, const uint32_t* __restrict__ bflag, uint32_t bvalue) {
-  if (build_pending(bflag, bvalue)) return;
-  constexpr int W = kOutlierThreads / 64;
-  constexpr int Q = kOutlierThreads;
-  constexpr int P = kOutPB;
-  __shared__ double sd[W][3];
-  __shared__ int sj[W][3];
-  __shared__ float sc3[P][W][3];
-  __shared__ float s_q[P][4];  // query x, y, z, screen
-  __shared__ int64_t s_n[P];
-  __shared__ int s_cnt[P];
-  __shared__ int s_cand[P][kOutCap];
-  const int b = blockIdx.y;
-  // rows that are coarse points take the coarse value (result[idx] = coarse; the last coarse
-  // row writing a point wins, as in the reference's index assignment)
-  for (int64_t n = (int64_t)blockIdx.x * Q + threadIdx.x; n < N; n += (int64_t)gridDim.x * Q) {
-    const uint32_t kn = known[b * N + n];
-    if (kn) {
-      const float* v = vals + (b * M + (int64_t)(kn - 1)) * 3;
-      float* o = out + (b * N + n) * 3;
-      o[0] = v[0]; o[1] = v[1]; o[2] = v[2];
-    }
-  }
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const float4* R = refs + b * M;
-  const float* V = vals + b * M * 3;
-  const int cnt = ocount[b];
-  if (cnt <= (int)gridDim.x) {  // at most one query per workgroup
-    for (int q = blockIdx.x; q < cnt; q += gridDim.x) {
-      const int64_t n = olist[b * N + q];
-      const float* p = orig + (b * N + n) * 3;
-      outlier_full<kk>(R, V, M, p[0], p[1], p[2], out + (b * N + n) * 3, sd, sj);
-    }
-    return;
-  }
-  for (int q0 = blockIdx.x * P; q0 < cnt; q0 += gridDim.x * P) {
-    if (threadIdx.x < P) {  // the iteration's queries; padding slots repeat the last one
-      const int qi = min(q0 + (int)threadIdx.x, cnt - 1);
-      const int64_t n = olist[b * N + qi];
-      const float* p = orig + (b * N + n) * 3;
-      s_n[threadIdx.x] = n;
-      s_q[threadIdx.x][0] = p[0]; s_q[threadIdx.x][1] = p[1]; s_q[threadIdx.x][2] = p[2];
-      s_cnt[threadIdx.x] = 0;
-    }
-    __syncthreads();
-    // query pairs in packed registers: one v_pk op scores a ref against two queries (the ref
-    // coordinate is broadcast to both halves); the same IEEE operations as dist32
-    f2 qx2[P / 2], qy2[P / 2], qz2[P / 2];
-    float c0[P], c1[P], c2[P];
-#pragma unroll
-    for (int u = 0; u < P / 2; ++u) {
-      qx2[u] = f2{s_q[2 * u][0], s_q[2 * u + 1][0]};
-      qy2[u] = f2{s_q[2 * u][1], s_q[2 * u + 1][1]};
-      qz2[u] = f2{s_q[2 * u][2], s_q[2 * u + 1][2]};
-    }
-#pragma unroll
-    for (int u = 0; u < P; ++u) c0[u] = c1[u] = c2[u] = INFINITY;
-    // phase 1
-    for (int64_t i = threadIdx.x; i < M; i += kOutLd * Q) {
-      float4 r[kOutLd];
-#pragma unroll
-      for (int k = 0; k < kOutLd; ++k)
-        if (i + k * Q < M) r[k] = R[i + k * Q];
-#pragma unroll
-      for (int k = 0; k < kOutLd; ++k)
-        if (i + k * Q < M) {
-          const f2 rx = {r[k].x, r[k].x}, ry = {r[k].y, r[k].y}, rz = {r[k].z, r[k].z};
-#pragma unroll
-          for (int u = 0; u < P / 2; ++u) {
-            const f2 d = dist2(qx2[u], qy2[u], qz2[u], rx, ry, rz);
-            top3f(c0[2 * u], c1[2 * u], c2[2 * u], d.x);
-            top3f(c0[2 * u + 1], c1[2 * u + 1], c2[2 * u + 1], d.y);
-          }
-        }
-    }
-#pragma unroll
-    for (int u = 0; u < P; ++u) {
-#pragma unroll
-      for (int off = 32; off >= 1; off >>= 1) {
-        const float o0 = __shfl_xor(c0[u], off), o1 = __shfl_xor(c1[u], off), o2 = __shfl_xor(c2[u], off);
-        top3f(c0[u], c1[u], c2[u], o0);
-        top3f(c0[u], c1[u], c2[u], o1);
-        top3f(c0[u], c1[u], c2[u], o2);
-      }
-      if (lane == 0) { sc3[u][wv][0] = c0[u]; sc3[u][wv][1] = c1[u]; sc3[u][wv][2] = c2[u]; }
-    }
-    __syncthreads();
-    if (wv < P) {  // wave u merges query u's 16 wave triples
-      float a0 = INFINITY, a1 = INFINITY, a2 = INFINITY;
-      if (lane < W) { a0 = sc3[wv][lane][0]; a1 = sc3[wv][lane][1]; a2 = sc3[wv][lane][2]; }
-#pragma unroll
-      for (int off = W / 2; off >= 1; off >>= 1) {
-        const float o0 = __shfl_xor(a0, off), o1 = __shfl_xor(a1, off), o2 = __shfl_xor(a2, off);
-        top3f(a0, a1, a2, o0);
-        top3f(a0, a1, a2, o1);
-        top3f(a0, a1, a2, o2);
-      }
-      if (lane == 0) {
-        const float ck = kk >= 3 ? a2 : (kk == 2 ? a1 : a0);
-        s_q[wv][3] = ck * 1.000002f + 1e-30f;  // the query pass's screen (fp32 error margin)
-      }
-    }
-    __syncthreads();
-    // phase 2: the screened-in refs of each query into its LDS list
-    f2 scr[P / 2];
-#pragma unroll
-    for (int u = 0; u < P / 2; ++u) scr[u] = f2{s_q[2 * u][3], s_q[2 * u + 1][3]};
-    for (int64_t i = threadIdx.x; i < M; i += kOutLd * Q) {
-      float4 r[kOutLd];
-#pragma unroll
-      for (int k = 0; k < kOutLd; ++k)
-        if (i + k * Q < M) r[k] = R[i + k * Q];
-#pragma unroll
-      for (int k = 0; k < kOutLd; ++k)
-        if (i + k * Q < M) {
-          const f2 rx = {r[k].x, r[k].x}, ry = {r[k].y, r[k].y}, rz = {r[k].z, r[k].z};
-#pragma unroll
-          for (int u = 0; u < P / 2; ++u) {
-            const f2 d = dist2(qx2[u], qy2[u], qz2[u], rx, ry, rz);
-#pragma unroll
-            for (int e = 0; e < 2; ++e)
-              if (d[e] <= scr[u][e]) {
-                const int slot = atomicAdd(&s_cnt[2 * u + e], 1);
-                if (slot < kOutCap) s_cand[2 * u + e][slot] = (int)(i + k * Q);
-              }
-          }
-        }
-    }
-    __syncthreads();
-    // rank: wave u, query u (a padding slot repeats a query: skipped)
-    if (wv < P && q0 + wv < cnt && s_cnt[wv] <= kOutCap) {
-      Query me;
-      me.init(s_q[wv][0], s_q[wv][1], s_q[wv][2]);
-      const int c = s_cnt[wv];
-      for (int k = lane; k < c; k += 64) me.exact(R[s_cand[wv][k]]);
-      wave_merge_top3(me.t);
-      if (lane == 0) idw_write(me.t, kk, V, out + (b * N + s_n[wv]) * 3);
-    }
-    // overflowed lists: the block-wide float64 scan (block-uniform condition)
-#pragma unroll 1
-    for (int u = 0; u < P; ++u)
-      if (q0 + u < cnt && s_cnt[u] > kOutCap)
-        outlier_full<kk>(R, V, M, s_q[u][0], s_q[u][1], s_q[u][2], out + (b * N + s_n[u]) * 3, sd, sj);
-    __syncthreads();
-  }
-}
-
 // Brick-shell search of the outlier queries: one wave per query.  Bricks (4x4x4 cells) are the
 // grid's coarse level for free: a brick's refs are one contiguous range of the cell-sorted refs,
 // [start(64 id), start(64 id + 64)).  The wave scans the box of bricks within Chebyshev brick
@@ -1262,20 +1261,23 @@ __global__ __launch_bounds__(kOutlierThreads) void knn_outlier_kernel(
 // bounds carry the same cell-rounding slack).  A shell's refs are split over the lanes
 // (scan_units_1q); after every shell the lanes' lists are merged into lane 0 (the others restart
 // empty with the merged screen), so no ref is offered twice.
-template <int kk>
+// Rows layout (ROWS): a brick's refs are one run from its first cell's first slot to its last
+// cell's end; the overflow refs are offered first; the known rows were copied by the query.
+template <int kk, bool ROWS>
 __global__ __launch_bounds__(256) void knn_outlier_brick_kernel(
     const float* __restrict__ vals, int64_t N, int64_t M, const float* __restrict__ orig,
     const float* __restrict__ gp, int64_t Cpad, const uint64_t* __restrict__ start,
     const float4* __restrict__ refs, const int32_t* __restrict__ olist,
     const float* __restrict__ obound, const int32_t* __restrict__ ocount,
     const uint32_t* __restrict__ known, float* __restrict__ out, NbrRec* __restrict__ nbr,
-    const uint32_t* __restrict__ bflag, uint32_t bvalue) {
+    const uint32_t* __restrict__ bflag, uint32_t bvalue, const KArgs ka) {
   const int b = blockIdx.y;
+  const int64_t cl = ROWS ? b % ka.C : b;
   if (build_pending(bflag, bvalue)) return;
   // rows that are coarse points take the coarse value (result[idx] = coarse; the last coarse
   // row writing a point wins, as in the reference's index assignment); the deferred search
   // leaves them to the finish pass
-  for (int64_t n = (int64_t)blockIdx.x * 256 + threadIdx.x; !nbr && n < N;
+  for (int64_t n = (int64_t)blockIdx.x * 256 + threadIdx.x; !ROWS && !nbr && n < N;
        n += (int64_t)gridDim.x * 256) {
     const uint32_t kn = known[b * N + n];
     if (kn) {
@@ -1286,18 +1288,22 @@ __global__ __launch_bounds__(256) void knn_outlier_brick_kernel(
   }
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   Grid g;
-  g.load(gp + b * 8);
+  g.load(gp + cl * 8);
   const int nbx = g.bx, nby = g.by, nbz = (g.d[2] + 3) >> 2;
-  const uint64_t* S = start + b * Cpad;
-  const float4* R = refs + b * M;
+  const uint64_t* S = start + cl * Cpad;
+  const float4* R = refs + b * (ROWS ? N : M);
+  const uint64_t* CW = ROWS ? ka.cw + b * Cpad : nullptr;
   const float* V = vals ? vals + b * M * 3 : nullptr;
   const int cnt = ocount[b];
+  const int novr = ROWS ? ka.ovn[b] : 0;
+  const uint32_t rlim = (uint32_t)(ROWS ? N : M);
   const double bs = 4.0 * (double)g.s;  // brick edge
   for (int q = blockIdx.x * 4 + wv; q < cnt; q += gridDim.x * 4) {
     const int64_t n = olist[b * N + q];
-    const float* qp = orig + (b * N + n) * 3;
+    const float* qp = orig + (cl * N + n) * 3;
     Query me;
     me.init(qp[0], qp[1], qp[2]);
+    for (int i = lane; i < novr; i += 64) me.consider(ka.over[b * M + i], kk);  // merged below
     const int qbx = cell_coord(me.fx, g.o[0], g.inv, g.d[0]) >> 2;
     const int qby = cell_coord(me.fy, g.o[1], g.inv, g.d[1]) >> 2;
     const int qbz = cell_coord(me.fz, g.o[2], g.inv, g.d[2]) >> 2;
@@ -1308,10 +1314,6 @@ __global__ __launch_bounds__(256) void knn_outlier_brick_kernel(
     double best = (double)obound[b * N + q];
     int r = 1;
     if (best != INFINITY) r = max(1, (int)fmin(floor(sqrt(best) * (1.0 + 1e-6) / bs) + 1.0, 4096.0));
-#ifdef KNN_TRACE
-    const unsigned long long ot0 = __builtin_amdgcn_s_memrealtime();
-    uint32_t oshells = 0, ostaged = 0, olastr = 0;
-#endif
     for (;;) {
       const Box bx = {max(qbx - r, 0), min(qbx + r, nbx - 1), max(qby - r, 0), min(qby + r, nby - 1),
                       max(qbz - r, 0), min(qbz + r, nbz - 1)};
@@ -1334,15 +1336,25 @@ __global__ __launch_bounds__(256) void knn_outlier_brick_kernel(
           const double e = fmax(sqrt(ex * ex + ey * ey + ez * ez) - g.slack, 0.0);
           if (e * e > lim) return;
           const int u0 = ((z * nby + y) * nbx + x) << 6;
-          lo = S[u0];
-          hi = S[u0 + 64];
+          uint32_t ra, re;
+          if constexpr (ROWS) {  // the brick's refs: its first cell's slot to its last cell's end
+            const uint64_t last = CW[u0 + 63];
+            ra = (uint32_t)CW[u0];
+            re = (uint32_t)last + (uint32_t)(last >> 32);
+          } else {
+            ra = (uint32_t)S[u0];
+            re = (uint32_t)S[u0 + 64];
+          }
+          if (re < ra || re > rlim) {
+            atomicOr(ka.err, 8);
+            return;
+          }
+          lo = ra;
+          hi = re;
         }
       };
       uint32_t staged = 0;
       scan_units_1q(vol, unit, R, me, kk, staged);
-#ifdef KNN_TRACE
-      ++oshells; ostaged += staged; olastr = r;
-#endif
       // merge the lanes' lists into lane 0; the others restart empty with the merged screen
       Top3 t = me.t;
       wave_merge_top3(t);
@@ -1371,15 +1383,6 @@ __global__ __launch_bounds__(256) void knn_outlier_brick_kernel(
       }
     }
     if (lane == 0) row_write(me.t, kk, V, out, nbr, b * N + n);
-#ifdef KNN_TRACE
-    if (lane == 0 && b < 2 && q < 4096) {
-      unsigned long long* tr = g_knn_otrace + ((int64_t)b * 4096 + q) * 4;
-      tr[0] = ot0;
-      tr[1] = __builtin_amdgcn_s_memrealtime();
-      tr[2] = ((unsigned long long)oshells << 32) | olastr;
-      tr[3] = ostaged;
-    }
-#endif
   }
 }
 
@@ -1506,7 +1509,7 @@ extern "C" int pcst_knn3_build(const float* orig, const int64_t* idx, int64_t B,
   hipLaunchKernelGGL(knn_pre_kernel, dim3(grid(kStatBlocks + kPreKnownBlocks), b), dim3(256), pad_pre,
                      s, orig, idx, (int)N, M, w.stats, w.known, w.err);
   hipLaunchKernelGGL(knn_count_kernel, dim3(grid(cdiv(M + N, kCountPerBlock)), b), dim3(256),
-                     pad_count, s, orig, idx, w.stats, w.known, N, M, w.Cmax, w.T, w.Cpad, w.gp,
+                     pad_count, s, orig, idx, w.stats, w.known, N, M, M, w.Cmax, w.T, w.Cpad, w.gp,
                      w.cnt, w.tsum, w.crank);
   hipLaunchKernelGGL(knn_scan_kernel, dim3(grid(w.T), b), dim3(256), pad_scan, s, w.cnt, w.tsum,
                      w.T, w.Cpad, w.chunks, w.maxch, w.nchunk);
@@ -1517,41 +1520,41 @@ extern "C" int pcst_knn3_build(const float* orig, const int64_t* idx, int64_t B,
   return PCST_OK;
 }
 
-// PCST_X_KNN_OUTLIER_EXHAUSTIVE (experiment builds, Makefile XDEF): the exhaustive outlier pass
-// instead of the brick-shell search (A/B only)
-#ifndef PCST_X_KNN_OUTLIER_EXHAUSTIVE
-#define PCST_X_KNN_OUTLIER_EXHAUSTIVE 0
-#endif
-
 // The query and outlier launches: vals/out given -> IDW written to out; nbr given (deferred
 // search, positions only) -> every query row's weights into the workspace's neighbour records.
-static void launch_knn_query(const KnnWS& w, const float* coarse, const float* orig, int64_t B,
-                             int64_t N, int64_t M, float* out, NbrRec* nbr, const uint32_t* bflag,
-                             uint32_t bvalue, int64_t grid_cap, hipStream_t s) {
+// Both layouts: the per-layout pointers (the compact workspace's or the rows workspace's) come in
+// as arguments; ka carries the rows layout's extras and the error word.
+template <bool ROWS>
+static void launch_knn_query(int64_t nch_max, const float* gp, const uint64_t* cnt, const float4* refs,
+                             const int32_t* qorder, const uint2* chunks, const int32_t* nchunk,
+                             int32_t* olist, float* obound, int32_t* ocount, const uint32_t* known,
+                             int64_t Cpad, const KArgs& ka, const float* coarse, const float* orig,
+                             int64_t B, int64_t N, int64_t M, float* out, NbrRec* nbr,
+                             const uint32_t* bflag, uint32_t bvalue, int64_t grid_cap, hipStream_t s) {
   const int b = (int)B;
   if (grid_cap <= 0) grid_cap = kQueryGridCapDefault;
   // fixed grids stride over the chunk and outlier lists (their lengths live on the device)
   const unsigned gq = (unsigned)std::min<int64_t>(
-      cdiv(w.maxch, 4), std::max<int64_t>(kQueryBlocksMin, std::min<int64_t>(kQueryBlocks, grid_cap / B)));
-  auto qk = nbr ? (M >= 3 ? knn_query_kernel<3, true>
-                          : (M == 2 ? knn_query_kernel<2, true> : knn_query_kernel<1, true>))
-                : (M >= 3 ? knn_query_kernel<3, false>
-                          : (M == 2 ? knn_query_kernel<2, false> : knn_query_kernel<1, false>));
-  hipLaunchKernelGGL(qk, dim3(gq, b), dim3(256), 0, s, orig, coarse, N, M, w.Cpad, w.gp, w.cnt,
-                     w.refs, w.qorder, w.chunks, w.maxch, w.nchunk, w.olist, w.obound, w.ocount, out,
-                     nbr, bflag, bvalue);
-  if (PCST_X_KNN_OUTLIER_EXHAUSTIVE && !nbr) {  // the exhaustive pass (A/B experiments)
-    auto ok = M >= 3 ? knn_outlier_kernel<3>
-                     : (M == 2 ? knn_outlier_kernel<2> : knn_outlier_kernel<1>);
-    hipLaunchKernelGGL(ok, dim3(kOutlierBlocks, b), dim3(kOutlierThreads), 0, s, coarse, N, M, orig,
-                       w.refs, w.olist, w.ocount, w.known, out, bflag, bvalue);
-  } else {
-    auto ok = M >= 3 ? knn_outlier_brick_kernel<3>
-                     : (M == 2 ? knn_outlier_brick_kernel<2> : knn_outlier_brick_kernel<1>);
-    hipLaunchKernelGGL(ok, dim3(kOutlierBrickBlocks, b), dim3(256), 0, s, coarse, N, M, orig, w.gp,
-                       w.Cpad, w.cnt, w.refs, w.olist, w.obound, w.ocount, w.known, out, nbr, bflag,
-                       bvalue);
-  }
+      cdiv(nch_max, 4), std::max<int64_t>(kQueryBlocksMin, std::min<int64_t>(kQueryBlocks, grid_cap / B)));
+  auto qk = nbr ? (M >= 3 ? knn_query_kernel<3, true, ROWS>
+                          : (M == 2 ? knn_query_kernel<2, true, ROWS> : knn_query_kernel<1, true, ROWS>))
+                : (M >= 3 ? knn_query_kernel<3, false, ROWS>
+                          : (M == 2 ? knn_query_kernel<2, false, ROWS> : knn_query_kernel<1, false, ROWS>));
+  hipLaunchKernelGGL(qk, dim3(gq, b), dim3(256), 0, s, orig, coarse, N, M, Cpad, gp, cnt, refs, qorder,
+                     chunks, nch_max, nchunk, olist, obound, ocount, out, nbr, bflag, bvalue, ka);
+  auto ok = M >= 3 ? knn_outlier_brick_kernel<3, ROWS>
+                   : (M == 2 ? knn_outlier_brick_kernel<2, ROWS> : knn_outlier_brick_kernel<1, ROWS>);
+  hipLaunchKernelGGL(ok, dim3(kOutlierBrickBlocks, b), dim3(256), 0, s, coarse, N, M, orig, gp, Cpad,
+                     cnt, refs, olist, obound, ocount, known, out, nbr, bflag, bvalue, ka);
+}
+
+static void launch_knn_query(const KnnWS& w, const float* coarse, const float* orig, int64_t B,
+                             int64_t N, int64_t M, float* out, NbrRec* nbr, const uint32_t* bflag,
+                             uint32_t bvalue, int64_t grid_cap, hipStream_t s) {
+  const KArgs ka = {B, nullptr, nullptr, nullptr, nullptr, w.err, nullptr, 0};
+  launch_knn_query<false>(w.maxch, w.gp, w.cnt, w.refs, w.qorder, w.chunks, w.nchunk, w.olist,
+                          w.obound, w.ocount, w.known, w.Cpad, ka, coarse, orig, B, N, M, out, nbr,
+                          bflag, bvalue, grid_cap, s);
 }
 
 #define PCST_KNN_SHAPE_CHECK(name)                                                      \
@@ -1626,27 +1629,6 @@ extern "C" int pcst_knn3_interp(const float* coarse, const float* orig, const in
   return pcst_knn3_query(coarse, orig, B, N, M, out, workspace, nullptr, 0u, 0, stream);
 }
 
-#ifdef KNN_TRACE
-extern "C" int pcst_knn_otrace_dump(void* host, size_t bytes) {
-  void* d = nullptr;
-  PCST_HIP(hipGetSymbolAddress(&d, HIP_SYMBOL(g_knn_otrace)), "knn_otrace: symbol");
-  PCST_HIP(hipDeviceSynchronize(), "knn_otrace: sync");
-  if (host) PCST_HIP(hipMemcpy(host, d, std::min(bytes, sizeof(g_knn_otrace)), hipMemcpyDeviceToHost), "knn_otrace: copy");
-  PCST_HIP(hipMemset(d, 0, sizeof(g_knn_otrace)), "knn_otrace: reset");
-  PCST_HIP(hipDeviceSynchronize(), "knn_otrace: sync");
-  return PCST_OK;
-}
-
-extern "C" int pcst_knn_trace_dump(void* host, size_t bytes) {
-  void* d = nullptr;
-  PCST_HIP(hipGetSymbolAddress(&d, HIP_SYMBOL(g_knn_trace)), "knn_trace: symbol");
-  PCST_HIP(hipDeviceSynchronize(), "knn_trace: sync");
-  if (host) PCST_HIP(hipMemcpy(host, d, std::min(bytes, sizeof(g_knn_trace)), hipMemcpyDeviceToHost), "knn_trace: copy");
-  PCST_HIP(hipMemset(d, 0, sizeof(g_knn_trace)), "knn_trace: reset");
-  PCST_HIP(hipDeviceSynchronize(), "knn_trace: sync");
-  return PCST_OK;
-}
-#endif
 
 // diagnostics: out[0] = error flag, out[1..B] = query chunks, out[1+B..2B] = outlier queries of
 // the last pcst_knn3_query on this workspace
@@ -1666,5 +1648,102 @@ extern "C" int pcst_knn_error(void* workspace, int64_t B, int64_t N, int64_t M, 
   KnnWS w = carve_knn(workspace, B, N, M);
   PCST_HIP(hipMemcpyAsync(err_out, w.err, sizeof(int32_t), hipMemcpyDeviceToDevice,
                           as_stream(stream)), "knn_error");
+  return PCST_OK;
+}
+
+// ---- rows layout ABI (pcst.h) ----
+#define PCST_KNN_ROWS_CHECK(name)                                                             \
+  PCST_CHECK_ARG(C >= 0 && copies >= 1 && N > 0 && M > 0 && N < (1ll << 31) && M < (1ll << 27), \
+                 name ": bad shape")
+
+extern "C" int pcst_knn_rows_workspace_size(int64_t C, int64_t copies, int64_t N, int64_t M,
+                                            size_t* bytes) {
+  PCST_KNN_ROWS_CHECK("knn_rows_workspace_size");
+  PCST_CHECK_ARG(bytes != nullptr, "knn_rows_workspace_size: null pointer");
+  *bytes = carve_knn_rows(nullptr, C, copies, N, M).bytes;
+  return PCST_OK;
+}
+
+extern "C" int pcst_knn3_rows_build(const float* x, int64_t C, int64_t copies, int64_t N, int64_t M,
+                                    void* workspace, uint32_t* refs_flag, uint32_t refs_value,
+                                    uint32_t* done_flag, uint32_t done_value, void* stream) {
+  PCST_KNN_ROWS_CHECK("knn3_rows_build");
+  if (C == 0) return PCST_OK;
+  PCST_CHECK_ARG(x && workspace, "knn3_rows_build: null pointer");
+  hipStream_t s = as_stream(stream);
+  KnnRowsWS w = carve_knn_rows(workspace, C, copies, N, M);
+  const int c = (int)C;
+  const size_t zbytes = (size_t)(w.bytes - ((char*)w.err - (char*)workspace));  // 256-B multiple
+  hipLaunchKernelGGL(knn_pre_kernel, dim3(kStatBlocks + kPreZeroBlocks, c), dim3(256), 0, s, x,
+                     (const int64_t*)nullptr, (int)N, (int64_t)0, w.stats, w.known, w.err,
+                     reinterpret_cast<uint4*>(w.err), (int64_t)(zbytes / 16));
+  hipLaunchKernelGGL(knn_count_kernel, dim3((unsigned)cdiv(N, kCountPerBlock), c), dim3(256), 0, s, x,
+                     (const int64_t*)nullptr, w.stats, (const uint32_t*)nullptr, N, (int64_t)0, M, w.Cmax,
+                     w.T, w.Cpad, w.gp, w.cnt, w.tsum, w.crank);
+  hipLaunchKernelGGL(knn_scan_kernel, dim3((unsigned)w.T, c), dim3(256), 0, s, w.cnt, w.tsum, w.T,
+                     w.Cpad, w.chunks, w.maxch, w.nchunk);
+  // the ref placement reads the starts and the rows' cells, not the fill's row order
+  if (refs_flag) hipLaunchKernelGGL(knn_flag_kernel, dim3(1), dim3(64), 0, s, refs_flag, refs_value);
+  hipLaunchKernelGGL(knn_fill_kernel, dim3((unsigned)std::min<int64_t>(cdiv(N, 256), 2048), c), dim3(256),
+                     0, s, x, (const int64_t*)nullptr, N, (int64_t)0, w.Cpad, w.cnt, w.crank,
+                     (float4*)nullptr, w.qorder);
+  if (done_flag) hipLaunchKernelGGL(knn_flag_kernel, dim3(1), dim3(64), 0, s, done_flag, done_value);
+  PCST_LAUNCH_CHECK("knn3_rows_build");
+  return PCST_OK;
+}
+
+extern "C" int pcst_knn3_rows_refs(const float* x, const int64_t* idx, int64_t C, int64_t copies,
+                                   int64_t N, int64_t M, void* workspace, const uint32_t* wait_flag,
+                                   uint32_t wait_value, int32_t* wait_err, int64_t max_polls,
+                                   void* stream) {
+  PCST_KNN_ROWS_CHECK("knn3_rows_refs");
+  if (C == 0) return PCST_OK;
+  PCST_CHECK_ARG(x && idx && workspace, "knn3_rows_refs: null pointer");
+  KnnRowsWS w = carve_knn_rows(workspace, C, copies, N, M);
+  hipStream_t s = as_stream(stream);
+  const dim3 gj((unsigned)std::min<int64_t>(cdiv(M, 256), 1024), (unsigned)w.B);
+  hipLaunchKernelGGL(knn_rows_rank_kernel, gj, dim3(256), 0, s, x, idx, C, N, M, w.Cpad, w.cnt, w.crank,
+                     w.known, w.rcnt, w.rrank, w.over, w.ovn, w.err, wait_flag, wait_value, wait_err,
+                     max_polls > 0 ? max_polls : (int64_t)kSignalPolls);
+  hipLaunchKernelGGL(knn_rows_cellscan_kernel, dim3((unsigned)cdiv(w.Cpad / 64, 4), (unsigned)w.B), dim3(256),
+                     0, s, C, w.Cpad, w.cnt, w.rcnt, w.cw);
+  hipLaunchKernelGGL(knn_rows_place_kernel, gj, dim3(256), 0, s, x, idx, C, N, M, w.Cpad, w.crank, w.rrank,
+                     w.cw, w.refs);
+  PCST_LAUNCH_CHECK("knn3_rows_refs");
+  return PCST_OK;
+}
+
+extern "C" int pcst_knn3_rows_query(const float* coarse, const float* x, int64_t C, int64_t copies,
+                                    int64_t N, int64_t M, float* out, void* workspace,
+                                    const uint32_t* built_flag, uint32_t built_value,
+                                    int32_t* wait_err, int64_t max_polls, int64_t grid_cap,
+                                    void* stream) {
+  PCST_KNN_ROWS_CHECK("knn3_rows_query");
+  if (C == 0) return PCST_OK;
+  PCST_CHECK_ARG(coarse && x && out && workspace, "knn3_rows_query: null pointer");
+  KnnRowsWS w = carve_knn_rows(workspace, C, copies, N, M);
+  const KArgs ka = {C, w.known, w.cw, w.over, w.ovn, w.err, wait_err,
+                    max_polls > 0 ? max_polls : (int64_t)kSignalPolls};
+  launch_knn_query<true>(w.maxch, w.gp, w.cnt, w.refs, w.qorder, w.chunks, w.nchunk, w.olist,
+                         w.obound, w.ocount, w.known, w.Cpad, ka, coarse, x, w.B, N, M, out, nullptr,
+                         built_flag, built_value, grid_cap, as_stream(stream));
+  PCST_LAUNCH_CHECK("knn3_rows_query");
+  return PCST_OK;
+}
+
+// out[0] = error word, out[1..C] = chunks per cloud, out[1+C..C+B] = outlier queries and
+// out[1+C+B..C+2B] = overflow refs per CFG row of the last build / refs / query on this workspace
+extern "C" int pcst_knn_rows_stats(void* workspace, int64_t C, int64_t copies, int64_t N, int64_t M,
+                                   int32_t* out, void* stream) {
+  PCST_KNN_ROWS_CHECK("knn_rows_stats");
+  PCST_CHECK_ARG(workspace && out, "knn_rows_stats: null pointer");
+  KnnRowsWS w = carve_knn_rows(workspace, C, copies, N, M);
+  hipStream_t s = as_stream(stream);
+  PCST_HIP(hipMemcpyAsync(out, w.err, sizeof(int32_t), hipMemcpyDeviceToDevice, s), "knn_rows_stats");
+  PCST_HIP(hipMemcpyAsync(out + 1, w.nchunk, sizeof(int32_t) * C, hipMemcpyDeviceToDevice, s), "knn_rows_stats");
+  PCST_HIP(hipMemcpyAsync(out + 1 + C, w.ocount, sizeof(int32_t) * w.B, hipMemcpyDeviceToDevice, s),
+           "knn_rows_stats");
+  PCST_HIP(hipMemcpyAsync(out + 1 + C + w.B, w.ovn, sizeof(int32_t) * w.B, hipMemcpyDeviceToDevice, s),
+           "knn_rows_stats");
   return PCST_OK;
 }

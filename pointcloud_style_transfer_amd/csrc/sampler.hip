@@ -83,7 +83,6 @@ __global__ void signal_write_kernel(uint32_t* flag, uint32_t value) {
 // one lane polls (agent-scope loads, L2-served, with s_sleep between polls) until the flag
 // reaches `value`, at most max_polls times (default kSignalPolls, ~10 s); then an agent-scope
 // acquire.  A wait that gives up sets *err: the caller must read it (the stream goes on).
-constexpr int kSignalPolls = 1 << 26;
 __global__ void signal_wait_kernel(const uint32_t* flag, uint32_t value, int32_t* err,
                                    int64_t max_polls) {
   if (threadIdx.x == 0) {

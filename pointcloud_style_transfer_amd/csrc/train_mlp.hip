@@ -372,13 +372,7 @@ __global__ __launch_bounds__(256) void gemm_ex_kernel(const TA* __restrict__ A, 
 
 // ---- bf16 x bf16 GEMM, K staged kBK deep through registers (the next slice's buffer loads in
 // flight during this slice's MFMAs) into a double-buffered LDS image: one barrier per slice.
-#ifndef PCST_GEMM_BK
-#define PCST_GEMM_BK 32
-#endif
-constexpr int kBK = PCST_GEMM_BK;   // k slice (32 or 64)
-#ifndef PCST_GEMM_PF  // experiment builds: 2 = two slices in flight (two register stages)
-#define PCST_GEMM_PF 1
-#endif
+constexpr int kBK = 32;             // k slice
 constexpr int kBLd = kBK + 8;       // LDS row, bf16 elements (+16 B pad: conflict-free row reads)
 constexpr int kCPR = kBK / 8;       // 16-byte chunks per row slice
 constexpr int kBIt = kCPR / 2;      // loads per thread per operand per slice
@@ -594,22 +588,6 @@ __global__ __launch_bounds__(256) void gemm_bf_kernel(const uint16_t* __restrict
   const int nk = K / kBK;
   BfRegs g;
   bf_load(ra, rb, va, vb, 0, g);
-#if PCST_GEMM_PF == 2
-  // two slices in flight (K % 64 == 0: nk is even): the register stages alternate, each loaded
-  // two slices ahead of its LDS store
-  BfRegs g1;
-  bf_load(ra, rb, va, vb, (uint32_t)(kBK * 2), g1);
-  for (int k = 0; k < nk; k += 2) {
-    bf_store(g, As0, Bs0, tid);
-    lds_barrier();
-    if (k + 2 < nk) bf_load(ra, rb, va, vb, (uint32_t)((k + 2) * kBK * 2), g);
-    bf_mma(As0, Bs0, wr, wc, l32, h, acc);
-    bf_store(g1, As1, Bs1, tid);
-    lds_barrier();
-    if (k + 3 < nk) bf_load(ra, rb, va, vb, (uint32_t)((k + 3) * kBK * 2), g1);
-    bf_mma(As1, Bs1, wr, wc, l32, h, acc);
-  }
-#else
   for (int k = 0; k < nk; ++k) {
     Row* As = (k & 1) ? As1 : As0;
     Row* Bs = (k & 1) ? Bs1 : Bs0;
@@ -618,7 +596,6 @@ __global__ __launch_bounds__(256) void gemm_bf_kernel(const uint16_t* __restrict
     if (k + 1 < nk) bf_load(ra, rb, va, vb, (uint32_t)((k + 1) * kBK * 2), g);
     bf_mma(As, Bs, wr, wc, l32, h, acc);
   }
-#endif
   __syncthreads();  // every wave's MFMA reads done before the epilogue reuses the LDS
   if (FAST)
     gemm_epilogue_fast<EP>(acc, reinterpret_cast<float (*)[kCLd]>(smem), M, O, m0, o0, args);
@@ -626,138 +603,15 @@ __global__ __launch_bounds__(256) void gemm_bf_kernel(const uint16_t* __restrict
     gemm_epilogue<EP>(acc, reinterpret_cast<float (*)[kCLd]>(smem), M, O, m0, o0, args);
 }
 
-// ---- bf16 x bf16 GEMM fed by LDS DMA (buffer_load ... lds, 16 B per lane): K staged 32 deep
-// through a ring of S LDS stages, S-1 slices in flight while a slice's MFMAs run, no staging
-// registers.  A DMA instruction fills 1 KiB of LDS contiguously (16 rows x 64 B), so the rows
-// are unpadded and the 16-byte chunk c of row r sits at c ^ ((r >> 2) & 3): conflict-free for
-// the 32x32x16 fragment reads under the ds_read_b128 lane groups (MI355X_MICROARCH.md, LDS).
-// One __shared__ array per stage lets the compiler's LDS-DMA tracking wait for exactly the
-// stage a read needs; the explicit vmcnt before each barrier makes every wave's part of the
-// slice land before any wave reads it.
-constexpr int kDK = 32;                      // k slice
-constexpr int kDStage = 2 * kXT * kDK * 2;   // A + B image, bytes (16 KiB)
-constexpr int kDStageAlloc = 32 * kCLd * 4;  // 16.5 KiB: a stage doubles as a 32-row epilogue pass
-static_assert(kDStageAlloc >= kDStage, "stage too small");
-
-__device__ __forceinline__ void dma_slice(rsrc_t ra, rsrc_t rb, uint32_t va0, uint32_t va1,
-                                          uint32_t vb0, uint32_t vb1, uint32_t soff, char* stage,
-                                          int wid) {
-  typedef __attribute__((address_space(3))) void* lds_ptr;
-  char* a = stage + wid * 2048;
-  char* b = stage + kXT * kDK * 2 + wid * 2048;
-  __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (lds_ptr)a, 16, (int)va0, (int)soff, 0, 0);
-  __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (lds_ptr)(a + 1024), 16, (int)va1, (int)soff, 0, 0);
-  __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (lds_ptr)b, 16, (int)vb0, (int)soff, 0, 0);
-  __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (lds_ptr)(b + 1024), 16, (int)vb1, (int)soff, 0, 0);
-}
-
-// Fragment reads in inline asm: invisible to the compiler's LDS-DMA tracking, which would
-// otherwise drain vmcnt(0) (every slice in flight) at the loop head.  Each read's wait is a
-// counted lgkmcnt tied to the registers it guards (as csrc/noise_mlp.hip does), so no MFMA
-// is scheduled above it; the vm_barrier before the reads makes the slice's DMA complete.
+// A 16-bit fragment read in inline asm (the residual-block kernels): invisible to the compiler's
+// LDS-DMA tracking, which would otherwise drain vmcnt(0) (every weight slice in flight) at the
+// loop head.  Each read's wait is a counted lgkmcnt tied to the registers it guards (as
+// csrc/noise_mlp.hip does), so no MFMA is scheduled above it.
 template <int OFF>
 __device__ __forceinline__ h16x8 dma_read(uint32_t addr) {
   h16x8 v;
   asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(v) : "v"(addr), "i"(OFF));
   return v;
-}
-template <int N>
-__device__ __forceinline__ void dma_wait4(h16x8& a, h16x8& b, h16x8& c, h16x8& d) {
-  asm volatile("s_waitcnt lgkmcnt(%4)" : "+v"(a), "+v"(b), "+v"(c), "+v"(d) : "n"(N));
-}
-
-// lane byte offsets of the four fragment rows/chunks within a stage (see dma_lane_offsets)
-struct DmaLane {
-  uint32_t a0, a1, b0, b1;  // A / B image, k-step 0 / 1 (t = 1 is +2048 immediate)
-};
-
-__device__ __forceinline__ DmaLane dma_lane_offsets(int wr, int wc, int l32, int h) {
-  const int sw = (l32 >> 2) & 3;
-  const uint32_t p0 = (uint32_t)(((h) ^ sw) * 16), p1 = (uint32_t)(((2 + h) ^ sw) * 16);
-  const uint32_t ra = (uint32_t)((wr * 64 + l32) * 64), rb = (uint32_t)(kXT * kDK * 2 + (wc * 64 + l32) * 64);
-  return DmaLane{ra + p0, ra + p1, rb + p0, rb + p1};
-}
-
-__device__ __forceinline__ void dma_mma(const char* stage, const DmaLane& ln, f32x16 (&acc)[2][2]) {
-  const uint32_t base = (uint32_t)(uintptr_t)stage;
-  h16x8 a0 = dma_read<0>(base + ln.a0), a1 = dma_read<2048>(base + ln.a0);
-  h16x8 b0 = dma_read<0>(base + ln.b0), b1 = dma_read<2048>(base + ln.b0);
-  h16x8 c0 = dma_read<0>(base + ln.a1), c1 = dma_read<2048>(base + ln.a1);
-  h16x8 d0 = dma_read<0>(base + ln.b1), d1 = dma_read<2048>(base + ln.b1);
-  dma_wait4<4>(a0, a1, b0, b1);
-  acc[0][0] = mfma32_h16(a0, b0, acc[0][0]);
-  acc[0][1] = mfma32_h16(a0, b1, acc[0][1]);
-  acc[1][0] = mfma32_h16(a1, b0, acc[1][0]);
-  acc[1][1] = mfma32_h16(a1, b1, acc[1][1]);
-  __builtin_amdgcn_sched_barrier(0);  // k-step 0's MFMAs stay above k-step 1's wait
-  dma_wait4<0>(c0, c1, d0, d1);
-  acc[0][0] = mfma32_h16(c0, d0, acc[0][0]);
-  acc[0][1] = mfma32_h16(c0, d1, acc[0][1]);
-  acc[1][0] = mfma32_h16(c1, d0, acc[1][0]);
-  acc[1][1] = mfma32_h16(c1, d1, acc[1][1]);
-}
-
-template <int S>
-__device__ __forceinline__ void vm_barrier() {  // this wave's slice k landed, then all waves
-  if (S == 4)
-    asm volatile("s_waitcnt vmcnt(8)\n\ts_barrier" ::: "memory");
-  else
-    asm volatile("s_waitcnt vmcnt(4)\n\ts_barrier" ::: "memory");
-}
-
-template <int EP, int S>
-__global__ __launch_bounds__(256) void gemm_dma_kernel(const uint16_t* __restrict__ A, int64_t M,
-                                                       int K, const uint16_t* __restrict__ B, int O,
-                                                       int tiles_o, int ntiles, int per_xcd,
-                                                       GemmExArgs args) {
-  static_assert(S == 3 || S == 4, "3 or 4 stages");
-  __shared__ __attribute__((aligned(16))) char st0[kDStageAlloc];
-  __shared__ __attribute__((aligned(16))) char st1[kDStageAlloc];
-  __shared__ __attribute__((aligned(16))) char st2[kDStageAlloc];
-  __shared__ __attribute__((aligned(16))) char st3[S == 4 ? kDStageAlloc : 16];
-  const int L = blockIdx.x;
-  const int t = (L & 7) * per_xcd + (L >> 3);
-  if (t >= ntiles) return;
-  const int64_t m0 = (int64_t)(t / tiles_o) * kXT;
-  const int o0 = (t % tiles_o) * kXT;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wr = wid >> 1, wc = wid & 1, h = lane >> 5, l32 = lane & 31;
-  f32x16 acc[2][2];
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j) acc[i][j] = f32x16{};
-  const rsrc_t ra = make_rsrc(A, (uint32_t)(M * K * 2));
-  const rsrc_t rb = make_rsrc(B, (uint32_t)((int64_t)O * K * 2));
-  // lane -> (row within its 16-row piece, logical chunk); the piece is rows 32 wid + 16 i
-  const int pr = lane >> 2, pc = (lane & 3) ^ ((lane >> 4) & 3);
-  const int r0 = 32 * wid + pr;
-  const uint32_t va0 = (uint32_t)(((m0 + r0) * K + 8 * pc) * 2);
-  const uint32_t va1 = (uint32_t)(((m0 + r0 + 16) * K + 8 * pc) * 2);
-  const uint32_t vb0 = (uint32_t)((((int64_t)o0 + r0) * K + 8 * pc) * 2);
-  const uint32_t vb1 = (uint32_t)((((int64_t)o0 + r0 + 16) * K + 8 * pc) * 2);
-  const int nk = K / kDK;
-  char* stages[4] = {st0, st1, st2, st3};
-  const DmaLane ln = dma_lane_offsets(wr, wc, l32, h);
-#pragma unroll
-  for (int q = 0; q < S - 1; ++q) dma_slice(ra, rb, va0, va1, vb0, vb1, q * kDK * 2, stages[q], wid);
-  for (int k = 0; k < nk; k += S) {
-#pragma unroll
-    for (int q = 0; q < S; ++q) {
-      if (k + q < nk) {
-        vm_barrier<S>();
-        // slice k+q+S-1 into the stage read one step ago (every wave is past that read);
-        // slices past K read unused rows or buffer-bound zeros
-        dma_slice(ra, rb, va0, va1, vb0, vb1, (uint32_t)((k + q + S - 1) * kDK * 2),
-                  stages[(q + S - 1) % S], wid);
-        dma_mma(stages[q], ln, acc);
-      }
-    }
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the look-ahead DMAs landed
-  __syncthreads();
-  gemm_epilogue_fast<EP, 4>(acc, reinterpret_cast<float (*)[kCLd]>(st0), M, O, m0, o0, args);
 }
 
 // ---- Dropout backward: dD = bf16(g * keep * s), 4 elements per thread (n % 4 == 0)
@@ -784,13 +638,7 @@ __global__ void dropout_grad_kernel(const float4* __restrict__ g, int64_t n4, ui
 }
 
 // ---- weight gradient with transposed LDS reads
-#ifndef PCST_WGRAD_WS  // experiment builds may override (32 or 64)
-#define PCST_WGRAD_WS 32
-#endif
-constexpr int kWS = PCST_WGRAD_WS;      // m rows per slice
-#ifndef PCST_WGRAD_PF  // experiment builds: 2 = two slices in flight (two register stages)
-#define PCST_WGRAD_PF 1
-#endif
+constexpr int kWS = 32;                 // m rows per slice
 constexpr int kWLdB = 2 * kXT + 64;     // LDS row bytes: 256 + 64 (row stride = 64 mod 256 B)
 
 // slice rows [m, m+32) x columns [c0, c0+128) of a row-major [*, Cn] matrix -> bf16 LDS image
@@ -905,13 +753,7 @@ __device__ __forceinline__ h16x8 tr_frag(const char* img, int c, int k, int lane
 // BUF (operands < 2 GiB): branch-free buffer loads, kWPF slices in flight in registers, the LDS
 // image double-buffered with one barrier per slice (slice s + 1 is stored after slice s's
 // barrier, beside slice s's MFMAs).  !BUF: the pointer loads, one slice ahead, two barriers.
-#ifndef PCST_WGRAD_BPF
-#define PCST_WGRAD_BPF 3
-#endif
-#ifndef PCST_X_WGRAD_BUF  // 0: the pointer-load kernel only (A/B)
-#define PCST_X_WGRAD_BUF 1
-#endif
-constexpr int kWPF = PCST_WGRAD_BPF;
+constexpr int kWPF = 3;
 template <typename TZ, typename TX, bool BUF = false>
 __global__ __launch_bounds__(256) void wgrad_ex_kernel(const TZ* __restrict__ dZ,
                                                        const TX* __restrict__ X, int64_t M, int I,
@@ -994,34 +836,6 @@ __global__ __launch_bounds__(256) void wgrad_ex_kernel(const TZ* __restrict__ dZ
   WStage<TX> gx;
   gz.load(dZ, me, O, mb, o0, tid);
   gx.load(X, me, I, mb, i0, tid);
-#if PCST_WGRAD_PF == 2
-  // two slices in flight: the register stages alternate, each loaded two slices ahead
-  WStage<TZ> gz1;
-  WStage<TX> gx1;
-  gz1.load(dZ, me, O, mb + kWS, o0, tid);
-  gx1.load(X, me, I, mb + kWS, i0, tid);
-  for (int64_t k0 = mb; k0 < me; k0 += 2 * kWS) {
-    gz.store(Zs, tid, bias ? csum : nullptr);
-    gx.store(Xs, tid, nullptr);
-    __syncthreads();
-    if (k0 + 2 * kWS < me) {
-      gz.load(dZ, me, O, k0 + 2 * kWS, o0, tid);
-      gx.load(X, me, I, k0 + 2 * kWS, i0, tid);
-    }
-    mma(Zs, Xs);
-    __syncthreads();
-    // the odd slice (rows past me in the last one load as zeros: the MFMAs add nothing)
-    gz1.store(Zs, tid, bias ? csum : nullptr);
-    gx1.store(Xs, tid, nullptr);
-    __syncthreads();
-    if (k0 + 3 * kWS < me) {
-      gz1.load(dZ, me, O, k0 + 3 * kWS, o0, tid);
-      gx1.load(X, me, I, k0 + 3 * kWS, i0, tid);
-    }
-    mma(Zs, Xs);
-    __syncthreads();
-  }
-#else
   for (int64_t k0 = mb; k0 < me; k0 += kWS) {
     gz.store(Zs, tid, bias ? csum : nullptr);
     gx.store(Xs, tid, nullptr);
@@ -1033,7 +847,6 @@ __global__ __launch_bounds__(256) void wgrad_ex_kernel(const TZ* __restrict__ dZ
     mma(Zs, Xs);
     __syncthreads();
   }
-#endif
   }
   float* pw = partW + (int64_t)chunk * O * I;
 #pragma unroll
@@ -1112,10 +925,7 @@ __global__ __launch_bounds__(256) void wgrad_ex_combine_kernel(
   }
 }
 
-// workgroups of one weight-gradient launch (experiment builds: XDEF=-DPCST_X_WGRAD_WG=N)
-#ifndef PCST_X_WGRAD_WG
-#define PCST_X_WGRAD_WG 512
-#endif
+constexpr int kWgradWG = 512;  // work-groups of one weight-gradient launch
 
 struct WgradExPlan {
   int tiles_i, tiles_o, ntile, chunks, total, per_xcd;
@@ -1127,7 +937,7 @@ static WgradExPlan wgrad_ex_plan(int64_t M, int64_t I, int64_t O) {
   p.tiles_i = (int)cdiv(I, kXT);
   p.tiles_o = (int)cdiv(O, kXT);
   p.ntile = p.tiles_i * p.tiles_o;
-  int64_t chunks = cdiv(PCST_X_WGRAD_WG, p.ntile);  // ~2 workgroups per CU
+  int64_t chunks = cdiv(kWgradWG, p.ntile);  // ~2 workgroups per CU
   chunks = std::max<int64_t>(1, std::min<int64_t>(chunks, cdiv(M, 512)));
   p.rows_per_chunk = cdiv(cdiv(M, chunks), kWS) * kWS;
   p.chunks = (int)cdiv(M, p.rows_per_chunk);
@@ -1171,39 +981,6 @@ static void launch_gemm_ex(int ep, const void* A, int64_t M, int64_t K, const vo
     hipLaunchKernelGGL((gemm_bf_kernel<EPV, false>), dim3((unsigned)(8 * per)), dim3(256), 0, s,    \
                        static_cast<const uint16_t*>(A), M, (int)K, static_cast<const uint16_t*>(B),  \
                        (int)O, tiles_o, ntiles, per, args)
-
-#define PCST_GEMM_DMA(EPV)                                                                         \
-  if (stages == 3)                                                                                 \
-    hipLaunchKernelGGL((gemm_dma_kernel<EPV, 3>), dim3((unsigned)(8 * per)), dim3(256), 0, s,       \
-                       static_cast<const uint16_t*>(A), M, (int)K, static_cast<const uint16_t*>(B),  \
-                       (int)O, tiles_o, ntiles, per, args);                                          \
-  else                                                                                             \
-    hipLaunchKernelGGL((gemm_dma_kernel<EPV, 4>), dim3((unsigned)(8 * per)), dim3(256), 0, s,       \
-                       static_cast<const uint16_t*>(A), M, (int)K, static_cast<const uint16_t*>(B),  \
-                       (int)O, tiles_o, ntiles, per, args)
-
-static void launch_gemm_dma(int ep, int stages, const void* A, int64_t M, int64_t K, const void* B,
-                            int64_t O, int tiles_o, int ntiles, int per, const GemmExArgs& args,
-                            hipStream_t s) {
-  switch (ep) {
-    case EP_F32: PCST_GEMM_DMA(EP_F32); break;
-    case EP_BF16: PCST_GEMM_DMA(EP_BF16); break;
-    case EP_RESID_DROP: PCST_GEMM_DMA(EP_RESID_DROP); break;
-    case EP_RELU_MASK: PCST_GEMM_DMA(EP_RELU_MASK); break;
-    case EP_RESID_DROP16: PCST_GEMM_DMA(EP_RESID_DROP16); break;
-    case EP_ADD16: PCST_GEMM_DMA(EP_ADD16); break;
-    default: PCST_GEMM_DMA(EP_ADD); break;
-  }
-}
-#undef PCST_GEMM_DMA
-
-// bf16 kernel choice (experiment builds: XDEF=-DPCST_X_GEMM_KERNEL=3|4 selects the LDS-DMA
-// kernel with that many stages; 0 = register staging, measured 140 us vs DMA 146 (3) / 173 (4)
-// at K = 256)
-#ifndef PCST_X_GEMM_KERNEL
-#define PCST_X_GEMM_KERNEL 0
-#endif
-static constexpr int gemm_kernel_choice() { return PCST_X_GEMM_KERNEL; }
 
 static void launch_gemm_bf(int ep, bool fast, const void* A, int64_t M, int64_t K, const void* B,
                            int64_t O, int tiles_o, int ntiles, int per, const GemmExArgs& args,
@@ -1260,11 +1037,9 @@ int gemm_ex_impl(const void* A, int a_bf16, int64_t M, int64_t K, const void* B,
   const int64_t lim = 1ll << 31;
   if (a_bf16 && b_bf16 && K % kBK == 0 && M * K * 2 < lim && O * K * 2 < lim) {
     const bool fast = O % kXT == 0 && epilogue != EP_COND && M * O * 4 < lim;
-    const int choice = gemm_kernel_choice();
-    if (fast && K % kDK == 0 && (choice == 3 || choice == 4))
-      launch_gemm_dma(epilogue, choice, A, M, K, B, O, tiles_o, ntiles, per, args, s);
-    else
-      launch_gemm_bf(epilogue, fast, A, M, K, B, O, tiles_o, ntiles, per, args, s);
+    // register staging (round 4: 140 us at K = 256 against 146 / 173 for an LDS-DMA kernel with
+    // three / four stages, since removed)
+    launch_gemm_bf(epilogue, fast, A, M, K, B, O, tiles_o, ntiles, per, args, s);
   } else if (a_bf16 && b_bf16)
     launch_gemm_ex<uint16_t, uint16_t>(epilogue, A, M, K, B, O, tiles_o, ntiles, per, args, s);
   else if (a_bf16)
@@ -1318,7 +1093,7 @@ int wgrad_ex_impl(const void* dZ, int dz_bf16, const void* X, int x_bf16, int64_
   const int64_t lim = 1ll << 31;
 #define PCST_WGRAD_EX(TZ, TX)                                                                     \
   do {                                                                                            \
-  if (PCST_X_WGRAD_BUF && M * O * (int64_t)sizeof(TZ) < lim && M * I * (int64_t)sizeof(TX) < lim) \
+  if (M * O * (int64_t)sizeof(TZ) < lim && M * I * (int64_t)sizeof(TX) < lim) \
     hipLaunchKernelGGL((wgrad_ex_kernel<TZ, TX, true>), grid, dim3(256), 0, s,                     \
                        static_cast<const TZ*>(dZ), static_cast<const TX*>(X), M, (int)I, (int)O,  \
                        p.rows_per_chunk, p.tiles_i, p.ntile, p.total, p.per_xcd, partW, partB);   \
@@ -1357,10 +1132,7 @@ int wgrad_ex_impl(const void* dZ, int dz_bf16, const void* X, int x_bf16, int64_
 // 512 threads = 8 waves, wave (wr, wc) = (w & 3, w >> 2): rows [32 wr, +32) x cols [64 wc, +64) of
 // each 128 x 128 output tile.  The weights stream through a double-buffered 64-deep B slice:
 // per chunk 4 slices of W1 (K = 256) then 2 x 2 slices of W2 (the two output halves, K = 128).
-#ifndef PCST_RB_TILE  // rows per tile: 128 (512 threads, 64-deep weight slices, one work-group
-#define PCST_RB_TILE 128  // per CU) or 64 (256 threads, 32-deep slices, two work-groups per CU)
-#endif
-constexpr int kRbRows = PCST_RB_TILE;
+constexpr int kRbRows = 128;   // rows per tile (512 threads, 64-deep weight slices, one work-group per CU)
 constexpr int kRbThreads = kRbRows * 4;          // (rows / 32) x 2 waves
 constexpr int kRbNWR = kRbRows / 32;             // wave rows
 constexpr int kRbK = kRbRows == 128 ? 64 : 32;   // weight slice depth
@@ -1368,10 +1140,7 @@ constexpr int kRbW1S = 256 / kRbK;               // first-product slices per hid
 constexpr int kRbW2S = 128 / kRbK;               // second-product slices per output half (K = 128)
 constexpr int kRbSPC = kRbW1S + 2 * kRbW2S;      // slices per chunk
 constexpr int kRbSlices = 4 * kRbSPC;
-#ifndef PCST_RB_PF  // experiment builds: weight slices in flight (1, 2 or 4; divides 32)
-#define PCST_RB_PF 4
-#endif
-constexpr int kRbPF = PCST_RB_PF;
+constexpr int kRbPF = 4;       // weight slices in flight (round 4: 1 / 2 / 4 = 12.15 / 11.94 / 11.94 ms)
 static_assert(kRbSlices % kRbPF == 0, "kRbPF must divide the slice count");
 constexpr int kRbBLd = kRbK + 8;         // B image row (16-bit elements): 144 B, conflict-free
 constexpr int kRbXLd = 256 + 8;          // x tile row: 528 B
@@ -1648,8 +1417,8 @@ __global__ __launch_bounds__(kRbThreads) __attribute__((amdgpu_waves_per_eu(2, 2
   }
 }
 
-// ---- fused residual block, version 2 (the forward's default, PCST_RB_V2_FWD; the backward's with
-// PCST_RB_V2_BWD=1, slower there -- DESIGN.md §6a; bit-identical to the kernel above and to
+// ---- fused residual block, version 2 (the forward's kernel; its backward direction is slower than
+// the kernel above -- DESIGN.md §6a; bit-identical to the kernel above and to
 // gemm_ex): one
 // wave per SIMD, each wave keeping its 64 rows' A operand (x / dD, 64 x 256) in registers for the
 // whole block, so the MFMAs read only weight fragments from LDS (one 1 KiB fragment feeds two
@@ -1663,30 +1432,8 @@ __global__ __launch_bounds__(kRbThreads) __attribute__((amdgpu_waves_per_eu(2, 2
 // weights stream per 32-unit hidden chunk (32 fragments, 32 KiB: W1 rows [32c, +32) x K 256 and
 // W2 rows 0..255 x k [32c, +32)) straight into LDS (global_load_lds from the row-major weights,
 // 16 B per lane), double-buffered, one barrier per chunk.
-#ifndef PCST_RB_V2  // 1: both directions on version 2 (experiment builds)
-#define PCST_RB_V2 0
-#endif
-#ifndef PCST_RB_V2_FWD  // the forward on version 2: 245 vs 274 us at M = 245760 (a31)
-#define PCST_RB_V2_FWD 1
-#endif
-#ifndef PCST_RB_V2_BWD  // the backward stays on the kernel above: 385 vs 337 us (HBM-write bound)
-#define PCST_RB_V2_BWD PCST_RB_V2
-#endif
-#ifndef PCST_X_RB2_EPI_PREFETCH  // the next tile's A rows loaded block by block in the final
-#define PCST_X_RB2_EPI_PREFETCH 0  // epilogue (1) or after it (0)
-#endif
-#ifndef PCST_X_RB2_NOFILL  // timing experiments only: no weight refills (wrong results)
-#define PCST_X_RB2_NOFILL 0
-#endif
-#ifndef PCST_X_RB2_NOHASH  // timing experiments only: no dropout draws (wrong results)
-#define PCST_X_RB2_NOHASH 0
-#endif
-#ifndef PCST_X_RB2_NOSTORE  // timing experiments only: the chunk h / dZ stores left out
-#define PCST_X_RB2_NOSTORE 0
-#endif
-#ifndef PCST_X_RB2_STAMPS  // timing probe builds only: wave 0 of tiles 0 and ntiles / 2 writes
-#define PCST_X_RB2_STAMPS 0  // s_memtime stamps over its first h row (tools/rb_probe.py)
-#endif
+// The forward runs on this kernel (245 vs 274 us at M = 245760, r04 a31); the backward on the
+// kernel above (385 vs 337 us here: it is HBM-write bound).
 constexpr int kR2Rows = 256;               // rows per work-group tile
 constexpr int kR2Slab = 32 * 1024;         // one hidden chunk's fragments
 constexpr int kR2Keep = 8 * 256 * 4;       // dropout keep bits: [8 output blocks][256 lanes] words
@@ -1793,15 +1540,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   // the dropout draws are made in the loop whether or not the backward writes its dropout copy:
   // a run-time condition there would cut the loop body into blocks the scheduler cannot
   // interleave with the MFMAs (measured: the backward 88 us slower with it)
-  const bool drop = !PCST_X_RB2_NOHASH;
+  const bool drop = true;
   const bool ddo = BWD && a.ddo != nullptr;  // backward: the dropout copy is written
-#if PCST_X_RB2_STAMPS
-  uint64_t stamp[24];
-  stamp[0] = __builtin_amdgcn_s_memtime();
-#define R2_STAMP(i) stamp[i] = __builtin_amdgcn_s_memtime()
-#else
-#define R2_STAMP(i) (void)0
-#endif
   if (!BWD) {
     sb1[tid] = a.b1[tid];
     sb1[256 + tid] = a.b1[256 + tid];
@@ -1861,7 +1601,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   const uint32_t lkeep = (uint32_t)(uintptr_t)skeep + 4 * tid;  // + 1024 ob bytes
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();  // slab 0 and the biases landed
-  R2_STAMP(1);
   int gc = 0;  // chunks done by this work-group
   int slab0 = 0, slab2 = 2;  // the running chunk's slab, the slab chunk gc + 2 loads into
 #pragma unroll 1
@@ -1904,7 +1643,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       // the chunk after next (this tile's c + 2 or the next tile's: the same weights) into the
       // slab chunk gc - 1 used
       const bool fill2 = c + 2 < 16 || more;
-      if (fill2 && !PCST_X_RB2_NOFILL) fill((c + 2) & 15, slab2);
+      if (fill2) fill((c + 2) & 15, slab2);
       // the chunk's 32 fragments in order: f < 16 the first product (acc1[p] += W1[32c.., 16f..]
       // x^T, k ascending), f >= 16 the second (acc2[ob][p] += W2[32ob.., 32c + 16kk ..] h^T, f =
       // 16 + 2 ob + kk); a ring of four reads in flight, the wait for fragment f counted over the
@@ -1953,9 +1692,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
             };
 #pragma unroll
       for (int f = 0; f < 16; ++f) frag_step(f);
-#if PCST_X_RB2_STAMPS
-        if (c == 9 && gc < 16) R2_STAMP(7);
-#endif
         // epilogue: forward h = 16-bit(relu(acc1 + b1)), backward dZ = 16-bit((acc1 + 0)
         // [h > 0]); to the second product's operand layout and out to global (16 B per lane)
         if (!BWD) asm volatile("s_waitcnt lgkmcnt(4)" : "+v"(bq[0]), "+v"(bq[1]), "+v"(bq[2]), "+v"(bq[3]));
@@ -1987,7 +1723,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
               }
             }
             hb[p][kk] = relayout(o);
-            if (!PCST_X_RB2_NOSTORE)
+            if (true)
               __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i32, hb[p][kk]), rh,
                                                      (int)(v512 + p * 32768 + kk * 32), 64 * c, 0);
           }
@@ -2002,14 +1738,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
                                                   4 * c, 0);
           }
         }
-#if PCST_X_RB2_STAMPS
-        if (c == 9 && gc < 16) R2_STAMP(8);
-#endif
 #pragma unroll
       for (int f = 16; f < 32; ++f) frag_step(f);
-#if PCST_X_RB2_STAMPS
-      if (c == 9 && gc < 16) R2_STAMP(9);
-#endif
       if (drop && (c & 1)) r2_write_u32(lkeep + 1024 * (c >> 1), keep2);
       // this wave's DMA of the next chunk (issued a chunk ago) and backward its mask rows landed;
       // the chunk-after-next DMA (8) and this chunk's h stores (4) may still be in flight
@@ -2022,20 +1752,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         if (fill2) asm volatile("s_waitcnt vmcnt(14)" ::: "memory");
         else asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
       }
-#if PCST_X_RB2_STAMPS
-      if (c == 9 && gc < 16) R2_STAMP(10);
-#endif
       __syncthreads();  // every wave's DMA of chunk gc + 1 landed; every wave is done with slab0
       slab0 = slab0 == kR2Slabs - 1 ? 0 : slab0 + 1;
       slab2 = slab2 == kR2Slabs - 1 ? 0 : slab2 + 1;
-#if PCST_X_RB2_STAMPS
-      if (gc == 0) R2_STAMP(2);
-      if (gc == 1) R2_STAMP(3);
-      if (gc == 7) R2_STAMP(4);
-      if (gc == 15) R2_STAMP(5);
-      if (gc == 9) R2_STAMP(11);
-      if (gc == 8) R2_STAMP(12);
-#endif
     }
     // final epilogue: forward x' = 16-bit(x + Dropout(acc2 + b2)); backward g' = 16-bit((acc2 +
     // 0) + g) and the dropout copy dD' = 16-bit(g' keep / (1 - p)); 16 B stores in operand
@@ -2108,19 +1827,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
           }
         }
       }
-#if PCST_X_RB2_EPI_PREFETCH
-      // not above this block's stores: the residual registers are free only after them
-      asm volatile("" ::: "memory");
-      if (more) {  // the next tile's A rows, k [32 ob, +32)
-#pragma unroll
-        for (int p = 0; p < 2; ++p)
-#pragma unroll
-          for (int kk = 0; kk < 2; ++kk)
-            xb[p][2 * ob + kk] = as_u32x4(bload16(rx, v256 + vstep256 + p * 16384 + ob * 64 + kk * 32, 0));
-      }
-#endif
     }
-#if !PCST_X_RB2_EPI_PREFETCH
     if (more) {  // the next tile's A rows
 #pragma unroll
       for (int p = 0; p < 2; ++p)
@@ -2128,10 +1835,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         for (int kb = 0; kb < 16; ++kb)
           xb[p][kb] = as_u32x4(bload16(rx, v256 + vstep256 + p * 16384 + kb * 32, 0));
     }
-#endif
-#if PCST_X_RB2_STAMPS
-    if (gc == 16) R2_STAMP(13);
-#endif
     if (!more) break;
     t += G;
     r0 += (int64_t)G * kR2Rows;
@@ -2139,17 +1842,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     v512 += vstep512;
     vrow16 += (uint32_t)G * kR2Rows * 64;
   }
-#if PCST_X_RB2_STAMPS
-  R2_STAMP(6);
-  if (wid == 0 && lane == 0) {
-    uint64_t* o = reinterpret_cast<uint64_t*>(a.h + (int64_t)blockIdx.x * kR2Rows * 512);
-#pragma unroll
-    for (int i = 0; i < 7; ++i) o[i] = stamp[i];
-    o[7] = (uint64_t)blockIdx.x;
-#pragma unroll
-    for (int i = 7; i < 14; ++i) o[i + 1] = stamp[i];
-  }
-#endif
 }
 
 // ---- batched weight casts: every 2-D weight of a step to the 16-bit format (optionally
@@ -2208,7 +1900,6 @@ int resblock_fwd_impl(const uint16_t* x, int64_t M, const uint16_t* w1, const fl
                       const uint16_t* w2, const float* b2, uint64_t seed, float drop_p,
                       uint16_t* h, uint16_t* xo, uint32_t* hbits, void* stream) {
   PCST_CHECK_ARG(M >= 0 && M * 512 * 2 < (1ll << 31), "resblock_fwd: bad M");
-  PCST_CHECK_ARG(hbits == nullptr || PCST_RB_V2_FWD, "resblock_fwd: hbits needs the v2 forward kernel");
   PCST_CHECK_ARG(drop_p >= 0.0f && drop_p < 1.0f, "resblock_fwd: dropout p must be in [0, 1)");
   if (M == 0) return PCST_OK;
   PCST_CHECK_ARG(x && w1 && b1 && w2 && b2 && h && xo, "resblock_fwd: null pointer");
@@ -2223,15 +1914,9 @@ int resblock_fwd_impl(const uint16_t* x, int64_t M, const uint16_t* w1, const fl
   a.scale = 1.0f / (1.0f - drop_p);
   a.hm = nullptr; a.g = nullptr; a.ddo = nullptr;
   a.hbo = hbits; a.hbi = nullptr;
-  if (PCST_RB_V2_FWD) {
-    const int ntiles = (int)cdiv(M, kR2Rows);
-    hipLaunchKernelGGL(resblock2_kernel<false>, dim3((unsigned)std::min(ntiles, r2_grid())), dim3(256),
-                       kR2Lds, as_stream(stream), a, ntiles);
-  } else {
-    const int ntiles = (int)cdiv(M, kRbRows), per = (int)cdiv(ntiles, 8);
-    hipLaunchKernelGGL(resblock_kernel<false>, dim3((unsigned)(8 * per)), dim3(kRbThreads), kRbLds,
-                       as_stream(stream), a, per, ntiles);
-  }
+  const int ntiles = (int)cdiv(M, kR2Rows);
+  hipLaunchKernelGGL(resblock2_kernel<false>, dim3((unsigned)std::min(ntiles, r2_grid())), dim3(256),
+                     kR2Lds, as_stream(stream), a, ntiles);
   PCST_LAUNCH_CHECK("resblock_fwd");
   return PCST_OK;
 }
@@ -2244,7 +1929,6 @@ int resblock_bwd_impl(const uint16_t* dd, int64_t M, const uint16_t* w2t, const 
   PCST_CHECK_ARG(drop_p >= 0.0f && drop_p < 1.0f, "resblock_bwd: dropout p must be in [0, 1)");
   if (M == 0) return PCST_OK;
   PCST_CHECK_ARG(dd && w2t && w1t && (h || hbits) && g && dz && g_out, "resblock_bwd: null pointer");
-  PCST_CHECK_ARG(hbits == nullptr || !PCST_RB_V2_BWD, "resblock_bwd: hbits needs the round-3 backward kernel");
   PCST_CHECK_ARG(((uintptr_t)hbits % 4) == 0, "resblock_bwd: hbits must be 4-byte aligned");
   PCST_CHECK_ARG(((uintptr_t)dd | (uintptr_t)w2t | (uintptr_t)w1t | (uintptr_t)h | (uintptr_t)g |
                   (uintptr_t)dz | (uintptr_t)g_out | (uintptr_t)dd_out) % 16 == 0,
@@ -2258,19 +1942,13 @@ int resblock_bwd_impl(const uint16_t* dd, int64_t M, const uint16_t* w2t, const 
   a.seed_hi = (uint32_t)(seed >> 32);
   a.thr = drop_threshold(drop_p);
   a.scale = 1.0f / (1.0f - drop_p);
-  if (PCST_RB_V2_BWD) {
-    const int ntiles = (int)cdiv(M, kR2Rows);
-    hipLaunchKernelGGL(resblock2_kernel<true>, dim3((unsigned)std::min(ntiles, r2_grid())), dim3(256),
-                       kR2Lds, as_stream(stream), a, ntiles);
-  } else {
-    const int ntiles = (int)cdiv(M, kRbRows), per = (int)cdiv(ntiles, 8);
-    if (hbits)
-      hipLaunchKernelGGL((resblock_kernel<true, true>), dim3((unsigned)(8 * per)), dim3(kRbThreads), kRbLds,
-                         as_stream(stream), a, per, ntiles);
-    else
-      hipLaunchKernelGGL(resblock_kernel<true>, dim3((unsigned)(8 * per)), dim3(kRbThreads), kRbLds,
-                         as_stream(stream), a, per, ntiles);
-  }
+  const int ntiles = (int)cdiv(M, kRbRows), per = (int)cdiv(ntiles, 8);
+  if (hbits)
+    hipLaunchKernelGGL((resblock_kernel<true, true>), dim3((unsigned)(8 * per)), dim3(kRbThreads), kRbLds,
+                       as_stream(stream), a, per, ntiles);
+  else
+    hipLaunchKernelGGL(resblock_kernel<true>, dim3((unsigned)(8 * per)), dim3(kRbThreads), kRbLds,
+                       as_stream(stream), a, per, ntiles);
   PCST_LAUNCH_CHECK("resblock_bwd");
   return PCST_OK;
 }

@@ -564,7 +564,12 @@ __global__ __launch_bounds__(256) void voxf_insert_kernel(const float* __restric
                                                           int32_t* __restrict__ cnt4,
                                                           int32_t* __restrict__ vlist, int pack,
                                                           int sshift, const float* __restrict__ pmm,
-                                                          int npm, int pool_made) {
+                                                          int npm, int pool_made,
+                                                          uint32_t* __restrict__ sflag, uint32_t svalue) {
+  // the start signal: every launch ahead of this one on its stream has completed (the points are
+  // final), published for another stream (pcst_voxel_downsample_copies_prepped's start_flag)
+  if (sflag && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0)
+    __hip_atomic_store(sflag, svalue, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const int nbins = 1 << (32 - sshift);
   // Each workgroup first aggregates its kVoxChunk points in an LDS table (LDS atomics), then
   // publishes one global (sum, count) per distinct voxel: dense voxels see at most one global
@@ -886,7 +891,8 @@ static size_t vox_zero_bytes(const VoxelFastWS& w, int64_t rows) {
 
 static int voxel_fast(const float* pts, int64_t B, int64_t N, int64_t copies, int64_t T,
                       void* workspace, uint64_t seed, const uint64_t* seed_p, int64_t* out_idx,
-                      float* out_pts, hipStream_t s, bool prepped = false, bool pool = false) {
+                      float* out_pts, hipStream_t s, bool prepped = false, bool pool = false,
+                      uint32_t* sflag = nullptr, uint32_t svalue = 0) {
   VoxelFastWS w = carve_voxel_fast(workspace, B, N, copies);
   const int b = (int)B, n = (int)N, rows = (int)(B * copies);
   if (!prepped)  // (a prepped call: pcst_cfg_ddim_voxel_prep made the partials and zeroed)
@@ -899,7 +905,8 @@ static int voxel_fast(const float* pts, int64_t B, int64_t N, int64_t copies, in
   PCST_CHECK_ARG((1 << (32 - sshift)) <= 2 * kVoxLds, "voxel_downsample: cloud too large for this build");
   hipLaunchKernelGGL(voxf_insert_kernel, dim3((unsigned)cdiv(N, kVoxChunk), b), dim3(256), 0, s,
                      pts, n, w.mm, T, w.H, w.tkey, w.tsum, w.tcnt, b, cp, seed, seed_p, w.hist, w.cnt4,
-                     w.vlist, pack, sshift, prepped ? w.pmm : nullptr, vox_prep_blocks(N), pool ? 1 : 0);
+                     w.vlist, pack, sshift, prepped ? w.pmm : nullptr, vox_prep_blocks(N), pool ? 1 : 0,
+                     sflag, svalue);
   uint32_t* hist = pool ? w.phist : w.hist;  // the pool histogram: made ahead, or by the insert
   hipLaunchKernelGGL(voxf_reps_kernel, dim3((unsigned)std::min<int64_t>(cdiv(N, 256), kVoxRepsBlocks), b),
                      dim3(256), 0, s, w.tkey, w.tsum, w.tcnt, w.H, n, w.cnt4, w.vlist, pack, w.reps,
@@ -1031,13 +1038,14 @@ extern "C" int pcst_voxel_downsample_copies(const float* pts, int64_t B, int64_t
 extern "C" int pcst_voxel_downsample_copies_prepped(const float* pts, int64_t B, int64_t N,
                                                     int64_t copies, int64_t target, void* workspace,
                                                     uint64_t seed, int pool, int64_t* out_idx,
-                                                    float* out_pts, void* stream) {
+                                                    float* out_pts, uint32_t* start_flag,
+                                                    uint32_t start_value, void* stream) {
   PCST_CHECK_ARG(B > 0 && copies >= 1 && B * copies < (1 << 15) && N > target && target > 0 &&
                      N < (1ll << 30),
                  "voxel_downsample_copies_prepped: bad shape");
   PCST_CHECK_ARG(pts && workspace && out_idx && out_pts, "voxel_downsample_copies_prepped: null pointer");
   return voxel_fast(pts, B, N, copies, target, workspace, seed, nullptr, out_idx, out_pts,
-                    as_stream(stream), true, pool != 0);
+                    as_stream(stream), true, pool != 0, start_flag, start_value);
 }
 
 extern "C" int pcst_cfg_ddim_voxel_prep(const float* x, const float* eps, const float* source,

@@ -101,6 +101,16 @@ def _draw_seed(p):
     return int(torch.randint(0, 2 ** 62, (1,)).item()) if p > 0 else 0
 
 
+# Rows the fused residual-block kernels take: they address the [M, 512] 16-bit hidden
+# activations with 32-bit byte offsets (pcst_resblock_fwd16 / _bwd16 reject M * 1024 >= 2^31);
+# larger batches take the two-GEMM path (bit-identical), which has no such limit.
+FUSED_BLOCK_MAX_ROWS = (2 ** 31 - 1) // 1024
+
+
+def fused_block_rows_ok(M: int) -> bool:
+    return M <= FUSED_BLOCK_MAX_ROWS
+
+
 def _block_fwd(x, xb, w1, b1, w2, b2, p, seed):
     """x + Dropout_p(Linear2(ReLU(Linear1(x)))): -> (y fp32, y 16-bit, h 16-bit); the 16-bit
     format is that of xb / w1 / w2."""
@@ -239,7 +249,8 @@ class NoisePredictorFn(torch.autograd.Function):
             seed = _draw_seed(ps[k])
             seeds.append(seed)
             saved.append(xb)
-            if r16 and FUSED_BLOCK_FWD and xb.shape[1] == 256 and wb[o].shape == (512, 256):
+            if (r16 and FUSED_BLOCK_FWD and xb.shape[1] == 256 and wb[o].shape == (512, 256)
+                    and fused_block_rows_ok(xb.shape[0])):
                 if MASK_BITS:
                     h, xb, hbits[k] = _hip.resblock_fwd16(xb, wb[o], wb[o + 1], wb[o + 2], wb[o + 3],
                                                           seed=seed, p=ps[k], mask_bits=True)
@@ -296,7 +307,8 @@ class NoisePredictorFn(torch.autograd.Function):
             for k in reversed(range(6)):
                 o = 6 + 4 * k
                 xbk, hk = blocks[k]
-                if FUSED_BLOCK_BWD and dd.shape[1] == 256 and hk.shape[1] == 512:
+                if (FUSED_BLOCK_BWD and dd.shape[1] == 256 and hk.shape[1] == 512
+                        and fused_block_rows_ok(dd.shape[0]) and (hk.shape[0] == dd.shape[0])):
                     w2t, w1t = tw[o + 2], tw[o]
                     grads[o + 2], grads[o + 3] = _hip.linear_wgrad_ex(dd, hk)
                     dz, g, dd = _hip.resblock_bwd16(dd, w2t, w1t, hk, g,

@@ -105,16 +105,12 @@ class NoisePredictor(nn.Module):
         self._pack_key = None
         self._packed = None
 
-    # ABI precision code of the "bf16" mode: the 16x16x32 solo kernel (SOLO16, round 5).  tools/
-    # may set it to packing.PAIR16 (the round-2..4 pair kernel: same arithmetic, other work split)
-    # for A/B timing; the product never changes it.
-    bf16_code = packing.SOLO16
-
     @property
     def precision_code(self) -> int:
-        """ABI precision code: "bf16" runs `bf16_code`, "fp32" the exact-f32 parity kernel."""
+        """ABI precision code: "bf16" runs the bf16 (solo) kernel, "fp32" the exact-f32 parity
+        kernel."""
         p = getattr(self.config, "precision", "fp32")
-        return self.bf16_code if p == "bf16" else packing.F32
+        return packing.BF16 if p == "bf16" else packing.F32
 
     def packed(self):
         """Packed MFMA weight stream + bias table, rebuilt when any weight changes."""
@@ -230,20 +226,21 @@ class HierarchicalProcessor:
     def downsample_copies(self, points: torch.Tensor, copies: int,
                           ws: Optional[torch.Tensor] = None,
                           prepped: bool = False, seed: Optional[int] = None,
-                          pool: bool = False) -> Tuple[torch.Tensor, torch.Tensor]:
+                          pool: bool = False, start=None) -> Tuple[torch.Tensor, torch.Tensor]:
         """downsample(torch.cat([points] * copies)) -- the CFG batch of guided_sample_loop
         (diffusion_model.py:244-247) -- without building or re-hashing the copies.  Replay runs
         take the concatenated path: the reference draws one permutation per row.  `ws`
         (_hip.voxel_copies_workspace of the same shape) is reused instead of allocated;
         prepped: `ws` was prepared for `points` by the previous step's update
         (_hip.cfg_ddim_voxel_prep).  seed: the subset seed drawn ahead by the loop (the one the
-        previous step's update made the pool histogram for: pool=True); None draws it here."""
+        previous step's update made the pool histogram for: pool=True); None draws it here.
+        start (prepped only): a signal value the launch publishes as it begins (knn_rows_begin)."""
         src = _rng.source()
         if points.shape[1] <= self.global_points or src.replaying:
             return self.downsample(torch.cat([points] * copies))
         return _hip.voxel_downsample(points, self.global_points,
                                      seed=src.device_seed() if seed is None else seed,
-                                     copies=copies, ws=ws, prepped=prepped, pool=pool)
+                                     copies=copies, ws=ws, prepped=prepped, pool=pool, start=start)
 
     def step_prep(self, points: torch.Tensor) -> bool:
         """Whether the next downsample_copies of `points` can take a workspace prepared by the
@@ -309,14 +306,33 @@ def step_streams(device) -> Tuple[torch.cuda.Stream, torch.cuda.Stream]:
     return loop.stream, side.stream
 
 
+# At most one overlapped loop per device at a time.  HIP maps streams onto at most
+# GPU_MAX_HW_QUEUES hardware queues per priority (4 on the MI355X boxes), so per-thread stream
+# pairs do not keep concurrent loops apart: with more loops than queues, one loop's in-queue flag
+# wait can sit ahead of the other loop's producer on a shared queue -- a cycle that only the poll
+# bound breaks (a SignalTimeout).  A loop that finds the device's overlapped slot taken runs the
+# single-stream layout (no cross-stream waits; the same bits).
+_OVERLAP_LOCKS = {}
+_OVERLAP_LOCKS_GUARD = threading.Lock()
+
+
+def overlap_slot(device):
+    """The device's overlapped-loop lock (acquire non-blocking; release when the loop ends)."""
+    idx = torch.device(device).index
+    idx = torch.cuda.current_device() if idx is None else idx
+    with _OVERLAP_LOCKS_GUARD:
+        return _OVERLAP_LOCKS.setdefault(idx, threading.Lock())
+
+
 # Poll bound of the step's device waits (0: the library's default, ~10 s).  Tests lower it.
 SIGNAL_MAX_POLLS = 0
 
 
 class StepState:
     """The overlapped step's streams and cross-stream dependencies for ONE sampling loop (or one
-    bench run): the calling thread's loop / side streams, two events and two device flags (0:
-    loop -> side, the voxel output is ready; 1: side -> loop, the kNN build is done).  The flags
+    bench run): the calling thread's loop / side streams, two events and three device flags (0:
+    loop -> side, the voxel output (rows layout: x) is ready; 1: side -> loop, the kNN build is
+    done (rows layout: the ref placement may run); 2: rows layout, the build is done).  The flags
     share one allocation, so `check()` reads both timeout words with one copy; it raises
     _hip.SignalTimeout when a wait gave up (the loop's results are then invalid).  Per loop, so
     concurrent loops never share a flag and a flag's host counter starts at zero every loop."""
@@ -326,9 +342,11 @@ class StepState:
         mk = _hip.DeviceEvent if DEVICE_EVENTS else _TorchEvent
         self.ready_ev, self.built_ev = mk(), mk()
         polls = SIGNAL_MAX_POLLS if max_polls is None else max_polls
-        self._flags = torch.zeros(2, 4, dtype=torch.int32, device=device)
+        self._flags = torch.zeros(3, 4, dtype=torch.int32, device=device)
         self.ready_sig = _hip.DeviceSignal(device, polls, self._flags[0])
         self.built_sig = _hip.DeviceSignal(device, polls, self._flags[1])
+        # the rows layout's second side -> loop flag: phase A fully done (the query waits for it)
+        self.done_sig = _hip.DeviceSignal(device, polls, self._flags[2])
 
     def begin(self, caller):
         """Order both streams after the caller's work so far (the flags' zero fill included)."""
@@ -349,8 +367,44 @@ class StepState:
                 "the voxel output it waited for never signalled); the loop's output is invalid")
 
 
+# The step's kNN in the rows layout (pcst_knn3_rows_*): the side stream bins every point of x
+# (positions only) while the loop stream runs the voxel downsample, and after it one launch places
+# the coarse refs; the query then skips the known rows.  With the one-round bf16 MLP (235
+# work-groups of 512 threads and every VGPR of their CUs) nothing beside it finds a CU, so the
+# compact build could only run after it (round 5: ~75 us on the step's critical path); here its
+# positions-only part overlaps the latency-bound voxel chain instead.  Bit-identical to the
+# compact layout (tests/test_gpu_knn_rows.py).  Only while the MLP is one round of work-groups
+# (<= ROWS_MAX_MLP_POINTS): with many rounds (32 clouds per GPU) the compact build still hides
+# under the MLP and the rows layout's query, which visits every point (34 % more chunks), loses
+# (b1 2706 vs 2614 steps/s, b32 8.26 vs 7.61 ms, profiles/r05/r5c).  tools/knobs.py may turn it
+# off for A/B runs.
+ROWS_LAYOUT = True
+ROWS_MAX_MLP_POINTS = 256 * 256
+
+
+def rows_layout_ok(mlp_points: int) -> bool:
+    return ROWS_LAYOUT and mlp_points <= ROWS_MAX_MLP_POINTS
+
+
+def knn_rows_begin(x, M, state, ws, by_downsample=False):
+    """Phase A of the step's kNN on the side stream, ordered after the loop stream's work so far
+    (x is ready): -> (the rows handle for hierarchical_eps(rows=...), start).  by_downsample: the
+    next launch on the loop stream, the prepared voxel downsample, publishes the loop -> side flag
+    as it begins (pass `start` to downsample_copies) instead of a signal launch here; else start is
+    None.  The side stream signals state.built_sig when done."""
+    start = None
+    if by_downsample:
+        start = state.ready_sig.next_value()
+    else:
+        state.ready_sig.signal(torch.cuda.current_stream())
+    state.ready_sig.wait(state.side)
+    with torch.cuda.stream(state.side):
+        h = _hip.knn3_rows_build(x, M, 2, ws, refs_sig=state.built_sig, done_sig=state.done_sig)
+    return h, start
+
+
 def hierarchical_eps(hp, mlp, xc, xi, x_cat, knn_ws=None, state=None, mlp_waits=False,
-                     mlp_signals=False):
+                     mlp_signals=False, rows=None):
     """eps for the CFG batch: mlp(xc) on the current stream, upsampled to the full clouds by
     kNN-3 (HierarchicalProcessor.upsample_knn).  With a StepState (and a preallocated
     workspace) the kNN build runs on its side stream, overlapping the MLP, with its work-groups
@@ -359,6 +413,9 @@ def hierarchical_eps(hp, mlp, xc, xi, x_cat, knn_ws=None, state=None, mlp_waits=
     if state is None:
         return hp.upsample_knn(mlp(xc), x_cat, xi)
     main = torch.cuda.current_stream()
+    if rows is not None:  # the rows layout: phase A ran beside the downsample (knn_rows_begin)
+        _hip.knn3_rows_refs(rows, xi, wait=state.built_sig)  # (they wait for phase A in-kernel)
+        return _hip.knn3_rows_query(mlp(xc), rows, state.done_sig)
     side = state.side
     ready, built = state.ready_ev, state.built_ev
     start = None
@@ -409,7 +466,8 @@ SEARCH_BESIDE_MLP = False
 
 
 def hierarchical_step(hp, mlp, xc, xi, x_cat, x, source, guidance_scale, coeffs, knn_ws=None,
-                      state=None, mlp_waits=False, mlp_signals=False, vox_ws=None, pool_seed=None):
+                      state=None, mlp_waits=False, mlp_signals=False, vox_ws=None, pool_seed=None,
+                      rows=None):
     """One guided step of the hierarchical branch (diffusion_model.py:240-260): eps of the CFG
     batch (mlp(xc) upsampled by kNN-3), then the fused CFG + DDIM update of x (x_cat takes the
     new x twice).  Returns the new x.  state: a StepState (overlapped layout) or None.
@@ -417,10 +475,11 @@ def hierarchical_step(hp, mlp, xc, xi, x_cat, x, source, guidance_scale, coeffs,
     (_hip.cfg_ddim_voxel_prep: one launch fewer); that call must then pass prepped=True.  Only
     on the query-after-MLP layout (voxel_prep_ok).  pool_seed (with vox_ws): the seed of that
     downsample, drawn ahead; the update also makes its pool-key histogram (POOL_PREP), and the
-    downsample must then pass seed=pool_seed, pool=True."""
+    downsample must then pass seed=pool_seed, pool=True.  rows: the knn_rows_begin handle of this
+    step (the rows layout)."""
     C = x.shape[0]
-    if state is None or not SEARCH_BESIDE_MLP:
-        eps = hierarchical_eps(hp, mlp, xc, xi, x_cat, knn_ws, state, mlp_waits, mlp_signals)
+    if state is None or not SEARCH_BESIDE_MLP or rows is not None:
+        eps = hierarchical_eps(hp, mlp, xc, xi, x_cat, knn_ws, state, mlp_waits, mlp_signals, rows)
         if vox_ws is not None:
             return _hip.cfg_ddim_voxel_prep(x, eps, source, guidance_scale, coeffs, x_cat, vox_ws,
                                             pool_seed=pool_seed)
@@ -457,7 +516,7 @@ KERNEL_SIGNAL = True
 # the driver-window trace the event wait left ~10 us between the MLP's end and the query's start
 # although the build had finished ~16 us earlier (profiles/r03/s8_*); a one-workgroup wait kernel
 # that finds the flag already set costs a few us.  MLP_WAITS: the MLP's last work-group waits for
-# the flag itself (pcst_noise_mlp_then_wait), no wait launch at all: 0.3765 -> 0.3740 ms/step
+# the flag itself (pcst_noise_mlp_ex's wait), no wait launch at all: 0.3765 -> 0.3740 ms/step
 # (profiles/r03/s15_*), within run-to-run noise, and the MLP's launch then also holds the build's
 # tail, so its measured duration (the bench's roofline) is no longer the MLP's own.  Off.
 # Round 4 tried publishing the flag from the build's last kernel (a counter over the fill
@@ -612,8 +671,6 @@ class DiffusionProcess:
         x = x_T.to(device).float() if x_T is not None else _rng.source().randn(shape, device)
         timesteps = self._timesteps(num_inference_steps)
         use_hierarchical = shape[1] > model.config.global_points
-        source = source_points.float().contiguous()
-        x_cat = torch.cat([x, x]).contiguous()
         npred = model.noise_predictor
         # the CFG batch's timestep rows for the whole schedule, built once (one copy, no
         # per-step fill kernel)
@@ -629,6 +686,22 @@ class DiffusionProcess:
             pk = npred.packed()  # the loop changes no weight
             conds = npred.cond(t_rows.reshape(-1), style_in.repeat(S, 1), pk).view(S, 2 * B, -1)
         overlap = use_hierarchical and overlap_knn_build(2 * B * model.config.global_points)
+        slot = overlap_slot(device) if overlap else None
+        if slot is not None and not slot.acquire(blocking=False):
+            overlap, slot = False, None  # another loop holds the device's overlapped layout
+        try:
+            return self._guided_loop_body(model, source_points, B, shape, hp, style_in, x, timesteps,
+                                          use_hierarchical, npred, t_rows, t_prevs, conds, pk,
+                                          overlap, guidance_scale, device)
+        finally:
+            if slot is not None:
+                slot.release()
+
+    def _guided_loop_body(self, model, source_points, B, shape, hp, style_in, x, timesteps,
+                          use_hierarchical, npred, t_rows, t_prevs, conds, pk, overlap,
+                          guidance_scale, device):
+        source = source_points.float().contiguous()
+        x_cat = torch.cat([x, x]).contiguous()
         state = ws = vws = None
         ctx = contextlib.nullcontext()
         if overlap:
@@ -636,8 +709,11 @@ class DiffusionProcess:
             caller = torch.cuda.current_stream(device)
             state.begin(caller)
             ctx = torch.cuda.stream(state.loop)
+        rows_ws = None
         with ctx:
-            if overlap:
+            if overlap and rows_layout_ok(2 * B * model.config.global_points):
+                rows_ws = _hip.knn_rows_workspace(B, 2, shape[1], model.config.global_points, device)
+            elif overlap:
                 ws = _hip.knn_workspace(2 * B, shape[1], model.config.global_points, device=device)
             if use_hierarchical:
                 vws = _hip.voxel_copies_workspace(B, shape[1], 2, device=device)
@@ -654,7 +730,10 @@ class DiffusionProcess:
                         mlp = lambda c: npred(c, t_in, style_in)  # noqa: E731
                     coeffs = self._coeffs(t, t_prevs[i])
                     if use_hierarchical:
-                        xc, xi = hp.downsample_copies(x, 2, vws, prepped, next_seed, pool)
+                        rows, start = (knn_rows_begin(x, model.config.global_points, state,
+                                                      rows_ws, by_downsample=prepped)
+                                       if rows_ws is not None else (None, None))
+                        xc, xi = hp.downsample_copies(x, 2, vws, prepped, next_seed, pool, start)
                         prep = i + 1 < len(timesteps) and voxel_prep_ok(hp, x, state)
                         # the next step's subset seed, drawn one step ahead for its pool histogram
                         next_seed = (_rng.source().device_seed() & (2**64 - 1)
@@ -663,7 +742,8 @@ class DiffusionProcess:
                                               coeffs, ws, state,
                                               mlp_waits=MLP_WAITS and conds is not None,
                                               mlp_signals=MLP_SIGNALS and conds is not None,
-                                              vox_ws=vws if prep else None, pool_seed=next_seed)
+                                              vox_ws=vws if prep else None, pool_seed=next_seed,
+                                              rows=rows)
                         prepped, pool = prep, next_seed is not None
                     else:
                         eps = mlp(x_cat)

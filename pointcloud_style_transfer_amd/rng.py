@@ -150,8 +150,8 @@ class GeneratorRNG(TorchRNG):
     def rand(self, shape, device=None):
         return torch.rand(shape, generator=self.g).to(device)
 
-    def randn_like(self, x):
-        return torch.randn(tuple(x.shape), generator=self.g).to(x.device)
+    def randn_like(self, x):  # x's dtype, as TorchRNG.randn_like (torch.randn_like)
+        return torch.randn(tuple(x.shape), generator=self.g, dtype=x.dtype).to(x.device)
 
     def device_seed(self):
         return int(torch.randint(0, 2**62, (1,), dtype=torch.long, generator=self.g).item())

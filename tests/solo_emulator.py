@@ -1,5 +1,5 @@
 """Lane-level numpy emulator of csrc/noise_mlp.hip solo::noise_mlp_solo_kernel (test
-infrastructure).  It consumes the packed SOLO16 blob and bias table exactly as one wave does
+infrastructure).  It consumes the packed BF16 blob and bias table exactly as one wave does
 (32 points = two 16-point column blocks) and follows the kernel's schedule literally: the fragment
 stream order, the v_mfma_f32_16x16x32_bf16 lane layouts, which accumulator starts from which bias,
 where each operand is converted and which hidden-operand buffer each W2 chunk reads.  bf16

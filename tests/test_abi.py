@@ -50,8 +50,9 @@ def test_ctypes_binding_covers_header(built):
     for name in declared():
         assert hasattr(L, name)
     assert _hip.version().startswith("pcst")
-    assert _hip.noise_mlp_blob_bytes(1) == 109 * 32768
-    assert _hip.noise_mlp_blob_bytes(0) == 217 * 32768
+    assert _hip.noise_mlp_blob_bytes(1) == 55 * 65536     # bf16: 55 superparts
+    assert _hip.noise_mlp_blob_bytes(0) == 217 * 32768    # f32: 217 parts
+    assert _hip.noise_mlp_blob_bytes(2) == _hip.noise_mlp_blob_bytes(3) == -1  # retired codes
 
 
 def test_no_process_global_mutable_state(built):

@@ -310,12 +310,12 @@ def test_noise_mlp_bf16_per_element_60000(det_state):
     cond = _hip.noise_cond(t, style, *cp)
     bias = torch.from_numpy(packing.pack_bias(det_state)).cuda()
     outs = []
-    for prec in (0, 1, 2, 3):   # f32, bf16 pair 32x32x16 / pair 16x16x32 / solo 16x16x32
+    for prec in (0, 1):   # f32, bf16 (solo 16x16x32)
         blob = torch.from_numpy(packing.pack_blob(det_state, prec)).cuda()
         outs.append(_hip.noise_mlp(pts, 30000, cond, blob, bias, prec).cpu().numpy())
     f32 = outs[0]
     scale = np.abs(f32).max()
-    for prec, bf in ((1, outs[1]), (2, outs[2]), (3, outs[3])):
+    for prec, bf in ((1, outs[1]),):
         d = np.abs(bf - f32)
         ok = d <= 0.05 * (np.abs(f32) + 0.1 * scale)
         print(f"bf16 (code {prec}) vs f32 at 60000 pts: frac ok {ok.mean():.6f}, max "

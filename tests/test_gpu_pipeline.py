@@ -194,7 +194,7 @@ def test_inference_entry_point_bf16(golden, tmp_path, monkeypatch):
             inf.main(["--checkpoint", ck, "--source", "src.npy", "--reference", "ref.npy",
                       "--output", f"out/{prec}.npy", "--num_steps", "10", "--precision", prec])
         assert len(codes) == 10, codes
-        assert set(codes) == {packing.F32 if prec == "fp32" else packing.SOLO16}, codes
+        assert set(codes) == {packing.F32 if prec == "fp32" else packing.BF16}, codes
         outs[prec] = np.load(f"out/{prec}.npy")
     # 2048-point clouds (no hierarchy), 10 steps, outputs denormalised (x25): bf16 moves the
     # trajectory by well under the cloud's point spacing

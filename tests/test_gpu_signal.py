@@ -57,7 +57,7 @@ def test_signal_values_are_monotonic_per_flag():
 def test_wait_that_times_out_is_reported():
     """A wait whose value is never signalled gives up after its poll bound (an argument of the
     call), lets its stream go on, and check() raises SignalTimeout; the MLP's last-group wait
-    (pcst_noise_mlp_then_wait) reports through the same error word."""
+    (pcst_noise_mlp_ex's wait) reports through the same error word."""
     from pointcloud_style_transfer_amd import _hip
 
     dev = torch.device("cuda", 0)
@@ -76,7 +76,7 @@ def test_wait_that_times_out_is_reported():
 
     torch.manual_seed(4)
     npred = NoisePredictor(Config(make_dirs=False, precision="bf16")).to(dev).eval()
-    assert npred.precision_code == packing.SOLO16
+    assert npred.precision_code == packing.BF16
     pts = torch.randn(2 * 4096, 3, device=dev)
     with torch.no_grad():
         cond = npred.cond(torch.tensor([5, 5], device=dev), torch.randn(2, 256, device=dev))
@@ -176,6 +176,51 @@ def test_two_loops_on_two_threads_match_serial():
     assert all(not t.is_alive() for t in ths)
     torch.cuda.synchronize()
     for k in range(2):
+        assert torch.equal(conc[k], serial[k]), k
+
+
+def test_more_loops_than_hw_queues_match_serial():
+    """Six guided loops at once from six host threads on one device -- more loops than the
+    GPU_MAX_HW_QUEUES hardware queues (4) HIP spreads its streams over -- give the bits of the same
+    loops run one after the other, with no SignalTimeout: one loop at a time holds the device's
+    overlapped layout (diffusion_model.overlap_slot); the others run the single-stream layout, which
+    has no cross-stream waits to deadlock on a shared queue."""
+    import threading
+
+    from pointcloud_style_transfer_amd import rng
+    from pointcloud_style_transfer_amd.synthetic import lidar_like_cloud, standard_normal
+
+    dev = torch.device("cuda", 0)
+    cfg, model, dp = _small_model(dev)
+    model.noise_predictor.packed()
+    n, K = 8192, 6
+    jobs = [tuple(torch.from_numpy(a).to(dev) for a in (
+        lidar_like_cloud(1100 + k, n)[None], lidar_like_cloud(2100 + k, n)[None],
+        standard_normal(3100 + k, (1, n, 3)))) for k in range(K)]
+    errors = []
+
+    def run(k, out):
+        try:
+            src, cond, xT = jobs[k]
+            with torch.no_grad(), rng.use(rng.GeneratorRNG(200 + k)):
+                out[k] = dp.guided_sample_loop(model, src, cond, 6, 7.5, x_T=xT)
+            torch.cuda.current_stream(dev).synchronize()
+        except Exception as e:  # noqa: BLE001  (reported by the main thread)
+            errors.append((k, repr(e)))
+
+    serial = {}
+    for k in range(K):
+        run(k, serial)
+    conc = {}
+    ths = [threading.Thread(target=run, args=(k, conc)) for k in range(K)]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join(timeout=120)
+    assert all(not t.is_alive() for t in ths)
+    torch.cuda.synchronize()
+    assert not errors, errors
+    for k in range(K):
         assert torch.equal(conc[k], serial[k]), k
 
 

@@ -255,7 +255,7 @@ def _noise_params(det_state, H, precision):
                         g("style_proj.bias"), g("point_encoder.4.bias"))
 
 
-@pytest.mark.parametrize("precision", [0, 1, 2, 3])
+@pytest.mark.parametrize("precision", [0, 1])
 def test_noise_mlp_golden(H, golden, det_state, precision):
     g = golden("noise_predictor.npz")
     blob, bias, cp = _noise_params(det_state, H, precision)
@@ -484,8 +484,8 @@ def test_device_events_order_streams(H):
     assert t0.elapsed_time(t1) > 0.0
 
 
-def test_noise_mlp_then_wait_orders_after_the_signal(H):
-    """pcst_noise_mlp_then_wait: the MLP's rows are the bits of pcst_noise_mlp, work queued after
+def test_noise_mlp_wait_orders_after_the_signal(H):
+    """pcst_noise_mlp_ex with a wait flag (the bf16 kernel's last work-group waits): the MLP's rows are the bits of pcst_noise_mlp, work queued after
     it on the stream sees what the signalling stream wrote before its pcst_signal_write (here a
     side stream that fills a 64 MB buffer after a delay), and the work-group counter is back to 0
     with no timeout."""
@@ -496,7 +496,7 @@ def test_noise_mlp_then_wait_orders_after_the_signal(H):
     torch.manual_seed(4)
     cfg = Config(make_dirs=False, precision="bf16")
     npred = NoisePredictor(cfg).cuda().eval()
-    assert npred.precision_code == packing.SOLO16
+    assert npred.precision_code == packing.BF16
     rng = np.random.default_rng(8)
     pts = dev(rng.standard_normal((2 * 30000, 3)).astype(np.float32))
     t = torch.tensor([999, 999], device="cuda")

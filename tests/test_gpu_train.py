@@ -463,6 +463,34 @@ def test_noise_predictor_fused_blocks_match_unfused(H):
         assert rel(a, b) < 5e-2
 
 
+def test_noise_predictor_row_limit_fallback_bit_identical(H, monkeypatch):
+    """Batches beyond the fused residual-block kernels' row limit take the two-GEMM path
+    (models/_autograd.py fused_block_rows_ok); with the limit lowered below this batch
+    the forward and every gradient are the bits of the fused path (dropout on: the same draws)."""
+    from pointcloud_style_transfer_amd.config.config import Config
+    from pointcloud_style_transfer_amd.models import _autograd as ag
+    from pointcloud_style_transfer_amd.models.diffusion_model import NoisePredictor
+
+    torch.manual_seed(0)
+    npred = NoisePredictor(Config(make_dirs=False)).cuda().train()
+    x = torch.randn(2, 3000, 3, device="cuda")
+    t = torch.tensor([10, 500], device="cuda")
+    sf = torch.randn(2, 256, device="cuda")
+    outs, grads = [], []
+    for lim in (ag.FUSED_BLOCK_MAX_ROWS, 5999):   # 6000 rows: fused, then over the limit
+        monkeypatch.setattr(ag, "FUSED_BLOCK_MAX_ROWS", lim)
+        npred.zero_grad()
+        torch.manual_seed(3)  # the dropout seeds
+        with torch.autocast("cuda", dtype=torch.float16):
+            out = npred(x, t, sf)
+        out.float().pow(2).sum().backward()
+        outs.append(out.detach().clone())
+        grads.append([p.grad.detach().clone() for p in npred.parameters()])
+    assert torch.equal(outs[0], outs[1])
+    for a, b in zip(grads[0], grads[1]):
+        assert torch.equal(a, b)
+
+
 def _unfused_forward(npred, noisy_points, timestep, style_feat):
     from pointcloud_style_transfer_amd.models import _autograd as ag
 

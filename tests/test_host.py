@@ -266,85 +266,8 @@ def test_hip_wrappers_run_on_the_tensors_device(monkeypatch):
     assert f(torch.zeros(2)) == "ok" and entered == [1, 1]  # CPU tensor: no switch
 
 
-def test_bf16_pair_packing_follows_the_kernel_read_schedule():
-    """packing.pack_blob(BF16) in the pair layout of noise_mlp_pair_kernel: replaying the
-    kernel's read schedule (part order, role halves, block / k-step per fragment, csrc/
-    noise_mlp.hip pair_wave) over the blob recovers every weight of every layer exactly (as
-    bf16), so a layout slip fails here rather than on the GPU."""
-    import torch
-
-    from pointcloud_style_transfer_amd import packing
-    from pointcloud_style_transfer_amd.model_spec import state_dict_shapes
-    from detweights import deterministic_state
-
-    sd = deterministic_state(state_dict_shapes())
-    pre = "noise_predictor"
-    blob = packing.pack_blob(sd, packing.BF16)
-    vals = torch.from_numpy(blob.copy()).view(torch.bfloat16).float().numpy()
-    fpe = 512                                   # bf16 elements per 1 KiB fragment
-    parts = vals.reshape(-1, packing.PART // 2)
-    km = packing._kmap(packing.BF16, 32)        # [S, 64, 8] logical k per (step, lane, j)
-    r = np.arange(64) & 31
-    state = {"q": 0}
-    got = {}
-
-    def frag(q, f):
-        return parts[q, f * fpe:(f + 1) * fpe].reshape(64, 8)
-
-    def put(name, block, step, q, f):
-        W = got.setdefault(name, {})
-        fr = frag(q, f)
-        for lane in range(64):
-            for j in range(8):
-                W[(block * 32 + r[lane], int(km[step, lane, j]))] = fr[lane, j]
-
-    def dense(name, nown, ns):
-        ownpp = 32 // ns // 2
-        done = 0
-        while done < nown:
-            now = min(nown - done, ownpp)
-            for role in (0, 1):
-                for i in range(now * ns):
-                    put(name, role * nown + done + i // ns, i % ns, state["q"], role * ownpp * ns + i)
-            done += now
-            if done < nown:
-                state["q"] += 1
-
-    dense("point_encoder.2", 4, 8)
-    state["q"] += 1
-    dense("point_encoder.4", 4, 16)
-    for layer in range(6):
-        for it in range(8):
-            state["q"] += 1
-            for role in (0, 1):
-                for i in range(16):
-                    put(f"layers.{layer}.0", it + 8 * role, i, state["q"], role * 16 + i)
-            state["q"] += 1
-            steps = [2 * it, 2 * it + 1, 2 * (8 + it), 2 * (8 + it) + 1]
-            for role in (0, 1):
-                for i in range(16):
-                    put(f"layers.{layer}.2", 4 * role + i // 4, steps[i % 4], state["q"], role * 16 + i)
-    state["q"] += 1
-    dense("output_mlp.0", 4, 16)
-    state["q"] += 1
-    dense("output_mlp.2", 2, 16)
-    state["q"] += 1
-    for i in range(8):
-        put("output_mlp.4", 0, i, state["q"], i)
-    assert state["q"] + 1 == parts.shape[0]
-    for name, W in got.items():
-        ref = torch.from_numpy(sd[f"{pre}.{name}.weight"]).bfloat16().float().numpy()
-        O, K = ref.shape
-        seen = np.full((max(O, 32), K), np.nan, np.float32)
-        for (o, k), v in W.items():
-            seen[o, k] = v
-        np.testing.assert_array_equal(seen[:O], ref, err_msg=name)
-        if O < 32:
-            assert (seen[O:] == 0).all(), name
-
-
-def test_bf16_solo16_packing_follows_the_kernel_read_schedule():
-    """packing.pack_blob(SOLO16), the stream of noise_mlp_solo_kernel: replaying that kernel's
+def test_bf16_packing_follows_the_solo_kernel_read_schedule():
+    """packing.pack_blob(BF16), the stream of noise_mlp_solo_kernel: replaying that kernel's
     consumption order (csrc/noise_mlp.hip solo::: h2 rb-major, x, per layer W2(15) of the previous
     layer then W1(0), then W1(k), W2(k-1) for k = 1..15, the tail W2(15), out0, out1, out2)
     recovers every weight of every layer exactly (as bf16), the layer-0 W2 slot is zero, and the
@@ -357,7 +280,7 @@ def test_bf16_solo16_packing_follows_the_kernel_read_schedule():
 
     sd = deterministic_state(state_dict_shapes())
     pre = "noise_predictor"
-    blob = packing.pack_blob(sd, packing.SOLO16)
+    blob = packing.pack_blob(sd, packing.BF16)
     assert len(blob) == 55 * packing.SUPERPART
     vals = torch.from_numpy(blob.copy()).view(torch.bfloat16).float().numpy()
     frags = vals.reshape(-1, 512)
@@ -414,7 +337,7 @@ def test_bf16_solo16_packing_follows_the_kernel_read_schedule():
 
 def test_solo16_kernel_schedule_emulated_matches_the_network():
     """tests/solo_emulator.py replays noise_mlp_solo_kernel's dataflow lane by lane over the packed
-    SOLO16 blob (fragment order, v_mfma_f32_16x16x32_bf16 layouts, bias placement, the hidden-chunk
+    BF16 blob (fragment order, v_mfma_f32_16x16x32_bf16 layouts, bias placement, the hidden-chunk
     software pipeline, bf16 operand rounding) for one wave's 32 points; it must equal the exact-f32
     network (oracle.noise_predictor) within the bf16 mode's normwise bound (3e-2, as the GPU
     tests) -- a schedule or layout error gives O(1) differences."""
@@ -425,7 +348,7 @@ def test_solo16_kernel_schedule_emulated_matches_the_network():
     import oracle.oracle as O
 
     sd = deterministic_state(state_dict_shapes())
-    blob = packing.pack_blob(sd, packing.SOLO16)
+    blob = packing.pack_blob(sd, packing.BF16)
     bias = packing.pack_bias(sd)
     rng = np.random.default_rng(11)
     pts = rng.standard_normal((1, 32, 3)).astype(np.float32)
@@ -438,83 +361,6 @@ def test_solo16_kernel_schedule_emulated_matches_the_network():
     out = SE.run_wave(blob, bias, pts[0], np.repeat(cond, 32, axis=0))
     err = np.linalg.norm(out - ref) / np.linalg.norm(ref)
     assert err < 3e-2, err
-
-
-def test_bf16_pair16_packing_follows_the_kernel_read_schedule():
-    """packing.pack_blob(PAIR16), the 16x16x32 layout of noise_mlp_pair16_kernel: replaying
-    that kernel's read schedule (csrc/noise_mlp.hip pair16_wave / dense16 / run16: part order,
-    role halves at fragment 16, fragment i = (row block i // NKS, k-step i % NKS)) over the blob
-    recovers every weight of every layer exactly (as bf16)."""
-    import torch
-
-    from pointcloud_style_transfer_amd import packing
-    from pointcloud_style_transfer_amd.model_spec import state_dict_shapes
-    from detweights import deterministic_state
-
-    sd = deterministic_state(state_dict_shapes())
-    pre = "noise_predictor"
-    blob = packing.pack_blob(sd, packing.PAIR16)
-    vals = torch.from_numpy(blob.copy()).view(torch.bfloat16).float().numpy()
-    parts = vals.reshape(-1, packing.PART // 2)
-    km = packing._kmap16(16)                    # [S, 64, 8]
-    r = np.arange(64) & 15
-    q = [0]
-    got = {}
-
-    def put(name, rb, step, f):
-        W = got.setdefault(name, {})
-        fr = parts[q[0], f * 512:(f + 1) * 512].reshape(64, 8)
-        for lane in range(64):
-            for j in range(8):
-                W[(rb * 16 + r[lane], int(km[step, lane, j]))] = fr[lane, j]
-
-    def dense(name, nown, nks):
-        ownpp = 32 // nks // 2
-        done = 0
-        while done < nown:
-            now = min(nown - done, ownpp)
-            for role in (0, 1):
-                for i in range(now * nks):
-                    put(name, role * nown + done + i // nks, i % nks, role * ownpp * nks + i)
-            done += now
-            if done < nown:
-                q[0] += 1
-
-    dense("point_encoder.2", 8, 4)
-    q[0] += 1
-    dense("point_encoder.4", 8, 8)
-    def w1(layer, it):
-        q[0] += 1
-        for role in (0, 1):
-            for i in range(16):
-                put(f"layers.{layer}.0", 2 * (it + 8 * role) + i // 8, i % 8, role * 16 + i)
-
-    for layer in range(6):   # software-pipelined: W1(0), then W1(it + 1) before W2(it)
-        w1(layer, 0)
-        for it in range(8):
-            if it < 7:
-                w1(layer, it + 1)
-            q[0] += 1
-            for role in (0, 1):
-                for i in range(16):
-                    put(f"layers.{layer}.2", 8 * role + i // 2, (it, 8 + it)[i % 2], role * 16 + i)
-    q[0] += 1
-    dense("output_mlp.0", 8, 8)
-    q[0] += 1
-    dense("output_mlp.2", 4, 8)
-    q[0] += 1
-    for i in range(4):
-        put("output_mlp.4", 0, i, i)
-    assert q[0] + 1 == parts.shape[0]
-    for name, W in got.items():
-        ref = torch.from_numpy(sd[f"{pre}.{name}.weight"]).bfloat16().float().numpy()
-        O, K = ref.shape
-        seen = np.full((max(O, 16), K), np.nan, np.float32)
-        for (o, k), v in W.items():
-            seen[o, k] = v
-        np.testing.assert_array_equal(seen[:O], ref, err_msg=name)
-        if O < 16:
-            assert (seen[O:] == 0).all(), name
 
 
 def test_chaos_floor_constants_match_profile():
@@ -564,3 +410,29 @@ def test_fused_adamw_resumes_a_non_fused_checkpoint():
     opt.step()
     assert float(opt.state[p[0]]["step"]) == 2.0
     assert not torch.equal(before, p[0].detach())
+
+
+def test_fused_block_row_limit_matches_the_kernels():
+    """The fused residual-block dispatch (models/_autograd.py) sends M rows to pcst_resblock_*16
+    only while M * 1024 < 2^31, the kernels' own bound; larger M takes the two-GEMM path."""
+    from pointcloud_style_transfer_amd.models import _autograd as A
+
+    lim = (2 ** 31 - 1) // 1024
+    assert A.fused_block_rows_ok(lim) and lim * 1024 < 2 ** 31
+    assert not A.fused_block_rows_ok(lim + 1) and (lim + 1) * 1024 >= 2 ** 31
+    assert A.fused_block_rows_ok(8 * 30000)          # the trainer's batch
+    assert not A.fused_block_rows_ok(70 * 30000)     # 70 clouds: the unfused path
+
+
+def test_generator_rng_randn_like_keeps_the_dtype():
+    """rng.GeneratorRNG.randn_like keeps x's dtype, as TorchRNG.randn_like (torch.randn_like)
+    does, so q_sample's noise has the same dtype whichever source the thread installed."""
+    from pointcloud_style_transfer_amd import rng
+
+    for dt in (torch.float32, torch.float64, torch.float16):
+        x = torch.zeros(3, 4, dtype=dt)
+        assert rng.GeneratorRNG(1).randn_like(x).dtype == dt
+        assert rng.TorchRNG().randn_like(x).dtype == dt
+    a = rng.GeneratorRNG(5).randn_like(torch.zeros(2, 3))
+    b = rng.GeneratorRNG(5).randn_like(torch.zeros(2, 3))
+    assert torch.equal(a, b)

@@ -1,6 +1,5 @@
 """FPS timing (the SA1 shape: N = 30000, 512 samples) on a lidar-like and a Gaussian cloud, B = 1
-and B = 32, HIP events over 20 calls.  An experiment build with XDEF=-DPCST_X_FPS_CULL=0 (loaded through
-PCST_LIB) times fps_key_kernel instead."""
+and B = 32, HIP events over 20 calls."""
 import os
 import sys
 

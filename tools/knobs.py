@@ -3,10 +3,10 @@
     import knobs; knobs.apply()
 
 reads PCST_KNN_OVERLAP=0|1, PCST_KNN_BUILD_LDS_FLOOR=<bytes>, PCST_DEVICE_EVENTS=0|1,
-PCST_KERNEL_SIGNAL=0|1, PCST_FUSED_BLOCK_FWD / _BWD=0|1 (models._autograd) and
-PCST_NM_BF16_KERNEL=1 (the 32x32x16 pair kernel) and sets the matching module constants of
-models.diffusion_model.  Kernel-side variants are experiment builds (csrc/Makefile XDEF,
-loaded through PCST_LIB)."""
+PCST_KERNEL_SIGNAL=0|1, PCST_ROWS_LAYOUT=0|1, PCST_FUSED_BLOCK_FWD / _BWD=0|1 (models._autograd)
+and sets the matching module constants of models.diffusion_model.  Kernel-side variants are
+experiment builds (csrc/Makefile XDEF): PCST_LIB=<path> points _hip.LIB_PATH at one before the
+library is loaded (the product _hip reads no environment)."""
 import os
 import sys
 
@@ -14,10 +14,14 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
 def apply():
-    from pointcloud_style_transfer_amd import packing
+    from pointcloud_style_transfer_amd import _hip
     from pointcloud_style_transfer_amd.models import diffusion_model as dm
 
     e = os.environ
+    if e.get("PCST_LIB"):
+        if _hip._lib is not None:
+            raise RuntimeError("knobs.apply(): PCST_LIB must be applied before the library loads")
+        _hip.LIB_PATH = e["PCST_LIB"]
     if "PCST_KNN_OVERLAP" in e:
         dm.OVERLAP_KNN_BUILD = e["PCST_KNN_OVERLAP"] != "0"
     if "PCST_KNN_BUILD_LDS_FLOOR" in e:
@@ -36,6 +40,8 @@ def apply():
         dm.MLP_WAITS = e["PCST_MLP_WAITS"] != "0"
     if "PCST_BUILT_SIGNAL" in e:
         dm.BUILT_SIGNAL = e["PCST_BUILT_SIGNAL"] != "0"
+    if "PCST_ROWS_LAYOUT" in e:  # the step's kNN in the rows layout (0: the compact build)
+        dm.ROWS_LAYOUT = e["PCST_ROWS_LAYOUT"] != "0"
     if "PCST_SEARCH_BESIDE_MLP" in e:
         dm.SEARCH_BESIDE_MLP = e["PCST_SEARCH_BESIDE_MLP"] != "0"
     if "PCST_KERNEL_SIGNAL" in e:
@@ -55,7 +61,3 @@ def apply():
     if "PCST_BATCH_CAST" in e:
         from pointcloud_style_transfer_amd.models import _autograd
         _autograd.BATCH_CAST = e["PCST_BATCH_CAST"] != "0"
-    if e.get("PCST_NM_BF16_KERNEL") == "1":
-        dm.NoisePredictor.bf16_code = packing.BF16
-    if "PCST_NM_CODE" in e:   # the bf16 mode's kernel: 1 pair 32x32x16, 2 pair16, 3 solo (product)
-        dm.NoisePredictor.bf16_code = int(e["PCST_NM_CODE"])

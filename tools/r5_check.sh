@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round-5 GPU check: tools/r5_check.sh TAG [STAGES...]  (round 4's stages plus variants= / timeline)
+# Round-5 GPU check: tools/r5_check.sh TAG [STAGES...]  (round 4's stages plus timeline)
 #   tests=EXPR   pytest -m gpu -k EXPR (tests=all: the whole GPU suite)
 #   smoke        __graft_entry__.smoke()
 #   bench        the driver's invocation (bench.py --gpus 1 --steps 20 --warmup 5)
@@ -112,22 +112,15 @@ for st in "$@"; do
           --no-other-precision --no-extra > "$OUT/b32prof.json" 2> "$OUT/b32prof.err"
       rc=$?; echo "b32prof rc=$rc"; if [ $rc -ne 0 ]; then tail -5 "$OUT/b32prof.err"; exit $rc; fi
       python tools/kstats.py "$OUT/b32prof/run_kernel_stats.csv" 25 | tee "$OUT/b32_kernel_top.txt" ;;
-    libtests=*)
-      # libtests=v_name,EXPR: pytest -m gpu -k EXPR against pointcloud_style_transfer_amd/libpcst_hip_<v_name>.so
-      A=${st#libtests=}; V=${A%%,*}; K=${A#*,}
-      PCST_LIB=$PWD/pointcloud_style_transfer_amd/libpcst_hip_$V.so timeout -k 10 600 python -u -m pytest tests -m gpu -x -v \
-          --timeout 300 --timeout-method thread -k "$K" > "$OUT/libtests_$V.log" 2>&1
-      rc=$?; echo "libtests $V rc=$rc"; grep -E "FAILED|ERROR" "$OUT/libtests_$V.log" | head; tail -1 "$OUT/libtests_$V.log"
-      if [ $rc -ne 0 ]; then exit $rc; fi ;;
     benchlib=*)
       # benchlib=v_a,v_b: the driver-window bench (and the 32-cloud bench) with each library, two passes
       VS=${st#benchlib=}
       for pass in 1 2; do
         for v in prod ${VS//,/ }; do
           if [ "$v" = prod ]; then lib=$PWD/pointcloud_style_transfer_amd/libpcst_hip.so; else lib=$PWD/pointcloud_style_transfer_amd/libpcst_hip_$v.so; fi
-          PCST_LIB=$lib timeout -k 10 200 python $BENCH > "$OUT/bench_$v.$pass.json" 2> "$OUT/bench_$v.$pass.err"
+          PCST_LIB=$lib timeout -k 10 200 python tools/bench_knobs.py ${BENCH#bench.py } > "$OUT/bench_$v.$pass.json" 2> "$OUT/bench_$v.$pass.err"
           rc=$?; if [ $rc -ne 0 ]; then tail -3 "$OUT/bench_$v.$pass.err"; exit $rc; fi
-          PCST_LIB=$lib timeout -k 10 200 python bench.py --gpus 1 --clouds-per-gpu 32 --steps 10 --warmup 3 \
+          PCST_LIB=$lib timeout -k 10 200 python tools/bench_knobs.py --gpus 1 --clouds-per-gpu 32 --steps 10 --warmup 3 \
               --no-cpu-baseline --no-encoder --no-other-precision --no-extra > "$OUT/b32_$v.$pass.json" 2> "$OUT/b32_$v.$pass.err"
           rc=$?; if [ $rc -ne 0 ]; then tail -3 "$OUT/b32_$v.$pass.err"; exit $rc; fi
           python -c "import json,sys; f=lambda p: json.loads(open(p).read().strip().splitlines()[-1]); a=f(sys.argv[1]); b=f(sys.argv[2]); print(sys.argv[3], 'b1', a['value'], a['ms_per_step'], a['roofline']['avg_launch_ms'], 'b32', b['ms_per_step'])" "$OUT/bench_$v.$pass.json" "$OUT/b32_$v.$pass.json" "$v.$pass"
@@ -149,10 +142,6 @@ for st in "$@"; do
           python -c "import json,sys; f=lambda p: json.loads(open(p).read().strip().splitlines()[-1]); a=f(sys.argv[1]); b=f(sys.argv[2]); print(sys.argv[3], 'b1', a['value'], a['ms_per_step'], a['roofline']['avg_launch_ms'], 'b32', b['ms_per_step'])" "$OUT/bench_$v.$pass.json" "$OUT/b32_$v.$pass.json" "$v.$pass"
         done
       done ;;
-    variants=*)
-      # variants=KD:PRIO:STAMPS,...: the solo-kernel harness builds (tools/solo_variants.sh)
-      V=${st#variants=}; tools/solo_variants.sh run "${V//,/ }" 2>&1 | tee "$OUT/variants.txt"
-      rc=${PIPESTATUS[0]}; if [ $rc -ne 0 ]; then exit $rc; fi ;;
     timeline)
       python tools/timeline.py "$OUT/prof/run_kernel_trace.csv" --last 18 --show 2 | tee "$OUT/driver_window_timeline.txt" | tail -40 ;;
     loop1000)
