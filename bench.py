@@ -509,20 +509,22 @@ def main():
             # the rows layout: the kNN's positions-only phase on the side stream beside the
             # downsample (as guided_sample_loop)
             rows, start = (dmod.knn_rows_begin(x, cfg.global_points, state, rows_ws,
-                                               by_downsample=prepped)
+                                               by_downsample=prepped,
+                                               beside_mlp=dmod.REFS_BESIDE_MLP)
                            if rows_ws is not None else (None, None))
             xc, xi = hp.downsample_copies(x, 2, vws, prepped, next_seed, pool, start)
 
-            def mlp(xc_, wait=None, start=None):
+            def mlp(xc_, wait=None, start=None, start_all=False):
                 if not timed:
-                    return npred.forward_cond(xc_, cnd, pk, wait, start)
+                    return npred.forward_cond(xc_, cnd, pk, wait, start, start_all)
                 # on the stream the MLP runs on; device-scope fences (no L2 writeback bubble
                 # around the timed kernel) unless tools/knobs.py turned them off
                 e0, e1 = timing_event(), timing_event()
                 blob, bias = pk[:2]
                 e0.record()
                 nc_ = _hip.noise_mlp(xc_.reshape(-1, 3), cfg.global_points, cnd, blob, bias,
-                                     npred.precision_code, wait=wait, signal=start).view(2 * C, -1, 3)
+                                     npred.precision_code, wait=wait, signal=start,
+                                     signal_all=start_all).view(2 * C, -1, 3)
                 e1.record()
                 ev.append((e0, e1))
                 return nc_
@@ -534,7 +536,9 @@ def main():
                          if prep and dmod.pool_prep_ok(x) else None)
             x = dmod.hierarchical_step(hp, mlp, xc, xi, x_cat, x, src, 7.5, dp._coeffs(t, t_prev),
                                        knn_ws, state, mlp_waits=dmod.MLP_WAITS,
-                                       mlp_signals=dmod.MLP_SIGNALS, vox_ws=vws if prep else None,
+                                       mlp_signals=(dmod.REFS_BESIDE_MLP if rows is not None
+                                                    else dmod.MLP_SIGNALS),
+                                       vox_ws=vws if prep else None,
                                        pool_seed=next_seed, rows=rows)
             prepped, pool = prep, next_seed is not None
 

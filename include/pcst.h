@@ -383,7 +383,10 @@ int pcst_noise_mlp(const float* pts, int64_t P, int64_t points_per_cloud, const 
 /* pcst_noise_mlp with optional cross-stream signalling folded into the launch (all optional):
  * start_flag: *start_flag = start_value (agent-scope store) as the launch begins, i.e. once every
  * kernel queued before it on `stream` has completed -- the producer side of pcst_signal_wait
- * without a pcst_signal_write launch; wait_flag: the launch completes only once *wait_flag >=
+ * without a pcst_signal_write launch; start_counter (with start_flag; a caller-owned uint32 that
+ * is zero before the call and zero again after it): the store happens once EVERY work-group of
+ * the launch has begun instead (precision 0: once the launch has completed), so work another
+ * stream starts behind the flag only finds the CUs the MLP leaves idle; wait_flag: the launch completes only once *wait_flag >=
  * wait_value as well -- after writing its rows, the MLP's last work-group (counted out by
  * wait_counter, a caller-owned uint32 that is zero before the call and zero again after it) polls
  * the flag with agent-scope loads (the producer on another stream writes it with
@@ -394,7 +397,8 @@ int pcst_noise_mlp(const float* pts, int64_t P, int64_t points_per_cloud, const 
 int pcst_noise_mlp_ex(const float* pts, int64_t P, int64_t points_per_cloud, const float* cond,
                       int64_t nclouds, const void* blob, int64_t blob_bytes, const float* bias,
                       int precision, float* out, uint32_t* start_flag, uint32_t start_value,
-                      const uint32_t* wait_flag, uint32_t wait_value, uint32_t* wait_counter,
+                      uint32_t* start_counter, const uint32_t* wait_flag, uint32_t wait_value,
+                      uint32_t* wait_counter,
                       int32_t* wait_err, int64_t max_polls, void* stream);
 
 /* CFG + DDIM update of guided_sample_loop (diffusion_model.py:248-260); eps_u == NULL gives

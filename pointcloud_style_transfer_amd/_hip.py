@@ -69,7 +69,7 @@ SIGNATURES = {
     "pcst_noise_cond": [_P, _P, _I, _P, _P, _P, _P, _P, _P, _P, _P],
     "pcst_noise_mlp": [_P, _I, _I, _P, _I, _P, _I, _P, ctypes.c_int, _P, _P],
     "pcst_noise_mlp_ex": [_P, _I, _I, _P, _I, _P, _I, _P, ctypes.c_int, _P, _P, ctypes.c_uint32, _P,
-                          ctypes.c_uint32, _P, _P, _I, _P],
+                          _P, ctypes.c_uint32, _P, _P, _I, _P],
     "pcst_cfg_ddim_step": [_P, _P, _P, _P, _I, _F, _F, _F, _F, _F, _P, _P, _P],
     "pcst_pointwise_linear": [_P, _I, _I, _P, _I, _P, _P, ctypes.c_int, _I, _P, _P],
     "pcst_voxel_center_dist": [_P, _I, _P, ctypes.c_float, _P, _P, _P, _P],
@@ -406,7 +406,8 @@ class DeviceSignal:
     VALUE_LIMIT = 1 << 31
 
     def __init__(self, device, max_polls=0, storage=None):
-        # [flag, timeout error, work-group counter of pcst_noise_mlp_ex's wait, pad]
+        # [flag, timeout error, work-group counter of pcst_noise_mlp_ex's wait, work-group
+        #  counter of its start signal (start_all)]
         self.flag = (storage if storage is not None
                      else torch.zeros(4, dtype=torch.int32, device=device))
         if self.flag.dtype != torch.int32 or self.flag.numel() != 4 or not self.flag.is_contiguous():
@@ -739,14 +740,17 @@ def noise_cond(t, style, freqs, wt, bt, ws_, bs, b4):
 
 
 def noise_mlp(pts, points_per_cloud, cond, blob, bias, precision, out=None, wait=None,
-              signal=None):
+              signal=None, signal_all=False):
     """pts [P,3] (P = clouds*points_per_cloud, cloud-major) -> eps [P,3].
     wait (a DeviceSignal signalled on another stream): work queued after the MLP on this stream
     is also ordered after that signal -- at precisions 2 and 3 by the MLP's last work-group
     (pcst_noise_mlp_ex's wait), otherwise by a wait launch after it.
     signal ((flag, value) from DeviceSignal.next_value()): the value is published as the MLP
     launch begins (everything queued before it on this stream is then done) --
-    pcst_noise_mlp_ex's start signal."""
+    pcst_noise_mlp_ex's start signal.  signal_all: published once every work-group of the launch
+    has begun (the flag's own DeviceSignal storage word 3 counts them: pcst_noise_mlp_ex's
+    start_counter), so work another stream starts behind it finds only the CUs the MLP leaves
+    idle."""
     require_device(pts, cond, blob, bias)
     pts = _f32(pts)
     P = pts.shape[0]
@@ -754,13 +758,15 @@ def noise_mlp(pts, points_per_cloud, cond, blob, bias, precision, out=None, wait
         out = torch.empty(P, 3, dtype=torch.float32, device=pts.device)
     if signal is not None:
         fl, val = signal
+        cnt = ctypes.c_void_p(fl.value + 12) if signal_all else None
         w = wait.wait_args() if wait is not None else (None, 0, None, None, 0)
         _call("pcst_noise_mlp_ex", _ptr(pts), P, points_per_cloud, _ptr(cond), cond.shape[0],
-              _ptr(blob), blob.numel(), _ptr(bias), precision, _ptr(out), fl, val, *w, _stream())
+              _ptr(blob), blob.numel(), _ptr(bias), precision, _ptr(out), fl, val, cnt, *w,
+              _stream())
         return out
     if wait is not None and precision == 1 and P > 0:
         _call("pcst_noise_mlp_ex", _ptr(pts), P, points_per_cloud, _ptr(cond), cond.shape[0],
-              _ptr(blob), blob.numel(), _ptr(bias), precision, _ptr(out), None, 0,
+              _ptr(blob), blob.numel(), _ptr(bias), precision, _ptr(out), None, 0, None,
               *wait.wait_args(), _stream())
         return out
     _call("pcst_noise_mlp", _ptr(pts), P, points_per_cloud, _ptr(cond), cond.shape[0], _ptr(blob),

@@ -576,12 +576,22 @@ __global__ __launch_bounds__(kThreads) void noise_mlp_solo_kernel(
     int64_t nclouds, const char* __restrict__ blob, int nsp, const float* __restrict__ bias,
     float* __restrict__ out, const uint32_t* __restrict__ wflag, uint32_t wvalue,
     uint32_t* __restrict__ wcount, int32_t* __restrict__ werr, int64_t wpolls,
-    uint32_t* __restrict__ sflag, uint32_t svalue) {
+    uint32_t* __restrict__ sflag, uint32_t svalue, uint32_t* __restrict__ scount) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   // the start signal: every launch ahead of this one on its stream has completed (its inputs are
-  // final), published for another stream (pcst_noise_mlp_ex's start_flag)
-  if (sflag && blockIdx.x == 0 && threadIdx.x == 0)
-    __hip_atomic_store(sflag, svalue, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  // final), published for another stream (pcst_noise_mlp_ex's start_flag) by the first
+  // work-group; with scount, by the last work-group to begin (counted out on *scount, which is
+  // zero again after it): every work-group of the launch then holds its CU, so work another
+  // stream starts behind the flag only finds the CUs the launch leaves idle
+  if (sflag && threadIdx.x == 0) {
+    if (!scount) {
+      if (blockIdx.x == 0) __hip_atomic_store(sflag, svalue, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else if (__hip_atomic_fetch_add(scount, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+               gridDim.x - 1) {
+      __hip_atomic_store(scount, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(sflag, svalue, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
   const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const uint32_t lds0 = (uint32_t)(uintptr_t)smem;
@@ -986,10 +996,10 @@ int check_mlp_args(const char* name, int64_t P, int64_t points_per_cloud, int64_
 void launch_solo(const float* pts, int64_t P, int64_t T, const float* cond, int64_t nclouds,
                  const void* blob, const float* bias, float* out, const uint32_t* wflag,
                  uint32_t wvalue, uint32_t* wcount, int32_t* werr, int64_t wpolls, uint32_t* sflag,
-                 uint32_t svalue, hipStream_t s) {
+                 uint32_t svalue, uint32_t* scount, hipStream_t s) {
   hipLaunchKernelGGL(solo::noise_mlp_solo_kernel, dim3((unsigned)cdiv(P, solo::kPts)), dim3(solo::kThreads),
                      solo::kLds, s, pts, P, T, cond, nclouds, (const char*)blob, solo::kNSP, bias, out,
-                     wflag, wvalue, wcount, werr, wpolls, sflag, svalue);
+                     wflag, wvalue, wcount, werr, wpolls, sflag, svalue, scount);
 }
 }  // namespace
 
@@ -1002,7 +1012,7 @@ extern "C" int pcst_noise_mlp(const float* pts, int64_t P, int64_t points_per_cl
   hipStream_t s = as_stream(stream);
   if (precision == 1)
     launch_solo(pts, P, points_per_cloud, cond, nclouds, blob, bias, out, nullptr, 0u, nullptr,
-                nullptr, 0, nullptr, 0u, s);
+                nullptr, 0, nullptr, 0u, nullptr, s);
   else
     launch_noise_mlp<TrF32>(pts, P, points_per_cloud, cond, nclouds, blob, blob_bytes, bias, out, s);
   PCST_LAUNCH_CHECK("noise_mlp");
@@ -1019,25 +1029,31 @@ extern "C" int pcst_noise_mlp_ex(const float* pts, int64_t P, int64_t points_per
                                  const float* cond, int64_t nclouds, const void* blob,
                                  int64_t blob_bytes, const float* bias, int precision, float* out,
                                  uint32_t* start_flag, uint32_t start_value,
-                                 const uint32_t* wait_flag, uint32_t wait_value,
-                                 uint32_t* wait_counter, int32_t* wait_err, int64_t max_polls,
-                                 void* stream) {
+                                 uint32_t* start_counter, const uint32_t* wait_flag,
+                                 uint32_t wait_value, uint32_t* wait_counter, int32_t* wait_err,
+                                 int64_t max_polls, void* stream) {
   if (precision != 1 || P == 0) {  // the f32 kernel has no fused form: separate launches
-    if (start_flag) {
+    if (start_flag && !start_counter) {
       hipLaunchKernelGGL(mlp_start_signal_kernel, dim3(1), dim3(64), 0, as_stream(stream), start_flag,
                          start_value);
       PCST_LAUNCH_CHECK("noise_mlp_ex: start signal");
     }
     const int rc = pcst_noise_mlp(pts, P, points_per_cloud, cond, nclouds, blob, blob_bytes, bias,
                                   precision, out, stream);
-    if (rc != PCST_OK || !wait_flag) return rc;
+    if (rc != PCST_OK) return rc;
+    if (start_flag && start_counter) {  // every work-group has begun: published once it completed
+      hipLaunchKernelGGL(mlp_start_signal_kernel, dim3(1), dim3(64), 0, as_stream(stream), start_flag,
+                         start_value);
+      PCST_LAUNCH_CHECK("noise_mlp_ex: start signal");
+    }
+    if (!wait_flag) return rc;
     return pcst_signal_wait(wait_flag, wait_value, wait_err, max_polls, stream);
   }
   if (int rc = check_mlp_args("noise_mlp_ex", P, points_per_cloud, nclouds, blob, blob_bytes, precision)) return rc;
   PCST_CHECK_ARG(!wait_flag || wait_counter, "noise_mlp_ex: a wait needs its counter");
   launch_solo(pts, P, points_per_cloud, cond, nclouds, blob, bias, out, wait_flag, wait_value,
               wait_counter, wait_err, max_polls > 0 ? max_polls : (int64_t)kSignalPolls, start_flag,
-              start_value, as_stream(stream));
+              start_value, start_counter, as_stream(stream));
   PCST_LAUNCH_CHECK("noise_mlp_ex");
   return PCST_OK;
 }

@@ -181,17 +181,20 @@ class NoisePredictor(nn.Module):
                     or (style_feat.requires_grad and torch.is_grad_enabled()))
 
     def forward_cond(self, noisy_points: torch.Tensor, cond: torch.Tensor,
-                     packed: Optional[tuple] = None, wait=None, signal=None) -> torch.Tensor:
+                     packed: Optional[tuple] = None, wait=None, signal=None,
+                     signal_all=False) -> torch.Tensor:
         """The fused inference forward with precomputed conditioning rows (`cond()` of the
         same timesteps and style features): the sampling loops compute every step's rows in one
         launch before the loop.  `packed` (this module's `packed()`, fetched once before a loop
         that does not change the weights) skips the per-call weight-version check.  `wait` (a
         DeviceSignal): later work on this stream also waits for it; `signal` (a DeviceSignal's
-        next_value()): published as the launch begins (_hip.noise_mlp)."""
+        next_value()): published as the launch begins (_hip.noise_mlp); signal_all: once every
+        work-group of the launch has begun."""
         B, N, _ = noisy_points.shape
         blob, bias = (packed if packed is not None else self.packed())[:2]
         out = _hip.noise_mlp(noisy_points.reshape(B * N, 3), N, cond, blob, bias,
-                             self.precision_code, wait=wait, signal=signal)
+                             self.precision_code, wait=wait, signal=signal,
+                             signal_all=signal_all)
         return out.view(B, N, 3)
 
     def forward(self, noisy_points: torch.Tensor, timestep: torch.Tensor,
@@ -342,11 +345,13 @@ class StepState:
         mk = _hip.DeviceEvent if DEVICE_EVENTS else _TorchEvent
         self.ready_ev, self.built_ev = mk(), mk()
         polls = SIGNAL_MAX_POLLS if max_polls is None else max_polls
-        self._flags = torch.zeros(3, 4, dtype=torch.int32, device=device)
+        self._flags = torch.zeros(4, 4, dtype=torch.int32, device=device)
         self.ready_sig = _hip.DeviceSignal(device, polls, self._flags[0])
         self.built_sig = _hip.DeviceSignal(device, polls, self._flags[1])
-        # the rows layout's second side -> loop flag: phase A fully done (the query waits for it)
+        # the rows layout's second side -> loop flag: the kNN rows are placed (the query waits)
         self.done_sig = _hip.DeviceSignal(device, polls, self._flags[2])
+        # loop -> side, rows layout with REFS_BESIDE_MLP: every MLP work-group has begun
+        self.mlp_sig = _hip.DeviceSignal(device, polls, self._flags[3])
 
     def begin(self, caller):
         """Order both streams after the caller's work so far (the flags' zero fill included)."""
@@ -380,18 +385,27 @@ class StepState:
 # off for A/B runs.
 ROWS_LAYOUT = True
 ROWS_MAX_MLP_POINTS = 256 * 256
+# Phase B of the rows layout (the coarse refs into their cells: three short launches, ~20 us)
+# on the side stream beside the MLP instead of between the voxel emit and the MLP on the loop
+# stream: the side stream waits (one one-lane wait launch) until EVERY MLP work-group has begun
+# (pcst_noise_mlp_ex's start_counter), so its launches only find the ~21 CUs the one-round MLP
+# leaves idle and never delay an MLP work-group; the query waits for their flag in-kernel.
+# Needs the fused-conditioning MLP (its launch publishes the flag).
+REFS_BESIDE_MLP = True
 
 
 def rows_layout_ok(mlp_points: int) -> bool:
     return ROWS_LAYOUT and mlp_points <= ROWS_MAX_MLP_POINTS
 
 
-def knn_rows_begin(x, M, state, ws, by_downsample=False):
+def knn_rows_begin(x, M, state, ws, by_downsample=False, beside_mlp=False):
     """Phase A of the step's kNN on the side stream, ordered after the loop stream's work so far
     (x is ready): -> (the rows handle for hierarchical_eps(rows=...), start).  by_downsample: the
     next launch on the loop stream, the prepared voxel downsample, publishes the loop -> side flag
     as it begins (pass `start` to downsample_copies) instead of a signal launch here; else start is
-    None.  The side stream signals state.built_sig when done."""
+    None.  beside_mlp (REFS_BESIDE_MLP): phase B follows on the side stream (hierarchical_eps),
+    so phase A signals nothing; else the side stream signals state.built_sig once phase B may
+    run and state.done_sig when done."""
     start = None
     if by_downsample:
         start = state.ready_sig.next_value()
@@ -399,7 +413,10 @@ def knn_rows_begin(x, M, state, ws, by_downsample=False):
         state.ready_sig.signal(torch.cuda.current_stream())
     state.ready_sig.wait(state.side)
     with torch.cuda.stream(state.side):
-        h = _hip.knn3_rows_build(x, M, 2, ws, refs_sig=state.built_sig, done_sig=state.done_sig)
+        if beside_mlp:
+            h = _hip.knn3_rows_build(x, M, 2, ws)
+        else:
+            h = _hip.knn3_rows_build(x, M, 2, ws, refs_sig=state.built_sig, done_sig=state.done_sig)
     return h, start
 
 
@@ -414,6 +431,13 @@ def hierarchical_eps(hp, mlp, xc, xi, x_cat, knn_ws=None, state=None, mlp_waits=
         return hp.upsample_knn(mlp(xc), x_cat, xi)
     main = torch.cuda.current_stream()
     if rows is not None:  # the rows layout: phase A ran beside the downsample (knn_rows_begin)
+        if mlp_signals:  # REFS_BESIDE_MLP: phase B on the side stream once the MLP holds its CUs
+            start = state.mlp_sig.next_value()
+            state.mlp_sig.wait(state.side)
+            with torch.cuda.stream(state.side):
+                _hip.knn3_rows_refs(rows, xi)
+                state.done_sig.signal(state.side)
+            return _hip.knn3_rows_query(mlp(xc, start=start, start_all=True), rows, state.done_sig)
         _hip.knn3_rows_refs(rows, xi, wait=state.built_sig)  # (they wait for phase A in-kernel)
         return _hip.knn3_rows_query(mlp(xc), rows, state.done_sig)
     side = state.side
@@ -724,14 +748,16 @@ class DiffusionProcess:
                     t_in = t_rows[i]
                     if conds is not None:
                         cond_i = conds[i]
-                        mlp = lambda c, wait=None, start=None: npred.forward_cond(  # noqa: E731
-                            c, cond_i, pk, wait, start)
+                        mlp = lambda c, wait=None, start=None, start_all=False: (  # noqa: E731
+                            npred.forward_cond(c, cond_i, pk, wait, start, start_all))
                     else:
                         mlp = lambda c: npred(c, t_in, style_in)  # noqa: E731
                     coeffs = self._coeffs(t, t_prevs[i])
                     if use_hierarchical:
+                        beside = REFS_BESIDE_MLP and conds is not None
                         rows, start = (knn_rows_begin(x, model.config.global_points, state,
-                                                      rows_ws, by_downsample=prepped)
+                                                      rows_ws, by_downsample=prepped,
+                                                      beside_mlp=beside)
                                        if rows_ws is not None else (None, None))
                         xc, xi = hp.downsample_copies(x, 2, vws, prepped, next_seed, pool, start)
                         prep = i + 1 < len(timesteps) and voxel_prep_ok(hp, x, state)
@@ -741,7 +767,8 @@ class DiffusionProcess:
                         x = hierarchical_step(hp, mlp, xc, xi, x_cat, x, source, guidance_scale,
                                               coeffs, ws, state,
                                               mlp_waits=MLP_WAITS and conds is not None,
-                                              mlp_signals=MLP_SIGNALS and conds is not None,
+                                              mlp_signals=(beside if rows is not None else
+                                                           MLP_SIGNALS and conds is not None),
                                               vox_ws=vws if prep else None, pool_seed=next_seed,
                                               rows=rows)
                         prepped, pool = prep, next_seed is not None

@@ -227,7 +227,9 @@ def test_more_loops_than_hw_queues_match_serial():
 def test_mlp_start_signal_orders_the_side_stream():
     """pcst_noise_mlp_ex's start signal (the MLP launch publishes the loop -> side flag as it
     begins): the side stream's work waits for it and sees what the loop stream wrote before the
-    MLP; the MLP's rows equal the plain launch's; f32 precision takes the separate-launch form."""
+    MLP; the MLP's rows equal the plain launch's; f32 precision takes the separate-launch form.
+    signal_all (the flag once every work-group has begun, counted on the signal's word 3): the
+    same ordering, and the counter is zero again after every launch."""
     from pointcloud_style_transfer_amd import _hip
     from pointcloud_style_transfer_amd.config.config import Config
     from pointcloud_style_transfer_amd.models.diffusion_model import NoisePredictor
@@ -235,7 +237,7 @@ def test_mlp_start_signal_orders_the_side_stream():
     dev = torch.device("cuda", 0)
     loop = torch.cuda.Stream(device=dev)
     side = torch.cuda.Stream(device=dev)
-    for prec in ("bf16", "fp32"):
+    for prec, every in (("bf16", False), ("fp32", False), ("bf16", True), ("fp32", True)):
         torch.manual_seed(5)
         npred = NoisePredictor(Config(make_dirs=False, precision=prec)).to(dev).eval()
         pts = torch.randn(2 * 4096, 3, device=dev)
@@ -259,11 +261,12 @@ def test_mlp_start_signal_orders_the_side_stream():
                     with torch.cuda.stream(side):
                         seen = buf.clone()  # ordered after the flag, hence after the fill
                     out = _hip.noise_mlp(pts, 4096, cond, blob, bias, npred.precision_code,
-                                         signal=start)
+                                         signal=start, signal_all=every)
                 outs.append((out, seen, rep))
             torch.cuda.synchronize()
         sig.check()
         assert int(sig.flag[0].item()) == 3
+        assert int(sig.flag[3].item()) == 0, (prec, every)
         for out, seen, rep in outs:
             assert torch.equal(out, ref)
             assert bool((seen == float(rep + 1)).all()), (prec, rep)

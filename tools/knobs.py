@@ -42,6 +42,8 @@ def apply():
         dm.BUILT_SIGNAL = e["PCST_BUILT_SIGNAL"] != "0"
     if "PCST_ROWS_LAYOUT" in e:  # the step's kNN in the rows layout (0: the compact build)
         dm.ROWS_LAYOUT = e["PCST_ROWS_LAYOUT"] != "0"
+    if "PCST_REFS_BESIDE_MLP" in e:  # rows layout: phase B beside the MLP (0: before it)
+        dm.REFS_BESIDE_MLP = e["PCST_REFS_BESIDE_MLP"] != "0"
     if "PCST_SEARCH_BESIDE_MLP" in e:
         dm.SEARCH_BESIDE_MLP = e["PCST_SEARCH_BESIDE_MLP"] != "0"
     if "PCST_KERNEL_SIGNAL" in e:
