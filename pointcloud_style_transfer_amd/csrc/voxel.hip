@@ -608,30 +608,6 @@ __global__ __launch_bounds__(256) void voxf_insert_kernel(const float* __restric
     atomicAdd(&lcnt[slot], 1u);
   }
   __syncthreads();
-#ifdef VOX_WAVE_LIST
-  for (int i = threadIdx.x; i < kVoxLds; i += 256) {  // wave-uniform trip count
-    const unsigned long long kw = lkey[i];
-    int64_t slot = mix32((uint32_t)kw) & (H - 1);
-    bool fresh = false;
-    if (kw) {
-      for (;;) {
-        const unsigned long long old = atomicCAS(&K[slot], 0ull, kw);
-        if (old == 0ull) { fresh = true; break; }
-        if (old == kw) break;
-        slot = (slot + 1) & (H - 1);
-      }
-    }
-    // the new voxels of this wave list their slots with ONE add on the list counter
-    const uint64_t nm = __ballot(fresh);
-    if (nm) {
-      const int lead = __builtin_ctzll(nm);
-      int base = 0;
-      if ((int)(threadIdx.x & 63) == lead) base = atomicAdd(&cnt4[b * 4 + 0], (int)__popcll(nm));
-      base = __shfl(base, lead);
-      if (fresh) vlist[(int64_t)b * N + base + (int)__popcll(nm & lanemask_lt())] = (int32_t)slot;
-    }
-    if (!kw) continue;
-#else
   for (int i = threadIdx.x; i < kVoxLds; i += 256) {
     const unsigned long long kw = lkey[i];
     if (!kw) continue;
@@ -645,7 +621,6 @@ __global__ __launch_bounds__(256) void voxf_insert_kernel(const float* __restric
       if (old == kw) break;
       slot = (slot + 1) & (H - 1);
     }
-#endif
     if (pack) {  // N < 2^20: (index sum << 20) | count in one 64-bit add (sum < 2^40)
       atomicAdd(&tsum[b * H + slot], (lsum[i] << 20) | (unsigned long long)lcnt[i]);
     } else {

@@ -389,9 +389,15 @@ ROWS_MAX_MLP_POINTS = 256 * 256
 # on the side stream beside the MLP instead of between the voxel emit and the MLP on the loop
 # stream: the side stream waits (one one-lane wait launch) until EVERY MLP work-group has begun
 # (pcst_noise_mlp_ex's start_counter), so its launches only find the ~21 CUs the one-round MLP
-# leaves idle and never delay an MLP work-group; the query waits for their flag in-kernel.
-# Needs the fused-conditioning MLP (its launch publishes the flag).
-REFS_BESIDE_MLP = True
+# leaves idle and never delay an MLP work-group.  The MLP's last work-group waits for phase B's
+# flag (pcst_noise_mlp_ex's wait), so the query -- whose work-groups also check it in-kernel --
+# is never dispatched while phase B still needs CUs (spinning query work-groups on every CU
+# would starve it: a SignalTimeout).  Needs the fused-conditioning MLP (its launch publishes the
+# flag).  Measured and OFF: phase B's atomics beside the MLP slow both -- the rank kernel took
+# 150 us on the idle CUs and the MLP 0.178 vs 0.155 ms -- so the step lost time: 2708 / 2707 vs
+# 2739 / 2730 steps/s off, b32 7.70 / 7.66 vs 7.66 / 7.59 ms (profiles/r05/s2c, two alternating
+# passes on one box).  tools/knobs.py may turn it on for A/B runs.
+REFS_BESIDE_MLP = False
 
 
 def rows_layout_ok(mlp_points: int) -> bool:
@@ -437,7 +443,10 @@ def hierarchical_eps(hp, mlp, xc, xi, x_cat, knn_ws=None, state=None, mlp_waits=
             with torch.cuda.stream(state.side):
                 _hip.knn3_rows_refs(rows, xi)
                 state.done_sig.signal(state.side)
-            return _hip.knn3_rows_query(mlp(xc, start=start, start_all=True), rows, state.done_sig)
+            # the MLP's last work-group also waits for phase B's flag: the query's work-groups
+            # (which wait for it in-kernel) must never sit on CUs phase B still needs
+            nc = mlp(xc, state.done_sig, start=start, start_all=True)
+            return _hip.knn3_rows_query(nc, rows, state.done_sig)
         _hip.knn3_rows_refs(rows, xi, wait=state.built_sig)  # (they wait for phase A in-kernel)
         return _hip.knn3_rows_query(mlp(xc), rows, state.done_sig)
     side = state.side

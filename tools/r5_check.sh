@@ -144,6 +144,15 @@ for st in "$@"; do
       done ;;
     timeline)
       python tools/timeline.py "$OUT/prof/run_kernel_trace.csv" --last 18 --show 2 | tee "$OUT/driver_window_timeline.txt" | tail -40 ;;
+    fpsab=*)
+      # fpsab=v_a,v_b: tools/fps_ab.py with the product library and each experiment library
+      VS=${st#fpsab=}
+      for v in prod ${VS//,/ }; do
+        lib=$PWD/pointcloud_style_transfer_amd/libpcst_hip.so
+        if [ "$v" != prod ]; then lib=$PWD/pointcloud_style_transfer_amd/libpcst_hip_$v.so; fi
+        PCST_LIB=$lib timeout -k 10 120 python tools/fps_ab.py > "$OUT/fps_$v.txt" 2>&1
+        rc=$?; cat "$OUT/fps_$v.txt"; if [ $rc -ne 0 ]; then exit $rc; fi
+      done ;;
     loop1000)
       timeout -k 10 600 python -u tools/loop1000_probe.py > "$OUT/loop1000.jsonl" 2> "$OUT/loop1000.err"
       rc=$?; echo "loop1000 rc=$rc"; cat "$OUT/loop1000.jsonl"; if [ $rc -ne 0 ]; then tail -3 "$OUT/loop1000.err"; exit $rc; fi ;;
