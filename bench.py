@@ -58,6 +58,10 @@ def parse():
     # default: one full 1000-step sampling trajectory (t = 999 .. 0)
     ap.add_argument("--steps", type=int, default=1000)
     ap.add_argument("--warmup", type=int, default=3)
+    # HIP events bracket the noise MLP on every EVENT_EVERY-th timed step (the roofline's live
+    # launch duration); every step by default (every 4th measured 2751 / 2745 vs 2742 / 2740
+    # steps/s: the events cost nothing measurable, profiles/r05/s2e)
+    ap.add_argument("--event-every", type=int, default=1)
     ap.add_argument("--clouds-per-gpu", type=int, default=1)
     ap.add_argument("--points", type=int, default=120000)
     ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32"])
@@ -561,7 +565,7 @@ def main():
         with lctx:
             conds = all_conds()  # the loop's one-time conditioning launch, inside the timed region
             for i in range(args.steps):
-                step(i, True)
+                step(i, i % max(1, args.event_every) == 0)
         torch.cuda.synchronize()
         elapsed = time.perf_counter() - t0
         if overlap:
@@ -653,7 +657,10 @@ def main():
                          "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
                          "frac": round(achieved / peak, 4), "traffic": traffic,
                          "algorithmic": f"{FLOP_PER_POINT} FLOP/pt x {2 * C * cfg.global_points} pts",
-                         "avg_launch_ms": round(mlp_ms, 4)},
+                         "avg_launch_ms": round(mlp_ms, 4),
+                         "timed_launches": len(ev),
+                         "timing": f"HIP events on the loop stream around every "
+                                   f"{max(1, args.event_every)}th timed step's MLP launch"},
             "other_precision": other,
             "cpu_baseline": base,
             "quality": quality,

@@ -153,6 +153,24 @@ for st in "$@"; do
         PCST_LIB=$lib timeout -k 10 120 python tools/fps_ab.py > "$OUT/fps_$v.txt" 2>&1
         rc=$?; cat "$OUT/fps_$v.txt"; if [ $rc -ne 0 ]; then exit $rc; fi
       done ;;
+    knnab=*)
+      # knnab=v_a,v_b: tools/knn_check.py result hashes with the product library and each experiment library
+      VS=${st#knnab=}
+      for v in prod ${VS//,/ }; do
+        lib=$PWD/pointcloud_style_transfer_amd/libpcst_hip.so
+        if [ "$v" != prod ]; then lib=$PWD/pointcloud_style_transfer_amd/libpcst_hip_$v.so; fi
+        PCST_LIB=$lib timeout -k 10 120 python tools/knn_check.py > "$OUT/knn_$v.txt" 2>&1
+        rc=$?; grep -v amdgpu.ids "$OUT/knn_$v.txt"; if [ $rc -ne 0 ]; then exit $rc; fi
+      done ;;
+    eventab)
+      # the driver-window bench with MLP events on every timed step vs every 4th (two alternating passes)
+      for pass in 1 2; do
+        for e in 1 4; do
+          timeout -k 10 200 python bench.py ${BENCH#bench.py } --event-every $e > "$OUT/bench_ev$e.$pass.json" 2> "$OUT/bench_ev$e.$pass.err"
+          rc=$?; if [ $rc -ne 0 ]; then tail -3 "$OUT/bench_ev$e.$pass.err"; exit $rc; fi
+          python -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print('events every', sys.argv[2], d['value'], d['ms_per_step'], d['roofline']['avg_launch_ms'])" "$OUT/bench_ev$e.$pass.json" "$e.$pass"
+        done
+      done ;;
     loop1000)
       timeout -k 10 600 python -u tools/loop1000_probe.py > "$OUT/loop1000.jsonl" 2> "$OUT/loop1000.err"
       rc=$?; echo "loop1000 rc=$rc"; cat "$OUT/loop1000.jsonl"; if [ $rc -ne 0 ]; then tail -3 "$OUT/loop1000.err"; exit $rc; fi ;;
