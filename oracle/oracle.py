@@ -363,6 +363,18 @@ def guided_sample_loop(sd, source, cond, steps, scale, replay, global_points=300
     return x
 
 
+def guided_step_given(sd, sched, x, source, style_in, t, t_prev, xi, scale=7.5):
+    """One step of `guided_sample_loop` (diffusion_model.py:240-260) on ONE cloud x [1,N,3] with
+    the CFG rows' subset indices given (xi [2,T], e.g. the product's own device-drawn subset):
+    xc = x_in[b][xi[b]], eps = upsample_knn(noise_predictor(xc)), then the CFG + DDIM update.
+    The subset is checked by the caller (voxel_reps); everything after it is the reference's."""
+    x_in = np.concatenate([_f32(x), _f32(x)])
+    xi = np.asarray(xi)
+    xc = np.stack([x_in[b][xi[b]] for b in range(2)])
+    eps = upsample_knn(noise_predictor(sd, xc, np.full(2, t), style_in), x_in, xi)
+    return guided_update(sched, _f32(x), eps[:1], eps[1:], source, int(t), int(t_prev), scale)
+
+
 def guided_loop_counter(sd, source, cond, x_T, steps, ctr, scale=7.5, global_points=30000,
                         num_timesteps=1000):
     """`guided_sample_loop` (diffusion_model.py:224-261) on ONE cloud with the draws of a
