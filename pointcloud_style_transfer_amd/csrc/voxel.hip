@@ -346,15 +346,9 @@ __global__ void vox_select_kernel(const float* __restrict__ pts, int N, int64_t 
 constexpr int kSelBins = 4096;  // histogram stride per row (the most bins)
 static int vox_sel_shift(int64_t N) { return N <= (4ll << 20) ? 22 : 20; }
 constexpr int kTieCap = 8192;
-#ifndef VOX_CHUNK  // experiment builds may override
-#define VOX_CHUNK 1024
-#endif
-#ifndef VOX_REPS_BLOCKS
-#define VOX_REPS_BLOCKS 64
-#endif
-constexpr int kVoxChunk = VOX_CHUNK;      // points aggregated per workgroup in LDS
+constexpr int kVoxChunk = 1024;           // points aggregated per workgroup in LDS (512 / 2048: DESIGN §6a)
 constexpr int kVoxLds = 2 * kVoxChunk;    // LDS table slots (load factor <= 1/2)
-constexpr int kVoxRepsBlocks = VOX_REPS_BLOCKS;  // workgroups per cloud over the voxel list
+constexpr int kVoxRepsBlocks = 64;        // workgroups per cloud over the voxel list
 
 // Copies.  guided_sample_loop downsamples the CFG batch cat([x] * 2) (diffusion_model.py:244-247):
 // identical clouds.  With copies = k the input is the B distinct clouds and the output has the
