@@ -171,6 +171,17 @@ for st in "$@"; do
           python -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print('events every', sys.argv[2], d['value'], d['ms_per_step'], d['roofline']['avg_launch_ms'])" "$OUT/bench_ev$e.$pass.json" "$e.$pass"
         done
       done ;;
+    graphab)
+      # configs[4]'s batch32 leg (eager and graph) with GRAPH_OVERLAP on and off, two alternating passes
+      for pass in 1 2; do
+        for v in prod PCST_GRAPH_OVERLAP=0; do
+          kv=PCST_NONE=1; if [ "$v" != prod ]; then kv=$v; fi
+          env "$kv" timeout -k 10 300 python tools/bench_knobs.py --gpus 1 --steps 5 --warmup 2 --no-cpu-baseline \
+              --no-encoder --no-other-precision > "$OUT/graph_$v.$pass.json" 2> "$OUT/graph_$v.$pass.err"
+          rc=$?; if [ $rc -ne 0 ]; then tail -3 "$OUT/graph_$v.$pass.err"; exit $rc; fi
+          python -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); b=d['batch32']; print(sys.argv[2], 'eager', b['eager']['ms_per_step'], 'graph', b['graph']['ms_per_step'], 'train', d['train_step']['ms_per_step'])" "$OUT/graph_$v.$pass.json" "$v.$pass"
+        done
+      done ;;
     loop1000)
       timeout -k 10 600 python -u tools/loop1000_probe.py > "$OUT/loop1000.jsonl" 2> "$OUT/loop1000.err"
       rc=$?; echo "loop1000 rc=$rc"; cat "$OUT/loop1000.jsonl"; if [ $rc -ne 0 ]; then tail -3 "$OUT/loop1000.err"; exit $rc; fi ;;
