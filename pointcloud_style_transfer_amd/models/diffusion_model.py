@@ -538,12 +538,6 @@ def hierarchical_step(hp, mlp, xc, xi, x_cat, x, source, guidance_scale, coeffs,
     return _hip.knn3_finish_cfg_ddim(nc, handle, x, source, guidance_scale, coeffs, x_cat=x_cat)
 
 
-# the hipGraph loop (guided_sample_loop(graph=True)) with the kNN build on a forked graph branch
-# beside the noise MLP.  Measured and OFF: 32 clouds 7.86 / 7.80 vs 7.45 / 7.50 ms per step
-# (profiles/r05/s2o) -- the graph launches both branches at once, so the build's work-groups take
-# CUs before the MLP's (the eager loop's side stream waits for the MLP's start flag).
-# tools/knobs.py may turn it on for A/B runs.
-GRAPH_OVERLAP = False
 # device-scope events for the step's cross-stream dependencies (tools/knobs.py: A/B only)
 DEVICE_EVENTS = True
 # The loop -> side dependency (the voxel output is ready) by kernel-side signalling instead of an
@@ -827,30 +821,13 @@ class DiffusionProcess:
         t_cur, coef_cur, seed_cur = t_tab[0].clone(), coef_tab[0].clone(), seed_tab[:1].clone()
         npred.packed()  # weight packing happens outside the capture
         M = model.config.global_points
-        # GRAPH_OVERLAP: the kNN build (positions only) on a forked branch of the graph beside
-        # the noise MLP, joined before the query -- the eager loop's overlap as graph edges (no
-        # device flags: their host counters cannot change between replays)
-        overlap = GRAPH_OVERLAP and overlap_knn_build(2 * B * M)
-        if overlap:
-            side = torch.cuda.Stream(device=device)
-            fork, join = torch.cuda.Event(), torch.cuda.Event()
-            knn_ws = _hip.knn_workspace(2 * B, shape[1], M, device=device)
 
+        # single stream: the kNN build on a forked graph branch beside the MLP measured slower at
+        # 32 clouds, with and without a per-replay MLP start flag gating the branch (7.65-7.86 vs
+        # 7.38-7.50 ms per step, profiles/r05/s2o, s2p)
         def step():
             xc, xi = _hip.voxel_downsample_copies_dseed(x, M, seed_cur, 2)
-            if overlap:
-                main = torch.cuda.current_stream()
-                fork.record(main)
-                side.wait_event(fork)
-                with torch.cuda.stream(side):
-                    h = _hip.knn3_build(x_cat, xi, knn_ws, knn_build_lds_floor(2 * B * M),
-                                        KNN_BUILD_MAX_WG)
-                    join.record(side)
-                nc = npred(xc, t_cur, style_in)
-                main.wait_event(join)
-                eps = _hip.knn3_query(nc, h)
-            else:
-                eps = hp.upsample_knn(npred(xc, t_cur, style_in), x_cat, xi)
+            eps = hp.upsample_knn(npred(xc, t_cur, style_in), x_cat, xi)
             _hip.cfg_ddim_step_dcoef(x, eps[:B], eps[B:], source, guidance_scale, coef_cur,
                                      x_cat=x_cat, out=x)
 

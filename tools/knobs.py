@@ -44,8 +44,6 @@ def apply():
         dm.ROWS_LAYOUT = e["PCST_ROWS_LAYOUT"] != "0"
     if "PCST_REFS_BESIDE_MLP" in e:  # rows layout: phase B beside the MLP (0: before it)
         dm.REFS_BESIDE_MLP = e["PCST_REFS_BESIDE_MLP"] != "0"
-    if "PCST_GRAPH_OVERLAP" in e:  # the hipGraph loop's kNN build on a forked branch
-        dm.GRAPH_OVERLAP = e["PCST_GRAPH_OVERLAP"] != "0"
     if "PCST_SEARCH_BESIDE_MLP" in e:
         dm.SEARCH_BESIDE_MLP = e["PCST_SEARCH_BESIDE_MLP"] != "0"
     if "PCST_KERNEL_SIGNAL" in e:
