@@ -539,7 +539,8 @@ def main():
             next_seed = (_rng.source().device_seed() & (2**64 - 1)
                          if prep and dmod.pool_prep_ok(x) else None)
             x = dmod.hierarchical_step(hp, mlp, xc, xi, x_cat, x, src, 7.5, dp._coeffs(t, t_prev),
-                                       knn_ws, state, mlp_waits=dmod.MLP_WAITS,
+                                       knn_ws, state,
+                                       mlp_waits=True if rows is not None else dmod.MLP_WAITS,
                                        mlp_signals=(dmod.REFS_BESIDE_MLP if rows is not None
                                                     else dmod.MLP_SIGNALS),
                                        vox_ws=vws if prep else None,

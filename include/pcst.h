@@ -344,7 +344,9 @@ int pcst_knn_error(void* workspace, int64_t B, int64_t N, int64_t M, int32_t* er
  *   rows_query (coarse [B,M,3] -> out [B,N,3]): the query and outlier passes of pcst_knn3_query
  *     over every point, known points copying their coarse value; built_flag (the build's
  *     done_flag): every query work-group waits for it itself (as rows_refs; on a timeout it sets
- *     *wait_err and writes eps = 0); grid_cap as pcst_knn3_query.
+ *     *wait_err and writes eps = 0); with wait_err == NULL the stream has already waited for it
+ *     (e.g. pcst_noise_mlp_ex's wait in the MLP launch before the query) and the work-groups only
+ *     check it (a flag short of built_value: eps = 0, nothing read); grid_cap as pcst_knn3_query.
  * Same bits as pcst_knn3_interp on cat([x] * copies).  An index outside [0, N) sets bit 1 of the
  * error word, a chunk or ref range outside the workspace's arrays bits 4 / 8 (the range is then
  * skipped, never read); pcst_knn_rows_stats copies out[0] = error word, out[1..C] chunks per

@@ -683,11 +683,12 @@ def knn3_rows_refs(handle, idx, wait=None):
     return handle
 
 
-def knn3_rows_query(coarse, handle, built=None, grid_cap=0):
+def knn3_rows_query(coarse, handle, built=None, grid_cap=0, waited=False):
     """coarse [C * copies, M, 3] -> [C * copies, N, 3] on the current stream (after
     knn3_rows_refs).  built (the DeviceSignal of the build's done_sig): the query's work-groups
     wait for its last value themselves (a timeout sets its error word and yields eps = 0);
-    grid_cap as knn3_query."""
+    waited=True: the stream already waited for it (the MLP launch's wait), the work-groups only
+    check it; grid_cap as knn3_query."""
     require_device(coarse)
     coarse = _f32(coarse)
     C, copies, N, M = handle.dims
@@ -696,6 +697,8 @@ def knn3_rows_query(coarse, handle, built=None, grid_cap=0):
     out = torch.empty(C * copies, N, 3, dtype=torch.float32, device=coarse.device)
     if built is not None:
         flag, value, _, err, polls = built.wait_args()
+        if waited:
+            err = None
     else:
         flag, value, err, polls = None, ctypes.c_uint32(0), None, ctypes.c_int64(0)
     _call("pcst_knn3_rows_query", _ptr(coarse), _ptr(handle.x), C, copies, N, M, _ptr(out),

@@ -400,6 +400,13 @@ ROWS_MAX_MLP_POINTS = 256 * 256
 REFS_BESIDE_MLP = False
 
 
+# Rows layout: the MLP launch's last work-group waits for phase A's done flag (pcst_noise_mlp_ex's
+# wait) and the query's work-groups only check it, instead of every query work-group waiting with
+# an agent-scope acquire (4 per CU: ~11 us per step, profiles/r05/s2r).  Needs the fused-
+# conditioning MLP (the loop passes mlp_waits); tools/knobs.py may turn it off for A/B runs.
+ROWS_MLP_WAITS = True
+
+
 def rows_layout_ok(mlp_points: int) -> bool:
     return ROWS_LAYOUT and mlp_points <= ROWS_MAX_MLP_POINTS
 
@@ -448,6 +455,8 @@ def hierarchical_eps(hp, mlp, xc, xi, x_cat, knn_ws=None, state=None, mlp_waits=
             nc = mlp(xc, state.done_sig, start=start, start_all=True)
             return _hip.knn3_rows_query(nc, rows, state.done_sig)
         _hip.knn3_rows_refs(rows, xi, wait=state.built_sig)  # (they wait for phase A in-kernel)
+        if ROWS_MLP_WAITS and mlp_waits:  # the MLP's last work-group waits for phase A's end
+            return _hip.knn3_rows_query(mlp(xc, state.done_sig), rows, state.done_sig, waited=True)
         return _hip.knn3_rows_query(mlp(xc), rows, state.done_sig)
     side = state.side
     ready, built = state.ready_ev, state.built_ev
@@ -775,7 +784,8 @@ class DiffusionProcess:
                                      if prep and pool_prep_ok(x) else None)
                         x = hierarchical_step(hp, mlp, xc, xi, x_cat, x, source, guidance_scale,
                                               coeffs, ws, state,
-                                              mlp_waits=MLP_WAITS and conds is not None,
+                                              mlp_waits=(conds is not None if rows is not None
+                                                         else MLP_WAITS and conds is not None),
                                               mlp_signals=(beside if rows is not None else
                                                            MLP_SIGNALS and conds is not None),
                                               vox_ws=vws if prep else None, pool_seed=next_seed,

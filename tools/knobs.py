@@ -44,6 +44,8 @@ def apply():
         dm.ROWS_LAYOUT = e["PCST_ROWS_LAYOUT"] != "0"
     if "PCST_REFS_BESIDE_MLP" in e:  # rows layout: phase B beside the MLP (0: before it)
         dm.REFS_BESIDE_MLP = e["PCST_REFS_BESIDE_MLP"] != "0"
+    if "PCST_ROWS_MLP_WAITS" in e:  # rows layout: the MLP waits for phase A (0: the query does)
+        dm.ROWS_MLP_WAITS = e["PCST_ROWS_MLP_WAITS"] != "0"
     if "PCST_SEARCH_BESIDE_MLP" in e:
         dm.SEARCH_BESIDE_MLP = e["PCST_SEARCH_BESIDE_MLP"] != "0"
     if "PCST_KERNEL_SIGNAL" in e:
