@@ -495,8 +495,8 @@ def main():
         vws = _hip.voxel_copies_workspace(C, args.points, 2, device=device)
         pk = npred.packed()  # the loop changes no weight (as guided_sample_loop)
         S = len(timesteps)
-        timing_event = ((lambda: _hip.DeviceEvent(timing=True)) if dmod.DEVICE_EVENTS
-                        else (lambda: torch.cuda.Event(enable_timing=True)))
+        # device-scope events: no L2 writeback bubble around the timed kernel
+        timing_event = lambda: _hip.DeviceEvent(timing=True)  # noqa: E731
         conds = None  # every step's conditioning rows, one launch per loop (as guided_sample_loop)
 
         def all_conds():
@@ -513,22 +513,20 @@ def main():
             # the rows layout: the kNN's positions-only phase on the side stream beside the
             # downsample (as guided_sample_loop)
             rows, start = (dmod.knn_rows_begin(x, cfg.global_points, state, rows_ws,
-                                               by_downsample=prepped,
-                                               beside_mlp=dmod.REFS_BESIDE_MLP)
+                                               by_downsample=prepped)
                            if rows_ws is not None else (None, None))
             xc, xi = hp.downsample_copies(x, 2, vws, prepped, next_seed, pool, start)
 
-            def mlp(xc_, wait=None, start=None, start_all=False):
+            def mlp(xc_, wait=None, start=None):
                 if not timed:
-                    return npred.forward_cond(xc_, cnd, pk, wait, start, start_all)
-                # on the stream the MLP runs on; device-scope fences (no L2 writeback bubble
-                # around the timed kernel) unless tools/knobs.py turned them off
+                    return npred.forward_cond(xc_, cnd, pk, wait, start)
+                # on the stream the MLP runs on
                 e0, e1 = timing_event(), timing_event()
                 blob, bias = pk[:2]
                 e0.record()
                 nc_ = _hip.noise_mlp(xc_.reshape(-1, 3), cfg.global_points, cnd, blob, bias,
-                                     npred.precision_code, wait=wait, signal=start,
-                                     signal_all=start_all).view(2 * C, -1, 3)
+                                     npred.precision_code, wait=wait,
+                                     signal=start).view(2 * C, -1, 3)
                 e1.record()
                 ev.append((e0, e1))
                 return nc_
@@ -539,11 +537,7 @@ def main():
             next_seed = (_rng.source().device_seed() & (2**64 - 1)
                          if prep and dmod.pool_prep_ok(x) else None)
             x = dmod.hierarchical_step(hp, mlp, xc, xi, x_cat, x, src, 7.5, dp._coeffs(t, t_prev),
-                                       knn_ws, state,
-                                       mlp_waits=True if rows is not None else dmod.MLP_WAITS,
-                                       mlp_signals=(dmod.REFS_BESIDE_MLP if rows is not None
-                                                    else dmod.MLP_SIGNALS),
-                                       vox_ws=vws if prep else None,
+                                       knn_ws, state, fused=True, vox_ws=vws if prep else None,
                                        pool_seed=next_seed, rows=rows)
             prepped, pool = prep, next_seed is not None
 

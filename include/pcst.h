@@ -293,35 +293,20 @@ int pcst_knn3_interp(const float* coarse, const float* orig, const int64_t* idx,
  * CUs the noise MLP leaves idle; 0 = no floor (knn3_interp passes 0).  max_wg (> 0): at most
  * this many workgroups per build launch over all clouds (each kernel strides over its work), so a
  * side-stream build holds few CUs; 0 = the natural grids (knn3_interp passes 0).
- * built_flag / built_value (query, finish, finish_cfg_ddim; NULL: none): the flag the build's
+ * built_flag / built_value (query; NULL: none): the flag the build's
  * producer publishes (pcst_signal_write) -- the consumer reads the workspace only if the flag
  * holds the value when its work-groups start; otherwise (a cross-stream wait that gave up) it
  * leaves the workspace alone and writes 0 for eps, so a timed-out wait can never make it read a
  * half-built workspace.  The caller reports the wait's error word.
- * grid_cap (query, search): the query grid's workgroups over all clouds of the launch (each
- * strides over its cloud's chunks; the result does not depend on it); <= 0: 16384, the winner
- * of the round-4 A/B at 32 clouds (profiles/r04/a5). */
+ * grid_cap (query): at most this many query work-groups over all clouds of the launch (the result
+ * does not depend on it); <= 0: the resident grid (4 work-groups per CU).  The query's waves are
+ * persistent: a wave's first chunk is its index, the next ones come from work counters of its CFG
+ * row (eight per row), which the build zeroes and the query's outlier launch zeroes again. */
 int pcst_knn3_build(const float* orig, const int64_t* idx, int64_t B, int64_t N, int64_t M,
                     int64_t lds_floor, int64_t max_wg, void* workspace, void* stream);
 int pcst_knn3_query(const float* coarse, const float* orig, int64_t B, int64_t N, int64_t M,
                     float* out, void* workspace, const uint32_t* built_flag, uint32_t built_value,
                     int64_t grid_cap, void* stream);
-/* The query in two halves (the same bits as pcst_knn3_query).  search (after build; positions
- * only): every unknown row's three neighbours and float64 IDW weights into the workspace, so it
- * can run beside the noise MLP too; finish: out [B,N,3] from coarse [B,M,3] (the gathers and the
- * weighted sums).  finish_cfg_ddim: the finish of a CFG batch (B = 2C clouds: rows c and C + c are
- * the conditional and unconditional eps of cloud c) fused with pcst_cfg_ddim_step's update of x
- * [C,N,3] (source [C,N,3] or NULL, x_cat [2C,N,3] or NULL). */
-int pcst_knn3_search(const float* orig, int64_t B, int64_t N, int64_t M, void* workspace,
-                     int64_t grid_cap, void* stream);
-int pcst_knn3_finish(const float* coarse, int64_t B, int64_t N, int64_t M, float* out,
-                     void* workspace, const uint32_t* built_flag, uint32_t built_value,
-                     void* stream);
-int pcst_knn3_finish_cfg_ddim(const float* coarse, int64_t B, int64_t N, int64_t M, void* workspace,
-                              const float* x, const float* source, float guidance_scale,
-                              float sqrt_1m_at, float sqrt_at_eps, float sqrt_aprev,
-                              float sqrt_1m_aprev, float* x_out, float* x_cat,
-                              const uint32_t* built_flag, uint32_t built_value, void* stream);
 /* diagnostics of the last query on a workspace: out[0] error flag, out[1..B] query chunks per
  * cloud, out[1+B..2B] outlier queries per cloud (device int32 buffer of 1 + 2B) */
 int pcst_knn_stats(void* workspace, int64_t B, int64_t N, int64_t M, int32_t* out, void* stream);
@@ -334,19 +319,21 @@ int pcst_knn_error(void* workspace, int64_t B, int64_t N, int64_t M, int32_t* er
  *     per-cell counts, scan, the query chunks over all points, the points in cell order.
  *     refs_flag / done_flag (NULL: none): written with their values once rows_refs may run on
  *     another stream (after the scan) and once the whole build is done (after the fill);
- *   rows_refs (idx [B,M] int64): each ref marks its point known (the last j wins) and takes a slot
- *     at the front of its point's cell range and one at the front of its brick's; a ref beyond
- *     either range's rows (repeated indices piling up) also goes to the row's overflow list, which
- *     the query offers wherever its scanned box holds them.  wait_flag (NULL: none): the kernel
- *     first waits, in every work-group, until the flag holds wait_value (the side stream's
- *     pcst_signal_write after rows_build), at most max_polls polls (<= 0: ~10 s); a wait that gives
- *     up sets *wait_err and places nothing (as pcst_signal_wait's error word);
+ *   rows_refs (idx [B,M] int64), one launch: each ref marks its point known (the last j wins),
+ *     takes a rank in its point's cell and the slot start(cell) + rank at the front of the cell's
+ *     row range (the build marks every slot empty first); a ref beyond its cell's rows (repeated
+ *     indices piling up) goes to the row's overflow list, which the query offers wherever its
+ *     scanned box holds them.  wait_flag (NULL: none): the kernel first waits, in every
+ *     work-group, until the flag holds wait_value (the side stream's pcst_signal_write after
+ *     rows_build), at most max_polls polls (<= 0: ~10 s); a work-group whose wait gives up sets
+ *     *wait_err and writes nothing (pass wait_err to rows_query as refs_err);
  *   rows_query (coarse [B,M,3] -> out [B,N,3]): the query and outlier passes of pcst_knn3_query
  *     over every point, known points copying their coarse value; built_flag (the build's
  *     done_flag): every query work-group waits for it itself (as rows_refs; on a timeout it sets
  *     *wait_err and writes eps = 0); with wait_err == NULL the stream has already waited for it
  *     (e.g. pcst_noise_mlp_ex's wait in the MLP launch before the query) and the work-groups only
- *     check it (a flag short of built_value: eps = 0, nothing read); grid_cap as pcst_knn3_query.
+ *     check it (a flag short of built_value: eps = 0, nothing read); refs_err (NULL: none): the
+ *     rows_refs wait's error word -- nonzero: eps = 0, nothing read; grid_cap as pcst_knn3_query.
  * Same bits as pcst_knn3_interp on cat([x] * copies).  An index outside [0, N) sets bit 1 of the
  * error word, a chunk or ref range outside the workspace's arrays bits 4 / 8 (the range is then
  * skipped, never read); pcst_knn_rows_stats copies out[0] = error word, out[1..C] chunks per
@@ -361,7 +348,7 @@ int pcst_knn3_rows_refs(const float* x, const int64_t* idx, int64_t C, int64_t c
 int pcst_knn3_rows_query(const float* coarse, const float* x, int64_t C, int64_t copies, int64_t N,
                          int64_t M, float* out, void* workspace, const uint32_t* built_flag,
                          uint32_t built_value, int32_t* wait_err, int64_t max_polls,
-                         int64_t grid_cap, void* stream);
+                         const int32_t* refs_err, int64_t grid_cap, void* stream);
 int pcst_knn_rows_stats(void* workspace, int64_t C, int64_t copies, int64_t N, int64_t M,
                         int32_t* out, void* stream);
 

@@ -54,16 +54,13 @@ SIGNATURES = {
     "pcst_cfg_ddim_step_dcoef": [_P, _P, _P, _P, _I, ctypes.c_float, _P, _P, _P, _P],
     "pcst_voxel_downsample_copies_dseed": [_P, _I, _I, _I, _I, _P, _P, _P, _P, _P],
     "pcst_knn3_query": [_P, _P, _I, _I, _I, _P, _P, _P, ctypes.c_uint32, _I, _P],
-    "pcst_knn3_search": [_P, _I, _I, _I, _P, _I, _P],
-    "pcst_knn3_finish": [_P, _I, _I, _I, _P, _P, _P, ctypes.c_uint32, _P],
-    "pcst_knn3_finish_cfg_ddim": [_P, _I, _I, _I, _P, _P, _P, _F, _F, _F, _F, _F, _P, _P, _P,
-                                  ctypes.c_uint32, _P],
     "pcst_knn_error": [_P, _I, _I, _I, _P, _P],
     "pcst_knn_stats": [_P, _I, _I, _I, _P, _P],
     "pcst_knn_rows_workspace_size": [_I, _I, _I, _I, _SZ],
     "pcst_knn3_rows_build": [_P, _I, _I, _I, _I, _P, _P, ctypes.c_uint32, _P, ctypes.c_uint32, _P],
     "pcst_knn3_rows_refs": [_P, _P, _I, _I, _I, _I, _P, _P, ctypes.c_uint32, _P, _I, _P],
-    "pcst_knn3_rows_query": [_P, _P, _I, _I, _I, _I, _P, _P, _P, ctypes.c_uint32, _P, _I, _I, _P],
+    "pcst_knn3_rows_query": [_P, _P, _I, _I, _I, _I, _P, _P, _P, ctypes.c_uint32, _P, _I, _P, _I,
+                             _P],
     "pcst_knn_rows_stats": [_P, _I, _I, _I, _I, _P, _P],
     "pcst_noise_mlp_blob_bytes": [ctypes.c_int],
     "pcst_noise_cond": [_P, _P, _I, _P, _P, _P, _P, _P, _P, _P, _P],
@@ -532,8 +529,8 @@ def knn3_query(coarse, handle, built=None, grid_cap=0):
     """Phase 2 of knn3_interp on the current stream: coarse [B,M,3] -> [B,N,3].  built (the
     DeviceSignal the side-stream build signalled): the query reads the workspace only if that
     flag holds its last value (pcst.h: a timed-out wait then yields eps = 0, reported by the
-    signal's error word, instead of a read of a half-built workspace).  grid_cap: the query
-    grid's workgroups over all clouds (0: the library default; the result never depends on
+    signal's error word, instead of a read of a half-built workspace).  grid_cap: at most this
+    many query work-groups over all clouds (0: the resident grid; the result never depends on
     it)."""
     orig, idx, ws = handle
     require_device(coarse)
@@ -545,60 +542,6 @@ def knn3_query(coarse, handle, built=None, grid_cap=0):
     out = torch.empty(B, N, 3, dtype=torch.float32, device=orig.device)
     _call("pcst_knn3_query", _ptr(coarse), _ptr(orig), B, N, M, _ptr(out), _ptr(ws),
           *_built_args(built), int(grid_cap), _stream())
-    return out
-
-
-def knn3_search(handle, grid_cap=0):
-    """The positions-only half of knn3_query on the current stream (after knn3_build on the
-    handle's workspace): every row's three neighbours and IDW weights into the workspace, so
-    that only the gather of the coarse values (knn3_finish / knn3_finish_cfg_ddim) waits for
-    the noise MLP.  Returns the handle."""
-    orig, idx, ws = handle
-    B, N, _ = orig.shape
-    _call("pcst_knn3_search", _ptr(orig), B, N, idx.shape[1], _ptr(ws), int(grid_cap), _stream())
-    return handle
-
-
-def _coarse_for(coarse, handle, name):
-    orig, idx, _ = handle
-    require_device(coarse)
-    coarse = _f32(coarse)
-    B, N, _ = orig.shape
-    M = idx.shape[1]
-    if coarse.shape != (B, M, 3):
-        raise RuntimeError(f"{name}: coarse {tuple(coarse.shape)} != {(B, M, 3)}")
-    return coarse, B, N, M
-
-
-def knn3_finish(coarse, handle, built=None):
-    """After knn3_search: coarse [B,M,3] -> [B,N,3], the same bits as knn3_query (built: as
-    knn3_query)."""
-    coarse, B, N, M = _coarse_for(coarse, handle, "knn3_finish")
-    out = torch.empty(B, N, 3, dtype=torch.float32, device=coarse.device)
-    _call("pcst_knn3_finish", _ptr(coarse), B, N, M, _ptr(out), _ptr(handle[2]),
-          *_built_args(built), _stream())
-    return out
-
-
-def knn3_finish_cfg_ddim(coarse, handle, x, source, guidance_scale, coeffs, x_cat=None, out=None,
-                         built=None):
-    """After knn3_search on the CFG batch (2C clouds): cfg_ddim_step(x, eps[:C], eps[C:], ...)
-    with eps = knn3_finish(coarse, handle), in one launch and with the same bits."""
-    coarse, B, N, M = _coarse_for(coarse, handle, "knn3_finish_cfg_ddim")
-    require_device(x, source, x_cat)
-    x = _f32(x)
-    if B % 2 or x.shape != (B // 2, N, 3):
-        raise RuntimeError(f"knn3_finish_cfg_ddim: x {tuple(x.shape)} != {(B // 2, N, 3)}")
-    if source is not None and source.shape != x.shape:
-        raise RuntimeError("knn3_finish_cfg_ddim: source shape != x shape")
-    if x_cat is not None and x_cat.shape != (B, N, 3):
-        raise RuntimeError("knn3_finish_cfg_ddim: x_cat shape != (2C, N, 3)")
-    if out is None:
-        out = torch.empty_like(x)
-    c1, c2, c3, c4 = (float(c) for c in coeffs)
-    _call("pcst_knn3_finish_cfg_ddim", _ptr(coarse), B, N, M, _ptr(handle[2]), _ptr(x),
-          _ptr(source), float(guidance_scale), c1, c2, c3, c4, _ptr(out), _ptr(x_cat),
-          *_built_args(built), _stream())
     return out
 
 
@@ -635,10 +578,13 @@ def knn_rows_workspace(C, copies, N, M, device):
 
 
 class KnnRows:
-    """Handle of a rows-layout build: the clouds x [C,N,3], the CFG copies, M and the workspace."""
+    """Handle of a rows-layout build: the clouds x [C,N,3], the CFG copies, M and the workspace;
+    refs_err: the error word of the ref placement's wait (knn3_rows_refs(wait=...)), which the
+    query checks."""
 
     def __init__(self, x, copies, M, ws):
         self.x, self.copies, self.M, self.ws = x, int(copies), int(M), ws
+        self.refs_err = None
 
     @property
     def dims(self):
@@ -664,10 +610,12 @@ def knn3_rows_build(x, M, copies=1, ws=None, refs_sig=None, done_sig=None):
 
 
 def knn3_rows_refs(handle, idx, wait=None):
-    """Phase B on the current stream (after knn3_rows_build on the handle): the coarse indices
-    idx [C * copies, M] into the rows layout.  wait (a DeviceSignal): the launch itself waits for
-    its last signal (phase A on another stream) instead of a wait launch ahead of it; a wait that
-    gives up sets the signal's error word (its check() raises).  Returns the handle."""
+    """Phase B on the current stream (after knn3_rows_build on the handle), one launch: the
+    coarse indices idx [C * copies, M] into the rows layout.  wait (a DeviceSignal): the launch
+    itself waits for its last signal (phase A on another stream) instead of a wait launch ahead
+    of it; a wait that gives up places nothing and sets the signal's error word (its check()
+    raises), which the handle's query then also reads (eps = 0, nothing read).  Returns the
+    handle."""
     require_device(idx)
     idx = _i64(idx)
     C, copies, N, M = handle.dims
@@ -678,6 +626,7 @@ def knn3_rows_refs(handle, idx, wait=None):
         flag, value, _, err, polls = wait.wait_args()
     else:
         flag, value, err, polls = None, ctypes.c_uint32(0), None, ctypes.c_int64(0)
+    handle.refs_err = err
     _call("pcst_knn3_rows_refs", _ptr(handle.x), _ptr(idx), C, copies, N, M, _ptr(handle.ws), flag,
           value, err, polls, _stream())
     return handle
@@ -702,7 +651,7 @@ def knn3_rows_query(coarse, handle, built=None, grid_cap=0, waited=False):
     else:
         flag, value, err, polls = None, ctypes.c_uint32(0), None, ctypes.c_int64(0)
     _call("pcst_knn3_rows_query", _ptr(coarse), _ptr(handle.x), C, copies, N, M, _ptr(out),
-          _ptr(handle.ws), flag, value, err, polls, int(grid_cap), _stream())
+          _ptr(handle.ws), flag, value, err, polls, handle.refs_err, int(grid_cap), _stream())
     return out
 
 
@@ -746,8 +695,8 @@ def noise_mlp(pts, points_per_cloud, cond, blob, bias, precision, out=None, wait
               signal=None, signal_all=False):
     """pts [P,3] (P = clouds*points_per_cloud, cloud-major) -> eps [P,3].
     wait (a DeviceSignal signalled on another stream): work queued after the MLP on this stream
-    is also ordered after that signal -- at precisions 2 and 3 by the MLP's last work-group
-    (pcst_noise_mlp_ex's wait), otherwise by a wait launch after it.
+    is also ordered after that signal -- at precision 1 (bf16, the solo kernel) by the MLP's
+    last work-group (pcst_noise_mlp_ex's wait), otherwise by a wait launch after it.
     signal ((flag, value) from DeviceSignal.next_value()): the value is published as the MLP
     launch begins (everything queued before it on this stream is then done) --
     pcst_noise_mlp_ex's start signal.  signal_all: published once every work-group of the launch
@@ -1343,7 +1292,6 @@ def voxel_downsample_copies_dseed(points, target, seed_dev, copies):
 # every public wrapper launches on its tensors' device (see _on_tensor_device)
 _GUARDED = ("square_distance", "index_points", "fps", "ball_query", "group_gather",
             "voxel_downsample", "voxel_stats", "knn3_build", "knn3_query", "knn3_interp",
-            "knn3_search", "knn3_finish", "knn3_finish_cfg_ddim",
             "noise_cond", "noise_mlp", "cfg_ddim_step", "cfg_ddim_voxel_prep", "pointwise_linear", "relu_bwd",
             "linear_wgrad", "gemm_nt_bf16", "channel_stats", "bn_train_stats", "affine_act", "chamfer_fwd",
             "chamfer_bwd", "l1_fwd", "l1_bwd", "knn_dist", "emd_greedy", "voxel_center_dist",

@@ -21,14 +21,26 @@ __device__ __forceinline__ void cloud_stats_block(const float* __restrict__ P, i
                                                   StatRec* __restrict__ part) {
   float mn[3] = {3.4e38f, 3.4e38f, 3.4e38f}, mx[3] = {-3.4e38f, -3.4e38f, -3.4e38f};
   double s[3] = {0, 0, 0}, ss[3] = {0, 0, 0};
-  for (int n = blk * 256 + threadIdx.x; n < N; n += kStatBlocks * 256) {
+  // eight of the thread's points per round, all loads in flight before the (in-order) sums
+  constexpr int kU = 8, kStride = kStatBlocks * 256;
+  for (int n0 = blk * 256 + threadIdx.x; n0 < N; n0 += kU * kStride) {
+    float v[kU][3];
 #pragma unroll
-    for (int c = 0; c < 3; ++c) {
-      const float v = P[n * 3 + c];
-      mn[c] = fminf(mn[c], v);
-      mx[c] = fmaxf(mx[c], v);
-      s[c] += v;
-      ss[c] += (double)v * v;
+    for (int u = 0; u < kU; ++u) {
+      const int n = n0 + u * kStride;
+#pragma unroll
+      for (int c = 0; c < 3; ++c) v[u][c] = n < N ? P[n * 3 + c] : 0.0f;
+    }
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      if (n0 + u * kStride >= N) break;
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        mn[c] = fminf(mn[c], v[u][c]);
+        mx[c] = fmaxf(mx[c], v[u][c]);
+        s[c] += v[u][c];
+        ss[c] += (double)v[u][c] * v[u][c];
+      }
     }
   }
 #pragma unroll

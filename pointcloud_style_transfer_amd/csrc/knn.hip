@@ -30,6 +30,18 @@
 // go to the outlier list: one wave per outlier query searches shells of bricks around it
 // (knn_outlier_brick_kernel).
 //
+// Chunk scheduling (round 6).  A chunk's time is a chain of dependent loads and one or two
+// staged windows (8-45 us, median ~19), and there are more chunk-waves than wave slots (6670 vs
+// 4096 at the bench's two CFG rows).  With one wave per chunk a wave slot is freed only when its
+// whole work-group retires, so the launch was two rounds of the slowest chunk of four.  Now the
+// query grid is the resident one (4 work-groups per CU) and every wave is persistent: its first
+// chunk is static (its wave index), the next ones come from a work counter of its CFG row, sharded
+// over eight counters (work-group m of a row takes from counter m % 8, i.e. all its users sit on
+// one XCD under round-robin placement), so a wave that finishes early takes the next chunk
+// instead of idling and no counter sees more than an eighth of the dequeues (one word saturates
+// at ~88 dequeues per us: MI355X_MICROARCH.md, dequeue).  The counters live in the build's zeroed
+// state; the outlier launch zeroes them again for the next query on the same workspace.
+//
 // Launches: memset, pre (cloud stats + known rows), count (grid params, per-cell counts with
 // each element's rank in its cell, per-tile sums, known-row copies), scan (single pass: tile
 // offsets from the per-tile sums; the chunk list), fill (no atomics: start + rank), query,
@@ -48,23 +60,13 @@ constexpr int kKnnTile = 4096;           // scan tile (256 threads x 16)
 constexpr int kKnnMaxTiles = 1024;       // per-block LDS tile histogram in the count kernel
 constexpr int kPreKnownBlocks = 64;      // known-row scatter blocks per cloud in the pre kernel
 constexpr int kCountPerBlock = 1024;     // elements per count-kernel block (4 per thread)
-constexpr int kQueryBlocks = 1024;       // query workgroups per cloud (grid-stride over chunks)
-// the query grid's cap over all clouds of one launch, when the caller passes grid_cap <= 0: at
-// 32 clouds (64 CFG rows) 16384 workgroups let each wave stride over several chunks (r04 A/B,
-// profiles/r04/a5: b32 8.79 -> 8.67 ms); at one cloud the per-cloud cap (kQueryBlocks) binds first
-constexpr int64_t kQueryGridCapDefault = 16384;
-constexpr int kQueryBlocksMin = 16;
 constexpr int kOvlLds = 256;             // overflow refs staged in LDS per query work-group
 constexpr int kOutlierBrickBlocks = 256; // outlier workgroups per cloud (brick search, 4 queries)
+constexpr int kQueryShards = 8;          // work counters per CFG row (one per XCD)
+constexpr int kCtrStride = 64;           // int32 words between counters: each on its own 256-B line
+constexpr int kBrickBatch = 4;           // bricks per brick-copy work item of the rows query
+constexpr int kQueryBlocksPerCU = 4;     // resident query work-groups per CU (waves_per_eu 4, 38 KiB LDS)
 
-
-// A query row's IDW weights and ref indices (kk of them used), written by the deferred search
-// and applied to the coarse values by the finish pass (pcst_knn3_search / pcst_knn3_finish).
-struct NbrRec {
-  double u0, u1, u2;
-  int j0, j1;
-  int j2, kk;
-};
 
 struct KnnWS {
   StatRec* stats;    // [B][kStatBlocks]
@@ -75,9 +77,9 @@ struct KnnWS {
   uint2* chunks;     // [B][maxch] query ranges [q0, q1) of <= 64 queries inside one brick
   int32_t* olist;    // [B][N]   outlier query rows
   float* obound;     // [B][N]   their kk-th best squared distance so far (rounded up; inf: none)
-  NbrRec* nbr;       // [B][N]   a query row's IDW weights (the deferred search: pcst_knn3_search)
   // zeroed every call (contiguous):
   int32_t* err;
+  int32_t* qctr;     // [B][8][kCtrStride] the query's work counters (chunk scheduling), one per line
   int32_t* nchunk;   // [B]
   int32_t* ocount;   // [B]
   uint32_t* known;   // [B][N]  (j+1 of the last coarse row writing n, 0 = query)
@@ -106,8 +108,8 @@ static KnnWS carve_knn(void* base, int64_t B, int64_t N, int64_t M) {
   w.chunks = c.take<uint2>(B * w.maxch);
   w.olist = c.take<int32_t>(B * N);
   w.obound = c.take<float>(B * N);
-  w.nbr = c.take<NbrRec>(B * N);
   w.err = c.take<int32_t>(4);
+  w.qctr = c.take<int32_t>(B * kQueryShards * kCtrStride);
   w.nchunk = c.take<int32_t>(B);
   w.ocount = c.take<int32_t>(B);
   w.known = c.take<uint32_t>(B * N);
@@ -444,36 +446,41 @@ __global__ __launch_bounds__(256) void knn_fill_kernel(const float* __restrict__
 // (before the coarse indices exist): every row of cloud cl is binned (statistics, grid, per-cell
 // row counts with each row's rank, the scan -- row starts and the chunk list over ALL rows --
 // and the fill: rows in cell order), shared by the `copies` CFG rows b = c * C + cl of the cloud.
-// Phase B (after the downsample), three short launches: (1) ref j of row b marks its point n
-// known (atomicMax: the last j wins, as the reference's index assignment) and takes a rank in
-// n's cell (atomicAdd); (2) one wave per brick turns its 64 cells' counts into slot offsets: the
-// brick's refs are one contiguous run at the front of the brick's row range, cell after cell
-// (the compact layout's order inside a brick); (3) each ref is stored at its slot.  Distinct refs
-// always fit (a cell has one row per distinct ref); refs repeating an index (the downsample's
-// representatives may share one: ~200 of 30000 per row in the bench) fit while their cell has
-// rows to spare, and the rest go to the row's overflow list, which the query offers wherever its
-// scanned box holds them.  The query skips known rows (copying their coarse value instead).  The
-// grid is the compact layout's (the same statistics and ref count), so both layouts give the
-// same bits.
+// Phase B (after the downsample), ONE launch: ref j of row b marks its point n known (atomicMax:
+// the last j wins, as the reference's index assignment), takes a rank in n's cell (atomicAdd) and
+// is stored at slot start(cell) + rank: a cell's refs are the front of the cell's own row range.
+// The outlier pass scans whole bricks, so it reads a second copy in which each brick's refs are
+// one run at the front of the brick's row range: the query's waves build it once they run out of
+// chunks (the query's tail, where waves otherwise idle behind the last long chunks; the outlier
+// launch is its only reader).  Distinct refs always fit (a cell has one row per distinct ref);
+// refs repeating an index (the downsample's representatives may share one: ~200 of 30000 per row
+// in the bench) fit while their cell has rows to spare, and the rest go to the row's overflow
+// list, which the query and the outlier pass offer wherever their scanned box holds them.
+// (Round 5 packed a brick's refs into one run with a cell-scan launch between a rank and a place
+// launch: three launches on the step's critical path instead of one.)  The query skips known rows
+// (copying their coarse value instead).  The grid is the compact layout's (the same statistics
+// and ref count), so both layouts give the same bits.
 struct KnnRowsWS {
   StatRec* stats;    // [C][kStatBlocks]
   float* gp;         // [C][8]
   int32_t* qorder;   // [C][N] rows in cell order
   int2* crank;       // [C][N] (cell, rank in cell)
   uint2* chunks;     // [C][maxch] row ranges [q0, q1) of <= 64 rows inside one brick
-  float4* refs;      // [B][N] refs (x, y, z, j), per brick at the front of its row range
+  float4* refs;      // [B][N] refs (x, y, z, j) at the front of their cell's row range
+  float4* brefs;     // [B][N] the placed refs at the front of their brick's row range (outlier
+                     // pass; built by the query's waves)
   float4* over;      // [B][M] overflow refs (an index named again)
-  uint32_t* rrank;   // [B][M] ref j's rank in its cell (~0u: overflow or a bad index)
-  uint64_t* cw;      // [B][Cpad] a cell's refs: first slot | count << 32
   int32_t* olist;    // [B][N] outlier query rows
   float* obound;     // [B][N]
   // zeroed every build (contiguous):
   int32_t* err;
+  int32_t* qctr;     // [B][2][8][kCtrStride] the query's work counters (chunks, brick batches)
   int32_t* nchunk;   // [C]
   int32_t* ocount;   // [B]
   int32_t* ovn;      // [B] overflow refs
   uint32_t* known;   // [B][N] j+1 of the last ref naming n, 0 = a query row
   uint32_t* rcnt;    // [B][Cpad] refs ranked per cell
+  uint32_t* bcnt;    // [B][Cpad / 64] the brick copy's ref counts (written if nonzero)
   uint64_t* tsum;    // [C][T]
   uint64_t* cnt;     // [C][Cpad] packed counts (0 | rows << 32) -> starts
   int64_t B, C, Cmax, T, Cpad, maxch;
@@ -495,17 +502,18 @@ static KnnRowsWS carve_knn_rows(void* base, int64_t C, int64_t copies, int64_t N
   w.crank = c.take<int2>(C * N);
   w.chunks = c.take<uint2>(C * w.maxch);
   w.refs = c.take<float4>(w.B * N);
+  w.brefs = c.take<float4>(w.B * N);
   w.over = c.take<float4>(w.B * M);
-  w.rrank = c.take<uint32_t>(w.B * M);
-  w.cw = c.take<uint64_t>(w.B * w.Cpad);
   w.olist = c.take<int32_t>(w.B * N);
   w.obound = c.take<float>(w.B * N);
   w.err = c.take<int32_t>(4);
+  w.qctr = c.take<int32_t>(w.B * 2 * kQueryShards * kCtrStride);
   w.nchunk = c.take<int32_t>(C);
   w.ocount = c.take<int32_t>(w.B);
   w.ovn = c.take<int32_t>(w.B);
   w.known = c.take<uint32_t>(w.B * N);
   w.rcnt = c.take<uint32_t>(w.B * w.Cpad);
+  w.bcnt = c.take<uint32_t>(w.B * (w.Cpad / 64));
   w.tsum = c.take<uint64_t>(C * w.T);
   w.cnt = c.take<uint64_t>(C * w.Cpad);
   w.bytes = c.bytes();
@@ -541,83 +549,43 @@ __device__ bool block_wait_flag(const uint32_t* flag, uint32_t value, int32_t* w
   return s_ok != 0;
 }
 
-// Phase B (1): ref j of CFG row b (cloud b % C): its known mark and its rank in its cell (both
-// atomics issued together); a rank beyond the cell's rows sends the ref to the overflow list.
+// Phase B: ref j of CFG row b (cloud b % C): its known mark (the last j wins), its rank in its
+// point's cell (both atomics issued together) and its slot start(cell) + rank at the front of the
+// cell's row range; a rank beyond the cell's rows sends the ref to the overflow list instead.
 // wflag (optional): the side stream's phase-A flag; every work-group waits until it holds wvalue
 // (the consumer side of the guide's hand-off: one relaxed poll loop, one agent-scope acquire, a
-// barrier), so no wait launch sits in front of this one; a wait that gives up sets werr and the
-// work-group leaves the workspace alone (the query's flag test then yields eps = 0 and the
-// caller raises).
-__global__ __launch_bounds__(256) void knn_rows_rank_kernel(
+// barrier), so no wait launch sits in front of this one; a work-group whose wait gives up sets
+// *werr and writes nothing at all -- no mark, rank, slot or overflow entry (the workspace may hold
+// anything then: an earlier build's state or, fresh, uninitialised memory) -- and the query and
+// outlier launches, handed werr as their refs_err, leave the workspace alone and write eps = 0.
+// The coarse indices are loaded before the wait (they do not depend on phase A).
+__global__ __launch_bounds__(256) void knn_rows_place_kernel(
     const float* __restrict__ x, const int64_t* __restrict__ idx, int64_t C, int64_t N, int64_t M,
     int64_t Cpad, const uint64_t* __restrict__ start, const int2* __restrict__ crank,
-    uint32_t* __restrict__ known, uint32_t* __restrict__ rcnt, uint32_t* __restrict__ rrank,
+    uint32_t* __restrict__ known, uint32_t* __restrict__ rcnt, float4* __restrict__ refs,
     float4* __restrict__ over, int32_t* __restrict__ ovn, int32_t* __restrict__ err,
     const uint32_t* __restrict__ wflag, uint32_t wvalue, int32_t* __restrict__ werr,
     int64_t max_polls) {
-  if (wflag && !block_wait_flag(wflag, wvalue, werr, max_polls)) return;
   const int b = blockIdx.y;
   const int64_t cl = b % C;
-  for (int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x; j < M; j += (int64_t)gridDim.x * 256) {
-    const int64_t n = idx[b * M + j];
+  const int64_t j0 = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  int64_t n0 = j0 < M ? idx[b * M + j0] : 0;
+  if (wflag && !block_wait_flag(wflag, wvalue, werr, max_polls)) return;
+  const uint64_t* S = start + cl * Cpad;
+  for (int64_t j = j0; j < M; j += (int64_t)gridDim.x * 256) {
+    const int64_t n = j == j0 ? n0 : idx[b * M + j];
     if (n < 0 || n >= N) {
       atomicOr(err, 1);
-      rrank[b * M + j] = ~0u;
       continue;
     }
     const int cell = crank[cl * N + n].x;
-    const uint32_t rows = (uint32_t)(start[cl * Cpad + cell + 1] >> 32) -
-                          (uint32_t)(start[cl * Cpad + cell] >> 32);
     atomicMax(&known[b * N + n], (uint32_t)(j + 1));
     const uint32_t rank = atomicAdd(&rcnt[b * Cpad + cell], 1u);
-    rrank[b * M + j] = rank < rows ? rank : ~0u;
-    if (rank >= rows) {
-      const float* p = x + (cl * N + n) * 3;
-      over[b * M + atomicAdd(&ovn[b], 1)] = make_float4(p[0], p[1], p[2], __int_as_float((int)j));
-    }
-  }
-}
-
-// Phase B (2): one wave per brick: cell c's refs take slots [cw, cw + count) with count =
-// min(ranked refs, rows of c) and the cells of the brick back to back from the brick's first row.
-__global__ __launch_bounds__(256) void knn_rows_cellscan_kernel(int64_t C, int64_t Cpad,
-                                                                const uint64_t* __restrict__ start,
-                                                                const uint32_t* __restrict__ rcnt,
-                                                                uint64_t* __restrict__ cw) {
-  const int b = blockIdx.y;
-  const int64_t cl = b % C;
-  const int lane = threadIdx.x & 63;
-  const int64_t brick = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (brick * 64 >= Cpad) return;
-  const int64_t c = brick * 64 + lane;
-  const uint64_t* S = start + cl * Cpad;
-  const uint32_t a = (uint32_t)(S[c] >> 32);
-  const uint32_t rows = (c + 1 < Cpad ? (uint32_t)(S[c + 1] >> 32) : a) - a;
-  const uint32_t v = min(rcnt[b * Cpad + c], rows);
-  uint32_t inc = v;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const uint32_t y = __shfl_up(inc, o);
-    if (lane >= o) inc += y;
-  }
-  const uint32_t base = (uint32_t)(S[brick * 64] >> 32);
-  cw[b * Cpad + c] = (uint64_t)(base + inc - v) | ((uint64_t)v << 32);
-}
-
-// Phase B (3): every ranked ref to its slot.
-__global__ __launch_bounds__(256) void knn_rows_place_kernel(
-    const float* __restrict__ x, const int64_t* __restrict__ idx, int64_t C, int64_t N, int64_t M,
-    int64_t Cpad, const int2* __restrict__ crank, const uint32_t* __restrict__ rrank,
-    const uint64_t* __restrict__ cw, float4* __restrict__ refs) {
-  const int b = blockIdx.y;
-  const int64_t cl = b % C;
-  for (int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x; j < M; j += (int64_t)gridDim.x * 256) {
-    const uint32_t rank = rrank[b * M + j];
-    if (rank == ~0u) continue;
-    const int64_t n = idx[b * M + j];
+    const uint32_t a = (uint32_t)(S[cell] >> 32), rows = (uint32_t)(S[cell + 1] >> 32) - a;
     const float* p = x + (cl * N + n) * 3;
-    const int cell = crank[cl * N + n].x;
-    refs[b * N + (uint32_t)cw[b * Cpad + cell] + rank] = make_float4(p[0], p[1], p[2], __int_as_float((int)j));
+    const float4 r = make_float4(p[0], p[1], p[2], __int_as_float((int)j));
+    if (rank < rows) refs[b * N + a + rank] = r;
+    else over[b * M + atomicAdd(&ovn[b], 1)] = r;
   }
 }
 
@@ -652,52 +620,31 @@ struct Top3 {
   }
 };
 
-// IDW of the reference (float64, sequential sums), rounded to float32, in two halves: the
-// weights (positions only) and their application to the coarse values
-__device__ __forceinline__ NbrRec idw_weights(const Top3& t, int kk) {
+// IDW of the reference (float64, sequential sums), rounded to float32.  A row that found no ref
+// at all (only after a timed-out wait left the workspace unplaced: every CFG row has M >= 1 refs)
+// writes 0 instead of reading a value at an invalid index.
+__device__ __forceinline__ void idw_write(const Top3& t, int kk, const float* __restrict__ V,
+                                          float* __restrict__ O) {
+  if (t.j0 == 0x7fffffff || (kk > 1 && t.j1 == 0x7fffffff) || (kk > 2 && t.j2 == 0x7fffffff)) {
+    O[0] = O[1] = O[2] = 0.0f;
+    return;
+  }
   const double w0 = __ddiv_rn(1.0, dadd(__dsqrt_rn(t.d0), 1e-8));
   const double w1 = kk > 1 ? __ddiv_rn(1.0, dadd(__dsqrt_rn(t.d1), 1e-8)) : 0.0;
   const double w2 = kk > 2 ? __ddiv_rn(1.0, dadd(__dsqrt_rn(t.d2), 1e-8)) : 0.0;
   double wsum = w0;
   if (kk > 1) wsum = dadd(wsum, w1);
   if (kk > 2) wsum = dadd(wsum, w2);
-  NbrRec r;
-  r.u0 = __ddiv_rn(w0, wsum);
-  r.u1 = __ddiv_rn(w1, wsum);
-  r.u2 = __ddiv_rn(w2, wsum);
-  r.j0 = t.j0;
-  r.j1 = kk > 1 ? t.j1 : t.j0;
-  r.j2 = kk > 2 ? t.j2 : t.j0;
-  r.kk = kk;
-  return r;
-}
-__device__ __forceinline__ void idw_apply(const NbrRec& r, const float* __restrict__ V, float (&o)[3]) {
-  const float* v0 = V + (int64_t)r.j0 * 3;
-  const float* v1 = V + (int64_t)r.j1 * 3;
-  const float* v2 = V + (int64_t)r.j2 * 3;
+  const double u0 = __ddiv_rn(w0, wsum), u1 = __ddiv_rn(w1, wsum), u2 = __ddiv_rn(w2, wsum);
+  const float* v0 = V + (int64_t)t.j0 * 3;
+  const float* v1 = V + (int64_t)(kk > 1 ? t.j1 : t.j0) * 3;
+  const float* v2 = V + (int64_t)(kk > 2 ? t.j2 : t.j0) * 3;
 #pragma unroll
   for (int c = 0; c < 3; ++c) {
-    double acc = dmul((double)v0[c], r.u0);
-    if (r.kk > 1) acc = dadd(acc, dmul((double)v1[c], r.u1));
-    if (r.kk > 2) acc = dadd(acc, dmul((double)v2[c], r.u2));
-    o[c] = (float)acc;
-  }
-}
-__device__ __forceinline__ void idw_write(const Top3& t, int kk, const float* __restrict__ V,
-                                          float* __restrict__ O) {
-  float o[3];
-  idw_apply(idw_weights(t, kk), V, o);
-  O[0] = o[0]; O[1] = o[1]; O[2] = o[2];
-}
-
-// the row's result: the IDW now (vals given) or its top-3 for the finish pass (deferred search)
-__device__ __forceinline__ void row_write(const Top3& t, int kk, const float* __restrict__ V,
-                                          float* __restrict__ out, NbrRec* __restrict__ nbr,
-                                          int64_t row) {
-  if (nbr) {
-    nbr[row] = idw_weights(t, kk);
-  } else {
-    idw_write(t, kk, V, out + row * 3);
+    double acc = dmul((double)v0[c], u0);
+    if (kk > 1) acc = dadd(acc, dmul((double)v1[c], u1));
+    if (kk > 2) acc = dadd(acc, dmul((double)v2[c], u2));
+    O[c] = (float)acc;
   }
 }
 
@@ -1014,27 +961,9 @@ __device__ __forceinline__ bool settled(const Query& me, const Box& cells, const
   return bound == INFINITY || (bound > 0 && me.t.last(kk) < bound * bound);
 }
 
-// One wave per chunk of <= 64 queries of one brick; the passes of the header comment.
-// The consumer side of the build -> query dependency (the `built_flag` / `built_value` of
-// pcst_knn3_query / _finish): the workspace is read only once the build's flag holds its value.
-// The stream waited for the flag before this launch (pcst_signal_wait, or the MLP's last
-// work-group); a wait that gave up lets the launch run anyway, and then every work-group finds
-// the flag short and leaves the workspace alone (its rows of the output get 0) instead of reading
-// a half-built one.  The caller raises on the wait's error word after the loop.
-__device__ __forceinline__ bool build_pending(const uint32_t* flag, uint32_t value) {
-  __shared__ int s_pending;
-  if (threadIdx.x == 0)
-    s_pending = flag != nullptr &&
-                __hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < value;
-  __syncthreads();
-  return s_pending != 0;
-}
-
 // amdgpu_waves_per_eu(4): 128 VGPRs (4 spilled) instead of 138, so 4 waves per SIMD (the LDS
 // allows 4 work-groups per CU) instead of 3: the ~5000 chunks of a step run in fewer rounds
 // (driver window 2379-2398 -> 2400-2429 steps/s, A/B on one box).
-// DEFER: the deferred search (positions only): the rows' IDW weights into nbr instead of the IDW
-// of vals into out.
 // The layout-specific arrays of the query and outlier launches.  Compact layout (pcst_knn3_build):
 // per CFG row b, refs cell-sorted in [0, M), the packed start words give a cell's ref range.
 // Rows layout (pcst_knn3_rows_*): the cloud cl = b % C holds the grid, the rows in cell order and
@@ -1044,42 +973,71 @@ __device__ __forceinline__ bool build_pending(const uint32_t* flag, uint32_t val
 struct KArgs {
   int64_t C;                  // clouds holding the grid / rows / chunks (compact: B)
   const uint32_t* known;      // [B][N] (rows layout)
-  const uint64_t* cw;         // [B][Cpad] a cell's refs: first slot | count << 32 (rows layout)
+  const uint32_t* rcnt;       // [B][Cpad] refs placed per cell (rows layout)
   const float4* over;         // [B][M] overflow refs (rows layout)
   const int32_t* ovn;         // [B] their counts (rows layout)
   int32_t* err;               // bit 4: a chunk outside [0, N], bit 8: a ref range outside the refs
+                              // (bit 1: a bad coarse index, bit 16: a brick over-full -- phase B)
   int32_t* werr;              // rows layout: the query waits for bflag itself (its timeout word)
   int64_t max_polls;
+  const int32_t* refs_err;    // rows layout: phase B's wait error word (nonzero: nothing placed)
+  int32_t* qctr;              // [B][kQueryShards][kCtrStride] chunk counters (zero at launch);
+                              // rows layout: [B..2B) the brick-batch counters
+  float4* brefs;              // [B][N] rows layout: the placed refs per brick (outlier pass)
+  uint32_t* bcnt;             // [B][Cpad / 64] their counts (zero unless written)
 };
 
-template <int kk, bool DEFER, bool ROWS>  // kk = min(M, 3), a compile-time constant so the top-3 stays in registers
+// The consumer side of the build -> query dependency (the `built_flag` / `built_value` of
+// pcst_knn3_query / _rows_query): the workspace is read only once the build's flag holds its
+// value.  The stream waited for the flag before this launch (pcst_signal_wait, or the MLP's last
+// work-group); a wait that gave up lets the launch run anyway, and then every work-group finds
+// the flag short -- or, rows layout, phase B's wait error word set (then the workspace holds no
+// placement of this step) -- and leaves the workspace alone (its rows of the output get 0)
+// instead of reading a half-built one.  The caller raises on the waits' error words after the
+// loop.
+__device__ __forceinline__ bool query_pending(const uint32_t* flag, uint32_t value,
+                                             const int32_t* refs_err) {
+  __shared__ int s_pending;
+  if (threadIdx.x == 0)
+    s_pending = (flag != nullptr &&
+                 __hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < value) ||
+                (refs_err != nullptr &&
+                 __hip_atomic_load(refs_err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0);
+  __syncthreads();
+  return s_pending != 0;
+}
+
+// Persistent chunk waves (header comment, "Chunk scheduling"): the grid is G = B * Gr
+// work-groups, row b = blockIdx.x % B, m = blockIdx.x / B its work-group index in the row.  Wave
+// (m, wv) takes chunk m * 4 + wv first, then chunks Wr + s + S * k (Wr = 4 Gr waves per row,
+// S = min(8, Gr) shards, s = m % S, k from counter s of the row) until the row's list ends.  The
+// counters' item sets are disjoint and together cover [Wr, nch), and every shard of every row has
+// work-groups (Gr >= S), so every chunk is processed exactly once whatever the residency.
+template <int kk, bool ROWS>  // kk = min(M, 3), a compile-time constant so the top-3 stays in registers
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) void knn_query_kernel(
-    const float* __restrict__ orig, const float* __restrict__ vals, int64_t N, int64_t M,
+    const float* __restrict__ orig, const float* __restrict__ vals, int64_t B, int64_t N, int64_t M,
     int64_t Cpad, const float* __restrict__ gp, const uint64_t* __restrict__ start,
     const float4* __restrict__ refs, const int32_t* __restrict__ qorder,
     const uint2* __restrict__ chunks, int64_t maxch, const int32_t* __restrict__ nchunk,
     int32_t* __restrict__ olist, float* __restrict__ obound, int32_t* __restrict__ ocount,
-    float* __restrict__ out, NbrRec* __restrict__ nbr, const uint32_t* __restrict__ bflag,
-    uint32_t bvalue, const KArgs ka) {
+    float* __restrict__ out, const uint32_t* __restrict__ bflag, uint32_t bvalue, const KArgs ka) {
   __shared__ __attribute__((aligned(16))) float cand[4][4][kCandCap];
-  // rows layout: the CFG rows' work-groups interleaved in dispatch order (x fastest), so both
-  // rows' chunk lists start together instead of row 1 waiting for row 0's work-groups to retire
-  // (non-MLP step 0.2096-0.2107 vs 0.2120-0.2121 ms, profiles/r05/s2k)
-  const unsigned lin = blockIdx.y * gridDim.x + blockIdx.x;
-  const int b = ROWS ? (int)(lin % gridDim.y) : (int)blockIdx.y;
-  const unsigned bx = ROWS ? lin / gridDim.y : blockIdx.x;
+  const unsigned Gr = gridDim.x / (unsigned)B;
+  const int b = (int)(blockIdx.x % (unsigned)B);
+  const unsigned m = blockIdx.x / (unsigned)B;
+  if (m >= Gr) return;  // (the host launches a multiple of B)
   const int64_t cl = ROWS ? b % ka.C : b;
   // compact layout: the stream waited for the build before this launch, the flag is only checked;
-  // rows layout: the work-groups wait for the build's last flag themselves (no wait launch)
-  // rows layout with wait_err == NULL: the stream already waited for the flag (the MLP's last
-  // work-group), so the work-groups only check it -- no acquire fence per work-group, which at 4
-  // work-groups per CU cost the step ~11 us (2849 / 2834 vs 2756 / 2739 steps/s, r05/s2r)
-  const bool pending = (ROWS && bflag && ka.werr) ? !block_wait_flag(bflag, bvalue, ka.werr, ka.max_polls)
-                                                  : build_pending(bflag, bvalue);
+  // rows layout with werr: the work-groups wait for the build's last flag themselves (no wait
+  // launch); with werr NULL the stream already waited for the flag (the MLP's last work-group),
+  // so the work-groups only check it -- no acquire fence per work-group, which at 4 work-groups
+  // per CU cost the step ~11 us (2849 / 2834 vs 2756 / 2739 steps/s, r05/s2r)
+  bool pending = (ROWS && bflag && ka.werr) ? !block_wait_flag(bflag, bvalue, ka.werr, ka.max_polls)
+                                            : false;
+  pending = pending || query_pending(bflag, bvalue, ROWS ? ka.refs_err : nullptr);
   if (pending) {
-    if (!DEFER)
-      for (int64_t n = (int64_t)bx * 256 + threadIdx.x; n < N * 3; n += (int64_t)gridDim.x * 256)
-        out[b * N * 3 + n] = 0.0f;
+    for (int64_t n = (int64_t)m * 256 + threadIdx.x; n < N * 3; n += (int64_t)Gr * 256)
+      out[b * N * 3 + n] = 0.0f;
     return;
   }
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -1087,16 +1045,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
   g.load(gp + cl * 8);
   const uint64_t* S = start + cl * Cpad;
   const float4* R = refs + b * (ROWS ? N : M);
-  const float* V = DEFER ? nullptr : vals + b * M * 3;
-  const uint64_t* CW = ROWS ? ka.cw + b * Cpad : nullptr;
+  const float* V = vals + b * M * 3;
+  const uint32_t* RC = ROWS ? ka.rcnt + b * Cpad : nullptr;
   const uint32_t rlim = (uint32_t)(ROWS ? N : M);
   // the ref range of cell u0, checked against the ref array (a bad build raises, never faults)
   auto rng = [&](int u0, uint64_t& lo, uint64_t& hi) {
     uint32_t a, e;
-    if constexpr (ROWS) {  // the cell's placed refs
-      const uint64_t cwv = CW[u0];
-      a = (uint32_t)cwv;
-      e = a + (uint32_t)(cwv >> 32);
+    if constexpr (ROWS) {  // the refs at the front of the cell's row range
+      a = (uint32_t)(S[u0] >> 32);
+      const uint32_t rows = (uint32_t)(S[u0 + 1] >> 32) - a;
+      e = a + min(RC[u0], rows);
     } else {
       a = (uint32_t)S[u0];
       e = (uint32_t)S[u0 + 1];
@@ -1156,10 +1114,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
       }
     }
   };
-  for (int item = (int)bx * 4 + wv; item < nch; item += gridDim.x * 4) {
+  const unsigned Sh = min((unsigned)kQueryShards, Gr), sh = m % Sh;
+  const int Wr = (int)Gr * 4;
+  int32_t* ctr = ka.qctr + (b * kQueryShards + sh) * kCtrStride;
+  // the wave's next chunk from its row's counter (taken as late as the chunk allows: once its
+  // passes are done, so the counter's latency hides under the result writes and no chunk waits
+  // behind a long one)
+  auto take = [&]() {
+    int nk = 0;
+    if (lane == 0) nk = atomicAdd(ctr, 1);
+    return Wr + (int)sh + (int)Sh * __shfl(nk, 0);
+  };
+  for (int item = (int)m * 4 + wv; item < nch;) {
     const uint2 ch = chunks[cl * maxch + item];
     if (ch.x > ch.y || ch.y > (uint32_t)N || ch.y - ch.x > 64u) {  // wave-uniform
       if (lane == 0) atomicOr(ka.err, 4);
+      item = take();
       continue;
     }
     bool valid = ch.x + lane < ch.y;
@@ -1168,14 +1138,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
     if constexpr (ROWS) {  // a known row takes its coarse value (the last coarse row naming it)
       const uint32_t kn = valid ? ka.known[b * N + n] : 0u;
       if (kn) {
-        if (!DEFER) {
-          const float* v = V + (int64_t)(kn - 1) * 3;
-          float* o = out + (b * N + n) * 3;
-          o[0] = v[0]; o[1] = v[1]; o[2] = v[2];
-        }
+        const float* v = V + (int64_t)(kn - 1) * 3;
+        float* o = out + (b * N + n) * 3;
+        o[0] = v[0]; o[1] = v[1]; o[2] = v[2];
         valid = false;
       }
-      if (!__any(valid)) continue;
+      if (!__any(valid)) {
+        item = take();
+        continue;
+      }
     }
     Query me;
     me.init(qp[0], qp[1], qp[2]);
@@ -1228,6 +1199,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
         }
       }
     }
+    const int next = take();
     // the rest (sparse neighbourhoods, ball too large, budget exceeded): the outlier pass
     const uint64_t rest = __ballot(open);
     if (rest) {
@@ -1241,7 +1213,71 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
         obound[o] = dk == INFINITY ? INFINITY : (float)(dk * (1.0 + 1e-6)) * 1.000001f;
       }
     }
-    if (valid && !open) row_write(me.t, kk, V, out, DEFER ? nbr : nullptr, b * N + n);
+    if (valid && !open) idw_write(me.t, kk, V, out + (b * N + n) * 3);
+    item = next;
+  }
+  // Rows layout: the brick copy of the placed refs for the outlier launch, by waves out of chunks.
+  // Batches of kBrickBatch bricks from the row's brick-batch counters (sharded as the chunks);
+  // per brick, lane = cell: the cells' placed counts, their prefix, then the brick's refs copied
+  // to the front of its row range (slot v of the run: the lane whose prefix holds v, found by a
+  // binary search over the lanes' offsets).  A brick without refs writes nothing (its count
+  // stays the build's zero).
+  if constexpr (ROWS) {
+    const int64_t nbr = Cpad / 64;
+    const int64_t nbatch = (nbr + kBrickBatch - 1) / kBrickBatch;
+    int32_t* bctr = ka.qctr + ((B + b) * kQueryShards + sh) * kCtrStride;
+    const float4* Rc = refs + b * N;
+    float4* Rb = ka.brefs + b * N;
+    for (;;) {
+      int k = 0;
+      if (lane == 0) k = atomicAdd(bctr, 1);
+      const int64_t gb = (int64_t)sh + (int64_t)Sh * __shfl(k, 0);
+      if (gb >= nbatch) break;
+      uint32_t ca[kBrickBatch], cn[kBrickBatch];
+#pragma unroll
+      for (int i = 0; i < kBrickBatch; ++i) {  // every brick's loads in flight together
+        const int64_t c = (gb * kBrickBatch + i) * 64 + lane;
+        ca[i] = cn[i] = 0;
+        if (c < Cpad) {
+          ca[i] = (uint32_t)(S[c] >> 32);
+          const uint32_t e = c + 1 < Cpad ? (uint32_t)(S[c + 1] >> 32) : ca[i];
+          if (e < ca[i] || e > rlim) {  // a bad build: skipped and reported, never read
+            atomicOr(ka.err, 8);
+            ca[i] = 0;
+          } else {
+            cn[i] = min(RC[c], e - ca[i]);
+          }
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < kBrickBatch; ++i) {
+        uint32_t off = cn[i];
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+          const uint32_t y = __shfl_up(off, o);
+          if (lane >= o) off += y;
+        }
+        const uint32_t tot = __shfl(off, 63);
+        off -= cn[i];
+        if (tot == 0) continue;  // wave-uniform
+        const int64_t brick = gb * kBrickBatch + i;
+        const uint32_t ba = __shfl(ca[i], 0);
+        if (tot > rlim - ba) {  // more refs than the brick's rows: impossible for a sound build
+          if (lane == 0) atomicOr(ka.err, 16);
+          continue;
+        }
+        if (lane == 0) ka.bcnt[b * nbr + brick] = tot;
+        for (uint32_t t0 = 0; t0 < tot; t0 += 64) {
+          const uint32_t v = t0 + lane;
+          int l = 0;  // last lane whose offset <= v (it owns slot v: zero-count lanes never do)
+#pragma unroll
+          for (int st = 32; st >= 1; st >>= 1)
+            if (__shfl(off, l + st) <= v) l += st;
+          const uint32_t src = __shfl(ca[i], l) + (v - __shfl(off, l));
+          if (v < tot) Rb[ba + v] = Rc[src];
+        }
+      }
+    }
   }
 }
 
@@ -1269,23 +1305,30 @@ __device__ __forceinline__ void wave_merge_top3(Top3& t, int top = 32) {
 // bounds carry the same cell-rounding slack).  A shell's refs are split over the lanes
 // (scan_units_1q); after every shell the lanes' lists are merged into lane 0 (the others restart
 // empty with the merged screen), so no ref is offered twice.
-// Rows layout (ROWS): a brick's refs are one run from its first cell's first slot to its last
-// cell's end; the overflow refs are offered first; the known rows were copied by the query.
+// Rows layout (ROWS): a brick's placed refs are one run at the front of its row range in the
+// brick copy (brefs); the overflow refs are offered first; the known rows were copied by the
+// query.
+// The launch also zeroes the query's work counters (the query before it on the stream is done
+// with them), so the next query on the workspace starts from zero as after a build.
 template <int kk, bool ROWS>
 __global__ __launch_bounds__(256) void knn_outlier_brick_kernel(
     const float* __restrict__ vals, int64_t N, int64_t M, const float* __restrict__ orig,
     const float* __restrict__ gp, int64_t Cpad, const uint64_t* __restrict__ start,
     const float4* __restrict__ refs, const int32_t* __restrict__ olist,
     const float* __restrict__ obound, const int32_t* __restrict__ ocount,
-    const uint32_t* __restrict__ known, float* __restrict__ out, NbrRec* __restrict__ nbr,
+    const uint32_t* __restrict__ known, float* __restrict__ out,
     const uint32_t* __restrict__ bflag, uint32_t bvalue, const KArgs ka) {
   const int b = blockIdx.y;
   const int64_t cl = ROWS ? b % ka.C : b;
-  if (build_pending(bflag, bvalue)) return;
+  if (blockIdx.x == 0 && threadIdx.x < kQueryShards) {
+    ka.qctr[(b * kQueryShards + threadIdx.x) * kCtrStride] = 0;
+    if (ROWS) ka.qctr[((gridDim.y + b) * kQueryShards + threadIdx.x) * kCtrStride] = 0;
+  }
+  if (query_pending(bflag, bvalue, ROWS ? ka.refs_err : nullptr)) return;
   // rows that are coarse points take the coarse value (result[idx] = coarse; the last coarse
-  // row writing a point wins, as in the reference's index assignment); the deferred search
-  // leaves them to the finish pass
-  for (int64_t n = (int64_t)blockIdx.x * 256 + threadIdx.x; !ROWS && !nbr && n < N;
+  // row writing a point wins, as in the reference's index assignment); the rows layout's query
+  // copied them already
+  for (int64_t n = (int64_t)blockIdx.x * 256 + threadIdx.x; !ROWS && n < N;
        n += (int64_t)gridDim.x * 256) {
     const uint32_t kn = known[b * N + n];
     if (kn) {
@@ -1299,9 +1342,9 @@ __global__ __launch_bounds__(256) void knn_outlier_brick_kernel(
   g.load(gp + cl * 8);
   const int nbx = g.bx, nby = g.by, nbz = (g.d[2] + 3) >> 2;
   const uint64_t* S = start + cl * Cpad;
-  const float4* R = refs + b * (ROWS ? N : M);
-  const uint64_t* CW = ROWS ? ka.cw + b * Cpad : nullptr;
-  const float* V = vals ? vals + b * M * 3 : nullptr;
+  const float4* R = ROWS ? ka.brefs + b * N : refs + b * M;
+  const uint32_t* BC = ROWS ? ka.bcnt + b * (Cpad / 64) : nullptr;
+  const float* V = vals + b * M * 3;
   const int cnt = ocount[b];
   const int novr = ROWS ? ka.ovn[b] : 0;
   const uint32_t rlim = (uint32_t)(ROWS ? N : M);
@@ -1345,10 +1388,9 @@ __global__ __launch_bounds__(256) void knn_outlier_brick_kernel(
           if (e * e > lim) return;
           const int u0 = ((z * nby + y) * nbx + x) << 6;
           uint32_t ra, re;
-          if constexpr (ROWS) {  // the brick's refs: its first cell's slot to its last cell's end
-            const uint64_t last = CW[u0 + 63];
-            ra = (uint32_t)CW[u0];
-            re = (uint32_t)last + (uint32_t)(last >> 32);
+          if constexpr (ROWS) {  // the brick's placed refs, at the front of its row range
+            ra = (uint32_t)(S[u0] >> 32);
+            re = ra + min(BC[u0 >> 6], (uint32_t)(S[u0 + 64] >> 32) - ra);
           } else {
             ra = (uint32_t)S[u0];
             re = (uint32_t)S[u0 + 64];
@@ -1390,71 +1432,7 @@ __global__ __launch_bounds__(256) void knn_outlier_brick_kernel(
         r += 1;  // sparse shells are cheap; a doubled box can reach into the dense core unpruned
       }
     }
-    if (lane == 0) row_write(me.t, kk, V, out, nbr, b * N + n);
-  }
-}
-
-// Finish pass of the deferred search: row n of cloud b takes the coarse value of the last coarse
-// row that is the point itself (known), else the IDW of its neighbour record.
-__device__ __forceinline__ void finish_row(const float* __restrict__ vals, int64_t N, int64_t M,
-                                           const uint32_t* __restrict__ known,
-                                           const NbrRec* __restrict__ nbr, int64_t b, int64_t n,
-                                           float (&o)[3]) {
-  const uint32_t kn = known[b * N + n];
-  const float* V = vals + b * M * 3;
-  if (kn) {
-    const float* v = V + (int64_t)(kn - 1) * 3;
-    o[0] = v[0]; o[1] = v[1]; o[2] = v[2];
-  } else {
-    idw_apply(nbr[b * N + n], V, o);
-  }
-}
-
-__global__ __launch_bounds__(256) void knn_finish_kernel(const float* __restrict__ vals, int64_t B,
-                                                         int64_t N, int64_t M,
-                                                         const uint32_t* __restrict__ known,
-                                                         const NbrRec* __restrict__ nbr,
-                                                         float* __restrict__ out,
-                                                         const uint32_t* __restrict__ bflag,
-                                                         uint32_t bvalue) {
-  const bool pending = build_pending(bflag, bvalue);
-  for (int64_t r = blockIdx.x * 256ll + threadIdx.x; r < B * N; r += (int64_t)gridDim.x * 256) {
-    float o[3] = {0.0f, 0.0f, 0.0f};
-    if (!pending) finish_row(vals, N, M, known, nbr, r / N, r % N, o);
-    out[r * 3 + 0] = o[0]; out[r * 3 + 1] = o[1]; out[r * 3 + 2] = o[2];
-  }
-}
-
-// The finish pass fused with the CFG + DDIM update (sampler.hip) over a CFG batch of 2C clouds:
-// eps_c is row n of cloud c, eps_u the same row of cloud C + c; x, src, x_out are [C, N, 3] and
-// x_cat [2C, N, 3] takes the new x twice.  Same operations as knn_finish_kernel followed by
-// cfg_ddim_kernel.
-__global__ __launch_bounds__(256) void knn_finish_cfg_ddim_kernel(
-    const float* __restrict__ vals, int64_t C, int64_t N, int64_t M,
-    const uint32_t* __restrict__ known, const NbrRec* __restrict__ nbr, const float* __restrict__ x,
-    const float* __restrict__ src, float scale, float c1, float c2, float c3, float c4,
-    float* __restrict__ x_out, float* __restrict__ x_cat, const uint32_t* __restrict__ bflag,
-    uint32_t bvalue) {
-  const int64_t rows = C * N;
-  const bool pending = build_pending(bflag, bvalue);
-  for (int64_t r = blockIdx.x * 256ll + threadIdx.x; r < rows; r += (int64_t)gridDim.x * 256) {
-    const int64_t c = r / N, n = r % N;
-    float ec[3] = {0.0f, 0.0f, 0.0f}, eu[3] = {0.0f, 0.0f, 0.0f};
-    if (!pending) {
-      finish_row(vals, N, M, known, nbr, c, n, ec);
-      finish_row(vals, N, M, known, nbr, C + c, n, eu);
-    }
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-      const int64_t e = r * 3 + k;
-      const float xn = cfg_ddim_value(x[e], ec[k], &eu[k], src ? src + e : nullptr, scale, c1, c2,
-                                      c3, c4);
-      x_out[e] = xn;
-      if (x_cat) {
-        x_cat[e] = xn;
-        x_cat[rows * 3 + e] = xn;
-      }
-    }
+    if (lane == 0) idw_write(me.t, kk, V, out + (b * N + n) * 3);
   }
 }
 
@@ -1528,40 +1506,40 @@ extern "C" int pcst_knn3_build(const float* orig, const int64_t* idx, int64_t B,
   return PCST_OK;
 }
 
-// The query and outlier launches: vals/out given -> IDW written to out; nbr given (deferred
-// search, positions only) -> every query row's weights into the workspace's neighbour records.
-// Both layouts: the per-layout pointers (the compact workspace's or the rows workspace's) come in
-// as arguments; ka carries the rows layout's extras and the error word.
+// The query and outlier launches.  Both layouts: the per-layout pointers (the compact workspace's
+// or the rows workspace's) come in as arguments; ka carries the rows layout's extras, the error
+// word and the work counters.  The query grid is the resident one (kQueryBlocksPerCU per CU,
+// grid_cap > 0 caps it), a multiple of B, and no larger than the rows' chunk lists need.
 template <bool ROWS>
 static void launch_knn_query(int64_t nch_max, const float* gp, const uint64_t* cnt, const float4* refs,
                              const int32_t* qorder, const uint2* chunks, const int32_t* nchunk,
                              int32_t* olist, float* obound, int32_t* ocount, const uint32_t* known,
                              int64_t Cpad, const KArgs& ka, const float* coarse, const float* orig,
-                             int64_t B, int64_t N, int64_t M, float* out, NbrRec* nbr,
-                             const uint32_t* bflag, uint32_t bvalue, int64_t grid_cap, hipStream_t s) {
-  const int b = (int)B;
-  if (grid_cap <= 0) grid_cap = kQueryGridCapDefault;
-  // fixed grids stride over the chunk and outlier lists (their lengths live on the device)
-  const unsigned gq = (unsigned)std::min<int64_t>(
-      cdiv(nch_max, 4), std::max<int64_t>(kQueryBlocksMin, std::min<int64_t>(kQueryBlocks, grid_cap / B)));
-  auto qk = nbr ? (M >= 3 ? knn_query_kernel<3, true, ROWS>
-                          : (M == 2 ? knn_query_kernel<2, true, ROWS> : knn_query_kernel<1, true, ROWS>))
-                : (M >= 3 ? knn_query_kernel<3, false, ROWS>
-                          : (M == 2 ? knn_query_kernel<2, false, ROWS> : knn_query_kernel<1, false, ROWS>));
-  hipLaunchKernelGGL(qk, dim3(gq, b), dim3(256), 0, s, orig, coarse, N, M, Cpad, gp, cnt, refs, qorder,
-                     chunks, nch_max, nchunk, olist, obound, ocount, out, nbr, bflag, bvalue, ka);
+                             int64_t B, int64_t N, int64_t M, float* out, const uint32_t* bflag,
+                             uint32_t bvalue, int64_t grid_cap, hipStream_t s) {
+  int dev = 0, cus = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+    cus = 256;
+  const int64_t cap = grid_cap > 0 ? grid_cap : (int64_t)cus * kQueryBlocksPerCU;
+  const int64_t Gr = std::max<int64_t>(1, std::min<int64_t>(cdiv(nch_max, 4), cap / B));
+  auto qk = M >= 3 ? knn_query_kernel<3, ROWS>
+                   : (M == 2 ? knn_query_kernel<2, ROWS> : knn_query_kernel<1, ROWS>);
+  hipLaunchKernelGGL(qk, dim3((unsigned)(Gr * B)), dim3(256), 0, s, orig, coarse, B, N, M, Cpad, gp, cnt,
+                     refs, qorder, chunks, nch_max, nchunk, olist, obound, ocount, out, bflag, bvalue, ka);
   auto ok = M >= 3 ? knn_outlier_brick_kernel<3, ROWS>
                    : (M == 2 ? knn_outlier_brick_kernel<2, ROWS> : knn_outlier_brick_kernel<1, ROWS>);
-  hipLaunchKernelGGL(ok, dim3(kOutlierBrickBlocks, b), dim3(256), 0, s, coarse, N, M, orig, gp, Cpad,
-                     cnt, refs, olist, obound, ocount, known, out, nbr, bflag, bvalue, ka);
+  hipLaunchKernelGGL(ok, dim3(kOutlierBrickBlocks, (unsigned)B), dim3(256), 0, s, coarse, N, M, orig, gp,
+                     Cpad, cnt, refs, olist, obound, ocount, known, out, bflag, bvalue, ka);
 }
 
 static void launch_knn_query(const KnnWS& w, const float* coarse, const float* orig, int64_t B,
-                             int64_t N, int64_t M, float* out, NbrRec* nbr, const uint32_t* bflag,
+                             int64_t N, int64_t M, float* out, const uint32_t* bflag,
                              uint32_t bvalue, int64_t grid_cap, hipStream_t s) {
-  const KArgs ka = {B, nullptr, nullptr, nullptr, nullptr, w.err, nullptr, 0};
+  const KArgs ka = {B, nullptr, nullptr, nullptr, nullptr, w.err, nullptr, 0, nullptr, w.qctr,
+                    nullptr, nullptr};
   launch_knn_query<false>(w.maxch, w.gp, w.cnt, w.refs, w.qorder, w.chunks, w.nchunk, w.olist,
-                          w.obound, w.ocount, w.known, w.Cpad, ka, coarse, orig, B, N, M, out, nbr,
+                          w.obound, w.ocount, w.known, w.Cpad, ka, coarse, orig, B, N, M, out,
                           bflag, bvalue, grid_cap, s);
 }
 
@@ -1577,55 +1555,9 @@ extern "C" int pcst_knn3_query(const float* coarse, const float* orig, int64_t B
   if (B == 0) return PCST_OK;
   PCST_CHECK_ARG(coarse && orig && out && workspace, "knn3_query: null pointer");
   KnnWS w = carve_knn(workspace, B, N, M);
-  launch_knn_query(w, coarse, orig, B, N, M, out, nullptr, built_flag, built_value, grid_cap,
+  launch_knn_query(w, coarse, orig, B, N, M, out, built_flag, built_value, grid_cap,
                    as_stream(stream));
   PCST_LAUNCH_CHECK("knn3_query");
-  return PCST_OK;
-}
-
-extern "C" int pcst_knn3_search(const float* orig, int64_t B, int64_t N, int64_t M,
-                                void* workspace, int64_t grid_cap, void* stream) {
-  PCST_KNN_SHAPE_CHECK("knn3_search");
-  if (B == 0) return PCST_OK;
-  PCST_CHECK_ARG(orig && workspace, "knn3_search: null pointer");
-  KnnWS w = carve_knn(workspace, B, N, M);
-  launch_knn_query(w, nullptr, orig, B, N, M, nullptr, w.nbr, nullptr, 0u, grid_cap,
-                   as_stream(stream));
-  PCST_LAUNCH_CHECK("knn3_search");
-  return PCST_OK;
-}
-
-extern "C" int pcst_knn3_finish(const float* coarse, int64_t B, int64_t N, int64_t M, float* out,
-                                void* workspace, const uint32_t* built_flag, uint32_t built_value,
-                                void* stream) {
-  PCST_KNN_SHAPE_CHECK("knn3_finish");
-  if (B == 0) return PCST_OK;
-  PCST_CHECK_ARG(coarse && out && workspace, "knn3_finish: null pointer");
-  KnnWS w = carve_knn(workspace, B, N, M);
-  const unsigned g = (unsigned)std::min<int64_t>(cdiv(B * N, 256), 4096);
-  hipLaunchKernelGGL(knn_finish_kernel, dim3(g), dim3(256), 0, as_stream(stream), coarse, B, N, M,
-                     w.known, w.nbr, out, built_flag, built_value);
-  PCST_LAUNCH_CHECK("knn3_finish");
-  return PCST_OK;
-}
-
-extern "C" int pcst_knn3_finish_cfg_ddim(const float* coarse, int64_t B, int64_t N, int64_t M,
-                                         void* workspace, const float* x, const float* source,
-                                         float guidance_scale, float sqrt_1m_at, float sqrt_at_eps,
-                                         float sqrt_aprev, float sqrt_1m_aprev, float* x_out,
-                                         float* x_cat, const uint32_t* built_flag,
-                                         uint32_t built_value, void* stream) {
-  PCST_KNN_SHAPE_CHECK("knn3_finish_cfg_ddim");
-  PCST_CHECK_ARG(B % 2 == 0, "knn3_finish_cfg_ddim: B must be the CFG batch (2 x clouds)");
-  if (B == 0) return PCST_OK;
-  PCST_CHECK_ARG(coarse && workspace && x && x_out, "knn3_finish_cfg_ddim: null pointer");
-  KnnWS w = carve_knn(workspace, B, N, M);
-  const int64_t C = B / 2;
-  const unsigned g = (unsigned)std::min<int64_t>(cdiv(C * N, 256), 4096);
-  hipLaunchKernelGGL(knn_finish_cfg_ddim_kernel, dim3(g), dim3(256), 0, as_stream(stream), coarse,
-                     C, N, M, w.known, w.nbr, x, source, guidance_scale, sqrt_1m_at, sqrt_at_eps,
-                     sqrt_aprev, sqrt_1m_aprev, x_out, x_cat, built_flag, built_value);
-  PCST_LAUNCH_CHECK("knn3_finish_cfg_ddim");
   return PCST_OK;
 }
 
@@ -1710,13 +1642,9 @@ extern "C" int pcst_knn3_rows_refs(const float* x, const int64_t* idx, int64_t C
   KnnRowsWS w = carve_knn_rows(workspace, C, copies, N, M);
   hipStream_t s = as_stream(stream);
   const dim3 gj((unsigned)std::min<int64_t>(cdiv(M, 256), 1024), (unsigned)w.B);
-  hipLaunchKernelGGL(knn_rows_rank_kernel, gj, dim3(256), 0, s, x, idx, C, N, M, w.Cpad, w.cnt, w.crank,
-                     w.known, w.rcnt, w.rrank, w.over, w.ovn, w.err, wait_flag, wait_value, wait_err,
+  hipLaunchKernelGGL(knn_rows_place_kernel, gj, dim3(256), 0, s, x, idx, C, N, M, w.Cpad, w.cnt, w.crank,
+                     w.known, w.rcnt, w.refs, w.over, w.ovn, w.err, wait_flag, wait_value, wait_err,
                      max_polls > 0 ? max_polls : (int64_t)kSignalPolls);
-  hipLaunchKernelGGL(knn_rows_cellscan_kernel, dim3((unsigned)cdiv(w.Cpad / 64, 4), (unsigned)w.B), dim3(256),
-                     0, s, C, w.Cpad, w.cnt, w.rcnt, w.cw);
-  hipLaunchKernelGGL(knn_rows_place_kernel, gj, dim3(256), 0, s, x, idx, C, N, M, w.Cpad, w.crank, w.rrank,
-                     w.cw, w.refs);
   PCST_LAUNCH_CHECK("knn3_rows_refs");
   return PCST_OK;
 }
@@ -1724,16 +1652,17 @@ extern "C" int pcst_knn3_rows_refs(const float* x, const int64_t* idx, int64_t C
 extern "C" int pcst_knn3_rows_query(const float* coarse, const float* x, int64_t C, int64_t copies,
                                     int64_t N, int64_t M, float* out, void* workspace,
                                     const uint32_t* built_flag, uint32_t built_value,
-                                    int32_t* wait_err, int64_t max_polls, int64_t grid_cap,
-                                    void* stream) {
+                                    int32_t* wait_err, int64_t max_polls, const int32_t* refs_err,
+                                    int64_t grid_cap, void* stream) {
   PCST_KNN_ROWS_CHECK("knn3_rows_query");
   if (C == 0) return PCST_OK;
   PCST_CHECK_ARG(coarse && x && out && workspace, "knn3_rows_query: null pointer");
   KnnRowsWS w = carve_knn_rows(workspace, C, copies, N, M);
-  const KArgs ka = {C, w.known, w.cw, w.over, w.ovn, w.err, wait_err,
-                    max_polls > 0 ? max_polls : (int64_t)kSignalPolls};
+  const KArgs ka = {C, w.known, w.rcnt, w.over, w.ovn, w.err, wait_err,
+                    max_polls > 0 ? max_polls : (int64_t)kSignalPolls, refs_err, w.qctr, w.brefs,
+                    w.bcnt};
   launch_knn_query<true>(w.maxch, w.gp, w.cnt, w.refs, w.qorder, w.chunks, w.nchunk, w.olist,
-                         w.obound, w.ocount, w.known, w.Cpad, ka, coarse, x, w.B, N, M, out, nullptr,
+                         w.obound, w.ocount, w.known, w.Cpad, ka, coarse, x, w.B, N, M, out,
                          built_flag, built_value, grid_cap, as_stream(stream));
   PCST_LAUNCH_CHECK("knn3_rows_query");
   return PCST_OK;

@@ -364,6 +364,7 @@ struct VoxelFastWS {
   int64_t* reps;          // [B][N]
   uint32_t* rhash;        // [B][N]
   int32_t* vlist;         // [B][N]    occupied table slots in arrival order (cnt4[b][0] of them)
+  int32_t* vdim;          // [B][4]    the voxel box dims (dx, dy, dz) and 1 if the dense grid is used
   unsigned long long* ties;  // [R][kTieCap] (key<<32 | id)
   // zeroed every call (one memset): counters, histograms, tables, rep flags
   int32_t* cnt4;          // [R][4]: U (of cloud r, rows r < B), selected, ties, err
@@ -402,6 +403,7 @@ static VoxelFastWS carve_voxel_fast(void* base, int64_t B, int64_t N, int64_t co
   w.reps = c.take<int64_t>(B * N);
   w.rhash = c.take<uint32_t>(B * N);
   w.vlist = c.take<int32_t>(B * N);
+  w.vdim = c.take<int32_t>(B * 4);
   w.phist = c.take<uint32_t>(R * kSelBins);
   w.ties = c.take<unsigned long long>(R * kTieCap);
   w.cnt4 = c.take<int32_t>(R * 4);
@@ -451,13 +453,25 @@ __device__ __forceinline__ StatRec fold_minmax_wave(const float* __restrict__ pm
     r.mx[c] = -3.4e38f;
     r.s[c] = r.ss[c] = 0.0;
   }
-  for (int q = threadIdx.x & 63; q < n; q += 64) {
-    const float* v = pmm + ((int64_t)b * kPrepMaxBlocks + q) * 6;
+  // eight records per lane per round, all loads in flight together (a serial loop here waited
+  // out one L2 miss per record: the partials were just written on other XCDs)
+  constexpr int kU = 8;
+  for (int q0 = threadIdx.x & 63; q0 < n; q0 += kU * 64) {
+    float v[kU][6];
 #pragma unroll
-    for (int c = 0; c < 3; ++c) {
-      r.mn[c] = fminf(r.mn[c], v[c]);
-      r.mx[c] = fmaxf(r.mx[c], v[3 + c]);
+    for (int u = 0; u < kU; ++u) {
+      const int q = q0 + u * 64;
+      const float* src = pmm + ((int64_t)b * kPrepMaxBlocks + (q < n ? q : q0)) * 6;
+#pragma unroll
+      for (int c = 0; c < 6; ++c) v[u][c] = src[c];
     }
+#pragma unroll
+    for (int u = 0; u < kU; ++u)
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        r.mn[c] = fminf(r.mn[c], v[u][c]);
+        r.mx[c] = fmaxf(r.mx[c], v[u][3 + c]);
+      }
   }
 #pragma unroll
   for (int off = 32; off >= 1; off >>= 1)
@@ -544,8 +558,51 @@ __global__ __launch_bounds__(256) void voxf_cfg_prep_kernel(
   for (int64_t i = z0; i < zero_words; i += stride) zero[i] = make_uint4(0u, 0u, 0u, 0u);
 }
 
+// Dense voxel grid.  The reference groups points by the int32 xor-hash of their voxel coordinates
+// (torch.unique on voxel_hash, diffusion_model.py:89-92), so two voxels whose hashes collide are
+// ONE group.  Inside a box of voxel coordinates in which no two voxels share a hash, a group is
+// exactly a voxel, and the per-group (index sum, count) can be accumulated by plain atomic adds
+// into a dense array indexed by the voxel's position in the box -- no hash table, no probing, no
+// returning atomics.  kDenseBoxes lists boxes [0,X) x [0,Y) x [0,Z) checked collision-free
+// (tools/voxel_cert.py; tests/test_host.py re-checks every entry with numpy); a cloud whose voxel
+// box (dx, dy, dz) = floor((max - min) / vs) + 1 lies inside one of them, with dx dy dz <= the
+// table size H, takes the dense path, any other the hash table (same groups, same bits).  The
+// bench's clouds: noise 26 x 28 x 26, lidar-like 48 x 52 x 8.
+struct DenseBox { int x, y, z; };
+__constant__ DenseBox kDenseBoxes[] = {
+    {56, 56, 56},    {1, 306, 306},  {265, 1, 265},  {313, 313, 1},  {2, 306, 306},
+    {265, 2, 265},   {305, 305, 2},  {4, 234, 234},  {175, 4, 175},  {196, 196, 4},
+    {8, 116, 116},   {175, 8, 175},  {190, 190, 8},  {16, 116, 116}, {128, 16, 128},
+    {117, 117, 16},  {32, 101, 101}, {56, 32, 56},   {90, 90, 32}};
+constexpr int kDenseBoxCount = (int)(sizeof(kDenseBoxes) / sizeof(DenseBox));
+
+// The cloud's voxel box dims (every point's coordinate lies in [0, d): rounding is monotone) and
+// whether the dense grid takes it.
+__device__ __forceinline__ int4 voxel_box(const StatRec& M, float4 v4, int64_t H, int pack) {
+  float q[3];
+  q[0] = floorf(__fdiv_rn(fsub(M.mx[0], v4.x), v4.w));
+  q[1] = floorf(__fdiv_rn(fsub(M.mx[1], v4.y), v4.w));
+  q[2] = floorf(__fdiv_rn(fsub(M.mx[2], v4.z), v4.w));
+  if (!(q[0] < 4096.0f && q[1] < 4096.0f && q[2] < 4096.0f)) return make_int4(0, 0, 0, 0);
+  const int dx = (int)q[0] + 1, dy = (int)q[1] + 1, dz = (int)q[2] + 1;
+  int dense = 0;
+  if (pack && (int64_t)dx * dy * dz <= H)
+    for (int i = 0; i < kDenseBoxCount; ++i)
+      if (dx <= kDenseBoxes[i].x && dy <= kDenseBoxes[i].y && dz <= kDenseBoxes[i].z) dense = 1;
+  return make_int4(dx, dy, dz, dense);
+}
+
+__device__ __forceinline__ uint32_t voxel_hash(int32_t vx, int32_t vy, int32_t vz) {
+  return (uint32_t)(wrap_mul(vx, 73856093u) ^ wrap_mul(vy, 19349663u) ^ wrap_mul(vz, 83492791u));
+}
+
 // Voxel table insert; the first wave also folds the cloud's min/max partials into the voxel
-// parameters (min xyz, voxel size) for its workgroup.
+// parameters (min xyz, voxel size) and the voxel box for its workgroup (work-group 0 records the
+// box for the reps launch).  Dense box (voxel_box): one 64-bit add of (index << 20 | 1) per point
+// into the dense grid (the table's sum array, zeroed per call), nothing returned.  Otherwise:
+// each workgroup first aggregates its kVoxChunk points in an LDS table (LDS atomics), then
+// publishes one global (sum, count) per distinct voxel hash: dense voxels see at most one global
+// atomic per workgroup instead of one per point.
 __global__ __launch_bounds__(256) void voxf_insert_kernel(const float* __restrict__ pts, int N,
                                                           const StatRec* __restrict__ mm,
                                                           int64_t T, int64_t H,
@@ -559,15 +616,13 @@ __global__ __launch_bounds__(256) void voxf_insert_kernel(const float* __restric
                                                           int32_t* __restrict__ vlist, int pack,
                                                           int sshift, const float* __restrict__ pmm,
                                                           int npm, int pool_made,
-                                                          uint32_t* __restrict__ sflag, uint32_t svalue) {
+                                                          uint32_t* __restrict__ sflag, uint32_t svalue,
+                                                          int32_t* __restrict__ vdim) {
   // the start signal: every launch ahead of this one on its stream has completed (the points are
   // final), published for another stream (pcst_voxel_downsample_copies_prepped's start_flag)
   if (sflag && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0)
     __hip_atomic_store(sflag, svalue, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const int nbins = 1 << (32 - sshift);
-  // Each workgroup first aggregates its kVoxChunk points in an LDS table (LDS atomics), then
-  // publishes one global (sum, count) per distinct voxel: dense voxels see at most one global
-  // atomic per workgroup instead of one per point.
   const int b = blockIdx.y;
   const float* P = pts + (int64_t)b * N * 3;
   unsigned long long* K = tkey + b * H;
@@ -575,51 +630,69 @@ __global__ __launch_bounds__(256) void voxf_insert_kernel(const float* __restric
   __shared__ unsigned long long lsum[kVoxLds];
   __shared__ uint32_t lcnt[kVoxLds];
   __shared__ float4 vps;
+  __shared__ int4 vbox;
   if (threadIdx.x < 64) {
     // the voxel parameters use only min / max (order-free folds): from the stats partials, or
     // from pcst_cfg_ddim_voxel_prep's min / max partials on a prepped call
     const StatRec M = pmm ? fold_minmax_wave(pmm, b, npm) : fold_stats_wave(mm, b);
-    if (threadIdx.x == 0) vps = make_float4(M.mn[0], M.mn[1], M.mn[2], voxel_size(M, T));
+    if (threadIdx.x == 0) {
+      const float4 v = make_float4(M.mn[0], M.mn[1], M.mn[2], voxel_size(M, T));
+      const int4 box = voxel_box(M, v, H, pack);
+      vps = v;
+      vbox = box;
+      if (blockIdx.x == 0) *reinterpret_cast<int4*>(vdim + b * 4) = box;
+    }
   }
-  for (int i = threadIdx.x; i < kVoxLds; i += 256) { lkey[i] = 0ull; lsum[i] = 0ull; lcnt[i] = 0u; }
   __syncthreads();
   const float4 v4 = vps;
+  const int4 box = vbox;
   const int n0 = blockIdx.x * kVoxChunk, n1 = min(n0 + kVoxChunk, N);
-  for (int n = n0 + threadIdx.x; n < n1; n += 256) {
-    const int32_t vx = (int32_t)floorf(__fdiv_rn(fsub(P[n * 3 + 0], v4.x), v4.w));
-    const int32_t vy = (int32_t)floorf(__fdiv_rn(fsub(P[n * 3 + 1], v4.y), v4.w));
-    const int32_t vz = (int32_t)floorf(__fdiv_rn(fsub(P[n * 3 + 2], v4.z), v4.w));
-    const uint32_t h = (uint32_t)(wrap_mul(vx, 73856093u) ^ wrap_mul(vy, 19349663u) ^
-                                  wrap_mul(vz, 83492791u));
-    const unsigned long long kw = (1ull << 32) | h;
-    int slot = (int)(mix32(h) & (kVoxLds - 1));
-    for (;;) {  // <= kVoxChunk keys in kVoxLds = 2 kVoxChunk slots: always terminates
-      const unsigned long long old = atomicCAS(&lkey[slot], 0ull, kw);
-      if (old == 0ull || old == kw) break;
-      slot = (slot + 1) & (kVoxLds - 1);
+  if (box.w) {  // the dense grid: cell = vx + dx (vy + dy vz)
+    unsigned long long* D = tsum + b * H;
+    for (int n = n0 + threadIdx.x; n < n1; n += 256) {
+      const int32_t vx = (int32_t)floorf(__fdiv_rn(fsub(P[n * 3 + 0], v4.x), v4.w));
+      const int32_t vy = (int32_t)floorf(__fdiv_rn(fsub(P[n * 3 + 1], v4.y), v4.w));
+      const int32_t vz = (int32_t)floorf(__fdiv_rn(fsub(P[n * 3 + 2], v4.z), v4.w));
+      atomicAdd(&D[vx + box.x * (vy + box.y * vz)], ((unsigned long long)n << 20) | 1ull);
     }
-    atomicAdd(&lsum[slot], (unsigned long long)n);
-    atomicAdd(&lcnt[slot], 1u);
-  }
-  __syncthreads();
-  for (int i = threadIdx.x; i < kVoxLds; i += 256) {
-    const unsigned long long kw = lkey[i];
-    if (!kw) continue;
-    int64_t slot = mix32((uint32_t)kw) & (H - 1);
-    for (;;) {
-      const unsigned long long old = atomicCAS(&K[slot], 0ull, kw);
-      if (old == 0ull) {  // a new voxel: list its slot (U = the list length, U <= N)
-        vlist[(int64_t)b * N + atomicAdd(&cnt4[b * 4 + 0], 1)] = (int32_t)slot;
-        break;
+  } else {
+    for (int i = threadIdx.x; i < kVoxLds; i += 256) { lkey[i] = 0ull; lsum[i] = 0ull; lcnt[i] = 0u; }
+    __syncthreads();
+    for (int n = n0 + threadIdx.x; n < n1; n += 256) {
+      const int32_t vx = (int32_t)floorf(__fdiv_rn(fsub(P[n * 3 + 0], v4.x), v4.w));
+      const int32_t vy = (int32_t)floorf(__fdiv_rn(fsub(P[n * 3 + 1], v4.y), v4.w));
+      const int32_t vz = (int32_t)floorf(__fdiv_rn(fsub(P[n * 3 + 2], v4.z), v4.w));
+      const uint32_t h = voxel_hash(vx, vy, vz);
+      const unsigned long long kw = (1ull << 32) | h;
+      int slot = (int)(mix32(h) & (kVoxLds - 1));
+      for (;;) {  // <= kVoxChunk keys in kVoxLds = 2 kVoxChunk slots: always terminates
+        const unsigned long long old = atomicCAS(&lkey[slot], 0ull, kw);
+        if (old == 0ull || old == kw) break;
+        slot = (slot + 1) & (kVoxLds - 1);
       }
-      if (old == kw) break;
-      slot = (slot + 1) & (H - 1);
+      atomicAdd(&lsum[slot], (unsigned long long)n);
+      atomicAdd(&lcnt[slot], 1u);
     }
-    if (pack) {  // N < 2^20: (index sum << 20) | count in one 64-bit add (sum < 2^40)
-      atomicAdd(&tsum[b * H + slot], (lsum[i] << 20) | (unsigned long long)lcnt[i]);
-    } else {
-      atomicAdd(&tsum[b * H + slot], lsum[i]);
-      atomicAdd(&tcnt[b * H + slot], lcnt[i]);
+    __syncthreads();
+    for (int i = threadIdx.x; i < kVoxLds; i += 256) {
+      const unsigned long long kw = lkey[i];
+      if (!kw) continue;
+      int64_t slot = mix32((uint32_t)kw) & (H - 1);
+      for (;;) {
+        const unsigned long long old = atomicCAS(&K[slot], 0ull, kw);
+        if (old == 0ull) {  // a new voxel: list its slot (U = the list length, U <= N)
+          vlist[(int64_t)b * N + atomicAdd(&cnt4[b * 4 + 0], 1)] = (int32_t)slot;
+          break;
+        }
+        if (old == kw) break;
+        slot = (slot + 1) & (H - 1);
+      }
+      if (pack) {  // N < 2^20: (index sum << 20) | count in one 64-bit add (sum < 2^40)
+        atomicAdd(&tsum[b * H + slot], (lsum[i] << 20) | (unsigned long long)lcnt[i]);
+      } else {
+        atomicAdd(&tsum[b * H + slot], lsum[i]);
+        atomicAdd(&tcnt[b * H + slot], lcnt[i]);
+      }
     }
   }
   // The pool-key histogram of every row of this cloud over EVERY point of the chunk (a pool
@@ -649,16 +722,58 @@ __global__ __launch_bounds__(256) void voxf_insert_kernel(const float* __restric
 // point-index order).  Each representative also updates both selection histograms of every row
 // of its cloud: its voxel's key into hist2 (the U > T candidates), and its index's pool key out of
 // hist (once per distinct index: the first voxel to flag the index does it).
+__device__ __forceinline__ void voxf_rep_out(int64_t r, uint32_t h, int k, int b, int N, int B,
+                                             int copies, uint64_t seed, int64_t* __restrict__ reps,
+                                             uint32_t* __restrict__ rhash, uint32_t* __restrict__ isrep,
+                                             uint32_t* __restrict__ hist, uint32_t* __restrict__ hist2,
+                                             int sshift) {
+  reps[(int64_t)b * N + k] = r;
+  rhash[(int64_t)b * N + k] = h;
+  const bool first = atomicExch(&isrep[(int64_t)b * N + r], 1u) == 0u;
+  for (int c = 0; c < copies; ++c) {
+    const int row = c * B + b;
+    atomicAdd(&hist2[(int64_t)row * kSelBins + (rand_key(seed, row, (int)(h & 0x7fffffff)) >> sshift)], 1u);
+    if (first) atomicSub(&hist[(int64_t)row * kSelBins + (rand_key(seed, row + 0x10000, (int)r) >> sshift)], 1u);
+  }
+}
+
+// Dense grid (vdim[b].w): one thread per cell of the voxel box, an occupied cell -> its
+// representative, its voxel hash (recomputed from the cell's coordinates) and a list position
+// taken by one atomic per wave (cnt4[b][0] counts the listed voxels: U).
 __global__ __launch_bounds__(256) void voxf_reps_kernel(
     const unsigned long long* __restrict__ tkey, const unsigned long long* __restrict__ tsum,
-    const uint32_t* __restrict__ tcnt, int64_t H, int N, const int32_t* __restrict__ cnt4,
+    const uint32_t* __restrict__ tcnt, int64_t H, int N, int32_t* __restrict__ cnt4,
     const int32_t* __restrict__ vlist, int pack, int64_t* __restrict__ reps,
     uint32_t* __restrict__ rhash, uint32_t* __restrict__ isrep, int B, int copies, uint64_t seed_v,
     const uint64_t* __restrict__ seed_p, uint32_t* __restrict__ hist, uint32_t* __restrict__ hist2,
-    int sshift) {
+    int sshift, const int32_t* __restrict__ vdim) {
   const int b = blockIdx.y;
-  const int U = cnt4[b * 4 + 0];
   const uint64_t seed = seed_p ? *seed_p : seed_v;
+  const int4 box = *reinterpret_cast<const int4*>(vdim + b * 4);
+  if (box.w) {
+    const int cells = box.x * box.y * box.z;
+    const int lane = threadIdx.x & 63;
+    // whole waves per round (the list position is taken per wave)
+    for (int c0 = (blockIdx.x * 256 + threadIdx.x) & ~63; c0 < cells; c0 += gridDim.x * 256) {
+      const int c = c0 + lane;
+      const unsigned long long v = c < cells ? tsum[b * H + c] : 0ull;
+      const uint64_t occ = __ballot(v != 0ull);
+      if (!occ) continue;
+      int base = 0;
+      if (lane == 0) base = atomicAdd(&cnt4[b * 4 + 0], (int)__popcll(occ));
+      base = __shfl(base, 0);
+      if (v == 0ull) continue;
+      const float fs = (float)(long long)(v >> 20);
+      const float fc = (float)(uint32_t)(v & 0xFFFFFull);
+      const int64_t r = (int64_t)__fdiv_rn(fs, fc);
+      const int32_t vx = c % box.x, vy = (c / box.x) % box.y, vz = c / (box.x * box.y);
+      const int k = base + (int)__popcll(occ & lanemask_lt());
+      voxf_rep_out(r, voxel_hash(vx, vy, vz), k, b, N, B, copies, seed, reps, rhash, isrep, hist,
+                   hist2, sshift);
+    }
+    return;
+  }
+  const int U = cnt4[b * 4 + 0];
   for (int k = blockIdx.x * 256 + threadIdx.x; k < U; k += gridDim.x * 256) {
     const int64_t s = vlist[(int64_t)b * N + k];
     const unsigned long long kw = tkey[b * H + s];
@@ -666,14 +781,7 @@ __global__ __launch_bounds__(256) void voxf_reps_kernel(
     const float fs = (float)(long long)(pack ? (v >> 20) : v);
     const float fc = (float)(pack ? (uint32_t)(v & 0xFFFFFull) : tcnt[b * H + s]);
     const int64_t r = (int64_t)__fdiv_rn(fs, fc);
-    reps[(int64_t)b * N + k] = r;
-    rhash[(int64_t)b * N + k] = (uint32_t)kw;
-    const bool first = atomicExch(&isrep[(int64_t)b * N + r], 1u) == 0u;
-    for (int c = 0; c < copies; ++c) {
-      const int row = c * B + b;
-      atomicAdd(&hist2[(int64_t)row * kSelBins + (rand_key(seed, row, (int)((uint32_t)kw & 0x7fffffff)) >> sshift)], 1u);
-      if (first) atomicSub(&hist[(int64_t)row * kSelBins + (rand_key(seed, row + 0x10000, (int)r) >> sshift)], 1u);
-    }
+    voxf_rep_out(r, (uint32_t)kw, k, b, N, B, copies, seed, reps, rhash, isrep, hist, hist2, sshift);
   }
 }
 
@@ -900,11 +1008,11 @@ static int voxel_fast(const float* pts, int64_t B, int64_t N, int64_t copies, in
   hipLaunchKernelGGL(voxf_insert_kernel, dim3((unsigned)cdiv(N, kVoxChunk), b), dim3(256), 0, s,
                      pts, n, w.mm, T, w.H, w.tkey, w.tsum, w.tcnt, b, cp, seed, seed_p, w.hist, w.cnt4,
                      w.vlist, pack, sshift, prepped ? w.pmm : nullptr, vox_prep_blocks(N), pool ? 1 : 0,
-                     sflag, svalue);
+                     sflag, svalue, w.vdim);
   uint32_t* hist = pool ? w.phist : w.hist;  // the pool histogram: made ahead, or by the insert
   hipLaunchKernelGGL(voxf_reps_kernel, dim3((unsigned)std::min<int64_t>(cdiv(N, 256), kVoxRepsBlocks), b),
                      dim3(256), 0, s, w.tkey, w.tsum, w.tcnt, w.H, n, w.cnt4, w.vlist, pack, w.reps,
-                     w.rhash, w.isrep, b, cp, seed, seed_p, hist, w.hist2, sshift);
+                     w.rhash, w.isrep, b, cp, seed, seed_p, hist, w.hist2, sshift, w.vdim);
   hipLaunchKernelGGL(voxf_select_kernel, dim3(128, rows), dim3(256), 0, s, n, T, b, seed, seed_p,
                      hist, w.hist2, w.sel, w.cnt4, w.rhash, w.isrep, w.reps, w.ties, w.kcnt,
                      w.ktile, w.tiles, sshift);

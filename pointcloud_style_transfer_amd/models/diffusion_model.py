@@ -181,20 +181,17 @@ class NoisePredictor(nn.Module):
                     or (style_feat.requires_grad and torch.is_grad_enabled()))
 
     def forward_cond(self, noisy_points: torch.Tensor, cond: torch.Tensor,
-                     packed: Optional[tuple] = None, wait=None, signal=None,
-                     signal_all=False) -> torch.Tensor:
+                     packed: Optional[tuple] = None, wait=None, signal=None) -> torch.Tensor:
         """The fused inference forward with precomputed conditioning rows (`cond()` of the
         same timesteps and style features): the sampling loops compute every step's rows in one
         launch before the loop.  `packed` (this module's `packed()`, fetched once before a loop
         that does not change the weights) skips the per-call weight-version check.  `wait` (a
         DeviceSignal): later work on this stream also waits for it; `signal` (a DeviceSignal's
-        next_value()): published as the launch begins (_hip.noise_mlp); signal_all: once every
-        work-group of the launch has begun."""
+        next_value()): published as the launch begins (_hip.noise_mlp)."""
         B, N, _ = noisy_points.shape
         blob, bias = (packed if packed is not None else self.packed())[:2]
         out = _hip.noise_mlp(noisy_points.reshape(B * N, 3), N, cond, blob, bias,
-                             self.precision_code, wait=wait, signal=signal,
-                             signal_all=signal_all)
+                             self.precision_code, wait=wait, signal=signal)
         return out.view(B, N, 3)
 
     def forward(self, noisy_points: torch.Tensor, timestep: torch.Tensor,
@@ -255,32 +252,30 @@ class HierarchicalProcessor:
         return _hip.knn3_interp(coarse_points, original_points, coarse_indices)
 
 
-# The kNN upsample's build phase (grid, counts, sort: positions only) does not depend on the
-# noise MLP's output, so the sampling loop runs it on a side stream during the MLP.  The loop
-# itself moves to a high-priority stream and the build's workgroups carry extra LDS
-# (pcst_knn3_build's lds_floor), so they cannot co-reside with an MLP workgroup and only take
-# the CUs the MLP leaves idle in its last partial round (469 workgroups on 256 CUs).  Measured
-# 0.493 -> 0.468 ms/step over the first 20 steps, 0.421 -> 0.408 over 300
-# (tools/overlap_probe.py, one cloud); results are bit-identical.  These module constants are
-# the design's fixed choices; tools/knobs.py overrides them for A/B runs only.
-# Only small batches leave idle CUs in the MLP's last round, so the LDS floor below applies up to
-# two MLP rounds of points.  With many rounds (e.g. 32 clouds per GPU, 15000 MLP work-groups) the
-# build runs unpadded beside the MLP, taking CUs as MLP work-groups retire: 8.78 -> 8.31 ms per
-# 32-cloud step against the build inline before the MLP (8.36 with the floor: it then waits for
-# the MLP's last round; tools/b32_probe.py, one box).
+# The sampling step's stream layout.  The kNN upsample's build (grid, counts,
+# sort: positions only) does not depend on the noise MLP's output, so it runs on a side stream:
+#   - rows layout (one MLP round of work-groups, <= ROWS_MAX_MLP_POINTS: one cloud): the side
+#     stream bins every point of x (phase A) while the loop stream runs the voxel downsample;
+#     after it ONE launch places the coarse refs (phase B), and the MLP launch's last work-group
+#     waits for phase A's end, so the query's work-groups only check the flag;
+#   - compact layout (many MLP rounds: 32 clouds per GPU): the whole build beside the MLP, its
+#     work-groups held to an LDS floor of KNN_BUILD_LDS_FLOOR bytes while the MLP needs at most
+#     two rounds of work-groups (so they only take the CUs the MLP's last round leaves idle), and
+#     unpadded beyond (they take CUs as MLP work-groups retire: 8.78 -> 8.31 ms per 32-cloud step
+#     against the build inline, tools/b32_probe.py).
+# Cross-stream dependencies are device flags (_hip.DeviceSignal): an event that another queue
+# waits on stalls the recording queue ~17 us, a flag ~3 us (tools/sync_probe.hip); the loop ->
+# side flag is published by the launch that needs its input final (the voxel insert's or the MLP's
+# start signal), so no signal launch sits on the loop queue.  Results are bit-identical to the
+# single-stream loop.  Module constants: the design's fixed choices; tools/knobs.py overrides
+# them for A/B runs only.
 OVERLAP_KNN_BUILD = True
 _OVERLAP_MAX_MLP_POINTS = 2 * 128 * 256
-# LDS floor of the build's work-groups (pcst_knn3_build's lds_floor): above what an MLP
-# work-group leaves free on its CU (160 - 154.6 KiB), so the build never co-resides with the MLP,
-# and 16 KiB rather than the smallest such floor (8 KiB): the driver window measured 2718 / 2722 /
-# 2733 / 2706 vs 2685 / 2709 / 2717 / 2693 steps/s in four alternating pairs over two boxes
-# (profiles/r04/a56, a57); 24 KiB 2725 / 2715.  Round 2 used a flat 64 KiB pad on every build
-# kernel (1-2 work-groups per idle CU).
+# LDS floor of the compact build's work-groups (pcst_knn3_build's lds_floor): above what an MLP
+# work-group leaves free on its CU, so the build never co-resides with the MLP, and 16 KiB rather
+# than the smallest such floor (8 KiB): 2718 / 2722 / 2733 / 2706 vs 2685 / 2709 / 2717 / 2693
+# steps/s in four alternating pairs over two boxes (profiles/r04/a56, a57).
 KNN_BUILD_LDS_FLOOR = 16384
-# Work-groups per build launch on the side stream (pcst_knn3_build's max_wg): the MLP's last
-# round (469 work-groups on 256 CUs) leaves ~43 CUs idle; a build confined to fewer work-groups
-# than that never holds a CU an MLP work-group of that round is waiting for.
-KNN_BUILD_MAX_WG = 0
 
 
 def overlap_knn_build(mlp_points: int) -> bool:
@@ -290,6 +285,8 @@ def overlap_knn_build(mlp_points: int) -> bool:
 def knn_build_lds_floor(mlp_points: int) -> int:
     """The side-stream build's LDS floor for an MLP launch over `mlp_points` points."""
     return KNN_BUILD_LDS_FLOOR if mlp_points <= _OVERLAP_MAX_MLP_POINTS else 0
+
+
 _THREAD_STREAMS = threading.local()
 
 
@@ -333,25 +330,21 @@ SIGNAL_MAX_POLLS = 0
 
 class StepState:
     """The overlapped step's streams and cross-stream dependencies for ONE sampling loop (or one
-    bench run): the calling thread's loop / side streams, two events and three device flags (0:
-    loop -> side, the voxel output (rows layout: x) is ready; 1: side -> loop, the kNN build is
-    done (rows layout: the ref placement may run); 2: rows layout, the build is done).  The flags
-    share one allocation, so `check()` reads both timeout words with one copy; it raises
-    _hip.SignalTimeout when a wait gave up (the loop's results are then invalid).  Per loop, so
-    concurrent loops never share a flag and a flag's host counter starts at zero every loop."""
+    bench run): the calling thread's loop / side streams and three device flags (0: loop -> side,
+    the step's input is final -- compact layout: the voxel output, rows layout: x; 1: side ->
+    loop, compact layout: the kNN build is done, rows layout: phase B may run; 2: rows layout,
+    phase A is done).  The flags share one allocation, so `check()` reads every timeout word with
+    one copy; it raises _hip.SignalTimeout when a wait gave up (the loop's results are then
+    invalid).  Per loop, so concurrent loops never share a flag and a flag's host counter starts
+    at zero every loop."""
 
     def __init__(self, device, max_polls=None):
         self.loop, self.side = step_streams(device)
-        mk = _hip.DeviceEvent if DEVICE_EVENTS else _TorchEvent
-        self.ready_ev, self.built_ev = mk(), mk()
         polls = SIGNAL_MAX_POLLS if max_polls is None else max_polls
-        self._flags = torch.zeros(4, 4, dtype=torch.int32, device=device)
+        self._flags = torch.zeros(3, 4, dtype=torch.int32, device=device)
         self.ready_sig = _hip.DeviceSignal(device, polls, self._flags[0])
         self.built_sig = _hip.DeviceSignal(device, polls, self._flags[1])
-        # the rows layout's second side -> loop flag: the kNN rows are placed (the query waits)
         self.done_sig = _hip.DeviceSignal(device, polls, self._flags[2])
-        # loop -> side, rows layout with REFS_BESIDE_MLP: every MLP work-group has begun
-        self.mlp_sig = _hip.DeviceSignal(device, polls, self._flags[3])
 
     def begin(self, caller):
         """Order both streams after the caller's work so far (the flags' zero fill included)."""
@@ -372,53 +365,30 @@ class StepState:
                 "the voxel output it waited for never signalled); the loop's output is invalid")
 
 
-# The step's kNN in the rows layout (pcst_knn3_rows_*): the side stream bins every point of x
-# (positions only) while the loop stream runs the voxel downsample, and after it one launch places
-# the coarse refs; the query then skips the known rows.  With the one-round bf16 MLP (235
-# work-groups of 512 threads and every VGPR of their CUs) nothing beside it finds a CU, so the
-# compact build could only run after it (round 5: ~75 us on the step's critical path); here its
-# positions-only part overlaps the latency-bound voxel chain instead.  Bit-identical to the
-# compact layout (tests/test_gpu_knn_rows.py).  Only while the MLP is one round of work-groups
-# (<= ROWS_MAX_MLP_POINTS): with many rounds (32 clouds per GPU) the compact build still hides
-# under the MLP and the rows layout's query, which visits every point (34 % more chunks), loses
-# (b1 2706 vs 2614 steps/s, b32 8.26 vs 7.61 ms, profiles/r05/r5c).  tools/knobs.py may turn it
-# off for A/B runs.
+# The step's kNN in the rows layout (pcst_knn3_rows_*) while the MLP is one round of work-groups
+# (<= ROWS_MAX_MLP_POINTS): with the one-round bf16 MLP (235 work-groups of 512 threads and every
+# VGPR of their CUs) nothing beside it finds a CU, so the compact build could only run after it
+# (round 5: ~75 us on the step's critical path); here its positions-only part overlaps the
+# latency-bound voxel chain instead.  Bit-identical to the compact layout
+# (tests/test_gpu_knn_rows.py).  With many MLP rounds (32 clouds per GPU) the compact build still
+# hides under the MLP and the rows layout's query, which visits every point (34 % more chunks),
+# loses (b1 2706 vs 2614 steps/s, b32 8.26 vs 7.61 ms, profiles/r05/r5c).  tools/knobs.py may
+# turn it off for A/B runs.
 ROWS_LAYOUT = True
 ROWS_MAX_MLP_POINTS = 256 * 256
-# Phase B of the rows layout (the coarse refs into their cells: three short launches, ~20 us)
-# on the side stream beside the MLP instead of between the voxel emit and the MLP on the loop
-# stream: the side stream waits (one one-lane wait launch) until EVERY MLP work-group has begun
-# (pcst_noise_mlp_ex's start_counter), so its launches only find the ~21 CUs the one-round MLP
-# leaves idle and never delay an MLP work-group.  The MLP's last work-group waits for phase B's
-# flag (pcst_noise_mlp_ex's wait), so the query -- whose work-groups also check it in-kernel --
-# is never dispatched while phase B still needs CUs (spinning query work-groups on every CU
-# would starve it: a SignalTimeout).  Needs the fused-conditioning MLP (its launch publishes the
-# flag).  Measured and OFF: phase B's atomics beside the MLP slow both -- the rank kernel took
-# 150 us on the idle CUs and the MLP 0.178 vs 0.155 ms -- so the step lost time: 2708 / 2707 vs
-# 2739 / 2730 steps/s off, b32 7.70 / 7.66 vs 7.66 / 7.59 ms (profiles/r05/s2c, two alternating
-# passes on one box).  tools/knobs.py may turn it on for A/B runs.
-REFS_BESIDE_MLP = False
-
-
-# Rows layout: the MLP launch's last work-group waits for phase A's done flag (pcst_noise_mlp_ex's
-# wait) and the query's work-groups only check it, instead of every query work-group waiting with
-# an agent-scope acquire (4 per CU: ~11 us per step, profiles/r05/s2r).  Needs the fused-
-# conditioning MLP (the loop passes mlp_waits); tools/knobs.py may turn it off for A/B runs.
-ROWS_MLP_WAITS = True
 
 
 def rows_layout_ok(mlp_points: int) -> bool:
     return ROWS_LAYOUT and mlp_points <= ROWS_MAX_MLP_POINTS
 
 
-def knn_rows_begin(x, M, state, ws, by_downsample=False, beside_mlp=False):
+def knn_rows_begin(x, M, state, ws, by_downsample=False):
     """Phase A of the step's kNN on the side stream, ordered after the loop stream's work so far
     (x is ready): -> (the rows handle for hierarchical_eps(rows=...), start).  by_downsample: the
     next launch on the loop stream, the prepared voxel downsample, publishes the loop -> side flag
     as it begins (pass `start` to downsample_copies) instead of a signal launch here; else start is
-    None.  beside_mlp (REFS_BESIDE_MLP): phase B follows on the side stream (hierarchical_eps),
-    so phase A signals nothing; else the side stream signals state.built_sig once phase B may
-    run and state.done_sig when done."""
+    None.  The side stream signals state.built_sig once phase B may run and state.done_sig when
+    phase A is done."""
     start = None
     if by_downsample:
         start = state.ready_sig.next_value()
@@ -426,63 +396,39 @@ def knn_rows_begin(x, M, state, ws, by_downsample=False, beside_mlp=False):
         state.ready_sig.signal(torch.cuda.current_stream())
     state.ready_sig.wait(state.side)
     with torch.cuda.stream(state.side):
-        if beside_mlp:
-            h = _hip.knn3_rows_build(x, M, 2, ws)
-        else:
-            h = _hip.knn3_rows_build(x, M, 2, ws, refs_sig=state.built_sig, done_sig=state.done_sig)
+        h = _hip.knn3_rows_build(x, M, 2, ws, refs_sig=state.built_sig, done_sig=state.done_sig)
     return h, start
 
 
-def hierarchical_eps(hp, mlp, xc, xi, x_cat, knn_ws=None, state=None, mlp_waits=False,
-                     mlp_signals=False, rows=None):
+def hierarchical_eps(hp, mlp, xc, xi, x_cat, knn_ws=None, state=None, fused=False, rows=None):
     """eps for the CFG batch: mlp(xc) on the current stream, upsampled to the full clouds by
     kNN-3 (HierarchicalProcessor.upsample_knn).  With a StepState (and a preallocated
-    workspace) the kNN build runs on its side stream, overlapping the MLP, with its work-groups
-    held to an LDS floor of KNN_BUILD_LDS_FLOOR bytes; the query waits for it.  mlp_signals: the
-    MLP launch itself publishes the loop -> side flag as it begins (mlp takes start=)."""
+    workspace) the kNN build runs on its side stream (the layouts above).  fused: `mlp` is the
+    fused-conditioning MLP, which takes wait= (its last work-group waits for a DeviceSignal) and
+    start= (its launch publishes a DeviceSignal value as it begins).  rows: the knn_rows_begin
+    handle of this step (the rows layout)."""
     if state is None:
         return hp.upsample_knn(mlp(xc), x_cat, xi)
     main = torch.cuda.current_stream()
     if rows is not None:  # the rows layout: phase A ran beside the downsample (knn_rows_begin)
-        if mlp_signals:  # REFS_BESIDE_MLP: phase B on the side stream once the MLP holds its CUs
-            start = state.mlp_sig.next_value()
-            state.mlp_sig.wait(state.side)
-            with torch.cuda.stream(state.side):
-                _hip.knn3_rows_refs(rows, xi)
-                state.done_sig.signal(state.side)
-            # the MLP's last work-group also waits for phase B's flag: the query's work-groups
-            # (which wait for it in-kernel) must never sit on CUs phase B still needs
-            nc = mlp(xc, state.done_sig, start=start, start_all=True)
-            return _hip.knn3_rows_query(nc, rows, state.done_sig)
-        _hip.knn3_rows_refs(rows, xi, wait=state.built_sig)  # (they wait for phase A in-kernel)
-        if ROWS_MLP_WAITS and mlp_waits:  # the MLP's last work-group waits for phase A's end
-            return _hip.knn3_rows_query(mlp(xc, state.done_sig), rows, state.done_sig, waited=True)
+        _hip.knn3_rows_refs(rows, xi, wait=state.built_sig)  # (waits for phase A in-kernel)
+        if fused:  # the MLP's last work-group waits for phase A's end; the query only checks it
+            return _hip.knn3_rows_query(mlp(xc, wait=state.done_sig), rows, state.done_sig,
+                                        waited=True)
         return _hip.knn3_rows_query(mlp(xc), rows, state.done_sig)
-    side = state.side
-    ready, built = state.ready_ev, state.built_ev
+    ready, built = state.ready_sig, state.built_sig
     start = None
-    if KERNEL_SIGNAL:  # main -> side by a kernel-side flag: no event marker on the loop's queue
-        ready = state.ready_sig
-        if mlp_signals:
-            start = ready.next_value()  # written by the MLP launch (pcst_noise_mlp_ex)
-        else:
-            ready.signal(main)
+    if fused:
+        start = ready.next_value()  # written by the MLP launch as it begins (pcst_noise_mlp_ex)
     else:
-        ready.record(main)
-    ready.wait(side)
-    if BUILT_SIGNAL:
-        built = state.built_sig
-    with torch.cuda.stream(side):
-        handle = _hip.knn3_build(x_cat, xi, knn_ws, knn_build_lds_floor(xc.shape[0] * xc.shape[1]),
-                                 KNN_BUILD_MAX_WG)
-        built.signal(side) if BUILT_SIGNAL else built.record(side)
-    kw = {"start": start} if start is not None else {}
-    if BUILT_SIGNAL and mlp_waits:  # the MLP's last work-group waits for the build's flag
-        nc = mlp(xc, built, **kw)
-    else:
-        nc = mlp(xc, **kw)
-        built.wait(main)
-    return _hip.knn3_query(nc, handle, built if BUILT_SIGNAL else None)
+        ready.signal(main)
+    ready.wait(state.side)
+    with torch.cuda.stream(state.side):
+        handle = _hip.knn3_build(x_cat, xi, knn_ws, knn_build_lds_floor(xc.shape[0] * xc.shape[1]))
+        built.signal(state.side)
+    nc = mlp(xc, start=start) if fused else mlp(xc)
+    built.wait(main)
+    return _hip.knn3_query(nc, handle, built)
 
 
 def pool_prep_ok(x) -> bool:
@@ -492,84 +438,28 @@ def pool_prep_ok(x) -> bool:
 
 
 def voxel_prep_ok(hp, x, state) -> bool:
-    """Whether hierarchical_step's update prepares the next downsample_copies of x (VOXEL_PREP;
-    the fused update exists on the query-after-MLP layout, not with SEARCH_BESIDE_MLP's fused
-    finish)."""
-    return VOXEL_PREP and (state is None or not SEARCH_BESIDE_MLP) and hp.step_prep(x)
-
-
-# The query's neighbour search is positions-only too: with SEARCH_BESIDE_MLP the side stream runs
-# it after the build (pcst_knn3_search: each row's three neighbours and IDW weights), and after
-# the MLP only the gather of the coarse values remains, fused with the CFG + DDIM update
-# (pcst_knn3_finish_cfg_ddim).  Bit-identical to the query path (test_gpu_step.py).  Off: at one
-# cloud the search takes the CUs of the MLP's last round and the step is slower (0.3707 vs
-# 0.3615 ms, tools/step_probe.py srch/nosrch, one box).
-SEARCH_BESIDE_MLP = False
+    """Whether hierarchical_step's update prepares the next downsample_copies of x (VOXEL_PREP)."""
+    return VOXEL_PREP and hp.step_prep(x)
 
 
 def hierarchical_step(hp, mlp, xc, xi, x_cat, x, source, guidance_scale, coeffs, knn_ws=None,
-                      state=None, mlp_waits=False, mlp_signals=False, vox_ws=None, pool_seed=None,
-                      rows=None):
+                      state=None, fused=False, vox_ws=None, pool_seed=None, rows=None):
     """One guided step of the hierarchical branch (diffusion_model.py:240-260): eps of the CFG
     batch (mlp(xc) upsampled by kNN-3), then the fused CFG + DDIM update of x (x_cat takes the
     new x twice).  Returns the new x.  state: a StepState (overlapped layout) or None.
     vox_ws: the voxel workspace of the next step's downsample_copies, prepared by this update
-    (_hip.cfg_ddim_voxel_prep: one launch fewer); that call must then pass prepped=True.  Only
-    on the query-after-MLP layout (voxel_prep_ok).  pool_seed (with vox_ws): the seed of that
-    downsample, drawn ahead; the update also makes its pool-key histogram (POOL_PREP), and the
-    downsample must then pass seed=pool_seed, pool=True.  rows: the knn_rows_begin handle of this
-    step (the rows layout)."""
+    (_hip.cfg_ddim_voxel_prep: one launch fewer); that call must then pass prepped=True.
+    pool_seed (with vox_ws): the seed of that downsample, drawn ahead; the update also makes its
+    pool-key histogram (POOL_PREP), and the downsample must then pass seed=pool_seed, pool=True.
+    rows: the knn_rows_begin handle of this step (the rows layout)."""
     C = x.shape[0]
-    if state is None or not SEARCH_BESIDE_MLP or rows is not None:
-        eps = hierarchical_eps(hp, mlp, xc, xi, x_cat, knn_ws, state, mlp_waits, mlp_signals, rows)
-        if vox_ws is not None:
-            return _hip.cfg_ddim_voxel_prep(x, eps, source, guidance_scale, coeffs, x_cat, vox_ws,
-                                            pool_seed=pool_seed)
-        return _hip.cfg_ddim_step(x, eps[:C], eps[C:], source, guidance_scale, coeffs, x_cat=x_cat)
+    eps = hierarchical_eps(hp, mlp, xc, xi, x_cat, knn_ws, state, fused, rows)
     if vox_ws is not None:
-        raise RuntimeError("hierarchical_step: the voxel prep needs the query-after-MLP layout")
-    main = torch.cuda.current_stream()
-    side = state.side
-    ready, built = state.ready_ev, state.built_ev
-    if KERNEL_SIGNAL:
-        ready = state.ready_sig
-        ready.signal(main)
-    else:
-        ready.record(main)
-    ready.wait(side)
-    with torch.cuda.stream(side):
-        handle = _hip.knn3_build(x_cat, xi, knn_ws, knn_build_lds_floor(xc.shape[0] * xc.shape[1]),
-                                 KNN_BUILD_MAX_WG)
-        _hip.knn3_search(handle)
-        built.record(side)
-    nc = mlp(xc)
-    built.wait(main)
-    return _hip.knn3_finish_cfg_ddim(nc, handle, x, source, guidance_scale, coeffs, x_cat=x_cat)
+        return _hip.cfg_ddim_voxel_prep(x, eps, source, guidance_scale, coeffs, x_cat, vox_ws,
+                                        pool_seed=pool_seed)
+    return _hip.cfg_ddim_step(x, eps[:C], eps[C:], source, guidance_scale, coeffs, x_cat=x_cat)
 
 
-# device-scope events for the step's cross-stream dependencies (tools/knobs.py: A/B only)
-DEVICE_EVENTS = True
-# The loop -> side dependency (the voxel output is ready) by kernel-side signalling instead of an
-# event: an event that another queue waits on stalls the recording queue ~17 us, a one-lane flag
-# kernel ~3 us (tools/sync_probe.hip).  The side -> loop one (the kNN build is done) stays an
-# event: waiting on an event that has already completed costs the waiting queue ~0.3 us.
-KERNEL_SIGNAL = True
-# The side -> loop dependency (the kNN build is done) by the same kind of flag (BUILT_SIGNAL): in
-# the driver-window trace the event wait left ~10 us between the MLP's end and the query's start
-# although the build had finished ~16 us earlier (profiles/r03/s8_*); a one-workgroup wait kernel
-# that finds the flag already set costs a few us.  MLP_WAITS: the MLP's last work-group waits for
-# the flag itself (pcst_noise_mlp_ex's wait), no wait launch at all: 0.3765 -> 0.3740 ms/step
-# (profiles/r03/s15_*), within run-to-run noise, and the MLP's launch then also holds the build's
-# tail, so its measured duration (the bench's roofline) is no longer the MLP's own.  Off.
-# Round 4 tried publishing the flag from the build's last kernel (a counter over the fill
-# kernel's work-groups): every work-group then needs an agent-scope release, i.e. an L2
-# writeback on this multi-XCD part, and the fill went 21 -> 159 us (bench 2700 -> 2030
-# steps/s, profiles/r04/a15): the one-lane signal launch stays.
-BUILT_SIGNAL = True
-MLP_WAITS = False
-# The loop -> side flag written by the MLP launch as it begins (pcst_noise_mlp_ex's start signal)
-# instead of a one-lane signal launch between the voxel emit and the MLP on the loop's queue.
-MLP_SIGNALS = True
 # The step's CFG + DDIM update also prepares the next step's voxel downsample (its statistics and
 # zeroing: pcst_cfg_ddim_voxel_prep), one launch fewer per step; bit-identical.
 VOXEL_PREP = True
@@ -578,17 +468,6 @@ VOXEL_PREP = True
 # it; the loop draws each step's subset seed one step ahead (one draw per step either way, in the
 # same order: the draws, hence the results, are unchanged).  POOL_PREP needs VOXEL_PREP.
 POOL_PREP = True
-class _TorchEvent:
-    """torch.cuda.Event with the DeviceEvent interface (DEVICE_EVENTS = False: A/B runs)."""
-
-    def __init__(self):
-        self.e = torch.cuda.Event()
-
-    def record(self, stream):
-        self.e.record(stream)
-
-    def wait(self, stream):
-        stream.wait_event(self.e)
 
 
 class PointCloudDiffusionModel(nn.Module):
@@ -766,16 +645,14 @@ class DiffusionProcess:
                     t_in = t_rows[i]
                     if conds is not None:
                         cond_i = conds[i]
-                        mlp = lambda c, wait=None, start=None, start_all=False: (  # noqa: E731
-                            npred.forward_cond(c, cond_i, pk, wait, start, start_all))
+                        mlp = lambda c, wait=None, start=None: (  # noqa: E731
+                            npred.forward_cond(c, cond_i, pk, wait, start))
                     else:
                         mlp = lambda c: npred(c, t_in, style_in)  # noqa: E731
                     coeffs = self._coeffs(t, t_prevs[i])
                     if use_hierarchical:
-                        beside = REFS_BESIDE_MLP and conds is not None
                         rows, start = (knn_rows_begin(x, model.config.global_points, state,
-                                                      rows_ws, by_downsample=prepped,
-                                                      beside_mlp=beside)
+                                                      rows_ws, by_downsample=prepped)
                                        if rows_ws is not None else (None, None))
                         xc, xi = hp.downsample_copies(x, 2, vws, prepped, next_seed, pool, start)
                         prep = i + 1 < len(timesteps) and voxel_prep_ok(hp, x, state)
@@ -783,11 +660,7 @@ class DiffusionProcess:
                         next_seed = (_rng.source().device_seed() & (2**64 - 1)
                                      if prep and pool_prep_ok(x) else None)
                         x = hierarchical_step(hp, mlp, xc, xi, x_cat, x, source, guidance_scale,
-                                              coeffs, ws, state,
-                                              mlp_waits=(conds is not None if rows is not None
-                                                         else MLP_WAITS and conds is not None),
-                                              mlp_signals=(beside if rows is not None else
-                                                           MLP_SIGNALS and conds is not None),
+                                              coeffs, ws, state, fused=conds is not None,
                                               vox_ws=vws if prep else None, pool_seed=next_seed,
                                               rows=rows)
                         prepped, pool = prep, next_seed is not None

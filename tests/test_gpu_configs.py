@@ -506,19 +506,24 @@ def test_loop_vs_oracle_1000_steps_120k(det_state, golden, precision):
     assert mx <= 1e-4
 
 
-def test_timed_path_teacher_forced_vs_oracle_120k(det_state):
-    """The bench's timed path end to end: the guided loop with its DEVICE-drawn voxel
-    subsets (no replay: the prepared downsample, the pool histogram made by the previous update,
-    the rows-layout kNN on the side stream), fp32 noise MLP, the 1000-step schedule, 120k cloud.
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_timed_path_teacher_forced_vs_oracle_120k(det_state, precision):
+    """The bench's timed path end to end: the guided loop with its DEVICE-drawn
+    voxel subsets (no replay: the prepared downsample, the pool histogram made by the previous
+    update, the rows-layout kNN on the side stream), the 1000-step schedule, 120k cloud, with the
+    fp32 (parity) noise MLP and with the bf16 one -- the mode bench.py times.
     For each of the first 6 steps the loop's own (x, subset) are recorded; (a) each CFG row's
     subset is a valid draw of the reference's downsample (diffusion_model.py:90-120): U > T -> T
     of the representatives (as a multiset), U < T -> every representative plus T - U distinct
     non-representatives, computed by the oracle's voxel_reps on the same x; (b) the oracle's step
-    (noise MLP, exact kNN-3 IDW, CFG + DDIM update) from that x and subset gives the loop's next x
-    within the fp32 criterion carried through the CFG combination: the noise MLP agrees to 1e-4
-    rel per element, and eps_u + 7.5 (eps_c - eps_u) scales the two rows' error difference by up
-    to 16x, so 2e-3 rel for >= 99.9 % of the elements and every element within 2e-5 absolute
-    (x is ~|eps| ~ 1e-2 here; round 5 measured max 6e-6)."""
+    (exact f32 noise MLP, exact kNN-3 IDW, CFG + DDIM update) from that x and subset gives the
+    loop's next x within the MLP's per-element bound carried through the CFG combination:
+    eps_u + 7.5 (eps_c - eps_u) scales the two rows' error difference by up to 16x, so a factor 20
+    on the MLP's bound.  fp32: the noise MLP agrees to 1e-4 rel per element -> 2e-3 rel for
+    >= 99.9 % of the elements and every element within 2e-5 absolute (x is ~|eps| ~ 1e-2 here;
+    round 5 measured max 6e-6).  bf16: the MLP's measured-launch bound
+    (test_noise_mlp_bf16_per_element_60000: >= 99.9 % within 0.05 rel, every element within
+    0.25 max|f32|) -> >= 99.9 % within 1.0 rel and every element within 5 max|x'|."""
     from collections import Counter
 
     from conftest import assert_mostly_close
@@ -529,7 +534,7 @@ def test_timed_path_teacher_forced_vs_oracle_120k(det_state):
                                                                         PointCloudDiffusionModel)
     from pointcloud_style_transfer_amd.synthetic import standard_normal
 
-    cfg = Config(make_dirs=False, precision="fp32")
+    cfg = Config(make_dirs=False, precision=precision)
     model = PointCloudDiffusionModel(cfg)
     load_into(model)
     model = model.cuda().eval()
@@ -538,6 +543,7 @@ def test_timed_path_teacher_forced_vs_oracle_120k(det_state):
     cond = _clouds(2000, 1, 120000)
     xT = torch.from_numpy(standard_normal(3000, (1, 120000, 3)))
     K, T = 6, cfg.global_points
+    rtol, max_abs_of = (2e-3, lambda scale: 2e-5) if precision == "fp32" else (1.0, lambda scale: 5.0 * scale)
     hp = model.hierarchical_processor
     rec, styles = [], []
     real_down = hp.downsample_copies
@@ -583,7 +589,8 @@ def test_timed_path_teacher_forced_vs_oracle_120k(det_state):
         hip = rec[i + 1][0].cpu().numpy()
         d = np.abs(hip - nxt)
         rel = lambda r: np.mean(d <= r * (np.abs(nxt) + 0.1 * np.abs(nxt).max()))  # noqa: E731
-        print(f"step {i} t={int(ts[i])}: U={U}, max|x| {np.abs(nxt).max():.3e}, max abs "
-              f"{d.max():.3e}, within 1e-4 / 1e-3 / 2e-3 rel {rel(1e-4):.6f} / {rel(1e-3):.6f} / "
-              f"{rel(2e-3):.6f}")
-        assert_mostly_close(hip, nxt, rtol=2e-3, frac=0.999, max_abs=2e-5)
+        print(f"{precision} step {i} t={int(ts[i])}: U={U}, max|x| {np.abs(nxt).max():.3e}, max abs "
+              f"{d.max():.3e}, within 1e-4 / 1e-3 / 2e-3 / 5e-2 rel {rel(1e-4):.6f} / {rel(1e-3):.6f} / "
+              f"{rel(2e-3):.6f} / {rel(5e-2):.6f}")
+        assert_mostly_close(hip, nxt, rtol=rtol, frac=0.999,
+                            max_abs=max_abs_of(float(np.abs(nxt).max())))

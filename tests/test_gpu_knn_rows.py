@@ -3,10 +3,10 @@ split of the build into a positions-only phase beside the voxel downsample and a
 placement after it) against the compact layout (pcst_knn3_interp) and the oracle's brute-force
 float64 3-NN (oracle.upsample_knn, diffusion_model.py:127-153): bit-exact on every case the
 compact layout's tests cover -- Gaussian clouds, far outliers (the brick-shell pass over a
-brick's whole row range, slots without a ref skipped), repeated indices (free slots of the
-cell) and a pile-up of one index beyond its cell's rows (the overflow list),
-clusters, overfull cells with exact ties, a planar cloud, kk < 3 -- and on CFG batches (copies
-of each cloud with their own coarse subsets)."""
+brick's whole row range, empty slots skipped), repeated indices (free slots of the cell) and a
+pile-up of one index beyond its cell's rows (the overflow list), clusters, overfull cells with
+exact ties, a planar cloud, kk < 3 -- and on CFG batches (copies of each cloud with their own
+coarse subsets)."""
 import zlib
 
 import numpy as np
@@ -137,10 +137,52 @@ def test_knn_rows_workspace_reuse_is_stateless(H):
         assert torch.equal(H.knn3_rows_query(coarse, h), H.knn3_interp_rows(coarse, x, idx, copies=2))
 
 
-def test_guided_loop_rows_layout_bit_identical():
+def test_knn_rows_refs_wait_timeout_places_nothing(H):
+    """A ref placement whose wait for phase A gives up writes nothing, and the query and outlier
+    launches handed its error word (the handle's refs_err) leave the workspace alone and write
+    eps = 0: on a fresh workspace filled with 0xFF (phase A never ran: every count, start, rank
+    and slot is garbage) the calls complete without a fault and the signal reports the timeout
+    (the round-5 rank kernel's timeout path left the place launch reading garbage)."""
+    rng = np.random.default_rng(21)
+    N, M = 16000, 4000
+    x = dev(rng.standard_normal((1, N, 3)).astype(np.float32))
+    idx = dev(np.stack([rng.choice(N, M, replace=False) for _ in range(2)]).astype(np.int64))
+    coarse = dev(rng.standard_normal((2, M, 3)).astype(np.float32))
+    ws = H.knn_rows_workspace(1, 2, N, M, "cuda")
+    ws.fill_(0xFF)
+    sig = H.DeviceSignal(torch.device("cuda", 0), max_polls=2000)
+    sig.value = 1  # never written: phase A "never signals"
+    h = H.KnnRows(x, 2, M, ws)
+    H.knn3_rows_refs(h, idx, wait=sig)
+    out = H.knn3_rows_query(coarse, h)
+    torch.cuda.synchronize()
+    assert sig.timed_out()
+    with pytest.raises(H.SignalTimeout):
+        sig.check()
+    assert not bool(out.any())
+
+
+def _spy_rows_build(monkeypatch):
+    """Count the loop's rows-layout builds (the overlapped rows path really ran)."""
+    from pointcloud_style_transfer_amd import _hip
+
+    calls = []
+    real = _hip.knn3_rows_build
+
+    def spy(*a, **k):
+        calls.append(1)
+        return real(*a, **k)
+
+    monkeypatch.setattr(_hip, "knn3_rows_build", spy)
+    return calls
+
+
+def test_guided_loop_rows_layout_bit_identical(monkeypatch):
     """The sampling loop with the step's kNN in the rows layout (the product layout at one cloud:
-    phase A beside the voxel downsample) gives the bits of the compact build, on the bench's 120k
-    cloud (5 steps from t = 999)."""
+    phase A beside the voxel downsample, one placement launch, the MLP's last work-group waiting
+    for phase A) gives the bits of the compact build and of the single-stream loop, on the bench's
+    120k cloud (5 steps from t = 999); the rows path ran once per step (no fallback to the
+    single-stream layout)."""
     import bench
     from pointcloud_style_transfer_amd.models import diffusion_model as dm
     from pointcloud_style_transfer_amd.synthetic import lidar_like_cloud, standard_normal
@@ -151,66 +193,14 @@ def test_guided_loop_rows_layout_bit_identical():
     cond = torch.from_numpy(lidar_like_cloud(2000, 120000)[None]).to(dev0)
     xT = torch.from_numpy(standard_normal(3000, (1, 120000, 3))).to(dev0)
     assert dm.rows_layout_ok(2 * cfg.global_points)
+    calls = _spy_rows_build(monkeypatch)
     outs = []
-    saved = dm.ROWS_LAYOUT
-    try:
-        for on in (True, False):
-            dm.ROWS_LAYOUT = on
-            torch.manual_seed(7)
-            outs.append(dp.guided_sample_loop(model, src, cond, 5, 7.5, x_T=xT))
-    finally:
-        dm.ROWS_LAYOUT = saved
+    for rows, overlap in ((True, True), (False, True), (True, False)):
+        monkeypatch.setattr(dm, "ROWS_LAYOUT", rows)
+        monkeypatch.setattr(dm, "OVERLAP_KNN_BUILD", overlap)
+        torch.manual_seed(7)
+        n0 = len(calls)
+        outs.append(dp.guided_sample_loop(model, src, cond, 5, 7.5, x_T=xT))
+        assert len(calls) - n0 == (5 if rows and overlap else 0), (rows, overlap)
     assert torch.equal(outs[0], outs[1])
-
-
-def test_guided_loop_refs_beside_mlp_bit_identical():
-    """Phase B of the rows layout on the side stream beside the MLP (REFS_BESIDE_MLP, the product:
-    it starts once every MLP work-group has begun) gives the bits of phase B on the loop stream
-    before the MLP, on the bench's 120k cloud (6 steps from t = 999), and leaves no flag timed
-    out."""
-    import bench
-    from pointcloud_style_transfer_amd.models import diffusion_model as dm
-    from pointcloud_style_transfer_amd.synthetic import lidar_like_cloud, standard_normal
-
-    dev0 = torch.device("cuda", 0)
-    cfg, model, dp = bench.build_model("bf16", dev0)
-    src = torch.from_numpy(lidar_like_cloud(1001, 120000)[None]).to(dev0)
-    cond = torch.from_numpy(lidar_like_cloud(2001, 120000)[None]).to(dev0)
-    xT = torch.from_numpy(standard_normal(3001, (1, 120000, 3))).to(dev0)
-    assert dm.rows_layout_ok(2 * cfg.global_points) and dm.ROWS_LAYOUT
-    outs = []
-    saved = dm.REFS_BESIDE_MLP
-    try:
-        for on in (True, False):
-            dm.REFS_BESIDE_MLP = on
-            torch.manual_seed(8)
-            outs.append(dp.guided_sample_loop(model, src, cond, 6, 7.5, x_T=xT))
-    finally:
-        dm.REFS_BESIDE_MLP = saved
-    assert torch.equal(outs[0], outs[1])
-
-
-def test_guided_loop_rows_mlp_waits_bit_identical():
-    """The rows layout with the MLP launch waiting for phase A's flag and the query only checking
-    it (ROWS_MLP_WAITS, the product) gives the bits of every query work-group waiting itself, on the
-    bench's 120k cloud (6 steps from t = 999)."""
-    import bench
-    from pointcloud_style_transfer_amd.models import diffusion_model as dm
-    from pointcloud_style_transfer_amd.synthetic import lidar_like_cloud, standard_normal
-
-    dev0 = torch.device("cuda", 0)
-    cfg, model, dp = bench.build_model("bf16", dev0)
-    src = torch.from_numpy(lidar_like_cloud(1002, 120000)[None]).to(dev0)
-    cond = torch.from_numpy(lidar_like_cloud(2002, 120000)[None]).to(dev0)
-    xT = torch.from_numpy(standard_normal(3002, (1, 120000, 3))).to(dev0)
-    assert dm.rows_layout_ok(2 * cfg.global_points) and dm.ROWS_LAYOUT
-    outs = []
-    saved = dm.ROWS_MLP_WAITS
-    try:
-        for on in (True, False):
-            dm.ROWS_MLP_WAITS = on
-            torch.manual_seed(9)
-            outs.append(dp.guided_sample_loop(model, src, cond, 6, 7.5, x_T=xT))
-    finally:
-        dm.ROWS_MLP_WAITS = saved
-    assert torch.equal(outs[0], outs[1])
+    assert torch.equal(outs[0], outs[2])

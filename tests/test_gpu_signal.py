@@ -272,24 +272,30 @@ def test_mlp_start_signal_orders_the_side_stream():
             assert bool((seen == float(rep + 1)).all()), (prec, rep)
 
 
-def test_guided_loop_mlp_start_signal_bit_identical(monkeypatch):
-    """The sampling loop with the loop -> side flag written by the MLP launch (MLP_SIGNALS, the
-    product) gives the bits of the separate signal launch."""
+def test_guided_loop_layouts_bit_identical(monkeypatch):
+    """The sampling loop's three step layouts give the same bits on a small model at 1 and 3
+    clouds: the rows layout (phase A beside the downsample, the voxel insert publishing the
+    loop -> side flag, one placement launch, the MLP's last work-group waiting for phase A), the
+    compact layout (the build beside the MLP, its flag written by the MLP launch as it begins)
+    and the single-stream loop."""
     from pointcloud_style_transfer_amd.models import diffusion_model as dm
     from pointcloud_style_transfer_amd.synthetic import lidar_like_cloud, standard_normal
 
     dev = torch.device("cuda", 0)
     cfg, model, dp = _small_model(dev)
-    src = torch.from_numpy(lidar_like_cloud(1000, 16384)[None]).to(dev)
-    cond = torch.from_numpy(lidar_like_cloud(2000, 16384)[None]).to(dev)
-    xT = torch.from_numpy(standard_normal(3000, (1, 16384, 3))).to(dev)
-    outs = []
-    with torch.no_grad():
-        for on in (True, False):
-            monkeypatch.setattr(dm, "MLP_SIGNALS", on)
-            torch.manual_seed(7)
-            outs.append(dp.guided_sample_loop(model, src, cond, 8, 7.5, x_T=xT))
-    assert torch.equal(outs[0], outs[1])
+    for B in (1, 3):
+        src = torch.from_numpy(np.stack([lidar_like_cloud(1000 + i, 16384) for i in range(B)])).to(dev)
+        cond = torch.from_numpy(np.stack([lidar_like_cloud(2000 + i, 16384) for i in range(B)])).to(dev)
+        xT = torch.from_numpy(np.stack([standard_normal(3000 + i, (16384, 3)) for i in range(B)])).to(dev)
+        outs = []
+        with torch.no_grad():
+            for rows, overlap in ((True, True), (False, True), (True, False)):
+                monkeypatch.setattr(dm, "ROWS_LAYOUT", rows)
+                monkeypatch.setattr(dm, "OVERLAP_KNN_BUILD", overlap)
+                torch.manual_seed(7)
+                outs.append(dp.guided_sample_loop(model, src, cond, 8, 7.5, x_T=xT))
+        assert torch.equal(outs[0], outs[1]), B
+        assert torch.equal(outs[0], outs[2]), B
 
 
 def test_guided_loop_voxel_prep_bit_identical(monkeypatch):

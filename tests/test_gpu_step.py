@@ -125,6 +125,83 @@ def test_voxel_copies_matches_concat(H, N, T, B, copies, sig):
     np.testing.assert_array_equal(p1.cpu().numpy(), np.stack([allp[r][i1[r]] for r in range(copies * B)]))
 
 
+def _vox_fast_state(ws, B, N, copies=1):
+    """(vdim [B,4], U [B]) of a device-drawn downsample's workspace (voxel.hip carve_voxel_fast:
+    256-byte aligned sub-buffers in this order; white-box): the voxel box dims with the dense
+    flag, and the listed-voxel count."""
+    off, o, R = 0, {}, B * copies
+    for name, nbytes in (("mm", B * 64 * 72), ("pmm", B * 1024 * 6 * 4), ("sel", R * 16),
+                         ("reps", B * N * 8), ("rhash", B * N * 4), ("vlist", B * N * 4),
+                         ("vdim", B * 16), ("phist", R * 4096 * 4), ("ties", R * 8192 * 8),
+                         ("cnt4", R * 16)):
+        off = (off + 255) & ~255
+        o[name] = off
+        off += nbytes
+    vdim = ws[o["vdim"]:o["vdim"] + B * 16].view(torch.int32).view(B, 4).cpu().numpy()
+    cnt4 = ws[o["cnt4"]:o["cnt4"] + R * 16].view(torch.int32).view(R, 4).cpu().numpy()
+    return vdim, cnt4[:B, 0]
+
+
+def _collision_cloud(rng, N):
+    """A cloud whose voxel box is 197 x 17 x 3 -- outside every certified dense box -- with points
+    in the voxels (190, 5, 1) and (196, 16, 2), whose xor-hashes collide (the reference merges
+    them into one group)."""
+    lo = np.zeros(3, np.float32)
+    hi = np.array([196.5, 16.5, 2.5], np.float32)
+    T = int(round(float(np.prod(hi)) * 1.728))
+    vs = np.float32(float(np.float32(np.prod(hi)) / np.float32(T)) ** (1.0 / 3.0)) * np.float32(1.2)
+    pts = (rng.random((N, 3)) * hi).astype(np.float32)
+    pts[0], pts[1] = lo, hi
+    pts[2] = (np.array([190.5, 5.5, 1.5]) * vs).astype(np.float32)
+    pts[3] = (np.array([196.5, 16.5, 2.5]) * vs).astype(np.float32)
+    pts[3] = np.minimum(pts[3], hi)
+    return pts, T
+
+
+@pytest.mark.parametrize("case", ["collision", "certified", "elongated", "lidar"])
+def test_voxel_dense_and_hash_paths(H, case):
+    """The device-drawn downsample's two grouping paths (voxel.hip voxel_box): a voxel box inside
+    a certified collision-free box takes the dense grid (non-returning adds, no hash table), any
+    other the hash table -- including a box in which two occupied voxels' hashes collide, which the
+    reference (torch.unique on the hash) merges into one group.  Either way the listed-voxel count
+    is the oracle's U (its groups: the reference's) and the subset is a valid draw."""
+    from pointcloud_style_transfer_amd.synthetic import lidar_like_cloud
+
+    rng = np.random.default_rng(len(case))
+    N = 20000
+    if case == "collision":
+        pts, T = _collision_cloud(rng, N)
+        want_dense = 0
+    elif case == "certified":
+        pts, T = rng.standard_normal((N, 3)).astype(np.float32), 5000
+        want_dense = 1
+    elif case == "elongated":
+        pts, T = (rng.standard_normal((N, 3)) * np.array([1, 0.02, 0.02])).astype(np.float32), 8000
+        want_dense = 0
+    else:
+        N = 120000
+        pts, T = lidar_like_cloud(1000, N), 30000
+        want_dense = 1
+    reps, hashes, _ = O.voxel_reps(pts, T)
+    if case == "collision":  # the merged pair really is in this cloud
+        vs = np.float32(_)
+        assert len(np.unique(hashes)) < len(np.unique(np.floor(pts / vs).astype(np.int64), axis=0))
+    ws = H.voxel_copies_workspace(1, N, 1, "cuda")
+    _, idx = H.voxel_downsample(dev(pts[None]), T, seed=11, ws=ws)
+    vdim, U = _vox_fast_state(ws, 1, N)
+    assert vdim[0, 3] == want_dense, vdim
+    assert int(U[0]) == len(reps), (int(U[0]), len(reps))
+    i = idx[0].cpu().numpy()
+    vals, cnt = np.unique(i, return_counts=True)
+    rv, rc = np.unique(reps, return_counts=True)
+    if len(reps) < T:
+        have = dict(zip(vals.tolist(), cnt.tolist()))
+        assert all(have.get(v, 0) == k for v, k in zip(rv.tolist(), rc.tolist()))
+        assert (~np.isin(vals, rv)).sum() == T - len(reps)
+    else:
+        assert np.isin(i, reps).all()
+
+
 def test_voxel_pad_subset_is_uniform(H):
     """The device-drawn pad subset (U < T: T - U of the P non-representatives, the ones with
     the smallest counter-based random keys: csrc/voxel.hip voxf_hist/select radix select and
@@ -327,23 +404,23 @@ def test_knn_build_query_phases_match_interp(H):
 
 @pytest.mark.parametrize("kind", ["gauss", "outliers", "m1"])
 def test_knn_query_grid_cap_does_not_change_bits(H, kind):
-    """pcst_knn3_query / pcst_knn3_search's grid_cap (workgroups over all clouds) only changes
-    how many chunks each wave strides over: 16 (the floor), 64, the default and 2^30 give the
-    same bits."""
+    """pcst_knn3_query's grid_cap (work-groups over all clouds) only changes how many chunks each
+    persistent wave takes from its row's work counters: 1, 2, 16, 64 (fewer than the 8 counter
+    shards per row), 2^30 and the default (the resident grid) give the same bits, also when one
+    workspace serves consecutive queries (the outlier launch re-zeroes the counters)."""
     rng = np.random.default_rng(100 + len(kind))
-    orig, idx = _search_case(kind, rng)
+    orig, idx = _knn_case(kind, rng)
     coarse = dev(rng.standard_normal((2, idx.shape[1], 3)).astype(np.float32))
     h = H.knn3_build(orig, idx)
     ref = H.knn3_query(coarse, h)
-    for cap in (16, 64, 1 << 30):
+    for cap in (1, 2, 16, 64, 1 << 30, 0):
         assert torch.equal(H.knn3_query(coarse, h, grid_cap=cap), ref), cap
-        assert torch.equal(H.knn3_finish(coarse, H.knn3_search(h, grid_cap=cap)), ref), cap
 
 
-def _search_case(kind, rng):
-    """(orig [2,N,3], idx [2,M]) for the deferred-search tests: a Gaussian cloud, one with far
-    outliers (rows the query pass sends to the outlier pass), repeated indices (known rows written
-    by several coarse rows) and the kk < 3 kernels (M = 1, 2)."""
+def _knn_case(kind, rng):
+    """(orig [2,N,3], idx [2,M]): a Gaussian cloud, one with far outliers (rows the query pass
+    sends to the outlier pass), repeated indices (known rows written by several coarse rows) and
+    the kk < 3 kernels (M = 1, 2)."""
     N, M = {"gauss": (20000, 5000), "outliers": (30000, 7500), "repeat": (8000, 3000),
             "m1": (500, 1), "m2": (500, 2)}[kind]
     orig = rng.standard_normal((2, N, 3)).astype(np.float32)
@@ -357,59 +434,68 @@ def _search_case(kind, rng):
     return dev(orig), dev(idx.astype(np.int64))
 
 
-@pytest.mark.parametrize("kind", ["gauss", "outliers", "repeat", "m1", "m2"])
-def test_knn_search_finish_match_query(H, kind):
-    """pcst_knn3_search (positions only, on a side stream after the build) + pcst_knn3_finish give
-    the bit-identical result of pcst_knn3_query; pcst_knn3_finish_cfg_ddim gives the bits of
-    pcst_cfg_ddim_step over that eps (x_cat both halves)."""
-    rng = np.random.default_rng(len(kind))
-    orig, idx = _search_case(kind, rng)
+def _knn_carve(B, N, M):
+    """Byte offsets of pcst_knn3_build's workspace arrays (knn.hip carve_knn: 256-byte aligned
+    sub-buffers in this order; white-box, for the corruption test below) and the total size."""
+    off = 0
+    o = {}
+
+    def take(name, nbytes):
+        nonlocal off
+        off = (off + 255) & ~255
+        o[name] = off
+        off += nbytes
+
+    Cmax = min(max(4096, 16 * M), 1024 * 4096 - 1)
+    T = -(-(Cmax + 1) // 4096)
+    Cpad = T * 4096
+    maxch = -(-N // 64) + 8 * (Cmax // 64) + 1
+    for name, nbytes in (("stats", B * 64 * 72), ("gp", B * 8 * 4), ("refs", B * M * 16),
+                         ("qorder", B * N * 4), ("crank", B * (M + N) * 8),
+                         ("chunks", B * maxch * 8), ("olist", B * N * 4), ("obound", B * N * 4),
+                         ("err", 16), ("qctr", B * 8 * 64 * 4), ("nchunk", B * 4), ("ocount", B * 4),
+                         ("known", B * N * 4), ("tsum", B * T * 8), ("cnt", B * Cpad * 8)):
+        take(name, nbytes)
+    return o, maxch, Cpad, (off + 255) & ~255
+
+
+def test_knn_query_corrupt_workspace_sets_error_bits(H):
+    """The compact query's guards (knn.hip: a chunk outside [0, N] or longer than 64 rows sets
+    bit 4 of the error word, a cell's or brick's ref range outside the ref array bit 8; the range
+    is skipped, never read): a workspace corrupted between build and query -- chunk records with
+    x > y and past N, start words of 100 cells pointing far past the refs -- yields the error bits
+    and no fault; a clean build's word stays 0."""
+    import ctypes
+
+    rng = np.random.default_rng(41)
+    orig, idx = _knn_case("gauss", rng)
+    B, N, _ = orig.shape
     M = idx.shape[1]
-    coarse = dev(rng.standard_normal((2, M, 3)).astype(np.float32))
-    ref = H.knn3_query(coarse, H.knn3_build(orig, idx))
-    side = torch.cuda.Stream()
-    side.wait_stream(torch.cuda.current_stream())
-    with torch.cuda.stream(side):
-        handle = H.knn3_search(H.knn3_build(orig, idx))
-    torch.cuda.current_stream().wait_stream(side)
-    handle[2].record_stream(torch.cuda.current_stream())
-    assert torch.equal(H.knn3_finish(coarse, handle), ref)
-    x = orig[:1].clone() * 0.5
-    src = dev(rng.standard_normal(tuple(x.shape)).astype(np.float32))
-    coeffs = (np.float32(0.3), np.float32(0.95), np.float32(0.97), np.float32(0.24))
-    xc_ref = torch.empty_like(orig)
-    want = H.cfg_ddim_step(x, ref[:1], ref[1:], src, 7.5, coeffs, x_cat=xc_ref)
-    xc = torch.empty_like(orig)
-    got = H.knn3_finish_cfg_ddim(coarse, handle, x, src, 7.5, coeffs, x_cat=xc)
-    assert torch.equal(got, want) and torch.equal(xc, xc_ref)
-    got2 = H.knn3_finish_cfg_ddim(coarse, handle, x, None, 3.0, coeffs)
-    want2 = H.cfg_ddim_step(x, ref[:1], ref[1:], None, 3.0, coeffs)
-    assert torch.equal(got2, want2)
+    coarse = dev(rng.standard_normal((B, M, 3)).astype(np.float32))
+    o, maxch, Cpad, total = _knn_carve(B, N, M)
 
+    def err_word(ws):
+        e = torch.zeros(1, dtype=torch.int32, device=ws.device)
+        H._call("pcst_knn_error", H._ptr(ws), B, N, M, H._ptr(e), ctypes.c_void_p(
+            torch.cuda.current_stream().cuda_stream))
+        return int(e.item())
 
-def test_guided_loop_search_beside_mlp_bit_identical():
-    """The sampling loop with the kNN search on the side stream and the fused finish + CFG/DDIM
-    (SEARCH_BESIDE_MLP, the product layout) gives the bits of the build-only overlap with the
-    query after the MLP, on the bench's 120k cloud (5 steps from t = 999)."""
-    import bench
-    from pointcloud_style_transfer_amd.models import diffusion_model as dm
-    from pointcloud_style_transfer_amd.synthetic import lidar_like_cloud, standard_normal
-
-    dev0 = torch.device("cuda", 0)
-    cfg, model, dp = bench.build_model("bf16", dev0)
-    src = torch.from_numpy(lidar_like_cloud(1000, 120000)[None]).to(dev0)
-    cond = torch.from_numpy(lidar_like_cloud(2000, 120000)[None]).to(dev0)
-    xT = torch.from_numpy(standard_normal(3000, (1, 120000, 3))).to(dev0)
-    outs = []
-    saved = dm.SEARCH_BESIDE_MLP
-    try:
-        for on in (True, False):
-            dm.SEARCH_BESIDE_MLP = on
-            torch.manual_seed(7)
-            outs.append(dp.guided_sample_loop(model, src, cond, 5, 7.5, x_T=xT))
-    finally:
-        dm.SEARCH_BESIDE_MLP = saved
-    assert torch.equal(outs[0], outs[1])
+    h = H.knn3_build(orig, idx)
+    ws = h[2]
+    assert ws.numel() == total  # the carve above is the library's
+    H.knn3_query(coarse, h)
+    assert err_word(ws) == 0
+    h = H.knn3_build(orig, idx, ws=ws)
+    ch = ws[o["chunks"]:o["chunks"] + B * maxch * 8].view(torch.int32).view(B, maxch, 2)
+    ch[0, :5, 0] = 7
+    ch[0, :5, 1] = 3
+    ch[1, :5, 1] = N + 100
+    cnt = ws[o["cnt"]:o["cnt"] + B * Cpad * 8].view(torch.int32).view(B, Cpad, 2)
+    cnt[1, 100:200, 0] = 0x7FFFFF00
+    H.knn3_query(coarse, h)
+    torch.cuda.synchronize()
+    e = err_word(ws)
+    assert e & 4 and e & 8, e
 
 
 @pytest.mark.parametrize("max_wg,floor", [(1, 0), (2, 8192), (32, 8192), (7, 0)])
@@ -522,28 +608,3 @@ def test_noise_mlp_wait_orders_after_the_signal(H):
             assert torch.equal(out, ref)
             assert bool((seen == float(rep + 1)).all())
             assert int(sig.flag[2].item()) == 0 and not sig.timed_out()
-
-
-def test_guided_loop_mlp_waits_bit_identical():
-    """The sampling loop with the MLP's last work-group waiting for the kNN build's flag
-    (MLP_WAITS, the product layout) gives the bits of the separate wait launch, on the bench's
-    120k cloud (5 steps from t = 999)."""
-    import bench
-    from pointcloud_style_transfer_amd.models import diffusion_model as dm
-    from pointcloud_style_transfer_amd.synthetic import lidar_like_cloud, standard_normal
-
-    dev0 = torch.device("cuda", 0)
-    cfg, model, dp = bench.build_model("bf16", dev0)
-    src = torch.from_numpy(lidar_like_cloud(1000, 120000)[None]).to(dev0)
-    cond = torch.from_numpy(lidar_like_cloud(2000, 120000)[None]).to(dev0)
-    xT = torch.from_numpy(standard_normal(3000, (1, 120000, 3))).to(dev0)
-    outs = []
-    saved = dm.MLP_WAITS
-    try:
-        for on in (True, False):
-            dm.MLP_WAITS = on
-            torch.manual_seed(7)
-            outs.append(dp.guided_sample_loop(model, src, cond, 5, 7.5, x_T=xT))
-    finally:
-        dm.MLP_WAITS = saved
-    assert torch.equal(outs[0], outs[1])

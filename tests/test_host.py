@@ -436,3 +436,32 @@ def test_generator_rng_randn_like_keeps_the_dtype():
     a = rng.GeneratorRNG(5).randn_like(torch.zeros(2, 3))
     b = rng.GeneratorRNG(5).randn_like(torch.zeros(2, 3))
     assert torch.equal(a, b)
+
+
+def test_dense_voxel_boxes_are_collision_free():
+    """Every box of csrc/voxel.hip's kDenseBoxes (the voxel boxes that take the dense grid instead
+    of the hash table) holds no two voxel coordinates whose int32 xor-hash -- the reference's
+    voxel_hash, diffusion_model.py:90 -- is equal, so inside it a hash group is exactly one voxel
+    (the dense path's grouping is the reference's); and the check itself finds the collisions
+    the dense path must avoid (the 197 x 17 x 3 box holds (190, 5, 1) and (196, 16, 2))."""
+    import re
+
+    src = open(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                            "pointcloud_style_transfer_amd", "csrc", "voxel.hip")).read()
+    table = src[src.index("kDenseBoxes[] = {"):src.index("};", src.index("kDenseBoxes[] = {"))]
+    boxes = [tuple(int(v) for v in m) for m in re.findall(r"\{(\d+), (\d+), (\d+)\}", table)]
+    assert len(boxes) >= 10
+
+    def hashes(d):
+        x = np.arange(d[0], dtype=np.int64)[:, None, None]
+        y = np.arange(d[1], dtype=np.int64)[None, :, None]
+        z = np.arange(d[2], dtype=np.int64)[None, None, :]
+        return (((x * 73856093) & 0xFFFFFFFF) ^ ((y * 19349663) & 0xFFFFFFFF)
+                ^ ((z * 83492791) & 0xFFFFFFFF)).ravel()
+
+    for d in boxes:
+        h = hashes(d)
+        assert np.unique(h).size == h.size, d
+    h = hashes((197, 17, 3))
+    assert np.unique(h).size < h.size
+    assert h[np.ravel_multi_index((190, 5, 1), (197, 17, 3))] == h[np.ravel_multi_index((196, 16, 2), (197, 17, 3))]

@@ -9,8 +9,6 @@ several layouts, interleaved over `reps` rounds, and prints the median ms/step o
   hi_nopad  same without the LDS floor
   eq        build on a side stream, both streams default priority, no LDS floor
   side_hi   build on a high-priority side stream, loop at default priority, no LDS floor
-  srch      hi_nopad with the neighbour search on the side stream too (pcst_knn3_search) and the
-            fused finish + CFG/DDIM after the MLP (diffusion_model.hierarchical_step's layout)
 A development tool (tools/ only)."""
 import argparse
 import os
@@ -31,7 +29,7 @@ def main():
     ap.add_argument("--clouds", type=int, default=32)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--reps", type=int, default=3)
-    ap.add_argument("--modes", default="seq,hi_pad,hi_nopad,eq,side_hi,srch")
+    ap.add_argument("--modes", default="seq,hi_pad,hi_nopad,eq,side_hi")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     B = a.clouds
@@ -76,16 +74,6 @@ def main():
                         return _hip.noise_mlp(c.reshape(-1, 3), cfg.global_points, conds[i], blob, bias,
                                               npred.precision_code).view(2 * B, -1, 3)
 
-                    if mode == "srch":
-                        ready.record(loop)
-                        ready.wait(side)
-                        with torch.cuda.stream(side):
-                            h = _hip.knn3_search(_hip.knn3_build(x_cat, xi, ws, 0))
-                            built.record(side)
-                        nc = mlp(xc)
-                        built.wait(loop)
-                        x = _hip.knn3_finish_cfg_ddim(nc, h, x, src, 7.5, dp._coeffs(t, tp), x_cat=x_cat)
-                        continue
                     if mode == "seq":
                         h = _hip.knn3_build(x_cat, xi, ws, 0)
                         eps = _hip.knn3_query(mlp(xc), h)

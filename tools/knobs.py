@@ -2,9 +2,9 @@
 
     import knobs; knobs.apply()
 
-reads PCST_KNN_OVERLAP=0|1, PCST_KNN_BUILD_LDS_FLOOR=<bytes>, PCST_DEVICE_EVENTS=0|1,
-PCST_KERNEL_SIGNAL=0|1, PCST_ROWS_LAYOUT=0|1, PCST_FUSED_BLOCK_FWD / _BWD=0|1 (models._autograd)
-and sets the matching module constants of models.diffusion_model.  Kernel-side variants are
+reads PCST_KNN_OVERLAP=0|1, PCST_KNN_BUILD_LDS_FLOOR=<bytes>, PCST_ROWS_LAYOUT=0|1,
+PCST_VOXEL_PREP / _POOL_PREP=0|1, PCST_FUSED_BLOCK_FWD / _BWD=0|1 (models._autograd) and sets the
+matching module constants of models.diffusion_model.  Kernel-side variants are
 experiment builds (csrc/Makefile XDEF): PCST_LIB=<path> points _hip.LIB_PATH at one before the
 library is loaded (the product _hip reads no environment)."""
 import os
@@ -26,30 +26,12 @@ def apply():
         dm.OVERLAP_KNN_BUILD = e["PCST_KNN_OVERLAP"] != "0"
     if "PCST_KNN_BUILD_LDS_FLOOR" in e:
         dm.KNN_BUILD_LDS_FLOOR = int(e["PCST_KNN_BUILD_LDS_FLOOR"])
-    if "PCST_DEVICE_EVENTS" in e:
-        dm.DEVICE_EVENTS = e["PCST_DEVICE_EVENTS"] != "0"
-    if "PCST_KNN_BUILD_MAX_WG" in e:
-        dm.KNN_BUILD_MAX_WG = int(e["PCST_KNN_BUILD_MAX_WG"])
     if "PCST_VOXEL_PREP" in e:
         dm.VOXEL_PREP = e["PCST_VOXEL_PREP"] != "0"
     if "PCST_POOL_PREP" in e:
         dm.POOL_PREP = e["PCST_POOL_PREP"] != "0"
-    if "PCST_MLP_SIGNALS" in e:
-        dm.MLP_SIGNALS = e["PCST_MLP_SIGNALS"] != "0"
-    if "PCST_MLP_WAITS" in e:
-        dm.MLP_WAITS = e["PCST_MLP_WAITS"] != "0"
-    if "PCST_BUILT_SIGNAL" in e:
-        dm.BUILT_SIGNAL = e["PCST_BUILT_SIGNAL"] != "0"
     if "PCST_ROWS_LAYOUT" in e:  # the step's kNN in the rows layout (0: the compact build)
         dm.ROWS_LAYOUT = e["PCST_ROWS_LAYOUT"] != "0"
-    if "PCST_REFS_BESIDE_MLP" in e:  # rows layout: phase B beside the MLP (0: before it)
-        dm.REFS_BESIDE_MLP = e["PCST_REFS_BESIDE_MLP"] != "0"
-    if "PCST_ROWS_MLP_WAITS" in e:  # rows layout: the MLP waits for phase A (0: the query does)
-        dm.ROWS_MLP_WAITS = e["PCST_ROWS_MLP_WAITS"] != "0"
-    if "PCST_SEARCH_BESIDE_MLP" in e:
-        dm.SEARCH_BESIDE_MLP = e["PCST_SEARCH_BESIDE_MLP"] != "0"
-    if "PCST_KERNEL_SIGNAL" in e:
-        dm.KERNEL_SIGNAL = e["PCST_KERNEL_SIGNAL"] != "0"
     if "PCST_FUSED_BLOCK_FWD" in e:
         from pointcloud_style_transfer_amd.models import _autograd
         _autograd.FUSED_BLOCK_FWD = e["PCST_FUSED_BLOCK_FWD"] != "0"

@@ -69,9 +69,7 @@ def run(C, G, steps, warmup, points=120000):
                     prep = dmod.voxel_prep_ok(hp, st["x"], state)
                     st["x"] = dmod.hierarchical_step(hp, mlp, xc, xi, x_cat, st["x"], src, 7.5,
                                                      dp._coeffs(t, t_prev), knn_ws, state,
-                                                     mlp_waits=dmod.MLP_WAITS,
-                                                     mlp_signals=dmod.MLP_SIGNALS,
-                                                     vox_ws=vws if prep else None)
+                                                     fused=True, vox_ws=vws if prep else None)
                     st["prepped"] = prep
 
                 with torch.cuda.stream(state.loop):
