@@ -441,6 +441,21 @@ __global__ __launch_bounds__(256) void knn_fill_kernel(const float* __restrict__
   }
 }
 
+// Rows layout fill: row n of cloud b at its cell-order position, as (x, y, z, n), so the query
+// reads a chunk's rows with one load (no index -> position chain).
+__global__ __launch_bounds__(256) void knn_rows_fill_kernel(const float* __restrict__ x, int64_t N,
+                                                            int64_t Cpad, const uint64_t* __restrict__ start,
+                                                            const int2* __restrict__ crank,
+                                                            float4* __restrict__ xs) {
+  const int b = blockIdx.y;
+  const uint64_t* S = start + b * Cpad;
+  for (int64_t n = (int64_t)blockIdx.x * 256 + threadIdx.x; n < N; n += gridDim.x * 256) {
+    const int2 cr = crank[b * N + n];
+    const float* p = x + (b * N + n) * 3;
+    xs[b * N + (uint32_t)(S[cr.x] >> 32) + (uint32_t)cr.y] = make_float4(p[0], p[1], p[2], __int_as_float((int)n));
+  }
+}
+
 // ---- Rows layout (the sampling loop's step: pcst_knn3_rows_build / _refs / _query) ----
 // Phase A needs the clouds' positions only, so the loop runs it beside the voxel downsample
 // (before the coarse indices exist): every row of cloud cl is binned (statistics, grid, per-cell
@@ -463,7 +478,7 @@ __global__ __launch_bounds__(256) void knn_fill_kernel(const float* __restrict__
 struct KnnRowsWS {
   StatRec* stats;    // [C][kStatBlocks]
   float* gp;         // [C][8]
-  int32_t* qorder;   // [C][N] rows in cell order
+  float4* xs;        // [C][N] rows in cell order: (x, y, z, point index n)
   int2* crank;       // [C][N] (cell, rank in cell)
   uint2* chunks;     // [C][maxch] row ranges [q0, q1) of <= 64 rows inside one brick
   float4* refs;      // [B][N] refs (x, y, z, j) at the front of their cell's row range
@@ -478,7 +493,7 @@ struct KnnRowsWS {
   int32_t* nchunk;   // [C]
   int32_t* ocount;   // [B]
   int32_t* ovn;      // [B] overflow refs
-  uint32_t* known;   // [B][N] j+1 of the last ref naming n, 0 = a query row
+  uint32_t* known;   // [B][N] j+1 of the last ref naming the row at cell-order position p, 0 = a query
   uint32_t* rcnt;    // [B][Cpad] refs ranked per cell
   uint32_t* bcnt;    // [B][Cpad / 64] the brick copy's ref counts (written if nonzero)
   uint64_t* tsum;    // [C][T]
@@ -498,7 +513,7 @@ static KnnRowsWS carve_knn_rows(void* base, int64_t C, int64_t copies, int64_t N
   w.maxch = cdiv(N, 64) + 8 * (w.Cmax / 64) + 1;
   w.stats = c.take<StatRec>(C * kStatBlocks);
   w.gp = c.take<float>(C * 8);
-  w.qorder = c.take<int32_t>(C * N);
+  w.xs = c.take<float4>(C * N);
   w.crank = c.take<int2>(C * N);
   w.chunks = c.take<uint2>(C * w.maxch);
   w.refs = c.take<float4>(w.B * N);
@@ -549,9 +564,10 @@ __device__ bool block_wait_flag(const uint32_t* flag, uint32_t value, int32_t* w
   return s_ok != 0;
 }
 
-// Phase B: ref j of CFG row b (cloud b % C): its known mark (the last j wins), its rank in its
-// point's cell (both atomics issued together) and its slot start(cell) + rank at the front of the
-// cell's row range; a rank beyond the cell's rows sends the ref to the overflow list instead.
+// Phase B: ref j of CFG row b (cloud b % C): its known mark at its point's cell-order position
+// (the last j wins), its rank in its point's cell (both atomics issued together) and its slot
+// start(cell) + rank at the front of the cell's row range; a rank beyond the cell's rows sends the
+// ref to the overflow list instead.
 // wflag (optional): the side stream's phase-A flag; every work-group waits until it holds wvalue
 // (the consumer side of the guide's hand-off: one relaxed poll loop, one agent-scope acquire, a
 // barrier), so no wait launch sits in front of this one; a work-group whose wait gives up sets
@@ -578,10 +594,11 @@ __global__ __launch_bounds__(256) void knn_rows_place_kernel(
       atomicOr(err, 1);
       continue;
     }
-    const int cell = crank[cl * N + n].x;
-    atomicMax(&known[b * N + n], (uint32_t)(j + 1));
+    const int2 cr = crank[cl * N + n];
+    const int cell = cr.x;
     const uint32_t rank = atomicAdd(&rcnt[b * Cpad + cell], 1u);
     const uint32_t a = (uint32_t)(S[cell] >> 32), rows = (uint32_t)(S[cell + 1] >> 32) - a;
+    atomicMax(&known[b * N + a + (uint32_t)cr.y], (uint32_t)(j + 1));  // n's cell-order position
     const float* p = x + (cl * N + n) * 3;
     const float4 r = make_float4(p[0], p[1], p[2], __int_as_float((int)j));
     if (rank < rows) refs[b * N + a + rank] = r;
@@ -972,7 +989,8 @@ __device__ __forceinline__ bool settled(const Query& me, const Box& cells, const
 // overflow refs (repeated indices) are offered to every query.
 struct KArgs {
   int64_t C;                  // clouds holding the grid / rows / chunks (compact: B)
-  const uint32_t* known;      // [B][N] (rows layout)
+  const uint32_t* known;      // [B][N] by cell-order position (rows layout)
+  const float4* xs;           // [C][N] the rows in cell order (rows layout)
   const uint32_t* rcnt;       // [B][Cpad] refs placed per cell (rows layout)
   const float4* over;         // [B][M] overflow refs (rows layout)
   const int32_t* ovn;         // [B] their counts (rows layout)
@@ -1133,11 +1151,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
       continue;
     }
     bool valid = ch.x + lane < ch.y;
-    const int64_t n = qorder[cl * N + (valid ? ch.x + lane : ch.x)];
-    const float* qp = orig + (cl * N + n) * 3;
-    if constexpr (ROWS) {  // a known row takes its coarse value (the last coarse row naming it)
-      const uint32_t kn = valid ? ka.known[b * N + n] : 0u;
-      if (kn) {
+    const uint32_t pos = valid ? ch.x + lane : ch.x;
+    int64_t n;
+    float qx, qy, qz;
+    if constexpr (ROWS) {  // the row and its known mark by cell-order position, loaded together
+      const float4 q = ka.xs[cl * N + pos];
+      const uint32_t kn = valid ? ka.known[b * N + pos] : 0u;
+      n = __float_as_int(q.w);
+      qx = q.x; qy = q.y; qz = q.z;
+      if (kn) {  // a known row takes its coarse value (the last coarse row naming it)
         const float* v = V + (int64_t)(kn - 1) * 3;
         float* o = out + (b * N + n) * 3;
         o[0] = v[0]; o[1] = v[1]; o[2] = v[2];
@@ -1147,9 +1169,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
         item = take();
         continue;
       }
+    } else {
+      n = qorder[cl * N + pos];
+      const float* qp = orig + (cl * N + n) * 3;
+      qx = qp[0]; qy = qp[1]; qz = qp[2];
     }
     Query me;
-    me.init(qp[0], qp[1], qp[2]);
+    me.init(qx, qy, qz);
     const int cx = cell_coord(me.fx, g.o[0], g.inv, g.d[0]);
     const int cy = cell_coord(me.fy, g.o[1], g.inv, g.d[1]);
     const int cz = cell_coord(me.fz, g.o[2], g.inv, g.d[2]);
@@ -1536,8 +1562,8 @@ static void launch_knn_query(int64_t nch_max, const float* gp, const uint64_t* c
 static void launch_knn_query(const KnnWS& w, const float* coarse, const float* orig, int64_t B,
                              int64_t N, int64_t M, float* out, const uint32_t* bflag,
                              uint32_t bvalue, int64_t grid_cap, hipStream_t s) {
-  const KArgs ka = {B, nullptr, nullptr, nullptr, nullptr, w.err, nullptr, 0, nullptr, w.qctr,
-                    nullptr, nullptr};
+  const KArgs ka = {B, nullptr, nullptr, nullptr, nullptr, nullptr, w.err, nullptr, 0, nullptr,
+                    w.qctr, nullptr, nullptr};
   launch_knn_query<false>(w.maxch, w.gp, w.cnt, w.refs, w.qorder, w.chunks, w.nchunk, w.olist,
                           w.obound, w.ocount, w.known, w.Cpad, ka, coarse, orig, B, N, M, out,
                           bflag, bvalue, grid_cap, s);
@@ -1624,9 +1650,8 @@ extern "C" int pcst_knn3_rows_build(const float* x, int64_t C, int64_t copies, i
                      w.Cpad, w.chunks, w.maxch, w.nchunk);
   // the ref placement reads the starts and the rows' cells, not the fill's row order
   if (refs_flag) hipLaunchKernelGGL(knn_flag_kernel, dim3(1), dim3(64), 0, s, refs_flag, refs_value);
-  hipLaunchKernelGGL(knn_fill_kernel, dim3((unsigned)std::min<int64_t>(cdiv(N, 256), 2048), c), dim3(256),
-                     0, s, x, (const int64_t*)nullptr, N, (int64_t)0, w.Cpad, w.cnt, w.crank,
-                     (float4*)nullptr, w.qorder);
+  hipLaunchKernelGGL(knn_rows_fill_kernel, dim3((unsigned)std::min<int64_t>(cdiv(N, 256), 2048), c),
+                     dim3(256), 0, s, x, N, w.Cpad, w.cnt, w.crank, w.xs);
   if (done_flag) hipLaunchKernelGGL(knn_flag_kernel, dim3(1), dim3(64), 0, s, done_flag, done_value);
   PCST_LAUNCH_CHECK("knn3_rows_build");
   return PCST_OK;
@@ -1658,10 +1683,10 @@ extern "C" int pcst_knn3_rows_query(const float* coarse, const float* x, int64_t
   if (C == 0) return PCST_OK;
   PCST_CHECK_ARG(coarse && x && out && workspace, "knn3_rows_query: null pointer");
   KnnRowsWS w = carve_knn_rows(workspace, C, copies, N, M);
-  const KArgs ka = {C, w.known, w.rcnt, w.over, w.ovn, w.err, wait_err,
+  const KArgs ka = {C, w.known, w.xs, w.rcnt, w.over, w.ovn, w.err, wait_err,
                     max_polls > 0 ? max_polls : (int64_t)kSignalPolls, refs_err, w.qctr, w.brefs,
                     w.bcnt};
-  launch_knn_query<true>(w.maxch, w.gp, w.cnt, w.refs, w.qorder, w.chunks, w.nchunk, w.olist,
+  launch_knn_query<true>(w.maxch, w.gp, w.cnt, w.refs, nullptr, w.chunks, w.nchunk, w.olist,
                          w.obound, w.ocount, w.known, w.Cpad, ka, coarse, x, w.B, N, M, out,
                          built_flag, built_value, grid_cap, as_stream(stream));
   PCST_LAUNCH_CHECK("knn3_rows_query");

@@ -586,10 +586,25 @@ __device__ __forceinline__ int4 voxel_box(const StatRec& M, float4 v4, int64_t H
   if (!(q[0] < 4096.0f && q[1] < 4096.0f && q[2] < 4096.0f)) return make_int4(0, 0, 0, 0);
   const int dx = (int)q[0] + 1, dy = (int)q[1] + 1, dz = (int)q[2] + 1;
   int dense = 0;
+#ifdef PCST_VOX_NO_DENSE  // experiment builds only (csrc/Makefile XDEF): the hash table always
+  pack = 0;
+#endif
   if (pack && (int64_t)dx * dy * dz <= H)
     for (int i = 0; i < kDenseBoxCount; ++i)
       if (dx <= kDenseBoxes[i].x && dy <= kDenseBoxes[i].y && dz <= kDenseBoxes[i].z) dense = 1;
   return make_int4(dx, dy, dz, dense);
+}
+
+// The dense grid's accumulators are spread over replicas (point n adds to replica n % R, the
+// reps launch sums them): the densest voxels of a noise cloud hold ~300 points, whose 64-bit adds
+// to ONE address serialise at the memory-side atomic unit (insert 15.9 us with one replica on a
+// squashed noise cloud, tools/voxel_probe.py).  R = the largest power of two <= 8 with R cells
+// in the table.
+constexpr int kDenseReplicas = 8;
+__device__ __forceinline__ int dense_replicas(int cells, int64_t H) {
+  int r = kDenseReplicas;
+  while (r > 1 && (int64_t)r * cells > H) r >>= 1;
+  return r;
 }
 
 __device__ __forceinline__ uint32_t voxel_hash(int32_t vx, int32_t vy, int32_t vz) {
@@ -647,13 +662,16 @@ __global__ __launch_bounds__(256) void voxf_insert_kernel(const float* __restric
   const float4 v4 = vps;
   const int4 box = vbox;
   const int n0 = blockIdx.x * kVoxChunk, n1 = min(n0 + kVoxChunk, N);
-  if (box.w) {  // the dense grid: cell = vx + dx (vy + dy vz)
+  if (box.w) {  // the dense grid: cell = vx + dx (vy + dy vz), replica n % kDenseReplicas
+    const int cells = box.x * box.y * box.z;
+    const int reps = dense_replicas(cells, H);
     unsigned long long* D = tsum + b * H;
     for (int n = n0 + threadIdx.x; n < n1; n += 256) {
       const int32_t vx = (int32_t)floorf(__fdiv_rn(fsub(P[n * 3 + 0], v4.x), v4.w));
       const int32_t vy = (int32_t)floorf(__fdiv_rn(fsub(P[n * 3 + 1], v4.y), v4.w));
       const int32_t vz = (int32_t)floorf(__fdiv_rn(fsub(P[n * 3 + 2], v4.z), v4.w));
-      atomicAdd(&D[vx + box.x * (vy + box.y * vz)], ((unsigned long long)n << 20) | 1ull);
+      atomicAdd(&D[(n & (reps - 1)) * cells + vx + box.x * (vy + box.y * vz)],
+                ((unsigned long long)n << 20) | 1ull);
     }
   } else {
     for (int i = threadIdx.x; i < kVoxLds; i += 256) { lkey[i] = 0ull; lsum[i] = 0ull; lcnt[i] = 0u; }
@@ -737,9 +755,9 @@ __device__ __forceinline__ void voxf_rep_out(int64_t r, uint32_t h, int k, int b
   }
 }
 
-// Dense grid (vdim[b].w): one thread per cell of the voxel box, an occupied cell -> its
-// representative, its voxel hash (recomputed from the cell's coordinates) and a list position
-// taken by one atomic per wave (cnt4[b][0] counts the listed voxels: U).
+// Dense grid (vdim[b].w): one thread per cell of the voxel box (its replicas summed), an
+// occupied cell -> its representative, its voxel hash (recomputed from the cell's coordinates)
+// and a list position taken by one atomic per wave (cnt4[b][0] counts the listed voxels: U).
 __global__ __launch_bounds__(256) void voxf_reps_kernel(
     const unsigned long long* __restrict__ tkey, const unsigned long long* __restrict__ tsum,
     const uint32_t* __restrict__ tcnt, int64_t H, int N, int32_t* __restrict__ cnt4,
@@ -754,9 +772,12 @@ __global__ __launch_bounds__(256) void voxf_reps_kernel(
     const int cells = box.x * box.y * box.z;
     const int lane = threadIdx.x & 63;
     // whole waves per round (the list position is taken per wave)
+    const int nrep = dense_replicas(cells, H);
     for (int c0 = (blockIdx.x * 256 + threadIdx.x) & ~63; c0 < cells; c0 += gridDim.x * 256) {
       const int c = c0 + lane;
-      const unsigned long long v = c < cells ? tsum[b * H + c] : 0ull;
+      unsigned long long v = 0ull;
+      if (c < cells)
+        for (int k = 0; k < nrep; ++k) v += tsum[b * H + (int64_t)k * cells + c];
       const uint64_t occ = __ballot(v != 0ull);
       if (!occ) continue;
       int base = 0;
