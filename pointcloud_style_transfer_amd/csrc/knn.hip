@@ -1143,7 +1143,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
     if (lane == 0) nk = atomicAdd(ctr, 1);
     return Wr + (int)sh + (int)Sh * __shfl(nk, 0);
   };
+#ifdef PCST_KNN_CHUNK_TRACE  // experiment builds only: per chunk (start, end, wave, pass-1 open
+  // lanes | pass-2 ran << 8 | outliers << 16) in 10 ns ticks, in the row's obound array past 4096
+  uint4* trace = reinterpret_cast<uint4*>(obound + b * N + 4096);
+  const uint32_t gw = blockIdx.x * 4 + wv;
+  uint32_t tr0 = 0, tr_open1 = 0, tr_p2 = 0;
+#endif
   for (int item = (int)m * 4 + wv; item < nch;) {
+#ifdef PCST_KNN_CHUNK_TRACE
+    tr0 = (uint32_t)__builtin_amdgcn_s_memrealtime();
+    tr_open1 = tr_p2 = 0;
+#endif
     const uint2 ch = chunks[cl * maxch + item];
     if (ch.x > ch.y || ch.y > (uint32_t)N || ch.y - ch.x > 64u) {  // wave-uniform
       if (lane == 0) atomicOr(ka.err, 4);
@@ -1189,6 +1199,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
     if constexpr (ROWS) offer_overflow(pb, none, me);
     bool open = valid && !settled(me, pb, g, kk);
     bool ok = true;
+#ifdef PCST_KNN_CHUNK_TRACE
+    tr_open1 = (uint32_t)__popcll(__ballot(open));
+#endif
     // 2. the balls of the open lanes that hold kk refs
     if (__any(open)) {
       const double dk = me.t.last(kk);
@@ -1213,6 +1226,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
                         min(pb.y0, wave_min(by0)), max(pb.y1, wave_max(by1)),
                         min(pb.z0, wave_min(bz0)), max(pb.z1, wave_max(bz1))};
         if (bb.volume() <= kBallUnion) {
+#ifdef PCST_KNN_CHUNK_TRACE
+          tr_p2 = 1;
+#endif
           uint32_t budget = kBallBudget;
           ok = scan_box(bb, pb, g, rng, R, W, me, kk, budget);
           if constexpr (ROWS) {
@@ -1240,6 +1256,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
       }
     }
     if (valid && !open) idw_write(me.t, kk, V, out + (b * N + n) * 3);
+#ifdef PCST_KNN_CHUNK_TRACE
+    if (lane == 0 && item < 16384)
+      trace[item] = make_uint4(tr0, (uint32_t)__builtin_amdgcn_s_memrealtime(), gw,
+                               tr_open1 | (tr_p2 << 8) | ((uint32_t)__popcll(rest) << 16));
+#endif
     item = next;
   }
   // Rows layout: the brick copy of the placed refs for the outlier launch, by waves out of chunks.

@@ -348,7 +348,7 @@ static int vox_sel_shift(int64_t N) { return N <= (4ll << 20) ? 22 : 20; }
 constexpr int kTieCap = 8192;
 constexpr int kVoxChunk = 1024;           // points aggregated per workgroup in LDS (512 / 2048: DESIGN §6a)
 constexpr int kVoxLds = 2 * kVoxChunk;    // LDS table slots (load factor <= 1/2)
-constexpr int kVoxRepsBlocks = 64;        // workgroups per cloud over the voxel list
+constexpr int kVoxRepsBlocks = 128;       // workgroups per cloud over the voxel list / dense cells
 
 // Copies.  guided_sample_loop downsamples the CFG batch cat([x] * 2) (diffusion_model.py:244-247):
 // identical clouds.  With copies = k the input is the B distinct clouds and the output has the
