@@ -515,7 +515,8 @@ def main():
             rows, start = (dmod.knn_rows_begin(x, cfg.global_points, state, rows_ws,
                                                by_downsample=prepped)
                            if rows_ws is not None else (None, None))
-            xc, xi = hp.downsample_copies(x, 2, vws, prepped, next_seed, pool, start)
+            xc, xi = hp.downsample_copies(x, 2, vws, prepped, next_seed, pool, start, rows=rows,
+                                          rows_wait=state.built_sig if rows is not None else None)
 
             def mlp(xc_, wait=None, start=None):
                 if not timed:

@@ -275,6 +275,21 @@ int pcst_voxel_downsample_copies_prepped(const float* pts, int64_t B, int64_t N,
                                          int64_t target, void* workspace, uint64_t seed, int pool,
                                          int64_t* out_idx, float* out_pts, uint32_t* start_flag,
                                          uint32_t start_value, void* stream);
+/* The device-drawn downsample of the CFG batch (pcst_voxel_downsample_copies, or _prepped with
+ * prepped = 1: pool and start_flag as there) that also places its coarse points as the refs of the
+ * kNN rows layout (phase B of pcst_knn3_rows_refs, inside the emit launch): knn_workspace is the
+ * rows workspace of B clouds x copies rows with M = target that pcst_knn3_rows_build is binning
+ * (on another stream); every emit work-group first writes its rows of out_idx / out_pts, then
+ * waits for wait_flag >= wait_value (the build's refs flag; NULL: the stream is ordered after the
+ * build already), at most max_polls polls (<= 0: ~10 s), and places its kept points -- the same
+ * placement as pcst_knn3_rows_refs(out_idx).  A work-group whose wait gives up places nothing and
+ * sets *wait_err: pass it to pcst_knn3_rows_query as refs_err. */
+int pcst_voxel_downsample_rows(const float* pts, int64_t B, int64_t N, int64_t copies,
+                               int64_t target, void* workspace, uint64_t seed, int prepped,
+                               int pool, int64_t* out_idx, float* out_pts, uint32_t* start_flag,
+                               uint32_t start_value, void* knn_workspace, const uint32_t* wait_flag,
+                               uint32_t wait_value, int32_t* wait_err, int64_t max_polls,
+                               void* stream);
 /* Copies the replay-validation error word (0 = ok) to err_out (device int32). */
 int pcst_voxel_error(void* workspace, int64_t B, int64_t N, int32_t* err_out, void* stream);
 

@@ -46,6 +46,8 @@ SIGNATURES = {
     "pcst_voxel_downsample_copies": [_P, _I, _I, _I, _I, _P, ctypes.c_uint64, _P, _P, _P],
     "pcst_voxel_downsample_copies_prepped": [_P, _I, _I, _I, _I, _P, ctypes.c_uint64, ctypes.c_int,
                                              _P, _P, _P, ctypes.c_uint32, _P],
+    "pcst_voxel_downsample_rows": [_P, _I, _I, _I, _I, _P, ctypes.c_uint64, ctypes.c_int, ctypes.c_int,
+                                   _P, _P, _P, ctypes.c_uint32, _P, _P, ctypes.c_uint32, _P, _I, _P],
     "pcst_cfg_ddim_voxel_prep": [_P, _P, _P, _I, _I, _F, _F, _F, _F, _F, _P, _P, _P, _I,
                                  ctypes.c_uint64, ctypes.c_int, _P],
     "pcst_knn_workspace_size": [_I, _I, _I, _SZ],
@@ -287,7 +289,7 @@ def voxel_copies_workspace(B, N, copies, device):
 
 
 def voxel_downsample(points, target, seed=0, perm_provider=None, copies=1, ws=None,
-                     prepped=False, pool=False, start=None):
+                     prepped=False, pool=False, start=None, rows=None, rows_wait=None):
     """HierarchicalProcessor._voxel_grid_downsample_torch for N > target, all clouds at once.
 
     perm_provider=None: the random subset is drawn on the device from `seed`.
@@ -300,6 +302,10 @@ def voxel_downsample(points, target, seed=0, perm_provider=None, copies=1, ws=No
     path skips its statistics / zeroing launch); pool=True: that prep also made the pool-key
     histogram for this `seed` (its pool_seed), so the insert skips it.  start (prepped only):
     (flag pointer, value) of a DeviceSignal.next_value() the launch publishes as it begins.
+    rows (a KnnRows handle of knn3_rows_build on these clouds, copies and M = target; device-drawn
+    path): the emit launch also places the kept points as the handle's refs (phase B,
+    pcst_voxel_downsample_rows), so no knn3_rows_refs follows; rows_wait (the build's refs
+    DeviceSignal): the placement waits for its last value in-kernel.
     Returns (points [k*B,T,3], idx [k*B,T] int64)."""
     require_device(points)
     points = _f32(points)
@@ -320,6 +326,21 @@ def voxel_downsample(points, target, seed=0, perm_provider=None, copies=1, ws=No
                 raise RuntimeError("voxel_downsample: workspace too small or on another device")
         out_idx = torch.empty(copies * B, target, dtype=torch.int64, device=dev)
         out_pts = torch.empty(copies * B, target, 3, dtype=torch.float32, device=dev)
+        if rows is not None:
+            if rows.dims != (B, copies, N, target):
+                raise RuntimeError(f"voxel_downsample: rows handle {rows.dims} != {(B, copies, N, target)}")
+            sflag, sval = start if start is not None else (None, ctypes.c_uint32(0))
+            if rows_wait is not None:
+                wflag, wval, _, werr, polls = rows_wait.wait_args()
+            else:
+                wflag, wval, werr, polls = None, ctypes.c_uint32(0), None, ctypes.c_int64(0)
+            rows.idx = out_idx
+            rows.refs_err = werr
+            rows.placed = True
+            _call("pcst_voxel_downsample_rows", _ptr(points), B, N, copies, target, _ptr(ws),
+                  seed & (2**64 - 1), 1 if prepped else 0, 1 if pool else 0, _ptr(out_idx),
+                  _ptr(out_pts), sflag, sval, _ptr(rows.ws), wflag, wval, werr, polls, _stream())
+            return out_pts, out_idx
         if prepped:
             sflag, sval = start if start is not None else (None, ctypes.c_uint32(0))
             _call("pcst_voxel_downsample_copies_prepped", _ptr(points), B, N, copies, target,
@@ -585,6 +606,7 @@ class KnnRows:
     def __init__(self, x, copies, M, ws):
         self.x, self.copies, self.M, self.ws = x, int(copies), int(M), ws
         self.refs_err = None
+        self.placed = False  # the refs were placed by the downsample (voxel_downsample(rows=))
 
     @property
     def dims(self):

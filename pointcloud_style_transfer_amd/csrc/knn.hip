@@ -48,6 +48,7 @@
 // outlier.
 #include "common.h"
 #include "cloud.h"
+#include "knn_rows.h"
 
 namespace pcst {
 
@@ -56,14 +57,10 @@ constexpr int kCandCap = 512;            // LDS candidates per wave
 constexpr int kBallCells = 512;          // largest cell box one lane's ball may ask for
 constexpr int kBallUnion = 1024;         // largest union box of a ball pass
 constexpr uint32_t kBallBudget = 2048;   // refs the ball pass may stage
-constexpr int kKnnTile = 4096;           // scan tile (256 threads x 16)
-constexpr int kKnnMaxTiles = 1024;       // per-block LDS tile histogram in the count kernel
 constexpr int kPreKnownBlocks = 64;      // known-row scatter blocks per cloud in the pre kernel
 constexpr int kCountPerBlock = 1024;     // elements per count-kernel block (4 per thread)
 constexpr int kOvlLds = 256;             // overflow refs staged in LDS per query work-group
 constexpr int kOutlierBrickBlocks = 256; // outlier workgroups per cloud (brick search, 4 queries)
-constexpr int kQueryShards = 8;          // work counters per CFG row (one per XCD)
-constexpr int kCtrStride = 64;           // int32 words between counters: each on its own 256-B line
 constexpr int kBrickBatch = 4;           // bricks per brick-copy work item of the rows query
 constexpr int kQueryBlocksPerCU = 4;     // resident query work-groups per CU (waves_per_eu 4, 38 KiB LDS)
 
@@ -88,10 +85,6 @@ struct KnnWS {
   int64_t Cmax, T, Cpad, maxch;
   size_t bytes;
 };
-
-static int64_t knn_cells(int64_t M) {
-  return std::min<int64_t>(std::max<int64_t>(4096, 16 * M), (int64_t)kKnnMaxTiles * kKnnTile - 1);
-}
 
 static KnnWS carve_knn(void* base, int64_t B, int64_t N, int64_t M) {
   Carver c(base);
@@ -475,99 +468,13 @@ __global__ __launch_bounds__(256) void knn_rows_fill_kernel(const float* __restr
 // launch: three launches on the step's critical path instead of one.)  The query skips known rows
 // (copying their coarse value instead).  The grid is the compact layout's (the same statistics
 // and ref count), so both layouts give the same bits.
-struct KnnRowsWS {
-  StatRec* stats;    // [C][kStatBlocks]
-  float* gp;         // [C][8]
-  float4* xs;        // [C][N] rows in cell order: (x, y, z, point index n)
-  int2* crank;       // [C][N] (cell, rank in cell)
-  uint2* chunks;     // [C][maxch] row ranges [q0, q1) of <= 64 rows inside one brick
-  float4* refs;      // [B][N] refs (x, y, z, j) at the front of their cell's row range
-  float4* brefs;     // [B][N] the placed refs at the front of their brick's row range (outlier
-                     // pass; built by the query's waves)
-  float4* over;      // [B][M] overflow refs (an index named again)
-  int32_t* olist;    // [B][N] outlier query rows
-  float* obound;     // [B][N]
-  // zeroed every build (contiguous):
-  int32_t* err;
-  int32_t* qctr;     // [B][2][8][kCtrStride] the query's work counters (chunks, brick batches)
-  int32_t* nchunk;   // [C]
-  int32_t* ocount;   // [B]
-  int32_t* ovn;      // [B] overflow refs
-  uint32_t* known;   // [B][N] j+1 of the last ref naming the row at cell-order position p, 0 = a query
-  uint32_t* rcnt;    // [B][Cpad] refs ranked per cell
-  uint32_t* bcnt;    // [B][Cpad / 64] the brick copy's ref counts (written if nonzero)
-  uint64_t* tsum;    // [C][T]
-  uint64_t* cnt;     // [C][Cpad] packed counts (0 | rows << 32) -> starts
-  int64_t B, C, Cmax, T, Cpad, maxch;
-  size_t bytes;
-};
-
-static KnnRowsWS carve_knn_rows(void* base, int64_t C, int64_t copies, int64_t N, int64_t M) {
-  Carver c(base);
-  KnnRowsWS w;
-  w.C = C;
-  w.B = C * copies;
-  w.Cmax = knn_cells(M);
-  w.T = cdiv(w.Cmax + 1, kKnnTile);
-  w.Cpad = w.T * kKnnTile;
-  w.maxch = cdiv(N, 64) + 8 * (w.Cmax / 64) + 1;
-  w.stats = c.take<StatRec>(C * kStatBlocks);
-  w.gp = c.take<float>(C * 8);
-  w.xs = c.take<float4>(C * N);
-  w.crank = c.take<int2>(C * N);
-  w.chunks = c.take<uint2>(C * w.maxch);
-  w.refs = c.take<float4>(w.B * N);
-  w.brefs = c.take<float4>(w.B * N);
-  w.over = c.take<float4>(w.B * M);
-  w.olist = c.take<int32_t>(w.B * N);
-  w.obound = c.take<float>(w.B * N);
-  w.err = c.take<int32_t>(4);
-  w.qctr = c.take<int32_t>(w.B * 2 * kQueryShards * kCtrStride);
-  w.nchunk = c.take<int32_t>(C);
-  w.ocount = c.take<int32_t>(w.B);
-  w.ovn = c.take<int32_t>(w.B);
-  w.known = c.take<uint32_t>(w.B * N);
-  w.rcnt = c.take<uint32_t>(w.B * w.Cpad);
-  w.bcnt = c.take<uint32_t>(w.B * (w.Cpad / 64));
-  w.tsum = c.take<uint64_t>(C * w.T);
-  w.cnt = c.take<uint64_t>(C * w.Cpad);
-  w.bytes = c.bytes();
-  return w;
-}
-
 // A flag for work on another stream: every launch ahead of this one on its stream has completed.
 __global__ void knn_flag_kernel(uint32_t* flag, uint32_t value) {
   if (threadIdx.x == 0) __hip_atomic_store(flag, value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// The consumer side of a flag hand-off inside a kernel (MI355X_MICROARCH.md, inter-workgroup
-// visibility): thread 0 polls (relaxed, agent scope) until the flag holds `value`, at most
-// max_polls times, then one agent-scope acquire; the block barrier lets every wave load after it.
-// A wait that gives up sets *werr and returns false for the whole block.
-__device__ bool block_wait_flag(const uint32_t* flag, uint32_t value, int32_t* werr, int64_t max_polls) {
-  __shared__ int s_ok;
-  if (threadIdx.x == 0) {
-    bool ok = false;
-    for (int64_t i = 0; i < max_polls; ++i) {
-      if (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= value) {
-        ok = true;
-        break;
-      }
-      __builtin_amdgcn_s_sleep(4);
-    }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (!ok && werr) __hip_atomic_store(werr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    s_ok = ok;
-  }
-  __syncthreads();
-  return s_ok != 0;
-}
-
-// Phase B: ref j of CFG row b (cloud b % C): its known mark at its point's cell-order position
-// (the last j wins), its rank in its point's cell (both atomics issued together) and its slot
-// start(cell) + rank at the front of the cell's row range; a rank beyond the cell's rows sends the
-// ref to the overflow list instead.
+// Phase B as its own launch (rows_place per ref; pcst_knn3_rows_refs).  The sampling step runs it
+// inside the voxel emit instead (voxel.hip, the same rows_place).
 // wflag (optional): the side stream's phase-A flag; every work-group waits until it holds wvalue
 // (the consumer side of the guide's hand-off: one relaxed poll loop, one agent-scope acquire, a
 // barrier), so no wait launch sits in front of this one; a work-group whose wait gives up sets
@@ -576,33 +483,21 @@ __device__ bool block_wait_flag(const uint32_t* flag, uint32_t value, int32_t* w
 // outlier launches, handed werr as their refs_err, leave the workspace alone and write eps = 0.
 // The coarse indices are loaded before the wait (they do not depend on phase A).
 __global__ __launch_bounds__(256) void knn_rows_place_kernel(
-    const float* __restrict__ x, const int64_t* __restrict__ idx, int64_t C, int64_t N, int64_t M,
-    int64_t Cpad, const uint64_t* __restrict__ start, const int2* __restrict__ crank,
-    uint32_t* __restrict__ known, uint32_t* __restrict__ rcnt, float4* __restrict__ refs,
-    float4* __restrict__ over, int32_t* __restrict__ ovn, int32_t* __restrict__ err,
-    const uint32_t* __restrict__ wflag, uint32_t wvalue, int32_t* __restrict__ werr,
-    int64_t max_polls) {
+    const float* __restrict__ x, const int64_t* __restrict__ idx, const RowsPlace rp,
+    int32_t* __restrict__ err, const uint32_t* __restrict__ wflag, uint32_t wvalue,
+    int32_t* __restrict__ werr, int64_t max_polls) {
   const int b = blockIdx.y;
-  const int64_t cl = b % C;
+  const int64_t N = rp.N, M = rp.M, cl = b % rp.C;
   const int64_t j0 = (int64_t)blockIdx.x * 256 + threadIdx.x;
   int64_t n0 = j0 < M ? idx[b * M + j0] : 0;
   if (wflag && !block_wait_flag(wflag, wvalue, werr, max_polls)) return;
-  const uint64_t* S = start + cl * Cpad;
   for (int64_t j = j0; j < M; j += (int64_t)gridDim.x * 256) {
     const int64_t n = j == j0 ? n0 : idx[b * M + j];
     if (n < 0 || n >= N) {
       atomicOr(err, 1);
       continue;
     }
-    const int2 cr = crank[cl * N + n];
-    const int cell = cr.x;
-    const uint32_t rank = atomicAdd(&rcnt[b * Cpad + cell], 1u);
-    const uint32_t a = (uint32_t)(S[cell] >> 32), rows = (uint32_t)(S[cell + 1] >> 32) - a;
-    atomicMax(&known[b * N + a + (uint32_t)cr.y], (uint32_t)(j + 1));  // n's cell-order position
-    const float* p = x + (cl * N + n) * 3;
-    const float4 r = make_float4(p[0], p[1], p[2], __int_as_float((int)j));
-    if (rank < rows) refs[b * N + a + rank] = r;
-    else over[b * M + atomicAdd(&ovn[b], 1)] = r;
+    rows_place(rp, b, n, j, x + (cl * N + n) * 3);
   }
 }
 
@@ -1688,9 +1583,8 @@ extern "C" int pcst_knn3_rows_refs(const float* x, const int64_t* idx, int64_t C
   KnnRowsWS w = carve_knn_rows(workspace, C, copies, N, M);
   hipStream_t s = as_stream(stream);
   const dim3 gj((unsigned)std::min<int64_t>(cdiv(M, 256), 1024), (unsigned)w.B);
-  hipLaunchKernelGGL(knn_rows_place_kernel, gj, dim3(256), 0, s, x, idx, C, N, M, w.Cpad, w.cnt, w.crank,
-                     w.known, w.rcnt, w.refs, w.over, w.ovn, w.err, wait_flag, wait_value, wait_err,
-                     max_polls > 0 ? max_polls : (int64_t)kSignalPolls);
+  hipLaunchKernelGGL(knn_rows_place_kernel, gj, dim3(256), 0, s, x, idx, rows_place_args(w, N, M), w.err,
+                     wait_flag, wait_value, wait_err, max_polls > 0 ? max_polls : (int64_t)kSignalPolls);
   PCST_LAUNCH_CHECK("knn3_rows_refs");
   return PCST_OK;
 }

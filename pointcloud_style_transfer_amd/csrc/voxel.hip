@@ -12,6 +12,7 @@
 //   with perm either replayed (parity) or drawn on the device: Philox-style 32-bit keys
 //   per candidate + the same radix sort = torch.randperm's random-key-sort construction.
 #include "common.h"
+#include "knn_rows.h"
 #include "sort.h"
 #include "cloud.h"
 
@@ -383,7 +384,7 @@ struct VoxelFastWS {
   size_t bytes;
 };
 
-constexpr int kEmitTile = 4096;   // 256 threads x 16 indices
+constexpr int kEmitTile = 1024;   // 256 threads x 4 indices
 constexpr int kMarkTiles = 1024;  // tiles counted in LDS by the marking kernels
 
 static int64_t vox_table_size(int64_t N) {
@@ -563,18 +564,25 @@ __global__ __launch_bounds__(256) void voxf_cfg_prep_kernel(
 // ONE group.  Inside a box of voxel coordinates in which no two voxels share a hash, a group is
 // exactly a voxel, and the per-group (index sum, count) can be accumulated by plain atomic adds
 // into a dense array indexed by the voxel's position in the box -- no hash table, no probing, no
-// returning atomics.  kDenseBoxes lists boxes [0,X) x [0,Y) x [0,Z) checked collision-free
+// returning atomics.  PCST_DENSE_BOXES lists boxes [0,X) x [0,Y) x [0,Z) checked collision-free
 // (tools/voxel_cert.py; tests/test_host.py re-checks every entry with numpy); a cloud whose voxel
 // box (dx, dy, dz) = floor((max - min) / vs) + 1 lies inside one of them, with dx dy dz <= the
 // table size H, takes the dense path, any other the hash table (same groups, same bits).  The
 // bench's clouds: noise 26 x 28 x 26, lidar-like 48 x 52 x 8.
-struct DenseBox { int x, y, z; };
-__constant__ DenseBox kDenseBoxes[] = {
-    {56, 56, 56},    {1, 306, 306},  {265, 1, 265},  {313, 313, 1},  {2, 306, 306},
-    {265, 2, 265},   {305, 305, 2},  {4, 234, 234},  {175, 4, 175},  {196, 196, 4},
-    {8, 116, 116},   {175, 8, 175},  {190, 190, 8},  {16, 116, 116}, {128, 16, 128},
-    {117, 117, 16},  {32, 101, 101}, {56, 32, 56},   {90, 90, 32}};
-constexpr int kDenseBoxCount = (int)(sizeof(kDenseBoxes) / sizeof(DenseBox));
+// (A table in the kernel's code: a __constant__ array would be a writable host-side symbol.)
+#define PCST_DENSE_BOXES                                                                       \
+  {56, 56, 56}, {1, 306, 306}, {265, 1, 265}, {313, 313, 1}, {2, 306, 306}, {265, 2, 265},      \
+      {305, 305, 2}, {4, 234, 234}, {175, 4, 175}, {196, 196, 4}, {8, 116, 116}, {175, 8, 175}, \
+      {190, 190, 8}, {16, 116, 116}, {128, 16, 128}, {117, 117, 16}, {32, 101, 101},            \
+      {56, 32, 56}, {90, 90, 32}
+__device__ __forceinline__ bool dense_box_ok(int dx, int dy, int dz) {
+  constexpr int kBoxes[][3] = {PCST_DENSE_BOXES};
+  bool ok = false;
+#pragma unroll
+  for (int i = 0; i < (int)(sizeof(kBoxes) / sizeof(kBoxes[0])); ++i)
+    ok = ok || (dx <= kBoxes[i][0] && dy <= kBoxes[i][1] && dz <= kBoxes[i][2]);
+  return ok;
+}
 
 // The cloud's voxel box dims (every point's coordinate lies in [0, d): rounding is monotone) and
 // whether the dense grid takes it.
@@ -589,9 +597,7 @@ __device__ __forceinline__ int4 voxel_box(const StatRec& M, float4 v4, int64_t H
 #ifdef PCST_VOX_NO_DENSE  // experiment builds only (csrc/Makefile XDEF): the hash table always
   pack = 0;
 #endif
-  if (pack && (int64_t)dx * dy * dz <= H)
-    for (int i = 0; i < kDenseBoxCount; ++i)
-      if (dx <= kDenseBoxes[i].x && dy <= kDenseBoxes[i].y && dz <= kDenseBoxes[i].z) dense = 1;
+  if (pack && (int64_t)dx * dy * dz <= H && dense_box_ok(dx, dy, dz)) dense = 1;
   return make_int4(dx, dy, dz, dense);
 }
 
@@ -933,7 +939,11 @@ __global__ __launch_bounds__(256) void voxf_emit_kernel(const float* __restrict_
                                                         const int64_t* __restrict__ reps,
                                                         int64_t* __restrict__ out_idx,
                                                         float* __restrict__ out_pts,
-                                                        uint32_t* __restrict__ phist) {
+                                                        uint32_t* __restrict__ phist,
+                                                        const RowsPlace rp,
+                                                        const uint32_t* __restrict__ wflag,
+                                                        uint32_t wvalue, int32_t* __restrict__ werr,
+                                                        int64_t max_polls) {
   constexpr int kPer = kEmitTile / 256;
   const int row = blockIdx.y, cl = row % B;
   const int64_t tile = blockIdx.x;
@@ -994,14 +1004,28 @@ __global__ __launch_bounds__(256) void voxf_emit_kernel(const float* __restrict_
   uint32_t tot0, tot;
   block_excl_scan_256(before, sh, tot0);  // tot0 = everything kept in the earlier tiles
   int64_t pos = (int64_t)tot0 + block_excl_scan_256(s, sh, tot);
+  int64_t p0[kPer];
 #pragma unroll
   for (int k = 0; k < kPer; ++k) {
+    p0[k] = pos;
     for (uint32_t r = 0; r < c[k]; ++r, ++pos) {
       if (pos >= T) { atomicOr(&cnt4[row * 4 + 3], 2); break; }
       out_idx[row * T + pos] = n0 + k;
       float* d = out_pts + (row * T + pos) * 3;
       d[0] = q[3 * k]; d[1] = q[3 * k + 1]; d[2] = q[3 * k + 2];
     }
+  }
+  // Phase B of the step's kNN rows layout (rp.refs given; knn_rows.h): every kept copy j of point
+  // n is placed as the query's ref j of this row, once phase A (the side stream's binning of the
+  // same points) has published its flag -- the wait comes after this launch's own output, and a
+  // work-group whose wait gives up places nothing and sets *werr (the query then reads nothing).
+  if (rp.refs && (!wflag || block_wait_flag(wflag, wvalue, werr, max_polls))) {
+#pragma unroll
+    for (int k = 0; k < kPer; ++k)
+      for (uint32_t r = 0; r < c[k] && p0[k] + r < T; ++r) {
+        const float pt[3] = {q[3 * k], q[3 * k + 1], q[3 * k + 2]};
+        rows_place(rp, row, n0 + k, p0[k] + r, pt);
+      }
   }
 }
 
@@ -1012,10 +1036,21 @@ static size_t vox_zero_bytes(const VoxelFastWS& w, int64_t rows) {
   return (size_t)((char*)(w.ktile + rows * w.tiles) - (char*)w.cnt4);
 }
 
+// place (optional): phase B of the kNN rows layout fused into the emit (knn_rows.h RowsPlace of
+// the rows workspace, with its phase-A flag wait).
+struct EmitPlace {
+  RowsPlace rp{};
+  const uint32_t* wflag = nullptr;
+  uint32_t wvalue = 0;
+  int32_t* werr = nullptr;
+  int64_t max_polls = 0;
+};
+
 static int voxel_fast(const float* pts, int64_t B, int64_t N, int64_t copies, int64_t T,
                       void* workspace, uint64_t seed, const uint64_t* seed_p, int64_t* out_idx,
                       float* out_pts, hipStream_t s, bool prepped = false, bool pool = false,
-                      uint32_t* sflag = nullptr, uint32_t svalue = 0) {
+                      uint32_t* sflag = nullptr, uint32_t svalue = 0,
+                      const EmitPlace& place = EmitPlace()) {
   VoxelFastWS w = carve_voxel_fast(workspace, B, N, copies);
   const int b = (int)B, n = (int)N, rows = (int)(B * copies);
   if (!prepped)  // (a prepped call: pcst_cfg_ddim_voxel_prep made the partials and zeroed)
@@ -1039,7 +1074,8 @@ static int voxel_fast(const float* pts, int64_t B, int64_t N, int64_t copies, in
                      w.ktile, w.tiles, sshift);
   hipLaunchKernelGGL(voxf_emit_kernel, dim3((unsigned)w.tiles, rows), dim3(256), 0, s, pts, n, T,
                      b, w.kcnt, w.ktile, w.tiles, w.cnt4, w.sel, w.ties, w.reps, out_idx, out_pts,
-                     w.phist);
+                     w.phist, place.rp, place.wflag, place.wvalue, place.werr,
+                     place.max_polls > 0 ? place.max_polls : (int64_t)kSignalPolls);
   PCST_LAUNCH_CHECK("voxel_downsample");
   return PCST_OK;
 }
@@ -1169,6 +1205,30 @@ extern "C" int pcst_voxel_downsample_copies_prepped(const float* pts, int64_t B,
   PCST_CHECK_ARG(pts && workspace && out_idx && out_pts, "voxel_downsample_copies_prepped: null pointer");
   return voxel_fast(pts, B, N, copies, target, workspace, seed, nullptr, out_idx, out_pts,
                     as_stream(stream), true, pool != 0, start_flag, start_value);
+}
+
+extern "C" int pcst_voxel_downsample_rows(const float* pts, int64_t B, int64_t N, int64_t copies,
+                                          int64_t target, void* workspace, uint64_t seed,
+                                          int prepped, int pool, int64_t* out_idx, float* out_pts,
+                                          uint32_t* start_flag, uint32_t start_value,
+                                          void* knn_workspace, const uint32_t* wait_flag,
+                                          uint32_t wait_value, int32_t* wait_err, int64_t max_polls,
+                                          void* stream) {
+  PCST_CHECK_ARG(B > 0 && copies >= 1 && B * copies < (1 << 15) && N > target && target > 0 &&
+                     N < (1ll << 30) && target < (1ll << 27),
+                 "voxel_downsample_rows: bad shape");
+  PCST_CHECK_ARG(pts && workspace && out_idx && out_pts && knn_workspace,
+                 "voxel_downsample_rows: null pointer");
+  PCST_CHECK_ARG(prepped || (!pool && !start_flag), "voxel_downsample_rows: pool / start need prepped");
+  const KnnRowsWS kw = carve_knn_rows(knn_workspace, B, copies, N, target);
+  EmitPlace place;
+  place.rp = rows_place_args(kw, N, target);
+  place.wflag = wait_flag;
+  place.wvalue = wait_value;
+  place.werr = wait_err;
+  place.max_polls = max_polls;
+  return voxel_fast(pts, B, N, copies, target, workspace, seed, nullptr, out_idx, out_pts,
+                    as_stream(stream), prepped != 0, pool != 0, start_flag, start_value, place);
 }
 
 extern "C" int pcst_cfg_ddim_voxel_prep(const float* x, const float* eps, const float* source,

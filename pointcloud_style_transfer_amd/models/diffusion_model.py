@@ -226,7 +226,8 @@ class HierarchicalProcessor:
     def downsample_copies(self, points: torch.Tensor, copies: int,
                           ws: Optional[torch.Tensor] = None,
                           prepped: bool = False, seed: Optional[int] = None,
-                          pool: bool = False, start=None) -> Tuple[torch.Tensor, torch.Tensor]:
+                          pool: bool = False, start=None, rows=None,
+                          rows_wait=None) -> Tuple[torch.Tensor, torch.Tensor]:
         """downsample(torch.cat([points] * copies)) -- the CFG batch of guided_sample_loop
         (diffusion_model.py:244-247) -- without building or re-hashing the copies.  Replay runs
         take the concatenated path: the reference draws one permutation per row.  `ws`
@@ -234,13 +235,17 @@ class HierarchicalProcessor:
         prepped: `ws` was prepared for `points` by the previous step's update
         (_hip.cfg_ddim_voxel_prep).  seed: the subset seed drawn ahead by the loop (the one the
         previous step's update made the pool histogram for: pool=True); None draws it here.
-        start (prepped only): a signal value the launch publishes as it begins (knn_rows_begin)."""
+        start (prepped only): a signal value the launch publishes as it begins (knn_rows_begin).
+        rows / rows_wait: the step's kNN rows handle and its refs signal -- the downsample's emit
+        places the coarse refs itself (phase B; the device-drawn path only: a replayed or
+        concatenated downsample leaves rows.placed False)."""
         src = _rng.source()
         if points.shape[1] <= self.global_points or src.replaying:
             return self.downsample(torch.cat([points] * copies))
         return _hip.voxel_downsample(points, self.global_points,
                                      seed=src.device_seed() if seed is None else seed,
-                                     copies=copies, ws=ws, prepped=prepped, pool=pool, start=start)
+                                     copies=copies, ws=ws, prepped=prepped, pool=pool, start=start,
+                                     rows=rows, rows_wait=rows_wait)
 
     def step_prep(self, points: torch.Tensor) -> bool:
         """Whether the next downsample_copies of `points` can take a workspace prepared by the
@@ -255,9 +260,10 @@ class HierarchicalProcessor:
 # The sampling step's stream layout.  The kNN upsample's build (grid, counts,
 # sort: positions only) does not depend on the noise MLP's output, so it runs on a side stream:
 #   - rows layout (one MLP round of work-groups, <= ROWS_MAX_MLP_POINTS: one cloud): the side
-#     stream bins every point of x (phase A) while the loop stream runs the voxel downsample;
-#     after it ONE launch places the coarse refs (phase B), and the MLP launch's last work-group
-#     waits for phase A's end, so the query's work-groups only check the flag;
+#     stream bins every point of x (phase A) while the loop stream runs the voxel downsample,
+#     whose emit launch places the coarse refs (phase B) once phase A's refs flag is up, and the
+#     MLP launch's last work-group waits for phase A's end, so the query's work-groups only check
+#     the flag;
 #   - compact layout (many MLP rounds: 32 clouds per GPU): the whole build beside the MLP, its
 #     work-groups held to an LDS floor of KNN_BUILD_LDS_FLOOR bytes while the MLP needs at most
 #     two rounds of work-groups (so they only take the CUs the MLP's last round leaves idle), and
@@ -411,7 +417,8 @@ def hierarchical_eps(hp, mlp, xc, xi, x_cat, knn_ws=None, state=None, fused=Fals
         return hp.upsample_knn(mlp(xc), x_cat, xi)
     main = torch.cuda.current_stream()
     if rows is not None:  # the rows layout: phase A ran beside the downsample (knn_rows_begin)
-        _hip.knn3_rows_refs(rows, xi, wait=state.built_sig)  # (waits for phase A in-kernel)
+        if not rows.placed:  # (the device-drawn downsample's emit placed the refs itself)
+            _hip.knn3_rows_refs(rows, xi, wait=state.built_sig)  # (waits for phase A in-kernel)
         if fused:  # the MLP's last work-group waits for phase A's end; the query only checks it
             return _hip.knn3_rows_query(mlp(xc, wait=state.done_sig), rows, state.done_sig,
                                         waited=True)
@@ -654,7 +661,9 @@ class DiffusionProcess:
                         rows, start = (knn_rows_begin(x, model.config.global_points, state,
                                                       rows_ws, by_downsample=prepped)
                                        if rows_ws is not None else (None, None))
-                        xc, xi = hp.downsample_copies(x, 2, vws, prepped, next_seed, pool, start)
+                        xc, xi = hp.downsample_copies(x, 2, vws, prepped, next_seed, pool, start,
+                                                      rows=rows,
+                                                      rows_wait=state.built_sig if rows else None)
                         prep = i + 1 < len(timesteps) and voxel_prep_ok(hp, x, state)
                         # the next step's subset seed, drawn one step ahead for its pool histogram
                         next_seed = (_rng.source().device_seed() & (2**64 - 1)

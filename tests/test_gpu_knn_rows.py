@@ -204,3 +204,22 @@ def test_guided_loop_rows_layout_bit_identical(monkeypatch):
         assert len(calls) - n0 == (5 if rows and overlap else 0), (rows, overlap)
     assert torch.equal(outs[0], outs[1])
     assert torch.equal(outs[0], outs[2])
+
+
+@pytest.mark.parametrize("N,M,C", [(40000, 10000, 1), (120000, 30000, 1), (20000, 5000, 2)])
+def test_downsample_places_rows_refs(H, N, M, C):
+    """Phase B inside the voxel emit (pcst_voxel_downsample_rows: the sampling step's layout)
+    places the same refs as pcst_knn3_rows_refs on the downsample's indices: the rows query gives
+    the bits of the separate placement and of the compact layout on cat([x, x])."""
+    rng = np.random.default_rng(N + C)
+    x = dev(rng.standard_normal((C, N, 3)).astype(np.float32))
+    coarse = dev(rng.standard_normal((2 * C, M, 3)).astype(np.float32))
+    h1 = H.knn3_rows_build(x, M, 2)
+    _, xi = H.voxel_downsample(x, M, seed=5, copies=2, rows=h1)
+    assert h1.placed
+    got = H.knn3_rows_query(coarse, h1)
+    h2 = H.knn3_rows_build(x, M, 2)
+    H.knn3_rows_refs(h2, xi)
+    assert torch.equal(got, H.knn3_rows_query(coarse, h2))
+    assert torch.equal(got, H.knn3_interp(coarse, torch.cat([x, x]), xi))
+    assert H.knn_rows_stats(h1)["err"] == 0

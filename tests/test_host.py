@@ -439,7 +439,7 @@ def test_generator_rng_randn_like_keeps_the_dtype():
 
 
 def test_dense_voxel_boxes_are_collision_free():
-    """Every box of csrc/voxel.hip's kDenseBoxes (the voxel boxes that take the dense grid instead
+    """Every box of csrc/voxel.hip's PCST_DENSE_BOXES (the voxel boxes that take the dense grid instead
     of the hash table) holds no two voxel coordinates whose int32 xor-hash -- the reference's
     voxel_hash, diffusion_model.py:90 -- is equal, so inside it a hash group is exactly one voxel
     (the dense path's grouping is the reference's); and the check itself finds the collisions
@@ -448,7 +448,7 @@ def test_dense_voxel_boxes_are_collision_free():
 
     src = open(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
                             "pointcloud_style_transfer_amd", "csrc", "voxel.hip")).read()
-    table = src[src.index("kDenseBoxes[] = {"):src.index("};", src.index("kDenseBoxes[] = {"))]
+    table = src[src.index("#define PCST_DENSE_BOXES"):src.index("__device__", src.index("#define PCST_DENSE_BOXES"))]
     boxes = [tuple(int(v) for v in m) for m in re.findall(r"\{(\d+), (\d+), (\d+)\}", table)]
     assert len(boxes) >= 10
 

@@ -1,4 +1,4 @@
-"""Certified collision-free voxel boxes for the dense voxel grid (csrc/voxel.hip kDenseBoxes).
+"""Certified collision-free voxel boxes for the dense voxel grid (csrc/voxel.hip PCST_DENSE_BOXES).
 
     python tools/voxel_cert.py
 
