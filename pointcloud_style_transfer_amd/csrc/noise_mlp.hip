@@ -1032,6 +1032,11 @@ extern "C" int pcst_noise_mlp_ex(const float* pts, int64_t P, int64_t points_per
                                  uint32_t* start_counter, const uint32_t* wait_flag,
                                  uint32_t wait_value, uint32_t* wait_counter, int32_t* wait_err,
                                  int64_t max_polls, void* stream) {
+  // every argument is checked before anything is launched: a start signal published for an
+  // invalid call would release a side stream although no MLP ran
+  if (int rc = check_mlp_args("noise_mlp_ex", P, points_per_cloud, nclouds, blob, blob_bytes, precision)) return rc;
+  PCST_CHECK_ARG(!wait_flag || precision != 1 || P == 0 || wait_counter,
+                 "noise_mlp_ex: a wait needs its counter");
   if (precision != 1 || P == 0) {  // the f32 kernel has no fused form: separate launches
     if (start_flag && !start_counter) {
       hipLaunchKernelGGL(mlp_start_signal_kernel, dim3(1), dim3(64), 0, as_stream(stream), start_flag,
@@ -1049,8 +1054,6 @@ extern "C" int pcst_noise_mlp_ex(const float* pts, int64_t P, int64_t points_per
     if (!wait_flag) return rc;
     return pcst_signal_wait(wait_flag, wait_value, wait_err, max_polls, stream);
   }
-  if (int rc = check_mlp_args("noise_mlp_ex", P, points_per_cloud, nclouds, blob, blob_bytes, precision)) return rc;
-  PCST_CHECK_ARG(!wait_flag || wait_counter, "noise_mlp_ex: a wait needs its counter");
   launch_solo(pts, P, points_per_cloud, cond, nclouds, blob, bias, out, wait_flag, wait_value,
               wait_counter, wait_err, max_polls > 0 ? max_polls : (int64_t)kSignalPolls, start_flag,
               start_value, start_counter, as_stream(stream));

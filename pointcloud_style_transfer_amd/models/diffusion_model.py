@@ -422,7 +422,12 @@ def hierarchical_eps(hp, mlp, xc, xi, x_cat, knn_ws=None, state=None, fused=Fals
         if fused:  # the MLP's last work-group waits for phase A's end; the query only checks it
             return _hip.knn3_rows_query(mlp(xc, wait=state.done_sig), rows, state.done_sig,
                                         waited=True)
-        return _hip.knn3_rows_query(mlp(xc), rows, state.done_sig)
+        # else one wait launch (one work-group polls) before the query, never the query's own
+        # work-groups: at 4 per CU they hold every VGPR of the device, and phase A's last launches
+        # could then find no CU ("Forward progress")
+        nc = mlp(xc)
+        state.done_sig.wait(main)
+        return _hip.knn3_rows_query(nc, rows, state.done_sig, waited=True)
     ready, built = state.ready_sig, state.built_sig
     start = None
     if fused:

@@ -367,3 +367,59 @@ def test_pool_prepped_downsample_matches_plain():
         got = _hip.voxel_downsample(x, T, seed=seed, copies=2, ws=ws, prepped=True, pool=True)
         want = _hip.voxel_downsample(x, T, seed=seed, copies=2)
         assert torch.equal(got[1], want[1]) and torch.equal(got[0], want[0]), r
+
+
+def test_waiters_launched_before_their_producer_on_a_saturated_device():
+    """Forward progress of the product's in-kernel spin-waits ("Forward progress"):
+    each waiter is queued BEFORE its producer's signal while a saturating kernel holds every CU
+    (the bf16 noise MLP over 32 x 30000 points: 7500 work-groups of 512 threads, ~30 rounds), and
+    completes without a timeout once the producer signals: (1) the voxel emit's wait for phase A
+    before it places the coarse refs (pcst_voxel_downsample_rows: every emit work-group waits),
+    (2) the MLP's last work-group's wait (pcst_noise_mlp_ex), (3) pcst_signal_wait.  The waiters'
+    grids are far below the device's capacity (1 / 235 / 236 work-groups), so the producer's
+    launches always find a CU; the results equal the unsynchronised computations'."""
+    from pointcloud_style_transfer_amd import _hip
+    from pointcloud_style_transfer_amd.config.config import Config
+    from pointcloud_style_transfer_amd.models.diffusion_model import NoisePredictor
+
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(12)
+    npred = NoisePredictor(Config(make_dirs=False, precision="bf16")).to(dev).eval()
+    rng = np.random.default_rng(12)
+    big = torch.randn(64 * 30000, 3, device=dev)
+    small = torch.randn(2 * 30000, 3, device=dev)
+    N, M = 120000, 30000
+    x = torch.from_numpy(rng.standard_normal((1, N, 3)).astype(np.float32)).to(dev)
+    coarse = torch.randn(2, M, 3, device=dev)
+    with torch.no_grad():
+        cbig = npred.cond(torch.full((64,), 900, device=dev), torch.randn(64, 256, device=dev))
+        csmall = npred.cond(torch.tensor([900, 900], device=dev), torch.randn(2, 256, device=dev))
+        blob, bias = npred.packed()[:2]
+        ref_small = _hip.noise_mlp(small, 30000, csmall, blob, bias, npred.precision_code)
+        h_ref = _hip.knn3_rows_build(x, M, 2)
+        _, xi_ref = _hip.voxel_downsample(x, M, seed=3, copies=2)
+        _hip.knn3_rows_refs(h_ref, xi_ref)
+        q_ref = _hip.knn3_rows_query(coarse, h_ref)
+        h = _hip.knn3_rows_build(x, M, 2)
+        torch.cuda.synchronize()
+        prod = torch.cuda.Stream(device=dev)
+        cons = torch.cuda.Stream(device=dev)
+        s1, s2, s3 = (_hip.DeviceSignal(dev) for _ in range(3))
+        for s in (prod, cons):
+            s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(prod):  # the saturating kernel first, then the three signals
+            _hip.noise_mlp(big, 30000, cbig, blob, bias, npred.precision_code)
+            s1.signal(prod)
+            s2.signal(prod)
+            s3.signal(prod)
+        with torch.cuda.stream(cons):  # the waiters, queued before the signals exist
+            _, xi = _hip.voxel_downsample(x, M, seed=3, copies=2, rows=h, rows_wait=s1)
+            out = _hip.noise_mlp(small, 30000, csmall, blob, bias, npred.precision_code, wait=s2)
+            s3.wait(cons)
+            q = _hip.knn3_rows_query(coarse, h)
+        torch.cuda.synchronize()
+    for s in (s1, s2, s3):
+        assert not s.timed_out()
+    assert torch.equal(xi, xi_ref)
+    assert torch.equal(out, ref_small)
+    assert torch.equal(q, q_ref)
