@@ -62,6 +62,11 @@ constexpr int kCountPerBlock = 1024;     // elements per count-kernel block (4 p
 constexpr int kOvlLds = 256;             // overflow refs staged in LDS per query work-group
 constexpr int kOutlierBrickBlocks = 256; // outlier workgroups per cloud (brick search, 4 queries)
 constexpr int kBrickBatch = 4;           // bricks per brick-copy work item of the rows query
+#ifndef PCST_KNN_WIDE_VOL                // experiment builds override (csrc/Makefile XDEF)
+#define PCST_KNN_WIDE_VOL 80
+#endif
+constexpr int kWideBoxVol = PCST_KNN_WIDE_VOL;  // a chunk whose one-ring box holds this many cells
+                                                // or more stages two rings in pass 1
 constexpr int kQueryBlocksPerCU = 4;     // resident query work-groups per CU (waves_per_eu 4, 38 KiB LDS)
 
 
@@ -1043,6 +1048,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
   uint4* trace = reinterpret_cast<uint4*>(obound + b * N + 4096);
   const uint32_t gw = blockIdx.x * 4 + wv;
   uint32_t tr0 = 0, tr_open1 = 0, tr_p2 = 0;
+  int tr_vol = 0;
 #endif
   for (int item = (int)m * 4 + wv; item < nch;) {
 #ifdef PCST_KNN_CHUNK_TRACE
@@ -1086,9 +1092,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
     const int cz = cell_coord(me.fz, g.o[2], g.inv, g.d[2]);
     const int lx = wave_min(cx), hx = wave_max(cx), ly = wave_min(cy), hy = wave_max(cy),
               lz = wave_min(cz), hz = wave_max(cz);
-    // 1. the chunk's cell box grown by one cell
-    Box pb = {max(lx - 1, 0), min(hx + 1, g.d[0] - 1), max(ly - 1, 0), min(hy + 1, g.d[1] - 1),
-              max(lz - 1, 0), min(hz + 1, g.d[2] - 1)};
+    // 1. the chunk's cell box grown by one cell -- by two when the chunk spans more than an octant
+    // (a sparse region: there pass 1 with one ring settles almost no lane and pass 2 ran in 90-96 %
+    // of such chunks, each pass a full chain of dependent loads; tools/knn_chunk_trace.py, r6n)
+    const int gr = (hx - lx + 3) * (hy - ly + 3) * (hz - lz + 3) >= kWideBoxVol ? 2 : 1;
+    Box pb = {max(lx - gr, 0), min(hx + gr, g.d[0] - 1), max(ly - gr, 0), min(hy + gr, g.d[1] - 1),
+              max(lz - gr, 0), min(hz + gr, g.d[2] - 1)};
     uint32_t unlimited = 0xffffffffu;
     scan_box(pb, none, g, rng, R, W, me, kk, unlimited);
     if constexpr (ROWS) offer_overflow(pb, none, me);
@@ -1096,6 +1105,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
     bool ok = true;
 #ifdef PCST_KNN_CHUNK_TRACE
     tr_open1 = (uint32_t)__popcll(__ballot(open));
+    tr_vol = pb.volume();
 #endif
     // 2. the balls of the open lanes that hold kk refs
     if (__any(open)) {
@@ -1153,8 +1163,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
     if (valid && !open) idw_write(me.t, kk, V, out + (b * N + n) * 3);
 #ifdef PCST_KNN_CHUNK_TRACE
     if (lane == 0 && item < 16384)
-      trace[item] = make_uint4(tr0, (uint32_t)__builtin_amdgcn_s_memrealtime(), gw,
-                               tr_open1 | (tr_p2 << 8) | ((uint32_t)__popcll(rest) << 16));
+      trace[item] = make_uint4(tr0, (uint32_t)__builtin_amdgcn_s_memrealtime(),
+                               gw | ((uint32_t)__popcll(rest) << 16),
+                               min(tr_open1, 127u) | (tr_p2 << 7) | ((ch.y - ch.x) << 8) |
+                                   ((uint32_t)min(tr_vol, 65535) << 16));
 #endif
     item = next;
   }

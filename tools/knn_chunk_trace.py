@@ -43,43 +43,66 @@ def main():
     x = torch.from_numpy(standard_normal(3000, (1, N, 3))).to(dev)
     ws = _hip.knn_rows_workspace(1, 2, N, M, dev)
     coarse = torch.randn(2, M, 3, device=dev)
+    off = rows_obound_offset(1, 2, N, M)
     for rep in range(3):
         xc, xi = _hip.voxel_downsample(x, M, seed=rep, copies=2)
         h = _hip.knn3_rows_build(x, M, 2, ws)
         _hip.knn3_rows_refs(h, xi)
+        for b in range(2):  # no stale records (chunks of known rows only are not recorded)
+            o = off + (b * N + 4096) * 4
+            ws[o:o + 16384 * 16].zero_()
         _hip.knn3_rows_query(coarse, h)
         torch.cuda.synchronize()
     st = _hip.knn_rows_stats(h)
     nch = st["chunks"][0]
-    off = rows_obound_offset(1, 2, N, M)
     tr = []
     for b in range(2):
         o = off + (b * N + 4096) * 4
         tr.append(ws[o:o + nch * 16].view(torch.int32).view(nch, 4).cpu().numpy().astype(np.int64))
     tr = np.concatenate(tr)
     t0, t1 = tr[:, 0] & 0xFFFFFFFF, tr[:, 1] & 0xFFFFFFFF
-    base = t0.min()
+    good = (t1 > t0) & (t1 - t0 < 100000)
+    base = t0[good].min()
     s, e = (t0 - base) / 100.0, (t1 - base) / 100.0   # us
     d = e - s
     info = tr[:, 3]
-    open1, p2, outl = info & 0xFF, (info >> 8) & 0xFF, info >> 16
-    print(f"chunks {nch} per row, outliers {st['outliers']}, span {e.max():.1f} us")
+    open1, p2, rows, vol = info & 0x7F, (info >> 7) & 1, (info >> 8) & 0xFF, info >> 16
+    outl = tr[:, 2] >> 16
+    wave = tr[:, 2] & 0xFFFF
+    ok = good
+    print(f"chunks {nch} per row, recorded {ok.sum()}, outliers {st['outliers']}")
     q = lambda a: " ".join(f"{np.percentile(a, p):.1f}" for p in (10, 50, 90, 99, 100))  # noqa: E731
-    print("duration p10/50/90/99/max:", q(d))
-    print("start    p10/50/90/99/max:", q(s))
-    print("end      p10/50/90/99/max:", q(e))
-    waves, cnt = np.unique(tr[:, 2], return_counts=True)
+    print("duration p10/50/90/99/max:", q(d[ok]))
+    print("start    p10/50/90/99/max:", q(s[ok]))
+    print("end      p10/50/90/99/max:", q(e[ok]))
+    waves, cnt = np.unique(wave[ok], return_counts=True)
     print("waves used", len(waves), "chunks per wave histogram", np.bincount(cnt)[:8].tolist())
-    print(f"pass 2 ran in {p2.mean():.3f} of chunks; mean dur with / without pass 2: "
-          f"{d[p2 > 0].mean():.1f} / {d[p2 == 0].mean():.1f}")
-    print(f"chunks with outliers {np.mean(outl > 0):.3f}; mean dur with / without: "
-          f"{d[outl > 0].mean() if (outl > 0).any() else 0:.1f} / {d[outl == 0].mean():.1f}")
-    print("mean open lanes after pass 1:", open1.mean())
-    # last-finishing waves: their chunk sequence
-    lastw = tr[np.argmax(e), 2]
-    sel = tr[:, 2] == lastw
+    print(f"pass 2 ran in {p2[ok].mean():.3f} of chunks; mean dur with / without pass 2: "
+          f"{d[ok & (p2 > 0)].mean():.1f} / {d[ok & (p2 == 0)].mean():.1f}")
+    print(f"chunks with outliers {np.mean(outl[ok] > 0):.3f}")
+    print("mean open lanes after pass 1:", open1[ok].mean())
+    for lo, hi in ((1, 16), (16, 32), (32, 48), (48, 64), (64, 65)):
+        m = ok & (rows >= lo) & (rows < hi)
+        if m.any():
+            print(f"rows [{lo},{hi}): n {m.sum()}, dur mean {d[m].mean():.1f} p90 {np.percentile(d[m], 90):.1f}, "
+                  f"pass2 {p2[m].mean():.2f}, box vol mean {vol[m].mean():.0f}")
+    for lo, hi in ((0, 40), (40, 80), (80, 150), (150, 250), (250, 65536)):
+        m = ok & (vol >= lo) & (vol < hi)
+        if m.any():
+            print(f"box vol [{lo},{hi}): n {m.sum()}, dur mean {d[m].mean():.1f} p90 {np.percentile(d[m], 90):.1f}, "
+                  f"pass2 {p2[m].mean():.2f}, rows mean {rows[m].mean():.0f}")
+    long = ok & (d >= np.percentile(d[ok], 95))
+    print(f"the longest 5 %: rows mean {rows[long].mean():.0f}, vol mean {vol[long].mean():.0f}, "
+          f"pass2 {p2[long].mean():.2f}, open1 mean {open1[long].mean():.1f}, start mean {s[long].mean():.1f}")
+    order = np.argsort(np.where(ok, np.arange(len(ok)) % nch, 1 << 30))
+    pos = (np.arange(len(ok)) % nch)
+    for lo in range(0, nch, nch // 8):
+        m = ok & (pos >= lo) & (pos < lo + nch // 8)
+        print(f"  items [{lo},{lo + nch // 8}): dur mean {d[m].mean():.1f}, pass2 {p2[m].mean():.2f}")
+    lastw = wave[np.argmax(np.where(ok, e, -1))]
+    sel = ok & (wave == lastw)
     print("slowest wave's chunks (start, dur):", list(zip(np.round(s[sel], 1), np.round(d[sel], 1))))
-    tot = d.sum()
+    tot = d[ok].sum()
     print(f"sum of chunk durations {tot:.0f} wave-us = {tot / len(waves):.1f} us per used wave")
 
 
