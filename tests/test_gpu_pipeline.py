@@ -158,7 +158,7 @@ def test_guided_sample_graph_matches_eager(B):
 
 def test_inference_entry_point_bf16(golden, tmp_path, monkeypatch):
     """`scripts/inference.py --precision bf16` reaches the measured mode: the noise MLP runs
-    the bf16 pair kernel (precision code 2) on every step, and the result stays within the
+    the bf16 solo kernel (precision code 1, `packing.BF16`) on every step, and the result stays within the
     bf16 mode's distance of the fp32 run (same draws)."""
     from detweights import load_into
     from pointcloud_style_transfer_amd import _hip, packing, rng
