@@ -384,7 +384,10 @@ struct VoxelFastWS {
   size_t bytes;
 };
 
-constexpr int kEmitTile = 1024;   // 256 threads x 4 indices
+#ifndef PCST_EMIT_TILE  // experiment builds override (csrc/Makefile XDEF)
+#define PCST_EMIT_TILE 1024
+#endif
+constexpr int kEmitTile = PCST_EMIT_TILE;  // 256 threads x 4 indices
 constexpr int kMarkTiles = 1024;  // tiles counted in LDS by the marking kernels
 
 static int64_t vox_table_size(int64_t N) {
@@ -606,7 +609,10 @@ __device__ __forceinline__ int4 voxel_box(const StatRec& M, float4 v4, int64_t H
 // to ONE address serialise at the memory-side atomic unit (insert 15.9 us with one replica on a
 // squashed noise cloud, tools/voxel_probe.py).  R = the largest power of two <= 8 with R cells
 // in the table.
-constexpr int kDenseReplicas = 8;
+#ifndef PCST_DENSE_REPLICAS  // experiment builds override (csrc/Makefile XDEF)
+#define PCST_DENSE_REPLICAS 8
+#endif
+constexpr int kDenseReplicas = PCST_DENSE_REPLICAS;
 __device__ __forceinline__ int dense_replicas(int cells, int64_t H) {
   int r = kDenseReplicas;
   while (r > 1 && (int64_t)r * cells > H) r >>= 1;

@@ -142,6 +142,17 @@ for st in "$@"; do
           python -c "import json,sys; f=lambda p: json.loads(open(p).read().strip().splitlines()[-1]); a=f(sys.argv[1]); b=f(sys.argv[2]); print(sys.argv[3], 'b1', a['value'], a['ms_per_step'], a['roofline']['avg_launch_ms'], 'b32', b['ms_per_step'])" "$OUT/bench_$v.$pass.json" "$OUT/b32_$v.$pass.json" "$v.$pass"
         done
       done ;;
+    proflib=*)
+      # proflib=v_a,v_b: kernel stats of the driver-window bench with each library (kNN / voxel rows)
+      VS=${st#proflib=}
+      for v in prod ${VS//,/ }; do
+        lib=$PWD/pointcloud_style_transfer_amd/libpcst_hip.so
+        if [ "$v" != prod ]; then lib=$PWD/pointcloud_style_transfer_amd/libpcst_hip_$v.so; fi
+        PCST_LIB=$lib timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_$v" -o run -- \
+            python tools/bench_knobs.py ${BENCH#bench.py } > "$OUT/pbench_$v.json" 2> "$OUT/pbench_$v.err"
+        rc=$?; if [ $rc -ne 0 ]; then tail -5 "$OUT/pbench_$v.err"; exit $rc; fi
+        echo "== $v"; python tools/kstats.py "$OUT/prof_$v/run_kernel_stats.csv" 12 | tee "$OUT/kernel_top_$v.txt"
+      done ;;
     timeline)
       python tools/timeline.py "$OUT/prof/run_kernel_trace.csv" --last 18 --show 2 | tee "$OUT/driver_window_timeline.txt" | tail -40 ;;
     fpsab=*)
