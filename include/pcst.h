@@ -282,8 +282,12 @@ int pcst_voxel_downsample_copies_prepped(const float* pts, int64_t B, int64_t N,
  * (on another stream); every emit work-group first writes its rows of out_idx / out_pts, then
  * waits for wait_flag >= wait_value (the build's refs flag; NULL: the stream is ordered after the
  * build already), at most max_polls polls (<= 0: ~10 s), and places its kept points -- the same
- * placement as pcst_knn3_rows_refs(out_idx).  A work-group whose wait gives up places nothing and
- * sets *wait_err: pass it to pcst_knn3_rows_query as refs_err. */
+ * placement as pcst_knn3_rows_refs(out_idx).  That in-launch wait is used only while the emit
+ * launch has at most one work-group per CU (one cloud: 236), so waiting work-groups never hold
+ * every CU while the build still needs some; a larger emit launch places nothing itself and is
+ * followed by pcst_knn3_rows_refs's own launch (the same wait, at most max(CUs, rows)
+ * work-groups).  A work-group whose wait gives up places nothing and sets *wait_err: pass it to
+ * pcst_knn3_rows_query as refs_err. */
 int pcst_voxel_downsample_rows(const float* pts, int64_t B, int64_t N, int64_t copies,
                                int64_t target, void* workspace, uint64_t seed, int prepped,
                                int pool, int64_t* out_idx, float* out_pts, uint32_t* start_flag,
@@ -341,13 +345,15 @@ int pcst_knn_error(void* workspace, int64_t B, int64_t N, int64_t M, int32_t* er
  *     scanned box holds them.  wait_flag (NULL: none): the kernel first waits, in every
  *     work-group, until the flag holds wait_value (the side stream's pcst_signal_write after
  *     rows_build), at most max_polls polls (<= 0: ~10 s); a work-group whose wait gives up sets
- *     *wait_err and writes nothing (pass wait_err to rows_query as refs_err);
+ *     *wait_err and writes nothing (pass wait_err to rows_query as refs_err).  At most max(CUs,
+ *     B) work-groups (each strides over its row's refs), so the waiting ones leave CUs free;
  *   rows_query (coarse [B,M,3] -> out [B,N,3]): the query and outlier passes of pcst_knn3_query
  *     over every point, known points copying their coarse value; built_flag (the build's
- *     done_flag): every query work-group waits for it itself (as rows_refs; on a timeout it sets
- *     *wait_err and writes eps = 0); with wait_err == NULL the stream has already waited for it
- *     (e.g. pcst_noise_mlp_ex's wait in the MLP launch before the query) and the work-groups only
- *     check it (a flag short of built_value: eps = 0, nothing read); refs_err (NULL: none): the
+ *     done_flag) with wait_err: a one-work-group wait launch (pcst_signal_wait) precedes the query
+ *     (the query's resident grid never waits itself: it would hold the CUs the build needs); with
+ *     wait_err == NULL the stream has already waited for it (e.g. pcst_noise_mlp_ex's wait in the
+ *     MLP launch before the query); either way the work-groups check the flag (short of
+ *     built_value: eps = 0, nothing read); refs_err (NULL: none): the
  *     rows_refs wait's error word -- nonzero: eps = 0, nothing read; grid_cap as pcst_knn3_query.
  * Same bits as pcst_knn3_interp on cat([x] * copies).  An index outside [0, N) sets bit 1 of the
  * error word, a chunk or ref range outside the workspace's arrays bits 4 / 8 (the range is then

@@ -896,8 +896,6 @@ struct KArgs {
   const int32_t* ovn;         // [B] their counts (rows layout)
   int32_t* err;               // bit 4: a chunk outside [0, N], bit 8: a ref range outside the refs
                               // (bit 1: a bad coarse index, bit 16: a brick over-full -- phase B)
-  int32_t* werr;              // rows layout: the query waits for bflag itself (its timeout word)
-  int64_t max_polls;
   const int32_t* refs_err;    // rows layout: phase B's wait error word (nonzero: nothing placed)
   int32_t* qctr;              // [B][kQueryShards][kCtrStride] chunk counters (zero at launch);
                               // rows layout: [B..2B) the brick-batch counters
@@ -945,14 +943,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
   const unsigned m = blockIdx.x / (unsigned)B;
   if (m >= Gr) return;  // (the host launches a multiple of B)
   const int64_t cl = ROWS ? b % ka.C : b;
-  // compact layout: the stream waited for the build before this launch, the flag is only checked;
-  // rows layout with werr: the work-groups wait for the build's last flag themselves (no wait
-  // launch); with werr NULL the stream already waited for the flag (the MLP's last work-group),
-  // so the work-groups only check it -- no acquire fence per work-group, which at 4 work-groups
-  // per CU cost the step ~11 us (2849 / 2834 vs 2756 / 2739 steps/s, r05/s2r)
-  bool pending = (ROWS && bflag && ka.werr) ? !block_wait_flag(bflag, bvalue, ka.werr, ka.max_polls)
-                                            : false;
-  pending = pending || query_pending(bflag, bvalue, ROWS ? ka.refs_err : nullptr);
+  // the stream waited for the build's flag before this launch (a wait launch, or the MLP's last
+  // work-group), so the work-groups only check it: no wait here (the resident grid fills every
+  // CU's LDS, so a waiting query could hold the CUs its producer needs) and no acquire fence per
+  // work-group, which at 4 work-groups per CU cost the step ~11 us (r05/s2r)
+  const bool pending = query_pending(bflag, bvalue, ROWS ? ka.refs_err : nullptr);
   if (pending) {
     for (int64_t n = (int64_t)m * 256 + threadIdx.x; n < N * 3; n += (int64_t)Gr * 256)
       out[b * N * 3 + n] = 0.0f;
@@ -1471,11 +1466,7 @@ static void launch_knn_query(int64_t nch_max, const float* gp, const uint64_t* c
                              int64_t Cpad, const KArgs& ka, const float* coarse, const float* orig,
                              int64_t B, int64_t N, int64_t M, float* out, const uint32_t* bflag,
                              uint32_t bvalue, int64_t grid_cap, hipStream_t s) {
-  int dev = 0, cus = 0;
-  if (hipGetDevice(&dev) != hipSuccess ||
-      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
-    cus = 256;
-  const int64_t cap = grid_cap > 0 ? grid_cap : (int64_t)cus * kQueryBlocksPerCU;
+  const int64_t cap = grid_cap > 0 ? grid_cap : (int64_t)device_cus() * kQueryBlocksPerCU;
   const int64_t Gr = std::max<int64_t>(1, std::min<int64_t>(cdiv(nch_max, 4), cap / B));
   auto qk = M >= 3 ? knn_query_kernel<3, ROWS>
                    : (M == 2 ? knn_query_kernel<2, ROWS> : knn_query_kernel<1, ROWS>);
@@ -1490,8 +1481,8 @@ static void launch_knn_query(int64_t nch_max, const float* gp, const uint64_t* c
 static void launch_knn_query(const KnnWS& w, const float* coarse, const float* orig, int64_t B,
                              int64_t N, int64_t M, float* out, const uint32_t* bflag,
                              uint32_t bvalue, int64_t grid_cap, hipStream_t s) {
-  const KArgs ka = {B, nullptr, nullptr, nullptr, nullptr, nullptr, w.err, nullptr, 0, nullptr,
-                    w.qctr, nullptr, nullptr};
+  const KArgs ka = {B, nullptr, nullptr, nullptr, nullptr, nullptr, w.err, nullptr, w.qctr, nullptr,
+                    nullptr};
   launch_knn_query<false>(w.maxch, w.gp, w.cnt, w.refs, w.qorder, w.chunks, w.nchunk, w.olist,
                           w.obound, w.ocount, w.known, w.Cpad, ka, coarse, orig, B, N, M, out,
                           bflag, bvalue, grid_cap, s);
@@ -1585,6 +1576,20 @@ extern "C" int pcst_knn3_rows_build(const float* x, int64_t C, int64_t copies, i
   return PCST_OK;
 }
 
+// Phase B as a launch of its own (pcst_knn3_rows_refs; the downsample when its emit grid is too
+// large to wait in-kernel): the work-groups load their indices, then wait for phase A's flag.  At
+// most max(CUs, rows) work-groups (grid-stride over the refs), so the waiting ones never hold
+// every CU while phase A still needs some.
+int pcst::rows_place_launch(const KnnRowsWS& w, const float* x, const int64_t* idx, int64_t N, int64_t M,
+                            const uint32_t* wflag, uint32_t wvalue, int32_t* werr, int64_t max_polls,
+                            hipStream_t s) {
+  const int64_t per = std::max<int64_t>(1, std::min<int64_t>(cdiv(M, 256), device_cus() / w.B));
+  hipLaunchKernelGGL(knn_rows_place_kernel, dim3((unsigned)per, (unsigned)w.B), dim3(256), 0, s, x, idx,
+                     rows_place_args(w, N, M), w.err, wflag, wvalue, werr,
+                     max_polls > 0 ? max_polls : (int64_t)kSignalPolls);
+  return PCST_OK;
+}
+
 extern "C" int pcst_knn3_rows_refs(const float* x, const int64_t* idx, int64_t C, int64_t copies,
                                    int64_t N, int64_t M, void* workspace, const uint32_t* wait_flag,
                                    uint32_t wait_value, int32_t* wait_err, int64_t max_polls,
@@ -1593,10 +1598,7 @@ extern "C" int pcst_knn3_rows_refs(const float* x, const int64_t* idx, int64_t C
   if (C == 0) return PCST_OK;
   PCST_CHECK_ARG(x && idx && workspace, "knn3_rows_refs: null pointer");
   KnnRowsWS w = carve_knn_rows(workspace, C, copies, N, M);
-  hipStream_t s = as_stream(stream);
-  const dim3 gj((unsigned)std::min<int64_t>(cdiv(M, 256), 1024), (unsigned)w.B);
-  hipLaunchKernelGGL(knn_rows_place_kernel, gj, dim3(256), 0, s, x, idx, rows_place_args(w, N, M), w.err,
-                     wait_flag, wait_value, wait_err, max_polls > 0 ? max_polls : (int64_t)kSignalPolls);
+  rows_place_launch(w, x, idx, N, M, wait_flag, wait_value, wait_err, max_polls, as_stream(stream));
   PCST_LAUNCH_CHECK("knn3_rows_refs");
   return PCST_OK;
 }
@@ -1610,9 +1612,12 @@ extern "C" int pcst_knn3_rows_query(const float* coarse, const float* x, int64_t
   if (C == 0) return PCST_OK;
   PCST_CHECK_ARG(coarse && x && out && workspace, "knn3_rows_query: null pointer");
   KnnRowsWS w = carve_knn_rows(workspace, C, copies, N, M);
-  const KArgs ka = {C, w.known, w.xs, w.rcnt, w.over, w.ovn, w.err, wait_err,
-                    max_polls > 0 ? max_polls : (int64_t)kSignalPolls, refs_err, w.qctr, w.brefs,
-                    w.bcnt};
+  const KArgs ka = {C, w.known, w.xs, w.rcnt, w.over, w.ovn, w.err, refs_err, w.qctr, w.brefs, w.bcnt};
+  // a wait for the build: one work-group before the query (never the query's own work-groups)
+  if (built_flag && wait_err) {
+    const int rc = pcst_signal_wait(built_flag, built_value, wait_err, max_polls, stream);
+    if (rc) return rc;
+  }
   launch_knn_query<true>(w.maxch, w.gp, w.cnt, w.refs, nullptr, w.chunks, w.nchunk, w.olist,
                          w.obound, w.ocount, w.known, w.Cpad, ka, coarse, x, w.B, N, M, out,
                          built_flag, built_value, grid_cap, as_stream(stream));

@@ -12,6 +12,15 @@ constexpr int kKnnMaxTiles = 1024;       // per-block LDS tile histogram in the 
 constexpr int kQueryShards = 8;          // work counters per CFG row (one per XCD)
 constexpr int kCtrStride = 64;           // int32 words between counters: each on its own 256-B line
 
+// CUs of the current device (queried per call: the library keeps no process-global state)
+static inline int device_cus() {
+  int dev = 0, n = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+    return 256;
+  return n;
+}
+
 static int64_t knn_cells(int64_t M) {
   return std::min<int64_t>(std::max<int64_t>(4096, 16 * M), (int64_t)kKnnMaxTiles * kKnnTile - 1);
 }
@@ -91,6 +100,11 @@ struct RowsPlace {
 static RowsPlace rows_place_args(const KnnRowsWS& w, int64_t N, int64_t M) {
   return RowsPlace{w.cnt, w.crank, w.known, w.rcnt, w.refs, w.over, w.ovn, w.C, N, M, w.Cpad};
 }
+
+// phase B's own launch (knn.hip)
+int rows_place_launch(const KnnRowsWS& w, const float* x, const int64_t* idx, int64_t N, int64_t M,
+                      const uint32_t* wflag, uint32_t wvalue, int32_t* werr, int64_t max_polls,
+                      hipStream_t s);
 
 // The consumer side of a flag hand-off inside a kernel (MI355X_MICROARCH.md, inter-workgroup
 // visibility): thread 0 polls (relaxed, agent scope) until the flag holds `value`, at most

@@ -1045,6 +1045,7 @@ static size_t vox_zero_bytes(const VoxelFastWS& w, int64_t rows) {
 // place (optional): phase B of the kNN rows layout fused into the emit (knn_rows.h RowsPlace of
 // the rows workspace, with its phase-A flag wait).
 struct EmitPlace {
+  const KnnRowsWS* kw = nullptr;  // the rows workspace (rp's arrays)
   RowsPlace rp{};
   const uint32_t* wflag = nullptr;
   uint32_t wvalue = 0;
@@ -1078,10 +1079,17 @@ static int voxel_fast(const float* pts, int64_t B, int64_t N, int64_t copies, in
   hipLaunchKernelGGL(voxf_select_kernel, dim3(128, rows), dim3(256), 0, s, n, T, b, seed, seed_p,
                      hist, w.hist2, w.sel, w.cnt4, w.rhash, w.isrep, w.reps, w.ties, w.kcnt,
                      w.ktile, w.tiles, sshift);
+  // the placement inside the emit only while its work-groups fit one per CU (each may wait for
+  // phase A, which needs CUs to finish); otherwise phase B's own, capped launch after it
+  const bool fuse = place.rp.refs != nullptr && (int64_t)w.tiles * rows <= device_cus();
+  const EmitPlace none;
+  const EmitPlace& ep = fuse ? place : none;
   hipLaunchKernelGGL(voxf_emit_kernel, dim3((unsigned)w.tiles, rows), dim3(256), 0, s, pts, n, T,
                      b, w.kcnt, w.ktile, w.tiles, w.cnt4, w.sel, w.ties, w.reps, out_idx, out_pts,
-                     w.phist, place.rp, place.wflag, place.wvalue, place.werr,
-                     place.max_polls > 0 ? place.max_polls : (int64_t)kSignalPolls);
+                     w.phist, ep.rp, ep.wflag, ep.wvalue, ep.werr,
+                     ep.max_polls > 0 ? ep.max_polls : (int64_t)kSignalPolls);
+  if (place.rp.refs != nullptr && !fuse)
+    rows_place_launch(*place.kw, pts, out_idx, N, T, place.wflag, place.wvalue, place.werr, place.max_polls, s);
   PCST_LAUNCH_CHECK("voxel_downsample");
   return PCST_OK;
 }
@@ -1228,6 +1236,7 @@ extern "C" int pcst_voxel_downsample_rows(const float* pts, int64_t B, int64_t N
   PCST_CHECK_ARG(prepped || (!pool && !start_flag), "voxel_downsample_rows: pool / start need prepped");
   const KnnRowsWS kw = carve_knn_rows(knn_workspace, B, copies, N, target);
   EmitPlace place;
+  place.kw = &kw;
   place.rp = rows_place_args(kw, N, target);
   place.wflag = wait_flag;
   place.wvalue = wait_value;

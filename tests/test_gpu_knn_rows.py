@@ -206,11 +206,14 @@ def test_guided_loop_rows_layout_bit_identical(monkeypatch):
     assert torch.equal(outs[0], outs[2])
 
 
-@pytest.mark.parametrize("N,M,C", [(40000, 10000, 1), (120000, 30000, 1), (20000, 5000, 2)])
+@pytest.mark.parametrize("N,M,C", [(40000, 10000, 1), (120000, 30000, 1), (20000, 5000, 2),
+                                   (120000, 30000, 3)])
 def test_downsample_places_rows_refs(H, N, M, C):
     """Phase B inside the voxel emit (pcst_voxel_downsample_rows: the sampling step's layout)
     places the same refs as pcst_knn3_rows_refs on the downsample's indices: the rows query gives
-    the bits of the separate placement and of the compact layout on cat([x, x])."""
+    the bits of the separate placement and of the compact layout on cat([x, x]).  At 3 clouds of
+    120k the emit launch has more work-groups than CUs (708): it places nothing itself and phase B
+    runs as its own launch inside the same call ("Forward progress")."""
     rng = np.random.default_rng(N + C)
     x = dev(rng.standard_normal((C, N, 3)).astype(np.float32))
     coarse = dev(rng.standard_normal((2 * C, M, 3)).astype(np.float32))

@@ -423,3 +423,51 @@ def test_waiters_launched_before_their_producer_on_a_saturated_device():
     assert torch.equal(xi, xi_ref)
     assert torch.equal(out, ref_small)
     assert torch.equal(q, q_ref)
+
+
+def test_waiting_grids_larger_than_the_device_never_hold_every_cu():
+    """The waits of phase B at many clouds ("Forward progress"): the rows downsample of
+    16 clouds x 2 CFG rows (an emit launch of 3776 work-groups) is queued while its producer (phase A,
+    knn3_rows_build with refs_sig, behind a saturating noise MLP on another stream) has not run.
+    The emit then places nothing itself and phase B's own launch (at most max(CUs, rows) waiting
+    work-groups) waits instead, so phase A finds CUs: no timeout, and the refs and the query equal
+    the unsynchronised computation's.  (With the placement inside this emit, the 32-cloud step's
+    waits ran into their poll bound: r6z.)"""
+    from pointcloud_style_transfer_amd import _hip
+    from pointcloud_style_transfer_amd.config.config import Config
+    from pointcloud_style_transfer_amd.models.diffusion_model import NoisePredictor
+
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(13)
+    npred = NoisePredictor(Config(make_dirs=False, precision="bf16")).to(dev).eval()
+    rng = np.random.default_rng(13)
+    C, N, M = 16, 120000, 30000
+    x = torch.from_numpy(rng.standard_normal((C, N, 3)).astype(np.float32)).to(dev)
+    coarse = torch.randn(2 * C, M, 3, device=dev)
+    big = torch.randn(64 * 30000, 3, device=dev)
+    with torch.no_grad():
+        cbig = npred.cond(torch.full((64,), 900, device=dev), torch.randn(64, 256, device=dev))
+        blob, bias = npred.packed()[:2]
+        h_ref = _hip.knn3_rows_build(x, M, 2)
+        _, xi_ref = _hip.voxel_downsample(x, M, seed=4, copies=2)
+        _hip.knn3_rows_refs(h_ref, xi_ref)
+        q_ref = _hip.knn3_rows_query(coarse, h_ref)
+        h = _hip.knn3_rows_build(x, M, 2)
+        torch.cuda.synchronize()
+        prod = torch.cuda.Stream(device=dev)
+        cons = torch.cuda.Stream(device=dev)
+        s1 = _hip.DeviceSignal(dev)
+        for s in (prod, cons):
+            s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(prod):  # phase A behind a saturating kernel
+            _hip.noise_mlp(big, 30000, cbig, blob, bias, npred.precision_code)
+            _hip.knn3_rows_build(x, M, 2, ws=h.ws, refs_sig=s1)
+        with torch.cuda.stream(cons):  # the waiting placement, queued before phase A can run
+            _, xi = _hip.voxel_downsample(x, M, seed=4, copies=2, rows=h, rows_wait=s1)
+            cons.wait_stream(prod)
+            q = _hip.knn3_rows_query(coarse, h)
+        torch.cuda.synchronize()
+    assert not s1.timed_out()
+    assert h.placed
+    assert torch.equal(xi, xi_ref)
+    assert torch.equal(q, q_ref)

@@ -3,6 +3,7 @@
     import knobs; knobs.apply()
 
 reads PCST_KNN_OVERLAP=0|1, PCST_KNN_BUILD_LDS_FLOOR=<bytes>, PCST_ROWS_LAYOUT=0|1,
+PCST_ROWS_MAX_MLP_POINTS=<n>,
 PCST_VOXEL_PREP / _POOL_PREP=0|1, PCST_FUSED_BLOCK_FWD / _BWD=0|1 (models._autograd) and sets the
 matching module constants of models.diffusion_model.  Kernel-side variants are
 experiment builds (csrc/Makefile XDEF): PCST_LIB=<path> points _hip.LIB_PATH at one before the
@@ -32,6 +33,8 @@ def apply():
         dm.POOL_PREP = e["PCST_POOL_PREP"] != "0"
     if "PCST_ROWS_LAYOUT" in e:  # the step's kNN in the rows layout (0: the compact build)
         dm.ROWS_LAYOUT = e["PCST_ROWS_LAYOUT"] != "0"
+    if "PCST_ROWS_MAX_MLP_POINTS" in e:  # the rows layout up to this many MLP points per launch
+        dm.ROWS_MAX_MLP_POINTS = int(e["PCST_ROWS_MAX_MLP_POINTS"])
     if "PCST_FUSED_BLOCK_FWD" in e:
         from pointcloud_style_transfer_amd.models import _autograd
         _autograd.FUSED_BLOCK_FWD = e["PCST_FUSED_BLOCK_FWD"] != "0"
