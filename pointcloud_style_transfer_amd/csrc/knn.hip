@@ -639,6 +639,19 @@ struct Query {
   // key's lower end lies within sc (near-ties: ~1e-3 of the lanes) re-screen the window the
   // two-pass way.  The exact top-3 is order-independent and repeats are rejected, so the result
   // is the bit-identical one of the two-pass window.
+  // The keys are compared as unsigned integers: for the non-negative distances their bit patterns
+  // order as the floats do, and integer min / med3 need no NaN canonicalisation (the float forms
+  // cost the screen a v_max per key under IEEE mode); the key itself is one v_and_or_b32.
+  static __device__ __forceinline__ uint32_t slot_key(float d, uint32_t mask, uint32_t slot) {
+    uint32_t k;
+    asm("v_and_or_b32 %0, %1, %2, %3" : "=v"(k) : "v"(__float_as_uint(d)), "v"(mask), "s"(slot));
+    return k;
+  }
+  static __device__ __forceinline__ uint32_t med3u(uint32_t a, uint32_t b, uint32_t c) {
+    uint32_t r;
+    asm("v_med3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+  }
   static __device__ __forceinline__ float key_lo(float k) { return __uint_as_float(__float_as_uint(k) & ~511u); }
   static __device__ __forceinline__ float key_hi(float k) {
     return k == INFINITY ? INFINITY : __uint_as_float(__float_as_uint(k) | 511u);
@@ -646,14 +659,17 @@ struct Query {
   __device__ __forceinline__ void window(const Win& W, int fill, int kk) {
     const float ax = fx, ay = fy, az = fz;  // by value: keeps the query out of private memory
     const f2 qx = {ax, ax}, qy = {ay, ay}, qz = {az, az};
-    float k0 = INFINITY, k1 = INFINITY, k2 = INFINITY, k3 = INFINITY;
+    const uint32_t inf = __float_as_uint(INFINITY);
+    uint32_t u0 = inf, u1 = inf, u2 = inf, u3 = inf;
+    uint32_t hi_mask = ~511u;
+    asm volatile("" : "+v"(hi_mask));  // a VGPR operand of v_and_or_b32 (no literal in VOP3)
     auto put = [&](float d, int slot) {
-      const float key = __uint_as_float((__float_as_uint(d) & ~511u) | (unsigned)slot);
-      const float n0 = fminf(k0, key);
-      const float n1 = __builtin_amdgcn_fmed3f(k0, k1, key);
-      const float n2 = __builtin_amdgcn_fmed3f(k1, k2, key);
-      const float n3 = __builtin_amdgcn_fmed3f(k2, k3, key);
-      k0 = n0; k1 = n1; k2 = n2; k3 = n3;
+      const uint32_t key = slot_key(d, hi_mask, (uint32_t)slot);
+      const uint32_t n0 = min(u0, key);
+      const uint32_t n1 = med3u(u0, u1, key);
+      const uint32_t n2 = med3u(u1, u2, key);
+      const uint32_t n3 = med3u(u2, u3, key);
+      u0 = n0; u1 = n1; u2 = n2; u3 = n3;
     };
     int i = 0;
     for (; i + 4 <= fill; i += 4) {
@@ -665,6 +681,8 @@ struct Query {
       put(d23.y, i + 3);
     }
     for (; i < fill; ++i) put(dist1(W, i, ax, ay, az), i);
+    const float k0 = __uint_as_float(u0), k1 = __uint_as_float(u1), k2 = __uint_as_float(u2),
+                k3 = __uint_as_float(u3);
     const float ck = kk >= 3 ? k2 : (kk == 2 ? k1 : k0);
     const float sc = fminf(key_hi(ck) * 1.000002f + 1e-30f, thr);
     const bool again = k3 != INFINITY && key_lo(k3) <= sc;
