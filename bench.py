@@ -380,7 +380,7 @@ def train_leg(device, batch=8, points=120000, steps=5, warmup=2):
              "resblock_fwd16": lambda a, k: 4 * a[0].shape[0] * 256 * 512,   # x W1^T, h W2^T
              "linear_wgrad_ex": lambda a, k: 2 * a[0].shape[0] * a[0].shape[1] * a[1].shape[1]}
     kernels = {"resblock_bwd16": "resblock_kernel<true, true> (pcst_resblock_bwd16)",
-               "resblock_fwd16": "resblock2_kernel (pcst_resblock_fwd16)",
+               "resblock_fwd16": "resblock3_kernel (pcst_resblock_fwd16)",
                "linear_wgrad_ex": "wgrad_ex_kernel + combine (pcst_linear_wgrad_ex)"}
     rec = {k: [] for k in flops}
     orig = {k: getattr(_hip, k) for k in flops}

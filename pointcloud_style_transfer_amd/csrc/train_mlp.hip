@@ -1844,6 +1844,210 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   }
 }
 
+// The forward on two waves per SIMD (round 6): resblock2_kernel's dataflow -- h^T = W1 x^T and
+// x'^T = W2 h^T per 32-unit hidden chunk, the chunk's accumulators relaid into the second
+// product's operand in registers, the weights streamed per chunk into a 3-slab LDS ring by
+// LDS-DMA, one barrier per chunk -- with 8 waves of 32 rows instead of 4 of 64.  A wave's
+// accumulators are then 128 registers instead of 256, so two waves share each SIMD and one wave's
+// chunk epilogue (ReLU, the h and mask-bit stores, the relayout) and its waits on fragment reads
+// run in the other's MFMA shadow, where one wave per SIMD left the MFMA pipe idle (resblock2:
+// 192 us per launch with the stores, refills and draws all removed, against a 52 us MFMA floor).
+// Every fragment read feeds one MFMA instead of two (twice resblock2's LDS reads: 256 KiB per
+// chunk and CU).  Each output's products and their order are resblock2's: the same bits.
+constexpr int kR3Threads = 512;               // 8 waves x 32 rows = a 256-row tile (kR2Rows)
+constexpr int kR3Keep = 8 * kR3Threads * 4;   // dropout keep bits: [8 output blocks][512 threads]
+constexpr int kR3Lds = kR2Slabs * kR2Slab + (512 + 256) * 4 + kR3Keep;
+
+__global__ __launch_bounds__(kR3Threads) __attribute__((amdgpu_waves_per_eu(2, 2))) void resblock3_kernel(
+    RbArgs a, int ntiles) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float* sb1 = reinterpret_cast<float*>(smem + kR2Slabs * kR2Slab);  // [512]
+  float* sb2 = sb1 + 512;                                             // [256]
+  uint32_t* skeep = reinterpret_cast<uint32_t*>(sb2 + 256);           // [8][512]
+  int t = blockIdx.x;
+  if (t >= ntiles) return;
+  const int G = gridDim.x;
+  const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, l32 = lane & 31;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int64_t M = a.M;
+  sb1[tid] = a.b1[tid];
+  if (tid < 256) sb2[tid] = a.b2[tid];
+  // chunk c's fragments -> slab: f < 16: W1 rows [32c, +32) k [16f, +16); f = 16 + 2 ob + kk:
+  // W2 rows [32 ob, +32) k [32c + 16kk, +16).  Waves 0-3 load the W1 half (4 fragments each),
+  // waves 4-7 the W2 half.
+  const bool w1half = wid < 4;
+  const rsrc_t rw1 = make_rsrc(a.w1, 512u * 256u * 2u), rw2 = make_rsrc(a.w2, 256u * 512u * 2u);
+  const uint32_t vw = w1half ? (uint32_t)((l32 * 256 + 8 * h) * 2) : (uint32_t)((l32 * 512 + 8 * h) * 2);
+  const rsrc_t rwv = w1half ? rw1 : rw2;
+  const uint32_t lds_slab0 = (uint32_t)(uintptr_t)smem + (w1half ? 4 * wid : 16 + 4 * (wid - 4)) * 1024;
+  auto fill = [&](int c, int slab) {
+    const uint32_t dst = lds_slab0 + slab * kR2Slab;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int j = 4 * (w1half ? wid : wid - 4) + i;
+      const int so = w1half ? (32 * c * 256 + 16 * j) * 2 : (32 * (j >> 1) * 512 + 32 * c + 16 * (j & 1)) * 2;
+      r2_dma16(rwv, vw, __builtin_amdgcn_readfirstlane(so), __builtin_amdgcn_readfirstlane(dst + i * 1024));
+    }
+  };
+  fill(0, 0);
+  fill(1, 1);
+  // the A rows in operand layout: xb[kb] = row r0, k [16kb + 8h, +8)
+  const rsrc_t rx = make_rsrc(a.x, (uint32_t)(M * 256 * 2));
+  int64_t r0 = (int64_t)t * kR2Rows + 32 * wid + l32;
+  uint32_t v256 = (uint32_t)((r0 * 256 + 8 * h) * 2);
+  uint32_t v512 = (uint32_t)((r0 * 512 + 8 * h) * 2);
+  uint32_t vrow16 = (uint32_t)(r0 * 64);
+  const uint32_t vstep256 = (uint32_t)G * kR2Rows * 256 * 2, vstep512 = (uint32_t)G * kR2Rows * 512 * 2;
+  u32x4 xb[16];
+#pragma unroll
+  for (int kb = 0; kb < 16; ++kb) xb[kb] = as_u32x4(bload16(rx, v256 + kb * 32, 0));
+  const rsrc_t rh = make_rsrc(a.h, (uint32_t)(M * 512 * 2));
+  const rsrc_t rhb = make_rsrc(a.hbo, a.hbo ? (uint32_t)(M * 16 * 4) : 0u);
+  const rsrc_t ro = make_rsrc(a.xo, (uint32_t)(M * 256 * 2));
+  const uint32_t lds0 = (uint32_t)(uintptr_t)smem + lane * 16;
+  const uint32_t lb1 = (uint32_t)(uintptr_t)sb1 + 16 * h;
+  const uint32_t lb2 = (uint32_t)(uintptr_t)sb2 + 16 * h;
+  const uint32_t lkeep = (uint32_t)(uintptr_t)skeep + 4 * tid;  // + 4 * 512 ob bytes
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();  // slabs 0, 1 and the biases landed
+  int slab0 = 0, slab2 = 2;
+#pragma unroll 1
+  for (;;) {
+    const bool more = __builtin_amdgcn_readfirstlane(t + G < ntiles ? 1 : 0) != 0;
+    f32x16 acc2[8];
+#pragma unroll
+    for (int ob = 0; ob < 8; ++ob) acc2[ob] = f32x16{};
+    uint32_t keep2 = 0;
+#pragma unroll 1
+    for (int c = 0; c < 16; ++c) {
+      const uint32_t a0 = lds0 + slab0 * kR2Slab;
+      const bool fill2 = c + 2 < 16 || more;
+      if (fill2) fill((c + 2) & 15, slab2);
+      h16x8 fr[4];
+      fr[0] = dma_read<0>(a0);
+      fr[1] = dma_read<1024>(a0);
+      fr[2] = dma_read<2048>(a0);
+      fr[3] = dma_read<3072>(a0);
+      f32x16 acc1 = f32x16{};
+      f32x4 bq[4];
+      u32x4 hb[2];
+      const uint32_t e0 = (uint32_t)(r0 * 256 + 32 * (c >> 1) + 4 * h);
+      if (!(c & 1)) keep2 = 0;
+      auto frag_step = [&](const int f) __attribute__((always_inline)) {
+        const int younger = (31 - f < 3 ? 31 - f : 3) + (f >= 12 && f < 16 ? 4 : 0);
+        if (younger == 7) r2_wait1<7>(fr[f & 3]);
+        else if (younger == 3) r2_wait1<3>(fr[f & 3]);
+        else if (younger == 2) r2_wait1<2>(fr[f & 3]);
+        else if (younger == 1) r2_wait1<1>(fr[f & 3]);
+        else r2_wait1<0>(fr[f & 3]);
+        if (f < 16) {
+          acc1 = mfma32_h16(fr[f & 3], as_h16x8(xb[f]), acc1);
+        } else {
+          const int ob = (f - 16) >> 1, kk = f & 1;
+          acc2[ob] = mfma32_h16(fr[f & 3], as_h16x8(hb[kk]), acc2[ob]);
+          // the final epilogue's dropout draws, in the MFMA shadow: output block c / 2, element
+          // r = 8 (c & 1) + (f - 16) / 2 at every second fragment (bit r of the block's word)
+          if (!(f & 1)) {
+            const int r = 8 * (c & 1) + ((f - 16) >> 1);
+            keep2 |= (uint32_t)(drop_hash(a.seed_lo, a.seed_hi, (uint64_t)(e0 + (r & 3) + 8 * (r >> 2))) >= a.thr)
+                     << r;
+          }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        if (f + 4 < 32) fr[f & 3] = r2_read_one(a0, (f + 4) * 1024);
+        if (f == 11) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) bq[q] = r2_read_f4(lb1 + 4 * (32 * c + 8 * q));
+        }
+      };
+#pragma unroll
+      for (int f = 0; f < 16; ++f) frag_step(f);
+      // chunk epilogue: h = 16-bit(relu(acc1 + b1)), to the second product's operand layout and
+      // out to global (16 B per lane), and the chunk's ReLU mask word of the row
+      asm volatile("s_waitcnt lgkmcnt(4)" : "+v"(bq[0]), "+v"(bq[1]), "+v"(bq[2]), "+v"(bq[3]));
+      {
+        float v[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) v[r] = fmaxf(acc1[r] + bq[r >> 2][r & 3], 0.0f);
+        uint32_t mb = 0;
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) {
+          const u32x4 o = {pack16(v[8 * kk + 0], v[8 * kk + 1]), pack16(v[8 * kk + 2], v[8 * kk + 3]),
+                           pack16(v[8 * kk + 4], v[8 * kk + 5]), pack16(v[8 * kk + 6], v[8 * kk + 7])};
+#pragma unroll
+          for (int d = 0; d < 4; ++d) {
+#pragma unroll
+            for (int s2 = 0; s2 < 2; ++s2) {
+              const uint32_t half16 = (o[d] >> (16 * s2)) & 0xffffu;
+              const int bit = ((2 * d + s2) & 3) + 16 * kk + 8 * (d >> 1);
+              mb |= (half16 - 1u < 0x7fffu ? 1u : 0u) << bit;  // 1 .. 0x7fff: positive
+            }
+          }
+          hb[kk] = relayout(o);
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i32, hb[kk]), rh, (int)(v512 + kk * 32),
+                                                 64 * c, 0);
+        }
+        mb <<= 4 * h;  // lane half h holds units + 4h; the halves' bits are disjoint
+        uint32_t lo = mb, hi = mb;
+        swap_halves(lo, hi);
+        const uint32_t word = mb | (h ? lo : hi);
+        __builtin_amdgcn_raw_buffer_store_b32(word, rhb, (int)(h ? 0x7ffffff0u : vrow16), 4 * c, 0);
+      }
+#pragma unroll
+      for (int f = 16; f < 32; ++f) frag_step(f);
+      if (c & 1) r2_write_u32(lkeep + 4 * kR3Threads * (c >> 1), keep2);
+      // this wave's DMA of the next chunk (issued a chunk ago) landed; the chunk-after-next DMA
+      // (4), this chunk's h stores (2) and its mask word (1) may still be in flight
+      if (fill2) asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+      __syncthreads();  // every wave's DMA of the next chunk landed; every wave is done with slab0
+      slab0 = slab0 == kR2Slabs - 1 ? 0 : slab0 + 1;
+      slab2 = slab2 == kR2Slabs - 1 ? 0 : slab2 + 1;
+    }
+    // final epilogue: x' = 16-bit(x + Dropout(acc2 + b2)), 16 B stores in operand layout
+#pragma unroll
+    for (int ob = 0; ob < 8; ++ob) {
+      uint32_t lb2o = lb2, lko = lkeep;
+      asm volatile("" : "+v"(lb2o), "+v"(lko));
+      f32x4 bq[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) bq[q] = r2_read_f4(lb2o + 4 * (32 * ob + 8 * q));
+      uint32_t kw = r2_read_u32(lko + 4 * kR3Threads * ob);
+      asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(bq[0]), "+v"(bq[1]), "+v"(bq[2]), "+v"(bq[3]), "+v"(kw));
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        __builtin_amdgcn_sched_barrier(0);
+        const u32x4 res = relayout(xb[2 * ob + kk]);  // x in the accumulator layout
+        uint32_t o[4];
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {
+          float y2[2];
+#pragma unroll
+          for (int s2 = 0; s2 < 2; ++s2) {
+            const int r = 8 * kk + 2 * d + s2;
+            float y = acc2[ob][r] + bq[r >> 2][r & 3];
+            y = (kw >> r) & 1u ? y * a.scale : 0.0f;
+            y += h16_to_f32((res[d] >> (16 * s2)) & 0xffffu);
+            y2[s2] = y;
+          }
+          o[d] = pack16(y2[0], y2[1]);
+        }
+        const u32x4 on = relayout(u32x4{o[0], o[1], o[2], o[3]});
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i32, on), ro, (int)(v256 + ob * 64 + kk * 32),
+                                               0, 0);
+      }
+    }
+    if (!more) break;
+#pragma unroll
+    for (int kb = 0; kb < 16; ++kb) xb[kb] = as_u32x4(bload16(rx, v256 + vstep256 + kb * 32, 0));
+    t += G;
+    r0 += (int64_t)G * kR2Rows;
+    v256 += vstep256;
+    v512 += vstep512;
+    vrow16 += (uint32_t)G * kR2Rows * 64;
+  }
+}
+
 // ---- batched weight casts: every 2-D weight of a step to the 16-bit format (optionally
 // transposed) in one launch, instead of one cast (and, transposed, one more copy) per tensor
 struct CastBatch {
@@ -1915,8 +2119,15 @@ int resblock_fwd_impl(const uint16_t* x, int64_t M, const uint16_t* w1, const fl
   a.hm = nullptr; a.g = nullptr; a.ddo = nullptr;
   a.hbo = hbits; a.hbi = nullptr;
   const int ntiles = (int)cdiv(M, kR2Rows);
-  hipLaunchKernelGGL(resblock2_kernel<false>, dim3((unsigned)std::min(ntiles, r2_grid())), dim3(256),
-                     kR2Lds, as_stream(stream), a, ntiles);
+#ifndef PCST_RB_FWD_V2  // experiment builds: 1 = the one-wave-per-SIMD forward (resblock2_kernel)
+#define PCST_RB_FWD_V2 0
+#endif
+  if (PCST_RB_FWD_V2)
+    hipLaunchKernelGGL(resblock2_kernel<false>, dim3((unsigned)std::min(ntiles, r2_grid())), dim3(256),
+                       kR2Lds, as_stream(stream), a, ntiles);
+  else
+    hipLaunchKernelGGL(resblock3_kernel, dim3((unsigned)std::min(ntiles, r2_grid())), dim3(kR3Threads),
+                       kR3Lds, as_stream(stream), a, ntiles);
   PCST_LAUNCH_CHECK("resblock_fwd");
   return PCST_OK;
 }

@@ -89,7 +89,7 @@ for st in "$@"; do
           SQ_LDS_BANK_CONFLICT SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_ANY --output-format csv -d "$OUT/psq2" -o pmc -- \
           python $TB > "$OUT/psq2.log" 2>&1
       rc=$?; echo "trainpmc2 rc=$rc"; if [ $rc -ne 0 ]; then tail -5 "$OUT/psq2.log"; exit $rc; fi
-      for k in "resblock_kernel<false" "resblock_kernel<true" "wgrad_ex_kernel<unsigned short, unsigned short"; do
+      for k in "resblock3_kernel" "resblock_kernel<true" "wgrad_ex_kernel<unsigned short, unsigned short"; do
         echo "== $k"; python tools/pmc_sq.py "$OUT" "$k" psq2
       done | tee "$OUT/train_sq2.txt" ;;
     trainab=*)
