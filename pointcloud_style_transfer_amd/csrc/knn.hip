@@ -82,7 +82,7 @@ struct KnnWS {
   // zeroed every call (contiguous):
   int32_t* err;
   int32_t* qctr;     // [B][8][kCtrStride] the query's work counters (chunk scheduling), one per line
-  int32_t* nchunk;   // [B]
+  int32_t* nchunk;   // [nchunk_stride(B)] chunks, then [B] u64 wide (list front) << 32 | narrow (back)
   int32_t* ocount;   // [B]
   uint32_t* known;   // [B][N]  (j+1 of the last coarse row writing n, 0 = query)
   uint64_t* tsum;    // [B][T]  per-tile sums of the packed counts
@@ -108,7 +108,7 @@ static KnnWS carve_knn(void* base, int64_t B, int64_t N, int64_t M) {
   w.obound = c.take<float>(B * N);
   w.err = c.take<int32_t>(4);
   w.qctr = c.take<int32_t>(B * kQueryShards * kCtrStride);
-  w.nchunk = c.take<int32_t>(B);
+  w.nchunk = c.take<int32_t>(3 * nchunk_stride(B));
   w.ocount = c.take<int32_t>(B);
   w.known = c.take<uint32_t>(B * N);
   w.tsum = c.take<uint64_t>(B * w.T);
@@ -328,7 +328,7 @@ __device__ __forceinline__ uint64_t block_excl_scan_256_u64(uint64_t v, unsigned
 // tiles' sums: at most kKnnMaxTiles words, read by the whole block), then the tile's 64
 // bricks are cut into chunks of <= 64 queries (by octant, below) appended to the cloud's chunk
 // list (order free: chunks are independent).
-__global__ __launch_bounds__(256) void knn_scan_kernel(uint64_t* __restrict__ cnt,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void knn_scan_kernel(uint64_t* __restrict__ cnt,
                                                        const uint64_t* __restrict__ tsum,
                                                        int64_t T, int64_t Cpad,
                                                        uint2* __restrict__ chunks, int64_t maxch,
@@ -376,40 +376,67 @@ __global__ __launch_bounds__(256) void knn_scan_kernel(uint64_t* __restrict__ cn
 #pragma unroll
       for (int o = 0; o < 8; ++o) qo[o] = (uint32_t)(buf[pad(t * 64 + 8 * o)] >> 32);
       qo[8] = (uint32_t)((t < 63 ? buf[pad(t * 64 + 64)] : base + tot) >> 32);
-      // walk the octants; emit(a, b) is called for every chunk [a, b) in order
+      // walk the octants; emit(a, b, wide) is called for every chunk [a, b) in order, wide for a
+      // run of two or more occupied octants (a sparse region: the query stages two rings and runs
+      // its ball pass for almost every such chunk -- the long chunks)
       auto walk = [&](auto&& emit) {
         uint32_t cs = qo[0];  // start of the open run of octants
+        int ro = 0;           // occupied octants in the run
 #pragma unroll
         for (int o = 0; o < 8; ++o) {
           const uint32_t a = qo[o], n = qo[o + 1] - a;
           if (n > 64) {
-            if (a > cs) emit(cs, a);
+            if (a > cs) emit(cs, a, ro > 1);
             const uint32_t k = (n + 63) / 64;
-            for (uint32_t i = 0; i < k; ++i) emit(a + (uint32_t)((uint64_t)n * i / k), a + (uint32_t)((uint64_t)n * (i + 1) / k));
+            for (uint32_t i = 0; i < k; ++i)
+              emit(a + (uint32_t)((uint64_t)n * i / k), a + (uint32_t)((uint64_t)n * (i + 1) / k), false);
             cs = a + n;
+            ro = 0;
           } else if (a + n - cs > 64) {
-            emit(cs, a);
+            emit(cs, a, ro > 1);
             cs = a;
+            ro = n > 0 ? 1 : 0;
+          } else {
+            ro += n > 0 ? 1 : 0;
           }
         }
-        if (qo[8] > cs) emit(cs, qo[8]);
+        if (qo[8] > cs) emit(cs, qo[8], ro > 1);
       };
-      uint32_t nch = 0;
-      walk([&](uint32_t, uint32_t) { ++nch; });
-      uint32_t off = nch;
+      // the cloud's list holds the wide chunks from the front and the others from the back, so
+      // the query's waves take the long chunks first (their first, static chunks) and the
+      // second round is short ones
+      uint32_t nw = 0, nn = 0;
+      walk([&](uint32_t, uint32_t, bool wide) {  // (branch-free: a selected ++ put both in scratch)
+        nw += wide ? 1u : 0u;
+        nn += wide ? 0u : 1u;
+      });
+      uint32_t offw = nw, offn = nn;
 #pragma unroll
       for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t y = __shfl_up(off, o);
-        if (t >= o) off += y;
+        const uint32_t yw = __shfl_up(offw, o), yn = __shfl_up(offn, o);
+        if (t >= o) {
+          offw += yw;
+          offn += yn;
+        }
       }
-      const uint32_t all = __shfl(off, 63);
-      off -= nch;
-      uint32_t at = 0;
-      if (t == 0 && all) at = (uint32_t)atomicAdd(&nchunk[b], (int32_t)all);
-      at = __shfl(at, 0);
-      uint2* Ch = chunks + b * maxch + at + off;
-      uint32_t i = 0;
-      walk([&](uint32_t a, uint32_t e) { Ch[i++] = make_uint2(a, e); });
+      const uint32_t allw = __shfl(offw, 63), alln = __shfl(offn, 63);
+      offw -= nw;
+      offn -= nn;
+      uint32_t atw = 0, atn = 0;
+      if (t == 0 && allw + alln) {  // both lists' bases from one returning atomic (wide << 32 | narrow)
+        unsigned long long* packed = reinterpret_cast<unsigned long long*>(nchunk + nchunk_stride(gridDim.y));
+        const unsigned long long old = atomicAdd(packed + b, ((unsigned long long)allw << 32) | alln);
+        atw = (uint32_t)(old >> 32);
+        atn = (uint32_t)old;
+        __hip_atomic_fetch_add(&nchunk[b], (int32_t)(allw + alln), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      atw = __shfl(atw, 0) + offw;
+      atn = __shfl(atn, 0) + offn;
+      uint2* Ch = chunks + b * maxch;
+      walk([&](uint32_t a, uint32_t e, bool wide) {
+        if (wide) Ch[atw++] = make_uint2(a, e);
+        else Ch[maxch - 1 - (atn++)] = make_uint2(a, e);
+      });
     }
   }  // tile
 }
@@ -999,7 +1026,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
   };
   const Win W = {cand[wv][0], cand[wv][1], cand[wv][2], reinterpret_cast<int*>(cand[wv][3])};
   const Box none = {1, 0, 1, 0, 1, 0};
-  const int nch = nchunk[cl];
+  const int nch = nchunk[cl];  // the scan kernel's counts: total, and the wide list's length
+  const int nwide = (int)(reinterpret_cast<const uint64_t*>(nchunk + nchunk_stride(ka.C))[cl] >> 32);
   // the row's overflow refs (rows layout; a few dozen in the bench), staged once per work-group
   // with their cell coordinates: a pass offers a query only those inside the box it scanned (the
   // settled test covers every ref outside it, as for the cell-placed refs)
@@ -1068,7 +1096,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
     tr0 = (uint32_t)__builtin_amdgcn_s_memrealtime();
     tr_open1 = tr_p2 = 0;
 #endif
-    const uint2 ch = chunks[cl * maxch + item];
+    const uint2 ch = chunks[cl * maxch + (item < nwide ? item : maxch - 1 - (item - nwide))];
     if (ch.x > ch.y || ch.y > (uint32_t)N || ch.y - ch.x > 64u) {  // wave-uniform
       if (lane == 0) atomicOr(ka.err, 4);
       item = take();
@@ -1317,6 +1345,12 @@ __global__ __launch_bounds__(256) void knn_outlier_brick_kernel(
   const uint32_t rlim = (uint32_t)(ROWS ? N : M);
   const double bs = 4.0 * (double)g.s;  // brick edge
   for (int q = blockIdx.x * 4 + wv; q < cnt; q += gridDim.x * 4) {
+#ifdef PCST_KNN_OUTLIER_TRACE  // experiment builds only: per outlier query (start, end, shells |
+    // initial bound infinite << 15 | final radius << 16, staged refs) in 10 ns ticks, in the row's
+    // obound array past 80000
+    const uint32_t tr0 = (uint32_t)__builtin_amdgcn_s_memrealtime();
+    uint32_t tr_shells = 0, tr_staged = 0;
+#endif
     const int64_t n = olist[b * N + q];
     const float* qp = orig + (cl * N + n) * 3;
     Query me;
@@ -1330,6 +1364,9 @@ __global__ __launch_bounds__(256) void knn_outlier_brick_kernel(
     // kk-th distance: the refs behind it lie inside it and are found again), then the merged
     // kk-th best of this search
     double best = (double)obound[b * N + q];
+#ifdef PCST_KNN_OUTLIER_TRACE
+    const uint32_t tr_inf = best == INFINITY ? 1u : 0u;
+#endif
     int r = 1;
     if (best != INFINITY) r = max(1, (int)fmin(floor(sqrt(best) * (1.0 + 1e-6) / bs) + 1.0, 4096.0));
     for (;;) {
@@ -1372,6 +1409,10 @@ __global__ __launch_bounds__(256) void knn_outlier_brick_kernel(
       };
       uint32_t staged = 0;
       scan_units_1q(vol, unit, R, me, kk, staged);
+#ifdef PCST_KNN_OUTLIER_TRACE
+      ++tr_shells;
+      tr_staged += staged;
+#endif
       // merge the lanes' lists into lane 0; the others restart empty with the merged screen
       Top3 t = me.t;
       wave_merge_top3(t);
@@ -1400,6 +1441,12 @@ __global__ __launch_bounds__(256) void knn_outlier_brick_kernel(
       }
     }
     if (lane == 0) idw_write(me.t, kk, V, out + (b * N + n) * 3);
+#ifdef PCST_KNN_OUTLIER_TRACE
+    if (lane == 0 && q < 8192)
+      reinterpret_cast<uint4*>(const_cast<float*>(obound) + b * N + 80000)[q] =
+          make_uint4(tr0, (uint32_t)__builtin_amdgcn_s_memrealtime(),
+                     min(tr_shells, 32767u) | (tr_inf << 15) | ((uint32_t)min(r, 65535) << 16), tr_staged);
+#endif
   }
 }
 

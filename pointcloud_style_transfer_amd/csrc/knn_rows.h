@@ -21,6 +21,10 @@ static inline int device_cus() {
   return n;
 }
 
+// the chunk counters: [stride] totals per cloud, then per cloud one u64 (wide list length << 32 |
+// narrow list length) on lines of their own (the scan reserves both lists with one atomic)
+__host__ __device__ inline int64_t nchunk_stride(int64_t C) { return (C + 63) & ~(int64_t)63; }
+
 static int64_t knn_cells(int64_t M) {
   return std::min<int64_t>(std::max<int64_t>(4096, 16 * M), (int64_t)kKnnMaxTiles * kKnnTile - 1);
 }
@@ -40,7 +44,7 @@ struct KnnRowsWS {
   // zeroed every build (contiguous):
   int32_t* err;
   int32_t* qctr;     // [B][2][8][kCtrStride] the query's work counters (chunks, brick batches)
-  int32_t* nchunk;   // [C]
+  int32_t* nchunk;   // [nchunk_stride(C)] chunks, then [C] u64 wide (list front) << 32 | narrow (back)
   int32_t* ocount;   // [B]
   int32_t* ovn;      // [B] overflow refs
   uint32_t* known;   // [B][N] j+1 of the last ref naming the row at cell-order position p, 0 = a query
@@ -73,7 +77,7 @@ static KnnRowsWS carve_knn_rows(void* base, int64_t C, int64_t copies, int64_t N
   w.obound = c.take<float>(w.B * N);
   w.err = c.take<int32_t>(4);
   w.qctr = c.take<int32_t>(w.B * 2 * kQueryShards * kCtrStride);
-  w.nchunk = c.take<int32_t>(C);
+  w.nchunk = c.take<int32_t>(3 * nchunk_stride(C));
   w.ocount = c.take<int32_t>(w.B);
   w.ovn = c.take<int32_t>(w.B);
   w.known = c.take<uint32_t>(w.B * N);

@@ -453,7 +453,7 @@ def _knn_carve(B, N, M):
     for name, nbytes in (("stats", B * 64 * 72), ("gp", B * 8 * 4), ("refs", B * M * 16),
                          ("qorder", B * N * 4), ("crank", B * (M + N) * 8),
                          ("chunks", B * maxch * 8), ("olist", B * N * 4), ("obound", B * N * 4),
-                         ("err", 16), ("qctr", B * 8 * 64 * 4), ("nchunk", B * 4), ("ocount", B * 4),
+                         ("err", 16), ("qctr", B * 8 * 64 * 4), ("nchunk", 3 * ((B + 63) // 64 * 64) * 4), ("ocount", B * 4),
                          ("known", B * N * 4), ("tsum", B * T * 8), ("cnt", B * Cpad * 8)):
         take(name, nbytes)
     return o, maxch, Cpad, (off + 255) & ~255
