@@ -39,7 +39,9 @@
 // over eight counters (work-group m of a row takes from counter m % 8, i.e. all its users sit on
 // one XCD under round-robin placement), so a wave that finishes early takes the next chunk
 // instead of idling and no counter sees more than an eighth of the dequeues (one word saturates
-// at ~88 dequeues per us: MI355X_MICROARCH.md, dequeue).  The counters live in the build's zeroed
+// at ~88 dequeues per us: MI355X_MICROARCH.md, dequeue).  The scan lists the wide chunks (runs of
+// two or more occupied octants: the long ones) first, so the static first chunks are the long
+// ones and the counters hand out the short ones.  The counters live in the build's zeroed
 // state; the outlier launch zeroes them again for the next query on the same workspace.
 //
 // Launches: memset, pre (cloud stats + known rows), count (grid params, per-cell counts with
