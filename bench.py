@@ -562,6 +562,7 @@ def main():
             conds = all_conds()  # the loop's one-time conditioning launch, inside the timed region
             for i in range(args.steps):
                 step(i, i % max(1, args.event_every) == 0)
+        host_elapsed = time.perf_counter() - t0  # the host's enqueue time (the GPU may still run)
         torch.cuda.synchronize()
         elapsed = time.perf_counter() - t0
         if overlap:
@@ -638,6 +639,9 @@ def main():
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            # the host's enqueue time of the timed steps (a diagnostic: below ms_per_step, the
+            # host runs ahead of the device)
+            "host_enqueue_ms_per_step": round(host_elapsed / args.steps * 1e3, 4),
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,

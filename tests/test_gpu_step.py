@@ -498,6 +498,37 @@ def test_knn_query_corrupt_workspace_sets_error_bits(H):
     assert e & 4 and e & 8, e
 
 
+@pytest.mark.parametrize("kind", ["gauss", "outliers", "repeat"])
+def test_knn_chunk_lists_tile_the_queries_long_chunks_first(H, kind):
+    """The scan kernel's chunk lists (white-box, knn.hip knn_scan_kernel): per cloud the wide
+    chunks (runs of two or more occupied octants) from the front of the array and the others from
+    the back, their lengths in one packed word (wide << 32 | narrow) and the total beside; together
+    the ranges tile the cloud's query positions [0, queries) exactly once, each 1..64 rows long."""
+    rng = np.random.default_rng(7 + len(kind))
+    orig, idx = _knn_case(kind, rng)
+    B, N, _ = orig.shape
+    M = idx.shape[1]
+    o, maxch, Cpad, total = _knn_carve(B, N, M)
+    h = H.knn3_build(orig, idx)
+    ws = h[2]
+    torch.cuda.synchronize()
+    stride = (B + 63) // 64 * 64
+    nch = ws[o["nchunk"]:o["nchunk"] + B * 4].view(torch.int32).cpu().numpy()
+    packed = ws[o["nchunk"] + stride * 4:o["nchunk"] + stride * 4 + B * 8].view(torch.int64).cpu().numpy()
+    ch = ws[o["chunks"]:o["chunks"] + B * maxch * 8].view(torch.int32).view(B, maxch, 2).cpu().numpy()
+    for b in range(B):
+        nw, nn = int(packed[b]) >> 32, int(packed[b]) & 0xFFFFFFFF
+        assert nw + nn == nch[b] and nn > 0, (nw, nn, nch[b])
+        rows = np.concatenate([ch[b, :nw], ch[b, maxch - nn:]])
+        lens = rows[:, 1] - rows[:, 0]
+        assert lens.min() >= 1 and lens.max() <= 64
+        order = np.argsort(rows[:, 0])
+        starts, ends = rows[order, 0], rows[order, 1]
+        queries = N - len(np.unique(idx[b].cpu().numpy()))
+        assert starts[0] == 0 and ends[-1] == queries
+        assert np.array_equal(starts[1:], ends[:-1])  # contiguous, no overlap, no gap
+
+
 @pytest.mark.parametrize("max_wg,floor", [(1, 0), (2, 8192), (32, 8192), (7, 0)])
 def test_knn_build_workgroup_cap_is_exact(H, max_wg, floor):
     """pcst_knn3_build's max_wg only changes how many work-groups stride over the build's work
