@@ -282,6 +282,15 @@ _OVERLAP_MAX_MLP_POINTS = 2 * 128 * 256
 # than the smallest such floor (8 KiB): 2718 / 2722 / 2733 / 2706 vs 2685 / 2709 / 2717 / 2693
 # steps/s in four alternating pairs over two boxes (profiles/r04/a56, a57).
 KNN_BUILD_LDS_FLOOR = 16384
+# Work-groups per launch of the compact build beside the MLP (pcst_knn3_build's max_wg; 0: the
+# natural grids).  Beside a many-round MLP (32 clouds: 7500 work-groups) every build work-group
+# that takes a slot as MLP work-groups retire holds it through its memory waits; 256 work-groups
+# that each stride over more of the build take fewer slots: 32-cloud step 7.17-7.28 vs 7.38-7.53 ms
+# (four pairs, profiles/r06/r6mw, r6mw2).  tools/knobs.py overrides it for A/B runs.
+KNN_BUILD_MAX_WG = 256
+# The hipGraph step (guided_sample_loop(graph=True)): the compact kNN build on a forked branch of
+# the captured graph beside the MLP, capped as above, instead of inline before it.
+GRAPH_FORK_BUILD = True
 
 
 def overlap_knn_build(mlp_points: int) -> bool:
@@ -436,7 +445,8 @@ def hierarchical_eps(hp, mlp, xc, xi, x_cat, knn_ws=None, state=None, fused=Fals
         ready.signal(main)
     ready.wait(state.side)
     with torch.cuda.stream(state.side):
-        handle = _hip.knn3_build(x_cat, xi, knn_ws, knn_build_lds_floor(xc.shape[0] * xc.shape[1]))
+        handle = _hip.knn3_build(x_cat, xi, knn_ws, knn_build_lds_floor(xc.shape[0] * xc.shape[1]),
+                                 KNN_BUILD_MAX_WG)
         built.signal(state.side)
     nc = mlp(xc, start=start) if fused else mlp(xc)
     built.wait(main)
@@ -719,17 +729,30 @@ class DiffusionProcess:
         npred.packed()  # weight packing happens outside the capture
         M = model.config.global_points
 
-        # single stream: the kNN build on a forked graph branch beside the MLP measured slower at
-        # 32 clouds, with and without a per-replay MLP start flag gating the branch (7.65-7.86 vs
-        # 7.38-7.50 ms per step, profiles/r05/s2o, s2p)
+        # the kNN build on a forked graph branch beside the MLP (GRAPH_FORK_BUILD; uncapped it
+        # measured slower than inline at 32 clouds: 7.65-7.86 vs 7.38-7.50 ms per step,
+        # profiles/r05/s2o, s2p)
+        capture = torch.cuda.Stream(device=device)
+        branch = torch.cuda.Stream(device=device)
+        knn_ws = _hip.knn_workspace(2 * B, x_cat.shape[1], M, device)
+
         def step():
             xc, xi = _hip.voxel_downsample_copies_dseed(x, M, seed_cur, 2)
-            eps = hp.upsample_knn(npred(xc, t_cur, style_in), x_cat, xi)
+            if GRAPH_FORK_BUILD:
+                # the build (positions only) on a graph branch beside the MLP, joined before the query
+                branch.wait_stream(capture)
+                with torch.cuda.stream(branch):
+                    handle = _hip.knn3_build(x_cat, xi, knn_ws, knn_build_lds_floor(xc.shape[0] * xc.shape[1]),
+                                             KNN_BUILD_MAX_WG)
+                nc = npred(xc, t_cur, style_in)
+                capture.wait_stream(branch)
+                eps = _hip.knn3_query(nc, handle)
+            else:
+                eps = hp.upsample_knn(npred(xc, t_cur, style_in), x_cat, xi)
             _hip.cfg_ddim_step_dcoef(x, eps[:B], eps[B:], source, guidance_scale, coef_cur,
                                      x_cat=x_cat, out=x)
 
         g = torch.cuda.CUDAGraph()
-        capture = torch.cuda.Stream(device=device)
         capture.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(capture):
             with torch.cuda.graph(g, stream=capture):

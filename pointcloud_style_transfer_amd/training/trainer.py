@@ -39,6 +39,7 @@ import torch.distributed as dist
 import torch.optim as optim
 from torch.amp import GradScaler, autocast
 
+from .. import _hip
 from .. import rng as _rng
 from ..config.config import Config
 from ..models.diffusion_model import DiffusionProcess, PointCloudDiffusionModel
@@ -182,6 +183,7 @@ class DiffusionTrainer:
         self.prefetch_style_geometry = self.device_type == "cuda"
         self._geo_next = None  # (condition tensor it was computed for, geometry, ready event)
         self._geo_stream = None
+        self._geo_dstream = None
         if self.distributed:
             from torch.nn.parallel import DistributedDataParallel as DDP
 
@@ -242,7 +244,12 @@ class DiffusionTrainer:
         real = batch["real_full"]
         main = torch.cuda.current_stream(self.device)
         if self._geo_stream is None:
-            self._geo_stream = torch.cuda.Stream(device=self.device)
+            # a stream of its own at the device's greatest priority: a pool stream
+            # (torch.cuda.Stream) can land on the hardware queue of the main stream, depending on
+            # how many streams the process created before (a forked hipGraph branch earlier in the
+            # bench made the step 9.7 -> 10.4 ms: the prefetch then serialised with the step)
+            self._geo_dstream = _hip.DeviceStream(self.device, priority=-1)
+            self._geo_stream = self._geo_dstream.stream
         side = self._geo_stream
         side.wait_stream(main)
         with torch.cuda.stream(side), torch.no_grad():

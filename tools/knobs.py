@@ -33,6 +33,10 @@ def apply():
         dm.POOL_PREP = e["PCST_POOL_PREP"] != "0"
     if "PCST_ROWS_LAYOUT" in e:  # the step's kNN in the rows layout (0: the compact build)
         dm.ROWS_LAYOUT = e["PCST_ROWS_LAYOUT"] != "0"
+    if "PCST_GRAPH_FORK_BUILD" in e:  # the graph step's kNN build on a forked branch (0: inline)
+        dm.GRAPH_FORK_BUILD = e["PCST_GRAPH_FORK_BUILD"] != "0"
+    if "PCST_KNN_BUILD_MAX_WG" in e:  # the compact build's work-groups per launch (0: natural)
+        dm.KNN_BUILD_MAX_WG = int(e["PCST_KNN_BUILD_MAX_WG"])
     if "PCST_ROWS_MAX_MLP_POINTS" in e:  # the rows layout up to this many MLP points per launch
         dm.ROWS_MAX_MLP_POINTS = int(e["PCST_ROWS_MAX_MLP_POINTS"])
     if "PCST_FUSED_BLOCK_FWD" in e:

@@ -183,9 +183,9 @@ for st in "$@"; do
         done
       done ;;
     graphab)
-      # configs[4]'s batch32 leg (eager and graph) with GRAPH_OVERLAP on and off, two alternating passes
+      # configs[4]'s batch32 leg (eager and graph) with GRAPH_FORK_BUILD on and off, two alternating passes
       for pass in 1 2; do
-        for v in prod PCST_GRAPH_OVERLAP=0; do
+        for v in prod PCST_GRAPH_FORK_BUILD=0; do
           kv=PCST_NONE=1; if [ "$v" != prod ]; then kv=$v; fi
           env "$kv" timeout -k 10 300 python tools/bench_knobs.py --gpus 1 --steps 5 --warmup 2 --no-cpu-baseline \
               --no-encoder --no-other-precision > "$OUT/graph_$v.$pass.json" 2> "$OUT/graph_$v.$pass.err"
