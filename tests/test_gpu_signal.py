@@ -369,6 +369,33 @@ def test_pool_prepped_downsample_matches_plain():
         assert torch.equal(got[1], want[1]) and torch.equal(got[0], want[0]), r
 
 
+@pytest.mark.parametrize("C,N,with_src", [(1, 4096, True), (2, 4099, True), (3, 60000, False),
+                                          (1, 120000, True)])
+def test_cfg_voxel_prep_matches_update_and_plain_downsample(C, N, with_src):
+    """pcst_cfg_ddim_voxel_prep's update (the four-point float4 path at N % 4 == 0, the per-point
+    loop otherwise) writes the bits of pcst_cfg_ddim_step into x_out and both halves of x_cat,
+    and its min / max partials prepare the same downsample as the plain one."""
+    from pointcloud_style_transfer_amd import _hip
+
+    dev = torch.device("cuda", 0)
+    rng = np.random.default_rng(N + C)
+    T = N // 4
+    x = torch.from_numpy(rng.standard_normal((C, N, 3)).astype(np.float32)).to(dev)
+    eps = torch.from_numpy(rng.standard_normal((2 * C, N, 3)).astype(np.float32)).to(dev)
+    src = torch.from_numpy(rng.standard_normal((C, N, 3)).astype(np.float32)).to(dev) if with_src else None
+    coeffs = (np.float32(0.3), np.float32(0.95), np.float32(0.97), np.float32(0.24))
+    ws = _hip.voxel_copies_workspace(C, N, 2, dev)
+    x_cat = torch.empty(2 * C, N, 3, device=dev)
+    got = _hip.cfg_ddim_voxel_prep(x, eps, src, 7.5, coeffs, x_cat, ws)
+    want_cat = torch.empty(2 * C, N, 3, device=dev)
+    want = _hip.cfg_ddim_step(x, eps[:C], eps[C:], src, 7.5, coeffs, x_cat=want_cat)
+    assert torch.equal(got, want)
+    assert torch.equal(x_cat, want_cat)
+    a = _hip.voxel_downsample(got, T, seed=77, copies=2, ws=ws, prepped=True)
+    b = _hip.voxel_downsample(got, T, seed=77, copies=2)
+    assert torch.equal(a[1], b[1]) and torch.equal(a[0], b[0])
+
+
 def test_waiters_launched_before_their_producer_on_a_saturated_device():
     """Forward progress of the product's in-kernel spin-waits ("Forward progress"):
     each waiter is queued BEFORE its producer's signal while a saturating kernel holds every CU
