@@ -564,6 +564,218 @@ __global__ __launch_bounds__(kFps2Threads) void fps_cull_kernel(const float* __r
   }
 }
 
+// Multi-CU FPS (pcst_fps_ws with a workspace, 8192 < N <= 32768, B * K <= kFpsXMaxGroups):
+// the same keys and result as fps_key_kernel with the cloud cut over K = ceil(N / 2048)
+// work-groups of 512 threads (4 points per lane: a round's distance update is ~60 VALU
+// instructions per wave instead of a culled 30-point region's ~250), which exchange their round
+// winners through global memory instead of one CU running every point.
+//   Round: every lane updates its points and keeps its best key with the point's coordinates; the
+//   wave maximum (DPP), one LDS exchange of the 8 wave winners and a barrier give the work-group's
+//   winner, which wave 0 publishes to its slot: ONE 64-bit word, (round + 1) << 48 | index << 32 |
+//   distance bits, single-copy atomic, so the tag validates the whole word and no fence orders
+//   anything.  Wave 0 then polls the cloud's K slots (lane j: slot j, agent-scope relaxed loads
+//   that bypass L1); a lane whose slot is ready loads that candidate's coordinates from the
+//   (read-only) cloud at once, so they are in flight while the other slots arrive; the maximum key
+//   and its coordinates reach the other waves through LDS and a second barrier.  Two slot sets
+//   alternate by round parity: a work-group overwrites its parity-p slot (round r + 2) only after
+//   it read every slot of round r + 1, each published after ITS work-group's barrier of round r + 1,
+//   which all its waves reached only after they were done with round r.  The workspace is zeroed
+//   per call (tags >= 1).
+//   Same-XCD mode: the work-groups first exchange their XCC ids (agent scope, once); if all K share
+//   one XCD -- checked, never assumed -- slots are published with plain stores, which keep the line
+//   in that L2 where the siblings' L1-bypassing polls hit it; otherwise with agent-scope stores,
+//   which write through and drop the line (a fabric round trip per round).  The launch has 8
+//   work-groups per working one and only those with blockIdx % 8 == 0 work, which round-robin
+//   dispatch puts on one XCD (speed only).
+//   Forward progress: a polling work-group needs its K - 1 siblings to run; at most kFpsXMaxGroups
+//   work-groups work, far below the device's resident capacity, and everything else on the device
+//   is finite, so every sibling gets a CU.  A poll that exceeds max_polls (a broken sibling) marks
+//   the work-group dead: it stops publishing and waiting, its siblings give up in turn, and the
+//   cloud's samples are written as -1 instead of hanging.
+//   Measured (tools/fps_ab.py, B = 1, N = 30000, 512 samples): 1.83 us per round against the culled
+//   kernel's 1.96-2.10; polling by every wave (3.0-3.6 with five-word slots carrying the
+//   coordinates, 2.1-2.5 with one-word slots) lost to L2 contention on the slot lines.
+constexpr int kFpsXThreads = 512;
+constexpr int kFpsXWaves = kFpsXThreads / 64;
+constexpr int kFpsXPPT = 2048 / kFpsXThreads;
+constexpr int kFpsXMaxGroups = 32;
+constexpr int kFpsXWords = 8;  // 5 tagged words per slot, padded to 64 B
+
+__device__ __forceinline__ void fpsx_store(uint64_t* p, uint64_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint64_t fpsx_load(const uint64_t* p) {
+  return __hip_atomic_load(const_cast<uint64_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint32_t xcc_id() {
+  uint32_t v;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(v));
+  return v & 0xfu;
+}
+
+__global__ __launch_bounds__(kFpsXThreads) void fps_multi_kernel(const float* __restrict__ xyz,
+                                                                 int N, int npoint,
+                                                                 const int64_t* __restrict__ start,
+                                                                 int64_t* __restrict__ out,
+                                                                 uint64_t* __restrict__ slots,
+                                                                 int K, int64_t max_polls) {
+  if (blockIdx.x & 7) return;  // (placement only: the working work-groups share an XCD)
+  constexpr int H = kFpsXPPT / 2;
+  const int gi = blockIdx.x >> 3;
+  const int b = gi / K, k = gi - b * K;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const float* P = xyz + (int64_t)b * N * 3;
+  const int base = k * (kFpsXThreads * kFpsXPPT);
+  fps_f2 X[H], Y[H], Z[H];
+  fps_i2 D[H];
+#pragma unroll
+  for (int j = 0; j < H; ++j) {
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const int n = base + tid + (2 * j + e) * kFpsXThreads;
+      const bool ok = n < N;
+      X[j][e] = ok ? P[n * 3 + 0] : 0.0f;
+      Y[j][e] = ok ? P[n * 3 + 1] : 0.0f;
+      Z[j][e] = ok ? P[n * 3 + 2] : 0.0f;
+      D[j][e] = __float_as_int(ok ? 1e10f : -1.0f);  // -1: a padding slot, never the arg-max
+    }
+  }
+  __shared__ uint64_t s_key[2][kFpsXWaves];
+  __shared__ float4 s_pt[2][kFpsXWaves];
+  __shared__ int s_dead;
+  __shared__ int s_far[2];
+  __shared__ float4 s_c[2];
+  if (tid == 0) s_dead = 0;
+  __syncthreads();
+  uint64_t* S = slots + (int64_t)b * K * 2 * kFpsXWords;  // [parity][k][word]
+  int far = (int)start[b];
+  float cx = P[far * 3 + 0], cy = P[far * 3 + 1], cz = P[far * 3 + 2];
+  int64_t* o = out + (int64_t)b * npoint;
+  bool dead = false;
+  // Same-XCD mode: the work-groups exchange their XCC ids once (word 5 of the parity-0 slots,
+  // tag 0xFFFFFFFF, agent scope).  If all K share one XCD -- checked, never assumed -- the rounds'
+  // slots are published with plain stores, which keep the line in that XCD's L2, where the other
+  // work-groups' L1-bypassing (sc1) polls find it; otherwise with agent-scope stores, which drop
+  // the line from L2 for readers on other XCDs (a fabric round trip per round).  Every work-group
+  // reads the same K ids, so all take the same mode.
+  bool local = false;
+  if (K > 1) {
+    if (tid == 0) fpsx_store(S + (int64_t)k * kFpsXWords + 5, (0xFFFFFFFFull << 32) | xcc_id());
+    uint64_t v = 0;
+    for (int64_t poll = 0;; ++poll) {
+      if (lane < K) v = fpsx_load(S + (int64_t)lane * kFpsXWords + 5);
+      if (__ballot(lane < K && (v >> 32) != 0xFFFFFFFFull) == 0ull) break;
+      if (poll >= max_polls) { dead = true; break; }
+    }
+    const uint32_t x0 = __builtin_amdgcn_readlane((uint32_t)v, 0);
+    local = !dead && __ballot(lane < K && (uint32_t)v != x0) == 0ull;
+    if (dead && lane == 0) s_dead = 1;
+  }
+  for (int it = 0; it < npoint; ++it) {
+    if (k == 0 && tid == 0) o[it] = far;
+    const fps_f2 c2x = {cx, cx}, c2y = {cy, cy}, c2z = {cz, cz};
+    uint64_t lk = 0;  // padding slots keep key 0, below every point's key
+    float bx = 0.0f, by = 0.0f, bz = 0.0f;
+#pragma unroll
+    for (int j = 0; j < H; ++j) {
+      // the same IEEE operations as fps_key_kernel ((dx*dx + dy*dy) + dz*dz, nothing fused)
+      const fps_f2 dx = X[j] - c2x, dy = Y[j] - c2y, dz = Z[j] - c2z;
+      const fps_f2 d = (dx * dx + dy * dy) + dz * dz;
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        D[j][e] = min(__float_as_int(d[e]), D[j][e]);
+        const uint32_t n = (uint32_t)(base + tid + (2 * j + e) * kFpsXThreads);
+        const uint64_t key = D[j][e] >= 0 ? ((uint64_t)(uint32_t)D[j][e] << 32) | (0xFFFFFFFFu - n) : 0ull;
+        if (key > lk) { lk = key; bx = X[j][e]; by = Y[j][e]; bz = Z[j][e]; }
+      }
+    }
+    // the wave's winner (key and coordinates), then the work-group's through LDS
+    const uint64_t wk = wave_max_u64(lk);
+    const uint64_t wl = __ballot(lk == wk);
+    const int wlane = __builtin_ffsll((long long)wl) - 1;
+    const float wx = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(bx), wlane));
+    const float wy = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(by), wlane));
+    const float wz = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(bz), wlane));
+    const int slot = it & 1;
+    if (lane == 0) {
+      s_key[slot][wid] = wk;
+      s_pt[slot][wid] = make_float4(wx, wy, wz, 0.0f);
+    }
+    __syncthreads();
+    if (s_dead) dead = true;  // a wave of this work-group gave up in an earlier round
+    uint64_t g = lane < kFpsXWaves ? s_key[slot][lane] : 0ull;
+    g = row_max_u64(g);
+    const uint32_t gk_hi = __builtin_amdgcn_readlane((uint32_t)(g >> 32), 0);  // (readlane's
+    const uint32_t gk_lo = __builtin_amdgcn_readlane((uint32_t)g, 0);          // int: no sign-extension)
+    const uint64_t gk = ((uint64_t)gk_hi << 32) | gk_lo;
+    if (K == 1) {  // the winning wave's coordinates (a full-wave ballot over the LDS keys)
+      const int gw = __builtin_ffsll((long long)__ballot(lane < kFpsXWaves && s_key[slot][lane & 7] == gk)) - 1;
+      const float4 q = s_pt[slot][gw];
+      far = (int)(0xFFFFFFFFu - (uint32_t)gk);
+      cx = q.x; cy = q.y; cz = q.z;
+      continue;
+    }
+    uint64_t* mine = S + ((int64_t)slot * K + k) * kFpsXWords;
+    // one word per slot: tag (16 bits) | index (16) | distance bits (32)
+    const uint64_t tag16 = (uint64_t)(uint32_t)(it + 1) << 48;
+    if (wid == 0 && lane == 0 && !dead) {
+      const uint64_t w = tag16 | ((uint64_t)(0xFFFFFFFFu - (uint32_t)gk) << 32) | (gk >> 32);
+      if (local) *reinterpret_cast<volatile uint64_t*>(mine) = w;
+      else fpsx_store(mine, w);
+    }
+    // wave 0 polls the K slots; a lane whose slot is ready loads that candidate's coordinates at
+    // once (read-only cloud), so they are in flight while the other slots arrive; then the
+    // winner's index and coordinates go to the other waves through LDS (one more barrier)
+    if (wid == 0) {
+      const uint64_t* sj = S + ((int64_t)slot * K + (lane < K ? lane : 0)) * kFpsXWords;
+      uint64_t w0 = 0;
+      bool have = lane >= K;
+      float px = 0.0f, py = 0.0f, pz = 0.0f;
+      for (int64_t poll = 0;; ++poll) {
+        if (!have) {
+          w0 = fpsx_load(sj);
+          if ((w0 >> 48) == (uint64_t)(uint32_t)(it + 1) || dead) {
+            const int j = min((int)((w0 >> 32) & 0xFFFFu), N - 1);
+            px = P[j * 3 + 0]; py = P[j * 3 + 1]; pz = P[j * 3 + 2];
+            have = true;
+          }
+        }
+        if (__ballot(!have) == 0ull) break;
+        if (poll >= max_polls) {
+          dead = true;
+          if (lane == 0) s_dead = 1;
+          break;
+        }
+      }
+      const uint64_t key = lane < K ? ((w0 & 0xFFFFFFFFull) << 32) |
+                                          (0xFFFFFFFFu - (uint32_t)((w0 >> 32) & 0xFFFFu))
+                                    : 0ull;
+      const uint64_t kmax = wave_max_u64(key);
+      const int wj = __builtin_ffsll((long long)__ballot(lane < K && key == kmax)) - 1;
+      const float ex = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(px), wj));
+      const float ey = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(py), wj));
+      const float ez = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(pz), wj));
+      if (lane == 0) {
+        s_far[slot] = dead ? -1 : (int)(0xFFFFFFFFu - (uint32_t)kmax);
+        s_c[slot] = make_float4(ex, ey, ez, 0.0f);
+      }
+    }
+    __syncthreads();
+    far = s_far[slot];
+    if (far < 0) dead = true;
+    far = dead ? 0 : far;
+    const float4 c = s_c[slot];
+    cx = c.x; cy = c.y; cz = c.z;
+  }
+  // a wave whose poll gave up (a sibling that never published): it stopped waiting and its
+  // work-group stopped publishing, so every work-group of the cloud gives up in turn; the cloud's
+  // samples are then -1 (no hang, no plausible-looking indices)
+  __syncthreads();
+  if (s_dead && k == 0)
+    for (int i = tid; i < npoint; i += kFpsXThreads) o[i] = -1;
+}
+
 // Fallback for N > 512*60: running distances in global memory (caller workspace), one
 // workgroup per cloud streaming the cloud every iteration.
 __global__ __launch_bounds__(1024) void fps_global_kernel(const float* __restrict__ xyz, int N,
@@ -812,8 +1024,17 @@ static void launch_fps_cull(const float* xyz, int B, int N, int npoint, const in
                      out);
 }
 
+// the multi-CU kernel's work-groups per cloud, or 0 where it does not apply
+static int64_t fps_multi_groups(int64_t B, int64_t N) {
+  const int64_t K = cdiv(N, (int64_t)kFpsXThreads * kFpsXPPT);
+  return (N > 8192 && K <= 16 && B * K <= kFpsXMaxGroups) ? K : 0;
+}
+
 extern "C" int pcst_fps_workspace_size(int64_t B, int64_t N, size_t* bytes) {
-  *bytes = (N > (int64_t)kFpsThreads * 60) ? (size_t)(B * N) * sizeof(float) : 0;
+  PCST_CHECK_ARG(B >= 0 && N >= 0 && bytes, "fps_workspace_size: bad args");
+  const int64_t K = fps_multi_groups(B, N);
+  if (K > 0) *bytes = (size_t)(B * K * 2 * kFpsXWords) * sizeof(uint64_t);
+  else *bytes = (N > (int64_t)kFpsThreads * 60) ? (size_t)(B * N) * sizeof(float) : 0;
   return PCST_OK;
 }
 
@@ -825,6 +1046,16 @@ extern "C" int pcst_fps_ws(const float* xyz, int64_t B, int64_t N, int64_t npoin
   PCST_CHECK_ARG(xyz && start_idx && out_idx, "fps: null pointer");
   hipStream_t s = as_stream(stream);
   const int b = (int)B, n = (int)N, np = (int)npoint;
+  const int64_t K = fps_multi_groups(B, N);
+  if (K > 0 && workspace != nullptr) {  // the cloud over K work-groups (one XCD), slots zeroed
+    const size_t bytes = (size_t)(B * K * 2 * kFpsXWords) * sizeof(uint64_t);
+    PCST_HIP(hipMemsetAsync(workspace, 0, bytes, s), "fps: memset");
+    hipLaunchKernelGGL(fps_multi_kernel, dim3((unsigned)(B * K * 8)), dim3(kFpsXThreads), 0, s, xyz, n,
+                       np, start_idx, out_idx, static_cast<uint64_t*>(workspace), (int)K,
+                       (int64_t)kSignalPolls);
+    PCST_LAUNCH_CHECK("fps");
+    return PCST_OK;
+  }
   const int64_t ppt2 = cdiv(N, kFps2Threads);
   if (ppt2 > 8 && ppt2 <= 30) {
     if (ppt2 <= 16) launch_fps_cull<16>(xyz, b, n, np, start_idx, out_idx, s);

@@ -53,13 +53,24 @@ def test_fps_vs_oracle_sizes(H, N, npoint, B):
     np.testing.assert_array_equal(out, O.farthest_point_sample(xyz, npoint, start))
 
 
+def _fps_one_group(H, x, npoint, start):
+    """pcst_fps (no workspace): the one-work-group-per-cloud kernels (culled for 8192 < N <=
+    30720, register-resident below), which pcst_fps_ws replaces by the multi-CU kernel where
+    that applies."""
+    out = torch.empty(x.shape[0], npoint, device=x.device, dtype=torch.int64)
+    H._call("pcst_fps", H._ptr(x), x.shape[0], x.shape[1], npoint, H._ptr(start), H._ptr(out),
+            H._stream())
+    return out
+
+
 @pytest.mark.parametrize("case", ["lidar", "duplicates", "one_bin", "lattice", "small_cluster",
                                   "empty_regions"])
 def test_fps_culled_vs_oracle(H, case):
     """The spatially culled FPS (8192 < N <= 30720: Morton regions per wave, an LDS overflow
-    set, skipped waves) against the oracle: clouds with exact distance ties (duplicated points,
-    a lattice), one dense Morton bin (the greedy fill falls back to index ranges), a
-    realistic cloud at the SA1 size."""
+    set, skipped waves) and the multi-CU FPS (the same clouds through pcst_fps_ws: B * K <= 32
+    work-groups exchanging tagged round winners) against the oracle: clouds with exact distance
+    ties (duplicated points, a lattice), one dense Morton bin (the greedy fill falls back to
+    index ranges), a realistic cloud at the SA1 size."""
     from pointcloud_style_transfer_amd.synthetic import lidar_like_cloud
 
     rng = np.random.default_rng(7)
@@ -80,8 +91,31 @@ def test_fps_culled_vs_oracle(H, case):
         xyz = rng.standard_normal((2, 9000, 3)).astype(np.float32)
     B, N = xyz.shape[:2]
     start = rng.integers(0, N, B)
+    ref = O.farthest_point_sample(xyz, 512, start)
     out = H.fps(dev(xyz), 512, dev(start)).cpu().numpy()
-    np.testing.assert_array_equal(out, O.farthest_point_sample(xyz, 512, start))
+    np.testing.assert_array_equal(out, ref)
+    one = _fps_one_group(H, dev(xyz), 512, dev(start)).cpu().numpy()
+    np.testing.assert_array_equal(one, ref)
+
+
+@pytest.mark.parametrize("N,npoint,B", [(8193, 200, 1), (16384, 300, 2), (30000, 512, 2),
+                                        (32768, 128, 2), (20000, 1, 1), (12000, 4000, 1)])
+def test_fps_multi_cu_vs_oracle(H, N, npoint, B):
+    """The multi-CU FPS at its shape limits (K = ceil(N / 2048) from 5 to 16 work-groups per
+    cloud, B * K up to 32, one sample, more samples than one work-group's points) against the
+    oracle; the call takes that kernel (its workspace is the tagged slots)."""
+    import ctypes
+
+    sz = ctypes.c_size_t(0)
+    H._call("pcst_fps_workspace_size", B, N, ctypes.byref(sz))
+    K = -(-N // 2048)
+    assert sz.value == B * K * 2 * 8 * 8
+    rng = np.random.default_rng(N + B)
+    xyz = rng.standard_normal((B, N, 3)).astype(np.float32)
+    xyz[:, 5:9] = xyz[:, :4]  # exact ties
+    start = rng.integers(0, N, B)
+    out = H.fps(dev(xyz), npoint, dev(start)).cpu().numpy()
+    np.testing.assert_array_equal(out, O.farthest_point_sample(xyz, npoint, start))
 
 
 @pytest.mark.parametrize("key", ["bq_sa1", "bq_sa2", "bq_edge"])
