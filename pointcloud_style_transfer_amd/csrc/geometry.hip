@@ -564,9 +564,9 @@ __global__ __launch_bounds__(kFps2Threads) void fps_cull_kernel(const float* __r
   }
 }
 
-// Multi-CU FPS (pcst_fps_ws with a workspace, 8192 < N <= 32768, B * K <= kFpsXMaxGroups):
-// the same keys and result as fps_key_kernel with the cloud cut over K = ceil(N / 2048)
-// work-groups of 512 threads (4 points per lane: a round's distance update is ~60 VALU
+// Multi-CU FPS (pcst_fps_ws with a workspace, 8192 < N <= 32768, B * K <= kFpsXMaxGroups = 32):
+// the same keys and result as fps_key_kernel with the cloud cut over K = ceil(N / 1024)
+// work-groups of 512 threads (2 points per lane: a round's distance update is ~30 VALU
 // instructions per wave instead of a culled 30-point region's ~250), which exchange their round
 // winners through global memory instead of one CU running every point.
 //   Round: every lane updates its points and keeps its best key with the point's coordinates; the
@@ -592,12 +592,16 @@ __global__ __launch_bounds__(kFps2Threads) void fps_cull_kernel(const float* __r
 //   is finite, so every sibling gets a CU.  A poll that exceeds max_polls (a broken sibling) marks
 //   the work-group dead: it stops publishing and waiting, its siblings give up in turn, and the
 //   cloud's samples are written as -1 instead of hanging.
-//   Measured (tools/fps_ab.py, B = 1, N = 30000, 512 samples): 1.83 us per round against the culled
-//   kernel's 1.96-2.10; polling by every wave (3.0-3.6 with five-word slots carrying the
-//   coordinates, 2.1-2.5 with one-word slots) lost to L2 contention on the slot lines.
+//   Measured (tools/fps_ab.py, B = 1, N = 30000, 512 samples): 1.48 us per round at 2 points per
+//   lane (K = 30) and 1.60 at 4 (K = 15), against the culled kernel's 1.96-2.10; polling by every
+//   wave (3.0-3.6 with five-word slots carrying the coordinates, 2.1-2.5 with one-word slots) lost
+//   to L2 contention on the slot lines.
 constexpr int kFpsXThreads = 512;
 constexpr int kFpsXWaves = kFpsXThreads / 64;
-constexpr int kFpsXPPT = 2048 / kFpsXThreads;
+#ifndef PCST_FPSX_PPT  // experiment builds (csrc/Makefile XDEF)
+#define PCST_FPSX_PPT 2
+#endif
+constexpr int kFpsXPPT = PCST_FPSX_PPT;
 constexpr int kFpsXMaxGroups = 32;
 constexpr int kFpsXWords = 8;  // 5 tagged words per slot, padded to 64 B
 
@@ -1027,7 +1031,7 @@ static void launch_fps_cull(const float* xyz, int B, int N, int npoint, const in
 // the multi-CU kernel's work-groups per cloud, or 0 where it does not apply
 static int64_t fps_multi_groups(int64_t B, int64_t N) {
   const int64_t K = cdiv(N, (int64_t)kFpsXThreads * kFpsXPPT);
-  return (N > 8192 && K <= 16 && B * K <= kFpsXMaxGroups) ? K : 0;
+  return (N > 8192 && K <= 32 && B * K <= kFpsXMaxGroups) ? K : 0;
 }
 
 extern "C" int pcst_fps_workspace_size(int64_t B, int64_t N, size_t* bytes) {

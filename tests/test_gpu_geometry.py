@@ -98,18 +98,19 @@ def test_fps_culled_vs_oracle(H, case):
     np.testing.assert_array_equal(one, ref)
 
 
-@pytest.mark.parametrize("N,npoint,B", [(8193, 200, 1), (16384, 300, 2), (30000, 512, 2),
-                                        (32768, 128, 2), (20000, 1, 1), (12000, 4000, 1)])
+@pytest.mark.parametrize("N,npoint,B", [(8193, 200, 1), (16384, 300, 2), (30000, 512, 1),
+                                        (32768, 128, 1), (9000, 300, 3), (20000, 1, 1),
+                                        (12000, 4000, 1)])
 def test_fps_multi_cu_vs_oracle(H, N, npoint, B):
-    """The multi-CU FPS at its shape limits (K = ceil(N / 2048) from 5 to 16 work-groups per
+    """The multi-CU FPS at its shape limits (K = ceil(N / 1024) from 9 to 32 work-groups per
     cloud, B * K up to 32, one sample, more samples than one work-group's points) against the
     oracle; the call takes that kernel (its workspace is the tagged slots)."""
     import ctypes
 
     sz = ctypes.c_size_t(0)
     H._call("pcst_fps_workspace_size", B, N, ctypes.byref(sz))
-    K = -(-N // 2048)
-    assert sz.value == B * K * 2 * 8 * 8
+    K = -(-N // 1024)
+    assert B * K <= 32 and sz.value == B * K * 2 * 8 * 8
     rng = np.random.default_rng(N + B)
     xyz = rng.standard_normal((B, N, 3)).astype(np.float32)
     xyz[:, 5:9] = xyz[:, :4]  # exact ties
