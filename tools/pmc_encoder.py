@@ -11,7 +11,10 @@ import os
 import sys
 from collections import defaultdict
 
-KERNELS = {"fps": "fps_cull_kernel<30>", "ball_query": "ball_query_split_kernel"}
+# (name, kernel substring, fixed tag or None: tag by grid size).  FPS at one cloud runs the
+# multi-CU kernel (geometry.hip fps_multi_kernel), at 32 clouds the culled one.
+KERNELS = [("fps", "fps_multi_kernel", "b1"), ("fps", "fps_cull_kernel<30>", "b32"),
+           ("ball_query", "ball_query_split_kernel", None)]
 
 
 def main():
@@ -22,20 +25,20 @@ def main():
     for c in ("FETCH_SIZE", "WRITE_SIZE"):
         with open(os.path.join(run, f"pmc_{c}", "pmc_counter_collection.csv")) as f:
             for r in csv.DictReader(f):
-                for name, sub in KERNELS.items():
+                for name, sub, tag in KERNELS:
                     if sub in r["Kernel_Name"]:
-                        acc[(name, int(r["Grid_Size"]), c)].append(float(r["Counter_Value"]))
-    grids = sorted({(n, g) for n, g, _ in acc})
+                        acc[(name, tag, int(r["Grid_Size"]), c)].append(float(r["Counter_Value"]))
+    grids = sorted({(n, t or "", g) for n, t, g, _ in acc})
     rec = {"source": run, "correction": "FETCH_SIZE x2 (gfx950 wide-read tally), WRITE_SIZE x1",
            "unit": "bytes per launch", "bytes_per_launch": {}, "launches": {}}
-    for name, g in grids:
-        f = acc.get((name, g, "FETCH_SIZE"), [])
-        w = acc.get((name, g, "WRITE_SIZE"), [])
+    for name, t, g in grids:
+        f = acc.get((name, t or None, g, "FETCH_SIZE"), [])
+        w = acc.get((name, t or None, g, "WRITE_SIZE"), [])
         if not f or not w:
             continue
-        # grid = threads; FPS runs one 1024-thread workgroup per cloud, ball query 16 waves per
-        # cloud-chunk; the smaller grid of each kernel is the B = 1 launch, the larger B = 32
-        tag = "b1" if g == min(gg for nn, gg in grids if nn == name) else "b32"
+        # grid = threads; ball query runs 16 waves per cloud-chunk: its smaller grid is the
+        # B = 1 launch, the larger B = 32
+        tag = t or ("b1" if g == min(gg for nn, tt, gg in grids if nn == name and not tt) else "b32")
         key = f"{name}_{tag}"
         rec["bytes_per_launch"][key] = round(2.0 * 1024 * sum(f) / len(f) + 1024 * sum(w) / len(w))
         rec["launches"][key] = {"grid": g, "n": len(f)}
