@@ -580,7 +580,7 @@ __global__ __launch_bounds__(kFps2Threads) void fps_cull_kernel(const float* __r
 //   alternate by round parity: a work-group overwrites its parity-p slot (round r + 2) only after
 //   it read every slot of round r + 1, each published after ITS work-group's barrier of round r + 1,
 //   which all its waves reached only after they were done with round r.  The workspace is zeroed
-//   per call (tags >= 1).
+//   per call by a kernel ahead of it on the stream (tags >= 1).
 //   Same-XCD mode: the work-groups first exchange their XCC ids (agent scope, once); if all K share
 //   one XCD -- checked, never assumed -- slots are published with plain stores, which keep the line
 //   in that L2 where the siblings' L1-bypassing polls hit it; otherwise with agent-scope stores,
@@ -615,6 +615,13 @@ __device__ __forceinline__ uint32_t xcc_id() {
   uint32_t v;
   asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(v));
   return v & 0xfu;
+}
+
+// the slots zeroed before the FPS launch (a kernel, not hipMemsetAsync: the host then never waits
+// here and keeps queueing while the previous call's FPS runs)
+__global__ __launch_bounds__(256) void fpsx_zero_kernel(uint64_t* __restrict__ w, int64_t words) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < words; i += (int64_t)gridDim.x * 256)
+    w[i] = 0ull;
 }
 
 __global__ __launch_bounds__(kFpsXThreads) void fps_multi_kernel(const float* __restrict__ xyz,
@@ -1052,8 +1059,9 @@ extern "C" int pcst_fps_ws(const float* xyz, int64_t B, int64_t N, int64_t npoin
   const int b = (int)B, n = (int)N, np = (int)npoint;
   const int64_t K = fps_multi_groups(B, N);
   if (K > 0 && workspace != nullptr) {  // the cloud over K work-groups (one XCD), slots zeroed
-    const size_t bytes = (size_t)(B * K * 2 * kFpsXWords) * sizeof(uint64_t);
-    PCST_HIP(hipMemsetAsync(workspace, 0, bytes, s), "fps: memset");
+    const int64_t words = B * K * 2 * kFpsXWords;
+    hipLaunchKernelGGL(fpsx_zero_kernel, dim3((unsigned)cdiv(words, 256)), dim3(256), 0, s,
+                       static_cast<uint64_t*>(workspace), words);
     hipLaunchKernelGGL(fps_multi_kernel, dim3((unsigned)(B * K * 8)), dim3(kFpsXThreads), 0, s, xyz, n,
                        np, start_idx, out_idx, static_cast<uint64_t*>(workspace), (int)K,
                        (int64_t)kSignalPolls);
