@@ -1043,9 +1043,12 @@ static int64_t fps_multi_groups(int64_t B, int64_t N) {
 
 extern "C" int pcst_fps_workspace_size(int64_t B, int64_t N, size_t* bytes) {
   PCST_CHECK_ARG(B >= 0 && N >= 0 && bytes, "fps_workspace_size: bad args");
+  // the larger of the multi-CU slots and the streaming fallback's distances (a call with
+  // npoint >= 65536 -- more than the slots' 16-bit round tag -- takes the fallback)
   const int64_t K = fps_multi_groups(B, N);
-  if (K > 0) *bytes = (size_t)(B * K * 2 * kFpsXWords) * sizeof(uint64_t);
-  else *bytes = (N > (int64_t)kFpsThreads * 60) ? (size_t)(B * N) * sizeof(float) : 0;
+  const size_t slots = K > 0 ? (size_t)(B * K * 2 * kFpsXWords) * sizeof(uint64_t) : 0;
+  const size_t dists = (N > (int64_t)kFpsThreads * 60) ? (size_t)(B * N) * sizeof(float) : 0;
+  *bytes = slots > dists ? slots : dists;
   return PCST_OK;
 }
 
@@ -1058,7 +1061,7 @@ extern "C" int pcst_fps_ws(const float* xyz, int64_t B, int64_t N, int64_t npoin
   hipStream_t s = as_stream(stream);
   const int b = (int)B, n = (int)N, np = (int)npoint;
   const int64_t K = fps_multi_groups(B, N);
-  if (K > 0 && workspace != nullptr) {  // the cloud over K work-groups (one XCD), slots zeroed
+  if (K > 0 && workspace != nullptr && npoint < 65536) {  // the cloud over K work-groups (one XCD), slots zeroed
     const int64_t words = B * K * 2 * kFpsXWords;
     hipLaunchKernelGGL(fpsx_zero_kernel, dim3((unsigned)cdiv(words, 256)), dim3(256), 0, s,
                        static_cast<uint64_t*>(workspace), words);
