@@ -55,6 +55,27 @@ def test_ctypes_binding_covers_header(built):
     assert _hip.noise_mlp_blob_bytes(2) == _hip.noise_mlp_blob_bytes(3) == -1  # retired codes
 
 
+def test_fps_workspace_sizes(built):
+    """pcst_fps_workspace_size (host arithmetic, no device): the multi-CU FPS's tagged slots
+    (B * ceil(N / 1024) <= 32 work-groups, 2 parities x 64 B each) where that kernel applies,
+    the streaming fallback's B * N floats above 30720 points, the larger of the two where both
+    may run, nothing for the one-work-group kernels."""
+    import ctypes
+
+    from pointcloud_style_transfer_amd import _hip
+
+    def size(B, N):
+        sz = ctypes.c_size_t(0)
+        _hip._call("pcst_fps_workspace_size", B, N, ctypes.byref(sz))
+        return sz.value
+
+    assert size(1, 30000) == 30 * 128
+    assert size(3, 9000) == 27 * 128
+    assert size(1, 8192) == 0 and size(2, 30000) == 0 and size(8, 30000) == 0
+    assert size(1, 32768) == 32768 * 4            # both paths possible: the fallback's is larger
+    assert size(2, 40000) == 2 * 40000 * 4
+
+
 def test_no_process_global_mutable_state(built):
     """pcst.h's contract: no global mutable state except the thread-local last-error string,
     and no environment variables -- every choice a call makes is one of its arguments.  The
