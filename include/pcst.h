@@ -67,8 +67,11 @@ int pcst_group_gather(const float* xyz, const float* feats, int64_t B, int64_t N
                       const int64_t* fps_idx, const int64_t* group_idx, int64_t S, int64_t ns,
                       float* new_xyz, float* grouped, void* stream);
 
-/* FPS for clouds larger than 30720 points: running distances in a caller workspace of
- * pcst_fps_workspace_size() bytes (0 when the register-resident kernel applies). */
+/* FPS with a caller workspace of pcst_fps_workspace_size() bytes (0 when a one-work-group
+ * kernel applies): clouds larger than 30720 points keep their running distances there; for
+ * 8192 < N <= 32768 with B * ceil(N / 1024) <= 32 (and npoint < 65536) it holds the round slots
+ * of the multi-CU kernel, which spreads each cloud over ceil(N / 1024) work-groups (same bits as
+ * pcst_fps; a cloud whose work-groups could not exchange within the poll bound gets -1 samples). */
 int pcst_fps_workspace_size(int64_t B, int64_t N, size_t* bytes);
 int pcst_fps_ws(const float* xyz, int64_t B, int64_t N, int64_t npoint, const int64_t* start_idx,
                 int64_t* out_idx, void* workspace, void* stream);
