@@ -595,7 +595,8 @@ __global__ __launch_bounds__(kFps2Threads) void fps_cull_kernel(const float* __r
 //   Measured (tools/fps_ab.py, B = 1, N = 30000, 512 samples): 1.48 us per round at 2 points per
 //   lane (K = 30) and 1.60 at 4 (K = 15), against the culled kernel's 1.96-2.10; polling by every
 //   wave (3.0-3.6 with five-word slots carrying the coordinates, 2.1-2.5 with one-word slots) lost
-//   to L2 contention on the slot lines.
+//   to L2 contention on the slot lines, and so did every wave publishing its own winner (no first
+//   barrier, wave 0 polling K x 8 words: 2.65).
 constexpr int kFpsXThreads = 512;
 constexpr int kFpsXWaves = kFpsXThreads / 64;
 #ifndef PCST_FPSX_PPT  // experiment builds (csrc/Makefile XDEF)
@@ -664,18 +665,20 @@ __global__ __launch_bounds__(kFpsXThreads) void fps_multi_kernel(const float* __
   float cx = P[far * 3 + 0], cy = P[far * 3 + 1], cz = P[far * 3 + 2];
   int64_t* o = out + (int64_t)b * npoint;
   bool dead = false;
-  // Same-XCD mode: the work-groups exchange their XCC ids once (word 5 of the parity-0 slots,
-  // tag 0xFFFFFFFF, agent scope).  If all K share one XCD -- checked, never assumed -- the rounds'
+  // Same-XCD mode: the work-groups exchange their XCC ids once (word 5 of the parity-1 slots,
+  // tag 0xFFFFFFFF, agent scope; a parity-1 slot is first rewritten in round 1, after every
+  // work-group published round 0, i.e. after it read the ids).  If all K share one XCD -- checked,
+  // never assumed -- the rounds'
   // slots are published with plain stores, which keep the line in that XCD's L2, where the other
   // work-groups' L1-bypassing (sc1) polls find it; otherwise with agent-scope stores, which drop
   // the line from L2 for readers on other XCDs (a fabric round trip per round).  Every work-group
   // reads the same K ids, so all take the same mode.
   bool local = false;
   if (K > 1) {
-    if (tid == 0) fpsx_store(S + (int64_t)k * kFpsXWords + 5, (0xFFFFFFFFull << 32) | xcc_id());
+    if (tid == 0) fpsx_store(S + (int64_t)(K + k) * kFpsXWords + 5, (0xFFFFFFFFull << 32) | xcc_id());
     uint64_t v = 0;
     for (int64_t poll = 0;; ++poll) {
-      if (lane < K) v = fpsx_load(S + (int64_t)lane * kFpsXWords + 5);
+      if (lane < K) v = fpsx_load(S + (int64_t)(K + lane) * kFpsXWords + 5);
       if (__ballot(lane < K && (v >> 32) != 0xFFFFFFFFull) == 0ull) break;
       if (poll >= max_polls) { dead = true; break; }
     }
