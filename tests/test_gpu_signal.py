@@ -498,3 +498,43 @@ def test_waiting_grids_larger_than_the_device_never_hold_every_cu():
     assert h.placed
     assert torch.equal(xi, xi_ref)
     assert torch.equal(q, q_ref)
+
+
+def test_multi_cu_fps_beside_a_saturating_kernel():
+    """Forward progress of the multi-CU FPS's in-kernel exchange (geometry.hip fps_multi_kernel,
+    DESIGN §3): its K = 30 work-groups are queued on one stream right behind a saturating kernel on
+    another (the bf16 noise MLP over 64 x 30000 points, ~30 rounds of 512-thread work-groups), so
+    they start one by one as the MLP's work-groups retire and the first ones poll for siblings that
+    have no CU yet.  Each waits only for its siblings, which the finite MLP leaves CUs to: the
+    samples equal the one-work-group kernel's (pcst_fps) and none is -1 (no poll gave up)."""
+    from pointcloud_style_transfer_amd import _hip
+    from pointcloud_style_transfer_amd.config.config import Config
+    from pointcloud_style_transfer_amd.models.diffusion_model import NoisePredictor
+    from pointcloud_style_transfer_amd.synthetic import lidar_like_cloud
+
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(14)
+    npred = NoisePredictor(Config(make_dirs=False, precision="bf16")).to(dev).eval()
+    big = torch.randn(64 * 30000, 3, device=dev)
+    xyz = torch.from_numpy(lidar_like_cloud(21, 30000)[None].astype(np.float32)).to(dev)
+    start = torch.tensor([17], device=dev)
+    with torch.no_grad():
+        cbig = npred.cond(torch.full((64,), 900, device=dev), torch.randn(64, 256, device=dev))
+        blob, bias = npred.packed()[:2]
+        ref = torch.empty(1, 512, dtype=torch.int64, device=dev)
+        _hip._call("pcst_fps", _hip._ptr(xyz), 1, 30000, 512, _hip._ptr(start), _hip._ptr(ref),
+                   _hip._stream())
+        torch.cuda.synchronize()
+        sat = torch.cuda.Stream(device=dev)
+        cons = torch.cuda.Stream(device=dev)
+        for s in (sat, cons):
+            s.wait_stream(torch.cuda.current_stream())
+        outs = []
+        with torch.cuda.stream(sat):
+            _hip.noise_mlp(big, 30000, cbig, blob, bias, npred.precision_code)
+        with torch.cuda.stream(cons):
+            for _ in range(3):
+                outs.append(_hip.fps(xyz, 512, start))
+        torch.cuda.synchronize()
+    for o in outs:
+        assert torch.equal(o, ref)
